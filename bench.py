@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X Groth16/BN254 hot path.
+
+Headline (BASELINE.json metric "... MSM G1 throughput (Mscalar-mul/s) ...",
+workload = configs[1]): BN254 G1 MSM over 2^20 resident points per GPU, scalars
+resident in HBM, one process per GPU.  A "step" is one full MSM (digits, sort,
+bucket accumulation, bucket reduction, result to host); for N > 1 each rank owns
+its own 2^20-point shard (weak scaling) and the per-rank Jacobian partials are
+all-gathered over RCCL and added on rank 0 (RCCL has no EC-add reduction).
+
+Also reported (not the headline): a Groth16 prove at --groth16-log-n with a
+synthetic key generated on the GPU, and the C restatement (oracle/) of the same
+MSM timed on the host cores as cpu_baseline.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gnark-fork_amd"))
+
+METRIC = ("Groth16 prove time + MSM G1 throughput (Mscalar-mul/s) BN254 2^24 R1CS, 1/2/4/8 GPU")
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def rand_scalars(n, seed):
+    """n random fr elements (Montgomery bytes) < 2^253 < r as uint64[n, 4]."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    raw = rng.integers(0, 2**63, size=(n, 4), dtype=np.uint64) * 2
+    raw ^= rng.integers(0, 2, size=(n, 4), dtype=np.uint64)
+    raw[:, 3] &= np.uint64((1 << 61) - 1)
+    return np.ascontiguousarray(raw)
+
+
+def g1_generator_mont():
+    from gnark_amd import fr
+    return fr.fp_mont(1) + fr.fp_mont(2)
+
+
+def g2_generator_mont():
+    from gnark_amd import fr
+    x0 = 10857046999023057135944570762232829481370756359578518086990519993285655852781
+    x1 = 11559732032986387107991004021392285783925812861821192530917403151452391805634
+    y0 = 8495653923123431417604973247489272438418190587263600148770280649306958101930
+    y1 = 4082367875863433681332203403145435568316851327593401208105741076214120093531
+    return b"".join(fr.fp_mont(v) for v in (x0, x1, y0, y1))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--log-n", type=int, default=20, help="MSM points per GPU = 2^log_n")
+    ap.add_argument("--groth16-log-n", type=int, default=20,
+                    help="domain size of the extra Groth16 prove measurement (0 = skip)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+    import gnark_amd
+    from gnark_amd import _lib, msm, DeviceBuffer
+
+    _lib.check(_lib.lib.gg_set_device(local_rank))
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        _lib.check(_lib.lib.gg_synchronize())
+
+    n = 1 << args.log_n
+    # ---- synthetic resident key shard (GPU fixed-base batch mul, distinct per rank)
+    t0 = time.time()
+    ks = rand_scalars(n, 1000 + rank)
+    pts = DeviceBuffer(64 * n)
+    msm.batch_scalar_mul(msm.G1, g1_generator_mont(), ks, n, out=pts)
+    base = msm.MsmBase(msm.G1, pts.ptr, n, on_device=True)
+    del pts
+    npts, c, W = base.info()
+    sc = rand_scalars(n, 2000 + rank)
+    dsc = DeviceBuffer.from_host(sc.tobytes())
+    log(f"[rank {rank}] key shard ready: n={npts} c={c} windows={W} ({time.time() - t0:.1f}s)")
+
+    def step():
+        j = base.msm_jac(dsc, n, on_device=True)
+        if dist is None:
+            return j
+        t = torch.frombuffer(bytearray(j), dtype=torch.uint8).cuda()
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        if rank == 0:
+            acc = bytes(parts[0].cpu().numpy())
+            for p in parts[1:]:
+                acc = msm.jac_add(msm.G1, acc, bytes(p.cpu().numpy()))
+            return acc
+        return j
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    ms_per_step = 1e3 * el / args.steps
+    value = world * n * args.steps / el / 1e6  # Mscalar-mul/s, whole job
+
+    # ---- roofline of the dominant kernel (bucket accumulation), HIP events on its stream
+    gnark_amd._lib.profile_enable(True)
+    prof_steps = max(3, min(10, args.steps))
+    for _ in range(prof_steps):
+        base.msm_jac(dsc, n, on_device=True)
+    kernels = {}
+    for name in ("msm_sort", "msm_accum", "msm_accum2", "msm_reduce"):
+        ms, cnt, units = gnark_amd._lib.profile_get(name)
+        kernels[name] = {"avg_ms": ms / cnt if cnt else None, "launches": cnt}
+    gnark_amd._lib.profile_enable(False)
+    acc_ms = kernels["msm_accum"]["avg_ms"]
+    alg_bytes = n * (64 + 32)  # N x (G1 affine 64 B + fr 32 B)
+    achieved = alg_bytes / (acc_ms * 1e-3) / 1e9 if acc_ms else None
+    roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                "kernel": "k_accum_affine<Fp> (bucket accumulation)",
+                "algorithmic_bytes_per_launch": alg_bytes, "kernel_avg_ms": acc_ms,
+                "note": "EC MSM is VALU-integer bound (SURVEY 8d); HBM fraction reported as required"}
+
+    out = {
+        "metric": METRIC, "value": value, "unit": "Mscalar-mul/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "u32 limbs (BN254 Fp/Fr Montgomery, integer)", "data": "synthetic",
+        "config": {"workload": "BN254 G1 MSM, 2^%d resident points + scalars per GPU "
+                               "(BASELINE configs[1])" % args.log_n,
+                   "points_per_gpu": n, "window_bits": c, "windows": W,
+                   "parallelism": "msm point-shard x%d, RCCL all_gather of partials" % world},
+        "roofline": roofline, "kernels": kernels,
+    }
+
+    # ---- Groth16 prove (extra, rank 0 / N = 1 only)
+    if rank == 0 and world == 1 and args.groth16_log_n:
+        try:
+            out["groth16"] = groth16_bench(args.groth16_log_n)
+        except Exception as e:  # report, never hide
+            out["groth16"] = {"error": repr(e)}
+
+    # ---- CPU baseline (oracle restatement on the host cores), rank 0 at N = 1
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(base, dsc, sc, n, args.cpu_threads)
+        except Exception as e:
+            out["cpu_baseline"] = {"error": repr(e)}
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(base, dsc, sc, n, threads):
+    """C restatement of the same MSM (oracle/c, OpenMP Pippenger) on a bounded
+    sample: the first 2^18 points/scalars of the workload, repeated ~10 s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle
+    from gnark_amd import msm
+    nt = threads or min(16, os.cpu_count() or 1)
+    m = min(n, 1 << 18)
+    # the sample's points: regenerate the first m on the GPU and copy to host
+    ks = rand_scalars(n, 1000)[:m]
+    pts = msm.batch_scalar_mul(msm.G1, g1_generator_mont(), ks, m)
+    sb = sc[:m].tobytes()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        coracle.msm_g1(pts, sb, m, nt)
+        reps += 1
+        if time.perf_counter() - t0 > 10.0 or reps >= 50:
+            break
+    el = time.perf_counter() - t0
+    return {"value": m * reps / el / 1e6, "unit": "Mscalar-mul/s", "cores": nt, "kind": "port",
+            "sample": f"G1 MSM 2^{m.bit_length() - 1} points x {reps} reps (C restatement, "
+                      f"signed-digit Pippenger, {nt} OpenMP threads, not gnark)"}
+
+
+def groth16_bench(log_n, reps=3):
+    """Synthetic 2^log_n Groth16 prove, key generated on the GPU; inputs resident."""
+    import numpy as np
+    from gnark_amd import backend, groth16, msm, DeviceBuffer
+    n = 1 << log_n
+    n_wires = n - 3
+    nb_public = 2
+    rng = np.random.default_rng(5)
+    infA = np.zeros(n_wires, dtype=np.uint8)
+    infB = (rng.random(n_wires) < 0.3).astype(np.uint8)
+    nA, nB, nK = n_wires, int((infB == 0).sum()), n_wires - nb_public
+    t0 = time.time()
+    g1 = g1_generator_mont()
+
+    def g1pts(k, seed):
+        return msm.batch_scalar_mul(msm.G1, g1, rand_scalars(k, seed), k)
+
+    d = groth16.ProvingKeyData(
+        log_n=log_n, g1_A=g1pts(nA, 1), g1_B=g1pts(nB, 2), g1_Z=g1pts(n - 1, 3), g1_K=g1pts(nK, 4),
+        alpha1=g1pts(1, 5), beta1=g1pts(1, 6), delta1=g1pts(1, 7),
+        g2_B=msm.batch_scalar_mul(msm.G2, g2_generator_mont(), rand_scalars(nB, 8), nB),
+        beta2=msm.batch_scalar_mul(msm.G2, g2_generator_mont(), rand_scalars(1, 9), 1),
+        delta2=msm.batch_scalar_mul(msm.G2, g2_generator_mont(), rand_scalars(1, 10), 1),
+        infinity_A=infA.tobytes(), infinity_B=infB.tobytes(), nb_public=nb_public)
+    pk = groth16.ProvingKey(d)
+    t_setup = time.time() - t0
+    wires = DeviceBuffer.from_host(rand_scalars(n_wires, 11).tobytes())
+    ncons = n - 5
+    sa, sb, sc = (DeviceBuffer.from_host(rand_scalars(ncons, 12 + i).tobytes()) for i in range(3))
+    sol = groth16.Solution(wires, sa, sb, sc, n_wires, ncons, on_device=True)
+    groth16.prove(pk, sol, backend.with_amd_acceleration())
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        groth16.prove(pk, sol, backend.with_amd_acceleration())
+        ts.append(1e3 * (time.perf_counter() - t))
+    tim = groth16.last_timings()
+    return {"log_n": log_n, "n_constraints": ncons, "n_wires": n_wires,
+            "prove_ms": min(ts), "prove_ms_all": ts, "constraints_per_s": ncons / (min(ts) * 1e-3),
+            "stage_ms": tim, "key_setup_s": t_setup, "inputs": "resident in HBM"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,97 @@
+// Shared runtime plumbing: error propagation into the C ABI, HIP checks,
+// device buffers with RAII.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdexcept>
+#include <string>
+#include <cstdio>
+#include "../../include/gnark_amd.h"
+
+namespace gg {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+void set_last_error(const std::string& m);
+
+#define GG_HIP(x)                                                                         \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) {                                                           \
+            int code_ = (e_ == hipErrorOutOfMemory) ? GG_ERR_OOM : GG_ERR_DEVICE;         \
+            throw ::gg::Error(code_, std::string(#x) + " failed: " + hipGetErrorString(e_) + \
+                                         " at " + __FILE__ + ":" + std::to_string(__LINE__)); \
+        }                                                                                 \
+    } while (0)
+
+#define GG_CHECK(cond, code, msg)                       \
+    do {                                                \
+        if (!(cond)) throw ::gg::Error((code), (msg));  \
+    } while (0)
+
+#define GG_CAPI_BEGIN try {
+#define GG_CAPI_END                                      \
+    return GG_OK;                                        \
+    }                                                    \
+    catch (const ::gg::Error& e) {                       \
+        ::gg::set_last_error(e.what());                  \
+        return e.code;                                   \
+    }                                                    \
+    catch (const std::bad_alloc&) {                      \
+        ::gg::set_last_error("host out of memory");      \
+        return GG_ERR_OOM;                               \
+    }                                                    \
+    catch (const std::exception& e) {                    \
+        ::gg::set_last_error(e.what());                  \
+        return GG_ERR_INTERNAL;                          \
+    }
+
+// owning device buffer
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    explicit DevBuf(size_t b) { alloc(b); }
+    void alloc(size_t b) {
+        release();
+        if (b) GG_HIP(hipMalloc(&p, b));
+        bytes = b;
+    }
+    // grow-only
+    void reserve(size_t b) {
+        if (b > bytes) alloc(b);
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const { return reinterpret_cast<T*>(p); }
+    ~DevBuf() { release(); }
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) { release(); p = o.p; bytes = o.bytes; o.p = nullptr; o.bytes = 0; }
+        return *this;
+    }
+};
+
+inline bool is_device_ptr(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
+inline unsigned grid_for(size_t n, unsigned block) {
+    size_t g = (n + block - 1) / block;
+    return (unsigned)(g ? g : 1);
+}
+
+}  // namespace gg

@@ -1,0 +1,237 @@
+// BN254 base field Fp, scalar field Fr and Fp2 for CDNA4 (gfx950) and host.
+//
+// Representation: 8 x u32 little-endian limbs, Montgomery form with R = 2^256.
+// This is bit-identical in memory to gnark-crypto's fp.Element / fr.Element
+// ([4]uint64 little-endian, R = 2^256), so buffers handed over by the Go side
+// (icicle.go:44-126 call sites) are used without any conversion.
+// Moduli: backend/groth16/bn254/solidity.go:41-42.
+//
+// Multiplication is CIOS with 32x32->64 products (v_mad_u64_u32 on gfx950);
+// add/sub are v_add_co/v_addc chains via __builtin_addc/__builtin_subc.
+// Both moduli are < 2^254, so a+b never overflows 256 bits and the CIOS
+// accumulator never needs a 10th word.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GG_HD __host__ __device__ __forceinline__
+
+namespace gg {
+
+struct FpCfg {
+    static constexpr uint32_t P[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
+                                      0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+    static constexpr uint32_t INV = 0xe4866389u;  // -p^-1 mod 2^32
+    static constexpr uint32_t ONE[8] = {0xc58f0d9du, 0xd35d438du, 0xf5c70b3du, 0x0a78eb28u,
+                                        0x7879462cu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+    static constexpr uint32_t R2[8] = {0x538afa89u, 0xf32cfc5bu, 0xd44501fbu, 0xb5e71911u,
+                                       0x0a417ff6u, 0x47ab1effu, 0xcab8351fu, 0x06d89f71u};
+};
+
+struct FrCfg {
+    static constexpr uint32_t P[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
+                                      0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
+    static constexpr uint32_t INV = 0xefffffffu;
+    static constexpr uint32_t ONE[8] = {0x4ffffffbu, 0xac96341cu, 0x9f60cd29u, 0x36fc7695u,
+                                        0x7879462eu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
+    static constexpr uint32_t R2[8] = {0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u,
+                                       0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
+};
+
+template <class C>
+struct Fe {
+    uint32_t v[8];
+
+    static GG_HD Fe zero() {
+        Fe r;
+#pragma unroll
+        for (int i = 0; i < 8; i++) r.v[i] = 0;
+        return r;
+    }
+    static GG_HD Fe one() {
+        Fe r;
+#pragma unroll
+        for (int i = 0; i < 8; i++) r.v[i] = C::ONE[i];
+        return r;
+    }
+    static GG_HD Fe r2() {
+        Fe r;
+#pragma unroll
+        for (int i = 0; i < 8; i++) r.v[i] = C::R2[i];
+        return r;
+    }
+    static GG_HD Fe modulus() {
+        Fe r;
+#pragma unroll
+        for (int i = 0; i < 8; i++) r.v[i] = C::P[i];
+        return r;
+    }
+    GG_HD bool is_zero() const {
+        uint32_t x = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) x |= v[i];
+        return x == 0;
+    }
+    GG_HD bool operator==(const Fe& o) const {
+        uint32_t x = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) x |= v[i] ^ o.v[i];
+        return x == 0;
+    }
+    GG_HD bool operator!=(const Fe& o) const { return !(*this == o); }
+};
+
+// r = a + b mod p   (inputs < p < 2^254)
+template <class C>
+GG_HD Fe<C> operator+(const Fe<C>& a, const Fe<C>& b) {
+    Fe<C> r, s;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = __builtin_subc(r.v[i], C::P[i], br, &br);
+    // br == 0  <=>  r >= p
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = br ? r.v[i] : s.v[i];
+    return r;
+}
+
+template <class C>
+GG_HD Fe<C> operator-(const Fe<C>& a, const Fe<C>& b) {
+    Fe<C> r, s;
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = __builtin_addc(r.v[i], C::P[i], c, &c);
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = br ? s.v[i] : r.v[i];
+    return r;
+}
+
+template <class C>
+GG_HD Fe<C> operator-(const Fe<C>& a) {
+    return Fe<C>::zero() - a;
+}
+
+template <class C>
+GG_HD Fe<C> dbl(const Fe<C>& a) {
+    return a + a;
+}
+
+// CIOS Montgomery multiplication, 8 x 32-bit limbs.
+template <class C>
+GG_HD Fe<C> operator*(const Fe<C>& a, const Fe<C>& b) {
+    uint32_t t[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) t[j] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint64_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            acc = (uint64_t)a.v[j] * b.v[i] + t[j] + (acc >> 32);
+            t[j] = (uint32_t)acc;
+        }
+        uint32_t t8 = (uint32_t)(acc >> 32);
+        uint32_t m = t[0] * C::INV;
+        acc = (uint64_t)m * C::P[0] + t[0];
+#pragma unroll
+        for (int j = 1; j < 8; j++) {
+            acc = (uint64_t)m * C::P[j] + t[j] + (acc >> 32);
+            t[j - 1] = (uint32_t)acc;
+        }
+        t[7] = t8 + (uint32_t)(acc >> 32);
+    }
+    Fe<C> r, s;
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = __builtin_subc(t[i], C::P[i], br, &br);
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = br ? t[i] : s.v[i];
+    return r;
+}
+
+template <class C>
+GG_HD Fe<C> sqr(const Fe<C>& a) {
+    return a * a;
+}
+
+template <class C>
+GG_HD Fe<C> to_mont(const Fe<C>& a) {
+    return a * Fe<C>::r2();
+}
+
+template <class C>
+GG_HD Fe<C> from_mont(const Fe<C>& a) {
+    Fe<C> one = Fe<C>::zero();
+    one.v[0] = 1;
+    return a * one;
+}
+
+// a^(p-2) (Fermat); a == 0 -> 0
+template <class C>
+GG_HD Fe<C> inverse(const Fe<C>& a) {
+    // exponent p - 2, scanned from the top bit
+    uint32_t e[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) e[i] = C::P[i];
+    e[0] -= 2;  // low limb of both moduli is >= 2
+    Fe<C> acc = Fe<C>::one();
+    for (int i = 255; i >= 0; i--) {
+        acc = sqr(acc);
+        if ((e[i >> 5] >> (i & 31)) & 1) acc = acc * a;
+    }
+    return acc;
+}
+
+// x^e for a small exponent (host-side table building)
+template <class C>
+GG_HD Fe<C> pow_u64(const Fe<C>& x, uint64_t e) {
+    Fe<C> acc = Fe<C>::one(), b = x;
+    while (e) {
+        if (e & 1) acc = acc * b;
+        b = sqr(b);
+        e >>= 1;
+    }
+    return acc;
+}
+
+using Fp = Fe<FpCfg>;
+using Fr = Fe<FrCfg>;
+
+// ---------------------------------------------------------------------------
+// Fp2 = Fp[u] / (u^2 + 1)   (gnark-crypto bn254 E2 layout: {A0, A1})
+// ---------------------------------------------------------------------------
+struct Fp2 {
+    Fp a0, a1;
+    static GG_HD Fp2 zero() { return Fp2{Fp::zero(), Fp::zero()}; }
+    static GG_HD Fp2 one() { return Fp2{Fp::one(), Fp::zero()}; }
+    GG_HD bool is_zero() const { return a0.is_zero() && a1.is_zero(); }
+    GG_HD bool operator==(const Fp2& o) const { return a0 == o.a0 && a1 == o.a1; }
+};
+
+GG_HD Fp2 operator+(const Fp2& a, const Fp2& b) { return Fp2{a.a0 + b.a0, a.a1 + b.a1}; }
+GG_HD Fp2 operator-(const Fp2& a, const Fp2& b) { return Fp2{a.a0 - b.a0, a.a1 - b.a1}; }
+GG_HD Fp2 operator-(const Fp2& a) { return Fp2{-a.a0, -a.a1}; }
+GG_HD Fp2 dbl(const Fp2& a) { return Fp2{a.a0 + a.a0, a.a1 + a.a1}; }
+GG_HD Fp2 operator*(const Fp2& a, const Fp2& b) {
+    Fp t0 = a.a0 * b.a0;
+    Fp t1 = a.a1 * b.a1;
+    Fp t2 = (a.a0 + a.a1) * (b.a0 + b.a1);
+    return Fp2{t0 - t1, t2 - t0 - t1};
+}
+GG_HD Fp2 sqr(const Fp2& a) {
+    Fp t0 = (a.a0 + a.a1) * (a.a0 - a.a1);
+    Fp t1 = a.a0 * a.a1;
+    return Fp2{t0, t1 + t1};
+}
+GG_HD Fp2 inverse(const Fp2& a) {
+    Fp n = sqr(a.a0) + sqr(a.a1);
+    Fp ni = inverse(n);
+    return Fp2{a.a0 * ni, -(a.a1 * ni)};
+}
+
+}  // namespace gg

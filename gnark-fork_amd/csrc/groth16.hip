@@ -1,0 +1,264 @@
+// Groth16 BN254 prover on one MI355X: the device section of gnark's
+// icicle_bn254.Prove (icicle.go:133-422) / groth16_bn254.Prove (prove.go:127-320).
+//
+//   host thread 1 / stream 1:  computeH (7 fused NTTs)  ->  Z-MSM over h
+//   host thread 0 / stream 0:  A-MSM, B1-MSM, K-MSM, G2-MSM (wire scalars
+//                              gathered through per-base index maps)
+//   host pool:                 r*delta, s*delta, kr*delta, s*delta2 while the
+//                              GPU works; s*Ar, r*Bs1 after the MSMs
+// Combination formulas are prove.go:206-299 verbatim.
+#include "common.h"
+#include "curve.cuh"
+#include <chrono>
+#include <future>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+#include <cstring>
+
+struct gg_domain;
+struct gg_msm_base;
+
+namespace gg {
+void compute_h_device(gg_domain* d, Fr* A, Fr* B, Fr* C, Fr* H, hipStream_t st);
+void msm_device(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st);
+size_t msm_scalars_needed(gg_msm_base* b);
+}  // namespace gg
+
+using namespace gg;
+
+struct gg_groth16_pk {
+    int log_n = 0;
+    size_t n = 0;
+    gg_domain_t dom = nullptr;
+    gg_msm_base_t A = nullptr, B = nullptr, K = nullptr, Z = nullptr, B2 = nullptr;
+    G1Affine alpha, beta, delta;
+    G2Affine beta2, delta2;
+    size_t n_wires = 0, nb_public = 0;
+    DevBuf wires, sa, sb, sc;
+    hipStream_t s0 = nullptr, s1 = nullptr;
+    int device = 0;
+    std::mutex mu;
+    ~gg_groth16_pk() {
+        if (A) gg_msm_base_release(A);
+        if (B) gg_msm_base_release(B);
+        if (K) gg_msm_base_release(K);
+        if (Z) gg_msm_base_release(Z);
+        if (B2) gg_msm_base_release(B2);
+        if (dom) gg_domain_release(dom);
+        if (s0) (void)hipStreamDestroy(s0);
+        if (s1) (void)hipStreamDestroy(s1);
+    }
+};
+
+static thread_local double g_timings[9];
+
+static void ck(int rc) {
+    if (rc != GG_OK) throw Error(rc, gg_last_error());
+}
+
+extern "C" int gg_groth16_pk_create(int log_n, const void* omega_mont, const void* coset_gen_mont,
+                                    const void* g1_A, size_t nA, const void* g1_B, size_t nB,
+                                    const void* g1_Z, size_t nZ, const void* g1_K, size_t nK,
+                                    const void* alpha1, const void* beta1, const void* delta1,
+                                    const void* g2_B, const void* beta2, const void* delta2,
+                                    const uint8_t* inf_A, const uint8_t* inf_B, size_t n_wires,
+                                    size_t nb_public, const uint32_t* k_wire_index,
+                                    gg_groth16_pk_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out && omega_mont && coset_gen_mont && alpha1 && beta1 && delta1 && beta2 && delta2,
+             GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(inf_A && inf_B, GG_ERR_INVALID_ARG, "null infinity masks");
+    GG_CHECK(nb_public <= n_wires, GG_ERR_INVALID_ARG, "nb_public > n_wires");
+    std::unique_ptr<gg_groth16_pk> pk(new gg_groth16_pk());
+    pk->log_n = log_n;
+    pk->n = (size_t)1 << log_n;
+    pk->n_wires = n_wires;
+    pk->nb_public = nb_public;
+    GG_CHECK(nZ + 1 == pk->n || (pk->n == 1 && nZ == 0), GG_ERR_INVALID_ARG,
+             "len(pk.G1.Z) must be domain cardinality - 1 (setup.go:266)");
+    GG_HIP(hipGetDevice(&pk->device));
+    memcpy(&pk->alpha, alpha1, 64);
+    memcpy(&pk->beta, beta1, 64);
+    memcpy(&pk->delta, delta1, 64);
+    memcpy(&pk->beta2, beta2, 128);
+    memcpy(&pk->delta2, delta2, 128);
+    ck(gg_domain_create(log_n, omega_mont, coset_gen_mont, &pk->dom));
+    // wire index maps (prove.go:151-175: drop wires whose A/B point is infinity)
+    std::vector<uint32_t> ia, ib, ik;
+    for (size_t i = 0; i < n_wires; i++) {
+        if (!inf_A[i]) ia.push_back((uint32_t)i);
+        if (!inf_B[i]) ib.push_back((uint32_t)i);
+    }
+    GG_CHECK(ia.size() == nA, GG_ERR_INVALID_ARG, "len(pk.G1.A) != n_wires - NbInfinityA");
+    GG_CHECK(ib.size() == nB, GG_ERR_INVALID_ARG, "len(pk.G1.B) != n_wires - NbInfinityB");
+    ik.resize(nK);
+    for (size_t i = 0; i < nK; i++) {
+        ik[i] = k_wire_index ? k_wire_index[i] : (uint32_t)(nb_public + i);
+        GG_CHECK(ik[i] < n_wires, GG_ERR_INVALID_ARG, "k_wire_index out of range");
+    }
+    GG_CHECK(nA == 0 || g1_A, GG_ERR_INVALID_ARG, "null g1_A");
+    GG_CHECK(nB == 0 || (g1_B && g2_B), GG_ERR_INVALID_ARG, "null g1_B / g2_B");
+    GG_CHECK(nK == 0 || g1_K, GG_ERR_INVALID_ARG, "null g1_K");
+    GG_CHECK(nZ == 0 || g1_Z, GG_ERR_INVALID_ARG, "null g1_Z");
+    ck(gg_msm_base_create(GG_G1, g1_A, nA, 0, ia.data(), 0, &pk->A));
+    ck(gg_msm_base_create(GG_G1, g1_B, nB, 0, ib.data(), 0, &pk->B));
+    ck(gg_msm_base_create(GG_G1, g1_K, nK, 0, ik.data(), 0, &pk->K));
+    ck(gg_msm_base_create(GG_G1, g1_Z, nZ, 0, nullptr, 0, &pk->Z));
+    ck(gg_msm_base_create(GG_G2, g2_B, nB, 0, ib.data(), 0, &pk->B2));
+    GG_HIP(hipStreamCreateWithFlags(&pk->s0, hipStreamNonBlocking));
+    GG_HIP(hipStreamCreateWithFlags(&pk->s1, hipStreamNonBlocking));
+    *out = pk.release();
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_pk_release(gg_groth16_pk_t pk) {
+    GG_CAPI_BEGIN
+    delete pk;
+    GG_CAPI_END
+}
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+static Fr fr_from(const void* p) {
+    Fr x;
+    memcpy(&x, p, 32);
+    return x;
+}
+
+extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_wires,
+                                const void* sol_a, const void* sol_b, const void* sol_c,
+                                size_t n_cons, int inputs_on_device, const void* r_mont,
+                                const void* s_mont, void* ar_aff, void* bs_aff, void* krs_aff,
+                                void* h_dev_out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(pk && wires && sol_a && sol_b && sol_c && r_mont && s_mont && ar_aff && bs_aff && krs_aff,
+             GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(n_wires == pk->n_wires, GG_ERR_INVALID_ARG, "len(wires) != pk wires");
+    GG_CHECK(n_cons <= pk->n, GG_ERR_INVALID_ARG, "nbConstraints > domain cardinality");
+    std::lock_guard<std::mutex> lk(pk->mu);
+    double t0 = now_ms();
+    const size_t n = pk->n;
+    const size_t nbytes = n * 32;
+    pk->wires.reserve(std::max<size_t>(n_wires, 1) * 32);
+    pk->sa.reserve(nbytes);
+    pk->sb.reserve(nbytes);
+    pk->sc.reserve(nbytes);
+    hipMemcpyKind kind = inputs_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+
+    // proof randomness (prove.go:177-189): kr = -r*s
+    Fr r = fr_from(r_mont), s = fr_from(s_mont);
+    Fr kr = -(r * s);
+    Fr rc = from_mont(r), sc = from_mont(s), krc = from_mont(kr);
+    // host pool: fixed-point terms independent of the MSMs (prove.go:192, 293-296)
+    G1Jac dl = G1Jac::from_affine(pk->delta);
+    auto f_rd = std::async(std::launch::async, [&] { return jac_mul(dl, rc.v); });
+    auto f_sd = std::async(std::launch::async, [&] { return jac_mul(dl, sc.v); });
+    auto f_krd = std::async(std::launch::async, [&] { return jac_mul(dl, krc.v); });
+    auto f_sd2 = std::async(std::launch::async,
+                            [&] { return jac_mul(G2Jac::from_affine(pk->delta2), sc.v); });
+
+    // uploads
+    const Fr* wdev = (const Fr*)wires;
+    if (!inputs_on_device) {
+        GG_HIP(hipMemcpyAsync(pk->wires.p, wires, n_wires * 32, hipMemcpyHostToDevice, pk->s0));
+        wdev = pk->wires.as<Fr>();
+    }
+    Fr* A = pk->sa.as<Fr>();
+    Fr* B = pk->sb.as<Fr>();
+    Fr* C = pk->sc.as<Fr>();
+    const void* src[3] = {sol_a, sol_b, sol_c};
+    Fr* dst[3] = {A, B, C};
+    for (int i = 0; i < 3; i++) {
+        if (n_cons) GG_HIP(hipMemcpyAsync(dst[i], src[i], n_cons * 32, kind, pk->s1));
+        if (n_cons < n) GG_HIP(hipMemsetAsync((char*)dst[i] + n_cons * 32, 0, nbytes - n_cons * 32, pk->s1));
+    }
+    GG_HIP(hipStreamSynchronize(pk->s0));
+    double t_up = now_ms();
+
+    // stream 1 (worker thread): computeH then Z-MSM; h lands in A
+    G1Jac jz = G1Jac::inf();
+    double t_h = 0, t_z = 0;
+    std::string werr;
+    int wcode = GG_OK;
+    int dev = pk->device;
+    std::thread worker([&] {
+        try {
+            GG_HIP(hipSetDevice(dev));
+            double a = now_ms();
+            compute_h_device(pk->dom, A, B, C, A, pk->s1);
+            GG_HIP(hipStreamSynchronize(pk->s1));
+            double b = now_ms();
+            t_h = b - a;
+            if (h_dev_out) GG_HIP(hipMemcpyAsync(h_dev_out, A, nbytes, hipMemcpyDeviceToDevice, pk->s1));
+            if (n > 1) msm_device(pk->Z, A, &jz, pk->s1);
+            t_z = now_ms() - b;
+        } catch (const Error& e) {
+            werr = e.what();
+            wcode = e.code;
+        } catch (const std::exception& e) {
+            werr = e.what();
+            wcode = GG_ERR_INTERNAL;
+        }
+    });
+
+    G1Jac ja, jb, jk;
+    G2Jac j2;
+    double ta = now_ms();
+    try {
+        msm_device(pk->A, wdev, &ja, pk->s0);
+        double tb = now_ms();
+        msm_device(pk->B, wdev, &jb, pk->s0);
+        double tk = now_ms();
+        msm_device(pk->K, wdev, &jk, pk->s0);
+        double t2 = now_ms();
+        msm_device(pk->B2, wdev, &j2, pk->s0);
+        double te = now_ms();
+        g_timings[2] = tb - ta;
+        g_timings[3] = tk - tb;
+        g_timings[4] = t2 - tk;
+        g_timings[6] = te - t2;
+    } catch (...) {
+        worker.join();
+        throw;
+    }
+    worker.join();
+    if (wcode != GG_OK) throw Error(wcode, werr);
+    double tep = now_ms();
+
+    // epilogue (prove.go:206-299)
+    G1Jac rd = f_rd.get(), sd = f_sd.get(), krd = f_krd.get();
+    G2Jac sd2 = f_sd2.get();
+    G1Jac ar = jac_add(jac_add_affine(ja, pk->alpha), rd);
+    G1Jac bs1 = jac_add(jac_add_affine(jb, pk->beta), sd);
+    auto f_sar = std::async(std::launch::async, [&] { return jac_mul(ar, sc.v); });
+    G1Jac rbs = jac_mul(bs1, rc.v);
+    G1Jac krs = jac_add(jac_add(jk, krd), jz);
+    krs = jac_add(krs, f_sar.get());
+    krs = jac_add(krs, rbs);
+    G2Jac bs = jac_add_affine(jac_add(j2, sd2), pk->beta2);
+    G1Affine o_ar = jac_to_affine(ar), o_krs = jac_to_affine(krs);
+    G2Affine o_bs = jac_to_affine(bs);
+    memcpy(ar_aff, &o_ar, 64);
+    memcpy(krs_aff, &o_krs, 64);
+    memcpy(bs_aff, &o_bs, 128);
+    double tend = now_ms();
+    g_timings[0] = t_up - t0;
+    g_timings[1] = t_h;
+    g_timings[5] = t_z;
+    g_timings[7] = tend - tep;
+    g_timings[8] = tend - t0;
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_last_timings(double* ms9) {
+    GG_CAPI_BEGIN
+    GG_CHECK(ms9, GG_ERR_INVALID_ARG, "null argument");
+    memcpy(ms9, g_timings, sizeof(g_timings));
+    GG_CAPI_END
+}

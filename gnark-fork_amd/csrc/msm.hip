@@ -1,0 +1,79 @@
+// C ABI of the MSM engine (see msm_impl.cuh for the algorithm).
+#include "msm_impl.cuh"
+
+namespace gg {
+void create_base_g1(gg_msm_base* b, const void* points, size_t n, int on_device,
+                    const uint32_t* sidx, int window_bits);
+void create_base_g2(gg_msm_base* b, const void* points, size_t n, int on_device,
+                    const uint32_t* sidx, int window_bits);
+void msm_run_g1(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st);
+void msm_run_g2(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st);
+}  // namespace gg
+
+using namespace gg;
+
+extern "C" int gg_msm_base_create(int group, const void* points, size_t n, int points_on_device,
+                                  const uint32_t* scalar_index, int window_bits,
+                                  gg_msm_base_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out, GG_ERR_INVALID_ARG, "null out");
+    GG_CHECK(group == GG_G1 || group == GG_G2, GG_ERR_INVALID_ARG, "group must be GG_G1 or GG_G2");
+    GG_CHECK(n == 0 || points, GG_ERR_INVALID_ARG, "null points");
+    GG_CHECK(n < 0x80000000ull, GG_ERR_INVALID_ARG, "n too large");
+    std::unique_ptr<gg_msm_base> b(new gg_msm_base());
+    b->group = group;
+    if (group == GG_G1) create_base_g1(b.get(), points, n, points_on_device, scalar_index, window_bits);
+    else create_base_g2(b.get(), points, n, points_on_device, scalar_index, window_bits);
+    *out = b.release();
+    GG_CAPI_END
+}
+
+extern "C" int gg_msm_base_release(gg_msm_base_t b) {
+    GG_CAPI_BEGIN
+    delete b;
+    GG_CAPI_END
+}
+
+extern "C" int gg_msm_base_info(gg_msm_base_t b, size_t* n_points, int* window_bits, int* n_windows) {
+    GG_CAPI_BEGIN
+    GG_CHECK(b, GG_ERR_INVALID_ARG, "null base");
+    if (n_points) *n_points = b->n;
+    if (window_bits) *window_bits = b->c;
+    if (n_windows) *n_windows = b->W;
+    GG_CAPI_END
+}
+
+namespace gg {
+static void msm_device_locked(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
+    if (b->group == GG_G1) msm_run_g1(b, scalars_dev, out_jac, st);
+    else msm_run_g2(b, scalars_dev, out_jac, st);
+}
+// used by the Groth16 prover as well
+void msm_device(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(b->mu);
+    msm_device_locked(b, scalars_dev, out_jac, st);
+}
+size_t msm_scalars_needed(gg_msm_base* b) {
+    return b->has_sidx ? (b->n ? (size_t)b->max_sidx + 1 : 0) : b->n;
+}
+}  // namespace gg
+
+extern "C" int gg_msm(gg_msm_base_t b, const void* scalars, size_t n_scalars, int scalars_on_device,
+                      void* out_jac, void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(b && out_jac, GG_ERR_INVALID_ARG, "null argument");
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : hipStreamPerThread;
+    size_t need = msm_scalars_needed(b);
+    GG_CHECK(n_scalars >= need, GG_ERR_INVALID_ARG,
+             "scalar vector shorter than the points/index map require");
+    GG_CHECK(need == 0 || scalars, GG_ERR_INVALID_ARG, "null scalars");
+    std::lock_guard<std::mutex> lk(b->mu);
+    const Fr* sdev = (const Fr*)scalars;
+    if (!scalars_on_device && need) {
+        b->scal.reserve(need * 32);
+        GG_HIP(hipMemcpyAsync(b->scal.p, scalars, need * 32, hipMemcpyHostToDevice, st));
+        sdev = b->scal.as<Fr>();
+    }
+    msm_device_locked(b, sdev, out_jac, st);
+    GG_CAPI_END
+}

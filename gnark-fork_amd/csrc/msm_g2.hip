@@ -1,0 +1,13 @@
+// G2 instantiation of the bucket MSM (separate TU for build parallelism).
+#include "msm_impl.cuh"
+
+namespace gg {
+void create_base_g2(gg_msm_base* b, const void* points, size_t n, int on_device,
+                      const uint32_t* sidx, int window_bits) {
+    create_base<Fp2>(b, points, n, on_device, sidx, window_bits);
+}
+void msm_run_g2(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
+    G2Jac j = xyzz_to_jac(msm_run<Fp2>(b, scalars_dev, st));
+    memcpy(out_jac, &j, sizeof(j));
+}
+}  // namespace gg

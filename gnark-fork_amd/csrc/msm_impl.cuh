@@ -1,0 +1,399 @@
+#pragma once
+// (shared by msm_g1.hip / msm_g2.hip)
+// Pippenger bucket MSM over BN254 G1 / G2 for gfx950.
+//
+// Replaces G1Jac/G2Jac.MultiExp (prove.go:201-290) and iciclegnark
+// MsmOnDevice / MsmG2OnDevice (icicle.go:302-382).
+//
+// Design (DESIGN.md "MSM"):
+//  * Fixed-base precomputation, sized for 288 GB HBM: at base creation every
+//    point P_i is stored with its window shifts 2^(c*w) * P_i (affine,
+//    w < W = ceil(255/c)).  All W windows then share ONE set of 2^(c-1)
+//    buckets: no per-window bucket reduction, no Horner doubling chain.
+//  * Signed c-bit digits (|d| <= 2^(c-1)); entry (w, i, sign) goes to bucket |d|-1.
+//  * Counting sort by bucket: histogram (atomics) -> exclusive scan -> scatter.
+//  * Bucket accumulation as a segmented reduction that is immune to skewed
+//    scalars (real witnesses are mostly 0/1): every bucket is cut into work
+//    items of <= K entries, one thread per item, mixed XYZZ additions; then
+//    the per-bucket partials are summed the same way until one remains.
+//  * Bucket reduction sum_b (b+1) S_b: one thread per segment of buckets with
+//    a running sum, plus a double-and-add shift, then a tree sum.
+#include "common.h"
+#include "curve.cuh"
+#include "prof.h"
+#include <mutex>
+#include <vector>
+#include <algorithm>
+#include <memory>
+#include <cstring>
+
+namespace gg {
+
+// ------------------------------------------------------------------ loads
+template <class T>
+__device__ __forceinline__ T ld(const T* p) {
+    static_assert(sizeof(T) % 16 == 0, "16B multiple");
+    T r;
+    const uint4* s = reinterpret_cast<const uint4*>(p);
+    uint4* d = reinterpret_cast<uint4*>(&r);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 16); i++) d[i] = s[i];
+    return r;
+}
+template <class T>
+__device__ __forceinline__ void st(T* p, const T& v) {
+    uint4* d = reinterpret_cast<uint4*>(p);
+    const uint4* s = reinterpret_cast<const uint4*>(&v);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 16); i++) d[i] = s[i];
+}
+
+// ---- non-template kernels (msm_common.hip)
+__global__ void k_scan_block(const uint32_t* in, uint32_t* out, uint32_t* sums, size_t n);
+__global__ void k_scan_add(uint32_t* out, const uint32_t* sums, size_t n);
+__global__ void k_set_total(uint32_t* out, const uint32_t* in, size_t n);
+__global__ void k_digits(const Fr* scalars, const uint32_t* sidx, size_t n, int c, int W,
+                         int32_t* digits, uint32_t* counts);
+__global__ void k_scatter(const int32_t* digits, size_t total, uint32_t* cursor, uint32_t* sorted);
+__global__ void k_item_counts(const uint32_t* offsets, size_t nb, int K, uint32_t* itemcnt,
+                              uint32_t* maxcnt);
+__global__ void k_item_buckets(const uint32_t* item_off, size_t nb, uint32_t* item_bucket);
+void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, hipStream_t st,
+                    std::vector<DevBuf>& tmp, int depth = 0);
+int choose_c(size_t n, size_t point_bytes);
+
+// level 1: sum up to K affine points of one bucket into an XYZZ partial
+template <class F>
+__global__ void __launch_bounds__(256) k_accum_affine(const Affine<F>* pts, const uint32_t* sorted,
+                                                      const uint32_t* offsets,
+                                                      const uint32_t* item_off,
+                                                      const uint32_t* item_bucket, size_t n_items,
+                                                      int K, Xyzz<F>* partial) {
+    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_items) return;
+    uint32_t b = item_bucket[t];
+    uint32_t j = (uint32_t)t - item_off[b];
+    uint32_t lo = offsets[b] + j * (uint32_t)K;
+    uint32_t hi = min(offsets[b + 1], lo + (uint32_t)K);
+    Xyzz<F> acc = Xyzz<F>::inf();
+    for (uint32_t e = lo; e < hi; e++) {
+        uint32_t v = sorted[e];
+        Affine<F> p = ld(pts + (v & 0x7fffffffu));
+        if (v >> 31) p.y = -p.y;
+        acc = xyzz_madd(acc, p);
+    }
+    st(partial + t, acc);
+}
+
+// level >= 2: sum up to K XYZZ partials of one bucket
+template <class F>
+__global__ void __launch_bounds__(256) k_accum_xyzz(const Xyzz<F>* in, const uint32_t* offsets,
+                                                    const uint32_t* item_off,
+                                                    const uint32_t* item_bucket, size_t n_items,
+                                                    int K, Xyzz<F>* partial) {
+    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_items) return;
+    uint32_t b = item_bucket[t];
+    uint32_t j = (uint32_t)t - item_off[b];
+    uint32_t lo = offsets[b] + j * (uint32_t)K;
+    uint32_t hi = min(offsets[b + 1], lo + (uint32_t)K);
+    Xyzz<F> acc = ld(in + lo);
+    for (uint32_t e = lo + 1; e < hi; e++) acc = xyzz_add(acc, ld(in + e));
+    st(partial + t, acc);
+}
+
+// segment running sums: V_s = sum_{b in seg} (b+1) * S_b
+template <class F>
+__global__ void __launch_bounds__(256) k_bucket_reduce(const Xyzz<F>* partial,
+                                                       const uint32_t* item_off, size_t nb,
+                                                       int seg_len, Xyzz<F>* out) {
+    size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t lo = s * (size_t)seg_len;
+    if (lo >= nb) return;
+    size_t hi = min(nb, lo + (size_t)seg_len);
+    Xyzz<F> run = Xyzz<F>::inf(), tot = Xyzz<F>::inf();
+    for (size_t b = hi; b-- > lo;) {
+        uint32_t o = item_off[b];
+        if (item_off[b + 1] > o) run = xyzz_add(run, ld(partial + o));
+        tot = xyzz_add(tot, run);
+    }
+    // tot += lo * run   (double-and-add, lo < 2^31)
+    if (lo && !run.is_inf()) {
+        Xyzz<F> acc = Xyzz<F>::inf();
+        int top = 31 - __clz((int)lo);
+        for (int bit = top; bit >= 0; bit--) {
+            acc = acc.is_inf() ? acc : xyzz_dbl(acc);
+            if ((lo >> bit) & 1) acc = xyzz_add(acc, run);
+        }
+        tot = xyzz_add(tot, acc);
+    }
+    st(out + s, tot);
+}
+
+template <class F>
+__global__ void __launch_bounds__(256) k_sum_groups(const Xyzz<F>* in, size_t n, int G, Xyzz<F>* out) {
+    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t lo = t * (size_t)G;
+    if (lo >= n) return;
+    size_t hi = min(n, lo + (size_t)G);
+    Xyzz<F> acc = ld(in + lo);
+    for (size_t e = lo + 1; e < hi; e++) acc = xyzz_add(acc, ld(in + e));
+    st(out + t, acc);
+}
+
+// ------------------------------------------------------------ precompute
+template <class F>
+__global__ void k_pre_init(const Affine<F>* in, size_t n, Affine<F>* out0, Xyzz<F>* cur) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Affine<F> p = ld(in + i);
+    st(out0 + i, p);
+    st(cur + i, Xyzz<F>{p.x, p.y, F::one(), F::one()});
+}
+
+template <class F>
+__global__ void __launch_bounds__(256) k_pre_dbl(Xyzz<F>* cur, size_t n, int c) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Xyzz<F> p = ld(cur + i);
+    for (int k = 0; k < c; k++) p = xyzz_dbl(p);
+    st(cur + i, p);
+}
+
+// batch-normalize XYZZ -> affine: thread t owns elements t, t+T, t+2T, ... (M of them)
+template <class F>
+__global__ void __launch_bounds__(256) k_pre_normalize(const Xyzz<F>* cur, size_t n, size_t T,
+                                                       F* prefix, Affine<F>* out) {
+    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    F acc = F::one();
+    for (size_t i = t; i < n; i += T) {
+        st(prefix + i, acc);
+        acc = acc * ld(cur + i).zzz;
+    }
+    F inv = inverse(acc);
+    size_t last = t + ((n - 1 - t) / T) * T;
+    for (size_t i = last;; i -= T) {
+        Xyzz<F> p = ld(cur + i);
+        F izzz = inv * ld(prefix + i);  // 1/ZZZ_i
+        inv = inv * p.zzz;
+        F izz = sqr(izzz) * sqr(p.zz);  // lambda^-6 * lambda^4 = 1/ZZ
+        st(out + i, Affine<F>{p.x * izz, p.y * izzz});
+        if (i < T) break;
+    }
+}
+
+}  // namespace gg
+
+using gg::DevBuf;
+struct gg_msm_base {
+    int group = GG_G1;
+    size_t n = 0;  // resident points
+    int c = 0, W = 0;
+    size_t nb = 0;
+    DevBuf pts;   // W * n affine points, window-major
+    DevBuf sidx;  // n u32 or empty
+    bool has_sidx = false;
+    uint32_t max_sidx = 0;
+    std::mutex mu;
+    // scratch
+    DevBuf digits, sorted, counts, offsets, cursor, itemcnt, item_off, item_bucket, maxcnt;
+    DevBuf partA, partB, segs, segs2, scal;
+    std::vector<DevBuf> scan_tmp;
+};
+
+namespace gg {
+
+template <class F>
+inline void precompute(gg_msm_base* b, const Affine<F>* dev_in, hipStream_t st) {
+    const size_t n = b->n;
+    b->pts.alloc((size_t)b->W * n * sizeof(Affine<F>));
+    Affine<F>* out = b->pts.as<Affine<F>>();
+    DevBuf cur(n * sizeof(Xyzz<F>));
+    // ~64 elements per thread amortise one Fermat inversion, >= 16K threads
+    const size_t T = std::min<size_t>(n, std::max<size_t>(16384, n / 64));
+    DevBuf prefix(n * sizeof(F));
+    hipLaunchKernelGGL(k_pre_init<F>, dim3(grid_for(n, 256)), dim3(256), 0, st, dev_in, n, out,
+                       cur.as<Xyzz<F>>());
+    GG_HIP(hipGetLastError());
+    for (int w = 1; w < b->W; w++) {
+        hipLaunchKernelGGL(k_pre_dbl<F>, dim3(grid_for(n, 256)), dim3(256), 0, st,
+                           cur.as<Xyzz<F>>(), n, b->c);
+        GG_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_pre_normalize<F>, dim3(grid_for(T, 256)), dim3(256), 0, st,
+                           (const Xyzz<F>*)cur.p, n, T, prefix.as<F>(), out + (size_t)w * n);
+        GG_HIP(hipGetLastError());
+    }
+    GG_HIP(hipStreamSynchronize(st));
+}
+
+template <class F>
+inline Xyzz<F> msm_run(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st) {
+    const size_t n = b->n, nb = b->nb;
+    const int c = b->c, W = b->W;
+    const size_t total = (size_t)W * n;
+    if (n == 0) return Xyzz<F>::inf();
+    b->digits.reserve(total * 4);
+    b->sorted.reserve(total * 4);
+    b->counts.reserve(nb * 4);
+    b->offsets.reserve((nb + 1) * 4);
+    b->cursor.reserve(nb * 4);
+    b->itemcnt.reserve(nb * 4);
+    b->item_off.reserve((nb + 1) * 4);
+    b->maxcnt.reserve(4);
+
+    ProfScope ps_sort("msm_sort", st, (double)n);
+    GG_HIP(hipMemsetAsync(b->counts.p, 0, nb * 4, st));
+    hipLaunchKernelGGL(k_digits, dim3(grid_for(n, 256)), dim3(256), 0, st, scalars_dev,
+                       b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W,
+                       b->digits.as<int32_t>(), b->counts.as<uint32_t>());
+    GG_HIP(hipGetLastError());
+    exclusive_scan(b->counts.as<uint32_t>(), b->offsets.as<uint32_t>(), nb, st, b->scan_tmp);
+    hipLaunchKernelGGL(k_set_total, dim3(1), dim3(1), 0, st, b->offsets.as<uint32_t>(),
+                       b->counts.as<uint32_t>(), nb);
+    GG_HIP(hipMemcpyAsync(b->cursor.p, b->offsets.p, nb * 4, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(k_scatter, dim3(grid_for(total, 256)), dim3(256), 0, st,
+                       b->digits.as<int32_t>(), total, b->cursor.as<uint32_t>(),
+                       b->sorted.as<uint32_t>());
+    GG_HIP(hipGetLastError());
+    ps_sort.stop(st);
+
+    // ---- level 1: affine entries -> partials
+    const int K1 = 32, K2 = 16;
+    uint32_t* offsets = b->offsets.as<uint32_t>();
+    uint32_t host[2];
+    GG_HIP(hipMemsetAsync(b->maxcnt.p, 0, 4, st));
+    hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nb, 256)), dim3(256), 0, st, offsets, nb, K1,
+                       b->itemcnt.as<uint32_t>(), b->maxcnt.as<uint32_t>());
+    GG_HIP(hipGetLastError());
+    exclusive_scan(b->itemcnt.as<uint32_t>(), b->item_off.as<uint32_t>(), nb, st, b->scan_tmp);
+    hipLaunchKernelGGL(k_set_total, dim3(1), dim3(1), 0, st, b->item_off.as<uint32_t>(),
+                       b->itemcnt.as<uint32_t>(), nb);
+    GG_HIP(hipMemcpyAsync(&host[0], b->item_off.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipMemcpyAsync(&host[1], b->maxcnt.p, 4, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipStreamSynchronize(st));
+    size_t n_items = host[0];
+    uint32_t max_items = host[1];
+    b->item_bucket.reserve((n_items + 1) * 4);
+    b->partA.reserve((n_items + 1) * sizeof(Xyzz<F>));
+    if (n_items) {
+        hipLaunchKernelGGL(k_item_buckets, dim3(grid_for(nb, 256)), dim3(256), 0, st,
+                           b->item_off.as<uint32_t>(), nb, b->item_bucket.as<uint32_t>());
+        GG_HIP(hipGetLastError());
+        ProfScope ps_acc("msm_accum", st, (double)n);
+        hipLaunchKernelGGL(k_accum_affine<F>, dim3(grid_for(n_items, 256)), dim3(256), 0, st,
+                           (const Affine<F>*)b->pts.p, b->sorted.as<uint32_t>(), offsets,
+                           b->item_off.as<uint32_t>(), b->item_bucket.as<uint32_t>(), n_items,
+                           K1, b->partA.as<Xyzz<F>>());
+        GG_HIP(hipGetLastError());
+        ps_acc.stop(st);
+    }
+    // ---- levels >= 2 until every bucket has <= 1 partial
+    // bucket b's partials: partA[item_off[b] .. item_off[b+1])
+    DevBuf* cur_part = &b->partA;
+    DevBuf* nxt_part = &b->partB;
+    ProfScope ps_acc2("msm_accum2", st, (double)n);
+    while (max_items > 1) {
+        // offsets <- item_off (partials are contiguous per bucket)
+        GG_HIP(hipMemcpyAsync(b->offsets.p, b->item_off.p, (nb + 1) * 4, hipMemcpyDeviceToDevice, st));
+        GG_HIP(hipMemsetAsync(b->maxcnt.p, 0, 4, st));
+        hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nb, 256)), dim3(256), 0, st, offsets, nb,
+                           K2, b->itemcnt.as<uint32_t>(), b->maxcnt.as<uint32_t>());
+        GG_HIP(hipGetLastError());
+        exclusive_scan(b->itemcnt.as<uint32_t>(), b->item_off.as<uint32_t>(), nb, st, b->scan_tmp);
+        hipLaunchKernelGGL(k_set_total, dim3(1), dim3(1), 0, st, b->item_off.as<uint32_t>(),
+                           b->itemcnt.as<uint32_t>(), nb);
+        GG_HIP(hipMemcpyAsync(&host[0], b->item_off.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
+        GG_HIP(hipMemcpyAsync(&host[1], b->maxcnt.p, 4, hipMemcpyDeviceToHost, st));
+        GG_HIP(hipStreamSynchronize(st));
+        n_items = host[0];
+        max_items = host[1];
+        b->item_bucket.reserve((n_items + 1) * 4);
+        nxt_part->reserve((n_items + 1) * sizeof(Xyzz<F>));
+        hipLaunchKernelGGL(k_item_buckets, dim3(grid_for(nb, 256)), dim3(256), 0, st,
+                           b->item_off.as<uint32_t>(), nb, b->item_bucket.as<uint32_t>());
+        GG_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_accum_xyzz<F>, dim3(grid_for(n_items, 256)), dim3(256), 0, st,
+                           (const Xyzz<F>*)cur_part->p, offsets, b->item_off.as<uint32_t>(),
+                           b->item_bucket.as<uint32_t>(), n_items, K2, nxt_part->as<Xyzz<F>>());
+        GG_HIP(hipGetLastError());
+        std::swap(cur_part, nxt_part);
+    }
+    ps_acc2.stop(st);
+    // ---- bucket reduction
+    ProfScope ps_red("msm_reduce", st, (double)nb);
+    const int SEG = 32;
+    size_t nseg = (nb + SEG - 1) / SEG;
+    b->segs.reserve(nseg * sizeof(Xyzz<F>));
+    b->segs2.reserve(nseg * sizeof(Xyzz<F>));
+    hipLaunchKernelGGL(k_bucket_reduce<F>, dim3(grid_for(nseg, 256)), dim3(256), 0, st,
+                       (const Xyzz<F>*)cur_part->p, b->item_off.as<uint32_t>(), nb, SEG,
+                       b->segs.as<Xyzz<F>>());
+    GG_HIP(hipGetLastError());
+    DevBuf* a = &b->segs;
+    DevBuf* o = &b->segs2;
+    size_t m = nseg;
+    const int G = 16;
+    while (m > 1) {
+        size_t mo = (m + G - 1) / G;
+        hipLaunchKernelGGL(k_sum_groups<F>, dim3(grid_for(mo, 256)), dim3(256), 0, st,
+                           (const Xyzz<F>*)a->p, m, G, o->as<Xyzz<F>>());
+        GG_HIP(hipGetLastError());
+        std::swap(a, o);
+        m = mo;
+    }
+    ps_red.stop(st);
+    Xyzz<F> res;
+    GG_HIP(hipMemcpyAsync(&res, a->p, sizeof(res), hipMemcpyDeviceToHost, st));
+    GG_HIP(hipStreamSynchronize(st));
+    return res;
+}
+
+template <class F>
+inline void create_base(gg_msm_base* b, const void* points, size_t n, int on_device,
+                        const uint32_t* sidx, int window_bits) {
+    const size_t pb = sizeof(Affine<F>);
+    std::vector<uint8_t> host;
+    const uint8_t* src;
+    if (on_device) {
+        host.resize(n * pb);
+        if (n) GG_HIP(hipMemcpy(host.data(), points, n * pb, hipMemcpyDeviceToHost));
+        src = host.data();
+    } else {
+        src = (const uint8_t*)points;
+    }
+    // drop infinity points, build the scalar index map
+    std::vector<uint8_t> keep;
+    keep.reserve(n * pb);
+    std::vector<uint32_t> idx;
+    idx.reserve(n);
+    bool dropped = false;
+    static const uint8_t zero[128] = {0};
+    for (size_t i = 0; i < n; i++) {
+        const uint8_t* p = src + i * pb;
+        if (memcmp(p, zero, pb) == 0) { dropped = true; continue; }
+        keep.insert(keep.end(), p, p + pb);
+        idx.push_back(sidx ? sidx[i] : (uint32_t)i);
+    }
+    b->n = idx.size();
+    b->has_sidx = dropped || sidx != nullptr;
+    b->max_sidx = 0;
+    for (uint32_t v : idx) b->max_sidx = std::max(b->max_sidx, v);
+    b->c = window_bits ? window_bits : choose_c(std::max<size_t>(b->n, 1), pb);
+    GG_CHECK(b->c >= 2 && b->c <= 24, GG_ERR_INVALID_ARG, "window_bits out of range [2, 24]");
+    b->W = (255 + b->c - 1) / b->c;
+    b->nb = (size_t)1 << (b->c - 1);
+    GG_CHECK((double)b->W * (double)b->n < 2147483648.0, GG_ERR_UNSUPPORTED,
+             "too many points x windows for 31-bit entry ids");
+    if (b->has_sidx) {
+        b->sidx.alloc(std::max<size_t>(b->n, 1) * 4);
+        if (b->n) GG_HIP(hipMemcpy(b->sidx.p, idx.data(), b->n * 4, hipMemcpyHostToDevice));
+    }
+    if (b->n == 0) return;
+    DevBuf tmp(b->n * pb);
+    GG_HIP(hipMemcpy(tmp.p, keep.data(), b->n * pb, hipMemcpyHostToDevice));
+    precompute<F>(b, tmp.as<Affine<F>>(), hipStreamPerThread);
+}
+
+}  // namespace gg
+

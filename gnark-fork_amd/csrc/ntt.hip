@@ -1,0 +1,421 @@
+// Radix-2 NTT over BN254 Fr for gfx950 with gnark-crypto's FFT conventions
+// (backend/groth16/bn254/prove.go:369-393 call sites; gnark-crypto fft [ext]):
+//   DIF: natural order in -> bit-reversed out;  DIT: bit-reversed in -> natural out.
+//
+// Layout / schedule (DESIGN.md "NTT"):
+//   * the 2^L vector lives in HBM as gnark fr.Element (32 B, Montgomery);
+//   * a transform is split into P passes; each pass owns k consecutive bit
+//     positions (butterfly spans) and moves tiles of 2^k x 2^tl elements
+//     (<= 2048 = 64 KiB) through LDS, running its k butterfly stages there;
+//     strided passes load 2^tl adjacent elements per row (256-B segments);
+//   * twiddles w^i (i < n/2) are a resident HBM table (256 MiB at 2^24);
+//   * coset / 1/n / den scalings are fused into the first or last pass as
+//     multiplication by hi[e >> S] * lo[e & (2^S-1)], e = i or bitrev(i),
+//     from two 2^(L/2)-entry tables (no n-sized coset tables);
+//   * computeH fuses PolyOps (a*b - c) into c's last coset-NTT pass and folds
+//     den = 1/(g^n - 1) into the final inverse-transform scaling.
+#include "common.h"
+#include "field.cuh"
+#include "prof.h"
+#include <vector>
+#include <mutex>
+#include <memory>
+#include <algorithm>
+#include <cstring>
+
+namespace gg {
+
+enum ScaleKind {
+    SK_G_NAT = 0,       // g^i
+    SK_G_BR = 1,        // g^bitrev(i)
+    SK_GINV_NAT_N = 2,  // g^-i / n
+    SK_GINV_BR_N = 3,   // g^-bitrev(i) / n
+    SK_NINV = 4,        // 1/n
+    SK_H_FWD = 5,       // g^bitrev(i) / n          (computeH: iFFT -> coset FFT)
+    SK_H_INV = 6,       // den * g^-bitrev(i) / n   (computeH: final coset iFFT)
+    SK_COUNT = 7
+};
+
+struct ScaleSpec {
+    const Fr* hi;  // 2^(L-S) entries (constant folded in)
+    const Fr* lo;  // 2^S entries
+    int shift;     // S
+    int bitrev;    // index by bitrev(i) instead of i
+};
+
+struct PassParams {
+    const Fr* in;
+    Fr* out;
+    const Fr* tw;
+    int log_n;
+    int b_lo;
+    int k;
+    int tl;
+    int dit;
+    int has_pre;
+    ScaleSpec pre;
+    int has_post;
+    ScaleSpec post;
+    int epi_mul_sub;  // out = ea*eb - x
+    const Fr* ea;
+    const Fr* eb;
+};
+
+__device__ __forceinline__ uint32_t brev_bits(uint32_t i, int L) {
+    return L ? (__brev(i) >> (32 - L)) : 0u;
+}
+
+__device__ __forceinline__ Fr load_fr(const Fr* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    uint4 a = q[0], b = q[1];
+    Fr r;
+    r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+    r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+    return r;
+}
+
+__device__ __forceinline__ void store_fr(Fr* p, const Fr& r) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    q[0] = make_uint4(r.v[0], r.v[1], r.v[2], r.v[3]);
+    q[1] = make_uint4(r.v[4], r.v[5], r.v[6], r.v[7]);
+}
+
+__device__ __forceinline__ Fr apply_scale(const ScaleSpec& s, uint32_t g, int L, const Fr& x) {
+    uint32_t e = s.bitrev ? brev_bits(g, L) : g;
+    Fr f = load_fr(s.hi + (e >> s.shift));
+    if (s.lo) f = f * load_fr(s.lo + (e & ((1u << s.shift) - 1)));
+    return x * f;
+}
+
+// LDS tile stored limb-major: lds[l * T + e]
+__device__ __forceinline__ Fr lds_get(const uint32_t* lds, int T, int e) {
+    Fr r;
+#pragma unroll
+    for (int l = 0; l < 8; l++) r.v[l] = lds[l * T + e];
+    return r;
+}
+__device__ __forceinline__ void lds_put(uint32_t* lds, int T, int e, const Fr& x) {
+#pragma unroll
+    for (int l = 0; l < 8; l++) lds[l * T + e] = x.v[l];
+}
+
+__global__ void __launch_bounds__(256) k_ntt_pass(PassParams P) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int k = P.k, tl = P.tl;
+    const int T = 1 << (k + tl);
+    const uint32_t tl_mask = (1u << tl) - 1;
+    const int nlo_log = P.b_lo - tl;
+    const uint32_t tile = blockIdx.x;
+    const uint32_t lob = tile & ((1u << nlo_log) - 1);
+    const uint32_t hi = tile >> nlo_log;
+    const uint32_t base_hi = hi << (P.b_lo + k);
+    const uint32_t lo0 = lob << tl;
+
+    for (int e = threadIdx.x; e < T; e += blockDim.x) {
+        uint32_t j = (uint32_t)e >> tl, lol = (uint32_t)e & tl_mask;
+        uint32_t g = base_hi | (j << P.b_lo) | (lo0 + lol);
+        Fr x = load_fr(P.in + g);
+        if (P.has_pre) x = apply_scale(P.pre, g, P.log_n, x);
+        lds_put(lds, T, e, x);
+    }
+    __syncthreads();
+
+    const int half = T >> 1;
+    for (int st = 0; st < k; st++) {
+        const int q = P.dit ? st : (k - 1 - st);
+        const int b = P.b_lo + q;
+        const uint32_t qmask = (1u << q) - 1;
+        const uint32_t bmask = (1u << b) - 1;
+        const int tshift = P.log_n - 1 - b;
+        for (int u = threadIdx.x; u < half; u += blockDim.x) {
+            uint32_t lol = (uint32_t)u & tl_mask;
+            uint32_t jj = (uint32_t)u >> tl;
+            uint32_t j = ((jj >> q) << (q + 1)) | (jj & qmask);
+            int e0 = (int)((j << tl) | lol);
+            int e1 = e0 + (1 << (q + tl));
+            uint32_t g0 = base_hi | (j << P.b_lo) | (lo0 + lol);
+            uint32_t texp = (g0 & bmask) << tshift;
+            Fr x0 = lds_get(lds, T, e0);
+            Fr x1 = lds_get(lds, T, e1);
+            if (P.dit) {
+                Fr t = (texp == 0) ? x1 : x1 * load_fr(P.tw + texp);
+                lds_put(lds, T, e0, x0 + t);
+                lds_put(lds, T, e1, x0 - t);
+            } else {
+                Fr d = x0 - x1;
+                lds_put(lds, T, e0, x0 + x1);
+                lds_put(lds, T, e1, (texp == 0) ? d : d * load_fr(P.tw + texp));
+            }
+        }
+        __syncthreads();
+    }
+
+    for (int e = threadIdx.x; e < T; e += blockDim.x) {
+        uint32_t j = (uint32_t)e >> tl, lol = (uint32_t)e & tl_mask;
+        uint32_t g = base_hi | (j << P.b_lo) | (lo0 + lol);
+        Fr x = lds_get(lds, T, e);
+        if (P.has_post) x = apply_scale(P.post, g, P.log_n, x);
+        if (P.epi_mul_sub) x = load_fr(P.ea + g) * load_fr(P.eb + g) - x;
+        store_fr(P.out + g, x);
+    }
+}
+
+// tw[i] = hi[i >> S] * lo[i & mask], i < count
+__global__ void k_power_table(Fr* out, size_t count, const Fr* hi, const Fr* lo, int S) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    Fr x = load_fr(hi + (i >> S)) * load_fr(lo + (i & ((1u << S) - 1)));
+    store_fr(out + i, x);
+}
+
+// ---------------------------------------------------------------------------
+struct Pass {
+    int b_lo, k, tl;
+};
+
+static std::vector<Pass> plan_passes(int L, bool dit) {
+    std::vector<Pass> v;
+    if (L <= 11) {
+        v.push_back({0, L, 0});
+        return v;
+    }
+    int P = 1 + (L - 11 + 7) / 8;
+    std::vector<int> ks(P, L / P);
+    for (int i = 0; i < L % P; i++) ks[i]++;  // ks[0] is the contiguous pass
+    // contiguous pass may take up to 11, strided passes up to 8
+    for (int i = 1; i < P; i++)
+        while (ks[i] > 8) { ks[i]--; ks[0]++; }
+    // build from the contiguous (b_lo = 0) pass upwards
+    std::vector<Pass> up;
+    int b = 0;
+    for (int i = 0; i < P; i++) {
+        int tl = (b == 0) ? 0 : std::min(3, b);
+        up.push_back({b, ks[i], tl});
+        b += ks[i];
+    }
+    if (dit) return up;  // DIT: low bits first
+    for (int i = P - 1; i >= 0; i--) v.push_back(up[i]);  // DIF: high bits first
+    return v;
+}
+
+}  // namespace gg
+
+using namespace gg;
+
+struct gg_domain {
+    int log_n = 0;
+    size_t n = 1;
+    Fr omega, omega_inv, g, g_inv, n_inv, den;
+    DevBuf tw, twinv;
+    int S = 0;
+    DevBuf scale_hi[SK_COUNT], scale_lo[SK_COUNT];
+    ScaleSpec spec[SK_COUNT];
+    DevBuf scratch;  // computeH b/c buffers
+    std::mutex mu;
+};
+
+namespace gg {
+
+static void build_pow_tables(int L, int S, const Fr& x, const Fr& c, std::vector<Fr>& hi,
+                             std::vector<Fr>& lo) {
+    size_t nlo = (size_t)1 << S, nhi = (size_t)1 << (L - S);
+    lo.resize(nlo);
+    hi.resize(nhi);
+    Fr acc = Fr::one();
+    for (size_t i = 0; i < nlo; i++) { lo[i] = acc; acc = acc * x; }
+    Fr step = acc;  // x^(2^S)
+    acc = c;
+    for (size_t i = 0; i < nhi; i++) { hi[i] = acc; acc = acc * step; }
+}
+
+static void upload(DevBuf& b, const std::vector<Fr>& v) {
+    b.alloc(v.size() * sizeof(Fr));
+    GG_HIP(hipMemcpy(b.p, v.data(), v.size() * sizeof(Fr), hipMemcpyHostToDevice));
+}
+
+static hipStream_t pick_stream(void* s) { return s ? (hipStream_t)s : hipStreamPerThread; }
+
+void run_transform(gg_domain* d, const Fr* in, Fr* out, bool dit, bool inverse_tw, int pre_kind,
+                   int post_kind, const Fr* ea, const Fr* eb, hipStream_t st) {
+    const int L = d->log_n;
+    auto passes = plan_passes(L, dit);
+    const Fr* src = in;
+    for (size_t pi = 0; pi < passes.size(); pi++) {
+        const Pass& ps = passes[pi];
+        PassParams P{};
+        P.in = src;
+        P.out = out;
+        P.tw = (const Fr*)(inverse_tw ? d->twinv.p : d->tw.p);
+        P.log_n = L;
+        P.b_lo = ps.b_lo;
+        P.k = ps.k;
+        P.tl = ps.tl;
+        P.dit = dit ? 1 : 0;
+        if (pi == 0 && pre_kind >= 0) { P.has_pre = 1; P.pre = d->spec[pre_kind]; }
+        bool last = (pi + 1 == passes.size());
+        if (last && post_kind >= 0) { P.has_post = 1; P.post = d->spec[post_kind]; }
+        if (last && ea) { P.epi_mul_sub = 1; P.ea = ea; P.eb = eb; }
+        int T = 1 << (ps.k + ps.tl);
+        unsigned tiles = (unsigned)(d->n / (size_t)T);
+        size_t lds = (size_t)T * 32;
+        ProfScope prof("ntt_pass", st, (double)d->n);
+        hipLaunchKernelGGL(k_ntt_pass, dim3(tiles), dim3(256), lds, st, P);
+        GG_HIP(hipGetLastError());
+        prof.stop(st);
+        src = out;
+    }
+}
+
+}  // namespace gg
+
+extern "C" int gg_domain_create(int log_n, const void* omega_mont, const void* coset_gen_mont,
+                                gg_domain_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out && omega_mont && coset_gen_mont, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(log_n >= 0 && log_n <= 28, GG_ERR_INVALID_ARG, "log_n out of range [0, 28]");
+    auto d = new gg_domain();
+    std::unique_ptr<gg_domain> guard(d);
+    d->log_n = log_n;
+    d->n = (size_t)1 << log_n;
+    memcpy(d->omega.v, omega_mont, 32);
+    memcpy(d->g.v, coset_gen_mont, 32);
+    // omega must have order exactly n
+    Fr x = d->omega;
+    for (int i = 0; i < log_n; i++) {
+        if (i == log_n - 1) GG_CHECK(!(x == Fr::one()), GG_ERR_INVALID_ARG, "omega order < n");
+        x = sqr(x);
+    }
+    GG_CHECK(x == Fr::one(), GG_ERR_INVALID_ARG, "omega^n != 1");
+    GG_CHECK(!d->g.is_zero(), GG_ERR_INVALID_ARG, "coset generator is zero");
+    d->omega_inv = inverse(d->omega);
+    d->g_inv = inverse(d->g);
+    Fr nn = to_mont(Fr{{(uint32_t)d->n, (uint32_t)((uint64_t)d->n >> 32), 0, 0, 0, 0, 0, 0}});
+    d->n_inv = inverse(nn);
+    Fr gn = pow_u64(d->g, d->n);
+    Fr t = gn - Fr::one();
+    GG_CHECK(!t.is_zero(), GG_ERR_INVALID_ARG, "g^n == 1: coset generator in the domain");
+    d->den = inverse(t);
+
+    const int L = log_n;
+    d->S = (L + 1) / 2;
+    const int S = d->S;
+    std::vector<Fr> hi, lo;
+    struct KindDef { Fr x, c; int br; };
+    KindDef defs[SK_COUNT] = {
+        {d->g, Fr::one(), 0},
+        {d->g, Fr::one(), 1},
+        {d->g_inv, d->n_inv, 0},
+        {d->g_inv, d->n_inv, 1},
+        {Fr::one(), d->n_inv, 0},
+        {d->g, d->n_inv, 1},
+        {d->g_inv, d->den * d->n_inv, 1},
+    };
+    for (int kd = 0; kd < SK_COUNT; kd++) {
+        build_pow_tables(L, S, defs[kd].x, defs[kd].c, hi, lo);
+        upload(d->scale_hi[kd], hi);
+        upload(d->scale_lo[kd], lo);
+        d->spec[kd] = ScaleSpec{(const Fr*)d->scale_hi[kd].p, (const Fr*)d->scale_lo[kd].p, S,
+                                defs[kd].br};
+    }
+    // twiddles w^i, i < n/2, generated on device from split tables
+    size_t half = d->n / 2;
+    if (half) {
+        DevBuf h1, l1;
+        build_pow_tables(L, S, d->omega, Fr::one(), hi, lo);
+        upload(h1, hi);
+        upload(l1, lo);
+        d->tw.alloc(half * 32);
+        hipLaunchKernelGGL(k_power_table, dim3(grid_for(half, 256)), dim3(256), 0, 0,
+                           d->tw.as<Fr>(), half, h1.as<Fr>(), l1.as<Fr>(), S);
+        GG_HIP(hipGetLastError());
+        build_pow_tables(L, S, d->omega_inv, Fr::one(), hi, lo);
+        DevBuf h2, l2;
+        upload(h2, hi);
+        upload(l2, lo);
+        d->twinv.alloc(half * 32);
+        hipLaunchKernelGGL(k_power_table, dim3(grid_for(half, 256)), dim3(256), 0, 0,
+                           d->twinv.as<Fr>(), half, h2.as<Fr>(), l2.as<Fr>(), S);
+        GG_HIP(hipGetLastError());
+        GG_HIP(hipDeviceSynchronize());
+    } else {
+        d->tw.alloc(32);
+        d->twinv.alloc(32);
+    }
+    *out = guard.release();
+    GG_CAPI_END
+}
+
+extern "C" int gg_domain_release(gg_domain_t d) {
+    GG_CAPI_BEGIN
+    delete d;
+    GG_CAPI_END
+}
+
+extern "C" int gg_domain_log_n(gg_domain_t d, int* log_n) {
+    GG_CAPI_BEGIN
+    GG_CHECK(d && log_n, GG_ERR_INVALID_ARG, "null argument");
+    *log_n = d->log_n;
+    GG_CAPI_END
+}
+
+extern "C" int gg_ntt(gg_domain_t d, void* data_dev, int inverse, int decimation, int coset,
+                      void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(d && data_dev, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(decimation == GG_DIF || decimation == GG_DIT, GG_ERR_INVALID_ARG, "bad decimation");
+    hipStream_t st = pick_stream(hip_stream);
+    bool dit = decimation == GG_DIT;
+    Fr* a = (Fr*)data_dev;
+    int pre = -1, post = -1;
+    if (!inverse) {
+        if (coset) pre = dit ? SK_G_BR : SK_G_NAT;
+    } else {
+        if (!coset) post = SK_NINV;
+        else post = dit ? SK_GINV_NAT_N : SK_GINV_BR_N;
+    }
+    run_transform(d, a, a, dit, inverse != 0, pre, post, nullptr, nullptr, st);
+    GG_CAPI_END
+}
+
+namespace gg {
+// computeH on device buffers A (becomes h), B, C, each 2^L fr (already padded)
+void compute_h_device(gg_domain* d, Fr* A, Fr* B, Fr* C, Fr* H, hipStream_t st) {
+    // a, b: iFFT(DIF) with g^br(i)/n folded in, then DIT FFT -> coset evaluations
+    run_transform(d, A, A, false, true, -1, SK_H_FWD, nullptr, nullptr, st);
+    run_transform(d, A, A, true, false, -1, -1, nullptr, nullptr, st);
+    run_transform(d, B, B, false, true, -1, SK_H_FWD, nullptr, nullptr, st);
+    run_transform(d, B, B, true, false, -1, -1, nullptr, nullptr, st);
+    run_transform(d, C, C, false, true, -1, SK_H_FWD, nullptr, nullptr, st);
+    // last pass of c's coset FFT emits a*b - c in place (PolyOps fused)
+    run_transform(d, C, C, true, false, -1, -1, A, B, st);
+    // coset iFFT (DIF) with den * g^-br(i) / n folded in -> h bit-reversed.
+    // H may alias A, B or C.
+    run_transform(d, C, H, false, true, -1, SK_H_INV, nullptr, nullptr, st);
+}
+}  // namespace gg
+
+extern "C" int gg_groth16_compute_h(gg_domain_t d, const void* a, const void* b, const void* c,
+                                    size_t len, int inputs_on_device, void* h_dev,
+                                    void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(d && a && b && c && h_dev, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(len <= d->n, GG_ERR_INVALID_ARG, "len > domain cardinality");
+    std::lock_guard<std::mutex> lk(d->mu);
+    hipStream_t st = pick_stream(hip_stream);
+    size_t nb = d->n * 32;
+    d->scratch.reserve(3 * nb);
+    char* base = (char*)d->scratch.p;
+    Fr* A = (Fr*)base;
+    Fr* B = (Fr*)(base + nb);
+    Fr* C = (Fr*)(base + 2 * nb);
+    hipMemcpyKind kind = inputs_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    const void* src[3] = {a, b, c};
+    Fr* dst[3] = {A, B, C};
+    for (int i = 0; i < 3; i++) {
+        if (len) GG_HIP(hipMemcpyAsync(dst[i], src[i], len * 32, kind, st));
+        if (len < d->n) GG_HIP(hipMemsetAsync((char*)dst[i] + len * 32, 0, nb - len * 32, st));
+    }
+    compute_h_device(d, A, B, C, (Fr*)h_dev, st);
+    GG_HIP(hipStreamSynchronize(st));
+    GG_CAPI_END
+}

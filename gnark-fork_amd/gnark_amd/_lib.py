@@ -1,0 +1,160 @@
+"""ctypes binding of libgnark_amd.so (include/gnark_amd.h).
+
+The HIP library is the product: there is no CPU fallback.  If the shared
+object is missing or cannot be loaded this module raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("GNARK_AMD_LIB", os.path.join(_PKG_DIR, "lib", "libgnark_amd.so"))
+
+GG_OK = 0
+GG_G1, GG_G2 = 1, 2
+GG_DIF, GG_DIT = 0, 1
+
+
+class GnarkAmdError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"gnark_amd error {code}: {msg}")
+        self.code = code
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libgnark_amd.so not found at {LIB_PATH}: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, S, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    PP = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "gg_last_error": ([], ctypes.c_char_p),
+        "gg_version": ([], I),
+        "gg_device_count": ([ctypes.POINTER(I)], I),
+        "gg_set_device": ([I], I),
+        "gg_malloc": ([PP, S], I),
+        "gg_free": ([P], I),
+        "gg_copy_to_device": ([P, P, S], I),
+        "gg_copy_to_host": ([P, P, S], I),
+        "gg_synchronize": ([], I),
+        "gg_domain_create": ([I, P, P, PP], I),
+        "gg_domain_release": ([P], I),
+        "gg_domain_log_n": ([P, ctypes.POINTER(I)], I),
+        "gg_ntt": ([P, P, I, I, I, P], I),
+        "gg_groth16_compute_h": ([P, P, P, P, S, I, P, P], I),
+        "gg_msm_base_create": ([I, P, S, I, P, I, PP], I),
+        "gg_msm_base_release": ([P], I),
+        "gg_msm_base_info": ([P, ctypes.POINTER(S), ctypes.POINTER(I), ctypes.POINTER(I)], I),
+        "gg_msm": ([P, P, S, I, P, P], I),
+        "gg_g1_jac_to_affine": ([P, P], I),
+        "gg_g2_jac_to_affine": ([P, P], I),
+        "gg_g1_jac_add": ([P, P, P], I),
+        "gg_g2_jac_add": ([P, P, P], I),
+        "gg_g1_scalar_mul": ([P, P, P], I),
+        "gg_g2_scalar_mul": ([P, P, P], I),
+        "gg_groth16_pk_create": ([I, P, P, P, S, P, S, P, S, P, S, P, P, P, P, P, P, P, P, S, S, P, PP], I),
+        "gg_groth16_pk_release": ([P], I),
+        "gg_groth16_prove": ([P, P, S, P, P, P, S, I, P, P, P, P, P, P], I),
+        "gg_groth16_last_timings": ([ctypes.POINTER(ctypes.c_double)], I),
+        "gg_batch_scalar_mul": ([I, P, P, S, I, P, I], I),
+        "gg_profile_enable": ([I], I),
+        "gg_profile_get": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                            ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)], I),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)  # AttributeError == missing export: fail loudly
+        fn.argtypes = args
+        fn.restype = res
+    return L
+
+
+lib = _load()
+EXPORTED = [
+    "gg_last_error", "gg_version", "gg_device_count", "gg_set_device", "gg_malloc", "gg_free",
+    "gg_copy_to_device", "gg_copy_to_host", "gg_synchronize", "gg_domain_create",
+    "gg_domain_release", "gg_domain_log_n", "gg_ntt", "gg_groth16_compute_h",
+    "gg_msm_base_create", "gg_msm_base_release", "gg_msm_base_info", "gg_msm",
+    "gg_g1_jac_to_affine", "gg_g2_jac_to_affine", "gg_g1_jac_add", "gg_g2_jac_add",
+    "gg_g1_scalar_mul", "gg_g2_scalar_mul", "gg_groth16_pk_create", "gg_groth16_pk_release",
+    "gg_groth16_prove", "gg_groth16_last_timings", "gg_batch_scalar_mul", "gg_profile_enable",
+    "gg_profile_get",
+]
+
+
+def check(rc):
+    if rc != GG_OK:
+        msg = lib.gg_last_error()
+        raise GnarkAmdError(rc, msg.decode() if msg else "")
+
+
+def ptr(obj):
+    """Pointer to a host or device buffer: bytes/bytearray/numpy/torch/int/None."""
+    if obj is None:
+        return None
+    if isinstance(obj, int):
+        return ctypes.c_void_p(obj)
+    if hasattr(obj, "data_ptr"):  # torch tensor (device or host)
+        return ctypes.c_void_p(obj.data_ptr())
+    if hasattr(obj, "ctypes"):  # numpy
+        return obj.ctypes.data_as(ctypes.c_void_p)
+    if isinstance(obj, bytearray):
+        return ctypes.cast((ctypes.c_char * len(obj)).from_buffer(obj), ctypes.c_void_p)
+    if isinstance(obj, (bytes, memoryview)):
+        return ctypes.cast(ctypes.c_char_p(bytes(obj)), ctypes.c_void_p)
+    if isinstance(obj, DeviceBuffer):
+        return ctypes.c_void_p(obj.ptr)
+    raise TypeError(f"cannot take a pointer of {type(obj)}")
+
+
+class DeviceBuffer:
+    """HBM buffer owned through gg_malloc / gg_free."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        check(lib.gg_malloc(ctypes.byref(p), nbytes))
+        self.ptr = p.value
+        self.nbytes = nbytes
+
+    @classmethod
+    def from_host(cls, data):
+        b = cls(len(data))
+        check(lib.gg_copy_to_device(ctypes.c_void_p(b.ptr), ptr(data), len(data)))
+        return b
+
+    def to_host(self, nbytes=None) -> bytes:
+        nbytes = self.nbytes if nbytes is None else nbytes
+        out = bytearray(nbytes)
+        check(lib.gg_copy_to_host(ptr(out), ctypes.c_void_p(self.ptr), nbytes))
+        return bytes(out)
+
+    def free(self):
+        if self.ptr:
+            lib.gg_free(ctypes.c_void_p(self.ptr))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def device_count() -> int:
+    n = ctypes.c_int()
+    check(lib.gg_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def profile_enable(on: bool = True):
+    check(lib.gg_profile_enable(int(on)))
+
+
+def profile_get(name: str):
+    ms = ctypes.c_double()
+    cnt = ctypes.c_int64()
+    units = ctypes.c_double()
+    check(lib.gg_profile_get(name.encode(), ctypes.byref(ms), ctypes.byref(cnt), ctypes.byref(units)))
+    return ms.value, cnt.value, units.value

@@ -1,0 +1,90 @@
+"""Resident MSM bases + multi-scalar multiplication (replaces iciclegnark
+CopyPointsToDevice / MsmOnDevice / MsmG2OnDevice, icicle.go:88-126, 302-382,
+and G1Jac/G2Jac.MultiExp at prove.go:201-290)."""
+from __future__ import annotations
+
+import ctypes
+
+from ._lib import GG_G1, GG_G2, check, lib, ptr
+
+G1, G2 = GG_G1, GG_G2
+_JAC = {G1: 96, G2: 192}
+_AFF = {G1: 64, G2: 128}
+
+
+class MsmBase:
+    """n affine points (gnark layout) uploaded once, precomputed, kept in HBM."""
+
+    def __init__(self, group: int, points, n: int, on_device=False, scalar_index=None,
+                 window_bits: int = 0):
+        import numpy as np
+        self.group = group
+        h = ctypes.c_void_p()
+        idx = None
+        if scalar_index is not None:
+            idx = np.ascontiguousarray(np.asarray(scalar_index, dtype=np.uint32))
+        check(lib.gg_msm_base_create(group, ptr(points), n, int(on_device),
+                                     ptr(idx), window_bits, ctypes.byref(h)))
+        self.handle = h
+
+    def info(self):
+        n = ctypes.c_size_t()
+        c = ctypes.c_int()
+        w = ctypes.c_int()
+        check(lib.gg_msm_base_info(self.handle, ctypes.byref(n), ctypes.byref(c), ctypes.byref(w)))
+        return n.value, c.value, w.value
+
+    def msm_jac(self, scalars, n_scalars: int, on_device=False, stream=None) -> bytes:
+        out = bytearray(_JAC[self.group])
+        check(lib.gg_msm(self.handle, ptr(scalars), n_scalars, int(on_device), ptr(out), ptr(stream)))
+        return bytes(out)
+
+    def msm(self, scalars, n_scalars: int, on_device=False, stream=None) -> bytes:
+        """Affine result (Montgomery, gnark layout; infinity = zeros)."""
+        return jac_to_affine(self.group, self.msm_jac(scalars, n_scalars, on_device, stream))
+
+    def close(self):
+        if self.handle:
+            lib.gg_msm_base_release(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def jac_to_affine(group: int, jac: bytes) -> bytes:
+    out = bytearray(_AFF[group])
+    fn = lib.gg_g1_jac_to_affine if group == G1 else lib.gg_g2_jac_to_affine
+    check(fn(ptr(jac), ptr(out)))
+    return bytes(out)
+
+
+def jac_add(group: int, a: bytes, b: bytes) -> bytes:
+    out = bytearray(_JAC[group])
+    fn = lib.gg_g1_jac_add if group == G1 else lib.gg_g2_jac_add
+    check(fn(ptr(a), ptr(b), ptr(out)))
+    return bytes(out)
+
+
+def scalar_mul(group: int, p_aff: bytes, k_mont: bytes) -> bytes:
+    out = bytearray(_JAC[group])
+    fn = lib.gg_g1_scalar_mul if group == G1 else lib.gg_g2_scalar_mul
+    check(fn(ptr(p_aff), ptr(k_mont), ptr(out)))
+    return bytes(out)
+
+
+def batch_scalar_mul(group: int, base_aff: bytes, scalars, n: int, scalars_on_device=False,
+                     out=None):
+    """out[i] = k_i * base (curve.BatchScalarMultiplicationG1/G2, setup.go:240-318).
+    Returns host bytes unless `out` (a device buffer) is given."""
+    if out is not None:
+        check(lib.gg_batch_scalar_mul(group, ptr(base_aff), ptr(scalars), n,
+                                      int(scalars_on_device), ptr(out), 1))
+        return out
+    res = bytearray(_AFF[group] * n)
+    check(lib.gg_batch_scalar_mul(group, ptr(base_aff), ptr(scalars), n, int(scalars_on_device),
+                                  ptr(res), 0))
+    return bytes(res)

@@ -1,0 +1,186 @@
+/*
+ * gnark_amd.h -- C ABI of the MI355X-native (gfx950) proving backend for gnark.
+ *
+ * This is the drop-in boundary that replaces the iciclegnark cgo calls made by
+ * gnark's `icicle` build-tag path (backend/groth16/bn254/icicle/icicle.go) and
+ * the gnark-crypto CPU kernels on the Groth16 hot path
+ * (backend/groth16/bn254/prove.go:127-396).  A Go binding (cgo) is shown in
+ * INTEGRATION.md; Python tests/bench bind it with ctypes.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Every field element / point buffer uses
+ *    gnark-crypto's in-memory layout: Montgomery form (R = 2^256), [4]uint64
+ *    little-endian limbs.  fr.Element = 32 B, G1Affine = 64 B {X,Y},
+ *    G2Affine = 128 B {X.A0,X.A1,Y.A0,Y.A1}, G1Jac = 96 B, G2Jac = 192 B.
+ *    Affine infinity is all-zero (as gnark's G1Affine zero value).
+ *  - Host buffers are borrowed for the duration of a call only (cgo rule).
+ *  - Every function returns 0 (GG_OK) on success or a GG_ERR_* code; the
+ *    message of the last failure on the calling thread is gg_last_error().
+ *  - Thread-safe: objects may be used from several host threads; each call
+ *    uses its own HIP stream unless one is passed explicitly.
+ */
+#ifndef GNARK_AMD_H
+#define GNARK_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GG_OK 0
+#define GG_ERR_INVALID_ARG 1
+#define GG_ERR_DEVICE 2
+#define GG_ERR_OOM 3
+#define GG_ERR_UNSUPPORTED 4
+#define GG_ERR_INTERNAL 5
+
+#define GG_G1 1
+#define GG_G2 2
+
+/* decimation (gnark-crypto fft.DIF / fft.DIT) */
+#define GG_DIF 0
+#define GG_DIT 1
+
+typedef struct gg_domain *gg_domain_t;
+typedef struct gg_msm_base *gg_msm_base_t;
+typedef struct gg_groth16_pk *gg_groth16_pk_t;
+
+/* ---------------------------------------------------------------- runtime */
+const char *gg_last_error(void);
+int gg_version(void);
+int gg_device_count(int *count);
+/* binds the calling host thread to a GPU (one process per GPU is the norm) */
+int gg_set_device(int device);
+
+/* ----------------------------------------------------------- device memory
+ * Replaces iciclegnark.CopyToDevice / FreeDevicePointer
+ * (icicle.go:44-47, 245, 269, 352, 356, 416-418, 478-480, 505-507). */
+int gg_malloc(void **dev_ptr, size_t bytes);
+int gg_free(void *dev_ptr);
+int gg_copy_to_device(void *dev_dst, const void *host_src, size_t bytes);
+int gg_copy_to_host(void *host_dst, const void *dev_src, size_t bytes);
+int gg_synchronize(void);
+
+/* ------------------------------------------------------------- NTT domain
+ * Replaces iciclegnark.GenerateTwiddleFactors + the CosetTable/CosetTableInv/
+ * den uploads (icicle.go:44-76).  omega and coset_gen are taken from gnark's
+ * pk.Domain (Generator, FrMultiplicativeGen) so no roots are hard-coded:
+ * omega_mont: primitive 2^log_n-th root of unity (fr, Montgomery);
+ * coset_gen_mont: coset shift g (fr, Montgomery). */
+int gg_domain_create(int log_n, const void *omega_mont, const void *coset_gen_mont,
+                     gg_domain_t *out);
+int gg_domain_release(gg_domain_t d);
+int gg_domain_log_n(gg_domain_t d, int *log_n);
+
+/* In-place transform of 2^log_n device fr elements with gnark-crypto
+ * semantics (replaces INttOnDevice / NttOnDevice / ReverseScalars,
+ * icicle.go:489-510, and domain.FFT / domain.FFTInverse, prove.go:369-393):
+ *   inverse = 0: domain.FFT(a, decimation, [OnCoset()])
+ *   inverse = 1: domain.FFTInverse(a, decimation, [OnCoset()])
+ * DIF: natural -> bit-reversed; DIT: bit-reversed -> natural. */
+int gg_ntt(gg_domain_t d, void *data_dev, int inverse, int decimation, int coset,
+           void *hip_stream);
+
+/* Fused Groth16 computeH (prove.go:353-396; icicle.go:453-513):
+ *   h = FFTInverse_coset_DIF( (FFT_coset_DIT(iFFT_DIF(a)) o ... b) - ...c ) / (g^n - 1)
+ * a, b, c: `len` <= 2^log_n fr elements (zero-padded to 2^log_n), host or
+ * device memory per inputs_on_device.  h_dev: device buffer of 2^log_n fr;
+ * h comes out in bit-reversed order, the order pk.G1.Z is stored in
+ * (setup.go:265), so it feeds the Z-MSM directly. */
+int gg_groth16_compute_h(gg_domain_t d, const void *a, const void *b, const void *c, size_t len,
+                         int inputs_on_device, void *h_dev, void *hip_stream);
+
+/* --------------------------------------------------------- MSM point bases
+ * Replaces iciclegnark.CopyPointsToDevice / CopyG2PointsToDevice
+ * (icicle.go:88-126).  Points stay resident in HBM together with the
+ * window-shifted copies 2^(c*w) * P_i that the bucket MSM uses, so every
+ * window shares one bucket set (fixed-base precomputation sized for 288 GB).
+ * group: GG_G1 or GG_G2.  points: n affine points (host or device memory).
+ * Infinity points are dropped at upload (fixes the index shift of
+ * icicle.go:343-347).
+ * scalar_index (nullable, host): scalar of point i is scalars[scalar_index[i]]
+ *   in gg_msm -- this expresses gnark's wire filtering (prove.go:151-175,
+ *   filterHeap prove.go:328-351) without copying the witness.
+ * window_bits: 0 = automatic. */
+int gg_msm_base_create(int group, const void *points, size_t n, int points_on_device,
+                       const uint32_t *scalar_index, int window_bits, gg_msm_base_t *out);
+int gg_msm_base_release(gg_msm_base_t b);
+/* number of resident (non-infinity) points, and window size actually used */
+int gg_msm_base_info(gg_msm_base_t b, size_t *n_points, int *window_bits, int *n_windows);
+
+/* out = sum_i scalars[idx(i)] * P_i as a Jacobian point (gnark G1Jac/G2Jac
+ * layout, Montgomery).  Replaces MsmOnDevice / MsmG2OnDevice
+ * (icicle.go:302-382) and G1Jac/G2Jac.MultiExp (prove.go:201-290).
+ * scalars: fr Montgomery (host or device per scalars_on_device);
+ * n_scalars: length of the scalar vector (must cover every referenced index).
+ * hip_stream may be NULL. */
+int gg_msm(gg_msm_base_t b, const void *scalars, size_t n_scalars, int scalars_on_device,
+           void *out_jac, void *hip_stream);
+
+/* host-side point helpers (epilogue of prove.go:206-299) */
+int gg_g1_jac_to_affine(const void *jac, void *aff);
+int gg_g2_jac_to_affine(const void *jac, void *aff);
+int gg_g1_jac_add(const void *a_jac, const void *b_jac, void *out_jac);
+int gg_g2_jac_add(const void *a_jac, const void *b_jac, void *out_jac);
+/* out = k * p, k fr Montgomery, p affine */
+int gg_g1_scalar_mul(const void *p_aff, const void *k_mont, void *out_jac);
+int gg_g2_scalar_mul(const void *p_aff, const void *k_mont, void *out_jac);
+
+/* Fixed-base batch scalar multiplication out[i] = k_i * base (affine,
+ * infinity for k_i = 0): replaces curve.BatchScalarMultiplicationG1/G2
+ * (setup.go:240-251, 306-318; prove.go:192).  Used to build proving keys on
+ * the GPU.  scalars: n fr Montgomery; out: n affine points. */
+int gg_batch_scalar_mul(int group, const void *base_aff, const void *scalars, size_t n,
+                        int scalars_on_device, void *out_aff, int out_on_device);
+
+/* ------------------------------------------------------------ Groth16 BN254
+ * Device-resident proving key: replaces setupDevicePointers (icicle.go:31-130)
+ * and holds the pk.G1/G2 arrays (setup.go:35-58).
+ *   log_n, omega, coset_gen : pk.Domain
+ *   g1_A[nA], g1_B[nB], g1_Z[nZ = 2^log_n - 1], g1_K[nK] : pk.G1.{A,B,Z,K}
+ *   alpha1, beta1, delta1 : pk.G1.{Alpha,Beta,Delta};  g2_B[nB], beta2, delta2
+ *   inf_A, inf_B : pk.InfinityA/B (n_wires bytes, 1 = infinity)
+ *   nb_public : r1cs.GetNbPublicVariables()
+ *   k_wire_index (nullable): wire index of the scalar for each pk.G1.K point,
+ *     i.e. the filterHeap result (prove.go:238-248); NULL = nb_public + i. */
+int gg_groth16_pk_create(int log_n, const void *omega_mont, const void *coset_gen_mont,
+                         const void *g1_A, size_t nA, const void *g1_B, size_t nB,
+                         const void *g1_Z, size_t nZ, const void *g1_K, size_t nK,
+                         const void *alpha1, const void *beta1, const void *delta1,
+                         const void *g2_B, const void *beta2, const void *delta2,
+                         const uint8_t *inf_A, const uint8_t *inf_B, size_t n_wires,
+                         size_t nb_public, const uint32_t *k_wire_index, gg_groth16_pk_t *out);
+int gg_groth16_pk_release(gg_groth16_pk_t pk);
+
+/* Groth16 Prove after Solve (prove.go:127-320; icicle.go:198-420):
+ *   wires[n_wires] = solution.W; sol_a/b/c[n_cons] = solution.A/B/C
+ *   (host or device memory per inputs_on_device)
+ *   r_mont, s_mont: the proof randomness (prove.go:177-189 samples it with
+ *   SetRandom; the caller passes it so tests can pin it).
+ * Outputs (host): Ar (G1Affine 64 B), Bs (G2Affine 128 B), Krs (G1Affine 64 B);
+ * h_dev_out (nullable): device buffer of 2^log_n fr receiving h (bit-reversed). */
+int gg_groth16_prove(gg_groth16_pk_t pk, const void *wires, size_t n_wires, const void *sol_a,
+                     const void *sol_b, const void *sol_c, size_t n_cons, int inputs_on_device,
+                     const void *r_mont, const void *s_mont, void *ar_aff, void *bs_aff,
+                     void *krs_aff, void *h_dev_out);
+
+/* per-stage timings (ms) of the last gg_groth16_prove on this thread:
+ * [0]=upload [1]=computeH [2]=msm_A [3]=msm_B1 [4]=msm_K [5]=msm_Z [6]=msm_G2
+ * [7]=epilogue [8]=total */
+int gg_groth16_last_timings(double *ms9);
+
+
+/* ------------------------------------------------------------ profiling
+ * Kernel-level timing with HIP events recorded on the stream each kernel is
+ * launched on (bench.py uses it for the roofline of the dominant kernel).
+ * gg_profile_enable(1) clears and enables; names: "msm_accum", "msm_sort",
+ * "msm_reduce", "ntt_pass", ... ; totals are summed over launches. */
+int gg_profile_enable(int on);
+int gg_profile_get(const char *name, double *total_ms, int64_t *launches, double *units);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GNARK_AMD_H */

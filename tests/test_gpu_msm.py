@@ -1,0 +1,124 @@
+"""GPU MSM parity (gg_msm) against the golden fixtures, the C oracle and the
+trapdoor identity MSM(k_i G, s_i) = (sum s_i k_i) G."""
+import numpy as np
+import pytest
+
+import bn254_oracle as o
+import coracle
+from helpers import b, golden, random_fr_mont, random_g1_points, random_g2_points
+
+pytestmark = pytest.mark.gpu
+
+
+def test_msm_golden():
+    from gnark_amd import msm
+    for c in golden()["msm"]:
+        base = msm.MsmBase(c["group"], b(c["points"]), c["n"])
+        got = base.msm(b(c["scalars"]), c["n"])
+        assert got.hex() == c["expected"], (c["group"], c["n"])
+
+
+@pytest.mark.parametrize("n,dist,c", [
+    (1000, "uniform", 0), (1000, "witness", 0), (4096, "uniform", 4), (4096, "uniform", 8),
+    (4096, "witness", 13), (1 << 16, "uniform", 0), (1 << 16, "witness", 0), (1 << 16, "small", 16),
+])
+def test_msm_g1_vs_oracle(n, dist, c):
+    from gnark_amd import msm
+    pts = random_g1_points(n, 1000 + n)
+    sc = random_fr_mont(n, 2000 + n, dist)
+    base = msm.MsmBase(msm.G1, pts, n, window_bits=c)
+    assert base.msm(sc, n) == coracle.msm_g1(pts.tobytes(), sc.tobytes(), n)
+
+
+def test_msm_g1_2p20_config2():
+    """BASELINE config 2: 2^20 random scalars/points, bit-exact vs the CPU oracle."""
+    from gnark_amd import msm
+    n = 1 << 20
+    pts = random_g1_points(n, 4242)
+    sc = random_fr_mont(n, 4343)
+    base = msm.MsmBase(msm.G1, pts, n)
+    exp = coracle.msm_g1(pts.tobytes(), sc.tobytes(), n)
+    assert base.msm(sc, n) == exp
+    sw = random_fr_mont(n, 4444, "witness")
+    assert base.msm(sw, n) == coracle.msm_g1(pts.tobytes(), sw.tobytes(), n)
+
+
+def test_msm_trapdoor_2p18():
+    from gnark_amd import msm
+    n = 1 << 18
+    ks = random_fr_mont(n, 77)
+    ss = random_fr_mont(n, 78)
+    pts = coracle.g1_batch_mul(o.g1_to_bytes(o.G1_GEN), ks.tobytes(), n)
+    base = msm.MsmBase(msm.G1, bytes(pts), n)
+    got = o.g1_from_bytes(base.msm(ss, n))
+    kv = o.fr_vec_from_bytes(ks.tobytes())
+    sv = o.fr_vec_from_bytes(ss.tobytes())
+    assert got == o.g1_mul(o.G1_GEN, sum(x * y for x, y in zip(kv, sv)) % o.R)
+
+
+def test_msm_edge_cases():
+    from gnark_amd import msm
+    n = 1 << 12
+    p = o.g1_to_bytes(o.g1_mul(o.G1_GEN, 123456789))
+    same = p * n  # DummySetup: every key point identical (setup.go:482-572)
+    sc = random_fr_mont(n, 5)
+    base = msm.MsmBase(msm.G1, same, n)
+    tot = sum(o.fr_vec_from_bytes(sc.tobytes())) % o.R
+    assert o.g1_from_bytes(base.msm(sc, n)) == o.g1_mul(o.g1_from_bytes(p), tot)
+    # all-zero scalars -> infinity
+    assert base.msm(np.zeros((n, 4), dtype=np.uint64), n) == bytes(64)
+    # all scalars = 1 and = r-1 (max digit carries)
+    one = np.frombuffer(o.fr_to_bytes(1) * n, dtype=np.uint64)
+    rm1 = np.frombuffer(o.fr_to_bytes(o.R - 1) * n, dtype=np.uint64)
+    pts = random_g1_points(n, 9)
+    base2 = msm.MsmBase(msm.G1, pts, n)
+    assert base2.msm(one, n) == coracle.msm_g1(pts.tobytes(), one.tobytes(), n)
+    assert base2.msm(rm1, n) == coracle.msm_g1(pts.tobytes(), rm1.tobytes(), n)
+    # infinity points inside the key are skipped (pk.G1.K, icicle.go:98-105)
+    pts3 = pts.copy().reshape(n, 64)
+    pts3[::7] = 0
+    base3 = msm.MsmBase(msm.G1, pts3, n)
+    assert base3.msm(sc, n) == coracle.msm_g1(pts3.tobytes(), sc.tobytes(), n)
+    # P and -P with equal scalars cancel
+    q = o.g1_mul(o.G1_GEN, 5)
+    pq = o.g1_to_bytes(q) + o.g1_to_bytes((q[0], (-q[1]) % o.P))
+    base4 = msm.MsmBase(msm.G1, pq, 2)
+    s2 = o.fr_to_bytes(99) * 2
+    assert base4.msm(s2, 2) == bytes(64)
+
+
+def test_msm_scalar_index_map():
+    from gnark_amd import msm
+    n, nw = 3000, 5000
+    pts = random_g1_points(n, 31)
+    w = random_fr_mont(nw, 32)
+    idx = np.random.default_rng(3).choice(nw, size=n, replace=False).astype(np.uint32)
+    base = msm.MsmBase(msm.G1, pts, n, scalar_index=idx)
+    gathered = np.ascontiguousarray(w[idx])
+    assert base.msm(w, nw) == coracle.msm_g1(pts.tobytes(), gathered.tobytes(), n)
+
+
+def test_msm_device_scalars_and_jacobian_add():
+    from gnark_amd import msm, DeviceBuffer
+    n = 1 << 14
+    pts = random_g1_points(n, 41)
+    sc = random_fr_mont(n, 42)
+    exp = coracle.msm_g1(pts.tobytes(), sc.tobytes(), n)
+    # shard in two halves, combine partials (the multi-GPU reduction path)
+    h = n // 2
+    b0 = msm.MsmBase(msm.G1, pts[: h * 64], h)
+    b1 = msm.MsmBase(msm.G1, pts[h * 64:], n - h)
+    d0 = DeviceBuffer.from_host(sc[:h].tobytes())
+    d1 = DeviceBuffer.from_host(sc[h:].tobytes())
+    j0 = b0.msm_jac(d0, h, on_device=True)
+    j1 = b1.msm_jac(d1, n - h, on_device=True)
+    assert msm.jac_to_affine(msm.G1, msm.jac_add(msm.G1, j0, j1)) == exp
+
+
+@pytest.mark.parametrize("n,dist", [(1000, "uniform"), (1 << 12, "witness"), (1 << 15, "uniform")])
+def test_msm_g2_vs_oracle(n, dist):
+    from gnark_amd import msm
+    pts = random_g2_points(n, 500 + n)
+    sc = random_fr_mont(n, 600 + n, dist)
+    base = msm.MsmBase(msm.G2, pts, n)
+    assert base.msm(sc, n) == coracle.msm_g2(pts.tobytes(), sc.tobytes(), n)
