@@ -22,6 +22,7 @@ struct FpCfg {
     static constexpr uint32_t P[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
                                       0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
     static constexpr uint32_t INV = 0xe4866389u;  // -p^-1 mod 2^32
+    static constexpr uint64_t INV64 = 0x87d20782e4866389ull;  // -p^-1 mod 2^64
     static constexpr uint32_t ONE[8] = {0xc58f0d9du, 0xd35d438du, 0xf5c70b3du, 0x0a78eb28u,
                                         0x7879462cu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
     static constexpr uint32_t R2[8] = {0x538afa89u, 0xf32cfc5bu, 0xd44501fbu, 0xb5e71911u,
@@ -32,6 +33,7 @@ struct FrCfg {
     static constexpr uint32_t P[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
                                       0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
     static constexpr uint32_t INV = 0xefffffffu;
+    static constexpr uint64_t INV64 = 0xc2e1f593efffffffull;
     static constexpr uint32_t ONE[8] = {0x4ffffffbu, 0xac96341cu, 0x9f60cd29u, 0x36fc7695u,
                                         0x7879462eu, 0x666ea36fu, 0x9a07df2fu, 0x0e0a77c1u};
     static constexpr uint32_t R2[8] = {0xae216da7u, 0x1bb8e645u, 0xe35c59e3u, 0x53fe3ab1u,
@@ -121,9 +123,67 @@ GG_HD Fe<C> dbl(const Fe<C>& a) {
     return a + a;
 }
 
-// CIOS Montgomery multiplication, 8 x 32-bit limbs.
+#if !defined(__HIP_DEVICE_COMPILE__)
+// Host side (epilogue, bucket-reduction tail): same Montgomery product on
+// 4 x 64-bit limbs with 128-bit intermediates -- identical bytes, ~4x fewer
+// host instructions than the 32-bit device formulation.
+template <class C>
+inline Fe<C> mont_mul_host(const Fe<C>& a, const Fe<C>& b) {
+    typedef unsigned __int128 u128;
+    uint64_t A[4], B[4], P[4], t[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 4; i++) {
+        A[i] = (uint64_t)a.v[2 * i] | ((uint64_t)a.v[2 * i + 1] << 32);
+        B[i] = (uint64_t)b.v[2 * i] | ((uint64_t)b.v[2 * i + 1] << 32);
+        P[i] = (uint64_t)C::P[2 * i] | ((uint64_t)C::P[2 * i + 1] << 32);
+    }
+    for (int i = 0; i < 4; i++) {
+        uint64_t carry = 0;
+        for (int j = 0; j < 4; j++) {
+            u128 x = (u128)A[j] * B[i] + t[j] + carry;
+            t[j] = (uint64_t)x;
+            carry = (uint64_t)(x >> 64);
+        }
+        u128 x = (u128)t[4] + carry;
+        t[4] = (uint64_t)x;
+        t[5] = (uint64_t)(x >> 64);
+        uint64_t m = t[0] * C::INV64;
+        x = (u128)m * P[0] + t[0];
+        carry = (uint64_t)(x >> 64);
+        for (int j = 1; j < 4; j++) {
+            x = (u128)m * P[j] + t[j] + carry;
+            t[j - 1] = (uint64_t)x;
+            carry = (uint64_t)(x >> 64);
+        }
+        x = (u128)t[4] + carry;
+        t[3] = (uint64_t)x;
+        t[4] = t[5] + (uint64_t)(x >> 64);
+    }
+    // conditional subtraction
+    uint64_t s[4];
+    uint64_t br = 0;
+    for (int i = 0; i < 4; i++) {
+        u128 x = (u128)t[i] - P[i] - br;
+        s[i] = (uint64_t)x;
+        br = (uint64_t)(x >> 64) & 1;
+    }
+    bool ge = t[4] || !br;
+    Fe<C> r;
+    for (int i = 0; i < 4; i++) {
+        uint64_t v = ge ? s[i] : t[i];
+        r.v[2 * i] = (uint32_t)v;
+        r.v[2 * i + 1] = (uint32_t)(v >> 32);
+    }
+    return r;
+}
+#endif
+
+// CIOS Montgomery multiplication, 8 x 32-bit limbs (device); host uses the
+// 64-bit-limb form above.
 template <class C>
 GG_HD Fe<C> operator*(const Fe<C>& a, const Fe<C>& b) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    return mont_mul_host(a, b);
+#else
     uint32_t t[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) t[j] = 0;
@@ -152,6 +212,7 @@ GG_HD Fe<C> operator*(const Fe<C>& a, const Fe<C>& b) {
 #pragma unroll
     for (int i = 0; i < 8; i++) r.v[i] = br ? t[i] : s.v[i];
     return r;
+#endif
 }
 
 template <class C>

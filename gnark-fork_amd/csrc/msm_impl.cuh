@@ -27,6 +27,8 @@
 #include <memory>
 #include <cstring>
 
+struct gg_msm_base;
+
 namespace gg {
 
 // ------------------------------------------------------------------ loads
@@ -61,6 +63,7 @@ __global__ void k_item_buckets(const uint32_t* item_off, size_t nb, uint32_t* it
 void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, hipStream_t st,
                     std::vector<DevBuf>& tmp, int depth = 0);
 int choose_c(size_t n, size_t point_bytes);
+void sort_entries(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st);
 
 // level 1: sum up to K affine points of one bucket into an XYZZ partial
 template <class F>
@@ -102,43 +105,46 @@ __global__ void __launch_bounds__(256) k_accum_xyzz(const Xyzz<F>* in, const uin
     st(partial + t, acc);
 }
 
-// segment running sums: V_s = sum_{b in seg} (b+1) * S_b
+// ------------------------------------------------------------ reduction v2
+// Dense bucket sums: S[b] = partial of bucket b (or infinity)
 template <class F>
-__global__ void __launch_bounds__(256) k_bucket_reduce(const Xyzz<F>* partial,
-                                                       const uint32_t* item_off, size_t nb,
-                                                       int seg_len, Xyzz<F>* out) {
-    size_t s = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    size_t lo = s * (size_t)seg_len;
-    if (lo >= nb) return;
-    size_t hi = min(nb, lo + (size_t)seg_len);
-    Xyzz<F> run = Xyzz<F>::inf(), tot = Xyzz<F>::inf();
-    for (size_t b = hi; b-- > lo;) {
-        uint32_t o = item_off[b];
-        if (item_off[b + 1] > o) run = xyzz_add(run, ld(partial + o));
-        tot = xyzz_add(tot, run);
-    }
-    // tot += lo * run   (double-and-add, lo < 2^31)
-    if (lo && !run.is_inf()) {
-        Xyzz<F> acc = Xyzz<F>::inf();
-        int top = 31 - __clz((int)lo);
-        for (int bit = top; bit >= 0; bit--) {
-            acc = acc.is_inf() ? acc : xyzz_dbl(acc);
-            if ((lo >> bit) & 1) acc = xyzz_add(acc, run);
-        }
-        tot = xyzz_add(tot, acc);
-    }
-    st(out + s, tot);
+__global__ void k_gather_buckets(const Xyzz<F>* partial, const uint32_t* item_off, size_t nb,
+                                 Xyzz<F>* S) {
+    size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    uint32_t o = item_off[b];
+    st(S + b, (item_off[b + 1] > o) ? ld(partial + o) : Xyzz<F>::inf());
 }
 
+// Generic strided group sum: view X[a][c] = in[a*sa + c*sb], a < A, c < Bc;
+// out[a'*Bc + c] = sum_{k<G, a'G+k<A} X[a'G+k][c].  Several jobs per launch so
+// independent reductions advance in lockstep (their latencies overlap).
 template <class F>
-__global__ void __launch_bounds__(256) k_sum_groups(const Xyzz<F>* in, size_t n, int G, Xyzz<F>* out) {
-    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    size_t lo = t * (size_t)G;
-    if (lo >= n) return;
-    size_t hi = min(n, lo + (size_t)G);
-    Xyzz<F> acc = ld(in + lo);
-    for (size_t e = lo + 1; e < hi; e++) acc = xyzz_add(acc, ld(in + e));
-    st(out + t, acc);
+struct RedJob {
+    const Xyzz<F>* in;
+    Xyzz<F>* out;
+    uint32_t A, Bc, sa, sb, G, nthreads;
+};
+constexpr int MAX_RED_JOBS = 16;
+template <class F>
+struct RedJobs {
+    RedJob<F> j[MAX_RED_JOBS];
+    int n;
+};
+
+template <class F>
+__global__ void __launch_bounds__(256) k_reduce_jobs(RedJobs<F> J) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    int q = 0;
+    while (q < J.n && t >= J.j[q].nthreads) { t -= J.j[q].nthreads; q++; }
+    if (q >= J.n) return;
+    const RedJob<F>& jb = J.j[q];
+    uint32_t a2 = t / jb.Bc, c = t % jb.Bc;
+    uint32_t a0 = a2 * jb.G;
+    uint32_t a1 = min(jb.A, a0 + jb.G);
+    Xyzz<F> acc = ld(jb.in + (size_t)a0 * jb.sa + (size_t)c * jb.sb);
+    for (uint32_t a = a0 + 1; a < a1; a++) acc = xyzz_add(acc, ld(jb.in + (size_t)a * jb.sa + (size_t)c * jb.sb));
+    st(jb.out + (size_t)a2 * jb.Bc + c, acc);
 }
 
 // ------------------------------------------------------------ precompute
@@ -198,6 +204,7 @@ struct gg_msm_base {
     std::mutex mu;
     // scratch
     DevBuf digits, sorted, counts, offsets, cursor, itemcnt, item_off, item_bucket, maxcnt;
+    DevBuf keys, tmp_entry, tmp_key, hist, hoff, bin_start;
     DevBuf partA, partB, segs, segs2, scal;
     std::vector<DevBuf> scan_tmp;
 };
@@ -227,35 +234,127 @@ inline void precompute(gg_msm_base* b, const Affine<F>* dev_in, hipStream_t st) 
     GG_HIP(hipStreamSynchronize(st));
 }
 
+// Weighted bucket sum sum_{b<nb} (b+1) S_b with log-depth, wide tree sums
+// (DESIGN.md "MSM / bucket reduction"): a weighted sum WS(X, off) =
+// sum_j (j + off) X_j over n = 2^k elements is split as j = q*M + r into
+// M * WS(H, 0) + WS(G, off) with row sums H_q and column sums G_r -- both plain
+// tree sums that run wide on the GPU.  Pieces of <= 16 elements finish on the
+// host, combined by Horner over their 2^mlog factors.
+template <class F>
+inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* partials, hipStream_t st) {
+    const size_t nb = b->nb;
+    const size_t XB = sizeof(Xyzz<F>);
+    b->segs.reserve(nb * XB);
+    const size_t arena_elems = 3 * nb + 1024;
+    b->segs2.reserve(arena_elems * XB);
+    Xyzz<F>* S = b->segs.as<Xyzz<F>>();
+    hipLaunchKernelGGL(k_gather_buckets<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, partials,
+                       b->item_off.as<uint32_t>(), nb, S);
+    GG_HIP(hipGetLastError());
+    Xyzz<F>* arena = b->segs2.as<Xyzz<F>>();
+    size_t used = 0;
+    auto alloc = [&](size_t cnt) {
+        GG_CHECK(used + cnt <= arena_elems, GG_ERR_INTERNAL, "bucket reduction arena overflow");
+        Xyzz<F>* p = arena + used;
+        used += cnt;
+        return p;
+    };
+    struct Item { const Xyzz<F>* X; uint32_t n, off; int mlog; };
+    struct Job { const Xyzz<F>* in; uint32_t A, Bc, sa, sb; Item dest; };
+    std::vector<Item> items{{S, (uint32_t)nb, 1u, 0}};
+    std::vector<Item> host_items;
+    const uint32_t HOST_N = 16;
+    while (!items.empty()) {
+        std::vector<Job> jobs;
+        for (const Item& it : items) {
+            if (it.n <= HOST_N) { host_items.push_back(it); continue; }
+            int lg = 31 - __builtin_clz(it.n);
+            int mlg = lg / 2;
+            uint32_t M = 1u << mlg, rows = it.n >> mlg;
+            jobs.push_back({it.X, M, rows, 1u, M, Item{nullptr, rows, 0u, it.mlog + mlg}});
+            jobs.push_back({it.X, rows, M, M, 1u, Item{nullptr, M, it.off, it.mlog}});
+        }
+        bool active = !jobs.empty();
+        while (active) {
+            size_t t2 = 0;
+            for (auto& j : jobs) if (j.A > 1) t2 += (size_t)((j.A + 1) / 2) * j.Bc;
+            uint32_t G = t2 >= (256u << 10) ? 8 : (t2 >= (96u << 10) ? 4 : 2);
+            RedJobs<F> J;
+            J.n = 0;
+            size_t threads = 0;
+            auto flush = [&]() {
+                if (!J.n) return;
+                hipLaunchKernelGGL(k_reduce_jobs<F>, dim3(grid_for(threads, 256)), dim3(256), 0, st, J);
+                GG_HIP(hipGetLastError());
+                J.n = 0;
+                threads = 0;
+            };
+            active = false;
+            for (auto& j : jobs) {
+                if (j.A <= 1) continue;
+                uint32_t A2 = (j.A + G - 1) / G;
+                Xyzz<F>* out = alloc((size_t)A2 * j.Bc);
+                J.j[J.n++] = RedJob<F>{j.in, out, j.A, j.Bc, j.sa, j.sb, G, A2 * j.Bc};
+                threads += (size_t)A2 * j.Bc;
+                j.in = out;
+                j.A = A2;
+                j.sa = j.Bc;
+                j.sb = 1;
+                if (A2 > 1) active = true;
+                if (J.n == MAX_RED_JOBS) flush();
+            }
+            flush();
+        }
+        std::vector<Item> next;
+        for (auto& j : jobs) { Item it = j.dest; it.X = j.in; next.push_back(it); }
+        items.swap(next);
+    }
+    // host: tiny weighted sums + Horner over the 2^mlog factors
+    std::vector<std::vector<Xyzz<F>>> hx(host_items.size());
+    for (size_t k = 0; k < host_items.size(); k++) {
+        hx[k].resize(host_items[k].n);
+        GG_HIP(hipMemcpyAsync(hx[k].data(), host_items[k].X, host_items[k].n * XB,
+                              hipMemcpyDeviceToHost, st));
+    }
+    GG_HIP(hipStreamSynchronize(st));
+    std::vector<std::pair<int, Xyzz<F>>> vals;
+    for (size_t k = 0; k < host_items.size(); k++) {
+        const auto& X = hx[k];
+        Xyzz<F> run = Xyzz<F>::inf(), acc = Xyzz<F>::inf();
+        for (size_t j = X.size(); j-- > 1;) {
+            run = xyzz_add(run, X[j]);
+            acc = xyzz_add(acc, run);
+        }
+        if (host_items[k].off) {
+            run = xyzz_add(run, X[0]);  // run = sum of all
+            for (uint32_t o = 0; o < host_items[k].off; o++) acc = xyzz_add(acc, run);
+        }
+        vals.push_back({host_items[k].mlog, acc});
+    }
+    std::sort(vals.begin(), vals.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
+    Xyzz<F> acc = Xyzz<F>::inf();
+    int cur = vals.empty() ? 0 : vals[0].first;
+    for (auto& v : vals) {
+        for (; cur > v.first; cur--) acc = acc.is_inf() ? acc : xyzz_dbl(acc);
+        acc = xyzz_add(acc, v.second);
+    }
+    for (; cur > 0; cur--) acc = acc.is_inf() ? acc : xyzz_dbl(acc);
+    return acc;
+}
+
 template <class F>
 inline Xyzz<F> msm_run(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st) {
     const size_t n = b->n, nb = b->nb;
     const int c = b->c, W = b->W;
     const size_t total = (size_t)W * n;
     if (n == 0) return Xyzz<F>::inf();
-    b->digits.reserve(total * 4);
-    b->sorted.reserve(total * 4);
     b->counts.reserve(nb * 4);
     b->offsets.reserve((nb + 1) * 4);
-    b->cursor.reserve(nb * 4);
     b->itemcnt.reserve(nb * 4);
     b->item_off.reserve((nb + 1) * 4);
     b->maxcnt.reserve(4);
-
     ProfScope ps_sort("msm_sort", st, (double)n);
-    GG_HIP(hipMemsetAsync(b->counts.p, 0, nb * 4, st));
-    hipLaunchKernelGGL(k_digits, dim3(grid_for(n, 256)), dim3(256), 0, st, scalars_dev,
-                       b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W,
-                       b->digits.as<int32_t>(), b->counts.as<uint32_t>());
-    GG_HIP(hipGetLastError());
-    exclusive_scan(b->counts.as<uint32_t>(), b->offsets.as<uint32_t>(), nb, st, b->scan_tmp);
-    hipLaunchKernelGGL(k_set_total, dim3(1), dim3(1), 0, st, b->offsets.as<uint32_t>(),
-                       b->counts.as<uint32_t>(), nb);
-    GG_HIP(hipMemcpyAsync(b->cursor.p, b->offsets.p, nb * 4, hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(k_scatter, dim3(grid_for(total, 256)), dim3(256), 0, st,
-                       b->digits.as<int32_t>(), total, b->cursor.as<uint32_t>(),
-                       b->sorted.as<uint32_t>());
-    GG_HIP(hipGetLastError());
+    sort_entries(b, scalars_dev, st);
     ps_sort.stop(st);
 
     // ---- level 1: affine entries -> partials
@@ -320,32 +419,10 @@ inline Xyzz<F> msm_run(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st) {
         std::swap(cur_part, nxt_part);
     }
     ps_acc2.stop(st);
-    // ---- bucket reduction
+    // ---- bucket reduction: sum_b (b+1) S_b
     ProfScope ps_red("msm_reduce", st, (double)nb);
-    const int SEG = 32;
-    size_t nseg = (nb + SEG - 1) / SEG;
-    b->segs.reserve(nseg * sizeof(Xyzz<F>));
-    b->segs2.reserve(nseg * sizeof(Xyzz<F>));
-    hipLaunchKernelGGL(k_bucket_reduce<F>, dim3(grid_for(nseg, 256)), dim3(256), 0, st,
-                       (const Xyzz<F>*)cur_part->p, b->item_off.as<uint32_t>(), nb, SEG,
-                       b->segs.as<Xyzz<F>>());
-    GG_HIP(hipGetLastError());
-    DevBuf* a = &b->segs;
-    DevBuf* o = &b->segs2;
-    size_t m = nseg;
-    const int G = 16;
-    while (m > 1) {
-        size_t mo = (m + G - 1) / G;
-        hipLaunchKernelGGL(k_sum_groups<F>, dim3(grid_for(mo, 256)), dim3(256), 0, st,
-                           (const Xyzz<F>*)a->p, m, G, o->as<Xyzz<F>>());
-        GG_HIP(hipGetLastError());
-        std::swap(a, o);
-        m = mo;
-    }
+    Xyzz<F> res = bucket_reduce_2d<F>(b, (const Xyzz<F>*)cur_part->p, st);
     ps_red.stop(st);
-    Xyzz<F> res;
-    GG_HIP(hipMemcpyAsync(&res, a->p, sizeof(res), hipMemcpyDeviceToHost, st));
-    GG_HIP(hipStreamSynchronize(st));
     return res;
 }
 
