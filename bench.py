@@ -99,19 +99,14 @@ def main():
     dsc = DeviceBuffer.from_host(sc.tobytes())
     log(f"[rank {rank}] key shard ready: n={npts} c={c} windows={W} ({time.time() - t0:.1f}s)")
 
+    from gnark_amd import dist as gdist
+
     def step():
         j = base.msm_jac(dsc, n, on_device=True)
         if dist is None:
             return j
-        t = torch.frombuffer(bytearray(j), dtype=torch.uint8).cuda()
-        parts = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(parts, t)
-        if rank == 0:
-            acc = bytes(parts[0].cpu().numpy())
-            for p in parts[1:]:
-                acc = msm.jac_add(msm.G1, acc, bytes(p.cpu().numpy()))
-            return acc
-        return j
+        # RCCL all-gather of the 96-B Jacobian partials + exact EC add (gnark_amd.dist)
+        return gdist.allgather_partial(msm.G1, j, device=torch.device("cuda", local_rank))
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,33 @@
+// Package amd_bn254 is the gnark-side shim of the MI355X backend: a drop-in
+// twin of backend/groth16/bn254/icicle (provingkey.go:30-48, icicle.go,
+// noicicle.go) that calls libgnark_amd.so through cgo (include/gnark_amd.h).
+// Source only in this repository (no Go toolchain in the build image); see
+// INTEGRATION.md for how it is wired into gnark.
+package amd_bn254
+
+import (
+	"unsafe"
+
+	groth16_bn254 "github.com/consensys/gnark/backend/groth16/bn254"
+	cs "github.com/consensys/gnark/constraint/bn254"
+)
+
+// deviceInfo holds the HBM-resident proving key (gg_groth16_pk_t).
+type deviceInfo struct {
+	handle unsafe.Pointer
+}
+
+// ProvingKey embeds the CPU key so WriteTo/ReadFrom/... are promoted unchanged
+// (same layout trick as icicle_bn254.ProvingKey, provingkey.go:45-48).
+type ProvingKey struct {
+	groth16_bn254.ProvingKey
+	*deviceInfo
+}
+
+func Setup(r1cs *cs.R1CS, pk *ProvingKey, vk *groth16_bn254.VerifyingKey) error {
+	return groth16_bn254.Setup(r1cs, &pk.ProvingKey, vk)
+}
+
+func DummySetup(r1cs *cs.R1CS, pk *ProvingKey) error {
+	return groth16_bn254.DummySetup(r1cs, &pk.ProvingKey)
+}
