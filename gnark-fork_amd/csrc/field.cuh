@@ -177,12 +177,64 @@ inline Fe<C> mont_mul_host(const Fe<C>& a, const Fe<C>& b) {
 }
 #endif
 
-// CIOS Montgomery multiplication, 8 x 32-bit limbs (device); host uses the
-// 64-bit-limb form above.
+#if defined(__HIP_DEVICE_COMPILE__)
+// acc(96 bit = {acc64, c2}) += x * y : one v_mad_u64_u32 with its carry-out in
+// VCC folded into the third word by one v_addc (2 instructions per product).
+__device__ __forceinline__ void mac96(uint64_t& acc, uint32_t& c2, uint32_t x, uint32_t y) {
+    asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
+        "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+        : "+v"(acc), "+v"(c2)
+        : "v"(x), "v"(y)
+        : "vcc");
+}
+__device__ __forceinline__ void mac96s(uint64_t& acc, uint32_t& c2, uint32_t x, uint32_t y_sgpr) {
+    asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
+        "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+        : "+v"(acc), "+v"(c2)
+        : "v"(x), "s"(y_sgpr)
+        : "vcc");
+}
+
+// Montgomery product by operand-interleaved product scanning (column-wise):
+// column k accumulates a_i*b_{k-i} and m_i*p_{k-i} into a 96-bit accumulator;
+// for k < 8 the new digit m_k = lo * (-p^-1) zeroes the column.  128
+// v_mad_u64_u32 + 128 v_addc and no per-product 64-bit add/move chains (the
+// CIOS form needs ~500 instructions, this one ~330).
+template <class C>
+__device__ __forceinline__ Fe<C> mont_mul_ps(const Fe<C>& a, const Fe<C>& b) {
+    const uint32_t a0 = a.v[0], a1 = a.v[1], a2 = a.v[2], a3 = a.v[3], a4 = a.v[4], a5 = a.v[5],
+                   a6 = a.v[6], a7 = a.v[7];
+    const uint32_t b0 = b.v[0], b1 = b.v[1], b2 = b.v[2], b3 = b.v[3], b4 = b.v[4], b5 = b.v[5],
+                   b6 = b.v[6], b7 = b.v[7];
+    const uint32_t P0 = C::P[0], P1 = C::P[1], P2 = C::P[2], P3 = C::P[3], P4 = C::P[4],
+                   P5 = C::P[5], P6 = C::P[6], P7 = C::P[7], INV = C::INV;
+    uint32_t m0, m1, m2, m3, m4, m5, m6, m7;
+    uint32_t t[8];
+    uint64_t acc = 0;
+    uint32_t c2 = 0;
+#include "mont_ps.inc"
+    Fe<C> r, s;
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = __builtin_subc(t[i], C::P[i], br, &br);
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = br ? t[i] : s.v[i];
+    return r;
+}
+#endif
+
+#ifndef GG_MUL_CIOS
+#define GG_MUL_CIOS 0
+#endif
+
+// Montgomery multiplication: product scanning on the device (GG_MUL_CIOS=1
+// selects the portable CIOS form below), 64-bit limbs on the host.
 template <class C>
 GG_HD Fe<C> operator*(const Fe<C>& a, const Fe<C>& b) {
 #if !defined(__HIP_DEVICE_COMPILE__)
     return mont_mul_host(a, b);
+#elif !GG_MUL_CIOS
+    return mont_mul_ps(a, b);
 #else
     uint32_t t[8];
 #pragma unroll

@@ -1,16 +1,53 @@
-// Microbenchmark: BN254 Fp Montgomery multiplication throughput on gfx950,
-// plus raw v_mad_u64_u32 throughput, to calibrate the MSM/NTT rooflines.
+// Microbenchmark: BN254 Fp Montgomery multiplication throughput on gfx950
+// (product-scanning asm form vs portable CIOS), plus raw v_mad_u64_u32 rate.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
 #include "../gnark-fork_amd/csrc/field.cuh"
 using namespace gg;
 
+template <class C>
+__device__ __forceinline__ Fe<C> mul_cios(const Fe<C>& a, const Fe<C>& b) {
+    uint32_t t[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) t[j] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint64_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) { acc = (uint64_t)a.v[j] * b.v[i] + t[j] + (acc >> 32); t[j] = (uint32_t)acc; }
+        uint32_t t8 = (uint32_t)(acc >> 32);
+        uint32_t m = t[0] * C::INV;
+        acc = (uint64_t)m * C::P[0] + t[0];
+#pragma unroll
+        for (int j = 1; j < 8; j++) { acc = (uint64_t)m * C::P[j] + t[j] + (acc >> 32); t[j - 1] = (uint32_t)acc; }
+        t[7] = t8 + (uint32_t)(acc >> 32);
+    }
+    Fe<C> r, s; uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = __builtin_subc(t[i], C::P[i], br, &br);
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = br ? t[i] : s.v[i];
+    return r;
+}
+
+template <int V>
 __global__ void __launch_bounds__(256) k_mulchain(Fp* data, int iters) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     Fp a = data[2 * i], b = data[2 * i + 1], c = a, d = b;
-    for (int k = 0; k < iters; k++) { a = a * b; c = c * d; b = b * a; d = d * c; }
+    for (int k = 0; k < iters; k++) {
+        if (V == 0) { a = mul_cios(a, b); c = mul_cios(c, d); b = mul_cios(b, a); d = mul_cios(d, c); }
+        else { a = a * b; c = c * d; b = b * a; d = d * c; }
+    }
     data[2 * i] = a + c; data[2 * i + 1] = b + d;
+}
+
+// single-wave latency probe: one wave, dependent chain
+template <int V>
+__global__ void k_latency(Fp* data, int iters) {
+    Fp a = data[threadIdx.x], b = data[64 + threadIdx.x];
+    for (int k = 0; k < iters; k++) { if (V == 0) a = mul_cios(a, b); else a = a * b; }
+    data[threadIdx.x] = a;
 }
 
 __global__ void __launch_bounds__(256) k_mad(uint64_t* out, int iters) {
@@ -30,24 +67,40 @@ int main() {
     size_t n = (size_t)blocks * threads;
     std::vector<Fp> h(2 * n);
     for (size_t i = 0; i < 2 * n; i++) for (int l = 0; l < 8; l++) h[i].v[l] = (uint32_t)(i * 2654435761u + l * 40503u) & (l == 7 ? 0x0fffffffu : 0xffffffffu);
-    Fp* d; hipMalloc(&d, 2 * n * sizeof(Fp));
-    hipMemcpy(d, h.data(), 2 * n * sizeof(Fp), hipMemcpyHostToDevice);
-    hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+    Fp* d; (void)hipMalloc(&d, 2 * n * sizeof(Fp));
+    Fp* d2; (void)hipMalloc(&d2, 2 * n * sizeof(Fp));
+    (void)hipMemcpy(d, h.data(), 2 * n * sizeof(Fp), hipMemcpyHostToDevice);
+    (void)hipMemcpy(d2, h.data(), 2 * n * sizeof(Fp), hipMemcpyHostToDevice);
+    hipEvent_t e0, e1; (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
     int iters = 256;
-    k_mulchain<<<blocks, threads>>>(d, 4);
-    hipEventRecord(e0);
-    k_mulchain<<<blocks, threads>>>(d, iters);
-    hipEventRecord(e1); hipEventSynchronize(e1);
-    float ms; hipEventElapsedTime(&ms, e0, e1);
-    double muls = (double)n * iters * 4;
-    printf("{\"fp_mont_mul_per_s\": %.4e, \"ms\": %.3f}\n", muls / (ms * 1e-3), ms);
-    uint64_t* o; hipMalloc(&o, n * 8);
+    float ms;
+    for (int rep = 0; rep < 3; rep++) {
+        k_mulchain<0><<<blocks, threads>>>(d, 4);
+        (void)hipEventRecord(e0); k_mulchain<0><<<blocks, threads>>>(d, iters); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        printf("{\"variant\": \"cios\", \"fp_mont_mul_per_s\": %.4e}\n", (double)n * iters * 4 / (ms * 1e-3));
+        k_mulchain<1><<<blocks, threads>>>(d2, 4);
+        (void)hipEventRecord(e0); k_mulchain<1><<<blocks, threads>>>(d2, iters); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        printf("{\"variant\": \"product_scanning\", \"fp_mont_mul_per_s\": %.4e}\n", (double)n * iters * 4 / (ms * 1e-3));
+    }
+    // equality of the two variants on the same data
+    k_mulchain<0><<<blocks, threads>>>(d, 7); k_mulchain<1><<<blocks, threads>>>(d2, 7);
+    std::vector<Fp> r1(2 * n), r2(2 * n);
+    (void)hipMemcpy(r1.data(), d, 2 * n * sizeof(Fp), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(r2.data(), d2, 2 * n * sizeof(Fp), hipMemcpyDeviceToHost);
+    size_t diff = 0; for (size_t i = 0; i < 2 * n; i++) diff += !(r1[i] == r2[i]);
+    printf("{\"variants_differ\": %zu}\n", diff);
+    for (int v = 0; v < 2; v++) {
+        (void)hipEventRecord(e0);
+        if (v == 0) k_latency<0><<<1, 64>>>(d, 2000); else k_latency<1><<<1, 64>>>(d, 2000);
+        (void)hipEventRecord(e1); (void)hipEventSynchronize(e1); (void)hipEventElapsedTime(&ms, e0, e1);
+        printf("{\"variant\": \"%s\", \"single_wave_mul_latency_ns\": %.1f}\n", v ? "product_scanning" : "cios", ms * 1e6 / 2000);
+    }
+    uint64_t* o; (void)hipMalloc(&o, n * 8);
     k_mad<<<blocks, threads>>>(o, 4);
-    hipEventRecord(e0);
-    k_mad<<<blocks, threads>>>(o, 4096);
-    hipEventRecord(e1); hipEventSynchronize(e1);
-    hipEventElapsedTime(&ms, e0, e1);
-    double mads = (double)n * 4096 * 8;
-    printf("{\"mad_u64_u32_per_s\": %.4e, \"ms\": %.3f}\n", mads / (ms * 1e-3), ms);
+    (void)hipEventRecord(e0); k_mad<<<blocks, threads>>>(o, 4096); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    printf("{\"mad_u64_u32_per_s\": %.4e}\n", (double)n * 4096 * 8 / (ms * 1e-3));
     return 0;
 }
