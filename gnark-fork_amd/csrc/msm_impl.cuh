@@ -54,12 +54,11 @@ __device__ __forceinline__ void st(T* p, const T& v) {
 __global__ void k_scan_block(const uint32_t* in, uint32_t* out, uint32_t* sums, size_t n);
 __global__ void k_scan_add(uint32_t* out, const uint32_t* sums, size_t n);
 __global__ void k_set_total(uint32_t* out, const uint32_t* in, size_t n);
-__global__ void k_digits(const Fr* scalars, const uint32_t* sidx, size_t n, int c, int W,
-                         int32_t* digits, uint32_t* counts);
-__global__ void k_scatter(const int32_t* digits, size_t total, uint32_t* cursor, uint32_t* sorted);
+__global__ void k_set_total_max(uint32_t* out, const uint32_t* in, size_t n, const uint32_t* maxcnt);
 __global__ void k_item_counts(const uint32_t* offsets, size_t nb, int K, uint32_t* itemcnt,
                               uint32_t* maxcnt);
-__global__ void k_item_buckets(const uint32_t* item_off, size_t nb, uint32_t* item_bucket);
+__global__ void k_item_buckets(const uint32_t* item_off, size_t nb, size_t n_items,
+                               uint32_t* item_bucket);
 void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, hipStream_t st,
                     std::vector<DevBuf>& tmp, int depth = 0);
 int choose_c(size_t n, size_t point_bytes);
@@ -88,32 +87,69 @@ __global__ void __launch_bounds__(256) k_accum_affine(const Affine<F>* pts, cons
     st(partial + t, acc);
 }
 
-// level >= 2: sum up to K XYZZ partials of one bucket
+constexpr uint32_t LIGHT = 16;  // buckets with <= LIGHT partials: k_bucket_sum
+
+// In-place segmented tree over the level-1 partials: bucket b owns slots
+// [item_off[b], item_off[b+1]); after the launches with stride 1, 2, 4, ...
+// slot item_off[b] holds the bucket sum.  One thread per slot, no host syncs.
 template <class F>
-__global__ void __launch_bounds__(256) k_accum_xyzz(const Xyzz<F>* in, const uint32_t* offsets,
-                                                    const uint32_t* item_off,
-                                                    const uint32_t* item_bucket, size_t n_items,
-                                                    int K, Xyzz<F>* partial) {
-    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_items) return;
-    uint32_t b = item_bucket[t];
-    uint32_t j = (uint32_t)t - item_off[b];
-    uint32_t lo = offsets[b] + j * (uint32_t)K;
-    uint32_t hi = min(offsets[b + 1], lo + (uint32_t)K);
-    Xyzz<F> acc = ld(in + lo);
-    for (uint32_t e = lo + 1; e < hi; e++) acc = xyzz_add(acc, ld(in + e));
-    st(partial + t, acc);
+__global__ void __launch_bounds__(256) k_seg_tree(Xyzz<F>* part, const uint32_t* item_off,
+                                                  const uint32_t* item_bucket, size_t T,
+                                                  uint32_t stride, uint32_t fan) {
+    size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= T) return;
+    uint32_t b = item_bucket[p];
+    uint32_t o = item_off[b];
+    uint32_t j = (uint32_t)p - o;
+    uint32_t cnt = item_off[b + 1] - o;
+    if (cnt <= LIGHT) return;  // done by k_bucket_sum
+    if (j % (fan * stride)) return;
+    if (j + stride >= cnt) return;
+    Xyzz<F> acc = ld(part + p);
+    for (uint32_t k = 1; k < fan && j + k * stride < cnt; k++) acc = xyzz_add(acc, ld(part + p + k * stride));
+    st(part + p, acc);
+}
+
+// One thread per bucket sums its <= LIGHT partials in a chain (all lanes busy);
+// heavier buckets are left to k_seg_tree (skipped here).
+template <class F>
+__global__ void __launch_bounds__(256) k_bucket_sum(Xyzz<F>* part, const uint32_t* item_off, size_t nb) {
+    size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    uint32_t o = item_off[b], cnt = item_off[b + 1] - o;
+    if (cnt < 2 || cnt > LIGHT) return;
+    Xyzz<F> acc = ld(part + o);
+    for (uint32_t k = 1; k < cnt; k++) acc = xyzz_add(acc, ld(part + o + k));
+    st(part + o, acc);
 }
 
 // ------------------------------------------------------------ reduction v2
 // Dense bucket sums: S[b] = partial of bucket b (or infinity)
+// (item_off is indexed in sort order pi(b) = bitrev_{c-1}(b), see sort_entries)
 template <class F>
-__global__ void k_gather_buckets(const Xyzz<F>* partial, const uint32_t* item_off, size_t nb,
+__global__ void k_gather_buckets(const Xyzz<F>* partial, const uint32_t* item_off, size_t nb, int c,
                                  Xyzz<F>* S) {
     size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
-    uint32_t o = item_off[b];
-    st(S + b, (item_off[b + 1] > o) ? ld(partial + o) : Xyzz<F>::inf());
+    uint32_t q = __brev((uint32_t)b) >> (33 - c);
+    uint32_t o = item_off[q];
+    st(S + b, (item_off[q + 1] > o) ? ld(partial + o) : Xyzz<F>::inf());
+}
+
+// copy a list of small device arrays into one contiguous staging buffer
+template <class F>
+struct GatherList {
+    const Xyzz<F>* src[64];
+    uint32_t off[65];
+    int n;
+};
+template <class F>
+__global__ void k_gather_items(GatherList<F> L, Xyzz<F>* out) {
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    int q = 0;
+    while (q < L.n && t >= L.off[q + 1]) q++;
+    if (q >= L.n) return;
+    st(out + t, ld(L.src[q] + (t - L.off[q])));
 }
 
 // Generic strided group sum: view X[a][c] = in[a*sa + c*sb], a < A, c < Bc;
@@ -204,7 +240,7 @@ struct gg_msm_base {
     std::mutex mu;
     // scratch
     DevBuf digits, sorted, counts, offsets, cursor, itemcnt, item_off, item_bucket, maxcnt;
-    DevBuf keys, tmp_entry, tmp_key, hist, hoff, bin_start;
+    DevBuf keys, tmp_entry, tmp_key, hist, hoff, bin_start, chunk_start, chunk_hist, chunk_pos;
     DevBuf partA, partB, segs, segs2, scal;
     std::vector<DevBuf> scan_tmp;
 };
@@ -241,7 +277,8 @@ inline void precompute(gg_msm_base* b, const Affine<F>* dev_in, hipStream_t st) 
 // tree sums that run wide on the GPU.  Pieces of <= 16 elements finish on the
 // host, combined by Horner over their 2^mlog factors.
 template <class F>
-inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* partials, hipStream_t st) {
+inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* partials, const uint32_t* item_off,
+                                hipStream_t st) {
     const size_t nb = b->nb;
     const size_t XB = sizeof(Xyzz<F>);
     b->segs.reserve(nb * XB);
@@ -249,7 +286,7 @@ inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* partials, hipStre
     b->segs2.reserve(arena_elems * XB);
     Xyzz<F>* S = b->segs.as<Xyzz<F>>();
     hipLaunchKernelGGL(k_gather_buckets<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, partials,
-                       b->item_off.as<uint32_t>(), nb, S);
+                       item_off, nb, b->c, S);
     GG_HIP(hipGetLastError());
     Xyzz<F>* arena = b->segs2.as<Xyzz<F>>();
     size_t used = 0;
@@ -310,13 +347,25 @@ inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* partials, hipStre
         items.swap(next);
     }
     // host: tiny weighted sums + Horner over the 2^mlog factors
-    std::vector<std::vector<Xyzz<F>>> hx(host_items.size());
+    GG_CHECK(host_items.size() <= 64, GG_ERR_INTERNAL, "too many host reduction items");
+    GatherList<F> GL;
+    GL.n = (int)host_items.size();
+    GL.off[0] = 0;
     for (size_t k = 0; k < host_items.size(); k++) {
-        hx[k].resize(host_items[k].n);
-        GG_HIP(hipMemcpyAsync(hx[k].data(), host_items[k].X, host_items[k].n * XB,
-                              hipMemcpyDeviceToHost, st));
+        GL.src[k] = host_items[k].X;
+        GL.off[k + 1] = GL.off[k] + host_items[k].n;
+    }
+    std::vector<Xyzz<F>> flat(GL.off[GL.n]);
+    if (GL.n) {
+        Xyzz<F>* stage = alloc(GL.off[GL.n]);
+        hipLaunchKernelGGL(k_gather_items<F>, dim3(grid_for(GL.off[GL.n], 256)), dim3(256), 0, st, GL, stage);
+        GG_HIP(hipGetLastError());
+        GG_HIP(hipMemcpyAsync(flat.data(), stage, flat.size() * XB, hipMemcpyDeviceToHost, st));
     }
     GG_HIP(hipStreamSynchronize(st));
+    std::vector<std::vector<Xyzz<F>>> hx(host_items.size());
+    for (size_t k = 0; k < host_items.size(); k++)
+        hx[k].assign(flat.begin() + GL.off[k], flat.begin() + GL.off[k + 1]);
     std::vector<std::pair<int, Xyzz<F>>> vals;
     for (size_t k = 0; k < host_items.size(); k++) {
         const auto& X = hx[k];
@@ -345,83 +394,74 @@ inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* partials, hipStre
 template <class F>
 inline Xyzz<F> msm_run(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st) {
     const size_t n = b->n, nb = b->nb;
-    const int c = b->c, W = b->W;
-    const size_t total = (size_t)W * n;
     if (n == 0) return Xyzz<F>::inf();
     b->counts.reserve(nb * 4);
     b->offsets.reserve((nb + 1) * 4);
     b->itemcnt.reserve(nb * 4);
-    b->item_off.reserve((nb + 1) * 4);
+    b->item_off.reserve((nb + 2) * 4);
     b->maxcnt.reserve(4);
     ProfScope ps_sort("msm_sort", st, (double)n);
     sort_entries(b, scalars_dev, st);
     ps_sort.stop(st);
 
-    // ---- level 1: affine entries -> partials
-    const int K1 = 32, K2 = 16;
-    uint32_t* offsets = b->offsets.as<uint32_t>();
+    // ---- level 1: affine entries -> partials.  Buckets are cut into items of
+    // <= K entries; bucket b's partials land at part[item_off[b] .. item_off[b+1]).
+    const int K1 = 32;
+    b->item_off.reserve((nb + 2) * 4);
+    uint32_t* offs = b->offsets.as<uint32_t>();
+    uint32_t* ioff = b->item_off.as<uint32_t>();
     uint32_t host[2];
-    GG_HIP(hipMemsetAsync(b->maxcnt.p, 0, 4, st));
-    hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nb, 256)), dim3(256), 0, st, offsets, nb, K1,
-                       b->itemcnt.as<uint32_t>(), b->maxcnt.as<uint32_t>());
-    GG_HIP(hipGetLastError());
-    exclusive_scan(b->itemcnt.as<uint32_t>(), b->item_off.as<uint32_t>(), nb, st, b->scan_tmp);
-    hipLaunchKernelGGL(k_set_total, dim3(1), dim3(1), 0, st, b->item_off.as<uint32_t>(),
-                       b->itemcnt.as<uint32_t>(), nb);
-    GG_HIP(hipMemcpyAsync(&host[0], b->item_off.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
-    GG_HIP(hipMemcpyAsync(&host[1], b->maxcnt.p, 4, hipMemcpyDeviceToHost, st));
-    GG_HIP(hipStreamSynchronize(st));
-    size_t n_items = host[0];
-    uint32_t max_items = host[1];
-    b->item_bucket.reserve((n_items + 1) * 4);
+    auto make_items = [&](const uint32_t* in_off, uint32_t* out_off, int K) {
+        GG_HIP(hipMemsetAsync(b->maxcnt.p, 0, 4, st));
+        hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nb, 256)), dim3(256), 0, st, in_off, nb, K,
+                           b->itemcnt.as<uint32_t>(), b->maxcnt.as<uint32_t>());
+        GG_HIP(hipGetLastError());
+        exclusive_scan(b->itemcnt.as<uint32_t>(), out_off, nb, st, b->scan_tmp);
+        hipLaunchKernelGGL(k_set_total_max, dim3(1), dim3(1), 0, st, out_off,
+                           b->itemcnt.as<uint32_t>(), nb, b->maxcnt.as<uint32_t>());
+        GG_HIP(hipMemcpyAsync(host, out_off + nb, 8, hipMemcpyDeviceToHost, st));
+        GG_HIP(hipStreamSynchronize(st));
+        b->item_bucket.reserve(((size_t)host[0] + 1) * 4);
+        if (host[0])
+            hipLaunchKernelGGL(k_item_buckets, dim3(grid_for(host[0], 256)), dim3(256), 0, st, out_off,
+                               nb, (size_t)host[0], b->item_bucket.as<uint32_t>());
+        GG_HIP(hipGetLastError());
+        return std::make_pair((size_t)host[0], host[1]);
+    };
+    auto it1 = make_items(offs, ioff, K1);
+    size_t n_items = it1.first;
+    uint32_t max_items = it1.second;
     b->partA.reserve((n_items + 1) * sizeof(Xyzz<F>));
     if (n_items) {
-        hipLaunchKernelGGL(k_item_buckets, dim3(grid_for(nb, 256)), dim3(256), 0, st,
-                           b->item_off.as<uint32_t>(), nb, b->item_bucket.as<uint32_t>());
-        GG_HIP(hipGetLastError());
         ProfScope ps_acc("msm_accum", st, (double)n);
         hipLaunchKernelGGL(k_accum_affine<F>, dim3(grid_for(n_items, 256)), dim3(256), 0, st,
-                           (const Affine<F>*)b->pts.p, b->sorted.as<uint32_t>(), offsets,
-                           b->item_off.as<uint32_t>(), b->item_bucket.as<uint32_t>(), n_items,
-                           K1, b->partA.as<Xyzz<F>>());
+                           (const Affine<F>*)b->pts.p, b->sorted.as<uint32_t>(), offs, ioff,
+                           b->item_bucket.as<uint32_t>(), n_items, K1, b->partA.as<Xyzz<F>>());
         GG_HIP(hipGetLastError());
         ps_acc.stop(st);
     }
-    // ---- levels >= 2 until every bucket has <= 1 partial
-    // bucket b's partials: partA[item_off[b] .. item_off[b+1])
-    DevBuf* cur_part = &b->partA;
-    DevBuf* nxt_part = &b->partB;
+    // ---- per-bucket tree over the partials (skew-robust: a bucket holding most
+    // entries costs log2(items) launches, not serial chains)
     ProfScope ps_acc2("msm_accum2", st, (double)n);
-    while (max_items > 1) {
-        // offsets <- item_off (partials are contiguous per bucket)
-        GG_HIP(hipMemcpyAsync(b->offsets.p, b->item_off.p, (nb + 1) * 4, hipMemcpyDeviceToDevice, st));
-        GG_HIP(hipMemsetAsync(b->maxcnt.p, 0, 4, st));
-        hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nb, 256)), dim3(256), 0, st, offsets, nb,
-                           K2, b->itemcnt.as<uint32_t>(), b->maxcnt.as<uint32_t>());
+    if (max_items > 1) {
+        hipLaunchKernelGGL(k_bucket_sum<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st,
+                           b->partA.as<Xyzz<F>>(), ioff, nb);
         GG_HIP(hipGetLastError());
-        exclusive_scan(b->itemcnt.as<uint32_t>(), b->item_off.as<uint32_t>(), nb, st, b->scan_tmp);
-        hipLaunchKernelGGL(k_set_total, dim3(1), dim3(1), 0, st, b->item_off.as<uint32_t>(),
-                           b->itemcnt.as<uint32_t>(), nb);
-        GG_HIP(hipMemcpyAsync(&host[0], b->item_off.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
-        GG_HIP(hipMemcpyAsync(&host[1], b->maxcnt.p, 4, hipMemcpyDeviceToHost, st));
-        GG_HIP(hipStreamSynchronize(st));
-        n_items = host[0];
-        max_items = host[1];
-        b->item_bucket.reserve((n_items + 1) * 4);
-        nxt_part->reserve((n_items + 1) * sizeof(Xyzz<F>));
-        hipLaunchKernelGGL(k_item_buckets, dim3(grid_for(nb, 256)), dim3(256), 0, st,
-                           b->item_off.as<uint32_t>(), nb, b->item_bucket.as<uint32_t>());
-        GG_HIP(hipGetLastError());
-        hipLaunchKernelGGL(k_accum_xyzz<F>, dim3(grid_for(n_items, 256)), dim3(256), 0, st,
-                           (const Xyzz<F>*)cur_part->p, offsets, b->item_off.as<uint32_t>(),
-                           b->item_bucket.as<uint32_t>(), n_items, K2, nxt_part->as<Xyzz<F>>());
-        GG_HIP(hipGetLastError());
-        std::swap(cur_part, nxt_part);
     }
+    // heavy buckets (> LIGHT items): fan-in 4 first, then binary steps
+    for (uint32_t stride = 1; max_items > LIGHT && stride < max_items;) {
+        uint32_t fan = (stride == 1) ? 4u : 2u;
+        hipLaunchKernelGGL(k_seg_tree<F>, dim3(grid_for(n_items, 256)), dim3(256), 0, st,
+                           b->partA.as<Xyzz<F>>(), ioff, b->item_bucket.as<uint32_t>(), n_items, stride,
+                           fan);
+        GG_HIP(hipGetLastError());
+        stride *= fan;
+    }
+    DevBuf* cur_part = &b->partA;
     ps_acc2.stop(st);
     // ---- bucket reduction: sum_b (b+1) S_b
     ProfScope ps_red("msm_reduce", st, (double)nb);
-    Xyzz<F> res = bucket_reduce_2d<F>(b, (const Xyzz<F>*)cur_part->p, st);
+    Xyzz<F> res = bucket_reduce_2d<F>(b, (const Xyzz<F>*)cur_part->p, ioff, st);
     ps_red.stop(st);
     return res;
 }

@@ -87,6 +87,19 @@ def test_msm_edge_cases():
     assert base4.msm(s2, 2) == bytes(64)
 
 
+@pytest.mark.parametrize("n,frac_one", [(1 << 16, 1.0), (1 << 18, 0.9)])
+def test_msm_skewed_scalars(n, frac_one):
+    """Real witnesses are 0/1-heavy: one bucket can hold most entries."""
+    from gnark_amd import msm
+    pts = random_g1_points(n, 70)
+    sc = random_fr_mont(n, 71)
+    one = np.frombuffer(o.fr_to_bytes(1), dtype=np.uint64)
+    sel = np.random.default_rng(72).random(n) < frac_one
+    sc[sel] = one
+    base = msm.MsmBase(msm.G1, pts, n)
+    assert base.msm(sc, n) == coracle.msm_g1(pts.tobytes(), sc.tobytes(), n)
+
+
 def test_msm_scalar_index_map():
     from gnark_amd import msm
     n, nw = 3000, 5000
