@@ -93,6 +93,31 @@ GG_HD Xyzz<F> xyzz_madd(const Xyzz<F>& p, const Affine<F>& q) {
     return Xyzz<F>{X3, Y3, p.zz * PP, p.zzz * PPP};
 }
 
+// madd-2008-s in place, ordered to keep few temporaries live (ZZ/ZZZ are
+// updated as soon as PP/PPP exist, X2/Y2 die right after first use).  Same
+// results as xyzz_madd; this is the bucket-accumulation hot loop.
+template <class F>
+GG_HD void xyzz_madd_inplace(Xyzz<F>& p, const Affine<F>& q) {
+    if (p.is_inf()) {
+        p = Xyzz<F>{q.x, q.y, F::one(), F::one()};
+        return;
+    }
+    F P = q.x * p.zz - p.x;
+    F R = q.y * p.zzz - p.y;
+    if (P.is_zero()) {
+        p = R.is_zero() ? xyzz_dbl_affine(q) : Xyzz<F>::inf();
+        return;
+    }
+    F PP = sqr(P);
+    p.zz = p.zz * PP;
+    F PPP = P * PP;
+    p.zzz = p.zzz * PPP;
+    F Q = p.x * PP;
+    F X3 = sqr(R) - PPP - dbl(Q);
+    p.y = R * (Q - X3) - p.y * PPP;
+    p.x = X3;
+}
+
 // add-2008-s
 template <class F>
 GG_HD Xyzz<F> xyzz_add(const Xyzz<F>& p, const Xyzz<F>& q) {
@@ -114,6 +139,31 @@ GG_HD Xyzz<F> xyzz_add(const Xyzz<F>& p, const Xyzz<F>& q) {
     F X3 = sqr(R) - PPP - dbl(Q);
     F Y3 = R * (Q - X3) - S1 * PPP;
     return Xyzz<F>{X3, Y3, p.zz * q.zz * PP, p.zzz * q.zzz * PPP};
+}
+
+// add-2008-s in place (p += q), ordered for low register pressure
+template <class F>
+GG_HD void xyzz_add_inplace(Xyzz<F>& p, const Xyzz<F>& q) {
+    if (q.is_inf()) return;
+    if (p.is_inf()) {
+        p = q;
+        return;
+    }
+    F U1 = p.x * q.zz;
+    F S1 = p.y * q.zzz;
+    F P = q.x * p.zz - U1;
+    F R = q.y * p.zzz - S1;
+    if (P.is_zero()) {
+        p = R.is_zero() ? xyzz_dbl(p) : Xyzz<F>::inf();
+        return;
+    }
+    F PP = sqr(P);
+    p.zz = p.zz * q.zz * PP;
+    F PPP = P * PP;
+    p.zzz = p.zzz * q.zzz * PPP;
+    F Q = U1 * PP;
+    p.x = sqr(R) - PPP - dbl(Q);
+    p.y = R * (Q - p.x) - S1 * PPP;
 }
 
 // XYZZ -> Jacobian: Z = ZZZ, X = X*ZZ^2, Y = Y*ZZZ^2

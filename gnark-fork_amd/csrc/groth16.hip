@@ -1,11 +1,11 @@
 // Groth16 BN254 prover on one MI355X: the device section of gnark's
 // icicle_bn254.Prove (icicle.go:133-422) / groth16_bn254.Prove (prove.go:127-320).
 //
-//   host thread 1 / stream 1:  computeH (7 fused NTTs)  ->  Z-MSM over h
-//   host thread 0 / stream 0:  A-MSM, B1-MSM, K-MSM, G2-MSM (wire scalars
-//                              gathered through per-base index maps)
-//   host pool:                 r*delta, s*delta, kr*delta, s*delta2 while the
-//                              GPU works; s*Ar, r*Bs1 after the MSMs
+//   stream 1: computeH (7 fused NTTs) -> Z-MSM over h
+//   streams 2, 3, 4, 0: A-MSM, B1-MSM, K-MSM, G2-MSM, concurrently (wire
+//                       scalars gathered through per-base index maps)
+//   host pool: r*delta, s*delta, kr*delta, s*delta2 while the GPU works;
+//              s*Ar, r*Bs1 after the MSMs
 // Combination formulas are prove.go:206-299 verbatim.
 #include "common.h"
 #include "curve.cuh"
@@ -37,7 +37,7 @@ struct gg_groth16_pk {
     G2Affine beta2, delta2;
     size_t n_wires = 0, nb_public = 0;
     DevBuf wires, sa, sb, sc;
-    hipStream_t s0 = nullptr, s1 = nullptr;
+    hipStream_t s0 = nullptr, s1 = nullptr, s2 = nullptr, s3 = nullptr, s4 = nullptr;
     int device = 0;
     std::mutex mu;
     ~gg_groth16_pk() {
@@ -47,8 +47,8 @@ struct gg_groth16_pk {
         if (Z) gg_msm_base_release(Z);
         if (B2) gg_msm_base_release(B2);
         if (dom) gg_domain_release(dom);
-        if (s0) (void)hipStreamDestroy(s0);
-        if (s1) (void)hipStreamDestroy(s1);
+        for (hipStream_t x : {s0, s1, s2, s3, s4})
+            if (x) (void)hipStreamDestroy(x);
     }
 };
 
@@ -107,8 +107,8 @@ extern "C" int gg_groth16_pk_create(int log_n, const void* omega_mont, const voi
     ck(gg_msm_base_create(GG_G1, g1_K, nK, 0, ik.data(), 0, &pk->K));
     ck(gg_msm_base_create(GG_G1, g1_Z, nZ, 0, nullptr, 0, &pk->Z));
     ck(gg_msm_base_create(GG_G2, g2_B, nB, 0, ib.data(), 0, &pk->B2));
-    GG_HIP(hipStreamCreateWithFlags(&pk->s0, hipStreamNonBlocking));
-    GG_HIP(hipStreamCreateWithFlags(&pk->s1, hipStreamNonBlocking));
+    for (hipStream_t* x : {&pk->s0, &pk->s1, &pk->s2, &pk->s3, &pk->s4})
+        GG_HIP(hipStreamCreateWithFlags(x, hipStreamNonBlocking));
     *out = pk.release();
     GG_CAPI_END
 }
@@ -181,54 +181,56 @@ extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_
     GG_HIP(hipStreamSynchronize(pk->s0));
     double t_up = now_ms();
 
-    // stream 1 (worker thread): computeH then Z-MSM; h lands in A
-    G1Jac jz = G1Jac::inf();
-    double t_h = 0, t_z = 0;
+    // Five concurrent tasks, one host thread + HIP stream each (MSM tails are
+    // latency-bound, so overlapping them fills the chip):
+    //   s1: computeH -> Z-MSM (h lands in A's buffer)    s2: A-MSM
+    //   s3: B1-MSM    s4: K-MSM    s0 (this thread): G2-MSM
+    G1Jac jz = G1Jac::inf(), ja, jb, jk;
+    G2Jac j2;
+    double t_h = 0, t_z = 0, t_a = 0, t_b = 0, t_k = 0;
+    std::mutex emu;
     std::string werr;
     int wcode = GG_OK;
-    int dev = pk->device;
-    std::thread worker([&] {
-        try {
-            GG_HIP(hipSetDevice(dev));
-            double a = now_ms();
-            compute_h_device(pk->dom, A, B, C, A, pk->s1);
-            GG_HIP(hipStreamSynchronize(pk->s1));
-            double b = now_ms();
-            t_h = b - a;
-            if (h_dev_out) GG_HIP(hipMemcpyAsync(h_dev_out, A, nbytes, hipMemcpyDeviceToDevice, pk->s1));
-            if (n > 1) msm_device(pk->Z, A, &jz, pk->s1);
-            t_z = now_ms() - b;
-        } catch (const Error& e) {
-            werr = e.what();
-            wcode = e.code;
-        } catch (const std::exception& e) {
-            werr = e.what();
-            wcode = GG_ERR_INTERNAL;
-        }
-    });
-
-    G1Jac ja, jb, jk;
-    G2Jac j2;
-    double ta = now_ms();
-    try {
-        msm_device(pk->A, wdev, &ja, pk->s0);
-        double tb = now_ms();
-        msm_device(pk->B, wdev, &jb, pk->s0);
-        double tk = now_ms();
-        msm_device(pk->K, wdev, &jk, pk->s0);
-        double t2 = now_ms();
-        msm_device(pk->B2, wdev, &j2, pk->s0);
-        double te = now_ms();
-        g_timings[2] = tb - ta;
-        g_timings[3] = tk - tb;
-        g_timings[4] = t2 - tk;
-        g_timings[6] = te - t2;
-    } catch (...) {
-        worker.join();
-        throw;
-    }
-    worker.join();
+    const int dev = pk->device;
+    auto guarded = [&](auto fn) {
+        return [&, fn]() {
+            try {
+                GG_HIP(hipSetDevice(dev));
+                fn();
+            } catch (const Error& e) {
+                std::lock_guard<std::mutex> g(emu);
+                werr = e.what();
+                wcode = e.code;
+            } catch (const std::exception& e) {
+                std::lock_guard<std::mutex> g(emu);
+                werr = e.what();
+                wcode = GG_ERR_INTERNAL;
+            }
+        };
+    };
+    std::vector<std::thread> workers;
+    workers.emplace_back(guarded([&] {
+        double a = now_ms();
+        compute_h_device(pk->dom, A, B, C, A, pk->s1);
+        GG_HIP(hipStreamSynchronize(pk->s1));
+        double b = now_ms();
+        t_h = b - a;
+        if (h_dev_out) GG_HIP(hipMemcpyAsync(h_dev_out, A, nbytes, hipMemcpyDeviceToDevice, pk->s1));
+        if (n > 1) msm_device(pk->Z, A, &jz, pk->s1);
+        t_z = now_ms() - b;
+    }));
+    workers.emplace_back(guarded([&] { double a = now_ms(); msm_device(pk->A, wdev, &ja, pk->s2); t_a = now_ms() - a; }));
+    workers.emplace_back(guarded([&] { double a = now_ms(); msm_device(pk->B, wdev, &jb, pk->s3); t_b = now_ms() - a; }));
+    workers.emplace_back(guarded([&] { double a = now_ms(); msm_device(pk->K, wdev, &jk, pk->s4); t_k = now_ms() - a; }));
+    double t2 = now_ms();
+    guarded([&] { msm_device(pk->B2, wdev, &j2, pk->s0); })();
+    double te = now_ms();
+    for (auto& w : workers) w.join();
     if (wcode != GG_OK) throw Error(wcode, werr);
+    g_timings[2] = t_a;
+    g_timings[3] = t_b;
+    g_timings[4] = t_k;
+    g_timings[6] = te - t2;
     double tep = now_ms();
 
     // epilogue (prove.go:206-299)

@@ -66,7 +66,7 @@ void sort_entries(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st);
 
 // level 1: sum up to K affine points of one bucket into an XYZZ partial
 template <class F>
-__global__ void __launch_bounds__(256) k_accum_affine(const Affine<F>* pts, const uint32_t* sorted,
+__global__ void __launch_bounds__(256, 2) k_accum_affine(const Affine<F>* pts, const uint32_t* sorted,
                                                       const uint32_t* offsets,
                                                       const uint32_t* item_off,
                                                       const uint32_t* item_bucket, size_t n_items,
@@ -82,7 +82,7 @@ __global__ void __launch_bounds__(256) k_accum_affine(const Affine<F>* pts, cons
         uint32_t v = sorted[e];
         Affine<F> p = ld(pts + (v & 0x7fffffffu));
         if (v >> 31) p.y = -p.y;
-        acc = xyzz_madd(acc, p);
+        xyzz_madd_inplace(acc, p);
     }
     st(partial + t, acc);
 }
@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(256) k_seg_tree(Xyzz<F>* part, const uint32_t*
     if (j % (fan * stride)) return;
     if (j + stride >= cnt) return;
     Xyzz<F> acc = ld(part + p);
-    for (uint32_t k = 1; k < fan && j + k * stride < cnt; k++) acc = xyzz_add(acc, ld(part + p + k * stride));
+    for (uint32_t k = 1; k < fan && j + k * stride < cnt; k++) xyzz_add_inplace(acc, ld(part + p + k * stride));
     st(part + p, acc);
 }
 
@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(256) k_bucket_sum(Xyzz<F>* part, const uint32_
     uint32_t o = item_off[b], cnt = item_off[b + 1] - o;
     if (cnt < 2 || cnt > LIGHT) return;
     Xyzz<F> acc = ld(part + o);
-    for (uint32_t k = 1; k < cnt; k++) acc = xyzz_add(acc, ld(part + o + k));
+    for (uint32_t k = 1; k < cnt; k++) xyzz_add_inplace(acc, ld(part + o + k));
     st(part + o, acc);
 }
 
@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(256) k_reduce_jobs(RedJobs<F> J) {
     uint32_t a0 = a2 * jb.G;
     uint32_t a1 = min(jb.A, a0 + jb.G);
     Xyzz<F> acc = ld(jb.in + (size_t)a0 * jb.sa + (size_t)c * jb.sb);
-    for (uint32_t a = a0 + 1; a < a1; a++) acc = xyzz_add(acc, ld(jb.in + (size_t)a * jb.sa + (size_t)c * jb.sb));
+    for (uint32_t a = a0 + 1; a < a1; a++) xyzz_add_inplace(acc, ld(jb.in + (size_t)a * jb.sa + (size_t)c * jb.sb));
     st(jb.out + (size_t)a2 * jb.Bc + c, acc);
 }
 
