@@ -4,11 +4,14 @@
 //
 // Layout / schedule (DESIGN.md "NTT"):
 //   * the 2^L vector lives in HBM as gnark fr.Element (32 B, Montgomery);
-//   * a transform is split into P passes; each pass owns k consecutive bit
-//     positions (butterfly spans) and moves tiles of 2^k x 2^tl elements
-//     (<= 2048 = 64 KiB) through LDS, running its k butterfly stages there;
-//     strided passes load 2^tl adjacent elements per row (256-B segments);
-//   * twiddles w^i (i < n/2) are a resident HBM table (256 MiB at 2^24);
+//   * a transform is split into passes; each pass owns k consecutive bit
+//     positions (butterfly spans) of a 2048-element tile (2^k rows x 2^tl
+//     adjacent columns; the first DIT / last DIF pass is contiguous, k = 11);
+//   * inside a pass the k stages run as radix-8 register rounds (3 stages per
+//     LDS exchange): the first round reads HBM, the last writes HBM, middle
+//     rounds go through a padded limb-major LDS tile (conflict-free);
+//   * twiddles: per-stage contiguous tables tw[2^b - 1 + i] = w^(i 2^(L-1-b))
+//     (n-1 entries, 512 MiB at 2^24), so every stage streams its own table;
 //   * coset / 1/n / den scalings are fused into the first or last pass as
 //     multiplication by hi[e >> S] * lo[e & (2^S-1)], e = i or bitrev(i),
 //     from two 2^(L/2)-entry tables (no n-sized coset tables);
@@ -87,86 +90,131 @@ __device__ __forceinline__ Fr apply_scale(const ScaleSpec& s, uint32_t g, int L,
     return x * f;
 }
 
-// LDS tile stored limb-major: lds[l * T + e]
-__device__ __forceinline__ Fr lds_get(const uint32_t* lds, int T, int e) {
-    Fr r;
+// ---- radix-8 register-round pass ------------------------------------------
+__device__ __forceinline__ int lidx(int e) { return e + (e >> 5); }  // padded LDS index
+
+template <int NB, bool DIT>
+__device__ __forceinline__ void ntt_round(const PassParams& P, uint32_t* lds, int TP, int T, int qlo,
+                                          bool first, bool last, uint32_t base_hi, uint32_t lo0) {
+    constexpr int R = 1 << NB;
+    const int tl = P.tl;
+    const uint32_t tl_mask = (1u << tl) - 1;
+    const int pos = qlo + tl;
+    const uint32_t lowmask = (1u << pos) - 1;
+    const int groups = T >> NB;
+    for (int gi = threadIdx.x; gi < groups; gi += blockDim.x) {
+        uint32_t e[R], g[R];
+        Fr x[R];
+        const uint32_t low = (uint32_t)gi & lowmask, high = ((uint32_t)gi >> pos) << (pos + NB);
 #pragma unroll
-    for (int l = 0; l < 8; l++) r.v[l] = lds[l * T + e];
-    return r;
-}
-__device__ __forceinline__ void lds_put(uint32_t* lds, int T, int e, const Fr& x) {
+        for (int m = 0; m < R; m++) {
+            e[m] = high | ((uint32_t)m << pos) | low;
+            g[m] = base_hi | ((e[m] >> tl) << P.b_lo) | (lo0 + (e[m] & tl_mask));
+        }
+        if (first) {
 #pragma unroll
-    for (int l = 0; l < 8; l++) lds[l * T + e] = x.v[l];
+            for (int m = 0; m < R; m++) {
+                x[m] = load_fr(P.in + g[m]);
+                if (P.has_pre) x[m] = apply_scale(P.pre, g[m], P.log_n, x[m]);
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < R; m++) {
+#pragma unroll
+                for (int l = 0; l < 8; l++) x[m].v[l] = lds[l * TP + lidx((int)e[m])];
+            }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < NB; s2++) {
+            const int r = DIT ? s2 : (NB - 1 - s2);
+            const int b = P.b_lo + qlo + r;
+            const uint32_t bmask = (1u << b) - 1;
+            const Fr* twb = P.tw + bmask;  // stage-b table starts at 2^b - 1
+#pragma unroll
+            for (int m = 0; m < R; m++) {
+                if (m & (1 << r)) continue;
+                const int m2 = m | (1 << r);
+                const uint32_t i = g[m] & bmask;
+                if (DIT) {
+                    Fr t = i ? x[m2] * load_fr(twb + i) : x[m2];
+                    x[m2] = x[m] - t;
+                    x[m] = x[m] + t;
+                } else {
+                    Fr d = x[m] - x[m2];
+                    x[m] = x[m] + x[m2];
+                    x[m2] = i ? d * load_fr(twb + i) : d;
+                }
+            }
+        }
+        if (last) {
+#pragma unroll
+            for (int m = 0; m < R; m++) {
+                Fr y = x[m];
+                if (P.has_post) y = apply_scale(P.post, g[m], P.log_n, y);
+                if (P.epi_mul_sub) y = load_fr(P.ea + g[m]) * load_fr(P.eb + g[m]) - y;
+                store_fr(P.out + g[m], y);
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < R; m++) {
+#pragma unroll
+                for (int l = 0; l < 8; l++) lds[l * TP + lidx((int)e[m])] = x[m].v[l];
+            }
+        }
+    }
 }
 
+template <bool DIT>
 __global__ void __launch_bounds__(256) k_ntt_pass(PassParams P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int k = P.k, tl = P.tl;
     const int T = 1 << (k + tl);
-    const uint32_t tl_mask = (1u << tl) - 1;
+    const int TP = T + (T >> 5);
     const int nlo_log = P.b_lo - tl;
     const uint32_t tile = blockIdx.x;
     const uint32_t lob = tile & ((1u << nlo_log) - 1);
     const uint32_t hi = tile >> nlo_log;
     const uint32_t base_hi = hi << (P.b_lo + k);
     const uint32_t lo0 = lob << tl;
-
-    for (int e = threadIdx.x; e < T; e += blockDim.x) {
-        uint32_t j = (uint32_t)e >> tl, lol = (uint32_t)e & tl_mask;
-        uint32_t g = base_hi | (j << P.b_lo) | (lo0 + lol);
-        Fr x = load_fr(P.in + g);
-        if (P.has_pre) x = apply_scale(P.pre, g, P.log_n, x);
-        lds_put(lds, T, e, x);
-    }
-    __syncthreads();
-
-    const int half = T >> 1;
-    for (int st = 0; st < k; st++) {
-        const int q = P.dit ? st : (k - 1 - st);
-        const int b = P.b_lo + q;
-        const uint32_t qmask = (1u << q) - 1;
-        const uint32_t bmask = (1u << b) - 1;
-        const int tshift = P.log_n - 1 - b;
-        for (int u = threadIdx.x; u < half; u += blockDim.x) {
-            uint32_t lol = (uint32_t)u & tl_mask;
-            uint32_t jj = (uint32_t)u >> tl;
-            uint32_t j = ((jj >> q) << (q + 1)) | (jj & qmask);
-            int e0 = (int)((j << tl) | lol);
-            int e1 = e0 + (1 << (q + tl));
-            uint32_t g0 = base_hi | (j << P.b_lo) | (lo0 + lol);
-            uint32_t texp = (g0 & bmask) << tshift;
-            Fr x0 = lds_get(lds, T, e0);
-            Fr x1 = lds_get(lds, T, e1);
-            if (P.dit) {
-                Fr t = (texp == 0) ? x1 : x1 * load_fr(P.tw + texp);
-                lds_put(lds, T, e0, x0 + t);
-                lds_put(lds, T, e1, x0 - t);
-            } else {
-                Fr d = x0 - x1;
-                lds_put(lds, T, e0, x0 + x1);
-                lds_put(lds, T, e1, (texp == 0) ? d : d * load_fr(P.tw + texp));
-            }
+    if (k == 0) {  // n = 1: scaling only
+        for (int e = threadIdx.x; e < T; e += blockDim.x) {
+            uint32_t g = base_hi | (lo0 + (uint32_t)e);
+            Fr x = load_fr(P.in + g);
+            if (P.has_pre) x = apply_scale(P.pre, g, P.log_n, x);
+            if (P.has_post) x = apply_scale(P.post, g, P.log_n, x);
+            if (P.epi_mul_sub) x = load_fr(P.ea + g) * load_fr(P.eb + g) - x;
+            store_fr(P.out + g, x);
         }
-        __syncthreads();
+        return;
     }
-
-    for (int e = threadIdx.x; e < T; e += blockDim.x) {
-        uint32_t j = (uint32_t)e >> tl, lol = (uint32_t)e & tl_mask;
-        uint32_t g = base_hi | (j << P.b_lo) | (lo0 + lol);
-        Fr x = lds_get(lds, T, e);
-        if (P.has_post) x = apply_scale(P.post, g, P.log_n, x);
-        if (P.epi_mul_sub) x = load_fr(P.ea + g) * load_fr(P.eb + g) - x;
-        store_fr(P.out + g, x);
+    // rounds of <= 3 stages in processing order (DIF: high bits first)
+    int done = 0;
+    bool first = true;
+    while (done < k) {
+        const int nb = min(3, k - done);
+        const int qlo = DIT ? done : (k - done - nb);
+        const bool last = (done + nb == k);
+        if (!first) __syncthreads();
+        if (nb == 3) ntt_round<3, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
+        else if (nb == 2) ntt_round<2, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
+        else ntt_round<1, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
+        first = false;
+        done += nb;
     }
 }
 
-// tw[i] = hi[i >> S] * lo[i & mask], i < count
-__global__ void k_power_table(Fr* out, size_t count, const Fr* hi, const Fr* lo, int S) {
-    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= count) return;
-    Fr x = load_fr(hi + (i >> S)) * load_fr(lo + (i & ((1u << S) - 1)));
-    store_fr(out + i, x);
+// per-stage twiddle table: tw[(2^b - 1) + i] = w^(i << (L-1-b)), i < 2^b
+__global__ void k_stage_twiddles(Fr* out, size_t count, int L, const Fr* hi, const Fr* lo, int S) {
+    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count) return;
+    uint32_t v = (uint32_t)t + 1;
+    int b = 31 - __clz((int)v);
+    uint32_t i = v - (1u << b);
+    uint32_t ex = i << (L - 1 - b);
+    Fr x = load_fr(hi + (ex >> S)) * load_fr(lo + (ex & ((1u << S) - 1)));
+    store_fr(out + t, x);
 }
+
 
 // ---------------------------------------------------------------------------
 struct Pass {
@@ -174,27 +222,23 @@ struct Pass {
 };
 
 static std::vector<Pass> plan_passes(int L, bool dit) {
-    std::vector<Pass> v;
-    if (L <= 11) {
-        v.push_back({0, L, 0});
-        return v;
-    }
-    int P = 1 + (L - 11 + 7) / 8;
-    std::vector<int> ks(P, L / P);
-    for (int i = 0; i < L % P; i++) ks[i]++;  // ks[0] is the contiguous pass
-    // contiguous pass may take up to 11, strided passes up to 8
-    for (int i = 1; i < P; i++)
-        while (ks[i] > 8) { ks[i]--; ks[0]++; }
-    // build from the contiguous (b_lo = 0) pass upwards
+    // every tile holds 2048 elements: the contiguous pass takes k = 11 bits,
+    // strided passes k <= 9 bits with 2^(11-k) adjacent columns (>= 128-B runs)
     std::vector<Pass> up;
-    int b = 0;
-    for (int i = 0; i < P; i++) {
-        int tl = (b == 0) ? 0 : std::min(3, b);
-        up.push_back({b, ks[i], tl});
-        b += ks[i];
+    if (L <= 11) {
+        up.push_back({0, L, 0});
+    } else {
+        up.push_back({0, 11, 0});
+        int rem = L - 11, P = (rem + 8) / 9, b = 11;
+        for (int i = 0; i < P; i++) {
+            int k = rem / (P - i);
+            up.push_back({b, k, 11 - k});
+            b += k;
+            rem -= k;
+        }
     }
     if (dit) return up;  // DIT: low bits first
-    for (int i = P - 1; i >= 0; i--) v.push_back(up[i]);  // DIF: high bits first
+    std::vector<Pass> v(up.rbegin(), up.rend());  // DIF: high bits first
     return v;
 }
 
@@ -257,9 +301,10 @@ void run_transform(gg_domain* d, const Fr* in, Fr* out, bool dit, bool inverse_t
         if (last && ea) { P.epi_mul_sub = 1; P.ea = ea; P.eb = eb; }
         int T = 1 << (ps.k + ps.tl);
         unsigned tiles = (unsigned)(d->n / (size_t)T);
-        size_t lds = (size_t)T * 32;
+        size_t lds = (ps.k > 3) ? (size_t)(T + (T >> 5)) * 32 : 0;  // single-round passes skip LDS
         ProfScope prof("ntt_pass", st, (double)d->n);
-        hipLaunchKernelGGL(k_ntt_pass, dim3(tiles), dim3(256), lds, st, P);
+        if (dit) hipLaunchKernelGGL(k_ntt_pass<true>, dim3(tiles), dim3(256), lds, st, P);
+        else hipLaunchKernelGGL(k_ntt_pass<false>, dim3(tiles), dim3(256), lds, st, P);
         GG_HIP(hipGetLastError());
         prof.stop(st);
         src = out;
@@ -317,29 +362,21 @@ extern "C" int gg_domain_create(int log_n, const void* omega_mont, const void* c
         d->spec[kd] = ScaleSpec{(const Fr*)d->scale_hi[kd].p, (const Fr*)d->scale_lo[kd].p, S,
                                 defs[kd].br};
     }
-    // twiddles w^i, i < n/2, generated on device from split tables
-    size_t half = d->n / 2;
-    if (half) {
-        DevBuf h1, l1;
-        build_pow_tables(L, S, d->omega, Fr::one(), hi, lo);
-        upload(h1, hi);
-        upload(l1, lo);
-        d->tw.alloc(half * 32);
-        hipLaunchKernelGGL(k_power_table, dim3(grid_for(half, 256)), dim3(256), 0, 0,
-                           d->tw.as<Fr>(), half, h1.as<Fr>(), l1.as<Fr>(), S);
-        GG_HIP(hipGetLastError());
-        build_pow_tables(L, S, d->omega_inv, Fr::one(), hi, lo);
-        DevBuf h2, l2;
-        upload(h2, hi);
-        upload(l2, lo);
-        d->twinv.alloc(half * 32);
-        hipLaunchKernelGGL(k_power_table, dim3(grid_for(half, 256)), dim3(256), 0, 0,
-                           d->twinv.as<Fr>(), half, h2.as<Fr>(), l2.as<Fr>(), S);
-        GG_HIP(hipGetLastError());
-        GG_HIP(hipDeviceSynchronize());
-    } else {
-        d->tw.alloc(32);
-        d->twinv.alloc(32);
+    // per-stage twiddles (n - 1 entries each for w and w^-1), generated on device
+    size_t cnt = d->n - 1;
+    d->tw.alloc((cnt + 1) * 32);
+    d->twinv.alloc((cnt + 1) * 32);
+    if (cnt) {
+        for (int inv = 0; inv < 2; inv++) {
+            DevBuf h1, l1;
+            build_pow_tables(L, S, inv ? d->omega_inv : d->omega, Fr::one(), hi, lo);
+            upload(h1, hi);
+            upload(l1, lo);
+            hipLaunchKernelGGL(k_stage_twiddles, dim3(grid_for(cnt, 256)), dim3(256), 0, 0,
+                               (inv ? d->twinv : d->tw).as<Fr>(), cnt, L, h1.as<Fr>(), l1.as<Fr>(), S);
+            GG_HIP(hipGetLastError());
+            GG_HIP(hipDeviceSynchronize());
+        }
     }
     *out = guard.release();
     GG_CAPI_END
