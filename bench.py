@@ -236,7 +236,17 @@ def groth16_bench(log_n, reps=3):
         groth16.prove(pk, sol, backend.with_amd_acceleration())
         ts.append(1e3 * (time.perf_counter() - t))
     tim = groth16.last_timings()
-    return {"log_n": log_n, "n_constraints": ncons, "n_wires": n_wires,
+    # the same prove with the five tasks run one after another: isolated stage times
+    os.environ["GG_G16_SERIAL"] = "1"
+    try:
+        t = time.perf_counter()
+        groth16.prove(pk, sol, backend.with_amd_acceleration())
+        t_serial = 1e3 * (time.perf_counter() - t)
+        tim_serial = groth16.last_timings()
+    finally:
+        del os.environ["GG_G16_SERIAL"]
+    return {"serial_prove_ms": t_serial, "serial_stage_ms": tim_serial,
+            "log_n": log_n, "n_constraints": ncons, "n_wires": n_wires,
             "prove_ms": min(ts), "prove_ms_all": ts, "constraints_per_s": ncons / (min(ts) * 1e-3),
             "stage_ms": tim, "key_setup_s": t_setup, "inputs": "resident in HBM"}
 

@@ -89,6 +89,14 @@ inline bool is_device_ptr(const void* p) {
     return a.type == hipMemoryTypeDevice;
 }
 
+// XCD-aware block swizzle (bijective for any nwg): consecutive logical blocks run
+// on one XCD (blocks b and b + 8 share an XCD under round-robin dispatch), so
+// neighbouring blocks' partial-line writes merge in that XCD's L2.  Speed only.
+__device__ __forceinline__ uint32_t xcd_swizzle(uint32_t bid, uint32_t nwg) {
+    const uint32_t q = nwg >> 3, r = nwg & 7, x = bid & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
 inline unsigned grid_for(size_t n, unsigned block) {
     size_t g = (n + block - 1) / block;
     return (unsigned)(g ? g : 1);

@@ -15,6 +15,7 @@
 #include <mutex>
 #include <thread>
 #include <vector>
+#include <cstdlib>
 #include <cstring>
 
 struct gg_domain;
@@ -208,8 +209,14 @@ extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_
             }
         };
     };
+    // GG_G16_SERIAL=1 runs the tasks one after another (per-stage isolated timings)
+    const bool serial = getenv("GG_G16_SERIAL") && atoi(getenv("GG_G16_SERIAL"));
     std::vector<std::thread> workers;
-    workers.emplace_back(guarded([&] {
+    auto spawn = [&](auto fn) {
+        if (serial) fn();
+        else workers.emplace_back(fn);
+    };
+    spawn(guarded([&] {
         double a = now_ms();
         compute_h_device(pk->dom, A, B, C, A, pk->s1);
         GG_HIP(hipStreamSynchronize(pk->s1));
@@ -219,9 +226,9 @@ extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_
         if (n > 1) msm_device(pk->Z, A, &jz, pk->s1);
         t_z = now_ms() - b;
     }));
-    workers.emplace_back(guarded([&] { double a = now_ms(); msm_device(pk->A, wdev, &ja, pk->s2); t_a = now_ms() - a; }));
-    workers.emplace_back(guarded([&] { double a = now_ms(); msm_device(pk->B, wdev, &jb, pk->s3); t_b = now_ms() - a; }));
-    workers.emplace_back(guarded([&] { double a = now_ms(); msm_device(pk->K, wdev, &jk, pk->s4); t_k = now_ms() - a; }));
+    spawn(guarded([&] { double a = now_ms(); msm_device(pk->A, wdev, &ja, pk->s2); t_a = now_ms() - a; }));
+    spawn(guarded([&] { double a = now_ms(); msm_device(pk->B, wdev, &jb, pk->s3); t_b = now_ms() - a; }));
+    spawn(guarded([&] { double a = now_ms(); msm_device(pk->K, wdev, &jk, pk->s4); t_k = now_ms() - a; }));
     double t2 = now_ms();
     guarded([&] { msm_device(pk->B2, wdev, &j2, pk->s0); })();
     double te = now_ms();

@@ -166,22 +166,78 @@ inline int sort_spb(int W) {
 // Sort order is by pi(b) = bitrev_{c-1}(b): bins take the LOW bits of the bucket
 // id, so the small ids of a narrow top window spread over all bins.
 __device__ __forceinline__ uint32_t pi_of(uint32_t b, int c) { return __brev(b) >> (33 - c); }
-__device__ __forceinline__ uint32_t bin_of(uint32_t b, int c) { return pi_of(b, c) >> (c - 1 - min(8, c - 1)); }
+__device__ __forceinline__ uint32_t bin_of(uint32_t b, int c, int h) { return pi_of(b, c) >> (c - 1 - h); }
+
+// exclusive scan of v over a 256-thread block (4 wave scans + one barrier);
+// `wsum` is 4 words of LDS.  Returns the exclusive prefix; *total = block sum.
+__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* wsum, uint32_t* total) {
+    const int lane = __lane_id(), wv = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        uint32_t w = wsum[i];
+        if (i < wv) pre += w;
+        tot += w;
+    }
+    *total = tot;
+    return pre + x - v;
+}
+
+// Wave-level multisplit rank: lanes with equal digit d form a group (found with
+// rbits ballots); one LDS atomic per group, the rank within the group comes from
+// a popcount.  Removes same-address LDS atomic serialisation.  Must be called by
+// all lanes of the wave (inactive lanes pass valid = false).
+__device__ __forceinline__ uint32_t wave_rank(uint32_t* cnt, uint32_t d, bool valid, int rbits) {
+    uint64_t match = __ballot(valid);
+    for (int bb = 0; bb < rbits; bb++) {
+        const bool bit = (d >> bb) & 1u;
+        const uint64_t bal = __ballot(bit);
+        match &= bit ? bal : ~bal;
+    }
+    const int lane = __lane_id();
+    const uint32_t rank = (uint32_t)__popcll(match & ((1ull << lane) - 1));
+    const int leader = match ? __ffsll((unsigned long long)match) - 1 : lane;
+    uint32_t b = 0;
+    if (valid && lane == leader) b = atomicAdd(&cnt[d], (uint32_t)__popcll(match));
+    b = __shfl(b, leader);
+    return b + rank;
+}
 
 __global__ void __launch_bounds__(256) k_digits_hist(const Fr* scalars, const uint32_t* sidx,
-                                                     size_t n, int c, int W, int spb, int nbins,
+                                                     size_t n, int c, int W, int spb, int nbins, int h,
                                                      uint32_t* keys, uint32_t* hist,
                                                      uint32_t nblocks) {
-    extern __shared__ uint32_t h[];
-    for (int j = threadIdx.x; j < nbins; j += blockDim.x) h[j] = 0;
+    extern __shared__ uint32_t hh[];
+    for (int j = threadIdx.x; j < nbins; j += blockDim.x) hh[j] = 0;
     __syncthreads();
     const int half = 1 << (c - 1);
-    for (int s = 0; s * 256 < spb; s++) {
-        if (s * 256 + (int)threadIdx.x >= spb) break;
-        size_t i = (size_t)blockIdx.x * spb + s * 256 + threadIdx.x;
-        if (i >= n) break;
-        Fr sc = ld(scalars + (sidx ? sidx[i] : i));
-        Fr k = from_mont(sc);
+    // spb <= 512: at most two scalars per thread, both loaded before any digit work
+    Fr scl[2];
+    size_t idx[2];
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        idx[s] = ~(size_t)0;
+        if (s * 256 + (int)threadIdx.x < spb) {
+            size_t i = (size_t)blockIdx.x * spb + s * 256 + threadIdx.x;
+            if (i < n) {
+                idx[s] = i;
+                scl[s] = ld(scalars + (sidx ? sidx[i] : i));
+            }
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+        if (idx[s] == ~(size_t)0) continue;
+        const size_t i = idx[s];
+        Fr k = from_mont(scl[s]);
         int carry = 0;
         for (int w = 0; w < W; w++) {
             int d = (int)extract_bits(k, w * c, c) + carry;
@@ -190,35 +246,36 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fr* scalars, const ui
             if (d) {
                 uint32_t bk = (uint32_t)((d > 0 ? d : -d) - 1);
                 key = bk | (d < 0 ? 0x80000000u : 0u);
-                atomicAdd(&h[bin_of(bk, c)], 1u);
+                atomicAdd(&hh[bin_of(bk, c, h)], 1u);
             }
             keys[(size_t)w * n + i] = key;
         }
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < nbins; j += blockDim.x) hist[(size_t)j * nblocks + blockIdx.x] = h[j];
+    for (int j = threadIdx.x; j < nbins; j += blockDim.x) hist[(size_t)j * nblocks + blockIdx.x] = hh[j];
 }
 
 // Phase C, LDS-staged: the block's entries are first partitioned by bin in LDS
 // (ranks from LDS atomics, bin bases from this block's own histogram), then
 // written out as contiguous per-bin runs -> coalesced stores.
 __global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_t n, int W, int c, int spb,
-                                                     int nbins, const uint32_t* hist,
+                                                     int nbins, int h, const uint32_t* hist,
                                                      const uint32_t* hoff, uint32_t nblocks,
                                                      uint32_t* tmp_entry, uint32_t* tmp_key) {
     extern __shared__ uint32_t sm[];
+    const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
     uint32_t* lbase = sm;             // nbins: local exclusive offsets
     uint32_t* lcur = sm + nbins;      // nbins: local cursors
     uint32_t* s_entry = sm + 2 * nbins;
     uint32_t* s_key = s_entry + spb * W;
-    const int lowbits = (c - 1) - min(8, c - 1);
+    const int lowbits = (c - 1) - h;
     // local exclusive scan of this block's histogram (column of hist)
     __shared__ uint32_t part[256];
     const int per = (nbins + 255) / 256;
     uint32_t s = 0;
     for (int k = 0; k < per; k++) {
         int j = threadIdx.x * per + k;
-        if (j < nbins) s += hist[(size_t)j * nblocks + blockIdx.x];
+        if (j < nbins) s += hist[(size_t)j * nblocks + tile];
     }
     part[threadIdx.x] = s;
     __syncthreads();
@@ -234,20 +291,35 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_
         if (j < nbins) {
             lbase[j] = run;
             lcur[j] = run;
-            run += hist[(size_t)j * nblocks + blockIdx.x];
+            run += hist[(size_t)j * nblocks + tile];
         }
     }
     __syncthreads();
-    const size_t i0 = (size_t)blockIdx.x * spb;
+    const size_t i0 = (size_t)tile * spb;
     const int ns = (int)min((size_t)spb, n - i0);
-    for (int w = 0; w < W; w++) {
-        for (int t = threadIdx.x; t < ns; t += blockDim.x) {
-            size_t e = (size_t)w * n + i0 + t;
-            uint32_t key = keys[e];
+    const int tot_e = ns * W;
+    // flat (window, scalar) index j = w * ns + t; keys loaded 8 per batch before
+    // the LDS atomics so the loads overlap
+    for (int jb0 = 0; jb0 < tot_e; jb0 += 8 * 256) {
+        uint32_t kk[8];
+        size_t ee[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            int j = jb0 + (int)threadIdx.x + u * 256;
+            kk[u] = 0xffffffffu;
+            if (j < tot_e) {
+                int w = j / ns, t = j - w * ns;
+                ee[u] = (size_t)w * n + i0 + t;
+                kk[u] = keys[ee[u]];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            uint32_t key = kk[u];
             if (key == 0xffffffffu) continue;
             uint32_t pk = pi_of(key & 0x7fffffffu, c);
             uint32_t q = atomicAdd(&lcur[pk >> lowbits], 1u);
-            s_entry[q] = (uint32_t)e | (key & 0x80000000u);
+            s_entry[q] = (uint32_t)ee[u] | (key & 0x80000000u);
             s_key[q] = pk;
         }
     }
@@ -256,9 +328,9 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_
     for (uint32_t q = threadIdx.x; q < tot; q += blockDim.x) {
         uint32_t pk = s_key[q];
         uint32_t bin = pk >> lowbits;
-        uint32_t pos = hoff[(size_t)bin * nblocks + blockIdx.x] + (q - lbase[bin]);
+        uint32_t pos = hoff[(size_t)bin * nblocks + tile] + (q - lbase[bin]);
         tmp_entry[pos] = s_entry[q];
-        tmp_key[pos] = pk;
+        if (tmp_key) tmp_key[pos] = pk;
     }
 }
 
@@ -273,158 +345,255 @@ __global__ void k_bin_starts(const uint32_t* hoff, const uint32_t* hist, uint32_
     }
 }
 
-// ---- phase D: chunked counting sort of every bin on its low bits.  Chunks of
-// <= SORT_CH entries never straddle a bin, so any skew (a bucket holding half of
-// all entries, as 0/1-heavy witnesses produce) spreads over many workgroups.
-constexpr uint32_t SORT_CH = 4096;
+// ---- phase D: segmented MSD passes.  Each pass splits every segment (a run of
+// entries sharing the bucket's high bits) on the next r <= 8 bits, in chunks of
+// <= SEG_CH entries that never straddle a segment, so any skew (a bucket holding
+// half of all entries, as 0/1-heavy witnesses produce) spreads over many
+// workgroups.  The scatter is LDS-staged: a chunk is first ordered by digit in
+// LDS, then written as per-digit runs of ~SEG_CH / 2^r entries (coalesced).
+#ifndef GG_SEG_CH
+#define GG_SEG_CH 4096
+#endif
+constexpr uint32_t SEG_CH = GG_SEG_CH;
+constexpr int SEG_PER = SEG_CH / 256;  // entries per thread
 
-// chunk_start[b] = first chunk of bin b, chunk_start[nbins] = total chunks
-__global__ void __launch_bounds__(256) k_chunk_setup(const uint32_t* bin_start, int nbins,
-                                                     uint32_t* chunk_start) {
-    __shared__ uint32_t part[256];
-    const int per = (nbins + 255) / 256;
-    const int b0 = threadIdx.x * per;
-    uint32_t s = 0;
-    for (int k = 0; k < per; k++) {
-        int b = b0 + k;
-        if (b < nbins) s += (bin_start[b + 1] - bin_start[b] + SORT_CH - 1) / SORT_CH;
-    }
-    part[threadIdx.x] = s;
-    __syncthreads();
-    for (int off = 1; off < 256; off <<= 1) {
-        uint32_t x = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
-        __syncthreads();
-        part[threadIdx.x] += x;
-        __syncthreads();
-    }
-    uint32_t run = part[threadIdx.x] - s;
-    for (int k = 0; k < per; k++) {
-        int b = b0 + k;
-        if (b < nbins) {
-            chunk_start[b] = run;
-            run += (bin_start[b + 1] - bin_start[b] + SORT_CH - 1) / SORT_CH;
-        }
-    }
-    if (threadIdx.x == 255) chunk_start[nbins] = part[255];
+__global__ void k_seg_chunk_counts(const uint32_t* seg_start, uint32_t nseg, uint32_t* cnt) {
+    uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < nseg) cnt[s] = (seg_start[s + 1] - seg_start[s] + SEG_CH - 1) / SEG_CH;
 }
 
-__device__ __forceinline__ int find_bin(const uint32_t* chunk_start, int nbins, uint32_t g) {
-    int lo = 0, hi = nbins;  // largest b with chunk_start[b] <= g
+__device__ __forceinline__ uint32_t find_seg(const uint32_t* chunk_start, uint32_t nseg, uint32_t g) {
+    uint32_t lo = 0, hi = nseg;  // largest s with chunk_start[s] <= g
     while (hi - lo > 1) {
-        int mid = (lo + hi) >> 1;
+        uint32_t mid = (lo + hi) >> 1;
         if (chunk_start[mid] <= g) lo = mid; else hi = mid;
     }
     return lo;
 }
 
-// counters laid out [bin][low][chunk-in-bin]: one global exclusive scan then
-// yields absolute output positions.
-__global__ void __launch_bounds__(256) k_chunk_hist(const uint32_t* tmp_key, const uint32_t* bin_start,
-                                                    const uint32_t* chunk_start, int nbins, int lowbits,
-                                                    uint32_t* ch) {
-    extern __shared__ uint32_t hist[];
-    const uint32_t g = blockIdx.x;
-    if (g >= chunk_start[nbins]) return;
-    const int L = 1 << lowbits;
-    const int b = find_bin(chunk_start, nbins, g);
-    const uint32_t g0 = chunk_start[b], nch = chunk_start[b + 1] - g0, k = g - g0;
-    const uint32_t lo = bin_start[b] + k * SORT_CH, hi = min(bin_start[b + 1], lo + SORT_CH);
-    for (int j = threadIdx.x; j < L; j += blockDim.x) hist[j] = 0;
-    __syncthreads();
-    for (uint32_t e = lo + threadIdx.x; e < hi; e += blockDim.x) atomicAdd(&hist[tmp_key[e] & (L - 1)], 1u);
-    __syncthreads();
-    for (int j = threadIdx.x; j < L; j += blockDim.x) ch[(size_t)g0 * L + (size_t)j * nch + k] = hist[j];
+// chunk descriptor {lo, hi, g0, nch}: entry range, first chunk of its segment,
+// chunks in the segment; nch = 0 marks a grid slot past the last chunk
+__global__ void k_seg_chunk_desc(const uint32_t* seg_start, const uint32_t* chunk_start, uint32_t nseg,
+                                 uint32_t max_chunks, uint4* desc) {
+    uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= max_chunks) return;
+    uint4 d = make_uint4(0, 0, 0, 0);
+    if (g < chunk_start[nseg]) {
+        uint32_t sg = find_seg(chunk_start, nseg, g);
+        uint32_t g0 = chunk_start[sg], nch = chunk_start[sg + 1] - g0, k = g - g0;
+        uint32_t lo = seg_start[sg] + k * SEG_CH, hi = min(seg_start[sg + 1], lo + SEG_CH);
+        d = make_uint4(lo, hi, g0, nch);
+    }
+    desc[g] = d;
 }
 
-__global__ void __launch_bounds__(256) k_chunk_scatter(const uint32_t* tmp_entry, const uint32_t* tmp_key,
-                                                       const uint32_t* bin_start,
-                                                       const uint32_t* chunk_start, int nbins,
-                                                       int lowbits, const uint32_t* chs,
-                                                       uint32_t* sorted) {
-    extern __shared__ uint32_t cur[];
-    const uint32_t g = blockIdx.x;
-    if (g >= chunk_start[nbins]) return;
-    const int L = 1 << lowbits;
-    const int b = find_bin(chunk_start, nbins, g);
-    const uint32_t g0 = chunk_start[b], nch = chunk_start[b + 1] - g0, k = g - g0;
-    const uint32_t lo = bin_start[b] + k * SORT_CH, hi = min(bin_start[b + 1], lo + SORT_CH);
-    for (int j = threadIdx.x; j < L; j += blockDim.x) cur[j] = chs[(size_t)g0 * L + (size_t)j * nch + k];
+// counters laid out [segment][digit][chunk-in-segment]: one global exclusive
+// scan then yields absolute output positions.
+__global__ void __launch_bounds__(256) k_seg_hist(const uint32_t* keys, const uint4* desc, int shift,
+                                                  int rbits, uint32_t* ch) {
+    __shared__ uint32_t hist[256];
+    const uint32_t g = xcd_swizzle(blockIdx.x, gridDim.x);
+    const uint4 dsc = desc[g];
+    const uint32_t lo = dsc.x, hi = dsc.y, g0 = dsc.z, nch = dsc.w, k = g - g0;
+    if (nch == 0) return;
+    const uint32_t R = 1u << rbits;
+    if (threadIdx.x < R) hist[threadIdx.x] = 0;
     __syncthreads();
-    for (uint32_t e = lo + threadIdx.x; e < hi; e += blockDim.x) {
-        uint32_t pos = atomicAdd(&cur[tmp_key[e] & (L - 1)], 1u);
-        sorted[pos] = tmp_entry[e];
+    for (uint32_t e = lo + threadIdx.x; e < hi; e += blockDim.x)
+        atomicAdd(&hist[(keys[e] >> shift) & (R - 1)], 1u);
+    __syncthreads();
+    if (threadIdx.x < R) ch[(size_t)g0 * R + (size_t)threadIdx.x * nch + k] = hist[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(256) k_seg_scatter(const uint32_t* ent_in, const uint32_t* key_in,
+                                                     const uint4* desc, int shift, int rbits,
+                                                     const uint32_t* chpos, uint32_t* ent_out,
+                                                     uint32_t* key_out) {
+    __shared__ uint32_t cnt[256], base[256], part[256];
+    extern __shared__ uint32_t stage[];  // SEG_CH entries, SEG_CH digits (u8) [, SEG_CH keys]
+    const uint32_t g = xcd_swizzle(blockIdx.x, gridDim.x);
+    const uint4 dsc = desc[g];
+    const uint32_t lo = dsc.x, hi = dsc.y, g0 = dsc.z, nch = dsc.w, k = g - g0;
+    if (nch == 0) return;
+    const uint32_t R = 1u << rbits;
+    const uint32_t m = hi - lo;
+    if (threadIdx.x < R) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t ek[SEG_PER], ee[SEG_PER], rk[SEG_PER];
+#pragma unroll
+    for (int j = 0; j < SEG_PER; j++) {
+        uint32_t q = threadIdx.x + 256u * j;
+        ek[j] = 0;
+        ee[j] = 0;
+        if (q < m) {
+            ek[j] = key_in[lo + q];
+            ee[j] = ent_in[lo + q];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < SEG_PER; j++) {
+        uint32_t q = threadIdx.x + 256u * j;
+        rk[j] = wave_rank(cnt, (ek[j] >> shift) & (R - 1), q < m, rbits);
+    }
+    __syncthreads();
+    // exclusive scan of the chunk's digit counts
+    uint32_t tot_unused;
+    const uint32_t v = threadIdx.x < R ? cnt[threadIdx.x] : 0u;
+    const uint32_t ex = block_excl_scan256(v, part, &tot_unused);
+    if (threadIdx.x < R) base[threadIdx.x] = ex;
+    uint8_t* s_dig = (uint8_t*)(stage + SEG_CH);
+    uint32_t* s_key = stage + SEG_CH + SEG_CH / 4;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SEG_PER; j++) {
+        uint32_t q = threadIdx.x + 256u * j;
+        if (q < m) {
+            const uint32_t d = (ek[j] >> shift) & (R - 1);
+            uint32_t p = base[d] + rk[j];
+            stage[p] = ee[j];
+            s_dig[p] = (uint8_t)d;
+            if (key_out) s_key[p] = ek[j];
+        }
+    }
+    // global position of each digit's run
+    if (threadIdx.x < R) cnt[threadIdx.x] = chpos[(size_t)g0 * R + (size_t)threadIdx.x * nch + k];
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < m; q += blockDim.x) {
+        uint32_t kk = key_out ? s_key[q] : 0u;
+        const uint32_t dl = s_dig[q];
+        uint32_t pos = cnt[dl] + (q - base[dl]);
+        ent_out[pos] = stage[q];
+        if (key_out) key_out[pos] = kk;
     }
 }
 
-// offsets[(bin << lowbits) + low] = start of that bucket (in pi order); [nb] = total
-__global__ void k_bucket_offsets(const uint32_t* bin_start, const uint32_t* chunk_start,
-                                 const uint32_t* chs, int nbins, int lowbits, uint32_t* offsets) {
+// start of every sub-segment: next[s * R + d]; next[nseg * R] = total
+__global__ void k_seg_next(const uint32_t* seg_start, const uint32_t* chunk_start, const uint32_t* chpos,
+                           uint32_t nseg, int rbits, uint32_t* next) {
     size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int L = 1 << lowbits;
-    if (q >= ((size_t)nbins << lowbits)) return;
-    int b = (int)(q >> lowbits), l = (int)(q & (L - 1));
-    uint32_t g0 = chunk_start[b], nch = chunk_start[b + 1] - g0;
-    offsets[q] = nch ? chs[(size_t)g0 * L + (size_t)l * nch] : bin_start[b];
-    if (q == 0) offsets[(size_t)nbins << lowbits] = bin_start[nbins];
+    const uint32_t R = 1u << rbits;
+    if (q >= (size_t)nseg * R) return;
+    uint32_t sg = (uint32_t)(q >> rbits), d = (uint32_t)(q & (R - 1));
+    uint32_t g0 = chunk_start[sg], nch = chunk_start[sg + 1] - g0;
+    next[q] = nch ? chpos[(size_t)g0 * R + (size_t)d * nch] : seg_start[sg];
+    if (q == 0) next[(size_t)nseg * R] = seg_start[nseg];
+}
+
+// number of bits of the first (bin) pass and the split of the rest into passes
+static void sort_plan(int c, int& h, std::vector<int>& rs) {
+    h = std::min(8, c - 1);
+    if (const char* e = getenv("GG_SORT_H")) h = std::max(1, std::min(atoi(e), std::min(8, c - 1)));
+    int rmax = 6;
+    if (const char* e = getenv("GG_SORT_RMAX")) rmax = std::max(1, std::min(atoi(e), 8));
+    int low = (c - 1) - h;
+    rs.clear();
+    if (low <= 0) return;
+    int np = (low + rmax - 1) / rmax;
+    for (int i = 0; i < np; i++) {
+        int r = low / (np - i);
+        rs.push_back(r);
+        low -= r;
+    }
 }
 
 void sort_entries(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st) {
     const size_t n = b->n, nb = b->nb;
     const int c = b->c, W = b->W;
     const size_t total = (size_t)W * n;
-    const int h = std::min(8, c - 1);
+    int h;
+    std::vector<int> rs;
+    sort_plan(c, h, rs);
     const int nbins = 1 << h;
-    const int lowbits = (c - 1) - h;
     const int spb = sort_spb(W);
     const uint32_t nblocks = (uint32_t)((n + spb - 1) / spb);
     const size_t nh = (size_t)nbins * nblocks;
+    // all scratch reserved up front (no reallocation between launches)
+    size_t ch_max = 0, chunks_max = 0;
+    {
+        size_t ns = (size_t)nbins;
+        for (int r : rs) {
+            chunks_max = std::max(chunks_max, (total + SEG_CH - 1) / SEG_CH + ns);
+            ch_max = std::max(ch_max, ((total + SEG_CH - 1) / SEG_CH + ns) << r);
+            ns <<= r;
+        }
+    }
     b->keys.reserve(total * 4);
     b->tmp_entry.reserve(total * 4);
     b->tmp_key.reserve(total * 4);
     b->sorted.reserve(total * 4);
     b->hist.reserve(nh * 4);
     b->hoff.reserve((nh + 1) * 4);
-    b->bin_start.reserve((nbins + 1) * 4);
+    b->bin_start.reserve(((size_t)nb + 1) * 4);
+    b->seg2.reserve(((size_t)nb + 1) * 4);
     b->offsets.reserve((nb + 1) * 4);
+    b->counts.reserve(nb * 4);
+    b->chunk_start.reserve(((size_t)nb + 1) * 4);
+    if (ch_max) {
+        b->chunk_hist.reserve(ch_max * 4);
+        b->chunk_pos.reserve((ch_max + 1) * 4);
+        b->chunk_desc.reserve(chunks_max * 16);
+    }
     hipLaunchKernelGGL(k_digits_hist, dim3(nblocks), dim3(256), nbins * 4, st, scalars_dev,
-                       b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, spb, nbins,
+                       b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, spb, nbins, h,
                        b->keys.as<uint32_t>(), b->hist.as<uint32_t>(), nblocks);
     GG_HIP(hipGetLastError());
     exclusive_scan(b->hist.as<uint32_t>(), b->hoff.as<uint32_t>(), nh, st, b->scan_tmp);
+    // segment starts ping-pong between bin_start and seg2; the last pass writes offsets
+    DevBuf* segb[2] = {&b->bin_start, &b->seg2};
     hipLaunchKernelGGL(k_bin_starts, dim3(grid_for(nbins, 256)), dim3(256), 0, st,
                        b->hoff.as<uint32_t>(), b->hist.as<uint32_t>(), nblocks, nbins,
-                       b->bin_start.as<uint32_t>());
+                       rs.empty() ? b->offsets.as<uint32_t>() : segb[0]->as<uint32_t>());
     GG_HIP(hipGetLastError());
     const size_t lds_c = (2 * (size_t)nbins + 2 * (size_t)spb * W) * 4;
     GG_CHECK(lds_c <= 160 * 1024, GG_ERR_INTERNAL, "bin scatter LDS tile too large");
+    // scatter stage j (0 = bin scatter) writes entries to `sorted` when the number
+    // of stages after it is even, else tmp_entry; keys to tmp_key (j even) / keys (j odd)
+    const int S = 1 + (int)rs.size();
+    auto ent_out = [&](int j) { return ((S - 1 - j) % 2 == 0) ? &b->sorted : &b->tmp_entry; };
+    auto key_out = [&](int j) { return (j % 2 == 0) ? &b->tmp_key : &b->keys; };
     hipLaunchKernelGGL(k_bin_scatter, dim3(nblocks), dim3(256), lds_c, st, b->keys.as<uint32_t>(),
-                       n, W, c, spb, nbins, b->hist.as<uint32_t>(), b->hoff.as<uint32_t>(), nblocks,
-                       b->tmp_entry.as<uint32_t>(), b->tmp_key.as<uint32_t>());
+                       n, W, c, spb, nbins, h, b->hist.as<uint32_t>(), b->hoff.as<uint32_t>(), nblocks,
+                       ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->as<uint32_t>() : nullptr);
     GG_HIP(hipGetLastError());
-    const size_t L = (size_t)1 << lowbits;
-    const size_t max_chunks = (total + SORT_CH - 1) / SORT_CH + nbins;
-    b->chunk_start.reserve((nbins + 1) * 4);
-    b->chunk_hist.reserve(max_chunks * L * 4);
-    b->chunk_pos.reserve((max_chunks * L + 1) * 4);
-    hipLaunchKernelGGL(k_chunk_setup, dim3(1), dim3(256), 0, st, b->bin_start.as<uint32_t>(), nbins,
-                       b->chunk_start.as<uint32_t>());
-    GG_HIP(hipGetLastError());
-    GG_HIP(hipMemsetAsync(b->chunk_hist.p, 0, max_chunks * L * 4, st));
-    hipLaunchKernelGGL(k_chunk_hist, dim3((unsigned)max_chunks), dim3(256), L * 4, st,
-                       b->tmp_key.as<uint32_t>(), b->bin_start.as<uint32_t>(),
-                       b->chunk_start.as<uint32_t>(), nbins, lowbits, b->chunk_hist.as<uint32_t>());
-    GG_HIP(hipGetLastError());
-    exclusive_scan(b->chunk_hist.as<uint32_t>(), b->chunk_pos.as<uint32_t>(), max_chunks * L, st,
-                   b->scan_tmp);
-    hipLaunchKernelGGL(k_chunk_scatter, dim3((unsigned)max_chunks), dim3(256), L * 4, st,
-                       b->tmp_entry.as<uint32_t>(), b->tmp_key.as<uint32_t>(),
-                       b->bin_start.as<uint32_t>(), b->chunk_start.as<uint32_t>(), nbins, lowbits,
-                       b->chunk_pos.as<uint32_t>(), b->sorted.as<uint32_t>());
-    GG_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_bucket_offsets, dim3(grid_for((size_t)nbins << lowbits, 256)), dim3(256), 0, st,
-                       b->bin_start.as<uint32_t>(), b->chunk_start.as<uint32_t>(),
-                       b->chunk_pos.as<uint32_t>(), nbins, lowbits, b->offsets.as<uint32_t>());
-    GG_HIP(hipGetLastError());
+    uint32_t nseg = (uint32_t)nbins;
+    int shift = (c - 1) - h;
+    for (int j = 1; j < S; j++) {
+        const int r = rs[j - 1];
+        const bool last = j == S - 1;
+        shift -= r;
+        const uint32_t R = 1u << r;
+        const size_t max_chunks = (total + SEG_CH - 1) / SEG_CH + nseg;
+        const uint32_t* segp = segb[(j - 1) & 1]->as<uint32_t>();
+        hipLaunchKernelGGL(k_seg_chunk_counts, dim3(grid_for(nseg, 256)), dim3(256), 0, st, segp, nseg,
+                           b->counts.as<uint32_t>());
+        GG_HIP(hipGetLastError());
+        exclusive_scan(b->counts.as<uint32_t>(), b->chunk_start.as<uint32_t>(), nseg, st, b->scan_tmp);
+        hipLaunchKernelGGL(k_set_total, dim3(1), dim3(1), 0, st, b->chunk_start.as<uint32_t>(),
+                           b->counts.as<uint32_t>(), (size_t)nseg);
+        GG_HIP(hipGetLastError());
+        GG_HIP(hipMemsetAsync(b->chunk_hist.p, 0, max_chunks * R * 4, st));
+        hipLaunchKernelGGL(k_seg_chunk_desc, dim3(grid_for(max_chunks, 256)), dim3(256), 0, st, segp,
+                           b->chunk_start.as<uint32_t>(), nseg, (uint32_t)max_chunks,
+                           b->chunk_desc.as<uint4>());
+        GG_HIP(hipGetLastError());
+        const uint32_t* kin = key_out(j - 1)->as<uint32_t>();
+        hipLaunchKernelGGL(k_seg_hist, dim3((unsigned)max_chunks), dim3(256), 0, st, kin,
+                           b->chunk_desc.as<uint4>(), shift, r, b->chunk_hist.as<uint32_t>());
+        GG_HIP(hipGetLastError());
+        exclusive_scan(b->chunk_hist.as<uint32_t>(), b->chunk_pos.as<uint32_t>(), max_chunks * R, st,
+                       b->scan_tmp);
+        const size_t lds_s = (size_t)SEG_CH * (last ? 5 : 9);
+        hipLaunchKernelGGL(k_seg_scatter, dim3((unsigned)max_chunks), dim3(256), lds_s, st,
+                           ent_out(j - 1)->as<uint32_t>(), kin, b->chunk_desc.as<uint4>(), shift, r,
+                           b->chunk_pos.as<uint32_t>(), ent_out(j)->as<uint32_t>(),
+                           last ? nullptr : key_out(j)->as<uint32_t>());
+        GG_HIP(hipGetLastError());
+        uint32_t* next = last ? b->offsets.as<uint32_t>() : segb[j & 1]->as<uint32_t>();
+        hipLaunchKernelGGL(k_seg_next, dim3(grid_for((size_t)nseg * R, 256)), dim3(256), 0, st, segp,
+                           b->chunk_start.as<uint32_t>(), b->chunk_pos.as<uint32_t>(), nseg, r, next);
+        GG_HIP(hipGetLastError());
+        nseg *= R;
+    }
 }
 
 }  // namespace gg

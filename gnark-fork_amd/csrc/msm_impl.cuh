@@ -75,14 +75,40 @@ __global__ void __launch_bounds__(256, 2) k_accum_affine(const Affine<F>* pts, c
     if (t >= n_items) return;
     uint32_t b = item_bucket[t];
     uint32_t j = (uint32_t)t - item_off[b];
-    uint32_t lo = offsets[b] + j * (uint32_t)K;
-    uint32_t hi = min(offsets[b + 1], lo + (uint32_t)K);
+    // bucket b (cnt entries) is cut into m = ceil(cnt / K) near-equal items
+    const uint32_t o = offsets[b], cnt = offsets[b + 1] - o;
+    const uint32_t m = (cnt + (uint32_t)K - 1) / (uint32_t)K;
+    const uint32_t lo = o + (uint32_t)(((uint64_t)j * cnt) / m);
+    const uint32_t hi = o + (uint32_t)(((uint64_t)(j + 1) * cnt) / m);
     Xyzz<F> acc = Xyzz<F>::inf();
-    for (uint32_t e = lo; e < hi; e++) {
-        uint32_t v = sorted[e];
-        Affine<F> p = ld(pts + (v & 0x7fffffffu));
-        if (v >> 31) p.y = -p.y;
-        xyzz_madd_inplace(acc, p);
+    if constexpr (sizeof(F) <= 32) {
+        // G1: software pipeline, the next point is in flight while this one is added
+        uint32_t v = 0, vn = 0;
+        Affine<F> p;
+        if (lo < hi) {
+            v = sorted[lo];
+            p = ld(pts + (v & 0x7fffffffu));
+        }
+        if (lo + 1 < hi) vn = sorted[lo + 1];
+        for (uint32_t e = lo; e < hi; e++) {
+            Affine<F> q = p;
+            const uint32_t cv = v;
+            if (e + 1 < hi) {
+                p = ld(pts + (vn & 0x7fffffffu));
+                v = vn;
+                if (e + 2 < hi) vn = sorted[e + 2];
+            }
+            if (cv >> 31) q.y = -q.y;
+            xyzz_madd_inplace(acc, q);
+        }
+    } else {
+        // G2: no room for a second point in registers (235 VGPRs at occupancy 2)
+        for (uint32_t e = lo; e < hi; e++) {
+            uint32_t v = sorted[e];
+            Affine<F> p = ld(pts + (v & 0x7fffffffu));
+            if (v >> 31) p.y = -p.y;
+            xyzz_madd_inplace(acc, p);
+        }
     }
     st(partial + t, acc);
 }
@@ -240,7 +266,7 @@ struct gg_msm_base {
     std::mutex mu;
     // scratch
     DevBuf digits, sorted, counts, offsets, cursor, itemcnt, item_off, item_bucket, maxcnt;
-    DevBuf keys, tmp_entry, tmp_key, hist, hoff, bin_start, chunk_start, chunk_hist, chunk_pos;
+    DevBuf keys, tmp_entry, tmp_key, hist, hoff, bin_start, seg2, chunk_start, chunk_hist, chunk_pos, chunk_desc;
     DevBuf partA, partB, segs, segs2, scal;
     std::vector<DevBuf> scan_tmp;
 };
@@ -406,7 +432,10 @@ inline Xyzz<F> msm_run(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st) {
 
     // ---- level 1: affine entries -> partials.  Buckets are cut into items of
     // <= K entries; bucket b's partials land at part[item_off[b] .. item_off[b+1]).
-    const int K1 = 32;
+    // item length: 32 entries, doubled (<= 256) while that still leaves > 3M items
+    int K1 = 32;
+    while (K1 < 256 && (size_t)b->W * n / (size_t)K1 > ((size_t)3 << 20)) K1 *= 2;
+    if (const char* e = getenv("GG_MSM_K1")) K1 = std::max(1, atoi(e));
     b->item_off.reserve((nb + 2) * 4);
     uint32_t* offs = b->offsets.as<uint32_t>();
     uint32_t* ioff = b->item_off.as<uint32_t>();
