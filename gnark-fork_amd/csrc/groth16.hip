@@ -22,9 +22,18 @@ struct gg_domain;
 struct gg_msm_base;
 
 namespace gg {
+struct MsmSort;
 void compute_h_device(gg_domain* d, Fr* A, Fr* B, Fr* C, Fr* H, hipStream_t st);
 void msm_device(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st);
 size_t msm_scalars_needed(gg_msm_base* b);
+gg_msm_base* msm_base_create_internal(int group, const void* host_points, size_t n,
+                                      const uint32_t* sidx, int window_bits, bool keep_inf);
+bool msm_same_shape(const gg_msm_base* a, const gg_msm_base* b);
+MsmSort* msm_own_sort(gg_msm_base* b);
+void msm_prepare_dev(gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
+void msm_finish_dev(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st);
+int msm_base_window(const gg_msm_base* b);
+int choose_c(size_t n, size_t point_bytes);
 }  // namespace gg
 
 using namespace gg;
@@ -37,6 +46,10 @@ struct gg_groth16_pk {
     G1Affine alpha, beta, delta;
     G2Affine beta2, delta2;
     size_t n_wires = 0, nb_public = 0;
+    // A and K are wire-indexed tables (infinity holes kept) sharing one sort of
+    // the wires; B1 and G2 share the sort of the B-filtered wires (same index map
+    // and window).  Falls back to separate sorts if the shapes ever differ.
+    bool share_AK = false, share_B = false;
     DevBuf wires, sa, sb, sc;
     hipStream_t s0 = nullptr, s1 = nullptr, s2 = nullptr, s3 = nullptr, s4 = nullptr;
     int device = 0;
@@ -103,11 +116,21 @@ extern "C" int gg_groth16_pk_create(int log_n, const void* omega_mont, const voi
     GG_CHECK(nB == 0 || (g1_B && g2_B), GG_ERR_INVALID_ARG, "null g1_B / g2_B");
     GG_CHECK(nK == 0 || g1_K, GG_ERR_INVALID_ARG, "null g1_K");
     GG_CHECK(nZ == 0 || g1_Z, GG_ERR_INVALID_ARG, "null g1_Z");
-    ck(gg_msm_base_create(GG_G1, g1_A, nA, 0, ia.data(), 0, &pk->A));
-    ck(gg_msm_base_create(GG_G1, g1_B, nB, 0, ib.data(), 0, &pk->B));
-    ck(gg_msm_base_create(GG_G1, g1_K, nK, 0, ik.data(), 0, &pk->K));
-    ck(gg_msm_base_create(GG_G1, g1_Z, nZ, 0, nullptr, 0, &pk->Z));
-    ck(gg_msm_base_create(GG_G2, g2_B, nB, 0, ib.data(), 0, &pk->B2));
+    // dense wire-indexed A and K (holes = infinity), one window size for both
+    {
+        std::vector<uint8_t> dense((size_t)n_wires * 64, 0);
+        for (size_t j = 0; j < nA; j++) memcpy(&dense[(size_t)ia[j] * 64], (const uint8_t*)g1_A + j * 64, 64);
+        const int cAK = choose_c(std::max<size_t>(n_wires, 1), 64);
+        pk->A = msm_base_create_internal(GG_G1, dense.data(), n_wires, nullptr, cAK, true);
+        std::fill(dense.begin(), dense.end(), 0);
+        for (size_t j = 0; j < nK; j++) memcpy(&dense[(size_t)ik[j] * 64], (const uint8_t*)g1_K + j * 64, 64);
+        pk->K = msm_base_create_internal(GG_G1, dense.data(), n_wires, nullptr, cAK, true);
+    }
+    pk->B = msm_base_create_internal(GG_G1, g1_B, nB, ib.data(), 0, false);
+    pk->B2 = msm_base_create_internal(GG_G2, g2_B, nB, ib.data(), msm_base_window(pk->B), false);
+    pk->Z = msm_base_create_internal(GG_G1, g1_Z, nZ, nullptr, 0, false);
+    pk->share_AK = msm_same_shape(pk->A, pk->K);
+    pk->share_B = msm_same_shape(pk->B, pk->B2);
     for (hipStream_t* x : {&pk->s0, &pk->s1, &pk->s2, &pk->s3, &pk->s4})
         GG_HIP(hipStreamCreateWithFlags(x, hipStreamNonBlocking));
     *out = pk.release();
@@ -226,11 +249,21 @@ extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_
         if (n > 1) msm_device(pk->Z, A, &jz, pk->s1);
         t_z = now_ms() - b;
     }));
-    spawn(guarded([&] { double a = now_ms(); msm_device(pk->A, wdev, &ja, pk->s2); t_a = now_ms() - a; }));
-    spawn(guarded([&] { double a = now_ms(); msm_device(pk->B, wdev, &jb, pk->s3); t_b = now_ms() - a; }));
-    spawn(guarded([&] { double a = now_ms(); msm_device(pk->K, wdev, &jk, pk->s4); t_k = now_ms() - a; }));
+    // wire sorts, enqueued from this thread before any finisher waits on their
+    // events: A's (shared with K) on s2, B1's (shared with G2) on s3
+    MsmSort* sAK = msm_own_sort(pk->A);
+    MsmSort* sB = msm_own_sort(pk->B);
+    MsmSort* sK = pk->share_AK ? sAK : msm_own_sort(pk->K);
+    MsmSort* sB2 = pk->share_B ? sB : msm_own_sort(pk->B2);
+    msm_prepare_dev(pk->A, sAK, wdev, pk->s2);
+    msm_prepare_dev(pk->B, sB, wdev, pk->s3);
+    if (!pk->share_AK) msm_prepare_dev(pk->K, sK, wdev, pk->s4);
+    if (!pk->share_B) msm_prepare_dev(pk->B2, sB2, wdev, pk->s0);
+    spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->A, sAK, &ja, pk->s2); t_a = now_ms() - a; }));
+    spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->B, sB, &jb, pk->s3); t_b = now_ms() - a; }));
+    spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->K, sK, &jk, pk->s4); t_k = now_ms() - a; }));
     double t2 = now_ms();
-    guarded([&] { msm_device(pk->B2, wdev, &j2, pk->s0); })();
+    guarded([&] { msm_finish_dev(pk->B2, sB2, &j2, pk->s0); })();
     double te = now_ms();
     for (auto& w : workers) w.join();
     if (wcode != GG_OK) throw Error(wcode, werr);

@@ -3,11 +3,13 @@
 
 namespace gg {
 void create_base_g1(gg_msm_base* b, const void* points, size_t n, int on_device,
-                    const uint32_t* sidx, int window_bits);
+                    const uint32_t* sidx, int window_bits, bool keep_inf);
 void create_base_g2(gg_msm_base* b, const void* points, size_t n, int on_device,
-                    const uint32_t* sidx, int window_bits);
+                    const uint32_t* sidx, int window_bits, bool keep_inf);
 void msm_run_g1(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st);
 void msm_run_g2(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st);
+void msm_finish_g1(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st);
+void msm_finish_g2(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st);
 }  // namespace gg
 
 using namespace gg;
@@ -22,8 +24,8 @@ extern "C" int gg_msm_base_create(int group, const void* points, size_t n, int p
     GG_CHECK(n < 0x80000000ull, GG_ERR_INVALID_ARG, "n too large");
     std::unique_ptr<gg_msm_base> b(new gg_msm_base());
     b->group = group;
-    if (group == GG_G1) create_base_g1(b.get(), points, n, points_on_device, scalar_index, window_bits);
-    else create_base_g2(b.get(), points, n, points_on_device, scalar_index, window_bits);
+    if (group == GG_G1) create_base_g1(b.get(), points, n, points_on_device, scalar_index, window_bits, false);
+    else create_base_g2(b.get(), points, n, points_on_device, scalar_index, window_bits, false);
     *out = b.release();
     GG_CAPI_END
 }
@@ -52,6 +54,32 @@ static void msm_device_locked(gg_msm_base* b, const Fr* scalars_dev, void* out_j
 void msm_device(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
     std::lock_guard<std::mutex> lk(b->mu);
     msm_device_locked(b, scalars_dev, out_jac, st);
+}
+// ---- shared sorts (Groth16): bases of one shape reuse one MsmSort
+gg_msm_base* msm_base_create_internal(int group, const void* host_points, size_t n,
+                                      const uint32_t* sidx, int window_bits, bool keep_inf) {
+    std::unique_ptr<gg_msm_base> b(new gg_msm_base());
+    b->group = group;
+    if (group == GG_G1) create_base_g1(b.get(), host_points, n, 0, sidx, window_bits, keep_inf);
+    else create_base_g2(b.get(), host_points, n, 0, sidx, window_bits, keep_inf);
+    return b.release();
+}
+bool msm_same_shape(const gg_msm_base* a, const gg_msm_base* b) {
+    if (a->n != b->n || a->c != b->c || a->W != b->W || a->has_sidx != b->has_sidx) return false;
+    if (!a->has_sidx || a->n == 0) return true;
+    std::vector<uint32_t> x(a->n), y(b->n);
+    GG_HIP(hipMemcpy(x.data(), a->sidx.p, a->n * 4, hipMemcpyDeviceToHost));
+    GG_HIP(hipMemcpy(y.data(), b->sidx.p, b->n * 4, hipMemcpyDeviceToHost));
+    return x == y;
+}
+MsmSort* msm_own_sort(gg_msm_base* b) { return &b->own; }
+int msm_base_window(const gg_msm_base* b) { return b->c; }
+void msm_prepare_dev(gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st) {
+    if (b->n) msm_prepare(b, s, scalars_dev, st);
+}
+void msm_finish_dev(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st) {
+    if (b->group == GG_G1) msm_finish_g1(b, s, out_jac, st);
+    else msm_finish_g2(b, s, out_jac, st);
 }
 size_t msm_scalars_needed(gg_msm_base* b) {
     return b->has_sidx ? (b->n ? (size_t)b->max_sidx + 1 : 0) : b->n;

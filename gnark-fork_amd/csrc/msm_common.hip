@@ -106,10 +106,10 @@ __global__ void __launch_bounds__(256) k_item_counts(const uint32_t* offsets, si
 
 // item -> bucket map: one thread per item, upper_bound over item_off (a heavy
 // bucket's thousands of items no longer serialise on one thread)
-__global__ void k_item_buckets(const uint32_t* item_off, size_t nb, size_t n_items,
+__global__ void k_item_buckets(const uint32_t* item_off, size_t nb, const uint32_t* n_items_dev,
                                uint32_t* item_bucket) {
     size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_items) return;
+    if (t >= *n_items_dev) return;
     size_t lo = 0, hi = nb;  // largest b with item_off[b] <= t (item_off[0] = 0)
     while (hi - lo > 1) {
         size_t mid = (lo + hi) >> 1;
@@ -496,7 +496,7 @@ static void sort_plan(int c, int& h, std::vector<int>& rs) {
     }
 }
 
-void sort_entries(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st) {
+void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st) {
     const size_t n = b->n, nb = b->nb;
     const int c = b->c, W = b->W;
     const size_t total = (size_t)W * n;
@@ -517,42 +517,42 @@ void sort_entries(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st) {
             ns <<= r;
         }
     }
-    b->keys.reserve(total * 4);
-    b->tmp_entry.reserve(total * 4);
-    b->tmp_key.reserve(total * 4);
-    b->sorted.reserve(total * 4);
-    b->hist.reserve(nh * 4);
-    b->hoff.reserve((nh + 1) * 4);
-    b->bin_start.reserve(((size_t)nb + 1) * 4);
-    b->seg2.reserve(((size_t)nb + 1) * 4);
-    b->offsets.reserve((nb + 1) * 4);
-    b->counts.reserve(nb * 4);
-    b->chunk_start.reserve(((size_t)nb + 1) * 4);
+    s->keys.reserve(total * 4);
+    s->tmp_entry.reserve(total * 4);
+    s->tmp_key.reserve(total * 4);
+    s->sorted.reserve(total * 4);
+    s->hist.reserve(nh * 4);
+    s->hoff.reserve((nh + 1) * 4);
+    s->bin_start.reserve(((size_t)nb + 1) * 4);
+    s->seg2.reserve(((size_t)nb + 1) * 4);
+    s->offsets.reserve((nb + 1) * 4);
+    s->counts.reserve(nb * 4);
+    s->chunk_start.reserve(((size_t)nb + 1) * 4);
     if (ch_max) {
-        b->chunk_hist.reserve(ch_max * 4);
-        b->chunk_pos.reserve((ch_max + 1) * 4);
-        b->chunk_desc.reserve(chunks_max * 16);
+        s->chunk_hist.reserve(ch_max * 4);
+        s->chunk_pos.reserve((ch_max + 1) * 4);
+        s->chunk_desc.reserve(chunks_max * 16);
     }
     hipLaunchKernelGGL(k_digits_hist, dim3(nblocks), dim3(256), nbins * 4, st, scalars_dev,
                        b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, spb, nbins, h,
-                       b->keys.as<uint32_t>(), b->hist.as<uint32_t>(), nblocks);
+                       s->keys.as<uint32_t>(), s->hist.as<uint32_t>(), nblocks);
     GG_HIP(hipGetLastError());
-    exclusive_scan(b->hist.as<uint32_t>(), b->hoff.as<uint32_t>(), nh, st, b->scan_tmp);
+    exclusive_scan(s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nh, st, s->scan_tmp);
     // segment starts ping-pong between bin_start and seg2; the last pass writes offsets
-    DevBuf* segb[2] = {&b->bin_start, &b->seg2};
+    DevBuf* segb[2] = {&s->bin_start, &s->seg2};
     hipLaunchKernelGGL(k_bin_starts, dim3(grid_for(nbins, 256)), dim3(256), 0, st,
-                       b->hoff.as<uint32_t>(), b->hist.as<uint32_t>(), nblocks, nbins,
-                       rs.empty() ? b->offsets.as<uint32_t>() : segb[0]->as<uint32_t>());
+                       s->hoff.as<uint32_t>(), s->hist.as<uint32_t>(), nblocks, nbins,
+                       rs.empty() ? s->offsets.as<uint32_t>() : segb[0]->as<uint32_t>());
     GG_HIP(hipGetLastError());
     const size_t lds_c = (2 * (size_t)nbins + 2 * (size_t)spb * W) * 4;
     GG_CHECK(lds_c <= 160 * 1024, GG_ERR_INTERNAL, "bin scatter LDS tile too large");
     // scatter stage j (0 = bin scatter) writes entries to `sorted` when the number
     // of stages after it is even, else tmp_entry; keys to tmp_key (j even) / keys (j odd)
     const int S = 1 + (int)rs.size();
-    auto ent_out = [&](int j) { return ((S - 1 - j) % 2 == 0) ? &b->sorted : &b->tmp_entry; };
-    auto key_out = [&](int j) { return (j % 2 == 0) ? &b->tmp_key : &b->keys; };
-    hipLaunchKernelGGL(k_bin_scatter, dim3(nblocks), dim3(256), lds_c, st, b->keys.as<uint32_t>(),
-                       n, W, c, spb, nbins, h, b->hist.as<uint32_t>(), b->hoff.as<uint32_t>(), nblocks,
+    auto ent_out = [&](int j) { return ((S - 1 - j) % 2 == 0) ? &s->sorted : &s->tmp_entry; };
+    auto key_out = [&](int j) { return (j % 2 == 0) ? &s->tmp_key : &s->keys; };
+    hipLaunchKernelGGL(k_bin_scatter, dim3(nblocks), dim3(256), lds_c, st, s->keys.as<uint32_t>(),
+                       n, W, c, spb, nbins, h, s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nblocks,
                        ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->as<uint32_t>() : nullptr);
     GG_HIP(hipGetLastError());
     uint32_t nseg = (uint32_t)nbins;
@@ -565,35 +565,78 @@ void sort_entries(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st) {
         const size_t max_chunks = (total + SEG_CH - 1) / SEG_CH + nseg;
         const uint32_t* segp = segb[(j - 1) & 1]->as<uint32_t>();
         hipLaunchKernelGGL(k_seg_chunk_counts, dim3(grid_for(nseg, 256)), dim3(256), 0, st, segp, nseg,
-                           b->counts.as<uint32_t>());
+                           s->counts.as<uint32_t>());
         GG_HIP(hipGetLastError());
-        exclusive_scan(b->counts.as<uint32_t>(), b->chunk_start.as<uint32_t>(), nseg, st, b->scan_tmp);
-        hipLaunchKernelGGL(k_set_total, dim3(1), dim3(1), 0, st, b->chunk_start.as<uint32_t>(),
-                           b->counts.as<uint32_t>(), (size_t)nseg);
+        exclusive_scan(s->counts.as<uint32_t>(), s->chunk_start.as<uint32_t>(), nseg, st, s->scan_tmp);
+        hipLaunchKernelGGL(k_set_total, dim3(1), dim3(1), 0, st, s->chunk_start.as<uint32_t>(),
+                           s->counts.as<uint32_t>(), (size_t)nseg);
         GG_HIP(hipGetLastError());
-        GG_HIP(hipMemsetAsync(b->chunk_hist.p, 0, max_chunks * R * 4, st));
+        GG_HIP(hipMemsetAsync(s->chunk_hist.p, 0, max_chunks * R * 4, st));
         hipLaunchKernelGGL(k_seg_chunk_desc, dim3(grid_for(max_chunks, 256)), dim3(256), 0, st, segp,
-                           b->chunk_start.as<uint32_t>(), nseg, (uint32_t)max_chunks,
-                           b->chunk_desc.as<uint4>());
+                           s->chunk_start.as<uint32_t>(), nseg, (uint32_t)max_chunks,
+                           s->chunk_desc.as<uint4>());
         GG_HIP(hipGetLastError());
         const uint32_t* kin = key_out(j - 1)->as<uint32_t>();
         hipLaunchKernelGGL(k_seg_hist, dim3((unsigned)max_chunks), dim3(256), 0, st, kin,
-                           b->chunk_desc.as<uint4>(), shift, r, b->chunk_hist.as<uint32_t>());
+                           s->chunk_desc.as<uint4>(), shift, r, s->chunk_hist.as<uint32_t>());
         GG_HIP(hipGetLastError());
-        exclusive_scan(b->chunk_hist.as<uint32_t>(), b->chunk_pos.as<uint32_t>(), max_chunks * R, st,
-                       b->scan_tmp);
+        exclusive_scan(s->chunk_hist.as<uint32_t>(), s->chunk_pos.as<uint32_t>(), max_chunks * R, st,
+                       s->scan_tmp);
         const size_t lds_s = (size_t)SEG_CH * (last ? 5 : 9);
         hipLaunchKernelGGL(k_seg_scatter, dim3((unsigned)max_chunks), dim3(256), lds_s, st,
-                           ent_out(j - 1)->as<uint32_t>(), kin, b->chunk_desc.as<uint4>(), shift, r,
-                           b->chunk_pos.as<uint32_t>(), ent_out(j)->as<uint32_t>(),
+                           ent_out(j - 1)->as<uint32_t>(), kin, s->chunk_desc.as<uint4>(), shift, r,
+                           s->chunk_pos.as<uint32_t>(), ent_out(j)->as<uint32_t>(),
                            last ? nullptr : key_out(j)->as<uint32_t>());
         GG_HIP(hipGetLastError());
-        uint32_t* next = last ? b->offsets.as<uint32_t>() : segb[j & 1]->as<uint32_t>();
+        uint32_t* next = last ? s->offsets.as<uint32_t>() : segb[j & 1]->as<uint32_t>();
         hipLaunchKernelGGL(k_seg_next, dim3(grid_for((size_t)nseg * R, 256)), dim3(256), 0, st, segp,
-                           b->chunk_start.as<uint32_t>(), b->chunk_pos.as<uint32_t>(), nseg, r, next);
+                           s->chunk_start.as<uint32_t>(), s->chunk_pos.as<uint32_t>(), nseg, r, next);
         GG_HIP(hipGetLastError());
         nseg *= R;
     }
+}
+
+// Sort + work items of one scalar vector over b's shape into s; records
+// s->ready_ev (items ready) and s->pin_ev ((n_items, max_items) on the host).
+void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st) {
+    const size_t n = b->n, nb = b->nb;
+    s->ensure_events();
+    s->counts.reserve(nb * 4);
+    s->offsets.reserve((nb + 1) * 4);
+    s->itemcnt.reserve(nb * 4);
+    s->item_off.reserve((nb + 2) * 4);
+    s->maxcnt.reserve(4);
+    {
+        ProfScope ps_sort("msm_sort", st, (double)n);
+        sort_entries(b, s, scalars_dev, st);
+        ps_sort.stop(st);
+    }
+    // Buckets are cut into items of <= K1 entries (32, doubled up to 256 while
+    // that still leaves > 3M items); bucket q's items are item_off[q] ..
+    // item_off[q+1].  (n_items, max_items) go to pinned memory behind an event
+    // while the accumulation runs on an upper-bound grid (no host stall).
+    int K1 = 32;
+    while (K1 < 256 && (size_t)b->W * n / (size_t)K1 > ((size_t)3 << 20)) K1 *= 2;
+    if (const char* e = getenv("GG_MSM_K1")) K1 = std::max(1, atoi(e));
+    s->K1 = K1;
+    s->items_ub = ((size_t)b->W * n + (size_t)K1 - 1) / (size_t)K1 + nb;
+    uint32_t* offs = s->offsets.as<uint32_t>();
+    uint32_t* ioff = s->item_off.as<uint32_t>();
+    GG_HIP(hipMemsetAsync(s->maxcnt.p, 0, 4, st));
+    hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nb, 256)), dim3(256), 0, st, offs, nb, K1,
+                       s->itemcnt.as<uint32_t>(), s->maxcnt.as<uint32_t>());
+    GG_HIP(hipGetLastError());
+    exclusive_scan(s->itemcnt.as<uint32_t>(), ioff, nb, st, s->scan_tmp);
+    hipLaunchKernelGGL(k_set_total_max, dim3(1), dim3(1), 0, st, ioff, s->itemcnt.as<uint32_t>(), nb,
+                       s->maxcnt.as<uint32_t>());
+    GG_HIP(hipGetLastError());
+    GG_HIP(hipMemcpyAsync(s->pin, ioff + nb, 8, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipEventRecord(s->pin_ev, st));
+    s->item_bucket.reserve((s->items_ub + 1) * 4);
+    hipLaunchKernelGGL(k_item_buckets, dim3(grid_for(s->items_ub, 256)), dim3(256), 0, st, ioff, nb,
+                       ioff + nb, s->item_bucket.as<uint32_t>());
+    GG_HIP(hipGetLastError());
+    GG_HIP(hipEventRecord(s->ready_ev, st));
 }
 
 }  // namespace gg

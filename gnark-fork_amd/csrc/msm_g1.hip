@@ -3,11 +3,15 @@
 
 namespace gg {
 void create_base_g1(gg_msm_base* b, const void* points, size_t n, int on_device,
-                      const uint32_t* sidx, int window_bits) {
-    create_base<Fp>(b, points, n, on_device, sidx, window_bits);
+                    const uint32_t* sidx, int window_bits, bool keep_inf) {
+    create_base<Fp>(b, points, n, on_device, sidx, window_bits, keep_inf);
 }
 void msm_run_g1(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
     G1Jac j = xyzz_to_jac(msm_run<Fp>(b, scalars_dev, st));
+    memcpy(out_jac, &j, sizeof(j));
+}
+void msm_finish_g1(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st) {
+    G1Jac j = xyzz_to_jac(msm_finish<Fp>(b, s, st));
     memcpy(out_jac, &j, sizeof(j));
 }
 }  // namespace gg

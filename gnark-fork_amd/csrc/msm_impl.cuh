@@ -57,30 +57,52 @@ __global__ void k_set_total(uint32_t* out, const uint32_t* in, size_t n);
 __global__ void k_set_total_max(uint32_t* out, const uint32_t* in, size_t n, const uint32_t* maxcnt);
 __global__ void k_item_counts(const uint32_t* offsets, size_t nb, int K, uint32_t* itemcnt,
                               uint32_t* maxcnt);
-__global__ void k_item_buckets(const uint32_t* item_off, size_t nb, size_t n_items,
+__global__ void k_item_buckets(const uint32_t* item_off, size_t nb, const uint32_t* n_items_dev,
                                uint32_t* item_bucket);
 void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, hipStream_t st,
                     std::vector<DevBuf>& tmp, int depth = 0);
 int choose_c(size_t n, size_t point_bytes);
-void sort_entries(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st);
+struct MsmSort;
+void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
+void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
 
-// level 1: sum up to K affine points of one bucket into an XYZZ partial
+constexpr uint32_t LIGHT = 16;  // buckets with <= LIGHT items: merged inside the accumulation block
+// In-block merge of light buckets' partials inside k_accum_affine: measured
+// slower on MI355X (the end-of-block tree is latency-bound: 2^20 accumulation
+// 1.45 -> 1.70 ms vs 0.11 ms for k_bucket_sum), so it is off for both groups.
+template <class F>
+constexpr bool kMergeInBlock = false;
+
+// level 1: sum up to K affine points of one bucket into an XYZZ partial, then
+// merge the partials of light buckets inside the block (LDS tree, <= 4 steps):
+// afterwards a light bucket's sum is part[item_off[b]] (+ part[next 256-item
+// block start] if the bucket straddles one).  Heavy buckets keep one partial per
+// item for k_seg_tree.  n_items is read from the device (no host sync).
 template <class F>
 __global__ void __launch_bounds__(256, 2) k_accum_affine(const Affine<F>* pts, const uint32_t* sorted,
                                                       const uint32_t* offsets,
                                                       const uint32_t* item_off,
-                                                      const uint32_t* item_bucket, size_t n_items,
-                                                      int K, Xyzz<F>* partial) {
-    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_items) return;
+                                                      const uint32_t* item_bucket,
+                                                      const uint32_t* n_items_dev, int K,
+                                                      int skip_inf, Xyzz<F>* partial) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char acc_lds[];
+    [[maybe_unused]] Xyzz<F>* sh = reinterpret_cast<Xyzz<F>*>(acc_lds);
+    const size_t n_items = *n_items_dev;
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if ((size_t)blockIdx.x * blockDim.x >= n_items) return;  // whole block past the end
+    const bool valid = t < n_items;
+    Xyzz<F> acc = Xyzz<F>::inf();
+    uint32_t io0 = 0, io1 = 0;
+    if (valid) {
     uint32_t b = item_bucket[t];
-    uint32_t j = (uint32_t)t - item_off[b];
+    io0 = item_off[b];
+    io1 = item_off[b + 1];
+    uint32_t j = (uint32_t)t - io0;
     // bucket b (cnt entries) is cut into m = ceil(cnt / K) near-equal items
     const uint32_t o = offsets[b], cnt = offsets[b + 1] - o;
     const uint32_t m = (cnt + (uint32_t)K - 1) / (uint32_t)K;
     const uint32_t lo = o + (uint32_t)(((uint64_t)j * cnt) / m);
     const uint32_t hi = o + (uint32_t)(((uint64_t)(j + 1) * cnt) / m);
-    Xyzz<F> acc = Xyzz<F>::inf();
     if constexpr (sizeof(F) <= 32) {
         // G1: software pipeline, the next point is in flight while this one is added
         uint32_t v = 0, vn = 0;
@@ -98,6 +120,7 @@ __global__ void __launch_bounds__(256, 2) k_accum_affine(const Affine<F>* pts, c
                 v = vn;
                 if (e + 2 < hi) vn = sorted[e + 2];
             }
+            if (skip_inf && q.is_inf()) continue;  // hole of a wire-indexed table
             if (cv >> 31) q.y = -q.y;
             xyzz_madd_inplace(acc, q);
         }
@@ -106,14 +129,36 @@ __global__ void __launch_bounds__(256, 2) k_accum_affine(const Affine<F>* pts, c
         for (uint32_t e = lo; e < hi; e++) {
             uint32_t v = sorted[e];
             Affine<F> p = ld(pts + (v & 0x7fffffffu));
+            if (skip_inf && p.is_inf()) continue;
             if (v >> 31) p.y = -p.y;
             xyzz_madd_inplace(acc, p);
         }
     }
-    st(partial + t, acc);
+    }  // valid
+    // in-block segmented tree over the light buckets' partials (G1 only: the G2
+    // XYZZ add does not fit the 256-VGPR budget of this kernel; G2 light
+    // buckets are summed by k_bucket_sum instead)
+    if constexpr (!kMergeInBlock<F>) {
+        if (valid) st(partial + t, acc);
+        return;
+    }
+    const bool light = valid && (io1 - io0) <= LIGHT;
+    const size_t blk0 = (size_t)blockIdx.x * blockDim.x;
+    const size_t seg_lo = light ? std::max<size_t>(io0, blk0) : t;
+    const size_t seg_hi = light ? std::min<size_t>(std::min<size_t>(io1, blk0 + blockDim.x), n_items) : t;
+    const uint32_t rel = (uint32_t)(t - seg_lo);
+    sh[threadIdx.x] = acc;
+    for (uint32_t s2 = 1; s2 < LIGHT; s2 <<= 1) {
+        const bool act = light && (rel % (2 * s2)) == 0 && t + s2 < seg_hi;
+        if (!__syncthreads_or(act)) break;
+        if (act) {
+            Xyzz<F> o2 = sh[threadIdx.x + s2];
+            xyzz_add_inplace(acc, o2);
+            sh[threadIdx.x] = acc;
+        }
+    }
+    if (valid) st(partial + t, acc);
 }
-
-constexpr uint32_t LIGHT = 16;  // buckets with <= LIGHT partials: k_bucket_sum
 
 // In-place segmented tree over the level-1 partials: bucket b owns slots
 // [item_off[b], item_off[b+1]); after the launches with stride 1, 2, 4, ...
@@ -136,8 +181,8 @@ __global__ void __launch_bounds__(256) k_seg_tree(Xyzz<F>* part, const uint32_t*
     st(part + p, acc);
 }
 
-// One thread per bucket sums its <= LIGHT partials in a chain (all lanes busy);
-// heavier buckets are left to k_seg_tree (skipped here).
+// One thread per light bucket sums its <= LIGHT partials in a chain (the G2
+// path; G1 merges light buckets inside k_accum_affine).
 template <class F>
 __global__ void __launch_bounds__(256) k_bucket_sum(Xyzz<F>* part, const uint32_t* item_off, size_t nb) {
     size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -158,8 +203,13 @@ __global__ void k_gather_buckets(const Xyzz<F>* partial, const uint32_t* item_of
     size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     uint32_t q = __brev((uint32_t)b) >> (33 - c);
-    uint32_t o = item_off[q];
-    st(S + b, (item_off[q + 1] > o) ? ld(partial + o) : Xyzz<F>::inf());
+    uint32_t o = item_off[q], e = item_off[q + 1];
+    Xyzz<F> v = (e > o) ? ld(partial + o) : Xyzz<F>::inf();
+    if (kMergeInBlock<F> && e - o > 1 && e - o <= LIGHT) {  // second in-block head
+        uint32_t k = ((o >> 8) + 1) << 8;
+        if (k < e) xyzz_add_inplace(v, ld(partial + k));
+    }
+    st(S + b, v);
 }
 
 // copy a list of small device arrays into one contiguous staging buffer
@@ -216,7 +266,7 @@ __global__ void k_pre_init(const Affine<F>* in, size_t n, Affine<F>* out0, Xyzz<
     if (i >= n) return;
     Affine<F> p = ld(in + i);
     st(out0 + i, p);
-    st(cur + i, Xyzz<F>{p.x, p.y, F::one(), F::one()});
+    st(cur + i, Xyzz<F>::from_affine(p));  // infinity (0, 0) -> ZZ = ZZZ = 0
 }
 
 template <class F>
@@ -234,19 +284,26 @@ __global__ void __launch_bounds__(256) k_pre_normalize(const Xyzz<F>* cur, size_
                                                        F* prefix, Affine<F>* out) {
     size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
+    // batch inversion of ZZZ along the thread's strided chain; infinity points
+    // (ZZZ = 0) enter the product as 1 and come out as (0, 0)
     F acc = F::one();
     for (size_t i = t; i < n; i += T) {
         st(prefix + i, acc);
-        acc = acc * ld(cur + i).zzz;
+        F z = ld(cur + i).zzz;
+        if (!z.is_zero()) acc = acc * z;
     }
     F inv = inverse(acc);
     size_t last = t + ((n - 1 - t) / T) * T;
     for (size_t i = last;; i -= T) {
         Xyzz<F> p = ld(cur + i);
-        F izzz = inv * ld(prefix + i);  // 1/ZZZ_i
-        inv = inv * p.zzz;
-        F izz = sqr(izzz) * sqr(p.zz);  // lambda^-6 * lambda^4 = 1/ZZ
-        st(out + i, Affine<F>{p.x * izz, p.y * izzz});
+        if (p.zzz.is_zero()) {
+            st(out + i, Affine<F>::inf());
+        } else {
+            F izzz = inv * ld(prefix + i);  // 1/ZZZ_i
+            inv = inv * p.zzz;
+            F izz = sqr(izzz) * sqr(p.zz);  // lambda^-6 * lambda^4 = 1/ZZ
+            st(out + i, Affine<F>{p.x * izz, p.y * izzz});
+        }
         if (i < T) break;
     }
 }
@@ -254,6 +311,36 @@ __global__ void __launch_bounds__(256) k_pre_normalize(const Xyzz<F>* cur, size_
 }  // namespace gg
 
 using gg::DevBuf;
+namespace gg {
+// Sorted entries + work items of one scalar vector over a base shape (n, c, W,
+// scalar index map).  Bases with identical shapes can share one: the Groth16
+// prover sorts the wires once for A/K and once for B1/G2.
+struct MsmSort {
+    DevBuf sorted, counts, offsets, itemcnt, item_off, item_bucket, maxcnt;
+    DevBuf keys, tmp_entry, tmp_key, hist, hoff, bin_start, seg2, chunk_start, chunk_hist, chunk_pos,
+        chunk_desc;
+    std::vector<DevBuf> scan_tmp;
+    uint32_t* pin = nullptr;          // pinned (n_items, max_items) read-back
+    hipEvent_t pin_ev = nullptr;      // after the read-back copy
+    hipEvent_t ready_ev = nullptr;    // after the item -> bucket map
+    int K1 = 32;
+    size_t items_ub = 0;
+    void ensure_events() {
+        if (!pin) GG_HIP(hipHostMalloc((void**)&pin, 16, hipHostMallocDefault));
+        if (!pin_ev) GG_HIP(hipEventCreateWithFlags(&pin_ev, hipEventDisableTiming));
+        if (!ready_ev) GG_HIP(hipEventCreateWithFlags(&ready_ev, hipEventDisableTiming));
+    }
+    MsmSort() = default;
+    MsmSort(const MsmSort&) = delete;
+    MsmSort& operator=(const MsmSort&) = delete;
+    ~MsmSort() {
+        if (pin) (void)hipHostFree(pin);
+        if (pin_ev) (void)hipEventDestroy(pin_ev);
+        if (ready_ev) (void)hipEventDestroy(ready_ev);
+    }
+};
+}  // namespace gg
+
 struct gg_msm_base {
     int group = GG_G1;
     size_t n = 0;  // resident points
@@ -262,13 +349,11 @@ struct gg_msm_base {
     DevBuf pts;   // W * n affine points, window-major
     DevBuf sidx;  // n u32 or empty
     bool has_sidx = false;
+    bool has_inf = false;  // wire-indexed table with infinity holes (skipped)
     uint32_t max_sidx = 0;
     std::mutex mu;
-    // scratch
-    DevBuf digits, sorted, counts, offsets, cursor, itemcnt, item_off, item_bucket, maxcnt;
-    DevBuf keys, tmp_entry, tmp_key, hist, hoff, bin_start, seg2, chunk_start, chunk_hist, chunk_pos, chunk_desc;
-    DevBuf partA, partB, segs, segs2, scal;
-    std::vector<DevBuf> scan_tmp;
+    gg::MsmSort own;                  // this base's sort state
+    DevBuf partA, segs, segs2, scal;  // per-base accumulation / reduction scratch
 };
 
 namespace gg {
@@ -417,87 +502,64 @@ inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* partials, const u
     return acc;
 }
 
+// Accumulation + reduction of base b over a prepared sort s (its own or one
+// shared with a base of identical shape).  Waits (device side) for s->ready_ev.
 template <class F>
-inline Xyzz<F> msm_run(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st) {
+inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, hipStream_t st) {
     const size_t n = b->n, nb = b->nb;
     if (n == 0) return Xyzz<F>::inf();
-    b->counts.reserve(nb * 4);
-    b->offsets.reserve((nb + 1) * 4);
-    b->itemcnt.reserve(nb * 4);
-    b->item_off.reserve((nb + 2) * 4);
-    b->maxcnt.reserve(4);
-    ProfScope ps_sort("msm_sort", st, (double)n);
-    sort_entries(b, scalars_dev, st);
-    ps_sort.stop(st);
-
-    // ---- level 1: affine entries -> partials.  Buckets are cut into items of
-    // <= K entries; bucket b's partials land at part[item_off[b] .. item_off[b+1]).
-    // item length: 32 entries, doubled (<= 256) while that still leaves > 3M items
-    int K1 = 32;
-    while (K1 < 256 && (size_t)b->W * n / (size_t)K1 > ((size_t)3 << 20)) K1 *= 2;
-    if (const char* e = getenv("GG_MSM_K1")) K1 = std::max(1, atoi(e));
-    b->item_off.reserve((nb + 2) * 4);
-    uint32_t* offs = b->offsets.as<uint32_t>();
-    uint32_t* ioff = b->item_off.as<uint32_t>();
-    uint32_t host[2];
-    auto make_items = [&](const uint32_t* in_off, uint32_t* out_off, int K) {
-        GG_HIP(hipMemsetAsync(b->maxcnt.p, 0, 4, st));
-        hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nb, 256)), dim3(256), 0, st, in_off, nb, K,
-                           b->itemcnt.as<uint32_t>(), b->maxcnt.as<uint32_t>());
-        GG_HIP(hipGetLastError());
-        exclusive_scan(b->itemcnt.as<uint32_t>(), out_off, nb, st, b->scan_tmp);
-        hipLaunchKernelGGL(k_set_total_max, dim3(1), dim3(1), 0, st, out_off,
-                           b->itemcnt.as<uint32_t>(), nb, b->maxcnt.as<uint32_t>());
-        GG_HIP(hipMemcpyAsync(host, out_off + nb, 8, hipMemcpyDeviceToHost, st));
-        GG_HIP(hipStreamSynchronize(st));
-        b->item_bucket.reserve(((size_t)host[0] + 1) * 4);
-        if (host[0])
-            hipLaunchKernelGGL(k_item_buckets, dim3(grid_for(host[0], 256)), dim3(256), 0, st, out_off,
-                               nb, (size_t)host[0], b->item_bucket.as<uint32_t>());
-        GG_HIP(hipGetLastError());
-        return std::make_pair((size_t)host[0], host[1]);
-    };
-    auto it1 = make_items(offs, ioff, K1);
-    size_t n_items = it1.first;
-    uint32_t max_items = it1.second;
-    b->partA.reserve((n_items + 1) * sizeof(Xyzz<F>));
-    if (n_items) {
+    GG_HIP(hipStreamWaitEvent(st, s->ready_ev, 0));
+    const uint32_t* offs = s->offsets.as<uint32_t>();
+    const uint32_t* ioff = s->item_off.as<uint32_t>();
+    const size_t items_ub = s->items_ub;
+    b->partA.reserve((items_ub + 1) * sizeof(Xyzz<F>));
+    {
         ProfScope ps_acc("msm_accum", st, (double)n);
-        hipLaunchKernelGGL(k_accum_affine<F>, dim3(grid_for(n_items, 256)), dim3(256), 0, st,
-                           (const Affine<F>*)b->pts.p, b->sorted.as<uint32_t>(), offs, ioff,
-                           b->item_bucket.as<uint32_t>(), n_items, K1, b->partA.as<Xyzz<F>>());
+        hipLaunchKernelGGL(k_accum_affine<F>, dim3(grid_for(items_ub, 256)), dim3(256),
+                           kMergeInBlock<F> ? 256 * sizeof(Xyzz<F>) : 0, st, (const Affine<F>*)b->pts.p,
+                           s->sorted.as<uint32_t>(), offs, ioff, s->item_bucket.as<uint32_t>(),
+                           ioff + nb, s->K1, (int)b->has_inf, b->partA.as<Xyzz<F>>());
         GG_HIP(hipGetLastError());
         ps_acc.stop(st);
     }
-    // ---- per-bucket tree over the partials (skew-robust: a bucket holding most
-    // entries costs log2(items) launches, not serial chains)
+    GG_HIP(hipEventSynchronize(s->pin_ev));
+    const size_t n_items = s->pin[0];
+    const uint32_t max_items = s->pin[1];
+    GG_CHECK(n_items <= items_ub, GG_ERR_INTERNAL, "item count above its bound");
+    // ---- level 2: light buckets summed by a thread each, heavy buckets (> LIGHT
+    // items) by a per-bucket tree (skew-robust: log2(items) launches)
     ProfScope ps_acc2("msm_accum2", st, (double)n);
-    if (max_items > 1) {
+    if (!kMergeInBlock<F> && max_items > 1) {
         hipLaunchKernelGGL(k_bucket_sum<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st,
                            b->partA.as<Xyzz<F>>(), ioff, nb);
         GG_HIP(hipGetLastError());
     }
-    // heavy buckets (> LIGHT items): fan-in 4 first, then binary steps
     for (uint32_t stride = 1; max_items > LIGHT && stride < max_items;) {
         uint32_t fan = (stride == 1) ? 4u : 2u;
         hipLaunchKernelGGL(k_seg_tree<F>, dim3(grid_for(n_items, 256)), dim3(256), 0, st,
-                           b->partA.as<Xyzz<F>>(), ioff, b->item_bucket.as<uint32_t>(), n_items, stride,
+                           b->partA.as<Xyzz<F>>(), ioff, s->item_bucket.as<uint32_t>(), n_items, stride,
                            fan);
         GG_HIP(hipGetLastError());
         stride *= fan;
     }
-    DevBuf* cur_part = &b->partA;
     ps_acc2.stop(st);
     // ---- bucket reduction: sum_b (b+1) S_b
     ProfScope ps_red("msm_reduce", st, (double)nb);
-    Xyzz<F> res = bucket_reduce_2d<F>(b, (const Xyzz<F>*)cur_part->p, ioff, st);
+    Xyzz<F> res = bucket_reduce_2d<F>(b, (const Xyzz<F>*)b->partA.p, ioff, st);
     ps_red.stop(st);
     return res;
 }
 
 template <class F>
+inline Xyzz<F> msm_run(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st) {
+    if (b->n == 0) return Xyzz<F>::inf();
+    msm_prepare(b, &b->own, scalars_dev, st);
+    return msm_finish<F>(b, &b->own, st);
+}
+
+template <class F>
 inline void create_base(gg_msm_base* b, const void* points, size_t n, int on_device,
-                        const uint32_t* sidx, int window_bits) {
+                        const uint32_t* sidx, int window_bits, bool keep_inf = false) {
     const size_t pb = sizeof(Affine<F>);
     std::vector<uint8_t> host;
     const uint8_t* src;
@@ -508,7 +570,8 @@ inline void create_base(gg_msm_base* b, const void* points, size_t n, int on_dev
     } else {
         src = (const uint8_t*)points;
     }
-    // drop infinity points, build the scalar index map
+    // drop infinity points, build the scalar index map (keep_inf: a wire-indexed
+    // table whose infinity holes stay in place and are skipped when summing)
     std::vector<uint8_t> keep;
     keep.reserve(n * pb);
     std::vector<uint32_t> idx;
@@ -517,7 +580,10 @@ inline void create_base(gg_msm_base* b, const void* points, size_t n, int on_dev
     static const uint8_t zero[128] = {0};
     for (size_t i = 0; i < n; i++) {
         const uint8_t* p = src + i * pb;
-        if (memcmp(p, zero, pb) == 0) { dropped = true; continue; }
+        if (memcmp(p, zero, pb) == 0) {
+            if (keep_inf) b->has_inf = true;
+            else { dropped = true; continue; }
+        }
         keep.insert(keep.end(), p, p + pb);
         idx.push_back(sidx ? sidx[i] : (uint32_t)i);
     }
