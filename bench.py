@@ -59,8 +59,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--log-n", type=int, default=20, help="MSM points per GPU = 2^log_n")
-    ap.add_argument("--groth16-log-n", type=int, default=20,
+    ap.add_argument("--groth16-log-n", type=int, default=24,
                     help="domain size of the extra Groth16 prove measurement (0 = skip)")
+    ap.add_argument("--ntt-log-n", type=int, default=24,
+                    help="size of the extra Fr NTT measurement, BASELINE configs[2] (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     args = ap.parse_args()
@@ -154,6 +156,13 @@ def main():
         "roofline": roofline, "kernels": kernels,
     }
 
+    # ---- Fr NTT 2^24 (BASELINE configs[2]; extra, rank 0 / N = 1 only)
+    if rank == 0 and world == 1 and args.ntt_log_n:
+        try:
+            out["ntt"] = ntt_bench(args.ntt_log_n)
+        except Exception as e:  # report, never hide
+            out["ntt"] = {"error": repr(e)}
+
     # ---- Groth16 prove (extra, rank 0 / N = 1 only)
     if rank == 0 and world == 1 and args.groth16_log_n:
         try:
@@ -197,6 +206,45 @@ def cpu_baseline(base, dsc, sc, n, threads):
     return {"value": m * reps / el / 1e6, "unit": "Mscalar-mul/s", "cores": nt, "kind": "port",
             "sample": f"G1 MSM 2^{m.bit_length() - 1} points x {reps} reps (C restatement, "
                       f"signed-digit Pippenger, {nt} OpenMP threads, not gnark)"}
+
+
+def ntt_bench(log_n, reps=10):
+    """Forward DIF + inverse DIT round trip on a resident 2^log_n Fr vector
+    (BASELINE configs[2]); per-transform time from wall clock and from HIP events
+    on the pass kernel (algorithmic bytes 2*n*32 per transform)."""
+    import gnark_amd
+    from gnark_amd import _lib, ntt, DeviceBuffer
+    n = 1 << log_n
+    d = ntt.Domain(log_n)
+    x = rand_scalars(n, 77)
+    buf = DeviceBuffer.from_host(x.tobytes())
+    d.fft(buf, ntt.DIF)
+    d.fft_inverse(buf, ntt.DIT)
+    _lib.check(_lib.lib.gg_synchronize())
+    t = time.perf_counter()
+    for _ in range(reps):
+        d.fft(buf, ntt.DIF)
+        d.fft_inverse(buf, ntt.DIT)
+    _lib.check(_lib.lib.gg_synchronize())
+    ms = 1e3 * (time.perf_counter() - t) / (2 * reps)
+    _lib.profile_enable(True)
+    for _ in range(3):
+        d.fft(buf, ntt.DIF)
+        d.fft_inverse(buf, ntt.DIT)
+    tot, cnt, _ = _lib.profile_get("ntt_pass")
+    _lib.profile_enable(False)
+    _lib.check(_lib.lib.gg_synchronize())
+    ok = buf.to_host() == x.tobytes()  # size-independent property: exact round trip
+    d.close()
+    alg = 2 * n * 32
+    passes_per_transform = cnt / 6 if cnt else None
+    return {"log_n": log_n, "ms_per_transform": ms, "round_trip_exact": ok,
+            "butterflies_per_s": (n // 2) * log_n / (ms * 1e-3),
+            "algorithmic_GBps": alg / (ms * 1e-3) / 1e9,
+            "hbm_frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "pass_kernel_avg_ms": tot / cnt if cnt else None,
+            "passes_per_transform": passes_per_transform,
+            "pass_GBps": (alg / (tot / cnt * 1e-3) / 1e9) if cnt else None}
 
 
 def groth16_bench(log_n, reps=3):

@@ -330,11 +330,102 @@ GG_HD Fp2 operator+(const Fp2& a, const Fp2& b) { return Fp2{a.a0 + b.a0, a.a1 +
 GG_HD Fp2 operator-(const Fp2& a, const Fp2& b) { return Fp2{a.a0 - b.a0, a.a1 - b.a1}; }
 GG_HD Fp2 operator-(const Fp2& a) { return Fp2{-a.a0, -a.a1}; }
 GG_HD Fp2 dbl(const Fp2& a) { return Fp2{a.a0 + a.a0, a.a1 + a.a1}; }
+#if defined(__HIP_DEVICE_COMPILE__)
+#include "wide_redc.inc"
+// 512-bit helpers (16 x u32, little endian)
+__device__ __forceinline__ void add512(const uint32_t* x, const uint32_t* y, uint32_t* o) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) o[i] = __builtin_addc(x[i], y[i], c, &c);
+}
+__device__ __forceinline__ void sub512(const uint32_t* x, const uint32_t* y, uint32_t* o) {
+    uint32_t b = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) o[i] = __builtin_subc(x[i], y[i], b, &b);
+}
+#define GG_WIDE_OPERANDS(A, B)                                                                  \
+    const uint32_t a0 = (A).v[0], a1 = (A).v[1], a2 = (A).v[2], a3 = (A).v[3], a4 = (A).v[4],     \
+                   a5 = (A).v[5], a6 = (A).v[6], a7 = (A).v[7];                                    \
+    const uint32_t b0 = (B).v[0], b1 = (B).v[1], b2 = (B).v[2], b3 = (B).v[3], b4 = (B).v[4],     \
+                   b5 = (B).v[5], b6 = (B).v[6], b7 = (B).v[7];
+// Montgomery reduction T * 2^-256 mod p of T < p * 2^256, canonical result
+__device__ __forceinline__ Fp fp_redc(const uint32_t* Tin) {
+    const uint32_t T0 = Tin[0], T1 = Tin[1], T2 = Tin[2], T3 = Tin[3], T4 = Tin[4], T5 = Tin[5],
+                   T6 = Tin[6], T7 = Tin[7], T8 = Tin[8], T9 = Tin[9], T10 = Tin[10], T11 = Tin[11],
+                   T12 = Tin[12], T13 = Tin[13], T14 = Tin[14], T15 = Tin[15];
+    const uint32_t P0 = FpCfg::P[0], P1 = FpCfg::P[1], P2 = FpCfg::P[2], P3 = FpCfg::P[3],
+                   P4 = FpCfg::P[4], P5 = FpCfg::P[5], P6 = FpCfg::P[6], P7 = FpCfg::P[7],
+                   INV = FpCfg::INV;
+    uint32_t m0, m1, m2, m3, m4, m5, m6, m7;
+    uint32_t r[8];
+    GG_REDC_BODY
+    Fp o, d;
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) d.v[i] = __builtin_subc(r[i], FpCfg::P[i], br, &br);
+#pragma unroll
+    for (int i = 0; i < 8; i++) o.v[i] = br ? r[i] : d.v[i];
+    return o;
+}
+// Fp2 product with lazy reduction (Karatsuba on 512-bit products, 2 reductions
+// instead of 3): c0 = REDC(a0b0 - a1b1 + p^2), c1 = REDC((a0+a1)(b0+b1) - a0b0 - a1b1);
+// both arguments are < 2p^2 < p * 2^256 (p < 2^254).  The products' digits are
+// folded into the two 512-bit accumulators column by column (no 512-bit temporaries).
+__device__ __forceinline__ Fp2 fp2_mul_lazy(const Fp2& x, const Fp2& y) {
+    uint32_t S[16], U[16];
+    {  // S = (x0 + x1)(y0 + y1), sums unreduced (< 2p < 2^255)
+        Fp sa, sb;
+        uint32_t ca = 0, cb = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            sa.v[i] = __builtin_addc(x.a0.v[i], x.a1.v[i], ca, &ca);
+            sb.v[i] = __builtin_addc(y.a0.v[i], y.a1.v[i], cb, &cb);
+        }
+        GG_WIDE_OPERANDS(sa, sb)
+#define GG_WIDE_COL(k, d) S[k] = (d);
+        GG_WIDE_BODY
+#undef GG_WIDE_COL
+    }
+    {  // t0 = x0 y0: S -= t0, U = t0 + p^2
+        GG_WIDE_OPERANDS(x.a0, y.a0)
+        uint32_t bs = 0, cu = 0;
+#define GG_WIDE_COL(k, d)                                          \
+    {                                                              \
+        const uint32_t d_ = (d);                                   \
+        S[k] = __builtin_subc(S[k], d_, bs, &bs);                  \
+        U[k] = __builtin_addc(d_, kFpP2[k], cu, &cu);              \
+    }
+        GG_WIDE_BODY
+#undef GG_WIDE_COL
+    }
+    {  // t1 = x1 y1: S -= t1, U -= t1
+        GG_WIDE_OPERANDS(x.a1, y.a1)
+        uint32_t bs = 0, bu = 0;
+#define GG_WIDE_COL(k, d)                                          \
+    {                                                              \
+        const uint32_t d_ = (d);                                   \
+        S[k] = __builtin_subc(S[k], d_, bs, &bs);                  \
+        U[k] = __builtin_subc(U[k], d_, bu, &bu);                  \
+    }
+        GG_WIDE_BODY
+#undef GG_WIDE_COL
+    }
+    return Fp2{fp_redc(U), fp_redc(S)};
+}
+#endif
+
+#ifndef GG_FP2_PLAIN
+#define GG_FP2_PLAIN 0
+#endif
 GG_HD Fp2 operator*(const Fp2& a, const Fp2& b) {
+#if defined(__HIP_DEVICE_COMPILE__) && !GG_FP2_PLAIN
+    return fp2_mul_lazy(a, b);
+#else
     Fp t0 = a.a0 * b.a0;
     Fp t1 = a.a1 * b.a1;
     Fp t2 = (a.a0 + a.a1) * (b.a0 + b.a1);
     return Fp2{t0 - t1, t2 - t0 - t1};
+#endif
 }
 GG_HD Fp2 sqr(const Fp2& a) {
     Fp t0 = (a.a0 + a.a1) * (a.a0 - a.a1);

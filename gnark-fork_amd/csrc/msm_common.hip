@@ -123,20 +123,18 @@ int choose_c(size_t n, size_t point_bytes) {
         int c = atoi(e);
         if (c >= 4 && c <= 24) return c;
     }
-    // cost ~ bucket additions (n*W) + reduction (~6 madd-equivalents per bucket:
-    // its tail is latency- not throughput-bound).  The top window holds only
-    // 254 - c(W-1) bits; if that is much narrower than c, all n of its entries
-    // pile into a few buckets (long chains, skewed sort bins): require
-    // top_bits >= c - 6 (measured on MI355X: c=18/19/21 at 2^20 are 2-3x slower).
+    // cost ~ bucket additions (n*W) + per-bucket work (sort bins, level-2 sums,
+    // reduction; ~24 madd-equivalents per bucket, fitted on MI355X: at 2^24 c=22
+    // W=12 is 2.6 ms slower than c=20 W=13).  Window widths are balanced
+    // (make_windows), so every c is usable.
     int best = 16;
     double bc = 1e300;
     for (int c = 4; c <= 23; c++) {
         int W = (255 + c - 1) / c;
-        int top_bits = 254 - c * (W - 1);
-        if (c > 8 && top_bits < c - 6) continue;
+        if ((255 + W - 1) / W != c) continue;  // same W as a narrower c
         double mem = (double)W * (double)n * (double)point_bytes;
         if (mem > 48e9) continue;  // precomputed table budget per base
-        double cost = (double)n * W + (double)(1u << (c - 1)) * 6.0;
+        double cost = (double)n * W + (double)(1u << (c - 1)) * 24.0;
         if (cost < bc) { bc = cost; best = c; }
     }
     return best;
@@ -212,13 +210,12 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t* cnt, uint32_t d, bool va
 }
 
 __global__ void __launch_bounds__(256) k_digits_hist(const Fr* scalars, const uint32_t* sidx,
-                                                     size_t n, int c, int W, int spb, int nbins, int h,
-                                                     uint32_t* keys, uint32_t* hist,
+                                                     size_t n, int c, int W, WinSpec ws, int spb,
+                                                     int nbins, int h, uint32_t* keys, uint32_t* hist,
                                                      uint32_t nblocks) {
     extern __shared__ uint32_t hh[];
     for (int j = threadIdx.x; j < nbins; j += blockDim.x) hh[j] = 0;
     __syncthreads();
-    const int half = 1 << (c - 1);
     // spb <= 512: at most two scalars per thread, both loaded before any digit work
     Fr scl[2];
     size_t idx[2];
@@ -240,8 +237,9 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fr* scalars, const ui
         Fr k = from_mont(scl[s]);
         int carry = 0;
         for (int w = 0; w < W; w++) {
-            int d = (int)extract_bits(k, w * c, c) + carry;
-            if (d > half) { d -= (1 << c); carry = 1; } else carry = 0;
+            const int bw = ws.bits[w];
+            int d = (int)extract_bits(k, ws.off[w], bw) + carry;
+            if (d > (1 << (bw - 1))) { d -= (1 << bw); carry = 1; } else carry = 0;
             uint32_t key = 0xffffffffu;
             if (d) {
                 uint32_t bk = (uint32_t)((d > 0 ? d : -d) - 1);
@@ -534,7 +532,7 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
         s->chunk_desc.reserve(chunks_max * 16);
     }
     hipLaunchKernelGGL(k_digits_hist, dim3(nblocks), dim3(256), nbins * 4, st, scalars_dev,
-                       b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, spb, nbins, h,
+                       b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, spb, nbins, h,
                        s->keys.as<uint32_t>(), s->hist.as<uint32_t>(), nblocks);
     GG_HIP(hipGetLastError());
     exclusive_scan(s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nh, st, s->scan_tmp);

@@ -62,6 +62,26 @@ __global__ void k_item_buckets(const uint32_t* item_off, size_t nb, const uint32
 void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, hipStream_t st,
                     std::vector<DevBuf>& tmp, int depth = 0);
 int choose_c(size_t n, size_t point_bytes);
+// Window layout: W windows of bits[w] (<= c) bits at bit offset off[w], sum 255
+// (254-bit scalars + the signed-digit carry).  Widths are balanced (they differ
+// by at most one bit), so no window is much narrower than c: a narrow top
+// window would pile all n of its entries into a few buckets.
+struct WinSpec {
+    uint8_t bits[64];
+    uint8_t off[64];
+};
+inline WinSpec make_windows(int c, int W) {
+    WinSpec ws{};
+    const int q = 255 / W, r = 255 % W;
+    int o = 0;
+    for (int w = 0; w < W; w++) {
+        ws.bits[w] = (uint8_t)(q + (w < r ? 1 : 0));
+        ws.off[w] = (uint8_t)o;
+        o += ws.bits[w];
+    }
+    (void)c;
+    return ws;
+}
 struct MsmSort;
 void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
 void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
@@ -345,6 +365,7 @@ struct gg_msm_base {
     int group = GG_G1;
     size_t n = 0;  // resident points
     int c = 0, W = 0;
+    gg::WinSpec win{};  // per-window bit widths / offsets
     size_t nb = 0;
     DevBuf pts;   // W * n affine points, window-major
     DevBuf sidx;  // n u32 or empty
@@ -372,7 +393,7 @@ inline void precompute(gg_msm_base* b, const Affine<F>* dev_in, hipStream_t st) 
     GG_HIP(hipGetLastError());
     for (int w = 1; w < b->W; w++) {
         hipLaunchKernelGGL(k_pre_dbl<F>, dim3(grid_for(n, 256)), dim3(256), 0, st,
-                           cur.as<Xyzz<F>>(), n, b->c);
+                           cur.as<Xyzz<F>>(), n, (int)b->win.bits[w - 1]);
         GG_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_pre_normalize<F>, dim3(grid_for(T, 256)), dim3(256), 0, st,
                            (const Xyzz<F>*)cur.p, n, T, prefix.as<F>(), out + (size_t)w * n);
@@ -594,6 +615,8 @@ inline void create_base(gg_msm_base* b, const void* points, size_t n, int on_dev
     b->c = window_bits ? window_bits : choose_c(std::max<size_t>(b->n, 1), pb);
     GG_CHECK(b->c >= 2 && b->c <= 24, GG_ERR_INVALID_ARG, "window_bits out of range [2, 24]");
     b->W = (255 + b->c - 1) / b->c;
+    b->c = (255 + b->W - 1) / b->W;  // widest balanced window for this W
+    b->win = make_windows(b->c, b->W);
     b->nb = (size_t)1 << (b->c - 1);
     GG_CHECK((double)b->W * (double)b->n < 2147483648.0, GG_ERR_UNSUPPORTED,
              "too many points x windows for 31-bit entry ids");

@@ -21,6 +21,8 @@ def test_msm_golden():
 @pytest.mark.parametrize("n,dist,c", [
     (1000, "uniform", 0), (1000, "witness", 0), (4096, "uniform", 4), (4096, "uniform", 8),
     (4096, "witness", 13), (1 << 16, "uniform", 0), (1 << 16, "witness", 0), (1 << 16, "small", 16),
+    # balanced window widths: 24 windows of 10/11 bits, 13 of 19/20, 12 of 21/22
+    (4096, "uniform", 11), (4096, "uniform", 20), (4096, "witness", 22),
 ])
 def test_msm_g1_vs_oracle(n, dist, c):
     from gnark_amd import msm
