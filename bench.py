@@ -23,6 +23,7 @@ sys.path.insert(0, os.path.join(ROOT, "gnark-fork_amd"))
 
 METRIC = ("Groth16 prove time + MSM G1 throughput (Mscalar-mul/s) BN254 2^24 R1CS, 1/2/4/8 GPU")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FPMUL_PEAK_G = 135.7  # measured BN254 Fp Montgomery multiplies/s (G), profiles/r01_v2_mbench_field.txt
 
 
 def log(*a):
@@ -138,12 +139,22 @@ def main():
     acc_ms = kernels["msm_accum"]["avg_ms"]
     alg_bytes = n * (64 + 32)  # N x (G1 affine 64 B + fr 32 B)
     achieved = alg_bytes / (acc_ms * 1e-3) / 1e9 if acc_ms else None
+    traffic, traffic_note = pmc_traffic("k_accum_affine<gg::Fe<gg::FpCfg> >", args.log_n, c, W)
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
+                "traffic_note": traffic_note,
                 "kernel": "k_accum_affine<Fp> (bucket accumulation)",
                 "algorithmic_bytes_per_launch": alg_bytes, "kernel_avg_ms": acc_ms,
                 "note": "EC MSM is VALU-integer bound (SURVEY 8d); HBM fraction reported as required"}
 
+    # VALU view of the same kernel: 8M+2S Fp multiplies per mixed add, one add per
+    # non-zero (window, scalar) entry, against the measured Fp-mul peak
+    # (profiles/r01_v2_mbench_field.txt, product-scanning Montgomery on MI355X)
+    if acc_ms:
+        mul_rate = n * W * 10 / (acc_ms * 1e-3) / 1e9
+        roofline["valu"] = {"achieved_Gfpmul_s": mul_rate, "peak_Gfpmul_s": FPMUL_PEAK_G,
+                            "frac": mul_rate / FPMUL_PEAK_G,
+                            "basis": "n*W mixed XYZZ adds x 10 Fp-mul (madd-2008-s)"}
     out = {
         "metric": METRIC, "value": value, "unit": "Mscalar-mul/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
@@ -182,6 +193,28 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel, log_n, c, W):
+    """HBM bytes per launch of `kernel` from the committed PMC profile of the same
+    workload (two separate rocprofv3 --pmc passes, FETCH_SIZE x2 per the gfx950
+    correction + WRITE_SIZE; tools/pmc_traffic.py).  None if no matching profile."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        wl = d.get("workload", {})
+        if (wl.get("log_n"), wl.get("window_bits"), wl.get("windows")) != (log_n, c, W):
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if kernel in k:
+                return v["traffic_bytes"], (
+                    f"{os.path.basename(f)}: FETCH_SIZE x2 + WRITE_SIZE per dispatch; the W={W} "
+                    f"precomputed window copies make the kernel read ~W x 64 B of points per scalar "
+                    f"(fixed-base trade: no doublings), so traffic >> the 96 B/scalar algorithmic bytes")
+    return None, "no committed PMC profile for this workload"
 
 
 def cpu_baseline(base, dsc, sc, n, threads):

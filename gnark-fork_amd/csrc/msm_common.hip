@@ -123,10 +123,11 @@ int choose_c(size_t n, size_t point_bytes) {
         int c = atoi(e);
         if (c >= 4 && c <= 24) return c;
     }
-    // cost ~ bucket additions (n*W) + per-bucket work (sort bins, level-2 sums,
-    // reduction; ~24 madd-equivalents per bucket, fitted on MI355X: at 2^24 c=22
-    // W=12 is 2.6 ms slower than c=20 W=13).  Window widths are balanced
-    // (make_windows), so every c is usable.
+    // cost ~ bucket additions (n*W) + ~6 madd-equivalents per bucket (reduction),
+    // with the entries-per-bucket (epb) sweet spot measured on MI355X (2^20:
+    // c=17; 2^22, 2^24: c=20): epb > 512 makes heavy buckets (level-2 trees,
+    // +25 %), epb < 100 leaves short, unbalanced items (+10 %).  Window widths
+    // are balanced (make_windows), so every c is usable.
     int best = 16;
     double bc = 1e300;
     for (int c = 4; c <= 23; c++) {
@@ -134,7 +135,10 @@ int choose_c(size_t n, size_t point_bytes) {
         if ((255 + W - 1) / W != c) continue;  // same W as a narrower c
         double mem = (double)W * (double)n * (double)point_bytes;
         if (mem > 48e9) continue;  // precomputed table budget per base
-        double cost = (double)n * W + (double)(1u << (c - 1)) * 24.0;
+        const double entries = (double)n * W, buckets = (double)(1u << (c - 1));
+        const double epb = entries / buckets;
+        double f = 1.0 + (epb > 512 ? 0.25 : 0.0) + (epb < 100 ? 0.10 : 0.0);
+        double cost = entries * f + buckets * 6.0;
         if (cost < bc) { bc = cost; best = c; }
     }
     return best;
