@@ -16,9 +16,9 @@ STEPS="${STEPS:-all}"
 if [[ "$STEPS" == *mb* || "$STEPS" == all ]]; then run 120 mbench.txt ./tools/mbench_field || ok $? || exit 2; fi
 if [[ "$STEPS" == *smoke* || "$STEPS" == all ]]; then run 300 smoke.txt python -c "import __graft_entry__ as g; g.smoke()" || ok $? || exit 2; fi
 if [[ "$STEPS" == *test* || "$STEPS" == all ]]; then run 900 pytest_gpu.txt python -m pytest tests -m gpu -q -x ${PYTEST_ARGS} || ok $? || exit 2; fi
-if [[ "$STEPS" == *bench* || "$STEPS" == all ]]; then run 600 bench.txt python bench.py --steps 10 --warmup 2 || ok $? || exit 2; fi
+if [[ "$STEPS" == *bench* || "$STEPS" == all ]]; then run 600 bench.txt python bench.py || ok $? || exit 2; fi
 if [[ "$STEPS" == *prof* || "$STEPS" == all ]]; then
   export TMPDIR=/tmp
-  run 600 rocprof.txt rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --groth16-log-n 20 || ok $? || exit 2
+  run 600 rocprof.txt rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline || ok $? || exit 2
 fi
 echo done >> gpurun_out/progress.txt
