@@ -76,12 +76,20 @@ def main():
     import gnark_amd
     from gnark_amd import _lib, msm, DeviceBuffer
 
-    _lib.check(_lib.lib.gg_set_device(local_rank))
-    torch.cuda.set_device(local_rank)
+    # one process per GPU over RCCL ("nccl").  GG_DIST_BACKEND=gloo is a rehearsal
+    # mode only (ranks may share a GPU; partials travel through host memory).
+    backend = os.environ.get("GG_DIST_BACKEND", "nccl")
+    dev = local_rank % max(1, torch.cuda.device_count())
+    _lib.check(_lib.lib.gg_set_device(dev))
+    torch.cuda.set_device(dev)
+    xdev = torch.device("cuda", dev) if backend == "nccl" else torch.device("cpu")
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         if dist is not None:
@@ -109,7 +117,7 @@ def main():
         if dist is None:
             return j
         # RCCL all-gather of the 96-B Jacobian partials + exact EC add (gnark_amd.dist)
-        return gdist.allgather_partial(msm.G1, j, device=torch.device("cuda", local_rank))
+        return gdist.allgather_partial(msm.G1, j, device=xdev)
 
     for _ in range(args.warmup):
         step()
@@ -120,7 +128,7 @@ def main():
     barrier()
     el = time.perf_counter() - t0
     if dist is not None:
-        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([el], dtype=torch.float64, device=xdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     ms_per_step = 1e3 * el / args.steps

@@ -62,7 +62,7 @@ def test_groth16_requires_accelerator_option():
         groth16.prove(pk, sol)
 
 
-def synthetic_case(log_n, n_wires, nb_public, seed, inf_frac=0.1):
+def synthetic_case(log_n, n_wires, nb_public, seed, inf_frac=0.1, k_inf_every=0):
     rng = np.random.default_rng(seed)
     n = 1 << log_n
     infA = (rng.random(n_wires) < inf_frac).astype(np.uint8)
@@ -79,6 +79,11 @@ def synthetic_case(log_n, n_wires, nb_public, seed, inf_frac=0.1):
 
     d = dict(log_n=log_n, g1_A=take(nA), g1_B=take(nB), g1_K=take(nK), g1_Z=take(n - 1),
              alpha1=take(1), beta1=take(1), delta1=take(1))
+    if k_inf_every:  # pk.G1.K may hold infinity points (setup.go:212-237; icicle.go:343-347)
+        k = bytearray(d["g1_K"])
+        for i in range(0, nK, k_inf_every):
+            k[i * 64:(i + 1) * 64] = bytes(64)
+        d["g1_K"] = bytes(k)
     g2 = random_g2_points(nB + 2, seed + 1).tobytes()
     d.update(g2_B=g2[:nB * 128], beta2=g2[nB * 128:(nB + 1) * 128], delta2=g2[(nB + 1) * 128:],
              infinity_A=infA.tobytes(), infinity_B=infB.tobytes(), nb_public=nb_public)
@@ -89,10 +94,12 @@ def synthetic_case(log_n, n_wires, nb_public, seed, inf_frac=0.1):
     return d, wires, sa, sb, sc, ncons, r, s
 
 
-@pytest.mark.parametrize("log_n,n_wires", [(6, 50), (12, 3000), (15, 30000)])
-def test_groth16_synthetic_vs_oracle(log_n, n_wires):
+@pytest.mark.parametrize("log_n,n_wires,k_inf_every", [(6, 50, 0), (12, 3000, 0), (12, 3000, 7),
+                                                       (15, 30000, 0)])
+def test_groth16_synthetic_vs_oracle(log_n, n_wires, k_inf_every):
     from gnark_amd import backend, groth16, DeviceBuffer
-    d, wires, sa, sb, sc, ncons, r, s = synthetic_case(log_n, n_wires, 3, 10 + log_n)
+    d, wires, sa, sb, sc, ncons, r, s = synthetic_case(log_n, n_wires, 3, 10 + log_n,
+                                                       k_inf_every=k_inf_every)
     pk = groth16.ProvingKey(groth16.ProvingKeyData(**d))
     nw = n_wires
     exp = coracle.groth16_prove(
