@@ -13,12 +13,12 @@
 
 namespace gg {
 
-template <class F>
-__global__ void __launch_bounds__(256) k_comb(const Affine<F>* table, const Fr* scalars, size_t n,
+template <class F, class SC>
+__global__ void __launch_bounds__(256) k_comb(const Affine<F>* table, const Fe<SC>* scalars, size_t n,
                                               Xyzz<F>* out) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    Fr k = from_mont(ld(scalars + i));
+    Fe<SC> k = from_mont(ld(scalars + i));
     Xyzz<F> acc = Xyzz<F>::inf();
     for (int w = 0; w < 32; w++) {
         uint32_t j = (k.v[w >> 2] >> ((w & 3) * 8)) & 0xffu;
@@ -84,7 +84,7 @@ static std::vector<Affine<F>> build_comb_table(const Affine<F>& base) {
     return T;
 }
 
-template <class F>
+template <class F, class SC>
 static void batch_mul(const void* base_aff, const void* scalars, size_t n, int scalars_on_device,
                       void* out, int out_on_device) {
     Affine<F> base;
@@ -94,11 +94,11 @@ static void batch_mul(const void* base_aff, const void* scalars, size_t n, int s
     DevBuf dtab(table.size() * sizeof(Affine<F>));
     GG_HIP(hipMemcpyAsync(dtab.p, table.data(), dtab.bytes, hipMemcpyHostToDevice, st));
     DevBuf dsc;
-    const Fr* sdev = (const Fr*)scalars;
+    const Fe<SC>* sdev = (const Fe<SC>*)scalars;
     if (!scalars_on_device) {
         dsc.alloc(n * 32);
         GG_HIP(hipMemcpyAsync(dsc.p, scalars, n * 32, hipMemcpyHostToDevice, st));
-        sdev = dsc.as<Fr>();
+        sdev = dsc.as<Fe<SC>>();
     }
     DevBuf cur(n * sizeof(Xyzz<F>)), prefix(n * sizeof(F));
     DevBuf dout;
@@ -107,7 +107,7 @@ static void batch_mul(const void* base_aff, const void* scalars, size_t n, int s
         dout.alloc(n * sizeof(Affine<F>));
         o = dout.as<Affine<F>>();
     }
-    hipLaunchKernelGGL(k_comb<F>, dim3(grid_for(n, 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL((k_comb<F, SC>), dim3(grid_for(n, 256)), dim3(256), 0, st,
                        (const Affine<F>*)dtab.p, sdev, n, cur.as<Xyzz<F>>());
     GG_HIP(hipGetLastError());
     const size_t T = std::min<size_t>(n, std::max<size_t>(16384, n / 64));
@@ -127,10 +127,11 @@ extern "C" int gg_batch_scalar_mul(int group, const void* base_aff, const void* 
                                    int scalars_on_device, void* out_aff, int out_on_device) {
     GG_CAPI_BEGIN
     GG_CHECK(base_aff && out_aff, GG_ERR_INVALID_ARG, "null argument");
-    GG_CHECK(group == GG_G1 || group == GG_G2, GG_ERR_INVALID_ARG, "bad group");
+    GG_CHECK(group == GG_G1 || group == GG_G2 || group == GG_BLS12_381_G1, GG_ERR_INVALID_ARG, "bad group");
     if (n == 0) return GG_OK;
     GG_CHECK(scalars, GG_ERR_INVALID_ARG, "null scalars");
-    if (group == GG_G1) batch_mul<Fp>(base_aff, scalars, n, scalars_on_device, out_aff, out_on_device);
-    else batch_mul<Fp2>(base_aff, scalars, n, scalars_on_device, out_aff, out_on_device);
+    if (group == GG_G1) batch_mul<Fp, FrCfg>(base_aff, scalars, n, scalars_on_device, out_aff, out_on_device);
+    else if (group == GG_G2) batch_mul<Fp2, FrCfg>(base_aff, scalars, n, scalars_on_device, out_aff, out_on_device);
+    else batch_mul<FpBls, FrBlsCfg>(base_aff, scalars, n, scalars_on_device, out_aff, out_on_device);
     GG_CAPI_END
 }

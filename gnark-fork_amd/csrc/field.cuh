@@ -19,6 +19,7 @@
 namespace gg {
 
 struct FpCfg {
+    static constexpr int N = 8;
     static constexpr uint32_t P[8] = {0xd87cfd47u, 0x3c208c16u, 0x6871ca8du, 0x97816a91u,
                                       0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
     static constexpr uint32_t INV = 0xe4866389u;  // -p^-1 mod 2^32
@@ -30,6 +31,7 @@ struct FpCfg {
 };
 
 struct FrCfg {
+    static constexpr int N = 8;
     static constexpr uint32_t P[8] = {0xf0000001u, 0x43e1f593u, 0x79b97091u, 0x2833e848u,
                                       0x8181585du, 0xb85045b6u, 0xe131a029u, 0x30644e72u};
     static constexpr uint32_t INV = 0xefffffffu;
@@ -40,62 +42,92 @@ struct FrCfg {
                                        0x53bb8085u, 0x8c49833du, 0x7f4e44a5u, 0x0216d0b1u};
 };
 
+// BLS12-381 base field (381-bit, 12 x u32, R = 2^384) and scalar field (255-bit,
+// 8 x u32, R = 2^256): gnark-crypto ecc/bls12-381 fp.Element ([6]uint64) /
+// fr.Element ([4]uint64) layouts.  Moduli: std/math/emulated/emparams/emparams.go:145-171.
+struct FpBlsCfg {
+    static constexpr int N = 12;
+    static constexpr uint32_t P[12] = {0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu,
+                                       0xf6b0f624u, 0x6730d2a0u, 0xf38512bfu, 0x64774b84u,
+                                       0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau};
+    static constexpr uint32_t INV = 0xfffcfffdu;
+    static constexpr uint64_t INV64 = 0x89f3fffcfffcfffdull;
+    static constexpr uint32_t ONE[12] = {0x0002fffdu, 0x76090000u, 0xc40c0002u, 0xebf4000bu,
+                                         0x53c758bau, 0x5f489857u, 0x70525745u, 0x77ce5853u,
+                                         0xa256ec6du, 0x5c071a97u, 0xfa80e493u, 0x15f65ec3u};
+    static constexpr uint32_t R2[12] = {0x1c341746u, 0xf4df1f34u, 0x09d104f1u, 0x0a76e6a6u,
+                                        0x4c95b6d5u, 0x8de5476cu, 0x939d83c0u, 0x67eb88a9u,
+                                        0xb519952du, 0x9a793e85u, 0x92cae3aau, 0x11988fe5u};
+};
+
+struct FrBlsCfg {
+    static constexpr int N = 8;
+    static constexpr uint32_t P[8] = {0x00000001u, 0xffffffffu, 0xfffe5bfeu, 0x53bda402u,
+                                      0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+    static constexpr uint32_t INV = 0xffffffffu;
+    static constexpr uint64_t INV64 = 0xfffffffeffffffffull;
+    static constexpr uint32_t ONE[8] = {0xfffffffeu, 0x00000001u, 0x00034802u, 0x5884b7fau,
+                                        0xecbc4ff5u, 0x998c4fefu, 0xacc5056fu, 0x1824b159u};
+    static constexpr uint32_t R2[8] = {0xf3f29c6du, 0xc999e990u, 0x87925c23u, 0x2b6cedcbu,
+                                       0x7254398fu, 0x05d31496u, 0x9f59ff11u, 0x0748d9d9u};
+};
+
 template <class C>
 struct Fe {
-    uint32_t v[8];
+    uint32_t v[C::N];
 
     static GG_HD Fe zero() {
         Fe r;
 #pragma unroll
-        for (int i = 0; i < 8; i++) r.v[i] = 0;
+        for (int i = 0; i < C::N; i++) r.v[i] = 0;
         return r;
     }
     static GG_HD Fe one() {
         Fe r;
 #pragma unroll
-        for (int i = 0; i < 8; i++) r.v[i] = C::ONE[i];
+        for (int i = 0; i < C::N; i++) r.v[i] = C::ONE[i];
         return r;
     }
     static GG_HD Fe r2() {
         Fe r;
 #pragma unroll
-        for (int i = 0; i < 8; i++) r.v[i] = C::R2[i];
+        for (int i = 0; i < C::N; i++) r.v[i] = C::R2[i];
         return r;
     }
     static GG_HD Fe modulus() {
         Fe r;
 #pragma unroll
-        for (int i = 0; i < 8; i++) r.v[i] = C::P[i];
+        for (int i = 0; i < C::N; i++) r.v[i] = C::P[i];
         return r;
     }
     GG_HD bool is_zero() const {
         uint32_t x = 0;
 #pragma unroll
-        for (int i = 0; i < 8; i++) x |= v[i];
+        for (int i = 0; i < C::N; i++) x |= v[i];
         return x == 0;
     }
     GG_HD bool operator==(const Fe& o) const {
         uint32_t x = 0;
 #pragma unroll
-        for (int i = 0; i < 8; i++) x |= v[i] ^ o.v[i];
+        for (int i = 0; i < C::N; i++) x |= v[i] ^ o.v[i];
         return x == 0;
     }
     GG_HD bool operator!=(const Fe& o) const { return !(*this == o); }
 };
 
-// r = a + b mod p   (inputs < p < 2^254)
+// r = a + b mod p   (inputs < p; p < 2^(32N-1), so no overflow)
 template <class C>
 GG_HD Fe<C> operator+(const Fe<C>& a, const Fe<C>& b) {
     Fe<C> r, s;
     uint32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) r.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+    for (int i = 0; i < C::N; i++) r.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
     uint32_t br = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) s.v[i] = __builtin_subc(r.v[i], C::P[i], br, &br);
+    for (int i = 0; i < C::N; i++) s.v[i] = __builtin_subc(r.v[i], C::P[i], br, &br);
     // br == 0  <=>  r >= p
 #pragma unroll
-    for (int i = 0; i < 8; i++) r.v[i] = br ? r.v[i] : s.v[i];
+    for (int i = 0; i < C::N; i++) r.v[i] = br ? r.v[i] : s.v[i];
     return r;
 }
 
@@ -104,12 +136,12 @@ GG_HD Fe<C> operator-(const Fe<C>& a, const Fe<C>& b) {
     Fe<C> r, s;
     uint32_t br = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) r.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
+    for (int i = 0; i < C::N; i++) r.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
     uint32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) s.v[i] = __builtin_addc(r.v[i], C::P[i], c, &c);
+    for (int i = 0; i < C::N; i++) s.v[i] = __builtin_addc(r.v[i], C::P[i], c, &c);
 #pragma unroll
-    for (int i = 0; i < 8; i++) r.v[i] = br ? s.v[i] : r.v[i];
+    for (int i = 0; i < C::N; i++) r.v[i] = br ? s.v[i] : r.v[i];
     return r;
 }
 
@@ -130,45 +162,47 @@ GG_HD Fe<C> dbl(const Fe<C>& a) {
 template <class C>
 inline Fe<C> mont_mul_host(const Fe<C>& a, const Fe<C>& b) {
     typedef unsigned __int128 u128;
-    uint64_t A[4], B[4], P[4], t[6] = {0, 0, 0, 0, 0, 0};
-    for (int i = 0; i < 4; i++) {
+    constexpr int K = C::N / 2;  // 64-bit limbs
+    uint64_t A[K], B[K], P[K], t[K + 2];
+    for (int i = 0; i < K + 2; i++) t[i] = 0;
+    for (int i = 0; i < K; i++) {
         A[i] = (uint64_t)a.v[2 * i] | ((uint64_t)a.v[2 * i + 1] << 32);
         B[i] = (uint64_t)b.v[2 * i] | ((uint64_t)b.v[2 * i + 1] << 32);
         P[i] = (uint64_t)C::P[2 * i] | ((uint64_t)C::P[2 * i + 1] << 32);
     }
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < K; i++) {
         uint64_t carry = 0;
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j < K; j++) {
             u128 x = (u128)A[j] * B[i] + t[j] + carry;
             t[j] = (uint64_t)x;
             carry = (uint64_t)(x >> 64);
         }
-        u128 x = (u128)t[4] + carry;
-        t[4] = (uint64_t)x;
-        t[5] = (uint64_t)(x >> 64);
+        u128 x = (u128)t[K] + carry;
+        t[K] = (uint64_t)x;
+        t[K + 1] = (uint64_t)(x >> 64);
         uint64_t m = t[0] * C::INV64;
         x = (u128)m * P[0] + t[0];
         carry = (uint64_t)(x >> 64);
-        for (int j = 1; j < 4; j++) {
+        for (int j = 1; j < K; j++) {
             x = (u128)m * P[j] + t[j] + carry;
             t[j - 1] = (uint64_t)x;
             carry = (uint64_t)(x >> 64);
         }
-        x = (u128)t[4] + carry;
-        t[3] = (uint64_t)x;
-        t[4] = t[5] + (uint64_t)(x >> 64);
+        x = (u128)t[K] + carry;
+        t[K - 1] = (uint64_t)x;
+        t[K] = t[K + 1] + (uint64_t)(x >> 64);
     }
     // conditional subtraction
-    uint64_t s[4];
+    uint64_t s[K];
     uint64_t br = 0;
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < K; i++) {
         u128 x = (u128)t[i] - P[i] - br;
         s[i] = (uint64_t)x;
         br = (uint64_t)(x >> 64) & 1;
     }
-    bool ge = t[4] || !br;
+    bool ge = t[K] || !br;
     Fe<C> r;
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < K; i++) {
         uint64_t v = ge ? s[i] : t[i];
         r.v[2 * i] = (uint32_t)v;
         r.v[2 * i + 1] = (uint32_t)(v >> 32);
@@ -201,7 +235,7 @@ __device__ __forceinline__ void mac96s(uint64_t& acc, uint32_t& c2, uint32_t x, 
 // v_mad_u64_u32 + 128 v_addc and no per-product 64-bit add/move chains (the
 // CIOS form needs ~500 instructions, this one ~330).
 template <class C>
-__device__ __forceinline__ Fe<C> mont_mul_ps(const Fe<C>& a, const Fe<C>& b) {
+__device__ __forceinline__ Fe<C> mont_mul_ps8(const Fe<C>& a, const Fe<C>& b) {
     const uint32_t a0 = a.v[0], a1 = a.v[1], a2 = a.v[2], a3 = a.v[3], a4 = a.v[4], a5 = a.v[5],
                    a6 = a.v[6], a7 = a.v[7];
     const uint32_t b0 = b.v[0], b1 = b.v[1], b2 = b.v[2], b3 = b.v[3], b4 = b.v[4], b5 = b.v[5],
@@ -221,6 +255,37 @@ __device__ __forceinline__ Fe<C> mont_mul_ps(const Fe<C>& a, const Fe<C>& b) {
     for (int i = 0; i < 8; i++) r.v[i] = br ? t[i] : s.v[i];
     return r;
 }
+// 12-limb (BLS12-381 Fp) product scanning: 288 v_mad_u64_u32 + 288 v_addc
+template <class C>
+__device__ __forceinline__ Fe<C> mont_mul_ps12(const Fe<C>& a, const Fe<C>& b) {
+    const uint32_t a0 = a.v[0], a1 = a.v[1], a2 = a.v[2], a3 = a.v[3], a4 = a.v[4], a5 = a.v[5],
+                   a6 = a.v[6], a7 = a.v[7], a8 = a.v[8], a9 = a.v[9], a10 = a.v[10], a11 = a.v[11];
+    const uint32_t b0 = b.v[0], b1 = b.v[1], b2 = b.v[2], b3 = b.v[3], b4 = b.v[4], b5 = b.v[5],
+                   b6 = b.v[6], b7 = b.v[7], b8 = b.v[8], b9 = b.v[9], b10 = b.v[10], b11 = b.v[11];
+    const uint32_t P0 = C::P[0], P1 = C::P[1], P2 = C::P[2], P3 = C::P[3], P4 = C::P[4],
+                   P5 = C::P[5], P6 = C::P[6], P7 = C::P[7], P8 = C::P[8], P9 = C::P[9],
+                   P10 = C::P[10], P11 = C::P[11], INV = C::INV;
+    uint32_t m0, m1, m2, m3, m4, m5, m6, m7, m8, m9, m10, m11;
+    uint32_t t[12];
+    uint64_t acc = 0;
+    uint32_t c2 = 0;
+#include "mont_ps12.inc"
+    Fe<C> r, s;
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 12; i++) s.v[i] = __builtin_subc(t[i], C::P[i], br, &br);
+#pragma unroll
+    for (int i = 0; i < 12; i++) r.v[i] = br ? t[i] : s.v[i];
+    return r;
+}
+template <class C>
+__device__ __forceinline__ Fe<C> mont_mul_ps(const Fe<C>& a, const Fe<C>& b) {
+    if constexpr (C::N == 8) return mont_mul_ps8(a, b);
+    else {
+        static_assert(C::N == 12, "limb count");
+        return mont_mul_ps12(a, b);
+    }
+}
 #endif
 
 #ifndef GG_MUL_CIOS
@@ -236,14 +301,14 @@ GG_HD Fe<C> operator*(const Fe<C>& a, const Fe<C>& b) {
 #elif !GG_MUL_CIOS
     return mont_mul_ps(a, b);
 #else
-    uint32_t t[8];
+    uint32_t t[C::N];
 #pragma unroll
-    for (int j = 0; j < 8; j++) t[j] = 0;
+    for (int j = 0; j < C::N; j++) t[j] = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
+    for (int i = 0; i < C::N; i++) {
         uint64_t acc = 0;
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
+        for (int j = 0; j < C::N; j++) {
             acc = (uint64_t)a.v[j] * b.v[i] + t[j] + (acc >> 32);
             t[j] = (uint32_t)acc;
         }
@@ -251,18 +316,18 @@ GG_HD Fe<C> operator*(const Fe<C>& a, const Fe<C>& b) {
         uint32_t m = t[0] * C::INV;
         acc = (uint64_t)m * C::P[0] + t[0];
 #pragma unroll
-        for (int j = 1; j < 8; j++) {
+        for (int j = 1; j < C::N; j++) {
             acc = (uint64_t)m * C::P[j] + t[j] + (acc >> 32);
             t[j - 1] = (uint32_t)acc;
         }
-        t[7] = t8 + (uint32_t)(acc >> 32);
+        t[C::N - 1] = t8 + (uint32_t)(acc >> 32);
     }
     Fe<C> r, s;
     uint32_t br = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) s.v[i] = __builtin_subc(t[i], C::P[i], br, &br);
+    for (int i = 0; i < C::N; i++) s.v[i] = __builtin_subc(t[i], C::P[i], br, &br);
 #pragma unroll
-    for (int i = 0; i < 8; i++) r.v[i] = br ? t[i] : s.v[i];
+    for (int i = 0; i < C::N; i++) r.v[i] = br ? t[i] : s.v[i];
     return r;
 #endif
 }
@@ -288,12 +353,12 @@ GG_HD Fe<C> from_mont(const Fe<C>& a) {
 template <class C>
 GG_HD Fe<C> inverse(const Fe<C>& a) {
     // exponent p - 2, scanned from the top bit
-    uint32_t e[8];
+    uint32_t e[C::N];
+    uint32_t br = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) e[i] = C::P[i];
-    e[0] -= 2;  // low limb of both moduli is >= 2
+    for (int i = 0; i < C::N; i++) e[i] = __builtin_subc(C::P[i], i == 0 ? 2u : 0u, br, &br);
     Fe<C> acc = Fe<C>::one();
-    for (int i = 255; i >= 0; i--) {
+    for (int i = 32 * C::N - 1; i >= 0; i--) {
         acc = sqr(acc);
         if ((e[i >> 5] >> (i & 31)) & 1) acc = acc * a;
     }
@@ -314,6 +379,8 @@ GG_HD Fe<C> pow_u64(const Fe<C>& x, uint64_t e) {
 
 using Fp = Fe<FpCfg>;
 using Fr = Fe<FrCfg>;
+using FpBls = Fe<FpBlsCfg>;
+using FrBls = Fe<FrBlsCfg>;
 
 // ---------------------------------------------------------------------------
 // Fp2 = Fp[u] / (u^2 + 1)   (gnark-crypto bn254 E2 layout: {A0, A1})

@@ -33,7 +33,7 @@ MsmSort* msm_own_sort(gg_msm_base* b);
 void msm_prepare_dev(gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
 void msm_finish_dev(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st);
 int msm_base_window(const gg_msm_base* b);
-int choose_c(size_t n, size_t point_bytes);
+int choose_c(size_t n, size_t point_bytes, int total_bits);
 }  // namespace gg
 
 using namespace gg;
@@ -120,7 +120,7 @@ extern "C" int gg_groth16_pk_create(int log_n, const void* omega_mont, const voi
     {
         std::vector<uint8_t> dense((size_t)n_wires * 64, 0);
         for (size_t j = 0; j < nA; j++) memcpy(&dense[(size_t)ia[j] * 64], (const uint8_t*)g1_A + j * 64, 64);
-        const int cAK = choose_c(std::max<size_t>(n_wires, 1), 64);
+        const int cAK = choose_c(std::max<size_t>(n_wires, 1), 64, 255);
         pk->A = msm_base_create_internal(GG_G1, dense.data(), n_wires, nullptr, cAK, true);
         std::fill(dense.begin(), dense.end(), 0);
         for (size_t j = 0; j < nK; j++) memcpy(&dense[(size_t)ik[j] * 64], (const uint8_t*)g1_K + j * 64, 64);

@@ -1,0 +1,19 @@
+// BLS12-381 G1 instantiation of the bucket MSM (KZG commitments of the PlonK
+// prover: backend/plonk/bls12-381/prove.go:336, 494, 769, 1165-1169, 1203-1213).
+// Coordinates in the 12-limb Fp (R = 2^384), scalars BLS12-381 fr (255-bit).
+#include "msm_impl.cuh"
+
+namespace gg {
+void create_base_bls(gg_msm_base* b, const void* points, size_t n, int on_device,
+                     const uint32_t* sidx, int window_bits, bool keep_inf) {
+    create_base<FpBls>(b, points, n, on_device, sidx, window_bits, keep_inf, 1);
+}
+void msm_run_bls(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
+    Jac<FpBls> j = xyzz_to_jac(msm_run<FpBls>(b, scalars_dev, st));
+    memcpy(out_jac, &j, sizeof(j));
+}
+void msm_finish_bls(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st) {
+    Jac<FpBls> j = xyzz_to_jac(msm_finish<FpBls>(b, s, st));
+    memcpy(out_jac, &j, sizeof(j));
+}
+}  // namespace gg

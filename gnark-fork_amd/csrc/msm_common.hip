@@ -76,7 +76,8 @@ __global__ void k_set_total(uint32_t* out, const uint32_t* in, size_t n) {
     else out[0] = 0;
 }
 
-__device__ __forceinline__ uint32_t extract_bits(const Fr& k, int bit, int c) {
+template <class E>
+__device__ __forceinline__ uint32_t extract_bits(const E& k, int bit, int c) {
     if (bit >= 256) return 0;
     int limb = bit >> 5, off = bit & 31;
     uint64_t v = k.v[limb] >> off;
@@ -118,7 +119,7 @@ __global__ void k_item_buckets(const uint32_t* item_off, size_t nb, const uint32
     item_bucket[t] = (uint32_t)lo;
 }
 
-int choose_c(size_t n, size_t point_bytes) {
+int choose_c(size_t n, size_t point_bytes, int total_bits) {
     if (const char* e = getenv("GG_MSM_WINDOW")) {  // tuning override
         int c = atoi(e);
         if (c >= 4 && c <= 24) return c;
@@ -131,8 +132,8 @@ int choose_c(size_t n, size_t point_bytes) {
     int best = 16;
     double bc = 1e300;
     for (int c = 4; c <= 23; c++) {
-        int W = (255 + c - 1) / c;
-        if ((255 + W - 1) / W != c) continue;  // same W as a narrower c
+        int W = (total_bits + c - 1) / c;
+        if ((total_bits + W - 1) / W != c) continue;  // same W as a narrower c
         double mem = (double)W * (double)n * (double)point_bytes;
         if (mem > 48e9) continue;  // precomputed table budget per base
         const double entries = (double)n * W, buckets = (double)(1u << (c - 1));
@@ -213,7 +214,8 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t* cnt, uint32_t d, bool va
     return b + rank;
 }
 
-__global__ void __launch_bounds__(256) k_digits_hist(const Fr* scalars, const uint32_t* sidx,
+template <class SC>
+__global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, const uint32_t* sidx,
                                                      size_t n, int c, int W, WinSpec ws, int spb,
                                                      int nbins, int h, uint32_t* keys, uint32_t* hist,
                                                      uint32_t nblocks) {
@@ -221,7 +223,7 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fr* scalars, const ui
     for (int j = threadIdx.x; j < nbins; j += blockDim.x) hh[j] = 0;
     __syncthreads();
     // spb <= 512: at most two scalars per thread, both loaded before any digit work
-    Fr scl[2];
+    Fe<SC> scl[2];
     size_t idx[2];
 #pragma unroll
     for (int s = 0; s < 2; s++) {
@@ -238,7 +240,7 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fr* scalars, const ui
     for (int s = 0; s < 2; s++) {
         if (idx[s] == ~(size_t)0) continue;
         const size_t i = idx[s];
-        Fr k = from_mont(scl[s]);
+        Fe<SC> k = from_mont(scl[s]);
         int carry = 0;
         for (int w = 0; w < W; w++) {
             const int bw = ws.bits[w];
@@ -535,9 +537,15 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
         s->chunk_pos.reserve((ch_max + 1) * 4);
         s->chunk_desc.reserve(chunks_max * 16);
     }
-    hipLaunchKernelGGL(k_digits_hist, dim3(nblocks), dim3(256), nbins * 4, st, scalars_dev,
-                       b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, spb, nbins, h,
-                       s->keys.as<uint32_t>(), s->hist.as<uint32_t>(), nblocks);
+    if (b->scurve)
+        hipLaunchKernelGGL(k_digits_hist<FrBlsCfg>, dim3(nblocks), dim3(256), nbins * 4, st,
+                           (const FrBls*)scalars_dev, b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n,
+                           c, W, b->win, spb, nbins, h, s->keys.as<uint32_t>(), s->hist.as<uint32_t>(),
+                           nblocks);
+    else
+        hipLaunchKernelGGL(k_digits_hist<FrCfg>, dim3(nblocks), dim3(256), nbins * 4, st, scalars_dev,
+                           b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, spb, nbins,
+                           h, s->keys.as<uint32_t>(), s->hist.as<uint32_t>(), nblocks);
     GG_HIP(hipGetLastError());
     exclusive_scan(s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nh, st, s->scan_tmp);
     // segment starts ping-pong between bin_start and seg2; the last pass writes offsets

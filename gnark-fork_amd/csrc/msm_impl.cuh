@@ -61,18 +61,21 @@ __global__ void k_item_buckets(const uint32_t* item_off, size_t nb, const uint32
                                uint32_t* item_bucket);
 void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, hipStream_t st,
                     std::vector<DevBuf>& tmp, int depth = 0);
-int choose_c(size_t n, size_t point_bytes);
-// Window layout: W windows of bits[w] (<= c) bits at bit offset off[w], sum 255
-// (254-bit scalars + the signed-digit carry).  Widths are balanced (they differ
+int choose_c(size_t n, size_t point_bytes, int total_bits = 255);
+// scalar field of a base: 0 = BN254 fr (254-bit), 1 = BLS12-381 fr (255-bit)
+inline int scalar_total_bits(int scurve) { return scurve ? 256 : 255; }
+// Window layout: W windows of bits[w] (<= c) bits at bit offset off[w], summing
+// to scalar bits + 1 (the signed-digit carry): 255 for BN254 fr (254-bit),
+// 256 for BLS12-381 fr (255-bit).  Widths are balanced (they differ
 // by at most one bit), so no window is much narrower than c: a narrow top
 // window would pile all n of its entries into a few buckets.
 struct WinSpec {
     uint8_t bits[64];
     uint8_t off[64];
 };
-inline WinSpec make_windows(int c, int W) {
+inline WinSpec make_windows(int c, int W, int total) {
     WinSpec ws{};
-    const int q = 255 / W, r = 255 % W;
+    const int q = total / W, r = total % W;
     int o = 0;
     for (int w = 0; w < W; w++) {
         ws.bits[w] = (uint8_t)(q + (w < r ? 1 : 0));
@@ -371,6 +374,7 @@ struct gg_msm_base {
     DevBuf sidx;  // n u32 or empty
     bool has_sidx = false;
     bool has_inf = false;  // wire-indexed table with infinity holes (skipped)
+    int scurve = 0;        // scalar field: 0 = BN254 fr, 1 = BLS12-381 fr
     uint32_t max_sidx = 0;
     std::mutex mu;
     gg::MsmSort own;                  // this base's sort state
@@ -580,7 +584,10 @@ inline Xyzz<F> msm_run(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st) {
 
 template <class F>
 inline void create_base(gg_msm_base* b, const void* points, size_t n, int on_device,
-                        const uint32_t* sidx, int window_bits, bool keep_inf = false) {
+                        const uint32_t* sidx, int window_bits, bool keep_inf = false,
+                        int scurve = 0) {
+    b->scurve = scurve;
+    const int total = scalar_total_bits(scurve);
     const size_t pb = sizeof(Affine<F>);
     std::vector<uint8_t> host;
     const uint8_t* src;
@@ -612,11 +619,12 @@ inline void create_base(gg_msm_base* b, const void* points, size_t n, int on_dev
     b->has_sidx = dropped || sidx != nullptr;
     b->max_sidx = 0;
     for (uint32_t v : idx) b->max_sidx = std::max(b->max_sidx, v);
-    b->c = window_bits ? window_bits : choose_c(std::max<size_t>(b->n, 1), pb);
+    b->c = window_bits ? window_bits : choose_c(std::max<size_t>(b->n, 1), pb, total);
     GG_CHECK(b->c >= 2 && b->c <= 24, GG_ERR_INVALID_ARG, "window_bits out of range [2, 24]");
-    b->W = (255 + b->c - 1) / b->c;
-    b->c = (255 + b->W - 1) / b->W;  // widest balanced window for this W
-    b->win = make_windows(b->c, b->W);
+    b->W = (total + b->c - 1) / b->c;
+    b->c = (total + b->W - 1) / b->W;  // widest balanced window for this W
+    GG_CHECK(b->W <= 64, GG_ERR_INVALID_ARG, "too many windows");
+    b->win = make_windows(b->c, b->W, total);
     b->nb = (size_t)1 << (b->c - 1);
     GG_CHECK((double)b->W * (double)b->n < 2147483648.0, GG_ERR_UNSUPPORTED,
              "too many points x windows for 31-bit entry ids");

@@ -39,53 +39,59 @@ enum ScaleKind {
     SK_COUNT = 7
 };
 
+template <class F>
 struct ScaleSpec {
-    const Fr* hi;  // 2^(L-S) entries (constant folded in)
-    const Fr* lo;  // 2^S entries
+    const F* hi;  // 2^(L-S) entries (constant folded in)
+    const F* lo;  // 2^S entries
     int shift;     // S
     int bitrev;    // index by bitrev(i) instead of i
 };
 
+template <class F>
 struct PassParams {
-    const Fr* in;
-    Fr* out;
-    const Fr* tw;
+    const F* in;
+    F* out;
+    const F* tw;
     int log_n;
     int b_lo;
     int k;
     int tl;
     int dit;
     int has_pre;
-    ScaleSpec pre;
+    ScaleSpec<F> pre;
     int has_post;
-    ScaleSpec post;
+    ScaleSpec<F> post;
     int epi_mul_sub;  // out = ea*eb - x
-    const Fr* ea;
-    const Fr* eb;
+    const F* ea;
+    const F* eb;
 };
 
 __device__ __forceinline__ uint32_t brev_bits(uint32_t i, int L) {
     return L ? (__brev(i) >> (32 - L)) : 0u;
 }
 
-__device__ __forceinline__ Fr load_fr(const Fr* p) {
+template <class F>
+__device__ __forceinline__ F load_fr(const F* p) {
+    static_assert(sizeof(F) == 32, "8-limb scalar field");
     const uint4* q = reinterpret_cast<const uint4*>(p);
     uint4 a = q[0], b = q[1];
-    Fr r;
+    F r;
     r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
     r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
     return r;
 }
 
-__device__ __forceinline__ void store_fr(Fr* p, const Fr& r) {
+template <class F>
+__device__ __forceinline__ void store_fr(F* p, const F& r) {
     uint4* q = reinterpret_cast<uint4*>(p);
     q[0] = make_uint4(r.v[0], r.v[1], r.v[2], r.v[3]);
     q[1] = make_uint4(r.v[4], r.v[5], r.v[6], r.v[7]);
 }
 
-__device__ __forceinline__ Fr apply_scale(const ScaleSpec& s, uint32_t g, int L, const Fr& x) {
+template <class F>
+__device__ __forceinline__ F apply_scale(const ScaleSpec<F>& s, uint32_t g, int L, const F& x) {
     uint32_t e = s.bitrev ? brev_bits(g, L) : g;
-    Fr f = load_fr(s.hi + (e >> s.shift));
+    F f = load_fr(s.hi + (e >> s.shift));
     if (s.lo) f = f * load_fr(s.lo + (e & ((1u << s.shift) - 1)));
     return x * f;
 }
@@ -93,8 +99,8 @@ __device__ __forceinline__ Fr apply_scale(const ScaleSpec& s, uint32_t g, int L,
 // ---- radix-8 register-round pass ------------------------------------------
 __device__ __forceinline__ int lidx(int e) { return e + (e >> 5); }  // padded LDS index
 
-template <int NB, bool DIT>
-__device__ __forceinline__ void ntt_round(const PassParams& P, uint32_t* lds, int TP, int T, int qlo,
+template <class F, int NB, bool DIT>
+__device__ __forceinline__ void ntt_round(const PassParams<F>& P, uint32_t* lds, int TP, int T, int qlo,
                                           bool first, bool last, uint32_t base_hi, uint32_t lo0) {
     constexpr int R = 1 << NB;
     const int tl = P.tl;
@@ -104,7 +110,7 @@ __device__ __forceinline__ void ntt_round(const PassParams& P, uint32_t* lds, in
     const int groups = T >> NB;
     for (int gi = threadIdx.x; gi < groups; gi += blockDim.x) {
         uint32_t e[R], g[R];
-        Fr x[R];
+        F x[R];
         const uint32_t low = (uint32_t)gi & lowmask, high = ((uint32_t)gi >> pos) << (pos + NB);
 #pragma unroll
         for (int m = 0; m < R; m++) {
@@ -129,18 +135,18 @@ __device__ __forceinline__ void ntt_round(const PassParams& P, uint32_t* lds, in
             const int r = DIT ? s2 : (NB - 1 - s2);
             const int b = P.b_lo + qlo + r;
             const uint32_t bmask = (1u << b) - 1;
-            const Fr* twb = P.tw + bmask;  // stage-b table starts at 2^b - 1
+            const F* twb = P.tw + bmask;  // stage-b table starts at 2^b - 1
 #pragma unroll
             for (int m = 0; m < R; m++) {
                 if (m & (1 << r)) continue;
                 const int m2 = m | (1 << r);
                 const uint32_t i = g[m] & bmask;
                 if (DIT) {
-                    Fr t = i ? x[m2] * load_fr(twb + i) : x[m2];
+                    F t = i ? x[m2] * load_fr(twb + i) : x[m2];
                     x[m2] = x[m] - t;
                     x[m] = x[m] + t;
                 } else {
-                    Fr d = x[m] - x[m2];
+                    F d = x[m] - x[m2];
                     x[m] = x[m] + x[m2];
                     x[m2] = i ? d * load_fr(twb + i) : d;
                 }
@@ -149,7 +155,7 @@ __device__ __forceinline__ void ntt_round(const PassParams& P, uint32_t* lds, in
         if (last) {
 #pragma unroll
             for (int m = 0; m < R; m++) {
-                Fr y = x[m];
+                F y = x[m];
                 if (P.has_post) y = apply_scale(P.post, g[m], P.log_n, y);
                 if (P.epi_mul_sub) y = load_fr(P.ea + g[m]) * load_fr(P.eb + g[m]) - y;
                 store_fr(P.out + g[m], y);
@@ -164,8 +170,8 @@ __device__ __forceinline__ void ntt_round(const PassParams& P, uint32_t* lds, in
     }
 }
 
-template <bool DIT>
-__global__ void __launch_bounds__(256) k_ntt_pass(PassParams P) {
+template <class F, bool DIT>
+__global__ void __launch_bounds__(256) k_ntt_pass(PassParams<F> P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int k = P.k, tl = P.tl;
     const int T = 1 << (k + tl);
@@ -179,7 +185,7 @@ __global__ void __launch_bounds__(256) k_ntt_pass(PassParams P) {
     if (k == 0) {  // n = 1: scaling only
         for (int e = threadIdx.x; e < T; e += blockDim.x) {
             uint32_t g = base_hi | (lo0 + (uint32_t)e);
-            Fr x = load_fr(P.in + g);
+            F x = load_fr(P.in + g);
             if (P.has_pre) x = apply_scale(P.pre, g, P.log_n, x);
             if (P.has_post) x = apply_scale(P.post, g, P.log_n, x);
             if (P.epi_mul_sub) x = load_fr(P.ea + g) * load_fr(P.eb + g) - x;
@@ -195,23 +201,24 @@ __global__ void __launch_bounds__(256) k_ntt_pass(PassParams P) {
         const int qlo = DIT ? done : (k - done - nb);
         const bool last = (done + nb == k);
         if (!first) __syncthreads();
-        if (nb == 3) ntt_round<3, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
-        else if (nb == 2) ntt_round<2, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
-        else ntt_round<1, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
+        if (nb == 3) ntt_round<F, 3, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
+        else if (nb == 2) ntt_round<F, 2, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
+        else ntt_round<F, 1, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
         first = false;
         done += nb;
     }
 }
 
 // per-stage twiddle table: tw[(2^b - 1) + i] = w^(i << (L-1-b)), i < 2^b
-__global__ void k_stage_twiddles(Fr* out, size_t count, int L, const Fr* hi, const Fr* lo, int S) {
+template <class F>
+__global__ void k_stage_twiddles(F* out, size_t count, int L, const F* hi, const F* lo, int S) {
     size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= count) return;
     uint32_t v = (uint32_t)t + 1;
     int b = 31 - __clz((int)v);
     uint32_t i = v - (1u << b);
     uint32_t ex = i << (L - 1 - b);
-    Fr x = load_fr(hi + (ex >> S)) * load_fr(lo + (ex & ((1u << S) - 1)));
+    F x = load_fr(hi + (ex >> S)) * load_fr(lo + (ex & ((1u << S) - 1)));
     store_fr(out + t, x);
 }
 
@@ -246,50 +253,69 @@ static std::vector<Pass> plan_passes(int L, bool dit) {
 
 using namespace gg;
 
-struct gg_domain {
+namespace gg {
+// Domain of one scalar field: gnark-crypto fft.Domain (Generator, FrMultiplicativeGen,
+// CardinalityInv) plus the device tables.
+template <class C>
+struct DomainT {
+    using F = Fe<C>;
     int log_n = 0;
     size_t n = 1;
-    Fr omega, omega_inv, g, g_inv, n_inv, den;
+    F omega, omega_inv, g, g_inv, n_inv, den;
     DevBuf tw, twinv;
     int S = 0;
     DevBuf scale_hi[SK_COUNT], scale_lo[SK_COUNT];
-    ScaleSpec spec[SK_COUNT];
+    ScaleSpec<F> spec[SK_COUNT];
+};
+}  // namespace gg
+
+// curve: GG_CURVE_BN254 (Groth16 domain) or GG_CURVE_BLS12_381 (PlonK domains)
+struct gg_domain {
+    int curve = GG_CURVE_BN254;
+    int log_n = 0;
+    size_t n = 1;
+    std::unique_ptr<DomainT<FrCfg>> bn;
+    std::unique_ptr<DomainT<FrBlsCfg>> bls;
     DevBuf scratch;  // computeH b/c buffers
     std::mutex mu;
 };
 
 namespace gg {
 
-static void build_pow_tables(int L, int S, const Fr& x, const Fr& c, std::vector<Fr>& hi,
-                             std::vector<Fr>& lo) {
+template <class F>
+static void build_pow_tables(int L, int S, const F& x, const F& c, std::vector<F>& hi,
+                             std::vector<F>& lo) {
     size_t nlo = (size_t)1 << S, nhi = (size_t)1 << (L - S);
     lo.resize(nlo);
     hi.resize(nhi);
-    Fr acc = Fr::one();
+    F acc = F::one();
     for (size_t i = 0; i < nlo; i++) { lo[i] = acc; acc = acc * x; }
-    Fr step = acc;  // x^(2^S)
+    F step = acc;  // x^(2^S)
     acc = c;
     for (size_t i = 0; i < nhi; i++) { hi[i] = acc; acc = acc * step; }
 }
 
-static void upload(DevBuf& b, const std::vector<Fr>& v) {
-    b.alloc(v.size() * sizeof(Fr));
-    GG_HIP(hipMemcpy(b.p, v.data(), v.size() * sizeof(Fr), hipMemcpyHostToDevice));
+template <class F>
+static void upload(DevBuf& b, const std::vector<F>& v) {
+    b.alloc(v.size() * sizeof(F));
+    GG_HIP(hipMemcpy(b.p, v.data(), v.size() * sizeof(F), hipMemcpyHostToDevice));
 }
 
 static hipStream_t pick_stream(void* s) { return s ? (hipStream_t)s : hipStreamPerThread; }
 
-void run_transform(gg_domain* d, const Fr* in, Fr* out, bool dit, bool inverse_tw, int pre_kind,
-                   int post_kind, const Fr* ea, const Fr* eb, hipStream_t st) {
+template <class C>
+void run_transform(DomainT<C>* d, const Fe<C>* in, Fe<C>* out, bool dit, bool inverse_tw, int pre_kind,
+                   int post_kind, const Fe<C>* ea, const Fe<C>* eb, hipStream_t st) {
+    using F = Fe<C>;
     const int L = d->log_n;
     auto passes = plan_passes(L, dit);
-    const Fr* src = in;
+    const F* src = in;
     for (size_t pi = 0; pi < passes.size(); pi++) {
         const Pass& ps = passes[pi];
-        PassParams P{};
+        PassParams<F> P{};
         P.in = src;
         P.out = out;
-        P.tw = (const Fr*)(inverse_tw ? d->twinv.p : d->tw.p);
+        P.tw = (const F*)(inverse_tw ? d->twinv.p : d->tw.p);
         P.log_n = L;
         P.b_lo = ps.b_lo;
         P.k = ps.k;
@@ -303,8 +329,8 @@ void run_transform(gg_domain* d, const Fr* in, Fr* out, bool dit, bool inverse_t
         unsigned tiles = (unsigned)(d->n / (size_t)T);
         size_t lds = (ps.k > 3) ? (size_t)(T + (T >> 5)) * 32 : 0;  // single-round passes skip LDS
         ProfScope prof("ntt_pass", st, (double)d->n);
-        if (dit) hipLaunchKernelGGL(k_ntt_pass<true>, dim3(tiles), dim3(256), lds, st, P);
-        else hipLaunchKernelGGL(k_ntt_pass<false>, dim3(tiles), dim3(256), lds, st, P);
+        if (dit) hipLaunchKernelGGL((k_ntt_pass<F, true>), dim3(tiles), dim3(256), lds, st, P);
+        else hipLaunchKernelGGL((k_ntt_pass<F, false>), dim3(tiles), dim3(256), lds, st, P);
         GG_HIP(hipGetLastError());
         prof.stop(st);
         src = out;
@@ -313,45 +339,46 @@ void run_transform(gg_domain* d, const Fr* in, Fr* out, bool dit, bool inverse_t
 
 }  // namespace gg
 
-extern "C" int gg_domain_create(int log_n, const void* omega_mont, const void* coset_gen_mont,
-                                gg_domain_t* out) {
-    GG_CAPI_BEGIN
-    GG_CHECK(out && omega_mont && coset_gen_mont, GG_ERR_INVALID_ARG, "null argument");
-    GG_CHECK(log_n >= 0 && log_n <= 28, GG_ERR_INVALID_ARG, "log_n out of range [0, 28]");
-    auto d = new gg_domain();
-    std::unique_ptr<gg_domain> guard(d);
+namespace gg {
+template <class C>
+static DomainT<C>* domain_build(int log_n, const void* omega_mont, const void* coset_gen_mont) {
+    using F = Fe<C>;
+    std::unique_ptr<DomainT<C>> d(new DomainT<C>());
     d->log_n = log_n;
     d->n = (size_t)1 << log_n;
     memcpy(d->omega.v, omega_mont, 32);
     memcpy(d->g.v, coset_gen_mont, 32);
     // omega must have order exactly n
-    Fr x = d->omega;
+    F x = d->omega;
     for (int i = 0; i < log_n; i++) {
-        if (i == log_n - 1) GG_CHECK(!(x == Fr::one()), GG_ERR_INVALID_ARG, "omega order < n");
+        if (i == log_n - 1) GG_CHECK(!(x == F::one()), GG_ERR_INVALID_ARG, "omega order < n");
         x = sqr(x);
     }
-    GG_CHECK(x == Fr::one(), GG_ERR_INVALID_ARG, "omega^n != 1");
+    GG_CHECK(x == F::one(), GG_ERR_INVALID_ARG, "omega^n != 1");
     GG_CHECK(!d->g.is_zero(), GG_ERR_INVALID_ARG, "coset generator is zero");
     d->omega_inv = inverse(d->omega);
     d->g_inv = inverse(d->g);
-    Fr nn = to_mont(Fr{{(uint32_t)d->n, (uint32_t)((uint64_t)d->n >> 32), 0, 0, 0, 0, 0, 0}});
+    F nn = F::zero();
+    nn.v[0] = (uint32_t)d->n;
+    nn.v[1] = (uint32_t)((uint64_t)d->n >> 32);
+    nn = to_mont(nn);
     d->n_inv = inverse(nn);
-    Fr gn = pow_u64(d->g, d->n);
-    Fr t = gn - Fr::one();
+    F gn = pow_u64(d->g, d->n);
+    F t = gn - F::one();
     GG_CHECK(!t.is_zero(), GG_ERR_INVALID_ARG, "g^n == 1: coset generator in the domain");
     d->den = inverse(t);
 
     const int L = log_n;
     d->S = (L + 1) / 2;
     const int S = d->S;
-    std::vector<Fr> hi, lo;
-    struct KindDef { Fr x, c; int br; };
+    std::vector<F> hi, lo;
+    struct KindDef { F x, c; int br; };
     KindDef defs[SK_COUNT] = {
-        {d->g, Fr::one(), 0},
-        {d->g, Fr::one(), 1},
+        {d->g, F::one(), 0},
+        {d->g, F::one(), 1},
         {d->g_inv, d->n_inv, 0},
         {d->g_inv, d->n_inv, 1},
-        {Fr::one(), d->n_inv, 0},
+        {F::one(), d->n_inv, 0},
         {d->g, d->n_inv, 1},
         {d->g_inv, d->den * d->n_inv, 1},
     };
@@ -359,8 +386,8 @@ extern "C" int gg_domain_create(int log_n, const void* omega_mont, const void* c
         build_pow_tables(L, S, defs[kd].x, defs[kd].c, hi, lo);
         upload(d->scale_hi[kd], hi);
         upload(d->scale_lo[kd], lo);
-        d->spec[kd] = ScaleSpec{(const Fr*)d->scale_hi[kd].p, (const Fr*)d->scale_lo[kd].p, S,
-                                defs[kd].br};
+        d->spec[kd] = ScaleSpec<F>{(const F*)d->scale_hi[kd].p, (const F*)d->scale_lo[kd].p, S,
+                                   defs[kd].br};
     }
     // per-stage twiddles (n - 1 entries each for w and w^-1), generated on device
     size_t cnt = d->n - 1;
@@ -369,17 +396,53 @@ extern "C" int gg_domain_create(int log_n, const void* omega_mont, const void* c
     if (cnt) {
         for (int inv = 0; inv < 2; inv++) {
             DevBuf h1, l1;
-            build_pow_tables(L, S, inv ? d->omega_inv : d->omega, Fr::one(), hi, lo);
+            build_pow_tables(L, S, inv ? d->omega_inv : d->omega, F::one(), hi, lo);
             upload(h1, hi);
             upload(l1, lo);
-            hipLaunchKernelGGL(k_stage_twiddles, dim3(grid_for(cnt, 256)), dim3(256), 0, 0,
-                               (inv ? d->twinv : d->tw).as<Fr>(), cnt, L, h1.as<Fr>(), l1.as<Fr>(), S);
+            hipLaunchKernelGGL(k_stage_twiddles<F>, dim3(grid_for(cnt, 256)), dim3(256), 0, 0,
+                               (inv ? d->twinv : d->tw).template as<F>(), cnt, L, h1.as<F>(), l1.as<F>(), S);
             GG_HIP(hipGetLastError());
             GG_HIP(hipDeviceSynchronize());
         }
     }
-    *out = guard.release();
+    return d.release();
+}
+
+template <class C>
+static void ntt_apply(DomainT<C>* d, void* data_dev, int inverse, bool dit, int coset, hipStream_t st) {
+    Fe<C>* a = (Fe<C>*)data_dev;
+    int pre = -1, post = -1;
+    if (!inverse) {
+        if (coset) pre = dit ? SK_G_BR : SK_G_NAT;
+    } else {
+        if (!coset) post = SK_NINV;
+        else post = dit ? SK_GINV_NAT_N : SK_GINV_BR_N;
+    }
+    run_transform(d, a, a, dit, inverse != 0, pre, post, (const Fe<C>*)nullptr, (const Fe<C>*)nullptr, st);
+}
+}  // namespace gg
+
+extern "C" int gg_domain_create_ex(int curve, int log_n, const void* omega_mont,
+                                   const void* coset_gen_mont, gg_domain_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out && omega_mont && coset_gen_mont, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(curve == GG_CURVE_BN254 || curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "bad curve");
+    // 2-adicity: BN254 fr 28, BLS12-381 fr 32 (table indices are u32 here)
+    GG_CHECK(log_n >= 0 && log_n <= (curve == GG_CURVE_BN254 ? 28 : 30), GG_ERR_INVALID_ARG,
+             "log_n out of range");
+    std::unique_ptr<gg_domain> d(new gg_domain());
+    d->curve = curve;
+    d->log_n = log_n;
+    d->n = (size_t)1 << log_n;
+    if (curve == GG_CURVE_BN254) d->bn.reset(domain_build<FrCfg>(log_n, omega_mont, coset_gen_mont));
+    else d->bls.reset(domain_build<FrBlsCfg>(log_n, omega_mont, coset_gen_mont));
+    *out = d.release();
     GG_CAPI_END
+}
+
+extern "C" int gg_domain_create(int log_n, const void* omega_mont, const void* coset_gen_mont,
+                                gg_domain_t* out) {
+    return gg_domain_create_ex(GG_CURVE_BN254, log_n, omega_mont, coset_gen_mont, out);
 }
 
 extern "C" int gg_domain_release(gg_domain_t d) {
@@ -402,32 +465,28 @@ extern "C" int gg_ntt(gg_domain_t d, void* data_dev, int inverse, int decimation
     GG_CHECK(decimation == GG_DIF || decimation == GG_DIT, GG_ERR_INVALID_ARG, "bad decimation");
     hipStream_t st = pick_stream(hip_stream);
     bool dit = decimation == GG_DIT;
-    Fr* a = (Fr*)data_dev;
-    int pre = -1, post = -1;
-    if (!inverse) {
-        if (coset) pre = dit ? SK_G_BR : SK_G_NAT;
-    } else {
-        if (!coset) post = SK_NINV;
-        else post = dit ? SK_GINV_NAT_N : SK_GINV_BR_N;
-    }
-    run_transform(d, a, a, dit, inverse != 0, pre, post, nullptr, nullptr, st);
+    if (d->curve == GG_CURVE_BN254) ntt_apply(d->bn.get(), data_dev, inverse, dit, coset, st);
+    else ntt_apply(d->bls.get(), data_dev, inverse, dit, coset, st);
     GG_CAPI_END
 }
 
 namespace gg {
 // computeH on device buffers A (becomes h), B, C, each 2^L fr (already padded)
-void compute_h_device(gg_domain* d, Fr* A, Fr* B, Fr* C, Fr* H, hipStream_t st) {
+void compute_h_device(gg_domain* dom, Fr* A, Fr* B, Fr* C, Fr* H, hipStream_t st) {
+    GG_CHECK(dom->curve == GG_CURVE_BN254, GG_ERR_INVALID_ARG, "computeH needs a BN254 domain");
+    DomainT<FrCfg>* d = dom->bn.get();
+    const Fr* nul = nullptr;
     // a, b: iFFT(DIF) with g^br(i)/n folded in, then DIT FFT -> coset evaluations
-    run_transform(d, A, A, false, true, -1, SK_H_FWD, nullptr, nullptr, st);
-    run_transform(d, A, A, true, false, -1, -1, nullptr, nullptr, st);
-    run_transform(d, B, B, false, true, -1, SK_H_FWD, nullptr, nullptr, st);
-    run_transform(d, B, B, true, false, -1, -1, nullptr, nullptr, st);
-    run_transform(d, C, C, false, true, -1, SK_H_FWD, nullptr, nullptr, st);
+    run_transform(d, A, A, false, true, -1, SK_H_FWD, nul, nul, st);
+    run_transform(d, A, A, true, false, -1, -1, nul, nul, st);
+    run_transform(d, B, B, false, true, -1, SK_H_FWD, nul, nul, st);
+    run_transform(d, B, B, true, false, -1, -1, nul, nul, st);
+    run_transform(d, C, C, false, true, -1, SK_H_FWD, nul, nul, st);
     // last pass of c's coset FFT emits a*b - c in place (PolyOps fused)
     run_transform(d, C, C, true, false, -1, -1, A, B, st);
     // coset iFFT (DIF) with den * g^-br(i) / n folded in -> h bit-reversed.
     // H may alias A, B or C.
-    run_transform(d, C, H, false, true, -1, SK_H_INV, nullptr, nullptr, st);
+    run_transform(d, C, H, false, true, -1, SK_H_INV, nul, nul, st);
 }
 }  // namespace gg
 

@@ -12,7 +12,8 @@ _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GNARK_AMD_LIB", os.path.join(_PKG_DIR, "lib", "libgnark_amd.so"))
 
 GG_OK = 0
-GG_G1, GG_G2 = 1, 2
+GG_G1, GG_G2, GG_BLS12_381_G1 = 1, 2, 3
+GG_CURVE_BN254, GG_CURVE_BLS12_381 = 0, 1
 GG_DIF, GG_DIT = 0, 1
 
 
@@ -41,6 +42,7 @@ def _load():
         "gg_copy_to_host": ([P, P, S], I),
         "gg_synchronize": ([], I),
         "gg_domain_create": ([I, P, P, PP], I),
+        "gg_domain_create_ex": ([I, I, P, P, PP], I),
         "gg_domain_release": ([P], I),
         "gg_domain_log_n": ([P, ctypes.POINTER(I)], I),
         "gg_ntt": ([P, P, I, I, I, P], I),
@@ -55,6 +57,8 @@ def _load():
         "gg_g2_jac_add": ([P, P, P], I),
         "gg_g1_scalar_mul": ([P, P, P], I),
         "gg_g2_scalar_mul": ([P, P, P], I),
+        "gg_bls12_381_g1_jac_to_affine": ([P, P], I),
+        "gg_bls12_381_g1_jac_add": ([P, P, P], I),
         "gg_groth16_pk_create": ([I, P, P, P, S, P, S, P, S, P, S, P, P, P, P, P, P, P, P, S, S, P, PP], I),
         "gg_groth16_pk_release": ([P], I),
         "gg_groth16_prove": ([P, P, S, P, P, P, S, I, P, P, P, P, P, P], I),
@@ -75,6 +79,7 @@ lib = _load()
 EXPORTED = [
     "gg_last_error", "gg_version", "gg_device_count", "gg_set_device", "gg_malloc", "gg_free",
     "gg_copy_to_device", "gg_copy_to_host", "gg_synchronize", "gg_domain_create",
+    "gg_domain_create_ex", "gg_bls12_381_g1_jac_to_affine", "gg_bls12_381_g1_jac_add",
     "gg_domain_release", "gg_domain_log_n", "gg_ntt", "gg_groth16_compute_h",
     "gg_msm_base_create", "gg_msm_base_release", "gg_msm_base_info", "gg_msm",
     "gg_g1_jac_to_affine", "gg_g2_jac_to_affine", "gg_g1_jac_add", "gg_g2_jac_add",

@@ -55,3 +55,35 @@ def g2_raw(aff: bytes) -> bytes:
         return bytes(out)
     x0, x1, y0, y1 = (fp_unmont(aff[i:i + 32]) for i in range(0, 128, 32))
     return b"".join(v.to_bytes(32, "big") for v in (x1, x0, y1, y0))
+
+
+# ---- BLS12-381 (PlonK path): std/math/emulated/emparams/emparams.go:145-171
+BLS_P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+BLS_R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+BLS_FR_MULTIPLICATIVE_GEN = 7  # gnark-crypto bls12-381 fr [ext]
+BLS_FR_TWO_ADICITY = 32
+
+
+def bls_fr_mont(x: int) -> bytes:
+    """bls12-381 fr.Element bytes: Montgomery R = 2^256, [4]uint64 LE."""
+    return (((x % BLS_R) << 256) % BLS_R).to_bytes(32, "little")
+
+
+def bls_fr_unmont(b: bytes) -> int:
+    return int.from_bytes(b[:32], "little") * pow(1 << 256, -1, BLS_R) % BLS_R
+
+
+def bls_fp_mont(x: int) -> bytes:
+    """bls12-381 fp.Element bytes: Montgomery R = 2^384, [6]uint64 LE."""
+    return (((x % BLS_P) << 384) % BLS_P).to_bytes(48, "little")
+
+
+def bls_fp_unmont(b: bytes) -> int:
+    return int.from_bytes(b[:48], "little") * pow(1 << 384, -1, BLS_P) % BLS_P
+
+
+def bls_domain_generator(log_n: int) -> int:
+    """7^((r-1)/2^log_n) -- gnark-crypto's choice for bls12-381 (unpinned by any
+    reference fixture; pass pk.Domain.Generator to mirror a real key)."""
+    assert 0 <= log_n <= BLS_FR_TWO_ADICITY
+    return pow(BLS_FR_MULTIPLICATIVE_GEN, (BLS_R - 1) >> log_n, BLS_R)

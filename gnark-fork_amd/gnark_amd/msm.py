@@ -5,15 +5,19 @@ from __future__ import annotations
 
 import ctypes
 
-from ._lib import GG_G1, GG_G2, check, lib, ptr
+from ._lib import GG_BLS12_381_G1, GG_G1, GG_G2, check, lib, ptr
 
-G1, G2 = GG_G1, GG_G2
-_JAC = {G1: 96, G2: 192}
-_AFF = {G1: 64, G2: 128}
+G1, G2, BLS12_381_G1 = GG_G1, GG_G2, GG_BLS12_381_G1
+_JAC = {G1: 96, G2: 192, BLS12_381_G1: 144}
+_AFF = {G1: 64, G2: 128, BLS12_381_G1: 96}
+_TO_AFF = {G1: "gg_g1_jac_to_affine", G2: "gg_g2_jac_to_affine",
+           BLS12_381_G1: "gg_bls12_381_g1_jac_to_affine"}
+_ADD = {G1: "gg_g1_jac_add", G2: "gg_g2_jac_add", BLS12_381_G1: "gg_bls12_381_g1_jac_add"}
 
 
 class MsmBase:
-    """n affine points (gnark layout) uploaded once, precomputed, kept in HBM."""
+    """n affine points (gnark layout) uploaded once, precomputed, kept in HBM.
+    group: G1 / G2 (BN254) or BLS12_381_G1 (PlonK KZG commitments)."""
 
     def __init__(self, group: int, points, n: int, on_device=False, scalar_index=None,
                  window_bits: int = 0):
@@ -57,15 +61,13 @@ class MsmBase:
 
 def jac_to_affine(group: int, jac: bytes) -> bytes:
     out = bytearray(_AFF[group])
-    fn = lib.gg_g1_jac_to_affine if group == G1 else lib.gg_g2_jac_to_affine
-    check(fn(ptr(jac), ptr(out)))
+    check(getattr(lib, _TO_AFF[group])(ptr(jac), ptr(out)))
     return bytes(out)
 
 
 def jac_add(group: int, a: bytes, b: bytes) -> bytes:
     out = bytearray(_JAC[group])
-    fn = lib.gg_g1_jac_add if group == G1 else lib.gg_g2_jac_add
-    check(fn(ptr(a), ptr(b), ptr(out)))
+    check(getattr(lib, _ADD[group])(ptr(a), ptr(b), ptr(out)))
     return bytes(out)
 
 

@@ -6,7 +6,7 @@ from __future__ import annotations
 import ctypes
 
 from . import fr
-from ._lib import GG_DIF, GG_DIT, DeviceBuffer, check, lib, ptr
+from ._lib import GG_CURVE_BLS12_381, GG_CURVE_BN254, GG_DIF, GG_DIT, DeviceBuffer, check, lib, ptr
 
 DIF, DIT = GG_DIF, GG_DIT
 
@@ -17,13 +17,20 @@ class Domain:
     omega / coset_gen default to gnark-crypto's fft.NewDomain choice; pass
     pk.Domain.Generator / FrMultiplicativeGen (Montgomery bytes) to mirror a key."""
 
-    def __init__(self, log_n: int, omega_mont: bytes = None, coset_gen_mont: bytes = None):
-        if omega_mont is None:
-            omega_mont = fr.fr_mont(fr.domain_generator(log_n))
-        if coset_gen_mont is None:
-            coset_gen_mont = fr.fr_mont(fr.FR_MULTIPLICATIVE_GEN)
+    def __init__(self, log_n: int, omega_mont: bytes = None, coset_gen_mont: bytes = None,
+                 curve: int = GG_CURVE_BN254):
+        if curve == GG_CURVE_BN254:
+            if omega_mont is None:
+                omega_mont = fr.fr_mont(fr.domain_generator(log_n))
+            if coset_gen_mont is None:
+                coset_gen_mont = fr.fr_mont(fr.FR_MULTIPLICATIVE_GEN)
+        elif omega_mont is None or coset_gen_mont is None:
+            # BLS12-381: take Generator / FrMultiplicativeGen from pk.Domain
+            raise ValueError("BLS12-381 domains need omega and the coset generator (pk.Domain)")
         h = ctypes.c_void_p()
-        check(lib.gg_domain_create(log_n, ptr(omega_mont), ptr(coset_gen_mont), ctypes.byref(h)))
+        check(lib.gg_domain_create_ex(curve, log_n, ptr(omega_mont), ptr(coset_gen_mont),
+                                      ctypes.byref(h)))
+        self.curve = curve
         self.handle = h
         self.log_n = log_n
         self.cardinality = 1 << log_n

@@ -38,6 +38,13 @@ extern "C" {
 
 #define GG_G1 1
 #define GG_G2 2
+/* BLS12-381 G1 (PlonK KZG commitments): affine 96 B (12-limb fp, R = 2^384),
+ * Jacobian 144 B, scalars BLS12-381 fr (32 B Montgomery) */
+#define GG_BLS12_381_G1 3
+
+/* curves of a domain (scalar field of the NTT) */
+#define GG_CURVE_BN254 0
+#define GG_CURVE_BLS12_381 1
 
 /* decimation (gnark-crypto fft.DIF / fft.DIT) */
 #define GG_DIF 0
@@ -71,6 +78,11 @@ int gg_synchronize(void);
  * coset_gen_mont: coset shift g (fr, Montgomery). */
 int gg_domain_create(int log_n, const void *omega_mont, const void *coset_gen_mont,
                      gg_domain_t *out);
+/* Same for a chosen scalar field: GG_CURVE_BN254 (= gg_domain_create) or
+ * GG_CURVE_BLS12_381 -- the PlonK prover's pk.Domain[0] / Domain[1] FFTs
+ * (backend/plonk/bls12-381/prove.go:995-1061, 1223-1276; fr 32 B Montgomery). */
+int gg_domain_create_ex(int curve, int log_n, const void *omega_mont, const void *coset_gen_mont,
+                        gg_domain_t *out);
 int gg_domain_release(gg_domain_t d);
 int gg_domain_log_n(gg_domain_t d, int *log_n);
 
@@ -97,7 +109,9 @@ int gg_groth16_compute_h(gg_domain_t d, const void *a, const void *b, const void
  * (icicle.go:88-126).  Points stay resident in HBM together with the
  * window-shifted copies 2^(c*w) * P_i that the bucket MSM uses, so every
  * window shares one bucket set (fixed-base precomputation sized for 288 GB).
- * group: GG_G1 or GG_G2.  points: n affine points (host or device memory).
+ * group: GG_G1 or GG_G2 (BN254), GG_BLS12_381_G1 (PlonK KZG commitments:
+ *   kzg.Commit / MultiExp at backend/plonk/bls12-381/prove.go:336, 494, 769,
+ *   1165-1169, 1203-1213).  points: n affine points (host or device memory).
  * Infinity points are dropped at upload (fixes the index shift of
  * icicle.go:343-347).
  * scalar_index (nullable, host): scalar of point i is scalars[scalar_index[i]]
@@ -127,11 +141,15 @@ int gg_g2_jac_add(const void *a_jac, const void *b_jac, void *out_jac);
 /* out = k * p, k fr Montgomery, p affine */
 int gg_g1_scalar_mul(const void *p_aff, const void *k_mont, void *out_jac);
 int gg_g2_scalar_mul(const void *p_aff, const void *k_mont, void *out_jac);
+/* BLS12-381 G1 (curve.G1Jac.FromJacobian / AddAssign of gnark-crypto bls12-381) */
+int gg_bls12_381_g1_jac_to_affine(const void *jac, void *aff);
+int gg_bls12_381_g1_jac_add(const void *a_jac, const void *b_jac, void *out_jac);
 
 /* Fixed-base batch scalar multiplication out[i] = k_i * base (affine,
  * infinity for k_i = 0): replaces curve.BatchScalarMultiplicationG1/G2
  * (setup.go:240-251, 306-318; prove.go:192).  Used to build proving keys on
- * the GPU.  scalars: n fr Montgomery; out: n affine points. */
+ * the GPU.  group: GG_G1, GG_G2 or GG_BLS12_381_G1 (scalars of that curve's
+ * fr).  scalars: n fr Montgomery; out: n affine points. */
 int gg_batch_scalar_mul(int group, const void *base_aff, const void *scalars, size_t n,
                         int scalars_on_device, void *out_aff, int out_on_device);
 

@@ -1,0 +1,237 @@
+"""ORACLE -- TEST INFRASTRUCTURE ONLY.
+
+Pure-Python big-integer restatement of the BLS12-381 arithmetic on the PlonK
+hot path of the reference (tumberger/gnark-fork, backend/plonk/bls12-381):
+KZG commitments are G1 MSMs (prove.go:336, 494, 769, 1165-1169, 1203-1213) and
+the quotient work is Fr FFTs on the small/big domains (prove.go:995-1061,
+1223-1276).  Only ``tests/`` may import this module, as the *checker*; the
+product path (``gnark-fork_amd``) never imports it.
+
+Parity pins (tests/test_oracle_bls.py):
+  * p, r: std/math/emulated/emparams/emparams.go:145-171 (hex and decimal);
+  * curve y^2 = x^3 + 4 and the order-r subgroup: every compressed G1 point of
+    the BLS12-381 verifying keys in backend/groth16/bellman_test.go:19-132
+    decompresses onto the curve and satisfies r * P = O.
+The arithmetic of gnark-crypto ecc/bls12-381 (go.mod:8, absent here) is
+restated from its published algorithm: Montgomery form (R = 2^384 for fp,
+2^256 for fr), little-endian u64 limbs; G1 affine {X, Y}, infinity = (0, 0).
+The FFT root of unity (7^((r-1)/n), gnark-crypto's FrMultiplicativeGen = 7) has
+no fixture in the reference: NTT values are "parity unpinned" and the device
+API takes omega / the coset generator from pk.Domain.
+"""
+from __future__ import annotations
+
+P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+B = 4
+FP_BYTES, FR_BYTES = 48, 32
+FP_MONT, FR_MONT = 1 << 384, 1 << 256
+FR_GEN = 7
+FR_TWO_ADICITY = 32
+
+# standard BLS12-381 G1 generator (validated by the pins: on curve, order r)
+G1_GEN = (0x17F1D3A73197D7942695638C4FA9AC0FC3688C4F9774B905A14E3A3F171BAC586C55E83FF97A1AEFFB3AF00ADB22C6BB,
+          0x08B3F481E3AAA0F1A09E30ED741D8AE4FCF5E095D5D00AF600DB18CB2C04B3EDD03CC744A2888AE40CAA232946C5E7E1)
+INF = None
+
+
+# ---------------------------------------------------------------- encodings
+def fp_to_bytes(x: int) -> bytes:
+    return (x % P * FP_MONT % P).to_bytes(FP_BYTES, "little")
+
+
+def fp_from_bytes(b: bytes) -> int:
+    return int.from_bytes(b, "little") * pow(FP_MONT, -1, P) % P
+
+
+def fr_to_bytes(x: int) -> bytes:
+    return (x % R * FR_MONT % R).to_bytes(FR_BYTES, "little")
+
+
+def fr_from_bytes(b: bytes) -> int:
+    return int.from_bytes(b, "little") * pow(FR_MONT, -1, R) % R
+
+
+def fr_vec_to_bytes(v) -> bytes:
+    return b"".join(fr_to_bytes(x) for x in v)
+
+
+def fr_vec_from_bytes(b: bytes):
+    return [fr_from_bytes(b[i:i + FR_BYTES]) for i in range(0, len(b), FR_BYTES)]
+
+
+def g1_to_bytes(p) -> bytes:
+    """gnark bls12381.G1Affine in memory; infinity = (0, 0)."""
+    if p is INF:
+        return bytes(2 * FP_BYTES)
+    return fp_to_bytes(p[0]) + fp_to_bytes(p[1])
+
+
+def g1_from_bytes(b: bytes):
+    if b == bytes(2 * FP_BYTES):
+        return INF
+    return (fp_from_bytes(b[:FP_BYTES]), fp_from_bytes(b[FP_BYTES:]))
+
+
+# ---------------------------------------------------------------- G1 (affine, exact)
+def on_curve(p) -> bool:
+    return p is INF or (p[1] * p[1] - p[0] ** 3 - B) % P == 0
+
+
+def g1_add(p, q):
+    if p is INF:
+        return q
+    if q is INF:
+        return p
+    if p[0] == q[0]:
+        if (p[1] + q[1]) % P == 0:
+            return INF
+        lam = 3 * p[0] * p[0] * pow(2 * p[1], -1, P) % P
+    else:
+        lam = (q[1] - p[1]) * pow(q[0] - p[0], -1, P) % P
+    x = (lam * lam - p[0] - q[0]) % P
+    return (x, (lam * (p[0] - x) - p[1]) % P)
+
+
+def g1_neg(p):
+    return INF if p is INF else (p[0], (-p[1]) % P)
+
+
+def g1_mul(p, k: int):
+    k %= R
+    acc, base = INF, p
+    while k:
+        if k & 1:
+            acc = g1_add(acc, base)
+        base = g1_add(base, base)
+        k >>= 1
+    return acc
+
+
+def g1_mul_raw(p, k: int):
+    """k * p without reducing k mod r (subgroup check)."""
+    acc, base = INF, p
+    while k:
+        if k & 1:
+            acc = g1_add(acc, base)
+        base = g1_add(base, base)
+        k >>= 1
+    return acc
+
+
+def msm_g1(points, scalars):
+    """sum_i s_i P_i (naive; small n)."""
+    acc = INF
+    for p, s in zip(points, scalars):
+        acc = g1_add(acc, g1_mul(p, s))
+    return acc
+
+
+def msm_g1_trapdoor(ks, scalars):
+    """MSM over P_i = k_i G: (sum_i s_i k_i) G -- O(n) field work, any n."""
+    t = 0
+    for k, s in zip(ks, scalars):
+        t = (t + k * s) % R
+    return g1_mul(G1_GEN, t)
+
+
+def g1_decompress_zcash(b: bytes):
+    """Zcash/bellman compressed G1 (48 B big-endian; flags: 0x80 compressed,
+    0x40 infinity, 0x20 y is the larger root)."""
+    assert len(b) == 48 and b[0] & 0x80
+    if b[0] & 0x40:
+        return INF
+    x = int.from_bytes(bytes([b[0] & 0x1F]) + b[1:], "big")
+    y = pow((x ** 3 + B) % P, (P + 1) // 4, P)  # p = 3 mod 4
+    if (y * y - x ** 3 - B) % P:
+        raise ValueError("not on curve")
+    if bool(b[0] & 0x20) != (y > P - y):
+        y = P - y
+    return (x, y)
+
+
+# ---------------------------------------------------------------- FFT (gnark conventions)
+def bitrev(i: int, logn: int) -> int:
+    return int(format(i, f"0{logn}b")[::-1], 2) if logn else 0
+
+
+class Domain:
+    """gnark-crypto fft.NewDomain for bls12-381 fr (omega_n = 7^((r-1)/n); unpinned)."""
+
+    def __init__(self, n: int, omega: int = None, gen: int = FR_GEN):
+        assert n & (n - 1) == 0
+        self.cardinality = n
+        self.log_n = n.bit_length() - 1
+        assert self.log_n <= FR_TWO_ADICITY
+        self.generator = omega if omega is not None else pow(FR_GEN, (R - 1) >> self.log_n, R)
+        self.generator_inv = pow(self.generator, -1, R)
+        self.cardinality_inv = pow(n, -1, R)
+        self.gen = gen
+        self.gen_inv = pow(gen, -1, R)
+
+
+def _dif(a, w):
+    n = len(a)
+    m = n >> 1
+    while m >= 1:
+        wm = pow(w, n // (2 * m), R)
+        for start in range(0, n, 2 * m):
+            t = 1
+            for j in range(m):
+                u, v = a[start + j], a[start + j + m]
+                a[start + j] = (u + v) % R
+                a[start + j + m] = (u - v) * t % R
+                t = t * wm % R
+        m >>= 1
+    return a
+
+
+def _dit(a, w):
+    n = len(a)
+    m = 1
+    while m < n:
+        wm = pow(w, n // (2 * m), R)
+        for start in range(0, n, 2 * m):
+            t = 1
+            for j in range(m):
+                u = a[start + j]
+                v = a[start + j + m] * t % R
+                a[start + j] = (u + v) % R
+                a[start + j + m] = (u - v) % R
+                t = t * wm % R
+        m <<= 1
+    return a
+
+
+DIF, DIT = "DIF", "DIT"
+
+
+def fft(dom: Domain, a, decimation, coset=False):
+    """domain.FFT(a, decimation, [OnCoset()])."""
+    n, logn = dom.cardinality, dom.log_n
+    if coset:
+        for i in range(n):
+            e = bitrev(i, logn) if decimation == DIT else i
+            a[i] = a[i] * pow(dom.gen, e, R) % R
+    return _dif(a, dom.generator) if decimation == DIF else _dit(a, dom.generator)
+
+
+def fft_inverse(dom: Domain, a, decimation, coset=False):
+    """domain.FFTInverse(a, decimation, [OnCoset()])."""
+    n, logn = dom.cardinality, dom.log_n
+    if decimation == DIF:
+        _dif(a, dom.generator_inv)
+    else:
+        _dit(a, dom.generator_inv)
+    for i in range(n):
+        x = a[i] * dom.cardinality_inv % R
+        if coset:
+            e = i if decimation == DIT else bitrev(i, logn)
+            x = x * pow(dom.gen_inv, e, R) % R
+        a[i] = x
+    return a
+
+
+def batch_invert(v):
+    """fr.BatchInvert (prove.go:1273): zeros map to zero."""
+    return [pow(x, -1, R) if x else 0 for x in v]
