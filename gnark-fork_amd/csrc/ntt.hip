@@ -515,3 +515,34 @@ extern "C" int gg_groth16_compute_h(gg_domain_t d, const void* a, const void* b,
     GG_HIP(hipStreamSynchronize(st));
     GG_CAPI_END
 }
+
+namespace gg {
+// helpers for the PlonK kernels (plonk.hip)
+size_t domain_size(gg_domain* d, int* curve) {
+    if (curve) *curve = d->curve;
+    return d->n;
+}
+void bls_ntt_inplace(gg_domain* d, void* data, int inverse, int dit, int coset, hipStream_t st) {
+    GG_CHECK(d->curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "needs a BLS12-381 domain");
+    ntt_apply(d->bls.get(), data, inverse, dit != 0, coset, st);
+}
+// evaluateXnMinusOneDomainBigCoset (backend/plonk/bls12-381/prove.go:1253-1276):
+// res[0] = g^n, res[i] = res[i-1] * w_big^n, res[i] -= 1, then fr.BatchInvert
+void bls_xn_minus_one_inv(gg_domain* big, size_t n_small, void* out) {
+    GG_CHECK(big->curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "needs a BLS12-381 domain");
+    using F = FrBls;
+    const DomainT<FrBlsCfg>* d = big->bls.get();
+    const size_t rho = d->n / n_small;
+    std::vector<F> res(rho);
+    res[0] = pow_u64(d->g, n_small);
+    const F t = pow_u64(d->omega, n_small);
+    for (size_t i = 1; i < rho; i++) res[i] = res[i - 1] * t;
+    for (size_t i = 0; i < rho; i++) {
+        res[i] = res[i] - F::one();
+        GG_CHECK(!res[i].is_zero(), GG_ERR_INVALID_ARG, "x^n - 1 vanishes on the big coset");
+        res[i] = inverse(res[i]);
+    }
+    memcpy(out, res.data(), rho * sizeof(F));
+}
+}  // namespace gg
+

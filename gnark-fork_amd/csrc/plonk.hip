@@ -1,0 +1,220 @@
+// PlonK BLS12-381 quotient-path kernels, BLS12-381 fr
+// (32 B Montgomery, R = 2^256) in gnark-crypto's memory layout.
+//
+//   gg_plonk_numerator_coset  allConstraints of computeNumerator on one coset of
+//                             the big domain + the bit-reversed scatter into cres
+//                             (backend/plonk/bls12-381/prove.go:850-935, 1030-1041)
+//   gg_plonk_divide_by_xn_minus_one
+//                             r[i] *= (x^n - 1)^-1 on the big coset, then the big
+//                             coset iFFT (DIT: bit-reversed in, canonical regular
+//                             out) -- divideByXMinusOne, prove.go:1223-1276
+//   gg_bls12_381_fr_batch_invert
+//                             fr.BatchInvert (prove.go:1273): zeros stay zero
+#include "common.h"
+#include "field.cuh"
+#include "prof.h"
+#include <vector>
+#include <cstring>
+
+struct gg_domain;
+namespace gg {
+void bls_ntt_inplace(gg_domain* d, void* data, int inverse, int dit, int coset, hipStream_t st);
+size_t domain_size(gg_domain* d, int* curve);
+void bls_xn_minus_one_inv(gg_domain* big, size_t n_small, void* out);
+}  // namespace gg
+
+namespace gg {
+
+using FrB = FrBls;
+
+__device__ __forceinline__ FrB ldf(const FrB* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    uint4 a = q[0], b = q[1];
+    FrB r;
+    r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+    r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+    return r;
+}
+__device__ __forceinline__ void stf(FrB* p, const FrB& r) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    q[0] = make_uint4(r.v[0], r.v[1], r.v[2], r.v[3]);
+    q[1] = make_uint4(r.v[4], r.v[5], r.v[6], r.v[7]);
+}
+
+// polynomial order ids of prove.go:60-77 (s.x) and blinding ids :80-86
+enum { ID_L, ID_R, ID_O, ID_Z, ID_ZS, ID_QL, ID_QR, ID_QM, ID_QO, ID_QK, ID_S1, ID_S2, ID_S3,
+       ID_ID, ID_LONE, ID_QCI };
+constexpr int MAX_X = ID_QCI + 2 * 8;  // up to 8 BSB22 commitments
+constexpr int MAX_BCOEF = 4;
+
+struct NumParams {
+    const FrB* x[MAX_X];        // Lagrange-regular evaluations on this coset, length n
+    int nx;
+    FrB bcoef[4][MAX_BCOEF];    // blinding polynomials Bl, Br, Bo, Bz (coset-scaled)
+    int bdeg[4];                // number of coefficients
+    const FrB* tw0;             // s.twiddles0: omega_small^j, j < n
+    FrB beta, gamma, alpha, cs, css;
+    uint32_t n, log_big, rho, coset;
+    FrB* cres;                  // rho * n, bit-reversed big-domain order
+};
+
+__device__ __forceinline__ FrB horner(const FrB* c, int nc, const FrB& x) {
+    FrB r = FrB::zero();
+    for (int k = nc - 1; k >= 0; k--) r = r * x + c[k];
+    return r;
+}
+
+__global__ void __launch_bounds__(256) k_numerator_coset(NumParams P) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= P.n) return;
+    const FrB one = FrB::one();
+    FrB L = ldf(P.x[ID_L] + j), R = ldf(P.x[ID_R] + j), O = ldf(P.x[ID_O] + j);
+    FrB Z = ldf(P.x[ID_Z] + j), ZS = ldf(P.x[ID_ZS] + j);
+    FrB S1 = ldf(P.x[ID_S1] + j) * P.beta, S2 = ldf(P.x[ID_S2] + j) * P.beta,
+        S3 = ldf(P.x[ID_S3] + j) * P.beta;
+    // blinding: bl/br/bo/bz evaluated at twiddles0[j], bz at twiddles0[(j+1) % n] for ZS
+    const FrB t0 = ldf(P.tw0 + j), t1 = ldf(P.tw0 + (j + 1) % P.n);
+    L = L + horner(P.bcoef[0], P.bdeg[0], t0);
+    R = R + horner(P.bcoef[1], P.bdeg[1], t0);
+    O = O + horner(P.bcoef[2], P.bdeg[2], t0);
+    Z = Z + horner(P.bcoef[3], P.bdeg[3], t0);
+    ZS = ZS + horner(P.bcoef[3], P.bdeg[3], t1);
+    // gateConstraint
+    FrB ic = ldf(P.x[ID_QL] + j) * L + ldf(P.x[ID_QR] + j) * R;
+    ic = ic + ldf(P.x[ID_QM] + j) * L * R;
+    ic = ic + ldf(P.x[ID_QO] + j) * O + ldf(P.x[ID_QK] + j);
+    for (int q = ID_QCI; q + 1 < P.nx; q += 2) ic = ic + ldf(P.x[q] + j) * ldf(P.x[q + 1] + j);
+    // orderingConstraint
+    const FrB id = ldf(P.x[ID_ID] + j);
+    FrB a = P.gamma + L + id, b = id * P.cs + R + P.gamma, c = id * P.css + O + P.gamma;
+    FrB r = a * b * c * Z;
+    a = S1 + L + P.gamma;
+    b = S2 + R + P.gamma;
+    c = S3 + O + P.gamma;
+    FrB l = a * b * c * ZS - r;
+    // ratioLocalConstraint
+    FrB rl = (Z - one) * ldf(P.x[ID_LONE] + j);
+    FrB res = (rl * P.alpha + l) * P.alpha + ic;
+    // cres[bitrev(rho*j + coset)] (prove.go:1036-1038)
+    const uint32_t pos = __brev(P.rho * j + P.coset) >> (32 - P.log_big);
+    stf(P.cres + (P.log_big ? pos : 0), res);
+}
+
+__global__ void k_mul_periodic_bitrev(FrB* r, size_t n, int log_n, const FrB* f, uint32_t rho) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t irev = log_n ? (__brev((uint32_t)i) >> (32 - log_n)) : 0u;
+    stf(r + i, ldf(r + i) * ldf(f + (irev % rho)));
+}
+
+// Montgomery batch inversion: thread t owns elements t, t+T, ... (zeros skipped)
+__global__ void __launch_bounds__(256) k_batch_invert(FrB* a, size_t n, size_t T, FrB* prefix) {
+    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T || t >= n) return;
+    FrB acc = FrB::one();
+    for (size_t i = t; i < n; i += T) {
+        stf(prefix + i, acc);
+        FrB x = ldf(a + i);
+        if (!x.is_zero()) acc = acc * x;
+    }
+    FrB inv = inverse(acc);
+    size_t last = t + ((n - 1 - t) / T) * T;
+    for (size_t i = last;; i -= T) {
+        FrB x = ldf(a + i);
+        if (!x.is_zero()) {
+            FrB xi = inv * ldf(prefix + i);
+            inv = inv * x;
+            stf(a + i, xi);
+        }
+        if (i < T) break;
+    }
+}
+
+}  // namespace gg
+
+using namespace gg;
+
+extern "C" int gg_plonk_numerator_coset(const void* const* x_dev, int nx, const void* bcoef,
+                                        const int* bdeg, const void* twiddles0_dev,
+                                        const void* beta, const void* gamma, const void* alpha,
+                                        const void* coset_gen, size_t n, int rho, int coset,
+                                        void* cres_dev, void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(x_dev && bcoef && bdeg && twiddles0_dev && beta && gamma && alpha && coset_gen && cres_dev,
+             GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(nx >= ID_QCI && nx <= MAX_X && (nx - ID_QCI) % 2 == 0, GG_ERR_INVALID_ARG,
+             "nx must be 15 + 2 * (number of BSB22 commitments), <= 8 commitments");
+    GG_CHECK(n >= 1 && (n & (n - 1)) == 0 && n <= (1u << 30), GG_ERR_INVALID_ARG, "n must be a power of 2");
+    GG_CHECK(rho >= 1 && (rho & (rho - 1)) == 0 && coset >= 0 && coset < rho, GG_ERR_INVALID_ARG, "bad rho/coset");
+    NumParams P{};
+    for (int q = 0; q < nx; q++) {
+        GG_CHECK(x_dev[q], GG_ERR_INVALID_ARG, "null polynomial");
+        P.x[q] = (const FrB*)x_dev[q];
+    }
+    P.nx = nx;
+    const uint8_t* bc = (const uint8_t*)bcoef;
+    for (int q = 0; q < 4; q++) {
+        GG_CHECK(bdeg[q] >= 0 && bdeg[q] <= MAX_BCOEF, GG_ERR_INVALID_ARG, "blinding order too large");
+        P.bdeg[q] = bdeg[q];
+        for (int k = 0; k < bdeg[q]; k++) memcpy(P.bcoef[q][k].v, bc + (q * MAX_BCOEF + k) * 32, 32);
+    }
+    P.tw0 = (const FrB*)twiddles0_dev;
+    memcpy(P.beta.v, beta, 32);
+    memcpy(P.gamma.v, gamma, 32);
+    memcpy(P.alpha.v, alpha, 32);
+    memcpy(P.cs.v, coset_gen, 32);
+    P.css = P.cs * P.cs;
+    P.n = (uint32_t)n;
+    P.rho = (uint32_t)rho;
+    P.coset = (uint32_t)coset;
+    int lb = 0;
+    while (((size_t)1 << lb) < n * (size_t)rho) lb++;
+    P.log_big = (uint32_t)lb;
+    P.cres = (FrB*)cres_dev;
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : hipStreamPerThread;
+    ProfScope prof("plonk_numerator", st, (double)n);
+    hipLaunchKernelGGL(k_numerator_coset, dim3(grid_for(n, 256)), dim3(256), 0, st, P);
+    GG_HIP(hipGetLastError());
+    prof.stop(st);
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_divide_by_xn_minus_one(gg_domain_t big, size_t n_small, void* data_dev,
+                                               void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(big && data_dev, GG_ERR_INVALID_ARG, "null argument");
+    int curve = -1;
+    const size_t m = domain_size(big, &curve);
+    GG_CHECK(curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "needs a BLS12-381 domain");
+    GG_CHECK(n_small >= 1 && m % n_small == 0, GG_ERR_INVALID_ARG, "big domain must be a multiple of n");
+    const uint32_t rho = (uint32_t)(m / n_small);
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : hipStreamPerThread;
+    // (x^n - 1)^-1 on the big coset has rho distinct values (prove.go:1253-1276)
+    std::vector<FrB> f(rho);
+    bls_xn_minus_one_inv(big, n_small, f.data());
+    DevBuf df(rho * 32);
+    GG_HIP(hipMemcpyAsync(df.p, f.data(), rho * 32, hipMemcpyHostToDevice, st));
+    int lm = 0;
+    while (((size_t)1 << lm) < m) lm++;
+    hipLaunchKernelGGL(k_mul_periodic_bitrev, dim3(grid_for(m, 256)), dim3(256), 0, st, (FrB*)data_dev, m,
+                       lm, df.as<FrB>(), rho);
+    GG_HIP(hipGetLastError());
+    // LagrangeCoset/BitReverse -> Canonical/Regular: FFTInverse(DIT, OnCoset)
+    bls_ntt_inplace(big, data_dev, 1, 1, 1, st);
+    GG_HIP(hipStreamSynchronize(st));  // df lifetime
+    GG_CAPI_END
+}
+
+extern "C" int gg_bls12_381_fr_batch_invert(void* data_dev, size_t n, void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(data_dev || n == 0, GG_ERR_INVALID_ARG, "null argument");
+    if (n == 0) return GG_OK;
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : hipStreamPerThread;
+    const size_t T = std::min<size_t>(n, std::max<size_t>(16384, n / 64));
+    DevBuf prefix(n * 32);
+    hipLaunchKernelGGL(k_batch_invert, dim3(grid_for(T, 256)), dim3(256), 0, st, (FrB*)data_dev, n, T,
+                       prefix.as<FrB>());
+    GG_HIP(hipGetLastError());
+    GG_HIP(hipStreamSynchronize(st));
+    GG_CAPI_END
+}

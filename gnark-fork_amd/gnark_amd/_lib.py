@@ -64,6 +64,10 @@ def _load():
         "gg_groth16_prove": ([P, P, S, P, P, P, S, I, P, P, P, P, P, P], I),
         "gg_groth16_last_timings": ([ctypes.POINTER(ctypes.c_double)], I),
         "gg_batch_scalar_mul": ([I, P, P, S, I, P, I], I),
+        "gg_plonk_numerator_coset": ([ctypes.POINTER(ctypes.c_void_p), I, P, ctypes.POINTER(I), P,
+                                      P, P, P, P, S, I, I, P, P], I),
+        "gg_plonk_divide_by_xn_minus_one": ([P, S, P, P], I),
+        "gg_bls12_381_fr_batch_invert": ([P, S, P], I),
         "gg_profile_enable": ([I], I),
         "gg_profile_get": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)], I),
@@ -85,6 +89,7 @@ EXPORTED = [
     "gg_g1_jac_to_affine", "gg_g2_jac_to_affine", "gg_g1_jac_add", "gg_g2_jac_add",
     "gg_g1_scalar_mul", "gg_g2_scalar_mul", "gg_groth16_pk_create", "gg_groth16_pk_release",
     "gg_groth16_prove", "gg_groth16_last_timings", "gg_batch_scalar_mul", "gg_profile_enable",
+    "gg_plonk_numerator_coset", "gg_plonk_divide_by_xn_minus_one", "gg_bls12_381_fr_batch_invert",
     "gg_profile_get",
 ]
 

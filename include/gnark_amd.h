@@ -190,6 +190,33 @@ int gg_groth16_prove(gg_groth16_pk_t pk, const void *wires, size_t n_wires, cons
 int gg_groth16_last_timings(double *ms9);
 
 
+/* ------------------------------------------------ PlonK BLS12-381 (fr, 32 B)
+ * Quotient-path kernels of backend/plonk/bls12-381/prove.go; all buffers are
+ * device memory, bls12-381 fr Montgomery.
+ *
+ * allConstraints of computeNumerator (prove.go:850-935) on coset `coset` of
+ * the big domain, written bit-reversed into cres (prove.go:1030-1041):
+ *   x_dev[nx]: host array of device pointers, the s.x polynomials in id_ order
+ *     (L, R, O, Z, ZS, Ql, Qr, Qm, Qo, Qk, S1, S2, S3, ID, LOne, Qc_i, Pi_i...;
+ *     prove.go:60-77), each n evaluations (Lagrange, regular) on this coset;
+ *   bcoef: 4 x 4 fr (host), the blinding polynomials Bl, Br, Bo, Bz already
+ *     scaled for this coset as prove.go:1003-1011 does; bdeg[4]: their lengths;
+ *   twiddles0_dev: s.twiddles0 (omega_small^j, j < n; prove.go:265-277);
+ *   beta, gamma, alpha, coset_gen (= pk.Domain[1].FrMultiplicativeGen): host fr;
+ *   rho = |Domain[1]| / n; cres_dev: rho * n fr. */
+int gg_plonk_numerator_coset(const void *const *x_dev, int nx, const void *bcoef, const int *bdeg,
+                             const void *twiddles0_dev, const void *beta, const void *gamma,
+                             const void *alpha, const void *coset_gen, size_t n, int rho, int coset,
+                             void *cres_dev, void *hip_stream);
+/* divideByXMinusOne (prove.go:1223-1276) in place on a LagrangeCoset/BitReverse
+ * vector of |big| elements: multiply by (x^n - 1)^-1 on the big coset, then the
+ * big coset iFFT (DIT) -> canonical regular.  big: a GG_CURVE_BLS12_381 domain
+ * (pk.Domain[1]); n_small = |pk.Domain[0]|. */
+int gg_plonk_divide_by_xn_minus_one(gg_domain_t big, size_t n_small, void *data_dev,
+                                    void *hip_stream);
+/* fr.BatchInvert in place (prove.go:1273; zeros stay zero) */
+int gg_bls12_381_fr_batch_invert(void *data_dev, size_t n, void *hip_stream);
+
 /* ------------------------------------------------------------ profiling
  * Kernel-level timing with HIP events recorded on the stream each kernel is
  * launched on (bench.py uses it for the roofline of the dominant kernel).

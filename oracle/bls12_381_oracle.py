@@ -235,3 +235,71 @@ def fft_inverse(dom: Domain, a, decimation, coset=False):
 def batch_invert(v):
     """fr.BatchInvert (prove.go:1273): zeros map to zero."""
     return [pow(x, -1, R) if x else 0 for x in v]
+
+
+# ---------------------------------------------------------------- PlonK quotient path
+# s.x ids (backend/plonk/bls12-381/prove.go:60-77)
+ID_L, ID_R, ID_O, ID_Z, ID_ZS, ID_QL, ID_QR, ID_QM, ID_QO, ID_QK, ID_S1, ID_S2, ID_S3, \
+    ID_ID, ID_LONE, ID_QCI = range(16)
+
+
+def _horner(coeffs, x):
+    r = 0
+    for c in reversed(coeffs):
+        r = (r * x + c) % R
+    return r
+
+
+def numerator_coset(x, bcoef, tw0, beta, gamma, alpha, cs, n, rho, coset, cres):
+    """allConstraints (prove.go:912-934, with gateConstraint :852-868,
+    orderingConstraint :874-892, ratioLocalConstraint :894-902) at every point j
+    of one coset, scattered to cres[bitrev(rho*j + coset)] (prove.go:1030-1041)."""
+    css = cs * cs % R
+    nb_bsb = (len(x) - ID_QCI + 1) >> 1
+    lb = (rho * n).bit_length() - 1
+    for j in range(n):
+        u = [p[j] for p in x]
+        u[ID_S1] = u[ID_S1] * beta % R
+        u[ID_S2] = u[ID_S2] * beta % R
+        u[ID_S3] = u[ID_S3] * beta % R
+        u[ID_L] = (u[ID_L] + _horner(bcoef[0], tw0[j])) % R
+        u[ID_R] = (u[ID_R] + _horner(bcoef[1], tw0[j])) % R
+        u[ID_O] = (u[ID_O] + _horner(bcoef[2], tw0[j])) % R
+        u[ID_Z] = (u[ID_Z] + _horner(bcoef[3], tw0[j])) % R
+        u[ID_ZS] = (u[ID_ZS] + _horner(bcoef[3], tw0[(j + 1) % n])) % R
+        ic = (u[ID_QL] * u[ID_L] + u[ID_QR] * u[ID_R] + u[ID_QM] * u[ID_L] * u[ID_R]
+              + u[ID_QO] * u[ID_O] + u[ID_QK]) % R
+        for i in range(nb_bsb):
+            ic = (ic + u[ID_QCI + 2 * i] * u[ID_QCI + 2 * i + 1]) % R
+        a = (gamma + u[ID_L] + u[ID_ID]) % R
+        b = (u[ID_ID] * cs + u[ID_R] + gamma) % R
+        c = (u[ID_ID] * css + u[ID_O] + gamma) % R
+        r = a * b * c * u[ID_Z] % R
+        a = (u[ID_S1] + u[ID_L] + gamma) % R
+        b = (u[ID_S2] + u[ID_R] + gamma) % R
+        c = (u[ID_S3] + u[ID_O] + gamma) % R
+        l = (a * b * c * u[ID_ZS] - r) % R
+        rl = (u[ID_Z] - 1) * u[ID_LONE] % R
+        res = ((rl * alpha + l) * alpha + ic) % R
+        cres[bitrev(rho * j + coset, lb)] = res
+    return cres
+
+
+def xn_minus_one_inv_big_coset(n_small, big: Domain):
+    """evaluateXnMinusOneDomainBigCoset (prove.go:1253-1276)."""
+    rho = big.cardinality // n_small
+    res = [pow(big.gen, n_small, R)]
+    t = pow(big.generator, n_small, R)
+    for _ in range(1, rho):
+        res.append(res[-1] * t % R)
+    return batch_invert([(v - 1) % R for v in res])
+
+
+def divide_by_xn_minus_one(a, n_small, big: Domain):
+    """divideByXMinusOne (prove.go:1223-1250): a is LagrangeCoset / BitReverse;
+    result Canonical / Regular (FFTInverse DIT on the coset)."""
+    f = xn_minus_one_inv_big_coset(n_small, big)
+    rho = len(f)
+    lb = big.log_n
+    a = [v * f[bitrev(i, lb) % rho] % R for i, v in enumerate(a)]
+    return fft_inverse(big, a, DIT, coset=True)

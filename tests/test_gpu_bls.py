@@ -117,3 +117,65 @@ def test_bls_ntt_roundtrip_large(log_n):
         d.fft(buf, ntt.DIF, coset)
         d.fft_inverse(buf, ntt.DIT, coset)
         assert buf.to_host() == x
+
+
+# ---------------------------------------------------------------- PlonK quotient kernels
+def _rand_fr(rng, k):
+    return [rng.randrange(b.R) for _ in range(k)]
+
+
+@pytest.mark.parametrize("log_n,rho,nb_bsb", [(0, 4, 0), (3, 4, 1), (10, 4, 2), (8, 2, 0)])
+def test_plonk_numerator_coset(log_n, rho, nb_bsb):
+    from gnark_amd import plonk, DeviceBuffer
+    rng = random.Random(log_n * 7 + rho + nb_bsb)
+    n = 1 << log_n
+    nx = 15 + 2 * nb_bsb
+    xs = [_rand_fr(rng, n) for _ in range(nx)]
+    bco = [_rand_fr(rng, 2), _rand_fr(rng, 2), _rand_fr(rng, 2), _rand_fr(rng, 3)]
+    w = pow(b.FR_GEN, (b.R - 1) >> log_n, b.R)
+    tw0 = [pow(w, j, b.R) for j in range(n)]
+    beta, gamma, alpha = _rand_fr(rng, 3)
+    cs = b.FR_GEN
+    xb = [DeviceBuffer.from_host(b.fr_vec_to_bytes(v)) for v in xs]
+    twb = DeviceBuffer.from_host(b.fr_vec_to_bytes(tw0))
+    cres = DeviceBuffer(rho * n * 32)
+    exp = [0] * (rho * n)
+    got = None
+    for coset in range(rho):
+        plonk.numerator_coset(xb, [[b.fr_to_bytes(c) for c in q] for q in bco], twb,
+                              b.fr_to_bytes(beta), b.fr_to_bytes(gamma), b.fr_to_bytes(alpha),
+                              b.fr_to_bytes(cs), n, rho, coset, cres)
+        b.numerator_coset(xs, bco, tw0, beta, gamma, alpha, cs, n, rho, coset, exp)
+    got = b.fr_vec_from_bytes(cres.to_host())
+    assert got == exp
+
+
+@pytest.mark.parametrize("log_n,rho", [(2, 4), (6, 4), (9, 2)])
+def test_plonk_divide_by_xn_minus_one(log_n, rho):
+    from gnark_amd import fr, ntt, plonk, DeviceBuffer
+    rng = random.Random(log_n + 100 * rho)
+    n = 1 << log_n
+    lb = (n * rho).bit_length() - 1
+    wb = fr.bls_domain_generator(lb)
+    big = ntt.Domain(lb, fr.bls_fr_mont(wb), fr.bls_fr_mont(fr.BLS_FR_MULTIPLICATIVE_GEN),
+                     curve=ntt.GG_CURVE_BLS12_381)
+    a = _rand_fr(rng, n * rho)
+    buf = DeviceBuffer.from_host(b.fr_vec_to_bytes(a))
+    plonk.divide_by_xn_minus_one(big, n, buf)
+    exp = b.divide_by_xn_minus_one(list(a), n, b.Domain(n * rho, wb))
+    assert b.fr_vec_from_bytes(buf.to_host()) == exp
+
+
+@pytest.mark.parametrize("n", [1, 5, 1000, 1 << 17])
+def test_bls_batch_invert(n):
+    from gnark_amd import plonk, DeviceBuffer
+    rng = random.Random(n)
+    a = [rng.randrange(b.R) if rng.random() > 0.05 else 0 for _ in range(n)]
+    buf = DeviceBuffer.from_host(b.fr_vec_to_bytes(a))
+    plonk.batch_invert(buf, n)
+    got = b.fr_vec_from_bytes(buf.to_host())
+    if n <= 1000:
+        assert got == b.batch_invert(a)
+    else:  # x * x^-1 == 1 (and zeros stay zero), checked on a sample
+        for i in rng.sample(range(n), 2000):
+            assert (a[i] * got[i] % b.R) == (1 if a[i] else 0)
