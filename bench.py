@@ -64,6 +64,8 @@ def main():
                     help="domain size of the extra Groth16 prove measurement (0 = skip)")
     ap.add_argument("--ntt-log-n", type=int, default=24,
                     help="size of the extra Fr NTT measurement, BASELINE configs[2] (0 = skip)")
+    ap.add_argument("--plonk-log-n", type=int, default=22,
+                    help="BLS12-381 PlonK hot-op measurement size, BASELINE configs[4] (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     args = ap.parse_args()
@@ -182,6 +184,13 @@ def main():
         except Exception as e:  # report, never hide
             out["ntt"] = {"error": repr(e)}
 
+    # ---- PlonK BLS12-381 hot ops (BASELINE configs[4] sizes; extra, rank 0 / N = 1 only)
+    if rank == 0 and world == 1 and args.plonk_log_n:
+        try:
+            out["plonk_bls12_381"] = plonk_bench(args.plonk_log_n)
+        except Exception as e:  # report, never hide
+            out["plonk_bls12_381"] = {"error": repr(e)}
+
     # ---- Groth16 prove (extra, rank 0 / N = 1 only)
     if rank == 0 and world == 1 and args.groth16_log_n:
         try:
@@ -286,6 +295,63 @@ def ntt_bench(log_n, reps=10):
             "pass_kernel_avg_ms": tot / cnt if cnt else None,
             "passes_per_transform": passes_per_transform,
             "pass_GBps": (alg / (tot / cnt * 1e-3) / 1e9) if cnt else None}
+
+
+BLS_G1_GEN = (0x17F1D3A73197D7942695638C4FA9AC0FC3688C4F9774B905A14E3A3F171BAC586C55E83FF97A1AEFFB3AF00ADB22C6BB,
+              0x08B3F481E3AAA0F1A09E30ED741D8AE4FCF5E095D5D00AF600DB18CB2C04B3EDD03CC744A2888AE40CAA232946C5E7E1)
+
+
+def plonk_bench(log_n, reps=5):
+    """BLS12-381 PlonK hot ops at n = 2^log_n (small domain), big domain 4n:
+    a KZG-commit-sized G1 MSM (2^log_n resident points), small/big domain Fr
+    FFTs, one coset of the fused numerator, divideByXMinusOne on the big domain."""
+    from gnark_amd import _lib, fr, msm, ntt, plonk, DeviceBuffer
+    n = 1 << log_n
+    res = {"log_n": log_n, "big_log_n": log_n + 2}
+
+    def timed(fn, k=reps):
+        fn()
+        _lib.check(_lib.lib.gg_synchronize())
+        t = time.perf_counter()
+        for _ in range(k):
+            fn()
+        _lib.check(_lib.lib.gg_synchronize())
+        return 1e3 * (time.perf_counter() - t) / k
+
+    def bls_scalars(k, seed):
+        a = rand_scalars(k, seed)
+        a[:, 3] &= np.uint64((1 << 60) - 1)  # < r_bls
+        return np.ascontiguousarray(a)
+
+    import numpy as np
+    gen = fr.bls_fp_mont(BLS_G1_GEN[0]) + fr.bls_fp_mont(BLS_G1_GEN[1])
+    pts = DeviceBuffer(96 * n)
+    msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bls_scalars(n, 31), n, out=pts)
+    base = msm.MsmBase(msm.BLS12_381_G1, pts.ptr, n, on_device=True)
+    del pts
+    npts, c, W = base.info()
+    dsc = DeviceBuffer.from_host(bls_scalars(n, 32).tobytes())
+    ms = timed(lambda: base.msm_jac(dsc, n, on_device=True))
+    res["msm_g1"] = {"ms": ms, "Mscalar_mul_per_s": n / (ms * 1e-3) / 1e6, "window_bits": c, "windows": W}
+    base.close()
+    for lg, key in ((log_n, "ntt_small"), (log_n + 2, "ntt_big")):
+        d = ntt.Domain(lg, fr.bls_fr_mont(fr.bls_domain_generator(lg)),
+                       fr.bls_fr_mont(fr.BLS_FR_MULTIPLICATIVE_GEN), curve=ntt.GG_CURVE_BLS12_381)
+        buf = DeviceBuffer.from_host(bls_scalars(1 << lg, 40 + lg).tobytes())
+        ms = timed(lambda: (d.fft(buf, ntt.DIF, True), d.fft_inverse(buf, ntt.DIT, True)))
+        res[key] = {"ms_per_transform": ms / 2}
+        if key == "ntt_big":
+            res["divide_by_xn_minus_one_ms"] = timed(lambda: plonk.divide_by_xn_minus_one(d, n, buf))
+        d.close()
+    # one coset of the numerator: 15 polynomials + 1 BSB22 pair
+    xs = [DeviceBuffer.from_host(bls_scalars(n, 50 + i).tobytes()) for i in range(17)]
+    tw0 = DeviceBuffer.from_host(bls_scalars(n, 70).tobytes())
+    cres = DeviceBuffer(4 * n * 32)
+    one = fr.bls_fr_mont(3)
+    bl = [[one, one], [one, one], [one, one], [one, one, one]]
+    res["numerator_coset_ms"] = timed(lambda: plonk.numerator_coset(
+        xs, bl, tw0, one, one, one, fr.bls_fr_mont(7), n, 4, 1, cres))
+    return res
 
 
 def groth16_bench(log_n, reps=3):
