@@ -46,6 +46,8 @@ struct gg_groth16_pk {
     G1Affine alpha, beta, delta;
     G2Affine beta2, delta2;
     size_t n_wires = 0, nb_public = 0;
+    // shard of a multi-GPU key: wires [wire_lo, wire_hi), Z positions [z_lo, z_lo + |Z|)
+    size_t wire_lo = 0, wire_hi = 0, z_lo = 0, nZ = 0;
     // A and K are wire-indexed tables (infinity holes kept) sharing one sort of
     // the wires; B1 and G2 share the sort of the B-filtered wires (same index map
     // and window).  Falls back to separate sorts if the shapes ever differ.
@@ -72,6 +74,83 @@ static void ck(int rc) {
     if (rc != GG_OK) throw Error(rc, gg_last_error());
 }
 
+// Builds the resident key of one shard: wires [wire_lo, wire_hi) of the A, B, K
+// and G2 tables and domain positions [z_lo, z_lo + nZ) of Z.  The full key is
+// the single shard (0, n_wires, 0, n - 1).  Point arrays are the shard's
+// slices, in pk order (setup.go:259-275): g1_A = the non-infinity A points of
+// the shard's wires, likewise g1_B / g2_B; g1_K = the K points whose wires lie
+// in the shard (k_wire_index gives their absolute wire ids; NULL = the default
+// nb_public + j numbering of the full key).
+static void pk_build(gg_groth16_pk* pk, int log_n, const void* omega_mont, const void* coset_gen_mont,
+                     const void* g1_A, size_t nA, const void* g1_B, size_t nB, const void* g1_Z,
+                     size_t z_lo, size_t nZ, const void* g1_K, size_t nK, const void* alpha1,
+                     const void* beta1, const void* delta1, const void* g2_B, const void* beta2,
+                     const void* delta2, const uint8_t* inf_A, const uint8_t* inf_B, size_t n_wires,
+                     size_t nb_public, const uint32_t* k_wire_index, size_t lo, size_t hi) {
+    GG_CHECK(omega_mont && coset_gen_mont && alpha1 && beta1 && delta1 && beta2 && delta2,
+             GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(inf_A && inf_B, GG_ERR_INVALID_ARG, "null infinity masks");
+    GG_CHECK(nb_public <= n_wires, GG_ERR_INVALID_ARG, "nb_public > n_wires");
+    GG_CHECK(log_n >= 0 && log_n <= 28, GG_ERR_INVALID_ARG, "log_n out of range");
+    GG_CHECK(lo <= hi && hi <= n_wires, GG_ERR_INVALID_ARG, "bad wire shard range");
+    pk->log_n = log_n;
+    pk->n = (size_t)1 << log_n;
+    pk->n_wires = n_wires;
+    pk->nb_public = nb_public;
+    pk->wire_lo = lo;
+    pk->wire_hi = hi;
+    pk->z_lo = z_lo;
+    pk->nZ = nZ;
+    const size_t nz_full = pk->n > 1 ? pk->n - 1 : 0;
+    GG_CHECK(z_lo + nZ <= nz_full, GG_ERR_INVALID_ARG,
+             "Z shard beyond domain cardinality - 1 (setup.go:266)");
+    GG_HIP(hipGetDevice(&pk->device));
+    memcpy(&pk->alpha, alpha1, 64);
+    memcpy(&pk->beta, beta1, 64);
+    memcpy(&pk->delta, delta1, 64);
+    memcpy(&pk->beta2, beta2, 128);
+    memcpy(&pk->delta2, delta2, 128);
+    ck(gg_domain_create(log_n, omega_mont, coset_gen_mont, &pk->dom));
+    // wire index maps (prove.go:151-175: drop wires whose A/B point is infinity),
+    // relative to the shard's first wire
+    std::vector<uint32_t> ia, ib, ik;
+    for (size_t i = lo; i < hi; i++) {
+        if (!inf_A[i]) ia.push_back((uint32_t)(i - lo));
+        if (!inf_B[i]) ib.push_back((uint32_t)(i - lo));
+    }
+    GG_CHECK(ia.size() == nA, GG_ERR_INVALID_ARG, "len(pk.G1.A) != n_wires - NbInfinityA (shard)");
+    GG_CHECK(ib.size() == nB, GG_ERR_INVALID_ARG, "len(pk.G1.B) != n_wires - NbInfinityB (shard)");
+    ik.resize(nK);
+    const size_t k0 = std::max(lo, nb_public);
+    for (size_t i = 0; i < nK; i++) {
+        size_t w = k_wire_index ? (size_t)k_wire_index[i] : k0 + i;
+        GG_CHECK(w >= lo && w < hi, GG_ERR_INVALID_ARG, "K wire index outside the shard");
+        ik[i] = (uint32_t)(w - lo);
+    }
+    GG_CHECK(nA == 0 || g1_A, GG_ERR_INVALID_ARG, "null g1_A");
+    GG_CHECK(nB == 0 || (g1_B && g2_B), GG_ERR_INVALID_ARG, "null g1_B / g2_B");
+    GG_CHECK(nK == 0 || g1_K, GG_ERR_INVALID_ARG, "null g1_K");
+    GG_CHECK(nZ == 0 || g1_Z, GG_ERR_INVALID_ARG, "null g1_Z");
+    const size_t nw = hi - lo;
+    // dense wire-indexed A and K (holes = infinity), one window size for both
+    {
+        std::vector<uint8_t> dense(nw * 64, 0);
+        for (size_t j = 0; j < nA; j++) memcpy(&dense[(size_t)ia[j] * 64], (const uint8_t*)g1_A + j * 64, 64);
+        const int cAK = choose_c(std::max<size_t>(nw, 1), 64, 255);
+        pk->A = msm_base_create_internal(GG_G1, dense.data(), nw, nullptr, cAK, true);
+        std::fill(dense.begin(), dense.end(), 0);
+        for (size_t j = 0; j < nK; j++) memcpy(&dense[(size_t)ik[j] * 64], (const uint8_t*)g1_K + j * 64, 64);
+        pk->K = msm_base_create_internal(GG_G1, dense.data(), nw, nullptr, cAK, true);
+    }
+    pk->B = msm_base_create_internal(GG_G1, g1_B, nB, ib.data(), 0, false);
+    pk->B2 = msm_base_create_internal(GG_G2, g2_B, nB, ib.data(), msm_base_window(pk->B), false);
+    pk->Z = msm_base_create_internal(GG_G1, g1_Z, nZ, nullptr, 0, false);
+    pk->share_AK = msm_same_shape(pk->A, pk->K);
+    pk->share_B = msm_same_shape(pk->B, pk->B2);
+    for (hipStream_t* x : {&pk->s0, &pk->s1, &pk->s2, &pk->s3, &pk->s4})
+        GG_HIP(hipStreamCreateWithFlags(x, hipStreamNonBlocking));
+}
+
 extern "C" int gg_groth16_pk_create(int log_n, const void* omega_mont, const void* coset_gen_mont,
                                     const void* g1_A, size_t nA, const void* g1_B, size_t nB,
                                     const void* g1_Z, size_t nZ, const void* g1_K, size_t nK,
@@ -81,58 +160,35 @@ extern "C" int gg_groth16_pk_create(int log_n, const void* omega_mont, const voi
                                     size_t nb_public, const uint32_t* k_wire_index,
                                     gg_groth16_pk_t* out) {
     GG_CAPI_BEGIN
-    GG_CHECK(out && omega_mont && coset_gen_mont && alpha1 && beta1 && delta1 && beta2 && delta2,
-             GG_ERR_INVALID_ARG, "null argument");
-    GG_CHECK(inf_A && inf_B, GG_ERR_INVALID_ARG, "null infinity masks");
-    GG_CHECK(nb_public <= n_wires, GG_ERR_INVALID_ARG, "nb_public > n_wires");
-    std::unique_ptr<gg_groth16_pk> pk(new gg_groth16_pk());
-    pk->log_n = log_n;
-    pk->n = (size_t)1 << log_n;
-    pk->n_wires = n_wires;
-    pk->nb_public = nb_public;
-    GG_CHECK(nZ + 1 == pk->n || (pk->n == 1 && nZ == 0), GG_ERR_INVALID_ARG,
+    GG_CHECK(out, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(log_n >= 0 && log_n <= 28, GG_ERR_INVALID_ARG, "log_n out of range");
+    const size_t n = (size_t)1 << log_n;
+    GG_CHECK(nZ + 1 == n || (n == 1 && nZ == 0), GG_ERR_INVALID_ARG,
              "len(pk.G1.Z) must be domain cardinality - 1 (setup.go:266)");
-    GG_HIP(hipGetDevice(&pk->device));
-    memcpy(&pk->alpha, alpha1, 64);
-    memcpy(&pk->beta, beta1, 64);
-    memcpy(&pk->delta, delta1, 64);
-    memcpy(&pk->beta2, beta2, 128);
-    memcpy(&pk->delta2, delta2, 128);
-    ck(gg_domain_create(log_n, omega_mont, coset_gen_mont, &pk->dom));
-    // wire index maps (prove.go:151-175: drop wires whose A/B point is infinity)
-    std::vector<uint32_t> ia, ib, ik;
-    for (size_t i = 0; i < n_wires; i++) {
-        if (!inf_A[i]) ia.push_back((uint32_t)i);
-        if (!inf_B[i]) ib.push_back((uint32_t)i);
-    }
-    GG_CHECK(ia.size() == nA, GG_ERR_INVALID_ARG, "len(pk.G1.A) != n_wires - NbInfinityA");
-    GG_CHECK(ib.size() == nB, GG_ERR_INVALID_ARG, "len(pk.G1.B) != n_wires - NbInfinityB");
-    ik.resize(nK);
-    for (size_t i = 0; i < nK; i++) {
-        ik[i] = k_wire_index ? k_wire_index[i] : (uint32_t)(nb_public + i);
-        GG_CHECK(ik[i] < n_wires, GG_ERR_INVALID_ARG, "k_wire_index out of range");
-    }
-    GG_CHECK(nA == 0 || g1_A, GG_ERR_INVALID_ARG, "null g1_A");
-    GG_CHECK(nB == 0 || (g1_B && g2_B), GG_ERR_INVALID_ARG, "null g1_B / g2_B");
-    GG_CHECK(nK == 0 || g1_K, GG_ERR_INVALID_ARG, "null g1_K");
-    GG_CHECK(nZ == 0 || g1_Z, GG_ERR_INVALID_ARG, "null g1_Z");
-    // dense wire-indexed A and K (holes = infinity), one window size for both
-    {
-        std::vector<uint8_t> dense((size_t)n_wires * 64, 0);
-        for (size_t j = 0; j < nA; j++) memcpy(&dense[(size_t)ia[j] * 64], (const uint8_t*)g1_A + j * 64, 64);
-        const int cAK = choose_c(std::max<size_t>(n_wires, 1), 64, 255);
-        pk->A = msm_base_create_internal(GG_G1, dense.data(), n_wires, nullptr, cAK, true);
-        std::fill(dense.begin(), dense.end(), 0);
-        for (size_t j = 0; j < nK; j++) memcpy(&dense[(size_t)ik[j] * 64], (const uint8_t*)g1_K + j * 64, 64);
-        pk->K = msm_base_create_internal(GG_G1, dense.data(), n_wires, nullptr, cAK, true);
-    }
-    pk->B = msm_base_create_internal(GG_G1, g1_B, nB, ib.data(), 0, false);
-    pk->B2 = msm_base_create_internal(GG_G2, g2_B, nB, ib.data(), msm_base_window(pk->B), false);
-    pk->Z = msm_base_create_internal(GG_G1, g1_Z, nZ, nullptr, 0, false);
-    pk->share_AK = msm_same_shape(pk->A, pk->K);
-    pk->share_B = msm_same_shape(pk->B, pk->B2);
-    for (hipStream_t* x : {&pk->s0, &pk->s1, &pk->s2, &pk->s3, &pk->s4})
-        GG_HIP(hipStreamCreateWithFlags(x, hipStreamNonBlocking));
+    std::unique_ptr<gg_groth16_pk> pk(new gg_groth16_pk());
+    if (!k_wire_index) GG_CHECK(nb_public + nK <= n_wires, GG_ERR_INVALID_ARG, "len(pk.G1.K) too large");
+    pk_build(pk.get(), log_n, omega_mont, coset_gen_mont, g1_A, nA, g1_B, nB, g1_Z, 0, nZ, g1_K, nK,
+             alpha1, beta1, delta1, g2_B, beta2, delta2, inf_A, inf_B, n_wires, nb_public,
+             k_wire_index, 0, n_wires);
+    *out = pk.release();
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_pk_create_shard(int log_n, const void* omega_mont, const void* coset_gen_mont,
+                                          const void* g1_A, size_t nA, const void* g1_B, size_t nB,
+                                          const void* g1_Z, size_t z_lo, size_t nZ, const void* g1_K,
+                                          size_t nK, const void* alpha1, const void* beta1,
+                                          const void* delta1, const void* g2_B, const void* beta2,
+                                          const void* delta2, const uint8_t* inf_A,
+                                          const uint8_t* inf_B, size_t n_wires, size_t nb_public,
+                                          const uint32_t* k_wire_index, size_t wire_lo,
+                                          size_t wire_hi, gg_groth16_pk_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out, GG_ERR_INVALID_ARG, "null argument");
+    std::unique_ptr<gg_groth16_pk> pk(new gg_groth16_pk());
+    pk_build(pk.get(), log_n, omega_mont, coset_gen_mont, g1_A, nA, g1_B, nB, g1_Z, z_lo, nZ, g1_K,
+             nK, alpha1, beta1, delta1, g2_B, beta2, delta2, inf_A, inf_B, n_wires, nb_public,
+             k_wire_index, wire_lo, wire_hi);
     *out = pk.release();
     GG_CAPI_END
 }
@@ -155,44 +211,31 @@ static Fr fr_from(const void* p) {
     return x;
 }
 
-extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_wires,
-                                const void* sol_a, const void* sol_b, const void* sol_c,
-                                size_t n_cons, int inputs_on_device, const void* r_mont,
-                                const void* s_mont, void* ar_aff, void* bs_aff, void* krs_aff,
-                                void* h_dev_out) {
-    GG_CAPI_BEGIN
-    GG_CHECK(pk && wires && sol_a && sol_b && sol_c && r_mont && s_mont && ar_aff && bs_aff && krs_aff,
-             GG_ERR_INVALID_ARG, "null argument");
-    GG_CHECK(n_wires == pk->n_wires, GG_ERR_INVALID_ARG, "len(wires) != pk wires");
-    GG_CHECK(n_cons <= pk->n, GG_ERR_INVALID_ARG, "nbConstraints > domain cardinality");
-    std::lock_guard<std::mutex> lk(pk->mu);
+// MSM partials of one key (shard): the device section of prove.go:198-301.
+struct G16Partials {
+    G1Jac a, b1, k, z;  // Σ w·A, Σ w·B1, Σ w·K (filtered), Σ h·Z
+    G2Jac b2;           // Σ w·B2
+};
+
+// Uploads the solution and runs computeH + the five MSMs of `pk` (a shard, or
+// the whole key).  g_timings[0..6] are filled.
+static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a,
+                         const void* sol_b, const void* sol_c, size_t n_cons,
+                         bool inputs_on_device, void* h_dev_out, G16Partials& out) {
     double t0 = now_ms();
-    const size_t n = pk->n;
+    const size_t n = pk->n, n_wires = pk->n_wires;
     const size_t nbytes = n * 32;
     pk->wires.reserve(std::max<size_t>(n_wires, 1) * 32);
     pk->sa.reserve(nbytes);
     pk->sb.reserve(nbytes);
     pk->sc.reserve(nbytes);
     hipMemcpyKind kind = inputs_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-
-    // proof randomness (prove.go:177-189): kr = -r*s
-    Fr r = fr_from(r_mont), s = fr_from(s_mont);
-    Fr kr = -(r * s);
-    Fr rc = from_mont(r), sc = from_mont(s), krc = from_mont(kr);
-    // host pool: fixed-point terms independent of the MSMs (prove.go:192, 293-296)
-    G1Jac dl = G1Jac::from_affine(pk->delta);
-    auto f_rd = std::async(std::launch::async, [&] { return jac_mul(dl, rc.v); });
-    auto f_sd = std::async(std::launch::async, [&] { return jac_mul(dl, sc.v); });
-    auto f_krd = std::async(std::launch::async, [&] { return jac_mul(dl, krc.v); });
-    auto f_sd2 = std::async(std::launch::async,
-                            [&] { return jac_mul(G2Jac::from_affine(pk->delta2), sc.v); });
-
-    // uploads
     const Fr* wdev = (const Fr*)wires;
     if (!inputs_on_device) {
         GG_HIP(hipMemcpyAsync(pk->wires.p, wires, n_wires * 32, hipMemcpyHostToDevice, pk->s0));
         wdev = pk->wires.as<Fr>();
     }
+    wdev += pk->wire_lo;  // the shard's tables are indexed from its first wire
     Fr* A = pk->sa.as<Fr>();
     Fr* B = pk->sb.as<Fr>();
     Fr* C = pk->sc.as<Fr>();
@@ -209,8 +252,7 @@ extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_
     // latency-bound, so overlapping them fills the chip):
     //   s1: computeH -> Z-MSM (h lands in A's buffer)    s2: A-MSM
     //   s3: B1-MSM    s4: K-MSM    s0 (this thread): G2-MSM
-    G1Jac jz = G1Jac::inf(), ja, jb, jk;
-    G2Jac j2;
+    out.z = G1Jac::inf();
     double t_h = 0, t_z = 0, t_a = 0, t_b = 0, t_k = 0;
     std::mutex emu;
     std::string werr;
@@ -246,7 +288,7 @@ extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_
         double b = now_ms();
         t_h = b - a;
         if (h_dev_out) GG_HIP(hipMemcpyAsync(h_dev_out, A, nbytes, hipMemcpyDeviceToDevice, pk->s1));
-        if (n > 1) msm_device(pk->Z, A, &jz, pk->s1);
+        if (n > 1) msm_device(pk->Z, A + pk->z_lo, &out.z, pk->s1);
         t_z = now_ms() - b;
     }));
     // wire sorts, enqueued from this thread before any finisher waits on their
@@ -259,42 +301,153 @@ extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_
     msm_prepare_dev(pk->B, sB, wdev, pk->s3);
     if (!pk->share_AK) msm_prepare_dev(pk->K, sK, wdev, pk->s4);
     if (!pk->share_B) msm_prepare_dev(pk->B2, sB2, wdev, pk->s0);
-    spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->A, sAK, &ja, pk->s2); t_a = now_ms() - a; }));
-    spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->B, sB, &jb, pk->s3); t_b = now_ms() - a; }));
-    spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->K, sK, &jk, pk->s4); t_k = now_ms() - a; }));
+    spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->A, sAK, &out.a, pk->s2); t_a = now_ms() - a; }));
+    spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->B, sB, &out.b1, pk->s3); t_b = now_ms() - a; }));
+    spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->K, sK, &out.k, pk->s4); t_k = now_ms() - a; }));
     double t2 = now_ms();
-    guarded([&] { msm_finish_dev(pk->B2, sB2, &j2, pk->s0); })();
+    guarded([&] { msm_finish_dev(pk->B2, sB2, &out.b2, pk->s0); })();
     double te = now_ms();
     for (auto& w : workers) w.join();
     if (wcode != GG_OK) throw Error(wcode, werr);
+    g_timings[0] = t_up - t0;
+    g_timings[1] = t_h;
     g_timings[2] = t_a;
     g_timings[3] = t_b;
     g_timings[4] = t_k;
+    g_timings[5] = t_z;
     g_timings[6] = te - t2;
-    double tep = now_ms();
+}
 
-    // epilogue (prove.go:206-299)
-    G1Jac rd = f_rd.get(), sd = f_sd.get(), krd = f_krd.get();
-    G2Jac sd2 = f_sd2.get();
-    G1Jac ar = jac_add(jac_add_affine(ja, pk->alpha), rd);
-    G1Jac bs1 = jac_add(jac_add_affine(jb, pk->beta), sd);
-    auto f_sar = std::async(std::launch::async, [&] { return jac_mul(ar, sc.v); });
-    G1Jac rbs = jac_mul(bs1, rc.v);
-    G1Jac krs = jac_add(jac_add(jk, krd), jz);
+// Fixed-point terms of the proof (prove.go:177-192, 293-296): kr = -r*s and
+// r*delta, s*delta, kr*delta, s*delta2 -- independent of the MSMs.
+struct G16Fixed {
+    Fr rc, sc;  // r, s in canonical form (scalar-mul digits)
+    G1Jac rd, sd, krd;
+    G2Jac sd2;
+};
+
+static std::future<G16Fixed> fixed_terms_async(const G1Affine& delta, const G2Affine& delta2,
+                                               const Fr& r, const Fr& s) {
+    return std::async(std::launch::async, [delta, delta2, r, s] {
+        G16Fixed f;
+        Fr kr = -(r * s);
+        f.rc = from_mont(r);
+        f.sc = from_mont(s);
+        Fr krc = from_mont(kr);
+        G1Jac dl = G1Jac::from_affine(delta);
+        auto f_rd = std::async(std::launch::async, [&] { return jac_mul(dl, f.rc.v); });
+        auto f_sd = std::async(std::launch::async, [&] { return jac_mul(dl, f.sc.v); });
+        auto f_sd2 = std::async(std::launch::async,
+                                [&] { return jac_mul(G2Jac::from_affine(delta2), f.sc.v); });
+        f.krd = jac_mul(dl, krc.v);
+        f.rd = f_rd.get();
+        f.sd = f_sd.get();
+        f.sd2 = f_sd2.get();
+        return f;
+    });
+}
+
+// Combination of the (summed) MSM partials, prove.go:206-299 verbatim:
+//   Ar  = Σ w·A + α + r·δ                  Bs1 = Σ w·B1 + β + s·δ
+//   Krs = Σ w·K + kr·δ + Σ h·Z + s·Ar + r·Bs1
+//   Bs  = Σ w·B2 + s·δ2 + β2
+static void g16_combine(const G16Partials& p, const G16Fixed& f, const G1Affine& alpha,
+                        const G1Affine& beta, const G2Affine& beta2, void* ar_aff, void* bs_aff,
+                        void* krs_aff) {
+    G1Jac ar = jac_add(jac_add_affine(p.a, alpha), f.rd);
+    G1Jac bs1 = jac_add(jac_add_affine(p.b1, beta), f.sd);
+    auto f_sar = std::async(std::launch::async, [&] { return jac_mul(ar, f.sc.v); });
+    G1Jac rbs = jac_mul(bs1, f.rc.v);
+    G1Jac krs = jac_add(jac_add(p.k, f.krd), p.z);
     krs = jac_add(krs, f_sar.get());
     krs = jac_add(krs, rbs);
-    G2Jac bs = jac_add_affine(jac_add(j2, sd2), pk->beta2);
+    G2Jac bs = jac_add_affine(jac_add(p.b2, f.sd2), beta2);
     G1Affine o_ar = jac_to_affine(ar), o_krs = jac_to_affine(krs);
     G2Affine o_bs = jac_to_affine(bs);
     memcpy(ar_aff, &o_ar, 64);
     memcpy(krs_aff, &o_krs, 64);
     memcpy(bs_aff, &o_bs, 128);
+}
+
+static void check_prove_args(gg_groth16_pk_t pk, const void* wires, size_t n_wires, const void* a,
+                             const void* b, const void* c, size_t n_cons) {
+    GG_CHECK(pk && wires && a && b && c, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(n_wires == pk->n_wires, GG_ERR_INVALID_ARG, "len(wires) != pk wires");
+    GG_CHECK(n_cons <= pk->n, GG_ERR_INVALID_ARG, "nbConstraints > domain cardinality");
+}
+
+extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_wires,
+                                const void* sol_a, const void* sol_b, const void* sol_c,
+                                size_t n_cons, int inputs_on_device, const void* r_mont,
+                                const void* s_mont, void* ar_aff, void* bs_aff, void* krs_aff,
+                                void* h_dev_out) {
+    GG_CAPI_BEGIN
+    check_prove_args(pk, wires, n_wires, sol_a, sol_b, sol_c, n_cons);
+    GG_CHECK(r_mont && s_mont && ar_aff && bs_aff && krs_aff, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(pk->wire_lo == 0 && pk->wire_hi == pk->n_wires && pk->z_lo == 0 &&
+                 pk->nZ == (pk->n > 1 ? pk->n - 1 : 0),
+             GG_ERR_INVALID_ARG, "gg_groth16_prove needs the whole key; a shard proves with "
+                                 "gg_groth16_prove_partial + gg_groth16_finalize");
+    std::lock_guard<std::mutex> lk(pk->mu);
+    double t0 = now_ms();
+    // host pool computes the fixed-point terms while the GPU works
+    auto fixed = fixed_terms_async(pk->delta, pk->delta2, fr_from(r_mont), fr_from(s_mont));
+    G16Partials p;
+    prove_device(pk, wires, sol_a, sol_b, sol_c, n_cons, inputs_on_device != 0, h_dev_out, p);
+    double tep = now_ms();
+    g16_combine(p, fixed.get(), pk->alpha, pk->beta, pk->beta2, ar_aff, bs_aff, krs_aff);
     double tend = now_ms();
-    g_timings[0] = t_up - t0;
-    g_timings[1] = t_h;
-    g_timings[5] = t_z;
     g_timings[7] = tend - tep;
     g_timings[8] = tend - t0;
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_prove_partial(gg_groth16_pk_t pk, const void* wires, size_t n_wires,
+                                        const void* sol_a, const void* sol_b, const void* sol_c,
+                                        size_t n_cons, int inputs_on_device, void* partials,
+                                        void* h_dev_out) {
+    GG_CAPI_BEGIN
+    check_prove_args(pk, wires, n_wires, sol_a, sol_b, sol_c, n_cons);
+    GG_CHECK(partials, GG_ERR_INVALID_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(pk->mu);
+    double t0 = now_ms();
+    G16Partials p;
+    prove_device(pk, wires, sol_a, sol_b, sol_c, n_cons, inputs_on_device != 0, h_dev_out, p);
+    uint8_t* o = (uint8_t*)partials;
+    memcpy(o, &p.a, 96);
+    memcpy(o + 96, &p.b1, 96);
+    memcpy(o + 192, &p.k, 96);
+    memcpy(o + 288, &p.z, 96);
+    memcpy(o + 384, &p.b2, 192);
+    g_timings[7] = 0;
+    g_timings[8] = now_ms() - t0;
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_finalize(const void* alpha1, const void* beta1, const void* delta1,
+                                   const void* beta2, const void* delta2, const void* partials,
+                                   const void* r_mont, const void* s_mont, void* ar_aff,
+                                   void* bs_aff, void* krs_aff) {
+    GG_CAPI_BEGIN
+    GG_CHECK(alpha1 && beta1 && delta1 && beta2 && delta2 && partials && r_mont && s_mont &&
+                 ar_aff && bs_aff && krs_aff,
+             GG_ERR_INVALID_ARG, "null argument");
+    G1Affine alpha, beta, delta;
+    G2Affine b2, d2;
+    memcpy(&alpha, alpha1, 64);
+    memcpy(&beta, beta1, 64);
+    memcpy(&delta, delta1, 64);
+    memcpy(&b2, beta2, 128);
+    memcpy(&d2, delta2, 128);
+    auto fixed = fixed_terms_async(delta, d2, fr_from(r_mont), fr_from(s_mont));
+    G16Partials p;
+    const uint8_t* q = (const uint8_t*)partials;
+    memcpy(&p.a, q, 96);
+    memcpy(&p.b1, q + 96, 96);
+    memcpy(&p.k, q + 192, 96);
+    memcpy(&p.z, q + 288, 96);
+    memcpy(&p.b2, q + 384, 192);
+    g16_combine(p, fixed.get(), alpha, beta, b2, ar_aff, bs_aff, krs_aff);
     GG_CAPI_END
 }
 

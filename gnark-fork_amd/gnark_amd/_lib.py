@@ -63,6 +63,10 @@ def _load():
         "gg_groth16_pk_release": ([P], I),
         "gg_groth16_prove": ([P, P, S, P, P, P, S, I, P, P, P, P, P, P], I),
         "gg_groth16_last_timings": ([ctypes.POINTER(ctypes.c_double)], I),
+        "gg_groth16_pk_create_shard": ([I, P, P, P, S, P, S, P, S, S, P, S, P, P, P, P, P, P, P, P, S,
+                                        S, P, S, S, PP], I),
+        "gg_groth16_prove_partial": ([P, P, S, P, P, P, S, I, P, P], I),
+        "gg_groth16_finalize": ([P, P, P, P, P, P, P, P, P, P, P], I),
         "gg_batch_scalar_mul": ([I, P, P, S, I, P, I], I),
         "gg_plonk_numerator_coset": ([ctypes.POINTER(ctypes.c_void_p), I, P, ctypes.POINTER(I), P,
                                       P, P, P, P, S, I, I, P, P], I),
@@ -90,7 +94,8 @@ EXPORTED = [
     "gg_g1_scalar_mul", "gg_g2_scalar_mul", "gg_groth16_pk_create", "gg_groth16_pk_release",
     "gg_groth16_prove", "gg_groth16_last_timings", "gg_batch_scalar_mul", "gg_profile_enable",
     "gg_plonk_numerator_coset", "gg_plonk_divide_by_xn_minus_one", "gg_bls12_381_fr_batch_invert",
-    "gg_profile_get",
+    "gg_profile_get", "gg_groth16_pk_create_shard", "gg_groth16_prove_partial",
+    "gg_groth16_finalize",
 ]
 
 

@@ -142,3 +142,151 @@ def last_timings() -> dict:
     check(lib.gg_groth16_last_timings(arr))
     keys = ["upload", "compute_h", "msm_A", "msm_B1", "msm_K", "msm_Z", "msm_G2", "epilogue", "total"]
     return dict(zip(keys, list(arr)))
+
+
+# ---------------------------------------------------------------- multi-GPU
+# One key shard per GPU: the MSM point sets partition by wire (A,
+# B1, K, G2) and by domain position (Z); every GPU computes h itself, so the
+# only cross-GPU traffic is the all-gather of the 576-B partials.
+
+PARTIALS_BYTES = 4 * 96 + 192  # G1Jac A | B1 | K | Z, G2Jac B2
+
+
+@dataclasses.dataclass
+class KeyShard:
+    """Slices of a ProvingKeyData owned by one shard (host bytes, key order)."""
+    wire_lo: int
+    wire_hi: int
+    z_lo: int
+    g1_A: bytes
+    g1_B: bytes
+    g2_B: bytes
+    g1_K: bytes
+    g1_Z: bytes
+    k_wire_index: Optional[np.ndarray]  # absolute wire ids of g1_K (None = default numbering)
+
+
+def shard_ranges(n_wires: int, n: int, rank: int, world: int):
+    """(wire_lo, wire_hi, z_lo, z_hi) of `rank`: contiguous balanced slices of the
+    wires and of the n - 1 Z positions."""
+    from .dist import shard_range
+    lo, hi = shard_range(n_wires, rank, world)
+    zl, zh = shard_range(max(n - 1, 0), rank, world)
+    return lo, hi, zl, zh
+
+
+def slice_key(data: ProvingKeyData, rank: int, world: int) -> KeyShard:
+    """Cut the key arrays of `data` for shard `rank` of `world` (pk order kept:
+    A/B are the non-infinity points in wire order, setup.go:259-275)."""
+    n = 1 << data.log_n
+    lo, hi, zl, zh = shard_ranges(data.n_wires, n, rank, world)
+    infA = np.frombuffer(bytes(data.infinity_A), dtype=np.uint8)
+    infB = np.frombuffer(bytes(data.infinity_B), dtype=np.uint8)
+    a0, a1 = int((infA[:lo] == 0).sum()), int((infA[:hi] == 0).sum())
+    b0, b1 = int((infB[:lo] == 0).sum()), int((infB[:hi] == 0).sum())
+    if data.k_wire_index is None:
+        k0 = max(lo, data.nb_public) - data.nb_public
+        k1 = max(hi, data.nb_public) - data.nb_public
+        k1 = min(k1, len(data.g1_K) // 64)
+        k0 = min(k0, k1)
+        g1K, kidx = data.g1_K[64 * k0:64 * k1], None
+    else:
+        kw = np.asarray(data.k_wire_index, dtype=np.uint32)
+        sel = np.nonzero((kw >= lo) & (kw < hi))[0]
+        kp = np.frombuffer(bytes(data.g1_K), dtype=np.uint8).reshape(-1, 64)
+        g1K, kidx = kp[sel].tobytes(), np.ascontiguousarray(kw[sel])
+    return KeyShard(lo, hi, zl, data.g1_A[64 * a0:64 * a1], data.g1_B[64 * b0:64 * b1],
+                    data.g2_B[128 * b0:128 * b1], g1K, data.g1_Z[64 * zl:64 * zh], kidx)
+
+
+class ProvingKeyShard:
+    """Device-resident shard `rank` of `world` of a proving key (gg_groth16_pk_create_shard).
+    `shard` may be given directly (slices already cut, e.g. generated per GPU)."""
+
+    def __init__(self, data: ProvingKeyData, rank: int = 0, world: int = 1,
+                 shard: Optional[KeyShard] = None):
+        sh = shard if shard is not None else slice_key(data, rank, world)
+        self.data, self.shard, self.rank, self.world = data, sh, rank, world
+        omega = data.domain_generator or fr.fr_mont(fr.domain_generator(data.log_n))
+        gen = data.domain_mul_gen or fr.fr_mont(fr.FR_MULTIPLICATIVE_GEN)
+        h = ctypes.c_void_p()
+        check(lib.gg_groth16_pk_create_shard(
+            data.log_n, ptr(omega), ptr(gen),
+            ptr(sh.g1_A), len(sh.g1_A) // 64, ptr(sh.g1_B), len(sh.g1_B) // 64,
+            ptr(sh.g1_Z), sh.z_lo, len(sh.g1_Z) // 64, ptr(sh.g1_K), len(sh.g1_K) // 64,
+            ptr(data.alpha1), ptr(data.beta1), ptr(data.delta1),
+            ptr(sh.g2_B), ptr(data.beta2), ptr(data.delta2),
+            ptr(bytes(data.infinity_A)), ptr(bytes(data.infinity_B)), data.n_wires,
+            data.nb_public, ptr(sh.k_wire_index), sh.wire_lo, sh.wire_hi, ctypes.byref(h)))
+        self.handle = h
+        self.n_wires = data.n_wires
+        self.log_n = data.log_n
+
+    close = ProvingKey.close
+    __del__ = ProvingKey.__del__
+
+
+def prove_partial(pk: ProvingKeyShard, solution: Solution, h_out=None) -> bytes:
+    """computeH + this shard's five MSMs (gg_groth16_prove_partial): 576-B partials."""
+    out = bytearray(PARTIALS_BYTES)
+    check(lib.gg_groth16_prove_partial(pk.handle, ptr(solution.W), solution.n_wires,
+                                       ptr(solution.A), ptr(solution.B), ptr(solution.C),
+                                       solution.n_constraints, int(solution.on_device), ptr(out),
+                                       ptr(h_out)))
+    return bytes(out)
+
+
+def add_partials(parts: Sequence[bytes]) -> bytes:
+    """Sum of shard partials with the library's exact group law."""
+    from . import msm
+    acc = bytearray(parts[0])
+    for p in parts[1:]:
+        for k in range(4):
+            acc[96 * k:96 * k + 96] = msm.jac_add(msm.G1, bytes(acc[96 * k:96 * k + 96]), p[96 * k:96 * k + 96])
+        acc[384:576] = msm.jac_add(msm.G2, bytes(acc[384:576]), p[384:576])
+    return bytes(acc)
+
+
+def finalize(data: ProvingKeyData, partials: bytes, r: bytes, s: bytes) -> Proof:
+    """Combination of prove.go:177-299 on the summed partials (host, gg_groth16_finalize)."""
+    ar, bs, krs = bytearray(64), bytearray(128), bytearray(64)
+    check(lib.gg_groth16_finalize(ptr(data.alpha1), ptr(data.beta1), ptr(data.delta1),
+                                  ptr(data.beta2), ptr(data.delta2), ptr(partials), ptr(r), ptr(s),
+                                  ptr(ar), ptr(bs), ptr(krs)))
+    return Proof(bytes(ar), bytes(bs), bytes(krs))
+
+
+def prove_distributed(pk: ProvingKeyShard, solution: Solution, *opts, r: bytes = None,
+                      s: bytes = None, device=None) -> Proof:
+    """Multi-GPU Prove, one process per GPU (torch.distributed, RCCL on ROCm):
+    shard partials -> all-gather (576 B per rank) -> exact sum -> combination.
+    r and s come from rank 0 (broadcast) unless given; every rank returns the proof."""
+    import torch
+    import torch.distributed as tdist
+    cfg = backend.new_prover_config(*opts)
+    if not backend.accelerated(cfg):
+        raise RuntimeError("accelerated prover requested without with_amd_acceleration()")
+    world = tdist.get_world_size() if tdist.is_initialized() else 1
+    if r is None or s is None:
+        rs = torch.frombuffer(bytearray(_rand_fr_mont() + _rand_fr_mont()), dtype=torch.uint8)
+        if world > 1:
+            rs = rs.to(device) if device is not None else rs
+            tdist.broadcast(rs, 0)
+        rsb = bytes(rs.cpu().numpy())
+        r, s = rsb[:32], rsb[32:]
+    return gather_and_finalize(pk.data, prove_partial(pk, solution), r, s, device)
+
+
+def gather_and_finalize(data: ProvingKeyData, part: bytes, r: bytes, s: bytes, device=None) -> Proof:
+    """All-gather every rank's 576-B partials, add them exactly, combine (all ranks)."""
+    import torch
+    import torch.distributed as tdist
+    world = tdist.get_world_size() if tdist.is_initialized() else 1
+    if world > 1:
+        t = torch.frombuffer(bytearray(part), dtype=torch.uint8)
+        if device is not None:
+            t = t.to(device)
+        bufs = [torch.empty_like(t) for _ in range(world)]
+        tdist.all_gather(bufs, t)
+        part = add_partials([bytes(b.cpu().numpy()) for b in bufs])
+    return finalize(data, part, r, s)

@@ -184,6 +184,41 @@ int gg_groth16_prove(gg_groth16_pk_t pk, const void *wires, size_t n_wires, cons
                      const void *r_mont, const void *s_mont, void *ar_aff, void *bs_aff,
                      void *krs_aff, void *h_dev_out);
 
+/* ---- multi-GPU Groth16: one key shard per GPU.
+ * A shard owns wires [wire_lo, wire_hi) of pk.G1.A / G1.B / G1.K / G2.B and
+ * positions [z_lo, z_lo + nZ) of pk.G1.Z (bit-reversed order, setup.go:265).
+ * The point arguments are the shard's slices of the key arrays, in key order:
+ * g1_A = the non-infinity A points of the shard's wires (inf_A/inf_B are the
+ * full n_wires masks), g1_B / g2_B likewise, g1_K = the K points whose wires
+ * lie in the shard; k_wire_index (nullable) their absolute wire ids, NULL =
+ * max(wire_lo, nb_public) + j.  The shards of a key partition it; every GPU
+ * holds the domain and computes h itself (no exchange on the H path). */
+int gg_groth16_pk_create_shard(int log_n, const void *omega_mont, const void *coset_gen_mont,
+                               const void *g1_A, size_t nA, const void *g1_B, size_t nB,
+                               const void *g1_Z, size_t z_lo, size_t nZ, const void *g1_K,
+                               size_t nK, const void *alpha1, const void *beta1,
+                               const void *delta1, const void *g2_B, const void *beta2,
+                               const void *delta2, const uint8_t *inf_A, const uint8_t *inf_B,
+                               size_t n_wires, size_t nb_public, const uint32_t *k_wire_index,
+                               size_t wire_lo, size_t wire_hi, gg_groth16_pk_t *out);
+/* Device section of Prove on one key (shard): computeH and the five MSMs of
+ * prove.go:198-301 without the combination.  Inputs as gg_groth16_prove (the
+ * whole solution).  partials (host, 576 B): G1Jac sum w.A | sum w.B1 |
+ * sum w.K | sum h.Z (96 B each) then G2Jac sum w.B2 (192 B).  The partials of
+ * all shards are added (gg_g1_jac_add / gg_g2_jac_add, e.g. after an RCCL
+ * all-gather) and handed to gg_groth16_finalize. */
+int gg_groth16_prove_partial(gg_groth16_pk_t pk, const void *wires, size_t n_wires,
+                             const void *sol_a, const void *sol_b, const void *sol_c,
+                             size_t n_cons, int inputs_on_device, void *partials,
+                             void *h_dev_out);
+/* Host-only combination of summed partials into the proof (prove.go:177-299):
+ * Ar = A + alpha + r.delta; Bs1 = B1 + beta + s.delta;
+ * Krs = K + kr.delta + Z + s.Ar + r.Bs1 (kr = -rs); Bs = B2 + s.delta2 + beta2. */
+int gg_groth16_finalize(const void *alpha1, const void *beta1, const void *delta1,
+                        const void *beta2, const void *delta2, const void *partials,
+                        const void *r_mont, const void *s_mont, void *ar_aff, void *bs_aff,
+                        void *krs_aff);
+
 /* per-stage timings (ms) of the last gg_groth16_prove on this thread:
  * [0]=upload [1]=computeH [2]=msm_A [3]=msm_B1 [4]=msm_K [5]=msm_Z [6]=msm_G2
  * [7]=epilogue [8]=total */
