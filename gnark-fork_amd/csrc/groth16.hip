@@ -34,7 +34,19 @@ void msm_prepare_dev(gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStrea
 void msm_finish_dev(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st);
 int msm_base_window(const gg_msm_base* b);
 int choose_c(size_t n, size_t point_bytes, int total_bits);
+void hshard_run(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len, Fr* send, Fr* recv,
+                gg_exchange_fn xchg, void* ctx, hipStream_t st);
+size_t hshard_m(const gg_hshard* hs, int* rank, int* world, int* log_n);
+Fr* hshard_h(gg_hshard* hs);
 }  // namespace gg
+
+// distributed computeH of a shard (gg_groth16_prove_partial_dist)
+struct DistH {
+    gg_hshard* hs;
+    gg_exchange_fn xchg;
+    void* ctx;
+    gg::Fr *send, *recv;
+};
 
 using namespace gg;
 
@@ -221,7 +233,8 @@ struct G16Partials {
 // the whole key).  g_timings[0..6] are filled.
 static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a,
                          const void* sol_b, const void* sol_c, size_t n_cons,
-                         bool inputs_on_device, void* h_dev_out, G16Partials& out) {
+                         bool inputs_on_device, void* h_dev_out, G16Partials& out,
+                         const DistH* dh = nullptr) {
     double t0 = now_ms();
     const size_t n = pk->n, n_wires = pk->n_wires;
     const size_t nbytes = n * 32;
@@ -242,9 +255,17 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
     const void* src[3] = {sol_a, sol_b, sol_c};
     Fr* dst[3] = {A, B, C};
     for (int i = 0; i < 3; i++) {
+        if (dh) {  // the distributed H gathers its cyclic slices (zero past n_cons) itself
+            if (inputs_on_device) dst[i] = (Fr*)src[i];
+            else if (n_cons) GG_HIP(hipMemcpyAsync(dst[i], src[i], n_cons * 32, kind, pk->s1));
+            continue;
+        }
         if (n_cons) GG_HIP(hipMemcpyAsync(dst[i], src[i], n_cons * 32, kind, pk->s1));
         if (n_cons < n) GG_HIP(hipMemsetAsync((char*)dst[i] + n_cons * 32, 0, nbytes - n_cons * 32, pk->s1));
     }
+    A = dst[0];
+    B = dst[1];
+    C = dst[2];
     GG_HIP(hipStreamSynchronize(pk->s0));
     double t_up = now_ms();
 
@@ -281,7 +302,16 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
         if (serial) fn();
         else workers.emplace_back(fn);
     };
-    spawn(guarded([&] {
+    if (dh) spawn(guarded([&] {
+        double a = now_ms();
+        hshard_run(dh->hs, A, B, C, n_cons, dh->send, dh->recv, dh->xchg, dh->ctx, pk->s1);
+        GG_HIP(hipStreamSynchronize(pk->s1));
+        double b = now_ms();
+        t_h = b - a;
+        msm_device(pk->Z, hshard_h(dh->hs), &out.z, pk->s1);
+        t_z = now_ms() - b;
+    }));
+    else spawn(guarded([&] {
         double a = now_ms();
         compute_h_device(pk->dom, A, B, C, A, pk->s1);
         GG_HIP(hipStreamSynchronize(pk->s1));
@@ -413,6 +443,35 @@ extern "C" int gg_groth16_prove_partial(gg_groth16_pk_t pk, const void* wires, s
     double t0 = now_ms();
     G16Partials p;
     prove_device(pk, wires, sol_a, sol_b, sol_c, n_cons, inputs_on_device != 0, h_dev_out, p);
+    uint8_t* o = (uint8_t*)partials;
+    memcpy(o, &p.a, 96);
+    memcpy(o + 96, &p.b1, 96);
+    memcpy(o + 192, &p.k, 96);
+    memcpy(o + 288, &p.z, 96);
+    memcpy(o + 384, &p.b2, 192);
+    g_timings[7] = 0;
+    g_timings[8] = now_ms() - t0;
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_prove_partial_dist(gg_groth16_pk_t pk, gg_hshard_t hs, const void* wires,
+                                             size_t n_wires, const void* sol_a, const void* sol_b,
+                                             const void* sol_c, size_t n_cons, int inputs_on_device,
+                                             gg_exchange_fn xchg, void* xchg_ctx, void* send_dev,
+                                             void* recv_dev, void* partials) {
+    GG_CAPI_BEGIN
+    check_prove_args(pk, wires, n_wires, sol_a, sol_b, sol_c, n_cons);
+    GG_CHECK(hs && xchg && send_dev && recv_dev && partials, GG_ERR_INVALID_ARG, "null argument");
+    int rank = 0, world = 1, log_n = 0;
+    size_t m = hshard_m(hs, &rank, &world, &log_n);
+    GG_CHECK(log_n == pk->log_n, GG_ERR_INVALID_ARG, "hshard and key have different domains");
+    GG_CHECK(pk->z_lo == (size_t)rank * m && pk->nZ == std::min(m, pk->n - 1 - pk->z_lo),
+             GG_ERR_INVALID_ARG, "key shard must own Z positions [rank*m, (rank+1)*m)");
+    std::lock_guard<std::mutex> lk(pk->mu);
+    double t0 = now_ms();
+    G16Partials p;
+    DistH dh{hs, xchg, xchg_ctx, (Fr*)send_dev, (Fr*)recv_dev};
+    prove_device(pk, wires, sol_a, sol_b, sol_c, n_cons, inputs_on_device != 0, nullptr, p, &dh);
     uint8_t* o = (uint8_t*)partials;
     memcpy(o, &p.a, 96);
     memcpy(o + 96, &p.b1, 96);

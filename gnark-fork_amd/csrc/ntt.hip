@@ -546,3 +546,358 @@ void bls_xn_minus_one_inv(gg_domain* big, size_t n_small, void* out) {
 }
 }  // namespace gg
 
+
+// ===========================================================================
+// Distributed computeH over N GPUs (DESIGN.md "Multi-GPU").
+// n = m * N.  Rank k holds the cyclic slice y_k[j] = x[k + N j] of every input
+// vector.  A transform of size n is a local size-m transform (root w^N),
+// a twist by w^(+-k c1), one all-to-all, and m/N size-N transforms per rank:
+//   iFFT:  x_coef[c1 + m c2] = (1/N) sum_k wN^(-k c2) w^(-k c1) iDFT_m(y_k)[c1]
+//   FFT:   E[k + N j] = DFT_m( c1 -> w^(c1 k) sum_c2 wN^(c2 k) x'[c1 + m c2] )[j]
+// Rank r owns the coefficients c1 = bitrev_m(p), p in [r m/N, (r+1) m/N), all
+// c2 < N, so each exchange moves contiguous chunks.  The last step writes h in
+// bit-reversed order: coefficient c1 + m c2 lands at r m + N q + bitrev_N(c2),
+// i.e. rank r holds h_bitrev[r m, (r+1) m) -- the Z slice [r m, (r+1) m) of
+// pk.G1.Z (setup.go:265) -- so the Z-MSM needs no further exchange.
+// Three all-to-alls per proof (a, b, c bundled; then a, b, c again; then h).
+// ===========================================================================
+struct gg_hshard {
+    int log_n = 0, rank = 0, world = 1, log_w = 0, M = 0;
+    size_t n = 0, m = 0, chunk = 0;  // chunk = m / N elements per (rank, poly)
+    std::unique_ptr<DomainT<FrCfg>> loc;  // size-m domain, root w^N
+    Fr invN, invN_den;
+    DevBuf w_hi, w_lo, wi_hi, wi_lo, g_hi, g_lo, gi_hi, gi_lo;  // split power tables over [0, n)
+    int S = 0;
+    Fr wN[16], wNi[16];
+    DevBuf y, full;  // 3 x m local vectors; staging of host inputs
+    DevBuf hblk;     // m elements: h_bitrev[rank m, (rank+1) m)
+    hipStream_t st = nullptr;
+    std::mutex mu;
+    ~gg_hshard() {
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+
+namespace gg {
+struct PowTab {
+    const Fr *hi, *lo;
+    int S;
+    __device__ __forceinline__ Fr at(uint32_t e) const {
+        return load_fr(hi + (e >> S)) * load_fr(lo + (e & ((1u << S) - 1)));
+    }
+};
+
+template <int N>
+struct SmallRoots {
+    Fr fwd[N], inv[N];
+};
+
+// y[j] = x[rank + N j] (zero past len)
+__global__ void k_gather_cyclic(Fr* y, const Fr* x, size_t len, size_t m, int rank, int N) {
+    size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= m) return;
+    size_t i = (size_t)rank + (size_t)N * j;
+    Fr v = i < len ? load_fr(x + i) : Fr::zero();
+    store_fr(y + j, v);
+}
+
+// send[(r * npoly + poly) * chunk + q] = y[p] * w^(sign * rank * bitrev_M(p)), p = r chunk + q
+__global__ void k_twist_scatter(Fr* send, const Fr* y, size_t m, size_t chunk, int M, int npoly,
+                                int poly, uint32_t rank, PowTab tw) {
+    size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= m) return;
+    uint32_t c1 = brev_bits((uint32_t)p, M);
+    Fr v = load_fr(y + p);
+    if (rank) v = v * tw.at(rank * c1);
+    size_t r = p / chunk, q = p - r * chunk;
+    store_fr(send + (r * npoly + poly) * chunk + q, v);
+}
+
+// phase 2: finish the inverse transform (size-N iDFT, 1/N), scale by g^c, start
+// the forward coset transform (size-N DFT, twist w^(c1 k')) -- per (poly, q)
+template <int N>
+__global__ void __launch_bounds__(256) k_cross_fwd(Fr* send, const Fr* recv, size_t chunk, int npoly,
+                                                   int M, uint32_t rank, size_t m, Fr invN,
+                                                   SmallRoots<N> R, PowTab gpow, PowTab wpow) {
+    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= chunk * npoly) return;
+    const int poly = (int)(t / chunk);
+    const size_t q = t - (size_t)poly * chunk;
+    const uint32_t c1 = brev_bits((uint32_t)(rank * chunk + q), M);
+    Fr in[N], co[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) in[k] = load_fr(recv + ((size_t)k * npoly + poly) * chunk + q);
+#pragma unroll
+    for (int c2 = 0; c2 < N; c2++) {
+        Fr acc = in[0];
+#pragma unroll
+        for (int k = 1; k < N; k++) acc = acc + in[k] * R.inv[(k * c2) % N];
+        co[c2] = acc * invN * gpow.at(c1 + (uint32_t)(m * c2));
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < N; k2++) {
+        Fr acc = co[0];
+#pragma unroll
+        for (int c2 = 1; c2 < N; c2++) acc = acc + co[c2] * R.fwd[(c2 * k2) % N];
+        if (k2) acc = acc * wpow.at(c1 * (uint32_t)k2);
+        store_fr(send + ((size_t)k2 * npoly + poly) * chunk + q, acc);
+    }
+}
+
+// y[p] = recv[(r * npoly + poly) * chunk + q], p = r chunk + q
+__global__ void k_unpack(Fr* y, const Fr* recv, size_t m, size_t chunk, int npoly, int poly) {
+    size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= m) return;
+    size_t r = p / chunk, q = p - r * chunk;
+    store_fr(y + p, load_fr(recv + (r * npoly + poly) * chunk + q));
+}
+
+// phase 4: size-N iDFT * den / N * g^-c, written at N q + bitrev_N(c2)
+template <int N>
+__global__ void __launch_bounds__(256) k_cross_inv_out(Fr* h, const Fr* recv, size_t chunk, int M,
+                                                       int logN, uint32_t rank, size_t m, Fr scale,
+                                                       SmallRoots<N> R, PowTab gipow) {
+    size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= chunk) return;
+    const uint32_t c1 = brev_bits((uint32_t)(rank * chunk + q), M);
+    Fr in[N];
+#pragma unroll
+    for (int k = 0; k < N; k++) in[k] = load_fr(recv + (size_t)k * chunk + q);
+#pragma unroll
+    for (int c2 = 0; c2 < N; c2++) {
+        Fr acc = in[0];
+#pragma unroll
+        for (int k = 1; k < N; k++) acc = acc + in[k] * R.inv[(k * c2) % N];
+        acc = acc * scale * gipow.at(c1 + (uint32_t)(m * c2));
+        store_fr(h + (size_t)N * q + brev_bits((uint32_t)c2, logN), acc);
+    }
+}
+
+static void pow_tab_upload(int L, int S, const Fr& x, DevBuf& hi, DevBuf& lo) {
+    std::vector<Fr> h, l;
+    build_pow_tables(L, S, x, Fr::one(), h, l);
+    upload(hi, h);
+    upload(lo, l);
+}
+
+template <int N>
+static void launch_cross_fwd(gg_hshard* hs, Fr* send, const Fr* recv, int npoly, hipStream_t st) {
+    SmallRoots<N> R;
+    for (int i = 0; i < N; i++) { R.fwd[i] = hs->wN[i]; R.inv[i] = hs->wNi[i]; }
+    PowTab gp{hs->g_hi.as<Fr>(), hs->g_lo.as<Fr>(), hs->S};
+    PowTab wp{hs->w_hi.as<Fr>(), hs->w_lo.as<Fr>(), hs->S};
+    hipLaunchKernelGGL(k_cross_fwd<N>, dim3(grid_for(hs->chunk * npoly, 256)), dim3(256), 0, st, send,
+                       recv, hs->chunk, npoly, hs->M, (uint32_t)hs->rank, hs->m, hs->invN, R, gp, wp);
+    GG_HIP(hipGetLastError());
+}
+
+template <int N>
+static void launch_cross_inv(gg_hshard* hs, Fr* h, const Fr* recv, hipStream_t st) {
+    SmallRoots<N> R;
+    for (int i = 0; i < N; i++) { R.fwd[i] = hs->wN[i]; R.inv[i] = hs->wNi[i]; }
+    PowTab gi{hs->gi_hi.as<Fr>(), hs->gi_lo.as<Fr>(), hs->S};
+    hipLaunchKernelGGL(k_cross_inv_out<N>, dim3(grid_for(hs->chunk, 256)), dim3(256), 0, st, h, recv,
+                       hs->chunk, hs->M, hs->log_w, (uint32_t)hs->rank, hs->m, hs->invN_den, R, gi);
+    GG_HIP(hipGetLastError());
+}
+
+// ---- the four local phases (exchanges between them are the caller's) ----
+void hshard_phase1(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len, Fr* send,
+                   hipStream_t st) {
+    const size_t m = hs->m;
+    Fr* y = hs->y.as<Fr>();
+    PowTab twi{hs->wi_hi.as<Fr>(), hs->wi_lo.as<Fr>(), hs->S};
+    const Fr* src[3] = {a, b, c};
+    for (int p = 0; p < 3; p++) {
+        Fr* yp = y + (size_t)p * m;
+        hipLaunchKernelGGL(k_gather_cyclic, dim3(grid_for(m, 256)), dim3(256), 0, st, yp, src[p], len,
+                           m, hs->rank, hs->world);
+        GG_HIP(hipGetLastError());
+        // iDFT_m (DIF: natural -> bit-reversed), 1/m folded in
+        run_transform(hs->loc.get(), yp, yp, false, true, -1, SK_NINV, (const Fr*)nullptr,
+                      (const Fr*)nullptr, st);
+        hipLaunchKernelGGL(k_twist_scatter, dim3(grid_for(m, 256)), dim3(256), 0, st, send, yp, m,
+                           hs->chunk, hs->M, 3, p, (uint32_t)hs->rank, twi);
+        GG_HIP(hipGetLastError());
+    }
+}
+
+void hshard_phase2(gg_hshard* hs, const Fr* recv, Fr* send, hipStream_t st) {
+    switch (hs->world) {
+        case 1: launch_cross_fwd<1>(hs, send, recv, 3, st); break;
+        case 2: launch_cross_fwd<2>(hs, send, recv, 3, st); break;
+        case 4: launch_cross_fwd<4>(hs, send, recv, 3, st); break;
+        case 8: launch_cross_fwd<8>(hs, send, recv, 3, st); break;
+        case 16: launch_cross_fwd<16>(hs, send, recv, 3, st); break;
+        default: throw Error(GG_ERR_UNSUPPORTED, "distributed computeH: world must be 1, 2, 4, 8 or 16");
+    }
+}
+
+void hshard_phase3(gg_hshard* hs, const Fr* recv, Fr* send, hipStream_t st) {
+    const size_t m = hs->m;
+    Fr* y = hs->y.as<Fr>();
+    const Fr* nul = nullptr;
+    for (int p = 0; p < 3; p++) {
+        hipLaunchKernelGGL(k_unpack, dim3(grid_for(m, 256)), dim3(256), 0, st, y + (size_t)p * m, recv, m,
+                           hs->chunk, 3, p);
+        GG_HIP(hipGetLastError());
+    }
+    // coset evaluations on this rank's points g w^(rank + N j) (DIT: bit-reversed -> natural);
+    // the last pass of c's transform emits a*b - c (PolyOps)
+    run_transform(hs->loc.get(), y, y, true, false, -1, -1, nul, nul, st);
+    run_transform(hs->loc.get(), y + m, y + m, true, false, -1, -1, nul, nul, st);
+    run_transform(hs->loc.get(), y + 2 * m, y + 2 * m, true, false, -1, -1, y, y + m, st);
+    // inverse of the quotient evaluations: iDFT_m, then twist w^(-rank c1)
+    run_transform(hs->loc.get(), y + 2 * m, y + 2 * m, false, true, -1, SK_NINV, nul, nul, st);
+    PowTab twi{hs->wi_hi.as<Fr>(), hs->wi_lo.as<Fr>(), hs->S};
+    hipLaunchKernelGGL(k_twist_scatter, dim3(grid_for(m, 256)), dim3(256), 0, st, send, y + 2 * m, m,
+                       hs->chunk, hs->M, 1, 0, (uint32_t)hs->rank, twi);
+    GG_HIP(hipGetLastError());
+}
+
+void hshard_phase4(gg_hshard* hs, const Fr* recv, Fr* h, hipStream_t st) {
+    switch (hs->world) {
+        case 1: launch_cross_inv<1>(hs, h, recv, st); break;
+        case 2: launch_cross_inv<2>(hs, h, recv, st); break;
+        case 4: launch_cross_inv<4>(hs, h, recv, st); break;
+        case 8: launch_cross_inv<8>(hs, h, recv, st); break;
+        case 16: launch_cross_inv<16>(hs, h, recv, st); break;
+        default: throw Error(GG_ERR_UNSUPPORTED, "distributed computeH: world must be 1, 2, 4, 8 or 16");
+    }
+}
+
+size_t hshard_m(const gg_hshard* hs, int* rank, int* world, int* log_n) {
+    *rank = hs->rank;
+    *world = hs->world;
+    *log_n = hs->log_n;
+    return hs->m;
+}
+Fr* hshard_h(gg_hshard* hs) { return hs->hblk.as<Fr>(); }
+
+size_t hshard_exchange_bytes(const gg_hshard* hs, int phase) {
+    return hs->chunk * 32 * (phase == 3 ? 1 : 3);
+}
+
+gg_hshard* hshard_create(int log_n, const void* omega_mont, const void* coset_gen_mont, int rank, int world) {
+    GG_CHECK(omega_mont && coset_gen_mont, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(world >= 1 && world <= 16 && (world & (world - 1)) == 0, GG_ERR_UNSUPPORTED,
+             "distributed computeH: world must be a power of two <= 16");
+    GG_CHECK(rank >= 0 && rank < world, GG_ERR_INVALID_ARG, "rank out of range");
+    int lw = 0;
+    while ((1 << lw) < world) lw++;
+    GG_CHECK(log_n >= 1 && log_n <= 28 && log_n >= 2 * lw, GG_ERR_INVALID_ARG,
+             "distributed computeH needs 2^log_n >= world^2");
+    std::unique_ptr<gg_hshard> hs(new gg_hshard());
+    hs->log_n = log_n;
+    hs->rank = rank;
+    hs->world = world;
+    hs->log_w = lw;
+    hs->n = (size_t)1 << log_n;
+    hs->M = log_n - lw;
+    hs->m = hs->n >> lw;
+    hs->chunk = hs->m >> lw;
+    Fr w, g;
+    memcpy(w.v, omega_mont, 32);
+    memcpy(g.v, coset_gen_mont, 32);
+    Fr wm = pow_u64(w, (uint64_t)world);
+    hs->loc.reset(domain_build<FrCfg>(hs->M, wm.v, g.v));  // checks the order of w^N = m
+    // w must have order exactly n: w^(n/2) != 1 (w^N already has order m)
+    GG_CHECK(!(pow_u64(w, hs->n / 2) == Fr::one()), GG_ERR_INVALID_ARG, "omega order < n");
+    GG_CHECK(pow_u64(w, hs->n) == Fr::one(), GG_ERR_INVALID_ARG, "omega^n != 1");
+    Fr wNroot = pow_u64(w, hs->m);  // primitive N-th root
+    Fr wNinv = inverse(wNroot);
+    Fr a = Fr::one(), b = Fr::one();
+    for (int i = 0; i < 16; i++) {
+        hs->wN[i] = a;
+        hs->wNi[i] = b;
+        a = a * wNroot;
+        b = b * wNinv;
+    }
+    Fr nn = Fr::zero();
+    nn.v[0] = (uint32_t)world;
+    hs->invN = inverse(to_mont(nn));
+    Fr gn = pow_u64(g, hs->n) - Fr::one();
+    GG_CHECK(!gn.is_zero(), GG_ERR_INVALID_ARG, "g^n == 1: coset generator in the domain");
+    hs->invN_den = hs->invN * inverse(gn);
+    hs->S = (log_n + 1) / 2;
+    pow_tab_upload(log_n, hs->S, w, hs->w_hi, hs->w_lo);
+    pow_tab_upload(log_n, hs->S, inverse(w), hs->wi_hi, hs->wi_lo);
+    pow_tab_upload(log_n, hs->S, g, hs->g_hi, hs->g_lo);
+    pow_tab_upload(log_n, hs->S, inverse(g), hs->gi_hi, hs->gi_lo);
+    hs->y.alloc(3 * hs->m * 32);
+    hs->hblk.alloc(hs->m * 32);
+    GG_HIP(hipStreamCreateWithFlags(&hs->st, hipStreamNonBlocking));
+    return hs.release();
+}
+
+// Whole distributed computeH on this rank; xchg(ctx, send, recv, bytes_per_rank)
+// performs the all-to-all (blocking).  a/b/c: full vectors on the device.
+void hshard_run(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len, Fr* send, Fr* recv,
+                gg_exchange_fn xchg, void* ctx, hipStream_t st) {
+    auto exchange = [&](int phase) {
+        GG_HIP(hipStreamSynchronize(st));
+        int rc = xchg(ctx, send, recv, hshard_exchange_bytes(hs, phase));
+        GG_CHECK(rc == 0, GG_ERR_INTERNAL, "exchange callback failed");
+    };
+    hshard_phase1(hs, a, b, c, len, send, st);
+    exchange(1);
+    hshard_phase2(hs, recv, send, st);
+    exchange(2);
+    hshard_phase3(hs, recv, send, st);
+    exchange(3);
+    hshard_phase4(hs, recv, hs->hblk.as<Fr>(), st);
+}
+}  // namespace gg
+
+extern "C" int gg_hshard_create(int log_n, const void* omega_mont, const void* coset_gen_mont, int rank,
+                                int world, gg_hshard_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out, GG_ERR_INVALID_ARG, "null argument");
+    *out = hshard_create(log_n, omega_mont, coset_gen_mont, rank, world);
+    GG_CAPI_END
+}
+
+extern "C" int gg_hshard_release(gg_hshard_t hs) {
+    GG_CAPI_BEGIN
+    delete hs;
+    GG_CAPI_END
+}
+
+extern "C" int gg_hshard_info(gg_hshard_t hs, size_t* m, size_t* exchange_bytes) {
+    GG_CAPI_BEGIN
+    GG_CHECK(hs, GG_ERR_INVALID_ARG, "null argument");
+    if (m) *m = hs->m;
+    if (exchange_bytes) *exchange_bytes = hs->world * hshard_exchange_bytes(hs, 1);
+    GG_CAPI_END
+}
+
+extern "C" int gg_hshard_phase(gg_hshard_t hs, int phase, const void* a, const void* b, const void* c,
+                               size_t len, int inputs_on_device, const void* recv, void* send_or_h,
+                               void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(hs && send_or_h, GG_ERR_INVALID_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(hs->mu);
+    hipStream_t st = pick_stream(hip_stream);
+    if (phase == 1) {
+        GG_CHECK(a && b && c, GG_ERR_INVALID_ARG, "null input");
+        GG_CHECK(len <= hs->n, GG_ERR_INVALID_ARG, "len > domain cardinality");
+        const Fr* src[3] = {(const Fr*)a, (const Fr*)b, (const Fr*)c};
+        if (!inputs_on_device) {
+            hs->full.reserve(3 * std::max<size_t>(len, 1) * 32);
+            for (int i = 0; i < 3; i++) {
+                Fr* d = hs->full.as<Fr>() + i * len;
+                if (len) GG_HIP(hipMemcpyAsync(d, src[i], len * 32, hipMemcpyHostToDevice, st));
+                src[i] = d;
+            }
+        }
+        hshard_phase1(hs, src[0], src[1], src[2], len, (Fr*)send_or_h, st);
+    } else {
+        GG_CHECK(recv, GG_ERR_INVALID_ARG, "null recv");
+        if (phase == 2) hshard_phase2(hs, (const Fr*)recv, (Fr*)send_or_h, st);
+        else if (phase == 3) hshard_phase3(hs, (const Fr*)recv, (Fr*)send_or_h, st);
+        else if (phase == 4) hshard_phase4(hs, (const Fr*)recv, (Fr*)send_or_h, st);
+        else throw Error(GG_ERR_INVALID_ARG, "phase must be 1..4");
+    }
+    GG_HIP(hipStreamSynchronize(st));
+    GG_CAPI_END
+}

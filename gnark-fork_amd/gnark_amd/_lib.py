@@ -17,6 +17,11 @@ GG_CURVE_BN254, GG_CURVE_BLS12_381 = 0, 1
 GG_DIF, GG_DIT = 0, 1
 
 
+# gg_exchange_fn (include/gnark_amd.h): all-to-all supplied by the caller
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_size_t)
+
+
 class GnarkAmdError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"gnark_amd error {code}: {msg}")
@@ -67,6 +72,11 @@ def _load():
                                         S, P, S, S, PP], I),
         "gg_groth16_prove_partial": ([P, P, S, P, P, P, S, I, P, P], I),
         "gg_groth16_finalize": ([P, P, P, P, P, P, P, P, P, P, P], I),
+        "gg_hshard_create": ([I, P, P, I, I, PP], I),
+        "gg_hshard_release": ([P], I),
+        "gg_hshard_info": ([P, ctypes.POINTER(S), ctypes.POINTER(S)], I),
+        "gg_hshard_phase": ([P, I, P, P, P, S, I, P, P, P], I),
+        "gg_groth16_prove_partial_dist": ([P, P, P, S, P, P, P, S, I, EXCHANGE_FN, P, P, P, P], I),
         "gg_batch_scalar_mul": ([I, P, P, S, I, P, I], I),
         "gg_plonk_numerator_coset": ([ctypes.POINTER(ctypes.c_void_p), I, P, ctypes.POINTER(I), P,
                                       P, P, P, P, S, I, I, P, P], I),
@@ -95,7 +105,8 @@ EXPORTED = [
     "gg_groth16_prove", "gg_groth16_last_timings", "gg_batch_scalar_mul", "gg_profile_enable",
     "gg_plonk_numerator_coset", "gg_plonk_divide_by_xn_minus_one", "gg_bls12_381_fr_batch_invert",
     "gg_profile_get", "gg_groth16_pk_create_shard", "gg_groth16_prove_partial",
-    "gg_groth16_finalize",
+    "gg_groth16_finalize", "gg_hshard_create", "gg_hshard_release", "gg_hshard_info",
+    "gg_hshard_phase", "gg_groth16_prove_partial_dist",
 ]
 
 

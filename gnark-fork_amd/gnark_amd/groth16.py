@@ -166,12 +166,24 @@ class KeyShard:
     k_wire_index: Optional[np.ndarray]  # absolute wire ids of g1_K (None = default numbering)
 
 
+def dist_h_supported(n: int, world: int) -> bool:
+    """The distributed computeH (gg_hshard_*) needs world a power of two <= 16
+    and n >= world^2."""
+    return 1 <= world <= 16 and world & (world - 1) == 0 and n >= 2 and n >= world * world
+
+
 def shard_ranges(n_wires: int, n: int, rank: int, world: int):
     """(wire_lo, wire_hi, z_lo, z_hi) of `rank`: contiguous balanced slices of the
-    wires and of the n - 1 Z positions."""
+    wires; Z positions [rank m, (rank+1) m) (m = n / world, the h block the
+    distributed computeH leaves on this rank) when dist_h_supported, else a
+    balanced slice of the n - 1 positions."""
     from .dist import shard_range
     lo, hi = shard_range(n_wires, rank, world)
-    zl, zh = shard_range(max(n - 1, 0), rank, world)
+    if dist_h_supported(n, world):
+        m = n // world
+        zl, zh = min(rank * m, n - 1), min((rank + 1) * m, n - 1)
+    else:
+        zl, zh = shard_range(max(n - 1, 0), rank, world)
     return lo, hi, zl, zh
 
 
@@ -290,3 +302,97 @@ def gather_and_finalize(data: ProvingKeyData, part: bytes, r: bytes, s: bytes, d
         tdist.all_gather(bufs, t)
         part = add_partials([bytes(b.cpu().numpy()) for b in bufs])
     return finalize(data, part, r, s)
+
+
+# ------------------------------------------------- distributed computeH
+class HShard:
+    """This rank's part of the distributed computeH (gg_hshard_*): three
+    all-to-alls per proof instead of h computed on every GPU."""
+
+    def __init__(self, log_n: int, rank: int, world: int, omega: bytes = None, gen: bytes = None):
+        omega = omega or fr.fr_mont(fr.domain_generator(log_n))
+        gen = gen or fr.fr_mont(fr.FR_MULTIPLICATIVE_GEN)
+        h = ctypes.c_void_p()
+        check(lib.gg_hshard_create(log_n, ptr(omega), ptr(gen), rank, world, ctypes.byref(h)))
+        self.handle, self.log_n, self.rank, self.world = h, log_n, rank, world
+        m, xb = ctypes.c_size_t(), ctypes.c_size_t()
+        check(lib.gg_hshard_info(h, ctypes.byref(m), ctypes.byref(xb)))
+        self.m, self.exchange_bytes = m.value, xb.value
+
+    def phase(self, k: int, a=None, b=None, c=None, length: int = 0, on_device: bool = False,
+              recv=None, out=None):
+        check(lib.gg_hshard_phase(self.handle, k, ptr(a), ptr(b), ptr(c), length, int(on_device),
+                                  ptr(recv), ptr(out), None))
+
+    def close(self):
+        if self.handle:
+            lib.gg_hshard_release(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def prove_partial_dist(pk: ProvingKeyShard, hs: HShard, solution: Solution, exchange, send, recv) -> bytes:
+    """gg_groth16_prove_partial_dist: shard partials with the distributed computeH.
+    exchange(send_ptr, recv_ptr, bytes_per_rank) performs the all-to-all."""
+    import traceback
+    from ._lib import EXCHANGE_FN
+
+    def _cb(ctx, s_ptr, r_ptr, nbytes):
+        try:
+            exchange(s_ptr, r_ptr, nbytes)
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return 1
+
+    cb = EXCHANGE_FN(_cb)
+    out = bytearray(PARTIALS_BYTES)
+    check(lib.gg_groth16_prove_partial_dist(
+        pk.handle, hs.handle, ptr(solution.W), solution.n_wires, ptr(solution.A), ptr(solution.B),
+        ptr(solution.C), solution.n_constraints, int(solution.on_device), cb, None, ptr(send),
+        ptr(recv), ptr(out)))
+    return bytes(out)
+
+
+class TorchExchange:
+    """All-to-all over torch.distributed for the distributed computeH: RCCL
+    (backend "nccl") on device buffers, or gloo through host staging."""
+
+    def __init__(self, nbytes: int, device):
+        import torch
+        import torch.distributed as tdist
+        self.dev = torch.device(device)
+        self.send = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+        self.recv = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
+        self.gloo = tdist.get_backend() != "nccl"
+        self.world = tdist.get_world_size()
+
+    def __call__(self, s_ptr, r_ptr, nbytes):
+        import torch
+        import torch.distributed as tdist
+        total = nbytes * self.world
+        s, r = self.send[:total], self.recv[:total]
+        with torch.cuda.device(self.dev):
+            if self.gloo:
+                rc = torch.empty(total, dtype=torch.uint8)
+                tdist.all_to_all_single(rc, s.cpu())
+                r.copy_(rc)
+            else:
+                tdist.all_to_all_single(r, s)
+            torch.cuda.current_stream(self.dev).synchronize()
+
+
+def prove_distributed_h(pk: ProvingKeyShard, hs: HShard, xchg: TorchExchange, solution: Solution,
+                        *opts, r: bytes, s: bytes, device=None) -> Proof:
+    """Multi-GPU Prove with the distributed computeH: per-rank partials (three
+    all-to-alls inside), all-gather of the 576-B partials, exact sum, combination."""
+    cfg = backend.new_prover_config(*opts)
+    if not backend.accelerated(cfg):
+        raise RuntimeError("accelerated prover requested without with_amd_acceleration()")
+    part = prove_partial_dist(pk, hs, solution, xchg, xchg.send.data_ptr(), xchg.recv.data_ptr())
+    return gather_and_finalize(pk.data, part, r, s, device)

@@ -53,6 +53,13 @@ extern "C" {
 typedef struct gg_domain *gg_domain_t;
 typedef struct gg_msm_base *gg_msm_base_t;
 typedef struct gg_groth16_pk *gg_groth16_pk_t;
+typedef struct gg_hshard *gg_hshard_t;
+/* All-to-all exchange supplied by the caller's transport (RCCL over xGMI via
+ * torch.distributed, or a Go RCCL binding): chunk r (bytes_per_rank bytes) of
+ * send_dev goes to rank r, chunk k of recv_dev comes from rank k.  Device
+ * buffers; must not return before recv_dev holds the data.  0 = success. */
+typedef int (*gg_exchange_fn)(void *ctx, const void *send_dev, void *recv_dev,
+                              size_t bytes_per_rank);
 
 /* ---------------------------------------------------------------- runtime */
 const char *gg_last_error(void);
@@ -218,6 +225,35 @@ int gg_groth16_finalize(const void *alpha1, const void *beta1, const void *delta
                         const void *beta2, const void *delta2, const void *partials,
                         const void *r_mont, const void *s_mont, void *ar_aff, void *bs_aff,
                         void *krs_aff);
+
+/* ---- distributed computeH ("four-step multi-GPU NTT").
+ * n = 2^log_n = m * world (world a power of two <= 16, n >= world^2).  Rank r
+ * computes the local transforms of the cyclic slices x[r + world*j] and, after
+ * three all-to-alls, holds h_bitrev[r*m, (r+1)*m): exactly the Z positions of
+ * its key shard (gg_groth16_pk_create_shard with z_lo = r*m).
+ * gg_hshard_info: m and the size of the send / recv device buffers the caller
+ * provides (bytes, all ranks' chunks).
+ * gg_hshard_phase (the building blocks, synchronous on hip_stream):
+ *   1: a, b, c (len <= n, full vectors, host or device per inputs_on_device)
+ *      -> send;   2: recv -> send;   3: recv -> send;   4: recv -> h (m fr)
+ * with an all-to-all send -> recv between consecutive phases. */
+int gg_hshard_create(int log_n, const void *omega_mont, const void *coset_gen_mont, int rank,
+                     int world, gg_hshard_t *out);
+int gg_hshard_release(gg_hshard_t hs);
+int gg_hshard_info(gg_hshard_t hs, size_t *m, size_t *exchange_bytes);
+int gg_hshard_phase(gg_hshard_t hs, int phase, const void *a, const void *b, const void *c,
+                    size_t len, int inputs_on_device, const void *recv, void *send_or_h,
+                    void *hip_stream);
+/* gg_groth16_prove_partial with the distributed computeH: the H task runs the
+ * four phases on this rank, calling xchg(ctx, send_dev, recv_dev, bytes) for
+ * the three exchanges while the A/B1/K/G2 MSMs run on other streams; the
+ * Z-MSM then uses the local h block.  pk must be the shard with wires of this
+ * rank and z_lo = rank*m.  send_dev / recv_dev: gg_hshard_info bytes each. */
+int gg_groth16_prove_partial_dist(gg_groth16_pk_t pk, gg_hshard_t hs, const void *wires,
+                                  size_t n_wires, const void *sol_a, const void *sol_b,
+                                  const void *sol_c, size_t n_cons, int inputs_on_device,
+                                  gg_exchange_fn xchg, void *xchg_ctx, void *send_dev,
+                                  void *recv_dev, void *partials);
 
 /* per-stage timings (ms) of the last gg_groth16_prove on this thread:
  * [0]=upload [1]=computeH [2]=msm_A [3]=msm_B1 [4]=msm_K [5]=msm_Z [6]=msm_G2
