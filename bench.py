@@ -456,12 +456,23 @@ def groth16_bench_sharded(log_n, rank, world, dist, xdev, barrier, reps=3):
     sol = groth16.Solution(wires, sa, sb, sc, n_wires, ncons, on_device=True)
     r, s = fr_const(12345), fr_const(67890)
     opt = backend.with_amd_acceleration()
-    groth16.prove_distributed(pk, sol, opt, r=r, s=s, device=xdev)
+    use_dist_h = groth16.dist_h_supported(n, world)
+    if use_dist_h:
+        # computeH split over the GPUs: three all-to-alls of n/N^2 x 32 B chunks per proof
+        hs = groth16.HShard(log_n, rank, world)
+        xchg = groth16.TorchExchange(hs.exchange_bytes, torch.device("cuda", torch.cuda.current_device()))
+
+        def prove_once():
+            return groth16.prove_distributed_h(pk, hs, xchg, sol, opt, r=r, s=s, device=xdev)
+    else:
+        def prove_once():
+            return groth16.prove_distributed(pk, sol, opt, r=r, s=s, device=xdev)
+    prove_once()
     ts = []
     for _ in range(reps):
         barrier()
         t = time.perf_counter()
-        pr = groth16.prove_distributed(pk, sol, opt, r=r, s=s, device=xdev)
+        pr = prove_once()
         barrier()
         el = time.perf_counter() - t
         tt = torch.tensor([el], dtype=torch.float64, device=xdev)
@@ -476,8 +487,10 @@ def groth16_bench_sharded(log_n, rank, world, dist, xdev, barrier, reps=3):
     return {"log_n": log_n, "n_gpus": world, "n_constraints": ncons, "n_wires": n_wires,
             "prove_ms": min(ts), "prove_ms_all": ts, "constraints_per_s": ncons / (min(ts) * 1e-3),
             "rank0_stage_ms": tim, "key_setup_s": t_setup, "proof_identical_on_all_ranks": same,
-            "sharding": "wires [lo,hi) of A/B1/K/G2 and Z positions per GPU; h on every GPU; "
-                        "576-B partials all-gathered", "inputs": "resident in HBM"}
+            "sharding": "wires [lo,hi) of A/B1/K/G2 and Z positions per GPU; 576-B partials all-gathered",
+            "compute_h": ("distributed: local n/N transforms + 3 all-to-alls (gg_hshard)" if use_dist_h
+                          else "replicated on every GPU"),
+            "inputs": "resident in HBM"}
 
 
 def fr_const(v):
