@@ -130,6 +130,16 @@ __global__ void __launch_bounds__(256) k_batch_invert(FrB* a, size_t n, size_t T
     }
 }
 
+// fr.BatchInvert on device memory (synchronous: the prefix scratch is freed on return)
+void bls_batch_invert(FrB* a, size_t n, hipStream_t st) {
+    if (n == 0) return;
+    const size_t T = std::min<size_t>(n, std::max<size_t>(16384, n / 64));
+    DevBuf prefix(n * 32);
+    hipLaunchKernelGGL(k_batch_invert, dim3(grid_for(T, 256)), dim3(256), 0, st, a, n, T, prefix.as<FrB>());
+    GG_HIP(hipGetLastError());
+    GG_HIP(hipStreamSynchronize(st));
+}
+
 }  // namespace gg
 
 using namespace gg;
@@ -210,11 +220,6 @@ extern "C" int gg_bls12_381_fr_batch_invert(void* data_dev, size_t n, void* hip_
     GG_CHECK(data_dev || n == 0, GG_ERR_INVALID_ARG, "null argument");
     if (n == 0) return GG_OK;
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : hipStreamPerThread;
-    const size_t T = std::min<size_t>(n, std::max<size_t>(16384, n / 64));
-    DevBuf prefix(n * 32);
-    hipLaunchKernelGGL(k_batch_invert, dim3(grid_for(T, 256)), dim3(256), 0, st, (FrB*)data_dev, n, T,
-                       prefix.as<FrB>());
-    GG_HIP(hipGetLastError());
-    GG_HIP(hipStreamSynchronize(st));
+    bls_batch_invert((FrB*)data_dev, n, st);
     GG_CAPI_END
 }

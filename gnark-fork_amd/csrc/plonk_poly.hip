@@ -1,0 +1,410 @@
+// PlonK BLS12-381 polynomial kernels of SURVEY 8a row a21 (fr, 32 B Montgomery):
+//
+//   gg_plonk_ratio_copy_constraint  iop.BuildRatioCopyConstraint (prove.go:600-621):
+//        Z[0] = 1, Z[i+1] = Z[i] * prod_j (f_j[i] + b*ID(j n + i) + g)
+//                                / prod_j (f_j[i] + b*ID(S[j n + i]) + g)
+//        with the permutation support ID(s) = u^(s div n) w^(s mod n)
+//        (getSupportPermutation, setup.go:391-407; u = FrMultiplicativeGen)
+//   gg_bls12_381_fr_prefix_product  inclusive running product (the Z recurrence)
+//   gg_bls12_381_fr_horner          Polynomial.Evaluate (Horner) and the KZG
+//        opening quotient (f - f(a)) / (X - a) (kzg.Open, prove.go:646, 823-830)
+//   gg_plonk_fold_h                 foldH (prove.go:670-705)
+//   gg_plonk_linearized             computeLinearizedPolynomial (prove.go:1289-1389)
+//
+// The two recurrences (running product; x_k = y_k + u x_(k-1)) are scans:
+// 8 elements per thread in registers, a Hillis-Steele scan of the 256 thread
+// aggregates in LDS, block aggregates scanned recursively (2048 per level),
+// then one fix-up pass.  Horner runs the affine scan over the reversed vector.
+#include "common.h"
+#include "field.cuh"
+#include "prof.h"
+#include <vector>
+#include <cstring>
+
+namespace gg {
+
+using FrB = FrBls;
+void bls_batch_invert(FrB* a, size_t n, hipStream_t st);
+
+namespace {
+__device__ __forceinline__ FrB ldb(const FrB* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    uint4 a = q[0], b = q[1];
+    FrB r;
+    r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+    r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+    return r;
+}
+__device__ __forceinline__ void stb(FrB* p, const FrB& r) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    q[0] = make_uint4(r.v[0], r.v[1], r.v[2], r.v[3]);
+    q[1] = make_uint4(r.v[4], r.v[5], r.v[6], r.v[7]);
+}
+}  // namespace
+
+constexpr int SCAN_PER = 8;                    // elements per thread
+constexpr int SCAN_BLK = 256 * SCAN_PER;       // elements per block
+enum { SCAN_PROD = 0, SCAN_AFFINE = 1 };
+
+// powers of the affine multiplier u of one scan level
+struct ScanPow {
+    FrB p[SCAN_PER + 1];  // u^0 .. u^8
+    FrB step[8];          // u^(8 * 2^d): block-scan combine at offset 2^d threads
+    const FrB* lo;        // u^i, i < 64
+    const FrB* hi;        // u^(64 j), j <= 32
+};
+
+// In place: inclusive scan of each 2048-element block; aux[b] = block aggregate.
+template <int MODE>
+__global__ void __launch_bounds__(256) k_scan_local(FrB* x, size_t m, ScanPow P, FrB* aux) {
+    __shared__ uint32_t sh[256 * 8];
+    const size_t base = (size_t)blockIdx.x * SCAN_BLK + (size_t)threadIdx.x * SCAN_PER;
+    FrB v[SCAN_PER];
+    const FrB id = MODE == SCAN_PROD ? FrB::one() : FrB::zero();
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) v[k] = base + k < m ? ldb(x + base + k) : id;
+#pragma unroll
+    for (int k = 1; k < SCAN_PER; k++) v[k] = MODE == SCAN_PROD ? v[k] * v[k - 1] : v[k] + P.p[1] * v[k - 1];
+    FrB agg = v[SCAN_PER - 1];
+    // Hillis-Steele over the 256 thread aggregates (LDS, limb-major: no bank conflicts)
+    auto put = [&](const FrB& a) {
+#pragma unroll
+        for (int l = 0; l < 8; l++) sh[l * 256 + threadIdx.x] = a.v[l];
+    };
+    auto get = [&](int t) {
+        FrB a;
+#pragma unroll
+        for (int l = 0; l < 8; l++) a.v[l] = sh[l * 256 + t];
+        return a;
+    };
+    put(agg);
+    __syncthreads();
+#pragma unroll 1
+    for (int d = 0; d < 8; d++) {
+        const int off = 1 << d;
+        FrB o = id;
+        const bool has = (int)threadIdx.x >= off;
+        if (has) o = get(threadIdx.x - off);
+        __syncthreads();
+        if (has) agg = MODE == SCAN_PROD ? agg * o : agg + P.step[d] * o;
+        put(agg);
+        __syncthreads();
+    }
+    // carry-in = inclusive aggregate of the previous thread
+    if (threadIdx.x > 0) {
+        const FrB c = get(threadIdx.x - 1);
+#pragma unroll
+        for (int k = 0; k < SCAN_PER; k++) v[k] = MODE == SCAN_PROD ? v[k] * c : v[k] + P.p[k + 1] * c;
+    }
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++)
+        if (base + k < m) stb(x + base + k, v[k]);
+    if (threadIdx.x == 255 && aux) stb(aux + blockIdx.x, agg);
+}
+
+// x[e] (block b > 0) combined with the inclusive aggregate of blocks < b
+template <int MODE>
+__global__ void __launch_bounds__(256) k_scan_fix(FrB* x, size_t m, ScanPow P, const FrB* aux) {
+    const size_t b = blockIdx.x + 1;
+    const FrB c = ldb(aux + b - 1);
+    const uint32_t o0 = threadIdx.x * SCAN_PER;
+    const size_t base = b * SCAN_BLK + o0;
+    FrB f;
+    if (MODE == SCAN_AFFINE) {
+        const uint32_t e = o0 + 1;  // u^(offset + 1)
+        f = ldb(P.hi + (e >> 6)) * ldb(P.lo + (e & 63)) * c;
+    }
+#pragma unroll
+    for (int k = 0; k < SCAN_PER; k++) {
+        if (base + k >= m) break;
+        FrB v = ldb(x + base + k);
+        if (MODE == SCAN_PROD) v = v * c;
+        else {
+            v = v + f;
+            f = f * P.p[1];
+        }
+        stb(x + base + k, v);
+    }
+}
+
+// host: powers of u for one level (u = 1 for the product scan, unused)
+static void scan_pow_host(const FrB& u, ScanPow& P, std::vector<FrB>& tab) {
+    P.p[0] = FrB::one();
+    for (int k = 1; k <= SCAN_PER; k++) P.p[k] = P.p[k - 1] * u;
+    FrB s = P.p[SCAN_PER];
+    for (int d = 0; d < 8; d++) {
+        P.step[d] = s;
+        s = s * s;
+    }
+    tab.resize(64 + 33);
+    tab[0] = FrB::one();
+    for (int i = 1; i < 64; i++) tab[i] = tab[i - 1] * u;
+    FrB u64 = tab[63] * u;
+    tab[64] = FrB::one();
+    for (int j = 1; j < 33; j++) tab[64 + j] = tab[64 + j - 1] * u64;
+}
+
+// recursive in-place scan of x[0..m); u: multiplier of this level (affine)
+template <int MODE>
+static void scan_rec(FrB* x, size_t m, const FrB& u, hipStream_t st, std::vector<DevBuf>& keep) {
+    ScanPow P{};
+    std::vector<FrB> tab;
+    scan_pow_host(u, P, tab);
+    if (MODE == SCAN_AFFINE) {
+        keep.emplace_back(tab.size() * 32);
+        GG_HIP(hipMemcpyAsync(keep.back().p, tab.data(), tab.size() * 32, hipMemcpyHostToDevice, st));
+        P.lo = keep.back().as<FrB>();
+        P.hi = P.lo + 64;
+    }
+    const size_t nblk = (m + SCAN_BLK - 1) / SCAN_BLK;
+    FrB* aux = nullptr;
+    if (nblk > 1) {
+        keep.emplace_back(nblk * 32);
+        aux = keep.back().as<FrB>();
+    }
+    hipLaunchKernelGGL(k_scan_local<MODE>, dim3((unsigned)nblk), dim3(256), 0, st, x, m, P, aux);
+    GG_HIP(hipGetLastError());
+    if (nblk <= 1) return;
+    // the next level's elements each stand for SCAN_BLK of this level: u^2048
+    FrB un = u;
+    for (int i = 0; i < 11; i++) un = un * un;
+    scan_rec<MODE>(aux, nblk, un, st, keep);
+    hipLaunchKernelGGL(k_scan_fix<MODE>, dim3((unsigned)(nblk - 1)), dim3(256), 0, st, x, m, P, aux);
+    GG_HIP(hipGetLastError());
+}
+
+template <int MODE>
+static void scan_run(FrB* x, size_t m, const FrB& u, hipStream_t st) {
+    if (m == 0) return;
+    std::vector<DevBuf> keep;
+    keep.reserve(16);
+    scan_rec<MODE>(x, m, u, st, keep);
+    GG_HIP(hipStreamSynchronize(st));  // scratch lifetime
+}
+
+__global__ void k_reverse_copy(FrB* dst, const FrB* src, size_t n) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) stb(dst + i, ldb(src + n - 1 - i));
+}
+
+// q[j] = g[n-2-j] for j < n-1 where g is the reversed affine scan
+__global__ void k_quotient_out(FrB* q, const FrB* g, size_t n) {
+    size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j + 1 < n) stb(q + j, ldb(g + n - 2 - j));
+}
+
+// ---------------------------------------------------------------- ratio
+struct PowSplit {  // x^e = hi[e >> S] * lo[e & (2^S - 1)]
+    const FrB *hi, *lo;
+    int S;
+    __device__ __forceinline__ FrB at(uint32_t e) const {
+        return ldb(hi + (e >> S)) * ldb(lo + (e & ((1u << S) - 1)));
+    }
+};
+
+__global__ void __launch_bounds__(256) k_ratio_numden(const FrB* L, const FrB* R, const FrB* O,
+                                                      const int64_t* perm, uint32_t n, int log_n,
+                                                      FrB beta, FrB gamma, FrB u, FrB uu, PowSplit w,
+                                                      FrB* num, FrB* den) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (i == 0) {
+        stb(num, FrB::one());
+        stb(den, FrB::one());
+    }
+    if (i + 1 >= n) return;
+    const FrB* f[3] = {L, R, O};
+    const FrB wi = w.at(i);
+    FrB b = FrB::one(), d = FrB::one();
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const FrB fv = ldb(f[j] + i);
+        FrB id = j == 0 ? wi : (j == 1 ? wi * u : wi * uu);
+        b = b * (fv + beta * id + gamma);
+        const uint64_t s = (uint64_t)perm[(size_t)j * n + i];
+        const uint32_t blk = (uint32_t)(s >> log_n), off = (uint32_t)(s & (n - 1));
+        FrB sg = w.at(off);
+        if (blk == 1) sg = sg * u;
+        else if (blk == 2) sg = sg * uu;
+        d = d * (fv + beta * sg + gamma);
+    }
+    stb(num + i + 1, b);
+    stb(den + i + 1, d);
+}
+
+__global__ void k_mul_inplace(FrB* a, const FrB* b, size_t n) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) stb(a + i, ldb(a + i) * ldb(b + i));
+}
+
+// ---------------------------------------------------------------- foldH / linearized
+__global__ void k_fold_h(const FrB* h, size_t np2, FrB z, FrB* out) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= np2) return;
+    FrB t = ldb(h + 2 * np2 + i) * z + ldb(h + np2 + i);
+    stb(out + i, t * z + ldb(h + i));
+}
+
+constexpr int MAX_CMT = 8;
+struct LinParams {
+    FrB* z;  // blinded Z canonical, in/out
+    size_t nz;
+    const FrB* s3;
+    size_t ns3;
+    const FrB *ql, *qr, *qm, *qo, *qk;
+    size_t nq;
+    const FrB* pi2[MAX_CMT];
+    FrB qcp[MAX_CMT];
+    int ncmt;
+    FrB s1, s2, alpha, l, r, rl, o, lag;
+};
+
+// prove.go:1347-1386, term by term
+__global__ void __launch_bounds__(256) k_linearized(LinParams P) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.nz) return;
+    const FrB zi = ldb(P.z + i);
+    FrB t = zi * P.s2;
+    if (i < P.ns3) t = t + ldb(P.s3 + i) * P.s1;
+    t = t * P.alpha;
+    if (i < P.nq) {
+        FrB t0 = ldb(P.ql + i) * P.l + ldb(P.qm + i) * P.rl;
+        t = t + t0;
+        t = t + ldb(P.qr + i) * P.r;
+        t = t + (ldb(P.qo + i) * P.o + ldb(P.qk + i));
+        for (int j = 0; j < P.ncmt; j++) t = t + ldb(P.pi2[j] + i) * P.qcp[j];
+    }
+    stb(P.z + i, t + zi * P.lag);
+}
+
+static FrB frb(const void* p) {
+    FrB x;
+    memcpy(x.v, p, 32);
+    return x;
+}
+static hipStream_t pick(void* s) { return s ? (hipStream_t)s : hipStreamPerThread; }
+
+}  // namespace gg
+
+using namespace gg;
+
+extern "C" int gg_bls12_381_fr_prefix_product(void* data_dev, size_t n, void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(data_dev || n == 0, GG_ERR_INVALID_ARG, "null argument");
+    scan_run<SCAN_PROD>((FrB*)data_dev, n, FrB::one(), pick(hip_stream));
+    GG_CAPI_END
+}
+
+extern "C" int gg_bls12_381_fr_horner(const void* f_dev, size_t n, const void* a_mont, void* q_dev,
+                                      void* value_out, void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(f_dev && a_mont && value_out, GG_ERR_INVALID_ARG, "null argument");
+    if (n == 0) {
+        memset(value_out, 0, 32);
+        return GG_OK;
+    }
+    hipStream_t st = pick(hip_stream);
+    DevBuf g(n * 32);
+    hipLaunchKernelGGL(k_reverse_copy, dim3(grid_for(n, 256)), dim3(256), 0, st, g.as<FrB>(),
+                       (const FrB*)f_dev, n);
+    GG_HIP(hipGetLastError());
+    // x_k = y_k + a x_(k-1) over y = reversed f: x_(n-1) = f(a), x_k = sum_(i >= n-1-k) f_i a^(i-(n-1-k))
+    scan_run<SCAN_AFFINE>(g.as<FrB>(), n, frb(a_mont), st);
+    if (q_dev && n > 1) {
+        hipLaunchKernelGGL(k_quotient_out, dim3(grid_for(n, 256)), dim3(256), 0, st, (FrB*)q_dev,
+                           g.as<FrB>(), n);
+        GG_HIP(hipGetLastError());
+    }
+    GG_HIP(hipMemcpyAsync(value_out, g.as<FrB>() + n - 1, 32, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipStreamSynchronize(st));
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_ratio_copy_constraint(const void* l_dev, const void* r_dev, const void* o_dev,
+                                              const int64_t* perm_dev, size_t n, const void* beta,
+                                              const void* gamma, const void* omega_mont,
+                                              const void* coset_shift_mont, void* z_dev,
+                                              void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(l_dev && r_dev && o_dev && perm_dev && beta && gamma && omega_mont && coset_shift_mont && z_dev,
+             GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(n >= 1 && (n & (n - 1)) == 0 && n <= ((size_t)1 << 30), GG_ERR_INVALID_ARG,
+             "n must be a power of 2");
+    hipStream_t st = pick(hip_stream);
+    int L = 0;
+    while (((size_t)1 << L) < n) L++;
+    const FrB w = frb(omega_mont), u = frb(coset_shift_mont);
+    GG_CHECK(pow_u64(w, n) == FrB::one(), GG_ERR_INVALID_ARG, "omega^n != 1");
+    // w^e tables (e < n)
+    const int S = (L + 1) / 2;
+    std::vector<FrB> lo((size_t)1 << S), hi((size_t)1 << (L - S));
+    FrB acc = FrB::one();
+    for (auto& x : lo) { x = acc; acc = acc * w; }
+    FrB step = acc;
+    acc = FrB::one();
+    for (auto& x : hi) { x = acc; acc = acc * step; }
+    DevBuf dt((lo.size() + hi.size()) * 32);
+    GG_HIP(hipMemcpyAsync(dt.p, lo.data(), lo.size() * 32, hipMemcpyHostToDevice, st));
+    GG_HIP(hipMemcpyAsync(dt.as<FrB>() + lo.size(), hi.data(), hi.size() * 32, hipMemcpyHostToDevice, st));
+    PowSplit ps{dt.as<FrB>() + lo.size(), dt.as<FrB>(), S};
+    DevBuf den(n * 32);
+    FrB* num = (FrB*)z_dev;
+    hipLaunchKernelGGL(k_ratio_numden, dim3(grid_for(n, 256)), dim3(256), 0, st, (const FrB*)l_dev,
+                       (const FrB*)r_dev, (const FrB*)o_dev, perm_dev, (uint32_t)n, L, frb(beta),
+                       frb(gamma), u, u * u, ps, num, den.as<FrB>());
+    GG_HIP(hipGetLastError());
+    bls_batch_invert(den.as<FrB>(), n, st);  // t = fr.BatchInvert(t)
+    hipLaunchKernelGGL(k_mul_inplace, dim3(grid_for(n, 256)), dim3(256), 0, st, num, (const FrB*)den.p, n);
+    GG_HIP(hipGetLastError());
+    scan_run<SCAN_PROD>(num, n, FrB::one(), st);  // Z[i] = Z[i-1] * num_i / den_i
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_fold_h(const void* h_dev, size_t n_small, const void* zeta_pow_np2,
+                               void* out_dev, void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(h_dev && zeta_pow_np2 && out_dev, GG_ERR_INVALID_ARG, "null argument");
+    hipStream_t st = pick(hip_stream);
+    const size_t np2 = n_small + 2;
+    hipLaunchKernelGGL(k_fold_h, dim3(grid_for(np2, 256)), dim3(256), 0, st, (const FrB*)h_dev, np2,
+                       frb(zeta_pow_np2), (FrB*)out_dev);
+    GG_HIP(hipGetLastError());
+    GG_HIP(hipStreamSynchronize(st));
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_linearized(void* blinded_z_dev, size_t nz, const void* s3_dev, size_t ns3,
+                                   const void* const* q_dev, size_t nq, const void* const* pi2_dev,
+                                   const void* qcp_zeta, int n_cmt, const void* scalars8,
+                                   void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(blinded_z_dev && (s3_dev || ns3 == 0) && q_dev && scalars8, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(n_cmt >= 0 && n_cmt <= MAX_CMT, GG_ERR_INVALID_ARG, "at most 8 BSB22 commitments");
+    GG_CHECK(n_cmt == 0 || (pi2_dev && qcp_zeta), GG_ERR_INVALID_ARG, "null commitment polynomials");
+    LinParams P{};
+    P.z = (FrB*)blinded_z_dev;
+    P.nz = nz;
+    P.s3 = (const FrB*)s3_dev;
+    P.ns3 = ns3;
+    for (int k = 0; k < 5; k++) GG_CHECK(q_dev[k] || nq == 0, GG_ERR_INVALID_ARG, "null selector");
+    P.ql = (const FrB*)q_dev[0];
+    P.qr = (const FrB*)q_dev[1];
+    P.qm = (const FrB*)q_dev[2];
+    P.qo = (const FrB*)q_dev[3];
+    P.qk = (const FrB*)q_dev[4];
+    P.nq = nq;
+    P.ncmt = n_cmt;
+    for (int j = 0; j < n_cmt; j++) {
+        GG_CHECK(pi2_dev[j], GG_ERR_INVALID_ARG, "null pi2 polynomial");
+        P.pi2[j] = (const FrB*)pi2_dev[j];
+        P.qcp[j] = frb((const uint8_t*)qcp_zeta + 32 * j);
+    }
+    const uint8_t* s = (const uint8_t*)scalars8;
+    FrB* dst[8] = {&P.s1, &P.s2, &P.alpha, &P.l, &P.r, &P.rl, &P.o, &P.lag};
+    for (int k = 0; k < 8; k++) *dst[k] = frb(s + 32 * k);
+    hipStream_t st = pick(hip_stream);
+    hipLaunchKernelGGL(k_linearized, dim3(grid_for(nz, 256)), dim3(256), 0, st, P);
+    GG_HIP(hipGetLastError());
+    GG_HIP(hipStreamSynchronize(st));
+    GG_CAPI_END
+}

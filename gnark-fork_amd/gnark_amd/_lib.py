@@ -72,6 +72,12 @@ def _load():
                                         S, P, S, S, PP], I),
         "gg_groth16_prove_partial": ([P, P, S, P, P, P, S, I, P, P], I),
         "gg_groth16_finalize": ([P, P, P, P, P, P, P, P, P, P, P], I),
+        "gg_plonk_ratio_copy_constraint": ([P, P, P, P, S, P, P, P, P, P, P], I),
+        "gg_bls12_381_fr_prefix_product": ([P, S, P], I),
+        "gg_bls12_381_fr_horner": ([P, S, P, P, P, P], I),
+        "gg_plonk_fold_h": ([P, S, P, P, P], I),
+        "gg_plonk_linearized": ([P, S, P, S, ctypes.POINTER(ctypes.c_void_p), S,
+                                 ctypes.POINTER(ctypes.c_void_p), P, I, P, P], I),
         "gg_hshard_create": ([I, P, P, I, I, PP], I),
         "gg_hshard_release": ([P], I),
         "gg_hshard_info": ([P, ctypes.POINTER(S), ctypes.POINTER(S)], I),
@@ -106,7 +112,9 @@ EXPORTED = [
     "gg_plonk_numerator_coset", "gg_plonk_divide_by_xn_minus_one", "gg_bls12_381_fr_batch_invert",
     "gg_profile_get", "gg_groth16_pk_create_shard", "gg_groth16_prove_partial",
     "gg_groth16_finalize", "gg_hshard_create", "gg_hshard_release", "gg_hshard_info",
-    "gg_hshard_phase", "gg_groth16_prove_partial_dist",
+    "gg_hshard_phase", "gg_groth16_prove_partial_dist", "gg_plonk_ratio_copy_constraint",
+    "gg_bls12_381_fr_prefix_product", "gg_bls12_381_fr_horner", "gg_plonk_fold_h",
+    "gg_plonk_linearized",
 ]
 
 

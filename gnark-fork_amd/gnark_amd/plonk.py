@@ -37,3 +37,61 @@ def divide_by_xn_minus_one(big_domain, n_small: int, data, stream=None):
 
 def batch_invert(data, n: int, stream=None):
     check(lib.gg_bls12_381_fr_batch_invert(ptr(data), n, ptr(stream)))
+
+
+# ------------------------------------------------ row a21: ratio, evaluate, fold, linearize
+def ratio_copy_constraint(l, r, o, perm_dev, n: int, beta: bytes, gamma: bytes, omega: bytes,
+                          coset_shift: bytes, z_out, stream=None):
+    """iop.BuildRatioCopyConstraint([L, R, O], pk.trace.S, beta, gamma,
+    {Lagrange, Regular}, pk.Domain[0]) -> z_out (n fr, device)."""
+    check(lib.gg_plonk_ratio_copy_constraint(ptr(l), ptr(r), ptr(o), ptr(perm_dev), n, ptr(beta),
+                                             ptr(gamma), ptr(omega), ptr(coset_shift), ptr(z_out),
+                                             ptr(stream)))
+
+
+def prefix_product(data, n: int, stream=None):
+    check(lib.gg_bls12_381_fr_prefix_product(ptr(data), n, ptr(stream)))
+
+
+def evaluate(f, n: int, a: bytes, q_out=None, stream=None) -> bytes:
+    """f(a) for canonical regular f (n fr, device); with q_out, also the KZG
+    opening quotient (f - f(a)) / (X - a) (n - 1 fr)."""
+    out = bytearray(32)
+    check(lib.gg_bls12_381_fr_horner(ptr(f), n, ptr(a), ptr(q_out), ptr(out), ptr(stream)))
+    return bytes(out)
+
+
+def fold_h(h, n_small: int, zeta_pow_np2: bytes, out, stream=None):
+    check(lib.gg_plonk_fold_h(ptr(h), n_small, ptr(zeta_pow_np2), ptr(out), ptr(stream)))
+
+
+def linearized_scalars(l_zeta: int, r_zeta: int, o_zeta: int, alpha: int, beta: int, gamma: int,
+                       zeta: int, zu: int, s1_zeta: int, s2_zeta: int, coset_shift: int, n: int):
+    """The eight scalars of computeLinearizedPolynomial (prove.go:1293-1336), as
+    canonical integers mod r: s1, s2, alpha, l, r, l*r, o, alpha^2 L1(zeta) / n."""
+    from .fr import BLS_R as R
+    s1 = (s1_zeta * beta + l_zeta + gamma) % R
+    t = (s2_zeta * beta + r_zeta + gamma) % R
+    s1 = s1 * t % R * zu % R * beta % R
+    uz = zeta * coset_shift % R
+    uuz = uz * coset_shift % R
+    s2 = (beta * zeta + l_zeta + gamma) % R
+    s2 = s2 * ((beta * uz + r_zeta + gamma) % R) % R
+    s2 = s2 * ((beta * uuz + o_zeta + gamma) % R) % R
+    s2 = (-s2) % R
+    lag = (pow(zeta, n, R) - 1) * pow(zeta - 1, -1, R) % R
+    lag = lag * alpha % R * alpha % R * pow(n, -1, R) % R
+    return [s1, s2, alpha % R, l_zeta % R, r_zeta % R, l_zeta * r_zeta % R, o_zeta % R, lag]
+
+
+def linearized(blinded_z, nz: int, s3, ns3: int, q5, nq: int, scalars, pi2=(), qcp_zeta=(),
+               stream=None):
+    """computeLinearizedPolynomial in place on blinded_z (device, canonical).
+    scalars: the 8 values of linearized_scalars (ints); q5 = (Ql, Qr, Qm, Qo, Qk)."""
+    from .fr import bls_fr_mont
+    qa = (ctypes.c_void_p * 5)(*[ptr(x).value for x in q5])
+    pa = (ctypes.c_void_p * max(1, len(pi2)))(*[ptr(x).value for x in pi2]) if pi2 else None
+    qc = b"".join(bls_fr_mont(v) for v in qcp_zeta) if qcp_zeta else None
+    sc = b"".join(bls_fr_mont(v) for v in scalars)
+    check(lib.gg_plonk_linearized(ptr(blinded_z), nz, ptr(s3), ns3, qa, nq, pa, ptr(qc), len(pi2),
+                                  ptr(sc), ptr(stream)))

@@ -288,6 +288,43 @@ int gg_plonk_divide_by_xn_minus_one(gg_domain_t big, size_t n_small, void *data_
 /* fr.BatchInvert in place (prove.go:1273; zeros stay zero) */
 int gg_bls12_381_fr_batch_invert(void *data_dev, size_t n, void *hip_stream);
 
+/* ---- PlonK BLS12-381 polynomial ops, device buffers,
+ * bls12-381 fr Montgomery (32 B).
+ *
+ * iop.BuildRatioCopyConstraint (prove.go:600-621) into Lagrange/Regular form:
+ *   Z[0] = 1, Z[i+1] = Z[i] * prod_j (f_j[i] + beta*ID(j*n+i) + gamma)
+ *                           / prod_j (f_j[i] + beta*ID(S[j*n+i]) + gamma),
+ *   f = (L, R, O) Lagrange/Regular (n each), perm_dev = pk.trace.S (3n int64),
+ *   ID(s) = u^(s div n) * omega^(s mod n) (getSupportPermutation, setup.go:391-407),
+ *   omega = pk.Domain[0].Generator, u = pk.Domain[0].FrMultiplicativeGen. */
+int gg_plonk_ratio_copy_constraint(const void *l_dev, const void *r_dev, const void *o_dev,
+                                   const int64_t *perm_dev, size_t n, const void *beta,
+                                   const void *gamma, const void *omega_mont,
+                                   const void *coset_shift_mont, void *z_dev, void *hip_stream);
+/* in place inclusive running product data[i] = data[0] * ... * data[i] */
+int gg_bls12_381_fr_prefix_product(void *data_dev, size_t n, void *hip_stream);
+/* value_out (host) = f(a) = sum f_i a^i (iop.Polynomial.Evaluate, canonical
+ * regular, prove.go:1118-1145, 1313-1320); q_dev (nullable, n - 1 fr) = the
+ * KZG opening quotient (f - f(a)) / (X - a) of kzg.Open (prove.go:646, 823-830). */
+int gg_bls12_381_fr_horner(const void *f_dev, size_t n, const void *a_mont, void *q_dev,
+                           void *value_out, void *hip_stream);
+/* foldH (prove.go:670-705): out[i] = (h3[i]*z + h2[i])*z + h1[i], i < n_small + 2,
+ * h_dev = h1 | h2 | h3 (3 (n_small + 2) fr), z = zeta^(n_small + 2) (host). */
+int gg_plonk_fold_h(const void *h_dev, size_t n_small, const void *zeta_pow_np2, void *out_dev,
+                    void *hip_stream);
+/* computeLinearizedPolynomial (prove.go:1289-1389), in place on the blinded Z
+ * (canonical, nz fr): with i < nz,
+ *   t = z[i]*s2 (+ s3[i]*s1 if i < ns3);  t *= alpha;
+ *   if i < nq: t += ql[i]*l + qm[i]*rl + qr[i]*r + qo[i]*o + qk[i] + sum_j pi2_j[i]*qcp_j;
+ *   z[i] = t + z[i]*lag
+ * q_dev[5] = {Ql, Qr, Qm, Qo, Qk} canonical (nq each); pi2_dev[n_cmt] and
+ * qcp_zeta (n_cmt fr, host): BSB22 terms; scalars8 (host, 8 fr) =
+ * {s1, s2, alpha, l(zeta), r(zeta), l(zeta)r(zeta), o(zeta), alpha^2 L1(zeta)/n}
+ * as computed at prove.go:1300-1336. */
+int gg_plonk_linearized(void *blinded_z_dev, size_t nz, const void *s3_dev, size_t ns3,
+                        const void *const *q_dev, size_t nq, const void *const *pi2_dev,
+                        const void *qcp_zeta, int n_cmt, const void *scalars8, void *hip_stream);
+
 /* ------------------------------------------------------------ profiling
  * Kernel-level timing with HIP events recorded on the stream each kernel is
  * launched on (bench.py uses it for the roofline of the dominant kernel).

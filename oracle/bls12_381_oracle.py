@@ -303,3 +303,75 @@ def divide_by_xn_minus_one(a, n_small, big: Domain):
     lb = big.log_n
     a = [v * f[bitrev(i, lb) % rho] % R for i, v in enumerate(a)]
     return fft_inverse(big, a, DIT, coset=True)
+
+
+# ---------------------------------------------------------------- row a21
+def support_permutation(n: int, dom: Domain):
+    """getSupportPermutation (setup.go:391-407): <w> || u<w> || u^2<w>, u = FrMultiplicativeGen."""
+    w, u = dom.generator, dom.gen
+    res = []
+    for blk in range(3):
+        f = pow(u, blk, R)
+        for i in range(n):
+            res.append(f * pow(w, i, R) % R)
+    return res
+
+
+def ratio_copy_constraint(entries, perm, beta, gamma, dom: Domain):
+    """iop.BuildRatioCopyConstraint (gnark-crypto [ext], called at prove.go:610-621),
+    restated from its published algorithm with the reference's own permutation
+    support (setup.go:391-407): Lagrange/Regular entries, result Lagrange/Regular."""
+    n = dom.cardinality
+    ids = support_permutation(n, dom)
+    z = [1] * n
+    num = [1] * n
+    den = [1] * n
+    for i in range(n - 1):
+        b = d = 1
+        for j, f in enumerate(entries):
+            b = b * ((f[i] + beta * ids[j * n + i] + gamma) % R) % R
+            d = d * ((f[i] + beta * ids[perm[j * n + i]] + gamma) % R) % R
+        num[i + 1], den[i + 1] = b, d
+    den = batch_invert(den)
+    for i in range(1, n):
+        z[i] = z[i - 1] * num[i] % R * den[i] % R
+    return z
+
+
+def evaluate(coeffs, x):
+    """iop.Polynomial.Evaluate on canonical regular coefficients (Horner)."""
+    return _horner(coeffs, x)
+
+
+def divide_by_x_minus_a(f, fa, a):
+    """kzg dividePolyByXminusA (gnark-crypto [ext], kzg.Open at prove.go:646,
+    823-830): f - f(a) divided by X - a by synthetic division; returns n - 1 coefficients."""
+    f = list(f)
+    f[0] = (f[0] - fa) % R
+    for i in range(len(f) - 2, -1, -1):
+        f[i] = (f[i] + f[i + 1] * a) % R
+    return f[1:]
+
+
+def fold_h(h, n_small, zeta):
+    """foldH (prove.go:670-705): H0 + zeta^(n+2) H1 + zeta^(2(n+2)) H2."""
+    m = n_small + 2
+    z = pow(zeta, m, R)
+    return [((h[2 * m + i] * z + h[m + i]) * z + h[i]) % R for i in range(m)]
+
+
+def linearized(blinded_z, s3, ql, qr, qm, qo, qk, pi2, qcp, s1, s2, alpha, l, r, o, lag):
+    """Inner loop of computeLinearizedPolynomial (prove.go:1347-1386), verbatim."""
+    rl = r * l % R
+    out = []
+    for i, zi in enumerate(blinded_z):
+        t = zi * s2 % R
+        if i < len(s3):
+            t = (t + s3[i] * s1) % R
+        t = t * alpha % R
+        if i < len(qm):
+            t = (t + ql[i] * l + qm[i] * rl + qr[i] * r + qo[i] * o + qk[i]) % R
+            for j in range(len(qcp)):
+                t = (t + pi2[j][i] * qcp[j]) % R
+        out.append((t + zi * lag) % R)
+    return out

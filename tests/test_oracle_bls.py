@@ -7,6 +7,7 @@ import os
 import random
 
 import bls12_381_oracle as b
+import bls12_381_oracle as bo
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PINS = json.load(open(os.path.join(HERE, "golden", "bls12_381_pins.json")))
@@ -65,3 +66,68 @@ def test_encodings_roundtrip():
     g = b.G1_GEN
     assert b.g1_from_bytes(b.g1_to_bytes(g)) == g
     assert b.g1_to_bytes(b.INF) == bytes(96)
+
+
+# ---- row a21 restatements: internal consistency (no GPU)
+def _copy_witness(n, seed):
+    """A random permutation of the 3n wire slots made of cycles, and L/R/O values
+    constant on each cycle (a witness that satisfies the copy constraints)."""
+    import random
+    rnd = random.Random(seed)
+    slots = list(range(3 * n))
+    rnd.shuffle(slots)
+    perm = [0] * (3 * n)
+    vals = [0] * (3 * n)
+    i = 0
+    while i < 3 * n:
+        k = min(rnd.randint(1, 5), 3 * n - i)
+        cyc = slots[i:i + k]
+        v = rnd.randrange(bo.R)
+        for a, b_ in zip(cyc, cyc[1:] + cyc[:1]):
+            perm[a] = b_
+            vals[a] = v
+        i += k
+    return perm, [vals[:n], vals[n:2 * n], vals[2 * n:]]
+
+
+def test_ratio_copy_constraint_wraps_to_one():
+    """For a satisfied permutation Z(w^n) = Z(1) = 1: the last ratio step closes the cycle."""
+    n = 16
+    dom = bo.Domain(n)
+    perm, f = _copy_witness(n, 3)
+    beta, gamma = 12345678910, 987654321
+    z = bo.ratio_copy_constraint(f, perm, beta, gamma, dom)
+    ids = bo.support_permutation(n, dom)
+    i = n - 1
+    num = den = 1
+    for j in range(3):
+        num = num * (f[j][i] + beta * ids[j * n + i] + gamma) % bo.R
+        den = den * (f[j][i] + beta * ids[perm[j * n + i]] + gamma) % bo.R
+    assert z[0] == 1
+    assert z[n - 1] * num * pow(den, -1, bo.R) % bo.R == 1
+    # a broken copy constraint does not close
+    f[0][3] = (f[0][3] + 1) % bo.R
+    z2 = bo.ratio_copy_constraint(f, perm, beta, gamma, dom)
+    assert z2 != z
+
+
+def test_divide_by_x_minus_a_identity():
+    import random
+    rnd = random.Random(5)
+    f = [rnd.randrange(bo.R) for _ in range(33)]
+    a = rnd.randrange(bo.R)
+    fa = bo.evaluate(f, a)
+    q = bo.divide_by_x_minus_a(f, fa, a)
+    x = rnd.randrange(bo.R)
+    assert (bo.evaluate(q, x) * (x - a) + fa - bo.evaluate(f, x)) % bo.R == 0
+
+
+def test_fold_h_is_evaluation_split():
+    import random
+    rnd = random.Random(6)
+    n = 8
+    h = [rnd.randrange(bo.R) for _ in range(3 * (n + 2))]
+    zeta = rnd.randrange(bo.R)
+    folded = bo.fold_h(h, n, zeta)
+    # sum_k zeta^(k(n+2)) H_k(X) evaluated at X = zeta equals h(zeta)
+    assert bo.evaluate(folded, zeta) == bo.evaluate(h, zeta)
