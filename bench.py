@@ -358,6 +358,20 @@ def plonk_bench(log_n, reps=5):
     bl = [[one, one], [one, one], [one, one], [one, one, one]]
     res["numerator_coset_ms"] = timed(lambda: plonk.numerator_coset(
         xs, bl, tw0, one, one, one, fr.bls_fr_mont(7), n, 4, 1, cres))
+    # row a21: copy-constraint ratio Z, Horner evaluation + KZG opening quotient,
+    # foldH, linearized polynomial (all at the small domain size n)
+    perm = DeviceBuffer.from_host(np.random.default_rng(3).permutation(3 * n).astype(np.int64).tobytes())
+    z = DeviceBuffer(32 * n)
+    w = fr.bls_fr_mont(fr.bls_domain_generator(log_n))
+    u = fr.bls_fr_mont(fr.BLS_FR_MULTIPLICATIVE_GEN)
+    res["ratio_copy_constraint_ms"] = timed(lambda: plonk.ratio_copy_constraint(
+        xs[0], xs[1], xs[2], perm, n, one, fr.bls_fr_mont(5), w, u, z))
+    q = DeviceBuffer(32 * n)
+    res["evaluate_and_open_quotient_ms"] = timed(lambda: plonk.evaluate(xs[3], n, fr.bls_fr_mont(11), q_out=q))
+    hbuf = DeviceBuffer(3 * (n + 2) * 32)
+    res["fold_h_ms"] = timed(lambda: plonk.fold_h(hbuf, n, fr.bls_fr_mont(13), q))
+    sc = [3, 5, 7, 11, 13, 17, 19, 23]
+    res["linearized_ms"] = timed(lambda: plonk.linearized(z, n, xs[4], n, xs[5:10], n, sc))
     return res
 
 
