@@ -369,7 +369,8 @@ def plonk_bench(log_n, reps=5):
     q = DeviceBuffer(32 * n)
     res["evaluate_and_open_quotient_ms"] = timed(lambda: plonk.evaluate(xs[3], n, fr.bls_fr_mont(11), q_out=q))
     hbuf = DeviceBuffer(3 * (n + 2) * 32)
-    res["fold_h_ms"] = timed(lambda: plonk.fold_h(hbuf, n, fr.bls_fr_mont(13), q))
+    folded = DeviceBuffer((n + 2) * 32)  # foldH writes n + 2 coefficients
+    res["fold_h_ms"] = timed(lambda: plonk.fold_h(hbuf, n, fr.bls_fr_mont(13), folded))
     sc = [3, 5, 7, 11, 13, 17, 19, 23]
     res["linearized_ms"] = timed(lambda: plonk.linearized(z, n, xs[4], n, xs[5:10], n, sc))
     return res

@@ -40,28 +40,47 @@ def batch_invert(data, n: int, stream=None):
 
 
 # ------------------------------------------------ row a21: ratio, evaluate, fold, linearize
+def _need(buf, nbytes: int, what: str):
+    """Host-side bound check for sized buffers (DeviceBuffer / torch): the kernels
+    cannot see the allocation, so an undersized buffer is refused before launch."""
+    have = getattr(buf, "nbytes", None)
+    if have is None and hasattr(buf, "numel"):
+        have = buf.numel() * buf.element_size()
+    if have is not None and have < nbytes:
+        raise ValueError(f"{what}: buffer of {have} B, needs {nbytes} B")
+
+
 def ratio_copy_constraint(l, r, o, perm_dev, n: int, beta: bytes, gamma: bytes, omega: bytes,
                           coset_shift: bytes, z_out, stream=None):
     """iop.BuildRatioCopyConstraint([L, R, O], pk.trace.S, beta, gamma,
     {Lagrange, Regular}, pk.Domain[0]) -> z_out (n fr, device)."""
+    for b_, nm in ((l, "L"), (r, "R"), (o, "O"), (z_out, "Z")):
+        _need(b_, 32 * n, nm)
+    _need(perm_dev, 24 * n, "permutation")
     check(lib.gg_plonk_ratio_copy_constraint(ptr(l), ptr(r), ptr(o), ptr(perm_dev), n, ptr(beta),
                                              ptr(gamma), ptr(omega), ptr(coset_shift), ptr(z_out),
                                              ptr(stream)))
 
 
 def prefix_product(data, n: int, stream=None):
+    _need(data, 32 * n, "data")
     check(lib.gg_bls12_381_fr_prefix_product(ptr(data), n, ptr(stream)))
 
 
 def evaluate(f, n: int, a: bytes, q_out=None, stream=None) -> bytes:
     """f(a) for canonical regular f (n fr, device); with q_out, also the KZG
     opening quotient (f - f(a)) / (X - a) (n - 1 fr)."""
+    _need(f, 32 * n, "f")
+    if q_out is not None:
+        _need(q_out, 32 * max(n - 1, 0), "quotient")
     out = bytearray(32)
     check(lib.gg_bls12_381_fr_horner(ptr(f), n, ptr(a), ptr(q_out), ptr(out), ptr(stream)))
     return bytes(out)
 
 
 def fold_h(h, n_small: int, zeta_pow_np2: bytes, out, stream=None):
+    _need(h, 3 * 32 * (n_small + 2), "h")
+    _need(out, 32 * (n_small + 2), "folded h")
     check(lib.gg_plonk_fold_h(ptr(h), n_small, ptr(zeta_pow_np2), ptr(out), ptr(stream)))
 
 
@@ -89,6 +108,10 @@ def linearized(blinded_z, nz: int, s3, ns3: int, q5, nq: int, scalars, pi2=(), q
     """computeLinearizedPolynomial in place on blinded_z (device, canonical).
     scalars: the 8 values of linearized_scalars (ints); q5 = (Ql, Qr, Qm, Qo, Qk)."""
     from .fr import bls_fr_mont
+    _need(blinded_z, 32 * nz, "blinded Z")
+    _need(s3, 32 * ns3, "S3")
+    for q in list(q5) + list(pi2):
+        _need(q, 32 * nq, "selector")
     qa = (ctypes.c_void_p * 5)(*[ptr(x).value for x in q5])
     pa = (ctypes.c_void_p * max(1, len(pi2)))(*[ptr(x).value for x in pi2]) if pi2 else None
     qc = b"".join(bls_fr_mont(v) for v in qcp_zeta) if qcp_zeta else None

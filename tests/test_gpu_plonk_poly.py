@@ -176,3 +176,13 @@ def test_linearized_vs_oracle(n, ncmt):
     exp = bo.linearized(bz, s3, qs[0], qs[1], qs[2], qs[3], qs[4], pi2, qcp, sc[0], sc[1], sc[2],
                         sc[3], sc[4], sc[6], sc[7])
     assert host(zb) == exp
+
+
+def test_undersized_buffers_refused_before_launch():
+    from gnark_amd import plonk, DeviceBuffer
+    n = 64
+    h = DeviceBuffer(3 * (n + 2) * 32)
+    with pytest.raises(ValueError):
+        plonk.fold_h(h, n, bo.fr_to_bytes(3), DeviceBuffer(32 * n))
+    with pytest.raises(ValueError):
+        plonk.evaluate(DeviceBuffer(32 * (n - 1)), n, bo.fr_to_bytes(3))
