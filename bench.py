@@ -13,6 +13,7 @@ synthetic key generated on the GPU, and the C restatement (oracle/) of the same
 MSM timed on the host cores as cpu_baseline.
 """
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -67,6 +68,10 @@ def main():
     ap.add_argument("--plonk-log-n", type=int, default=22,
                     help="BLS12-381 PlonK hot-op measurement size, BASELINE configs[4] (0 = skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--extras-timeout", type=float, default=480.0,
+                    help="seconds allowed for the extra measurements after the headline; past it "
+                         "the headline line is printed with the extras marked timed out and the "
+                         "process exits (a stuck collective never swallows the headline)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     args = ap.parse_args()
 
@@ -89,9 +94,10 @@ def main():
     if world > 1:
         import torch.distributed as dist
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev),
+                                    timeout=datetime.timedelta(minutes=10))
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=datetime.timedelta(minutes=10))
 
     def barrier():
         if dist is not None:
@@ -177,6 +183,27 @@ def main():
         "roofline": roofline, "kernels": kernels,
     }
 
+    # watchdog over the extras: the headline is already measured
+    import threading
+    printed = threading.Lock()
+    stage = {"now": "ntt"}
+
+    def emit():
+        if printed.acquire(blocking=False):
+            if rank == 0:
+                print(json.dumps(out), flush=True)
+            return True
+        return False
+
+    def bail():
+        out.setdefault("extras_timeout", {"stage": stage["now"], "seconds": args.extras_timeout})
+        emit()
+        os._exit(0)
+
+    wd = threading.Timer(args.extras_timeout, bail)
+    wd.daemon = True
+    wd.start()
+
     # ---- Fr NTT 2^24 (BASELINE configs[2]; extra, rank 0 / N = 1 only)
     if rank == 0 and world == 1 and args.ntt_log_n:
         try:
@@ -185,6 +212,7 @@ def main():
             out["ntt"] = {"error": repr(e)}
 
     # ---- PlonK BLS12-381 hot ops (BASELINE configs[4] sizes; extra, rank 0 / N = 1 only)
+    stage["now"] = "plonk"
     if rank == 0 and world == 1 and args.plonk_log_n:
         try:
             out["plonk_bls12_381"] = plonk_bench(args.plonk_log_n)
@@ -194,6 +222,7 @@ def main():
     # ---- Groth16 prove (extra): whole key at N = 1; at N > 1 one key shard per
     # GPU (wires and Z positions partitioned, h computed on every GPU, 576-B
     # partials all-gathered) -- strong scaling of one 2^log_n proof
+    stage["now"] = "groth16"
     if args.groth16_log_n:
         try:
             if world == 1:
@@ -206,14 +235,15 @@ def main():
             out["groth16"] = g16
 
     # ---- CPU baseline (oracle restatement on the host cores), rank 0 at N = 1
+    stage["now"] = "cpu_baseline"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(base, dsc, sc, n, args.cpu_threads)
         except Exception as e:
             out["cpu_baseline"] = {"error": repr(e)}
 
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    wd.cancel()
+    emit()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -89,7 +89,7 @@ GG_HD Xyzz<F> xyzz_madd(const Xyzz<F>& p, const Affine<F>& q) {
     F PPP = P * PP;
     F Q = p.x * PP;
     F X3 = sqr(R) - PPP - dbl(Q);
-    F Y3 = R * (Q - X3) - p.y * PPP;
+    F Y3 = mul_sub(R, Q - X3, p.y, PPP);
     return Xyzz<F>{X3, Y3, p.zz * PP, p.zzz * PPP};
 }
 
@@ -114,7 +114,7 @@ GG_HD void xyzz_madd_inplace(Xyzz<F>& p, const Affine<F>& q) {
     p.zzz = p.zzz * PPP;
     F Q = p.x * PP;
     F X3 = sqr(R) - PPP - dbl(Q);
-    p.y = R * (Q - X3) - p.y * PPP;
+    p.y = mul_sub(R, Q - X3, p.y, PPP);
     p.x = X3;
 }
 
@@ -137,7 +137,7 @@ GG_HD Xyzz<F> xyzz_add(const Xyzz<F>& p, const Xyzz<F>& q) {
     F PPP = P * PP;
     F Q = U1 * PP;
     F X3 = sqr(R) - PPP - dbl(Q);
-    F Y3 = R * (Q - X3) - S1 * PPP;
+    F Y3 = mul_sub(R, Q - X3, S1, PPP);
     return Xyzz<F>{X3, Y3, p.zz * q.zz * PP, p.zzz * q.zzz * PPP};
 }
 
@@ -163,7 +163,7 @@ GG_HD void xyzz_add_inplace(Xyzz<F>& p, const Xyzz<F>& q) {
     p.zzz = p.zzz * q.zzz * PPP;
     F Q = U1 * PP;
     p.x = sqr(R) - PPP - dbl(Q);
-    p.y = R * (Q - p.x) - S1 * PPP;
+    p.y = mul_sub(R, Q - p.x, S1, PPP);
 }
 
 // XYZZ -> Jacobian: Z = ZZZ, X = X*ZZ^2, Y = Y*ZZZ^2

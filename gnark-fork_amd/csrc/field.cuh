@@ -13,6 +13,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #define GG_HD __host__ __device__ __forceinline__
 
@@ -479,7 +480,37 @@ __device__ __forceinline__ Fp2 fp2_mul_lazy(const Fp2& x, const Fp2& y) {
     }
     return Fp2{fp_redc(U), fp_redc(S)};
 }
+// a*b - c*d with one Montgomery reduction: REDC(a*b + p^2 - c*d), the argument
+// in (0, 2p^2) < p * 2^256 (inputs canonical, p < 2^254); canonical result.
+__device__ __forceinline__ Fp fp_mul_sub_lazy(const Fp& x, const Fp& y, const Fp& z, const Fp& w) {
+    uint32_t U[16];
+    {
+        GG_WIDE_OPERANDS(x, y)
+        uint32_t cu = 0;
+#define GG_WIDE_COL(k, dd) U[k] = __builtin_addc((dd), kFpP2[k], cu, &cu);
+        GG_WIDE_BODY
+#undef GG_WIDE_COL
+    }
+    {
+        GG_WIDE_OPERANDS(z, w)
+        uint32_t bu = 0;
+#define GG_WIDE_COL(k, dd) U[k] = __builtin_subc(U[k], (dd), bu, &bu);
+        GG_WIDE_BODY
+#undef GG_WIDE_COL
+    }
+    return fp_redc(U);
+}
 #endif
+
+// a*b - c*d (lazily reduced for BN254 Fp on the device)
+template <class F>
+GG_HD F mul_sub(const F& a, const F& b, const F& c, const F& d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (std::is_same<F, Fp>::value) return fp_mul_sub_lazy(a, b, c, d);
+    else
+#endif
+        return a * b - c * d;
+}
 
 #ifndef GG_FP2_PLAIN
 #define GG_FP2_PLAIN 0
