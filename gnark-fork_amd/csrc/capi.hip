@@ -53,6 +53,18 @@ extern "C" int gg_copy_to_host(void* host_dst, const void* dev_src, size_t bytes
     GG_CAPI_END
 }
 
+extern "C" int gg_copy_device(void* dev_dst, const void* dev_src, size_t bytes) {
+    GG_CAPI_BEGIN
+    if (bytes) GG_HIP(hipMemcpy(dev_dst, dev_src, bytes, hipMemcpyDeviceToDevice));
+    GG_CAPI_END
+}
+
+extern "C" int gg_memset_device(void* dev_dst, int value, size_t bytes) {
+    GG_CAPI_BEGIN
+    if (bytes) GG_HIP(hipMemset(dev_dst, value, bytes));
+    GG_CAPI_END
+}
+
 extern "C" int gg_synchronize(void) {
     GG_CAPI_BEGIN
     GG_HIP(hipDeviceSynchronize());

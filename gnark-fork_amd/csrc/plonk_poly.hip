@@ -277,6 +277,20 @@ __global__ void __launch_bounds__(256) k_linearized(LinParams P) {
     stb(P.z + i, t + zi * P.lag);
 }
 
+// out[bitrev(i)] = in[i] (out-of-place; fft.BitReverse / iop ToRegular)
+__global__ void k_bit_reverse(FrB* out, const FrB* in, size_t n, int log_n) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t r = log_n ? (__brev((uint32_t)i) >> (32 - log_n)) : 0u;
+    stb(out + r, ldb(in + i));
+}
+
+// y[i] += a * x[i]
+__global__ void k_axpy(FrB* y, const FrB* x, size_t n, FrB a) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) stb(y + i, ldb(y + i) + a * ldb(x + i));
+}
+
 static FrB frb(const void* p) {
     FrB x;
     memcpy(x.v, p, 32);
@@ -404,6 +418,33 @@ extern "C" int gg_plonk_linearized(void* blinded_z_dev, size_t nz, const void* s
     for (int k = 0; k < 8; k++) *dst[k] = frb(s + 32 * k);
     hipStream_t st = pick(hip_stream);
     hipLaunchKernelGGL(k_linearized, dim3(grid_for(nz, 256)), dim3(256), 0, st, P);
+    GG_HIP(hipGetLastError());
+    GG_HIP(hipStreamSynchronize(st));
+    GG_CAPI_END
+}
+
+extern "C" int gg_bls12_381_fr_bit_reverse(const void* in_dev, void* out_dev, size_t n, void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(in_dev && out_dev && in_dev != out_dev, GG_ERR_INVALID_ARG, "need distinct in / out buffers");
+    GG_CHECK(n >= 1 && (n & (n - 1)) == 0 && n <= ((size_t)1 << 31), GG_ERR_INVALID_ARG, "n must be a power of 2");
+    int L = 0;
+    while (((size_t)1 << L) < n) L++;
+    hipStream_t st = pick(hip_stream);
+    hipLaunchKernelGGL(k_bit_reverse, dim3(grid_for(n, 256)), dim3(256), 0, st, (FrB*)out_dev,
+                       (const FrB*)in_dev, n, L);
+    GG_HIP(hipGetLastError());
+    GG_HIP(hipStreamSynchronize(st));
+    GG_CAPI_END
+}
+
+extern "C" int gg_bls12_381_fr_axpy(void* y_dev, const void* x_dev, size_t n, const void* a_mont,
+                                    void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(y_dev && x_dev && a_mont, GG_ERR_INVALID_ARG, "null argument");
+    if (n == 0) return GG_OK;
+    hipStream_t st = pick(hip_stream);
+    hipLaunchKernelGGL(k_axpy, dim3(grid_for(n, 256)), dim3(256), 0, st, (FrB*)y_dev, (const FrB*)x_dev, n,
+                       frb(a_mont));
     GG_HIP(hipGetLastError());
     GG_HIP(hipStreamSynchronize(st));
     GG_CAPI_END

@@ -46,6 +46,10 @@ def _load():
         "gg_copy_to_device": ([P, P, S], I),
         "gg_copy_to_host": ([P, P, S], I),
         "gg_synchronize": ([], I),
+        "gg_copy_device": ([P, P, S], I),
+        "gg_memset_device": ([P, I, S], I),
+        "gg_bls12_381_fr_bit_reverse": ([P, P, S, P], I),
+        "gg_bls12_381_fr_axpy": ([P, P, S, P, P], I),
         "gg_domain_create": ([I, P, P, PP], I),
         "gg_domain_create_ex": ([I, I, P, P, PP], I),
         "gg_domain_release": ([P], I),
@@ -114,7 +118,8 @@ EXPORTED = [
     "gg_groth16_finalize", "gg_hshard_create", "gg_hshard_release", "gg_hshard_info",
     "gg_hshard_phase", "gg_groth16_prove_partial_dist", "gg_plonk_ratio_copy_constraint",
     "gg_bls12_381_fr_prefix_product", "gg_bls12_381_fr_horner", "gg_plonk_fold_h",
-    "gg_plonk_linearized",
+    "gg_plonk_linearized", "gg_copy_device", "gg_memset_device", "gg_bls12_381_fr_bit_reverse",
+    "gg_bls12_381_fr_axpy",
 ]
 
 
@@ -128,6 +133,8 @@ def ptr(obj):
     """Pointer to a host or device buffer: bytes/bytearray/numpy/torch/int/None."""
     if obj is None:
         return None
+    if isinstance(obj, ctypes.c_void_p):
+        return obj
     if isinstance(obj, int):
         return ctypes.c_void_p(obj)
     if hasattr(obj, "data_ptr"):  # torch tensor (device or host)

@@ -75,6 +75,8 @@ int gg_malloc(void **dev_ptr, size_t bytes);
 int gg_free(void *dev_ptr);
 int gg_copy_to_device(void *dev_dst, const void *host_src, size_t bytes);
 int gg_copy_to_host(void *host_dst, const void *dev_src, size_t bytes);
+int gg_copy_device(void *dev_dst, const void *dev_src, size_t bytes);
+int gg_memset_device(void *dev_dst, int value, size_t bytes);
 int gg_synchronize(void);
 
 /* ------------------------------------------------------------- NTT domain
@@ -301,6 +303,10 @@ int gg_plonk_ratio_copy_constraint(const void *l_dev, const void *r_dev, const v
                                    const int64_t *perm_dev, size_t n, const void *beta,
                                    const void *gamma, const void *omega_mont,
                                    const void *coset_shift_mont, void *z_dev, void *hip_stream);
+/* out[bitrev(i)] = in[i] (fft.BitReverse out of place; iop ToRegular / ToBitReverse) */
+int gg_bls12_381_fr_bit_reverse(const void *in_dev, void *out_dev, size_t n, void *hip_stream);
+/* y[i] += a * x[i] (kzg.BatchOpenSinglePoint folding, sum gamma^i p_i) */
+int gg_bls12_381_fr_axpy(void *y_dev, const void *x_dev, size_t n, const void *a_mont, void *hip_stream);
 /* in place inclusive running product data[i] = data[0] * ... * data[i] */
 int gg_bls12_381_fr_prefix_product(void *data_dev, size_t n, void *hip_stream);
 /* value_out (host) = f(a) = sum f_i a^i (iop.Polynomial.Evaluate, canonical

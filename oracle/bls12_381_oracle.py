@@ -375,3 +375,103 @@ def linearized(blinded_z, s3, ql, qr, qm, qo, qk, pi2, qcp, s1, s2, alpha, l, r,
                 t = (t + pi2[j][i] * qcp[j]) % R
         out.append((t + zi * lag) % R)
     return out
+
+
+# ---------------------------------------------------------------- PlonK verifier (trapdoor)
+def g1_marshal(p) -> bytes:
+    """G1Affine.Marshal (RawBytes): X | Y big-endian; infinity = 0x40 | zeros."""
+    if p is INF:
+        return bytes([0x40]) + bytes(95)
+    return p[0].to_bytes(48, "big") + p[1].to_bytes(48, "big")
+
+
+class Transcript:
+    """gnark-crypto fiat-shamir (restated): challenge i = H(name_i | value_(i-1) | bindings_i)."""
+
+    def __init__(self, *names):
+        import hashlib
+        self.h = hashlib.sha256
+        self.order, self.data, self.values = list(names), {n: [] for n in names}, {}
+
+    def bind(self, name, b):
+        self.data[name].append(bytes(b))
+
+    def challenge(self, name) -> int:
+        i = self.order.index(name)
+        h = self.h()
+        h.update(name.encode())
+        if i:
+            h.update(self.values[self.order[i - 1]])
+        for d in self.data[name]:
+            h.update(d)
+        self.values[name] = h.digest()
+        return int.from_bytes(self.values[name], "big") % R
+
+
+def _derive(fs, name, *points):
+    for p in points:
+        fs.bind(name, g1_marshal(p))
+    return fs.challenge(name)
+
+
+def _kzg_check_trapdoor(digest, proof_h, point, value, tau) -> bool:
+    """KZG opening check with the SRS secret instead of the pairing:
+    [w(tau)] (tau - z) == C - [y] G  <=>  e(W, [tau - z]_2) == e(C - [y]G, G2)."""
+    lhs = g1_mul(proof_h, (tau - point) % R)
+    rhs = g1_add(digest, g1_neg(g1_mul(G1_GEN, value)))
+    return lhs == rhs
+
+
+def plonk_verify_trapdoor(proof, vk, tau) -> bool:
+    """backend/plonk/bls12-381 Verify (verify.go:45-290) for a circuit without
+    public inputs or BSB22 commitments; the two KZG batch checks use the SRS
+    trapdoor tau.  proof / vk: plain dicts of affine points (x, y ints) and fr ints:
+      proof: LRO[3], Z, H[3], batched_H, claimed[7], zs_H, zu
+      vk: n, omega, u (coset shift), S[3], Ql, Qr, Qm, Qo, Qk."""
+    n, u = vk["n"], vk["u"]
+    fs = Transcript("gamma", "beta", "alpha", "zeta")
+    for p in list(vk["S"]) + [vk["Ql"], vk["Qr"], vk["Qm"], vk["Qo"], vk["Qk"]]:
+        fs.bind("gamma", g1_marshal(p))
+    gamma = _derive(fs, "gamma", *proof["LRO"])
+    beta = _derive(fs, "beta")
+    alpha = _derive(fs, "alpha", proof["Z"])
+    zeta = _derive(fs, "zeta", *proof["H"])
+    zn = pow(zeta, n, R)
+    lag1 = (zn - 1) * pow(zeta - 1, -1, R) % R * pow(n, -1, R) % R
+    zu = proof["zu"]
+    hq, lin, l, r, o, s1, s2 = proof["claimed"]
+    # quotient identity (verify.go:158-195)
+    t = (s1 * beta + l + gamma) * (s2 * beta + r + gamma) % R * (o + gamma) % R * alpha % R * zu % R
+    rhs = (lin + t - lag1 * alpha % R * alpha) % R * pow((zn - 1) % R, -1, R) % R
+    if hq != rhs:
+        return False
+    # folded H digest and linearized digest (verify.go:197-250)
+    zp = pow(zeta, n + 2, R)
+    fh = g1_add(g1_add(proof["H"][0], g1_mul(proof["H"][1], zp)), g1_mul(proof["H"][2], zp * zp % R))
+    a1 = zu * beta % R * ((beta * s1 + l + gamma) % R) % R * ((beta * s2 + r + gamma) % R) % R * alpha % R
+    a2 = (beta * zeta + l + gamma) * ((beta * zeta * u + r + gamma) % R) % R * \
+        ((beta * zeta * u * u + o + gamma) % R) % R
+    a2 = ((-a2) * alpha + lag1 * alpha % R * alpha) % R
+    pts = [vk["Ql"], vk["Qr"], vk["Qm"], vk["Qo"], vk["Qk"], vk["S"][2], proof["Z"]]
+    scs = [l, r, l * r % R, o, 1, a1, a2]
+    lin_d = INF
+    for p, s in zip(pts, scs):
+        lin_d = g1_add(lin_d, g1_mul(p, s))
+    # kzg.FoldProof + BatchVerifyMultiPoints (verify.go:252-290), trapdoor checks
+    digests = [fh, lin_d, proof["LRO"][0], proof["LRO"][1], proof["LRO"][2], vk["S"][0], vk["S"][1]]
+    fsg = Transcript("gamma")
+    fsg.bind("gamma", (zeta % R).to_bytes(32, "big"))
+    for d in digests:
+        fsg.bind("gamma", g1_marshal(d))
+    for c in proof["claimed"]:
+        fsg.bind("gamma", (c % R).to_bytes(32, "big"))
+    fsg.bind("gamma", (zu % R).to_bytes(32, "big"))
+    gf = fsg.challenge("gamma")
+    fd, fy, gp = INF, 0, 1
+    for d, y in zip(digests, proof["claimed"]):
+        fd = g1_add(fd, g1_mul(d, gp))
+        fy = (fy + gp * y) % R
+        gp = gp * gf % R
+    if not _kzg_check_trapdoor(fd, proof["batched_H"], zeta, fy, tau):
+        return False
+    return _kzg_check_trapdoor(proof["Z"], proof["zs_H"], zeta * vk["omega"] % R, zu, tau)
