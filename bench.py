@@ -219,6 +219,14 @@ def main():
         except Exception as e:  # report, never hide
             out["plonk_bls12_381"] = {"error": repr(e)}
 
+    # ---- PlonK BLS12-381 prove, end to end (BASELINE configs[4]; rank 0 / N = 1 only)
+    stage["now"] = "plonk_prove"
+    if rank == 0 and world == 1 and args.plonk_log_n:
+        try:
+            out.setdefault("plonk_bls12_381", {})["prove"] = plonk_prove_bench(args.plonk_log_n)
+        except Exception as e:  # report, never hide
+            out.setdefault("plonk_bls12_381", {})["prove"] = {"error": repr(e)}
+
     # ---- Groth16 prove (extra): whole key at N = 1; at N > 1 one key shard per
     # GPU (wires and Z positions partitioned, h computed on every GPU, 576-B
     # partials all-gathered) -- strong scaling of one 2^log_n proof
@@ -404,6 +412,48 @@ def plonk_bench(log_n, reps=5):
     sc = [3, 5, 7, 11, 13, 17, 19, 23]
     res["linearized_ms"] = timed(lambda: plonk.linearized(z, n, xs[4], n, xs[5:10], n, sc))
     return res
+
+
+def plonk_prove_bench(log_n, reps=2, per_rep=False):
+    """BLS12-381 PlonK prove (gnark_amd.plonk_prover: every step of prove.go on the
+    GPU) at n = 2^log_n with a synthetic key (random SRS points, selectors and
+    copy permutation) and a random witness, inputs resident in HBM.  The proof of
+    a random witness does not verify; the work is that of a real proof."""
+    import numpy as np
+    from gnark_amd import fr, msm, plonk_prover as pp, DeviceBuffer
+    n = 1 << log_n
+
+    def bls_dev(k, seed):
+        a = rand_scalars(k, seed)
+        a[:, 3] &= np.uint64((1 << 60) - 1)
+        return DeviceBuffer.from_host(np.ascontiguousarray(a).tobytes())
+
+    t0 = time.time()
+    gen = fr.bls_fp_mont(BLS_G1_GEN[0]) + fr.bls_fp_mont(BLS_G1_GEN[1])
+    kzg = DeviceBuffer(96 * (n + 3))
+    msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bls_dev(n + 3, 61), n + 3, scalars_on_device=True, out=kzg)
+    lag = DeviceBuffer(96 * n)
+    msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bls_dev(n, 62), n, scalars_on_device=True, out=lag)
+    sel = [bls_dev(n, 70 + i) for i in range(8)]
+    perm = np.random.default_rng(71).permutation(3 * n).astype(np.int64).tobytes()
+    pk = pp.ProvingKey(log_n, kzg, lag, *sel, perm)
+    del kzg, lag, sel
+    L, R_, O = (bls_dev(n, 80 + i) for i in range(3))
+    t_setup = time.time() - t0
+    pp.prove(pk, L, R_, O)
+    ts, tim, tims = [], {}, []
+    for _ in range(reps):
+        t = time.perf_counter()
+        tim = {}
+        pp.prove(pk, L, R_, O, timings=tim)
+        ts.append(1e3 * (time.perf_counter() - t))
+        tims.append(tim)
+    tim = tims[ts.index(min(ts))]
+    extra = {"stage_ms_all": tims} if per_rep else {}
+    return {"log_n": log_n, "prove_ms": min(ts), "prove_ms_all": ts, "stage_ms": tim, **extra,
+            "key_setup_s": t_setup, "msms_per_proof": 10, "ntts_per_proof": "4 cosets x 14 + 4 + 1 big",
+            "note": "synthetic key + random witness (timing only; proofs of valid witnesses verify in "
+                    "tests/test_gpu_plonk_prove.py)"}
 
 
 def groth16_bench(log_n, reps=3):

@@ -88,13 +88,13 @@ static void jac_add_bytes(const void* a, const void* b, void* out) {
     memcpy(out, &r, sizeof(r));
 }
 
-template <class F>
+template <class F, class S = Fr>
 static void scalar_mul_bytes(const void* p_aff, const void* k_mont, void* out) {
     Affine<F> p;
     memcpy(&p, p_aff, sizeof(p));
-    Fr k;
+    S k;
     memcpy(&k, k_mont, 32);
-    Fr kc = from_mont(k);
+    S kc = from_mont(k);
     Jac<F> r = jac_mul(Jac<F>::from_affine(p), kc.v);
     memcpy(out, &r, sizeof(r));
 }
@@ -139,6 +139,12 @@ extern "C" int gg_g1_scalar_mul(const void* p, const void* k, void* out) {
     GG_CAPI_BEGIN
     GG_CHECK(p && k && out, GG_ERR_INVALID_ARG, "null argument");
     scalar_mul_bytes<Fp>(p, k, out);
+    GG_CAPI_END
+}
+extern "C" int gg_bls12_381_g1_scalar_mul(const void* p, const void* k, void* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(p && k && out, GG_ERR_INVALID_ARG, "null argument");
+    scalar_mul_bytes<FpBls, FrBls>(p, k, out);
     GG_CAPI_END
 }
 extern "C" int gg_g2_scalar_mul(const void* p, const void* k, void* out) {

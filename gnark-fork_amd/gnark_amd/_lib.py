@@ -68,6 +68,7 @@ def _load():
         "gg_g2_scalar_mul": ([P, P, P], I),
         "gg_bls12_381_g1_jac_to_affine": ([P, P], I),
         "gg_bls12_381_g1_jac_add": ([P, P, P], I),
+        "gg_bls12_381_g1_scalar_mul": ([P, P, P], I),
         "gg_groth16_pk_create": ([I, P, P, P, S, P, S, P, S, P, S, P, P, P, P, P, P, P, P, S, S, P, PP], I),
         "gg_groth16_pk_release": ([P], I),
         "gg_groth16_prove": ([P, P, S, P, P, P, S, I, P, P, P, P, P, P], I),
@@ -119,7 +120,7 @@ EXPORTED = [
     "gg_hshard_phase", "gg_groth16_prove_partial_dist", "gg_plonk_ratio_copy_constraint",
     "gg_bls12_381_fr_prefix_product", "gg_bls12_381_fr_horner", "gg_plonk_fold_h",
     "gg_plonk_linearized", "gg_copy_device", "gg_memset_device", "gg_bls12_381_fr_bit_reverse",
-    "gg_bls12_381_fr_axpy",
+    "gg_bls12_381_fr_axpy", "gg_bls12_381_g1_scalar_mul",
 ]
 
 

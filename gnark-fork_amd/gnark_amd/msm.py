@@ -73,7 +73,8 @@ def jac_add(group: int, a: bytes, b: bytes) -> bytes:
 
 def scalar_mul(group: int, p_aff: bytes, k_mont: bytes) -> bytes:
     out = bytearray(_JAC[group])
-    fn = lib.gg_g1_scalar_mul if group == G1 else lib.gg_g2_scalar_mul
+    fn = {G1: lib.gg_g1_scalar_mul, G2: lib.gg_g2_scalar_mul,
+          BLS12_381_G1: lib.gg_bls12_381_g1_scalar_mul}[group]
     check(fn(ptr(p_aff), ptr(k_mont), ptr(out)))
     return bytes(out)
 

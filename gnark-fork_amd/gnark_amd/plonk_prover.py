@@ -162,9 +162,17 @@ class ProvingKey:
         # coset domains of computeNumerator: coset i of the big domain is shift s_i = g wb^i
         self.coset_shift = [g * pow(wb, i, R) % R for i in range(self.rho)]
         self.dcos = [ntt.Domain(log_n, fr_b(w), fr_b(s), curve=GG_CURVE_BLS12_381) for s in self.coset_shift]
-        self.kzg_host = kzg_g1
-        self.kzg = msm.MsmBase(msm.BLS12_381_G1, kzg_g1, n + 3)
-        self.kzg_lag = msm.MsmBase(msm.BLS12_381_G1, kzg_lagrange_g1, n)
+        on_dev = isinstance(kzg_g1, DeviceBuffer)
+        self.kzg = msm.MsmBase(msm.BLS12_381_G1, kzg_g1, n + 3, on_device=on_dev)
+        self.kzg_lag = msm.MsmBase(msm.BLS12_381_G1, kzg_lagrange_g1, n,
+                                   on_device=isinstance(kzg_lagrange_g1, DeviceBuffer))
+        if on_dev:  # the two 3-point slices of commitBlindingFactor, to the host
+            lo, hi = bytearray(96 * 3), bytearray(96 * 3)
+            check(lib.gg_copy_to_host(ptr(lo), ptr(kzg_g1), len(lo)))
+            check(lib.gg_copy_to_host(ptr(hi), ctypes.c_void_p(kzg_g1.ptr + 96 * n), len(hi)))
+            blind_lo, blind_hi = bytes(lo), bytes(hi)
+        else:
+            blind_lo, blind_hi = kzg_g1[:96 * 3], kzg_g1[96 * n:96 * (n + 3)]
         nb = 32 * n
         # trace: canonical regular (commitments, openings, linearization) and
         # canonical bit-reversed (input of the coset DIT FFTs)
@@ -182,15 +190,52 @@ class ProvingKey:
             self.brev[name], self.reg[name] = b, reg
         self.perm = DeviceBuffer.from_host(perm) if not isinstance(perm, DeviceBuffer) else perm
         # blinding-commitment bases: G1[:3] and G1[n:n+3] (commitBlindingFactor)
-        self.blind_lo = msm.MsmBase(msm.BLS12_381_G1, kzg_g1[:96 * 3], 3)
-        self.blind_hi = msm.MsmBase(msm.BLS12_381_G1, kzg_g1[96 * n:96 * (n + 3)], 3)
+        self.blind_lo, self.blind_hi = blind_lo, blind_hi  # G1[:3], G1[n:n+3] (host)
+        # constant polynomials of computeNumerator: LOne (canonical: 1/n everywhere)
+        # and s.twiddles0 (w^j)
+        self.lone = DeviceBuffer(nb)
+        inv_n = fr_b(pow(n, -1, R))
+        chunk = inv_n * min(n, 1 << 16)
+        for off in range(0, nb, len(chunk)):
+            m = min(len(chunk), nb - off)
+            check(lib.gg_copy_to_device(ctypes.c_void_p(self.lone.ptr + off), ptr(chunk[:m]), m))
+        self.tw0 = _twiddles_dev(self)
+        # coset evaluations of the key's polynomials, computed once (the reference
+        # recomputes these rho * 2 FFTs per proof, prove.go:990-994, to save memory;
+        # on 288 GB of HBM they stay resident): Ql..S3, X (for ID = beta X) and LOne
+        xb = DeviceBuffer(nb)
+        dzero(xb, nb)
+        if n > 1:
+            check(lib.gg_copy_to_device(ctypes.c_void_p(xb.ptr + 32 * (n // 2)), ptr(fr_b(1)), 32))
+        else:
+            check(lib.gg_copy_to_device(ctypes.c_void_p(xb.ptr), ptr(fr_b(0)), 32))
+        src = dict(self.brev)
+        src["X"], src["LOne"] = xb, self.lone
+        self.coset_evals = {}
+        for name, b in src.items():
+            evs = []
+            for i in range(self.rho):
+                e = DeviceBuffer(nb)
+                dcopy(e, b, nb)
+                self.dcos[i].fft(e, ntt.DIT, coset=True)
+                evs.append(e)
+            self.coset_evals[name] = evs
+        del xb
+        self.ws = {}  # per-proof workspace, allocated on first use and reused
         self.vk = vk if vk is not None else commit_trace(self)
+
+    def buf(self, name: str, nbytes: int) -> DeviceBuffer:
+        """Workspace buffer reused across proofs (no per-proof hipMalloc)."""
+        b = self.ws.get(name)
+        if b is None or b.nbytes < nbytes:
+            b = self.ws[name] = DeviceBuffer(nbytes)
+        return b
 
     def commit(self, buf, length: int) -> bytes:
         """kzg.Commit(p, pk.Kzg) of a canonical polynomial of `length` <= n+3 coefficients."""
         if length == self.n + 3:
             return self.kzg.msm(buf, length, on_device=True)
-        pad = DeviceBuffer(32 * (self.n + 3))
+        pad = self.buf("commit_pad", 32 * (self.n + 3))
         dzero(pad, pad.nbytes)
         dcopy(pad, buf, 32 * length)
         return self.kzg.msm(pad, self.n + 3, on_device=True)
@@ -218,10 +263,13 @@ class Proof:
 # ------------------------------------------------------------------ prover
 def _blind_commit(pk: ProvingKey, coeffs: List[int]) -> bytes:
     """commitBlindingFactor (prove.go:1159-1172): [b(X) (X^n - 1)]."""
-    sc = b"".join(fr_b(c) for c in coeffs) + bytes(32 * (3 - len(coeffs)))
-    hi = pk.blind_hi.msm_jac(sc, 3)
-    lo = pk.blind_lo.msm_jac(b"".join(fr_b((-c) % R) for c in coeffs) + bytes(32 * (3 - len(coeffs))), 3)
-    return msm.jac_add(msm.BLS12_381_G1, hi, lo)
+    G = msm.BLS12_381_G1
+    acc = None
+    for j, c in enumerate(coeffs):
+        for base, k in ((pk.blind_hi, c), (pk.blind_lo, (-c) % R)):
+            t = msm.scalar_mul(G, base[96 * j:96 * (j + 1)], fr_b(k))
+            acc = t if acc is None else msm.jac_add(G, acc, t)
+    return acc
 
 
 def _commit_poly_and_blinding(pk: ProvingKey, lag, coeffs: List[int]) -> bytes:
@@ -230,10 +278,10 @@ def _commit_poly_and_blinding(pk: ProvingKey, lag, coeffs: List[int]) -> bytes:
     return msm.jac_to_affine(msm.BLS12_381_G1, msm.jac_add(msm.BLS12_381_G1, j, _blind_commit(pk, coeffs)))
 
 
-def _blinded_coeffs(pk: ProvingKey, canon_reg, b: List[int]):
+def _blinded_coeffs(pk: ProvingKey, canon_reg, b: List[int], name: str):
     """getBlindedCoefficients (prove.go:1148-1157): p | b, with p[i] -= b[i]."""
     n = pk.n
-    out = DeviceBuffer(32 * (n + len(b)))
+    out = pk.buf("blinded_" + name, 32 * (n + len(b)))
     dcopy(out, canon_reg, 32 * n)
     tail = b"".join(fr_b(c) for c in b)
     check(lib.gg_copy_to_device(ctypes.c_void_p(out.ptr + 32 * n), ptr(tail), len(tail)))
@@ -244,7 +292,7 @@ def _blinded_coeffs(pk: ProvingKey, canon_reg, b: List[int]):
 
 def _open(pk: ProvingKey, poly, length: int, point: int):
     """kzg.Open (gnark-crypto [ext]): claimed value f(point) and H = Commit((f - f(a))/(X - a))."""
-    q = DeviceBuffer(32 * max(length - 1, 1))
+    q = pk.buf("open_q", 32 * max(length - 1, 1))
     val = fr_int(plonk.evaluate(poly, length, fr_b(point), q_out=q))
     return val, pk.commit(q, length - 1)
 
@@ -282,7 +330,7 @@ def prove(pk: ProvingKey, L, R_, O, rng=None, timings: Optional[dict] = None) ->
     beta = int.from_bytes(fs.compute("beta"), "big") % R
 
     # buildRatioCopyConstraint
-    z = DeviceBuffer(nb)
+    z = pk.buf("z", nb)
     plonk.ratio_copy_constraint(x["L"], x["R"], x["O"], pk.perm, n, fr_b(beta), fr_b(gamma),
                                 fr_b(pk.omega), fr_b(pk.g), z)
     z_commit = _commit_poly_and_blinding(pk, z, bp[3])
@@ -292,36 +340,31 @@ def prove(pk: ProvingKey, L, R_, O, rng=None, timings: Optional[dict] = None) ->
     # canonical forms: bit-reversed (coset FFT input) and regular (openings)
     brev, reg = {}, {}
     for k, v in (("L", x["L"]), ("R", x["R"]), ("O", x["O"]), ("Z", z)):
-        b = DeviceBuffer(nb)
+        b = pk.buf("brev_" + k, nb)
         dcopy(b, v, nb)
         pk.d0.fft_inverse(b, ntt.DIF)
-        r = DeviceBuffer(nb)
+        r = pk.buf("reg_" + k, nb)
         bit_reverse(b, r, n)
         brev[k], reg[k] = b, r
-    # ID = beta X (canonical; prove.go:578-580), LOne = Lagrange [1, 0, ...]
-    idb = DeviceBuffer(nb)
-    dzero(idb, nb)
-    if n > 1:
-        check(lib.gg_copy_to_device(ctypes.c_void_p(idb.ptr + 32 * (n // 2)), ptr(fr_b(beta)), 32))
-    lone = DeviceBuffer(nb)
-    check(lib.gg_copy_to_device(ctypes.c_void_p(lone.ptr), ptr(fr.bls_fr_mont(pow(n, -1, R)) * n), nb))
-    brev["ID"], brev["LOne"] = idb, lone  # LOne canonical = 1/n everywhere (order-free)
     mark("canonical")
 
-    # computeNumerator: per coset i, evaluations of every polynomial on g wb^i <w>
+    # computeNumerator: per coset i, evaluations of every polynomial on g wb^i <w>;
+    # the key's polynomials (and X, LOne) come precomputed from the key
     order = ["L", "R", "O", "Z", None, "Ql", "Qr", "Qm", "Qo", "Qk", "S1", "S2", "S3", "ID", "LOne"]
-    ev = [DeviceBuffer(nb) for _ in order]
-    cres = DeviceBuffer(32 * n * pk.rho)
-    tw0 = DeviceBuffer.from_host(b"".join(fr_b(pow(pk.omega, j, R)) for j in range(n))) \
-        if n <= 4096 else _twiddles_dev(pk)
+    ev = [pk.buf("ev%d" % k, nb) for k in range(5)] + [None] * 10
+    idb = pk.buf("ev_id", nb)
+    cres = pk.buf("cres", 32 * n * pk.rho)
+    tw0 = pk.tw0
     for i in range(pk.rho):
         s = pk.coset_shift[i]
-        for slot, k in enumerate(order):
-            if k is None:
-                continue
-            src = brev[k] if k in brev else pk.brev[k]
-            dcopy(ev[slot], src, nb)
+        for slot, k in enumerate(order[:4]):
+            dcopy(ev[slot], brev[k], nb)
             pk.dcos[i].fft(ev[slot], ntt.DIT, coset=True)  # bit-reversed -> natural coset evaluations
+        for slot in range(5, 13):
+            ev[slot] = pk.coset_evals[order[slot]][i]
+        dzero(idb, nb)
+        axpy(idb, pk.coset_evals["X"][i], n, beta)  # ID = beta X (prove.go:578-580)
+        ev[13], ev[14] = idb, pk.coset_evals["LOne"][i]
         # ZS(x) = Z(w x): the evaluations shifted by one (Shift(1), prove.go:582)
         dcopy(ev[4], ctypes.c_void_p(ev[3].ptr + 32), nb - 32)
         dcopy(ctypes.c_void_p(ev[4].ptr + nb - 32), ev[3], 32)
@@ -329,8 +372,10 @@ def prove(pk: ProvingKey, L, R_, O, rng=None, timings: Optional[dict] = None) ->
         bl = [[fr_b(c * pow(s, j, R) % R * sn1) for j, c in enumerate(q)] for q in bp]
         plonk.numerator_coset(ev, bl, tw0, fr_b(beta), fr_b(gamma), fr_b(alpha), fr_b(pk.g), n,
                               pk.rho, i, cres)
+    check(lib.gg_synchronize())
     mark("numerator")
     plonk.divide_by_xn_minus_one(pk.d1, n, cres)  # h, canonical regular, rho n
+    mark("divide")
     # commitToQuotient: h1, h2, h3 of n + 2 coefficients
     hs = [ctypes.c_void_p(cres.ptr + 32 * (n + 2) * k) for k in range(3)]
     H = [pk.commit(hs[k], n + 2) for k in range(3)]
@@ -338,16 +383,16 @@ def prove(pk: ProvingKey, L, R_, O, rng=None, timings: Optional[dict] = None) ->
     zeta = derive_randomness(fs, "zeta", *H)
 
     # openZ at w zeta (blinded Z)
-    bz = _blinded_coeffs(pk, reg["Z"], bp[3])
+    bz = _blinded_coeffs(pk, reg["Z"], bp[3], "Z")
     zu, zs_H = _open(pk, bz, n + 3, zeta * pk.omega % R)
     mark("open_z")
 
     # foldH
     zp = pow(zeta, n + 2, R)
-    folded = DeviceBuffer(32 * (n + 2))
+    folded = pk.buf("folded_h", 32 * (n + 2))
     plonk.fold_h(cres, n, fr_b(zp), folded)
-    hb = msm.MsmBase(msm.BLS12_381_G1, b"".join(H), 3)
-    folded_digest = hb.msm(fr_b(1) + fr_b(zp) + fr_b(zp * zp), 3)
+    folded_digest = fold_digests(H, [1, zp, zp * zp % R])
+    mark("fold_h")
 
     # computeLinearizedPolynomial
     zn1 = (pow(zeta, n, R) - 1) % R
@@ -357,22 +402,25 @@ def prove(pk: ProvingKey, L, R_, O, rng=None, timings: Optional[dict] = None) ->
 
     l_z, r_z, o_z = blinded_eval("L", bp[0]), blinded_eval("R", bp[1]), blinded_eval("O", bp[2])
     s1_z, s2_z = poly_eval(pk.reg["S1"], n, zeta), poly_eval(pk.reg["S2"], n, zeta)
+    mark("evaluations")
     sc = plonk.linearized_scalars(l_z, r_z, o_z, alpha, beta, gamma, zeta, zu, s1_z, s2_z, pk.g, n)
-    lin = DeviceBuffer(32 * (n + 3))
+    lin = pk.buf("lin", 32 * (n + 3))
     dcopy(lin, bz, 32 * (n + 3))
     plonk.linearized(lin, n + 3, pk.reg["S3"], n,
                      [pk.reg[k] for k in ("Ql", "Qr", "Qm", "Qo", "Qk")], n, sc)
+    mark("linearize")
     lin_digest = pk.commit(lin, n + 3)
     mark("linearized")
 
     # batchOpening: kzg.BatchOpenSinglePoint at zeta
-    polys = [(folded, n + 2), (lin, n + 3), (_blinded_coeffs(pk, reg["L"], bp[0]), n + 2),
-             (_blinded_coeffs(pk, reg["R"], bp[1]), n + 2), (_blinded_coeffs(pk, reg["O"], bp[2]), n + 2),
+    polys = [(folded, n + 2), (lin, n + 3), (_blinded_coeffs(pk, reg["L"], bp[0], "L"), n + 2),
+             (_blinded_coeffs(pk, reg["R"], bp[1], "R"), n + 2),
+             (_blinded_coeffs(pk, reg["O"], bp[2], "O"), n + 2),
              (pk.reg["S1"], n), (pk.reg["S2"], n)]
     digests = [folded_digest, lin_digest, lro[0], lro[1], lro[2], pk.vk.S[0], pk.vk.S[1]]
     claimed = [poly_eval(p_, m, zeta) for p_, m in polys]
     gfold = fold_gamma(zeta, digests, claimed, fr_marshal(zu))
-    acc = DeviceBuffer(32 * (n + 3))
+    acc = pk.buf("fold_acc", 32 * (n + 3))
     dzero(acc, acc.nbytes)
     gp = 1
     for p_, m in polys:
@@ -387,6 +435,16 @@ def prove(pk: ProvingKey, L, R_, O, rng=None, timings: Optional[dict] = None) ->
             prev = v
         timings["total"] = 1e3 * (prev - t0)
     return Proof(lro, z_commit, H, batched_H, claimed, zs_H, zu)
+
+
+def fold_digests(points: List[bytes], scalars: List[int]) -> bytes:
+    """sum k_i P_i for a handful of digests (host scalar multiplications)."""
+    G = msm.BLS12_381_G1
+    acc = None
+    for p_, k in zip(points, scalars):
+        j = msm.scalar_mul(G, p_, fr_b(k))
+        acc = j if acc is None else msm.jac_add(G, acc, j)
+    return msm.jac_to_affine(G, acc)
 
 
 def fold_gamma(point: int, digests: List[bytes], claimed: List[int], data: bytes) -> int:
@@ -406,6 +464,8 @@ def fold_gamma(point: int, digests: List[bytes], claimed: List[int], data: bytes
 def _twiddles_dev(pk: ProvingKey):
     """s.twiddles0 = w^j (j < n) on the device: FFT of the coefficient vector e_1."""
     n = pk.n
+    if n == 1:
+        return DeviceBuffer.from_host(fr_b(1))
     b = DeviceBuffer(32 * n)
     dzero(b, b.nbytes)
     check(lib.gg_copy_to_device(ctypes.c_void_p(b.ptr + 32 * (n // 2)), ptr(fr_b(1)), 32))

@@ -153,6 +153,8 @@ int gg_g2_scalar_mul(const void *p_aff, const void *k_mont, void *out_jac);
 /* BLS12-381 G1 (curve.G1Jac.FromJacobian / AddAssign of gnark-crypto bls12-381) */
 int gg_bls12_381_g1_jac_to_affine(const void *jac, void *aff);
 int gg_bls12_381_g1_jac_add(const void *a_jac, const void *b_jac, void *out_jac);
+/* out (Jacobian) = k * p, p affine, k bls12-381 fr Montgomery (host; KZG digest folding) */
+int gg_bls12_381_g1_scalar_mul(const void *p_aff, const void *k_mont, void *out_jac);
 
 /* Fixed-base batch scalar multiplication out[i] = k_i * base (affine,
  * infinity for k_i = 0): replaces curve.BatchScalarMultiplicationG1/G2

@@ -1,0 +1,22 @@
+#!/usr/bin/env python3
+"""PlonK BLS12-381 prove timing (gnark_amd.plonk_prover) with per-stage times.
+usage: bench_plonk.py log_n [reps]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gnark-fork_amd"))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def main():
+    L = int(sys.argv[1]) if len(sys.argv) > 1 else 22
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+    r = bench.plonk_prove_bench(L, reps=reps, per_rep=True)
+    print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
