@@ -220,12 +220,17 @@ def main():
             out["plonk_bls12_381"] = {"error": repr(e)}
 
     # ---- PlonK BLS12-381 prove, end to end (BASELINE configs[4]; rank 0 / N = 1 only)
+    # (at N > 1 every rank keeps a 1/N slice of the KZG bases; commitments are
+    # partial MSMs all-gathered over RCCL, the rest of the prover is replicated)
     stage["now"] = "plonk_prove"
-    if rank == 0 and world == 1 and args.plonk_log_n:
+    if args.plonk_log_n:
         try:
-            out.setdefault("plonk_bls12_381", {})["prove"] = plonk_prove_bench(args.plonk_log_n)
+            pr = plonk_prove_bench(args.plonk_log_n, rank=rank, world=world, dist=dist, xdev=xdev,
+                                   barrier=barrier)
         except Exception as e:  # report, never hide
-            out.setdefault("plonk_bls12_381", {})["prove"] = {"error": repr(e)}
+            pr = {"error": repr(e)}
+        if rank == 0:
+            out.setdefault("plonk_bls12_381", {})["prove"] = pr
 
     # ---- Groth16 prove (extra): whole key at N = 1; at N > 1 one key shard per
     # GPU (wires and Z positions partitioned, h computed on every GPU, 576-B
@@ -414,7 +419,8 @@ def plonk_bench(log_n, reps=5):
     return res
 
 
-def plonk_prove_bench(log_n, reps=2, per_rep=False):
+def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, xdev=None,
+                      barrier=None):
     """BLS12-381 PlonK prove (gnark_amd.plonk_prover: every step of prove.go on the
     GPU) at n = 2^log_n with a synthetic key (random SRS points, selectors and
     copy permutation) and a random witness, inputs resident in HBM.  The proof of
@@ -436,22 +442,45 @@ def plonk_prove_bench(log_n, reps=2, per_rep=False):
     msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bls_dev(n, 62), n, scalars_on_device=True, out=lag)
     sel = [bls_dev(n, 70 + i) for i in range(8)]
     perm = np.random.default_rng(71).permutation(3 * n).astype(np.int64).tobytes()
-    pk = pp.ProvingKey(log_n, kzg, lag, *sel, perm)
+    shard, reduce = None, None
+    if world > 1:
+        from gnark_amd import dist as gdist
+        shard = (rank, world)
+
+        def reduce(jac):
+            return gdist.allgather_partial(msm.BLS12_381_G1, jac, device=xdev)
+    pk = pp.ProvingKey(log_n, kzg, lag, *sel, perm, shard=shard, reduce=reduce)
     del kzg, lag, sel
     L, R_, O = (bls_dev(n, 80 + i) for i in range(3))
     t_setup = time.time() - t0
-    pp.prove(pk, L, R_, O)
+
+    def rng():  # the blinding randomness must be identical on every rank
+        import random
+        return random.Random(1234)
+
+    pp.prove(pk, L, R_, O, rng=rng())
     ts, tim, tims = [], {}, []
     for _ in range(reps):
+        if barrier is not None and world > 1:
+            barrier()
         t = time.perf_counter()
         tim = {}
-        pp.prove(pk, L, R_, O, timings=tim)
-        ts.append(1e3 * (time.perf_counter() - t))
+        pp.prove(pk, L, R_, O, timings=tim, rng=rng())
+        if barrier is not None and world > 1:
+            barrier()
+        el = 1e3 * (time.perf_counter() - t)
+        if world > 1:
+            import torch
+            tt = torch.tensor([el], dtype=torch.float64, device=xdev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        ts.append(el)
         tims.append(tim)
     tim = tims[ts.index(min(ts))]
     extra = {"stage_ms_all": tims} if per_rep else {}
-    return {"log_n": log_n, "prove_ms": min(ts), "prove_ms_all": ts, "stage_ms": tim, **extra,
-            "key_setup_s": t_setup, "msms_per_proof": 10, "ntts_per_proof": "4 cosets x 14 + 4 + 1 big",
+    return {"log_n": log_n, "n_gpus": world, "prove_ms": min(ts), "prove_ms_all": ts, "stage_ms": tim,
+            **extra, "kzg_bases": "1/%d slice per GPU, partial commitments all-gathered" % world,
+            "key_setup_s": t_setup, "msms_per_proof": 10, "ntts_per_proof": "16 coset FFTs (L,R,O,Z x 4 cosets; key polynomials resident) + 4 iFFTs of n + 1 coset iFFT of 4n",
             "note": "synthetic key + random witness (timing only; proofs of valid witnesses verify in "
                     "tests/test_gpu_plonk_prove.py)"}
 

@@ -144,11 +144,19 @@ class ProvingKey:
     KZG bases (pk.Kzg.G1[:n+3] and pk.KzgLagrange.G1[:n]) and the domains."""
 
     def __init__(self, log_n: int, kzg_g1: bytes, kzg_lagrange_g1: bytes, ql, qr, qm, qo, qk,
-                 s1, s2, s3, perm, vk: Optional[VerifyingKey] = None, big_log: int = None):
+                 s1, s2, s3, perm, vk: Optional[VerifyingKey] = None, big_log: int = None,
+                 shard=None, reduce=None):
         """kzg_g1: n+3 affine points [tau^i]G; kzg_lagrange_g1: n points [L_i(tau)]G;
         ql..qk: Lagrange regular selectors; s1..s3: permutation polynomials in
         Lagrange regular form (computePermutationPolynomials); perm: 3n int64
-        (pk.trace.S).  All fr vectors: Montgomery bytes or device buffers of n fr."""
+        (pk.trace.S).  All fr vectors: Montgomery bytes or device buffers of n fr.
+
+        Multi-GPU: shard = (rank, world) keeps only this rank's
+        contiguous slice of each KZG base resident; every commitment is then a
+        partial MSM over the slice and `reduce(jac) -> jac` (an all-gather + exact
+        add across ranks, gnark_amd.dist.allgather_partial) completes it.  All
+        other work is replicated, so every rank holds the same polynomials and
+        transcript (the blinding randomness must be the same on all ranks)."""
         self.log_n = log_n
         self.n = n = 1 << log_n
         self.big_log = big_log if big_log is not None else log_n + 2
@@ -163,9 +171,20 @@ class ProvingKey:
         self.coset_shift = [g * pow(wb, i, R) % R for i in range(self.rho)]
         self.dcos = [ntt.Domain(log_n, fr_b(w), fr_b(s), curve=GG_CURVE_BLS12_381) for s in self.coset_shift]
         on_dev = isinstance(kzg_g1, DeviceBuffer)
-        self.kzg = msm.MsmBase(msm.BLS12_381_G1, kzg_g1, n + 3, on_device=on_dev)
-        self.kzg_lag = msm.MsmBase(msm.BLS12_381_G1, kzg_lagrange_g1, n,
-                                   on_device=isinstance(kzg_lagrange_g1, DeviceBuffer))
+        from .dist import shard_range
+        rank, world = shard if shard is not None else (0, 1)
+        self.reduce = reduce if reduce is not None else (lambda j: j)
+        self.k_lo, self.k_hi = shard_range(n + 3, rank, world)
+        self.l_lo, self.l_hi = shard_range(n, rank, world)
+
+        def base(points, lo, hi, dev):
+            if dev:
+                return msm.MsmBase(msm.BLS12_381_G1, points.ptr + 96 * lo, hi - lo, on_device=True)
+            return msm.MsmBase(msm.BLS12_381_G1, points[96 * lo:96 * hi], hi - lo)
+
+        self.kzg = base(kzg_g1, self.k_lo, self.k_hi, on_dev)
+        self.kzg_lag = base(kzg_lagrange_g1, self.l_lo, self.l_hi,
+                            isinstance(kzg_lagrange_g1, DeviceBuffer))
         if on_dev:  # the two 3-point slices of commitBlindingFactor, to the host
             lo, hi = bytearray(96 * 3), bytearray(96 * 3)
             check(lib.gg_copy_to_host(ptr(lo), ptr(kzg_g1), len(lo)))
@@ -231,14 +250,24 @@ class ProvingKey:
             b = self.ws[name] = DeviceBuffer(nbytes)
         return b
 
+    def commit_jac(self, buf, length: int) -> bytes:
+        """kzg.Commit(p, pk.Kzg) (Jacobian) of a canonical polynomial of `length`
+        <= n+3 coefficients: this rank's partial MSM, completed by reduce()."""
+        src = buf
+        if length < self.k_hi:
+            src = self.buf("commit_pad", 32 * (self.n + 3))
+            dzero(src, src.nbytes)
+            dcopy(src, buf, 32 * length)
+        addr = (src.ptr if isinstance(src, DeviceBuffer) else src.value) + 32 * self.k_lo
+        return self.reduce(self.kzg.msm_jac(addr, self.k_hi - self.k_lo, on_device=True))
+
     def commit(self, buf, length: int) -> bytes:
-        """kzg.Commit(p, pk.Kzg) of a canonical polynomial of `length` <= n+3 coefficients."""
-        if length == self.n + 3:
-            return self.kzg.msm(buf, length, on_device=True)
-        pad = self.buf("commit_pad", 32 * (self.n + 3))
-        dzero(pad, pad.nbytes)
-        dcopy(pad, buf, 32 * length)
-        return self.kzg.msm(pad, self.n + 3, on_device=True)
+        return msm.jac_to_affine(msm.BLS12_381_G1, self.commit_jac(buf, length))
+
+    def commit_lagrange_jac(self, buf) -> bytes:
+        """kzg.Commit(p, pk.KzgLagrange) of n Lagrange values (Jacobian)."""
+        addr = (buf.ptr if isinstance(buf, DeviceBuffer) else buf.value) + 32 * self.l_lo
+        return self.reduce(self.kzg_lag.msm_jac(addr, self.l_hi - self.l_lo, on_device=True))
 
 
 def commit_trace(pk: ProvingKey) -> VerifyingKey:
@@ -274,7 +303,7 @@ def _blind_commit(pk: ProvingKey, coeffs: List[int]) -> bytes:
 
 def _commit_poly_and_blinding(pk: ProvingKey, lag, coeffs: List[int]) -> bytes:
     """commitToPolyAndBlinding (prove.go:492-502): Commit(p, pk.KzgLagrange) + [b (X^n - 1)]."""
-    j = pk.kzg_lag.msm_jac(lag, pk.n, on_device=True)
+    j = pk.commit_lagrange_jac(lag)
     return msm.jac_to_affine(msm.BLS12_381_G1, msm.jac_add(msm.BLS12_381_G1, j, _blind_commit(pk, coeffs)))
 
 

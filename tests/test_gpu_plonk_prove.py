@@ -78,21 +78,29 @@ def build_circuit(log_n, seed, break_gate=False, break_copy=False):
     return n, (ql, qr, qm, qo, qk), perm, (L, Rv, O)
 
 
-def make_key(log_n, sel, perm, tau):
-    from gnark_amd import msm, plonk_prover as pp, fr
+def srs(log_n, tau):
+    from gnark_amd import msm, fr
     n = 1 << log_n
     w = fr.bls_domain_generator(log_n)
-    u = fr.BLS_FR_MULTIPLICATIVE_GEN
     gen = bo.g1_to_bytes(bo.G1_GEN)
     pw = b"".join(bo.fr_to_bytes(pow(tau, i, R)) for i in range(n + 3))
     kzg = msm.batch_scalar_mul(msm.BLS12_381_G1, gen, pw, n + 3)
     zn = (pow(tau, n, R) - 1) % R
     lag = [pow(w, i, R) * zn % R * pow(n * (tau - pow(w, i, R)), -1, R) % R for i in range(n)]
-    kzg_lag = msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bo.fr_vec_to_bytes(lag), n)
+    return kzg, msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bo.fr_vec_to_bytes(lag), n)
+
+
+def make_key(log_n, sel, perm, tau, shard=None, reduce=None, key_srs=None):
+    from gnark_amd import msm, plonk_prover as pp, fr
+    n = 1 << log_n
+    w = fr.bls_domain_generator(log_n)
+    u = fr.BLS_FR_MULTIPLICATIVE_GEN
+    kzg, kzg_lag = key_srs if key_srs is not None else srs(log_n, tau)
     ids = [pow(u, s // n, R) * pow(w, s % n, R) % R for s in range(3 * n)]
     s123 = [[ids[perm[j * n + i]] for i in range(n)] for j in range(3)]
     pk = pp.ProvingKey(log_n, kzg, kzg_lag, *[bo.fr_vec_to_bytes(q) for q in sel],
-                       *[bo.fr_vec_to_bytes(s) for s in s123], np.asarray(perm, np.int64).tobytes())
+                       *[bo.fr_vec_to_bytes(s) for s in s123], np.asarray(perm, np.int64).tobytes(),
+                       shard=shard, reduce=reduce)
     return pk
 
 
@@ -142,3 +150,53 @@ def test_plonk_prove_rejects_bad_witness(which):
                      rng=random.Random(5))
     pr, vk = to_oracle(pk, proof)
     assert not bo.plonk_verify_trapdoor(pr, vk, tau)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_plonk_prove_sharded_kzg_matches(world):
+    """Multi-GPU layout rehearsed on one GPU: `world` key shards (a KZG-base slice
+    each, one thread per rank, partial commitments summed through an in-process
+    all-gather) produce exactly the single-key proof."""
+    import threading
+    from gnark_amd import msm, plonk_prover as pp
+    log_n = 6
+    n, sel, perm, (L, Rv, O) = build_circuit(log_n, 21)
+    tau = random.Random(8).randrange(2, R)
+    key_srs = srs(log_n, tau)
+    wit = [bo.fr_vec_to_bytes(v) for v in (L, Rv, O)]
+    pk0 = make_key(log_n, sel, perm, tau, key_srs=key_srs)
+    ref = pp.prove(pk0, *wit, rng=random.Random(42))
+    slots = [None] * world
+    bar = threading.Barrier(world)
+
+    def reducer(r):
+        def red(jac):
+            slots[r] = jac
+            bar.wait()
+            acc = slots[0]
+            for j in slots[1:]:
+                acc = msm.jac_add(msm.BLS12_381_G1, acc, j)
+            bar.wait()
+            return acc
+        return red
+
+    keys, proofs, errs = [None] * world, [None] * world, []
+
+    def run(r):
+        try:
+            keys[r] = make_key(log_n, sel, perm, tau, shard=(r, world), reduce=reducer(r), key_srs=key_srs)
+            proofs[r] = pp.prove(keys[r], *wit, rng=random.Random(42))
+        except Exception as e:  # pragma: no cover
+            errs.append(e)
+            bar.abort()
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not errs, errs
+    for p in proofs:
+        assert p == ref
+    pr, vk = to_oracle(pk0, proofs[0])
+    assert bo.plonk_verify_trapdoor(pr, vk, tau)
