@@ -47,6 +47,8 @@ def _load():
         "gg_copy_to_host": ([P, P, S], I),
         "gg_synchronize": ([], I),
         "gg_copy_device": ([P, P, S], I),
+        "gg_fr_from_canonical_be": ([I, P, P, S, ctypes.POINTER(ctypes.c_uint64), P], I),
+        "gg_fr_to_canonical_be": ([I, P, P, S, P], I),
         "gg_memset_device": ([P, I, S], I),
         "gg_bls12_381_fr_bit_reverse": ([P, P, S, P], I),
         "gg_bls12_381_fr_axpy": ([P, P, S, P, P], I),
@@ -120,7 +122,8 @@ EXPORTED = [
     "gg_hshard_phase", "gg_groth16_prove_partial_dist", "gg_plonk_ratio_copy_constraint",
     "gg_bls12_381_fr_prefix_product", "gg_bls12_381_fr_horner", "gg_plonk_fold_h",
     "gg_plonk_linearized", "gg_copy_device", "gg_memset_device", "gg_bls12_381_fr_bit_reverse",
-    "gg_bls12_381_fr_axpy", "gg_bls12_381_g1_scalar_mul",
+    "gg_bls12_381_fr_axpy", "gg_bls12_381_g1_scalar_mul", "gg_fr_from_canonical_be",
+    "gg_fr_to_canonical_be",
 ]
 
 

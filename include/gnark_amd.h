@@ -333,6 +333,18 @@ int gg_plonk_linearized(void *blinded_z_dev, size_t nz, const void *s3_dev, size
                         const void *const *q_dev, size_t nq, const void *const *pi2_dev,
                         const void *qcp_zeta, int n_cmt, const void *scalars8, void *hip_stream);
 
+/* ---- witness / fr.Vector binary format (backend/witness/witness.go:15-36)
+ * Field elements are serialised as 32-byte big-endian canonical integers; the
+ * prover uses gnark-crypto's in-memory layout (Montgomery, LE limbs).
+ * gg_fr_from_canonical_be: in_dev (n x 32 B big-endian) -> out_dev (Montgomery),
+ *   may alias; fails (GG_ERR_INVALID_ARG) if any element is >= r, as
+ *   fr.Vector.ReadFrom does; *n_invalid (nullable) = their count.
+ * gg_fr_to_canonical_be: the inverse (fr.Vector.WriteTo element encoding).
+ * curve: GG_CURVE_BN254 or GG_CURVE_BLS12_381 (scalar field). */
+int gg_fr_from_canonical_be(int curve, const void *in_dev, void *out_dev, size_t n,
+                            uint64_t *n_invalid, void *hip_stream);
+int gg_fr_to_canonical_be(int curve, const void *in_dev, void *out_dev, size_t n, void *hip_stream);
+
 /* ------------------------------------------------------------ profiling
  * Kernel-level timing with HIP events recorded on the stream each kernel is
  * launched on (bench.py uses it for the roofline of the dominant kernel).
