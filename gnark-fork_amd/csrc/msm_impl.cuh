@@ -185,13 +185,16 @@ __global__ void __launch_bounds__(256, 2) k_accum_affine(const Affine<F>* pts, c
 
 // In-place segmented tree over the level-1 partials: bucket b owns slots
 // [item_off[b], item_off[b+1]); after the launches with stride 1, 2, 4, ...
-// slot item_off[b] holds the bucket sum.  One thread per slot, no host syncs.
+// slot item_off[b] holds the bucket sum.  One quad per slot (xyzz_add_quad), no
+// host syncs.
 template <class F>
 __global__ void __launch_bounds__(256) k_seg_tree(Xyzz<F>* part, const uint32_t* item_off,
                                                   const uint32_t* item_bucket, size_t T,
                                                   uint32_t stride, uint32_t fan) {
-    size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= T) return;
+    const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = (uint32_t)g & 3;
+    const size_t p = g >> 2;
+    if (p >= T) return;  // every branch below is uniform over the quad
     uint32_t b = item_bucket[p];
     uint32_t o = item_off[b];
     uint32_t j = (uint32_t)p - o;
@@ -200,21 +203,111 @@ __global__ void __launch_bounds__(256) k_seg_tree(Xyzz<F>* part, const uint32_t*
     if (j % (fan * stride)) return;
     if (j + stride >= cnt) return;
     Xyzz<F> acc = ld(part + p);
-    for (uint32_t k = 1; k < fan && j + k * stride < cnt; k++) xyzz_add_inplace(acc, ld(part + p + k * stride));
-    st(part + p, acc);
+    for (uint32_t k = 1; k < fan && j + k * stride < cnt; k++) xyzz_add_quad(acc, ld(part + p + k * stride), lane);
+    if (lane == 0) st(part + p, acc);
 }
 
-// One thread per light bucket sums its <= LIGHT partials in a chain (the G2
-// path; G1 merges light buckets inside k_accum_affine).
+// ---- quad-cooperative XYZZ add (latency-bound tree levels) -----------------
+// The four lanes of a quad (lanes 4j..4j+3 of a wave) hold the same p and q and
+// compute p + q (add-2008-s) together: in each of four rounds every lane does
+// one of the independent products and the quad swaps them through DPP
+// quad_perm broadcasts.  The dependent chain is 4 products instead of the ~15
+// one lane issues, which is what the reduction levels pay: there are few sums
+// in flight there, so the chip is idle and a level lasts one add's latency.
+template <int SRC, class T>
+__device__ __forceinline__ T quad_bcast(const T& v) {
+    static_assert(sizeof(T) % 4 == 0 && SRC >= 0 && SRC < 4, "word-sized, lane of a quad");
+    T r;
+    const int* s = reinterpret_cast<const int*>(&v);
+    int* d = reinterpret_cast<int*>(&r);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); i++)
+        d[i] = __builtin_amdgcn_mov_dpp(s[i], SRC * 0x55, 0xf, 0xf, false);  // quad_perm(S,S,S,S)
+    return r;
+}
+
+template <class T>
+__device__ __forceinline__ T sel4(uint32_t k, const T& a0, const T& a1, const T& a2, const T& a3) {
+    T r;
+    const uint32_t* w0 = reinterpret_cast<const uint32_t*>(&a0);
+    const uint32_t* w1 = reinterpret_cast<const uint32_t*>(&a1);
+    const uint32_t* w2 = reinterpret_cast<const uint32_t*>(&a2);
+    const uint32_t* w3 = reinterpret_cast<const uint32_t*>(&a3);
+    uint32_t* d = reinterpret_cast<uint32_t*>(&r);
+    // masks, not a select of pointers: every word is loaded from all four
+    // operands, which keeps them in registers (a pointer select forced them
+    // into scratch)
+    const uint32_t m0 = 0u - (k == 0), m1 = 0u - (k == 1), m2 = 0u - (k == 2), m3 = 0u - (k == 3);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); i++)
+        d[i] = (w0[i] & m0) | (w1[i] & m1) | (w2[i] & m2) | (w3[i] & m3);
+    return r;
+}
+
+// p += q on a quad; k = lane & 3.  p and q must be the same on the four lanes
+// (then every branch is uniform over the quad and the result is too).
 template <class F>
+__device__ __forceinline__ void xyzz_add_quad(Xyzz<F>& p, const Xyzz<F>& q, uint32_t k) {
+    if (q.is_inf()) return;
+    if (p.is_inf()) {
+        p = q;
+        return;
+    }
+    F m = sel4(k, p.x, p.y, q.x, q.y) * sel4(k, q.zz, q.zzz, p.zz, p.zzz);
+    const F U1 = quad_bcast<0>(m), S1 = quad_bcast<1>(m);
+    const F P = quad_bcast<2>(m) - U1, R = quad_bcast<3>(m) - S1;
+    if (P.is_zero()) {
+        p = R.is_zero() ? xyzz_dbl(p) : Xyzz<F>::inf();
+        return;
+    }
+    m = sel4(k, P, R, p.zz, p.zzz) * sel4(k, P, R, q.zz, q.zzz);
+    const F PP = quad_bcast<0>(m), RR = quad_bcast<1>(m), Z2 = quad_bcast<2>(m), Z3 = quad_bcast<3>(m);
+    m = sel4(k, P, U1, Z2, P) * PP;
+    const F PPP = quad_bcast<0>(m), Q = quad_bcast<1>(m), ZZ3 = quad_bcast<2>(m);
+    const F X3 = RR - PPP - dbl(Q);
+    const F D = Q - X3;
+    m = sel4(k, R, S1, Z3, R) * sel4(k, D, PPP, PPP, D);
+    p.y = quad_bcast<0>(m) - quad_bcast<1>(m);
+    p.zzz = quad_bcast<2>(m);
+    p.x = X3;
+    p.zz = ZZ3;
+}
+
+template <class T>
+__device__ __forceinline__ T shfl_xor_words(const T& v, int mask) {
+    static_assert(sizeof(T) % 4 == 0, "word-sized struct");
+    T r;
+    const int* s = reinterpret_cast<const int*>(&v);
+    int* d = reinterpret_cast<int*>(&r);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 4); i++) d[i] = __shfl_xor(s[i], mask, 64);
+    return r;
+}
+
+// Level 2 for light buckets (2..LIGHT partials): QB quads per bucket.  Quad j
+// adds partials j, j + QB, ... of its bucket with quad adds, then log2(QB)
+// xor-shuffle rounds (lane masks 4, 8, ...) combine the quads.  Every lane
+// takes part in the shuffles; only the adds are predicated.
+template <class F, uint32_t QB>
 __global__ void __launch_bounds__(256) k_bucket_sum(Xyzz<F>* part, const uint32_t* item_off, size_t nb) {
-    size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
-    uint32_t o = item_off[b], cnt = item_off[b + 1] - o;
-    if (cnt < 2 || cnt > LIGHT) return;
-    Xyzz<F> acc = ld(part + o);
-    for (uint32_t k = 1; k < cnt; k++) xyzz_add_inplace(acc, ld(part + o + k));
-    st(part + o, acc);
+    static_assert(QB == 1 || QB == 2 || QB == 4, "quads per bucket");
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t b = t / (4 * QB);
+    const uint32_t k = (uint32_t)t & 3, j = (uint32_t)(t >> 2) & (QB - 1);
+    uint32_t o = 0, cnt = 0;
+    if (b < nb) {
+        o = item_off[b];
+        cnt = item_off[b + 1] - o;
+    }
+    const bool act = cnt >= 2 && cnt <= LIGHT;
+    Xyzz<F> acc = Xyzz<F>::inf();
+    if (act)
+        for (uint32_t i = j; i < cnt; i += QB) xyzz_add_quad(acc, ld(part + o + i), k);
+    for (int s = 4; s < (int)(4 * QB); s <<= 1) {
+        const Xyzz<F> other = shfl_xor_words(acc, s);
+        if (act) xyzz_add_quad(acc, other, k);
+    }
+    if (act && j == 0 && k == 0) st(part + o, acc);
 }
 
 // ------------------------------------------------------------ reduction v2
@@ -267,19 +360,49 @@ struct RedJobs {
     int n;
 };
 
+// One output per quad (xyzz_add_quad): launch 4 lanes per output.
 template <class F>
 __global__ void __launch_bounds__(256) k_reduce_jobs(RedJobs<F> J) {
-    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = g & 3;
+    uint32_t t = g >> 2;
     int q = 0;
     while (q < J.n && t >= J.j[q].nthreads) { t -= J.j[q].nthreads; q++; }
-    if (q >= J.n) return;
+    if (q >= J.n) return;  // uniform over the quad
     const RedJob<F>& jb = J.j[q];
     uint32_t a2 = t / jb.Bc, c = t % jb.Bc;
     uint32_t a0 = a2 * jb.G;
     uint32_t a1 = min(jb.A, a0 + jb.G);
     Xyzz<F> acc = ld(jb.in + (size_t)a0 * jb.sa + (size_t)c * jb.sb);
-    for (uint32_t a = a0 + 1; a < a1; a++) xyzz_add_inplace(acc, ld(jb.in + (size_t)a * jb.sa + (size_t)c * jb.sb));
-    st(jb.out + (size_t)a2 * jb.Bc + c, acc);
+    for (uint32_t a = a0 + 1; a < a1; a++)
+        xyzz_add_quad(acc, ld(jb.in + (size_t)a * jb.sa + (size_t)c * jb.sb), lane);
+    if (lane == 0) st(jb.out + (size_t)a2 * jb.Bc + c, acc);
+}
+
+// Whole tree sums in one launch: block t of job q writes
+// out[t] = sum_{a < A} in[a*sa + t*sb].  The block's NQ = blockDim/4 quads take
+// a = quad, quad + NQ, ... with quad adds, then a log2(NQ)-level tree through LDS
+// finishes it.  Replaces log2(A) lockstep launches of k_reduce_jobs (each level
+// cost a launch plus one add's latency).
+template <class F>
+__global__ void __launch_bounds__(256) k_reduce_block(RedJobs<F> J) {
+    __shared__ Xyzz<F> sh[32];
+    uint32_t t = blockIdx.x;
+    int q = 0;
+    while (q < J.n && t >= J.j[q].nthreads) { t -= J.j[q].nthreads; q++; }
+    if (q >= J.n) return;  // uniform over the block
+    const RedJob<F>& jb = J.j[q];
+    const uint32_t lane = threadIdx.x & 3, quad = threadIdx.x >> 2, NQ = blockDim.x >> 2;
+    Xyzz<F> acc = Xyzz<F>::inf();
+    for (uint32_t a = quad; a < jb.A; a += NQ)
+        xyzz_add_quad(acc, ld(jb.in + (size_t)a * jb.sa + (size_t)t * jb.sb), lane);
+    for (uint32_t h = NQ >> 1; h >= 1; h >>= 1) {
+        if (quad >= h && quad < 2 * h && lane == 0) sh[quad - h] = acc;
+        __syncthreads();
+        if (quad < h) xyzz_add_quad(acc, sh[quad], lane);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) st(jb.out + t, acc);
 }
 
 // ------------------------------------------------------------ precompute
@@ -436,7 +559,8 @@ inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* partials, const u
     struct Job { const Xyzz<F>* in; uint32_t A, Bc, sa, sb; Item dest; };
     std::vector<Item> items{{S, (uint32_t)nb, 1u, 0}};
     std::vector<Item> host_items;
-    const uint32_t HOST_N = 16;
+    uint32_t HOST_N = 8;  // weighted sums of <= HOST_N elements finish on the host (MI355X sweep: 8)
+    if (const char* e = getenv("GG_RED_HOST_N")) HOST_N = (uint32_t)std::max(2, atoi(e));  // tuning
     while (!items.empty()) {
         std::vector<Job> jobs;
         for (const Item& it : items) {
@@ -447,7 +571,38 @@ inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* partials, const u
             jobs.push_back({it.X, M, rows, 1u, M, Item{nullptr, rows, 0u, it.mlog + mlg}});
             jobs.push_back({it.X, rows, M, M, 1u, Item{nullptr, M, it.off, it.mlog}});
         }
-        bool active = !jobs.empty();
+        // one launch per round: every output of every job is a block-wide sum
+        static const bool block_mode = !(getenv("GG_RED_BLOCK") && atoi(getenv("GG_RED_BLOCK")) == 0);
+        if (block_mode && !jobs.empty()) {
+            RedJobs<F> J;
+            J.n = 0;
+            size_t blocks = 0;
+            uint32_t maxA = 1;
+            auto flush = [&]() {
+                if (!J.n) return;
+                uint32_t nq = 1;
+                while (nq < maxA && nq < 64) nq <<= 1;
+                hipLaunchKernelGGL(k_reduce_block<F>, dim3((unsigned)blocks), dim3(4 * nq), 0, st, J);
+                GG_HIP(hipGetLastError());
+                J.n = 0;
+                blocks = 0;
+                maxA = 1;
+            };
+            for (auto& j : jobs) {
+                Xyzz<F>* out = alloc(j.Bc);
+                J.j[J.n++] = RedJob<F>{j.in, out, j.A, j.Bc, j.sa, j.sb, j.A, j.Bc};
+                blocks += j.Bc;
+                maxA = std::max(maxA, j.A);
+                j.in = out;
+                j.A = 1;
+                j.sa = j.Bc;
+                j.sb = 1;
+                if (J.n == MAX_RED_JOBS) flush();
+            }
+            flush();
+        }
+        bool active = false;
+        for (auto& j : jobs) if (j.A > 1) active = true;
         while (active) {
             size_t t2 = 0;
             for (auto& j : jobs) if (j.A > 1) t2 += (size_t)((j.A + 1) / 2) * j.Bc;
@@ -457,7 +612,7 @@ inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* partials, const u
             size_t threads = 0;
             auto flush = [&]() {
                 if (!J.n) return;
-                hipLaunchKernelGGL(k_reduce_jobs<F>, dim3(grid_for(threads, 256)), dim3(256), 0, st, J);
+                hipLaunchKernelGGL(k_reduce_jobs<F>, dim3(grid_for(4 * threads, 256)), dim3(256), 0, st, J);
                 GG_HIP(hipGetLastError());
                 J.n = 0;
                 threads = 0;
@@ -555,13 +710,18 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, hipStream_t st) {
     // items) by a per-bucket tree (skew-robust: log2(items) launches)
     ProfScope ps_acc2("msm_accum2", st, (double)n);
     if (!kMergeInBlock<F> && max_items > 1) {
-        hipLaunchKernelGGL(k_bucket_sum<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st,
-                           b->partA.as<Xyzz<F>>(), ioff, nb);
+        // quads per bucket (MI355X sweep: one quad per bucket at 2^20; more
+        // lanes make the level throughput-bound)
+        static const int l2qb = getenv("GG_L2_QB") ? atoi(getenv("GG_L2_QB")) : 1;
+        Xyzz<F>* pa = b->partA.as<Xyzz<F>>();
+        if (l2qb >= 4) hipLaunchKernelGGL((k_bucket_sum<F, 4>), dim3(grid_for(16 * nb, 256)), dim3(256), 0, st, pa, ioff, nb);
+        else if (l2qb == 2) hipLaunchKernelGGL((k_bucket_sum<F, 2>), dim3(grid_for(8 * nb, 256)), dim3(256), 0, st, pa, ioff, nb);
+        else hipLaunchKernelGGL((k_bucket_sum<F, 1>), dim3(grid_for(4 * nb, 256)), dim3(256), 0, st, pa, ioff, nb);
         GG_HIP(hipGetLastError());
     }
     for (uint32_t stride = 1; max_items > LIGHT && stride < max_items;) {
         uint32_t fan = (stride == 1) ? 4u : 2u;
-        hipLaunchKernelGGL(k_seg_tree<F>, dim3(grid_for(n_items, 256)), dim3(256), 0, st,
+        hipLaunchKernelGGL(k_seg_tree<F>, dim3(grid_for(4 * n_items, 256)), dim3(256), 0, st,
                            b->partA.as<Xyzz<F>>(), ioff, s->item_bucket.as<uint32_t>(), n_items, stride,
                            fan);
         GG_HIP(hipGetLastError());
