@@ -1,16 +1,25 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X Groth16/BN254 hot path.
 
-Headline (BASELINE.json metric "... MSM G1 throughput (Mscalar-mul/s) ...",
-workload = configs[1]): BN254 G1 MSM over 2^20 resident points per GPU, scalars
-resident in HBM, one process per GPU.  A "step" is one full MSM (digits, sort,
-bucket accumulation, bucket reduction, result to host); for N > 1 each rank owns
-its own 2^20-point shard (weak scaling) and the per-rank Jacobian partials are
-all-gathered over RCCL and added on rank 0 (RCCL has no EC-add reduction).
+Headline (BASELINE.json metric "Groth16 prove time + MSM G1 throughput ...
+BN254 2^24 R1CS", workload = configs[3]): one full Groth16 prove of a
+2^24-constraint R1CS shaped like independent MiMC x^5 chains, the solution
+(W, A, B, C) handed over in HOST memory as gnark's Prove does
+(prove.go:127-320; icicle.go:231-278, 478-480 copy it to the GPU per proof), so
+the H2D of the 2 GB solution is inside the timed span.  A "step" is one proof:
+solution upload (pinned, chunked, overlapped with the MSMs), computeH (7 fused
+NTTs), the A/B1/K/Z G1 MSMs and the B G2 MSM, and the host combination.  The
+key is resident in HBM (uploaded once, as setupDevicePointers does).
+value = constraints / s.  For N > 1 one proof is spread over the N GPUs (strong
+scaling): every rank holds a key shard (wires and Z positions), uploads only its
+wire slice and its cyclic slices of A/B/C, computeH runs as a four-step
+distributed NTT with three RCCL all-to-alls, and the 576-B partials are
+all-gathered and combined.
 
-Also reported (not the headline): a Groth16 prove at --groth16-log-n with a
-synthetic key generated on the GPU, and the C restatement (oracle/) of the same
-MSM timed on the host cores as cpu_baseline.
+Also reported: the G1 MSM throughput inside the prove and a standalone 2^20 G1
+MSM (configs[1]), the 2^24 Fr NTT round trip (configs[2]), the BLS12-381 PlonK
+hot ops and prove (configs[4]), and the C restatement (oracle/) of the same
+prove timed on the host cores as cpu_baseline.
 """
 import argparse
 import datetime
@@ -25,6 +34,7 @@ sys.path.insert(0, os.path.join(ROOT, "gnark-fork_amd"))
 METRIC = ("Groth16 prove time + MSM G1 throughput (Mscalar-mul/s) BN254 2^24 R1CS, 1/2/4/8 GPU")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FPMUL_PEAK_G = 135.7  # measured BN254 Fp Montgomery multiplies/s (G), profiles/r01_v2_mbench_field.txt
+MIMC_ROUNDS = 85      # 3 constraints per round; 2^(log_n-8) chains -> 255 * 2^(log_n-8) constraints
 
 
 def log(*a):
@@ -55,20 +65,47 @@ def g2_generator_mont():
     return b"".join(fr.fp_mont(v) for v in (x0, x1, y0, y1))
 
 
+def mimc_shape(log_n):
+    """Wire layout of the MiMC-chain R1CS (oracle/c/oracle_r1cs.c shape): wire 0 =
+    ONE, 1..K chain inputs (input 1 public), then t, u, x' per round.  Which
+    setup.go:212-237 infinity flags that gives: A (L terms x, t, u) is infinity
+    for ONE and each chain's last x'; B (R terms x, t) also for every u."""
+    import numpy as np
+    chains = 1 << (log_n - 8)
+    ncons = 3 * chains * MIMC_ROUNDS
+    nw = 1 + chains + ncons
+    infA = np.zeros(nw, dtype=np.uint8)
+    infB = np.zeros(nw, dtype=np.uint8)
+    infA[0] = infB[0] = 1
+    body = np.arange(ncons, dtype=np.int64)
+    kind = body % 3                      # 0 = t, 1 = u, 2 = x'
+    rd = (body // 3) % MIMC_ROUNDS
+    w = 1 + chains + body
+    infB[w[kind == 1]] = 1
+    last = w[(kind == 2) & (rd == MIMC_ROUNDS - 1)]
+    infA[last] = 1
+    infB[last] = 1
+    return dict(chains=chains, ncons=ncons, nw=nw, nb_public=2, infA=infA, infB=infB)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--log-n", type=int, default=20, help="MSM points per GPU = 2^log_n")
-    ap.add_argument("--groth16-log-n", type=int, default=24,
-                    help="domain size of the extra Groth16 prove measurement (0 = skip)")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--log-n", type=int, default=24, help="Groth16 domain 2^log_n (headline)")
+    ap.add_argument("--msm-log-n", type=int, default=20,
+                    help="size of the extra standalone G1 MSM, BASELINE configs[1] (0 = skip)")
     ap.add_argument("--ntt-log-n", type=int, default=24,
                     help="size of the extra Fr NTT measurement, BASELINE configs[2] (0 = skip)")
     ap.add_argument("--plonk-log-n", type=int, default=22,
-                    help="BLS12-381 PlonK hot-op measurement size, BASELINE configs[4] (0 = skip)")
+                    help="BLS12-381 PlonK measurement size, BASELINE configs[4] (0 = skip)")
+    ap.add_argument("--device-inputs", action="store_true",
+                    help="solution resident in HBM instead of host memory (not the headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--extras-timeout", type=float, default=480.0,
+    ap.add_argument("--no-variants", action="store_true",
+                    help="skip the serial / device-input prove variants (profiling runs)")
+    ap.add_argument("--extras-timeout", type=float, default=420.0,
                     help="seconds allowed for the extra measurements after the headline; past it "
                          "the headline line is printed with the extras marked timed out and the "
                          "process exits (a stuck collective never swallows the headline)")
@@ -78,10 +115,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import numpy as np
     import torch
-    import gnark_amd
-    from gnark_amd import _lib, msm, DeviceBuffer
+    from gnark_amd import _lib
 
     # one process per GPU over RCCL ("nccl").  GG_DIST_BACKEND=gloo is a rehearsal
     # mode only (ranks may share a GPU; partials travel through host memory).
@@ -105,88 +140,92 @@ def main():
         torch.cuda.synchronize()
         _lib.check(_lib.lib.gg_synchronize())
 
-    n = 1 << args.log_n
-    # ---- synthetic resident key shard (GPU fixed-base batch mul, distinct per rank)
-    t0 = time.time()
-    ks = rand_scalars(n, 1000 + rank)
-    pts = DeviceBuffer(64 * n)
-    msm.batch_scalar_mul(msm.G1, g1_generator_mont(), ks, n, out=pts)
-    base = msm.MsmBase(msm.G1, pts.ptr, n, on_device=True)
-    del pts
-    npts, c, W = base.info()
-    sc = rand_scalars(n, 2000 + rank)
-    dsc = DeviceBuffer.from_host(sc.tobytes())
-    log(f"[rank {rank}] key shard ready: n={npts} c={c} windows={W} ({time.time() - t0:.1f}s)")
-
-    from gnark_amd import dist as gdist
-
-    def step():
-        j = base.msm_jac(dsc, n, on_device=True)
+    def max_over_ranks(x):
         if dist is None:
-            return j
-        # RCCL all-gather of the 96-B Jacobian partials + exact EC add (gnark_amd.dist)
-        return gdist.allgather_partial(msm.G1, j, device=xdev)
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=xdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
 
+    # ---- headline: Groth16 prove of a 2^log_n MiMC-shaped R1CS
+    t0 = time.time()
+    g = Groth16Bench(args.log_n, rank, world, dist, xdev, host_inputs=not args.device_inputs)
+    log(f"[rank {rank}] key ready: 2^{args.log_n}, {g.shape['ncons']} constraints, "
+        f"{g.shape['nw']} wires ({time.time() - t0:.1f}s)")
     for _ in range(args.warmup):
-        step()
+        g.prove()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res = step()
+        g.prove()
     barrier()
-    el = time.perf_counter() - t0
-    if dist is not None:
-        tt = torch.tensor([el], dtype=torch.float64, device=xdev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
+    el = max_over_ranks(time.perf_counter() - t0)
     ms_per_step = 1e3 * el / args.steps
-    value = world * n * args.steps / el / 1e6  # Mscalar-mul/s, whole job
+    ncons = g.shape["ncons"]
+    value = ncons * args.steps / el  # constraints/s of the whole job (one proof per step)
+    stage = g.timings()
+    same = g.proof_identical_on_all_ranks()
 
-    # ---- roofline of the dominant kernel (bucket accumulation), HIP events on its stream
-    gnark_amd._lib.profile_enable(True)
-    prof_steps = max(3, min(10, args.steps))
+    # ---- roofline of the dominant kernel, HIP events on its launch stream,
+    # over proves exactly like the timed ones (concurrent streams)
+    _lib.profile_enable(True)
+    prof_steps = 3
     for _ in range(prof_steps):
-        base.msm_jac(dsc, n, on_device=True)
+        g.prove()
     kernels = {}
-    for name in ("msm_sort", "msm_accum", "msm_accum2", "msm_reduce"):
-        ms, cnt, units = gnark_amd._lib.profile_get(name)
-        kernels[name] = {"avg_ms": ms / cnt if cnt else None, "launches": cnt}
-    gnark_amd._lib.profile_enable(False)
-    acc_ms = kernels["msm_accum"]["avg_ms"]
-    alg_bytes = n * (64 + 32)  # N x (G1 affine 64 B + fr 32 B)
-    achieved = alg_bytes / (acc_ms * 1e-3) / 1e9 if acc_ms else None
-    traffic, traffic_note = pmc_traffic("k_accum_affine<gg::Fe<gg::FpCfg> >", args.log_n, c, W)
+    for name in ("msm_sort", "msm_accum", "msm_accum_g2", "msm_accum2", "msm_reduce", "ntt_pass"):
+        tot, cnt, units = _lib.profile_get(name)
+        kernels[name] = {"avg_ms": tot / cnt if cnt else None, "launches_per_proof": cnt / prof_steps,
+                         "total_ms_per_proof": tot / prof_steps}
+    _lib.profile_enable(False)
+    nB2 = g.nB2
+    g2_ms = kernels["msm_accum_g2"]["avg_ms"]
+    alg_bytes = nB2 * (128 + 32)  # |B2| x (G2 affine 128 B + fr 32 B)
+    achieved = alg_bytes / (g2_ms * 1e-3) / 1e9 if g2_ms else None
+    traffic, traffic_note = pmc_traffic("k_accum_affine<gg::Fp2>", {"workload": "groth16", "log_n": args.log_n,
+                                                                    "n_gpus": world})
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                 "traffic_note": traffic_note,
-                "kernel": "k_accum_affine<Fp> (bucket accumulation)",
-                "algorithmic_bytes_per_launch": alg_bytes, "kernel_avg_ms": acc_ms,
+                "kernel": "k_accum_affine<Fp2> (G2 bucket accumulation of the B MSM: the longest "
+                          "single launch of the prove)",
+                "algorithmic_bytes_per_launch": alg_bytes, "kernel_avg_ms": g2_ms,
+                "timing": "HIP events on the kernel's launch stream, during proves with all five "
+                          "streams busy (same launches the rocprof summary averages)",
                 "note": "EC MSM is VALU-integer bound (SURVEY 8d); HBM fraction reported as required"}
-
-    # VALU view of the same kernel: 8M+2S Fp multiplies per mixed add, one add per
-    # non-zero (window, scalar) entry, against the measured Fp-mul peak
-    # (profiles/r01_v2_mbench_field.txt, product-scanning Montgomery on MI355X)
-    if acc_ms:
-        mul_rate = n * W * 10 / (acc_ms * 1e-3) / 1e9
+    if g2_ms:
+        W2 = g.g2_windows
+        mul_rate = nB2 * W2 * 10 * 3 / (g2_ms * 1e-3) / 1e9  # Fp2 mul ~ 3 Fp mul (Karatsuba)
         roofline["valu"] = {"achieved_Gfpmul_s": mul_rate, "peak_Gfpmul_s": FPMUL_PEAK_G,
                             "frac": mul_rate / FPMUL_PEAK_G,
-                            "basis": "n*W mixed XYZZ adds x 10 Fp-mul (madd-2008-s)"}
+                            "basis": "|B2| x W mixed XYZZ adds x 10 Fp2-mul x 3 Fp-mul (Karatsuba); "
+                                     "the kernel shares the GPU with four other MSM streams"}
+
     out = {
-        "metric": METRIC, "value": value, "unit": "Mscalar-mul/s", "n_gpus": world,
+        "metric": METRIC, "value": value, "unit": "constraints/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "u32 limbs (BN254 Fp/Fr Montgomery, integer)", "data": "synthetic",
-        "config": {"workload": "BN254 G1 MSM, 2^%d resident points + scalars per GPU "
-                               "(BASELINE configs[1])" % args.log_n,
-                   "points_per_gpu": n, "window_bits": c, "windows": W,
-                   "parallelism": "msm point-shard x%d, RCCL all_gather of partials" % world},
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "u32 limbs (BN254 Fp/Fr Montgomery, integer)",
+        "data": "synthetic: random solution vectors W, A, B, C of the 2^%d MiMC-chain R1CS shape; key "
+                "points = random multiples of the generators (GPU batch scalar mul); bit-exact parity of "
+                "satisfied instances of the same shape: tests/test_gpu_groth16_size.py" % args.log_n,
+        "config": {"workload": "BN254 Groth16 full prove, 2^%d-constraint MiMC-chain R1CS (%d constraints, "
+                               "%d wires), solution in %s (BASELINE configs[3])"
+                               % (args.log_n, ncons, g.shape["nw"],
+                                  "device memory" if args.device_inputs else "host memory, H2D inside the step"),
+                   "log_n": args.log_n, "n_constraints": ncons, "n_wires": g.shape["nw"],
+                   "inputs": "device" if args.device_inputs else "host",
+                   "parallelism": ("key shard x%d (wires + Z positions), distributed computeH "
+                                   "(3 RCCL all-to-alls), RCCL all-gather of 576-B partials" % world)
+                   if world > 1 else "one GPU, 5 concurrent HIP streams"},
+        "prove_ms": ms_per_step, "stage_ms": stage, "proof_identical_on_all_ranks": same,
         "roofline": roofline, "kernels": kernels,
     }
 
     # watchdog over the extras: the headline is already measured
     import threading
     printed = threading.Lock()
-    stage = {"now": "ntt"}
+    stage_now = {"now": "serial"}
 
     def emit():
         if printed.acquire(blocking=False):
@@ -196,7 +235,7 @@ def main():
         return False
 
     def bail():
-        out.setdefault("extras_timeout", {"stage": stage["now"], "seconds": args.extras_timeout})
+        out.setdefault("extras_timeout", {"stage": stage_now["now"], "seconds": args.extras_timeout})
         emit()
         os._exit(0)
 
@@ -204,25 +243,44 @@ def main():
     wd.daemon = True
     wd.start()
 
-    # ---- Fr NTT 2^24 (BASELINE configs[2]; extra, rank 0 / N = 1 only)
+    # ---- the same prove with the five tasks one after another (isolated stage
+    # times), and with the solution already in HBM (upload cost), N = 1 only
+    if world == 1 and not args.no_variants:
+        try:
+            out["groth16_variants"] = g.variants()
+        except Exception as e:  # report, never hide
+            out["groth16_variants"] = {"error": repr(e)}
+    g.close()
+    del g
+
+    # ---- standalone 2^20 G1 MSM (BASELINE configs[1]); weak scaling at N > 1
+    stage_now["now"] = "msm"
+    if args.msm_log_n:
+        try:
+            m = msm_bench(args.msm_log_n, rank, world, dist, xdev, barrier, max_over_ranks)
+        except Exception as e:
+            m = {"error": repr(e)}
+        if rank == 0:
+            out["msm_g1"] = m
+
+    # ---- Fr NTT 2^24 (BASELINE configs[2]; rank 0 / N = 1 only)
+    stage_now["now"] = "ntt"
     if rank == 0 and world == 1 and args.ntt_log_n:
         try:
             out["ntt"] = ntt_bench(args.ntt_log_n)
         except Exception as e:  # report, never hide
             out["ntt"] = {"error": repr(e)}
 
-    # ---- PlonK BLS12-381 hot ops (BASELINE configs[4] sizes; extra, rank 0 / N = 1 only)
-    stage["now"] = "plonk"
+    # ---- PlonK BLS12-381 hot ops (BASELINE configs[4] sizes; rank 0 / N = 1 only)
+    stage_now["now"] = "plonk"
     if rank == 0 and world == 1 and args.plonk_log_n:
         try:
             out["plonk_bls12_381"] = plonk_bench(args.plonk_log_n)
         except Exception as e:  # report, never hide
             out["plonk_bls12_381"] = {"error": repr(e)}
 
-    # ---- PlonK BLS12-381 prove, end to end (BASELINE configs[4]; rank 0 / N = 1 only)
-    # (at N > 1 every rank keeps a 1/N slice of the KZG bases; commitments are
-    # partial MSMs all-gathered over RCCL, the rest of the prover is replicated)
-    stage["now"] = "plonk_prove"
+    # ---- PlonK BLS12-381 prove, end to end (BASELINE configs[4])
+    stage_now["now"] = "plonk_prove"
     if args.plonk_log_n:
         try:
             pr = plonk_prove_bench(args.plonk_log_n, rank=rank, world=world, dist=dist, xdev=xdev,
@@ -232,26 +290,11 @@ def main():
         if rank == 0:
             out.setdefault("plonk_bls12_381", {})["prove"] = pr
 
-    # ---- Groth16 prove (extra): whole key at N = 1; at N > 1 one key shard per
-    # GPU (wires and Z positions partitioned, h computed on every GPU, 576-B
-    # partials all-gathered) -- strong scaling of one 2^log_n proof
-    stage["now"] = "groth16"
-    if args.groth16_log_n:
-        try:
-            if world == 1:
-                g16 = groth16_bench(args.groth16_log_n)
-            else:
-                g16 = groth16_bench_sharded(args.groth16_log_n, rank, world, dist, xdev, barrier)
-        except Exception as e:  # report, never hide
-            g16 = {"error": repr(e)}
-        if rank == 0:
-            out["groth16"] = g16
-
     # ---- CPU baseline (oracle restatement on the host cores), rank 0 at N = 1
-    stage["now"] = "cpu_baseline"
+    stage_now["now"] = "cpu_baseline"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(base, dsc, sc, n, args.cpu_threads)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_threads, ms_per_step, ncons)
         except Exception as e:
             out["cpu_baseline"] = {"error": repr(e)}
 
@@ -262,8 +305,181 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(kernel, log_n, c, W):
-    """HBM bytes per launch of `kernel` from the committed PMC profile of the same
+class Groth16Bench:
+    """A resident 2^log_n Groth16 key (whole key at N = 1, this rank's shard at
+    N > 1) of the MiMC-chain shape, and the host (or device) solution vectors."""
+
+    def __init__(self, log_n, rank, world, dist, xdev, host_inputs=True):
+        import numpy as np
+        import torch
+        from gnark_amd import backend, groth16, msm, DeviceBuffer
+        self.log_n, self.rank, self.world, self.dist, self.xdev = log_n, rank, world, dist, xdev
+        self.shape = sh = mimc_shape(log_n)
+        n, nw, nbp = 1 << log_n, sh["nw"], sh["nb_public"]
+        infA, infB = sh["infA"], sh["infB"]
+        g1, g2 = g1_generator_mont(), g2_generator_mont()
+        sd = 100 * (rank + 1)
+
+        def g1pts(k, seed):
+            return msm.batch_scalar_mul(msm.G1, g1, rand_scalars(k, seed), k) if k else b""
+
+        def g2pts(k, seed):
+            return msm.batch_scalar_mul(msm.G2, g2, rand_scalars(k, seed), k) if k else b""
+        common = dict(alpha1=g1pts(1, 5), beta1=g1pts(1, 6), delta1=g1pts(1, 7),
+                      beta2=g2pts(1, 9), delta2=g2pts(1, 10), infinity_A=infA.tobytes(),
+                      infinity_B=infB.tobytes(), nb_public=nbp)
+        if world == 1:
+            nA, nB = int((infA == 0).sum()), int((infB == 0).sum())
+            self.data = groth16.ProvingKeyData(
+                log_n=log_n, g1_A=g1pts(nA, sd + 1), g1_B=g1pts(nB, sd + 2), g1_Z=g1pts(n - 1, sd + 3),
+                g1_K=g1pts(nw - nbp, sd + 4), g2_B=g2pts(nB, sd + 8), **common)
+            self.pk = groth16.ProvingKey(self.data)
+            self.nB2 = nB
+        else:
+            lo, hi, zl, zh = groth16.shard_ranges(nw, n, rank, world)
+            nA = int((infA[lo:hi] == 0).sum())
+            nB = int((infB[lo:hi] == 0).sum())
+            nK = max(hi, nbp) - max(lo, nbp)
+            shard = groth16.KeyShard(lo, hi, zl, g1_A=g1pts(nA, sd + 1), g1_B=g1pts(nB, sd + 2),
+                                     g2_B=g2pts(nB, sd + 8), g1_K=g1pts(nK, sd + 4),
+                                     g1_Z=g1pts(zh - zl, sd + 3), k_wire_index=None)
+            self.data = groth16.ProvingKeyData(log_n=log_n, g1_A=b"", g1_B=b"", g1_Z=b"", g1_K=b"",
+                                               g2_B=b"", **common)
+            self.pk = groth16.ProvingKeyShard(self.data, rank, world, shard=shard)
+            self.nB2 = nB
+            del shard
+            assert groth16.dist_h_supported(n, world)
+            self.hs = groth16.HShard(log_n, rank, world)
+            self.xchg = groth16.TorchExchange(self.hs.exchange_bytes,
+                                              torch.device("cuda", torch.cuda.current_device()))
+        # the solution (same on every rank: seeds independent of the rank)
+        ncons = sh["ncons"]
+        self.host = [rand_scalars(nw, 11)] + [rand_scalars(ncons, 12 + i) for i in range(3)]
+        if host_inputs:
+            self.sol = groth16.Solution(*self.host, nw, ncons)
+        else:
+            self.dev = [DeviceBuffer.from_host(x.tobytes()) for x in self.host]
+            self.sol = groth16.Solution(*self.dev, nw, ncons, on_device=True)
+        self.opt = backend.with_amd_acceleration()
+        self.r, self.s = fr_const(12345), fr_const(67890)
+        self.last = None
+        self.g2_windows = self.pk.base_info(groth16.BASE_B2)[2]
+
+    def prove(self):
+        from gnark_amd import groth16
+        if self.world == 1:
+            self.last = groth16.prove(self.pk, self.sol, self.opt, r=self.r, s=self.s)
+        else:
+            self.last = groth16.prove_distributed_h(self.pk, self.hs, self.xchg, self.sol, self.opt,
+                                                    r=self.r, s=self.s, device=self.xdev)
+        return self.last
+
+    def timings(self):
+        from gnark_amd import groth16
+        return groth16.last_timings()
+
+    def proof_identical_on_all_ranks(self):
+        if self.world == 1:
+            return True
+        import torch
+        pr = self.last
+        pt = torch.frombuffer(bytearray(pr.Ar + pr.Bs + pr.Krs), dtype=torch.uint8).to(self.xdev)
+        p0 = pt.clone()
+        self.dist.broadcast(p0, 0)
+        return bool(torch.equal(pt, p0))
+
+    def variants(self, reps=2):
+        from gnark_amd import DeviceBuffer, groth16
+        res = {}
+        os.environ["GG_G16_SERIAL"] = "1"
+        try:
+            ts = []
+            for _ in range(reps):
+                t = time.perf_counter()
+                self.prove()
+                ts.append(1e3 * (time.perf_counter() - t))
+            res["serial_prove_ms"] = min(ts)
+            res["serial_stage_ms"] = self.timings()
+        finally:
+            del os.environ["GG_G16_SERIAL"]
+        st = res["serial_stage_ms"]
+        n = 1 << self.log_n
+        if st.get("msm_A"):
+            res["msm_g1_A_Mscalar_mul_per_s"] = self.shape["nw"] / (st["msm_A"] * 1e-3) / 1e6
+            res["msm_g1_Z_Mscalar_mul_per_s"] = (n - 1) / (st["msm_Z"] * 1e-3) / 1e6
+            res["msm_g2_Mscalar_mul_per_s"] = self.nB2 / (st["msm_G2"] * 1e-3) / 1e6
+        if self.sol.on_device is False:
+            dev = [DeviceBuffer.from_host(x.tobytes()) for x in self.host]
+            sol = groth16.Solution(*dev, self.shape["nw"], self.shape["ncons"], on_device=True)
+            groth16.prove(self.pk, sol, self.opt, r=self.r, s=self.s)
+            ts = []
+            for _ in range(reps + 1):
+                t = time.perf_counter()
+                groth16.prove(self.pk, sol, self.opt, r=self.r, s=self.s)
+                ts.append(1e3 * (time.perf_counter() - t))
+            res["device_inputs_prove_ms"] = min(ts)
+            res["device_inputs_stage_ms"] = self.timings()
+            del dev, sol
+        return res
+
+    def close(self):
+        self.pk.close()
+        if self.world > 1:
+            self.hs.close()
+
+
+def msm_bench(log_n, rank, world, dist, xdev, barrier, max_over_ranks, steps=20, warmup=3):
+    """Standalone G1 MSM over 2^log_n resident points + scalars per GPU (BASELINE
+    configs[1]); at N > 1 every rank owns its own 2^log_n shard (weak scaling) and
+    the 96-B Jacobian partials are all-gathered over RCCL and added exactly."""
+    from gnark_amd import _lib, msm, DeviceBuffer
+    from gnark_amd import dist as gdist
+    n = 1 << log_n
+    pts = DeviceBuffer(64 * n)
+    msm.batch_scalar_mul(msm.G1, g1_generator_mont(), rand_scalars(n, 1000 + rank), n, out=pts)
+    base = msm.MsmBase(msm.G1, pts.ptr, n, on_device=True)
+    del pts
+    npts, c, W = base.info()
+    dsc = DeviceBuffer.from_host(rand_scalars(n, 2000 + rank).tobytes())
+
+    def step():
+        j = base.msm_jac(dsc, n, on_device=True)
+        return gdist.allgather_partial(msm.G1, j, device=xdev) if world > 1 else j
+    for _ in range(warmup):
+        step()
+    barrier()
+    t = time.perf_counter()
+    for _ in range(steps):
+        step()
+    barrier()
+    el = max_over_ranks(time.perf_counter() - t)
+    _lib.profile_enable(True)
+    for _ in range(5):
+        base.msm_jac(dsc, n, on_device=True)
+    kern = {}
+    for name in ("msm_sort", "msm_accum", "msm_accum2", "msm_reduce"):
+        tot, cnt, _ = _lib.profile_get(name)
+        kern[name] = tot / cnt if cnt else None
+    _lib.profile_enable(False)
+    acc = kern["msm_accum"]
+    base.close()
+    res = {"log_n": log_n, "n_gpus": world, "ms_per_msm": 1e3 * el / steps,
+           "Mscalar_mul_per_s": world * n * steps / el / 1e6, "scaling": "weak",
+           "window_bits": c, "windows": W, "kernel_avg_ms": kern}
+    if acc:
+        alg = n * 96
+        traffic, note = pmc_traffic("k_accum_affine<gg::Fe<gg::FpCfg> >",
+                                    {"log_n": log_n, "window_bits": c, "windows": W})
+        res["accum_roofline"] = {"achieved_GBps": alg / (acc * 1e-3) / 1e9,
+                                 "frac_hbm": alg / (acc * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                 "traffic_bytes": traffic, "traffic_note": note,
+                                 "valu_Gfpmul_s": n * W * 10 / (acc * 1e-3) / 1e9,
+                                 "valu_frac": n * W * 10 / (acc * 1e-3) / 1e9 / FPMUL_PEAK_G}
+    return res
+
+
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from a committed PMC profile of the same
     workload (two separate rocprofv3 --pmc passes, FETCH_SIZE x2 per the gfx950
     correction + WRITE_SIZE; tools/pmc_traffic.py).  None if no matching profile."""
     import glob
@@ -273,39 +489,66 @@ def pmc_traffic(kernel, log_n, c, W):
         except (OSError, ValueError):
             continue
         wl = d.get("workload", {})
-        if (wl.get("log_n"), wl.get("window_bits"), wl.get("windows")) != (log_n, c, W):
+        if any(wl.get(k) != v for k, v in workload.items()):
             continue
         for k, v in d.get("kernels", {}).items():
             if kernel in k:
                 return v["traffic_bytes"], (
-                    f"{os.path.basename(f)}: FETCH_SIZE x2 + WRITE_SIZE per dispatch; the W={W} "
-                    f"precomputed window copies make the kernel read ~W x 64 B of points per scalar "
-                    f"(fixed-base trade: no doublings), so traffic >> the 96 B/scalar algorithmic bytes")
+                    f"{os.path.basename(f)}: FETCH_SIZE x2 + WRITE_SIZE per dispatch; the W "
+                    f"precomputed window copies of the fixed-base tables make the kernel read ~W x "
+                    f"the point bytes per scalar (no doublings at prove time), so traffic >> the "
+                    f"algorithmic bytes")
     return None, "no committed PMC profile for this workload"
 
 
-def cpu_baseline(base, dsc, sc, n, threads):
-    """C restatement of the same MSM (oracle/c, OpenMP Pippenger) on a bounded
-    sample: the first 2^18 points/scalars of the workload, repeated ~10 s."""
+def cpu_baseline(threads, gpu_prove_ms, gpu_ncons, log_n=20):
+    """The C restatement of the same prove (oracle/c oc_groth16_prove: OpenMP
+    signed-digit Pippenger MSMs with XYZZ buckets, radix-2 NTT computeH) on a
+    bounded sample: one 2^log_n MiMC-shaped proof (random solution, key from the
+    GPU batch scalar mul), repeated to ~10 s.  "port": our restatement, not gnark."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import coracle
     from gnark_amd import msm
-    nt = threads or min(16, os.cpu_count() or 1)
-    m = min(n, 1 << 18)
-    # the sample's points: regenerate the first m on the GPU and copy to host
-    ks = rand_scalars(n, 1000)[:m]
-    pts = msm.batch_scalar_mul(msm.G1, g1_generator_mont(), ks, m)
-    sb = sc[:m].tobytes()
+    nt = threads or (os.cpu_count() or 1)
+    sh = mimc_shape(log_n)
+    n, nw, ncons, nbp = 1 << log_n, sh["nw"], sh["ncons"], sh["nb_public"]
+    infA, infB = sh["infA"], sh["infB"]
+    nA, nB = int((infA == 0).sum()), int((infB == 0).sum())
+    g1, g2 = g1_generator_mont(), g2_generator_mont()
+
+    def p1(k, seed):
+        return msm.batch_scalar_mul(msm.G1, g1, rand_scalars(k, seed), k)
+
+    def p2(k, seed):
+        return msm.batch_scalar_mul(msm.G2, g2, rand_scalars(k, seed), k)
+    args = (log_n, p1(nA, 1), nA, p1(nB, 2), nB, p1(n - 1, 3), p1(nw - nbp, 4), nw - nbp,
+            p1(1, 5), p1(1, 6), p1(1, 7), p2(nB, 8), p2(1, 9), p2(1, 10), infA.tobytes(), infB.tobytes(),
+            rand_scalars(nw, 11).tobytes(), nw, nbp, rand_scalars(ncons, 12).tobytes(),
+            rand_scalars(ncons, 13).tobytes(), rand_scalars(ncons, 14).tobytes(), ncons,
+            fr_const(12345), fr_const(67890), nt)
     reps, t0 = 0, time.perf_counter()
     while True:
-        coracle.msm_g1(pts, sb, m, nt)
+        coracle.groth16_prove(*args)
         reps += 1
-        if time.perf_counter() - t0 > 10.0 or reps >= 50:
+        if time.perf_counter() - t0 > 10.0 or reps >= 20:
             break
     el = time.perf_counter() - t0
-    return {"value": m * reps / el / 1e6, "unit": "Mscalar-mul/s", "cores": nt, "kind": "port",
-            "sample": f"G1 MSM 2^{m.bit_length() - 1} points x {reps} reps (C restatement, "
-                      f"signed-digit Pippenger, {nt} OpenMP threads, not gnark)"}
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    v = ncons * reps / el
+    return {"value": v, "unit": "constraints/s", "cores": nt, "kind": "port",
+            "prove_ms": 1e3 * el / reps, "cpu_model": cpu_model, "host_cpus_visible": os.cpu_count(),
+            "sample": f"Groth16 prove of a 2^{log_n} MiMC-chain R1CS ({ncons} constraints) x {reps} "
+                      f"(C restatement of prove.go: OpenMP Pippenger + radix-2 NTT, {nt} threads, "
+                      f"not gnark); the GPU line is 2^{gpu_ncons.bit_length() - 1}-scale: compare "
+                      f"constraints/s",
+            "gpu_over_cpu_constraints_per_s": (gpu_ncons / (gpu_prove_ms * 1e-3)) / v}
 
 
 def ntt_bench(log_n, reps=10):
@@ -483,138 +726,6 @@ def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, 
             "key_setup_s": t_setup, "msms_per_proof": 10, "ntts_per_proof": "16 coset FFTs (L,R,O,Z x 4 cosets; key polynomials resident) + 4 iFFTs of n + 1 coset iFFT of 4n",
             "note": "synthetic key + random witness (timing only; proofs of valid witnesses verify in "
                     "tests/test_gpu_plonk_prove.py)"}
-
-
-def groth16_bench(log_n, reps=3):
-    """Synthetic 2^log_n Groth16 prove, key generated on the GPU; inputs resident."""
-    import numpy as np
-    from gnark_amd import backend, groth16, msm, DeviceBuffer
-    n = 1 << log_n
-    n_wires = n - 3
-    nb_public = 2
-    rng = np.random.default_rng(5)
-    infA = np.zeros(n_wires, dtype=np.uint8)
-    infB = (rng.random(n_wires) < 0.3).astype(np.uint8)
-    nA, nB, nK = n_wires, int((infB == 0).sum()), n_wires - nb_public
-    t0 = time.time()
-    g1 = g1_generator_mont()
-
-    def g1pts(k, seed):
-        return msm.batch_scalar_mul(msm.G1, g1, rand_scalars(k, seed), k)
-
-    d = groth16.ProvingKeyData(
-        log_n=log_n, g1_A=g1pts(nA, 1), g1_B=g1pts(nB, 2), g1_Z=g1pts(n - 1, 3), g1_K=g1pts(nK, 4),
-        alpha1=g1pts(1, 5), beta1=g1pts(1, 6), delta1=g1pts(1, 7),
-        g2_B=msm.batch_scalar_mul(msm.G2, g2_generator_mont(), rand_scalars(nB, 8), nB),
-        beta2=msm.batch_scalar_mul(msm.G2, g2_generator_mont(), rand_scalars(1, 9), 1),
-        delta2=msm.batch_scalar_mul(msm.G2, g2_generator_mont(), rand_scalars(1, 10), 1),
-        infinity_A=infA.tobytes(), infinity_B=infB.tobytes(), nb_public=nb_public)
-    pk = groth16.ProvingKey(d)
-    t_setup = time.time() - t0
-    wires = DeviceBuffer.from_host(rand_scalars(n_wires, 11).tobytes())
-    ncons = n - 5
-    sa, sb, sc = (DeviceBuffer.from_host(rand_scalars(ncons, 12 + i).tobytes()) for i in range(3))
-    sol = groth16.Solution(wires, sa, sb, sc, n_wires, ncons, on_device=True)
-    groth16.prove(pk, sol, backend.with_amd_acceleration())
-    ts = []
-    for _ in range(reps):
-        t = time.perf_counter()
-        groth16.prove(pk, sol, backend.with_amd_acceleration())
-        ts.append(1e3 * (time.perf_counter() - t))
-    tim = groth16.last_timings()
-    # the same prove with the five tasks run one after another: isolated stage times
-    os.environ["GG_G16_SERIAL"] = "1"
-    try:
-        t = time.perf_counter()
-        groth16.prove(pk, sol, backend.with_amd_acceleration())
-        t_serial = 1e3 * (time.perf_counter() - t)
-        tim_serial = groth16.last_timings()
-    finally:
-        del os.environ["GG_G16_SERIAL"]
-    return {"serial_prove_ms": t_serial, "serial_stage_ms": tim_serial,
-            "log_n": log_n, "n_constraints": ncons, "n_wires": n_wires,
-            "prove_ms": min(ts), "prove_ms_all": ts, "constraints_per_s": ncons / (min(ts) * 1e-3),
-            "stage_ms": tim, "key_setup_s": t_setup, "inputs": "resident in HBM"}
-
-
-def groth16_bench_sharded(log_n, rank, world, dist, xdev, barrier, reps=3):
-    """Synthetic 2^log_n Groth16 prove over `world` GPUs: this rank generates only
-    its own key shard on its GPU (groth16.KeyShard), inputs resident; the prove
-    time is the max over ranks between barriers."""
-    import numpy as np
-    import torch
-    from gnark_amd import backend, groth16, msm, DeviceBuffer
-    n = 1 << log_n
-    n_wires = n - 3
-    nb_public = 2
-    rng = np.random.default_rng(5)
-    infA = np.zeros(n_wires, dtype=np.uint8)
-    infB = (rng.random(n_wires) < 0.3).astype(np.uint8)
-    lo, hi, zl, zh = groth16.shard_ranges(n_wires, n, rank, world)
-    t0 = time.time()
-    g1 = g1_generator_mont()
-    sd = 100 * (rank + 1)
-
-    def g1pts(k, seed):
-        return msm.batch_scalar_mul(msm.G1, g1, rand_scalars(k, seed), k) if k else b""
-
-    nA = int((infA[lo:hi] == 0).sum())
-    nB = int((infB[lo:hi] == 0).sum())
-    nK = max(hi, nb_public) - max(lo, nb_public)
-    sh = groth16.KeyShard(lo, hi, zl, g1_A=g1pts(nA, sd + 1), g1_B=g1pts(nB, sd + 2),
-                          g2_B=msm.batch_scalar_mul(msm.G2, g2_generator_mont(),
-                                                    rand_scalars(nB, sd + 8), nB) if nB else b"",
-                          g1_K=g1pts(nK, sd + 4), g1_Z=g1pts(zh - zl, sd + 3), k_wire_index=None)
-    d = groth16.ProvingKeyData(
-        log_n=log_n, g1_A=b"", g1_B=b"", g1_Z=b"", g1_K=b"",
-        alpha1=g1pts(1, 5), beta1=g1pts(1, 6), delta1=g1pts(1, 7), g2_B=b"",
-        beta2=msm.batch_scalar_mul(msm.G2, g2_generator_mont(), rand_scalars(1, 9), 1),
-        delta2=msm.batch_scalar_mul(msm.G2, g2_generator_mont(), rand_scalars(1, 10), 1),
-        infinity_A=infA.tobytes(), infinity_B=infB.tobytes(), nb_public=nb_public)
-    pk = groth16.ProvingKeyShard(d, rank, world, shard=sh)
-    del sh
-    t_setup = time.time() - t0
-    wires = DeviceBuffer.from_host(rand_scalars(n_wires, 11).tobytes())
-    ncons = n - 5
-    sa, sb, sc = (DeviceBuffer.from_host(rand_scalars(ncons, 12 + i).tobytes()) for i in range(3))
-    sol = groth16.Solution(wires, sa, sb, sc, n_wires, ncons, on_device=True)
-    r, s = fr_const(12345), fr_const(67890)
-    opt = backend.with_amd_acceleration()
-    use_dist_h = groth16.dist_h_supported(n, world)
-    if use_dist_h:
-        # computeH split over the GPUs: three all-to-alls of n/N^2 x 32 B chunks per proof
-        hs = groth16.HShard(log_n, rank, world)
-        xchg = groth16.TorchExchange(hs.exchange_bytes, torch.device("cuda", torch.cuda.current_device()))
-
-        def prove_once():
-            return groth16.prove_distributed_h(pk, hs, xchg, sol, opt, r=r, s=s, device=xdev)
-    else:
-        def prove_once():
-            return groth16.prove_distributed(pk, sol, opt, r=r, s=s, device=xdev)
-    prove_once()
-    ts = []
-    for _ in range(reps):
-        barrier()
-        t = time.perf_counter()
-        pr = prove_once()
-        barrier()
-        el = time.perf_counter() - t
-        tt = torch.tensor([el], dtype=torch.float64, device=xdev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        ts.append(1e3 * float(tt.item()))
-    tim = groth16.last_timings()
-    # every rank must hold the same proof
-    pt = torch.frombuffer(bytearray(pr.Ar + pr.Bs + pr.Krs), dtype=torch.uint8).to(xdev)
-    p0 = pt.clone()
-    dist.broadcast(p0, 0)
-    same = bool(torch.equal(pt, p0))
-    return {"log_n": log_n, "n_gpus": world, "n_constraints": ncons, "n_wires": n_wires,
-            "prove_ms": min(ts), "prove_ms_all": ts, "constraints_per_s": ncons / (min(ts) * 1e-3),
-            "rank0_stage_ms": tim, "key_setup_s": t_setup, "proof_identical_on_all_ranks": same,
-            "sharding": "wires [lo,hi) of A/B1/K/G2 and Z positions per GPU; 576-B partials all-gathered",
-            "compute_h": ("distributed: local n/N transforms + 3 all-to-alls (gg_hshard)" if use_dist_h
-                          else "replicated on every GPU"),
-            "inputs": "resident in HBM"}
 
 
 def fr_const(v):

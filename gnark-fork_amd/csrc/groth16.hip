@@ -9,6 +9,7 @@
 // Combination formulas are prove.go:206-299 verbatim.
 #include "common.h"
 #include "curve.cuh"
+#include "stage.h"
 #include <chrono>
 #include <future>
 #include <memory>
@@ -34,8 +35,8 @@ void msm_prepare_dev(gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStrea
 void msm_finish_dev(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st);
 int msm_base_window(const gg_msm_base* b);
 int choose_c(size_t n, size_t point_bytes, int total_bits);
-void hshard_run(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len, Fr* send, Fr* recv,
-                gg_exchange_fn xchg, void* ctx, hipStream_t st);
+void hshard_run(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len, bool compact, Fr* send,
+                Fr* recv, gg_exchange_fn xchg, void* ctx, hipStream_t st);
 size_t hshard_m(const gg_hshard* hs, int* rank, int* world, int* log_n);
 Fr* hshard_h(gg_hshard* hs);
 }  // namespace gg
@@ -66,9 +67,11 @@ struct gg_groth16_pk {
     bool share_AK = false, share_B = false;
     DevBuf wires, sa, sb, sc;
     hipStream_t s0 = nullptr, s1 = nullptr, s2 = nullptr, s3 = nullptr, s4 = nullptr;
+    std::unique_ptr<Stager> stager;  // host inputs -> HBM (created on first host-input prove)
     int device = 0;
     std::mutex mu;
     ~gg_groth16_pk() {
+        stager.reset();
         if (A) gg_msm_base_release(A);
         if (B) gg_msm_base_release(B);
         if (K) gg_msm_base_release(K);
@@ -81,6 +84,8 @@ struct gg_groth16_pk {
 };
 
 static thread_local double g_timings[9];
+// [0] = host staging of A, B, C (inside the H task, overlapped with the MSMs)
+static thread_local double g_ext[1];
 
 static void ck(int rc) {
     if (rc != GG_OK) throw Error(rc, gg_last_error());
@@ -205,6 +210,15 @@ extern "C" int gg_groth16_pk_create_shard(int log_n, const void* omega_mont, con
     GG_CAPI_END
 }
 
+extern "C" int gg_groth16_pk_base_info(gg_groth16_pk_t pk, int which, size_t* n_points, int* window_bits,
+                                       int* n_windows) {
+    GG_CAPI_BEGIN
+    GG_CHECK(pk && which >= 0 && which <= 4, GG_ERR_INVALID_ARG, "bad argument");
+    gg_msm_base_t b[5] = {pk->A, pk->B, pk->K, pk->Z, pk->B2};
+    return gg_msm_base_info(b[which], n_points, window_bits, n_windows);
+    GG_CAPI_END
+}
+
 extern "C" int gg_groth16_pk_release(gg_groth16_pk_t pk) {
     GG_CAPI_BEGIN
     delete pk;
@@ -229,52 +243,49 @@ struct G16Partials {
     G2Jac b2;           // Σ w·B2
 };
 
+// Joins every worker on scope exit, also while an exception unwinds (the
+// workers reference locals of prove_device, declared before the joiner).
+struct Joiner {
+    std::vector<std::thread>& v;
+    ~Joiner() {
+        for (auto& t : v)
+            if (t.joinable()) t.join();
+    }
+};
+
 // Uploads the solution and runs computeH + the five MSMs of `pk` (a shard, or
-// the whole key).  g_timings[0..6] are filled.
+// the whole key).  Host inputs go through the key's pinned stager: the wires
+// first (the MSM sorts start as soon as they land), then A, B, C from the H
+// task while the MSMs already run (icicle.go:231-278, 478-480 copy them
+// synchronously before any compute).  g_timings[0..6] and g_ext[0..1] are filled.
 static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a,
                          const void* sol_b, const void* sol_c, size_t n_cons,
                          bool inputs_on_device, void* h_dev_out, G16Partials& out,
                          const DistH* dh = nullptr) {
     double t0 = now_ms();
-    const size_t n = pk->n, n_wires = pk->n_wires;
+    const size_t n = pk->n;
     const size_t nbytes = n * 32;
-    pk->wires.reserve(std::max<size_t>(n_wires, 1) * 32);
-    pk->sa.reserve(nbytes);
-    pk->sb.reserve(nbytes);
-    pk->sc.reserve(nbytes);
-    hipMemcpyKind kind = inputs_on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    const size_t nw_shard = pk->wire_hi - pk->wire_lo;
     const Fr* wdev = (const Fr*)wires;
     if (!inputs_on_device) {
-        GG_HIP(hipMemcpyAsync(pk->wires.p, wires, n_wires * 32, hipMemcpyHostToDevice, pk->s0));
+        if (!pk->stager) pk->stager.reset(new Stager(pk->device));
+        // the shard's tables are indexed from its first wire: upload only its wires
+        pk->wires.reserve(std::max<size_t>(nw_shard, 1) * 32);
+        pk->stager->upload(pk->wires.p, (const uint8_t*)wires + pk->wire_lo * 32, nw_shard * 32);
+        const hipStream_t cons[4] = {pk->s0, pk->s2, pk->s3, pk->s4};
+        pk->stager->ready(cons, 4);
         wdev = pk->wires.as<Fr>();
+    } else {
+        wdev += pk->wire_lo;
     }
-    wdev += pk->wire_lo;  // the shard's tables are indexed from its first wire
-    Fr* A = pk->sa.as<Fr>();
-    Fr* B = pk->sb.as<Fr>();
-    Fr* C = pk->sc.as<Fr>();
-    const void* src[3] = {sol_a, sol_b, sol_c};
-    Fr* dst[3] = {A, B, C};
-    for (int i = 0; i < 3; i++) {
-        if (dh) {  // the distributed H gathers its cyclic slices (zero past n_cons) itself
-            if (inputs_on_device) dst[i] = (Fr*)src[i];
-            else if (n_cons) GG_HIP(hipMemcpyAsync(dst[i], src[i], n_cons * 32, kind, pk->s1));
-            continue;
-        }
-        if (n_cons) GG_HIP(hipMemcpyAsync(dst[i], src[i], n_cons * 32, kind, pk->s1));
-        if (n_cons < n) GG_HIP(hipMemsetAsync((char*)dst[i] + n_cons * 32, 0, nbytes - n_cons * 32, pk->s1));
-    }
-    A = dst[0];
-    B = dst[1];
-    C = dst[2];
-    GG_HIP(hipStreamSynchronize(pk->s0));
     double t_up = now_ms();
 
     // Five concurrent tasks, one host thread + HIP stream each (MSM tails are
     // latency-bound, so overlapping them fills the chip):
-    //   s1: computeH -> Z-MSM (h lands in A's buffer)    s2: A-MSM
-    //   s3: B1-MSM    s4: K-MSM    s0 (this thread): G2-MSM
+    //   s1: [A, B, C upload] computeH -> Z-MSM (h lands in A's buffer)
+    //   s2: A-MSM    s3: B1-MSM    s4: K-MSM    s0 (this thread): G2-MSM
     out.z = G1Jac::inf();
-    double t_h = 0, t_z = 0, t_a = 0, t_b = 0, t_k = 0;
+    double t_h = 0, t_z = 0, t_a = 0, t_b = 0, t_k = 0, t_upabc = 0;
     std::mutex emu;
     std::string werr;
     int wcode = GG_OK;
@@ -286,25 +297,64 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
                 fn();
             } catch (const Error& e) {
                 std::lock_guard<std::mutex> g(emu);
-                werr = e.what();
-                wcode = e.code;
+                if (wcode == GG_OK) { werr = e.what(); wcode = e.code; }
             } catch (const std::exception& e) {
                 std::lock_guard<std::mutex> g(emu);
-                werr = e.what();
-                wcode = GG_ERR_INTERNAL;
+                if (wcode == GG_OK) { werr = e.what(); wcode = GG_ERR_INTERNAL; }
             }
         };
     };
     // GG_G16_SERIAL=1 runs the tasks one after another (per-stage isolated timings)
     const bool serial = getenv("GG_G16_SERIAL") && atoi(getenv("GG_G16_SERIAL"));
     std::vector<std::thread> workers;
+    Joiner joiner{workers};
     auto spawn = [&](auto fn) {
         if (serial) fn();
         else workers.emplace_back(fn);
     };
+    // A, B, C -> device (or the distributed H's cyclic slices), on the H task
+    auto inputs_abc = [&](Fr*& A, Fr*& B, Fr*& C, size_t& len) {
+        const void* src[3] = {sol_a, sol_b, sol_c};
+        Fr* dst[3] = {pk->sa.as<Fr>(), pk->sb.as<Fr>(), pk->sc.as<Fr>()};
+        len = n_cons;
+        const double a = now_ms();
+        if (inputs_on_device) {
+            for (int i = 0; i < 3; i++) {
+                if (dh) { dst[i] = (Fr*)src[i]; continue; }
+                if (n_cons) GG_HIP(hipMemcpyAsync(dst[i], src[i], n_cons * 32, hipMemcpyDeviceToDevice, pk->s1));
+                if (n_cons < n) GG_HIP(hipMemsetAsync((char*)dst[i] + n_cons * 32, 0, nbytes - n_cons * 32, pk->s1));
+            }
+        } else if (dh) {
+            // rank r of the distributed computeH reads x[r + N j] only: gather that
+            // cyclic slice on the host (1/N of the bytes over this GPU's link)
+            int rank = 0, world = 1, lg = 0;
+            hshard_m(dh->hs, &rank, &world, &lg);
+            len = n_cons > (size_t)rank ? (n_cons - (size_t)rank + world - 1) / world : 0;
+            for (int i = 0; i < 3; i++)
+                pk->stager->upload_strided(dst[i], src[i], 32, (size_t)rank, (size_t)world, len);
+            pk->stager->ready(&pk->s1, 1);
+        } else {
+            for (int i = 0; i < 3; i++) {
+                if (n_cons < n) GG_HIP(hipMemsetAsync((char*)dst[i] + n_cons * 32, 0, nbytes - n_cons * 32, pk->s1));
+                pk->stager->upload(dst[i], src[i], n_cons * 32);
+            }
+            pk->stager->ready(&pk->s1, 1);
+        }
+        t_upabc = now_ms() - a;
+        A = dst[0];
+        B = dst[1];
+        C = dst[2];
+    };
+    pk->sa.reserve(nbytes);
+    pk->sb.reserve(nbytes);
+    pk->sc.reserve(nbytes);
     if (dh) spawn(guarded([&] {
+        Fr *A, *B, *C;
+        size_t len;
         double a = now_ms();
-        hshard_run(dh->hs, A, B, C, n_cons, dh->send, dh->recv, dh->xchg, dh->ctx, pk->s1);
+        inputs_abc(A, B, C, len);
+        const bool compact = !inputs_on_device;
+        hshard_run(dh->hs, A, B, C, len, compact, dh->send, dh->recv, dh->xchg, dh->ctx, pk->s1);
         GG_HIP(hipStreamSynchronize(pk->s1));
         double b = now_ms();
         t_h = b - a;
@@ -312,7 +362,10 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
         t_z = now_ms() - b;
     }));
     else spawn(guarded([&] {
+        Fr *A, *B, *C;
+        size_t len;
         double a = now_ms();
+        inputs_abc(A, B, C, len);
         compute_h_device(pk->dom, A, B, C, A, pk->s1);
         GG_HIP(hipStreamSynchronize(pk->s1));
         double b = now_ms();
@@ -323,20 +376,26 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
     }));
     // wire sorts, enqueued from this thread before any finisher waits on their
     // events: A's (shared with K) on s2, B1's (shared with G2) on s3
-    MsmSort* sAK = msm_own_sort(pk->A);
-    MsmSort* sB = msm_own_sort(pk->B);
-    MsmSort* sK = pk->share_AK ? sAK : msm_own_sort(pk->K);
-    MsmSort* sB2 = pk->share_B ? sB : msm_own_sort(pk->B2);
-    msm_prepare_dev(pk->A, sAK, wdev, pk->s2);
-    msm_prepare_dev(pk->B, sB, wdev, pk->s3);
-    if (!pk->share_AK) msm_prepare_dev(pk->K, sK, wdev, pk->s4);
-    if (!pk->share_B) msm_prepare_dev(pk->B2, sB2, wdev, pk->s0);
-    spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->A, sAK, &out.a, pk->s2); t_a = now_ms() - a; }));
-    spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->B, sB, &out.b1, pk->s3); t_b = now_ms() - a; }));
-    spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->K, sK, &out.k, pk->s4); t_k = now_ms() - a; }));
-    double t2 = now_ms();
-    guarded([&] { msm_finish_dev(pk->B2, sB2, &out.b2, pk->s0); })();
-    double te = now_ms();
+    MsmSort *sAK = nullptr, *sB = nullptr, *sK = nullptr, *sB2 = nullptr;
+    guarded([&] {
+        sAK = msm_own_sort(pk->A);
+        sB = msm_own_sort(pk->B);
+        sK = pk->share_AK ? sAK : msm_own_sort(pk->K);
+        sB2 = pk->share_B ? sB : msm_own_sort(pk->B2);
+        msm_prepare_dev(pk->A, sAK, wdev, pk->s2);
+        msm_prepare_dev(pk->B, sB, wdev, pk->s3);
+        if (!pk->share_AK) msm_prepare_dev(pk->K, sK, wdev, pk->s4);
+        if (!pk->share_B) msm_prepare_dev(pk->B2, sB2, wdev, pk->s0);
+    })();
+    double t2 = now_ms(), te = t2;
+    if (wcode == GG_OK) {  // the sorts are enqueued: run the finishers
+        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->A, sAK, &out.a, pk->s2); t_a = now_ms() - a; }));
+        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->B, sB, &out.b1, pk->s3); t_b = now_ms() - a; }));
+        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->K, sK, &out.k, pk->s4); t_k = now_ms() - a; }));
+        t2 = now_ms();
+        guarded([&] { msm_finish_dev(pk->B2, sB2, &out.b2, pk->s0); })();
+        te = now_ms();
+    }
     for (auto& w : workers) w.join();
     if (wcode != GG_OK) throw Error(wcode, werr);
     g_timings[0] = t_up - t0;
@@ -346,6 +405,7 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
     g_timings[4] = t_k;
     g_timings[5] = t_z;
     g_timings[6] = te - t2;
+    g_ext[0] = t_upabc;
 }
 
 // Fixed-point terms of the proof (prove.go:177-192, 293-296): kr = -r*s and
@@ -419,6 +479,7 @@ extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_
              GG_ERR_INVALID_ARG, "gg_groth16_prove needs the whole key; a shard proves with "
                                  "gg_groth16_prove_partial + gg_groth16_finalize");
     std::lock_guard<std::mutex> lk(pk->mu);
+    g_ext[0] = 0;
     double t0 = now_ms();
     // host pool computes the fixed-point terms while the GPU works
     auto fixed = fixed_terms_async(pk->delta, pk->delta2, fr_from(r_mont), fr_from(s_mont));
@@ -440,6 +501,7 @@ extern "C" int gg_groth16_prove_partial(gg_groth16_pk_t pk, const void* wires, s
     check_prove_args(pk, wires, n_wires, sol_a, sol_b, sol_c, n_cons);
     GG_CHECK(partials, GG_ERR_INVALID_ARG, "null argument");
     std::lock_guard<std::mutex> lk(pk->mu);
+    g_ext[0] = 0;
     double t0 = now_ms();
     G16Partials p;
     prove_device(pk, wires, sol_a, sol_b, sol_c, n_cons, inputs_on_device != 0, h_dev_out, p);
@@ -468,6 +530,7 @@ extern "C" int gg_groth16_prove_partial_dist(gg_groth16_pk_t pk, gg_hshard_t hs,
     GG_CHECK(pk->z_lo == (size_t)rank * m && pk->nZ == std::min(m, pk->n - 1 - pk->z_lo),
              GG_ERR_INVALID_ARG, "key shard must own Z positions [rank*m, (rank+1)*m)");
     std::lock_guard<std::mutex> lk(pk->mu);
+    g_ext[0] = 0;
     double t0 = now_ms();
     G16Partials p;
     DistH dh{hs, xchg, xchg_ctx, (Fr*)send_dev, (Fr*)recv_dev};
@@ -507,6 +570,16 @@ extern "C" int gg_groth16_finalize(const void* alpha1, const void* beta1, const 
     memcpy(&p.z, q + 288, 96);
     memcpy(&p.b2, q + 384, 192);
     g16_combine(p, fixed.get(), alpha, beta, b2, ar_aff, bs_aff, krs_aff);
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_last_timings_ex(double* ms, int cap) {
+    GG_CAPI_BEGIN
+    GG_CHECK(ms && cap >= 0, GG_ERR_INVALID_ARG, "null argument");
+    double all[10];
+    memcpy(all, g_timings, sizeof(g_timings));
+    all[9] = g_ext[0];
+    memcpy(ms, all, sizeof(double) * (size_t)std::min(cap, 10));
     GG_CAPI_END
 }
 

@@ -694,7 +694,9 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, hipStream_t st) {
     const size_t items_ub = s->items_ub;
     b->partA.reserve((items_ub + 1) * sizeof(Xyzz<F>));
     {
-        ProfScope ps_acc("msm_accum", st, (double)n);
+        // per-group names: the Groth16 prove runs G1 and G2 accumulations at once
+        const char* acc_name = sizeof(F) == sizeof(Fp) ? "msm_accum" : (sizeof(F) == sizeof(Fp2) ? "msm_accum_g2" : "msm_accum_bls");
+        ProfScope ps_acc(acc_name, st, (double)n);
         hipLaunchKernelGGL(k_accum_affine<F>, dim3(grid_for(items_ub, 256)), dim3(256),
                            kMergeInBlock<F> ? 256 * sizeof(Xyzz<F>) : 0, st, (const Affine<F>*)b->pts.p,
                            s->sorted.as<uint32_t>(), offs, ioff, s->item_bucket.as<uint32_t>(),

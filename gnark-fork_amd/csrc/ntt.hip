@@ -702,8 +702,10 @@ static void launch_cross_inv(gg_hshard* hs, Fr* h, const Fr* recv, hipStream_t s
 }
 
 // ---- the four local phases (exchanges between them are the caller's) ----
+// compact: a, b, c already hold this rank's cyclic slices x[rank + N j] (len of
+// them), e.g. gathered on the host by the stager, instead of full vectors
 void hshard_phase1(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len, Fr* send,
-                   hipStream_t st) {
+                   hipStream_t st, bool compact = false) {
     const size_t m = hs->m;
     Fr* y = hs->y.as<Fr>();
     PowTab twi{hs->wi_hi.as<Fr>(), hs->wi_lo.as<Fr>(), hs->S};
@@ -711,7 +713,7 @@ void hshard_phase1(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t 
     for (int p = 0; p < 3; p++) {
         Fr* yp = y + (size_t)p * m;
         hipLaunchKernelGGL(k_gather_cyclic, dim3(grid_for(m, 256)), dim3(256), 0, st, yp, src[p], len,
-                           m, hs->rank, hs->world);
+                           m, compact ? 0 : hs->rank, compact ? 1 : hs->world);
         GG_HIP(hipGetLastError());
         // iDFT_m (DIF: natural -> bit-reversed), 1/m folded in
         run_transform(hs->loc.get(), yp, yp, false, true, -1, SK_NINV, (const Fr*)nullptr,
@@ -832,14 +834,15 @@ gg_hshard* hshard_create(int log_n, const void* omega_mont, const void* coset_ge
 
 // Whole distributed computeH on this rank; xchg(ctx, send, recv, bytes_per_rank)
 // performs the all-to-all (blocking).  a/b/c: full vectors on the device.
-void hshard_run(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len, Fr* send, Fr* recv,
-                gg_exchange_fn xchg, void* ctx, hipStream_t st) {
+void hshard_run(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len, bool compact, Fr* send,
+                Fr* recv, gg_exchange_fn xchg, void* ctx, hipStream_t st) {
+    std::lock_guard<std::mutex> lk(hs->mu);  // hs->y / hblk are per-handle scratch
     auto exchange = [&](int phase) {
         GG_HIP(hipStreamSynchronize(st));
         int rc = xchg(ctx, send, recv, hshard_exchange_bytes(hs, phase));
         GG_CHECK(rc == 0, GG_ERR_INTERNAL, "exchange callback failed");
     };
-    hshard_phase1(hs, a, b, c, len, send, st);
+    hshard_phase1(hs, a, b, c, len, send, st, compact);
     exchange(1);
     hshard_phase2(hs, recv, send, st);
     exchange(2);

@@ -62,6 +62,9 @@ extern "C" int gg_fr_from_canonical_be(int curve, const void* in_dev, void* out_
     GG_CAPI_BEGIN
     GG_CHECK(in_dev && out_dev, GG_ERR_INVALID_ARG, "null argument");
     GG_CHECK(curve == GG_CURVE_BN254 || curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "bad curve");
+    // the kernels move 16-B vectors (a raw witness blob + 12 header bytes is not aligned)
+    GG_CHECK(((uintptr_t)in_dev & 15) == 0 && ((uintptr_t)out_dev & 15) == 0, GG_ERR_INVALID_ARG,
+             "in_dev / out_dev must be 16-byte aligned");
     if (n_invalid) *n_invalid = 0;
     if (n == 0) return GG_OK;
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : hipStreamPerThread;
@@ -87,6 +90,8 @@ extern "C" int gg_fr_to_canonical_be(int curve, const void* in_dev, void* out_de
     GG_CAPI_BEGIN
     GG_CHECK(in_dev && out_dev, GG_ERR_INVALID_ARG, "null argument");
     GG_CHECK(curve == GG_CURVE_BN254 || curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "bad curve");
+    GG_CHECK(((uintptr_t)in_dev & 15) == 0 && ((uintptr_t)out_dev & 15) == 0, GG_ERR_INVALID_ARG,
+             "in_dev / out_dev must be 16-byte aligned");
     if (n == 0) return GG_OK;
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : hipStreamPerThread;
     if (curve == GG_CURVE_BN254)

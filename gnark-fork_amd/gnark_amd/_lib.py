@@ -75,6 +75,8 @@ def _load():
         "gg_groth16_pk_release": ([P], I),
         "gg_groth16_prove": ([P, P, S, P, P, P, S, I, P, P, P, P, P, P], I),
         "gg_groth16_last_timings": ([ctypes.POINTER(ctypes.c_double)], I),
+        "gg_groth16_last_timings_ex": ([ctypes.POINTER(ctypes.c_double), I], I),
+        "gg_groth16_pk_base_info": ([P, I, P, P, P], I),
         "gg_groth16_pk_create_shard": ([I, P, P, P, S, P, S, P, S, S, P, S, P, P, P, P, P, P, P, P, S,
                                         S, P, S, S, PP], I),
         "gg_groth16_prove_partial": ([P, P, S, P, P, P, S, I, P, P], I),
@@ -123,7 +125,8 @@ EXPORTED = [
     "gg_bls12_381_fr_prefix_product", "gg_bls12_381_fr_horner", "gg_plonk_fold_h",
     "gg_plonk_linearized", "gg_copy_device", "gg_memset_device", "gg_bls12_381_fr_bit_reverse",
     "gg_bls12_381_fr_axpy", "gg_bls12_381_g1_scalar_mul", "gg_fr_from_canonical_be",
-    "gg_fr_to_canonical_be",
+    "gg_fr_to_canonical_be", "gg_groth16_last_timings_ex",
+    "gg_groth16_pk_base_info",
 ]
 
 

@@ -78,6 +78,9 @@ class Proof:
                 + struct.pack(">I", 0) + fr.g1_raw(bytes(64)))
 
 
+BASE_A, BASE_B1, BASE_K, BASE_Z, BASE_B2 = range(5)
+
+
 class ProvingKey:
     """icicle_bn254.ProvingKey {ProvingKey; *deviceInfo}: device-resident key."""
 
@@ -102,6 +105,13 @@ class ProvingKey:
         self.handle = h
         self.n_wires = n_wires
         self.log_n = data.log_n
+
+    def base_info(self, which: int):
+        """(resident points, window bits, windows) of MSM base `which` (BASE_*)."""
+        n, c, w = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_int()
+        check(lib.gg_groth16_pk_base_info(self.handle, which, ctypes.byref(n), ctypes.byref(c),
+                                          ctypes.byref(w)))
+        return n.value, c.value, w.value
 
     def close(self):
         if self.handle:
@@ -138,9 +148,13 @@ def prove(pk: ProvingKey, solution: Solution, *opts, r: bytes = None, s: bytes =
 
 
 def last_timings() -> dict:
-    arr = (ctypes.c_double * 9)()
-    check(lib.gg_groth16_last_timings(arr))
-    keys = ["upload", "compute_h", "msm_A", "msm_B1", "msm_K", "msm_Z", "msm_G2", "epilogue", "total"]
+    """Per-stage wall times (ms) of this thread's last prove: upload = host staging
+    of the wires (before the MSMs start); upload_abc = host staging of A, B, C
+    inside the computeH task (overlapped with the MSMs, included in compute_h)."""
+    arr = (ctypes.c_double * 10)()
+    check(lib.gg_groth16_last_timings_ex(arr, 10))
+    keys = ["upload", "compute_h", "msm_A", "msm_B1", "msm_K", "msm_Z", "msm_G2", "epilogue", "total",
+            "upload_abc"]
     return dict(zip(keys, list(arr)))
 
 
@@ -234,6 +248,7 @@ class ProvingKeyShard:
         self.n_wires = data.n_wires
         self.log_n = data.log_n
 
+    base_info = ProvingKey.base_info
     close = ProvingKey.close
     __del__ = ProvingKey.__del__
 

@@ -43,8 +43,8 @@ def parse_header(data: bytes):
     nb_public, nb_secret, n = struct.unpack(">III", data[:12])
     if len(data) < 12 + 32 * n:
         raise ValueError("witness: truncated vector")
-    if n != nb_public + nb_secret:
-        raise ValueError("witness: vector length != nbPublic + nbSecret")
+    # witness.ReadFrom (witness.go:140-190) reads the header and then the
+    # fr.Vector as-is, without checking len == nbPublic + nbSecret; neither do we
     return nb_public, nb_secret, n, 12
 
 

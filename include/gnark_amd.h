@@ -182,6 +182,10 @@ int gg_groth16_pk_create(int log_n, const void *omega_mont, const void *coset_ge
                          const uint8_t *inf_A, const uint8_t *inf_B, size_t n_wires,
                          size_t nb_public, const uint32_t *k_wire_index, gg_groth16_pk_t *out);
 int gg_groth16_pk_release(gg_groth16_pk_t pk);
+/* resident MSM base `which` of a key (0 = G1.A, 1 = G1.B, 2 = G1.K, 3 = G1.Z,
+ * 4 = G2.B): as gg_msm_base_info */
+int gg_groth16_pk_base_info(gg_groth16_pk_t pk, int which, size_t *n_points, int *window_bits,
+                            int *n_windows);
 
 /* Groth16 Prove after Solve (prove.go:127-320; icicle.go:198-420):
  *   wires[n_wires] = solution.W; sol_a/b/c[n_cons] = solution.A/B/C
@@ -263,6 +267,10 @@ int gg_groth16_prove_partial_dist(gg_groth16_pk_t pk, gg_hshard_t hs, const void
  * [0]=upload [1]=computeH [2]=msm_A [3]=msm_B1 [4]=msm_K [5]=msm_Z [6]=msm_G2
  * [7]=epilogue [8]=total */
 int gg_groth16_last_timings(double *ms9);
+/* the same plus [9] = host staging of the solution's A, B, C (host inputs: done
+ * by the computeH task through pinned buffers while the MSMs run; part of [1]).
+ * [0] is the staging of the wires (before any MSM starts).  cap: entries wanted. */
+int gg_groth16_last_timings_ex(double *ms, int cap);
 
 
 /* ------------------------------------------------ PlonK BLS12-381 (fr, 32 B)

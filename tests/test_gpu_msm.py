@@ -137,3 +137,41 @@ def test_msm_g2_vs_oracle(n, dist):
     sc = random_fr_mont(n, 600 + n, dist)
     base = msm.MsmBase(msm.G2, pts, n)
     assert base.msm(sc, n) == coracle.msm_g2(pts.tobytes(), sc.tobytes(), n)
+
+
+def _g2_trapdoor(ks, ss):
+    e = coracle.fr_dot(ks, ss, len(ks))
+    return bytes(coracle.g2_batch_mul(o.g2_to_bytes(o.G2_GEN), e, 1))
+
+
+@pytest.mark.parametrize("n,dist", [(1 << 16, "uniform"), (1 << 18, "witness"), (1 << 16, "skew")])
+def test_msm_g2_window20(n, dist):
+    """The window choose_c picks for the 2^24 G2 base of config 4 (c = 20: 13
+    windows, 2^19 Fp2 buckets, the Fp2 reduction arena), here forced on smaller
+    bases; 'skew' puts half of all scalars on one value (one heavy bucket per
+    window, the segmented heavy-bucket tree)."""
+    from gnark_amd import msm
+    ks = random_fr_mont(n, 700 + n)
+    pts = coracle.g2_batch_mul(o.g2_to_bytes(o.G2_GEN), ks.tobytes(), n)
+    if dist == "skew":
+        ss = random_fr_mont(n, 800 + n)
+        ss[: n // 2] = ss[0]
+    else:
+        ss = random_fr_mont(n, 800 + n, dist)
+    base = msm.MsmBase(msm.G2, bytes(pts), n, window_bits=20)
+    assert base.info()[1:] == (20, 13)
+    assert base.msm(ss, n) == _g2_trapdoor(ks, ss)
+
+
+def test_msm_g2_window20_2p20():
+    """2^20 G2 points at c = 20, trapdoor-checked."""
+    from gnark_amd import msm
+    n = 1 << 20
+    ks = random_fr_mont(n, 901)
+    ss = random_fr_mont(n, 902, "witness")
+    pts = msm.batch_scalar_mul(msm.G2, o.g2_to_bytes(o.G2_GEN), ks, n)
+    base = msm.MsmBase(msm.G2, pts, n)
+    assert base.info()[1] in (17, 18, 19, 20)
+    assert base.msm(ss, n) == _g2_trapdoor(ks, ss)
+    base20 = msm.MsmBase(msm.G2, pts, n, window_bits=20)
+    assert base20.msm(ss, n) == _g2_trapdoor(ks, ss)
