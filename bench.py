@@ -35,6 +35,7 @@ METRIC = ("Groth16 prove time + MSM G1 throughput (Mscalar-mul/s) BN254 2^24 R1C
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FPMUL_PEAK_G = 135.7  # measured BN254 Fp Montgomery multiplies/s (G), profiles/r01_v2_mbench_field.txt
 MIMC_ROUNDS = 85      # 3 constraints per round; 2^(log_n-8) chains -> 255 * 2^(log_n-8) constraints
+ROOFLINE_PROVES = 3   # serial proves timed kernel by kernel for the roofline
 
 
 def log(*a):
@@ -166,17 +167,25 @@ def main():
     stage = g.timings()
     same = g.proof_identical_on_all_ranks()
 
-    # ---- roofline of the dominant kernel, HIP events on its launch stream,
-    # over proves exactly like the timed ones (concurrent streams)
+    # ---- roofline of the dominant kernel: HIP events on its launch stream, over
+    # ROOFLINE_PROVES proves with the five tasks run one after another
+    # (GG_G16_SERIAL=1), so an event pair brackets the kernel alone -- with five
+    # busy streams it would also count the wait for CUs held by the other MSMs.
+    # These are the last k_accum_affine<Fp2> launches of the run; the committed
+    # rocprof summary reports the average of exactly those dispatches
+    # (tools/prof_summary.py --last).
     _lib.profile_enable(True)
-    prof_steps = 3
-    for _ in range(prof_steps):
-        g.prove()
+    os.environ["GG_G16_SERIAL"] = "1"
+    try:
+        for _ in range(ROOFLINE_PROVES):
+            g.prove()
+    finally:
+        del os.environ["GG_G16_SERIAL"]
     kernels = {}
     for name in ("msm_sort", "msm_accum", "msm_accum_g2", "msm_accum2", "msm_reduce", "ntt_pass"):
         tot, cnt, units = _lib.profile_get(name)
-        kernels[name] = {"avg_ms": tot / cnt if cnt else None, "launches_per_proof": cnt / prof_steps,
-                         "total_ms_per_proof": tot / prof_steps}
+        kernels[name] = {"avg_ms": tot / cnt if cnt else None, "launches_per_proof": cnt / ROOFLINE_PROVES,
+                         "total_ms_per_proof": tot / ROOFLINE_PROVES}
     _lib.profile_enable(False)
     nB2 = g.nB2
     g2_ms = kernels["msm_accum_g2"]["avg_ms"]
@@ -190,16 +199,16 @@ def main():
                 "kernel": "k_accum_affine<Fp2> (G2 bucket accumulation of the B MSM: the longest "
                           "single launch of the prove)",
                 "algorithmic_bytes_per_launch": alg_bytes, "kernel_avg_ms": g2_ms,
-                "timing": "HIP events on the kernel's launch stream, during proves with all five "
-                          "streams busy (same launches the rocprof summary averages)",
+                "timing": "HIP events on the kernel's launch stream over %d proves run task by task "
+                          "(the last %d launches of the kernel in the run; rocprof summary: "
+                          "profiles/r02_*_kernel_stats.md, 'last %d' column)" % ((ROOFLINE_PROVES,) * 3),
                 "note": "EC MSM is VALU-integer bound (SURVEY 8d); HBM fraction reported as required"}
     if g2_ms:
         W2 = g.g2_windows
         mul_rate = nB2 * W2 * 10 * 3 / (g2_ms * 1e-3) / 1e9  # Fp2 mul ~ 3 Fp mul (Karatsuba)
         roofline["valu"] = {"achieved_Gfpmul_s": mul_rate, "peak_Gfpmul_s": FPMUL_PEAK_G,
                             "frac": mul_rate / FPMUL_PEAK_G,
-                            "basis": "|B2| x W mixed XYZZ adds x 10 Fp2-mul x 3 Fp-mul (Karatsuba); "
-                                     "the kernel shares the GPU with four other MSM streams"}
+                            "basis": "|B2| x W mixed XYZZ adds x 10 Fp2-mul x 3 Fp-mul (Karatsuba)"}
 
     out = {
         "metric": METRIC, "value": value, "unit": "constraints/s", "n_gpus": world,
