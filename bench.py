@@ -673,10 +673,11 @@ def plonk_bench(log_n, reps=5):
 
 def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, xdev=None,
                       barrier=None):
-    """BLS12-381 PlonK prove (gnark_amd.plonk_prover: every step of prove.go on the
-    GPU) at n = 2^log_n with a synthetic key (random SRS points, selectors and
-    copy permutation) and a random witness, inputs resident in HBM.  The proof of
-    a random witness does not verify; the work is that of a real proof."""
+    """BLS12-381 PlonK prove (gg_plonk_prove: prove.go:116-1079 inside the library,
+    errgroup DAG on HIP streams) at n = 2^log_n with a synthetic key (random SRS
+    points, selectors and copy permutation) and a random witness, inputs resident
+    in HBM.  The proof of a random witness does not verify; the work is that of a
+    real proof (satisfied 2^22 circuits verify in tests/test_gpu_plonk_prove.py)."""
     import numpy as np
     from gnark_amd import fr, msm, plonk_prover as pp, DeviceBuffer
     n = 1 << log_n
@@ -732,7 +733,9 @@ def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, 
     extra = {"stage_ms_all": tims} if per_rep else {}
     return {"log_n": log_n, "n_gpus": world, "prove_ms": min(ts), "prove_ms_all": ts, "stage_ms": tim,
             **extra, "kzg_bases": "1/%d slice per GPU, partial commitments all-gathered" % world,
-            "key_setup_s": t_setup, "msms_per_proof": 10, "ntts_per_proof": "16 coset FFTs (L,R,O,Z x 4 cosets; key polynomials resident) + 4 iFFTs of n + 1 coset iFFT of 4n",
+            "key_setup_s": t_setup, "msms_per_proof": 10,
+            "ntts_per_proof": "20 coset FFTs (L,R,O,Z,Qk x 4 cosets; key polynomials resident) + 5 iFFTs of n + 1 coset iFFT of 4n",
+            "orchestration": "C++ (gg_plonk_prove): 3 concurrent KZG MSMs for LRO and for H, openZ || linearized, two cosets in flight",
             "note": "synthetic key + random witness (timing only; proofs of valid witnesses verify in "
                     "tests/test_gpu_plonk_prove.py)"}
 

@@ -80,6 +80,27 @@ struct DevBuf {
     }
 };
 
+// bump allocator over one device buffer: per-task scratch that is reused across
+// calls (no hipMalloc / hipFree -- which synchronise the device -- inside a
+// prove).  get() hands out 256-B aligned slices; reset() recycles them all.
+struct Arena {
+    DevBuf buf;
+    size_t off = 0;
+    void reserve(size_t b) {
+        if (b > buf.bytes) buf.alloc(b);
+        off = 0;
+    }
+    void reset() { off = 0; }
+    template <class T>
+    T* get(size_t count) {
+        const size_t b = (count * sizeof(T) + 255) & ~(size_t)255;
+        GG_CHECK(off + b <= buf.bytes, GG_ERR_INTERNAL, "device arena overflow");
+        T* p = reinterpret_cast<T*>((char*)buf.p + off);
+        off += b;
+        return p;
+    }
+};
+
 inline bool is_device_ptr(const void* p) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {

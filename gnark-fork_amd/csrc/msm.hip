@@ -6,14 +6,14 @@ void create_base_g1(gg_msm_base* b, const void* points, size_t n, int on_device,
                     const uint32_t* sidx, int window_bits, bool keep_inf);
 void create_base_g2(gg_msm_base* b, const void* points, size_t n, int on_device,
                     const uint32_t* sidx, int window_bits, bool keep_inf);
-void msm_run_g1(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st);
-void msm_run_g2(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st);
-void msm_finish_g1(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st);
-void msm_finish_g2(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st);
 void create_base_bls(gg_msm_base* b, const void* points, size_t n, int on_device,
                      const uint32_t* sidx, int window_bits, bool keep_inf);
-void msm_run_bls(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st);
-void msm_finish_bls(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st);
+void msm_run_g1(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st);
+void msm_run_g2(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st);
+void msm_run_bls(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st);
+void msm_finish_g1(gg_msm_base* b, MsmSort* s, MsmScratch* scr, void* out_jac, hipStream_t st);
+void msm_finish_g2(gg_msm_base* b, MsmSort* s, MsmScratch* scr, void* out_jac, hipStream_t st);
+void msm_finish_bls(gg_msm_base* b, MsmSort* s, MsmScratch* scr, void* out_jac, hipStream_t st);
 }  // namespace gg
 
 using namespace gg;
@@ -52,10 +52,14 @@ extern "C" int gg_msm_base_info(gg_msm_base_t b, size_t* n_points, int* window_b
 }
 
 namespace gg {
+// one MSM over b with the work state w (no lock: b is read-only, w is the caller's)
+void msm_device_work(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
+    if (b->group == GG_G1) msm_run_g1(b, w, scalars_dev, out_jac, st);
+    else if (b->group == GG_G2) msm_run_g2(b, w, scalars_dev, out_jac, st);
+    else msm_run_bls(b, w, scalars_dev, out_jac, st);
+}
 static void msm_device_locked(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
-    if (b->group == GG_G1) msm_run_g1(b, scalars_dev, out_jac, st);
-    else if (b->group == GG_G2) msm_run_g2(b, scalars_dev, out_jac, st);
-    else msm_run_bls(b, scalars_dev, out_jac, st);
+    msm_device_work(b, &b->own, scalars_dev, out_jac, st);
 }
 // used by the Groth16 prover as well
 void msm_device(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
@@ -80,15 +84,17 @@ bool msm_same_shape(const gg_msm_base* a, const gg_msm_base* b) {
     GG_HIP(hipMemcpy(y.data(), b->sidx.p, b->n * 4, hipMemcpyDeviceToHost));
     return x == y;
 }
-MsmSort* msm_own_sort(gg_msm_base* b) { return &b->own; }
+MsmSort* msm_own_sort(gg_msm_base* b) { return &b->own.sort; }
+MsmWork* msm_work_new() { return new MsmWork(); }
+void msm_work_delete(MsmWork* w) { delete w; }
 int msm_base_window(const gg_msm_base* b) { return b->c; }
 void msm_prepare_dev(gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st) {
     if (b->n) msm_prepare(b, s, scalars_dev, st);
 }
 void msm_finish_dev(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st) {
-    if (b->group == GG_G1) msm_finish_g1(b, s, out_jac, st);
-    else if (b->group == GG_G2) msm_finish_g2(b, s, out_jac, st);
-    else msm_finish_bls(b, s, out_jac, st);
+    if (b->group == GG_G1) msm_finish_g1(b, s, &b->own.scr, out_jac, st);
+    else if (b->group == GG_G2) msm_finish_g2(b, s, &b->own.scr, out_jac, st);
+    else msm_finish_bls(b, s, &b->own.scr, out_jac, st);
 }
 size_t msm_scalars_needed(gg_msm_base* b) {
     return b->has_sidx ? (b->n ? (size_t)b->max_sidx + 1 : 0) : b->n;
@@ -107,9 +113,9 @@ extern "C" int gg_msm(gg_msm_base_t b, const void* scalars, size_t n_scalars, in
     std::lock_guard<std::mutex> lk(b->mu);
     const Fr* sdev = (const Fr*)scalars;
     if (!scalars_on_device && need) {
-        b->scal.reserve(need * 32);
-        GG_HIP(hipMemcpyAsync(b->scal.p, scalars, need * 32, hipMemcpyHostToDevice, st));
-        sdev = b->scal.as<Fr>();
+        b->own.scr.scal.reserve(need * 32);
+        GG_HIP(hipMemcpyAsync(b->own.scr.scal.p, scalars, need * 32, hipMemcpyHostToDevice, st));
+        sdev = b->own.scr.scal.as<Fr>();
     }
     msm_device_locked(b, sdev, out_jac, st);
     GG_CAPI_END

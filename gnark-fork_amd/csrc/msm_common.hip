@@ -63,13 +63,6 @@ void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, hipStream_t st,
 }
 
 // ------------------------------------------------------------------ kernels
-// total count of entries for out[n] of the scan is handled by k_total.
-// out[n] = total, out[n+1] = *maxcnt (one 8-byte read-back per level)
-__global__ void k_set_total_max(uint32_t* out, const uint32_t* in, size_t n, const uint32_t* maxcnt) {
-    out[n] = n ? out[n - 1] + in[n - 1] : 0u;
-    out[n + 1] = *maxcnt;
-}
-
 __global__ void k_set_total(uint32_t* out, const uint32_t* in, size_t n) {
     // out[n] = out[n-1] + in[n-1]
     if (n) out[n] = out[n - 1] + in[n - 1];
@@ -85,17 +78,11 @@ __device__ __forceinline__ uint32_t extract_bits(const E& k, int bit, int c) {
     return (uint32_t)(v & ((1u << c) - 1));
 }
 
-// items per bucket = ceil(cnt / K); block-level max, one atomic per block
-__global__ void __launch_bounds__(256) k_item_counts(const uint32_t* offsets, size_t nb, int K,
-                                                     uint32_t* itemcnt, uint32_t* maxcnt) {
+// entries of the fullest bucket: block-level max, one atomic per block
+__global__ void __launch_bounds__(256) k_bucket_max(const uint32_t* offsets, size_t nb, uint32_t* maxcnt) {
     __shared__ uint32_t wmax[4];
     size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t v = 0;
-    if (b < nb) {
-        uint32_t cnt = offsets[b + 1] - offsets[b];
-        v = (cnt + K - 1) / K;
-        itemcnt[b] = v;
-    }
+    uint32_t v = b < nb ? offsets[b + 1] - offsets[b] : 0u;
     for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
     if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = v;
     __syncthreads();
@@ -103,20 +90,6 @@ __global__ void __launch_bounds__(256) k_item_counts(const uint32_t* offsets, si
         uint32_t m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
         if (m) atomicMax(maxcnt, m);
     }
-}
-
-// item -> bucket map: one thread per item, upper_bound over item_off (a heavy
-// bucket's thousands of items no longer serialise on one thread)
-__global__ void k_item_buckets(const uint32_t* item_off, size_t nb, const uint32_t* n_items_dev,
-                               uint32_t* item_bucket) {
-    size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= *n_items_dev) return;
-    size_t lo = 0, hi = nb;  // largest b with item_off[b] <= t (item_off[0] = 0)
-    while (hi - lo > 1) {
-        size_t mid = (lo + hi) >> 1;
-        if (item_off[mid] <= (uint32_t)t) lo = mid; else hi = mid;
-    }
-    item_bucket[t] = (uint32_t)lo;
 }
 
 int choose_c(size_t n, size_t point_bytes, int total_bits) {
@@ -606,46 +579,34 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     }
 }
 
-// Sort + work items of one scalar vector over b's shape into s; records
-// s->ready_ev (items ready) and s->pin_ev ((n_items, max_items) on the host).
+// Sort of one scalar vector over b's shape into s; records s->ready_ev (sort
+// done) and s->pin_ev (the fullest bucket's entry count on the host).
 void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st) {
     const size_t n = b->n, nb = b->nb;
     s->ensure_events();
     s->counts.reserve(nb * 4);
     s->offsets.reserve((nb + 1) * 4);
-    s->itemcnt.reserve(nb * 4);
-    s->item_off.reserve((nb + 2) * 4);
     s->maxcnt.reserve(4);
     {
         ProfScope ps_sort("msm_sort", st, (double)n);
         sort_entries(b, s, scalars_dev, st);
         ps_sort.stop(st);
     }
-    // Buckets are cut into items of <= K1 entries (32, doubled up to 256 while
-    // that still leaves > 4M items; MI355X sweep: 2^24 best at K1 = 56..64); bucket q's items are item_off[q] ..
-    // item_off[q+1].  (n_items, max_items) go to pinned memory behind an event
-    // while the accumulation runs on an upper-bound grid (no host stall).
-    int K1 = 32;
-    while (K1 < 256 && (size_t)b->W * n / (size_t)K1 > ((size_t)4 << 20)) K1 *= 2;
-    if (const char* e = getenv("GG_MSM_K1")) K1 = std::max(1, atoi(e));
-    s->K1 = K1;
-    s->items_ub = ((size_t)b->W * n + (size_t)K1 - 1) / (size_t)K1 + nb;
-    uint32_t* offs = s->offsets.as<uint32_t>();
-    uint32_t* ioff = s->item_off.as<uint32_t>();
+    // Accumulation ranges of K sorted entries, one thread each (32, doubled up
+    // to 256 while that still leaves > 4M ranges; MI355X sweep of the item
+    // version: 2^24 best at 56..64).  The fullest bucket's size goes to pinned
+    // memory behind an event while the accumulation runs (no host stall).
+    uint32_t K = 32;
+    while (K < 256 && (size_t)b->W * n / (size_t)K > ((size_t)4 << 20)) K *= 2;
+    if (const char* e = getenv("GG_MSM_K1")) K = (uint32_t)std::max(1, atoi(e));
+    s->K = K;
+    s->ranges_ub = ((size_t)b->W * n + K - 1) / K;
     GG_HIP(hipMemsetAsync(s->maxcnt.p, 0, 4, st));
-    hipLaunchKernelGGL(k_item_counts, dim3(grid_for(nb, 256)), dim3(256), 0, st, offs, nb, K1,
-                       s->itemcnt.as<uint32_t>(), s->maxcnt.as<uint32_t>());
-    GG_HIP(hipGetLastError());
-    exclusive_scan(s->itemcnt.as<uint32_t>(), ioff, nb, st, s->scan_tmp);
-    hipLaunchKernelGGL(k_set_total_max, dim3(1), dim3(1), 0, st, ioff, s->itemcnt.as<uint32_t>(), nb,
+    hipLaunchKernelGGL(k_bucket_max, dim3(grid_for(nb, 256)), dim3(256), 0, st, s->offsets.as<uint32_t>(), nb,
                        s->maxcnt.as<uint32_t>());
     GG_HIP(hipGetLastError());
-    GG_HIP(hipMemcpyAsync(s->pin, ioff + nb, 8, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipMemcpyAsync(s->pin, s->maxcnt.p, 4, hipMemcpyDeviceToHost, st));
     GG_HIP(hipEventRecord(s->pin_ev, st));
-    s->item_bucket.reserve((s->items_ub + 1) * 4);
-    hipLaunchKernelGGL(k_item_buckets, dim3(grid_for(s->items_ub, 256)), dim3(256), 0, st, ioff, nb,
-                       ioff + nb, s->item_bucket.as<uint32_t>());
-    GG_HIP(hipGetLastError());
     GG_HIP(hipEventRecord(s->ready_ev, st));
 }
 

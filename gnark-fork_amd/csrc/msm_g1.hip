@@ -6,12 +6,12 @@ void create_base_g1(gg_msm_base* b, const void* points, size_t n, int on_device,
                     const uint32_t* sidx, int window_bits, bool keep_inf) {
     create_base<Fp>(b, points, n, on_device, sidx, window_bits, keep_inf);
 }
-void msm_run_g1(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
-    G1Jac j = xyzz_to_jac(msm_run<Fp>(b, scalars_dev, st));
+void msm_run_g1(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
+    G1Jac j = xyzz_to_jac(msm_run<Fp>(b, w, scalars_dev, st));
     memcpy(out_jac, &j, sizeof(j));
 }
-void msm_finish_g1(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st) {
-    G1Jac j = xyzz_to_jac(msm_finish<Fp>(b, s, st));
+void msm_finish_g1(gg_msm_base* b, MsmSort* s, MsmScratch* scr, void* out_jac, hipStream_t st) {
+    G1Jac j = xyzz_to_jac(msm_finish<Fp>(b, s, scr, st));
     memcpy(out_jac, &j, sizeof(j));
 }
 }  // namespace gg

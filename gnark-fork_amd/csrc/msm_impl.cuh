@@ -54,11 +54,7 @@ __device__ __forceinline__ void st(T* p, const T& v) {
 __global__ void k_scan_block(const uint32_t* in, uint32_t* out, uint32_t* sums, size_t n);
 __global__ void k_scan_add(uint32_t* out, const uint32_t* sums, size_t n);
 __global__ void k_set_total(uint32_t* out, const uint32_t* in, size_t n);
-__global__ void k_set_total_max(uint32_t* out, const uint32_t* in, size_t n, const uint32_t* maxcnt);
-__global__ void k_item_counts(const uint32_t* offsets, size_t nb, int K, uint32_t* itemcnt,
-                              uint32_t* maxcnt);
-__global__ void k_item_buckets(const uint32_t* item_off, size_t nb, const uint32_t* n_items_dev,
-                               uint32_t* item_bucket);
+__global__ void k_bucket_max(const uint32_t* offsets, size_t nb, uint32_t* maxcnt);
 void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, hipStream_t st,
                     std::vector<DevBuf>& tmp, int depth = 0);
 int choose_c(size_t n, size_t point_bytes, int total_bits = 255);
@@ -89,122 +85,87 @@ struct MsmSort;
 void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
 void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
 
-constexpr uint32_t LIGHT = 16;  // buckets with <= LIGHT items: merged inside the accumulation block
-// In-block merge of light buckets' partials inside k_accum_affine: measured
-// slower on MI355X (the end-of-block tree is latency-bound: 2^20 accumulation
-// 1.45 -> 1.70 ms vs 0.11 ms for k_bucket_sum), so it is off for both groups.
-template <class F>
-constexpr bool kMergeInBlock = false;
+constexpr uint32_t LIGHT = 16;  // buckets spanning <= LIGHT ranges are combined serially
 
-// level 1: sum up to K affine points of one bucket into an XYZZ partial, then
-// merge the partials of light buckets inside the block (LDS tree, <= 4 steps):
-// afterwards a light bucket's sum is part[item_off[b]] (+ part[next 256-item
-// block start] if the bucket straddles one).  Heavy buckets keep one partial per
-// item for k_seg_tree.  n_items is read from the device (no host sync).
+// Level 1, balanced: thread t adds the sorted entries [t K, min((t+1) K, E)) --
+// every lane does exactly K mixed XYZZ adds, whatever the bucket sizes (the
+// per-bucket items this replaces were K(m-1)/m..K long, and a wave waited for
+// its longest).  Where the range crosses a bucket boundary the running sum is
+// flushed: the range's first segment goes to head[t], its last to tail[t], and
+// a segment that starts and ends inside the range is a whole bucket, written
+// straight to S[brev(q)] (natural bucket order, see sort_entries).
+// tbucket[t] = bucket (sort order) of the range's first entry.
 template <class F>
-__global__ void __launch_bounds__(256, 2) k_accum_affine(const Affine<F>* pts, const uint32_t* sorted,
-                                                      const uint32_t* offsets,
-                                                      const uint32_t* item_off,
-                                                      const uint32_t* item_bucket,
-                                                      const uint32_t* n_items_dev, int K,
-                                                      int skip_inf, Xyzz<F>* partial) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char acc_lds[];
-    [[maybe_unused]] Xyzz<F>* sh = reinterpret_cast<Xyzz<F>*>(acc_lds);
-    const size_t n_items = *n_items_dev;
+__device__ __forceinline__ void range_store(const Xyzz<F>& acc, bool first, bool last, uint32_t q, int c,
+                                            size_t t, Xyzz<F>* head, Xyzz<F>* tail, Xyzz<F>* S) {
+    if (first) st(head + t, acc);
+    else if (last) st(tail + t, acc);
+    else st(S + (__brev(q) >> (33 - c)), acc);
+}
+
+template <class F>
+__global__ void __launch_bounds__(256, 2) k_accum_range(const Affine<F>* pts, const uint32_t* sorted,
+                                                     const uint32_t* offsets, uint32_t nb, int c,
+                                                     uint32_t K, int skip_inf, Xyzz<F>* head,
+                                                     Xyzz<F>* tail, Xyzz<F>* S, uint32_t* tbucket) {
+    const uint32_t E = offsets[nb];
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if ((size_t)blockIdx.x * blockDim.x >= n_items) return;  // whole block past the end
-    const bool valid = t < n_items;
+    const uint64_t e0w = (uint64_t)t * K;
+    if (e0w >= E) return;
+    const uint32_t e0 = (uint32_t)e0w;
+    const uint32_t e1 = (uint32_t)min<uint64_t>(e0w + K, E);
+    // bucket of e0: the largest q with offsets[q] <= e0 (empty buckets share
+    // their successor's offset, so this is the non-empty one holding e0)
+    uint32_t lo = 0, hi = nb;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (offsets[mid] <= e0) lo = mid;
+        else hi = mid;
+    }
+    uint32_t q = lo;
+    tbucket[t] = q;
+    uint32_t bnd = offsets[q + 1];
+    uint32_t seg0 = e0;
     Xyzz<F> acc = Xyzz<F>::inf();
-    uint32_t io0 = 0, io1 = 0;
-    if (valid) {
-    uint32_t b = item_bucket[t];
-    io0 = item_off[b];
-    io1 = item_off[b + 1];
-    uint32_t j = (uint32_t)t - io0;
-    // bucket b (cnt entries) is cut into m = ceil(cnt / K) near-equal items
-    const uint32_t o = offsets[b], cnt = offsets[b + 1] - o;
-    const uint32_t m = (cnt + (uint32_t)K - 1) / (uint32_t)K;
-    const uint32_t lo = o + (uint32_t)(((uint64_t)j * cnt) / m);
-    const uint32_t hi = o + (uint32_t)(((uint64_t)(j + 1) * cnt) / m);
     if constexpr (sizeof(F) <= 32) {
         // G1: software pipeline, the next point is in flight while this one is added
-        uint32_t v = 0, vn = 0;
-        Affine<F> p;
-        if (lo < hi) {
-            v = sorted[lo];
-            p = ld(pts + (v & 0x7fffffffu));
-        }
-        if (lo + 1 < hi) vn = sorted[lo + 1];
-        for (uint32_t e = lo; e < hi; e++) {
-            Affine<F> q = p;
+        uint32_t v = sorted[e0], vn = (e0 + 1 < e1) ? sorted[e0 + 1] : 0u;
+        Affine<F> p = ld(pts + (v & 0x7fffffffu));
+        for (uint32_t e = e0; e < e1; e++) {
+            Affine<F> qp = p;
             const uint32_t cv = v;
-            if (e + 1 < hi) {
+            if (e + 1 < e1) {
                 p = ld(pts + (vn & 0x7fffffffu));
                 v = vn;
-                if (e + 2 < hi) vn = sorted[e + 2];
+                if (e + 2 < e1) vn = sorted[e + 2];
             }
-            if (skip_inf && q.is_inf()) continue;  // hole of a wire-indexed table
-            if (cv >> 31) q.y = -q.y;
-            xyzz_madd_inplace(acc, q);
+            if (e == bnd) {  // bucket boundary: flush [seg0, e) of bucket q
+                range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
+                acc = Xyzz<F>::inf();
+                seg0 = e;
+                do { q++; bnd = offsets[q + 1]; } while (bnd == e);
+            }
+            if (skip_inf && qp.is_inf()) continue;  // hole of a wire-indexed table
+            if (cv >> 31) qp.y = -qp.y;
+            xyzz_madd_inplace(acc, qp);
         }
     } else {
-        // G2: no room for a second point in registers (235 VGPRs at occupancy 2)
-        for (uint32_t e = lo; e < hi; e++) {
-            uint32_t v = sorted[e];
+        // G2: no room for a second point in registers
+        for (uint32_t e = e0; e < e1; e++) {
+            if (e == bnd) {
+                range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
+                acc = Xyzz<F>::inf();
+                seg0 = e;
+                do { q++; bnd = offsets[q + 1]; } while (bnd == e);
+            }
+            const uint32_t v = sorted[e];
             Affine<F> p = ld(pts + (v & 0x7fffffffu));
             if (skip_inf && p.is_inf()) continue;
             if (v >> 31) p.y = -p.y;
             xyzz_madd_inplace(acc, p);
         }
     }
-    }  // valid
-    // in-block segmented tree over the light buckets' partials (G1 only: the G2
-    // XYZZ add does not fit the 256-VGPR budget of this kernel; G2 light
-    // buckets are summed by k_bucket_sum instead)
-    if constexpr (!kMergeInBlock<F>) {
-        if (valid) st(partial + t, acc);
-        return;
-    }
-    const bool light = valid && (io1 - io0) <= LIGHT;
-    const size_t blk0 = (size_t)blockIdx.x * blockDim.x;
-    const size_t seg_lo = light ? std::max<size_t>(io0, blk0) : t;
-    const size_t seg_hi = light ? std::min<size_t>(std::min<size_t>(io1, blk0 + blockDim.x), n_items) : t;
-    const uint32_t rel = (uint32_t)(t - seg_lo);
-    sh[threadIdx.x] = acc;
-    for (uint32_t s2 = 1; s2 < LIGHT; s2 <<= 1) {
-        const bool act = light && (rel % (2 * s2)) == 0 && t + s2 < seg_hi;
-        if (!__syncthreads_or(act)) break;
-        if (act) {
-            Xyzz<F> o2 = sh[threadIdx.x + s2];
-            xyzz_add_inplace(acc, o2);
-            sh[threadIdx.x] = acc;
-        }
-    }
-    if (valid) st(partial + t, acc);
-}
-
-// In-place segmented tree over the level-1 partials: bucket b owns slots
-// [item_off[b], item_off[b+1]); after the launches with stride 1, 2, 4, ...
-// slot item_off[b] holds the bucket sum.  One quad per slot (xyzz_add_quad), no
-// host syncs.
-template <class F>
-__global__ void __launch_bounds__(256) k_seg_tree(Xyzz<F>* part, const uint32_t* item_off,
-                                                  const uint32_t* item_bucket, size_t T,
-                                                  uint32_t stride, uint32_t fan) {
-    const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t lane = (uint32_t)g & 3;
-    const size_t p = g >> 2;
-    if (p >= T) return;  // every branch below is uniform over the quad
-    uint32_t b = item_bucket[p];
-    uint32_t o = item_off[b];
-    uint32_t j = (uint32_t)p - o;
-    uint32_t cnt = item_off[b + 1] - o;
-    if (cnt <= LIGHT) return;  // done by k_bucket_sum
-    if (j % (fan * stride)) return;
-    if (j + stride >= cnt) return;
-    Xyzz<F> acc = ld(part + p);
-    for (uint32_t k = 1; k < fan && j + k * stride < cnt; k++) xyzz_add_quad(acc, ld(part + p + k * stride), lane);
-    if (lane == 0) st(part + p, acc);
+    range_store(acc, seg0 == e0, true, q, c, t, head, tail, S);
 }
 
 // ---- quad-cooperative XYZZ add (latency-bound tree levels) -----------------
@@ -284,48 +245,74 @@ __device__ __forceinline__ T shfl_xor_words(const T& v, int mask) {
     return r;
 }
 
-// Level 2 for light buckets (2..LIGHT partials): QB quads per bucket.  Quad j
-// adds partials j, j + QB, ... of its bucket with quad adds, then log2(QB)
-// xor-shuffle rounds (lane masks 4, 8, ...) combine the quads.  Every lane
-// takes part in the shuffles; only the adds are predicated.
-template <class F, uint32_t QB>
-__global__ void __launch_bounds__(256) k_bucket_sum(Xyzz<F>* part, const uint32_t* item_off, size_t nb) {
-    static_assert(QB == 1 || QB == 2 || QB == 4, "quads per bucket");
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t b = t / (4 * QB);
-    const uint32_t k = (uint32_t)t & 3, j = (uint32_t)(t >> 2) & (QB - 1);
-    uint32_t o = 0, cnt = 0;
-    if (b < nb) {
-        o = item_off[b];
-        cnt = item_off[b + 1] - o;
-    }
-    const bool act = cnt >= 2 && cnt <= LIGHT;
-    Xyzz<F> acc = Xyzz<F>::inf();
-    if (act)
-        for (uint32_t i = j; i < cnt; i += QB) xyzz_add_quad(acc, ld(part + o + i), k);
-    for (int s = 4; s < (int)(4 * QB); s <<= 1) {
-        const Xyzz<F> other = shfl_xor_words(acc, s);
-        if (act) xyzz_add_quad(acc, other, k);
-    }
-    if (act && j == 0 && k == 0) st(part + o, acc);
+// Ranges [t0, t1] covering bucket q (sort order) of the balanced accumulation:
+// the bucket's sum is X(t0) + head[t0+1] + ... + head[t1], where X(t0) is
+// head[t0] if the bucket starts at t0's first entry, else tail[t0].
+struct BucketSpan {
+    uint32_t t0, t1;
+    bool empty, first, direct;  // direct: a whole bucket inside one range, already in S
+};
+__device__ __forceinline__ BucketSpan bucket_span(const uint32_t* offsets, uint32_t q, uint32_t E, uint32_t K) {
+    BucketSpan s{};
+    const uint32_t o0 = offsets[q], o1 = offsets[q + 1];
+    s.empty = o0 == o1;
+    if (s.empty) return s;
+    s.t0 = o0 / K;
+    s.t1 = (o1 - 1) / K;
+    s.first = o0 == s.t0 * K;
+    const uint32_t end1 = (uint32_t)min<uint64_t>((uint64_t)(s.t1 + 1) * K, E);
+    s.direct = s.t0 == s.t1 && !s.first && o1 != end1;
+    return s;
 }
 
-// ------------------------------------------------------------ reduction v2
-// Dense bucket sums: S[b] = partial of bucket b (or infinity)
-// (item_off is indexed in sort order pi(b) = bitrev_{c-1}(b), see sort_entries)
+// Heavy buckets (> LIGHT ranges, e.g. the digit-1 bucket of a 0/1-heavy
+// witness): in-place segmented tree over head[t0+1 .. t1], one quad per slot;
+// after the launches with stride 1, fan, fan^2, ... head[t0+1] holds the sum.
 template <class F>
-__global__ void k_gather_buckets(const Xyzz<F>* partial, const uint32_t* item_off, size_t nb, int c,
-                                 Xyzz<F>* S) {
-    size_t b = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
-    uint32_t q = __brev((uint32_t)b) >> (33 - c);
-    uint32_t o = item_off[q], e = item_off[q + 1];
-    Xyzz<F> v = (e > o) ? ld(partial + o) : Xyzz<F>::inf();
-    if (kMergeInBlock<F> && e - o > 1 && e - o <= LIGHT) {  // second in-block head
-        uint32_t k = ((o >> 8) + 1) << 8;
-        if (k < e) xyzz_add_inplace(v, ld(partial + k));
+__global__ void __launch_bounds__(256) k_range_tree(Xyzz<F>* head, const uint32_t* tbucket,
+                                                    const uint32_t* offsets, uint32_t nb, uint32_t K,
+                                                    uint32_t stride, uint32_t fan) {
+    const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = (uint32_t)g & 3;
+    const size_t p = g >> 2;
+    const uint32_t E = offsets[nb];
+    if ((uint64_t)p * K >= E) return;  // every branch below is uniform over the quad
+    const uint32_t q = tbucket[p];
+    const BucketSpan s = bucket_span(offsets, q, E, K);
+    const uint32_t m = s.t1 - s.t0;  // ranges after t0
+    if (m <= LIGHT || p <= s.t0) return;
+    const uint32_t j = (uint32_t)p - (s.t0 + 1);
+    if (j % (fan * stride)) return;
+    if (j + stride >= m) return;
+    Xyzz<F> acc = ld(head + p);
+    for (uint32_t k = 1; k < fan && j + k * stride < m; k++) xyzz_add_quad(acc, ld(head + p + k * stride), lane);
+    if (lane == 0) st(head + p, acc);
+}
+
+// Level 2: one quad per bucket combines its ranges' partials into S in natural
+// bucket order b = brev(q) (the sort order is pi(b) = bitrev_{c-1}(b)).
+template <class F>
+__global__ void __launch_bounds__(256) k_bucket_combine(const Xyzz<F>* head, const Xyzz<F>* tail,
+                                                        const uint32_t* offsets, uint32_t nb, int c,
+                                                        uint32_t K, Xyzz<F>* S) {
+    const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = (uint32_t)g & 3;
+    const size_t q = g >> 2;
+    if (q >= nb) return;
+    const uint32_t E = offsets[nb];
+    const BucketSpan s = bucket_span(offsets, (uint32_t)q, E, K);
+    Xyzz<F>* out = S + (__brev((uint32_t)q) >> (33 - c));
+    if (s.empty) {
+        if (lane == 0) st(out, Xyzz<F>::inf());
+        return;
     }
-    st(S + b, v);
+    if (s.direct) return;
+    Xyzz<F> acc = ld((s.first ? head : tail) + s.t0);
+    const uint32_t m = s.t1 - s.t0;
+    if (m > LIGHT) xyzz_add_quad(acc, ld(head + s.t0 + 1), lane);  // tree result
+    else
+        for (uint32_t t = s.t0 + 1; t <= s.t1; t++) xyzz_add_quad(acc, ld(head + t), lane);
+    if (lane == 0) st(out, acc);
 }
 
 // copy a list of small device arrays into one contiguous staging buffer
@@ -458,19 +445,19 @@ __global__ void __launch_bounds__(256) k_pre_normalize(const Xyzz<F>* cur, size_
 
 using gg::DevBuf;
 namespace gg {
-// Sorted entries + work items of one scalar vector over a base shape (n, c, W,
-// scalar index map).  Bases with identical shapes can share one: the Groth16
-// prover sorts the wires once for A/K and once for B1/G2.
+// Sorted entries of one scalar vector over a base shape (n, c, W, scalar index
+// map).  Bases with identical shapes can share one: the Groth16 prover sorts
+// the wires once for A/K and once for B1/G2.
 struct MsmSort {
-    DevBuf sorted, counts, offsets, itemcnt, item_off, item_bucket, maxcnt;
+    DevBuf sorted, counts, offsets, maxcnt;
     DevBuf keys, tmp_entry, tmp_key, hist, hoff, bin_start, seg2, chunk_start, chunk_hist, chunk_pos,
         chunk_desc;
     std::vector<DevBuf> scan_tmp;
-    uint32_t* pin = nullptr;          // pinned (n_items, max_items) read-back
+    uint32_t* pin = nullptr;          // pinned read-back: [0] = entries of the fullest bucket
     hipEvent_t pin_ev = nullptr;      // after the read-back copy
-    hipEvent_t ready_ev = nullptr;    // after the item -> bucket map
-    int K1 = 32;
-    size_t items_ub = 0;
+    hipEvent_t ready_ev = nullptr;    // after the sort
+    uint32_t K = 32;                  // entries per accumulation range
+    size_t ranges_ub = 0;             // upper bound of ceil(entries / K)
     void ensure_events() {
         if (!pin) GG_HIP(hipHostMalloc((void**)&pin, 16, hipHostMallocDefault));
         if (!pin_ev) GG_HIP(hipEventCreateWithFlags(&pin_ev, hipEventDisableTiming));
@@ -484,6 +471,17 @@ struct MsmSort {
         if (pin_ev) (void)hipEventDestroy(pin_ev);
         if (ready_ev) (void)hipEventDestroy(ready_ev);
     }
+};
+// Accumulation / reduction scratch of one MSM in flight: range partials
+// (head, tail), range -> bucket map, dense bucket sums S, reduction arena.
+struct MsmScratch {
+    DevBuf head, tail, tbucket, S, arena, scal;
+};
+// Everything one MSM needs besides the (read-only) base: several MSMs over one
+// base run concurrently on different streams with one MsmWork each.
+struct MsmWork {
+    MsmSort sort;
+    MsmScratch scr;
 };
 }  // namespace gg
 
@@ -500,8 +498,7 @@ struct gg_msm_base {
     int scurve = 0;        // scalar field: 0 = BN254 fr, 1 = BLS12-381 fr
     uint32_t max_sidx = 0;
     std::mutex mu;
-    gg::MsmSort own;                  // this base's sort state
-    DevBuf partA, segs, segs2, scal;  // per-base accumulation / reduction scratch
+    gg::MsmWork own;  // this base's sort + scratch (gg_msm, the Groth16 prover)
 };
 
 namespace gg {
@@ -536,18 +533,12 @@ inline void precompute(gg_msm_base* b, const Affine<F>* dev_in, hipStream_t st) 
 // tree sums that run wide on the GPU.  Pieces of <= 16 elements finish on the
 // host, combined by Horner over their 2^mlog factors.
 template <class F>
-inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* partials, const uint32_t* item_off,
-                                hipStream_t st) {
+inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* S, MsmScratch* scr, hipStream_t st) {
     const size_t nb = b->nb;
     const size_t XB = sizeof(Xyzz<F>);
-    b->segs.reserve(nb * XB);
     const size_t arena_elems = 3 * nb + 1024;
-    b->segs2.reserve(arena_elems * XB);
-    Xyzz<F>* S = b->segs.as<Xyzz<F>>();
-    hipLaunchKernelGGL(k_gather_buckets<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, partials,
-                       item_off, nb, b->c, S);
-    GG_HIP(hipGetLastError());
-    Xyzz<F>* arena = b->segs2.as<Xyzz<F>>();
+    scr->arena.reserve(arena_elems * XB);
+    Xyzz<F>* arena = scr->arena.as<Xyzz<F>>();
     size_t used = 0;
     auto alloc = [&](size_t cnt) {
         GG_CHECK(used + cnt <= arena_elems, GG_ERR_INTERNAL, "bucket reduction arena overflow");
@@ -683,65 +674,62 @@ inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* partials, const u
 }
 
 // Accumulation + reduction of base b over a prepared sort s (its own or one
-// shared with a base of identical shape).  Waits (device side) for s->ready_ev.
+// shared with a base of identical shape), scratch scr.  Waits (device side) for
+// s->ready_ev.
 template <class F>
-inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, hipStream_t st) {
+inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream_t st) {
     const size_t n = b->n, nb = b->nb;
     if (n == 0) return Xyzz<F>::inf();
     GG_HIP(hipStreamWaitEvent(st, s->ready_ev, 0));
     const uint32_t* offs = s->offsets.as<uint32_t>();
-    const uint32_t* ioff = s->item_off.as<uint32_t>();
-    const size_t items_ub = s->items_ub;
-    b->partA.reserve((items_ub + 1) * sizeof(Xyzz<F>));
+    const size_t T = s->ranges_ub;
+    const uint32_t K = s->K;
+    scr->head.reserve((T + 1) * sizeof(Xyzz<F>));
+    scr->tail.reserve((T + 1) * sizeof(Xyzz<F>));
+    scr->tbucket.reserve((T + 1) * 4);
+    scr->S.reserve(nb * sizeof(Xyzz<F>));
+    Xyzz<F>* head = scr->head.as<Xyzz<F>>();
+    Xyzz<F>* S = scr->S.as<Xyzz<F>>();
     {
         // per-group names: the Groth16 prove runs G1 and G2 accumulations at once
         const char* acc_name = sizeof(F) == sizeof(Fp) ? "msm_accum" : (sizeof(F) == sizeof(Fp2) ? "msm_accum_g2" : "msm_accum_bls");
         ProfScope ps_acc(acc_name, st, (double)n);
-        hipLaunchKernelGGL(k_accum_affine<F>, dim3(grid_for(items_ub, 256)), dim3(256),
-                           kMergeInBlock<F> ? 256 * sizeof(Xyzz<F>) : 0, st, (const Affine<F>*)b->pts.p,
-                           s->sorted.as<uint32_t>(), offs, ioff, s->item_bucket.as<uint32_t>(),
-                           ioff + nb, s->K1, (int)b->has_inf, b->partA.as<Xyzz<F>>());
+        hipLaunchKernelGGL(k_accum_range<F>, dim3(grid_for(T, 256)), dim3(256), 0, st, (const Affine<F>*)b->pts.p,
+                           s->sorted.as<uint32_t>(), offs, (uint32_t)nb, b->c, K, (int)b->has_inf, head,
+                           scr->tail.as<Xyzz<F>>(), S, scr->tbucket.as<uint32_t>());
         GG_HIP(hipGetLastError());
         ps_acc.stop(st);
     }
     GG_HIP(hipEventSynchronize(s->pin_ev));
-    const size_t n_items = s->pin[0];
-    const uint32_t max_items = s->pin[1];
-    GG_CHECK(n_items <= items_ub, GG_ERR_INTERNAL, "item count above its bound");
-    // ---- level 2: light buckets summed by a thread each, heavy buckets (> LIGHT
-    // items) by a per-bucket tree (skew-robust: log2(items) launches)
+    const uint32_t maxcnt = s->pin[0];
+    // ranges after the first one of the fullest bucket (upper bound)
+    const uint32_t max_ranges = maxcnt / K + 1;
+    // ---- level 2: heavy buckets' ranges by a segmented tree (skew-robust,
+    // log_fan(ranges) launches), then every bucket's partials into S
     ProfScope ps_acc2("msm_accum2", st, (double)n);
-    if (!kMergeInBlock<F> && max_items > 1) {
-        // quads per bucket (MI355X sweep: one quad per bucket at 2^20; more
-        // lanes make the level throughput-bound)
-        static const int l2qb = getenv("GG_L2_QB") ? atoi(getenv("GG_L2_QB")) : 1;
-        Xyzz<F>* pa = b->partA.as<Xyzz<F>>();
-        if (l2qb >= 4) hipLaunchKernelGGL((k_bucket_sum<F, 4>), dim3(grid_for(16 * nb, 256)), dim3(256), 0, st, pa, ioff, nb);
-        else if (l2qb == 2) hipLaunchKernelGGL((k_bucket_sum<F, 2>), dim3(grid_for(8 * nb, 256)), dim3(256), 0, st, pa, ioff, nb);
-        else hipLaunchKernelGGL((k_bucket_sum<F, 1>), dim3(grid_for(4 * nb, 256)), dim3(256), 0, st, pa, ioff, nb);
-        GG_HIP(hipGetLastError());
-    }
-    for (uint32_t stride = 1; max_items > LIGHT && stride < max_items;) {
-        uint32_t fan = (stride == 1) ? 4u : 2u;
-        hipLaunchKernelGGL(k_seg_tree<F>, dim3(grid_for(4 * n_items, 256)), dim3(256), 0, st,
-                           b->partA.as<Xyzz<F>>(), ioff, s->item_bucket.as<uint32_t>(), n_items, stride,
-                           fan);
+    for (uint32_t stride = 1; max_ranges > LIGHT && stride < max_ranges;) {
+        const uint32_t fan = (stride == 1) ? 4u : 2u;
+        hipLaunchKernelGGL(k_range_tree<F>, dim3(grid_for(4 * T, 256)), dim3(256), 0, st, head,
+                           (const uint32_t*)scr->tbucket.p, offs, (uint32_t)nb, K, stride, fan);
         GG_HIP(hipGetLastError());
         stride *= fan;
     }
+    hipLaunchKernelGGL(k_bucket_combine<F>, dim3(grid_for(4 * nb, 256)), dim3(256), 0, st, (const Xyzz<F>*)head,
+                       (const Xyzz<F>*)scr->tail.p, offs, (uint32_t)nb, b->c, K, S);
+    GG_HIP(hipGetLastError());
     ps_acc2.stop(st);
     // ---- bucket reduction: sum_b (b+1) S_b
     ProfScope ps_red("msm_reduce", st, (double)nb);
-    Xyzz<F> res = bucket_reduce_2d<F>(b, (const Xyzz<F>*)b->partA.p, ioff, st);
+    Xyzz<F> res = bucket_reduce_2d<F>(b, (const Xyzz<F>*)S, scr, st);
     ps_red.stop(st);
     return res;
 }
 
 template <class F>
-inline Xyzz<F> msm_run(gg_msm_base* b, const Fr* scalars_dev, hipStream_t st) {
+inline Xyzz<F> msm_run(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, hipStream_t st) {
     if (b->n == 0) return Xyzz<F>::inf();
-    msm_prepare(b, &b->own, scalars_dev, st);
-    return msm_finish<F>(b, &b->own, st);
+    msm_prepare(b, &w->sort, scalars_dev, st);
+    return msm_finish<F>(b, &w->sort, &w->scr, st);
 }
 
 template <class F>

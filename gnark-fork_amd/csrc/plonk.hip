@@ -10,13 +10,11 @@
 //                             out) -- divideByXMinusOne, prove.go:1223-1276
 //   gg_bls12_381_fr_batch_invert
 //                             fr.BatchInvert (prove.go:1273): zeros stay zero
-#include "common.h"
-#include "field.cuh"
+#include "plonk_ops.h"
 #include "prof.h"
 #include <vector>
 #include <cstring>
 
-struct gg_domain;
 namespace gg {
 void bls_ntt_inplace(gg_domain* d, void* data, int inverse, int dit, int coset, hipStream_t st);
 size_t domain_size(gg_domain* d, int* curve);
@@ -24,8 +22,7 @@ void bls_xn_minus_one_inv(gg_domain* big, size_t n_small, void* out);
 }  // namespace gg
 
 namespace gg {
-
-using FrB = FrBls;
+namespace plk {
 
 __device__ __forceinline__ FrB ldf(const FrB* p) {
     const uint4* q = reinterpret_cast<const uint4*>(p);
@@ -40,23 +37,6 @@ __device__ __forceinline__ void stf(FrB* p, const FrB& r) {
     q[0] = make_uint4(r.v[0], r.v[1], r.v[2], r.v[3]);
     q[1] = make_uint4(r.v[4], r.v[5], r.v[6], r.v[7]);
 }
-
-// polynomial order ids of prove.go:60-77 (s.x) and blinding ids :80-86
-enum { ID_L, ID_R, ID_O, ID_Z, ID_ZS, ID_QL, ID_QR, ID_QM, ID_QO, ID_QK, ID_S1, ID_S2, ID_S3,
-       ID_ID, ID_LONE, ID_QCI };
-constexpr int MAX_X = ID_QCI + 2 * 8;  // up to 8 BSB22 commitments
-constexpr int MAX_BCOEF = 4;
-
-struct NumParams {
-    const FrB* x[MAX_X];        // Lagrange-regular evaluations on this coset, length n
-    int nx;
-    FrB bcoef[4][MAX_BCOEF];    // blinding polynomials Bl, Br, Bo, Bz (coset-scaled)
-    int bdeg[4];                // number of coefficients
-    const FrB* tw0;             // s.twiddles0: omega_small^j, j < n
-    FrB beta, gamma, alpha, cs, css;
-    uint32_t n, log_big, rho, coset;
-    FrB* cres;                  // rho * n, bit-reversed big-domain order
-};
 
 __device__ __forceinline__ FrB horner(const FrB* c, int nc, const FrB& x) {
     FrB r = FrB::zero();
@@ -100,11 +80,14 @@ __global__ void __launch_bounds__(256) k_numerator_coset(NumParams P) {
     stf(P.cres + (P.log_big ? pos : 0), res);
 }
 
-__global__ void k_mul_periodic_bitrev(FrB* r, size_t n, int log_n, const FrB* f, uint32_t rho) {
+struct PeriodicTab {
+    FrB f[8];
+};
+__global__ void k_mul_periodic_bitrev(FrB* r, size_t n, int log_n, PeriodicTab t, uint32_t rho) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t irev = log_n ? (__brev((uint32_t)i) >> (32 - log_n)) : 0u;
-    stf(r + i, ldf(r + i) * ldf(f + (irev % rho)));
+    stf(r + i, ldf(r + i) * t.f[irev % rho]);
 }
 
 // Montgomery batch inversion: thread t owns elements t, t+T, ... (zeros skipped)
@@ -130,19 +113,53 @@ __global__ void __launch_bounds__(256) k_batch_invert(FrB* a, size_t n, size_t T
     }
 }
 
-// fr.BatchInvert on device memory (synchronous: the prefix scratch is freed on return)
-void bls_batch_invert(FrB* a, size_t n, hipStream_t st) {
+size_t batch_invert_arena_bytes(size_t n) { return ((n * 32 + 255) & ~(size_t)255) + 256; }
+
+// fr.BatchInvert on device memory (zeros stay zero)
+void batch_invert(FrB* a, size_t n, hipStream_t st, Arena& ar) {
     if (n == 0) return;
     const size_t T = std::min<size_t>(n, std::max<size_t>(16384, n / 64));
-    DevBuf prefix(n * 32);
-    hipLaunchKernelGGL(k_batch_invert, dim3(grid_for(T, 256)), dim3(256), 0, st, a, n, T, prefix.as<FrB>());
+    FrB* prefix = ar.get<FrB>(n);
+    hipLaunchKernelGGL(k_batch_invert, dim3(grid_for(T, 256)), dim3(256), 0, st, a, n, T, prefix);
     GG_HIP(hipGetLastError());
-    GG_HIP(hipStreamSynchronize(st));
 }
 
+void numerator(const NumParams& P, hipStream_t st) {
+    ProfScope prof("plonk_numerator", st, (double)P.n);
+    hipLaunchKernelGGL(k_numerator_coset, dim3(grid_for(P.n, 256)), dim3(256), 0, st, P);
+    GG_HIP(hipGetLastError());
+    prof.stop(st);
+}
+
+void divide_by_xn_minus_one(gg_domain* big, size_t n_small, FrB* data, hipStream_t st) {
+    int curve = -1;
+    const size_t m = domain_size(big, &curve);
+    GG_CHECK(curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "needs a BLS12-381 domain");
+    GG_CHECK(n_small >= 1 && m % n_small == 0, GG_ERR_INVALID_ARG, "big domain must be a multiple of n");
+    const uint32_t rho = (uint32_t)(m / n_small);
+    GG_CHECK(rho <= 8, GG_ERR_INVALID_ARG, "|big domain| / n > 8");
+    // (x^n - 1)^-1 on the big coset has rho distinct values (prove.go:1253-1276)
+    PeriodicTab t{};
+    bls_xn_minus_one_inv(big, n_small, t.f);
+    int lm = 0;
+    while (((size_t)1 << lm) < m) lm++;
+    hipLaunchKernelGGL(k_mul_periodic_bitrev, dim3(grid_for(m, 256)), dim3(256), 0, st, data, m, lm, t, rho);
+    GG_HIP(hipGetLastError());
+    // LagrangeCoset/BitReverse -> Canonical/Regular: FFTInverse(DIT, OnCoset)
+    bls_ntt_inplace(big, data, 1, 1, 1, st);
+}
+
+void ntt(gg_domain* d, void* data, int inverse, int dit, int coset, hipStream_t st) {
+    bls_ntt_inplace(d, data, inverse, dit, coset, st);
+}
+
+}  // namespace plk
 }  // namespace gg
 
 using namespace gg;
+
+using plk::FrB;
+using plk::NumParams;
 
 extern "C" int gg_plonk_numerator_coset(const void* const* x_dev, int nx, const void* bcoef,
                                         const int* bdeg, const void* twiddles0_dev,
@@ -152,7 +169,7 @@ extern "C" int gg_plonk_numerator_coset(const void* const* x_dev, int nx, const 
     GG_CAPI_BEGIN
     GG_CHECK(x_dev && bcoef && bdeg && twiddles0_dev && beta && gamma && alpha && coset_gen && cres_dev,
              GG_ERR_INVALID_ARG, "null argument");
-    GG_CHECK(nx >= ID_QCI && nx <= MAX_X && (nx - ID_QCI) % 2 == 0, GG_ERR_INVALID_ARG,
+    GG_CHECK(nx >= plk::ID_QCI && nx <= plk::MAX_X && (nx - plk::ID_QCI) % 2 == 0, GG_ERR_INVALID_ARG,
              "nx must be 15 + 2 * (number of BSB22 commitments), <= 8 commitments");
     GG_CHECK(n >= 1 && (n & (n - 1)) == 0 && n <= (1u << 30), GG_ERR_INVALID_ARG, "n must be a power of 2");
     GG_CHECK(rho >= 1 && (rho & (rho - 1)) == 0 && coset >= 0 && coset < rho, GG_ERR_INVALID_ARG, "bad rho/coset");
@@ -164,9 +181,9 @@ extern "C" int gg_plonk_numerator_coset(const void* const* x_dev, int nx, const 
     P.nx = nx;
     const uint8_t* bc = (const uint8_t*)bcoef;
     for (int q = 0; q < 4; q++) {
-        GG_CHECK(bdeg[q] >= 0 && bdeg[q] <= MAX_BCOEF, GG_ERR_INVALID_ARG, "blinding order too large");
+        GG_CHECK(bdeg[q] >= 0 && bdeg[q] <= plk::MAX_BCOEF, GG_ERR_INVALID_ARG, "blinding order too large");
         P.bdeg[q] = bdeg[q];
-        for (int k = 0; k < bdeg[q]; k++) memcpy(P.bcoef[q][k].v, bc + (q * MAX_BCOEF + k) * 32, 32);
+        for (int k = 0; k < bdeg[q]; k++) memcpy(P.bcoef[q][k].v, bc + (q * plk::MAX_BCOEF + k) * 32, 32);
     }
     P.tw0 = (const FrB*)twiddles0_dev;
     memcpy(P.beta.v, beta, 32);
@@ -182,10 +199,7 @@ extern "C" int gg_plonk_numerator_coset(const void* const* x_dev, int nx, const 
     P.log_big = (uint32_t)lb;
     P.cres = (FrB*)cres_dev;
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : hipStreamPerThread;
-    ProfScope prof("plonk_numerator", st, (double)n);
-    hipLaunchKernelGGL(k_numerator_coset, dim3(grid_for(n, 256)), dim3(256), 0, st, P);
-    GG_HIP(hipGetLastError());
-    prof.stop(st);
+    plk::numerator(P, st);
     GG_CAPI_END
 }
 
@@ -193,25 +207,9 @@ extern "C" int gg_plonk_divide_by_xn_minus_one(gg_domain_t big, size_t n_small, 
                                                void* hip_stream) {
     GG_CAPI_BEGIN
     GG_CHECK(big && data_dev, GG_ERR_INVALID_ARG, "null argument");
-    int curve = -1;
-    const size_t m = domain_size(big, &curve);
-    GG_CHECK(curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "needs a BLS12-381 domain");
-    GG_CHECK(n_small >= 1 && m % n_small == 0, GG_ERR_INVALID_ARG, "big domain must be a multiple of n");
-    const uint32_t rho = (uint32_t)(m / n_small);
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : hipStreamPerThread;
-    // (x^n - 1)^-1 on the big coset has rho distinct values (prove.go:1253-1276)
-    std::vector<FrB> f(rho);
-    bls_xn_minus_one_inv(big, n_small, f.data());
-    DevBuf df(rho * 32);
-    GG_HIP(hipMemcpyAsync(df.p, f.data(), rho * 32, hipMemcpyHostToDevice, st));
-    int lm = 0;
-    while (((size_t)1 << lm) < m) lm++;
-    hipLaunchKernelGGL(k_mul_periodic_bitrev, dim3(grid_for(m, 256)), dim3(256), 0, st, (FrB*)data_dev, m,
-                       lm, df.as<FrB>(), rho);
-    GG_HIP(hipGetLastError());
-    // LagrangeCoset/BitReverse -> Canonical/Regular: FFTInverse(DIT, OnCoset)
-    bls_ntt_inplace(big, data_dev, 1, 1, 1, st);
-    GG_HIP(hipStreamSynchronize(st));  // df lifetime
+    plk::divide_by_xn_minus_one(big, n_small, (FrB*)data_dev, st);
+    GG_HIP(hipStreamSynchronize(st));
     GG_CAPI_END
 }
 
@@ -220,6 +218,9 @@ extern "C" int gg_bls12_381_fr_batch_invert(void* data_dev, size_t n, void* hip_
     GG_CHECK(data_dev || n == 0, GG_ERR_INVALID_ARG, "null argument");
     if (n == 0) return GG_OK;
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : hipStreamPerThread;
-    bls_batch_invert((FrB*)data_dev, n, st);
+    Arena ar;
+    ar.reserve(plk::batch_invert_arena_bytes(n));
+    plk::batch_invert((FrB*)data_dev, n, st, ar);
+    GG_HIP(hipStreamSynchronize(st));
     GG_CAPI_END
 }

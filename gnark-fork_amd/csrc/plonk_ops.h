@@ -1,0 +1,74 @@
+// Asynchronous PlonK BLS12-381 device operations (bls12-381 fr, 32 B
+// Montgomery), shared by the C-ABI wrappers of plonk.hip / plonk_poly.hip and
+// the prover orchestration of plonk_prover.hip.  Nothing here allocates or
+// synchronises: scratch comes from the caller's Arena, work is enqueued on `st`.
+#pragma once
+#include "common.h"
+#include "field.cuh"
+
+struct gg_domain;
+
+namespace gg {
+namespace plk {
+
+using FrB = FrBls;
+constexpr int MAX_CMT = 8;  // BSB22 commitments per circuit
+constexpr int MAX_BCOEF = 4;
+
+// polynomial order ids of prove.go:60-77 (s.x)
+enum { ID_L, ID_R, ID_O, ID_Z, ID_ZS, ID_QL, ID_QR, ID_QM, ID_QO, ID_QK, ID_S1, ID_S2, ID_S3, ID_ID,
+       ID_LONE, ID_QCI };
+constexpr int MAX_X = ID_QCI + 2 * MAX_CMT;
+
+// ---- plonk_poly.hip
+size_t scan_arena_bytes(size_t m);
+// in place inclusive running product
+void scan_prod(FrB* x, size_t m, hipStream_t st, Arena& ar);
+size_t horner_arena_bytes(size_t n);
+// value_dev[0] = f(a) (Polynomial.Evaluate); q (nullable, n - 1 fr) = (f - f(a)) / (X - a)
+void horner(const FrB* f, size_t n, const FrB& a, FrB* q, FrB* value_dev, hipStream_t st, Arena& ar);
+size_t ratio_arena_bytes(size_t n);
+// iop.BuildRatioCopyConstraint into Lagrange/Regular z (prove.go:600-621)
+void ratio(const FrB* l, const FrB* r, const FrB* o, const int64_t* perm, size_t n, const FrB& beta,
+           const FrB& gamma, const FrB& omega, const FrB& u, FrB* z, hipStream_t st, Arena& ar);
+size_t batch_invert_arena_bytes(size_t n);
+void batch_invert(FrB* a, size_t n, hipStream_t st, Arena& ar);
+void fold_h(const FrB* h, size_t n_small, const FrB& z, FrB* out, hipStream_t st);
+struct LinParams {
+    FrB* z;  // blinded Z canonical, in/out
+    size_t nz;
+    const FrB* s3;
+    size_t ns3;
+    const FrB *ql, *qr, *qm, *qo, *qk;
+    size_t nq;
+    const FrB* pi2[MAX_CMT];
+    FrB qcp[MAX_CMT];
+    int ncmt;
+    FrB s1, s2, alpha, l, r, rl, o, lag;
+};
+void linearized(const LinParams& P, hipStream_t st);
+void bit_reverse(const FrB* in, FrB* out, size_t n, hipStream_t st);
+void axpy(FrB* y, const FrB* x, size_t n, const FrB& a, hipStream_t st);  // y += a x
+void scale(FrB* y, size_t n, const FrB& a, hipStream_t st);               // y *= a
+void shift_copy(const FrB* in, FrB* out, size_t n, hipStream_t st);        // out[i] = in[(i+1) % n]
+
+// ---- plonk.hip
+struct NumParams {
+    const FrB* x[MAX_X];  // Lagrange-regular evaluations on this coset, length n
+    int nx;
+    FrB bcoef[4][MAX_BCOEF];  // blinding polynomials Bl, Br, Bo, Bz (coset-scaled)
+    int bdeg[4];              // number of coefficients
+    const FrB* tw0;           // s.twiddles0: omega_small^j, j < n
+    FrB beta, gamma, alpha, cs, css;
+    uint32_t n, log_big, rho, coset;
+    FrB* cres;  // rho * n, bit-reversed big-domain order
+};
+void numerator(const NumParams& P, hipStream_t st);
+// divideByXMinusOne in place (prove.go:1223-1276), asynchronous
+void divide_by_xn_minus_one(gg_domain* big, size_t n_small, FrB* data, hipStream_t st);
+
+// ---- ntt.hip
+void ntt(gg_domain* d, void* data, int inverse, int dit, int coset, hipStream_t st);
+
+}  // namespace plk
+}  // namespace gg

@@ -15,16 +15,13 @@
 // 8 elements per thread in registers, a Hillis-Steele scan of the 256 thread
 // aggregates in LDS, block aggregates scanned recursively (2048 per level),
 // then one fix-up pass.  Horner runs the affine scan over the reversed vector.
-#include "common.h"
-#include "field.cuh"
+#include "plonk_ops.h"
 #include "prof.h"
 #include <vector>
 #include <cstring>
 
 namespace gg {
-
-using FrB = FrBls;
-void bls_batch_invert(FrB* a, size_t n, hipStream_t st);
+namespace plk {
 
 namespace {
 __device__ __forceinline__ FrB ldb(const FrB* p) {
@@ -127,8 +124,9 @@ __global__ void __launch_bounds__(256) k_scan_fix(FrB* x, size_t m, ScanPow P, c
     }
 }
 
-// host: powers of u for one level (u = 1 for the product scan, unused)
-static void scan_pow_host(const FrB& u, ScanPow& P, std::vector<FrB>& tab) {
+// powers of u for one level (host, small) and the 97-entry u^i / u^(64 j)
+// table of the affine fix-up (device, one thread: no host buffer in flight)
+static void scan_pow_host(const FrB& u, ScanPow& P) {
     P.p[0] = FrB::one();
     for (int k = 1; k <= SCAN_PER; k++) P.p[k] = P.p[k - 1] * u;
     FrB s = P.p[SCAN_PER];
@@ -136,50 +134,54 @@ static void scan_pow_host(const FrB& u, ScanPow& P, std::vector<FrB>& tab) {
         P.step[d] = s;
         s = s * s;
     }
-    tab.resize(64 + 33);
-    tab[0] = FrB::one();
-    for (int i = 1; i < 64; i++) tab[i] = tab[i - 1] * u;
-    FrB u64 = tab[63] * u;
-    tab[64] = FrB::one();
-    for (int j = 1; j < 33; j++) tab[64 + j] = tab[64 + j - 1] * u64;
+}
+__global__ void k_pow_tab(FrB u, FrB* tab) {
+    if (threadIdx.x || blockIdx.x) return;
+    FrB a = FrB::one();
+    for (int i = 0; i < 64; i++) { stb(tab + i, a); a = a * u; }
+    const FrB u64 = a;
+    a = FrB::one();
+    for (int j = 0; j < 33; j++) { stb(tab + 64 + j, a); a = a * u64; }
+}
+
+size_t scan_arena_bytes(size_t m) {
+    size_t b = 0;
+    for (;;) {  // one level per recursion of scan_rec: table + block aggregates
+        const size_t nblk = (m + SCAN_BLK - 1) / SCAN_BLK;
+        b += 256 + ((97 * 32 + 255) & ~(size_t)255) + ((nblk * 32 + 255) & ~(size_t)255);
+        if (nblk <= 1) break;
+        m = nblk;
+    }
+    return b + 512;
 }
 
 // recursive in-place scan of x[0..m); u: multiplier of this level (affine)
 template <int MODE>
-static void scan_rec(FrB* x, size_t m, const FrB& u, hipStream_t st, std::vector<DevBuf>& keep) {
+static void scan_rec(FrB* x, size_t m, const FrB& u, hipStream_t st, Arena& ar) {
     ScanPow P{};
-    std::vector<FrB> tab;
-    scan_pow_host(u, P, tab);
+    scan_pow_host(u, P);
     if (MODE == SCAN_AFFINE) {
-        keep.emplace_back(tab.size() * 32);
-        GG_HIP(hipMemcpyAsync(keep.back().p, tab.data(), tab.size() * 32, hipMemcpyHostToDevice, st));
-        P.lo = keep.back().as<FrB>();
-        P.hi = P.lo + 64;
+        FrB* tab = ar.get<FrB>(97);
+        hipLaunchKernelGGL(k_pow_tab, dim3(1), dim3(64), 0, st, u, tab);
+        GG_HIP(hipGetLastError());
+        P.lo = tab;
+        P.hi = tab + 64;
     }
     const size_t nblk = (m + SCAN_BLK - 1) / SCAN_BLK;
-    FrB* aux = nullptr;
-    if (nblk > 1) {
-        keep.emplace_back(nblk * 32);
-        aux = keep.back().as<FrB>();
-    }
+    FrB* aux = nblk > 1 ? ar.get<FrB>(nblk) : nullptr;
     hipLaunchKernelGGL(k_scan_local<MODE>, dim3((unsigned)nblk), dim3(256), 0, st, x, m, P, aux);
     GG_HIP(hipGetLastError());
     if (nblk <= 1) return;
     // the next level's elements each stand for SCAN_BLK of this level: u^2048
     FrB un = u;
     for (int i = 0; i < 11; i++) un = un * un;
-    scan_rec<MODE>(aux, nblk, un, st, keep);
+    scan_rec<MODE>(aux, nblk, un, st, ar);
     hipLaunchKernelGGL(k_scan_fix<MODE>, dim3((unsigned)(nblk - 1)), dim3(256), 0, st, x, m, P, aux);
     GG_HIP(hipGetLastError());
 }
 
-template <int MODE>
-static void scan_run(FrB* x, size_t m, const FrB& u, hipStream_t st) {
-    if (m == 0) return;
-    std::vector<DevBuf> keep;
-    keep.reserve(16);
-    scan_rec<MODE>(x, m, u, st, keep);
-    GG_HIP(hipStreamSynchronize(st));  // scratch lifetime
+void scan_prod(FrB* x, size_t m, hipStream_t st, Arena& ar) {
+    if (m) scan_rec<SCAN_PROD>(x, m, FrB::one(), st, ar);
 }
 
 __global__ void k_reverse_copy(FrB* dst, const FrB* src, size_t n) {
@@ -245,20 +247,6 @@ __global__ void k_fold_h(const FrB* h, size_t np2, FrB z, FrB* out) {
     stb(out + i, t * z + ldb(h + i));
 }
 
-constexpr int MAX_CMT = 8;
-struct LinParams {
-    FrB* z;  // blinded Z canonical, in/out
-    size_t nz;
-    const FrB* s3;
-    size_t ns3;
-    const FrB *ql, *qr, *qm, *qo, *qk;
-    size_t nq;
-    const FrB* pi2[MAX_CMT];
-    FrB qcp[MAX_CMT];
-    int ncmt;
-    FrB s1, s2, alpha, l, r, rl, o, lag;
-};
-
 // prove.go:1347-1386, term by term
 __global__ void __launch_bounds__(256) k_linearized(LinParams P) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -291,8 +279,127 @@ __global__ void k_axpy(FrB* y, const FrB* x, size_t n, FrB a) {
     if (i < n) stb(y + i, ldb(y + i) + a * ldb(x + i));
 }
 
-static FrB frb(const void* p) {
-    FrB x;
+__global__ void k_scale(FrB* y, size_t n, FrB a) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) stb(y + i, ldb(y + i) * a);
+}
+__global__ void k_shift_copy(const FrB* in, FrB* out, size_t n) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) stb(out + i, ldb(in + (i + 1 == n ? 0 : i + 1)));
+}
+
+size_t horner_arena_bytes(size_t n) { return ((n * 32 + 255) & ~(size_t)255) + scan_arena_bytes(n); }
+
+void horner(const FrB* f, size_t n, const FrB& a, FrB* q, FrB* value_dev, hipStream_t st, Arena& ar) {
+    if (n == 0) {
+        GG_HIP(hipMemsetAsync(value_dev, 0, 32, st));
+        return;
+    }
+    FrB* g = ar.get<FrB>(n);
+    hipLaunchKernelGGL(k_reverse_copy, dim3(grid_for(n, 256)), dim3(256), 0, st, g, f, n);
+    GG_HIP(hipGetLastError());
+    // x_k = y_k + a x_(k-1) over y = reversed f: x_(n-1) = f(a), x_k = sum_(i >= n-1-k) f_i a^(i-(n-1-k))
+    scan_rec<SCAN_AFFINE>(g, n, a, st, ar);
+    if (q && n > 1) {
+        hipLaunchKernelGGL(k_quotient_out, dim3(grid_for(n, 256)), dim3(256), 0, st, q, (const FrB*)g, n);
+        GG_HIP(hipGetLastError());
+    }
+    GG_HIP(hipMemcpyAsync(value_dev, g + n - 1, 32, hipMemcpyDeviceToDevice, st));
+}
+
+// x^e tables for e < n split as hi[e >> S] * lo[e & (2^S - 1)]: thread t
+// computes lo[t] = w^t and hi[t] = w^(t 2^S) by square-and-multiply (no host
+// buffer in flight)
+__global__ void k_pow_split(FrB w, FrB step, FrB* lo, uint32_t nlo, FrB* hi, uint32_t nhi) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    auto pw = [](FrB b, uint32_t e) {
+        FrB r = FrB::one();
+        while (e) {
+            if (e & 1) r = r * b;
+            b = b * b;
+            e >>= 1;
+        }
+        return r;
+    };
+    if (t < nlo) stb(lo + t, pw(w, t));
+    if (t < nhi) stb(hi + t, pw(step, t));
+}
+
+static int log2_ceil(size_t n) {
+    int L = 0;
+    while (((size_t)1 << L) < n) L++;
+    return L;
+}
+
+size_t ratio_arena_bytes(size_t n) {
+    const int L = log2_ceil(n), S = (L + 1) / 2;
+    const size_t tabs = (((size_t)1 << S) + ((size_t)1 << (L - S))) * 32 + 512;
+    return tabs + ((n * 32 + 255) & ~(size_t)255) + batch_invert_arena_bytes(n) + scan_arena_bytes(n) + 1024;
+}
+
+void ratio(const FrB* l, const FrB* r, const FrB* o, const int64_t* perm, size_t n, const FrB& beta,
+           const FrB& gamma, const FrB& w, const FrB& u, FrB* z, hipStream_t st, Arena& ar) {
+    const int L = log2_ceil(n);
+    const int S = (L + 1) / 2;
+    const uint32_t nlo = 1u << S, nhi = 1u << (L - S);
+    FrB* lo = ar.get<FrB>(nlo);
+    FrB* hi = ar.get<FrB>(nhi);
+    FrB step = w;
+    for (int i = 0; i < S; i++) step = step * step;  // w^(2^S)
+    hipLaunchKernelGGL(k_pow_split, dim3(grid_for(std::max(nlo, nhi), 256)), dim3(256), 0, st, w, step, lo, nlo,
+                       hi, nhi);
+    GG_HIP(hipGetLastError());
+    PowSplit ps{hi, lo, S};
+    FrB* den = ar.get<FrB>(n);
+    hipLaunchKernelGGL(k_ratio_numden, dim3(grid_for(n, 256)), dim3(256), 0, st, l, r, o, perm, (uint32_t)n, L,
+                       beta, gamma, u, u * u, ps, z, den);
+    GG_HIP(hipGetLastError());
+    batch_invert(den, n, st, ar);  // t = fr.BatchInvert(t)
+    hipLaunchKernelGGL(k_mul_inplace, dim3(grid_for(n, 256)), dim3(256), 0, st, z, (const FrB*)den, n);
+    GG_HIP(hipGetLastError());
+    scan_prod(z, n, st, ar);  // Z[i] = Z[i-1] * num_i / den_i
+}
+
+void fold_h(const FrB* h, size_t n_small, const FrB& zz, FrB* out, hipStream_t st) {
+    const size_t np2 = n_small + 2;
+    hipLaunchKernelGGL(k_fold_h, dim3(grid_for(np2, 256)), dim3(256), 0, st, h, np2, zz, out);
+    GG_HIP(hipGetLastError());
+}
+
+void linearized(const LinParams& P, hipStream_t st) {
+    hipLaunchKernelGGL(k_linearized, dim3(grid_for(P.nz, 256)), dim3(256), 0, st, P);
+    GG_HIP(hipGetLastError());
+}
+
+void bit_reverse(const FrB* in, FrB* out, size_t n, hipStream_t st) {
+    int L = 0;
+    while (((size_t)1 << L) < n) L++;
+    hipLaunchKernelGGL(k_bit_reverse, dim3(grid_for(n, 256)), dim3(256), 0, st, out, in, n, L);
+    GG_HIP(hipGetLastError());
+}
+
+void axpy(FrB* y, const FrB* x, size_t n, const FrB& a, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_axpy, dim3(grid_for(n, 256)), dim3(256), 0, st, y, x, n, a);
+    GG_HIP(hipGetLastError());
+}
+
+void scale(FrB* y, size_t n, const FrB& a, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_scale, dim3(grid_for(n, 256)), dim3(256), 0, st, y, n, a);
+    GG_HIP(hipGetLastError());
+}
+
+void shift_copy(const FrB* in, FrB* out, size_t n, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_shift_copy, dim3(grid_for(n, 256)), dim3(256), 0, st, in, out, n);
+    GG_HIP(hipGetLastError());
+}
+
+}  // namespace plk
+
+static plk::FrB frb(const void* p) {
+    plk::FrB x;
     memcpy(x.v, p, 32);
     return x;
 }
@@ -301,11 +408,17 @@ static hipStream_t pick(void* s) { return s ? (hipStream_t)s : hipStreamPerThrea
 }  // namespace gg
 
 using namespace gg;
+using plk::FrB;
 
+// ---- C ABI: synchronous wrappers (scratch lives for the call)
 extern "C" int gg_bls12_381_fr_prefix_product(void* data_dev, size_t n, void* hip_stream) {
     GG_CAPI_BEGIN
     GG_CHECK(data_dev || n == 0, GG_ERR_INVALID_ARG, "null argument");
-    scan_run<SCAN_PROD>((FrB*)data_dev, n, FrB::one(), pick(hip_stream));
+    hipStream_t st = pick(hip_stream);
+    Arena ar;
+    ar.reserve(plk::scan_arena_bytes(n));
+    plk::scan_prod((FrB*)data_dev, n, st, ar);
+    GG_HIP(hipStreamSynchronize(st));
     GG_CAPI_END
 }
 
@@ -318,18 +431,11 @@ extern "C" int gg_bls12_381_fr_horner(const void* f_dev, size_t n, const void* a
         return GG_OK;
     }
     hipStream_t st = pick(hip_stream);
-    DevBuf g(n * 32);
-    hipLaunchKernelGGL(k_reverse_copy, dim3(grid_for(n, 256)), dim3(256), 0, st, g.as<FrB>(),
-                       (const FrB*)f_dev, n);
-    GG_HIP(hipGetLastError());
-    // x_k = y_k + a x_(k-1) over y = reversed f: x_(n-1) = f(a), x_k = sum_(i >= n-1-k) f_i a^(i-(n-1-k))
-    scan_run<SCAN_AFFINE>(g.as<FrB>(), n, frb(a_mont), st);
-    if (q_dev && n > 1) {
-        hipLaunchKernelGGL(k_quotient_out, dim3(grid_for(n, 256)), dim3(256), 0, st, (FrB*)q_dev,
-                           g.as<FrB>(), n);
-        GG_HIP(hipGetLastError());
-    }
-    GG_HIP(hipMemcpyAsync(value_out, g.as<FrB>() + n - 1, 32, hipMemcpyDeviceToHost, st));
+    Arena ar;
+    ar.reserve(plk::horner_arena_bytes(n) + 256);
+    FrB* v = ar.get<FrB>(1);
+    plk::horner((const FrB*)f_dev, n, frb(a_mont), (FrB*)q_dev, v, st, ar);
+    GG_HIP(hipMemcpyAsync(value_out, v, 32, hipMemcpyDeviceToHost, st));
     GG_HIP(hipStreamSynchronize(st));
     GG_CAPI_END
 }
@@ -344,33 +450,14 @@ extern "C" int gg_plonk_ratio_copy_constraint(const void* l_dev, const void* r_d
              GG_ERR_INVALID_ARG, "null argument");
     GG_CHECK(n >= 1 && (n & (n - 1)) == 0 && n <= ((size_t)1 << 30), GG_ERR_INVALID_ARG,
              "n must be a power of 2");
-    hipStream_t st = pick(hip_stream);
-    int L = 0;
-    while (((size_t)1 << L) < n) L++;
-    const FrB w = frb(omega_mont), u = frb(coset_shift_mont);
+    const FrB w = frb(omega_mont);
     GG_CHECK(pow_u64(w, n) == FrB::one(), GG_ERR_INVALID_ARG, "omega^n != 1");
-    // w^e tables (e < n)
-    const int S = (L + 1) / 2;
-    std::vector<FrB> lo((size_t)1 << S), hi((size_t)1 << (L - S));
-    FrB acc = FrB::one();
-    for (auto& x : lo) { x = acc; acc = acc * w; }
-    FrB step = acc;
-    acc = FrB::one();
-    for (auto& x : hi) { x = acc; acc = acc * step; }
-    DevBuf dt((lo.size() + hi.size()) * 32);
-    GG_HIP(hipMemcpyAsync(dt.p, lo.data(), lo.size() * 32, hipMemcpyHostToDevice, st));
-    GG_HIP(hipMemcpyAsync(dt.as<FrB>() + lo.size(), hi.data(), hi.size() * 32, hipMemcpyHostToDevice, st));
-    PowSplit ps{dt.as<FrB>() + lo.size(), dt.as<FrB>(), S};
-    DevBuf den(n * 32);
-    FrB* num = (FrB*)z_dev;
-    hipLaunchKernelGGL(k_ratio_numden, dim3(grid_for(n, 256)), dim3(256), 0, st, (const FrB*)l_dev,
-                       (const FrB*)r_dev, (const FrB*)o_dev, perm_dev, (uint32_t)n, L, frb(beta),
-                       frb(gamma), u, u * u, ps, num, den.as<FrB>());
-    GG_HIP(hipGetLastError());
-    bls_batch_invert(den.as<FrB>(), n, st);  // t = fr.BatchInvert(t)
-    hipLaunchKernelGGL(k_mul_inplace, dim3(grid_for(n, 256)), dim3(256), 0, st, num, (const FrB*)den.p, n);
-    GG_HIP(hipGetLastError());
-    scan_run<SCAN_PROD>(num, n, FrB::one(), st);  // Z[i] = Z[i-1] * num_i / den_i
+    hipStream_t st = pick(hip_stream);
+    Arena ar;
+    ar.reserve(plk::ratio_arena_bytes(n));
+    plk::ratio((const FrB*)l_dev, (const FrB*)r_dev, (const FrB*)o_dev, perm_dev, n, frb(beta), frb(gamma), w,
+               frb(coset_shift_mont), (FrB*)z_dev, st, ar);
+    GG_HIP(hipStreamSynchronize(st));
     GG_CAPI_END
 }
 
@@ -379,10 +466,7 @@ extern "C" int gg_plonk_fold_h(const void* h_dev, size_t n_small, const void* ze
     GG_CAPI_BEGIN
     GG_CHECK(h_dev && zeta_pow_np2 && out_dev, GG_ERR_INVALID_ARG, "null argument");
     hipStream_t st = pick(hip_stream);
-    const size_t np2 = n_small + 2;
-    hipLaunchKernelGGL(k_fold_h, dim3(grid_for(np2, 256)), dim3(256), 0, st, (const FrB*)h_dev, np2,
-                       frb(zeta_pow_np2), (FrB*)out_dev);
-    GG_HIP(hipGetLastError());
+    plk::fold_h((const FrB*)h_dev, n_small, frb(zeta_pow_np2), (FrB*)out_dev, st);
     GG_HIP(hipStreamSynchronize(st));
     GG_CAPI_END
 }
@@ -393,9 +477,9 @@ extern "C" int gg_plonk_linearized(void* blinded_z_dev, size_t nz, const void* s
                                    void* hip_stream) {
     GG_CAPI_BEGIN
     GG_CHECK(blinded_z_dev && (s3_dev || ns3 == 0) && q_dev && scalars8, GG_ERR_INVALID_ARG, "null argument");
-    GG_CHECK(n_cmt >= 0 && n_cmt <= MAX_CMT, GG_ERR_INVALID_ARG, "at most 8 BSB22 commitments");
+    GG_CHECK(n_cmt >= 0 && n_cmt <= plk::MAX_CMT, GG_ERR_INVALID_ARG, "at most 8 BSB22 commitments");
     GG_CHECK(n_cmt == 0 || (pi2_dev && qcp_zeta), GG_ERR_INVALID_ARG, "null commitment polynomials");
-    LinParams P{};
+    plk::LinParams P{};
     P.z = (FrB*)blinded_z_dev;
     P.nz = nz;
     P.s3 = (const FrB*)s3_dev;
@@ -417,8 +501,7 @@ extern "C" int gg_plonk_linearized(void* blinded_z_dev, size_t nz, const void* s
     FrB* dst[8] = {&P.s1, &P.s2, &P.alpha, &P.l, &P.r, &P.rl, &P.o, &P.lag};
     for (int k = 0; k < 8; k++) *dst[k] = frb(s + 32 * k);
     hipStream_t st = pick(hip_stream);
-    hipLaunchKernelGGL(k_linearized, dim3(grid_for(nz, 256)), dim3(256), 0, st, P);
-    GG_HIP(hipGetLastError());
+    plk::linearized(P, st);
     GG_HIP(hipStreamSynchronize(st));
     GG_CAPI_END
 }
@@ -427,12 +510,8 @@ extern "C" int gg_bls12_381_fr_bit_reverse(const void* in_dev, void* out_dev, si
     GG_CAPI_BEGIN
     GG_CHECK(in_dev && out_dev && in_dev != out_dev, GG_ERR_INVALID_ARG, "need distinct in / out buffers");
     GG_CHECK(n >= 1 && (n & (n - 1)) == 0 && n <= ((size_t)1 << 31), GG_ERR_INVALID_ARG, "n must be a power of 2");
-    int L = 0;
-    while (((size_t)1 << L) < n) L++;
     hipStream_t st = pick(hip_stream);
-    hipLaunchKernelGGL(k_bit_reverse, dim3(grid_for(n, 256)), dim3(256), 0, st, (FrB*)out_dev,
-                       (const FrB*)in_dev, n, L);
-    GG_HIP(hipGetLastError());
+    plk::bit_reverse((const FrB*)in_dev, (FrB*)out_dev, n, st);
     GG_HIP(hipStreamSynchronize(st));
     GG_CAPI_END
 }
@@ -443,9 +522,7 @@ extern "C" int gg_bls12_381_fr_axpy(void* y_dev, const void* x_dev, size_t n, co
     GG_CHECK(y_dev && x_dev && a_mont, GG_ERR_INVALID_ARG, "null argument");
     if (n == 0) return GG_OK;
     hipStream_t st = pick(hip_stream);
-    hipLaunchKernelGGL(k_axpy, dim3(grid_for(n, 256)), dim3(256), 0, st, (FrB*)y_dev, (const FrB*)x_dev, n,
-                       frb(a_mont));
-    GG_HIP(hipGetLastError());
+    plk::axpy((FrB*)y_dev, (const FrB*)x_dev, n, frb(a_mont), st);
     GG_HIP(hipStreamSynchronize(st));
     GG_CAPI_END
 }

@@ -1,0 +1,934 @@
+// PlonK BLS12-381 prover behind the C ABI: the device section of gnark's
+// backend/plonk/bls12-381 Prove (prove.go:116-1079) after the solver.
+//
+// Stages (prove.go's errgroup DAG, mapped onto 4 HIP streams and host threads):
+//   commitToLRO        3 KZG MSMs on pk.KzgLagrange at once (one MsmWork each),
+//                      blinding commitments on the host meanwhile; canonical
+//                      L, R, O, completeQk and the BSB22 Pi_i on another stream
+//   gamma, beta        Fiat-Shamir (bindPublicData: vk digests, public inputs)
+//   ratio Z            BuildRatioCopyConstraint + its commitment
+//   alpha              Bsb22Commitments, Z
+//   computeNumerator   per coset of the big domain (two cosets in flight):
+//                      coset FFTs of L, R, O, Z, Qk, Pi_i (the key's polynomials
+//                      are resident coset evaluations), allConstraints kernel
+//   divideByXMinusOne  big-coset iFFT, then H1, H2, H3 committed at once
+//   zeta               H
+//   openZ | linearize  Z opened at zeta*omega (its quotient MSM overlaps the
+//                      linearized polynomial and its MSM); foldH
+//   batchOpening       kzg.BatchOpenSinglePoint at zeta
+// Transcripts: fiat-shamir (challenge = H(name | previous | bindings)),
+// points bound with RawBytes (deriveRandomness, verify.go:342-360) or Marshal
+// (compressed: bindPublicData verify.go:296-340, kzg deriveGamma), scalars as
+// 32-B big-endian.  The hash is the caller's (gg_hash_fn) or SHA-256.
+#include "plonk_ops.h"
+#include "curve.cuh"
+#include "sha256.h"
+#include <future>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+#include <cstring>
+#include <chrono>
+#include <cstdlib>
+#include <fstream>
+
+struct gg_msm_base;
+namespace gg {
+struct MsmWork;
+void msm_device_work(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st);
+MsmWork* msm_work_new();
+void msm_work_delete(MsmWork* w);
+}  // namespace gg
+
+using namespace gg;
+using plk::FrB;
+using BAff = Affine<FpBls>;
+using BJac = Jac<FpBls>;
+
+namespace {
+
+// ------------------------------------------------------------ encodings
+// canonical little-endian u32 limbs -> big-endian bytes
+template <int N>
+void be_bytes(const uint32_t* v, uint8_t* out) {
+    for (int i = 0; i < N; i++) {
+        const uint32_t w = v[N - 1 - i];
+        out[4 * i] = (uint8_t)(w >> 24);
+        out[4 * i + 1] = (uint8_t)(w >> 16);
+        out[4 * i + 2] = (uint8_t)(w >> 8);
+        out[4 * i + 3] = (uint8_t)w;
+    }
+}
+// fr.Element.Marshal: 32-B big-endian canonical
+void fr_marshal(const FrB& x, uint8_t out[32]) {
+    const FrB c = from_mont(x);
+    be_bytes<8>(c.v, out);
+}
+// fr.Element.SetBytes: big-endian integer mod r
+FrB fr_set_bytes(const uint8_t* b, size_t n) {
+    FrB acc = FrB::zero();
+    FrB b256 = FrB::zero();
+    b256.v[0] = 256;
+    b256 = to_mont(b256);
+    for (size_t i = 0; i < n; i++) {
+        FrB d = FrB::zero();
+        d.v[0] = b[i];
+        acc = acc * b256 + to_mont(d);
+    }
+    return acc;
+}
+bool fp_lex_largest(const FpBls& y) {  // y > (p - 1) / 2  <=>  y > p - y
+    const FpBls c = from_mont(y), nc = from_mont(-y);
+    for (int i = 11; i >= 0; i--)
+        if (c.v[i] != nc.v[i]) return c.v[i] > nc.v[i];
+    return false;
+}
+// G1Affine.RawBytes (uncompressed, 96 B; infinity = 0x40 | zeros)
+void g1_raw_bytes(const BAff& p, uint8_t out[96]) {
+    memset(out, 0, 96);
+    if (p.is_inf()) {
+        out[0] = 0x40;
+        return;
+    }
+    be_bytes<12>(from_mont(p.x).v, out);
+    be_bytes<12>(from_mont(p.y).v, out + 48);
+}
+// G1Affine.Marshal = Bytes (compressed, 48 B; 0x80 smallest y, 0xA0 largest, 0xC0 infinity)
+void g1_marshal(const BAff& p, uint8_t out[48]) {
+    memset(out, 0, 48);
+    if (p.is_inf()) {
+        out[0] = 0xC0;
+        return;
+    }
+    be_bytes<12>(from_mont(p.x).v, out);
+    out[0] |= fp_lex_largest(p.y) ? 0xA0 : 0x80;
+}
+
+// ------------------------------------------------------------ transcript
+struct Hasher {
+    gg_hash_fn fn;
+    void* ctx;
+    std::vector<uint8_t> operator()(const std::vector<uint8_t>& msg) const {
+        if (!fn) {
+            std::vector<uint8_t> d(32);
+            Sha256::hash(msg.data(), msg.size(), d.data());
+            return d;
+        }
+        std::vector<uint8_t> d(128);
+        size_t len = d.size();
+        GG_CHECK(fn(ctx, msg.data(), msg.size(), d.data(), &len) == 0, GG_ERR_INVALID_ARG, "hash callback failed");
+        GG_CHECK(len >= 1 && len <= 128, GG_ERR_INVALID_ARG, "hash callback: digest of 1..128 bytes");
+        d.resize(len);
+        return d;
+    }
+};
+
+// gnark-crypto fiat-shamir Transcript: challenge i = H(name_i | value_(i-1) | bindings_i)
+struct Transcript {
+    std::vector<std::string> names;
+    std::vector<std::vector<uint8_t>> bound, value;
+    Hasher h;
+    Transcript(std::initializer_list<const char*> ns, Hasher hh) : h(hh) {
+        for (const char* s : ns) names.emplace_back(s);
+        bound.resize(names.size());
+        value.resize(names.size());
+    }
+    size_t idx(const char* n) const {
+        for (size_t i = 0; i < names.size(); i++)
+            if (names[i] == n) return i;
+        throw Error(GG_ERR_INTERNAL, "unknown challenge");
+    }
+    void bind(const char* n, const uint8_t* b, size_t len) {
+        auto& v = bound[idx(n)];
+        v.insert(v.end(), b, b + len);
+    }
+    FrB compute(const char* n) {
+        const size_t i = idx(n);
+        std::vector<uint8_t> msg(names[i].begin(), names[i].end());
+        if (i) msg.insert(msg.end(), value[i - 1].begin(), value[i - 1].end());
+        msg.insert(msg.end(), bound[i].begin(), bound[i].end());
+        value[i] = h(msg);
+        return fr_set_bytes(value[i].data(), value[i].size());
+    }
+};
+// deriveRandomness (verify.go:342-360): RawBytes of each point, then the challenge
+FrB derive(Transcript& fs, const char* n, std::initializer_list<const BAff*> pts) {
+    uint8_t b[96];
+    for (const BAff* p : pts) {
+        g1_raw_bytes(*p, b);
+        fs.bind(n, b, 96);
+    }
+    return fs.compute(n);
+}
+
+// ------------------------------------------------------------ host G1 helpers
+BJac jmul(const BAff& p, const FrB& k) {
+    const FrB c = from_mont(k);
+    return jac_mul(BJac::from_affine(p), c.v);
+}
+BAff to_aff(const BJac& j) { return jac_to_affine(j); }
+FrB frv(uint64_t x) {
+    FrB r = FrB::zero();
+    r.v[0] = (uint32_t)x;
+    r.v[1] = (uint32_t)(x >> 32);
+    return to_mont(r);
+}
+FrB horner_host(const std::vector<FrB>& c, const FrB& x) {
+    FrB r = FrB::zero();
+    for (size_t k = c.size(); k-- > 0;) r = r * x + c[k];
+    return r;
+}
+// 255-bit random fr (rejection sampled, SetRandom of gnark-crypto)
+FrB fr_random() {
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    static std::ifstream ur("/dev/urandom", std::ios::binary);
+    GG_CHECK(ur.good(), GG_ERR_INTERNAL, "no /dev/urandom");
+    const FrB p = FrB::modulus();
+    for (;;) {
+        FrB x;
+        ur.read((char*)x.v, 32);
+        x.v[7] &= 0x7fffffffu;  // r < 2^255
+        bool lt = false;
+        for (int i = 7; i >= 0; i--)
+            if (x.v[i] != p.v[i]) { lt = x.v[i] < p.v[i]; break; }
+        if (lt) return to_mont(x);
+    }
+}
+
+}  // namespace
+
+// ============================================================== key
+struct gg_plonk_pk {
+    int log_n = 0, log_big = 0;
+    size_t n = 0, big = 0, rho = 0;
+    FrB omega, omega_big, u, n_inv;
+    gg_domain_t d0 = nullptr, d1 = nullptr;
+    std::vector<gg_domain_t> dcos;
+    std::vector<FrB> coset_shift;
+    // trace, canonical regular (reg) and bit-reversed (brev); Qk incomplete
+    enum { QL, QR, QM, QO, QK, S1, S2, S3, NTRACE };
+    DevBuf reg[NTRACE], brev[NTRACE], qk_lag;
+    std::vector<DevBuf> qcp_reg, qcp_brev;
+    // resident coset evaluations [poly][coset]: Ql Qr Qm Qo S1 S2 S3 X LOne Qcp_i
+    enum { E_QL, E_QR, E_QM, E_QO, E_S1, E_S2, E_S3, E_X, E_LONE, E_QCP0 };
+    std::vector<std::vector<DevBuf>> ev;
+    DevBuf perm, tw0;
+    gg_msm_base_t kzg = nullptr, kzg_lag = nullptr;
+    BAff blind_lo[3], blind_hi[3];  // G1[0..3), G1[n..n+3)
+    BAff vkS[3], vkQ[5];            // S1 S2 S3, Ql Qr Qm Qo Qk
+    std::vector<BAff> vkQcp;
+    size_t nb_public = 0;
+    std::vector<uint64_t> cmt_idx;
+    // multi-GPU: this rank keeps pk.Kzg.G1[k_lo, k_hi) and pk.KzgLagrange.G1[l_lo, l_hi);
+    // every commitment is a partial MSM completed by `reduce` (sum over ranks)
+    int rank = 0, world = 1;
+    size_t k_lo = 0, k_hi = 0, l_lo = 0, l_hi = 0;
+    gg_g1_reduce_fn reduce = nullptr;
+    void* reduce_ctx = nullptr;
+    int n_cmt = 0;
+    hipStream_t s[4] = {nullptr, nullptr, nullptr, nullptr};
+    MsmWork* work[3] = {nullptr, nullptr, nullptr};
+    Arena ar[4];
+    // per-proof buffers
+    DevBuf lag[3], can[4], cbrev[4], zlag, qkc, pi_reg[plk::MAX_CMT], pi_brev[plk::MAX_CMT];
+    DevBuf cev[2][7 + plk::MAX_CMT];  // coset evaluation slots (two cosets in flight)
+    DevBuf cres, hpad[3], bz, bl[3], fold, lin, q1, q2, vals, pad;
+    int device = 0;
+    std::vector<hipEvent_t> evs;  // cross-stream ordering events, reused by every prove
+    size_t ev_next = 0;
+    std::mutex mu;
+    ~gg_plonk_pk() {
+        for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+        for (auto w : work)
+            if (w) msm_work_delete(w);
+        if (kzg) gg_msm_base_release(kzg);
+        if (kzg_lag) gg_msm_base_release(kzg_lag);
+        if (d0) gg_domain_release(d0);
+        if (d1) gg_domain_release(d1);
+        for (auto d : dcos) gg_domain_release(d);
+        for (hipStream_t x : s)
+            if (x) (void)hipStreamDestroy(x);
+    }
+};
+
+namespace {
+
+FrB* F(const DevBuf& b) { return b.as<FrB>(); }
+void dcopy(void* dst, const void* src, size_t bytes, hipStream_t st) {
+    if (bytes) GG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
+}
+void zero(void* dst, size_t bytes, hipStream_t st) {
+    if (bytes) GG_HIP(hipMemsetAsync(dst, 0, bytes, st));
+}
+void up(void* dst, const void* src, size_t bytes, bool on_dev, hipStream_t st) {
+    if (bytes) GG_HIP(hipMemcpyAsync(dst, src, bytes, on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+}
+// canonical regular -> canonical bit-reversed copy
+void to_brev(gg_plonk_pk* pk, const FrB* reg, FrB* brev, hipStream_t st) { plk::bit_reverse(reg, brev, pk->n, st); }
+// Lagrange regular (n) -> canonical bit-reversed (out) + canonical regular (reg)
+void lag_to_canonical(gg_plonk_pk* pk, const FrB* lag, FrB* brev, FrB* reg, hipStream_t st) {
+    dcopy(brev, lag, pk->n * 32, st);
+    plk::ntt(pk->d0, brev, 1, 0, 0, st);  // FFTInverse DIF: natural in -> bit-reversed out
+    if (reg) plk::bit_reverse(brev, reg, pk->n, st);
+}
+// evaluations on coset i (natural order) of a canonical bit-reversed polynomial
+void coset_eval(gg_plonk_pk* pk, const FrB* brev, FrB* out, int i, hipStream_t st) {
+    dcopy(out, brev, pk->n * 32, st);
+    plk::ntt(pk->dcos[i], out, 0, 1, 1, st);  // FFT DIT on the coset: bit-reversed in -> natural out
+}
+// `to` waits for the work enqueued on `from` so far (events live as long as the key)
+void record_wait(gg_plonk_pk* pk, hipStream_t from, hipStream_t to) {
+    if (from == to) return;
+    if (pk->ev_next == pk->evs.size()) {
+        hipEvent_t e;
+        GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        pk->evs.push_back(e);
+    }
+    hipEvent_t e = pk->evs[pk->ev_next++];
+    GG_HIP(hipEventRecord(e, from));
+    GG_HIP(hipStreamWaitEvent(to, e, 0));
+}
+// this rank's partial MSM (whole MSM on one GPU); red() completes it
+BJac msm_jac(gg_plonk_pk* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStream_t st) {
+    BJac j = BJac::inf();
+    const size_t lo = base == pk->kzg ? pk->k_lo : pk->l_lo;
+    msm_device_work(base, pk->work[wi], (const Fr*)(scal + lo), &j, st);
+    return j;
+}
+// kzg.Commit(p, pk.Kzg) of a buffer of n + 3 scalars (zero beyond the polynomial)
+BJac commit_kzg(gg_plonk_pk* pk, int wi, const FrB* scal, hipStream_t st) { return msm_jac(pk, pk->kzg, wi, scal, st); }
+// sum of the ranks' partials (called in one fixed order on every rank)
+BJac red(gg_plonk_pk* pk, BJac j) {
+    if (pk->world == 1) return j;
+    GG_CHECK(pk->reduce(pk->reduce_ctx, &j) == 0, GG_ERR_DEVICE, "commitment reduce callback failed");
+    return j;
+}
+// commitBlindingFactor (prove.go:1159-1172): sum_j b_j (G1[n + j] - G1[j])
+BJac blind_commit(gg_plonk_pk* pk, const std::vector<FrB>& b) {
+    BJac acc = BJac::inf();
+    for (size_t j = 0; j < b.size(); j++) {
+        acc = jac_add(acc, jmul(pk->blind_hi[j], b[j]));
+        acc = jac_add(acc, jmul(pk->blind_lo[j], -b[j]));
+    }
+    return acc;
+}
+FrB fetch(const FrB* dev, hipStream_t st) {
+    FrB v;
+    GG_HIP(hipMemcpyAsync(v.v, dev, 32, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipStreamSynchronize(st));
+    return v;
+}
+FrB eval_dev(gg_plonk_pk* pk, const FrB* f, size_t len, const FrB& a, FrB* q, FrB* slot, int ai, hipStream_t st) {
+    pk->ar[ai].reset();
+    plk::horner(f, len, a, q, slot, st, pk->ar[ai]);
+    return fetch(slot, st);
+}
+
+}  // namespace
+
+static void plonk_pk_build(gg_plonk_pk* pk, int log_n, int log_big, const void* omega, const void* omega_big,
+                           const void* coset_shift, const void* kzg_g1, size_t n_kzg,
+                           const void* kzg_lagrange_g1, const void* const* trace, const void* const* qcp,
+                           int n_cmt, const int64_t* perm, size_t nb_public, const uint64_t* cmt_idx,
+                           const void* vk_digests, int rank, int world, gg_g1_reduce_fn reduce, void* rctx) {
+    GG_CHECK(world >= 1 && rank >= 0 && rank < world && (world == 1 || reduce), GG_ERR_INVALID_ARG,
+             "bad shard (rank, world) or missing reduce callback");
+    pk->rank = rank;
+    pk->world = world;
+    pk->reduce = reduce;
+    pk->reduce_ctx = rctx;
+    GG_CHECK(log_n >= 1 && log_n <= 27 && log_big > log_n && log_big - log_n <= 3 && log_big <= 30,
+             GG_ERR_INVALID_ARG, "need 2 <= n, |big| / n in {2, 4, 8}");
+    GG_CHECK(omega && omega_big && coset_shift && kzg_g1 && kzg_lagrange_g1 && trace && perm, GG_ERR_INVALID_ARG,
+             "null argument");
+    GG_CHECK(n_cmt >= 0 && n_cmt <= plk::MAX_CMT && (n_cmt == 0 || (qcp && cmt_idx)), GG_ERR_INVALID_ARG,
+             "0..8 BSB22 commitments with their Qcp polynomials and constraint indexes");
+    pk->log_n = log_n;
+    pk->log_big = log_big;
+    pk->n = (size_t)1 << log_n;
+    pk->big = (size_t)1 << log_big;
+    pk->rho = pk->big / pk->n;
+    const size_t n = pk->n, nb = 32 * n;
+    GG_CHECK(n_kzg >= n + 3, GG_ERR_INVALID_ARG, "len(pk.Kzg.G1) < n + 3 (setup.go:150)");
+    GG_CHECK(nb_public < n, GG_ERR_INVALID_ARG, "nb_public >= n");
+    pk->nb_public = nb_public;
+    pk->n_cmt = n_cmt;
+    for (int i = 0; i < n_cmt; i++) {
+        GG_CHECK(nb_public + cmt_idx[i] < n, GG_ERR_INVALID_ARG, "commitment constraint index out of range");
+        pk->cmt_idx.push_back(cmt_idx[i]);
+    }
+    GG_HIP(hipGetDevice(&pk->device));
+    memcpy(pk->omega.v, omega, 32);
+    memcpy(pk->omega_big.v, omega_big, 32);
+    memcpy(pk->u.v, coset_shift, 32);
+    pk->n_inv = inverse(frv(n));
+    GG_CHECK(pow_u64(pk->omega_big, pk->rho) == pk->omega, GG_ERR_INVALID_ARG, "omega_big^(|big|/n) != omega");
+    auto dom = [&](int lg, const FrB& w, const FrB& g) {
+        gg_domain_t d;
+        int rc = gg_domain_create_ex(GG_CURVE_BLS12_381, lg, w.v, g.v, &d);
+        GG_CHECK(rc == GG_OK, rc, gg_last_error());
+        return d;
+    };
+    pk->d0 = dom(log_n, pk->omega, pk->u);
+    pk->d1 = dom(log_big, pk->omega_big, pk->u);
+    FrB sh = pk->u;
+    for (size_t i = 0; i < pk->rho; i++) {  // coset i of the big domain: shift u w_big^i
+        pk->coset_shift.push_back(sh);
+        pk->dcos.push_back(dom(log_n, pk->omega, sh));
+        sh = sh * pk->omega_big;
+    }
+    for (hipStream_t& x : pk->s) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    for (auto& w : pk->work) w = msm_work_new();
+    hipStream_t st = pk->s[0];
+    // KZG bases (resident, fixed-base precomputation): pk.Kzg.G1[:n+3], pk.KzgLagrange.G1
+    {
+        auto range = [&](size_t m, size_t& lo, size_t& hi) {  // dist.shard_range
+            lo = m * (size_t)pk->rank / (size_t)pk->world;
+            hi = m * (size_t)(pk->rank + 1) / (size_t)pk->world;
+        };
+        range(n + 3, pk->k_lo, pk->k_hi);
+        range(n, pk->l_lo, pk->l_hi);
+        int rc = gg_msm_base_create(GG_BLS12_381_G1, (const uint8_t*)kzg_g1 + 96 * pk->k_lo, pk->k_hi - pk->k_lo, 0,
+                                    nullptr, 0, &pk->kzg);
+        GG_CHECK(rc == GG_OK, rc, gg_last_error());
+        rc = gg_msm_base_create(GG_BLS12_381_G1, (const uint8_t*)kzg_lagrange_g1 + 96 * pk->l_lo,
+                                pk->l_hi - pk->l_lo, 0, nullptr, 0, &pk->kzg_lag);
+        GG_CHECK(rc == GG_OK, rc, gg_last_error());
+        const uint8_t* g = (const uint8_t*)kzg_g1;
+        for (int j = 0; j < 3; j++) {
+            memcpy(&pk->blind_lo[j], g + 96 * j, 96);
+            memcpy(&pk->blind_hi[j], g + 96 * (n + j), 96);
+        }
+    }
+    // trace polynomials
+    for (int k = 0; k < gg_plonk_pk::NTRACE; k++) {
+        GG_CHECK(trace[k], GG_ERR_INVALID_ARG, "null trace polynomial");
+        pk->reg[k].alloc(nb);
+        pk->brev[k].alloc(nb);
+        up(pk->reg[k].p, trace[k], nb, false, st);
+        to_brev(pk, F(pk->reg[k]), F(pk->brev[k]), st);
+    }
+    pk->qcp_reg.resize(n_cmt);
+    pk->qcp_brev.resize(n_cmt);
+    for (int i = 0; i < n_cmt; i++) {
+        GG_CHECK(qcp[i], GG_ERR_INVALID_ARG, "null Qcp polynomial");
+        pk->qcp_reg[i].alloc(nb);
+        pk->qcp_brev[i].alloc(nb);
+        up(pk->qcp_reg[i].p, qcp[i], nb, false, st);
+        to_brev(pk, F(pk->qcp_reg[i]), F(pk->qcp_brev[i]), st);
+    }
+    // Qk in Lagrange regular form (completeQk: trace.Qk.Clone().ToLagrange().ToRegular())
+    {
+        DevBuf t(nb);
+        dcopy(t.p, pk->reg[gg_plonk_pk::QK].p, nb, st);
+        plk::ntt(pk->d0, t.p, 0, 0, 0, st);  // FFT DIF: natural in -> bit-reversed out
+        pk->qk_lag.alloc(nb);
+        plk::bit_reverse(F(t), F(pk->qk_lag), n, st);
+        GG_HIP(hipStreamSynchronize(st));
+    }
+    // s.twiddles0 = w^j: DIT FFT of the coefficients of X (bit-reversed layout)
+    // (every upload below is ordered on st and waited for: a plain hipMemcpy runs
+    // on the null stream, which does not order against the non-blocking st)
+    pk->tw0.alloc(nb);
+    zero(pk->tw0.p, nb, st);
+    const FrB one = FrB::one();
+    GG_HIP(hipMemcpyAsync(F(pk->tw0) + n / 2, one.v, 32, hipMemcpyHostToDevice, st));
+    GG_HIP(hipStreamSynchronize(st));
+    plk::ntt(pk->d0, pk->tw0.p, 0, 1, 0, st);
+    // resident coset evaluations of the key's polynomials (the reference redoes
+    // these 2 rho FFTs per polynomial per proof, prove.go:995-1017)
+    DevBuf xb(nb), lone(nb);
+    zero(xb.p, nb, st);
+    GG_HIP(hipMemcpyAsync(F(xb) + n / 2, one.v, 32, hipMemcpyHostToDevice, st));  // X, bit-reversed
+    {
+        std::vector<FrB> v(n, pk->n_inv);  // LOne canonical: 1/n everywhere
+        GG_HIP(hipMemcpyAsync(lone.p, v.data(), nb, hipMemcpyHostToDevice, st));
+        GG_HIP(hipStreamSynchronize(st));
+    }
+    std::vector<const FrB*> srcs = {F(pk->brev[gg_plonk_pk::QL]), F(pk->brev[gg_plonk_pk::QR]),
+                                    F(pk->brev[gg_plonk_pk::QM]), F(pk->brev[gg_plonk_pk::QO]),
+                                    F(pk->brev[gg_plonk_pk::S1]), F(pk->brev[gg_plonk_pk::S2]),
+                                    F(pk->brev[gg_plonk_pk::S3]), F(xb), F(lone)};
+    for (int i = 0; i < n_cmt; i++) srcs.push_back(F(pk->qcp_brev[i]));
+    pk->ev.resize(srcs.size());
+    for (size_t k = 0; k < srcs.size(); k++) {
+        pk->ev[k].resize(pk->rho);
+        for (size_t i = 0; i < pk->rho; i++) {
+            pk->ev[k][i].alloc(nb);
+            coset_eval(pk, srcs[k], F(pk->ev[k][i]), (int)i, st);
+        }
+    }
+    pk->perm.alloc(3 * n * 8);
+    up(pk->perm.p, perm, 3 * n * 8, false, st);
+    // per-proof buffers
+    for (auto& b : pk->lag) b.alloc(nb);
+    for (auto& b : pk->can) b.alloc(nb);
+    for (auto& b : pk->cbrev) b.alloc(nb);
+    pk->zlag.alloc(nb);
+    pk->qkc.alloc(nb);
+    for (int i = 0; i < n_cmt; i++) {
+        pk->pi_reg[i].alloc(nb);
+        pk->pi_brev[i].alloc(nb);
+    }
+    for (auto& slot : pk->cev)
+        for (int k = 0; k < 7 + n_cmt; k++) slot[k].alloc(nb);
+    pk->cres.alloc(32 * pk->big);
+    const size_t nb3 = 32 * (n + 3);
+    for (auto& b : pk->hpad) b.alloc(nb3);
+    pk->bz.alloc(nb3);
+    for (auto& b : pk->bl) b.alloc(nb3);
+    pk->fold.alloc(nb3);
+    pk->lin.alloc(nb3);
+    pk->q1.alloc(nb3);
+    pk->q2.alloc(nb3);
+    pk->pad.alloc(nb3);
+    pk->vals.alloc(32 * 64);
+    const size_t ab = std::max(plk::ratio_arena_bytes(n), plk::horner_arena_bytes(n + 3)) + 65536;
+    for (auto& a : pk->ar) a.reserve(ab);
+    GG_HIP(hipStreamSynchronize(st));
+    // vk digests (commitTrace, setup.go:229-272) unless the caller has them
+    pk->vkQcp.resize(n_cmt);
+    if (vk_digests) {
+        const uint8_t* d = (const uint8_t*)vk_digests;
+        for (int k = 0; k < 3; k++) memcpy(&pk->vkS[k], d + 96 * k, 96);
+        for (int k = 0; k < 5; k++) memcpy(&pk->vkQ[k], d + 96 * (3 + k), 96);
+        for (int i = 0; i < n_cmt; i++) memcpy(&pk->vkQcp[i], d + 96 * (8 + i), 96);
+    } else {
+        auto cm = [&](const DevBuf& reg) {
+            zero(pk->pad.p, nb3, st);
+            dcopy(pk->pad.p, reg.p, nb, st);
+            return to_aff(red(pk, commit_kzg(pk, 0, F(pk->pad), st)));
+        };
+        for (int k = 0; k < 3; k++) pk->vkS[k] = cm(pk->reg[gg_plonk_pk::S1 + k]);
+        for (int k = 0; k < 5; k++) pk->vkQ[k] = cm(pk->reg[gg_plonk_pk::QL + k]);
+        for (int i = 0; i < n_cmt; i++) pk->vkQcp[i] = cm(pk->qcp_reg[i]);
+    }
+}
+
+// ============================================================== prove
+namespace {
+
+struct PlonkProof {
+    BAff lro[3], z, h[3], batched_h, zs_h;
+    std::vector<BAff> bsb22;
+    std::vector<FrB> claimed;
+    FrB zs_value;
+};
+
+// GG_PLONK_SERIAL=1: the concurrent MSM groups run one after another (A/B timing)
+std::launch msm_policy() {
+    static const bool serial = getenv("GG_PLONK_SERIAL") && atoi(getenv("GG_PLONK_SERIAL"));
+    return serial ? std::launch::deferred : std::launch::async;
+}
+
+void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB* pub, size_t nb_pub,
+           const void* const* cmt_values, const BAff* cmt_digests, const FrB* cmt_hashed, int n_cmt,
+           const FrB* blinding, Hasher ch, Hasher fh, PlonkProof& P, double* tms) {
+    const size_t n = pk->n, nb = 32 * n, nb3 = 32 * (n + 3);
+    hipStream_t* s = pk->s;
+    pk->ev_next = 0;
+    auto t0 = std::chrono::steady_clock::now();
+    int tk = 0;
+    auto mark = [&]() {
+        if (!tms) return;
+        auto t = std::chrono::steady_clock::now();
+        tms[tk++] = std::chrono::duration<double, std::milli>(t - t0).count();
+    };
+    // blinding polynomials (initBlindingPolynomials, prove.go:295-302): orders 1, 1, 1, 2
+    std::vector<FrB> bp[4];
+    const int ord[4] = {1, 1, 1, 2};
+    for (int q = 0, k = 0; q < 4; q++)
+        for (int j = 0; j <= ord[q]; j++) bp[q].push_back(blinding ? blinding[k++] : fr_random());
+    // ---- inputs: L, R, O (Lagrange regular) on streams 0..2
+    for (int k = 0; k < 3; k++) up(pk->lag[k].p, lro_in[k], nb, on_dev, s[k]);
+    // blinding commitments of L, R, O, Z on host threads while the GPU works
+    std::future<BJac> fblind[4];
+    for (int q = 0; q < 4; q++) fblind[q] = std::async(std::launch::async, [pk, &bp, q] { return blind_commit(pk, bp[q]); });
+    // ---- commitToLRO: three KZG MSMs on pk.KzgLagrange at once
+    BJac lroj[3];
+    {
+        std::vector<std::future<void>> fs;
+        for (int k = 0; k < 3; k++)
+            fs.push_back(std::async(msm_policy(), [&, k] {
+                GG_HIP(hipSetDevice(pk->device));
+                lroj[k] = msm_jac(pk, pk->kzg_lag, k, F(pk->lag[k]), s[k]);
+            }));
+        // meanwhile on stream 3: completeQk (prove.go:397-423) and the BSB22 Pi_i
+        {
+            hipStream_t q = s[3];
+            dcopy(pk->qkc.p, pk->qk_lag.p, nb, q);
+            if (nb_pub) GG_HIP(hipMemcpyAsync(pk->qkc.p, pub, 32 * nb_pub, hipMemcpyHostToDevice, q));
+            for (int i = 0; i < n_cmt; i++)
+                GG_HIP(hipMemcpyAsync(F(pk->qkc) + pk->nb_public + pk->cmt_idx[i], cmt_hashed[i].v, 32,
+                                      hipMemcpyHostToDevice, q));
+            plk::ntt(pk->d0, pk->qkc.p, 1, 0, 0, q);  // -> canonical bit-reversed
+            for (int i = 0; i < n_cmt; i++) {
+                up(pk->pi_reg[i].p, cmt_values[i], nb, false, q);
+                lag_to_canonical(pk, F(pk->pi_reg[i]), F(pk->pi_brev[i]), nullptr, q);
+                plk::bit_reverse(F(pk->pi_brev[i]), F(pk->pi_reg[i]), n, q);
+            }
+            GG_HIP(hipStreamSynchronize(q));
+        }
+        for (auto& f : fs) f.get();
+    }
+    for (int k = 0; k < 3; k++) P.lro[k] = to_aff(jac_add(red(pk, lroj[k]), fblind[k].get()));
+    // canonical L, R, O (bit-reversed for the coset FFTs, regular for the openings)
+    for (int k = 0; k < 3; k++) lag_to_canonical(pk, F(pk->lag[k]), F(pk->cbrev[k]), F(pk->can[k]), s[k]);
+    mark();
+    // ---- gamma, beta (deriveGammaAndBeta, prove.go:454-489; bindPublicData, verify.go:296-340)
+    Transcript fs({"gamma", "beta", "alpha", "zeta"}, ch);
+    {
+        uint8_t b[48];
+        for (int k = 0; k < 3; k++) { g1_marshal(pk->vkS[k], b); fs.bind("gamma", b, 48); }
+        for (int k = 0; k < 5; k++) { g1_marshal(pk->vkQ[k], b); fs.bind("gamma", b, 48); }
+        for (int i = 0; i < pk->n_cmt; i++) { g1_marshal(pk->vkQcp[i], b); fs.bind("gamma", b, 48); }
+        uint8_t f32[32];
+        for (size_t i = 0; i < nb_pub; i++) { fr_marshal(pub[i], f32); fs.bind("gamma", f32, 32); }
+    }
+    const FrB gamma = derive(fs, "gamma", {&P.lro[0], &P.lro[1], &P.lro[2]});
+    const FrB beta = fs.compute("beta");
+    // ---- ratio Z (buildRatioCopyConstraint, prove.go:600-632) + its commitment
+    for (int k = 0; k < 3; k++) record_wait(pk, s[k], s[0]);
+    pk->ar[0].reset();
+    plk::ratio(F(pk->lag[0]), F(pk->lag[1]), F(pk->lag[2]), pk->perm.as<int64_t>(), n, beta, gamma, pk->omega,
+               pk->u, F(pk->zlag), s[0], pk->ar[0]);
+    record_wait(pk, s[0], s[1]);
+    lag_to_canonical(pk, F(pk->zlag), F(pk->cbrev[3]), F(pk->can[3]), s[1]);  // overlaps the Z commitment
+    P.z = to_aff(jac_add(red(pk, msm_jac(pk, pk->kzg_lag, 0, F(pk->zlag), s[0])), fblind[3].get()));
+    mark();
+    // ---- alpha (deriveAlpha, prove.go:504-512)
+    P.bsb22.assign(cmt_digests, cmt_digests + n_cmt);
+    {
+        uint8_t b[96];
+        for (int i = 0; i < n_cmt; i++) { g1_raw_bytes(P.bsb22[i], b); fs.bind("alpha", b, 96); }
+    }
+    const FrB alpha = derive(fs, "alpha", {&P.z});
+    // ---- computeNumerator (prove.go:837-1079): two cosets in flight on s[2], s[3]
+    for (int k = 0; k < 4; k++) record_wait(pk, s[k == 3 ? 1 : k], s[2]), record_wait(pk, s[k == 3 ? 1 : k], s[3]);
+    {
+        const FrB cs = pk->u, css = pk->u * pk->u;
+        int lb = pk->log_big;
+        for (size_t i = 0; i < pk->rho; i++) {
+            const int slot = (int)(i & 1);
+            hipStream_t q = s[2 + slot];
+            DevBuf* e = pk->cev[slot];
+            // per-proof polynomials on this coset: L R O Z, ZS (shift), ID = beta X, Qk, Pi_j
+            for (int k = 0; k < 4; k++) coset_eval(pk, F(pk->cbrev[k]), F(e[k]), (int)i, q);
+            plk::shift_copy(F(e[3]), F(e[4]), n, q);
+            dcopy(e[5].p, pk->ev[gg_plonk_pk::E_X][i].p, nb, q);
+            plk::scale(F(e[5]), n, beta, q);
+            coset_eval(pk, F(pk->qkc), F(e[6]), (int)i, q);
+            for (int j = 0; j < n_cmt; j++) coset_eval(pk, F(pk->pi_brev[j]), F(e[7 + j]), (int)i, q);
+            plk::NumParams NP{};
+            NP.x[plk::ID_L] = F(e[0]);
+            NP.x[plk::ID_R] = F(e[1]);
+            NP.x[plk::ID_O] = F(e[2]);
+            NP.x[plk::ID_Z] = F(e[3]);
+            NP.x[plk::ID_ZS] = F(e[4]);
+            NP.x[plk::ID_QL] = F(pk->ev[gg_plonk_pk::E_QL][i]);
+            NP.x[plk::ID_QR] = F(pk->ev[gg_plonk_pk::E_QR][i]);
+            NP.x[plk::ID_QM] = F(pk->ev[gg_plonk_pk::E_QM][i]);
+            NP.x[plk::ID_QO] = F(pk->ev[gg_plonk_pk::E_QO][i]);
+            NP.x[plk::ID_QK] = F(e[6]);
+            NP.x[plk::ID_S1] = F(pk->ev[gg_plonk_pk::E_S1][i]);
+            NP.x[plk::ID_S2] = F(pk->ev[gg_plonk_pk::E_S2][i]);
+            NP.x[plk::ID_S3] = F(pk->ev[gg_plonk_pk::E_S3][i]);
+            NP.x[plk::ID_ID] = F(e[5]);
+            NP.x[plk::ID_LONE] = F(pk->ev[gg_plonk_pk::E_LONE][i]);
+            for (int j = 0; j < n_cmt; j++) {
+                NP.x[plk::ID_QCI + 2 * j] = F(pk->ev[gg_plonk_pk::E_QCP0 + j][i]);
+                NP.x[plk::ID_QCI + 2 * j + 1] = F(e[7 + j]);
+            }
+            NP.nx = plk::ID_QCI + 2 * n_cmt;
+            // blinding polynomials scaled for this coset: b_j s^j (s^n - 1) (prove.go:985-993)
+            const FrB sc = pk->coset_shift[i];
+            const FrB sn1 = pow_u64(sc, n) - FrB::one();
+            for (int q4 = 0; q4 < 4; q4++) {
+                FrB acc = sn1;
+                NP.bdeg[q4] = (int)bp[q4].size();
+                for (size_t j = 0; j < bp[q4].size(); j++) {
+                    NP.bcoef[q4][j] = bp[q4][j] * acc;
+                    acc = acc * sc;
+                }
+            }
+            NP.tw0 = F(pk->tw0);
+            NP.beta = beta;
+            NP.gamma = gamma;
+            NP.alpha = alpha;
+            NP.cs = cs;
+            NP.css = css;
+            NP.n = (uint32_t)n;
+            NP.rho = (uint32_t)pk->rho;
+            NP.coset = (uint32_t)i;
+            NP.log_big = (uint32_t)lb;
+            NP.cres = F(pk->cres);
+            plk::numerator(NP, q);
+        }
+    }
+    record_wait(pk, s[3], s[2]);
+    plk::divide_by_xn_minus_one(pk->d1, n, F(pk->cres), s[2]);  // h, canonical regular
+    for (int k = 0; k < 3; k++) {
+        zero(pk->hpad[k].p, nb3, s[2]);
+        dcopy(pk->hpad[k].p, F(pk->cres) + (n + 2) * k, 32 * (n + 2), s[2]);
+    }
+    for (int k = 0; k < 3; k++) record_wait(pk, s[2], s[k]);
+    mark();
+    // ---- commitToQuotient: H1, H2, H3 at once (prove.go:1199-1218)
+    {
+        BJac hj[3];
+        std::vector<std::future<void>> fs3;
+        for (int k = 0; k < 3; k++)
+            fs3.push_back(std::async(msm_policy(), [&, k] {
+                GG_HIP(hipSetDevice(pk->device));
+                hj[k] = commit_kzg(pk, k, F(pk->hpad[k]), s[k]);
+            }));
+        for (auto& f : fs3) f.get();
+        for (int k = 0; k < 3; k++) P.h[k] = to_aff(red(pk, hj[k]));
+    }
+    mark();
+    const FrB zeta = derive(fs, "zeta", {&P.h[0], &P.h[1], &P.h[2]});
+    const FrB zn = pow_u64(zeta, n), zn1 = zn - FrB::one();
+    // ---- openZ (prove.go:635-652): blinded Z = Z - bz + bz X^n, opened at zeta * omega
+    auto blinded = [&](const DevBuf& canon, const std::vector<FrB>& b, DevBuf& out, hipStream_t q) {
+        zero(out.p, nb3, q);
+        dcopy(out.p, canon.p, nb, q);
+        std::vector<FrB> head(b.size()), tail(b);
+        for (size_t j = 0; j < b.size(); j++) head[j] = -b[j];
+        GG_HIP(hipMemcpyAsync(F(pk->pad), head.data(), 32 * b.size(), hipMemcpyHostToDevice, q));
+        plk::axpy(F(out), F(pk->pad), b.size(), FrB::one(), q);
+        GG_HIP(hipMemcpyAsync(F(out) + n, tail.data(), 32 * b.size(), hipMemcpyHostToDevice, q));
+        GG_HIP(hipStreamSynchronize(q));  // host vectors
+    };
+    blinded(pk->can[3], bp[3], pk->bz, s[0]);
+    zero(pk->q1.p, nb3, s[0]);
+    const FrB zu = eval_dev(pk, F(pk->bz), n + 3, zeta * pk->omega, F(pk->q1), F(pk->vals), 0, s[0]);
+    P.zs_value = zu;
+    std::future<BJac> fzs = std::async(msm_policy(), [&] {
+        GG_HIP(hipSetDevice(pk->device));
+        return commit_kzg(pk, 0, F(pk->q1), s[0]);
+    });
+    // ---- foldH (prove.go:670-705) on s[2]
+    const FrB zp = pow_u64(zeta, n + 2);
+    zero(pk->fold.p, nb3, s[2]);
+    plk::fold_h(F(pk->cres), n, zp, F(pk->fold), s[2]);
+    BJac fhd = jac_add(jac_add(BJac::from_affine(P.h[0]), jmul(P.h[1], zp)), jmul(P.h[2], zp * zp));
+    const BAff folded_digest = to_aff(fhd);
+    // ---- evaluations at zeta (blinded L, R, O; S1, S2; Qcp_i) on s[1]
+    for (int k = 0; k < 3; k++) blinded(pk->can[k], bp[k], pk->bl[k], s[1]);
+    FrB lz[3];
+    for (int k = 0; k < 3; k++) lz[k] = eval_dev(pk, F(pk->bl[k]), n + 2, zeta, nullptr, F(pk->vals) + 1 + k, 1, s[1]);
+    const FrB s1z = eval_dev(pk, F(pk->reg[gg_plonk_pk::S1]), n, zeta, nullptr, F(pk->vals) + 4, 1, s[1]);
+    const FrB s2z = eval_dev(pk, F(pk->reg[gg_plonk_pk::S2]), n, zeta, nullptr, F(pk->vals) + 5, 1, s[1]);
+    std::vector<FrB> qcpz(n_cmt);
+    for (int j = 0; j < n_cmt; j++) qcpz[j] = eval_dev(pk, F(pk->qcp_reg[j]), n, zeta, nullptr, F(pk->vals) + 6 + j, 1, s[1]);
+    // ---- computeLinearizedPolynomial (prove.go:1289-1389) on s[1]
+    {
+        const FrB l = lz[0], r = lz[1], o = lz[2];
+        FrB sa = (s1z * beta + l + gamma) * (s2z * beta + r + gamma) * zu * beta;
+        const FrB uz = zeta * pk->u, uuz = uz * pk->u;
+        FrB sb = (beta * zeta + l + gamma) * (beta * uz + r + gamma) * (beta * uuz + o + gamma);
+        sb = -sb;
+        const FrB lag = zn1 * inverse(zeta - FrB::one()) * alpha * alpha * pk->n_inv;
+        dcopy(pk->lin.p, pk->bz.p, nb3, s[1]);  // bz is complete: openZ's Horner synchronised s[0]
+        plk::LinParams LP{};
+        LP.z = F(pk->lin);
+        LP.nz = n + 3;
+        LP.s3 = F(pk->reg[gg_plonk_pk::S3]);
+        LP.ns3 = n;
+        LP.ql = F(pk->reg[gg_plonk_pk::QL]);
+        LP.qr = F(pk->reg[gg_plonk_pk::QR]);
+        LP.qm = F(pk->reg[gg_plonk_pk::QM]);
+        LP.qo = F(pk->reg[gg_plonk_pk::QO]);
+        LP.qk = F(pk->reg[gg_plonk_pk::QK]);
+        LP.nq = n;
+        LP.ncmt = n_cmt;
+        for (int j = 0; j < n_cmt; j++) {
+            LP.pi2[j] = F(pk->pi_reg[j]);
+            LP.qcp[j] = qcpz[j];
+        }
+        LP.s1 = sa;
+        LP.s2 = sb;
+        LP.alpha = alpha;
+        LP.l = l;
+        LP.r = r;
+        LP.rl = l * r;
+        LP.o = o;
+        LP.lag = lag;
+        plk::linearized(LP, s[1]);
+    }
+    mark();
+    const BAff lin_digest = to_aff(red(pk, commit_kzg(pk, 1, F(pk->lin), s[1])));
+    mark();
+    // ---- batchOpening: kzg.BatchOpenSinglePoint at zeta (prove.go:777-835)
+    GG_HIP(hipStreamSynchronize(s[2]));  // folded H
+    std::vector<std::pair<const FrB*, size_t>> polys = {
+        {F(pk->fold), n + 2}, {F(pk->lin), n + 3}, {F(pk->bl[0]), n + 2}, {F(pk->bl[1]), n + 2},
+        {F(pk->bl[2]), n + 2}, {F(pk->reg[gg_plonk_pk::S1]), n}, {F(pk->reg[gg_plonk_pk::S2]), n}};
+    for (int j = 0; j < n_cmt; j++) polys.push_back({F(pk->qcp_reg[j]), n});
+    std::vector<BAff> digests = {folded_digest, lin_digest, P.lro[0], P.lro[1], P.lro[2], pk->vkS[0], pk->vkS[1]};
+    for (int j = 0; j < n_cmt; j++) digests.push_back(pk->vkQcp[j]);
+    P.claimed.resize(polys.size());
+    P.claimed[0] = eval_dev(pk, polys[0].first, polys[0].second, zeta, nullptr, F(pk->vals) + 16, 2, s[2]);
+    P.claimed[1] = eval_dev(pk, polys[1].first, polys[1].second, zeta, nullptr, F(pk->vals) + 17, 2, s[2]);
+    for (int k = 0; k < 3; k++) P.claimed[2 + k] = lz[k];
+    P.claimed[5] = s1z;
+    P.claimed[6] = s2z;
+    for (int j = 0; j < n_cmt; j++) P.claimed[7 + j] = qcpz[j];
+    // deriveGamma of kzg (gnark-crypto [ext]): point, digests (Marshal), claimed values, Z(w zeta)
+    Transcript fg({"gamma"}, fh);
+    {
+        uint8_t b[48];
+        fr_marshal(zeta, b);
+        fg.bind("gamma", b, 32);
+        for (auto& d : digests) { g1_marshal(d, b); fg.bind("gamma", b, 48); }
+        for (auto& c : P.claimed) { fr_marshal(c, b); fg.bind("gamma", b, 32); }
+        fr_marshal(zu, b);
+        fg.bind("gamma", b, 32);
+    }
+    const FrB gf = fg.compute("gamma");
+    FrB fe = P.claimed.back();
+    for (size_t i = P.claimed.size() - 1; i-- > 0;) fe = fe * gf + P.claimed[i];
+    // folded polynomial sum_i gamma^i p_i, then the quotient (f - f(zeta)) / (X - zeta)
+    zero(pk->q2.p, nb3, s[2]);
+    dcopy(pk->q2.p, polys[0].first, 32 * polys[0].second, s[2]);
+    FrB gp = gf;
+    for (size_t i = 1; i < polys.size(); i++) {
+        plk::axpy(F(pk->q2), polys[i].first, polys[i].second, gp, s[2]);
+        gp = gp * gf;
+    }
+    zero(pk->fold.p, nb3, s[2]);  // reuse as the batch quotient (n + 2 of n + 3)
+    const FrB fv = eval_dev(pk, F(pk->q2), n + 3, zeta, F(pk->fold), F(pk->vals) + 18, 2, s[2]);
+    GG_CHECK(fv == fe, GG_ERR_INTERNAL, "batch opening: folded evaluation mismatch");
+    P.batched_h = to_aff(red(pk, commit_kzg(pk, 2, F(pk->fold), s[2])));
+    P.zs_h = to_aff(red(pk, fzs.get()));
+    mark();
+    for (hipStream_t q : pk->s) GG_HIP(hipStreamSynchronize(q));
+}
+
+}  // namespace
+
+// ============================================================== C ABI
+// cumulative stage ends (ms) of the last gg_plonk_prove on this thread
+static thread_local double g_plonk_ms[8];
+
+extern "C" int gg_plonk_pk_create(int log_n, int log_big, const void* omega_mont, const void* omega_big_mont,
+                                  const void* coset_shift_mont, const void* kzg_g1, size_t n_kzg,
+                                  const void* kzg_lagrange_g1, const void* const* trace, const void* const* qcp,
+                                  int n_cmt, const int64_t* perm, size_t nb_public,
+                                  const uint64_t* commitment_constraint_indexes, const void* vk_digests,
+                                  gg_plonk_pk_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out, GG_ERR_INVALID_ARG, "null out");
+    std::unique_ptr<gg_plonk_pk> pk(new gg_plonk_pk());
+    plonk_pk_build(pk.get(), log_n, log_big, omega_mont, omega_big_mont, coset_shift_mont, kzg_g1, n_kzg,
+                   kzg_lagrange_g1, trace, qcp, n_cmt, perm, nb_public, commitment_constraint_indexes,
+                   vk_digests, 0, 1, nullptr, nullptr);
+    *out = pk.release();
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_pk_create_shard(int log_n, int log_big, const void* omega_mont, const void* omega_big_mont,
+                                        const void* coset_shift_mont, const void* kzg_g1, size_t n_kzg,
+                                        const void* kzg_lagrange_g1, const void* const* trace,
+                                        const void* const* qcp, int n_cmt, const int64_t* perm, size_t nb_public,
+                                        const uint64_t* commitment_constraint_indexes, const void* vk_digests,
+                                        int rank, int world, gg_g1_reduce_fn reduce, void* reduce_ctx,
+                                        gg_plonk_pk_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out, GG_ERR_INVALID_ARG, "null out");
+    std::unique_ptr<gg_plonk_pk> pk(new gg_plonk_pk());
+    plonk_pk_build(pk.get(), log_n, log_big, omega_mont, omega_big_mont, coset_shift_mont, kzg_g1, n_kzg,
+                   kzg_lagrange_g1, trace, qcp, n_cmt, perm, nb_public, commitment_constraint_indexes,
+                   vk_digests, rank, world, reduce, reduce_ctx);
+    *out = pk.release();
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_pk_release(gg_plonk_pk_t pk) {
+    GG_CAPI_BEGIN
+    delete pk;
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_pk_vk(gg_plonk_pk_t pk, void* out, size_t cap) {
+    GG_CAPI_BEGIN
+    GG_CHECK(pk && out, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(cap >= 96 * (size_t)(8 + pk->n_cmt), GG_ERR_INVALID_ARG, "vk buffer too small");
+    uint8_t* o = (uint8_t*)out;
+    for (int k = 0; k < 3; k++) memcpy(o + 96 * k, &pk->vkS[k], 96);
+    for (int k = 0; k < 5; k++) memcpy(o + 96 * (3 + k), &pk->vkQ[k], 96);
+    for (int i = 0; i < pk->n_cmt; i++) memcpy(o + 96 * (8 + i), &pk->vkQcp[i], 96);
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_commit_lagrange(gg_plonk_pk_t pk, const void* values, int on_device, void* out_aff) {
+    GG_CAPI_BEGIN
+    GG_CHECK(pk && values && out_aff, GG_ERR_INVALID_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(pk->mu);
+    hipStream_t st = pk->s[3];
+    up(pk->pad.p, values, 32 * pk->n, on_device != 0, st);
+    BAff a = to_aff(red(pk, msm_jac(pk, pk->kzg_lag, 2, F(pk->pad), st)));
+    memcpy(out_aff, &a, 96);
+    GG_CAPI_END
+}
+
+extern "C" size_t gg_plonk_proof_size(int n_cmt) {
+    return 96 * (3 + 1 + 3 + (size_t)n_cmt + 1 + 1) + 32 * (7 + (size_t)n_cmt) + 32;
+}
+
+extern "C" int gg_plonk_prove(gg_plonk_pk_t pk, const void* l, const void* r, const void* o, int inputs_on_device,
+                              const void* public_witness, size_t nb_public, const void* const* cmt_values,
+                              const void* cmt_digests, const void* cmt_hashed, int n_cmt, const void* blinding,
+                              gg_hash_fn challenge_hash, void* challenge_ctx, gg_hash_fn folding_hash,
+                              void* folding_ctx, void* proof_out, size_t proof_cap) {
+    GG_CAPI_BEGIN
+    GG_CHECK(pk && l && r && o && proof_out, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(nb_public == pk->nb_public, GG_ERR_INVALID_ARG, "len(public witness) != vk.NbPublicVariables");
+    GG_CHECK(nb_public == 0 || public_witness, GG_ERR_INVALID_ARG, "null public witness");
+    GG_CHECK(n_cmt == pk->n_cmt, GG_ERR_INVALID_ARG, "BSB22 commitment count differs from the key's");
+    GG_CHECK(n_cmt == 0 || (cmt_values && cmt_digests && cmt_hashed), GG_ERR_INVALID_ARG,
+             "null BSB22 commitment data");
+    GG_CHECK(proof_cap >= gg_plonk_proof_size(n_cmt), GG_ERR_INVALID_ARG, "proof buffer too small");
+    std::lock_guard<std::mutex> lk(pk->mu);
+    GG_HIP(hipSetDevice(pk->device));
+    std::vector<FrB> pub(nb_public), hashed(n_cmt), blind;
+    if (nb_public) memcpy(pub.data(), public_witness, 32 * nb_public);
+    if (n_cmt) memcpy(hashed.data(), cmt_hashed, 32 * (size_t)n_cmt);
+    std::vector<BAff> dg(n_cmt);
+    if (n_cmt) memcpy(dg.data(), cmt_digests, 96 * (size_t)n_cmt);
+    if (blinding) {
+        blind.resize(9);
+        memcpy(blind.data(), blinding, 9 * 32);
+    }
+    const void* lro[3] = {l, r, o};
+    PlonkProof P;
+    double tms[8] = {0};
+    prove(pk, lro, inputs_on_device != 0, pub.data(), nb_public, cmt_values, dg.data(), hashed.data(), n_cmt,
+          blinding ? blind.data() : nullptr, Hasher{challenge_hash, challenge_ctx},
+          Hasher{folding_hash, folding_ctx}, P, tms);
+    uint8_t* w = (uint8_t*)proof_out;
+    auto put = [&](const void* src, size_t b) {
+        memcpy(w, src, b);
+        w += b;
+    };
+    for (auto& p : P.lro) put(&p, 96);
+    put(&P.z, 96);
+    for (auto& p : P.h) put(&p, 96);
+    for (auto& p : P.bsb22) put(&p, 96);
+    put(&P.batched_h, 96);
+    for (auto& c : P.claimed) put(c.v, 32);
+    put(&P.zs_h, 96);
+    put(P.zs_value.v, 32);
+    memcpy(g_plonk_ms, tms, sizeof(tms));
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_last_timings(double* ms, int cap) {
+    GG_CAPI_BEGIN
+    GG_CHECK(ms && cap >= 0, GG_ERR_INVALID_ARG, "null argument");
+    memcpy(ms, g_plonk_ms, sizeof(double) * (size_t)std::min(cap, 8));
+    GG_CAPI_END
+}

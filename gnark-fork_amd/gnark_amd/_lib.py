@@ -22,6 +22,12 @@ EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, c
                                ctypes.c_size_t)
 
 
+# gg_hash_fn / gg_g1_reduce_fn (include/gnark_amd.h): PlonK transcript hash, KZG partial reduce
+HASH_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                           ctypes.POINTER(ctypes.c_size_t))
+REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)
+
+
 class GnarkAmdError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"gnark_amd error {code}: {msg}")
@@ -97,6 +103,14 @@ def _load():
                                       P, P, P, P, S, I, I, P, P], I),
         "gg_plonk_divide_by_xn_minus_one": ([P, S, P, P], I),
         "gg_bls12_381_fr_batch_invert": ([P, S, P], I),
+        "gg_plonk_pk_create": ([I, I, P, P, P, P, S, P, PP, PP, I, P, S, P, P, PP], I),
+        "gg_plonk_pk_create_shard": ([I, I, P, P, P, P, S, P, PP, PP, I, P, S, P, P, I, I, REDUCE_FN, P, PP], I),
+        "gg_plonk_pk_release": ([P], I),
+        "gg_plonk_pk_vk": ([P, P, S], I),
+        "gg_plonk_commit_lagrange": ([P, P, I, P], I),
+        "gg_plonk_proof_size": ([I], S),
+        "gg_plonk_prove": ([P, P, P, P, I, P, S, PP, P, P, I, P, HASH_FN, P, HASH_FN, P, P, S], I),
+        "gg_plonk_last_timings": ([ctypes.POINTER(ctypes.c_double), I], I),
         "gg_profile_enable": ([I], I),
         "gg_profile_get": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)], I),
@@ -126,7 +140,9 @@ EXPORTED = [
     "gg_plonk_linearized", "gg_copy_device", "gg_memset_device", "gg_bls12_381_fr_bit_reverse",
     "gg_bls12_381_fr_axpy", "gg_bls12_381_g1_scalar_mul", "gg_fr_from_canonical_be",
     "gg_fr_to_canonical_be", "gg_groth16_last_timings_ex",
-    "gg_groth16_pk_base_info",
+    "gg_groth16_pk_base_info", "gg_plonk_pk_create", "gg_plonk_pk_create_shard", "gg_plonk_pk_release",
+    "gg_plonk_pk_vk", "gg_plonk_commit_lagrange", "gg_plonk_proof_size", "gg_plonk_prove",
+    "gg_plonk_last_timings",
 ]
 
 

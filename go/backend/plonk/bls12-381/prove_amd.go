@@ -1,0 +1,242 @@
+//go:build amd
+
+// MI355X path of plonk.Prove for BLS12-381: a file of package plonk
+// (backend/plonk/bls12-381) so it reads pk.trace / pk.Kzg / pk.KzgLagrange
+// directly.  Prove (prove.go:116) dispatches here when the prover option
+// WithAMDAcceleration() / WithIcicleAcceleration() is set (INTEGRATION.md §4).
+// The solver stays gnark's (prove.go:365-395) with the BSB22 hint committing on
+// the GPU; everything after Solve -- prove.go:116-176's errgroup DAG -- is one
+// gg_plonk_prove call.  Source only here (no Go toolchain in the build image).
+package plonk
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../../../include
+#cgo LDFLAGS: -L${SRCDIR}/../../../../gnark-fork_amd/lib -lgnark_amd -Wl,-rpath,${SRCDIR}/../../../../gnark-fork_amd/lib
+#include <stdlib.h>
+#include "gnark_amd.h"
+extern int ggGoHash(void *ctx, void *data, size_t len, void *out, size_t *out_len);
+static int gg_go_hash(void *ctx, const void *data, size_t len, void *out, size_t *out_len) {
+	return ggGoHash(ctx, (void *)data, len, out, out_len);
+}
+static gg_hash_fn gg_go_hash_fn(void) { return gg_go_hash; }
+*/
+import "C"
+
+import (
+	"errors"
+	"fmt"
+	"hash"
+	"math/big"
+	"runtime/cgo"
+	"sync"
+	"unsafe"
+
+	curve "github.com/consensys/gnark-crypto/ecc/bls12-381"
+	"github.com/consensys/gnark-crypto/ecc/bls12-381/fr"
+	"github.com/consensys/gnark-crypto/ecc/bls12-381/fr/hash_to_field"
+	"github.com/consensys/gnark-crypto/ecc/bls12-381/fr/iop"
+	"github.com/consensys/gnark/backend"
+	"github.com/consensys/gnark/backend/witness"
+	"github.com/consensys/gnark/constraint"
+	cs "github.com/consensys/gnark/constraint/bls12-381"
+	"github.com/consensys/gnark/constraint/solver"
+	fcs "github.com/consensys/gnark/frontend/cs"
+)
+
+// HasAMD mirrors icicle's HasIcicle.
+const HasAMD = true
+
+func amdError() error { return fmt.Errorf("gnark_amd: %s", C.GoString(C.gg_last_error())) }
+
+// device keys, one per *ProvingKey (HBM-resident; released by ReleaseAMD)
+var amdKeys sync.Map
+
+func (pk *ProvingKey) amdKey() (C.gg_plonk_pk_t, error) {
+	if h, ok := amdKeys.Load(pk); ok {
+		return h.(C.gg_plonk_pk_t), nil
+	}
+	n := pk.Domain[0].Cardinality
+	logN, logBig := 0, 0
+	for (uint64(1) << logN) < n {
+		logN++
+	}
+	for (uint64(1) << logBig) < pk.Domain[1].Cardinality {
+		logBig++
+	}
+	tr := [8]unsafe.Pointer{}
+	for i, p := range []*iop.Polynomial{pk.trace.Ql, pk.trace.Qr, pk.trace.Qm, pk.trace.Qo, pk.trace.Qk,
+		pk.trace.S1, pk.trace.S2, pk.trace.S3} {
+		tr[i] = unsafe.Pointer(&p.Coefficients()[0]) // canonical regular after Setup (setup.go:229-240)
+	}
+	qcp := make([]unsafe.Pointer, len(pk.trace.Qcp)+1)
+	for i, p := range pk.trace.Qcp {
+		qcp[i] = unsafe.Pointer(&p.Coefficients()[0])
+	}
+	idx := append(pk.Vk.CommitmentConstraintIndexes, 0)
+	vk := make([]curve.G1Affine, 0, 8+len(pk.Vk.Qcp))
+	vk = append(vk, pk.Vk.S[0], pk.Vk.S[1], pk.Vk.S[2], pk.Vk.Ql, pk.Vk.Qr, pk.Vk.Qm, pk.Vk.Qo, pk.Vk.Qk)
+	vk = append(vk, pk.Vk.Qcp...)
+	// the C side copies everything it needs before returning (cgo pointer rules)
+	ctr := C.malloc(C.size_t(8 * unsafe.Sizeof(uintptr(0))))
+	defer C.free(ctr)
+	copy(unsafe.Slice((*unsafe.Pointer)(ctr), 8), tr[:])
+	cqcp := C.malloc(C.size_t(len(qcp)) * C.size_t(unsafe.Sizeof(uintptr(0))))
+	defer C.free(cqcp)
+	copy(unsafe.Slice((*unsafe.Pointer)(cqcp), len(qcp)), qcp)
+	var h C.gg_plonk_pk_t
+	rc := C.gg_plonk_pk_create(C.int(logN), C.int(logBig),
+		unsafe.Pointer(&pk.Domain[0].Generator), unsafe.Pointer(&pk.Domain[1].Generator),
+		unsafe.Pointer(&pk.Domain[0].FrMultiplicativeGen),
+		unsafe.Pointer(&pk.Kzg.G1[0]), C.size_t(len(pk.Kzg.G1)), unsafe.Pointer(&pk.KzgLagrange.G1[0]),
+		(*unsafe.Pointer)(ctr), (*unsafe.Pointer)(cqcp), C.int(len(pk.trace.Qcp)),
+		(*C.int64_t)(unsafe.Pointer(&pk.trace.S[0])), C.size_t(pk.Vk.NbPublicVariables),
+		(*C.uint64_t)(unsafe.Pointer(&idx[0])), unsafe.Pointer(&vk[0]), &h)
+	if rc != C.GG_OK {
+		return nil, amdError()
+	}
+	if old, loaded := amdKeys.LoadOrStore(pk, h); loaded {
+		C.gg_plonk_pk_release(h)
+		return old.(C.gg_plonk_pk_t), nil
+	}
+	return h, nil
+}
+
+// ReleaseAMD frees the HBM-resident copy of pk.
+func (pk *ProvingKey) ReleaseAMD() {
+	if h, ok := amdKeys.LoadAndDelete(pk); ok {
+		C.gg_plonk_pk_release(h.(C.gg_plonk_pk_t))
+	}
+}
+
+//export ggGoHash
+func ggGoHash(ctx unsafe.Pointer, data unsafe.Pointer, n C.size_t, out unsafe.Pointer, outLen *C.size_t) C.int {
+	h := cgo.Handle(ctx).Value().(hash.Hash)
+	h.Reset()
+	h.Write(C.GoBytes(data, C.int(n)))
+	d := h.Sum(nil)
+	h.Reset()
+	if C.size_t(len(d)) > *outLen {
+		return 1
+	}
+	copy(unsafe.Slice((*byte)(out), len(d)), d)
+	*outLen = C.size_t(len(d))
+	return 0
+}
+
+// proveAMD replaces prove.go:129-176 after NewProverConfig.
+func proveAMD(spr *cs.SparseR1CS, pk *ProvingKey, fullWitness witness.Witness, opt *backend.ProverConfig) (*Proof, error) {
+	h, err := pk.amdKey()
+	if err != nil {
+		return nil, err
+	}
+	if opt.HashToFieldFn == nil {
+		opt.HashToFieldFn = hash_to_field.New([]byte("BSB22-Plonk"))
+	}
+	proof := &Proof{}
+	commitmentInfo := spr.CommitmentInfo.(constraint.PlonkCommitments)
+	nCmt := len(commitmentInfo)
+	commitmentVal := make([]fr.Element, nCmt)
+	committed := make([][]fr.Element, nCmt)
+	proof.Bsb22Commitments = make([]curve.G1Affine, nCmt)
+	// bsb22Hint (prove.go:316-352) with the commitment on the GPU
+	bsb22ID := solver.GetHintID(fcs.Bsb22CommitmentComputePlaceholder)
+	opt.SolverOpts = append(opt.SolverOpts, solver.OverrideHint(bsb22ID, func(_ *big.Int, ins, outs []*big.Int) error {
+		commDepth := int(ins[0].Int64())
+		ins = ins[1:]
+		info := commitmentInfo[commDepth]
+		vals := make([]fr.Element, pk.Domain[0].Cardinality)
+		offset := spr.GetNbPublicVariables()
+		for i := range ins {
+			vals[offset+info.Committed[i]].SetBigInt(ins[i])
+		}
+		if _, err := vals[offset+info.CommitmentIndex].SetRandom(); err != nil {
+			return err
+		}
+		if _, err := vals[offset+spr.GetNbConstraints()-1].SetRandom(); err != nil {
+			return err
+		}
+		if C.gg_plonk_commit_lagrange(h, unsafe.Pointer(&vals[0]), 0, unsafe.Pointer(&proof.Bsb22Commitments[commDepth])) != C.GG_OK {
+			return amdError()
+		}
+		committed[commDepth] = vals
+		opt.HashToFieldFn.Write(proof.Bsb22Commitments[commDepth].Marshal())
+		hashBts := opt.HashToFieldFn.Sum(nil)
+		opt.HashToFieldFn.Reset()
+		nbBuf := fr.Bytes
+		if opt.HashToFieldFn.Size() < fr.Bytes {
+			nbBuf = opt.HashToFieldFn.Size()
+		}
+		commitmentVal[commDepth].SetBytes(hashBts[:nbBuf])
+		commitmentVal[commDepth].BigInt(outs[0])
+		return nil
+	}))
+	if spr.GkrInfo.Is() { // setupGKRHints (prove.go:354-361)
+		var gkrData cs.GkrSolvingData
+		opt.SolverOpts = append(opt.SolverOpts,
+			solver.OverrideHint(spr.GkrInfo.SolveHintID, cs.GkrSolveHint(spr.GkrInfo, &gkrData)),
+			solver.OverrideHint(spr.GkrInfo.ProveHintID, cs.GkrProveHint(spr.GkrInfo.HashName, &gkrData)))
+	}
+	_solution, err := spr.Solve(fullWitness, opt.SolverOpts...)
+	if err != nil {
+		return nil, err
+	}
+	sol := _solution.(*cs.SparseR1CSSolution)
+	w, ok := fullWitness.Vector().(fr.Vector)
+	if !ok {
+		return nil, witness.ErrInvalidWitness
+	}
+	nbPub := len(spr.Public)
+	cv := C.malloc(C.size_t(nCmt+1) * C.size_t(unsafe.Sizeof(uintptr(0))))
+	defer C.free(cv)
+	cvs := unsafe.Slice((*unsafe.Pointer)(cv), nCmt+1)
+	for i := range committed {
+		cvs[i] = C.CBytes(unsafe.Slice((*byte)(unsafe.Pointer(&committed[i][0])), len(committed[i])*fr.Bytes))
+		defer C.free(cvs[i])
+	}
+	hc := cgo.NewHandle(opt.ChallengeHash)
+	defer hc.Delete()
+	hf := cgo.NewHandle(opt.KZGFoldingHash)
+	defer hf.Delete()
+	size := C.gg_plonk_proof_size(C.int(nCmt))
+	out := make([]byte, size)
+	var pubPtr, dgPtr, hvPtr unsafe.Pointer
+	if nbPub > 0 {
+		pubPtr = unsafe.Pointer(&w[0])
+	}
+	if nCmt > 0 {
+		dgPtr = unsafe.Pointer(&proof.Bsb22Commitments[0])
+		hvPtr = unsafe.Pointer(&commitmentVal[0])
+	}
+	rc := C.gg_plonk_prove(h, unsafe.Pointer(&sol.L[0]), unsafe.Pointer(&sol.R[0]), unsafe.Pointer(&sol.O[0]), 0,
+		pubPtr, C.size_t(nbPub), (*unsafe.Pointer)(cv), dgPtr, hvPtr, C.int(nCmt), nil,
+		C.gg_go_hash_fn(), unsafe.Pointer(uintptr(hc)), C.gg_go_hash_fn(), unsafe.Pointer(uintptr(hf)),
+		unsafe.Pointer(&out[0]), size)
+	if rc != C.GG_OK {
+		return nil, amdError()
+	}
+	// proof layout: include/gnark_amd.h gg_plonk_prove (gnark-crypto memory layout)
+	o := 0
+	g1 := func(p *curve.G1Affine) { *p = *(*curve.G1Affine)(unsafe.Pointer(&out[o])); o += 96 }
+	frv := func(e *fr.Element) { *e = *(*fr.Element)(unsafe.Pointer(&out[o])); o += 32 }
+	for i := 0; i < 3; i++ {
+		g1(&proof.LRO[i])
+	}
+	g1(&proof.Z)
+	for i := 0; i < 3; i++ {
+		g1(&proof.H[i])
+	}
+	for i := 0; i < nCmt; i++ {
+		g1(&proof.Bsb22Commitments[i])
+	}
+	g1(&proof.BatchedProof.H)
+	proof.BatchedProof.ClaimedValues = make([]fr.Element, 7+nCmt)
+	for i := range proof.BatchedProof.ClaimedValues {
+		frv(&proof.BatchedProof.ClaimedValues[i])
+	}
+	g1(&proof.ZShiftedOpening.H)
+	frv(&proof.ZShiftedOpening.ClaimedValue)
+	if o != len(out) {
+		return nil, errors.New("gnark_amd: proof size mismatch")
+	}
+	return proof, nil
+}

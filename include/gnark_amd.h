@@ -54,6 +54,12 @@ typedef struct gg_domain *gg_domain_t;
 typedef struct gg_msm_base *gg_msm_base_t;
 typedef struct gg_groth16_pk *gg_groth16_pk_t;
 typedef struct gg_hshard *gg_hshard_t;
+typedef struct gg_plonk_pk *gg_plonk_pk_t;
+/* One-shot hash for Fiat-Shamir transcripts: out[0..*out_len) = H(data[0..len)),
+ * *out_len = capacity of out on entry (128 B), digest length on return; 0 = ok.
+ * A Go caller wraps its hash.Hash (Reset, Write, Sum).  NULL = SHA-256, gnark's
+ * default ChallengeHash / KZGFoldingHash (backend/backend.go:74-75). */
+typedef int (*gg_hash_fn)(void *ctx, const void *data, size_t len, void *out, size_t *out_len);
 /* All-to-all exchange supplied by the caller's transport (RCCL over xGMI via
  * torch.distributed, or a Go RCCL binding): chunk r (bytes_per_rank bytes) of
  * send_dev goes to rank r, chunk k of recv_dev comes from rank k.  Device
@@ -340,6 +346,68 @@ int gg_plonk_fold_h(const void *h_dev, size_t n_small, const void *zeta_pow_np2,
 int gg_plonk_linearized(void *blinded_z_dev, size_t nz, const void *s3_dev, size_t ns3,
                         const void *const *q_dev, size_t nq, const void *const *pi2_dev,
                         const void *qcp_zeta, int n_cmt, const void *scalars8, void *hip_stream);
+
+/* ---- PlonK BLS12-381 prover (plonk.Prove after the solver; prove.go:116-1079)
+ * Device-resident proving key: replaces backend/plonk/bls12-381 ProvingKey
+ * (setup.go:88-106) on the GPU.
+ *   log_n, log_big: pk.Domain[0] / Domain[1] sizes (|big| / n in {2, 4, 8});
+ *   omega_mont, omega_big_mont: their generators; coset_shift_mont:
+ *   Domain[0].FrMultiplicativeGen (= vk.CosetShift);
+ *   kzg_g1[n_kzg >= n + 3]: pk.Kzg.G1 (affine 96 B); kzg_lagrange_g1[n]: pk.KzgLagrange.G1;
+ *   trace[8]: pk.trace Ql, Qr, Qm, Qo, Qk (incomplete), S1, S2, S3 in canonical
+ *     regular form (n fr each, host) -- the form Setup leaves them in (setup.go:229-240);
+ *   qcp[n_cmt]: pk.trace.Qcp (canonical); perm: pk.trace.S (3n int64);
+ *   nb_public: vk.NbPublicVariables; commitment_constraint_indexes[n_cmt]:
+ *     vk.CommitmentConstraintIndexes;
+ *   vk_digests (nullable): 96-B affine S[0..2], Ql, Qr, Qm, Qo, Qk, Qcp[..] of pk.Vk;
+ *     NULL = commit them on the GPU (commitTrace, setup.go:229-272). */
+int gg_plonk_pk_create(int log_n, int log_big, const void *omega_mont, const void *omega_big_mont,
+                       const void *coset_shift_mont, const void *kzg_g1, size_t n_kzg,
+                       const void *kzg_lagrange_g1, const void *const *trace, const void *const *qcp,
+                       int n_cmt, const int64_t *perm, size_t nb_public,
+                       const uint64_t *commitment_constraint_indexes, const void *vk_digests,
+                       gg_plonk_pk_t *out);
+int gg_plonk_pk_release(gg_plonk_pk_t pk);
+/* Multi-GPU: rank `rank` of `world` keeps the contiguous slice
+ * [m rank / world, m (rank + 1) / world) of pk.Kzg.G1 (m = n + 3) and of
+ * pk.KzgLagrange.G1 (m = n); every commitment is a partial MSM that
+ * reduce(ctx, jac) turns into the sum over all ranks (BLS12-381 G1Jac, 144 B, in
+ * place; e.g. an RCCL all-gather + exact adds).  reduce is called from the
+ * proving thread in the same order on every rank.  All other work is
+ * replicated (the blinding must be the same on all ranks). */
+typedef int (*gg_g1_reduce_fn)(void *ctx, void *jac_inout);
+int gg_plonk_pk_create_shard(int log_n, int log_big, const void *omega_mont, const void *omega_big_mont,
+                             const void *coset_shift_mont, const void *kzg_g1, size_t n_kzg,
+                             const void *kzg_lagrange_g1, const void *const *trace, const void *const *qcp,
+                             int n_cmt, const int64_t *perm, size_t nb_public,
+                             const uint64_t *commitment_constraint_indexes, const void *vk_digests, int rank,
+                             int world, gg_g1_reduce_fn reduce, void *reduce_ctx, gg_plonk_pk_t *out);
+/* the key's vk digests, 96-B affine each: S[0..2], Ql, Qr, Qm, Qo, Qk, Qcp[0..n_cmt) */
+int gg_plonk_pk_vk(gg_plonk_pk_t pk, void *out, size_t cap);
+/* kzg.Commit(values, pk.KzgLagrange): n Lagrange values (host or device) -> affine 96 B.
+ * The BSB22 solver hint (bsb22Hint, prove.go:316-352) commits through this. */
+int gg_plonk_commit_lagrange(gg_plonk_pk_t pk, const void *values, int on_device, void *out_aff);
+/* bytes of a proof with n_cmt BSB22 commitments (layout below) */
+size_t gg_plonk_proof_size(int n_cmt);
+/* Prove after Solve (prove.go:116-176; the errgroup DAG as HIP streams):
+ *   l, r, o: solution.L, R, O (n fr Lagrange regular, host or device);
+ *   public_witness[nb_public]: fullWitness[:len(spr.Public)] (host, completeQk + bindPublicData);
+ *   BSB22 (n_cmt as the key): cmt_values[i] = the bsb22Hint's committed-value vector (n fr,
+ *     Lagrange, host), cmt_digests = proof.Bsb22Commitments (96 B each), cmt_hashed =
+ *     s.commitmentVal (fr each);
+ *   blinding (nullable): the 9 coefficients of Bl, Br, Bo (2 each) and Bz (3); NULL = random;
+ *   challenge_hash / folding_hash (+ ctx): opts.ChallengeHash / KZGFoldingHash, NULL = SHA-256.
+ * proof_out (gg_plonk_proof_size bytes): affine 96 B / fr 32 B, Montgomery:
+ *   LRO[3] | Z | H[3] | Bsb22Commitments[n_cmt] | BatchedProof.H |
+ *   BatchedProof.ClaimedValues[7 + n_cmt] | ZShiftedOpening.H | ZShiftedOpening.ClaimedValue */
+int gg_plonk_prove(gg_plonk_pk_t pk, const void *l, const void *r, const void *o, int inputs_on_device,
+                   const void *public_witness, size_t nb_public, const void *const *cmt_values,
+                   const void *cmt_digests, const void *cmt_hashed, int n_cmt, const void *blinding,
+                   gg_hash_fn challenge_hash, void *challenge_ctx, gg_hash_fn folding_hash,
+                   void *folding_ctx, void *proof_out, size_t proof_cap);
+/* cumulative stage ends (ms) of the last gg_plonk_prove on this thread: commitToLRO,
+ * Z, quotient, H commitments, linearized, batch opening */
+int gg_plonk_last_timings(double *ms, int cap);
 
 /* ---- witness / fr.Vector binary format (backend/witness/witness.go:15-36)
  * Field elements are serialised as 32-byte big-endian canonical integers; the

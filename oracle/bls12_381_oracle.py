@@ -378,19 +378,57 @@ def linearized(blinded_z, s3, ql, qr, qm, qo, qk, pi2, qcp, s1, s2, alpha, l, r,
 
 
 # ---------------------------------------------------------------- PlonK verifier (trapdoor)
-def g1_marshal(p) -> bytes:
-    """G1Affine.Marshal (RawBytes): X | Y big-endian; infinity = 0x40 | zeros."""
+def g1_raw_bytes(p) -> bytes:
+    """G1Affine.RawBytes (deriveRandomness, verify.go:342-360): X | Y big-endian,
+    infinity = 0x40 | zeros (gnark-crypto mUncompressedInfinity)."""
     if p is INF:
         return bytes([0x40]) + bytes(95)
     return p[0].to_bytes(48, "big") + p[1].to_bytes(48, "big")
 
 
+g1_marshal = g1_raw_bytes  # round-1 name
+
+
+def g1_compress(p) -> bytes:
+    """G1Affine.Marshal = Bytes (bindPublicData verify.go:296-340, kzg deriveGamma):
+    X big-endian with the zcash flags 0x80 (y smallest) / 0xA0 (y largest) / 0xC0
+    (infinity); inverse of g1_decompress_zcash, which the bellman_test.go keys pin."""
+    if p is INF:
+        return bytes([0xC0]) + bytes(47)
+    b = bytearray(p[0].to_bytes(48, "big"))
+    b[0] |= 0xA0 if p[1] > P - p[1] else 0x80
+    return bytes(b)
+
+
+def expand_message_xmd(msg: bytes, dst: bytes, n: int) -> bytes:
+    """RFC 9380 section 5.3.1 with SHA-256 (gnark-crypto ecc/hash.ExpandMsgXmd [ext])."""
+    import hashlib
+    b_in, r_in = 64, 32
+    ell = (n + r_in - 1) // r_in
+    assert ell <= 255 and len(dst) <= 255
+    dst_prime = dst + bytes([len(dst)])
+    b0 = hashlib.sha256(bytes(b_in) + msg + n.to_bytes(2, "big") + b"\x00" + dst_prime).digest()
+    out, bi = b"", b"\x00" * r_in
+    for i in range(1, ell + 1):
+        bi = hashlib.sha256(bytes(x ^ y for x, y in zip(b0, bi)) + bytes([i]) + dst_prime).digest()
+        out += bi
+    return out[:n]
+
+
+def hash_to_field(msg: bytes, dst: bytes = b"BSB22-Plonk") -> int:
+    """gnark-crypto bls12-381 fr.Hash(msg, dst, 1) (hash_to_field.New, the default
+    HashToFieldFn of the PlonK prover/verifier: prove.go:232-234, verify.go:127-129):
+    L = 16 + 32 bytes of expand_message_xmd, big-endian, mod r.  Parity unpinned
+    (gnark-crypto is absent); prover and verifier here share it."""
+    return int.from_bytes(expand_message_xmd(msg, dst, 48), "big") % R
+
+
 class Transcript:
     """gnark-crypto fiat-shamir (restated): challenge i = H(name_i | value_(i-1) | bindings_i)."""
 
-    def __init__(self, *names):
+    def __init__(self, *names, h=None):
         import hashlib
-        self.h = hashlib.sha256
+        self.h = h or hashlib.sha256
         self.order, self.data, self.values = list(names), {n: [] for n in names}, {}
 
     def bind(self, name, b):
@@ -410,7 +448,7 @@ class Transcript:
 
 def _derive(fs, name, *points):
     for p in points:
-        fs.bind(name, g1_marshal(p))
+        fs.bind(name, g1_raw_bytes(p))
     return fs.challenge(name)
 
 
@@ -422,27 +460,48 @@ def _kzg_check_trapdoor(digest, proof_h, point, value, tau) -> bool:
     return lhs == rhs
 
 
-def plonk_verify_trapdoor(proof, vk, tau) -> bool:
-    """backend/plonk/bls12-381 Verify (verify.go:45-290) for a circuit without
-    public inputs or BSB22 commitments; the two KZG batch checks use the SRS
-    trapdoor tau.  proof / vk: plain dicts of affine points (x, y ints) and fr ints:
-      proof: LRO[3], Z, H[3], batched_H, claimed[7], zs_H, zu
-      vk: n, omega, u (coset shift), S[3], Ql, Qr, Qm, Qo, Qk."""
+def plonk_verify_trapdoor(proof, vk, tau, public=(), challenge_hash=None, folding_hash=None) -> bool:
+    """backend/plonk/bls12-381 Verify (verify.go:45-290) with public inputs and
+    BSB22 commitments; the two KZG batch checks use the SRS trapdoor tau.
+    proof / vk: plain dicts of affine points (x, y ints) and fr ints:
+      proof: LRO[3], Z, H[3], batched_H, claimed[7 + ncmt], zs_H, zu, bsb22[ncmt]
+      vk: n, omega, u (coset shift), S[3], Ql, Qr, Qm, Qo, Qk, Qcp[ncmt],
+          nb_public, cmt_idx[ncmt]."""
     n, u = vk["n"], vk["u"]
-    fs = Transcript("gamma", "beta", "alpha", "zeta")
-    for p in list(vk["S"]) + [vk["Ql"], vk["Qr"], vk["Qm"], vk["Qo"], vk["Qk"]]:
-        fs.bind("gamma", g1_marshal(p))
+    qcp = vk.get("Qcp", [])
+    bsb = proof.get("bsb22", [])
+    if len(bsb) != len(qcp) or len(public) != vk.get("nb_public", 0):
+        return False
+    fs = Transcript("gamma", "beta", "alpha", "zeta", h=challenge_hash)
+    for p in list(vk["S"]) + [vk["Ql"], vk["Qr"], vk["Qm"], vk["Qo"], vk["Qk"]] + list(qcp):
+        fs.bind("gamma", g1_compress(p))
+    for x in public:
+        fs.bind("gamma", (x % R).to_bytes(32, "big"))
     gamma = _derive(fs, "gamma", *proof["LRO"])
     beta = _derive(fs, "beta")
-    alpha = _derive(fs, "alpha", proof["Z"])
+    alpha = _derive(fs, "alpha", *bsb, proof["Z"])
     zeta = _derive(fs, "zeta", *proof["H"])
     zn = pow(zeta, n, R)
     lag1 = (zn - 1) * pow(zeta - 1, -1, R) % R * pow(n, -1, R) % R
+    # PI(zeta) = sum_i L_i(zeta) w_i + hashed BSB22 commitments at their rows (verify.go:102-155)
+    w = vk["omega"]
+    pi = 0
+    for i, x in enumerate(public):
+        wi = pow(w, i, R)
+        li = wi * (zn - 1) % R * pow(n * (zeta - wi), -1, R) % R
+        pi = (pi + li * x) % R
+    for j, c in enumerate(bsb):
+        hc = hash_to_field(g1_compress(c))
+        wi = pow(w, vk["nb_public"] + vk["cmt_idx"][j], R)
+        li = wi * (zn - 1) % R * pow(n * (zeta - wi), -1, R) % R
+        pi = (pi + li * hc) % R
     zu = proof["zu"]
-    hq, lin, l, r, o, s1, s2 = proof["claimed"]
+    cl = proof["claimed"]
+    hq, lin, l, r, o, s1, s2 = cl[:7]
+    qcz = cl[7:]
     # quotient identity (verify.go:158-195)
     t = (s1 * beta + l + gamma) * (s2 * beta + r + gamma) % R * (o + gamma) % R * alpha % R * zu % R
-    rhs = (lin + t - lag1 * alpha % R * alpha) % R * pow((zn - 1) % R, -1, R) % R
+    rhs = (lin + pi + t - lag1 * alpha % R * alpha) % R * pow((zn - 1) % R, -1, R) % R
     if hq != rhs:
         return False
     # folded H digest and linearized digest (verify.go:197-250)
@@ -452,23 +511,23 @@ def plonk_verify_trapdoor(proof, vk, tau) -> bool:
     a2 = (beta * zeta + l + gamma) * ((beta * zeta * u + r + gamma) % R) % R * \
         ((beta * zeta * u * u + o + gamma) % R) % R
     a2 = ((-a2) * alpha + lag1 * alpha % R * alpha) % R
-    pts = [vk["Ql"], vk["Qr"], vk["Qm"], vk["Qo"], vk["Qk"], vk["S"][2], proof["Z"]]
-    scs = [l, r, l * r % R, o, 1, a1, a2]
+    pts = list(bsb) + [vk["Ql"], vk["Qr"], vk["Qm"], vk["Qo"], vk["Qk"], vk["S"][2], proof["Z"]]
+    scs = list(qcz) + [l, r, l * r % R, o, 1, a1, a2]
     lin_d = INF
     for p, s in zip(pts, scs):
         lin_d = g1_add(lin_d, g1_mul(p, s))
     # kzg.FoldProof + BatchVerifyMultiPoints (verify.go:252-290), trapdoor checks
-    digests = [fh, lin_d, proof["LRO"][0], proof["LRO"][1], proof["LRO"][2], vk["S"][0], vk["S"][1]]
-    fsg = Transcript("gamma")
+    digests = [fh, lin_d, proof["LRO"][0], proof["LRO"][1], proof["LRO"][2], vk["S"][0], vk["S"][1]] + list(qcp)
+    fsg = Transcript("gamma", h=folding_hash)
     fsg.bind("gamma", (zeta % R).to_bytes(32, "big"))
     for d in digests:
-        fsg.bind("gamma", g1_marshal(d))
-    for c in proof["claimed"]:
+        fsg.bind("gamma", g1_compress(d))
+    for c in cl:
         fsg.bind("gamma", (c % R).to_bytes(32, "big"))
     fsg.bind("gamma", (zu % R).to_bytes(32, "big"))
     gf = fsg.challenge("gamma")
     fd, fy, gp = INF, 0, 1
-    for d, y in zip(digests, proof["claimed"]):
+    for d, y in zip(digests, cl):
         fd = g1_add(fd, g1_mul(d, gp))
         fy = (fy + gp * y) % R
         gp = gp * gf % R

@@ -131,3 +131,28 @@ def test_fold_h_is_evaluation_split():
     folded = bo.fold_h(h, n, zeta)
     # sum_k zeta^(k(n+2)) H_k(X) evaluated at X = zeta equals h(zeta)
     assert bo.evaluate(folded, zeta) == bo.evaluate(h, zeta)
+
+
+def test_g1_marshal_is_zcash_compression():
+    """G1Affine.Marshal (the encoding bindPublicData and kzg's deriveGamma hash,
+    verify.go:296-340) re-creates the reference's own compressed keys byte for
+    byte (backend/groth16/bellman_test.go:19-132), and both encodings keep the
+    gnark-crypto infinity flags."""
+    for h in PINS["g1_compressed"]:
+        raw = bytes.fromhex(h)
+        assert b.g1_compress(b.g1_decompress_zcash(raw)) == raw
+    assert b.g1_compress(b.INF) == bytes([0xC0]) + bytes(47)
+    assert b.g1_raw_bytes(b.INF) == bytes([0x40]) + bytes(95)
+    p = b.g1_mul(b.G1_GEN, 12345)
+    assert b.g1_raw_bytes(p) == p[0].to_bytes(48, "big") + p[1].to_bytes(48, "big")
+
+
+def test_expand_message_xmd_rfc9380_vectors():
+    """expand_message_xmd(SHA-256) against RFC 9380 appendix K.1
+    (DST QUUX-V01-CS02-with-expander-SHA256-128): the hash_to_field of the BSB22
+    commitment value (prove.go:341-348) builds on it."""
+    dst = b"QUUX-V01-CS02-with-expander-SHA256-128"
+    assert b.expand_message_xmd(b"", dst, 0x20).hex() == \
+        "68a985b87eb6b46952128911f2a4412bbc302a9d759667f87f7a21d803f07235"
+    assert b.expand_message_xmd(b"abc", dst, 0x20).hex() == \
+        "d8ccab23b5985ccea865c6c97b6e5b8350e794e603b4b97902f53a8a0d605615"
