@@ -171,7 +171,7 @@ def main():
     # ROOFLINE_PROVES proves with the five tasks run one after another
     # (GG_G16_SERIAL=1), so an event pair brackets the kernel alone -- with five
     # busy streams it would also count the wait for CUs held by the other MSMs.
-    # These are the last k_accum_affine<Fp2> launches of the run; the committed
+    # These are the last k_accum_range<Fp2> launches of the run; the committed
     # rocprof summary reports the average of exactly those dispatches
     # (tools/prof_summary.py --last).
     _lib.profile_enable(True)
@@ -191,12 +191,12 @@ def main():
     g2_ms = kernels["msm_accum_g2"]["avg_ms"]
     alg_bytes = nB2 * (128 + 32)  # |B2| x (G2 affine 128 B + fr 32 B)
     achieved = alg_bytes / (g2_ms * 1e-3) / 1e9 if g2_ms else None
-    traffic, traffic_note = pmc_traffic("k_accum_affine<gg::Fp2>", {"workload": "groth16", "log_n": args.log_n,
+    traffic, traffic_note = pmc_traffic("k_accum_range<gg::Fp2>", {"workload": "groth16", "log_n": args.log_n,
                                                                     "n_gpus": world})
     roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                 "traffic_note": traffic_note,
-                "kernel": "k_accum_affine<Fp2> (G2 bucket accumulation of the B MSM: the longest "
+                "kernel": "k_accum_range<Fp2> (G2 bucket accumulation of the B MSM: the longest "
                           "single launch of the prove)",
                 "algorithmic_bytes_per_launch": alg_bytes, "kernel_avg_ms": g2_ms,
                 "timing": "HIP events on the kernel's launch stream over %d proves run task by task "
@@ -477,7 +477,7 @@ def msm_bench(log_n, rank, world, dist, xdev, barrier, max_over_ranks, steps=20,
            "window_bits": c, "windows": W, "kernel_avg_ms": kern}
     if acc:
         alg = n * 96
-        traffic, note = pmc_traffic("k_accum_affine<gg::Fe<gg::FpCfg> >",
+        traffic, note = pmc_traffic("k_accum_range<gg::Fe<gg::FpCfg> >",
                                     {"log_n": log_n, "window_bits": c, "windows": W})
         res["accum_roofline"] = {"achieved_GBps": alg / (acc * 1e-3) / 1e9,
                                  "frac_hbm": alg / (acc * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -502,6 +502,13 @@ def pmc_traffic(kernel, workload):
             continue
         for k, v in d.get("kernels", {}).items():
             if kernel in k:
+                if "traffic_bytes_raw" in v and "accum" in kernel:
+                    return v["traffic_bytes_raw"], (
+                        f"{os.path.basename(f)}: FETCH_SIZE + WRITE_SIZE per dispatch, no x2 (64-B point "
+                        f"gathers: the guide's x2 is calibrated for 16-B/lane coalesced streams; with x2: "
+                        f"{v['traffic_bytes']:.4g} B); the W precomputed window copies of the fixed-base "
+                        f"tables make the kernel read ~W x the point bytes per scalar (no doublings at "
+                        f"prove time), so traffic >> the algorithmic bytes")
                 return v["traffic_bytes"], (
                     f"{os.path.basename(f)}: FETCH_SIZE x2 + WRITE_SIZE per dispatch; the W "
                     f"precomputed window copies of the fixed-base tables make the kernel read ~W x "

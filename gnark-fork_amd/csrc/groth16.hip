@@ -159,7 +159,8 @@ static void pk_build(gg_groth16_pk* pk, int log_n, const void* omega_mont, const
         for (size_t j = 0; j < nK; j++) memcpy(&dense[(size_t)ik[j] * 64], (const uint8_t*)g1_K + j * 64, 64);
         pk->K = msm_base_create_internal(GG_G1, dense.data(), nw, nullptr, cAK, true);
     }
-    pk->B = msm_base_create_internal(GG_G1, g1_B, nB, ib.data(), 0, false);
+    // B1 shares its sort with the G2 base: the window that suits G2
+    pk->B = msm_base_create_internal(GG_G1, g1_B, nB, ib.data(), choose_c(std::max<size_t>(nB, 1), 128, 255), false);
     pk->B2 = msm_base_create_internal(GG_G2, g2_B, nB, ib.data(), msm_base_window(pk->B), false);
     pk->Z = msm_base_create_internal(GG_G1, g1_Z, nZ, nullptr, 0, false);
     pk->share_AK = msm_same_shape(pk->A, pk->K);

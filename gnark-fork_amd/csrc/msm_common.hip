@@ -97,11 +97,13 @@ int choose_c(size_t n, size_t point_bytes, int total_bits) {
         int c = atoi(e);
         if (c >= 4 && c <= 24) return c;
     }
-    // cost ~ bucket additions (n*W) + ~6 madd-equivalents per bucket (reduction),
-    // with the entries-per-bucket (epb) sweet spot measured on MI355X (2^20:
-    // c=17; 2^22, 2^24: c=20): epb > 512 makes heavy buckets (level-2 trees,
-    // +25 %), epb < 100 leaves short, unbalanced items (+10 %).  Window widths
-    // are balanced (make_windows), so every c is usable.
+    // cost ~ bucket additions (n*W) + per-bucket level-2 / reduction work, fitted
+    // to MI355X sweeps (2^20: c=17; 2^24 G1: c=22; G2 and G1 bases sharing a G2
+    // sort, point_bytes = 128: c=20 -- the Fp2 bucket reduction weighs twice);
+    // epb > 512 (entries per bucket) makes heavy buckets (+25 %).  With balanced
+    // accumulation ranges short buckets cost nothing extra.  Window widths are
+    // balanced (make_windows), so every c is usable.
+    const double per_bucket = point_bytes >= 128 ? 12.0 : 6.0;
     int best = 16;
     double bc = 1e300;
     for (int c = 4; c <= 23; c++) {
@@ -111,8 +113,8 @@ int choose_c(size_t n, size_t point_bytes, int total_bits) {
         if (mem > 48e9) continue;  // precomputed table budget per base
         const double entries = (double)n * W, buckets = (double)(1u << (c - 1));
         const double epb = entries / buckets;
-        double f = 1.0 + (epb > 512 ? 0.25 : 0.0) + (epb < 100 ? 0.10 : 0.0);
-        double cost = entries * f + buckets * 6.0;
+        double f = 1.0 + (epb > 512 ? 0.25 : 0.0);
+        double cost = entries * f + buckets * per_bucket;
         if (cost < bc) { bc = cost; best = c; }
     }
     return best;
@@ -592,12 +594,12 @@ void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStr
         sort_entries(b, s, scalars_dev, st);
         ps_sort.stop(st);
     }
-    // Accumulation ranges of K sorted entries, one thread each (32, doubled up
-    // to 256 while that still leaves > 4M ranges; MI355X sweep of the item
-    // version: 2^24 best at 56..64).  The fullest bucket's size goes to pinned
+    // Accumulation ranges of K sorted entries, one thread each (32 for small
+    // MSMs, else 64 doubled up to 256 while that leaves > 2M ranges).  The fullest bucket's size goes to pinned
     // memory behind an event while the accumulation runs (no host stall).
-    uint32_t K = 32;
-    while (K < 256 && (size_t)b->W * n / (size_t)K > ((size_t)4 << 20)) K *= 2;
+    const size_t E = (size_t)b->W * n;
+    uint32_t K = E < ((size_t)4 << 20) ? 32 : 64;  // MI355X sweep: 2^20 best at 64, 2^24 at 128
+    while (K < 256 && E / (size_t)K > ((size_t)2 << 20)) K *= 2;
     if (const char* e = getenv("GG_MSM_K1")) K = (uint32_t)std::max(1, atoi(e));
     s->K = K;
     s->ranges_ub = ((size_t)b->W * n + K - 1) / K;

@@ -33,10 +33,14 @@ def main(fdb, wdb, out, workload=None):
         write_b = wk[0] * 1024.0
         res[k] = {"dispatches": max(fk[1], wk[1]),
                   "fetch_bytes_raw": fetch_b, "fetch_bytes_x2": 2.0 * fetch_b,
-                  "write_bytes": write_b, "traffic_bytes": 2.0 * fetch_b + write_b}
+                  "write_bytes": write_b, "traffic_bytes": 2.0 * fetch_b + write_b,
+                  "traffic_bytes_raw": fetch_b + write_b}
     json.dump({"source": [fdb, wdb], "unit": "bytes per dispatch",
                "workload": json.loads(workload) if workload else {},
-               "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 wide-read undercount), WRITE_SIZE KiB x 1024",
+               "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 wide-read undercount, measured for 16-B/lane "
+                             "coalesced streams), WRITE_SIZE KiB x 1024; traffic_bytes_raw: no x2 (the "
+                             "point gathers of the MSM accumulation are 64-B requests, outside the "
+                             "calibrated case)",
                "kernels": res}, open(out, "w"), indent=1)
     for k, v in sorted(res.items(), key=lambda x: -x[1]["traffic_bytes"])[:15]:
         print(f"{k[:60]:60s} {v['dispatches']:5d} fetch {v['fetch_bytes_x2'] / 1e6:10.2f} MB write {v['write_bytes'] / 1e6:10.2f} MB")
