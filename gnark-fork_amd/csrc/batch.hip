@@ -127,11 +127,13 @@ extern "C" int gg_batch_scalar_mul(int group, const void* base_aff, const void* 
                                    int scalars_on_device, void* out_aff, int out_on_device) {
     GG_CAPI_BEGIN
     GG_CHECK(base_aff && out_aff, GG_ERR_INVALID_ARG, "null argument");
-    GG_CHECK(group == GG_G1 || group == GG_G2 || group == GG_BLS12_381_G1, GG_ERR_INVALID_ARG, "bad group");
+    GG_CHECK(group == GG_G1 || group == GG_G2 || group == GG_BLS12_381_G1 || group == GG_BLS12_381_G2,
+             GG_ERR_INVALID_ARG, "bad group");
     if (n == 0) return GG_OK;
     GG_CHECK(scalars, GG_ERR_INVALID_ARG, "null scalars");
     if (group == GG_G1) batch_mul<Fp, FrCfg>(base_aff, scalars, n, scalars_on_device, out_aff, out_on_device);
     else if (group == GG_G2) batch_mul<Fp2, FrCfg>(base_aff, scalars, n, scalars_on_device, out_aff, out_on_device);
-    else batch_mul<FpBls, FrBlsCfg>(base_aff, scalars, n, scalars_on_device, out_aff, out_on_device);
+    else if (group == GG_BLS12_381_G1) batch_mul<FpBls, FrBlsCfg>(base_aff, scalars, n, scalars_on_device, out_aff, out_on_device);
+    else batch_mul<Fp2Bls, FrBlsCfg>(base_aff, scalars, n, scalars_on_device, out_aff, out_on_device);
     GG_CAPI_END
 }

@@ -147,6 +147,24 @@ extern "C" int gg_bls12_381_g1_scalar_mul(const void* p, const void* k, void* ou
     scalar_mul_bytes<FpBls, FrBls>(p, k, out);
     GG_CAPI_END
 }
+extern "C" int gg_bls12_381_g2_jac_to_affine(const void* jac, void* aff) {
+    GG_CAPI_BEGIN
+    GG_CHECK(jac && aff, GG_ERR_INVALID_ARG, "null argument");
+    jac_to_aff_bytes<Fp2Bls>(jac, aff);
+    GG_CAPI_END
+}
+extern "C" int gg_bls12_381_g2_jac_add(const void* a, const void* b, void* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(a && b && out, GG_ERR_INVALID_ARG, "null argument");
+    jac_add_bytes<Fp2Bls>(a, b, out);
+    GG_CAPI_END
+}
+extern "C" int gg_bls12_381_g2_scalar_mul(const void* p, const void* k, void* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(p && k && out, GG_ERR_INVALID_ARG, "null argument");
+    scalar_mul_bytes<Fp2Bls, FrBls>(p, k, out);
+    GG_CAPI_END
+}
 extern "C" int gg_g2_scalar_mul(const void* p, const void* k, void* out) {
     GG_CAPI_BEGIN
     GG_CHECK(p && k && out, GG_ERR_INVALID_ARG, "null argument");

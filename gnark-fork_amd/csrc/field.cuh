@@ -536,4 +536,37 @@ GG_HD Fp2 inverse(const Fp2& a) {
     return Fp2{a.a0 * ni, -(a.a1 * ni)};
 }
 
+// ---------------------------------------------------------------------------
+// Fp2 over BLS12-381 Fp = Fp[u] / (u^2 + 1) (gnark-crypto ecc/bls12-381 E2
+// layout {A0, A1}: 2 x 48 B): the field of the G2 points of a BLS12-381
+// Groth16 key (backend/groth16/bls12-381/setup.go).  Karatsuba product (three
+// 12-limb Montgomery products), complex squaring (two).
+// ---------------------------------------------------------------------------
+struct Fp2Bls {
+    FpBls a0, a1;
+    static GG_HD Fp2Bls zero() { return Fp2Bls{FpBls::zero(), FpBls::zero()}; }
+    static GG_HD Fp2Bls one() { return Fp2Bls{FpBls::one(), FpBls::zero()}; }
+    GG_HD bool is_zero() const { return a0.is_zero() && a1.is_zero(); }
+    GG_HD bool operator==(const Fp2Bls& o) const { return a0 == o.a0 && a1 == o.a1; }
+    GG_HD bool operator!=(const Fp2Bls& o) const { return !(*this == o); }
+};
+GG_HD Fp2Bls operator+(const Fp2Bls& a, const Fp2Bls& b) { return Fp2Bls{a.a0 + b.a0, a.a1 + b.a1}; }
+GG_HD Fp2Bls operator-(const Fp2Bls& a, const Fp2Bls& b) { return Fp2Bls{a.a0 - b.a0, a.a1 - b.a1}; }
+GG_HD Fp2Bls operator-(const Fp2Bls& a) { return Fp2Bls{-a.a0, -a.a1}; }
+GG_HD Fp2Bls dbl(const Fp2Bls& a) { return Fp2Bls{a.a0 + a.a0, a.a1 + a.a1}; }
+GG_HD Fp2Bls operator*(const Fp2Bls& a, const Fp2Bls& b) {
+    const FpBls t0 = a.a0 * b.a0, t1 = a.a1 * b.a1;
+    const FpBls t2 = (a.a0 + a.a1) * (b.a0 + b.a1);
+    return Fp2Bls{t0 - t1, t2 - t0 - t1};
+}
+GG_HD Fp2Bls sqr(const Fp2Bls& a) {
+    const FpBls t0 = (a.a0 + a.a1) * (a.a0 - a.a1);
+    const FpBls t1 = a.a0 * a.a1;
+    return Fp2Bls{t0, t1 + t1};
+}
+GG_HD Fp2Bls inverse(const Fp2Bls& a) {
+    const FpBls ni = inverse(sqr(a.a0) + sqr(a.a1));
+    return Fp2Bls{a.a0 * ni, -(a.a1 * ni)};
+}
+
 }  // namespace gg

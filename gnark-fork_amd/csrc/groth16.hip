@@ -51,13 +51,37 @@ struct DistH {
 
 using namespace gg;
 
+// curve traits of the prover: BN254 (backend/groth16/bn254) and BLS12-381
+// (backend/groth16/bls12-381; prove.go there is the same code over another curve)
+struct CurveBn254 {
+    using FrT = Fr;
+    using G1F = Fp;
+    using G2F = Fp2;
+    static constexpr int curve = GG_CURVE_BN254, g1 = GG_G1, g2 = GG_G2, total_bits = 255;
+};
+struct CurveBls12381 {
+    using FrT = FrBls;
+    using G1F = FpBls;
+    using G2F = Fp2Bls;
+    static constexpr int curve = GG_CURVE_BLS12_381, g1 = GG_BLS12_381_G1, g2 = GG_BLS12_381_G2, total_bits = 256;
+};
+// byte sizes of the curve's affine / Jacobian points
+struct PointSizes {
+    size_t g1a, g2a, g1j, g2j;
+};
+static PointSizes point_sizes(int curve) {
+    if (curve == GG_CURVE_BN254) return {64, 128, 96, 192};
+    return {96, 192, 144, 288};
+}
+
 struct gg_groth16_pk {
+    int curve = GG_CURVE_BN254;
     int log_n = 0;
     size_t n = 0;
     gg_domain_t dom = nullptr;
     gg_msm_base_t A = nullptr, B = nullptr, K = nullptr, Z = nullptr, B2 = nullptr;
-    G1Affine alpha, beta, delta;
-    G2Affine beta2, delta2;
+    // pk.G1.{Alpha, Beta, Delta}, pk.G2.{Beta, Delta} in the curve's affine layout
+    uint8_t alpha[96], beta[96], delta[96], beta2[192], delta2[192];
     size_t n_wires = 0, nb_public = 0;
     // shard of a multi-GPU key: wires [wire_lo, wire_hi), Z positions [z_lo, z_lo + |Z|)
     size_t wire_lo = 0, wire_hi = 0, z_lo = 0, nZ = 0;
@@ -98,7 +122,7 @@ static void ck(int rc) {
 // the shard's wires, likewise g1_B / g2_B; g1_K = the K points whose wires lie
 // in the shard (k_wire_index gives their absolute wire ids; NULL = the default
 // nb_public + j numbering of the full key).
-static void pk_build(gg_groth16_pk* pk, int log_n, const void* omega_mont, const void* coset_gen_mont,
+static void pk_build(gg_groth16_pk* pk, int curve, int log_n, const void* omega_mont, const void* coset_gen_mont,
                      const void* g1_A, size_t nA, const void* g1_B, size_t nB, const void* g1_Z,
                      size_t z_lo, size_t nZ, const void* g1_K, size_t nK, const void* alpha1,
                      const void* beta1, const void* delta1, const void* g2_B, const void* beta2,
@@ -110,6 +134,12 @@ static void pk_build(gg_groth16_pk* pk, int log_n, const void* omega_mont, const
     GG_CHECK(nb_public <= n_wires, GG_ERR_INVALID_ARG, "nb_public > n_wires");
     GG_CHECK(log_n >= 0 && log_n <= 28, GG_ERR_INVALID_ARG, "log_n out of range");
     GG_CHECK(lo <= hi && hi <= n_wires, GG_ERR_INVALID_ARG, "bad wire shard range");
+    GG_CHECK(curve == GG_CURVE_BN254 || curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "bad curve");
+    const PointSizes ps = point_sizes(curve);
+    const int g1 = curve == GG_CURVE_BN254 ? GG_G1 : GG_BLS12_381_G1;
+    const int g2 = curve == GG_CURVE_BN254 ? GG_G2 : GG_BLS12_381_G2;
+    const int tbits = curve == GG_CURVE_BN254 ? 255 : 256;
+    pk->curve = curve;
     pk->log_n = log_n;
     pk->n = (size_t)1 << log_n;
     pk->n_wires = n_wires;
@@ -122,12 +152,12 @@ static void pk_build(gg_groth16_pk* pk, int log_n, const void* omega_mont, const
     GG_CHECK(z_lo + nZ <= nz_full, GG_ERR_INVALID_ARG,
              "Z shard beyond domain cardinality - 1 (setup.go:266)");
     GG_HIP(hipGetDevice(&pk->device));
-    memcpy(&pk->alpha, alpha1, 64);
-    memcpy(&pk->beta, beta1, 64);
-    memcpy(&pk->delta, delta1, 64);
-    memcpy(&pk->beta2, beta2, 128);
-    memcpy(&pk->delta2, delta2, 128);
-    ck(gg_domain_create(log_n, omega_mont, coset_gen_mont, &pk->dom));
+    memcpy(pk->alpha, alpha1, ps.g1a);
+    memcpy(pk->beta, beta1, ps.g1a);
+    memcpy(pk->delta, delta1, ps.g1a);
+    memcpy(pk->beta2, beta2, ps.g2a);
+    memcpy(pk->delta2, delta2, ps.g2a);
+    ck(gg_domain_create_ex(curve, log_n, omega_mont, coset_gen_mont, &pk->dom));
     // wire index maps (prove.go:151-175: drop wires whose A/B point is infinity),
     // relative to the shard's first wire
     std::vector<uint32_t> ia, ib, ik;
@@ -151,22 +181,46 @@ static void pk_build(gg_groth16_pk* pk, int log_n, const void* omega_mont, const
     const size_t nw = hi - lo;
     // dense wire-indexed A and K (holes = infinity), one window size for both
     {
-        std::vector<uint8_t> dense(nw * 64, 0);
-        for (size_t j = 0; j < nA; j++) memcpy(&dense[(size_t)ia[j] * 64], (const uint8_t*)g1_A + j * 64, 64);
-        const int cAK = choose_c(std::max<size_t>(nw, 1), 64, 255);
-        pk->A = msm_base_create_internal(GG_G1, dense.data(), nw, nullptr, cAK, true);
+        const size_t pb = ps.g1a;
+        std::vector<uint8_t> dense(nw * pb, 0);
+        for (size_t j = 0; j < nA; j++) memcpy(&dense[(size_t)ia[j] * pb], (const uint8_t*)g1_A + j * pb, pb);
+        const int cAK = choose_c(std::max<size_t>(nw, 1), pb, tbits);
+        pk->A = msm_base_create_internal(g1, dense.data(), nw, nullptr, cAK, true);
         std::fill(dense.begin(), dense.end(), 0);
-        for (size_t j = 0; j < nK; j++) memcpy(&dense[(size_t)ik[j] * 64], (const uint8_t*)g1_K + j * 64, 64);
-        pk->K = msm_base_create_internal(GG_G1, dense.data(), nw, nullptr, cAK, true);
+        for (size_t j = 0; j < nK; j++) memcpy(&dense[(size_t)ik[j] * pb], (const uint8_t*)g1_K + j * pb, pb);
+        pk->K = msm_base_create_internal(g1, dense.data(), nw, nullptr, cAK, true);
     }
     // B1 shares its sort with the G2 base: the window that suits G2
-    pk->B = msm_base_create_internal(GG_G1, g1_B, nB, ib.data(), choose_c(std::max<size_t>(nB, 1), 128, 255), false);
-    pk->B2 = msm_base_create_internal(GG_G2, g2_B, nB, ib.data(), msm_base_window(pk->B), false);
-    pk->Z = msm_base_create_internal(GG_G1, g1_Z, nZ, nullptr, 0, false);
+    pk->B = msm_base_create_internal(g1, g1_B, nB, ib.data(), choose_c(std::max<size_t>(nB, 1), 128, tbits), false);
+    pk->B2 = msm_base_create_internal(g2, g2_B, nB, ib.data(), msm_base_window(pk->B), false);
+    pk->Z = msm_base_create_internal(g1, g1_Z, nZ, nullptr, 0, false);
     pk->share_AK = msm_same_shape(pk->A, pk->K);
     pk->share_B = msm_same_shape(pk->B, pk->B2);
     for (hipStream_t* x : {&pk->s0, &pk->s1, &pk->s2, &pk->s3, &pk->s4})
         GG_HIP(hipStreamCreateWithFlags(x, hipStreamNonBlocking));
+}
+
+extern "C" int gg_groth16_pk_create_ex(int curve, int log_n, const void* omega_mont, const void* coset_gen_mont,
+                                       const void* g1_A, size_t nA, const void* g1_B, size_t nB,
+                                       const void* g1_Z, size_t nZ, const void* g1_K, size_t nK,
+                                       const void* alpha1, const void* beta1, const void* delta1,
+                                       const void* g2_B, const void* beta2, const void* delta2,
+                                       const uint8_t* inf_A, const uint8_t* inf_B, size_t n_wires,
+                                       size_t nb_public, const uint32_t* k_wire_index,
+                                       gg_groth16_pk_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(log_n >= 0 && log_n <= 28, GG_ERR_INVALID_ARG, "log_n out of range");
+    const size_t n = (size_t)1 << log_n;
+    GG_CHECK(nZ + 1 == n || (n == 1 && nZ == 0), GG_ERR_INVALID_ARG,
+             "len(pk.G1.Z) must be domain cardinality - 1 (setup.go:266)");
+    std::unique_ptr<gg_groth16_pk> pk(new gg_groth16_pk());
+    if (!k_wire_index) GG_CHECK(nb_public + nK <= n_wires, GG_ERR_INVALID_ARG, "len(pk.G1.K) too large");
+    pk_build(pk.get(), curve, log_n, omega_mont, coset_gen_mont, g1_A, nA, g1_B, nB, g1_Z, 0, nZ, g1_K, nK,
+             alpha1, beta1, delta1, g2_B, beta2, delta2, inf_A, inf_B, n_wires, nb_public,
+             k_wire_index, 0, n_wires);
+    *out = pk.release();
+    GG_CAPI_END
 }
 
 extern "C" int gg_groth16_pk_create(int log_n, const void* omega_mont, const void* coset_gen_mont,
@@ -177,19 +231,9 @@ extern "C" int gg_groth16_pk_create(int log_n, const void* omega_mont, const voi
                                     const uint8_t* inf_A, const uint8_t* inf_B, size_t n_wires,
                                     size_t nb_public, const uint32_t* k_wire_index,
                                     gg_groth16_pk_t* out) {
-    GG_CAPI_BEGIN
-    GG_CHECK(out, GG_ERR_INVALID_ARG, "null argument");
-    GG_CHECK(log_n >= 0 && log_n <= 28, GG_ERR_INVALID_ARG, "log_n out of range");
-    const size_t n = (size_t)1 << log_n;
-    GG_CHECK(nZ + 1 == n || (n == 1 && nZ == 0), GG_ERR_INVALID_ARG,
-             "len(pk.G1.Z) must be domain cardinality - 1 (setup.go:266)");
-    std::unique_ptr<gg_groth16_pk> pk(new gg_groth16_pk());
-    if (!k_wire_index) GG_CHECK(nb_public + nK <= n_wires, GG_ERR_INVALID_ARG, "len(pk.G1.K) too large");
-    pk_build(pk.get(), log_n, omega_mont, coset_gen_mont, g1_A, nA, g1_B, nB, g1_Z, 0, nZ, g1_K, nK,
-             alpha1, beta1, delta1, g2_B, beta2, delta2, inf_A, inf_B, n_wires, nb_public,
-             k_wire_index, 0, n_wires);
-    *out = pk.release();
-    GG_CAPI_END
+    return gg_groth16_pk_create_ex(GG_CURVE_BN254, log_n, omega_mont, coset_gen_mont, g1_A, nA, g1_B, nB, g1_Z,
+                                   nZ, g1_K, nK, alpha1, beta1, delta1, g2_B, beta2, delta2, inf_A, inf_B,
+                                   n_wires, nb_public, k_wire_index, out);
 }
 
 extern "C" int gg_groth16_pk_create_shard(int log_n, const void* omega_mont, const void* coset_gen_mont,
@@ -204,7 +248,7 @@ extern "C" int gg_groth16_pk_create_shard(int log_n, const void* omega_mont, con
     GG_CAPI_BEGIN
     GG_CHECK(out, GG_ERR_INVALID_ARG, "null argument");
     std::unique_ptr<gg_groth16_pk> pk(new gg_groth16_pk());
-    pk_build(pk.get(), log_n, omega_mont, coset_gen_mont, g1_A, nA, g1_B, nB, g1_Z, z_lo, nZ, g1_K,
+    pk_build(pk.get(), GG_CURVE_BN254, log_n, omega_mont, coset_gen_mont, g1_A, nA, g1_B, nB, g1_Z, z_lo, nZ, g1_K,
              nK, alpha1, beta1, delta1, g2_B, beta2, delta2, inf_A, inf_B, n_wires, nb_public,
              k_wire_index, wire_lo, wire_hi);
     *out = pk.release();
@@ -232,17 +276,47 @@ static double now_ms() {
         .count();
 }
 
-static Fr fr_from(const void* p) {
-    Fr x;
-    memcpy(&x, p, 32);
+template <class T>
+static T from_bytes(const void* p) {
+    T x;
+    memcpy(&x, p, sizeof(T));
     return x;
 }
 
-// MSM partials of one key (shard): the device section of prove.go:198-301.
+// MSM partials of one key (shard): the device section of prove.go:198-301, as
+// the curve's Jacobian points (BN254 96 / 192 B, BLS12-381 144 / 288 B)
 struct G16Partials {
-    G1Jac a, b1, k, z;  // Σ w·A, Σ w·B1, Σ w·K (filtered), Σ h·Z
-    G2Jac b2;           // Σ w·B2
+    alignas(16) uint8_t a[144], b1[144], k[144], z[144];  // Σ w·A, Σ w·B1, Σ w·K (filtered), Σ h·Z
+    alignas(16) uint8_t b2[288];                          // Σ w·B2
 };
+static void set_g1_inf(int curve, void* p) {
+    if (curve == GG_CURVE_BN254) {
+        G1Jac j = G1Jac::inf();
+        memcpy(p, &j, sizeof(j));
+    } else {
+        Jac<FpBls> j = Jac<FpBls>::inf();
+        memcpy(p, &j, sizeof(j));
+    }
+}
+// partials <-> the flat layout of gg_groth16_prove_partial: a | b1 | k | z | b2
+static void partials_put(int curve, const G16Partials& p, void* out) {
+    const PointSizes ps = point_sizes(curve);
+    uint8_t* o = (uint8_t*)out;
+    memcpy(o, p.a, ps.g1j);
+    memcpy(o + ps.g1j, p.b1, ps.g1j);
+    memcpy(o + 2 * ps.g1j, p.k, ps.g1j);
+    memcpy(o + 3 * ps.g1j, p.z, ps.g1j);
+    memcpy(o + 4 * ps.g1j, p.b2, ps.g2j);
+}
+static void partials_get(int curve, const void* in, G16Partials& p) {
+    const PointSizes ps = point_sizes(curve);
+    const uint8_t* q = (const uint8_t*)in;
+    memcpy(p.a, q, ps.g1j);
+    memcpy(p.b1, q + ps.g1j, ps.g1j);
+    memcpy(p.k, q + 2 * ps.g1j, ps.g1j);
+    memcpy(p.z, q + 3 * ps.g1j, ps.g1j);
+    memcpy(p.b2, q + 4 * ps.g1j, ps.g2j);
+}
 
 // Joins every worker on scope exit, also while an exception unwinds (the
 // workers reference locals of prove_device, declared before the joiner).
@@ -285,7 +359,7 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
     // latency-bound, so overlapping them fills the chip):
     //   s1: [A, B, C upload] computeH -> Z-MSM (h lands in A's buffer)
     //   s2: A-MSM    s3: B1-MSM    s4: K-MSM    s0 (this thread): G2-MSM
-    out.z = G1Jac::inf();
+    set_g1_inf(pk->curve, out.z);
     double t_h = 0, t_z = 0, t_a = 0, t_b = 0, t_k = 0, t_upabc = 0;
     std::mutex emu;
     std::string werr;
@@ -359,7 +433,7 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
         GG_HIP(hipStreamSynchronize(pk->s1));
         double b = now_ms();
         t_h = b - a;
-        msm_device(pk->Z, hshard_h(dh->hs), &out.z, pk->s1);
+        msm_device(pk->Z, hshard_h(dh->hs), out.z, pk->s1);
         t_z = now_ms() - b;
     }));
     else spawn(guarded([&] {
@@ -372,7 +446,7 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
         double b = now_ms();
         t_h = b - a;
         if (h_dev_out) GG_HIP(hipMemcpyAsync(h_dev_out, A, nbytes, hipMemcpyDeviceToDevice, pk->s1));
-        if (n > 1) msm_device(pk->Z, A + pk->z_lo, &out.z, pk->s1);
+        if (n > 1) msm_device(pk->Z, A + pk->z_lo, out.z, pk->s1);
         t_z = now_ms() - b;
     }));
     // wire sorts, enqueued from this thread before any finisher waits on their
@@ -390,11 +464,11 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
     })();
     double t2 = now_ms(), te = t2;
     if (wcode == GG_OK) {  // the sorts are enqueued: run the finishers
-        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->A, sAK, &out.a, pk->s2); t_a = now_ms() - a; }));
-        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->B, sB, &out.b1, pk->s3); t_b = now_ms() - a; }));
-        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->K, sK, &out.k, pk->s4); t_k = now_ms() - a; }));
+        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->A, sAK, out.a, pk->s2); t_a = now_ms() - a; }));
+        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->B, sB, out.b1, pk->s3); t_b = now_ms() - a; }));
+        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->K, sK, out.k, pk->s4); t_k = now_ms() - a; }));
         t2 = now_ms();
-        guarded([&] { msm_finish_dev(pk->B2, sB2, &out.b2, pk->s0); })();
+        guarded([&] { msm_finish_dev(pk->B2, sB2, out.b2, pk->s0); })();
         te = now_ms();
     }
     for (auto& w : workers) w.join();
@@ -411,25 +485,32 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
 
 // Fixed-point terms of the proof (prove.go:177-192, 293-296): kr = -r*s and
 // r*delta, s*delta, kr*delta, s*delta2 -- independent of the MSMs.
+template <class Cv>
 struct G16Fixed {
-    Fr rc, sc;  // r, s in canonical form (scalar-mul digits)
-    G1Jac rd, sd, krd;
-    G2Jac sd2;
+    typename Cv::FrT rc, sc;  // r, s in canonical form (scalar-mul digits)
+    Jac<typename Cv::G1F> rd, sd, krd;
+    Jac<typename Cv::G2F> sd2;
 };
 
-static std::future<G16Fixed> fixed_terms_async(const G1Affine& delta, const G2Affine& delta2,
-                                               const Fr& r, const Fr& s) {
+template <class Cv>
+static std::future<G16Fixed<Cv>> fixed_terms_async(const void* delta_aff, const void* delta2_aff, const void* r_mont,
+                                                   const void* s_mont) {
+    using G1 = typename Cv::G1F;
+    using G2 = typename Cv::G2F;
+    using FrT = typename Cv::FrT;
+    const Affine<G1> delta = from_bytes<Affine<G1>>(delta_aff);
+    const Affine<G2> delta2 = from_bytes<Affine<G2>>(delta2_aff);
+    const FrT r = from_bytes<FrT>(r_mont), s = from_bytes<FrT>(s_mont);
     return std::async(std::launch::async, [delta, delta2, r, s] {
-        G16Fixed f;
-        Fr kr = -(r * s);
+        G16Fixed<Cv> f;
+        FrT kr = -(r * s);
         f.rc = from_mont(r);
         f.sc = from_mont(s);
-        Fr krc = from_mont(kr);
-        G1Jac dl = G1Jac::from_affine(delta);
+        FrT krc = from_mont(kr);
+        Jac<G1> dl = Jac<G1>::from_affine(delta);
         auto f_rd = std::async(std::launch::async, [&] { return jac_mul(dl, f.rc.v); });
         auto f_sd = std::async(std::launch::async, [&] { return jac_mul(dl, f.sc.v); });
-        auto f_sd2 = std::async(std::launch::async,
-                                [&] { return jac_mul(G2Jac::from_affine(delta2), f.sc.v); });
+        auto f_sd2 = std::async(std::launch::async, [&] { return jac_mul(Jac<G2>::from_affine(delta2), f.sc.v); });
         f.krd = jac_mul(dl, krc.v);
         f.rd = f_rd.get();
         f.sd = f_sd.get();
@@ -442,22 +523,45 @@ static std::future<G16Fixed> fixed_terms_async(const G1Affine& delta, const G2Af
 //   Ar  = Σ w·A + α + r·δ                  Bs1 = Σ w·B1 + β + s·δ
 //   Krs = Σ w·K + kr·δ + Σ h·Z + s·Ar + r·Bs1
 //   Bs  = Σ w·B2 + s·δ2 + β2
-static void g16_combine(const G16Partials& p, const G16Fixed& f, const G1Affine& alpha,
-                        const G1Affine& beta, const G2Affine& beta2, void* ar_aff, void* bs_aff,
-                        void* krs_aff) {
-    G1Jac ar = jac_add(jac_add_affine(p.a, alpha), f.rd);
-    G1Jac bs1 = jac_add(jac_add_affine(p.b1, beta), f.sd);
+template <class Cv>
+static void g16_combine(const G16Partials& p, const G16Fixed<Cv>& f, const void* alpha_aff, const void* beta_aff,
+                        const void* beta2_aff, void* ar_aff, void* bs_aff, void* krs_aff) {
+    using G1 = typename Cv::G1F;
+    using G2 = typename Cv::G2F;
+    const Affine<G1> alpha = from_bytes<Affine<G1>>(alpha_aff), beta = from_bytes<Affine<G1>>(beta_aff);
+    const Affine<G2> beta2 = from_bytes<Affine<G2>>(beta2_aff);
+    const Jac<G1> pa = from_bytes<Jac<G1>>(p.a), pb1 = from_bytes<Jac<G1>>(p.b1), pk = from_bytes<Jac<G1>>(p.k),
+                  pz = from_bytes<Jac<G1>>(p.z);
+    const Jac<G2> pb2 = from_bytes<Jac<G2>>(p.b2);
+    Jac<G1> ar = jac_add(jac_add_affine(pa, alpha), f.rd);
+    Jac<G1> bs1 = jac_add(jac_add_affine(pb1, beta), f.sd);
     auto f_sar = std::async(std::launch::async, [&] { return jac_mul(ar, f.sc.v); });
-    G1Jac rbs = jac_mul(bs1, f.rc.v);
-    G1Jac krs = jac_add(jac_add(p.k, f.krd), p.z);
+    Jac<G1> rbs = jac_mul(bs1, f.rc.v);
+    Jac<G1> krs = jac_add(jac_add(pk, f.krd), pz);
     krs = jac_add(krs, f_sar.get());
     krs = jac_add(krs, rbs);
-    G2Jac bs = jac_add_affine(jac_add(p.b2, f.sd2), beta2);
-    G1Affine o_ar = jac_to_affine(ar), o_krs = jac_to_affine(krs);
-    G2Affine o_bs = jac_to_affine(bs);
-    memcpy(ar_aff, &o_ar, 64);
-    memcpy(krs_aff, &o_krs, 64);
-    memcpy(bs_aff, &o_bs, 128);
+    Jac<G2> bs = jac_add_affine(jac_add(pb2, f.sd2), beta2);
+    const Affine<G1> o_ar = jac_to_affine(ar), o_krs = jac_to_affine(krs);
+    const Affine<G2> o_bs = jac_to_affine(bs);
+    memcpy(ar_aff, &o_ar, sizeof(o_ar));
+    memcpy(krs_aff, &o_krs, sizeof(o_krs));
+    memcpy(bs_aff, &o_bs, sizeof(o_bs));
+}
+
+template <class Cv>
+static void prove_whole(gg_groth16_pk* pk, const void* wires, const void* sol_a, const void* sol_b,
+                        const void* sol_c, size_t n_cons, bool on_dev, const void* r_mont, const void* s_mont,
+                        void* ar_aff, void* bs_aff, void* krs_aff, void* h_dev_out) {
+    double t0 = now_ms();
+    // host pool computes the fixed-point terms while the GPU works
+    auto fixed = fixed_terms_async<Cv>(pk->delta, pk->delta2, r_mont, s_mont);
+    G16Partials p;
+    prove_device(pk, wires, sol_a, sol_b, sol_c, n_cons, on_dev, h_dev_out, p);
+    double tep = now_ms();
+    g16_combine<Cv>(p, fixed.get(), pk->alpha, pk->beta, pk->beta2, ar_aff, bs_aff, krs_aff);
+    double tend = now_ms();
+    g_timings[7] = tend - tep;
+    g_timings[8] = tend - t0;
 }
 
 static void check_prove_args(gg_groth16_pk_t pk, const void* wires, size_t n_wires, const void* a,
@@ -481,16 +585,12 @@ extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_
                                  "gg_groth16_prove_partial + gg_groth16_finalize");
     std::lock_guard<std::mutex> lk(pk->mu);
     g_ext[0] = 0;
-    double t0 = now_ms();
-    // host pool computes the fixed-point terms while the GPU works
-    auto fixed = fixed_terms_async(pk->delta, pk->delta2, fr_from(r_mont), fr_from(s_mont));
-    G16Partials p;
-    prove_device(pk, wires, sol_a, sol_b, sol_c, n_cons, inputs_on_device != 0, h_dev_out, p);
-    double tep = now_ms();
-    g16_combine(p, fixed.get(), pk->alpha, pk->beta, pk->beta2, ar_aff, bs_aff, krs_aff);
-    double tend = now_ms();
-    g_timings[7] = tend - tep;
-    g_timings[8] = tend - t0;
+    if (pk->curve == GG_CURVE_BN254)
+        prove_whole<CurveBn254>(pk, wires, sol_a, sol_b, sol_c, n_cons, inputs_on_device != 0, r_mont, s_mont,
+                                ar_aff, bs_aff, krs_aff, h_dev_out);
+    else
+        prove_whole<CurveBls12381>(pk, wires, sol_a, sol_b, sol_c, n_cons, inputs_on_device != 0, r_mont, s_mont,
+                                   ar_aff, bs_aff, krs_aff, h_dev_out);
     GG_CAPI_END
 }
 
@@ -506,12 +606,7 @@ extern "C" int gg_groth16_prove_partial(gg_groth16_pk_t pk, const void* wires, s
     double t0 = now_ms();
     G16Partials p;
     prove_device(pk, wires, sol_a, sol_b, sol_c, n_cons, inputs_on_device != 0, h_dev_out, p);
-    uint8_t* o = (uint8_t*)partials;
-    memcpy(o, &p.a, 96);
-    memcpy(o + 96, &p.b1, 96);
-    memcpy(o + 192, &p.k, 96);
-    memcpy(o + 288, &p.z, 96);
-    memcpy(o + 384, &p.b2, 192);
+    partials_put(pk->curve, p, partials);
     g_timings[7] = 0;
     g_timings[8] = now_ms() - t0;
     GG_CAPI_END
@@ -525,6 +620,7 @@ extern "C" int gg_groth16_prove_partial_dist(gg_groth16_pk_t pk, gg_hshard_t hs,
     GG_CAPI_BEGIN
     check_prove_args(pk, wires, n_wires, sol_a, sol_b, sol_c, n_cons);
     GG_CHECK(hs && xchg && send_dev && recv_dev && partials, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(pk->curve == GG_CURVE_BN254, GG_ERR_UNSUPPORTED, "distributed computeH: BN254 only");
     int rank = 0, world = 1, log_n = 0;
     size_t m = hshard_m(hs, &rank, &world, &log_n);
     GG_CHECK(log_n == pk->log_n, GG_ERR_INVALID_ARG, "hshard and key have different domains");
@@ -536,14 +632,30 @@ extern "C" int gg_groth16_prove_partial_dist(gg_groth16_pk_t pk, gg_hshard_t hs,
     G16Partials p;
     DistH dh{hs, xchg, xchg_ctx, (Fr*)send_dev, (Fr*)recv_dev};
     prove_device(pk, wires, sol_a, sol_b, sol_c, n_cons, inputs_on_device != 0, nullptr, p, &dh);
-    uint8_t* o = (uint8_t*)partials;
-    memcpy(o, &p.a, 96);
-    memcpy(o + 96, &p.b1, 96);
-    memcpy(o + 192, &p.k, 96);
-    memcpy(o + 288, &p.z, 96);
-    memcpy(o + 384, &p.b2, 192);
+    partials_put(pk->curve, p, partials);
     g_timings[7] = 0;
     g_timings[8] = now_ms() - t0;
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_finalize_ex(int curve, const void* alpha1, const void* beta1, const void* delta1,
+                                      const void* beta2, const void* delta2, const void* partials,
+                                      const void* r_mont, const void* s_mont, void* ar_aff, void* bs_aff,
+                                      void* krs_aff) {
+    GG_CAPI_BEGIN
+    GG_CHECK(alpha1 && beta1 && delta1 && beta2 && delta2 && partials && r_mont && s_mont && ar_aff && bs_aff &&
+                 krs_aff,
+             GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(curve == GG_CURVE_BN254 || curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "bad curve");
+    G16Partials p;
+    partials_get(curve, partials, p);
+    if (curve == GG_CURVE_BN254) {
+        auto fixed = fixed_terms_async<CurveBn254>(delta1, delta2, r_mont, s_mont);
+        g16_combine<CurveBn254>(p, fixed.get(), alpha1, beta1, beta2, ar_aff, bs_aff, krs_aff);
+    } else {
+        auto fixed = fixed_terms_async<CurveBls12381>(delta1, delta2, r_mont, s_mont);
+        g16_combine<CurveBls12381>(p, fixed.get(), alpha1, beta1, beta2, ar_aff, bs_aff, krs_aff);
+    }
     GG_CAPI_END
 }
 
@@ -551,27 +663,8 @@ extern "C" int gg_groth16_finalize(const void* alpha1, const void* beta1, const 
                                    const void* beta2, const void* delta2, const void* partials,
                                    const void* r_mont, const void* s_mont, void* ar_aff,
                                    void* bs_aff, void* krs_aff) {
-    GG_CAPI_BEGIN
-    GG_CHECK(alpha1 && beta1 && delta1 && beta2 && delta2 && partials && r_mont && s_mont &&
-                 ar_aff && bs_aff && krs_aff,
-             GG_ERR_INVALID_ARG, "null argument");
-    G1Affine alpha, beta, delta;
-    G2Affine b2, d2;
-    memcpy(&alpha, alpha1, 64);
-    memcpy(&beta, beta1, 64);
-    memcpy(&delta, delta1, 64);
-    memcpy(&b2, beta2, 128);
-    memcpy(&d2, delta2, 128);
-    auto fixed = fixed_terms_async(delta, d2, fr_from(r_mont), fr_from(s_mont));
-    G16Partials p;
-    const uint8_t* q = (const uint8_t*)partials;
-    memcpy(&p.a, q, 96);
-    memcpy(&p.b1, q + 96, 96);
-    memcpy(&p.k, q + 192, 96);
-    memcpy(&p.z, q + 288, 96);
-    memcpy(&p.b2, q + 384, 192);
-    g16_combine(p, fixed.get(), alpha, beta, b2, ar_aff, bs_aff, krs_aff);
-    GG_CAPI_END
+    return gg_groth16_finalize_ex(GG_CURVE_BN254, alpha1, beta1, delta1, beta2, delta2, partials, r_mont, s_mont,
+                                  ar_aff, bs_aff, krs_aff);
 }
 
 extern "C" int gg_groth16_last_timings_ex(double* ms, int cap) {

@@ -8,6 +8,10 @@ void create_base_g2(gg_msm_base* b, const void* points, size_t n, int on_device,
                     const uint32_t* sidx, int window_bits, bool keep_inf);
 void create_base_bls(gg_msm_base* b, const void* points, size_t n, int on_device,
                      const uint32_t* sidx, int window_bits, bool keep_inf);
+void create_base_bls2(gg_msm_base* b, const void* points, size_t n, int on_device,
+                      const uint32_t* sidx, int window_bits, bool keep_inf);
+void msm_run_bls2(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st);
+void msm_finish_bls2(gg_msm_base* b, MsmSort* s, MsmScratch* scr, void* out_jac, hipStream_t st);
 void msm_run_g1(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st);
 void msm_run_g2(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st);
 void msm_run_bls(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st);
@@ -23,15 +27,16 @@ extern "C" int gg_msm_base_create(int group, const void* points, size_t n, int p
                                   gg_msm_base_t* out) {
     GG_CAPI_BEGIN
     GG_CHECK(out, GG_ERR_INVALID_ARG, "null out");
-    GG_CHECK(group == GG_G1 || group == GG_G2 || group == GG_BLS12_381_G1, GG_ERR_INVALID_ARG,
-             "group must be GG_G1, GG_G2 or GG_BLS12_381_G1");
+    GG_CHECK(group == GG_G1 || group == GG_G2 || group == GG_BLS12_381_G1 || group == GG_BLS12_381_G2,
+             GG_ERR_INVALID_ARG, "group must be GG_G1, GG_G2, GG_BLS12_381_G1 or GG_BLS12_381_G2");
     GG_CHECK(n == 0 || points, GG_ERR_INVALID_ARG, "null points");
     GG_CHECK(n < 0x80000000ull, GG_ERR_INVALID_ARG, "n too large");
     std::unique_ptr<gg_msm_base> b(new gg_msm_base());
     b->group = group;
     if (group == GG_G1) create_base_g1(b.get(), points, n, points_on_device, scalar_index, window_bits, false);
     else if (group == GG_G2) create_base_g2(b.get(), points, n, points_on_device, scalar_index, window_bits, false);
-    else create_base_bls(b.get(), points, n, points_on_device, scalar_index, window_bits, false);
+    else if (group == GG_BLS12_381_G1) create_base_bls(b.get(), points, n, points_on_device, scalar_index, window_bits, false);
+    else create_base_bls2(b.get(), points, n, points_on_device, scalar_index, window_bits, false);
     *out = b.release();
     GG_CAPI_END
 }
@@ -56,7 +61,8 @@ namespace gg {
 void msm_device_work(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
     if (b->group == GG_G1) msm_run_g1(b, w, scalars_dev, out_jac, st);
     else if (b->group == GG_G2) msm_run_g2(b, w, scalars_dev, out_jac, st);
-    else msm_run_bls(b, w, scalars_dev, out_jac, st);
+    else if (b->group == GG_BLS12_381_G1) msm_run_bls(b, w, scalars_dev, out_jac, st);
+    else msm_run_bls2(b, w, scalars_dev, out_jac, st);
 }
 static void msm_device_locked(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
     msm_device_work(b, &b->own, scalars_dev, out_jac, st);
@@ -73,7 +79,8 @@ gg_msm_base* msm_base_create_internal(int group, const void* host_points, size_t
     b->group = group;
     if (group == GG_G1) create_base_g1(b.get(), host_points, n, 0, sidx, window_bits, keep_inf);
     else if (group == GG_G2) create_base_g2(b.get(), host_points, n, 0, sidx, window_bits, keep_inf);
-    else create_base_bls(b.get(), host_points, n, 0, sidx, window_bits, keep_inf);
+    else if (group == GG_BLS12_381_G1) create_base_bls(b.get(), host_points, n, 0, sidx, window_bits, keep_inf);
+    else create_base_bls2(b.get(), host_points, n, 0, sidx, window_bits, keep_inf);
     return b.release();
 }
 bool msm_same_shape(const gg_msm_base* a, const gg_msm_base* b) {
@@ -94,7 +101,8 @@ void msm_prepare_dev(gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStrea
 void msm_finish_dev(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st) {
     if (b->group == GG_G1) msm_finish_g1(b, s, &b->own.scr, out_jac, st);
     else if (b->group == GG_G2) msm_finish_g2(b, s, &b->own.scr, out_jac, st);
-    else msm_finish_bls(b, s, &b->own.scr, out_jac, st);
+    else if (b->group == GG_BLS12_381_G1) msm_finish_bls(b, s, &b->own.scr, out_jac, st);
+    else msm_finish_bls2(b, s, &b->own.scr, out_jac, st);
 }
 size_t msm_scalars_needed(gg_msm_base* b) {
     return b->has_sidx ? (b->n ? (size_t)b->max_sidx + 1 : 0) : b->n;

@@ -594,15 +594,6 @@ void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStr
         sort_entries(b, s, scalars_dev, st);
         ps_sort.stop(st);
     }
-    // Accumulation ranges of K sorted entries, one thread each (32 for small
-    // MSMs, else 64 doubled up to 256 while that leaves > 2M ranges).  The fullest bucket's size goes to pinned
-    // memory behind an event while the accumulation runs (no host stall).
-    const size_t E = (size_t)b->W * n;
-    uint32_t K = E < ((size_t)4 << 20) ? 32 : 64;  // MI355X sweep: 2^20 best at 64, 2^24 at 128
-    while (K < 256 && E / (size_t)K > ((size_t)2 << 20)) K *= 2;
-    if (const char* e = getenv("GG_MSM_K1")) K = (uint32_t)std::max(1, atoi(e));
-    s->K = K;
-    s->ranges_ub = ((size_t)b->W * n + K - 1) / K;
     GG_HIP(hipMemsetAsync(s->maxcnt.p, 0, 4, st));
     hipLaunchKernelGGL(k_bucket_max, dim3(grid_for(nb, 256)), dim3(256), 0, st, s->offsets.as<uint32_t>(), nb,
                        s->maxcnt.as<uint32_t>());

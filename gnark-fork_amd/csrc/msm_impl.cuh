@@ -25,6 +25,8 @@
 #include <vector>
 #include <algorithm>
 #include <memory>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 struct gg_msm_base;
@@ -103,8 +105,13 @@ __device__ __forceinline__ void range_store(const Xyzz<F>& acc, bool first, bool
     else st(S + (__brev(q) >> (33 - c)), acc);
 }
 
+// waves per SIMD the accumulation is compiled for: 2 (<= 256 VGPRs) up to Fp2
+// over the 8-limb BN254 Fp; 1 (512 VGPRs, no scratch spills) for BLS12-381 Fp2
 template <class F>
-__global__ void __launch_bounds__(256, 2) k_accum_range(const Affine<F>* pts, const uint32_t* sorted,
+constexpr int kAccumWaves = sizeof(F) > 64 ? 1 : 2;
+
+template <class F>
+__global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affine<F>* pts, const uint32_t* sorted,
                                                      const uint32_t* offsets, uint32_t nb, int c,
                                                      uint32_t K, int skip_inf, Xyzz<F>* head,
                                                      Xyzz<F>* tail, Xyzz<F>* S, uint32_t* tbucket) {
@@ -456,8 +463,6 @@ struct MsmSort {
     uint32_t* pin = nullptr;          // pinned read-back: [0] = entries of the fullest bucket
     hipEvent_t pin_ev = nullptr;      // after the read-back copy
     hipEvent_t ready_ev = nullptr;    // after the sort
-    uint32_t K = 32;                  // entries per accumulation range
-    size_t ranges_ub = 0;             // upper bound of ceil(entries / K)
     void ensure_events() {
         if (!pin) GG_HIP(hipHostMalloc((void**)&pin, 16, hipHostMallocDefault));
         if (!pin_ev) GG_HIP(hipEventCreateWithFlags(&pin_ev, hipEventDisableTiming));
@@ -673,6 +678,31 @@ inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* S, MsmScratch* sc
     return acc;
 }
 
+// Entries per accumulation range (one thread each).  Every range costs the same,
+// so the grid runs in whole "rounds" of the chip's concurrent threads C (occupancy
+// of k_accum_range<F> x CUs x 256): R = entries / (C K_pref) rounds, rounded, and
+// K = entries / (R C) -- no half-empty last round.  K_pref: 32 below 4M entries,
+// 64, 128 from 2^26 (MI355X sweeps: 2^20 G1 best at 64-80, 2^24 at 128; longer
+// ranges mean fewer level-2 partials).  GG_MSM_K1 overrides.
+template <class F>
+inline uint32_t range_length(size_t E) {
+    if (const char* e = getenv("GG_MSM_K1")) return (uint32_t)std::max(1, atoi(e));
+    static const double C = [] {
+        int blocks = 0, cus = 0, dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_accum_range<F>, 256, 0) != hipSuccess ||
+            blocks < 1 || cus < 1) {
+            (void)hipGetLastError();
+            return 256.0 * 256 * 2;
+        }
+        return (double)blocks * cus * 256;
+    }();
+    const double kpref = E < ((size_t)4 << 20) ? 32 : (E >= ((size_t)1 << 26) ? 128 : 64);
+    const double rounds = std::max(1.0, std::round((double)E / (C * kpref)));
+    return (uint32_t)std::max(1.0, std::ceil((double)E / (rounds * C)));
+}
+
 // Accumulation + reduction of base b over a prepared sort s (its own or one
 // shared with a base of identical shape), scratch scr.  Waits (device side) for
 // s->ready_ev.
@@ -682,8 +712,8 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
     if (n == 0) return Xyzz<F>::inf();
     GG_HIP(hipStreamWaitEvent(st, s->ready_ev, 0));
     const uint32_t* offs = s->offsets.as<uint32_t>();
-    const size_t T = s->ranges_ub;
-    const uint32_t K = s->K;
+    const uint32_t K = range_length<F>((size_t)b->W * n);
+    const size_t T = ((size_t)b->W * n + K - 1) / K;  // ranges (upper bound: digit-0 entries are not sorted)
     scr->head.reserve((T + 1) * sizeof(Xyzz<F>));
     scr->tail.reserve((T + 1) * sizeof(Xyzz<F>));
     scr->tbucket.reserve((T + 1) * 4);

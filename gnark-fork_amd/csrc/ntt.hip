@@ -471,22 +471,27 @@ extern "C" int gg_ntt(gg_domain_t d, void* data_dev, int inverse, int decimation
 }
 
 namespace gg {
-// computeH on device buffers A (becomes h), B, C, each 2^L fr (already padded)
-void compute_h_device(gg_domain* dom, Fr* A, Fr* B, Fr* C, Fr* H, hipStream_t st) {
-    GG_CHECK(dom->curve == GG_CURVE_BN254, GG_ERR_INVALID_ARG, "computeH needs a BN254 domain");
-    DomainT<FrCfg>* d = dom->bn.get();
-    const Fr* nul = nullptr;
+// computeH (prove.go:353-396) on device buffers A (becomes h), B, C, each 2^L fr
+// (already padded), for the domain's scalar field
+template <class C>
+static void compute_h_t(DomainT<C>* d, Fe<C>* A, Fe<C>* B, Fe<C>* Cv, Fe<C>* H, hipStream_t st) {
+    const Fe<C>* nul = nullptr;
     // a, b: iFFT(DIF) with g^br(i)/n folded in, then DIT FFT -> coset evaluations
     run_transform(d, A, A, false, true, -1, SK_H_FWD, nul, nul, st);
     run_transform(d, A, A, true, false, -1, -1, nul, nul, st);
     run_transform(d, B, B, false, true, -1, SK_H_FWD, nul, nul, st);
     run_transform(d, B, B, true, false, -1, -1, nul, nul, st);
-    run_transform(d, C, C, false, true, -1, SK_H_FWD, nul, nul, st);
+    run_transform(d, Cv, Cv, false, true, -1, SK_H_FWD, nul, nul, st);
     // last pass of c's coset FFT emits a*b - c in place (PolyOps fused)
-    run_transform(d, C, C, true, false, -1, -1, A, B, st);
+    run_transform(d, Cv, Cv, true, false, -1, -1, (const Fe<C>*)A, (const Fe<C>*)B, st);
     // coset iFFT (DIF) with den * g^-br(i) / n folded in -> h bit-reversed.
     // H may alias A, B or C.
-    run_transform(d, C, H, false, true, -1, SK_H_INV, nul, nul, st);
+    run_transform(d, Cv, H, false, true, -1, SK_H_INV, nul, nul, st);
+}
+// any curve's domain (BN254 or BLS12-381 Groth16); fr buffers as opaque 32-B elements
+void compute_h_device(gg_domain* dom, Fr* A, Fr* B, Fr* C, Fr* H, hipStream_t st) {
+    if (dom->curve == GG_CURVE_BN254) compute_h_t(dom->bn.get(), A, B, C, H, st);
+    else compute_h_t(dom->bls.get(), (FrBls*)A, (FrBls*)B, (FrBls*)C, (FrBls*)H, st);
 }
 }  // namespace gg
 

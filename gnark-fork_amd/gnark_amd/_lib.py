@@ -12,7 +12,7 @@ _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GNARK_AMD_LIB", os.path.join(_PKG_DIR, "lib", "libgnark_amd.so"))
 
 GG_OK = 0
-GG_G1, GG_G2, GG_BLS12_381_G1 = 1, 2, 3
+GG_G1, GG_G2, GG_BLS12_381_G1, GG_BLS12_381_G2 = 1, 2, 3, 4
 GG_CURVE_BN254, GG_CURVE_BLS12_381 = 0, 1
 GG_DIF, GG_DIT = 0, 1
 
@@ -79,6 +79,11 @@ def _load():
         "gg_bls12_381_g1_scalar_mul": ([P, P, P], I),
         "gg_groth16_pk_create": ([I, P, P, P, S, P, S, P, S, P, S, P, P, P, P, P, P, P, P, S, S, P, PP], I),
         "gg_groth16_pk_release": ([P], I),
+        "gg_groth16_pk_create_ex": ([I, I, P, P, P, S, P, S, P, S, P, S, P, P, P, P, P, P, P, P, S, S, P, PP], I),
+        "gg_groth16_finalize_ex": ([I, P, P, P, P, P, P, P, P, P, P, P], I),
+        "gg_bls12_381_g2_jac_to_affine": ([P, P], I),
+        "gg_bls12_381_g2_jac_add": ([P, P, P], I),
+        "gg_bls12_381_g2_scalar_mul": ([P, P, P], I),
         "gg_groth16_prove": ([P, P, S, P, P, P, S, I, P, P, P, P, P, P], I),
         "gg_groth16_last_timings": ([ctypes.POINTER(ctypes.c_double)], I),
         "gg_groth16_last_timings_ex": ([ctypes.POINTER(ctypes.c_double), I], I),
@@ -142,7 +147,8 @@ EXPORTED = [
     "gg_fr_to_canonical_be", "gg_groth16_last_timings_ex",
     "gg_groth16_pk_base_info", "gg_plonk_pk_create", "gg_plonk_pk_create_shard", "gg_plonk_pk_release",
     "gg_plonk_pk_vk", "gg_plonk_commit_lagrange", "gg_plonk_proof_size", "gg_plonk_prove",
-    "gg_plonk_last_timings",
+    "gg_plonk_last_timings", "gg_groth16_pk_create_ex", "gg_groth16_finalize_ex",
+    "gg_bls12_381_g2_jac_to_affine", "gg_bls12_381_g2_jac_add", "gg_bls12_381_g2_scalar_mul",
 ]
 
 

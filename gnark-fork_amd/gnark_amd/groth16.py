@@ -1,5 +1,6 @@
-"""Groth16 BN254 on MI355X: mirror of gnark's icicle_bn254 package
-(backend/groth16/bn254/icicle/{icicle.go,provingkey.go}).
+"""Groth16 (BN254, BLS12-381) on MI355X: mirror of gnark's icicle_bn254 package
+(backend/groth16/bn254/icicle/{icicle.go,provingkey.go}); ProvingKeyData(curve=
+"bls12-381") is backend/groth16/bls12-381's key (same prover over BLS12-381).
 
     pk_dev = ProvingKey(pk_data)                      # setupDevicePointers, once
     proof  = prove(pk_dev, solution, opts=[with_amd_acceleration()])
@@ -21,7 +22,10 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import backend, fr
-from ._lib import check, lib, ptr
+from ._lib import check, lib, ptr, GG_CURVE_BN254, GG_CURVE_BLS12_381
+
+# (G1 affine, G2 affine) bytes per curve
+_SIZES = {"bn254": (64, 128), "bls12-381": (96, 192)}
 
 HasAMD = True  # mirrors icicle_bn254.HasIcicle (noicicle.go:16 / icicle.go:29)
 
@@ -46,6 +50,7 @@ class ProvingKeyData:
     domain_generator: Optional[bytes] = None        # pk.Domain.Generator (Montgomery)
     domain_mul_gen: Optional[bytes] = None          # pk.Domain.FrMultiplicativeGen
     k_wire_index: Optional[Sequence[int]] = None    # filterHeap result; None = nb_public + i
+    curve: str = "bn254"                            # or "bls12-381"
 
     @property
     def n_wires(self):
@@ -87,16 +92,25 @@ class ProvingKey:
     def __init__(self, data: ProvingKeyData):
         self.data = data
         n_wires = data.n_wires
-        nA, nB = len(data.g1_A) // 64, len(data.g1_B) // 64
-        nZ, nK = len(data.g1_Z) // 64, len(data.g1_K) // 64
-        omega = data.domain_generator or fr.fr_mont(fr.domain_generator(data.log_n))
-        gen = data.domain_mul_gen or fr.fr_mont(fr.FR_MULTIPLICATIVE_GEN)
+        self.curve = data.curve
+        g1b, self.g2b = _SIZES[data.curve]
+        self.g1b = g1b
+        nA, nB = len(data.g1_A) // g1b, len(data.g1_B) // g1b
+        nZ, nK = len(data.g1_Z) // g1b, len(data.g1_K) // g1b
+        if data.curve == "bn254":
+            cid = GG_CURVE_BN254
+            omega = data.domain_generator or fr.fr_mont(fr.domain_generator(data.log_n))
+            gen = data.domain_mul_gen or fr.fr_mont(fr.FR_MULTIPLICATIVE_GEN)
+        else:
+            cid = GG_CURVE_BLS12_381
+            omega = data.domain_generator or fr.bls_fr_mont(fr.bls_domain_generator(data.log_n))
+            gen = data.domain_mul_gen or fr.bls_fr_mont(fr.BLS_FR_MULTIPLICATIVE_GEN)
         kidx = None
         if data.k_wire_index is not None:
             kidx = np.ascontiguousarray(np.asarray(data.k_wire_index, dtype=np.uint32))
         h = ctypes.c_void_p()
-        check(lib.gg_groth16_pk_create(
-            data.log_n, ptr(omega), ptr(gen),
+        check(lib.gg_groth16_pk_create_ex(
+            cid, data.log_n, ptr(omega), ptr(gen),
             ptr(data.g1_A), nA, ptr(data.g1_B), nB, ptr(data.g1_Z), nZ, ptr(data.g1_K), nK,
             ptr(data.alpha1), ptr(data.beta1), ptr(data.delta1),
             ptr(data.g2_B), ptr(data.beta2), ptr(data.delta2),
@@ -137,9 +151,12 @@ def prove(pk: ProvingKey, solution: Solution, *opts, r: bytes = None, s: bytes =
     if not backend.accelerated(cfg):
         raise RuntimeError("accelerated prover requested without with_amd_acceleration(); "
                            "the CPU prover is gnark's groth16_bn254.Prove (prove.go:63)")
-    r = r if r is not None else _rand_fr_mont()
-    s = s if s is not None else _rand_fr_mont()
-    ar, bs, krs = bytearray(64), bytearray(128), bytearray(64)
+    rnd = _rand_fr_mont if getattr(pk, "curve", "bn254") == "bn254" else \
+        (lambda: fr.bls_fr_mont(secrets.randbelow(fr.BLS_R)))
+    r = r if r is not None else rnd()
+    s = s if s is not None else rnd()
+    g1b, g2b = _SIZES[getattr(pk, "curve", "bn254")]
+    ar, bs, krs = bytearray(g1b), bytearray(g2b), bytearray(g1b)
     check(lib.gg_groth16_prove(pk.handle, ptr(solution.W), solution.n_wires, ptr(solution.A),
                                ptr(solution.B), ptr(solution.C), solution.n_constraints,
                                int(solution.on_device), ptr(r), ptr(s), ptr(ar), ptr(bs),
@@ -275,9 +292,11 @@ def add_partials(parts: Sequence[bytes]) -> bytes:
 
 
 def finalize(data: ProvingKeyData, partials: bytes, r: bytes, s: bytes) -> Proof:
-    """Combination of prove.go:177-299 on the summed partials (host, gg_groth16_finalize)."""
-    ar, bs, krs = bytearray(64), bytearray(128), bytearray(64)
-    check(lib.gg_groth16_finalize(ptr(data.alpha1), ptr(data.beta1), ptr(data.delta1),
+    """Combination of prove.go:177-299 on the summed partials (host, gg_groth16_finalize_ex)."""
+    g1b, g2b = _SIZES[data.curve]
+    ar, bs, krs = bytearray(g1b), bytearray(g2b), bytearray(g1b)
+    cid = GG_CURVE_BN254 if data.curve == "bn254" else GG_CURVE_BLS12_381
+    check(lib.gg_groth16_finalize_ex(cid, ptr(data.alpha1), ptr(data.beta1), ptr(data.delta1),
                                   ptr(data.beta2), ptr(data.delta2), ptr(partials), ptr(r), ptr(s),
                                   ptr(ar), ptr(bs), ptr(krs)))
     return Proof(bytes(ar), bytes(bs), bytes(krs))

@@ -5,19 +5,21 @@ from __future__ import annotations
 
 import ctypes
 
-from ._lib import GG_BLS12_381_G1, GG_G1, GG_G2, check, lib, ptr
+from ._lib import GG_BLS12_381_G1, GG_BLS12_381_G2, GG_G1, GG_G2, check, lib, ptr
 
-G1, G2, BLS12_381_G1 = GG_G1, GG_G2, GG_BLS12_381_G1
-_JAC = {G1: 96, G2: 192, BLS12_381_G1: 144}
-_AFF = {G1: 64, G2: 128, BLS12_381_G1: 96}
+G1, G2, BLS12_381_G1, BLS12_381_G2 = GG_G1, GG_G2, GG_BLS12_381_G1, GG_BLS12_381_G2
+_JAC = {G1: 96, G2: 192, BLS12_381_G1: 144, BLS12_381_G2: 288}
+_AFF = {G1: 64, G2: 128, BLS12_381_G1: 96, BLS12_381_G2: 192}
 _TO_AFF = {G1: "gg_g1_jac_to_affine", G2: "gg_g2_jac_to_affine",
-           BLS12_381_G1: "gg_bls12_381_g1_jac_to_affine"}
-_ADD = {G1: "gg_g1_jac_add", G2: "gg_g2_jac_add", BLS12_381_G1: "gg_bls12_381_g1_jac_add"}
+           BLS12_381_G1: "gg_bls12_381_g1_jac_to_affine", BLS12_381_G2: "gg_bls12_381_g2_jac_to_affine"}
+_ADD = {G1: "gg_g1_jac_add", G2: "gg_g2_jac_add", BLS12_381_G1: "gg_bls12_381_g1_jac_add",
+        BLS12_381_G2: "gg_bls12_381_g2_jac_add"}
 
 
 class MsmBase:
     """n affine points (gnark layout) uploaded once, precomputed, kept in HBM.
-    group: G1 / G2 (BN254) or BLS12_381_G1 (PlonK KZG commitments)."""
+    group: G1 / G2 (BN254), BLS12_381_G1 (PlonK KZG commitments, BLS12-381 Groth16)
+    or BLS12_381_G2 (BLS12-381 Groth16)."""
 
     def __init__(self, group: int, points, n: int, on_device=False, scalar_index=None,
                  window_bits: int = 0):
@@ -74,7 +76,7 @@ def jac_add(group: int, a: bytes, b: bytes) -> bytes:
 def scalar_mul(group: int, p_aff: bytes, k_mont: bytes) -> bytes:
     out = bytearray(_JAC[group])
     fn = {G1: lib.gg_g1_scalar_mul, G2: lib.gg_g2_scalar_mul,
-          BLS12_381_G1: lib.gg_bls12_381_g1_scalar_mul}[group]
+          BLS12_381_G1: lib.gg_bls12_381_g1_scalar_mul, BLS12_381_G2: lib.gg_bls12_381_g2_scalar_mul}[group]
     check(fn(ptr(p_aff), ptr(k_mont), ptr(out)))
     return bytes(out)
 

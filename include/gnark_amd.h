@@ -41,6 +41,9 @@ extern "C" {
 /* BLS12-381 G1 (PlonK KZG commitments): affine 96 B (12-limb fp, R = 2^384),
  * Jacobian 144 B, scalars BLS12-381 fr (32 B Montgomery) */
 #define GG_BLS12_381_G1 3
+/* BLS12-381 G2 (BLS12-381 Groth16 B MSM): affine 192 B ({X.A0, X.A1, Y.A0, Y.A1},
+ * 12-limb fp each), Jacobian 288 B, scalars BLS12-381 fr */
+#define GG_BLS12_381_G2 4
 
 /* curves of a domain (scalar field of the NTT) */
 #define GG_CURVE_BN254 0
@@ -124,7 +127,7 @@ int gg_groth16_compute_h(gg_domain_t d, const void *a, const void *b, const void
  * (icicle.go:88-126).  Points stay resident in HBM together with the
  * window-shifted copies 2^(c*w) * P_i that the bucket MSM uses, so every
  * window shares one bucket set (fixed-base precomputation sized for 288 GB).
- * group: GG_G1 or GG_G2 (BN254), GG_BLS12_381_G1 (PlonK KZG commitments:
+ * group: GG_G1 or GG_G2 (BN254), GG_BLS12_381_G2 (BLS12-381 Groth16), GG_BLS12_381_G1 (PlonK KZG commitments:
  *   kzg.Commit / MultiExp at backend/plonk/bls12-381/prove.go:336, 494, 769,
  *   1165-1169, 1203-1213).  points: n affine points (host or device memory).
  * Infinity points are dropped at upload (fixes the index shift of
@@ -161,6 +164,10 @@ int gg_bls12_381_g1_jac_to_affine(const void *jac, void *aff);
 int gg_bls12_381_g1_jac_add(const void *a_jac, const void *b_jac, void *out_jac);
 /* out (Jacobian) = k * p, p affine, k bls12-381 fr Montgomery (host; KZG digest folding) */
 int gg_bls12_381_g1_scalar_mul(const void *p_aff, const void *k_mont, void *out_jac);
+/* BLS12-381 G2 (G2Jac.FromJacobian / AddAssign / ScalarMultiplication, BLS12-381 Groth16 epilogue) */
+int gg_bls12_381_g2_jac_to_affine(const void *jac, void *aff);
+int gg_bls12_381_g2_jac_add(const void *a_jac, const void *b_jac, void *out_jac);
+int gg_bls12_381_g2_scalar_mul(const void *p_aff, const void *k_mont, void *out_jac);
 
 /* Fixed-base batch scalar multiplication out[i] = k_i * base (affine,
  * infinity for k_i = 0): replaces curve.BatchScalarMultiplicationG1/G2
@@ -187,6 +194,17 @@ int gg_groth16_pk_create(int log_n, const void *omega_mont, const void *coset_ge
                          const void *g2_B, const void *beta2, const void *delta2,
                          const uint8_t *inf_A, const uint8_t *inf_B, size_t n_wires,
                          size_t nb_public, const uint32_t *k_wire_index, gg_groth16_pk_t *out);
+/* Same for a chosen curve: GG_CURVE_BN254 (= gg_groth16_pk_create) or
+ * GG_CURVE_BLS12_381 (backend/groth16/bls12-381: the same prover over
+ * BLS12-381; points in that curve's layout: G1 affine 96 B, G2 affine 192 B,
+ * fr 32 B).  Output points of gg_groth16_prove then have those sizes too. */
+int gg_groth16_pk_create_ex(int curve, int log_n, const void *omega_mont, const void *coset_gen_mont,
+                            const void *g1_A, size_t nA, const void *g1_B, size_t nB,
+                            const void *g1_Z, size_t nZ, const void *g1_K, size_t nK,
+                            const void *alpha1, const void *beta1, const void *delta1,
+                            const void *g2_B, const void *beta2, const void *delta2,
+                            const uint8_t *inf_A, const uint8_t *inf_B, size_t n_wires,
+                            size_t nb_public, const uint32_t *k_wire_index, gg_groth16_pk_t *out);
 int gg_groth16_pk_release(gg_groth16_pk_t pk);
 /* resident MSM base `which` of a key (0 = G1.A, 1 = G1.B, 2 = G1.K, 3 = G1.Z,
  * 4 = G2.B): as gg_msm_base_info */
@@ -239,6 +257,11 @@ int gg_groth16_finalize(const void *alpha1, const void *beta1, const void *delta
                         const void *beta2, const void *delta2, const void *partials,
                         const void *r_mont, const void *s_mont, void *ar_aff, void *bs_aff,
                         void *krs_aff);
+/* gg_groth16_finalize for a chosen curve (BLS12-381 partials: 4 x 144 + 288 B) */
+int gg_groth16_finalize_ex(int curve, const void *alpha1, const void *beta1, const void *delta1,
+                           const void *beta2, const void *delta2, const void *partials,
+                           const void *r_mont, const void *s_mont, void *ar_aff, void *bs_aff,
+                           void *krs_aff);
 
 /* ---- distributed computeH ("four-step multi-GPU NTT").
  * n = 2^log_n = m * world (world a power of two <= 16, n >= world^2).  Rank r

@@ -150,6 +150,189 @@ def g1_decompress_zcash(b: bytes):
     return (x, y)
 
 
+# ---------------------------------------------------------------- Fp2 / G2 (exact, affine)
+# Fp2 = Fp[u] / (u^2 + 1), elements (a0, a1); G2: y^2 = x^3 + 4 (1 + u) (the M-twist
+# of gnark-crypto ecc/bls12-381), pinned by the compressed G2 points of
+# backend/groth16/bellman_test.go (on the curve, order r).
+B2 = (4, 4)
+G2_GEN = ((0x024AA2B2F08F0A91260805272DC51051C6E47AD4FA403B02B4510B647AE3D1770BAC0326A805BBEFD48056C8C121BDB8,
+           0x13E02B6052719F607DACD3A088274F65596BD0D09920B61AB5DA61BBDC7F5049334CF11213945D57E5AC7D055D042B7E),
+          (0x0CE5D527727D6E118CC9CDC6DA2E351AADFD9BAA8CBDD3A76D429A695160D12C923AC9CC3BACA289E193548608B82801,
+           0x0606C4A02EA734CC32ACD2B02BC28B99CB3E287E85A763AF267492AB572E99AB3F370D275CEC1DA1AAA9075FF05F79BE))
+
+
+def f2_add(a, b):
+    return ((a[0] + b[0]) % P, (a[1] + b[1]) % P)
+
+
+def f2_sub(a, b):
+    return ((a[0] - b[0]) % P, (a[1] - b[1]) % P)
+
+
+def f2_mul(a, b):
+    return ((a[0] * b[0] - a[1] * b[1]) % P, (a[0] * b[1] + a[1] * b[0]) % P)
+
+
+def f2_inv(a):
+    t = pow((a[0] * a[0] + a[1] * a[1]) % P, -1, P)
+    return (a[0] * t % P, (-a[1]) * t % P)
+
+
+def f2_pow(a, e):
+    r, b = (1, 0), a
+    while e:
+        if e & 1:
+            r = f2_mul(r, b)
+        b = f2_mul(b, b)
+        e >>= 1
+    return r
+
+
+def f2_sqrt(a):
+    """sqrt in Fp2 for p = 3 mod 4 (Adj-Rodriguez-Henriquez, algorithm 9); None if a is a non-square."""
+    a1 = f2_pow(a, (P - 3) // 4)
+    alpha = f2_mul(a1, f2_mul(a1, a))
+    a0 = f2_mul((alpha[0], (-alpha[1]) % P), alpha)  # alpha^p * alpha
+    if a0 == (P - 1, 0):
+        return None
+    x0 = f2_mul(a1, a)
+    if alpha == (P - 1, 0):
+        x = f2_mul((0, 1), x0)
+    else:
+        x = f2_mul(f2_pow(f2_add((1, 0), alpha), (P - 1) // 2), x0)
+    return x if f2_mul(x, x) == (a[0] % P, a[1] % P) else None
+
+
+def g2_on_curve(p) -> bool:
+    if p is INF:
+        return True
+    x, y = p
+    return f2_sub(f2_mul(y, y), f2_add(f2_mul(f2_mul(x, x), x), B2)) == (0, 0)
+
+
+def g2_add(p, q):
+    if p is INF:
+        return q
+    if q is INF:
+        return p
+    if p[0] == q[0]:
+        if f2_add(p[1], q[1]) == (0, 0):
+            return INF
+        xx = f2_mul(p[0], p[0])
+        lam = f2_mul(f2_add(f2_add(xx, xx), xx), f2_inv(f2_add(p[1], p[1])))
+    else:
+        lam = f2_mul(f2_sub(q[1], p[1]), f2_inv(f2_sub(q[0], p[0])))
+    x = f2_sub(f2_sub(f2_mul(lam, lam), p[0]), q[0])
+    return (x, f2_sub(f2_mul(lam, f2_sub(p[0], x)), p[1]))
+
+
+def g2_mul(p, k: int, reduce=True):
+    if reduce:
+        k %= R
+    acc, base = INF, p
+    while k:
+        if k & 1:
+            acc = g2_add(acc, base)
+        base = g2_add(base, base)
+        k >>= 1
+    return acc
+
+
+def f2_lex_largest(y) -> bool:
+    """E2.LexicographicallyLargest: compare A1 first, A0 if A1 = 0."""
+    if y[1]:
+        return y[1] > P - y[1]
+    return y[0] > P - y[0]
+
+
+def g2_decompress_zcash(b: bytes):
+    """Zcash/bellman compressed G2 (96 B: X.A1 | X.A0 big-endian; flags on the first byte)."""
+    assert len(b) == 96 and b[0] & 0x80
+    if b[0] & 0x40:
+        return INF
+    x1 = int.from_bytes(bytes([b[0] & 0x1F]) + b[1:48], "big")
+    x0 = int.from_bytes(b[48:], "big")
+    x = (x0, x1)
+    y = f2_sqrt(f2_add(f2_mul(f2_mul(x, x), x), B2))
+    if y is None:
+        raise ValueError("not on curve")
+    if bool(b[0] & 0x20) != f2_lex_largest(y):
+        y = ((-y[0]) % P, (-y[1]) % P)
+    return (x, y)
+
+
+def g2_compress(p) -> bytes:
+    if p is INF:
+        return bytes([0xC0]) + bytes(95)
+    b = bytearray(p[0][1].to_bytes(48, "big") + p[0][0].to_bytes(48, "big"))
+    b[0] |= 0xA0 if f2_lex_largest(p[1]) else 0x80
+    return bytes(b)
+
+
+def g2_to_bytes(p) -> bytes:
+    """gnark bls12381.G2Affine in memory {X.A0, X.A1, Y.A0, Y.A1}; infinity = zeros."""
+    if p is INF:
+        return bytes(192)
+    return b"".join(fp_to_bytes(v) for v in (p[0][0], p[0][1], p[1][0], p[1][1]))
+
+
+def g2_from_bytes(b: bytes):
+    if b == bytes(192):
+        return INF
+    v = [fp_from_bytes(b[i:i + 48]) for i in range(0, 192, 48)]
+    return ((v[0], v[1]), (v[2], v[3]))
+
+
+# ---------------------------------------------------------------- Groth16 over BLS12-381
+def groth16_setup_scalars(constraints, nb_wires, nb_public, log_n, t, alpha, beta, delta):
+    """Discrete logs of a backend/groth16/bls12-381 proving key (setup.go:85-337
+    with given toxic waste): per-wire u_i(t), v_i(t), w_i(t) by the Lagrange
+    recurrence of setup.go:352-434, then pk.G1.A/B (filtered), K, Z (bit-reversed,
+    n - 1) and the infinity masks.  constraints: [(L, R, O)], each [(wire, coeff)]."""
+    n = 1 << log_n
+    w = pow(FR_GEN, (R - 1) >> log_n, R)
+    A, B, C = [0] * nb_wires, [0] * nb_wires, [0] * nb_wires
+    tv = []
+    wi = 1
+    for _ in range(len(constraints) + 1):
+        tv.append((t - wi) % R)
+        wi = wi * w % R
+    L = (pow(t, n, R) - 1) * pow(tv[0], -1, R) % R * pow(n, -1, R) % R
+    for j, (lc, rc, oc) in enumerate(constraints):
+        for wid, k in lc:
+            A[wid] = (A[wid] + k * L) % R
+        for wid, k in rc:
+            B[wid] = (B[wid] + k * L) % R
+        for wid, k in oc:
+            C[wid] = (C[wid] + k * L) % R
+        L = L * w % R * tv[j] % R * pow(tv[j + 1], -1, R) % R
+    dinv = pow(delta, -1, R)
+    K = [(A[i] * beta + B[i] * alpha + C[i]) * dinv % R for i in range(nb_public, nb_wires)]
+    zt = (pow(t, n, R) - 1) * dinv % R
+    Z = [zt * pow(t, i, R) % R for i in range(n)]
+    Z = [Z[bitrev(i, log_n)] for i in range(n)][: n - 1]
+    return {"A": [a for a in A if a], "B": [b for b in B if b], "K": K, "Z": Z,
+            "infA": [int(a == 0) for a in A], "infB": [int(b == 0) for b in B], "u": A, "v": B, "w": C}
+
+
+def groth16_expected_scalars(constraints, wires, nb_public, log_n, ks, t, alpha, beta, delta, r, s):
+    """Discrete logs (a, b, c) of the proof Ar, Bs, Krs of prove.go:63-322 for a
+    satisfied instance: h(t) Z(t) = A(t) B(t) - C(t) with A(t) = sum_j A_j L_j(t)
+    over the constraint rows -- no FFT needed."""
+    n = 1 << log_n
+    u, v, wv = ks["u"], ks["v"], ks["w"]
+    a = (alpha + sum(x * y for x, y in zip(wires, u)) + r * delta) % R
+    b = (beta + sum(x * y for x, y in zip(wires, v)) + s * delta) % R
+    ct = sum(x * y for x, y in zip(wires, wv)) % R
+    # A(t) B(t) - C(t) = a' b' - c' with a' = sum w_i u_i(t) etc. (u_i(t) already Lagrange-summed)
+    at = sum(x * y for x, y in zip(wires, u)) % R
+    bt = sum(x * y for x, y in zip(wires, v)) % R
+    hz = (at * bt - ct) % R
+    priv = sum(wires[i] * ((u[i] * beta + v[i] * alpha + wv[i]) % R) for i in range(nb_public, len(wires))) % R
+    c = ((priv + hz) * pow(delta, -1, R) + s * a + r * b - r * s * delta) % R
+    return a, b, c
+
+
 # ---------------------------------------------------------------- FFT (gnark conventions)
 def bitrev(i: int, logn: int) -> int:
     return int(format(i, f"0{logn}b")[::-1], 2) if logn else 0

@@ -156,3 +156,48 @@ def test_expand_message_xmd_rfc9380_vectors():
         "68a985b87eb6b46952128911f2a4412bbc302a9d759667f87f7a21d803f07235"
     assert b.expand_message_xmd(b"abc", dst, 0x20).hex() == \
         "d8ccab23b5985ccea865c6c97b6e5b8350e794e603b4b97902f53a8a0d605615"
+
+
+def test_bellman_g2_points_decompress_recompress():
+    """The compressed G2 points of the reference's BLS12-381 Groth16 KATs
+    (bellman_test.go: vk beta/gamma/delta_g2, proof B) decompress onto
+    y^2 = x^3 + 4(1 + u), lie in the order-r subgroup and re-encode byte for
+    byte; the standard generator G2_GEN used by the tests is on the same curve."""
+    assert len(PINS["g2_compressed"]) >= 10
+    for h in PINS["g2_compressed"][:12]:
+        raw = bytes.fromhex(h)
+        p = b.g2_decompress_zcash(raw)
+        assert b.g2_on_curve(p)
+        assert b.g2_compress(p) == raw
+        assert b.g2_mul(p, b.R, reduce=False) is b.INF
+    assert b.g2_on_curve(b.G2_GEN) and b.g2_mul(b.G2_GEN, b.R, reduce=False) is b.INF
+    q = b.g2_mul(b.G2_GEN, 7)
+    assert b.g2_add(q, b.g2_mul(b.G2_GEN, 5)) == b.g2_mul(b.G2_GEN, 12)
+    assert b.g2_from_bytes(b.g2_to_bytes(q)) == q
+
+
+def test_groth16_bls_oracle_scalars_cubic():
+    """groth16_expected_scalars on the cubic circuit (examples/cubic, x^3 + x + 5 = y)
+    over BLS12-381: the h(t) Z(t) = A(t) B(t) - C(t) shortcut agrees with an explicit
+    interpolation of A, B, C over the domain."""
+    R = b.R
+    cons = [([(2, 1)], [(2, 1)], [(3, 1)]), ([(3, 1)], [(2, 1)], [(4, 1)]),
+            ([(0, 1)], [(1, 1)], [(4, 1), (2, 1), (0, 5)])]
+    w = [1, 35, 3, 9, 27]
+    ks = b.groth16_setup_scalars(cons, 5, 2, 2, 123456789, 11, 13, 17)
+    a, bb, c = b.groth16_expected_scalars(cons, w, 2, 2, ks, 123456789, 11, 13, 17, 3, 4)
+    # A(t) = sum_j A_j L_j(t), by direct Lagrange interpolation over the 4-point domain
+    n, t = 4, 123456789
+    om = pow(b.FR_GEN, (R - 1) >> 2, R)
+    pts = [pow(om, j, R) for j in range(n)]
+
+    def lag(j):
+        num, den = 1, 1
+        for k in range(n):
+            if k != j:
+                num = num * (t - pts[k]) % R
+                den = den * (pts[j] - pts[k]) % R
+        return num * pow(den, -1, R) % R
+    ev = [sum(w[i] * k for i, k in row) % R for row in (r[0] for r in cons)]
+    At = sum(ev[j] * lag(j) for j in range(3)) % R
+    assert a == (11 + At + 3 * 17) % R
