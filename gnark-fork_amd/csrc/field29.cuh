@@ -1,0 +1,188 @@
+// Reduced-radix Montgomery arithmetic for the bucket-accumulation hot loop.
+//
+// An element of BN254 Fp is held as 9 limbs of 29 bits (261 bits) in
+// Montgomery form with R' = 2^261, lazily reduced (value < a small multiple of
+// p, tracked per call site).  Why: on gfx950 the 32-bit-limb product-scanning
+// multiply (field.cuh) spends one v_addc per v_mad_u64_u32 to fold the column
+// carry (128 + 128 instructions plus the final subtraction).  With 29-bit limbs
+// a column of the Montgomery product is at most 18 products of < 2^58 (or 9 of
+// < 2^60 plus 9 of < 2^58 when one operand is an unnormalised sum), which fits
+// a 64-bit accumulator with no carry-out: 162 v_mad_u64_u32 and ~60 shifts /
+// masks, no carry chain, no final subtraction.
+//
+// The representation never leaves the accumulation kernels: base points are
+// stored as x * 2^261 mod p (canonical, packed into the 8 x u32 gnark layout,
+// prepared once when the base is built) and unpacked with funnel shifts; the
+// bucket partials are converted back to gnark's x * 2^256 mod p (canonical)
+// before they are written.  Results are therefore bit-identical to the
+// 32-bit-limb path.
+//
+// Bounds (M = 2^261 = 169.28 p):
+//   mul(a, b) < a b / M + p      (any a, b < 2^260 with limbs < 2^30)
+//   sub<k>(a, b) = a + k p - b   (requires b < (k - 1) p + 2^232, so the
+//                                 borrowed limbs of k p dominate b's)
+#pragma once
+#include "field.cuh"
+
+namespace gg {
+
+struct Fp29Cfg {
+    static constexpr int N = 9;
+    static constexpr int B = 29;
+    static constexpr uint32_t MASK = (1u << B) - 1;
+    static constexpr uint32_t P[9] = {0x187cfd47u, 0x010460b6u, 0x1c72a34fu, 0x02d522d0u, 0x1585d978u,
+                                      0x02db40c0u, 0x00a6e141u, 0x0e5c2634u, 0x0030644eu};
+    static constexpr uint32_t INV = 0x04866389u;   // -p^-1 mod 2^29
+    static constexpr uint32_t PINV = 0x1b799c77u;  // p^-1 mod 2^29
+    // 2^256 mod p as a 29-bit-limb integer: mul(x * 2^261, C_OUT) = x * 2^256
+    static constexpr uint32_t C_OUT[9] = {0x058f0d9du, 0x1aea1c6eu, 0x11c2cf74u, 0x11d651ebu, 0x1462c0a7u,
+                                          0x11b7bc3cu, 0x1cbd99bau, 0x183340fbu, 0x000e0a77u};
+    // 2^261 mod p in the gnark 32-bit layout: mont256(x * 2^256, C_IN) = x * 2^261
+    static constexpr uint32_t C_IN[8] = {0x157ccc21u, 0x4e8384ebu, 0x0ce148c3u, 0xfb90a602u,
+                                         0x819caa36u, 0x5301fa84u, 0x563d4475u, 0x0dc83629u};
+    // k p (k = 1..8) with limbs 0..7 borrowed into [2^29, 2^30): k p - b limb by
+    // limb never goes negative for normalised b < (k - 1) p + 2^232.
+    static constexpr uint32_t KP[8][9] = {
+        {0x387cfd47u, 0x210460b5u, 0x3c72a34eu, 0x22d522cfu, 0x3585d977u, 0x22db40bfu, 0x20a6e140u, 0x2e5c2633u, 0x0030644du},
+        {0x30f9fa8eu, 0x2208c16cu, 0x38e5469du, 0x25aa45a0u, 0x2b0bb2efu, 0x25b68180u, 0x214dc281u, 0x3cb84c67u, 0x0060c89bu},
+        {0x2976f7d5u, 0x230d2223u, 0x3557e9ecu, 0x287f6871u, 0x20918c67u, 0x2891c241u, 0x21f4a3c2u, 0x2b14729bu, 0x00912ceau},
+        {0x21f3f51cu, 0x241182dau, 0x31ca8d3bu, 0x2b548b42u, 0x361765dfu, 0x2b6d0301u, 0x229b8503u, 0x397098cfu, 0x00c19138u},
+        {0x3a70f263u, 0x2515e390u, 0x2e3d308au, 0x2e29ae13u, 0x2b9d3f57u, 0x2e4843c2u, 0x23426644u, 0x27ccbf03u, 0x00f1f587u},
+        {0x32edefaau, 0x261a4447u, 0x2aafd3d9u, 0x30fed0e4u, 0x212318cfu, 0x31238483u, 0x23e94785u, 0x3628e537u, 0x012259d5u},
+        {0x2b6aecf1u, 0x271ea4feu, 0x27227728u, 0x33d3f3b5u, 0x36a8f247u, 0x33fec543u, 0x249028c6u, 0x24850b6bu, 0x0152be24u},
+        {0x23e7ea38u, 0x282305b5u, 0x23951a77u, 0x36a91686u, 0x2c2ecbbfu, 0x36da0604u, 0x25370a07u, 0x32e1319fu, 0x01832272u}};
+};
+
+template <class C>
+struct Fl {
+    uint32_t l[C::N];
+};
+using Fp29 = Fl<Fp29Cfg>;
+
+// Montgomery product a b / 2^(B N) by operand-interleaved product scanning.
+// Output limbs 0..N-2 < 2^B (normalised); value < a b / M + p.
+template <class C>
+__device__ __forceinline__ Fl<C> mul(const Fl<C>& a, const Fl<C>& b) {
+    constexpr int N = C::N, B = C::B;
+    uint32_t m[N];
+    Fl<C> r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++)
+            acc += (uint64_t)a.l[i] * b.l[k - i];
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k - 1 : N - 1); i++)
+            acc += (uint64_t)m[i] * C::P[k - i];
+        if (k < N) {
+            m[k] = ((uint32_t)acc * C::INV) & C::MASK;
+            acc += (uint64_t)m[k] * C::P[0];
+        } else {
+            r.l[k - N] = (uint32_t)acc & C::MASK;
+        }
+        acc >>= B;
+    }
+    r.l[N - 1] = (uint32_t)acc;
+    return r;
+}
+
+// a + b, normalised
+template <class C>
+__device__ __forceinline__ Fl<C> add(const Fl<C>& a, const Fl<C>& b) {
+    Fl<C> r;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < C::N - 1; i++) {
+        const uint32_t t = a.l[i] + b.l[i] + c;
+        r.l[i] = t & C::MASK;
+        c = t >> C::B;
+    }
+    r.l[C::N - 1] = a.l[C::N - 1] + b.l[C::N - 1] + c;
+    return r;
+}
+
+// a + k p - b, normalised (b < (k - 1) p + 2^232, see KP)
+template <int K, class C>
+__device__ __forceinline__ Fl<C> sub(const Fl<C>& a, const Fl<C>& b) {
+    static_assert(K >= 1 && K <= 8, "multiple of p");
+    Fl<C> r;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < C::N - 1; i++) {
+        const uint32_t t = a.l[i] + (C::KP[K - 1][i] - b.l[i]) + c;
+        r.l[i] = t & C::MASK;
+        c = t >> C::B;
+    }
+    r.l[C::N - 1] = a.l[C::N - 1] + (C::KP[K - 1][C::N - 1] - b.l[C::N - 1]) + c;
+    return r;
+}
+
+// v == 0 mod p for a normalised v < kmax p: v = j p with j = v_0 p^-1 mod 2^B
+template <class C>
+__device__ __forceinline__ bool is_zero_mod(const Fl<C>& v, uint32_t kmax) {
+    const uint32_t j = (v.l[0] * C::PINV) & C::MASK;
+    if (j > kmax) return false;
+    uint64_t acc = 0;
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < C::N - 1; i++) {
+        acc += (uint64_t)j * C::P[i];
+        diff |= ((uint32_t)acc & C::MASK) ^ v.l[i];
+        acc >>= C::B;
+    }
+    acc += (uint64_t)j * C::P[C::N - 1];
+    diff |= (uint32_t)acc ^ v.l[C::N - 1];
+    return diff == 0;
+}
+
+// 8 x u32 (x * 2^261 mod p, < 2^256) -> 9 x 29-bit limbs
+__device__ __forceinline__ Fp29 unpack29(const Fp& w) {
+    Fp29 r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        const int bit = 29 * i, wi = bit >> 5, off = bit & 31;
+        uint32_t x = w.v[wi] >> off;
+        if (off > 3 && wi + 1 < 8) x |= w.v[wi + 1] << (32 - off);
+        r.l[i] = i == 8 ? x : (x & Fp29Cfg::MASK);
+    }
+    return r;
+}
+// normalised 9 x 29-bit limbs of a value < 2^256 -> 8 x u32
+__device__ __forceinline__ Fp pack29(const Fp29& a) {
+    Fp r;
+#pragma unroll
+    for (int wi = 0; wi < 8; wi++) {
+        const int bit = 32 * wi, i = bit / 29, off = bit % 29;
+        uint32_t x = a.l[i] >> off;
+        if (i + 1 < 9) x |= a.l[i + 1] << (29 - off);
+        if (off > 26 && i + 2 < 9) x |= a.l[i + 2] << (58 - off);
+        r.v[wi] = x;
+    }
+    return r;
+}
+// a (R' form, any normalised value < 8 p) -> canonical gnark Montgomery x * 2^256 mod p
+__device__ __forceinline__ Fp to_std(const Fp29& a) {
+    Fp29 c;
+#pragma unroll
+    for (int i = 0; i < 9; i++) c.l[i] = Fp29Cfg::C_OUT[i];
+    Fp t = pack29(mul(a, c));  // < 8 p * p / M + p < 1.05 p
+    Fp s;
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = __builtin_subc(t.v[i], FpCfg::P[i], br, &br);
+#pragma unroll
+    for (int i = 0; i < 8; i++) t.v[i] = br ? t.v[i] : s.v[i];
+    return t;
+}
+
+// gnark Montgomery x * 2^256 -> x * 2^261 mod p (canonical, 8 x u32): the
+// stored form of precomputed base points
+GG_HD Fp to_r261(const Fp& x) {
+    Fp c;
+#pragma unroll
+    for (int i = 0; i < 8; i++) c.v[i] = Fp29Cfg::C_IN[i];
+    return x * c;
+}
+
+}  // namespace gg

@@ -3,7 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
-#include "../gnark-fork_amd/csrc/field.cuh"
+#include "../gnark-fork_amd/csrc/field29.cuh"
 using namespace gg;
 
 template <class C>
@@ -35,6 +35,12 @@ template <int V>
 __global__ void __launch_bounds__(256) k_mulchain(Fp* data, int iters) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     Fp a = data[2 * i], b = data[2 * i + 1], c = a, d = b;
+    if (V == 2) {  // 29-bit reduced-radix form (field29.cuh)
+        Fp29 a2 = unpack29(to_r261(a)), b2 = unpack29(to_r261(b)), c2 = a2, d2 = b2;
+        for (int k = 0; k < iters; k++) { a2 = mul(a2, b2); c2 = mul(c2, d2); b2 = mul(b2, a2); d2 = mul(d2, c2); }
+        data[2 * i] = to_std(a2) + to_std(c2); data[2 * i + 1] = to_std(b2) + to_std(d2);
+        return;
+    }
     for (int k = 0; k < iters; k++) {
         if (V == 0) { a = mul_cios(a, b); c = mul_cios(c, d); b = mul_cios(b, a); d = mul_cios(d, c); }
         else { a = a * b; c = c * d; b = b * a; d = d * c; }
@@ -62,6 +68,33 @@ __global__ void __launch_bounds__(256) k_mad(uint64_t* out, int iters) {
     out[i] = x0 ^ x1 ^ x2 ^ x3 ^ x4 ^ x5 ^ x6 ^ x7;
 }
 
+// pure v_mad_u64_u32 throughput: 16 independent accumulators; MIX adds 16
+// independent 32-bit add chains per iteration (do they co-issue with the mads?)
+template <int MIX>
+__global__ void __launch_bounds__(256) k_mad_tp(uint64_t* out, int iters) {
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t a[16], b = (uint32_t)i ^ 0x9e3779b9u;
+    uint64_t x[16];
+    uint32_t y[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) a[j] = (uint32_t)i * 2654435761u + j;
+#pragma unroll
+    for (int j = 0; j < 16; j++) { x[j] = i + j; y[j] = (uint32_t)i ^ (j * 77u); }
+    for (int k = 0; k < iters; k++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) asm volatile("" : "+v"(a[j]));
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            x[j] = (uint64_t)a[j] * b + x[j];
+            if (MIX) asm volatile("v_add_u32 %0, %0, %1\n\tv_xor_b32 %0, %0, %2" : "+v"(y[j]) : "v"(a[j]), "v"(b));
+        }
+    }
+    uint64_t r = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) r ^= x[j] + y[j];
+    out[i] = r;
+}
+
 int main() {
     const int blocks = 256 * 16, threads = 256;
     size_t n = (size_t)blocks * threads;
@@ -84,8 +117,26 @@ int main() {
         (void)hipEventElapsedTime(&ms, e0, e1);
         printf("{\"variant\": \"product_scanning\", \"fp_mont_mul_per_s\": %.4e}\n", (double)n * iters * 4 / (ms * 1e-3));
     }
-    // equality of the two variants on the same data
-    k_mulchain<0><<<blocks, threads>>>(d, 7); k_mulchain<1><<<blocks, threads>>>(d2, 7);
+    Fp* d3; (void)hipMalloc(&d3, 2 * n * sizeof(Fp));
+    (void)hipMemcpy(d3, h.data(), 2 * n * sizeof(Fp), hipMemcpyHostToDevice);
+    for (int rep = 0; rep < 3; rep++) {
+        k_mulchain<2><<<blocks, threads>>>(d3, 4);
+        (void)hipEventRecord(e0); k_mulchain<2><<<blocks, threads>>>(d3, iters); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        printf("{\"variant\": \"radix29\", \"fp_mont_mul_per_s\": %.4e}\n", (double)n * iters * 4 / (ms * 1e-3));
+    }
+    // equality of the variants on the same data
+    (void)hipMemcpy(d, h.data(), 2 * n * sizeof(Fp), hipMemcpyHostToDevice);
+    (void)hipMemcpy(d2, h.data(), 2 * n * sizeof(Fp), hipMemcpyHostToDevice);
+    (void)hipMemcpy(d3, h.data(), 2 * n * sizeof(Fp), hipMemcpyHostToDevice);
+    k_mulchain<0><<<blocks, threads>>>(d, 7); k_mulchain<1><<<blocks, threads>>>(d2, 7); k_mulchain<2><<<blocks, threads>>>(d3, 7);
+    {
+        std::vector<Fp> r1(2 * n), r3(2 * n);
+        (void)hipMemcpy(r1.data(), d, 2 * n * sizeof(Fp), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(r3.data(), d3, 2 * n * sizeof(Fp), hipMemcpyDeviceToHost);
+        size_t diff = 0; for (size_t i = 0; i < 2 * n; i++) diff += !(r1[i] == r3[i]);
+        printf("{\"radix29_differs\": %zu}\n", diff);
+    }
     std::vector<Fp> r1(2 * n), r2(2 * n);
     (void)hipMemcpy(r1.data(), d, 2 * n * sizeof(Fp), hipMemcpyDeviceToHost);
     (void)hipMemcpy(r2.data(), d2, 2 * n * sizeof(Fp), hipMemcpyDeviceToHost);
@@ -102,5 +153,16 @@ int main() {
     (void)hipEventRecord(e0); k_mad<<<blocks, threads>>>(o, 4096); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
     (void)hipEventElapsedTime(&ms, e0, e1);
     printf("{\"mad_u64_u32_per_s\": %.4e}\n", (double)n * 4096 * 8 / (ms * 1e-3));
+    for (int mix = 0; mix < 2; mix++) {
+        for (int rep = 0; rep < 2; rep++) {
+            if (mix) k_mad_tp<1><<<blocks, threads>>>(o, 4); else k_mad_tp<0><<<blocks, threads>>>(o, 4);
+            (void)hipEventRecord(e0);
+            if (mix) k_mad_tp<1><<<blocks, threads>>>(o, 2048); else k_mad_tp<0><<<blocks, threads>>>(o, 2048);
+            (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            printf("{\"mad_tp_mix\": %d, \"mad_per_s\": %.4e, \"wave_cycles_per_iter_at_2.4GHz\": %.1f}\n", mix,
+                   (double)n * 2048 * 16 / (ms * 1e-3), ms * 1e-3 * 2.4e9 * 1024 / ((double)n / 64 * 2048));
+        }
+    }
     return 0;
 }
