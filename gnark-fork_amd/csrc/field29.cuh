@@ -22,7 +22,7 @@
 //   sub<k>(a, b) = a + k p - b   (requires b < (k - 1) p + 2^232, so the
 //                                 borrowed limbs of k p dominate b's)
 #pragma once
-#include "field.cuh"
+#include "curve.cuh"
 
 namespace gg {
 
@@ -32,6 +32,9 @@ struct Fp29Cfg {
     static constexpr uint32_t MASK = (1u << B) - 1;
     static constexpr uint32_t P[9] = {0x187cfd47u, 0x010460b6u, 0x1c72a34fu, 0x02d522d0u, 0x1585d978u,
                                       0x02db40c0u, 0x00a6e141u, 0x0e5c2634u, 0x0030644eu};
+    // 2^261 mod p: one in R' form
+    static constexpr uint32_t ONE[9] = {0x157ccc21u, 0x141c2758u, 0x185230d3u, 0x014c0419u, 0x0aa36fb9u,
+                                        0x1d4240ceu, 0x11d54c07u, 0x052ac7a8u, 0x000dc836u};
     static constexpr uint32_t INV = 0x04866389u;   // -p^-1 mod 2^29
     static constexpr uint32_t PINV = 0x1b799c77u;  // p^-1 mod 2^29
     // 2^256 mod p as a 29-bit-limb integer: mul(x * 2^261, C_OUT) = x * 2^256
@@ -87,6 +90,66 @@ __device__ __forceinline__ Fl<C> mul(const Fl<C>& a, const Fl<C>& b) {
     return r;
 }
 
+// a b + c d with one reduction: (a b + c d) / M, value < (a b + c d) / M + p.
+// A column holds 18 products and 9 reduction products of < 2^58: < 2^63.
+template <class C>
+__device__ __forceinline__ Fl<C> mul2(const Fl<C>& a, const Fl<C>& b, const Fl<C>& c, const Fl<C>& d) {
+    constexpr int N = C::N, B = C::B;
+    uint32_t m[N];
+    Fl<C> r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) {
+            acc += (uint64_t)a.l[i] * b.l[k - i];
+            acc += (uint64_t)c.l[i] * d.l[k - i];
+        }
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k - 1 : N - 1); i++)
+            acc += (uint64_t)m[i] * C::P[k - i];
+        if (k < N) {
+            m[k] = ((uint32_t)acc * C::INV) & C::MASK;
+            acc += (uint64_t)m[k] * C::P[0];
+        } else {
+            r.l[k - N] = (uint32_t)acc & C::MASK;
+        }
+        acc >>= B;
+    }
+    r.l[N - 1] = (uint32_t)acc;
+    return r;
+}
+
+// a b / M + K p - s with the subtraction folded into the output columns (the
+// reduction's carry chain normalises it): same bound rule on s as sub<K>
+template <int K, class C>
+__device__ __forceinline__ Fl<C> mul_sub(const Fl<C>& a, const Fl<C>& b, const Fl<C>& s) {
+    static_assert(K >= 1 && K <= 8, "multiple of p");
+    constexpr int N = C::N, B = C::B;
+    uint32_t m[N];
+    Fl<C> r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++)
+            acc += (uint64_t)a.l[i] * b.l[k - i];
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k - 1 : N - 1); i++)
+            acc += (uint64_t)m[i] * C::P[k - i];
+        if (k < N) {
+            m[k] = ((uint32_t)acc * C::INV) & C::MASK;
+            acc += (uint64_t)m[k] * C::P[0];
+        } else {
+            acc += C::KP[K - 1][k - N] - s.l[k - N];
+            r.l[k - N] = (uint32_t)acc & C::MASK;
+        }
+        acc >>= B;
+    }
+    r.l[N - 1] = (uint32_t)acc + (C::KP[K - 1][N - 1] - s.l[N - 1]);
+    return r;
+}
+
 // a + b, normalised
 template <class C>
 __device__ __forceinline__ Fl<C> add(const Fl<C>& a, const Fl<C>& b) {
@@ -136,6 +199,14 @@ __device__ __forceinline__ bool is_zero_mod(const Fl<C>& v, uint32_t kmax) {
     return diff == 0;
 }
 
+template <class C>
+__device__ __forceinline__ Fl<C> fl_const(const uint32_t (&v)[C::N]) {
+    Fl<C> r;
+#pragma unroll
+    for (int i = 0; i < C::N; i++) r.l[i] = v[i];
+    return r;
+}
+
 // 8 x u32 (x * 2^261 mod p, < 2^256) -> 9 x 29-bit limbs
 __device__ __forceinline__ Fp29 unpack29(const Fp& w) {
     Fp29 r;
@@ -163,10 +234,7 @@ __device__ __forceinline__ Fp pack29(const Fp29& a) {
 }
 // a (R' form, any normalised value < 8 p) -> canonical gnark Montgomery x * 2^256 mod p
 __device__ __forceinline__ Fp to_std(const Fp29& a) {
-    Fp29 c;
-#pragma unroll
-    for (int i = 0; i < 9; i++) c.l[i] = Fp29Cfg::C_OUT[i];
-    Fp t = pack29(mul(a, c));  // < 8 p * p / M + p < 1.05 p
+    Fp t = pack29(mul(a, fl_const<Fp29Cfg>(Fp29Cfg::C_OUT)));  // < 8 p * p / M + p < 1.05 p
     Fp s;
     uint32_t br = 0;
 #pragma unroll
@@ -183,6 +251,70 @@ GG_HD Fp to_r261(const Fp& x) {
 #pragma unroll
     for (int i = 0; i < 8; i++) c.v[i] = Fp29Cfg::C_IN[i];
     return x * c;
+}
+
+// ---------------------------------------------------------------------------
+// XYZZ bucket accumulator over the radix-2^29 form (BN254 G1).  Coordinates
+// stay below 7 p between additions (bounds in the comments, M = 169.28 p);
+// infinity is ZZ = 0 (all limbs), as in curve.cuh.
+struct Xyzz29 {
+    Fp29 x, y, zz, zzz;
+};
+
+__device__ __forceinline__ bool is_inf29(const Xyzz29& p) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) o |= p.zz.l[i];
+    return o == 0;
+}
+__device__ __forceinline__ Xyzz29 inf29() {
+    Xyzz29 r;
+#pragma unroll
+    for (int i = 0; i < 9; i++) r.x.l[i] = r.y.l[i] = r.zz.l[i] = r.zzz.l[i] = 0;
+    return r;
+}
+
+// mdbl-2008-s-1 of an affine point (x < p, y < 2p); result coordinates < 6 p
+__device__ __forceinline__ Xyzz29 xyzz29_dbl_affine(const Fp29& x, const Fp29& y) {
+    const Fp29 U = add(y, y);                  // < 4p
+    const Fp29 V = mul(U, U);                  // < 1.1p
+    const Fp29 W = mul(U, V);                  // < 1.03p
+    const Fp29 S = mul(x, V);                  // < 1.01p
+    const Fp29 xx = mul(x, x);                 // < 1.01p
+    const Fp29 M = add(xx, add(xx, xx));       // < 3.03p
+    const Fp29 X3 = sub<4>(mul(M, M), add(S, S));  // 2S < 3p: < 5.07p
+    const Fp29 D = sub<7>(S, X3);              // X3 < 6p: < 8.01p
+    const Fp29 Y3 = sub<3>(mul(M, D), mul(W, y));  // W y < 2p: < 4.15p
+    return Xyzz29{X3, Y3, V, W};
+}
+
+// acc += (x, y): madd-2008-s (the same formula, hence the same projective
+// representative, as xyzz_madd_inplace); x < p, y < 2p, acc coordinates < 7 p.
+__device__ __forceinline__ void xyzz29_madd(Xyzz29& p, const Fp29& x, const Fp29& y) {
+    if (is_inf29(p)) {
+        p = Xyzz29{x, y, fl_const<Fp29Cfg>(Fp29Cfg::ONE), fl_const<Fp29Cfg>(Fp29Cfg::ONE)};
+        return;
+    }
+    const Fp29 P = mul_sub<8>(x, p.zz, p.x);    // x ZZ < 1.05p, X < 7p: < 9.05p
+    const Fp29 R = mul_sub<8>(y, p.zzz, p.y);   // y ZZZ < 1.09p: < 9.09p
+    if (is_zero_mod(P, 9)) {
+        p = is_zero_mod(R, 9) ? xyzz29_dbl_affine(x, y) : inf29();
+        return;
+    }
+    const Fp29 PP = mul(P, P);                  // < 1.49p
+    p.zz = mul(p.zz, PP);                       // < 1.07p
+    const Fp29 PPP = mul(P, PP);                // < 1.08p
+    p.zzz = mul(p.zzz, PPP);                    // < 1.05p
+    const Fp29 Q = mul(p.x, PP);                // < 1.07p
+    const Fp29 X3 = sub<5>(mul(R, R), add(PPP, add(Q, Q)));  // PPP + 2Q < 3.22p: < 6.49p
+    // Y3 = R (Q - X3) - Y PPP in one reduction: R (Q - X3) + Y (3p - PPP)
+    // (Q - X3 < 9.06p, 3p - PPP < 3p, Y < 7p): < (82.4 + 21) p / 169.28 + p < 1.62p
+    p.y = mul2(R, sub<8>(Q, X3), p.y, sub<3>(Fp29{}, PPP));
+    p.x = X3;
+}
+
+__device__ __forceinline__ Xyzz<Fp> to_std(const Xyzz29& p) {
+    return Xyzz<Fp>{to_std(p.x), to_std(p.y), to_std(p.zz), to_std(p.zzz)};
 }
 
 }  // namespace gg

@@ -20,6 +20,7 @@
 //    a running sum, plus a double-and-add shift, then a tree sum.
 #include "common.h"
 #include "curve.cuh"
+#include "field29.cuh"
 #include "prof.h"
 #include <mutex>
 #include <vector>
@@ -133,6 +134,35 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
     tbucket[t] = q;
     uint32_t bnd = offsets[q + 1];
     uint32_t seg0 = e0;
+    if constexpr (std::is_same<F, Fp>::value) {
+        // BN254 G1: radix-2^29 accumulator (field29.cuh); the base holds
+        // x * 2^261 mod p, partials leave in gnark's form
+        Xyzz29 acc = inf29();
+        uint32_t v = sorted[e0], vn = (e0 + 1 < e1) ? sorted[e0 + 1] : 0u;
+        Affine<F> p = ld(pts + (v & 0x7fffffffu));
+        for (uint32_t e = e0; e < e1; e++) {
+            Affine<F> qp = p;
+            const uint32_t cv = v;
+            if (e + 1 < e1) {
+                p = ld(pts + (vn & 0x7fffffffu));
+                v = vn;
+                if (e + 2 < e1) vn = sorted[e + 2];
+            }
+            if (e == bnd) {
+                range_store(to_std(acc), seg0 == e0, false, q, c, t, head, tail, S);
+                acc = inf29();
+                seg0 = e;
+                do { q++; bnd = offsets[q + 1]; } while (bnd == e);
+            }
+            if (skip_inf && qp.is_inf()) continue;
+            const Fp29 x = unpack29(qp.x);
+            Fp29 y = unpack29(qp.y);
+            if (cv >> 31) y = sub<2>(Fp29{}, y);  // 2p - y
+            xyzz29_madd(acc, x, y);
+        }
+        range_store(to_std(acc), seg0 == e0, true, q, c, t, head, tail, S);
+        return;
+    }
     Xyzz<F> acc = Xyzz<F>::inf();
     if constexpr (sizeof(F) <= 32) {
         // G1: software pipeline, the next point is in flight while this one is added
@@ -418,6 +448,8 @@ __global__ void __launch_bounds__(256) k_pre_dbl(Xyzz<F>* cur, size_t n, int c) 
     st(cur + i, p);
 }
 
+__global__ void __launch_bounds__(256) k_pts_to_r261(Affine<Fp>* pts, size_t n);
+
 // batch-normalize XYZZ -> affine: thread t owns elements t, t+T, t+2T, ... (M of them)
 template <class F>
 __global__ void __launch_bounds__(256) k_pre_normalize(const Xyzz<F>* cur, size_t n, size_t T,
@@ -526,6 +558,13 @@ inline void precompute(gg_msm_base* b, const Affine<F>* dev_in, hipStream_t st) 
         GG_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_pre_normalize<F>, dim3(grid_for(T, 256)), dim3(256), 0, st,
                            (const Xyzz<F>*)cur.p, n, T, prefix.as<F>(), out + (size_t)w * n);
+        GG_HIP(hipGetLastError());
+    }
+    if constexpr (std::is_same<F, Fp>::value) {
+        // the accumulation reads BN254 G1 points in the radix-2^29 Montgomery
+        // domain (field29.cuh): x * 2^261 mod p, same 64-B layout
+        const size_t total = (size_t)b->W * n;
+        hipLaunchKernelGGL(k_pts_to_r261, dim3(grid_for(total, 256)), dim3(256), 0, st, out, total);
         GG_HIP(hipGetLastError());
     }
     GG_HIP(hipStreamSynchronize(st));
