@@ -90,6 +90,35 @@ __device__ __forceinline__ Fl<C> mul(const Fl<C>& a, const Fl<C>& b) {
     return r;
 }
 
+// a^2: the off-diagonal products once, doubled with one shift-add per column
+template <class C>
+__device__ __forceinline__ Fl<C> sqr(const Fl<C>& a) {
+    constexpr int N = C::N, B = C::B;
+    uint32_t m[N];
+    Fl<C> r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * N - 1; k++) {
+        uint64_t s = 0;
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); 2 * i < k; i++) s += (uint64_t)a.l[i] * a.l[k - i];
+        acc += s << 1;
+        if ((k & 1) == 0) acc += (uint64_t)a.l[k / 2] * a.l[k / 2];
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k - 1 : N - 1); i++)
+            acc += (uint64_t)m[i] * C::P[k - i];
+        if (k < N) {
+            m[k] = ((uint32_t)acc * C::INV) & C::MASK;
+            acc += (uint64_t)m[k] * C::P[0];
+        } else {
+            r.l[k - N] = (uint32_t)acc & C::MASK;
+        }
+        acc >>= B;
+    }
+    r.l[N - 1] = (uint32_t)acc;
+    return r;
+}
+
 // a b + c d with one reduction: (a b + c d) / M, value < (a b + c d) / M + p.
 // A column holds 18 products and 9 reduction products of < 2^58: < 2^63.
 template <class C>
@@ -301,12 +330,12 @@ __device__ __forceinline__ void xyzz29_madd(Xyzz29& p, const Fp29& x, const Fp29
         p = is_zero_mod(R, 9) ? xyzz29_dbl_affine(x, y) : inf29();
         return;
     }
-    const Fp29 PP = mul(P, P);                  // < 1.49p
+    const Fp29 PP = sqr(P);                     // < 1.49p
     p.zz = mul(p.zz, PP);                       // < 1.07p
     const Fp29 PPP = mul(P, PP);                // < 1.08p
     p.zzz = mul(p.zzz, PPP);                    // < 1.05p
     const Fp29 Q = mul(p.x, PP);                // < 1.07p
-    const Fp29 X3 = sub<5>(mul(R, R), add(PPP, add(Q, Q)));  // PPP + 2Q < 3.22p: < 6.49p
+    const Fp29 X3 = sub<5>(sqr(R), add(PPP, add(Q, Q)));  // PPP + 2Q < 3.22p: < 6.49p
     // Y3 = R (Q - X3) - Y PPP in one reduction: R (Q - X3) + Y (3p - PPP)
     // (Q - X3 < 9.06p, 3p - PPP < 3p, Y < 7p): < (82.4 + 21) p / 169.28 + p < 1.62p
     p.y = mul2(R, sub<8>(Q, X3), p.y, sub<3>(Fp29{}, PPP));

@@ -38,6 +38,7 @@ __global__ void __launch_bounds__(256) k_mulchain(Fp* data, int iters) {
     if (V == 2) {  // 29-bit reduced-radix form (field29.cuh)
         Fp29 a2 = unpack29(to_r261(a)), b2 = unpack29(to_r261(b)), c2 = a2, d2 = b2;
         for (int k = 0; k < iters; k++) { a2 = mul(a2, b2); c2 = mul(c2, d2); b2 = mul(b2, a2); d2 = mul(d2, c2); }
+        if (iters == 7) { a2 = sqr(a2); c2 = mul(c2, c2); a2 = mul(a2, c2); c2 = sqr(c2); }
         data[2 * i] = to_std(a2) + to_std(c2); data[2 * i + 1] = to_std(b2) + to_std(d2);
         return;
     }
@@ -45,6 +46,7 @@ __global__ void __launch_bounds__(256) k_mulchain(Fp* data, int iters) {
         if (V == 0) { a = mul_cios(a, b); c = mul_cios(c, d); b = mul_cios(b, a); d = mul_cios(d, c); }
         else { a = a * b; c = c * d; b = b * a; d = d * c; }
     }
+    if (iters == 7) { a = a * a; c = c * c; a = a * c; c = c * c; }
     data[2 * i] = a + c; data[2 * i + 1] = b + d;
 }
 
