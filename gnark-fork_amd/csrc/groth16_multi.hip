@@ -1,0 +1,335 @@
+// One-process multi-GPU Groth16 (SURVEY.md 8(b) "gg_init(ngpu)" shape, 8(e)):
+// a Go (or any single-process) caller hands over the whole proving key once and
+// gets proofs computed on `world` GPUs, with no transport of its own.
+//
+// This is the runtime layer a cgo caller would otherwise have to write around
+// the per-shard entry points: it places key shard r on devices[r]
+// (gg_groth16_pk_create_shard, slices cut as groth16.slice_key does), runs one
+// host thread per shard through gg_groth16_prove_partial_dist, and performs the
+// three all-to-alls of the distributed computeH itself -- peer copies
+// (hipMemcpyPeerAsync, xGMI DMA between MI355X GPUs) between the shards' device
+// buffers, fenced by an in-process barrier.  The 576-B partials are added with
+// the exact group law and combined by gg_groth16_finalize (prove.go:206-299).
+//
+// devices[] may repeat a GPU: several shards on one device rehearse the
+// N-GPU layout (the peer copy degenerates to a device-local copy), which is how
+// the one-GPU tests check it bit-exact against the single-key prover.
+#include "common.h"
+#include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+// reusable barrier that can be broken (a failing shard releases the others)
+struct Barrier {
+    std::mutex mu;
+    std::condition_variable cv;
+    int n = 1, count = 0;
+    uint64_t gen = 0;
+    bool broken = false;
+    bool wait() {
+        std::unique_lock<std::mutex> l(mu);
+        if (broken) return false;
+        const uint64_t g = gen;
+        if (++count == n) {
+            count = 0;
+            gen++;
+            cv.notify_all();
+            return true;
+        }
+        cv.wait(l, [&] { return gen != g || broken; });
+        return !broken;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> l(mu);
+        broken = true;
+        cv.notify_all();
+    }
+    void reset() {
+        std::lock_guard<std::mutex> l(mu);
+        broken = false;
+        count = 0;
+    }
+};
+
+bool dist_h_ok(size_t n, int world) {
+    return world >= 1 && world <= 16 && (world & (world - 1)) == 0 && n >= 2 && n >= (size_t)world * world;
+}
+
+}  // namespace
+
+struct gg_groth16_mpk {
+    int world = 0;
+    size_t n = 0, n_wires = 0;
+    bool dist = false;
+    std::vector<int> dev;
+    std::vector<gg_groth16_pk_t> pk;
+    std::vector<gg_hshard_t> hs;
+    std::vector<void*> send, recv;
+    std::vector<hipStream_t> st;
+    uint8_t alpha1[64], beta1[64], delta1[64], beta2[128], delta2[128];
+    Barrier bar;
+    std::mutex mu;  // one proof at a time per key
+    double last_ms[4] = {0, 0, 0, 0};
+};
+
+namespace {
+
+struct XCtx {
+    gg_groth16_mpk* m;
+    int rank;
+};
+
+// gg_exchange_fn of shard `rank`: chunk k of its send buffer -> chunk rank of
+// shard k's recv buffer.  First barrier: every shard's send is written and its
+// recv no longer read (the caller synchronised its stream); second: every push
+// into this shard's recv has landed.
+int mpk_exchange(void* ctx, const void* send_dev, void* recv_dev, size_t bytes) {
+    XCtx* x = (XCtx*)ctx;
+    gg_groth16_mpk* m = x->m;
+    const int r = x->rank;
+    (void)recv_dev;
+    if (!m->bar.wait()) return GG_ERR_INTERNAL;
+    bool ok = hipSetDevice(m->dev[r]) == hipSuccess;
+    for (int k = 0; ok && k < m->world; k++)
+        ok = hipMemcpyPeerAsync((char*)m->recv[k] + (size_t)r * bytes, m->dev[k],
+                                (const char*)send_dev + (size_t)k * bytes, m->dev[r], bytes, m->st[r]) == hipSuccess;
+    ok = ok && hipStreamSynchronize(m->st[r]) == hipSuccess;
+    if (!ok) {
+        (void)hipGetLastError();
+        m->bar.abort();
+        return GG_ERR_DEVICE;
+    }
+    return m->bar.wait() ? 0 : GG_ERR_INTERNAL;
+}
+
+void mpk_free(gg_groth16_mpk* m) {
+    for (int r = 0; r < (int)m->dev.size(); r++) {
+        if (hipSetDevice(m->dev[r]) != hipSuccess) continue;
+        if (r < (int)m->pk.size() && m->pk[r]) gg_groth16_pk_release(m->pk[r]);
+        if (r < (int)m->hs.size() && m->hs[r]) gg_hshard_release(m->hs[r]);
+        if (r < (int)m->send.size() && m->send[r]) (void)hipFree(m->send[r]);
+        if (r < (int)m->recv.size() && m->recv[r]) (void)hipFree(m->recv[r]);
+        if (r < (int)m->st.size() && m->st[r]) (void)hipStreamDestroy(m->st[r]);
+    }
+    delete m;
+}
+
+// run fn(r) on one host thread per shard (bound to its device); first error wins
+template <class Fn>
+void on_shards(gg_groth16_mpk* m, Fn fn) {
+    std::mutex emu;
+    std::string err;
+    int code = GG_OK;
+    std::vector<std::thread> th;
+    for (int r = 0; r < m->world; r++)
+        th.emplace_back([&, r] {
+            int rc = gg_set_device(m->dev[r]);
+            std::string msg = rc ? gg_last_error() : "";
+            if (!rc) {
+                rc = fn(r);
+                if (rc) msg = gg_last_error();
+            }
+            if (rc) {
+                m->bar.abort();
+                std::lock_guard<std::mutex> g(emu);
+                if (code == GG_OK) {
+                    code = rc;
+                    err = "shard " + std::to_string(r) + " (device " + std::to_string(m->dev[r]) + "): " + msg;
+                }
+            }
+        });
+    for (auto& t : th) t.join();
+    if (code != GG_OK) throw gg::Error(code, err);
+}
+
+}  // namespace
+
+extern "C" int gg_groth16_mpk_create(int log_n, const void* omega_mont, const void* coset_gen_mont,
+                                     const void* g1_A, size_t nA, const void* g1_B, size_t nB,
+                                     const void* g1_Z, size_t nZ, const void* g1_K, size_t nK,
+                                     const void* alpha1, const void* beta1, const void* delta1,
+                                     const void* g2_B, const void* beta2, const void* delta2,
+                                     const uint8_t* inf_A, const uint8_t* inf_B, size_t n_wires,
+                                     size_t nb_public, const uint32_t* k_wire_index, int world,
+                                     const int* devices, gg_groth16_mpk_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out && alpha1 && beta1 && delta1 && beta2 && delta2 && inf_A && inf_B && devices, GG_ERR_INVALID_ARG,
+             "null argument");
+    GG_CHECK(world >= 1 && world <= 64, GG_ERR_INVALID_ARG, "world must be in [1, 64]");
+    GG_CHECK(log_n >= 0 && log_n <= 28, GG_ERR_INVALID_ARG, "log_n out of range");
+    const size_t n = (size_t)1 << log_n;
+    GG_CHECK(nZ <= n, GG_ERR_INVALID_ARG, "more Z points than the domain");
+    int ndev = 0;
+    GG_HIP(hipGetDeviceCount(&ndev));
+    for (int r = 0; r < world; r++)
+        GG_CHECK(devices[r] >= 0 && devices[r] < ndev, GG_ERR_INVALID_ARG, "device id out of range");
+    std::unique_ptr<gg_groth16_mpk, void (*)(gg_groth16_mpk*)> m(new gg_groth16_mpk, mpk_free);
+    m->world = world;
+    m->n = n;
+    m->n_wires = n_wires;
+    m->dist = dist_h_ok(n, world);
+    m->dev.assign(devices, devices + world);
+    m->pk.assign(world, nullptr);
+    m->hs.assign(world, nullptr);
+    m->send.assign(world, nullptr);
+    m->recv.assign(world, nullptr);
+    m->st.assign(world, nullptr);
+    m->bar.n = world;
+    memcpy(m->alpha1, alpha1, 64);
+    memcpy(m->beta1, beta1, 64);
+    memcpy(m->delta1, delta1, 64);
+    memcpy(m->beta2, beta2, 128);
+    memcpy(m->delta2, delta2, 128);
+    // xGMI peer access between the distinct devices (copies work without it,
+    // staged by the runtime)
+    for (int i = 0; i < world; i++)
+        for (int j = 0; j < world; j++) {
+            if (m->dev[i] == m->dev[j]) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, m->dev[i], m->dev[j]) == hipSuccess && can &&
+                hipSetDevice(m->dev[i]) == hipSuccess) {
+                const hipError_t e = hipDeviceEnablePeerAccess(m->dev[j], 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+            }
+        }
+    // prefix counts of the non-infinity A / B points (key order = wire order)
+    std::vector<size_t> pa(n_wires + 1, 0), pb(n_wires + 1, 0);
+    for (size_t w = 0; w < n_wires; w++) {
+        pa[w + 1] = pa[w] + (inf_A[w] == 0);
+        pb[w + 1] = pb[w] + (inf_B[w] == 0);
+    }
+    GG_CHECK(pa[n_wires] == nA && pb[n_wires] == nB, GG_ERR_INVALID_ARG,
+             "point counts disagree with the infinity masks");
+    const uint8_t* A = (const uint8_t*)g1_A;
+    const uint8_t* B = (const uint8_t*)g1_B;
+    const uint8_t* B2 = (const uint8_t*)g2_B;
+    const uint8_t* K = (const uint8_t*)g1_K;
+    const uint8_t* Z = (const uint8_t*)g1_Z;
+    on_shards(m.get(), [&](int r) -> int {
+        const size_t lo = n_wires * r / world, hi = n_wires * (r + 1) / world;
+        size_t zl, zh;
+        if (m->dist) {
+            const size_t mm = n / world;
+            zl = std::min(r * mm, n - 1);
+            zh = std::min((r + 1) * mm, n - 1);
+        } else {
+            zl = (n - 1) * r / world;
+            zh = (n - 1) * (r + 1) / world;
+        }
+        zl = std::min(zl, nZ);
+        zh = std::min(zh, nZ);
+        // K points of this shard's wires, with absolute wire ids
+        std::vector<uint8_t> kp;
+        std::vector<uint32_t> kidx;
+        const uint8_t* kptr;
+        size_t kcnt;
+        const uint32_t* kix = nullptr;
+        if (k_wire_index) {
+            for (size_t j = 0; j < nK; j++)
+                if (k_wire_index[j] >= lo && k_wire_index[j] < hi) {
+                    kp.insert(kp.end(), K + j * 64, K + (j + 1) * 64);
+                    kidx.push_back(k_wire_index[j]);
+                }
+            kptr = kp.data();
+            kcnt = kidx.size();
+            kix = kidx.data();
+        } else {
+            size_t k1 = std::max(hi, nb_public) - nb_public, k0 = std::max(lo, nb_public) - nb_public;
+            k1 = std::min(k1, nK);
+            k0 = std::min(k0, k1);
+            kptr = K + k0 * 64;
+            kcnt = k1 - k0;
+        }
+        int rc = gg_groth16_pk_create_shard(log_n, omega_mont, coset_gen_mont, A + pa[lo] * 64, pa[hi] - pa[lo],
+                                            B + pb[lo] * 64, pb[hi] - pb[lo], Z + zl * 64, zl, zh - zl, kptr, kcnt,
+                                            alpha1, beta1, delta1, B2 + pb[lo] * 128, beta2, delta2, inf_A, inf_B,
+                                            n_wires, nb_public, kix, lo, hi, &m->pk[r]);
+        if (rc) return rc;
+        if (hipStreamCreateWithFlags(&m->st[r], hipStreamNonBlocking) != hipSuccess) return GG_ERR_DEVICE;
+        if (!m->dist) return 0;
+        rc = gg_hshard_create(log_n, omega_mont, coset_gen_mont, r, world, &m->hs[r]);
+        if (rc) return rc;
+        size_t mm = 0, xb = 0;
+        rc = gg_hshard_info(m->hs[r], &mm, &xb);
+        if (rc) return rc;
+        if (hipMalloc(&m->send[r], std::max<size_t>(xb, 256)) != hipSuccess ||
+            hipMalloc(&m->recv[r], std::max<size_t>(xb, 256)) != hipSuccess)
+            return GG_ERR_OOM;
+        return 0;
+    });
+    *out = m.release();
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_mpk_release(gg_groth16_mpk_t m) {
+    GG_CAPI_BEGIN
+    if (m) mpk_free(m);
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_mpk_info(gg_groth16_mpk_t m, int* world, int* distributed_h) {
+    GG_CAPI_BEGIN
+    GG_CHECK(m, GG_ERR_INVALID_ARG, "null key");
+    if (world) *world = m->world;
+    if (distributed_h) *distributed_h = m->dist ? 1 : 0;
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_mpk_prove(gg_groth16_mpk_t m, const void* wires, size_t n_wires, const void* sol_a,
+                                    const void* sol_b, const void* sol_c, size_t n_cons, const void* r_mont,
+                                    const void* s_mont, void* ar_aff, void* bs_aff, void* krs_aff) {
+    GG_CAPI_BEGIN
+    GG_CHECK(m && wires && sol_a && sol_b && sol_c && r_mont && s_mont && ar_aff && bs_aff && krs_aff,
+             GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(n_wires == m->n_wires, GG_ERR_INVALID_ARG, "wire count differs from the key's");
+    GG_CHECK(n_cons <= m->n, GG_ERR_INVALID_ARG, "more constraints than the domain");
+    std::lock_guard<std::mutex> lk(m->mu);
+    const auto t0 = std::chrono::steady_clock::now();
+    m->bar.reset();
+    std::vector<std::vector<uint8_t>> parts(m->world, std::vector<uint8_t>(576));
+    std::vector<XCtx> ctx(m->world);
+    on_shards(m, [&](int r) -> int {
+        ctx[r] = XCtx{m, r};
+        if (m->dist)
+            return gg_groth16_prove_partial_dist(m->pk[r], m->hs[r], wires, n_wires, sol_a, sol_b, sol_c, n_cons, 0,
+                                                 mpk_exchange, &ctx[r], m->send[r], m->recv[r], parts[r].data());
+        return gg_groth16_prove_partial(m->pk[r], wires, n_wires, sol_a, sol_b, sol_c, n_cons, 0, parts[r].data(),
+                                        nullptr);
+    });
+    const auto t1 = std::chrono::steady_clock::now();
+    // exact sum of the partials: 4 G1Jac (96 B) then one G2Jac (192 B)
+    std::vector<uint8_t> sum = parts[0];
+    for (int r = 1; r < m->world; r++) {
+        for (int i = 0; i < 4; i++) {
+            uint8_t tmp[96];
+            GG_CHECK(gg_g1_jac_add(sum.data() + 96 * i, parts[r].data() + 96 * i, tmp) == GG_OK, GG_ERR_INTERNAL,
+                     "partial sum");
+            memcpy(sum.data() + 96 * i, tmp, 96);
+        }
+        uint8_t tmp2[192];
+        GG_CHECK(gg_g2_jac_add(sum.data() + 384, parts[r].data() + 384, tmp2) == GG_OK, GG_ERR_INTERNAL, "partial sum");
+        memcpy(sum.data() + 384, tmp2, 192);
+    }
+    const int rc = gg_groth16_finalize(m->alpha1, m->beta1, m->delta1, m->beta2, m->delta2, sum.data(), r_mont,
+                                       s_mont, ar_aff, bs_aff, krs_aff);
+    GG_CHECK(rc == GG_OK, rc, gg_last_error());
+    const auto t2 = std::chrono::steady_clock::now();
+    m->last_ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    m->last_ms[1] = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    m->last_ms[2] = std::chrono::duration<double, std::milli>(t2 - t0).count();
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_mpk_last_timings(gg_groth16_mpk_t m, double* ms3) {
+    GG_CAPI_BEGIN
+    GG_CHECK(m && ms3, GG_ERR_INVALID_ARG, "null argument");
+    for (int i = 0; i < 3; i++) ms3[i] = m->last_ms[i];
+    GG_CAPI_END
+}

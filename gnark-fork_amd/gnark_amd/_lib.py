@@ -103,6 +103,12 @@ def _load():
         "gg_hshard_info": ([P, ctypes.POINTER(S), ctypes.POINTER(S)], I),
         "gg_hshard_phase": ([P, I, P, P, P, S, I, P, P, P], I),
         "gg_groth16_prove_partial_dist": ([P, P, P, S, P, P, P, S, I, EXCHANGE_FN, P, P, P, P], I),
+        "gg_groth16_mpk_create": ([I, P, P, P, S, P, S, P, S, P, S, P, P, P, P, P, P, P, P, S, S, P, I,
+                                   ctypes.POINTER(ctypes.c_int), PP], I),
+        "gg_groth16_mpk_release": ([P], I),
+        "gg_groth16_mpk_info": ([P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], I),
+        "gg_groth16_mpk_prove": ([P, P, S, P, P, P, S, P, P, P, P, P], I),
+        "gg_groth16_mpk_last_timings": ([P, ctypes.POINTER(ctypes.c_double)], I),
         "gg_batch_scalar_mul": ([I, P, P, S, I, P, I], I),
         "gg_plonk_numerator_coset": ([ctypes.POINTER(ctypes.c_void_p), I, P, ctypes.POINTER(I), P,
                                       P, P, P, P, S, I, I, P, P], I),
@@ -149,6 +155,8 @@ EXPORTED = [
     "gg_plonk_pk_vk", "gg_plonk_commit_lagrange", "gg_plonk_proof_size", "gg_plonk_prove",
     "gg_plonk_last_timings", "gg_groth16_pk_create_ex", "gg_groth16_finalize_ex",
     "gg_bls12_381_g2_jac_to_affine", "gg_bls12_381_g2_jac_add", "gg_bls12_381_g2_scalar_mul",
+    "gg_groth16_mpk_create", "gg_groth16_mpk_release", "gg_groth16_mpk_info", "gg_groth16_mpk_prove",
+    "gg_groth16_mpk_last_timings",
 ]
 
 

@@ -139,6 +139,72 @@ class ProvingKey:
             pass
 
 
+class MultiGpuProvingKey:
+    """One-process multi-GPU key (gg_groth16_mpk_create): shard r of the whole
+    key on devices[r] (ids may repeat: several shards per GPU); proofs run one
+    host thread per shard with the distributed computeH's all-to-alls done as
+    peer copies inside the library -- the shape a Go caller uses, no
+    torch.distributed.  BN254, host inputs."""
+
+    def __init__(self, data: ProvingKeyData, devices):
+        if data.curve != "bn254":
+            raise ValueError("multi-GPU key: BN254 only")
+        self.data = data
+        devs = (ctypes.c_int * len(devices))(*devices)
+        omega = data.domain_generator or fr.fr_mont(fr.domain_generator(data.log_n))
+        gen = data.domain_mul_gen or fr.fr_mont(fr.FR_MULTIPLICATIVE_GEN)
+        kidx = None
+        if data.k_wire_index is not None:
+            kidx = np.ascontiguousarray(np.asarray(data.k_wire_index, dtype=np.uint32))
+        h = ctypes.c_void_p()
+        check(lib.gg_groth16_mpk_create(
+            data.log_n, ptr(omega), ptr(gen),
+            ptr(data.g1_A), len(data.g1_A) // 64, ptr(data.g1_B), len(data.g1_B) // 64,
+            ptr(data.g1_Z), len(data.g1_Z) // 64, ptr(data.g1_K), len(data.g1_K) // 64,
+            ptr(data.alpha1), ptr(data.beta1), ptr(data.delta1),
+            ptr(data.g2_B), ptr(data.beta2), ptr(data.delta2),
+            ptr(bytes(data.infinity_A)), ptr(bytes(data.infinity_B)), data.n_wires, data.nb_public,
+            ptr(kidx), len(devices), devs, ctypes.byref(h)))
+        self.handle = h
+        self.devices = list(devices)
+
+    def info(self):
+        """(world, distributed computeH?)"""
+        w, d = ctypes.c_int(), ctypes.c_int()
+        check(lib.gg_groth16_mpk_info(self.handle, ctypes.byref(w), ctypes.byref(d)))
+        return w.value, bool(d.value)
+
+    def prove(self, solution: "Solution", *opts, r: bytes = None, s: bytes = None) -> "Proof":
+        cfg = backend.new_prover_config(*opts)
+        if not backend.accelerated(cfg):
+            raise RuntimeError("accelerated prover requested without with_amd_acceleration()")
+        if solution.on_device:
+            raise ValueError("multi-GPU prove takes host inputs")
+        r = r if r is not None else _rand_fr_mont()
+        s = s if s is not None else _rand_fr_mont()
+        ar, bs, krs = bytearray(64), bytearray(128), bytearray(64)
+        check(lib.gg_groth16_mpk_prove(self.handle, ptr(solution.W), solution.n_wires, ptr(solution.A),
+                                       ptr(solution.B), ptr(solution.C), solution.n_constraints, ptr(r),
+                                       ptr(s), ptr(ar), ptr(bs), ptr(krs)))
+        return Proof(bytes(ar), bytes(bs), bytes(krs))
+
+    def last_timings(self) -> dict:
+        t = (ctypes.c_double * 3)()
+        check(lib.gg_groth16_mpk_last_timings(self.handle, t))
+        return {"shards": t[0], "combine": t[1], "total": t[2]}
+
+    def close(self):
+        if self.handle:
+            lib.gg_groth16_mpk_release(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def _rand_fr_mont() -> bytes:
     # fr.Element.SetRandom (prove.go:180-185)
     return fr.fr_mont(secrets.randbelow(fr.R))

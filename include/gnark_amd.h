@@ -292,6 +292,37 @@ int gg_groth16_prove_partial_dist(gg_groth16_pk_t pk, gg_hshard_t hs, const void
                                   gg_exchange_fn xchg, void *xchg_ctx, void *send_dev,
                                   void *recv_dev, void *partials);
 
+/* ---- one-process multi-GPU Groth16 (SURVEY 8(b) gg_init(ngpu) shape, 8(e)):
+ * the caller passes the WHOLE key (arguments as gg_groth16_pk_create) and
+ * `world` device ids; shard r (wires [n_wires r/world, n_wires (r+1)/world),
+ * Z positions of the distributed computeH) is placed on devices[r].  A proof
+ * runs one host thread per shard; the three all-to-alls of the distributed
+ * computeH are peer copies between the shards' device buffers (xGMI DMA), done
+ * inside the library -- no transport from the caller.  world a power of two
+ * <= 16 with n >= world^2 distributes computeH; otherwise every shard computes
+ * h itself.  devices may repeat (several shards per GPU).  BN254, host inputs.
+ * replaces: the per-GPU setupDevicePointers + Prove of icicle.go:31-420 for a
+ * node of GPUs driven from one Go process. */
+typedef struct gg_groth16_mpk *gg_groth16_mpk_t;
+int gg_groth16_mpk_create(int log_n, const void *omega_mont, const void *coset_gen_mont,
+                          const void *g1_A, size_t nA, const void *g1_B, size_t nB,
+                          const void *g1_Z, size_t nZ, const void *g1_K, size_t nK,
+                          const void *alpha1, const void *beta1, const void *delta1,
+                          const void *g2_B, const void *beta2, const void *delta2,
+                          const uint8_t *inf_A, const uint8_t *inf_B, size_t n_wires,
+                          size_t nb_public, const uint32_t *k_wire_index, int world,
+                          const int *devices, gg_groth16_mpk_t *out);
+int gg_groth16_mpk_release(gg_groth16_mpk_t mpk);
+/* world and whether computeH is distributed (1) or replicated per shard (0) */
+int gg_groth16_mpk_info(gg_groth16_mpk_t mpk, int *world, int *distributed_h);
+/* as gg_groth16_prove (host inputs): Ar, Bs, Krs affine */
+int gg_groth16_mpk_prove(gg_groth16_mpk_t mpk, const void *wires, size_t n_wires, const void *sol_a,
+                         const void *sol_b, const void *sol_c, size_t n_cons, const void *r_mont,
+                         const void *s_mont, void *ar_aff, void *bs_aff, void *krs_aff);
+/* ms of the last gg_groth16_mpk_prove: [0] shards (device work + exchanges),
+ * [1] partial sum + finalize, [2] total */
+int gg_groth16_mpk_last_timings(gg_groth16_mpk_t mpk, double *ms3);
+
 /* per-stage timings (ms) of the last gg_groth16_prove on this thread:
  * [0]=upload [1]=computeH [2]=msm_A [3]=msm_B1 [4]=msm_K [5]=msm_Z [6]=msm_G2
  * [7]=epilogue [8]=total */
