@@ -64,8 +64,34 @@ func (pk *ProvingKey) setupDevicePointers(nbPublic int, kWireIndex []uint32) err
 			infB[i] = 1
 		}
 	}
-	var h C.gg_groth16_pk_t
 	p := func(s unsafe.Pointer, n int) unsafe.Pointer { return ptrOr(n > 0, s) }
+	if devs := configuredDevices(); len(devs) > 1 {
+		// one shard per GPU, driven from this process (gg_groth16_mpk_create)
+		cdevs := make([]C.int, len(devs))
+		for i, d := range devs {
+			cdevs[i] = C.int(d)
+		}
+		var mh C.gg_groth16_mpk_t
+		rc := C.gg_groth16_mpk_create(C.int(logN),
+			unsafe.Pointer(&pk.Domain.Generator), unsafe.Pointer(&pk.Domain.FrMultiplicativeGen),
+			p(unsafe.Pointer(unsafe.SliceData(pk.G1.A)), len(pk.G1.A)), C.size_t(len(pk.G1.A)),
+			p(unsafe.Pointer(unsafe.SliceData(pk.G1.B)), len(pk.G1.B)), C.size_t(len(pk.G1.B)),
+			p(unsafe.Pointer(unsafe.SliceData(pk.G1.Z)), len(pk.G1.Z)), C.size_t(len(pk.G1.Z)),
+			p(unsafe.Pointer(unsafe.SliceData(pk.G1.K)), len(pk.G1.K)), C.size_t(len(pk.G1.K)),
+			unsafe.Pointer(&pk.G1.Alpha), unsafe.Pointer(&pk.G1.Beta), unsafe.Pointer(&pk.G1.Delta),
+			p(unsafe.Pointer(unsafe.SliceData(pk.G2.B)), len(pk.G2.B)),
+			unsafe.Pointer(&pk.G2.Beta), unsafe.Pointer(&pk.G2.Delta),
+			(*C.uint8_t)(unsafe.Pointer(&infA[0])), (*C.uint8_t)(unsafe.Pointer(&infB[0])),
+			C.size_t(nWires), C.size_t(nbPublic),
+			(*C.uint32_t)(p(unsafe.Pointer(unsafe.SliceData(kWireIndex)), len(kWireIndex))),
+			C.int(len(devs)), &cdevs[0], &mh)
+		if rc != C.GG_OK {
+			return lastError()
+		}
+		pk.deviceInfo = &deviceInfo{handle: unsafe.Pointer(mh), multi: true}
+		return nil
+	}
+	var h C.gg_groth16_pk_t
 	rc := C.gg_groth16_pk_create(C.int(logN),
 		unsafe.Pointer(&pk.Domain.Generator), unsafe.Pointer(&pk.Domain.FrMultiplicativeGen),
 		p(unsafe.Pointer(unsafe.SliceData(pk.G1.A)), len(pk.G1.A)), C.size_t(len(pk.G1.A)),
@@ -88,7 +114,11 @@ func (pk *ProvingKey) setupDevicePointers(nbPublic int, kWireIndex []uint32) err
 // Release frees the HBM-resident key (the icicle path never frees it).
 func (pk *ProvingKey) Release() {
 	if pk.deviceInfo != nil {
-		C.gg_groth16_pk_release(C.gg_groth16_pk_t(pk.deviceInfo.handle))
+		if pk.deviceInfo.multi {
+			C.gg_groth16_mpk_release(C.gg_groth16_mpk_t(pk.deviceInfo.handle))
+		} else {
+			C.gg_groth16_pk_release(C.gg_groth16_pk_t(pk.deviceInfo.handle))
+		}
 		pk.deviceInfo = nil
 	}
 }
@@ -194,12 +224,22 @@ func Prove(r1cs *cs.R1CS, pk *ProvingKey, fullWitness witness.Witness, opts ...b
 	}
 	var ar, krs curve.G1Affine
 	var bs curve.G2Affine
-	rc := C.gg_groth16_prove(C.gg_groth16_pk_t(pk.deviceInfo.handle),
-		unsafe.Pointer(&wireValues[0]), C.size_t(len(wireValues)),
-		unsafe.Pointer(&solution.A[0]), unsafe.Pointer(&solution.B[0]), unsafe.Pointer(&solution.C[0]),
-		C.size_t(len(solution.A)), 0,
-		unsafe.Pointer(&r), unsafe.Pointer(&s),
-		unsafe.Pointer(&ar), unsafe.Pointer(&bs), unsafe.Pointer(&krs), nil)
+	var rc C.int
+	if pk.deviceInfo.multi {
+		rc = C.gg_groth16_mpk_prove(C.gg_groth16_mpk_t(pk.deviceInfo.handle),
+			unsafe.Pointer(&wireValues[0]), C.size_t(len(wireValues)),
+			unsafe.Pointer(&solution.A[0]), unsafe.Pointer(&solution.B[0]), unsafe.Pointer(&solution.C[0]),
+			C.size_t(len(solution.A)),
+			unsafe.Pointer(&r), unsafe.Pointer(&s),
+			unsafe.Pointer(&ar), unsafe.Pointer(&bs), unsafe.Pointer(&krs))
+	} else {
+		rc = C.gg_groth16_prove(C.gg_groth16_pk_t(pk.deviceInfo.handle),
+			unsafe.Pointer(&wireValues[0]), C.size_t(len(wireValues)),
+			unsafe.Pointer(&solution.A[0]), unsafe.Pointer(&solution.B[0]), unsafe.Pointer(&solution.C[0]),
+			C.size_t(len(solution.A)), 0,
+			unsafe.Pointer(&r), unsafe.Pointer(&s),
+			unsafe.Pointer(&ar), unsafe.Pointer(&bs), unsafe.Pointer(&krs), nil)
+	}
 	if rc != C.GG_OK {
 		return nil, lastError()
 	}

@@ -6,15 +6,49 @@
 package amd_bn254
 
 import (
+	"os"
+	"strconv"
+	"strings"
+	"sync"
 	"unsafe"
 
 	groth16_bn254 "github.com/consensys/gnark/backend/groth16/bn254"
 	cs "github.com/consensys/gnark/constraint/bn254"
 )
 
-// deviceInfo holds the HBM-resident proving key (gg_groth16_pk_t).
+// deviceInfo holds the HBM-resident proving key: one gg_groth16_pk_t, or, when
+// several devices are configured, one gg_groth16_mpk_t (a shard per GPU, the
+// distributed computeH's exchanges done inside the library).
 type deviceInfo struct {
 	handle unsafe.Pointer
+	multi  bool
+}
+
+var (
+	devicesMu sync.Mutex
+	devices   []int
+)
+
+// SetDevices selects the GPUs keys created afterwards are sharded over
+// (the SURVEY 8(b) gg_init(ngpu) shape).  nil / one id: a single GPU.  The
+// default comes from GNARK_AMD_DEVICES ("0,1,2,3,4,5,6,7").
+func SetDevices(ids []int) {
+	devicesMu.Lock()
+	defer devicesMu.Unlock()
+	devices = append([]int(nil), ids...)
+}
+
+func configuredDevices() []int {
+	devicesMu.Lock()
+	defer devicesMu.Unlock()
+	if devices == nil {
+		for _, f := range strings.Split(os.Getenv("GNARK_AMD_DEVICES"), ",") {
+			if id, err := strconv.Atoi(strings.TrimSpace(f)); err == nil {
+				devices = append(devices, id)
+			}
+		}
+	}
+	return devices
 }
 
 // ProvingKey embeds the CPU key so WriteTo/ReadFrom/... are promoted unchanged
