@@ -179,6 +179,89 @@ __device__ __forceinline__ Fl<C> mul_sub(const Fl<C>& a, const Fl<C>& b, const F
     return r;
 }
 
+// (a b + c d) / M + K p - s: mul2 with the subtraction folded into the output
+// columns (bound rule on s as sub<K>)
+template <int K, class C>
+__device__ __forceinline__ Fl<C> mul2_sub(const Fl<C>& a, const Fl<C>& b, const Fl<C>& c, const Fl<C>& d,
+                                          const Fl<C>& s) {
+    static_assert(K >= 1 && K <= 8, "multiple of p");
+    constexpr int N = C::N, B = C::B;
+    uint32_t m[N];
+    Fl<C> r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) {
+            acc += (uint64_t)a.l[i] * b.l[k - i];
+            acc += (uint64_t)c.l[i] * d.l[k - i];
+        }
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k - 1 : N - 1); i++)
+            acc += (uint64_t)m[i] * C::P[k - i];
+        if (k < N) {
+            m[k] = ((uint32_t)acc * C::INV) & C::MASK;
+            acc += (uint64_t)m[k] * C::P[0];
+        } else {
+            acc += C::KP[K - 1][k - N] - s.l[k - N];
+            r.l[k - N] = (uint32_t)acc & C::MASK;
+        }
+        acc >>= B;
+    }
+    r.l[N - 1] = (uint32_t)acc + (C::KP[K - 1][N - 1] - s.l[N - 1]);
+    return r;
+}
+
+// (a b + c d + e f + g h) / M with one reduction: a column holds 36 products
+// and 9 reduction products of < 2^58 (< 2^63.5)
+template <class C>
+__device__ __forceinline__ Fl<C> mul4(const Fl<C>& a, const Fl<C>& b, const Fl<C>& c, const Fl<C>& d,
+                                      const Fl<C>& e, const Fl<C>& f, const Fl<C>& g, const Fl<C>& h) {
+    constexpr int N = C::N, B = C::B;
+    uint32_t m[N];
+    Fl<C> r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) {
+            acc += (uint64_t)a.l[i] * b.l[k - i];
+            acc += (uint64_t)c.l[i] * d.l[k - i];
+            acc += (uint64_t)e.l[i] * f.l[k - i];
+            acc += (uint64_t)g.l[i] * h.l[k - i];
+        }
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k - 1 : N - 1); i++)
+            acc += (uint64_t)m[i] * C::P[k - i];
+        if (k < N) {
+            m[k] = ((uint32_t)acc * C::INV) & C::MASK;
+            acc += (uint64_t)m[k] * C::P[0];
+        } else {
+            r.l[k - N] = (uint32_t)acc & C::MASK;
+        }
+        acc >>= B;
+    }
+    r.l[N - 1] = (uint32_t)acc;
+    return r;
+}
+
+// v - q p with q = floor(v_top / (p_top + 1)) <= floor(v / p): a normalised
+// v < 8 p comes out < 2 p (nine products, no comparison)
+template <class C>
+__device__ __forceinline__ Fl<C> reduce_small(const Fl<C>& v) {
+    const uint32_t q = v.l[C::N - 1] / (C::P[C::N - 1] + 1);
+    Fl<C> r;
+    int64_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < C::N - 1; i++) {
+        acc += (int64_t)v.l[i] - (int64_t)((uint64_t)q * C::P[i]);
+        r.l[i] = (uint32_t)acc & C::MASK;
+        acc >>= C::B;  // arithmetic: the borrow
+    }
+    r.l[C::N - 1] = (uint32_t)((int64_t)v.l[C::N - 1] - (int64_t)((uint64_t)q * C::P[C::N - 1]) + acc);
+    return r;
+}
+
 // a + b, normalised
 template <class C>
 __device__ __forceinline__ Fl<C> add(const Fl<C>& a, const Fl<C>& b) {
@@ -344,6 +427,112 @@ __device__ __forceinline__ void xyzz29_madd(Xyzz29& p, const Fp29& x, const Fp29
 
 __device__ __forceinline__ Xyzz<Fp> to_std(const Xyzz29& p) {
     return Xyzz<Fp>{to_std(p.x), to_std(p.y), to_std(p.zz), to_std(p.zzz)};
+}
+
+// ---------------------------------------------------------------------------
+// BN254 G2 accumulator over Fp2 = Fp[u]/(u^2 + 1) in the radix-2^29 form.
+// Products as sums of limb products with one reduction per component:
+//   (a b)_0 = a0 b0 + a1 (k p - b1),  (a b)_1 = a0 b1 + a1 b0.
+// Coordinates between additions: X < 2p (reduce_small), Y < 1.3p,
+// ZZ, ZZZ < 1.04p (each component; bounds at the call sites, M = 169.28 p).
+struct Fp2_29 {
+    Fp29 c0, c1;
+};
+struct Xyzz2_29 {
+    Fp2_29 x, y, zz, zzz;
+};
+
+__device__ __forceinline__ Xyzz2_29 inf2_29() {
+    Xyzz2_29 r;
+#pragma unroll
+    for (int i = 0; i < 9; i++)
+        r.x.c0.l[i] = r.x.c1.l[i] = r.y.c0.l[i] = r.y.c1.l[i] = r.zz.c0.l[i] = r.zz.c1.l[i] = r.zzz.c0.l[i] =
+            r.zzz.c1.l[i] = 0;
+    return r;
+}
+__device__ __forceinline__ bool is_inf2_29(const Xyzz2_29& p) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) o |= p.zz.c0.l[i] | p.zz.c1.l[i];
+    return o == 0;
+}
+// a b for b1 < (K - 1) p
+template <int K>
+__device__ __forceinline__ Fp2_29 mul_fp2(const Fp2_29& a, const Fp2_29& b) {
+    const Fp29 nb1 = sub<K>(Fp29{}, b.c1);
+    return Fp2_29{mul2(a.c0, b.c0, a.c1, nb1), mul2(a.c0, b.c1, a.c1, b.c0)};
+}
+// a^2 = ((a0 + a1)(a0 - a1), 2 a0 a1) for a1 < (K - 1) p
+template <int K>
+__device__ __forceinline__ Fp2_29 sqr_fp2(const Fp2_29& a) {
+    return Fp2_29{mul(add(a.c0, a.c1), sub<K>(a.c0, a.c1)), mul(a.c0, add(a.c1, a.c1))};
+}
+__device__ __forceinline__ Fp2 to_std2(const Fp2_29& a) { return Fp2{to_std(a.c0), to_std(a.c1)}; }
+
+// mdbl-2008-s-1 of an affine point over Fp2 (x < p, y < 2p per component):
+// X3 < 2p, Y3 < 1.3p, ZZ = V < 1.5p, ZZZ = W < 1.2p
+__device__ __forceinline__ Xyzz2_29 xyzz2_29_dbl_affine(const Fp2_29& x, const Fp2_29& y) {
+    const Fp2_29 U{add(y.c0, y.c0), add(y.c1, y.c1)};  // < 4p
+    const Fp2_29 V = sqr_fp2<6>(U);                      // (1.47p, 1.19p)
+    const Fp2_29 W = mul_fp2<3>(U, V);                   // (1.11p, 1.06p)
+    const Fp2_29 S = mul_fp2<3>(x, V);                   // < 1.03p
+    const Fp2_29 xx = sqr_fp2<3>(x);                     // < 1.05p
+    const Fp2_29 M{add(xx.c0, add(xx.c0, xx.c0)), add(xx.c1, add(xx.c1, xx.c1))};  // < 3.15p
+    const Fp2_29 MM = sqr_fp2<5>(M);                     // (1.30p, 1.12p)
+    const Fp2_29 X3{reduce_small(sub<4>(MM.c0, add(S.c0, S.c0))), reduce_small(sub<4>(MM.c1, add(S.c1, S.c1)))};
+    const Fp2_29 D{sub<3>(S.c0, X3.c0), sub<3>(S.c1, X3.c1)};  // < 4.03p
+    // Y3 = M D - W y: c0 = M0 D0 + M1 (6p - D1) + y0 (3p - W0) + y1 W1,
+    //                 c1 = M0 D1 + M1 D0 + y0 (3p - W1) + y1 (3p - W0)   (< 1.25p)
+    const Fp29 nD1 = sub<6>(Fp29{}, D.c1), nW0 = sub<3>(Fp29{}, W.c0), nW1 = sub<3>(Fp29{}, W.c1);
+    const Fp2_29 Y3{mul4(M.c0, D.c0, M.c1, nD1, y.c0, nW0, y.c1, W.c1),
+                    mul4(M.c0, D.c1, M.c1, D.c0, y.c0, nW1, y.c1, nW0)};
+    return Xyzz2_29{X3, Y3, V, W};
+}
+
+// acc += (x, y), madd-2008-s over Fp2 (the formula of xyzz_madd_inplace, so
+// the same projective representative); x < p, y < 2p per component
+__device__ __forceinline__ void xyzz2_29_madd(Xyzz2_29& p, const Fp2_29& x, const Fp2_29& y) {
+    if (is_inf2_29(p)) {
+        const Fp29 one = fl_const<Fp29Cfg>(Fp29Cfg::ONE);
+        p = Xyzz2_29{x, y, Fp2_29{one, Fp29{}}, Fp2_29{one, Fp29{}}};
+        return;
+    }
+    // P = x ZZ - X, R = y ZZZ - Y (ZZ1, ZZZ1 < 2p; X < 2p; Y < 2p): < 4.05p
+    // (x and y die here on the common path: fewer live registers)
+    auto r_of = [&]() {
+        const Fp29 nzzz1 = sub<3>(Fp29{}, p.zzz.c1);
+        return Fp2_29{mul2_sub<3>(y.c0, p.zzz.c0, y.c1, nzzz1, p.y.c0),
+                      mul2_sub<3>(y.c0, p.zzz.c1, y.c1, p.zzz.c0, p.y.c1)};
+    };
+    const Fp29 nzz1 = sub<3>(Fp29{}, p.zz.c1);
+    const Fp2_29 P{mul2_sub<3>(x.c0, p.zz.c0, x.c1, nzz1, p.x.c0), mul2_sub<3>(x.c0, p.zz.c1, x.c1, p.zz.c0, p.x.c1)};
+    if (is_zero_mod(P.c0, 5) && is_zero_mod(P.c1, 5)) {
+        const Fp2_29 R0 = r_of();
+        p = (is_zero_mod(R0.c0, 5) && is_zero_mod(R0.c1, 5)) ? xyzz2_29_dbl_affine(x, y) : inf2_29();
+        return;
+    }
+    const Fp2_29 R = r_of();
+    const Fp2_29 PP = sqr_fp2<6>(P);            // (1.48p, 1.19p)
+    p.zz = mul_fp2<3>(p.zz, PP);                // < 1.03p
+    const Fp2_29 PPP = mul_fp2<3>(P, PP);       // (1.11p, 1.06p)
+    p.zzz = mul_fp2<3>(p.zzz, PPP);             // < 1.03p
+    const Fp2_29 Q = mul_fp2<3>(p.x, PP);       // (1.05p, 1.03p)
+    const Fp2_29 RR = sqr_fp2<6>(R);            // (1.48p, 1.19p)
+    // X3 = RR - (PPP + 2Q): < 1.48p + 5p, then reduced below 2p
+    const Fp2_29 X3{reduce_small(sub<5>(RR.c0, add(PPP.c0, add(Q.c0, Q.c0)))),
+                    reduce_small(sub<5>(RR.c1, add(PPP.c1, add(Q.c1, Q.c1))))};
+    // Y3 = R (Q - X3) - Y PPP, one reduction per component:
+    //   c0 = R0 U0 + R1 (6p - U1) + Y0 (3p - PPP0) + Y1 PPP1
+    //   c1 = R0 U1 + R1 U0 + Y0 (3p - PPP1) + Y1 (3p - PPP0)      (< 1.3p)
+    const Fp2_29 U{sub<3>(Q.c0, X3.c0), sub<3>(Q.c1, X3.c1)};  // < 4.05p
+    const Fp29 nU1 = sub<6>(Fp29{}, U.c1), nP0 = sub<3>(Fp29{}, PPP.c0), nP1 = sub<3>(Fp29{}, PPP.c1);
+    p.y = Fp2_29{mul4(R.c0, U.c0, R.c1, nU1, p.y.c0, nP0, p.y.c1, PPP.c1),
+                 mul4(R.c0, U.c1, R.c1, U.c0, p.y.c0, nP1, p.y.c1, nP0)};
+    p.x = X3;
+}
+
+__device__ __forceinline__ Xyzz<Fp2> to_std(const Xyzz2_29& p) {
+    return Xyzz<Fp2>{to_std2(p.x), to_std2(p.y), to_std2(p.zz), to_std2(p.zzz)};
 }
 
 }  // namespace gg

@@ -106,10 +106,14 @@ __device__ __forceinline__ void range_store(const Xyzz<F>& acc, bool first, bool
     else st(S + (__brev(q) >> (33 - c)), acc);
 }
 
-// waves per SIMD the accumulation is compiled for: 2 (<= 256 VGPRs) up to Fp2
-// over the 8-limb BN254 Fp; 1 (512 VGPRs, no scratch spills) for BLS12-381 Fp2
+// waves per SIMD the accumulation is compiled for: 2 (<= 256 VGPRs) for the G1
+// groups; 1 (512 VGPRs, no scratch spills) for the Fp2 groups (BN254 G2 in the
+// radix-2^29 form needs ~300, BLS12-381 G2 more)
+#ifndef GG_G2_WAVES1
+#define GG_G2_WAVES1 0
+#endif
 template <class F>
-constexpr int kAccumWaves = sizeof(F) > 64 ? 1 : 2;
+constexpr int kAccumWaves = (GG_G2_WAVES1 && std::is_same<F, Fp2>::value) || std::is_same<F, Fp2Bls>::value ? 1 : 2;
 
 template <class F>
 __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affine<F>* pts, const uint32_t* sorted,
@@ -159,6 +163,27 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
             Fp29 y = unpack29(qp.y);
             if (cv >> 31) y = sub<2>(Fp29{}, y);  // 2p - y
             xyzz29_madd(acc, x, y);
+        }
+        range_store(to_std(acc), seg0 == e0, true, q, c, t, head, tail, S);
+        return;
+    }
+    if constexpr (std::is_same<F, Fp2>::value) {
+        // BN254 G2: radix-2^29 Fp2 accumulator (field29.cuh), base in x * 2^261 form
+        Xyzz2_29 acc = inf2_29();
+        for (uint32_t e = e0; e < e1; e++) {
+            if (e == bnd) {
+                range_store(to_std(acc), seg0 == e0, false, q, c, t, head, tail, S);
+                acc = inf2_29();
+                seg0 = e;
+                do { q++; bnd = offsets[q + 1]; } while (bnd == e);
+            }
+            const uint32_t v = sorted[e];
+            const Affine<F> pt = ld(pts + (v & 0x7fffffffu));
+            if (skip_inf && pt.is_inf()) continue;
+            const Fp2_29 x{unpack29(pt.x.a0), unpack29(pt.x.a1)};
+            Fp2_29 y{unpack29(pt.y.a0), unpack29(pt.y.a1)};
+            if (v >> 31) y = Fp2_29{sub<2>(Fp29{}, y.c0), sub<2>(Fp29{}, y.c1)};  // 2p - y
+            xyzz2_29_madd(acc, x, y);
         }
         range_store(to_std(acc), seg0 == e0, true, q, c, t, head, tail, S);
         return;
@@ -560,11 +585,11 @@ inline void precompute(gg_msm_base* b, const Affine<F>* dev_in, hipStream_t st) 
                            (const Xyzz<F>*)cur.p, n, T, prefix.as<F>(), out + (size_t)w * n);
         GG_HIP(hipGetLastError());
     }
-    if constexpr (std::is_same<F, Fp>::value) {
-        // the accumulation reads BN254 G1 points in the radix-2^29 Montgomery
-        // domain (field29.cuh): x * 2^261 mod p, same 64-B layout
-        const size_t total = (size_t)b->W * n;
-        hipLaunchKernelGGL(k_pts_to_r261, dim3(grid_for(total, 256)), dim3(256), 0, st, out, total);
+    if constexpr (std::is_same<F, Fp>::value || std::is_same<F, Fp2>::value) {
+        // the accumulation reads BN254 G1 / G2 points in the radix-2^29
+        // Montgomery domain (field29.cuh): x * 2^261 mod p, same layout
+        const size_t total = (size_t)b->W * n * (sizeof(F) / sizeof(Fp));
+        hipLaunchKernelGGL(k_pts_to_r261, dim3(grid_for(total, 256)), dim3(256), 0, st, (Affine<Fp>*)out, total);
         GG_HIP(hipGetLastError());
     }
     GG_HIP(hipStreamSynchronize(st));
