@@ -27,6 +27,7 @@
 namespace gg {
 
 struct Fp29Cfg {
+    using Std = FpCfg;  // the gnark (32-bit limb, R = 2^256) layout of the same field
     static constexpr int N = 9;
     static constexpr int B = 29;
     static constexpr uint32_t MASK = (1u << B) - 1;
@@ -56,11 +57,43 @@ struct Fp29Cfg {
         {0x23e7ea38u, 0x282305b5u, 0x23951a77u, 0x36a91686u, 0x2c2ecbbfu, 0x36da0604u, 0x25370a07u, 0x32e1319fu, 0x01832272u}};
 };
 
+// BLS12-381 Fp in 14 x 28-bit limbs, R' = 2^392 = 2520 p: a column is at most
+// 28 products of < 2^56 (mul4: 70), far inside 64 bits.  tools/gen_field29.py
+struct FpBls28Cfg {
+    using Std = FpBlsCfg;
+    static constexpr int N = 14;
+    static constexpr int B = 28;
+    static constexpr uint32_t MASK = (1u << B) - 1;
+    static constexpr uint32_t P[14] = {0x0fffaaabu, 0x0fefffffu, 0x03ffffb9u, 0x0fffeb15u, 0x06241eabu,
+                                       0x0a0f6b0fu, 0x0f6730d2u, 0x0f38512bu, 0x04774b84u, 0x04bacd76u,
+                                       0x0ba7b643u, 0x0e69a4b1u, 0x01ea397fu, 0x0001a011u};
+    static constexpr uint32_t ONE[14] = {0x0347fcb8u, 0x0d800000u, 0x0002b119u, 0x00cde6d2u, 0x0c7212e0u,
+                                         0x083a2090u, 0x0037669fu, 0x0da0f73eu, 0x09b09b42u, 0x01297bb0u,
+                                         0x0515d98fu, 0x0012ca7cu, 0x0659fcfau, 0x0000577au};
+    static constexpr uint32_t INV = 0x0ffcfffdu;
+    static constexpr uint32_t PINV = 0x00030003u;
+    static constexpr uint32_t C_OUT[14] = {0x0002fffdu, 0x00900000u, 0x0c000276u, 0x0000bc40u, 0x08baebf4u,
+                                           0x05753c75u, 0x055f4898u, 0x07052574u, 0x07ce5853u, 0x056ec6d7u,
+                                           0x071a97a2u, 0x0e4935c0u, 0x0ec3fa80u, 0x00015f65u};
+    static constexpr uint32_t C_IN[12] = {0x0347fcb8u, 0x19d80000u, 0x6d2002b1u, 0x12e00cdeu, 0xa2090c72u, 0x37669f83u,
+                                          0xda0f73e0u, 0x09b09b42u, 0x8f1297bbu, 0xa7c515d9u, 0xfcfa012cu, 0x0577a659u};
+    static constexpr uint32_t KP[8][14] = {
+        {0x1fffaaabu, 0x1feffffeu, 0x13ffffb8u, 0x1fffeb14u, 0x16241eaau, 0x1a0f6b0eu, 0x1f6730d1u, 0x1f38512au, 0x14774b83u, 0x14bacd75u, 0x1ba7b642u, 0x1e69a4b0u, 0x11ea397eu, 0x0001a010u},
+        {0x1fff5556u, 0x1fdffffeu, 0x17ffff72u, 0x1fffd629u, 0x1c483d56u, 0x141ed61du, 0x1ece61a4u, 0x1e70a256u, 0x18ee9708u, 0x19759aebu, 0x174f6c85u, 0x1cd34962u, 0x13d472feu, 0x00034021u},
+        {0x1fff0001u, 0x1fcffffeu, 0x1bffff2cu, 0x1fffc13eu, 0x126c5c02u, 0x1e2e412du, 0x1e359276u, 0x1da8f382u, 0x1d65e28du, 0x1e306861u, 0x12f722c8u, 0x1b3cee14u, 0x15beac7eu, 0x0004e032u},
+        {0x1ffeaaacu, 0x1fbffffeu, 0x1ffffee6u, 0x1fffac53u, 0x18907aaeu, 0x183dac3cu, 0x1d9cc349u, 0x1ce144aeu, 0x11dd2e12u, 0x12eb35d8u, 0x1e9ed90cu, 0x19a692c5u, 0x17a8e5feu, 0x00068043u},
+        {0x1ffe5557u, 0x1faffffeu, 0x13fffea0u, 0x1fff9769u, 0x1eb4995au, 0x124d174bu, 0x1d03f41cu, 0x1c1995dau, 0x16547997u, 0x17a6034eu, 0x1a468f4fu, 0x18103777u, 0x19931f7eu, 0x00082054u},
+        {0x1ffe0002u, 0x1f9ffffeu, 0x17fffe5au, 0x1fff827eu, 0x14d8b806u, 0x1c5c825bu, 0x1c6b24eeu, 0x1b51e706u, 0x1acbc51cu, 0x1c60d0c4u, 0x15ee4592u, 0x1679dc29u, 0x1b7d58feu, 0x0009c065u},
+        {0x1ffdaaadu, 0x1f8ffffeu, 0x1bfffe14u, 0x1fff6d93u, 0x1afcd6b2u, 0x166bed6au, 0x1bd255c1u, 0x1a8a3832u, 0x1f4310a1u, 0x111b9e3au, 0x1195fbd6u, 0x14e380dbu, 0x1d67927eu, 0x000b6076u},
+        {0x1ffd5558u, 0x1f7ffffeu, 0x1ffffdceu, 0x1fff58a8u, 0x1120f55eu, 0x107b587au, 0x1b398694u, 0x19c2895eu, 0x13ba5c26u, 0x15d66bb1u, 0x1d3db219u, 0x134d258cu, 0x1f51cbfeu, 0x000d0087u}};
+};
+
 template <class C>
 struct Fl {
     uint32_t l[C::N];
 };
 using Fp29 = Fl<Fp29Cfg>;
+using FpBls28 = Fl<FpBls28Cfg>;
 
 // Montgomery product a b / 2^(B N) by operand-interleaved product scanning.
 // Output limbs 0..N-2 < 2^B (normalised); value < a b / M + p.
@@ -319,114 +352,134 @@ __device__ __forceinline__ Fl<C> fl_const(const uint32_t (&v)[C::N]) {
     return r;
 }
 
-// 8 x u32 (x * 2^261 mod p, < 2^256) -> 9 x 29-bit limbs
-__device__ __forceinline__ Fp29 unpack29(const Fp& w) {
-    Fp29 r;
+// gnark-layout words of x * R' mod p (canonical) -> N normalised B-bit limbs
+template <class C>
+__device__ __forceinline__ Fl<C> unpack_l(const Fe<typename C::Std>& w) {
+    constexpr int NW = C::Std::N;
+    Fl<C> r;
 #pragma unroll
-    for (int i = 0; i < 9; i++) {
-        const int bit = 29 * i, wi = bit >> 5, off = bit & 31;
+    for (int i = 0; i < C::N; i++) {
+        const int bit = C::B * i, wi = bit >> 5, off = bit & 31;
         uint32_t x = w.v[wi] >> off;
-        if (off > 3 && wi + 1 < 8) x |= w.v[wi + 1] << (32 - off);
-        r.l[i] = i == 8 ? x : (x & Fp29Cfg::MASK);
+        if (off > 32 - C::B && wi + 1 < NW) x |= w.v[wi + 1] << (32 - off);
+        r.l[i] = i == C::N - 1 ? x : (x & C::MASK);
     }
     return r;
 }
-// normalised 9 x 29-bit limbs of a value < 2^256 -> 8 x u32
-__device__ __forceinline__ Fp pack29(const Fp29& a) {
-    Fp r;
+// normalised limbs of a value < 2^(32 NW) -> gnark-layout words
+template <class C>
+__device__ __forceinline__ Fe<typename C::Std> pack_l(const Fl<C>& a) {
+    constexpr int NW = C::Std::N, B = C::B;
+    Fe<typename C::Std> r;
 #pragma unroll
-    for (int wi = 0; wi < 8; wi++) {
-        const int bit = 32 * wi, i = bit / 29, off = bit % 29;
+    for (int wi = 0; wi < NW; wi++) {
+        const int bit = 32 * wi, i = bit / B, off = bit % B;
         uint32_t x = a.l[i] >> off;
-        if (i + 1 < 9) x |= a.l[i + 1] << (29 - off);
-        if (off > 26 && i + 2 < 9) x |= a.l[i + 2] << (58 - off);
+        if (i + 1 < C::N) x |= a.l[i + 1] << (B - off);
+        if (off > 2 * B - 32 && i + 2 < C::N) x |= a.l[i + 2] << (2 * B - off);
         r.v[wi] = x;
     }
     return r;
 }
-// a (R' form, any normalised value < 8 p) -> canonical gnark Montgomery x * 2^256 mod p
-__device__ __forceinline__ Fp to_std(const Fp29& a) {
-    Fp t = pack29(mul(a, fl_const<Fp29Cfg>(Fp29Cfg::C_OUT)));  // < 8 p * p / M + p < 1.05 p
-    Fp s;
+// a (R' form, any normalised value < 8 p) -> canonical gnark Montgomery form
+template <class C>
+__device__ __forceinline__ Fe<typename C::Std> to_std(const Fl<C>& a) {
+    using S = typename C::Std;
+    constexpr int NW = S::N;
+    Fe<S> t = pack_l(mul(a, fl_const<C>(C::C_OUT)));  // < 8p * p / M + p < 1.05 p
+    Fe<S> d;
     uint32_t br = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) s.v[i] = __builtin_subc(t.v[i], FpCfg::P[i], br, &br);
+    for (int i = 0; i < NW; i++) d.v[i] = __builtin_subc(t.v[i], S::P[i], br, &br);
 #pragma unroll
-    for (int i = 0; i < 8; i++) t.v[i] = br ? t.v[i] : s.v[i];
+    for (int i = 0; i < NW; i++) t.v[i] = br ? t.v[i] : d.v[i];
     return t;
 }
+__device__ __forceinline__ Fp29 unpack29(const Fp& w) { return unpack_l<Fp29Cfg>(w); }
 
-// gnark Montgomery x * 2^256 -> x * 2^261 mod p (canonical, 8 x u32): the
-// stored form of precomputed base points
-GG_HD Fp to_r261(const Fp& x) {
-    Fp c;
+// gnark Montgomery x R -> x R' mod p (canonical, gnark words): the stored form
+// of precomputed base points
+template <class C>
+GG_HD Fe<typename C::Std> to_rl(const Fe<typename C::Std>& x) {
+    Fe<typename C::Std> c;
 #pragma unroll
-    for (int i = 0; i < 8; i++) c.v[i] = Fp29Cfg::C_IN[i];
+    for (int i = 0; i < C::Std::N; i++) c.v[i] = C::C_IN[i];
     return x * c;
 }
+GG_HD Fp to_r261(const Fp& x) { return to_rl<Fp29Cfg>(x); }
 
 // ---------------------------------------------------------------------------
-// XYZZ bucket accumulator over the radix-2^29 form (BN254 G1).  Coordinates
-// stay below 7 p between additions (bounds in the comments, M = 169.28 p);
-// infinity is ZZ = 0 (all limbs), as in curve.cuh.
-struct Xyzz29 {
-    Fp29 x, y, zz, zzz;
+// XYZZ bucket accumulator over a reduced-radix form (BN254 G1: 9 x 29, and
+// BLS12-381 G1: 14 x 28 bits).  Coordinates stay below 7 p between additions
+// (bounds in the comments for BN254's M = 169.28 p; BLS12-381's M = 2520 p
+// only makes every product term smaller); infinity is ZZ = 0 (all limbs).
+template <class C>
+struct XyzzL {
+    Fl<C> x, y, zz, zzz;
 };
+using Xyzz29 = XyzzL<Fp29Cfg>;
 
-__device__ __forceinline__ bool is_inf29(const Xyzz29& p) {
+template <class C>
+__device__ __forceinline__ bool is_inf_l(const XyzzL<C>& p) {
     uint32_t o = 0;
 #pragma unroll
-    for (int i = 0; i < 9; i++) o |= p.zz.l[i];
+    for (int i = 0; i < C::N; i++) o |= p.zz.l[i];
     return o == 0;
 }
-__device__ __forceinline__ Xyzz29 inf29() {
-    Xyzz29 r;
+template <class C>
+__device__ __forceinline__ XyzzL<C> inf_l() {
+    XyzzL<C> r;
 #pragma unroll
-    for (int i = 0; i < 9; i++) r.x.l[i] = r.y.l[i] = r.zz.l[i] = r.zzz.l[i] = 0;
+    for (int i = 0; i < C::N; i++) r.x.l[i] = r.y.l[i] = r.zz.l[i] = r.zzz.l[i] = 0;
     return r;
 }
+__device__ __forceinline__ Xyzz29 inf29() { return inf_l<Fp29Cfg>(); }
 
 // mdbl-2008-s-1 of an affine point (x < p, y < 2p); result coordinates < 6 p
-__device__ __forceinline__ Xyzz29 xyzz29_dbl_affine(const Fp29& x, const Fp29& y) {
-    const Fp29 U = add(y, y);                  // < 4p
-    const Fp29 V = mul(U, U);                  // < 1.1p
-    const Fp29 W = mul(U, V);                  // < 1.03p
-    const Fp29 S = mul(x, V);                  // < 1.01p
-    const Fp29 xx = mul(x, x);                 // < 1.01p
-    const Fp29 M = add(xx, add(xx, xx));       // < 3.03p
-    const Fp29 X3 = sub<4>(mul(M, M), add(S, S));  // 2S < 3p: < 5.07p
-    const Fp29 D = sub<7>(S, X3);              // X3 < 6p: < 8.01p
-    const Fp29 Y3 = sub<3>(mul(M, D), mul(W, y));  // W y < 2p: < 4.15p
-    return Xyzz29{X3, Y3, V, W};
+template <class C>
+__device__ __forceinline__ XyzzL<C> xyzzl_dbl_affine(const Fl<C>& x, const Fl<C>& y) {
+    const Fl<C> U = add(y, y);                    // < 4p
+    const Fl<C> V = mul(U, U);                    // < 1.1p
+    const Fl<C> W = mul(U, V);                    // < 1.03p
+    const Fl<C> S = mul(x, V);                    // < 1.01p
+    const Fl<C> xx = mul(x, x);                   // < 1.01p
+    const Fl<C> M = add(xx, add(xx, xx));         // < 3.03p
+    const Fl<C> X3 = sub<4>(mul(M, M), add(S, S));  // 2S < 3p: < 5.07p
+    const Fl<C> D = sub<7>(S, X3);                // X3 < 6p: < 8.01p
+    const Fl<C> Y3 = sub<3>(mul(M, D), mul(W, y));  // W y < 2p: < 4.15p
+    return XyzzL<C>{X3, Y3, V, W};
 }
 
 // acc += (x, y): madd-2008-s (the same formula, hence the same projective
 // representative, as xyzz_madd_inplace); x < p, y < 2p, acc coordinates < 7 p.
-__device__ __forceinline__ void xyzz29_madd(Xyzz29& p, const Fp29& x, const Fp29& y) {
-    if (is_inf29(p)) {
-        p = Xyzz29{x, y, fl_const<Fp29Cfg>(Fp29Cfg::ONE), fl_const<Fp29Cfg>(Fp29Cfg::ONE)};
+template <class C>
+__device__ __forceinline__ void xyzzl_madd(XyzzL<C>& p, const Fl<C>& x, const Fl<C>& y) {
+    if (is_inf_l(p)) {
+        p = XyzzL<C>{x, y, fl_const<C>(C::ONE), fl_const<C>(C::ONE)};
         return;
     }
-    const Fp29 P = mul_sub<8>(x, p.zz, p.x);    // x ZZ < 1.05p, X < 7p: < 9.05p
-    const Fp29 R = mul_sub<8>(y, p.zzz, p.y);   // y ZZZ < 1.09p: < 9.09p
+    const Fl<C> P = mul_sub<8>(x, p.zz, p.x);    // x ZZ < 1.05p, X < 7p: < 9.05p
+    const Fl<C> R = mul_sub<8>(y, p.zzz, p.y);   // y ZZZ < 1.09p: < 9.09p
     if (is_zero_mod(P, 9)) {
-        p = is_zero_mod(R, 9) ? xyzz29_dbl_affine(x, y) : inf29();
+        p = is_zero_mod(R, 9) ? xyzzl_dbl_affine(x, y) : inf_l<C>();
         return;
     }
-    const Fp29 PP = sqr(P);                     // < 1.49p
-    p.zz = mul(p.zz, PP);                       // < 1.07p
-    const Fp29 PPP = mul(P, PP);                // < 1.08p
-    p.zzz = mul(p.zzz, PPP);                    // < 1.05p
-    const Fp29 Q = mul(p.x, PP);                // < 1.07p
-    const Fp29 X3 = sub<5>(sqr(R), add(PPP, add(Q, Q)));  // PPP + 2Q < 3.22p: < 6.49p
+    const Fl<C> PP = sqr(P);                     // < 1.49p
+    p.zz = mul(p.zz, PP);                        // < 1.07p
+    const Fl<C> PPP = mul(P, PP);                // < 1.08p
+    p.zzz = mul(p.zzz, PPP);                     // < 1.05p
+    const Fl<C> Q = mul(p.x, PP);                // < 1.07p
+    const Fl<C> X3 = sub<5>(sqr(R), add(PPP, add(Q, Q)));  // PPP + 2Q < 3.22p: < 6.49p
     // Y3 = R (Q - X3) - Y PPP in one reduction: R (Q - X3) + Y (3p - PPP)
     // (Q - X3 < 9.06p, 3p - PPP < 3p, Y < 7p): < (82.4 + 21) p / 169.28 + p < 1.62p
-    p.y = mul2(R, sub<8>(Q, X3), p.y, sub<3>(Fp29{}, PPP));
+    p.y = mul2(R, sub<8>(Q, X3), p.y, sub<3>(Fl<C>{}, PPP));
     p.x = X3;
 }
+__device__ __forceinline__ void xyzz29_madd(Xyzz29& p, const Fp29& x, const Fp29& y) { xyzzl_madd(p, x, y); }
 
-__device__ __forceinline__ Xyzz<Fp> to_std(const Xyzz29& p) {
-    return Xyzz<Fp>{to_std(p.x), to_std(p.y), to_std(p.zz), to_std(p.zzz)};
+template <class C>
+__device__ __forceinline__ Xyzz<Fe<typename C::Std>> to_std(const XyzzL<C>& p) {
+    return Xyzz<Fe<typename C::Std>>{to_std(p.x), to_std(p.y), to_std(p.zz), to_std(p.zzz)};
 }
 
 // ---------------------------------------------------------------------------

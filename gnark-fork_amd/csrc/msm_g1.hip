@@ -16,12 +16,3 @@ void msm_finish_g1(gg_msm_base* b, MsmSort* s, MsmScratch* scr, void* out_jac, h
 }
 }  // namespace gg
 
-namespace gg {
-// base points -> x * 2^261 mod p (the accumulation's input domain, field29.cuh)
-__global__ void __launch_bounds__(256) k_pts_to_r261(Affine<Fp>* pts, size_t n) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    Affine<Fp> p = ld(pts + i);
-    st(pts + i, Affine<Fp>{to_r261(p.x), to_r261(p.y)});
-}
-}  // namespace gg

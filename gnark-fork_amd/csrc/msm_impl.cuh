@@ -88,7 +88,37 @@ struct MsmSort;
 void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
 void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
 
-constexpr uint32_t LIGHT = 16;  // buckets spanning <= LIGHT ranges are combined serially
+constexpr uint32_t LIGHT = 16; 
+// which groups accumulate in a reduced-radix form, and which one
+template <class F>
+struct RadixOf {
+    static constexpr bool on = false;
+    using C = Fp29Cfg;
+};
+template <>
+struct RadixOf<Fp> {
+    static constexpr bool on = true;
+    using C = Fp29Cfg;
+};
+template <>
+struct RadixOf<Fp2> {
+    static constexpr bool on = true;
+    using C = Fp29Cfg;
+};
+template <>
+struct RadixOf<FpBls> {
+    static constexpr bool on = true;
+    using C = FpBls28Cfg;
+};
+// base coordinates (field elements, gnark form) -> x R' mod p in place
+template <class C>
+__global__ void __launch_bounds__(256) k_to_radix(Fe<typename C::Std>* v, size_t n) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fe<typename C::Std> x = v[i];
+    v[i] = to_rl<C>(x);
+}
+ // buckets spanning <= LIGHT ranges are combined serially
 
 // Level 1, balanced: thread t adds the sorted entries [t K, min((t+1) K, E)) --
 // every lane does exactly K mixed XYZZ adds, whatever the bucket sizes (the
@@ -138,10 +168,11 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
     tbucket[t] = q;
     uint32_t bnd = offsets[q + 1];
     uint32_t seg0 = e0;
-    if constexpr (std::is_same<F, Fp>::value) {
-        // BN254 G1: radix-2^29 accumulator (field29.cuh); the base holds
-        // x * 2^261 mod p, partials leave in gnark's form
-        Xyzz29 acc = inf29();
+    if constexpr (std::is_same<F, Fp>::value || std::is_same<F, FpBls>::value) {
+        // G1: reduced-radix accumulator (field29.cuh; BN254 9 x 29, BLS12-381
+        // 14 x 28 bits); the base holds x R' mod p, partials leave in gnark's form
+        using C = typename RadixOf<F>::C;
+        XyzzL<C> acc = inf_l<C>();
         uint32_t v = sorted[e0], vn = (e0 + 1 < e1) ? sorted[e0 + 1] : 0u;
         Affine<F> p = ld(pts + (v & 0x7fffffffu));
         for (uint32_t e = e0; e < e1; e++) {
@@ -154,15 +185,15 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
             }
             if (e == bnd) {
                 range_store(to_std(acc), seg0 == e0, false, q, c, t, head, tail, S);
-                acc = inf29();
+                acc = inf_l<C>();
                 seg0 = e;
                 do { q++; bnd = offsets[q + 1]; } while (bnd == e);
             }
             if (skip_inf && qp.is_inf()) continue;
-            const Fp29 x = unpack29(qp.x);
-            Fp29 y = unpack29(qp.y);
-            if (cv >> 31) y = sub<2>(Fp29{}, y);  // 2p - y
-            xyzz29_madd(acc, x, y);
+            const Fl<C> x = unpack_l<C>(qp.x);
+            Fl<C> y = unpack_l<C>(qp.y);
+            if (cv >> 31) y = sub<2>(Fl<C>{}, y);  // 2p - y
+            xyzzl_madd(acc, x, y);
         }
         range_store(to_std(acc), seg0 == e0, true, q, c, t, head, tail, S);
         return;
@@ -473,7 +504,6 @@ __global__ void __launch_bounds__(256) k_pre_dbl(Xyzz<F>* cur, size_t n, int c) 
     st(cur + i, p);
 }
 
-__global__ void __launch_bounds__(256) k_pts_to_r261(Affine<Fp>* pts, size_t n);
 
 // batch-normalize XYZZ -> affine: thread t owns elements t, t+T, t+2T, ... (M of them)
 template <class F>
@@ -585,11 +615,13 @@ inline void precompute(gg_msm_base* b, const Affine<F>* dev_in, hipStream_t st) 
                            (const Xyzz<F>*)cur.p, n, T, prefix.as<F>(), out + (size_t)w * n);
         GG_HIP(hipGetLastError());
     }
-    if constexpr (std::is_same<F, Fp>::value || std::is_same<F, Fp2>::value) {
-        // the accumulation reads BN254 G1 / G2 points in the radix-2^29
-        // Montgomery domain (field29.cuh): x * 2^261 mod p, same layout
-        const size_t total = (size_t)b->W * n * (sizeof(F) / sizeof(Fp));
-        hipLaunchKernelGGL(k_pts_to_r261, dim3(grid_for(total, 256)), dim3(256), 0, st, (Affine<Fp>*)out, total);
+    if constexpr (RadixOf<F>::on) {
+        // the accumulation reads the points in its reduced-radix Montgomery
+        // domain (field29.cuh): x R' mod p, same layout
+        using C = typename RadixOf<F>::C;
+        using E = Fe<typename C::Std>;
+        const size_t total = (size_t)b->W * n * 2 * (sizeof(F) / sizeof(E));
+        hipLaunchKernelGGL(k_to_radix<C>, dim3(grid_for(total, 256)), dim3(256), 0, st, (E*)out, total);
         GG_HIP(hipGetLastError());
     }
     GG_HIP(hipStreamSynchronize(st));
