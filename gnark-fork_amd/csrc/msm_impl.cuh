@@ -142,8 +142,13 @@ __device__ __forceinline__ void range_store(const Xyzz<F>& acc, bool first, bool
 #ifndef GG_G2_WAVES1
 #define GG_G2_WAVES1 0
 #endif
+#ifndef GG_G1_WAVES
+#define GG_G1_WAVES 2
+#endif
 template <class F>
-constexpr int kAccumWaves = (GG_G2_WAVES1 && std::is_same<F, Fp2>::value) || std::is_same<F, Fp2Bls>::value ? 1 : 2;
+constexpr int kAccumWaves = (GG_G2_WAVES1 && std::is_same<F, Fp2>::value) || std::is_same<F, Fp2Bls>::value
+                                ? 1
+                                : (std::is_same<F, Fp>::value ? GG_G1_WAVES : 2);
 
 template <class F>
 __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affine<F>* pts, const uint32_t* sorted,

@@ -461,7 +461,15 @@ def prove_partial_dist(pk: ProvingKeyShard, hs: HShard, solution: Solution, exch
 
 class TorchExchange:
     """All-to-all over torch.distributed for the distributed computeH: RCCL
-    (backend "nccl") on device buffers, or gloo through host staging."""
+    (backend "nccl") on device buffers, or gloo through host staging.
+
+    Failure semantics: a rank whose prove fails before or inside an exchange
+    leaves its peers blocked in all_to_all_single until the process group's
+    timeout (torch.distributed's, 10 minutes by default) -- the collective
+    cannot be cancelled from one side.  Jobs that must fail fast should create
+    the group with a short `timeout=`; the one-process multi-GPU prover
+    (MultiGpuProvingKey) has no such wait: its in-library barrier is broken by
+    the failing shard and every shard returns the error."""
 
     def __init__(self, nbytes: int, device):
         import torch
