@@ -24,6 +24,23 @@
 #pragma once
 #include "curve.cuh"
 
+// Column schedule of the product-scanning loops.  GG_R29_SPLIT = 1: the
+// operand products of a column go to their own accumulator, added once to the
+// running (carry + reduction) accumulator -- they do not depend on the
+// previous column's reduction digit, so the two chains interleave (ILP 2).
+#ifndef GG_R29_SPLIT
+#define GG_R29_SPLIT 0
+#endif
+#if GG_R29_SPLIT
+#define GG_COL_BEGIN uint64_t col_ = 0;
+#define GG_COL_ACC col_
+#define GG_COL_END acc += col_;
+#else
+#define GG_COL_BEGIN
+#define GG_COL_ACC acc
+#define GG_COL_END
+#endif
+
 namespace gg {
 
 struct Fp29Cfg {
@@ -105,9 +122,11 @@ __device__ __forceinline__ Fl<C> mul(const Fl<C>& a, const Fl<C>& b) {
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 2 * N - 1; k++) {
+        GG_COL_BEGIN
 #pragma unroll
         for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++)
-            acc += (uint64_t)a.l[i] * b.l[k - i];
+            GG_COL_ACC += (uint64_t)a.l[i] * b.l[k - i];
+        GG_COL_END
 #pragma unroll
         for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k - 1 : N - 1); i++)
             acc += (uint64_t)m[i] * C::P[k - i];
@@ -135,8 +154,9 @@ __device__ __forceinline__ Fl<C> sqr(const Fl<C>& a) {
         uint64_t s = 0;
 #pragma unroll
         for (int i = (k < N ? 0 : k - N + 1); 2 * i < k; i++) s += (uint64_t)a.l[i] * a.l[k - i];
-        acc += s << 1;
-        if ((k & 1) == 0) acc += (uint64_t)a.l[k / 2] * a.l[k / 2];
+        if ((k & 1) == 0) s = (s << 1) + (uint64_t)a.l[k / 2] * a.l[k / 2];
+        else s <<= 1;
+        acc += s;
 #pragma unroll
         for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k - 1 : N - 1); i++)
             acc += (uint64_t)m[i] * C::P[k - i];
@@ -162,11 +182,13 @@ __device__ __forceinline__ Fl<C> mul2(const Fl<C>& a, const Fl<C>& b, const Fl<C
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 2 * N - 1; k++) {
+        GG_COL_BEGIN
 #pragma unroll
         for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) {
-            acc += (uint64_t)a.l[i] * b.l[k - i];
-            acc += (uint64_t)c.l[i] * d.l[k - i];
+            GG_COL_ACC += (uint64_t)a.l[i] * b.l[k - i];
+            GG_COL_ACC += (uint64_t)c.l[i] * d.l[k - i];
         }
+        GG_COL_END
 #pragma unroll
         for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k - 1 : N - 1); i++)
             acc += (uint64_t)m[i] * C::P[k - i];
@@ -193,9 +215,11 @@ __device__ __forceinline__ Fl<C> mul_sub(const Fl<C>& a, const Fl<C>& b, const F
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 2 * N - 1; k++) {
+        GG_COL_BEGIN
 #pragma unroll
         for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++)
-            acc += (uint64_t)a.l[i] * b.l[k - i];
+            GG_COL_ACC += (uint64_t)a.l[i] * b.l[k - i];
+        GG_COL_END
 #pragma unroll
         for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k - 1 : N - 1); i++)
             acc += (uint64_t)m[i] * C::P[k - i];
@@ -224,11 +248,13 @@ __device__ __forceinline__ Fl<C> mul2_sub(const Fl<C>& a, const Fl<C>& b, const 
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 2 * N - 1; k++) {
+        GG_COL_BEGIN
 #pragma unroll
         for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) {
-            acc += (uint64_t)a.l[i] * b.l[k - i];
-            acc += (uint64_t)c.l[i] * d.l[k - i];
+            GG_COL_ACC += (uint64_t)a.l[i] * b.l[k - i];
+            GG_COL_ACC += (uint64_t)c.l[i] * d.l[k - i];
         }
+        GG_COL_END
 #pragma unroll
         for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k - 1 : N - 1); i++)
             acc += (uint64_t)m[i] * C::P[k - i];
@@ -256,13 +282,15 @@ __device__ __forceinline__ Fl<C> mul4(const Fl<C>& a, const Fl<C>& b, const Fl<C
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 2 * N - 1; k++) {
+        GG_COL_BEGIN
 #pragma unroll
         for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) {
-            acc += (uint64_t)a.l[i] * b.l[k - i];
-            acc += (uint64_t)c.l[i] * d.l[k - i];
-            acc += (uint64_t)e.l[i] * f.l[k - i];
-            acc += (uint64_t)g.l[i] * h.l[k - i];
+            GG_COL_ACC += (uint64_t)a.l[i] * b.l[k - i];
+            GG_COL_ACC += (uint64_t)c.l[i] * d.l[k - i];
+            GG_COL_ACC += (uint64_t)e.l[i] * f.l[k - i];
+            GG_COL_ACC += (uint64_t)g.l[i] * h.l[k - i];
         }
+        GG_COL_END
 #pragma unroll
         for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k - 1 : N - 1); i++)
             acc += (uint64_t)m[i] * C::P[k - i];

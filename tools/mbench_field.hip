@@ -31,10 +31,46 @@ __device__ __forceinline__ Fe<C> mul_cios(const Fe<C>& a, const Fe<C>& b) {
     return r;
 }
 
+// radix-29 product with the column shift done on 32-bit halves (v_alignbit_b32
+// + v_lshrrev_b32 in asm, so the compiler cannot fold it back into a 64-bit shift)
+__device__ __forceinline__ uint64_t shr29(uint64_t acc) {
+    uint32_t lo = (uint32_t)acc, hi = (uint32_t)(acc >> 32), nlo, nhi;
+    asm volatile("v_alignbit_b32 %0, %2, %3, 29\n\tv_lshrrev_b32 %1, 29, %2" : "=v"(nlo), "=v"(nhi) : "v"(hi), "v"(lo));
+    return ((uint64_t)nhi << 32) | nlo;
+}
+__device__ __forceinline__ Fp29 mul_alt(const Fp29& a, const Fp29& b) {
+    constexpr int N = 9;
+    uint32_t m[N];
+    Fp29 r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * N - 1; k++) {
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k : N - 1); i++) acc += (uint64_t)a.l[i] * b.l[k - i];
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k - 1 : N - 1); i++) acc += (uint64_t)m[i] * Fp29Cfg::P[k - i];
+        if (k < N) {
+            m[k] = ((uint32_t)acc * Fp29Cfg::INV) & Fp29Cfg::MASK;
+            acc += (uint64_t)m[k] * Fp29Cfg::P[0];
+        } else {
+            r.l[k - N] = (uint32_t)acc & Fp29Cfg::MASK;
+        }
+        acc = shr29(acc);
+    }
+    r.l[N - 1] = (uint32_t)acc;
+    return r;
+}
+
 template <int V>
 __global__ void __launch_bounds__(256) k_mulchain(Fp* data, int iters) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     Fp a = data[2 * i], b = data[2 * i + 1], c = a, d = b;
+    if (V == 3) {  // radix 29 with 32-bit column shifts
+        Fp29 a2 = unpack29(to_r261(a)), b2 = unpack29(to_r261(b)), c2 = a2, d2 = b2;
+        for (int k = 0; k < iters; k++) { a2 = mul_alt(a2, b2); c2 = mul_alt(c2, d2); b2 = mul_alt(b2, a2); d2 = mul_alt(d2, c2); }
+        data[2 * i] = to_std(a2) + to_std(c2); data[2 * i + 1] = to_std(b2) + to_std(d2);
+        return;
+    }
     if (V == 2) {  // 29-bit reduced-radix form (field29.cuh)
         Fp29 a2 = unpack29(to_r261(a)), b2 = unpack29(to_r261(b)), c2 = a2, d2 = b2;
         for (int k = 0; k < iters; k++) { a2 = mul(a2, b2); c2 = mul(c2, d2); b2 = mul(b2, a2); d2 = mul(d2, c2); }
@@ -126,6 +162,16 @@ int main() {
         (void)hipEventRecord(e0); k_mulchain<2><<<blocks, threads>>>(d3, iters); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
         (void)hipEventElapsedTime(&ms, e0, e1);
         printf("{\"variant\": \"radix29\", \"fp_mont_mul_per_s\": %.4e}\n", (double)n * iters * 4 / (ms * 1e-3));
+    }
+    {
+        Fp* d4; (void)hipMalloc(&d4, 2 * n * sizeof(Fp));
+        (void)hipMemcpy(d4, h.data(), 2 * n * sizeof(Fp), hipMemcpyHostToDevice);
+        for (int rep = 0; rep < 3; rep++) {
+            k_mulchain<3><<<blocks, threads>>>(d4, 4);
+            (void)hipEventRecord(e0); k_mulchain<3><<<blocks, threads>>>(d4, iters); (void)hipEventRecord(e1); (void)hipEventSynchronize(e1);
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            printf("{\"variant\": \"radix29_shift32\", \"fp_mont_mul_per_s\": %.4e}\n", (double)n * iters * 4 / (ms * 1e-3));
+        }
     }
     // equality of the variants on the same data
     (void)hipMemcpy(d, h.data(), 2 * n * sizeof(Fp), hipMemcpyHostToDevice);
