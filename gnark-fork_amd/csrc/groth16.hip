@@ -108,8 +108,9 @@ struct gg_groth16_pk {
 };
 
 static thread_local double g_timings[9];
-// [0] = host staging of A, B, C (inside the H task, overlapped with the MSMs)
-static thread_local double g_ext[1];
+// [0] = host staging of A, B, C (inside the H task, overlapped with the MSMs);
+// [1], [2] = steady-clock ms at entry to / return from the last prove call
+static thread_local double g_ext[3];
 
 static void ck(int rc) {
     if (rc != GG_OK) throw Error(rc, gg_last_error());
@@ -583,6 +584,7 @@ extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_
                  pk->nZ == (pk->n > 1 ? pk->n - 1 : 0),
              GG_ERR_INVALID_ARG, "gg_groth16_prove needs the whole key; a shard proves with "
                                  "gg_groth16_prove_partial + gg_groth16_finalize");
+    g_ext[1] = now_ms();
     std::lock_guard<std::mutex> lk(pk->mu);
     g_ext[0] = 0;
     if (pk->curve == GG_CURVE_BN254)
@@ -591,6 +593,7 @@ extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_
     else
         prove_whole<CurveBls12381>(pk, wires, sol_a, sol_b, sol_c, n_cons, inputs_on_device != 0, r_mont, s_mont,
                                    ar_aff, bs_aff, krs_aff, h_dev_out);
+    g_ext[2] = now_ms();
     GG_CAPI_END
 }
 
@@ -670,10 +673,12 @@ extern "C" int gg_groth16_finalize(const void* alpha1, const void* beta1, const 
 extern "C" int gg_groth16_last_timings_ex(double* ms, int cap) {
     GG_CAPI_BEGIN
     GG_CHECK(ms && cap >= 0, GG_ERR_INVALID_ARG, "null argument");
-    double all[10];
+    double all[12];
     memcpy(all, g_timings, sizeof(g_timings));
     all[9] = g_ext[0];
-    memcpy(ms, all, sizeof(double) * (size_t)std::min(cap, 10));
+    all[10] = g_ext[1];
+    all[11] = g_ext[2];
+    memcpy(ms, all, sizeof(double) * (size_t)std::min(cap, 12));
     GG_CAPI_END
 }
 

@@ -38,9 +38,11 @@ __device__ __forceinline__ void stf(FrB* p, const FrB& r) {
     q[1] = make_uint4(r.v[4], r.v[5], r.v[6], r.v[7]);
 }
 
+// sum c[k] x^k: nc - 1 products (the leading coefficient starts the chain)
 __device__ __forceinline__ FrB horner(const FrB* c, int nc, const FrB& x) {
-    FrB r = FrB::zero();
-    for (int k = nc - 1; k >= 0; k--) r = r * x + c[k];
+    if (nc <= 0) return FrB::zero();
+    FrB r = c[nc - 1];
+    for (int k = nc - 2; k >= 0; k--) r = r * x + c[k];
     return r;
 }
 
@@ -49,7 +51,8 @@ __global__ void __launch_bounds__(256) k_numerator_coset(NumParams P) {
     if (j >= P.n) return;
     const FrB one = FrB::one();
     FrB L = ldf(P.x[ID_L] + j), R = ldf(P.x[ID_R] + j), O = ldf(P.x[ID_O] + j);
-    FrB Z = ldf(P.x[ID_Z] + j), ZS = ldf(P.x[ID_ZS] + j);
+    FrB Z = ldf(P.x[ID_Z] + j);
+    FrB ZS = P.x[ID_ZS] ? ldf(P.x[ID_ZS] + j) : ldf(P.x[ID_Z] + (j + 1 == P.n ? 0 : j + 1));
     FrB S1 = ldf(P.x[ID_S1] + j) * P.beta, S2 = ldf(P.x[ID_S2] + j) * P.beta,
         S3 = ldf(P.x[ID_S3] + j) * P.beta;
     // blinding: bl/br/bo/bz evaluated at twiddles0[j], bz at twiddles0[(j+1) % n] for ZS
@@ -66,7 +69,7 @@ __global__ void __launch_bounds__(256) k_numerator_coset(NumParams P) {
     for (int q = ID_QCI; q + 1 < P.nx; q += 2) ic = ic + ldf(P.x[q] + j) * ldf(P.x[q + 1] + j);
     // orderingConstraint
     const FrB id = ldf(P.x[ID_ID] + j);
-    FrB a = P.gamma + L + id, b = id * P.cs + R + P.gamma, c = id * P.css + O + P.gamma;
+    FrB a = P.gamma + L + id * P.ka, b = id * P.kb + R + P.gamma, c = id * P.kc + O + P.gamma;
     FrB r = a * b * c * Z;
     a = S1 + L + P.gamma;
     b = S2 + R + P.gamma;
@@ -191,6 +194,9 @@ extern "C" int gg_plonk_numerator_coset(const void* const* x_dev, int nx, const 
     memcpy(P.alpha.v, alpha, 32);
     memcpy(P.cs.v, coset_gen, 32);
     P.css = P.cs * P.cs;
+    P.ka = FrB::one();  // x[ID_ID] = beta X (C ABI contract)
+    P.kb = P.cs;
+    P.kc = P.css;
     P.n = (uint32_t)n;
     P.rho = (uint32_t)rho;
     P.coset = (uint32_t)coset;

@@ -60,8 +60,12 @@ struct NumParams {
     int bdeg[4];              // number of coefficients
     const FrB* tw0;           // s.twiddles0: omega_small^j, j < n
     FrB beta, gamma, alpha, cs, css;
+    // orderingConstraint's identity terms: a, b, c use ka, kb, kc times x[ID_ID]
+    // (x[ID_ID] = beta X with ka = 1, kb = cs, kc = cs^2; or X with ka = beta, ...)
+    FrB ka, kb, kc;
     uint32_t n, log_big, rho, coset;
     FrB* cres;  // rho * n, bit-reversed big-domain order
+    // x[ID_ZS] == nullptr: ZS[j] = Z[(j + 1) % n] read from x[ID_Z] (no shifted copy)
 };
 void numerator(const NumParams& P, hipStream_t st);
 // divideByXMinusOne in place (prove.go:1223-1276), asynchronous

@@ -474,7 +474,8 @@ static void plonk_pk_build(gg_plonk_pk* pk, int log_n, int log_big, const void* 
         pk->pi_brev[i].alloc(nb);
     }
     for (auto& slot : pk->cev)
-        for (int k = 0; k < 7 + n_cmt; k++) slot[k].alloc(nb);
+        for (int k = 0; k < 7 + n_cmt; k++)
+            if (k != 4 && k != 5) slot[k].alloc(nb);  // 4 (ZS), 5 (beta X): formed in the numerator kernel
     pk->cres.alloc(32 * pk->big);
     const size_t nb3 = 32 * (n + 3);
     for (auto& b : pk->hpad) b.alloc(nb3);
@@ -616,10 +617,8 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
             hipStream_t q = s[2 + slot];
             DevBuf* e = pk->cev[slot];
             // per-proof polynomials on this coset: L R O Z, ZS (shift), ID = beta X, Qk, Pi_j
+            // (ZS = Z shifted and beta X are formed inside the numerator kernel)
             for (int k = 0; k < 4; k++) coset_eval(pk, F(pk->cbrev[k]), F(e[k]), (int)i, q);
-            plk::shift_copy(F(e[3]), F(e[4]), n, q);
-            dcopy(e[5].p, pk->ev[gg_plonk_pk::E_X][i].p, nb, q);
-            plk::scale(F(e[5]), n, beta, q);
             coset_eval(pk, F(pk->qkc), F(e[6]), (int)i, q);
             for (int j = 0; j < n_cmt; j++) coset_eval(pk, F(pk->pi_brev[j]), F(e[7 + j]), (int)i, q);
             plk::NumParams NP{};
@@ -627,7 +626,7 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
             NP.x[plk::ID_R] = F(e[1]);
             NP.x[plk::ID_O] = F(e[2]);
             NP.x[plk::ID_Z] = F(e[3]);
-            NP.x[plk::ID_ZS] = F(e[4]);
+            NP.x[plk::ID_ZS] = nullptr;  // Z[(j + 1) % n]
             NP.x[plk::ID_QL] = F(pk->ev[gg_plonk_pk::E_QL][i]);
             NP.x[plk::ID_QR] = F(pk->ev[gg_plonk_pk::E_QR][i]);
             NP.x[plk::ID_QM] = F(pk->ev[gg_plonk_pk::E_QM][i]);
@@ -636,7 +635,7 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
             NP.x[plk::ID_S1] = F(pk->ev[gg_plonk_pk::E_S1][i]);
             NP.x[plk::ID_S2] = F(pk->ev[gg_plonk_pk::E_S2][i]);
             NP.x[plk::ID_S3] = F(pk->ev[gg_plonk_pk::E_S3][i]);
-            NP.x[plk::ID_ID] = F(e[5]);
+            NP.x[plk::ID_ID] = F(pk->ev[gg_plonk_pk::E_X][i]);  // X; beta folded into ka, kb, kc
             NP.x[plk::ID_LONE] = F(pk->ev[gg_plonk_pk::E_LONE][i]);
             for (int j = 0; j < n_cmt; j++) {
                 NP.x[plk::ID_QCI + 2 * j] = F(pk->ev[gg_plonk_pk::E_QCP0 + j][i]);
@@ -660,6 +659,9 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
             NP.alpha = alpha;
             NP.cs = cs;
             NP.css = css;
+            NP.ka = beta;
+            NP.kb = beta * cs;
+            NP.kc = beta * css;
             NP.n = (uint32_t)n;
             NP.rho = (uint32_t)pk->rho;
             NP.coset = (uint32_t)i;

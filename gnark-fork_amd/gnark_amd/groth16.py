@@ -234,10 +234,10 @@ def last_timings() -> dict:
     """Per-stage wall times (ms) of this thread's last prove: upload = host staging
     of the wires (before the MSMs start); upload_abc = host staging of A, B, C
     inside the computeH task (overlapped with the MSMs, included in compute_h)."""
-    arr = (ctypes.c_double * 10)()
-    check(lib.gg_groth16_last_timings_ex(arr, 10))
+    arr = (ctypes.c_double * 12)()
+    check(lib.gg_groth16_last_timings_ex(arr, 12))
     keys = ["upload", "compute_h", "msm_A", "msm_B1", "msm_K", "msm_Z", "msm_G2", "epilogue", "total",
-            "upload_abc"]
+            "upload_abc", "t_enter", "t_exit"]
     return dict(zip(keys, list(arr)))
 
 

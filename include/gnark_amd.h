@@ -329,7 +329,9 @@ int gg_groth16_mpk_last_timings(gg_groth16_mpk_t mpk, double *ms3);
 int gg_groth16_last_timings(double *ms9);
 /* the same plus [9] = host staging of the solution's A, B, C (host inputs: done
  * by the computeH task through pinned buffers while the MSMs run; part of [1]).
- * [0] is the staging of the wires (before any MSM starts).  cap: entries wanted. */
+ * [0] is the staging of the wires (before any MSM starts); [10], [11] = the
+ * steady clock (CLOCK_MONOTONIC, ms) at entry to / return from gg_groth16_prove.
+ * cap: entries wanted (<= 12). */
 int gg_groth16_last_timings_ex(double *ms, int cap);
 
 
