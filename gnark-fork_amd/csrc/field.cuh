@@ -256,6 +256,27 @@ __device__ __forceinline__ Fe<C> mont_mul_ps8(const Fe<C>& a, const Fe<C>& b) {
     for (int i = 0; i < 8; i++) r.v[i] = br ? t[i] : s.v[i];
     return r;
 }
+// The same product without the final subtraction: t = (a b + m p) / R < a b / R + p,
+// so a < 4p, b < p gives t < 2p whenever 4p < R (BN254 fr) -- the lazily reduced
+// NTT butterflies (ntt.hip) keep their values below 2p
+template <class C>
+__device__ __forceinline__ Fe<C> mont_mul_ps8_nored(const Fe<C>& a, const Fe<C>& b) {
+    const uint32_t a0 = a.v[0], a1 = a.v[1], a2 = a.v[2], a3 = a.v[3], a4 = a.v[4], a5 = a.v[5],
+                   a6 = a.v[6], a7 = a.v[7];
+    const uint32_t b0 = b.v[0], b1 = b.v[1], b2 = b.v[2], b3 = b.v[3], b4 = b.v[4], b5 = b.v[5],
+                   b6 = b.v[6], b7 = b.v[7];
+    const uint32_t P0 = C::P[0], P1 = C::P[1], P2 = C::P[2], P3 = C::P[3], P4 = C::P[4],
+                   P5 = C::P[5], P6 = C::P[6], P7 = C::P[7], INV = C::INV;
+    uint32_t m0, m1, m2, m3, m4, m5, m6, m7;
+    uint32_t t[8];
+    uint64_t acc = 0;
+    uint32_t c2 = 0;
+#include "mont_ps.inc"
+    Fe<C> r;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = t[i];
+    return r;
+}
 // 12-limb (BLS12-381 Fp) product scanning: 288 v_mad_u64_u32 + 288 v_addc
 template <class C>
 __device__ __forceinline__ Fe<C> mont_mul_ps12(const Fe<C>& a, const Fe<C>& b) {
@@ -288,6 +309,17 @@ __device__ __forceinline__ Fe<C> mont_mul_ps(const Fe<C>& a, const Fe<C>& b) {
     }
 }
 #endif
+
+// a b mod p as some representative < 2p (see mont_mul_ps8_nored; 8-limb fields)
+template <class C>
+GG_HD Fe<C> mul_nored(const Fe<C>& a, const Fe<C>& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    static_assert(C::N == 8, "8-limb fields");
+    return mont_mul_ps8_nored(a, b);
+#else
+    return mont_mul_host(a, b);  // canonical, also < 2p
+#endif
+}
 
 #ifndef GG_MUL_CIOS
 #define GG_MUL_CIOS 0

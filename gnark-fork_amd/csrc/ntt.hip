@@ -64,7 +64,88 @@ struct PassParams {
     int epi_mul_sub;  // out = ea*eb - x
     const F* ea;
     const F* eb;
+    int canon_out;    // last pass of the transform: write canonical values (lazy fields)
 };
+
+// Lazily reduced butterflies for BN254 fr (4r < 2^256): values stay below 2r
+// inside a transform (also between passes, in HBM), the twiddle product skips
+// its final subtraction (mul_nored: a < 4r, w < r -> < 2r), the DIF difference
+// a - b + 2r is multiplied unreduced, and the last pass writes canonical values.
+// BLS12-381 fr (2r < 2^256 < 4r) keeps the canonical butterflies.
+template <class F>
+struct NttLazy {
+    static constexpr bool on = false;
+};
+template <>
+struct NttLazy<Fr> {
+    static constexpr bool on = true;
+};
+template <class C>
+GG_HD constexpr uint32_t twop_limb(int i) {
+    uint64_t c = 0;
+    uint32_t v = 0;
+    for (int j = 0; j <= i; j++) {
+        const uint64_t t = (uint64_t)C::P[j] * 2 + c;
+        v = (uint32_t)t;
+        c = t >> 32;
+    }
+    return v;
+}
+// x < 4p -> representative < 2p
+template <class C>
+__device__ __forceinline__ Fe<C> red2p(const Fe<C>& x) {
+    Fe<C> s, r;
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = __builtin_subc(x.v[i], twop_limb<C>(i), br, &br);
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = br ? x.v[i] : s.v[i];
+    return r;
+}
+// a, b < 2p: a + b reduced below 2p
+template <class C>
+__device__ __forceinline__ Fe<C> add2p(const Fe<C>& a, const Fe<C>& b) {
+    Fe<C> r;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = __builtin_addc(a.v[i], b.v[i], c, &c);
+    return red2p(r);
+}
+// a, b < 2p: a - b + 2p in (0, 4p), unreduced
+template <class C>
+__device__ __forceinline__ Fe<C> subnr2p(const Fe<C>& a, const Fe<C>& b) {
+    Fe<C> r;
+    uint32_t br = 0, c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = __builtin_addc(r.v[i], twop_limb<C>(i), c, &c);
+    return r;
+}
+// a, b < 2p: (a - b) mod 2p, below 2p
+template <class C>
+__device__ __forceinline__ Fe<C> sub2p(const Fe<C>& a, const Fe<C>& b) {
+    Fe<C> r, s;
+    uint32_t br = 0, c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = __builtin_subc(a.v[i], b.v[i], br, &br);
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = __builtin_addc(r.v[i], twop_limb<C>(i), c, &c);
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = br ? s.v[i] : r.v[i];
+    return r;
+}
+// x < 2p -> canonical
+template <class C>
+__device__ __forceinline__ Fe<C> canon(const Fe<C>& x) {
+    Fe<C> s, r;
+    uint32_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) s.v[i] = __builtin_subc(x.v[i], C::P[i], br, &br);
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = br ? x.v[i] : s.v[i];
+    return r;
+}
 
 __device__ __forceinline__ uint32_t brev_bits(uint32_t i, int L) {
     return L ? (__brev(i) >> (32 - L)) : 0u;
@@ -141,6 +222,18 @@ __device__ __forceinline__ void ntt_round(const PassParams<F>& P, uint32_t* lds,
                 if (m & (1 << r)) continue;
                 const int m2 = m | (1 << r);
                 const uint32_t i = g[m] & bmask;
+                if constexpr (NttLazy<F>::on) {
+                    if (DIT) {
+                        F t = i ? mul_nored(x[m2], load_fr(twb + i)) : x[m2];
+                        x[m2] = sub2p(x[m], t);
+                        x[m] = add2p(x[m], t);
+                    } else {
+                        F d = subnr2p(x[m], x[m2]);
+                        x[m] = add2p(x[m], x[m2]);
+                        x[m2] = i ? mul_nored(d, load_fr(twb + i)) : red2p(d);
+                    }
+                    continue;
+                }
                 if (DIT) {
                     F t = i ? x[m2] * load_fr(twb + i) : x[m2];
                     x[m2] = x[m] - t;
@@ -156,6 +249,8 @@ __device__ __forceinline__ void ntt_round(const PassParams<F>& P, uint32_t* lds,
 #pragma unroll
             for (int m = 0; m < R; m++) {
                 F y = x[m];
+                // lazy fields: the post-scale's full product also brings y < 2r below r
+                if (NttLazy<F>::on && P.canon_out && !P.has_post) y = canon(y);
                 if (P.has_post) y = apply_scale(P.post, g[m], P.log_n, y);
                 if (P.epi_mul_sub) y = load_fr(P.ea + g[m]) * load_fr(P.eb + g[m]) - y;
                 store_fr(P.out + g[m], y);
@@ -325,6 +420,7 @@ void run_transform(DomainT<C>* d, const Fe<C>* in, Fe<C>* out, bool dit, bool in
         bool last = (pi + 1 == passes.size());
         if (last && post_kind >= 0) { P.has_post = 1; P.post = d->spec[post_kind]; }
         if (last && ea) { P.epi_mul_sub = 1; P.ea = ea; P.eb = eb; }
+        P.canon_out = last ? 1 : 0;
         int T = 1 << (ps.k + ps.tl);
         unsigned tiles = (unsigned)(d->n / (size_t)T);
         size_t lds = (ps.k > 3) ? (size_t)(T + (T >> 5)) * 32 : 0;  // single-round passes skip LDS
