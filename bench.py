@@ -244,7 +244,19 @@ def main():
         mul_rate = nB2 * W2 * 10 * 3 / (g2_ms * 1e-3) / 1e9  # Fp2 mul ~ 3 Fp mul (Karatsuba)
         roofline["valu"] = {"achieved_Gfpmul_s": mul_rate, "peak_Gfpmul_s": FPMUL_PEAK_G,
                             "frac": mul_rate / FPMUL_PEAK_G,
-                            "basis": "|B2| x W mixed XYZZ adds x 10 Fp2-mul x 3 Fp-mul (Karatsuba)"}
+                            "basis": "|B2| x W mixed XYZZ adds x 10 Fp2-mul x 3 Fp-mul (Karatsuba); the "
+                                     "radix-2^29 form does a product in fewer instructions than the 32-bit "
+                                     "limb multiply the peak was measured with, hence frac > 1"}
+        sq = pmc_sq("k_accum_range<gg::Fp2>", {"workload": "groth16", "log_n": args.log_n, "n_gpus": world})
+        if sq:
+            # VALU issue rate: wave instructions per SIMD cycle (1024 SIMDs, 2.4 GHz);
+            # the instruction mix (~60 % v_mad_u64_u32 at ~5.5 cycles, the rest ~3.1)
+            # caps it at ~0.22 on gfx950 (profiles/r02_mbench_field29_v2.txt)
+            ipc = sq["valu_insts"] / (g2_ms * 1e-3 * 2.4e9 * 1024)
+            roofline["valu"]["pmc"] = {"valu_insts_per_launch": sq["valu_insts"],
+                                       "insts_per_madd_per_lane": sq["valu_insts"] * 64 / (nB2 * W2),
+                                       "insts_per_simd_cycle": ipc, "issue_cap_for_mix": 0.22,
+                                       "source": sq["source"]}
 
     out = {
         "metric": METRIC, "value": value, "unit": "constraints/s", "n_gpus": world,
@@ -542,6 +554,24 @@ def pmc_traffic(kernel, workload):
                     f"the point bytes per scalar (no doublings at prove time), so traffic >> the "
                     f"algorithmic bytes")
     return None, "no committed PMC profile for this workload"
+
+
+def pmc_sq(kernel, workload):
+    """SQ_INSTS_VALU / SQ_WAVES per launch of `kernel` from a committed SQ-counter
+    profile of the same workload (tools/pmc_counters.py); None if absent."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_sq*.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if any(d.get("workload", {}).get(k) != v for k, v in workload.items()):
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if kernel in k and "SQ_INSTS_VALU" in v:
+                return {"valu_insts": v["SQ_INSTS_VALU"], "waves": v.get("SQ_WAVES"),
+                        "source": os.path.basename(f)}
+    return None
 
 
 def cpu_baseline(threads, gpu_prove_ms, gpu_ncons, log_n=20):

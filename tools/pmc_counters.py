@@ -1,6 +1,6 @@
 """Per-kernel averages of arbitrary rocprofv3 --pmc counters (rocpd sqlite),
 plus derived VALU figures when the SQ counters are present.
-usage: pmc_counters.py out.json db1 [db2 ...]   (one db per --pmc pass)
+usage: pmc_counters.py out.json db1 [db2 ...]   (one db per --pmc pass; a "workload" key is added by hand)
 SQ_* cycle counters count quad-cycles on gfx950 (MI355X_MICROARCH.md, PMC units):
   valu_busy = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES   (fraction of resident-wave
   time a VALU instruction issues), insts_per_wave = SQ_INSTS_VALU / SQ_WAVES."""
