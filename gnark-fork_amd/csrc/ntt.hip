@@ -265,8 +265,13 @@ __device__ __forceinline__ void ntt_round(const PassParams<F>& P, uint32_t* lds,
     }
 }
 
-template <class F, bool DIT>
-__global__ void __launch_bounds__(256) k_ntt_pass(PassParams<F> P) {
+// MAXNB = stages per register round: 3 (radix-8, 256 threads per 2048-element
+// tile, ~190 VGPRs: 2 waves per SIMD) or 2 (radix-4, 512 threads, <= 128 VGPRs:
+// 4 waves per SIMD -- more LDS exchanges, better latency hiding)
+template <int MAXNB>
+constexpr int kNttThreads = MAXNB == 3 ? 256 : 512;
+template <class F, bool DIT, int MAXNB>
+__global__ void __launch_bounds__(kNttThreads<MAXNB>, MAXNB == 3 ? 1 : 4) k_ntt_pass(PassParams<F> P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int k = P.k, tl = P.tl;
     const int T = 1 << (k + tl);
@@ -292,12 +297,19 @@ __global__ void __launch_bounds__(256) k_ntt_pass(PassParams<F> P) {
     int done = 0;
     bool first = true;
     while (done < k) {
-        const int nb = min(3, k - done);
+        const int nb = min(MAXNB, k - done);
         const int qlo = DIT ? done : (k - done - nb);
         const bool last = (done + nb == k);
         if (!first) __syncthreads();
-        if (nb == 3) ntt_round<F, 3, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
-        else if (nb == 2) ntt_round<F, 2, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
+        if constexpr (MAXNB >= 3) {
+            if (nb == 3) {
+                ntt_round<F, 3, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
+                first = false;
+                done += nb;
+                continue;
+            }
+        }
+        if (nb == 2) ntt_round<F, 2, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
         else ntt_round<F, 1, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
         first = false;
         done += nb;
@@ -396,6 +408,13 @@ static void upload(DevBuf& b, const std::vector<F>& v) {
     GG_HIP(hipMemcpy(b.p, v.data(), v.size() * sizeof(F), hipMemcpyHostToDevice));
 }
 
+// NTT pass flavour (k_ntt_pass MAXNB); GG_NTT_RADIX=4 or 8 overrides the default
+static bool ntt_radix4() {
+    const char* e = getenv("GG_NTT_RADIX");
+    if (e) return atoi(e) == 4;
+    return false;
+}
+
 static hipStream_t pick_stream(void* s) { return s ? (hipStream_t)s : hipStreamPerThread; }
 
 template <class C>
@@ -425,8 +444,15 @@ void run_transform(DomainT<C>* d, const Fe<C>* in, Fe<C>* out, bool dit, bool in
         unsigned tiles = (unsigned)(d->n / (size_t)T);
         size_t lds = (ps.k > 3) ? (size_t)(T + (T >> 5)) * 32 : 0;  // single-round passes skip LDS
         ProfScope prof("ntt_pass", st, (double)d->n);
-        if (dit) hipLaunchKernelGGL((k_ntt_pass<F, true>), dim3(tiles), dim3(256), lds, st, P);
-        else hipLaunchKernelGGL((k_ntt_pass<F, false>), dim3(tiles), dim3(256), lds, st, P);
+        static const bool r4 = ntt_radix4();
+        if (r4) {
+            lds = (ps.k > 2) ? (size_t)(T + (T >> 5)) * 32 : 0;
+            if (dit) hipLaunchKernelGGL((k_ntt_pass<F, true, 2>), dim3(tiles), dim3(512), lds, st, P);
+            else hipLaunchKernelGGL((k_ntt_pass<F, false, 2>), dim3(tiles), dim3(512), lds, st, P);
+        } else {
+            if (dit) hipLaunchKernelGGL((k_ntt_pass<F, true, 3>), dim3(tiles), dim3(256), lds, st, P);
+            else hipLaunchKernelGGL((k_ntt_pass<F, false, 3>), dim3(tiles), dim3(256), lds, st, P);
+        }
         GG_HIP(hipGetLastError());
         prof.stop(st);
         src = out;
