@@ -269,9 +269,11 @@ __device__ __forceinline__ void ntt_round(const PassParams<F>& P, uint32_t* lds,
 // tile, ~190 VGPRs: 2 waves per SIMD) or 2 (radix-4, 512 threads, <= 128 VGPRs:
 // 4 waves per SIMD -- more LDS exchanges, better latency hiding)
 template <int MAXNB>
-constexpr int kNttThreads = MAXNB == 3 ? 256 : 512;
+constexpr int kNttThreads = MAXNB == 3 ? 256 : (MAXNB == 2 ? 512 : 1024);
+template <int MAXNB>
+constexpr int kNttWaves = MAXNB == 3 ? 1 : (MAXNB == 2 ? 4 : 8);
 template <class F, bool DIT, int MAXNB>
-__global__ void __launch_bounds__(kNttThreads<MAXNB>, MAXNB == 3 ? 1 : 4) k_ntt_pass(PassParams<F> P) {
+__global__ void __launch_bounds__(kNttThreads<MAXNB>, kNttWaves<MAXNB>) k_ntt_pass(PassParams<F> P) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const int k = P.k, tl = P.tl;
     const int T = 1 << (k + tl);
@@ -309,8 +311,15 @@ __global__ void __launch_bounds__(kNttThreads<MAXNB>, MAXNB == 3 ? 1 : 4) k_ntt_
                 continue;
             }
         }
-        if (nb == 2) ntt_round<F, 2, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
-        else ntt_round<F, 1, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
+        if constexpr (MAXNB >= 2) {
+            if (nb == 2) {
+                ntt_round<F, 2, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
+                first = false;
+                done += nb;
+                continue;
+            }
+        }
+        ntt_round<F, 1, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
         first = false;
         done += nb;
     }
@@ -412,10 +421,10 @@ static void upload(DevBuf& b, const std::vector<F>& v) {
 // Radix-4 rounds at 4 waves per SIMD measured faster on MI355X than radix-8 at 2
 // (2^24 BN254: DIF 2.63 -> 2.44 ms, computeH 18.5 -> 16.7 ms; BLS12-381 2^22
 // 0.72 -> 0.67 ms): the extra LDS exchanges cost less than the latency they hide.
-static bool ntt_radix4() {
+static int ntt_radix() {
     const char* e = getenv("GG_NTT_RADIX");
-    if (e) return atoi(e) == 4;
-    return true;
+    const int r = e ? atoi(e) : 4;
+    return (r == 2 || r == 8) ? r : 4;
 }
 
 static hipStream_t pick_stream(void* s) { return s ? (hipStream_t)s : hipStreamPerThread; }
@@ -447,11 +456,15 @@ void run_transform(DomainT<C>* d, const Fe<C>* in, Fe<C>* out, bool dit, bool in
         unsigned tiles = (unsigned)(d->n / (size_t)T);
         size_t lds = (ps.k > 3) ? (size_t)(T + (T >> 5)) * 32 : 0;  // single-round passes skip LDS
         ProfScope prof("ntt_pass", st, (double)d->n);
-        static const bool r4 = ntt_radix4();
-        if (r4) {
+        static const int radix = ntt_radix();
+        if (radix == 4) {
             lds = (ps.k > 2) ? (size_t)(T + (T >> 5)) * 32 : 0;
             if (dit) hipLaunchKernelGGL((k_ntt_pass<F, true, 2>), dim3(tiles), dim3(512), lds, st, P);
             else hipLaunchKernelGGL((k_ntt_pass<F, false, 2>), dim3(tiles), dim3(512), lds, st, P);
+        } else if (radix == 2) {
+            lds = (ps.k > 1) ? (size_t)(T + (T >> 5)) * 32 : 0;
+            if (dit) hipLaunchKernelGGL((k_ntt_pass<F, true, 1>), dim3(tiles), dim3(1024), lds, st, P);
+            else hipLaunchKernelGGL((k_ntt_pass<F, false, 1>), dim3(tiles), dim3(1024), lds, st, P);
         } else {
             if (dit) hipLaunchKernelGGL((k_ntt_pass<F, true, 3>), dim3(tiles), dim3(256), lds, st, P);
             else hipLaunchKernelGGL((k_ntt_pass<F, false, 3>), dim3(tiles), dim3(256), lds, st, P);
