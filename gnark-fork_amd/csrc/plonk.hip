@@ -46,9 +46,8 @@ __device__ __forceinline__ FrB horner(const FrB* c, int nc, const FrB& x) {
     return r;
 }
 
-__global__ void __launch_bounds__(256) k_numerator_coset(NumParams P) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= P.n) return;
+// allConstraints at point j of the coset (prove.go:928-954)
+__device__ __forceinline__ FrB numerator_at(const NumParams& P, uint32_t j) {
     const FrB one = FrB::one();
     FrB L = ldf(P.x[ID_L] + j), R = ldf(P.x[ID_R] + j), O = ldf(P.x[ID_O] + j);
     FrB Z = ldf(P.x[ID_Z] + j);
@@ -77,10 +76,43 @@ __global__ void __launch_bounds__(256) k_numerator_coset(NumParams P) {
     FrB l = a * b * c * ZS - r;
     // ratioLocalConstraint
     FrB rl = (Z - one) * ldf(P.x[ID_LONE] + j);
-    FrB res = (rl * P.alpha + l) * P.alpha + ic;
-    // cres[bitrev(rho*j + coset)] (prove.go:1036-1038)
+    return (rl * P.alpha + l) * P.alpha + ic;
+}
+
+// small domains: one point per thread, cres[bitrev(rho*j + coset)] (prove.go:1036-1038)
+__global__ void __launch_bounds__(256) k_numerator_coset(NumParams P) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= P.n) return;
+    const FrB res = numerator_at(P, j);
     const uint32_t pos = __brev(P.rho * j + P.coset) >> (32 - P.log_big);
     stf(P.cres + (P.log_big ? pos : 0), res);
+}
+
+// n >= 256: 16 x 16 tiles.  Thread t of block m computes j = h 2^(L-4) + 16 m + l
+// (h = t >> 4, l = t & 15): rows of 16 consecutive j, coalesced loads.  With
+// rho = 2^r the cres slot is
+//   bitrev_{L+r}(rho j + coset) = brev_r(coset) << L | brev4(l) << (L-4)
+//                                 | brev_{L-8}(m) << 4 | brev4(h),
+// so for each l the 16 values of h fill 16 consecutive slots: the results are
+// transposed through LDS and stored as 16 runs of 512 B (not 256 scattered 32-B
+// writes).
+__global__ void __launch_bounds__(256) k_numerator_coset_tiled(NumParams P, uint32_t log_n) {
+    __shared__ uint32_t tile[8][256 + 8];  // limb-major, padded
+    const uint32_t t = threadIdx.x, h = t >> 4, l = t & 15, m = blockIdx.x;
+    const uint32_t j = (h << (log_n - 4)) | (m << 4) | l;
+    const FrB res = numerator_at(P, j);
+    const uint32_t slot = l * 16 + (__brev(h) >> 28);
+#pragma unroll
+    for (int k = 0; k < 8; k++) tile[k][slot + (slot >> 5)] = res.v[k];
+    __syncthreads();
+    const uint32_t r = P.log_big - log_n;
+    const uint32_t l2 = t >> 4, col = t & 15;
+    const uint32_t pos = (r ? (__brev(P.coset) >> (32 - r)) << log_n : 0u) | ((__brev(l2) >> 28) << (log_n - 4)) |
+                         (log_n > 8 ? (__brev(m) >> (40 - log_n)) << 4 : 0u) | col;
+    FrB o;
+#pragma unroll
+    for (int k = 0; k < 8; k++) o.v[k] = tile[k][t + (t >> 5)];
+    stf(P.cres + pos, o);
 }
 
 struct PeriodicTab {
@@ -129,7 +161,12 @@ void batch_invert(FrB* a, size_t n, hipStream_t st, Arena& ar) {
 
 void numerator(const NumParams& P, hipStream_t st) {
     ProfScope prof("plonk_numerator", st, (double)P.n);
-    hipLaunchKernelGGL(k_numerator_coset, dim3(grid_for(P.n, 256)), dim3(256), 0, st, P);
+    uint32_t log_n = 0;
+    while ((1u << log_n) < P.n) log_n++;
+    if (log_n >= 8)
+        hipLaunchKernelGGL(k_numerator_coset_tiled, dim3(P.n >> 8), dim3(256), 0, st, P, log_n);
+    else
+        hipLaunchKernelGGL(k_numerator_coset, dim3(grid_for(P.n, 256)), dim3(256), 0, st, P);
     GG_HIP(hipGetLastError());
     prof.stop(st);
 }
