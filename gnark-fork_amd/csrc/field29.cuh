@@ -72,6 +72,10 @@ struct Fp29Cfg {
         {0x32edefaau, 0x261a4447u, 0x2aafd3d9u, 0x30fed0e4u, 0x212318cfu, 0x31238483u, 0x23e94785u, 0x3628e537u, 0x012259d5u},
         {0x2b6aecf1u, 0x271ea4feu, 0x27227728u, 0x33d3f3b5u, 0x36a8f247u, 0x33fec543u, 0x249028c6u, 0x24850b6bu, 0x0152be24u},
         {0x23e7ea38u, 0x282305b5u, 0x23951a77u, 0x36a91686u, 0x2c2ecbbfu, 0x36da0604u, 0x25370a07u, 0x32e1319fu, 0x01832272u}};
+    // 5 p with limbs 0..7 in [2^31 - 4, 2^31 + 2^29): dominates every limb of an
+    // unnormalised sum of three normalised values (< 3 * 2^29), see sqr_subw5
+    static constexpr uint32_t KPW5[9] = {0x9a70f263u, 0x8515e38du, 0x8e3d3087u, 0x8e29ae10u, 0x8b9d3f54u,
+                                         0x8e4843bfu, 0x83426641u, 0x87ccbf00u, 0x00f1f584u};
 };
 
 // BLS12-381 Fp in 14 x 28-bit limbs, R' = 2^392 = 2520 p: a column is at most
@@ -103,6 +107,10 @@ struct FpBls28Cfg {
         {0x1ffe0002u, 0x1f9ffffeu, 0x17fffe5au, 0x1fff827eu, 0x14d8b806u, 0x1c5c825bu, 0x1c6b24eeu, 0x1b51e706u, 0x1acbc51cu, 0x1c60d0c4u, 0x15ee4592u, 0x1679dc29u, 0x1b7d58feu, 0x0009c065u},
         {0x1ffdaaadu, 0x1f8ffffeu, 0x1bfffe14u, 0x1fff6d93u, 0x1afcd6b2u, 0x166bed6au, 0x1bd255c1u, 0x1a8a3832u, 0x1f4310a1u, 0x111b9e3au, 0x1195fbd6u, 0x14e380dbu, 0x1d67927eu, 0x000b6076u},
         {0x1ffd5558u, 0x1f7ffffeu, 0x1ffffdceu, 0x1fff58a8u, 0x1120f55eu, 0x107b587au, 0x1b398694u, 0x19c2895eu, 0x13ba5c26u, 0x15d66bb1u, 0x1d3db219u, 0x134d258cu, 0x1f51cbfeu, 0x000d0087u}};
+    // 5 p with limbs 0..12 in [2^30 - 4, 2^30 + 2^28) (see Fp29Cfg::KPW5)
+    static constexpr uint32_t KPW5[14] = {0x4ffe5557u, 0x4faffffbu, 0x43fffe9du, 0x4fff9766u, 0x4eb49957u,
+                                          0x424d1748u, 0x4d03f419u, 0x4c1995d7u, 0x46547994u, 0x47a6034bu,
+                                          0x4a468f4cu, 0x48103774u, 0x49931f7bu, 0x00082051u};
 };
 
 template <class C>
@@ -201,6 +209,40 @@ __device__ __forceinline__ Fl<C> mul2(const Fl<C>& a, const Fl<C>& b, const Fl<C
         acc >>= B;
     }
     r.l[N - 1] = (uint32_t)acc;
+    return r;
+}
+
+// a^2 / M + 5 p - s, s an UNNORMALISED sum of three normalised values (limbs
+// < 3 * 2^B, value < 5 p): the subtraction is folded into the output columns
+// against KPW5, whose limbs dominate s's, so every column term is >= 0; the
+// reduction's carry chain normalises the result
+template <class C>
+__device__ __forceinline__ Fl<C> sqr_subw5(const Fl<C>& a, const Fl<C>& s) {
+    constexpr int N = C::N, B = C::B;
+    uint32_t m[N];
+    Fl<C> r;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * N - 1; k++) {
+        uint64_t t = 0;
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); 2 * i < k; i++) t += (uint64_t)a.l[i] * a.l[k - i];
+        if ((k & 1) == 0) t = (t << 1) + (uint64_t)a.l[k / 2] * a.l[k / 2];
+        else t <<= 1;
+        acc += t;
+#pragma unroll
+        for (int i = (k < N ? 0 : k - N + 1); i <= (k < N ? k - 1 : N - 1); i++)
+            acc += (uint64_t)m[i] * C::P[k - i];
+        if (k < N) {
+            m[k] = ((uint32_t)acc * C::INV) & C::MASK;
+            acc += (uint64_t)m[k] * C::P[0];
+        } else {
+            acc += C::KPW5[k - N] - s.l[k - N];
+            r.l[k - N] = (uint32_t)acc & C::MASK;
+        }
+        acc >>= B;
+    }
+    r.l[N - 1] = (uint32_t)acc + (C::KPW5[N - 1] - s.l[N - 1]);
     return r;
 }
 
@@ -354,6 +396,42 @@ __device__ __forceinline__ Fl<C> sub(const Fl<C>& a, const Fl<C>& b) {
     return r;
 }
 
+// a + b limb by limb, unnormalised (limbs < 2^(B+1) for normalised a, b)
+template <class C>
+__device__ __forceinline__ Fl<C> add_nn(const Fl<C>& a, const Fl<C>& b) {
+    Fl<C> r;
+#pragma unroll
+    for (int i = 0; i < C::N; i++) r.l[i] = a.l[i] + b.l[i];
+    return r;
+}
+
+// a + K p - b limb by limb, unnormalised: b normalised (its limbs never exceed
+// KP's, as in sub<K>), result limbs < 2^B + 2^(B+1).  Only as a product operand
+// whose column bound allows it (one such operand per product, see the callers).
+template <int K, class C>
+__device__ __forceinline__ Fl<C> sub_nn(const Fl<C>& a, const Fl<C>& b) {
+    static_assert(K >= 1 && K <= 8, "multiple of p");
+    Fl<C> r;
+#pragma unroll
+    for (int i = 0; i < C::N; i++) r.l[i] = a.l[i] + (C::KP[K - 1][i] - b.l[i]);
+    return r;
+}
+
+// carry-propagate limbs < 2^31 (value unchanged)
+template <class C>
+__device__ __forceinline__ Fl<C> norm(const Fl<C>& a) {
+    Fl<C> r;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < C::N - 1; i++) {
+        const uint32_t t = a.l[i] + c;
+        r.l[i] = t & C::MASK;
+        c = t >> C::B;
+    }
+    r.l[C::N - 1] = a.l[C::N - 1] + c;
+    return r;
+}
+
 // v == 0 mod p for a normalised v < kmax p: v = j p with j = v_0 p^-1 mod 2^B
 template <class C>
 __device__ __forceinline__ bool is_zero_mod(const Fl<C>& v, uint32_t kmax) {
@@ -479,11 +557,13 @@ __device__ __forceinline__ XyzzL<C> xyzzl_dbl_affine(const Fl<C>& x, const Fl<C>
 }
 
 // acc += (x, y): madd-2008-s (the same formula, hence the same projective
-// representative, as xyzz_madd_inplace); x < p, y < 2p, acc coordinates < 7 p.
+// representative, as xyzz_madd_inplace); x < p normalised, y < 2p with limbs
+// < 2^(B+1) (a negated point arrives unnormalised, sub_nn), acc coordinates < 7 p
+// and normalised.
 template <class C>
 __device__ __forceinline__ void xyzzl_madd(XyzzL<C>& p, const Fl<C>& x, const Fl<C>& y) {
     if (is_inf_l(p)) {
-        p = XyzzL<C>{x, y, fl_const<C>(C::ONE), fl_const<C>(C::ONE)};
+        p = XyzzL<C>{x, norm(y), fl_const<C>(C::ONE), fl_const<C>(C::ONE)};
         return;
     }
     const Fl<C> P = mul_sub<8>(x, p.zz, p.x);    // x ZZ < 1.05p, X < 7p: < 9.05p
@@ -497,10 +577,15 @@ __device__ __forceinline__ void xyzzl_madd(XyzzL<C>& p, const Fl<C>& x, const Fl
     const Fl<C> PPP = mul(P, PP);                // < 1.08p
     p.zzz = mul(p.zzz, PPP);                     // < 1.05p
     const Fl<C> Q = mul(p.x, PP);                // < 1.07p
-    const Fl<C> X3 = sub<5>(sqr(R), add(PPP, add(Q, Q)));  // PPP + 2Q < 3.22p: < 6.49p
+    // X3 = R^2 - (PPP + 2Q), the unnormalised sum folded into R^2's output
+    // columns (PPP + 2Q < 3.22p; limbs < 3 * 2^B): < 1.5p + 5p = 6.5p, normalised
+    const Fl<C> X3 = sqr_subw5(R, add_nn(PPP, add_nn(Q, Q)));
     // Y3 = R (Q - X3) - Y PPP in one reduction: R (Q - X3) + Y (3p - PPP)
-    // (Q - X3 < 9.06p, 3p - PPP < 3p, Y < 7p): < (82.4 + 21) p / 169.28 + p < 1.62p
-    p.y = mul2(R, sub<8>(Q, X3), p.y, sub<3>(Fl<C>{}, PPP));
+    // (Q - X3 < 9.06p, 3p - PPP < 3p, Y < 7p): < (82.4 + 21) p / 169.28 + p < 1.62p.
+    // Q + 8p - X3 stays unnormalised (limbs < 1.5 * 2^(B+1)): its 9 column
+    // products < 2^62.8, plus Y (3p - PPP) and the reduction < 2^61.2 each,
+    // stay below 2^64 (BLS12-381, 14 x 28 bits: < 2^62.2)
+    p.y = mul2(R, sub_nn<8>(Q, X3), p.y, sub<3>(Fl<C>{}, PPP));
     p.x = X3;
 }
 __device__ __forceinline__ void xyzz29_madd(Xyzz29& p, const Fp29& x, const Fp29& y) { xyzzl_madd(p, x, y); }

@@ -197,7 +197,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
             if (skip_inf && qp.is_inf()) continue;
             const Fl<C> x = unpack_l<C>(qp.x);
             Fl<C> y = unpack_l<C>(qp.y);
-            if (cv >> 31) y = sub<2>(Fl<C>{}, y);  // 2p - y
+            if (cv >> 31) y = sub_nn<2>(Fl<C>{}, y);  // 2p - y, limbs < 2^(B+1) (xyzzl_madd takes it)
             xyzzl_madd(acc, x, y);
         }
         range_store(to_std(acc), seg0 == e0, true, q, c, t, head, tail, S);
