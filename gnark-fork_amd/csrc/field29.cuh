@@ -417,6 +417,22 @@ __device__ __forceinline__ Fl<C> sub_nn(const Fl<C>& a, const Fl<C>& b) {
     return r;
 }
 
+// a + 5 p - s, normalised, for s an unnormalised sum of three normalised
+// values (limbs < 3 * 2^B, value < 5 p), against the wide-limb KPW5
+template <class C>
+__device__ __forceinline__ Fl<C> subw5(const Fl<C>& a, const Fl<C>& s) {
+    Fl<C> r;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < C::N - 1; i++) {
+        const uint32_t t = a.l[i] + (C::KPW5[i] - s.l[i]) + c;
+        r.l[i] = t & C::MASK;
+        c = t >> C::B;
+    }
+    r.l[C::N - 1] = a.l[C::N - 1] + (C::KPW5[C::N - 1] - s.l[C::N - 1]) + c;
+    return r;
+}
+
 // carry-propagate limbs < 2^31 (value unchanged)
 template <class C>
 __device__ __forceinline__ Fl<C> norm(const Fl<C>& a) {
@@ -622,16 +638,19 @@ __device__ __forceinline__ bool is_inf2_29(const Xyzz2_29& p) {
     for (int i = 0; i < 9; i++) o |= p.zz.c0.l[i] | p.zz.c1.l[i];
     return o == 0;
 }
-// a b for b1 < (K - 1) p
+// a b for b1 < (K - 1) p (a, b normalised).  Kp - b1 stays unnormalised
+// (limbs < 2^30): a column holds 9 products < 2^59, 9 < 2^58 and 9 reduction
+// products < 2^58: < 2^63.2
 template <int K>
 __device__ __forceinline__ Fp2_29 mul_fp2(const Fp2_29& a, const Fp2_29& b) {
-    const Fp29 nb1 = sub<K>(Fp29{}, b.c1);
+    const Fp29 nb1 = sub_nn<K>(Fp29{}, b.c1);
     return Fp2_29{mul2(a.c0, b.c0, a.c1, nb1), mul2(a.c0, b.c1, a.c1, b.c0)};
 }
-// a^2 = ((a0 + a1)(a0 - a1), 2 a0 a1) for a1 < (K - 1) p
+// a^2 = ((a0 + a1)(a0 - a1), 2 a0 a1) for a1 < (K - 1) p (a normalised); the
+// sums stay unnormalised (limbs < 2^30) against a normalised factor
 template <int K>
 __device__ __forceinline__ Fp2_29 sqr_fp2(const Fp2_29& a) {
-    return Fp2_29{mul(add(a.c0, a.c1), sub<K>(a.c0, a.c1)), mul(a.c0, add(a.c1, a.c1))};
+    return Fp2_29{mul(add_nn(a.c0, a.c1), sub<K>(a.c0, a.c1)), mul(a.c0, add_nn(a.c1, a.c1))};
 }
 __device__ __forceinline__ Fp2 to_std2(const Fp2_29& a) { return Fp2{to_std(a.c0), to_std(a.c1)}; }
 
@@ -665,12 +684,14 @@ __device__ __forceinline__ void xyzz2_29_madd(Xyzz2_29& p, const Fp2_29& x, cons
     }
     // P = x ZZ - X, R = y ZZZ - Y (ZZ1, ZZZ1 < 2p; X < 2p; Y < 2p): < 4.05p
     // (x and y die here on the common path: fewer live registers)
+    // (3p - ZZ1 / ZZZ1 unnormalised, limbs < 2^30: 9 products < 2^59 per column
+    // next to 9 < 2^58, the reduction and the folded subtraction: < 2^63.2)
     auto r_of = [&]() {
-        const Fp29 nzzz1 = sub<3>(Fp29{}, p.zzz.c1);
+        const Fp29 nzzz1 = sub_nn<3>(Fp29{}, p.zzz.c1);
         return Fp2_29{mul2_sub<3>(y.c0, p.zzz.c0, y.c1, nzzz1, p.y.c0),
                       mul2_sub<3>(y.c0, p.zzz.c1, y.c1, p.zzz.c0, p.y.c1)};
     };
-    const Fp29 nzz1 = sub<3>(Fp29{}, p.zz.c1);
+    const Fp29 nzz1 = sub_nn<3>(Fp29{}, p.zz.c1);
     const Fp2_29 P{mul2_sub<3>(x.c0, p.zz.c0, x.c1, nzz1, p.x.c0), mul2_sub<3>(x.c0, p.zz.c1, x.c1, p.zz.c0, p.x.c1)};
     if (is_zero_mod(P.c0, 5) && is_zero_mod(P.c1, 5)) {
         const Fp2_29 R0 = r_of();
@@ -684,9 +705,10 @@ __device__ __forceinline__ void xyzz2_29_madd(Xyzz2_29& p, const Fp2_29& x, cons
     p.zzz = mul_fp2<3>(p.zzz, PPP);             // < 1.03p
     const Fp2_29 Q = mul_fp2<3>(p.x, PP);       // (1.05p, 1.03p)
     const Fp2_29 RR = sqr_fp2<6>(R);            // (1.48p, 1.19p)
-    // X3 = RR - (PPP + 2Q): < 1.48p + 5p, then reduced below 2p
-    const Fp2_29 X3{reduce_small(sub<5>(RR.c0, add(PPP.c0, add(Q.c0, Q.c0)))),
-                    reduce_small(sub<5>(RR.c1, add(PPP.c1, add(Q.c1, Q.c1))))};
+    // X3 = RR - (PPP + 2Q): < 1.48p + 5p (the sum unnormalised, subtracted
+    // against the wide-limb 5p), then reduced below 2p
+    const Fp2_29 X3{reduce_small(subw5(RR.c0, add_nn(PPP.c0, add_nn(Q.c0, Q.c0)))),
+                    reduce_small(subw5(RR.c1, add_nn(PPP.c1, add_nn(Q.c1, Q.c1))))};
     // Y3 = R (Q - X3) - Y PPP, one reduction per component:
     //   c0 = R0 U0 + R1 (6p - U1) + Y0 (3p - PPP0) + Y1 PPP1
     //   c1 = R0 U1 + R1 U0 + Y0 (3p - PPP1) + Y1 (3p - PPP0)      (< 1.3p)
