@@ -598,10 +598,10 @@ __device__ __forceinline__ void xyzzl_madd(XyzzL<C>& p, const Fl<C>& x, const Fl
     const Fl<C> X3 = sqr_subw5(R, add_nn(PPP, add_nn(Q, Q)));
     // Y3 = R (Q - X3) - Y PPP in one reduction: R (Q - X3) + Y (3p - PPP)
     // (Q - X3 < 9.06p, 3p - PPP < 3p, Y < 7p): < (82.4 + 21) p / 169.28 + p < 1.62p.
-    // Q + 8p - X3 stays unnormalised (limbs < 1.5 * 2^(B+1)): its 9 column
-    // products < 2^62.8, plus Y (3p - PPP) and the reduction < 2^61.2 each,
-    // stay below 2^64 (BLS12-381, 14 x 28 bits: < 2^62.2)
-    p.y = mul2(R, sub_nn<8>(Q, X3), p.y, sub<3>(Fl<C>{}, PPP));
+    // Q + 8p - X3 and 3p - PPP stay unnormalised (limbs < 1.5 * 2^(B+1) and
+    // < 2^(B+1)): per column 9 products < 2^62.8 + 9 < 2^62.2 + the reduction
+    // < 2^61.2 = 1.45e19 < 2^64 (BLS12-381, 14 x 28 bits: < 2^62.8)
+    p.y = mul2(R, sub_nn<8>(Q, X3), p.y, sub_nn<3>(Fl<C>{}, PPP));
     p.x = X3;
 }
 __device__ __forceinline__ void xyzz29_madd(Xyzz29& p, const Fp29& x, const Fp29& y) { xyzzl_madd(p, x, y); }
