@@ -248,30 +248,19 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_
     uint32_t* s_entry = sm + 2 * nbins;
     uint32_t* s_key = s_entry + spb * W;
     const int lowbits = (c - 1) - h;
-    // local exclusive scan of this block's histogram (column of hist)
-    __shared__ uint32_t part[256];
-    const int per = (nbins + 255) / 256;
-    uint32_t s = 0;
-    for (int k = 0; k < per; k++) {
-        int j = threadIdx.x * per + k;
-        if (j < nbins) s += hist[(size_t)j * nblocks + tile];
-    }
-    part[threadIdx.x] = s;
-    __syncthreads();
-    for (int off = 1; off < 256; off <<= 1) {
-        uint32_t x = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
-        __syncthreads();
-        part[threadIdx.x] += x;
-        __syncthreads();
-    }
-    uint32_t run = part[threadIdx.x] - s;
-    for (int k = 0; k < per; k++) {
-        int j = threadIdx.x * per + k;
-        if (j < nbins) {
-            lbase[j] = run;
-            lcur[j] = run;
-            run += hist[(size_t)j * nblocks + tile];
-        }
+    // this block's column of the histogram and of the global bin offsets, one bin
+    // per thread (nbins <= 256), both loads in flight together; the local
+    // exclusive scan is a wave scan + one barrier
+    const uint32_t jb = threadIdx.x;
+    const bool has = (int)jb < nbins;
+    const uint32_t cnt = has ? hist[(size_t)jb * nblocks + tile] : 0u;
+    const uint32_t gof = has ? hoff[(size_t)jb * nblocks + tile] : 0u;
+    __shared__ uint32_t wsum[4];
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan256(cnt, wsum, &tot);
+    if (has) {
+        lbase[jb] = ex;
+        lcur[jb] = ex;
     }
     __syncthreads();
     const size_t i0 = (size_t)tile * spb;
@@ -303,11 +292,13 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_
         }
     }
     __syncthreads();
-    const uint32_t tot = part[255];
+    // staged slot q of bin b goes to hoff[b][tile] + (q - lbase[b]): the
+    // difference per bin, from LDS
+    if (has) lbase[jb] = gof - ex;
+    __syncthreads();
     for (uint32_t q = threadIdx.x; q < tot; q += blockDim.x) {
-        uint32_t pk = s_key[q];
-        uint32_t bin = pk >> lowbits;
-        uint32_t pos = hoff[(size_t)bin * nblocks + tile] + (q - lbase[bin]);
+        const uint32_t pk = s_key[q];
+        const uint32_t pos = lbase[pk >> lowbits] + q;
         tmp_entry[pos] = s_entry[q];
         if (tmp_key) tmp_key[pos] = pk;
     }
@@ -531,6 +522,7 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     GG_HIP(hipGetLastError());
     const size_t lds_c = (2 * (size_t)nbins + 2 * (size_t)spb * W) * 4;
     GG_CHECK(lds_c <= 160 * 1024, GG_ERR_INTERNAL, "bin scatter LDS tile too large");
+    GG_CHECK(nbins <= 256, GG_ERR_INTERNAL, "bin scatter: one bin per thread");
     // scatter stage j (0 = bin scatter) writes entries to `sorted` when the number
     // of stages after it is even, else tmp_entry; keys to tmp_key (j even) / keys (j odd)
     const int S = 1 + (int)rs.size();
