@@ -26,6 +26,7 @@ import argparse
 import datetime
 import json
 import os
+import re
 import sys
 import time
 
@@ -526,12 +527,18 @@ def msm_bench(log_n, rank, world, dist, xdev, barrier, max_over_ranks, steps=20,
     return res
 
 
+def _profile_order(path):
+    """(round, version) of a profiles/rNN_vMM_* file, so r02_v13 sorts after r02_v9."""
+    m = re.match(r"r(\d+)_v(\d+)_", os.path.basename(path))
+    return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
+
+
 def pmc_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from a committed PMC profile of the same
     workload (two separate rocprofv3 --pmc passes, FETCH_SIZE x2 per the gfx950
     correction + WRITE_SIZE; tools/pmc_traffic.py).  None if no matching profile."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")), key=_profile_order, reverse=True):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
@@ -560,7 +567,7 @@ def pmc_sq(kernel, workload):
     """SQ_INSTS_VALU / SQ_WAVES per launch of `kernel` from a committed SQ-counter
     profile of the same workload (tools/pmc_counters.py); None if absent."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_sq*.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_sq*.json")), key=_profile_order, reverse=True):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
