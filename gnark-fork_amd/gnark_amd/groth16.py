@@ -51,6 +51,7 @@ class ProvingKeyData:
     domain_mul_gen: Optional[bytes] = None          # pk.Domain.FrMultiplicativeGen
     k_wire_index: Optional[Sequence[int]] = None    # filterHeap result; None = nb_public + i
     curve: str = "bn254"                            # or "bls12-381"
+    commitment_keys: Optional[Sequence] = None      # pk.CommitmentKeys (pedersen.ProvingKey), BN254
 
     @property
     def n_wires(self):
@@ -71,16 +72,20 @@ class Solution:
 
 @dataclasses.dataclass
 class Proof:
-    """groth16_bn254.Proof (prove.go:45-50): affine points, gnark memory layout."""
+    """groth16_bn254.Proof (prove.go:45-50): affine points, gnark memory layout;
+    Commitments / CommitmentPok are set by BSB22 circuits (pedersen.Bsb22Hints)."""
     Ar: bytes
     Bs: bytes
     Krs: bytes
+    Commitments: Sequence[bytes] = ()
+    CommitmentPok: bytes = bytes(64)
 
     def write_raw(self) -> bytes:
-        """WriteRawTo (marshal.go:41-66): Ar | Bs | Krs | Commitments | CommitmentPok,
-        uncompressed; no commitments -> u32 length 0 and an infinity PoK [ext enc]."""
+        """WriteRawTo (marshal.go:41-66): Ar | Bs | Krs | u32 len(Commitments) |
+        Commitments | CommitmentPok, uncompressed (infinity PoK without commitments)."""
         return (fr.g1_raw(self.Ar) + fr.g2_raw(self.Bs) + fr.g1_raw(self.Krs)
-                + struct.pack(">I", 0) + fr.g1_raw(bytes(64)))
+                + struct.pack(">I", len(self.Commitments)) + b"".join(fr.g1_raw(c) for c in self.Commitments)
+                + fr.g1_raw(self.CommitmentPok))
 
 
 BASE_A, BASE_B1, BASE_K, BASE_Z, BASE_B2 = range(5)
@@ -119,6 +124,13 @@ class ProvingKey:
         self.handle = h
         self.n_wires = n_wires
         self.log_n = data.log_n
+        # pk.CommitmentKeys: both Pedersen bases resident next to the key
+        self.commitment_keys = []
+        if data.commitment_keys:
+            if data.curve != "bn254":
+                raise ValueError("BSB22 commitment keys: BN254 only")
+            from . import pedersen
+            self.commitment_keys = [pedersen.DevicePedersenKey(k) for k in data.commitment_keys]
 
     def base_info(self, which: int):
         """(resident points, window bits, windows) of MSM base `which` (BASE_*)."""
@@ -128,6 +140,9 @@ class ProvingKey:
         return n.value, c.value, w.value
 
     def close(self):
+        for k in getattr(self, "commitment_keys", ()):
+            k.close()
+        self.commitment_keys = []
         if self.handle:
             lib.gg_groth16_pk_release(self.handle)
             self.handle = None
@@ -211,12 +226,21 @@ def _rand_fr_mont() -> bytes:
 
 
 def prove(pk: ProvingKey, solution: Solution, *opts, r: bytes = None, s: bytes = None,
-          h_out=None) -> Proof:
-    """icicle_bn254.Prove after Solve (icicle.go:198-422)."""
+          h_out=None, bsb22=None) -> Proof:
+    """icicle_bn254.Prove after Solve (icicle.go:198-422).  BSB22 circuits pass
+    the solved hints (pedersen.Bsb22Hints): their commitments go into the proof
+    and the proof of knowledge is pedersen.BatchProve on the resident bases
+    (prove.go:128-136); the key's K points must then exclude the committed and
+    commitment wires (k_wire_index = pedersen.k_wire_index(...), prove.go:238-248)."""
     cfg = backend.new_prover_config(*opts)
     if not backend.accelerated(cfg):
         raise RuntimeError("accelerated prover requested without with_amd_acceleration(); "
                            "the CPU prover is gnark's groth16_bn254.Prove (prove.go:63)")
+    ncom = len(getattr(pk, "commitment_keys", ()))
+    if ncom and (bsb22 is None or len(bsb22.keys) != ncom):
+        raise ValueError("key has %d commitment keys: pass the solved pedersen.Bsb22Hints" % ncom)
+    if bsb22 is not None and not ncom and bsb22.keys:
+        raise ValueError("BSB22 hints for a key without commitment keys")
     rnd = _rand_fr_mont if getattr(pk, "curve", "bn254") == "bn254" else \
         (lambda: fr.bls_fr_mont(secrets.randbelow(fr.BLS_R)))
     r = r if r is not None else rnd()
@@ -227,6 +251,8 @@ def prove(pk: ProvingKey, solution: Solution, *opts, r: bytes = None, s: bytes =
                                ptr(solution.B), ptr(solution.C), solution.n_constraints,
                                int(solution.on_device), ptr(r), ptr(s), ptr(ar), ptr(bs),
                                ptr(krs), ptr(h_out)))
+    if ncom:
+        return Proof(bytes(ar), bytes(bs), bytes(krs), list(bsb22.commitments), bsb22.pok())
     return Proof(bytes(ar), bytes(bs), bytes(krs))
 
 
