@@ -55,6 +55,21 @@ def test_bsb22_host_logic_matches_oracle():
         "68a985b87eb6b46952128911f2a4412bbc302a9d759667f87f7a21d803f07235"
 
 
+def test_bsb22_host_errors():
+    from gnark_amd import pedersen
+    with pytest.raises(ValueError):
+        pedersen.batch_prove([], [[1]], b"")
+    with pytest.raises(ValueError):
+        pedersen.ProvingKey(bytes(64), bytes(128)).n and pedersen.DevicePedersenKey(
+            pedersen.ProvingKey(bytes(64), bytes(128)))
+    h = pedersen.Bsb22Hints([])
+    assert h.complete() and h.pok() == bytes(64)
+    h2 = pedersen.Bsb22Hints([None])  # a key whose hint never ran
+    with pytest.raises(RuntimeError):
+        h2.pok()
+    assert pedersen.k_wire_index(2, 6, [[3]], [5]) == [2, 4]
+
+
 # ---------------------------------------------------------------- GPU
 def _pk_data(rcs, pk, cinfo):
     from gnark_amd import groth16, pedersen
