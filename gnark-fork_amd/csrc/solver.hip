@@ -1,0 +1,323 @@
+// R1CS solver on the GPU: constraint/bn254/solver.go:418-608
+// (run + solveR1C) for BN254 R1CS without hint calls.
+//
+// The system is handed over once in CSR form -- exactly what gnark's public
+// R1CS API yields (r1cs.GetR1Cs() terms, r1cs.Coefficients, r1cs.Levels):
+//   term_off[3 c + s] .. term_off[3 c + s + 1]   terms of side s (L, R, O) of c
+//   term_wire[t], term_coeff[t]                   wire id and coefficient index
+//   coeffs                                        fr table (Montgomery)
+//   level_off / level_cons                        r1cs.Levels flattened
+// A solve runs one launch per level (constraints of a level are independent,
+// solver.go:421-428), a thread per constraint:
+//   a, b, c = sum of the solved terms of L, R, O (accumulateInto);
+//   at most one unsolved term: its wire gets (c / b - a), (c / a - b) or
+//   (a b - c), divided by its coefficient (divByCoeff), and the term joins its
+//   side's sum; no unsolved term: a b == c is checked (solver.go:553-571);
+//   a zero divisor leaves the wire at 0 after the same check (solver.go:582-601).
+// Outputs W (wires) and A, B, C (per-constraint L.w, R.w, O.w: R1CSSolution,
+// system.go:269-272) stay in HBM for gg_groth16_prove (inputs_on_device = 1).
+// The level loop is captured once into a HIP graph per handle (256+ tiny
+// launches per solve otherwise).
+#include "common.h"
+#include "field.cuh"
+#include <algorithm>
+#include <mutex>
+#include <vector>
+
+namespace gg {
+
+struct R1csDev {
+    const uint32_t* off;
+    const uint32_t* wire;
+    const uint32_t* cidx;
+    const Fr* coef;
+    const Fr* coef_inv;
+    uint32_t ncoef;
+    Fr* W;
+    Fr* A;
+    Fr* B;
+    Fr* C;
+    uint8_t* solved;
+    uint32_t* fail;  // [0] = first unsatisfied constraint, [1] = first malformed one
+};
+
+__device__ __forceinline__ Fr ldfr(const Fr* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    uint4 a = q[0], b = q[1];
+    Fr r;
+    r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+    r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+    return r;
+}
+__device__ __forceinline__ void stfr(Fr* p, const Fr& r) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    q[0] = make_uint4(r.v[0], r.v[1], r.v[2], r.v[3]);
+    q[1] = make_uint4(r.v[4], r.v[5], r.v[6], r.v[7]);
+}
+
+__global__ void __launch_bounds__(256) k_solve_level(R1csDev d, const uint32_t* cons, uint32_t count) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint32_t c = cons[i];
+    Fr acc[3] = {Fr::zero(), Fr::zero(), Fr::zero()};
+    int loc = -1;
+    uint32_t ut = 0;
+    bool malformed = false;
+    for (int s = 0; s < 3; s++) {
+        const uint32_t t0 = d.off[3 * c + s], t1 = d.off[3 * c + s + 1];
+        for (uint32_t t = t0; t < t1; t++) {
+            const uint32_t w = d.wire[t];
+            if (d.solved[w]) {
+                acc[s] = acc[s] + ldfr(d.coef + d.cidx[t]) * ldfr(d.W + w);
+                continue;
+            }
+            if (loc >= 0) malformed = true;  // "found more than one wire to instantiate"
+            loc = s;
+            ut = t;
+        }
+    }
+    bool ok = true;
+    if (malformed) {
+        atomicMin(d.fail + 1, c);
+        ok = false;
+    } else if (loc < 0) {
+        ok = acc[0] * acc[1] == acc[2];
+    } else {
+        Fr v = Fr::zero();
+        const Fr a = acc[0], b = acc[1], cc = acc[2];
+        if (loc == 0) {
+            if (!b.is_zero()) { v = cc * inverse(b) - a; acc[0] = a + v; }
+            else ok = a * b == cc;
+        } else if (loc == 1) {
+            if (!a.is_zero()) { v = cc * inverse(a) - b; acc[1] = b + v; }
+            else ok = a * b == cc;
+        } else {
+            v = a * b - cc;
+            acc[2] = cc + v;
+        }
+        const uint32_t k = d.cidx[ut];
+        const Fr kinv = ldfr(d.coef_inv + k);
+        if (kinv.is_zero()) {  // zero coefficient on the unknown: no division possible
+            atomicMin(d.fail + 1, c);
+            ok = false;
+        }
+        const uint32_t w = d.wire[ut];
+        stfr(d.W + w, v * kinv);
+        d.solved[w] = 1;
+    }
+    if (!ok) atomicMin(d.fail, c);
+    stfr(d.A + c, acc[0]);
+    stfr(d.B + c, acc[1]);
+    stfr(d.C + c, acc[2]);
+}
+
+__global__ void k_solver_init(Fr* W, uint8_t* solved, size_t nw, const Fr* inputs, size_t n_in, uint32_t* fail) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        fail[0] = 0xffffffffu;
+        fail[1] = 0xffffffffu;
+    }
+    if (i >= nw) return;
+    if (i == 0) stfr(W, Fr::one());  // ONE_WIRE (solver.go:103-105)
+    else if (i <= n_in) stfr(W + i, ldfr(inputs + (i - 1)));
+    else stfr(W + i, Fr::zero());
+    solved[i] = i <= n_in ? 1 : 0;
+}
+
+// number of unsolved wires (solver.go:530-532)
+__global__ void k_count_unsolved(const uint8_t* solved, size_t nw, unsigned long long* cnt) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool u = i < nw && !solved[i];
+    const unsigned long long b = __ballot(u);
+    if (u && (threadIdx.x & 63) == (uint32_t)(__ffsll(b) - 1)) atomicAdd(cnt, (unsigned long long)__popcll(b));
+}
+
+}  // namespace gg
+
+using namespace gg;
+
+struct gg_r1cs {
+    int device = 0;
+    size_t nw = 0, ncons = 0, nterms = 0, ncoef = 0;
+    std::vector<uint32_t> level_off;  // host copy (launch sizes)
+    DevBuf off, wire, cidx, coef, coef_inv, level_cons, W, A, B, C, solved, fail, inputs, cnt;
+    hipStream_t st = nullptr;
+    hipGraphExec_t graph = nullptr;
+    std::mutex mu;
+    ~gg_r1cs() {
+        if (graph) (void)hipGraphExecDestroy(graph);
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+
+extern "C" int gg_r1cs_create(size_t n_wires, size_t n_constraints, const uint32_t* term_off,
+                              const uint32_t* term_wire, const uint32_t* term_coeff, const void* coeffs,
+                              size_t n_coeffs, const uint32_t* level_off, const uint32_t* level_cons,
+                              size_t n_levels, gg_r1cs_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out && term_off && coeffs && level_off, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(n_wires >= 1 && n_wires < 0xffffffffu && n_constraints < 0xffffffffu, GG_ERR_INVALID_ARG,
+             "wire / constraint count out of range");
+    GG_CHECK(n_coeffs >= 1 && n_coeffs < 0xffffffffu, GG_ERR_INVALID_ARG, "empty coefficient table");
+    const size_t nterms = term_off[3 * n_constraints];
+    GG_CHECK(term_off[0] == 0, GG_ERR_INVALID_ARG, "term_off[0] must be 0");
+    for (size_t i = 0; i < 3 * n_constraints; i++)
+        GG_CHECK(term_off[i] <= term_off[i + 1], GG_ERR_INVALID_ARG, "term_off not monotonic");
+    GG_CHECK(nterms == 0 || (term_wire && term_coeff), GG_ERR_INVALID_ARG, "null term arrays");
+    for (size_t t = 0; t < nterms; t++) {
+        GG_CHECK(term_wire[t] < n_wires, GG_ERR_INVALID_ARG, "term wire id out of range");
+        GG_CHECK(term_coeff[t] < n_coeffs, GG_ERR_INVALID_ARG, "term coefficient id out of range");
+    }
+    // r1cs.Levels: every constraint exactly once
+    GG_CHECK(level_off[0] == 0 && level_off[n_levels] == n_constraints, GG_ERR_INVALID_ARG,
+             "levels must cover every constraint once");
+    GG_CHECK(n_constraints == 0 || level_cons, GG_ERR_INVALID_ARG, "null level_cons");
+    std::vector<uint8_t> seen(n_constraints, 0);
+    for (size_t l = 0; l < n_levels; l++) {
+        GG_CHECK(level_off[l] <= level_off[l + 1], GG_ERR_INVALID_ARG, "level_off not monotonic");
+        for (uint32_t i = level_off[l]; i < level_off[l + 1]; i++) {
+            const uint32_t c = level_cons[i];
+            GG_CHECK(c < n_constraints && !seen[c], GG_ERR_INVALID_ARG,
+                     "levels must cover every constraint once");
+            seen[c] = 1;
+        }
+    }
+    // divByCoeff: host inverses of the coefficient table (0 for a zero coefficient)
+    const Fr* cf = (const Fr*)coeffs;
+    std::vector<Fr> inv(n_coeffs);
+    for (size_t i = 0; i < n_coeffs; i++) inv[i] = cf[i].is_zero() ? Fr::zero() : inverse(cf[i]);
+    auto* r = new gg_r1cs();
+    try {
+        GG_HIP(hipGetDevice(&r->device));
+        r->nw = n_wires;
+        r->ncons = n_constraints;
+        r->nterms = nterms;
+        r->ncoef = n_coeffs;
+        r->level_off.assign(level_off, level_off + n_levels + 1);
+        auto up = [](DevBuf& b, const void* src, size_t bytes) {
+            b.alloc(std::max<size_t>(bytes, 16));
+            if (bytes) GG_HIP(hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+        };
+        up(r->off, term_off, (3 * n_constraints + 1) * 4);
+        up(r->wire, term_wire, nterms * 4);
+        up(r->cidx, term_coeff, nterms * 4);
+        up(r->coef, coeffs, n_coeffs * 32);
+        up(r->coef_inv, inv.data(), n_coeffs * 32);
+        up(r->level_cons, level_cons, n_constraints * 4);
+        r->W.alloc(n_wires * 32);
+        r->A.alloc(std::max<size_t>(n_constraints, 1) * 32);
+        r->B.alloc(std::max<size_t>(n_constraints, 1) * 32);
+        r->C.alloc(std::max<size_t>(n_constraints, 1) * 32);
+        r->solved.alloc(n_wires);
+        r->fail.alloc(16);
+        r->cnt.alloc(16);
+        GG_HIP(hipStreamCreateWithFlags(&r->st, hipStreamNonBlocking));
+    } catch (...) {
+        delete r;
+        throw;
+    }
+    *out = r;
+    GG_CAPI_END
+}
+
+extern "C" int gg_r1cs_release(gg_r1cs_t r) {
+    delete r;
+    return GG_OK;
+}
+
+extern "C" int gg_r1cs_info(gg_r1cs_t r, size_t* n_wires, size_t* n_constraints, size_t* n_levels) {
+    GG_CAPI_BEGIN
+    GG_CHECK(r, GG_ERR_INVALID_ARG, "null handle");
+    if (n_wires) *n_wires = r->nw;
+    if (n_constraints) *n_constraints = r->ncons;
+    if (n_levels) *n_levels = r->level_off.size() - 1;
+    GG_CAPI_END
+}
+
+// the per-level launches, enqueued on r->st (recorded once into a graph)
+static void enqueue_levels(gg_r1cs* r) {
+    R1csDev d{r->off.as<uint32_t>(), r->wire.as<uint32_t>(), r->cidx.as<uint32_t>(), r->coef.as<Fr>(),
+              r->coef_inv.as<Fr>(), (uint32_t)r->ncoef, r->W.as<Fr>(), r->A.as<Fr>(), r->B.as<Fr>(),
+              r->C.as<Fr>(), r->solved.as<uint8_t>(), r->fail.as<uint32_t>()};
+    const uint32_t* lc = r->level_cons.as<uint32_t>();
+    for (size_t l = 0; l + 1 < r->level_off.size(); l++) {
+        const uint32_t a = r->level_off[l], cnt = r->level_off[l + 1] - a;
+        if (!cnt) continue;
+        hipLaunchKernelGGL(k_solve_level, dim3(grid_for(cnt, 256)), dim3(256), 0, r->st, d, lc + a, cnt);
+        GG_HIP(hipGetLastError());
+    }
+}
+
+extern "C" int gg_r1cs_solve(gg_r1cs_t r, const void* witness, size_t n_witness, int witness_on_device,
+                             void* w_out, void* a_out, void* b_out, void* c_out, int out_on_device,
+                             int64_t* unsatisfied) {
+    GG_CAPI_BEGIN
+    GG_CHECK(r, GG_ERR_INVALID_ARG, "null handle");
+    GG_CHECK(n_witness + 1 <= r->nw, GG_ERR_INVALID_ARG, "witness longer than the wire vector");
+    GG_CHECK(n_witness == 0 || witness, GG_ERR_INVALID_ARG, "null witness");
+    std::lock_guard<std::mutex> lk(r->mu);
+    GG_HIP(hipSetDevice(r->device));
+    if (unsatisfied) *unsatisfied = -1;
+    const Fr* in = (const Fr*)witness;
+    if (n_witness && !witness_on_device) {
+        r->inputs.reserve(n_witness * 32);
+        GG_HIP(hipMemcpyAsync(r->inputs.p, witness, n_witness * 32, hipMemcpyHostToDevice, r->st));
+        in = r->inputs.as<Fr>();
+    }
+    hipLaunchKernelGGL(k_solver_init, dim3(grid_for(r->nw, 256)), dim3(256), 0, r->st, r->W.as<Fr>(),
+                       r->solved.as<uint8_t>(), r->nw, in, n_witness, r->fail.as<uint32_t>());
+    GG_HIP(hipGetLastError());
+    // the level launches: captured once into a graph, replayed afterwards
+    if (!r->graph) {
+        hipGraph_t g;
+        GG_HIP(hipStreamBeginCapture(r->st, hipStreamCaptureModeThreadLocal));
+        try {
+            enqueue_levels(r);
+        } catch (...) {
+            (void)hipStreamEndCapture(r->st, &g);
+            throw;
+        }
+        GG_HIP(hipStreamEndCapture(r->st, &g));
+        hipError_t e = hipGraphInstantiate(&r->graph, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        GG_HIP(e);
+    }
+    GG_HIP(hipGraphLaunch(r->graph, r->st));
+    GG_HIP(hipMemsetAsync(r->cnt.p, 0, 8, r->st));
+    hipLaunchKernelGGL(k_count_unsolved, dim3(grid_for(r->nw, 256)), dim3(256), 0, r->st,
+                       r->solved.as<uint8_t>(), r->nw, r->cnt.as<unsigned long long>());
+    GG_HIP(hipGetLastError());
+    uint32_t fail[2];
+    unsigned long long unsolved = 0;
+    GG_HIP(hipMemcpyAsync(fail, r->fail.p, 8, hipMemcpyDeviceToHost, r->st));
+    GG_HIP(hipMemcpyAsync(&unsolved, r->cnt.p, 8, hipMemcpyDeviceToHost, r->st));
+    GG_HIP(hipStreamSynchronize(r->st));
+    GG_CHECK(fail[1] == 0xffffffffu, GG_ERR_INVALID_ARG,
+             "constraint #" + std::to_string(fail[1]) +
+                 ": more than one unsolved wire at its level, or a zero coefficient on the unknown "
+                 "(the levels do not match the system)");
+    if (fail[0] != 0xffffffffu) {
+        if (unsatisfied) *unsatisfied = fail[0];
+        throw Error(GG_ERR_UNSATISFIED, "constraint #" + std::to_string(fail[0]) + " is not satisfied");
+    }
+    GG_CHECK(unsolved == 0, GG_ERR_UNSATISFIED,
+             "solver didn't assign a value to all wires (" + std::to_string(unsolved) + " left)");
+    const hipMemcpyKind k = out_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    if (w_out) GG_HIP(hipMemcpyAsync(w_out, r->W.p, r->nw * 32, k, r->st));
+    if (a_out && r->ncons) GG_HIP(hipMemcpyAsync(a_out, r->A.p, r->ncons * 32, k, r->st));
+    if (b_out && r->ncons) GG_HIP(hipMemcpyAsync(b_out, r->B.p, r->ncons * 32, k, r->st));
+    if (c_out && r->ncons) GG_HIP(hipMemcpyAsync(c_out, r->C.p, r->ncons * 32, k, r->st));
+    GG_HIP(hipStreamSynchronize(r->st));
+    GG_CAPI_END
+}
+
+// device pointers of the resident solution (valid until the next solve / release)
+extern "C" int gg_r1cs_solution_dev(gg_r1cs_t r, void** w, void** a, void** b, void** c) {
+    GG_CAPI_BEGIN
+    GG_CHECK(r, GG_ERR_INVALID_ARG, "null handle");
+    if (w) *w = r->W.p;
+    if (a) *a = r->A.p;
+    if (b) *b = r->B.p;
+    if (c) *c = r->C.p;
+    GG_CAPI_END
+}

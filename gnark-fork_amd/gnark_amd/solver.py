@@ -1,0 +1,148 @@
+"""R1CS solver on MI355X: mirror of cs.R1CS's Solve for BN254 circuits without
+hint calls (constraint/bn254/solver.go:418-608, system.go:64-104), the system
+resident in HBM and the solution left there for the prover.
+
+    sys = R1CS.from_terms(nb_public, nb_secret, n_wires, constraints)   # once
+    sol = sys.solve(witness_values)            # -> groth16.Solution (on device)
+    proof = groth16.prove(pk, sol, with_amd_acceleration())
+
+``constraints`` are (L, R, O) lists of (wire, coefficient) pairs, the terms
+r1cs.GetR1Cs() yields; the coefficient table and the CSR arrays are built here
+(r1cs.Coefficients), and the levels are r1cs.Levels as gnark's level builder
+assigns them (constraint/blueprint_r1cs.go:61-96: an R1C sits one level above
+the deepest internal wire it reads and places its unsolved wires there)."""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import fr
+from ._lib import check, lib, ptr, DeviceBuffer
+
+GG_ERR_UNSATISFIED = 6
+
+
+class UnsatisfiedConstraintError(RuntimeError):
+    """solver.UnsatisfiedConstraintError (solver.go:610-623)."""
+
+    def __init__(self, cid: int, msg: str):
+        super().__init__(msg)
+        self.cid = cid
+
+
+def compute_levels(nb_inputs: int, n_wires: int, term_off, term_wire) -> list:
+    """r1cs.Levels from the CSR terms (blueprint_r1cs.go:61-96, core.go:405-419):
+    wires < nb_inputs are inputs (not in the instruction tree)."""
+    level = np.full(n_wires, -1, dtype=np.int64)
+    ncons = (len(term_off) - 1) // 3
+    out = []
+    for c in range(ncons):
+        lo, hi = int(term_off[3 * c]), int(term_off[3 * c + 3])
+        mx, outs = -1, []
+        for w in term_wire[lo:hi]:
+            w = int(w)
+            if w < nb_inputs:
+                continue
+            if level[w] < 0:
+                outs.append(w)
+            elif level[w] > mx:
+                mx = int(level[w])
+        mx += 1
+        for w in outs:
+            level[w] = mx
+        while len(out) <= mx:
+            out.append([])
+        out[mx].append(c)
+    return out
+
+
+class R1CS:
+    """Device-resident R1CS (gg_r1cs_create) with its solver."""
+
+    def __init__(self, nb_public: int, nb_secret: int, n_wires: int, term_off, term_wire, term_coeff,
+                 coeffs: Sequence[int], levels: Optional[Sequence[Sequence[int]]] = None):
+        self.nb_public, self.nb_secret, self.n_wires = nb_public, nb_secret, n_wires
+        self.term_off = np.ascontiguousarray(term_off, dtype=np.uint32)
+        self.term_wire = np.ascontiguousarray(term_wire, dtype=np.uint32)
+        self.term_coeff = np.ascontiguousarray(term_coeff, dtype=np.uint32)
+        self.n_constraints = (len(self.term_off) - 1) // 3
+        if levels is None:
+            levels = compute_levels(nb_public + nb_secret, n_wires, self.term_off, self.term_wire)
+        self.levels = levels
+        lo = np.zeros(len(levels) + 1, dtype=np.uint32)
+        lo[1:] = np.cumsum([len(x) for x in levels])
+        lc = np.ascontiguousarray(np.concatenate([np.asarray(x, dtype=np.uint32) for x in levels])
+                                  if levels else np.zeros(0, dtype=np.uint32), dtype=np.uint32)
+        cbytes = b"".join(fr.fr_mont(int(k) % fr.R) for k in coeffs)
+        h = ctypes.c_void_p()
+        check(lib.gg_r1cs_create(n_wires, self.n_constraints, ptr(self.term_off), ptr(self.term_wire),
+                                 ptr(self.term_coeff), ptr(cbytes), len(coeffs), ptr(lo), ptr(lc),
+                                 len(levels), ctypes.byref(h)))
+        self.handle = h
+
+    @classmethod
+    def from_terms(cls, nb_public: int, nb_secret: int, n_wires: int, constraints, levels=None) -> "R1CS":
+        """constraints: [(L, R, O)] with L = [(wire, coeff int), ...]."""
+        table, index = [], {}
+        off, wires, cids = [0], [], []
+        for L, R, O in constraints:
+            for side in (L, R, O):
+                for w, k in side:
+                    k %= fr.R
+                    if k not in index:
+                        index[k] = len(table)
+                        table.append(k)
+                    wires.append(w)
+                    cids.append(index[k])
+                off.append(len(wires))
+        if not table:
+            table = [1]
+        return cls(nb_public, nb_secret, n_wires, off, wires, cids, table, levels)
+
+    def info(self):
+        a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        check(lib.gg_r1cs_info(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+    def solve(self, witness, on_device: bool = True):
+        """r1cs.Solve(fullWitness): witness = public (without ONE_WIRE) then
+        secret values (ints, or Montgomery bytes / a DeviceBuffer).  Returns a
+        groth16.Solution whose W, A, B, C live in HBM (on_device) or on the host."""
+        from .groth16 import Solution
+        n_in = self.nb_public - 1 + self.nb_secret
+        wdev = False
+        if isinstance(witness, DeviceBuffer):
+            wbuf, wdev = witness, True
+        elif isinstance(witness, (bytes, bytearray)):
+            wbuf = bytes(witness)
+        else:
+            wbuf = b"".join(fr.fr_mont(int(v) % fr.R) for v in witness)
+            if len(witness) != n_in:
+                raise ValueError("invalid witness size, got %d, expected %d" % (len(witness), n_in))
+        if not wdev and len(wbuf) != 32 * n_in:
+            raise ValueError("invalid witness size, got %d bytes, expected %d" % (len(wbuf), 32 * n_in))
+        nw, nc = self.n_wires, self.n_constraints
+        if on_device:
+            W, A, B, C = (DeviceBuffer(max(32 * k, 32)) for k in (nw, nc, nc, nc))
+        else:
+            W, A, B, C = (bytearray(32 * k) for k in (nw, nc, nc, nc))
+        bad = ctypes.c_int64(-1)
+        rc = lib.gg_r1cs_solve(self.handle, ptr(wbuf), n_in, int(wdev), ptr(W), ptr(A), ptr(B), ptr(C),
+                               int(on_device), ctypes.byref(bad))
+        if rc == GG_ERR_UNSATISFIED:
+            raise UnsatisfiedConstraintError(bad.value, lib.gg_last_error().decode())
+        check(rc)
+        return Solution(W, A, B, C, nw, nc, on_device=on_device)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib.gg_r1cs_release(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

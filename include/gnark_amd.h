@@ -35,6 +35,7 @@ extern "C" {
 #define GG_ERR_OOM 3
 #define GG_ERR_UNSUPPORTED 4
 #define GG_ERR_INTERNAL 5
+#define GG_ERR_UNSATISFIED 6 /* R1CS solver: a constraint is not satisfied */
 
 #define GG_G1 1
 #define GG_G2 2
@@ -476,6 +477,34 @@ int gg_plonk_last_timings(double *ms, int cap);
 int gg_fr_from_canonical_be(int curve, const void *in_dev, void *out_dev, size_t n,
                             uint64_t *n_invalid, void *hip_stream);
 int gg_fr_to_canonical_be(int curve, const void *in_dev, void *out_dev, size_t n, void *hip_stream);
+
+/* ---- R1CS solver (constraint/bn254/solver.go:418-608, R1CS without hints)
+ * replaces r1cs.Solve(fullWitness) -> R1CSSolution{W, A, B, C} (prove.go:119-126,
+ * system.go:64-104) on the GPU, leaving the solution in HBM for gg_groth16_prove
+ * (inputs_on_device = 1).  The system in CSR form, as gnark's public API gives it:
+ *   term_off[3 c + s] .. term_off[3 c + s + 1]: terms of side s (0 L, 1 R, 2 O) of
+ *     constraint c (r1cs.GetR1Cs()); term_wire / term_coeff: wire id and index
+ *     into coeffs (r1cs.Coefficients, fr Montgomery);
+ *   level_off[l] .. level_off[l + 1]: the constraints of level l (r1cs.Levels).
+ * gg_r1cs_solve: witness = public (without ONE_WIRE) then secret values, fr
+ *   Montgomery (witness.Vector(), solver.go:65-114); W (n_wires) and A, B, C
+ *   (n_constraints) copied to the caller's buffers when non-null (host or device
+ *   per out_on_device).  GG_ERR_UNSATISFIED: *unsatisfied = the first failing
+ *   constraint (-1 when every constraint holds but wires were left unsolved).
+ *   Circuits with hint calls solve on the host (gnark's solver). BN254 only. */
+typedef struct gg_r1cs *gg_r1cs_t;
+int gg_r1cs_create(size_t n_wires, size_t n_constraints, const uint32_t *term_off,
+                   const uint32_t *term_wire, const uint32_t *term_coeff, const void *coeffs,
+                   size_t n_coeffs, const uint32_t *level_off, const uint32_t *level_cons,
+                   size_t n_levels, gg_r1cs_t *out);
+int gg_r1cs_release(gg_r1cs_t r);
+int gg_r1cs_info(gg_r1cs_t r, size_t *n_wires, size_t *n_constraints, size_t *n_levels);
+int gg_r1cs_solve(gg_r1cs_t r, const void *witness, size_t n_witness, int witness_on_device,
+                  void *w_out, void *a_out, void *b_out, void *c_out, int out_on_device,
+                  int64_t *unsatisfied);
+/* device pointers of the handle's resident W, A, B, C (valid until the next
+ * solve or the release): a prove can read them without a copy */
+int gg_r1cs_solution_dev(gg_r1cs_t r, void **w, void **a, void **b, void **c);
 
 /* ------------------------------------------------------------ profiling
  * Kernel-level timing with HIP events recorded on the stream each kernel is
