@@ -136,6 +136,23 @@ class R1CS:
         check(rc)
         return Solution(W, A, B, C, nw, nc, on_device=on_device)
 
+    def solve_resident(self, witness: bytes):
+        """solve() without copies: the returned Solution points at the handle's own
+        HBM buffers (valid until the next solve or close) -- the shape a prover
+        pipeline uses (witness in, proof out, the solution never leaves HBM)."""
+        from .groth16 import Solution
+        n_in = self.nb_public - 1 + self.nb_secret
+        if len(witness) != 32 * n_in:
+            raise ValueError("invalid witness size, got %d bytes, expected %d" % (len(witness), 32 * n_in))
+        bad = ctypes.c_int64(-1)
+        rc = lib.gg_r1cs_solve(self.handle, ptr(witness), n_in, 0, None, None, None, None, 1, ctypes.byref(bad))
+        if rc == GG_ERR_UNSATISFIED:
+            raise UnsatisfiedConstraintError(bad.value, lib.gg_last_error().decode())
+        check(rc)
+        p = [ctypes.c_void_p() for _ in range(4)]
+        check(lib.gg_r1cs_solution_dev(self.handle, *(ctypes.byref(x) for x in p)))
+        return Solution(p[0], p[1], p[2], p[3], self.n_wires, self.n_constraints, on_device=True)
+
     def close(self):
         if getattr(self, "handle", None):
             lib.gg_r1cs_release(self.handle)
