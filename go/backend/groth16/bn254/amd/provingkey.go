@@ -20,8 +20,10 @@ import (
 // several devices are configured, one gg_groth16_mpk_t (a shard per GPU, the
 // distributed computeH's exchanges done inside the library).
 type deviceInfo struct {
-	handle unsafe.Pointer
-	multi  bool
+	handle      unsafe.Pointer
+	multi       bool
+	solver      *deviceSolver // GPU r1cs.Solve (nil: the system has hints)
+	solverTried bool
 }
 
 var (
