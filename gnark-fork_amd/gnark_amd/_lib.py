@@ -127,6 +127,11 @@ def _load():
         "gg_r1cs_info": ([P, ctypes.POINTER(S), ctypes.POINTER(S), ctypes.POINTER(S)], I),
         "gg_r1cs_solve": ([P, P, S, I, P, P, P, P, I, ctypes.POINTER(ctypes.c_int64)], I),
         "gg_r1cs_solution_dev": ([P, PP, PP, PP, PP], I),
+        "gg_scs_create": ([I, S, S, S, P, P, P, P, S, P, P, S, PP], I),
+        "gg_scs_release": ([P], I),
+        "gg_scs_info": ([P, ctypes.POINTER(S), ctypes.POINTER(S), ctypes.POINTER(S)], I),
+        "gg_scs_solve": ([P, P, S, I, P, P, P, P, I, ctypes.POINTER(ctypes.c_int64)], I),
+        "gg_scs_solution_dev": ([P, PP, PP, PP, PP], I),
         "gg_profile_enable": ([I], I),
         "gg_profile_get": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)], I),
@@ -162,7 +167,8 @@ EXPORTED = [
     "gg_bls12_381_g2_jac_to_affine", "gg_bls12_381_g2_jac_add", "gg_bls12_381_g2_scalar_mul",
     "gg_groth16_mpk_create", "gg_groth16_mpk_release", "gg_groth16_mpk_info", "gg_groth16_mpk_prove",
     "gg_groth16_mpk_last_timings", "gg_r1cs_create", "gg_r1cs_release", "gg_r1cs_info", "gg_r1cs_solve",
-    "gg_r1cs_solution_dev",
+    "gg_r1cs_solution_dev", "gg_scs_create", "gg_scs_release", "gg_scs_info", "gg_scs_solve",
+    "gg_scs_solution_dev",
 ]
 
 

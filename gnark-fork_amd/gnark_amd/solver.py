@@ -163,3 +163,111 @@ class R1CS:
             self.close()
         except Exception:
             pass
+
+
+def compute_scs_levels(nb_inputs: int, n_wires: int, wires) -> list:
+    """r1cs.Levels of a sparse R1CS (blueprint.go updateInstructionTree over
+    xa, xb, xc): wires < nb_inputs are the witness."""
+    level = np.full(n_wires, -1, dtype=np.int64)
+    w = np.asarray(wires, dtype=np.int64).reshape(-1, 3)
+    out = []
+    for c in range(len(w)):
+        mx, outs = -1, []
+        for x in w[c]:
+            x = int(x)
+            if x < nb_inputs:
+                continue
+            if level[x] < 0:
+                if x not in outs:
+                    outs.append(x)
+            elif level[x] > mx:
+                mx = int(level[x])
+        mx += 1
+        for x in outs:
+            level[x] = mx
+        while len(out) <= mx:
+            out.append([])
+        out[mx].append(c)
+    return out
+
+
+class SparseR1CS:
+    """Device-resident sparse R1CS (gg_scs_create) with its solver: the PlonK
+    side of r1cs.Solve (constraint/blueprint_scs.go:53-151), returning the
+    L, R, O columns of evaluateLROSmallDomain (system.go:221-264)."""
+
+    def __init__(self, nb_public: int, nb_secret: int, n_wires: int, wires, qidx, coeffs: Sequence[int],
+                 flags=None, levels=None, curve: str = "bls12-381"):
+        from ._lib import GG_CURVE_BN254, GG_CURVE_BLS12_381
+        self.curve = curve
+        self.mod = fr.BLS_R if curve == "bls12-381" else fr.R
+        self._mont = fr.bls_fr_mont if curve == "bls12-381" else fr.fr_mont
+        cid = GG_CURVE_BLS12_381 if curve == "bls12-381" else GG_CURVE_BN254
+        self.nb_public, self.nb_secret, self.n_wires = nb_public, nb_secret, n_wires
+        self.wires = np.ascontiguousarray(wires, dtype=np.uint32)
+        self.qidx = np.ascontiguousarray(qidx, dtype=np.uint32)
+        self.n_constraints = len(self.wires) // 3
+        self.flags = None if flags is None else np.ascontiguousarray(flags, dtype=np.uint8)
+        if levels is None:
+            levels = compute_scs_levels(nb_public + nb_secret, n_wires, self.wires)
+        self.levels = levels
+        lo = np.zeros(len(levels) + 1, dtype=np.uint32)
+        lo[1:] = np.cumsum([len(x) for x in levels])
+        lc = np.ascontiguousarray(np.concatenate([np.asarray(x, dtype=np.uint32) for x in levels])
+                                  if levels else np.zeros(0, dtype=np.uint32), dtype=np.uint32)
+        cbytes = b"".join(self._mont(int(k) % self.mod) for k in coeffs)
+        h = ctypes.c_void_p()
+        check(lib.gg_scs_create(cid, n_wires, self.n_constraints, nb_public, ptr(self.wires), ptr(self.qidx),
+                                ptr(self.flags), ptr(cbytes), len(coeffs), ptr(lo), ptr(lc), len(levels),
+                                ctypes.byref(h)))
+        self.handle = h
+        d = ctypes.c_size_t()
+        check(lib.gg_scs_info(h, None, None, ctypes.byref(d)))
+        self.domain = d.value
+
+    @classmethod
+    def from_constraints(cls, nb_public: int, nb_secret: int, n_wires: int, constraints, flags=None,
+                         levels=None, curve: str = "bls12-381") -> "SparseR1CS":
+        """constraints: [(xa, xb, xc, qL, qR, qO, qM, qC)] with int coefficients."""
+        mod = fr.BLS_R if curve == "bls12-381" else fr.R
+        table, index = [0, 1], {0: 0, 1: 1}
+        wires, qidx = [], []
+        for xa, xb, xc, *qs in constraints:
+            wires += [xa, xb, xc]
+            for k in qs:
+                k %= mod
+                if k not in index:
+                    index[k] = len(table)
+                    table.append(k)
+                qidx.append(index[k])
+        return cls(nb_public, nb_secret, n_wires, wires, qidx, table, flags, levels, curve)
+
+    def solve(self, witness, on_device: bool = True):
+        """spr.Solve(fullWitness) -> (W, L, R, O): host bytes or DeviceBuffers."""
+        n_in = self.nb_public + self.nb_secret
+        if len(witness) != n_in:
+            raise ValueError("invalid witness size, got %d, expected %d" % (len(witness), n_in))
+        wbuf = b"".join(self._mont(int(v) % self.mod) for v in witness)
+        nw, d = self.n_wires, self.domain
+        if on_device:
+            out = [DeviceBuffer(32 * nw), DeviceBuffer(32 * d), DeviceBuffer(32 * d), DeviceBuffer(32 * d)]
+        else:
+            out = [bytearray(32 * nw), bytearray(32 * d), bytearray(32 * d), bytearray(32 * d)]
+        bad = ctypes.c_int64(-1)
+        rc = lib.gg_scs_solve(self.handle, ptr(wbuf), n_in, 0, *(ptr(x) for x in out), int(on_device),
+                              ctypes.byref(bad))
+        if rc == GG_ERR_UNSATISFIED:
+            raise UnsatisfiedConstraintError(bad.value, lib.gg_last_error().decode())
+        check(rc)
+        return out
+
+    def close(self):
+        if getattr(self, "handle", None):
+            lib.gg_scs_release(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -506,6 +506,29 @@ int gg_r1cs_solve(gg_r1cs_t r, const void *witness, size_t n_witness, int witnes
  * solve or the release): a prove can read them without a copy */
 int gg_r1cs_solution_dev(gg_r1cs_t r, void **w, void **a, void **b, void **c);
 
+/* ---- sparse-R1CS (PlonK) solver: the SCS blueprints' Solve
+ * (constraint/blueprint_scs.go:53-151) level by level (solver.go:418-533) and
+ * evaluateLROSmallDomain (constraint/bls12-381/system.go:221-264): replaces
+ * spr.Solve(fullWitness) -> SparseR1CSSolution{L, R, O} (plonk prove.go:180-187)
+ * for hint-free systems; L, R, O (domain = next power of two of
+ * n_constraints + nb_public) stay in HBM for gg_plonk_prove (inputs_on_device).
+ *   wires[3 c + 0..2] = xa, xb, xc; qidx[5 c + 0..4] = qL, qR, qO, qM, qC
+ *   (indices into coeffs, fr Montgomery); flags[c] & 1: a BSB22 commitment
+ *   constraint (not solved, blueprint_scs.go:56-60), flags nullable;
+ *   levels as for gg_r1cs_create.  witness = public then secret values (no
+ *   ONE_WIRE).  curve: GG_CURVE_BLS12_381 or GG_CURVE_BN254 (scalar field).
+ *   GG_ERR_UNSATISFIED: *failed = the first failing constraint (unsatisfied or
+ *   a zero divisor: errDivideByZero). */
+typedef struct gg_scs *gg_scs_t;
+int gg_scs_create(int curve, size_t n_wires, size_t n_constraints, size_t nb_public, const uint32_t *wires,
+                  const uint32_t *qidx, const uint8_t *flags, const void *coeffs, size_t n_coeffs,
+                  const uint32_t *level_off, const uint32_t *level_cons, size_t n_levels, gg_scs_t *out);
+int gg_scs_release(gg_scs_t h);
+int gg_scs_info(gg_scs_t h, size_t *n_wires, size_t *n_constraints, size_t *domain);
+int gg_scs_solve(gg_scs_t h, const void *witness, size_t n_witness, int witness_on_device, void *w_out,
+                 void *l_out, void *r_out, void *o_out, int out_on_device, int64_t *failed);
+int gg_scs_solution_dev(gg_scs_t h, void **w, void **l, void **r, void **o);
+
 /* ------------------------------------------------------------ profiling
  * Kernel-level timing with HIP events recorded on the stream each kernel is
  * launched on (bench.py uses it for the roofline of the dominant kernel).
