@@ -85,3 +85,70 @@ def test_gpu_scs_solver_errors():
     with pytest.raises(GnarkAmdError):
         sys_.solve([5])
     sys_.close()
+
+
+class _ScsCircuit:
+    """A sparse R1CS laid out as gnark's BuildTrace does (setup.go:173-220):
+    public placeholder rows (-x + qk = 0, qk completed by the prover), the
+    constraints, padding rows; every unused slot is wire 0, matching
+    evaluateLROSmallDomain's solution[0] padding.  Provides what
+    plonk_circuits.make_key reads (selectors, permutation, S polynomials)."""
+
+    def __init__(self, cons, nb_public, n_wires):
+        import numpy as np
+        from plonk_circuits import Circuit
+        self._C = Circuit
+        n = 1
+        while n < len(cons) + nb_public:
+            n <<= 1
+        self.n, self.log_n = n, n.bit_length() - 1
+        self.nb_public, self.n_cmt, self.cmt_idx, self.committed = nb_public, 0, [], []
+        self.nvar, self.cons = n_wires, cons
+        self.a, self.b, self.c = (np.zeros(n, np.int64) for _ in range(3))
+        self.a[:nb_public] = np.arange(nb_public)
+        for j, k in enumerate(cons):
+            self.a[nb_public + j], self.b[nb_public + j], self.c[nb_public + j] = k[0], k[1], k[2]
+
+    def selectors(self):
+        from plonk_circuits import m2b, MONT, NEG_ONE_M
+        cols = [bytearray(32 * self.n) for _ in range(5)]  # ql, qr, qm, qo, qk
+        for i in range(self.nb_public):
+            cols[0][32 * i:32 * i + 32] = m2b(NEG_ONE_M)
+        for j, (xa, xb, xc, qL, qR, qO, qM, qC) in enumerate(self.cons):
+            r = self.nb_public + j
+            for col, q in zip(cols, (qL, qR, qM, qO, qC)):
+                col[32 * r:32 * r + 32] = m2b(q % BLS_R * MONT % BLS_R)
+        return [bytes(c) for c in cols], []
+
+    def permutation(self):
+        return self._C.permutation(self)
+
+    def s_polys(self, perm, omega, u):
+        return self._C.s_polys(self, perm, omega, u)
+
+
+@pytest.mark.gpu
+def test_gpu_scs_solve_feeds_plonk_prove():
+    """spr.Solve on the GPU -> L, R, O in HBM -> gg_plonk_prove -> the restated
+    verifier accepts; a wrong public input is rejected."""
+    import bls12_381_oracle as blo
+    from gnark_amd import plonk_prover as pp, solver
+    from plonk_circuits import make_key, to_oracle
+    rng = random.Random(21)
+    nbp, nbs = 2, 3
+    cons, flags, nw = ss.random_circuit(rng, BLS_R, nbp, nbs, 100)
+    wit = [rng.randrange(BLS_R) for _ in range(nbp + nbs)]
+    cons = ss.fill_assertions(BLS_R, cons, wit)
+    circ = _ScsCircuit(cons, nbp, nw)
+    tau = 987654321
+    pk = make_key(circ, tau)
+    sys_ = solver.SparseR1CS.from_constraints(nbp, nbs, nw, cons, curve="bls12-381")
+    assert sys_.domain == circ.n
+    W, L, Rv, O = sys_.solve(wit)  # DeviceBuffers
+    pub = wit[:nbp]
+    proof = pp.prove(pk, L, Rv, O, rng=random.Random(5), public=pub)
+    pr, vk = to_oracle(pk, proof)
+    assert blo.plonk_verify_trapdoor(pr, vk, tau, public=pub)
+    assert not blo.plonk_verify_trapdoor(pr, vk, tau, public=[pub[0] + 1, pub[1]])
+    sys_.close()
+    pk.close()
