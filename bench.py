@@ -551,9 +551,10 @@ def solver_bench(g, log_n, reps=5):
             "constraints_per_s": m["ncons"] / (min(ts) * 1e-3),
             "witness_to_proof_ms": min(e2e), "witness_to_proof_ms_all": [round(x, 2) for x in e2e],
             "system_setup_s": setup_s,
-            "note": "gg_r1cs_solve: one launch per level (255 levels x 65,536 chains at 2^24) in a HIP "
-                    "graph; the solution stays in HBM and feeds gg_groth16_prove (inputs on device), so "
-                    "witness -> proof moves only the 2 MB witness over PCIe"}
+            "note": "gg_r1cs_solve: strand schedule (a thread per dependency chain: 65,536 chains x 255 "
+                    "constraints at 2^24, one launch; GG_SOLVER_LEVELS=1 = one launch per r1cs.Levels level) "
+                    "in a HIP graph; the solution stays in HBM and feeds gg_groth16_prove (inputs on device), "
+                    "so witness -> proof moves only the 2 MB witness over PCIe"}
 
 
 def msm_bench(log_n, rank, world, dist, xdev, barrier, max_over_ranks, steps=20, warmup=3):

@@ -21,6 +21,7 @@
 #include "common.h"
 #include "field.cuh"
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -33,6 +34,7 @@ struct R1csDev {
     const Fr* coef;
     const Fr* coef_inv;
     uint32_t ncoef;
+    uint32_t one_idx;  // index of the coefficient 1 (CoeffIdOne), ~0 if absent: no product
     Fr* W;
     Fr* A;
     Fr* B;
@@ -68,7 +70,8 @@ __global__ void __launch_bounds__(256) k_solve_level(R1csDev d, const uint32_t* 
         for (uint32_t t = t0; t < t1; t++) {
             const uint32_t w = d.wire[t];
             if (d.solved[w]) {
-                acc[s] = acc[s] + ldfr(d.coef + d.cidx[t]) * ldfr(d.W + w);
+                const uint32_t k = d.cidx[t];
+                acc[s] = acc[s] + (k == d.one_idx ? ldfr(d.W + w) : ldfr(d.coef + k) * ldfr(d.W + w));
                 continue;
             }
             if (loc >= 0) malformed = true;  // "found more than one wire to instantiate"
@@ -102,13 +105,85 @@ __global__ void __launch_bounds__(256) k_solve_level(R1csDev d, const uint32_t* 
             ok = false;
         }
         const uint32_t w = d.wire[ut];
-        stfr(d.W + w, v * kinv);
+        stfr(d.W + w, k == d.one_idx ? v : v * kinv);
         d.solved[w] = 1;
     }
     if (!ok) atomicMin(d.fail, c);
     stfr(d.A + c, acc[0]);
     stfr(d.B + c, acc[1]);
     stfr(d.C + c, acc[2]);
+}
+
+// W read around the (write-through, non-coherent) L1: within a strand kernel a
+// thread reads values it stored earlier in the same launch
+__device__ __forceinline__ Fr ldfr_l2(const Fr* p) {
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+    Fr r;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint64_t x = __hip_atomic_load(q + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r.v[2 * k] = (uint32_t)x;
+        r.v[2 * k + 1] = (uint32_t)(x >> 32);
+    }
+    return r;
+}
+
+// Strand schedule (solve_strands): thread s walks segment s of this launch --
+// consecutive constraints of one dependency chain -- in order; the unknown
+// term of each constraint is known statically (unk[c], ~0 = none), so no
+// solved flags are read inside the launch.  Dependencies on other strands were
+// solved by earlier launches.
+__global__ void __launch_bounds__(256) k_solve_strands(R1csDev d, const uint32_t* unk, const uint32_t* order,
+                                                       const uint32_t* seg_start, uint32_t nseg) {
+    const uint32_t sg = blockIdx.x * blockDim.x + threadIdx.x;
+    if (sg >= nseg) return;
+    for (uint32_t i = seg_start[sg], e = seg_start[sg + 1]; i < e; i++) {
+        const uint32_t c = order[i], ut = unk[c];
+        Fr acc[3] = {Fr::zero(), Fr::zero(), Fr::zero()};
+        int loc = -1;
+        for (int s = 0; s < 3; s++) {
+            const uint32_t t0 = d.off[3 * c + s], t1 = d.off[3 * c + s + 1];
+            for (uint32_t t = t0; t < t1; t++) {
+                if (t == ut) {
+                    loc = s;
+                    continue;
+                }
+                const uint32_t k = d.cidx[t];
+                const Fr x = ldfr_l2(d.W + d.wire[t]);
+                acc[s] = acc[s] + (k == d.one_idx ? x : ldfr(d.coef + k) * x);
+            }
+        }
+        bool ok = true;
+        if (loc < 0) {
+            ok = acc[0] * acc[1] == acc[2];
+        } else {
+            Fr v = Fr::zero();
+            const Fr a = acc[0], b = acc[1], cc = acc[2];
+            if (loc == 0) {
+                if (!b.is_zero()) { v = cc * inverse(b) - a; acc[0] = a + v; }
+                else ok = a * b == cc;
+            } else if (loc == 1) {
+                if (!a.is_zero()) { v = cc * inverse(a) - b; acc[1] = b + v; }
+                else ok = a * b == cc;
+            } else {
+                v = a * b - cc;
+                acc[2] = cc + v;
+            }
+            const uint32_t k = d.cidx[ut];
+            const Fr kinv = ldfr(d.coef_inv + k);
+            if (kinv.is_zero()) {
+                atomicMin(d.fail + 1, c);
+                ok = false;
+            }
+            const uint32_t w = d.wire[ut];
+            stfr(d.W + w, k == d.one_idx ? v : v * kinv);
+            d.solved[w] = 1;
+        }
+        if (!ok) atomicMin(d.fail, c);
+        stfr(d.A + c, acc[0]);
+        stfr(d.B + c, acc[1]);
+        stfr(d.C + c, acc[2]);
+    }
 }
 
 __global__ void k_solver_init(Fr* W, uint8_t* solved, size_t nw, const Fr* inputs, size_t n_in, uint32_t* fail) {
@@ -139,8 +214,16 @@ using namespace gg;
 struct gg_r1cs {
     int device = 0;
     size_t nw = 0, ncons = 0, nterms = 0, ncoef = 0;
+    uint32_t one_idx = 0xffffffffu;
     std::vector<uint32_t> level_off;  // host copy (launch sizes)
+    std::vector<uint32_t> h_off, h_wire, h_level_cons;  // host copies for the strand analysis
     DevBuf off, wire, cidx, coef, coef_inv, level_cons, W, A, B, C, solved, fail, inputs, cnt;
+    // strand schedule (built at the first solve, per witness length)
+    long long strand_nin = -1;   // witness length it was built for
+    bool strands = false;        // false: the level-by-level launches
+    std::vector<uint32_t> sl_seg_off;  // segments of super-level l: [sl_seg_off[l], sl_seg_off[l+1])
+    DevBuf unk, order, seg_start;
+    size_t n_super = 0, n_seg = 0;
     hipStream_t st = nullptr;
     hipGraphExec_t graph = nullptr;
     std::mutex mu;
@@ -149,6 +232,94 @@ struct gg_r1cs {
         if (st) (void)hipStreamDestroy(st);
     }
 };
+
+// Strand schedule for a witness of n_in values (wires 0..n_in are solved up
+// front).  In r1cs.Levels order: the unknown term of every constraint (the
+// single term whose wire no earlier level produced), its producer map, then
+// greedy chains -- a constraint extends the strand whose tail produced one of
+// its inputs -- and super-levels: sl(c) = max(sl(previous in its strand),
+// sl(d) + 1 for every dependency d on another strand).  One launch per
+// super-level, a thread per strand segment (the MiMC headline: 65,536 chains,
+// one launch instead of 255).  Returns false (level launches instead) when the
+// levels do not match the system; the level kernel then reports it.
+static bool build_strands(gg_r1cs* r, size_t n_in) {
+    const uint32_t NONE = 0xffffffffu, nin = (uint32_t)n_in + 1;
+    const size_t nc = r->ncons;
+    std::vector<uint32_t> lev(nc), prod(r->nw, NONE), unk(nc, NONE);
+    for (size_t l = 0; l + 1 < r->level_off.size(); l++)
+        for (uint32_t i = r->level_off[l]; i < r->level_off[l + 1]; i++) lev[r->h_level_cons[i]] = (uint32_t)l;
+    std::vector<uint32_t> strand(nc), sl(nc), tail, deps;
+    std::vector<std::pair<uint64_t, uint32_t>> key(nc);  // ((sl, strand), position) -> order
+    for (size_t l = 0; l + 1 < r->level_off.size(); l++) {
+        for (uint32_t i = r->level_off[l]; i < r->level_off[l + 1]; i++) {
+            const uint32_t c = r->h_level_cons[i];
+            deps.clear();
+            uint32_t u = NONE;
+            for (uint32_t t = r->h_off[3 * c]; t < r->h_off[3 * c + 3]; t++) {
+                const uint32_t w = r->h_wire[t];
+                if (w < nin) continue;
+                const uint32_t p = prod[w];
+                if (p == NONE) {
+                    if (u != NONE) return false;  // two unknown terms
+                    u = t;
+                } else if (p != c) {
+                    if (lev[p] >= l) return false;  // produced in this or a later level
+                    deps.push_back(p);
+                }
+            }
+            if (u != NONE) prod[r->h_wire[u]] = c;
+            unk[c] = u;
+            uint32_t best = NONE;
+            for (uint32_t d : deps)
+                if (tail[strand[d]] == d && (best == NONE || lev[d] > lev[best])) best = d;
+            uint32_t s, level = 0;
+            if (best != NONE) {
+                s = strand[best];
+                level = sl[best];
+            } else {
+                s = (uint32_t)tail.size();
+                tail.push_back(NONE);
+            }
+            for (uint32_t d : deps)
+                if (strand[d] != s) level = std::max(level, sl[d] + 1);
+            strand[c] = s;
+            tail[s] = c;
+            sl[c] = level;
+            key[c] = {((uint64_t)level << 32) | s, (uint32_t)i};
+        }
+    }
+    std::vector<uint32_t> order(nc);
+    for (size_t c = 0; c < nc; c++) order[c] = (uint32_t)c;
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
+    std::vector<uint32_t> seg_start;
+    r->sl_seg_off.clear();
+    uint64_t prev = ~0ull;
+    uint32_t cur_sl = NONE;
+    for (size_t i = 0; i < nc; i++) {
+        const uint64_t k = key[order[i]].first;
+        if (k != prev) {
+            const uint32_t lvl = (uint32_t)(k >> 32);
+            while (cur_sl == NONE || cur_sl < lvl) {
+                r->sl_seg_off.push_back((uint32_t)seg_start.size());
+                cur_sl = cur_sl == NONE ? 0 : cur_sl + 1;
+            }
+            seg_start.push_back((uint32_t)i);
+            prev = k;
+        }
+    }
+    seg_start.push_back((uint32_t)nc);
+    r->sl_seg_off.push_back((uint32_t)seg_start.size() - 1);
+    auto up = [](DevBuf& b, const void* src, size_t bytes) {
+        b.alloc(std::max<size_t>(bytes, 16));
+        if (bytes) GG_HIP(hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+    };
+    up(r->unk, unk.data(), nc * 4);
+    up(r->order, order.data(), nc * 4);
+    up(r->seg_start, seg_start.data(), seg_start.size() * 4);
+    r->n_seg = seg_start.size() - 1;
+    r->n_super = r->sl_seg_off.size() - 1;
+    return true;
+}
 
 extern "C" int gg_r1cs_create(size_t n_wires, size_t n_constraints, const uint32_t* term_off,
                               const uint32_t* term_wire, const uint32_t* term_coeff, const void* coeffs,
@@ -185,7 +356,11 @@ extern "C" int gg_r1cs_create(size_t n_wires, size_t n_constraints, const uint32
     // divByCoeff: host inverses of the coefficient table (0 for a zero coefficient)
     const Fr* cf = (const Fr*)coeffs;
     std::vector<Fr> inv(n_coeffs);
-    for (size_t i = 0; i < n_coeffs; i++) inv[i] = cf[i].is_zero() ? Fr::zero() : inverse(cf[i]);
+    uint32_t one_idx = 0xffffffffu;
+    for (size_t i = 0; i < n_coeffs; i++) {
+        inv[i] = cf[i].is_zero() ? Fr::zero() : inverse(cf[i]);
+        if (one_idx == 0xffffffffu && cf[i] == Fr::one()) one_idx = (uint32_t)i;
+    }
     auto* r = new gg_r1cs();
     try {
         GG_HIP(hipGetDevice(&r->device));
@@ -193,7 +368,11 @@ extern "C" int gg_r1cs_create(size_t n_wires, size_t n_constraints, const uint32
         r->ncons = n_constraints;
         r->nterms = nterms;
         r->ncoef = n_coeffs;
+        r->one_idx = one_idx;
         r->level_off.assign(level_off, level_off + n_levels + 1);
+        r->h_off.assign(term_off, term_off + 3 * n_constraints + 1);
+        r->h_wire.assign(term_wire, term_wire + nterms);
+        r->h_level_cons.assign(level_cons, level_cons + n_constraints);
         auto up = [](DevBuf& b, const void* src, size_t bytes) {
             b.alloc(std::max<size_t>(bytes, 16));
             if (bytes) GG_HIP(hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
@@ -234,11 +413,23 @@ extern "C" int gg_r1cs_info(gg_r1cs_t r, size_t* n_wires, size_t* n_constraints,
     GG_CAPI_END
 }
 
-// the per-level launches, enqueued on r->st (recorded once into a graph)
+// the per-level (or per-super-level strand) launches, enqueued on r->st
+// (recorded once into a graph)
 static void enqueue_levels(gg_r1cs* r) {
     R1csDev d{r->off.as<uint32_t>(), r->wire.as<uint32_t>(), r->cidx.as<uint32_t>(), r->coef.as<Fr>(),
-              r->coef_inv.as<Fr>(), (uint32_t)r->ncoef, r->W.as<Fr>(), r->A.as<Fr>(), r->B.as<Fr>(),
+              r->coef_inv.as<Fr>(), (uint32_t)r->ncoef, r->one_idx, r->W.as<Fr>(), r->A.as<Fr>(), r->B.as<Fr>(),
               r->C.as<Fr>(), r->solved.as<uint8_t>(), r->fail.as<uint32_t>()};
+    if (r->strands) {
+        for (size_t l = 0; l < r->n_super; l++) {
+            const uint32_t a = r->sl_seg_off[l], cnt = r->sl_seg_off[l + 1] - a;
+            if (!cnt) continue;
+            hipLaunchKernelGGL(k_solve_strands, dim3(grid_for(cnt, 256)), dim3(256), 0, r->st, d,
+                               r->unk.as<uint32_t>(), r->order.as<uint32_t>(), r->seg_start.as<uint32_t>() + a,
+                               cnt);
+            GG_HIP(hipGetLastError());
+        }
+        return;
+    }
     const uint32_t* lc = r->level_cons.as<uint32_t>();
     for (size_t l = 0; l + 1 < r->level_off.size(); l++) {
         const uint32_t a = r->level_off[l], cnt = r->level_off[l + 1] - a;
@@ -267,7 +458,17 @@ extern "C" int gg_r1cs_solve(gg_r1cs_t r, const void* witness, size_t n_witness,
     hipLaunchKernelGGL(k_solver_init, dim3(grid_for(r->nw, 256)), dim3(256), 0, r->st, r->W.as<Fr>(),
                        r->solved.as<uint8_t>(), r->nw, in, n_witness, r->fail.as<uint32_t>());
     GG_HIP(hipGetLastError());
-    // the level launches: captured once into a graph, replayed afterwards
+    // schedule: strands when the levels allow it (GG_SOLVER_LEVELS=1: level launches)
+    if (r->strand_nin != (long long)n_witness) {
+        const bool levels_only = getenv("GG_SOLVER_LEVELS") && atoi(getenv("GG_SOLVER_LEVELS"));
+        r->strands = !levels_only && build_strands(r, n_witness);
+        r->strand_nin = (long long)n_witness;
+        if (r->graph) {
+            (void)hipGraphExecDestroy(r->graph);
+            r->graph = nullptr;
+        }
+    }
+    // the launches: captured once into a graph, replayed afterwards
     if (!r->graph) {
         hipGraph_t g;
         GG_HIP(hipStreamBeginCapture(r->st, hipStreamCaptureModeThreadLocal));

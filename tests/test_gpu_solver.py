@@ -182,3 +182,32 @@ def test_gpu_solver_feeds_groth16_bit_exact():
     assert (pr.Ar.hex(), pr.Bs.hex(), pr.Krs.hex()) == (g["Ar"], g["Bs"], g["Krs"])
     sys_.close()
     pk.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("levels_only", [False, True])
+def test_gpu_solver_strand_and_level_schedules_agree(levels_only, monkeypatch):
+    """The strand schedule (one launch per super-level, a thread per chain
+    segment) and the plain level launches (GG_SOLVER_LEVELS=1) give the same
+    bit-exact solution (MiMC 2^12 shape and a random circuit)."""
+    import coracle
+    from gnark_amd import solver
+    from helpers import random_fr_mont
+    monkeypatch.setenv("GG_SOLVER_LEVELS", "1" if levels_only else "0")
+    m = mimc_csr(16, 85, 1)
+    sys_ = solver.R1CS(m["nb_public"], m["nb_secret"], m["nw"], m["off"], m["wires"], m["coef"], m["table"],
+                       levels=m["levels"])
+    inputs = random_fr_mont(16, seed=3).tobytes()
+    ref = coracle.MimcR1CS(16, 85, 1)
+    wref = ref.solve(inputs)
+    assert _host(sys_.solve(inputs))[0] == bytes(wref)
+    sys_.close()
+    ref.close()
+    rng = random.Random(9)
+    cons = rs.random_circuit(rng, 2, 3, 200, zero_divisor=True)
+    wit = [rng.randrange(o.R) for _ in range(4)]
+    W, A, B, C = rs.solve(205, 5, cons, wit, rs.levels_of(5, cons))
+    sys_ = solver.R1CS.from_terms(2, 3, 205, cons)
+    gW, gA, gB, gC = _host(sys_.solve(wit))
+    assert _fr_list(gW) == W and _fr_list(gC) == C
+    sys_.close()
