@@ -4,8 +4,9 @@
 // (backend/plonk/bls12-381) so it reads pk.trace / pk.Kzg / pk.KzgLagrange
 // directly.  Prove (prove.go:116) dispatches here when the prover option
 // WithAMDAcceleration() / WithIcicleAcceleration() is set (INTEGRATION.md §4).
-// The solver stays gnark's (prove.go:365-395) with the BSB22 hint committing on
-// the GPU; everything after Solve -- prove.go:116-176's errgroup DAG -- is one
+// Hint-free systems without commitments solve on the GPU (solver_amd.go);
+// otherwise the solver stays gnark's (prove.go:365-395) with the BSB22 hint
+// committing on the GPU; everything after Solve -- prove.go:116-176's errgroup DAG -- is one
 // gg_plonk_prove call.  Source only here (no Go toolchain in the build image).
 package plonk
 
@@ -103,6 +104,7 @@ func (pk *ProvingKey) amdKey() (C.gg_plonk_pk_t, error) {
 
 // ReleaseAMD frees the HBM-resident copy of pk.
 func (pk *ProvingKey) ReleaseAMD() {
+	pk.releaseSolver()
 	if h, ok := amdKeys.LoadAndDelete(pk); ok {
 		C.gg_plonk_pk_release(h.(C.gg_plonk_pk_t))
 	}
@@ -135,6 +137,7 @@ func proveAMD(spr *cs.SparseR1CS, pk *ProvingKey, fullWitness witness.Witness, o
 	proof := &Proof{}
 	commitmentInfo := spr.CommitmentInfo.(constraint.PlonkCommitments)
 	nCmt := len(commitmentInfo)
+	userHints := len(opt.SolverOpts) > 0
 	commitmentVal := make([]fr.Element, nCmt)
 	committed := make([][]fr.Element, nCmt)
 	proof.Bsb22Commitments = make([]curve.G1Affine, nCmt)
@@ -176,14 +179,33 @@ func proveAMD(spr *cs.SparseR1CS, pk *ProvingKey, fullWitness witness.Witness, o
 			solver.OverrideHint(spr.GkrInfo.SolveHintID, cs.GkrSolveHint(spr.GkrInfo, &gkrData)),
 			solver.OverrideHint(spr.GkrInfo.ProveHintID, cs.GkrProveHint(spr.GkrInfo.HashName, &gkrData)))
 	}
-	_solution, err := spr.Solve(fullWitness, opt.SolverOpts...)
-	if err != nil {
-		return nil, err
-	}
-	sol := _solution.(*cs.SparseR1CSSolution)
 	w, ok := fullWitness.Vector().(fr.Vector)
 	if !ok {
 		return nil, witness.ErrInvalidWitness
+	}
+	// hint-free systems without commitments: spr.Solve on the GPU, L, R, O stay
+	// in HBM (solver_amd.go); everything else keeps gnark's solver
+	var lro [3]unsafe.Pointer
+	onDevice := 0
+	if nCmt == 0 && !userHints && !spr.GkrInfo.Is() {
+		ds, err := pk.amdSolver(spr)
+		if err != nil {
+			return nil, err
+		}
+		if ds != nil {
+			if lro[0], lro[1], lro[2], err = ds.solve(fullWitness); err != nil {
+				return nil, err
+			}
+			onDevice = 1
+		}
+	}
+	if onDevice == 0 {
+		_solution, err := spr.Solve(fullWitness, opt.SolverOpts...)
+		if err != nil {
+			return nil, err
+		}
+		sol := _solution.(*cs.SparseR1CSSolution)
+		lro = [3]unsafe.Pointer{unsafe.Pointer(&sol.L[0]), unsafe.Pointer(&sol.R[0]), unsafe.Pointer(&sol.O[0])}
 	}
 	nbPub := len(spr.Public)
 	cv := C.malloc(C.size_t(nCmt+1) * C.size_t(unsafe.Sizeof(uintptr(0))))
@@ -207,7 +229,7 @@ func proveAMD(spr *cs.SparseR1CS, pk *ProvingKey, fullWitness witness.Witness, o
 		dgPtr = unsafe.Pointer(&proof.Bsb22Commitments[0])
 		hvPtr = unsafe.Pointer(&commitmentVal[0])
 	}
-	rc := C.gg_plonk_prove(h, unsafe.Pointer(&sol.L[0]), unsafe.Pointer(&sol.R[0]), unsafe.Pointer(&sol.O[0]), 0,
+	rc := C.gg_plonk_prove(h, lro[0], lro[1], lro[2], C.int(onDevice),
 		pubPtr, C.size_t(nbPub), (*unsafe.Pointer)(cv), dgPtr, hvPtr, C.int(nCmt), nil,
 		C.gg_go_hash_fn(), unsafe.Pointer(uintptr(hc)), C.gg_go_hash_fn(), unsafe.Pointer(uintptr(hf)),
 		unsafe.Pointer(&out[0]), size)
