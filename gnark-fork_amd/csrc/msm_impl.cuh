@@ -863,6 +863,79 @@ inline Xyzz<F> msm_run(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, hipStr
     return msm_finish<F>(b, &w->sort, &w->scr, st);
 }
 
+// device-resident points: keep[i] = point i is not infinity (or keep_inf)
+template <class F>
+__global__ void k_base_keep(const Affine<F>* pts, size_t n, int keep_inf, uint32_t* keep, uint32_t* any_inf) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const bool inf = pts[i].is_inf();
+    if (inf) *any_inf = 1u;
+    keep[i] = (!inf || keep_inf) ? 1u : 0u;
+}
+template <class F>
+__global__ void k_base_compact(const Affine<F>* pts, size_t n, const uint32_t* keep, const uint32_t* pos,
+                               Affine<F>* out, uint32_t* idx) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !keep[i]) return;
+    out[pos[i]] = pts[i];
+    idx[pos[i]] = (uint32_t)i;
+}
+
+template <class F>
+inline void window_layout(gg_msm_base* b, int window_bits, int total) {
+    const size_t pb = sizeof(Affine<F>);
+    b->c = window_bits ? window_bits : choose_c(std::max<size_t>(b->n, 1), pb, total);
+    GG_CHECK(b->c >= 2 && b->c <= 24, GG_ERR_INVALID_ARG, "window_bits out of range [2, 24]");
+    b->W = (total + b->c - 1) / b->c;
+    b->c = (total + b->W - 1) / b->W;  // widest balanced window for this W
+    GG_CHECK(b->W <= 64, GG_ERR_INVALID_ARG, "too many windows");
+    b->win = make_windows(b->c, b->W, total);
+    b->nb = (size_t)1 << (b->c - 1);
+    GG_CHECK((double)b->W * (double)b->n < 2147483648.0, GG_ERR_UNSUPPORTED,
+             "too many points x windows for 31-bit entry ids");
+}
+
+// points already in HBM (no scalar index map): infinity points dropped by a
+// flag / scan / scatter on the device, no round trip through host memory
+template <class F>
+inline void create_base_dev(gg_msm_base* b, const Affine<F>* pts, size_t n, int window_bits, bool keep_inf,
+                            int total) {
+    hipStream_t st = hipStreamPerThread;
+    DevBuf keep(std::max<size_t>(n, 1) * 4), pos(std::max<size_t>(n, 1) * 4), flag(16);
+    GG_HIP(hipMemsetAsync(flag.p, 0, 4, st));
+    hipLaunchKernelGGL(k_base_keep<F>, dim3(grid_for(n, 256)), dim3(256), 0, st, pts, n, (int)keep_inf,
+                       keep.as<uint32_t>(), flag.as<uint32_t>());
+    GG_HIP(hipGetLastError());
+    std::vector<DevBuf> tmp;
+    exclusive_scan(keep.as<uint32_t>(), pos.as<uint32_t>(), n, st, tmp);
+    uint32_t last_pos = 0, last_keep = 0, any_inf = 0;
+    GG_HIP(hipMemcpyAsync(&last_pos, pos.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipMemcpyAsync(&last_keep, keep.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipMemcpyAsync(&any_inf, flag.p, 4, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipStreamSynchronize(st));
+    const size_t kept = (size_t)last_pos + last_keep;
+    b->n = kept;
+    b->has_inf = keep_inf && any_inf;
+    const bool dropped = kept < n;
+    b->has_sidx = dropped;
+    window_layout<F>(b, window_bits, total);
+    if (!kept) {
+        b->max_sidx = 0;
+        if (dropped) b->sidx.alloc(4);
+        return;
+    }
+    DevBuf cmp(kept * sizeof(Affine<F>)), idx(kept * 4);
+    hipLaunchKernelGGL(k_base_compact<F>, dim3(grid_for(n, 256)), dim3(256), 0, st, pts, n, keep.as<uint32_t>(),
+                       pos.as<uint32_t>(), cmp.as<Affine<F>>(), idx.as<uint32_t>());
+    GG_HIP(hipGetLastError());
+    uint32_t max_idx = 0;  // indices increase: the last kept one is the largest
+    GG_HIP(hipMemcpyAsync(&max_idx, idx.as<uint32_t>() + (kept - 1), 4, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipStreamSynchronize(st));
+    b->max_sidx = max_idx;
+    if (dropped) b->sidx = std::move(idx);
+    precompute<F>(b, cmp.as<Affine<F>>(), st);
+}
+
 template <class F>
 inline void create_base(gg_msm_base* b, const void* points, size_t n, int on_device,
                         const uint32_t* sidx, int window_bits, bool keep_inf = false,
@@ -870,9 +943,13 @@ inline void create_base(gg_msm_base* b, const void* points, size_t n, int on_dev
     b->scurve = scurve;
     const int total = scalar_total_bits(scurve);
     const size_t pb = sizeof(Affine<F>);
+    if (on_device && !sidx && n) {
+        create_base_dev<F>(b, (const Affine<F>*)points, n, window_bits, keep_inf, total);
+        return;
+    }
     std::vector<uint8_t> host;
     const uint8_t* src;
-    if (on_device) {
+    if (on_device) {  // with a caller's scalar index map: compact on the host
         host.resize(n * pb);
         if (n) GG_HIP(hipMemcpy(host.data(), points, n * pb, hipMemcpyDeviceToHost));
         src = host.data();
@@ -900,15 +977,7 @@ inline void create_base(gg_msm_base* b, const void* points, size_t n, int on_dev
     b->has_sidx = dropped || sidx != nullptr;
     b->max_sidx = 0;
     for (uint32_t v : idx) b->max_sidx = std::max(b->max_sidx, v);
-    b->c = window_bits ? window_bits : choose_c(std::max<size_t>(b->n, 1), pb, total);
-    GG_CHECK(b->c >= 2 && b->c <= 24, GG_ERR_INVALID_ARG, "window_bits out of range [2, 24]");
-    b->W = (total + b->c - 1) / b->c;
-    b->c = (total + b->W - 1) / b->W;  // widest balanced window for this W
-    GG_CHECK(b->W <= 64, GG_ERR_INVALID_ARG, "too many windows");
-    b->win = make_windows(b->c, b->W, total);
-    b->nb = (size_t)1 << (b->c - 1);
-    GG_CHECK((double)b->W * (double)b->n < 2147483648.0, GG_ERR_UNSUPPORTED,
-             "too many points x windows for 31-bit entry ids");
+    window_layout<F>(b, window_bits, total);
     if (b->has_sidx) {
         b->sidx.alloc(std::max<size_t>(b->n, 1) * 4);
         if (b->n) GG_HIP(hipMemcpy(b->sidx.p, idx.data(), b->n * 4, hipMemcpyHostToDevice));
