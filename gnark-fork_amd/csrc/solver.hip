@@ -35,6 +35,7 @@ struct R1csDev {
     const Fr* coef_inv;
     uint32_t ncoef;
     uint32_t one_idx;  // index of the coefficient 1 (CoeffIdOne), ~0 if absent: no product
+    uint32_t nin;      // wires < nin are ONE_WIRE + the witness (never written by a solve)
     Fr* W;
     Fr* A;
     Fr* B;
@@ -137,6 +138,14 @@ __global__ void __launch_bounds__(256) k_solve_strands(R1csDev d, const uint32_t
                                                        const uint32_t* seg_start, uint32_t nseg) {
     const uint32_t sg = blockIdx.x * blockDim.x + threadIdx.x;
     if (sg >= nseg) return;
+    // the last RC wires this thread produced, kept in registers: a chain reads
+    // its own recent outputs (the MiMC rounds: all of them)
+    constexpr int RC = 4;
+    uint32_t cw[RC];
+    Fr cv[RC];
+#pragma unroll
+    for (int k = 0; k < RC; k++) cw[k] = 0xffffffffu;
+    int cpos = 0;
     for (uint32_t i = seg_start[sg], e = seg_start[sg + 1]; i < e; i++) {
         const uint32_t c = order[i], ut = unk[c];
         Fr acc[3] = {Fr::zero(), Fr::zero(), Fr::zero()};
@@ -148,8 +157,19 @@ __global__ void __launch_bounds__(256) k_solve_strands(R1csDev d, const uint32_t
                     loc = s;
                     continue;
                 }
-                const uint32_t k = d.cidx[t];
-                const Fr x = ldfr_l2(d.W + d.wire[t]);
+                const uint32_t k = d.cidx[t], w = d.wire[t];
+                Fr x;
+                int hit = -1;
+#pragma unroll
+                for (int q = 0; q < RC; q++)
+                    if (cw[q] == w) hit = q;
+                if (hit >= 0) {
+#pragma unroll
+                    for (int q = 0; q < RC; q++)
+                        if (q == hit) x = cv[q];
+                } else {
+                    x = w < d.nin ? ldfr(d.W + w) : ldfr_l2(d.W + w);
+                }
                 acc[s] = acc[s] + (k == d.one_idx ? x : ldfr(d.coef + k) * x);
             }
         }
@@ -176,8 +196,16 @@ __global__ void __launch_bounds__(256) k_solve_strands(R1csDev d, const uint32_t
                 ok = false;
             }
             const uint32_t w = d.wire[ut];
-            stfr(d.W + w, k == d.one_idx ? v : v * kinv);
+            const Fr val = k == d.one_idx ? v : v * kinv;
+            stfr(d.W + w, val);
             d.solved[w] = 1;
+#pragma unroll
+            for (int q = 0; q < RC; q++)
+                if (q == cpos) {
+                    cw[q] = w;
+                    cv[q] = val;
+                }
+            cpos = (cpos + 1) & (RC - 1);
         }
         if (!ok) atomicMin(d.fail, c);
         stfr(d.A + c, acc[0]);
@@ -417,7 +445,8 @@ extern "C" int gg_r1cs_info(gg_r1cs_t r, size_t* n_wires, size_t* n_constraints,
 // (recorded once into a graph)
 static void enqueue_levels(gg_r1cs* r) {
     R1csDev d{r->off.as<uint32_t>(), r->wire.as<uint32_t>(), r->cidx.as<uint32_t>(), r->coef.as<Fr>(),
-              r->coef_inv.as<Fr>(), (uint32_t)r->ncoef, r->one_idx, r->W.as<Fr>(), r->A.as<Fr>(), r->B.as<Fr>(),
+              r->coef_inv.as<Fr>(), (uint32_t)r->ncoef, r->one_idx, (uint32_t)(r->strand_nin + 1), r->W.as<Fr>(),
+              r->A.as<Fr>(), r->B.as<Fr>(),
               r->C.as<Fr>(), r->solved.as<uint8_t>(), r->fail.as<uint32_t>()};
     if (r->strands) {
         for (size_t l = 0; l < r->n_super; l++) {
