@@ -1,5 +1,6 @@
 // R1CS solver on the GPU: constraint/bn254/solver.go:418-608
-// (run + solveR1C) for BN254 R1CS without hint calls.
+// (run + solveR1C) for R1CS without hint calls, BN254 or BLS12-381 fr
+// (gg_r1cs_create_ex; constraint/bls12-381/solver.go is the same code).
 //
 // The system is handed over once in CSR form -- exactly what gnark's public
 // R1CS API yields (r1cs.GetR1Cs() terms, r1cs.Coefficients, r1cs.Levels):
@@ -27,7 +28,9 @@
 
 namespace gg {
 
+template <class FC>
 struct R1csDev {
+    using Fr = Fe<FC>;
     const uint32_t* off;
     const uint32_t* wire;
     const uint32_t* cidx;
@@ -44,21 +47,25 @@ struct R1csDev {
     uint32_t* fail;  // [0] = first unsatisfied constraint, [1] = first malformed one
 };
 
-__device__ __forceinline__ Fr ldfr(const Fr* p) {
+template <class F>
+__device__ __forceinline__ F ldfr(const F* p) {
     const uint4* q = reinterpret_cast<const uint4*>(p);
     uint4 a = q[0], b = q[1];
-    Fr r;
+    F r;
     r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
     r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
     return r;
 }
-__device__ __forceinline__ void stfr(Fr* p, const Fr& r) {
+template <class F>
+__device__ __forceinline__ void stfr(F* p, const F& r) {
     uint4* q = reinterpret_cast<uint4*>(p);
     q[0] = make_uint4(r.v[0], r.v[1], r.v[2], r.v[3]);
     q[1] = make_uint4(r.v[4], r.v[5], r.v[6], r.v[7]);
 }
 
-__global__ void __launch_bounds__(256) k_solve_level(R1csDev d, const uint32_t* cons, uint32_t count) {
+template <class FC>
+__global__ void __launch_bounds__(256) k_solve_level(R1csDev<FC> d, const uint32_t* cons, uint32_t count) {
+    using Fr = Fe<FC>;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= count) return;
     const uint32_t c = cons[i];
@@ -117,9 +124,10 @@ __global__ void __launch_bounds__(256) k_solve_level(R1csDev d, const uint32_t* 
 
 // W read around the (write-through, non-coherent) L1: within a strand kernel a
 // thread reads values it stored earlier in the same launch
-__device__ __forceinline__ Fr ldfr_l2(const Fr* p) {
+template <class F>
+__device__ __forceinline__ F ldfr_l2(const F* p) {
     const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
-    Fr r;
+    F r;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const uint64_t x = __hip_atomic_load(q + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -134,8 +142,10 @@ __device__ __forceinline__ Fr ldfr_l2(const Fr* p) {
 // term of each constraint is known statically (unk[c], ~0 = none), so no
 // solved flags are read inside the launch.  Dependencies on other strands were
 // solved by earlier launches.
-__global__ void __launch_bounds__(256) k_solve_strands(R1csDev d, const uint32_t* unk, const uint32_t* order,
+template <class FC>
+__global__ void __launch_bounds__(256) k_solve_strands(R1csDev<FC> d, const uint32_t* unk, const uint32_t* order,
                                                        const uint32_t* seg_start, uint32_t nseg) {
+    using Fr = Fe<FC>;
     const uint32_t sg = blockIdx.x * blockDim.x + threadIdx.x;
     if (sg >= nseg) return;
     // the last RC wires this thread produced, kept in registers: a chain reads
@@ -214,7 +224,10 @@ __global__ void __launch_bounds__(256) k_solve_strands(R1csDev d, const uint32_t
     }
 }
 
-__global__ void k_solver_init(Fr* W, uint8_t* solved, size_t nw, const Fr* inputs, size_t n_in, uint32_t* fail) {
+template <class FC>
+__global__ void k_solver_init(Fe<FC>* W, uint8_t* solved, size_t nw, const Fe<FC>* inputs, size_t n_in,
+                              uint32_t* fail) {
+    using Fr = Fe<FC>;
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) {
         fail[0] = 0xffffffffu;
@@ -241,6 +254,7 @@ using namespace gg;
 
 struct gg_r1cs {
     int device = 0;
+    int curve = GG_CURVE_BN254;  // scalar field: BN254 fr or BLS12-381 fr
     size_t nw = 0, ncons = 0, nterms = 0, ncoef = 0;
     uint32_t one_idx = 0xffffffffu;
     std::vector<uint32_t> level_off;  // host copy (launch sizes)
@@ -349,12 +363,29 @@ static bool build_strands(gg_r1cs* r, size_t n_in) {
     return true;
 }
 
-extern "C" int gg_r1cs_create(size_t n_wires, size_t n_constraints, const uint32_t* term_off,
-                              const uint32_t* term_wire, const uint32_t* term_coeff, const void* coeffs,
-                              size_t n_coeffs, const uint32_t* level_off, const uint32_t* level_cons,
-                              size_t n_levels, gg_r1cs_t* out) {
+// divByCoeff: host inverses of the coefficient table (0 for a zero coefficient)
+// and the index of the coefficient 1
+template <class FC>
+static uint32_t invert_coeffs(const void* coeffs, size_t n, std::vector<uint8_t>& out) {
+    using F = Fe<FC>;
+    const F* cf = (const F*)coeffs;
+    out.resize(n * 32);
+    F* inv = (F*)out.data();
+    uint32_t one_idx = 0xffffffffu;
+    for (size_t i = 0; i < n; i++) {
+        inv[i] = cf[i].is_zero() ? F::zero() : inverse(cf[i]);
+        if (one_idx == 0xffffffffu && cf[i] == F::one()) one_idx = (uint32_t)i;
+    }
+    return one_idx;
+}
+
+extern "C" int gg_r1cs_create_ex(int curve, size_t n_wires, size_t n_constraints, const uint32_t* term_off,
+                                 const uint32_t* term_wire, const uint32_t* term_coeff, const void* coeffs,
+                                 size_t n_coeffs, const uint32_t* level_off, const uint32_t* level_cons,
+                                 size_t n_levels, gg_r1cs_t* out) {
     GG_CAPI_BEGIN
     GG_CHECK(out && term_off && coeffs && level_off, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(curve == GG_CURVE_BN254 || curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "unknown curve");
     GG_CHECK(n_wires >= 1 && n_wires < 0xffffffffu && n_constraints < 0xffffffffu, GG_ERR_INVALID_ARG,
              "wire / constraint count out of range");
     GG_CHECK(n_coeffs >= 1 && n_coeffs < 0xffffffffu, GG_ERR_INVALID_ARG, "empty coefficient table");
@@ -381,17 +412,13 @@ extern "C" int gg_r1cs_create(size_t n_wires, size_t n_constraints, const uint32
             seen[c] = 1;
         }
     }
-    // divByCoeff: host inverses of the coefficient table (0 for a zero coefficient)
-    const Fr* cf = (const Fr*)coeffs;
-    std::vector<Fr> inv(n_coeffs);
-    uint32_t one_idx = 0xffffffffu;
-    for (size_t i = 0; i < n_coeffs; i++) {
-        inv[i] = cf[i].is_zero() ? Fr::zero() : inverse(cf[i]);
-        if (one_idx == 0xffffffffu && cf[i] == Fr::one()) one_idx = (uint32_t)i;
-    }
+    std::vector<uint8_t> inv;
+    const uint32_t one_idx = curve == GG_CURVE_BN254 ? invert_coeffs<FrCfg>(coeffs, n_coeffs, inv)
+                                                     : invert_coeffs<FrBlsCfg>(coeffs, n_coeffs, inv);
     auto* r = new gg_r1cs();
     try {
         GG_HIP(hipGetDevice(&r->device));
+        r->curve = curve;
         r->nw = n_wires;
         r->ncons = n_constraints;
         r->nterms = nterms;
@@ -427,6 +454,14 @@ extern "C" int gg_r1cs_create(size_t n_wires, size_t n_constraints, const uint32
     GG_CAPI_END
 }
 
+extern "C" int gg_r1cs_create(size_t n_wires, size_t n_constraints, const uint32_t* term_off,
+                              const uint32_t* term_wire, const uint32_t* term_coeff, const void* coeffs,
+                              size_t n_coeffs, const uint32_t* level_off, const uint32_t* level_cons,
+                              size_t n_levels, gg_r1cs_t* out) {
+    return gg_r1cs_create_ex(GG_CURVE_BN254, n_wires, n_constraints, term_off, term_wire, term_coeff, coeffs,
+                             n_coeffs, level_off, level_cons, n_levels, out);
+}
+
 extern "C" int gg_r1cs_release(gg_r1cs_t r) {
     delete r;
     return GG_OK;
@@ -443,8 +478,10 @@ extern "C" int gg_r1cs_info(gg_r1cs_t r, size_t* n_wires, size_t* n_constraints,
 
 // the per-level (or per-super-level strand) launches, enqueued on r->st
 // (recorded once into a graph)
-static void enqueue_levels(gg_r1cs* r) {
-    R1csDev d{r->off.as<uint32_t>(), r->wire.as<uint32_t>(), r->cidx.as<uint32_t>(), r->coef.as<Fr>(),
+template <class FC>
+static void enqueue_levels_t(gg_r1cs* r) {
+    using Fr = Fe<FC>;
+    R1csDev<FC> d{r->off.as<uint32_t>(), r->wire.as<uint32_t>(), r->cidx.as<uint32_t>(), r->coef.as<Fr>(),
               r->coef_inv.as<Fr>(), (uint32_t)r->ncoef, r->one_idx, (uint32_t)(r->strand_nin + 1), r->W.as<Fr>(),
               r->A.as<Fr>(), r->B.as<Fr>(),
               r->C.as<Fr>(), r->solved.as<uint8_t>(), r->fail.as<uint32_t>()};
@@ -452,7 +489,7 @@ static void enqueue_levels(gg_r1cs* r) {
         for (size_t l = 0; l < r->n_super; l++) {
             const uint32_t a = r->sl_seg_off[l], cnt = r->sl_seg_off[l + 1] - a;
             if (!cnt) continue;
-            hipLaunchKernelGGL(k_solve_strands, dim3(grid_for(cnt, 256)), dim3(256), 0, r->st, d,
+            hipLaunchKernelGGL(k_solve_strands<FC>, dim3(grid_for(cnt, 256)), dim3(256), 0, r->st, d,
                                r->unk.as<uint32_t>(), r->order.as<uint32_t>(), r->seg_start.as<uint32_t>() + a,
                                cnt);
             GG_HIP(hipGetLastError());
@@ -463,9 +500,13 @@ static void enqueue_levels(gg_r1cs* r) {
     for (size_t l = 0; l + 1 < r->level_off.size(); l++) {
         const uint32_t a = r->level_off[l], cnt = r->level_off[l + 1] - a;
         if (!cnt) continue;
-        hipLaunchKernelGGL(k_solve_level, dim3(grid_for(cnt, 256)), dim3(256), 0, r->st, d, lc + a, cnt);
+        hipLaunchKernelGGL(k_solve_level<FC>, dim3(grid_for(cnt, 256)), dim3(256), 0, r->st, d, lc + a, cnt);
         GG_HIP(hipGetLastError());
     }
+}
+static void enqueue_levels(gg_r1cs* r) {
+    if (r->curve == GG_CURVE_BN254) enqueue_levels_t<FrCfg>(r);
+    else enqueue_levels_t<FrBlsCfg>(r);
 }
 
 extern "C" int gg_r1cs_solve(gg_r1cs_t r, const void* witness, size_t n_witness, int witness_on_device,
@@ -478,14 +519,19 @@ extern "C" int gg_r1cs_solve(gg_r1cs_t r, const void* witness, size_t n_witness,
     std::lock_guard<std::mutex> lk(r->mu);
     GG_HIP(hipSetDevice(r->device));
     if (unsatisfied) *unsatisfied = -1;
-    const Fr* in = (const Fr*)witness;
+    const void* in = witness;
     if (n_witness && !witness_on_device) {
         r->inputs.reserve(n_witness * 32);
         GG_HIP(hipMemcpyAsync(r->inputs.p, witness, n_witness * 32, hipMemcpyHostToDevice, r->st));
-        in = r->inputs.as<Fr>();
+        in = r->inputs.p;
     }
-    hipLaunchKernelGGL(k_solver_init, dim3(grid_for(r->nw, 256)), dim3(256), 0, r->st, r->W.as<Fr>(),
-                       r->solved.as<uint8_t>(), r->nw, in, n_witness, r->fail.as<uint32_t>());
+    if (r->curve == GG_CURVE_BN254)
+        hipLaunchKernelGGL(k_solver_init<FrCfg>, dim3(grid_for(r->nw, 256)), dim3(256), 0, r->st, r->W.as<Fr>(),
+                           r->solved.as<uint8_t>(), r->nw, (const Fr*)in, n_witness, r->fail.as<uint32_t>());
+    else
+        hipLaunchKernelGGL(k_solver_init<FrBlsCfg>, dim3(grid_for(r->nw, 256)), dim3(256), 0, r->st,
+                           r->W.as<FrBls>(), r->solved.as<uint8_t>(), r->nw, (const FrBls*)in, n_witness,
+                           r->fail.as<uint32_t>());
     GG_HIP(hipGetLastError());
     // schedule: strands when the levels allow it (GG_SOLVER_LEVELS=1: level launches)
     if (r->strand_nin != (long long)n_witness) {

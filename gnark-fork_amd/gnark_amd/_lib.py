@@ -123,6 +123,7 @@ def _load():
         "gg_plonk_prove": ([P, P, P, P, I, P, S, PP, P, P, I, P, HASH_FN, P, HASH_FN, P, P, S], I),
         "gg_plonk_last_timings": ([ctypes.POINTER(ctypes.c_double), I], I),
         "gg_r1cs_create": ([S, S, P, P, P, P, S, P, P, S, PP], I),
+        "gg_r1cs_create_ex": ([I, S, S, P, P, P, P, S, P, P, S, PP], I),
         "gg_r1cs_release": ([P], I),
         "gg_r1cs_info": ([P, ctypes.POINTER(S), ctypes.POINTER(S), ctypes.POINTER(S)], I),
         "gg_r1cs_solve": ([P, P, S, I, P, P, P, P, I, ctypes.POINTER(ctypes.c_int64)], I),
@@ -166,7 +167,7 @@ EXPORTED = [
     "gg_plonk_last_timings", "gg_groth16_pk_create_ex", "gg_groth16_finalize_ex",
     "gg_bls12_381_g2_jac_to_affine", "gg_bls12_381_g2_jac_add", "gg_bls12_381_g2_scalar_mul",
     "gg_groth16_mpk_create", "gg_groth16_mpk_release", "gg_groth16_mpk_info", "gg_groth16_mpk_prove",
-    "gg_groth16_mpk_last_timings", "gg_r1cs_create", "gg_r1cs_release", "gg_r1cs_info", "gg_r1cs_solve",
+    "gg_groth16_mpk_last_timings", "gg_r1cs_create", "gg_r1cs_create_ex", "gg_r1cs_release", "gg_r1cs_info", "gg_r1cs_solve",
     "gg_r1cs_solution_dev", "gg_scs_create", "gg_scs_release", "gg_scs_info", "gg_scs_solve",
     "gg_scs_solution_dev",
 ]

@@ -62,7 +62,12 @@ class R1CS:
     """Device-resident R1CS (gg_r1cs_create) with its solver."""
 
     def __init__(self, nb_public: int, nb_secret: int, n_wires: int, term_off, term_wire, term_coeff,
-                 coeffs: Sequence[int], levels: Optional[Sequence[Sequence[int]]] = None):
+                 coeffs: Sequence[int], levels: Optional[Sequence[Sequence[int]]] = None,
+                 curve: str = "bn254"):
+        from ._lib import GG_CURVE_BN254, GG_CURVE_BLS12_381
+        self.curve = curve
+        self.mod = fr.R if curve == "bn254" else fr.BLS_R
+        self._mont = fr.fr_mont if curve == "bn254" else fr.bls_fr_mont
         self.nb_public, self.nb_secret, self.n_wires = nb_public, nb_secret, n_wires
         self.term_off = np.ascontiguousarray(term_off, dtype=np.uint32)
         self.term_wire = np.ascontiguousarray(term_wire, dtype=np.uint32)
@@ -75,22 +80,25 @@ class R1CS:
         lo[1:] = np.cumsum([len(x) for x in levels])
         lc = np.ascontiguousarray(np.concatenate([np.asarray(x, dtype=np.uint32) for x in levels])
                                   if levels else np.zeros(0, dtype=np.uint32), dtype=np.uint32)
-        cbytes = b"".join(fr.fr_mont(int(k) % fr.R) for k in coeffs)
+        cbytes = b"".join(self._mont(int(k) % self.mod) for k in coeffs)
         h = ctypes.c_void_p()
-        check(lib.gg_r1cs_create(n_wires, self.n_constraints, ptr(self.term_off), ptr(self.term_wire),
-                                 ptr(self.term_coeff), ptr(cbytes), len(coeffs), ptr(lo), ptr(lc),
-                                 len(levels), ctypes.byref(h)))
+        check(lib.gg_r1cs_create_ex(GG_CURVE_BN254 if curve == "bn254" else GG_CURVE_BLS12_381, n_wires,
+                                    self.n_constraints, ptr(self.term_off), ptr(self.term_wire),
+                                    ptr(self.term_coeff), ptr(cbytes), len(coeffs), ptr(lo), ptr(lc),
+                                    len(levels), ctypes.byref(h)))
         self.handle = h
 
     @classmethod
-    def from_terms(cls, nb_public: int, nb_secret: int, n_wires: int, constraints, levels=None) -> "R1CS":
+    def from_terms(cls, nb_public: int, nb_secret: int, n_wires: int, constraints, levels=None,
+                   curve: str = "bn254") -> "R1CS":
         """constraints: [(L, R, O)] with L = [(wire, coeff int), ...]."""
+        mod = fr.R if curve == "bn254" else fr.BLS_R
         table, index = [], {}
         off, wires, cids = [0], [], []
         for L, R, O in constraints:
             for side in (L, R, O):
                 for w, k in side:
-                    k %= fr.R
+                    k %= mod
                     if k not in index:
                         index[k] = len(table)
                         table.append(k)
@@ -99,7 +107,7 @@ class R1CS:
                 off.append(len(wires))
         if not table:
             table = [1]
-        return cls(nb_public, nb_secret, n_wires, off, wires, cids, table, levels)
+        return cls(nb_public, nb_secret, n_wires, off, wires, cids, table, levels, curve)
 
     def info(self):
         a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
@@ -118,7 +126,7 @@ class R1CS:
         elif isinstance(witness, (bytes, bytearray)):
             wbuf = bytes(witness)
         else:
-            wbuf = b"".join(fr.fr_mont(int(v) % fr.R) for v in witness)
+            wbuf = b"".join(self._mont(int(v) % self.mod) for v in witness)
             if len(witness) != n_in:
                 raise ValueError("invalid witness size, got %d, expected %d" % (len(witness), n_in))
         if not wdev and len(wbuf) != 32 * n_in:

@@ -497,6 +497,12 @@ int gg_r1cs_create(size_t n_wires, size_t n_constraints, const uint32_t *term_of
                    const uint32_t *term_wire, const uint32_t *term_coeff, const void *coeffs,
                    size_t n_coeffs, const uint32_t *level_off, const uint32_t *level_cons,
                    size_t n_levels, gg_r1cs_t *out);
+/* the same for curve GG_CURVE_BN254 or GG_CURVE_BLS12_381 (the scalar field of
+ * backend/groth16/bls12-381, whose solver is constraint/bls12-381/solver.go) */
+int gg_r1cs_create_ex(int curve, size_t n_wires, size_t n_constraints, const uint32_t *term_off,
+                      const uint32_t *term_wire, const uint32_t *term_coeff, const void *coeffs,
+                      size_t n_coeffs, const uint32_t *level_off, const uint32_t *level_cons,
+                      size_t n_levels, gg_r1cs_t *out);
 int gg_r1cs_release(gg_r1cs_t r);
 int gg_r1cs_info(gg_r1cs_t r, size_t *n_wires, size_t *n_constraints, size_t *n_levels);
 int gg_r1cs_solve(gg_r1cs_t r, const void *witness, size_t n_witness, int witness_on_device,

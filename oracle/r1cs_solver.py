@@ -50,8 +50,9 @@ def levels_of(nb_inputs, constraints):
     return out
 
 
-def solve(nb_wires, nb_inputs, constraints, witness, levels):
-    """witness: the nb_inputs - 1 values after ONE_WIRE."""
+def solve(nb_wires, nb_inputs, constraints, witness, levels, R=R):
+    """witness: the nb_inputs - 1 values after ONE_WIRE (R: the scalar field,
+    BN254 by default; constraint/bls12-381/solver.go is the same code)."""
     W = [0] * nb_wires
     solved = [False] * nb_wires
     W[0], solved[0] = 1, True
@@ -101,7 +102,7 @@ def solve(nb_wires, nb_inputs, constraints, witness, levels):
     return W, A, B, C
 
 
-def random_circuit(rng, nb_public, nb_secret, n_internal, zero_divisor=False):
+def random_circuit(rng, nb_public, nb_secret, n_internal, zero_divisor=False, R=R):
     """A random R1CS the frontend could emit: every constraint introduces one new
     internal wire on a random side (L, R or O) with a random coefficient, next
     to up to two solved terms per side; with zero_divisor, some constraints

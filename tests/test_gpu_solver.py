@@ -211,3 +211,21 @@ def test_gpu_solver_strand_and_level_schedules_agree(levels_only, monkeypatch):
     gW, gA, gB, gC = _host(sys_.solve(wit))
     assert _fr_list(gW) == W and _fr_list(gC) == C
     sys_.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,zero", [(5, False), (6, True)])
+def test_gpu_solver_bls12_381(seed, zero):
+    """gg_r1cs_create_ex(GG_CURVE_BLS12_381): backend/groth16/bls12-381's solver
+    (constraint/bls12-381/solver.go), bit-exact vs the oracle over r_BLS."""
+    from gnark_amd import fr, solver
+    Rb = fr.BLS_R
+    rng = random.Random(seed)
+    cons = rs.random_circuit(rng, 3, 4, 300, zero_divisor=zero, R=Rb)
+    wit = [rng.randrange(Rb) for _ in range(6)]
+    W, A, B, C = rs.solve(307, 7, cons, wit, rs.levels_of(7, cons), R=Rb)
+    sys_ = solver.R1CS.from_terms(3, 4, 307, cons, curve="bls12-381")
+    gW, gA, gB, gC = _host(sys_.solve(wit))
+    vals = lambda b: [fr.bls_fr_unmont(bytes(b)[i:i + 32]) for i in range(0, len(b), 32)]
+    assert vals(gW) == W and vals(gA) == A and vals(gB) == B and vals(gC) == C
+    sys_.close()
