@@ -88,6 +88,7 @@ func (pk *ProvingKey) setupDevicePointers(nbPublic int, kWireIndex []uint32) err
 // Release frees the HBM-resident key (the icicle path never frees it).
 func (pk *ProvingKey) Release() {
 	if pk.deviceInfo != nil {
+		pk.deviceInfo.solver.release()
 		C.gg_groth16_pk_release(C.gg_groth16_pk_t(pk.deviceInfo.handle))
 		pk.deviceInfo = nil
 	}
@@ -167,6 +168,39 @@ func Prove(r1cs *cs.R1CS, pk *ProvingKey, fullWitness witness.Witness, opts ...b
 		solverOpts = append(solverOpts,
 			solver.OverrideHint(r1cs.GkrInfo.SolveHintID, cs.GkrSolveHint(r1cs.GkrInfo, &gkrData)),
 			solver.OverrideHint(r1cs.GkrInfo.ProveHintID, cs.GkrProveHint(r1cs.GkrInfo.HashName, &gkrData)))
+	}
+
+	// hint-free systems without commitments: r1cs.Solve on the GPU over
+	// BLS12-381 fr (gg_r1cs_create_ex), the solution stays in HBM (solver_amd.go)
+	if len(commitmentInfo) == 0 && len(opt.SolverOpts) == 0 && !r1cs.GkrInfo.Is() {
+		if !pk.deviceInfo.solverTried {
+			pk.deviceInfo.solverTried = true
+			if pk.deviceInfo.solver, err = newDeviceSolver(r1cs); err != nil {
+				return nil, fmt.Errorf("device solver: %w", err)
+			}
+		}
+		if ds := pk.deviceInfo.solver; ds != nil {
+			w, a, b, c, err := ds.solve(fullWitness)
+			if err != nil {
+				return nil, err
+			}
+			var r, s fr.Element
+			if _, err := r.SetRandom(); err != nil {
+				return nil, err
+			}
+			if _, err := s.SetRandom(); err != nil {
+				return nil, err
+			}
+			var ar, krs curve.G1Affine
+			var bs curve.G2Affine
+			if C.gg_groth16_prove(C.gg_groth16_pk_t(pk.deviceInfo.handle), w, C.size_t(ds.nbWires), a, b, c,
+				C.size_t(ds.nbCons), 1, unsafe.Pointer(&r), unsafe.Pointer(&s),
+				unsafe.Pointer(&ar), unsafe.Pointer(&bs), unsafe.Pointer(&krs), nil) != C.GG_OK {
+				return nil, lastError()
+			}
+			proof.Ar, proof.Bs, proof.Krs = ar, bs, krs
+			return proof, nil
+		}
 	}
 
 	_solution, err := r1cs.Solve(fullWitness, solverOpts...)

@@ -20,3 +20,6 @@ func Prove(r1cs *cs.R1CS, pk *ProvingKey, fullWitness witness.Witness, opts ...b
 
 // Release frees the HBM-resident key (no-op without the build tag).
 func (pk *ProvingKey) Release() {}
+
+// deviceSolver exists only with the build tag (solver_amd.go); deviceInfo names it.
+type deviceSolver struct{}

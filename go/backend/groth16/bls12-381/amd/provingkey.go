@@ -15,7 +15,9 @@ import (
 
 // deviceInfo holds the HBM-resident proving key (gg_groth16_pk_t).
 type deviceInfo struct {
-	handle unsafe.Pointer
+	handle      unsafe.Pointer
+	solver      *deviceSolver // GPU r1cs.Solve (nil: the system has hints)
+	solverTried bool
 }
 
 // ProvingKey embeds the CPU key so WriteTo/ReadFrom/... are promoted unchanged
