@@ -143,6 +143,12 @@ def test_groth16_bls12_381_bit_exact(log_n):
     dev = [DeviceBuffer.from_host(frv(x)) for x in (w, A, B, C)]
     pr2 = groth16.prove(pk, groth16.Solution(*dev, nw, len(cons), on_device=True), opt, r=frb(r), s=frb(s))
     assert (pr2.Ar, pr2.Bs, pr2.Krs) == (pr.Ar, pr.Bs, pr.Krs)
+    # the same witness solved on the GPU over BLS12-381 fr (gg_r1cs_create_ex), proved from HBM
+    from gnark_amd import solver
+    sys_ = solver.R1CS.from_terms(1, chains, nw, cons, curve="bls12-381")
+    pr4 = groth16.prove(pk, sys_.solve(w[1:1 + chains]), opt, r=frb(r), s=frb(s))
+    assert (pr4.Ar, pr4.Bs, pr4.Krs) == (pr.Ar, pr.Bs, pr.Krs)
+    sys_.close()
     bad = list(w)
     bad[-1] = (bad[-1] + 1) % R
     pr3 = groth16.prove(pk, groth16.Solution(frv(bad), frv(A), frv(B), frv(C), nw, len(cons)), opt,
