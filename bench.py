@@ -36,6 +36,7 @@ sys.path.insert(0, os.path.join(ROOT, "gnark-fork_amd"))
 METRIC = ("Groth16 prove time + MSM G1 throughput (Mscalar-mul/s) BN254 2^24 R1CS, 1/2/4/8 GPU")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FPMUL_PEAK_G = 135.7  # measured BN254 Fp Montgomery multiplies/s (G), profiles/r01_v2_mbench_field.txt
+VALU_ISSUE_CAP = 0.22  # wave-instructions / SIMD-cycle of the ~60 %-mad mix (profiles/r02_mbench_field29_v2.txt)
 MIMC_ROUNDS = 85      # 3 constraints per round; 2^(log_n-8) chains -> 255 * 2^(log_n-8) constraints
 ROOFLINE_PROVES = 3   # serial proves timed kernel by kernel for the roofline
 
@@ -114,14 +115,40 @@ def main():
                     help="seconds allowed for the extra measurements after the headline; past it "
                          "the headline line is printed with the extras marked timed out and the "
                          "process exits (a stuck collective never swallows the headline)")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="host threads of the CPU baseline (0 = every core this process may run on, "
+                         "len(os.sched_getaffinity(0)))")
+    ap.add_argument("--launcher", choices=("auto", "torch", "mpk"), default="auto",
+                    help="N > 1: 'mpk' = ONE process driving the N GPUs through gg_groth16_mpk_* (the Go "
+                         "shape: SetDevices, in-library peer copies over xGMI); 'torch' = one process per GPU "
+                         "under torch.distributed.run (RCCL).  auto: torch when launched by torchrun "
+                         "(WORLD_SIZE > 1), else mpk")
+    ap.add_argument("--devices", default=None,
+                    help="one-process path: comma-separated GPU id per key shard (default 0..N-1); ids may "
+                         "repeat to rehearse N shards on fewer GPUs (n_gpus = distinct ids)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if env_world > 1 or args.launcher == "torch":
+        if env_world != args.gpus:
+            raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={env_world} ranks "
+                             f"(--launcher torch runs one process per GPU under torch.distributed.run)")
+        mode, world, devices = "torch", env_world, None
+    elif args.gpus > 1 or args.devices:
+        devices = [int(x) for x in args.devices.split(",")] if args.devices else list(range(args.gpus))
+        if len(devices) != args.gpus:
+            raise SystemExit(f"bench: --gpus {args.gpus} but {len(devices)} devices listed")
+        mode, world = "mpk", 1
+    else:
+        mode, world, devices = "single", 1, None
     import torch
     from gnark_amd import _lib
+    if mode == "mpk":
+        ndev = torch.cuda.device_count()
+        if max(devices) >= ndev:
+            raise SystemExit(f"bench: devices {devices} but {ndev} GPU(s) visible")
 
     # one process per GPU over RCCL ("nccl").  GG_DIST_BACKEND=gloo is a rehearsal
     # mode only (ranks may share a GPU; partials travel through host memory).
@@ -156,9 +183,11 @@ def main():
     # solution (W, A, B, C) already resident in HBM when the timed region starts;
     # the same prove from host memory (PCIe H2D inside the step) is timed beside it.
     t0 = time.time()
-    g = Groth16Bench(args.log_n, rank, world, dist, xdev, host_inputs=args.host_inputs)
+    g = Groth16Bench(args.log_n, rank, world, dist, xdev, host_inputs=args.host_inputs, devices=devices)
     log(f"[rank {rank}] key ready: 2^{args.log_n}, {g.shape['ncons']} constraints, "
         f"{g.shape['nw']} wires ({time.time() - t0:.1f}s)")
+    n_gpus = len(set(devices)) if mode == "mpk" else world
+    n_shards = len(devices) if mode == "mpk" else world
     import gc
 
     def timed_proves(steps, warmup):
@@ -199,7 +228,7 @@ def main():
     value = ncons * args.steps / el  # constraints/s of the whole job (one proof per step)
     same = g.proof_identical_on_all_ranks()
     other = None
-    if world == 1:  # the other input placement, same key, same step count
+    if world == 1:  # the other input placement, same key, same step count (also N GPUs in one process)
         g.sol = g.sol_dev if args.host_inputs else g.sol_host
         o_el, o_steps, o_slow, o_stage = timed_proves(args.steps, 1)
         other = {"inputs": "device" if args.host_inputs else "host",
@@ -227,45 +256,22 @@ def main():
     for name in ("msm_sort", "msm_accum", "msm_accum_g2", "msm_accum2", "msm_reduce", "ntt_pass"):
         tot, cnt, units = _lib.profile_get(name)
         kernels[name] = {"avg_ms": tot / cnt if cnt else None, "launches_per_proof": cnt / ROOFLINE_PROVES,
-                         "total_ms_per_proof": tot / ROOFLINE_PROVES}
+                         "total_ms_per_proof": tot / ROOFLINE_PROVES, "units_per_launch": units / cnt if cnt else None}
     _lib.profile_enable(False)
-    nB2 = g.nB2
-    g2_ms = kernels["msm_accum_g2"]["avg_ms"]
-    alg_bytes = nB2 * (128 + 32)  # |B2| x (G2 affine 128 B + fr 32 B)
-    achieved = alg_bytes / (g2_ms * 1e-3) / 1e9 if g2_ms else None
-    traffic, traffic_note = pmc_traffic("k_accum_range<gg::Fp2>", {"workload": "groth16", "log_n": args.log_n,
-                                                                    "n_gpus": world})
-    roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                "traffic_note": traffic_note,
-                "kernel": "k_accum_range<Fp2> (G2 bucket accumulation of the B MSM: the longest "
-                          "single launch of the prove)",
-                "algorithmic_bytes_per_launch": alg_bytes, "kernel_avg_ms": g2_ms,
-                "timing": "HIP events on the kernel's launch stream over %d proves run task by task "
-                          "(the last %d launches of the kernel in the run; rocprof summary: "
-                          "profiles/r02_*_kernel_stats.md, 'last %d' column)" % ((ROOFLINE_PROVES,) * 3),
-                "note": "EC MSM is VALU-integer bound (SURVEY 8d); HBM fraction reported as required"}
-    if g2_ms:
-        W2 = g.g2_windows
-        mul_rate = nB2 * W2 * 10 * 3 / (g2_ms * 1e-3) / 1e9  # Fp2 mul ~ 3 Fp mul (Karatsuba)
-        roofline["valu"] = {"achieved_Gfpmul_s": mul_rate, "peak_Gfpmul_s": FPMUL_PEAK_G,
-                            "frac": mul_rate / FPMUL_PEAK_G,
-                            "basis": "|B2| x W mixed XYZZ adds x 10 Fp2-mul x 3 Fp-mul (Karatsuba); the "
-                                     "radix-2^29 form does a product in fewer instructions than the 32-bit "
-                                     "limb multiply the peak was measured with, hence frac > 1"}
-        sq = pmc_sq("k_accum_range<gg::Fp2>", {"workload": "groth16", "log_n": args.log_n, "n_gpus": world})
-        if sq:
-            # VALU issue rate: wave instructions per SIMD cycle (1024 SIMDs, 2.4 GHz);
-            # the instruction mix (~60 % v_mad_u64_u32 at ~5.5 cycles, the rest ~3.1)
-            # caps it at ~0.22 on gfx950 (profiles/r02_mbench_field29_v2.txt)
-            ipc = sq["valu_insts"] / (g2_ms * 1e-3 * 2.4e9 * 1024)
-            roofline["valu"]["pmc"] = {"valu_insts_per_launch": sq["valu_insts"],
-                                       "insts_per_madd_per_lane": sq["valu_insts"] * 64 / (nB2 * W2),
-                                       "insts_per_simd_cycle": ipc, "issue_cap_for_mix": 0.22,
-                                       "source": sq["source"]}
+    wl = {"workload": "groth16", "log_n": args.log_n, "n_gpus": n_shards}
+    # dominant kernel per proof: the G1 bucket accumulation (4 launches: A, B1, K, Z);
+    # the G2 accumulation (the longest single launch) is the second entry
+    r_g1 = accum_roofline(kernels["msm_accum"], 64, "k_accum_range<gg::Fe<gg::FpCfg> >", wl,
+                          "k_accum_range<Fe<FpCfg>> (BN254 G1 bucket accumulation, radix-2^29 XYZZ mixed adds: "
+                          "the A, B1, K and Z MSMs -- the largest share of each proof)", g.g1_windows)
+    r_g2 = accum_roofline(kernels["msm_accum_g2"], 128, "k_accum_range<gg::Fp2>", wl,
+                          "k_accum_range<Fp2> (BN254 G2 bucket accumulation of the B MSM: the longest single "
+                          "launch of the prove)", g.g2_windows)
+    roofline = dict(r_g1)
+    roofline["others"] = [r_g2]
 
     out = {
-        "metric": METRIC, "value": value, "unit": "constraints/s", "n_gpus": world,
+        "metric": METRIC, "value": value, "unit": "constraints/s", "n_gpus": n_gpus,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
         "step_ms": [round(x, 2) for x in step_ms], "slow_steps": slow_steps,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
@@ -281,10 +287,24 @@ def main():
                    "log_n": args.log_n, "n_constraints": ncons, "n_wires": g.shape["nw"],
                    "inputs": "host" if args.host_inputs else "device",
                    "parallelism": ("key shard x%d (wires + Z positions), distributed computeH "
-                                   "(3 RCCL all-to-alls), RCCL all-gather of 576-B partials" % world)
-                   if world > 1 else "one GPU, 5 concurrent HIP streams"},
+                                   "(3 RCCL all-to-alls), RCCL all-gather of 576-B partials; one process per "
+                                   "GPU (torch.distributed.run)" % world) if mode == "torch" else
+                                  ("key shard x%d on devices %s (wires + Z positions), distributed computeH "
+                                   "(3 all-to-alls as in-library xGMI peer copies), partials summed in the "
+                                   "library; ONE process (gg_groth16_mpk_*, the Go shape)"
+                                   % (n_shards, devices)) if mode == "mpk" else
+                                  "one GPU, 5 concurrent HIP streams",
+                   "launcher": mode, "shards": n_shards},
         "prove_ms": ms_per_step, "stage_ms": stage, "proof_identical_on_all_ranks": same,
         "other_inputs": other,
+        "product_paths": {
+            "value": "solution resident in HBM: the drop-in's path for hint-free circuits, whose R1CS the "
+                     "GPU solver (gg_r1cs_solve) solves in place (Go shim solver_amd.go)" if not args.host_inputs
+                     else "solution in host memory: the path of circuits with hints (gnark's CPU solver hands "
+                          "W, A, B, C over; PCIe upload inside the step)",
+            "other_inputs": "the other placement of the same key and solution (see its note)",
+            "solver.witness_to_proof_ms": "witness (host, 2 MB) -> GPU solve -> proof from HBM: the end-to-end "
+                                          "time of the hint-free path"},
         "roofline": roofline, "kernels": kernels,
     }
 
@@ -311,7 +331,7 @@ def main():
 
     # ---- the same prove with the five tasks one after another (isolated stage
     # times), and with the solution already in HBM (upload cost), N = 1 only
-    if world == 1 and not args.no_variants:
+    if mode == "single" and not args.no_variants:
         try:
             out["groth16_variants"] = g.variants()
         except Exception as e:  # report, never hide
@@ -319,7 +339,7 @@ def main():
     # ---- the R1CS solver on the GPU feeding the same prove:
     # witness in host memory -> solution in HBM -> proof (N = 1)
     stage_now["now"] = "solver"
-    if world == 1 and args.solver:
+    if mode == "single" and args.solver:
         try:
             out["solver"] = solver_bench(g, args.log_n)
         except Exception as e:  # report, never hide
@@ -339,7 +359,7 @@ def main():
 
     # ---- Fr NTT 2^24 (BASELINE configs[2]; rank 0 / N = 1 only)
     stage_now["now"] = "ntt"
-    if rank == 0 and world == 1 and args.ntt_log_n:
+    if mode == "single" and args.ntt_log_n:
         try:
             out["ntt"] = ntt_bench(args.ntt_log_n)
         except Exception as e:  # report, never hide
@@ -347,7 +367,7 @@ def main():
 
     # ---- PlonK BLS12-381 hot ops (BASELINE configs[4] sizes; rank 0 / N = 1 only)
     stage_now["now"] = "plonk"
-    if rank == 0 and world == 1 and args.plonk_log_n:
+    if mode == "single" and args.plonk_log_n:
         try:
             out["plonk_bls12_381"] = plonk_bench(args.plonk_log_n)
         except Exception as e:  # report, never hide
@@ -366,7 +386,7 @@ def main():
 
     # ---- CPU baseline (oracle restatement on the host cores), rank 0 at N = 1
     stage_now["now"] = "cpu_baseline"
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if mode == "single" and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.cpu_threads, ms_per_step, ncons)
         except Exception as e:
@@ -383,11 +403,12 @@ class Groth16Bench:
     """A resident 2^log_n Groth16 key (whole key at N = 1, this rank's shard at
     N > 1) of the MiMC-chain shape, and the host (or device) solution vectors."""
 
-    def __init__(self, log_n, rank, world, dist, xdev, host_inputs=True):
+    def __init__(self, log_n, rank, world, dist, xdev, host_inputs=True, devices=None):
         import numpy as np
         import torch
         from gnark_amd import backend, groth16, msm, DeviceBuffer
         self.log_n, self.rank, self.world, self.dist, self.xdev = log_n, rank, world, dist, xdev
+        self.devices = devices  # one process, N GPUs (gg_groth16_mpk_*)
         self.shape = sh = mimc_shape(log_n)
         n, nw, nbp = 1 << log_n, sh["nw"], sh["nb_public"]
         infA, infB = sh["infA"], sh["infB"]
@@ -407,8 +428,12 @@ class Groth16Bench:
             self.data = groth16.ProvingKeyData(
                 log_n=log_n, g1_A=g1pts(nA, sd + 1), g1_B=g1pts(nB, sd + 2), g1_Z=g1pts(n - 1, sd + 3),
                 g1_K=g1pts(nw - nbp, sd + 4), g2_B=g2pts(nB, sd + 8), **common)
-            self.pk = groth16.ProvingKey(self.data)
-            self.nB2 = nB
+            if devices:
+                self.pk = groth16.MultiGpuProvingKey(self.data, devices)
+                self.nB2 = self.pk.base_info(groth16.BASE_B2)[0]
+            else:
+                self.pk = groth16.ProvingKey(self.data)
+                self.nB2 = nB
         else:
             lo, hi, zl, zh = groth16.shard_ranges(nw, n, rank, world)
             nA = int((infA[lo:hi] == 0).sum())
@@ -430,17 +455,23 @@ class Groth16Bench:
         ncons = sh["ncons"]
         self.host = [rand_scalars(nw, 11)] + [rand_scalars(ncons, 12 + i) for i in range(3)]
         self.sol_host = groth16.Solution(*self.host, nw, ncons)
-        self.dev = [DeviceBuffer.from_host(x.tobytes()) for x in self.host]
-        self.sol_dev = groth16.Solution(*self.dev, nw, ncons, on_device=True)
+        if devices:  # the solution resident on every GPU (as per-device GPU solves leave it)
+            self.sol_dev = groth16.replicate_solution(self.sol_host, devices)
+        else:
+            self.dev = [DeviceBuffer.from_host(x.tobytes()) for x in self.host]
+            self.sol_dev = groth16.Solution(*self.dev, nw, ncons, on_device=True)
         self.sol = self.sol_host if host_inputs else self.sol_dev
         self.opt = backend.with_amd_acceleration()
         self.r, self.s = fr_const(12345), fr_const(67890)
         self.last = None
         self.g2_windows = self.pk.base_info(groth16.BASE_B2)[2]
+        self.g1_windows = self.pk.base_info(groth16.BASE_A)[2]
 
     def prove(self):
         from gnark_amd import groth16
-        if self.world == 1:
+        if self.devices:
+            self.last = self.pk.prove(self.sol, self.opt, r=self.r, s=self.s)
+        elif self.world == 1:
             self.last = groth16.prove(self.pk, self.sol, self.opt, r=self.r, s=self.s)
         else:
             self.last = groth16.prove_distributed_h(self.pk, self.hs, self.xchg, self.sol, self.opt,
@@ -449,6 +480,8 @@ class Groth16Bench:
 
     def timings(self):
         from gnark_amd import groth16
+        if self.devices:
+            return self.pk.last_timings()
         return groth16.last_timings()
 
     def proof_identical_on_all_ranks(self):
@@ -598,13 +631,56 @@ def msm_bench(log_n, rank, world, dist, xdev, barrier, max_over_ranks, steps=20,
     if acc:
         alg = n * 96
         traffic, note = pmc_traffic("k_accum_range<gg::Fe<gg::FpCfg> >",
-                                    {"log_n": log_n, "window_bits": c, "windows": W})
+                                    {"log_n": log_n, "window_bits": c, "windows": W}, 64)
         res["accum_roofline"] = {"achieved_GBps": alg / (acc * 1e-3) / 1e9,
                                  "frac_hbm": alg / (acc * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                  "traffic_bytes": traffic, "traffic_note": note,
-                                 "valu_Gfpmul_s": n * W * 10 / (acc * 1e-3) / 1e9,
-                                 "valu_frac": n * W * 10 / (acc * 1e-3) / 1e9 / FPMUL_PEAK_G}
+                                 "fpmul_equiv_G_per_s": n * W * 10 / (acc * 1e-3) / 1e9}
     return res
+
+
+def accum_roofline(k, pt_bytes, kernel, workload, desc, windows):
+    """Roofline entry of a bucket-accumulation kernel from its HIP-event profile
+    (k: bench `kernels` entry).  achieved = SURVEY 8(d) algorithmic bytes (one
+    point + one 32-B scalar per MSM unit) x units per launch / average launch
+    time.  traffic: the committed PMC profile of the same workload, FETCH_SIZE
+    scaled by the width calibration of the kernel's point gathers; the design
+    bytes (W windows x units x point bytes + 4-B sorted entries) printed beside
+    it.  valu: the SQ-counter issue rate against the measured ceiling of the
+    kernel's instruction mix."""
+    ms, units = k.get("avg_ms"), k.get("units_per_launch")
+    if not ms or not units:
+        return {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
+                "traffic": None, "kernel": desc}
+    alg = units * (pt_bytes + 32)
+    achieved = alg / (ms * 1e-3) / 1e9
+    design = units * windows * (pt_bytes + 4)
+    traffic, note = pmc_traffic(kernel, workload, pt_bytes)
+    r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_note": note,
+         "design_bytes_per_launch": design,
+         "design_bytes_note": "W x units x (point bytes + 4-B sorted entry): the fixed-base tables hold a "
+                              "window-shifted copy of every point per window (no doublings at prove time), "
+                              "so the kernel reads ~W x the point bytes of an MSM unit",
+         "kernel": desc, "algorithmic_bytes_per_launch": alg, "units_per_launch": units, "windows": windows,
+         "kernel_avg_ms": ms,
+         "timing": "HIP events on the kernel's launch stream over %d proves run task by task (rocprof summary of "
+                   "the same workload: profiles/r03_*groth16_2p24_kernel_stats.md)" % ROOFLINE_PROVES,
+         "note": "EC MSM is VALU-integer bound (SURVEY 8d); the HBM fraction is reported as required, the "
+                 "issue-rate fraction below is the kernel's real ceiling"}
+    sq = pmc_sq(kernel, workload)
+    if sq:
+        # VALU issue rate: wave instructions per SIMD cycle (1024 SIMDs at 2.4 GHz);
+        # ~60 % of the mix is v_mad_u64_u32 (~5.5 cycles/wave), the rest ~3.1, which
+        # caps the mix at ~0.22 (profiles/r02_mbench_field29_v2.txt)
+        ipc = sq["valu_insts"] / (ms * 1e-3 * 2.4e9 * 1024)
+        r["valu"] = {"insts_per_launch": sq["valu_insts"],
+                     "insts_per_madd_per_lane": sq["valu_insts"] * 64 / (units * windows),
+                     "insts_per_simd_cycle": ipc, "issue_cap_for_mix": VALU_ISSUE_CAP,
+                     "frac": ipc / VALU_ISSUE_CAP, "source": sq["source"],
+                     "basis": "SQ_INSTS_VALU of the committed SQ-counter profile / (launch ms x 2.4 GHz x 1024 "
+                              "SIMDs) against the measured issue ceiling of this instruction mix"}
+    return r
 
 
 def _profile_order(path):
@@ -613,11 +689,30 @@ def _profile_order(path):
     return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
 
 
-def pmc_traffic(kernel, workload):
-    """HBM bytes per launch of `kernel` from a committed PMC profile of the same
-    workload (two separate rocprofv3 --pmc passes, FETCH_SIZE x2 per the gfx950
-    correction + WRITE_SIZE; tools/pmc_traffic.py).  None if no matching profile."""
+def fetch_calibration():
+    """FETCH_SIZE scale per access width from the committed calibration run
+    (tools/mbench_gather_calib.hip: known byte counts of 16-B/lane streams and of
+    64/96/128-B point gathers through a permutation, one rocprofv3 --pmc
+    FETCH_SIZE pass; tools/pmc_calib.py).  None if absent."""
     import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*fetch_calibration*.json")))
+    if not fs:
+        return None
+    try:
+        d = json.load(open(fs[-1]))
+    except (OSError, ValueError):
+        return None
+    return {int(k): v for k, v in d.get("factor", {}).items()}, os.path.basename(fs[-1])
+
+
+def pmc_traffic(kernel, workload, gather_bytes=None):
+    """HBM bytes per launch of `kernel` from a committed PMC profile of the same
+    workload (two separate rocprofv3 --pmc passes, FETCH_SIZE and WRITE_SIZE;
+    tools/pmc_traffic.py): FETCH_SIZE x the guide's x2 for coalesced streams, or
+    x the measured factor of the kernel's gather width (fetch_calibration) for
+    the point-gathering accumulation, + WRITE_SIZE.  None if no matching profile."""
+    import glob
+    cal = fetch_calibration()
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json")), key=_profile_order, reverse=True):
         try:
             d = json.load(open(f))
@@ -627,19 +722,19 @@ def pmc_traffic(kernel, workload):
         if any(wl.get(k) != v for k, v in workload.items()):
             continue
         for k, v in d.get("kernels", {}).items():
-            if kernel in k:
-                if "traffic_bytes_raw" in v and "accum" in kernel:
-                    return v["traffic_bytes_raw"], (
-                        f"{os.path.basename(f)}: FETCH_SIZE + WRITE_SIZE per dispatch, no x2 (64-B point "
-                        f"gathers: the guide's x2 is calibrated for 16-B/lane coalesced streams; with x2: "
-                        f"{v['traffic_bytes']:.4g} B); the W precomputed window copies of the fixed-base "
-                        f"tables make the kernel read ~W x the point bytes per scalar (no doublings at "
-                        f"prove time), so traffic >> the algorithmic bytes")
-                return v["traffic_bytes"], (
-                    f"{os.path.basename(f)}: FETCH_SIZE x2 + WRITE_SIZE per dispatch; the W "
-                    f"precomputed window copies of the fixed-base tables make the kernel read ~W x "
-                    f"the point bytes per scalar (no doublings at prove time), so traffic >> the "
-                    f"algorithmic bytes")
+            if kernel not in k:
+                continue
+            raw = v["fetch_bytes_raw"]
+            if gather_bytes and cal and gather_bytes in cal[0]:
+                fac = cal[0][gather_bytes]
+                how = f"FETCH_SIZE x {fac:.3f} (measured for {gather_bytes}-B point gathers, {cal[1]})"
+            elif gather_bytes:
+                fac = 2.0 if gather_bytes >= 128 else 1.0
+                how = (f"FETCH_SIZE x {fac:.0f} ({gather_bytes}-B gathers: 128-B requests tallied at 64 B "
+                       f"per the guide; uncalibrated width)")
+            else:
+                fac, how = 2.0, "FETCH_SIZE x 2 (gfx950 wide-read correction)"
+            return raw * fac + v["write_bytes"], f"{os.path.basename(f)}: {how} + WRITE_SIZE, per dispatch"
     return None, "no committed PMC profile for this workload"
 
 
@@ -661,19 +756,31 @@ def pmc_sq(kernel, workload):
     return None
 
 
-def cpu_baseline(threads, gpu_prove_ms, gpu_ncons, log_n=20):
+def cpu_threads(requested):
+    """(threads, allotment note) of the CPU baseline: every core this process may
+    run on (sched_getaffinity), capped by OMP_NUM_THREADS when the launcher sets
+    one -- the GPU pool gives each one-GPU job a 16-CPU share of its host (it
+    exports OMP_NUM_THREADS=16), although nproc shows every core of the machine."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    if requested:
+        return requested, f"--cpu-threads {requested} ({aff} CPUs in this process's affinity mask)"
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp and omp < aff:
+        return omp, (f"OMP_NUM_THREADS={omp}: the CPU share of this job on a shared host ({aff} CPUs in the "
+                     f"affinity mask, {os.cpu_count()} in the machine)")
+    return aff, f"all {aff} CPUs of this process's affinity mask"
+
+
+def cpu_baseline(threads, gpu_prove_ms, gpu_ncons, log_ns=(20, 22), budget_s=(10.0, 25.0)):
     """The C restatement of the same prove (oracle/c oc_groth16_prove: OpenMP
-    signed-digit Pippenger MSMs with XYZZ buckets, radix-2 NTT computeH) on a
-    bounded sample: one 2^log_n MiMC-shaped proof (random solution, key from the
-    GPU batch scalar mul), repeated to ~10 s.  "port": our restatement, not gnark."""
+    signed-digit Pippenger MSMs with XYZZ buckets, radix-2 NTT computeH) on
+    bounded samples: one 2^20 and one 2^22 MiMC-shaped proof (random solution,
+    key from the GPU batch scalar mul), the 2^20 one repeated to ~10 s, so the
+    port's scaling with size is visible.  kind "port": our restatement, not gnark."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import coracle
     from gnark_amd import msm
-    nt = threads or (os.cpu_count() or 1)
-    sh = mimc_shape(log_n)
-    n, nw, ncons, nbp = 1 << log_n, sh["nw"], sh["ncons"], sh["nb_public"]
-    infA, infB = sh["infA"], sh["infB"]
-    nA, nB = int((infA == 0).sum()), int((infB == 0).sum())
+    nt, allot = cpu_threads(threads)
     g1, g2 = g1_generator_mont(), g2_generator_mont()
 
     def p1(k, seed):
@@ -681,18 +788,27 @@ def cpu_baseline(threads, gpu_prove_ms, gpu_ncons, log_n=20):
 
     def p2(k, seed):
         return msm.batch_scalar_mul(msm.G2, g2, rand_scalars(k, seed), k)
-    args = (log_n, p1(nA, 1), nA, p1(nB, 2), nB, p1(n - 1, 3), p1(nw - nbp, 4), nw - nbp,
-            p1(1, 5), p1(1, 6), p1(1, 7), p2(nB, 8), p2(1, 9), p2(1, 10), infA.tobytes(), infB.tobytes(),
-            rand_scalars(nw, 11).tobytes(), nw, nbp, rand_scalars(ncons, 12).tobytes(),
-            rand_scalars(ncons, 13).tobytes(), rand_scalars(ncons, 14).tobytes(), ncons,
-            fr_const(12345), fr_const(67890), nt)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        coracle.groth16_prove(*args)
-        reps += 1
-        if time.perf_counter() - t0 > 10.0 or reps >= 20:
-            break
-    el = time.perf_counter() - t0
+    samples = []
+    for log_n, budget in zip(log_ns, budget_s):
+        sh = mimc_shape(log_n)
+        n, nw, ncons, nbp = 1 << log_n, sh["nw"], sh["ncons"], sh["nb_public"]
+        infA, infB = sh["infA"], sh["infB"]
+        nA, nB = int((infA == 0).sum()), int((infB == 0).sum())
+        args = (log_n, p1(nA, 1), nA, p1(nB, 2), nB, p1(n - 1, 3), p1(nw - nbp, 4), nw - nbp,
+                p1(1, 5), p1(1, 6), p1(1, 7), p2(nB, 8), p2(1, 9), p2(1, 10), infA.tobytes(), infB.tobytes(),
+                rand_scalars(nw, 11).tobytes(), nw, nbp, rand_scalars(ncons, 12).tobytes(),
+                rand_scalars(ncons, 13).tobytes(), rand_scalars(ncons, 14).tobytes(), ncons,
+                fr_const(12345), fr_const(67890), nt)
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            coracle.groth16_prove(*args)
+            reps += 1
+            if time.perf_counter() - t0 > budget or reps >= 20:
+                break
+        el = time.perf_counter() - t0
+        samples.append({"log_n": log_n, "n_constraints": ncons, "proves": reps, "prove_ms": 1e3 * el / reps,
+                        "constraints_per_s": ncons * reps / el})
+        del args
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -701,13 +817,15 @@ def cpu_baseline(threads, gpu_prove_ms, gpu_ncons, log_n=20):
                 break
     except OSError:
         pass
-    v = ncons * reps / el
+    v = samples[0]["constraints_per_s"]
+    gl = (gpu_ncons - 1).bit_length()
     return {"value": v, "unit": "constraints/s", "cores": nt, "kind": "port",
-            "prove_ms": 1e3 * el / reps, "cpu_model": cpu_model, "host_cpus_visible": os.cpu_count(),
-            "sample": f"Groth16 prove of a 2^{log_n} MiMC-chain R1CS ({ncons} constraints) x {reps} "
-                      f"(C restatement of prove.go: OpenMP Pippenger + radix-2 NTT, {nt} threads, "
-                      f"not gnark); the GPU line is 2^{gpu_ncons.bit_length() - 1}-scale: compare "
-                      f"constraints/s",
+            "prove_ms": samples[0]["prove_ms"], "cpu_model": cpu_model, "host_cpus_visible": os.cpu_count(),
+            "threads_allotment": allot, "samples": samples,
+            "sample": (f"Groth16 prove of a 2^{log_ns[0]} MiMC-chain R1CS ({samples[0]['n_constraints']} "
+                       f"constraints) x {samples[0]['proves']}, and one 2^{log_ns[-1]} proof beside it (C "
+                       f"restatement of prove.go: OpenMP Pippenger + radix-2 NTT, {nt} threads; a port, NOT "
+                       f"gnark); the GPU line is the 2^{gl} prove: compare constraints/s"),
             "gpu_over_cpu_constraints_per_s": (gpu_ncons / (gpu_prove_ms * 1e-3)) / v}
 
 

@@ -237,6 +237,25 @@ extern "C" int gg_groth16_pk_create(int log_n, const void* omega_mont, const voi
                                    n_wires, nb_public, k_wire_index, out);
 }
 
+extern "C" int gg_groth16_pk_create_shard_ex(int curve, int log_n, const void* omega_mont,
+                                             const void* coset_gen_mont, const void* g1_A, size_t nA,
+                                             const void* g1_B, size_t nB, const void* g1_Z, size_t z_lo,
+                                             size_t nZ, const void* g1_K, size_t nK, const void* alpha1,
+                                             const void* beta1, const void* delta1, const void* g2_B,
+                                             const void* beta2, const void* delta2, const uint8_t* inf_A,
+                                             const uint8_t* inf_B, size_t n_wires, size_t nb_public,
+                                             const uint32_t* k_wire_index, size_t wire_lo, size_t wire_hi,
+                                             gg_groth16_pk_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out, GG_ERR_INVALID_ARG, "null argument");
+    std::unique_ptr<gg_groth16_pk> pk(new gg_groth16_pk());
+    pk_build(pk.get(), curve, log_n, omega_mont, coset_gen_mont, g1_A, nA, g1_B, nB, g1_Z, z_lo, nZ, g1_K, nK,
+             alpha1, beta1, delta1, g2_B, beta2, delta2, inf_A, inf_B, n_wires, nb_public, k_wire_index, wire_lo,
+             wire_hi);
+    *out = pk.release();
+    GG_CAPI_END
+}
+
 extern "C" int gg_groth16_pk_create_shard(int log_n, const void* omega_mont, const void* coset_gen_mont,
                                           const void* g1_A, size_t nA, const void* g1_B, size_t nB,
                                           const void* g1_Z, size_t z_lo, size_t nZ, const void* g1_K,
@@ -246,14 +265,9 @@ extern "C" int gg_groth16_pk_create_shard(int log_n, const void* omega_mont, con
                                           const uint8_t* inf_B, size_t n_wires, size_t nb_public,
                                           const uint32_t* k_wire_index, size_t wire_lo,
                                           size_t wire_hi, gg_groth16_pk_t* out) {
-    GG_CAPI_BEGIN
-    GG_CHECK(out, GG_ERR_INVALID_ARG, "null argument");
-    std::unique_ptr<gg_groth16_pk> pk(new gg_groth16_pk());
-    pk_build(pk.get(), GG_CURVE_BN254, log_n, omega_mont, coset_gen_mont, g1_A, nA, g1_B, nB, g1_Z, z_lo, nZ, g1_K,
-             nK, alpha1, beta1, delta1, g2_B, beta2, delta2, inf_A, inf_B, n_wires, nb_public,
-             k_wire_index, wire_lo, wire_hi);
-    *out = pk.release();
-    GG_CAPI_END
+    return gg_groth16_pk_create_shard_ex(GG_CURVE_BN254, log_n, omega_mont, coset_gen_mont, g1_A, nA, g1_B, nB,
+                                         g1_Z, z_lo, nZ, g1_K, nK, alpha1, beta1, delta1, g2_B, beta2, delta2,
+                                         inf_A, inf_B, n_wires, nb_public, k_wire_index, wire_lo, wire_hi, out);
 }
 
 extern "C" int gg_groth16_pk_base_info(gg_groth16_pk_t pk, int which, size_t* n_points, int* window_bits,

@@ -65,15 +65,16 @@ bool dist_h_ok(size_t n, int world) {
 }  // namespace
 
 struct gg_groth16_mpk {
-    int world = 0;
+    int world = 0, curve = GG_CURVE_BN254;
     size_t n = 0, n_wires = 0;
+    size_t g1a = 64, g2a = 128, g1j = 96, g2j = 192;  // the curve's point sizes
     bool dist = false;
     std::vector<int> dev;
     std::vector<gg_groth16_pk_t> pk;
     std::vector<gg_hshard_t> hs;
     std::vector<void*> send, recv;
     std::vector<hipStream_t> st;
-    uint8_t alpha1[64], beta1[64], delta1[64], beta2[128], delta2[128];
+    uint8_t alpha1[96], beta1[96], delta1[96], beta2[192], delta2[192];
     Barrier bar;
     std::mutex mu;  // one proof at a time per key
     double last_ms[4] = {0, 0, 0, 0};
@@ -151,17 +152,18 @@ void on_shards(gg_groth16_mpk* m, Fn fn) {
 
 }  // namespace
 
-extern "C" int gg_groth16_mpk_create(int log_n, const void* omega_mont, const void* coset_gen_mont,
-                                     const void* g1_A, size_t nA, const void* g1_B, size_t nB,
-                                     const void* g1_Z, size_t nZ, const void* g1_K, size_t nK,
-                                     const void* alpha1, const void* beta1, const void* delta1,
-                                     const void* g2_B, const void* beta2, const void* delta2,
-                                     const uint8_t* inf_A, const uint8_t* inf_B, size_t n_wires,
-                                     size_t nb_public, const uint32_t* k_wire_index, int world,
-                                     const int* devices, gg_groth16_mpk_t* out) {
+extern "C" int gg_groth16_mpk_create_ex(int curve, int log_n, const void* omega_mont,
+                                        const void* coset_gen_mont, const void* g1_A, size_t nA,
+                                        const void* g1_B, size_t nB, const void* g1_Z, size_t nZ,
+                                        const void* g1_K, size_t nK, const void* alpha1, const void* beta1,
+                                        const void* delta1, const void* g2_B, const void* beta2,
+                                        const void* delta2, const uint8_t* inf_A, const uint8_t* inf_B,
+                                        size_t n_wires, size_t nb_public, const uint32_t* k_wire_index,
+                                        int world, const int* devices, gg_groth16_mpk_t* out) {
     GG_CAPI_BEGIN
     GG_CHECK(out && alpha1 && beta1 && delta1 && beta2 && delta2 && inf_A && inf_B && devices, GG_ERR_INVALID_ARG,
              "null argument");
+    GG_CHECK(curve == GG_CURVE_BN254 || curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "bad curve");
     GG_CHECK(world >= 1 && world <= 64, GG_ERR_INVALID_ARG, "world must be in [1, 64]");
     GG_CHECK(log_n >= 0 && log_n <= 28, GG_ERR_INVALID_ARG, "log_n out of range");
     const size_t n = (size_t)1 << log_n;
@@ -172,9 +174,18 @@ extern "C" int gg_groth16_mpk_create(int log_n, const void* omega_mont, const vo
         GG_CHECK(devices[r] >= 0 && devices[r] < ndev, GG_ERR_INVALID_ARG, "device id out of range");
     std::unique_ptr<gg_groth16_mpk, void (*)(gg_groth16_mpk*)> m(new gg_groth16_mpk, mpk_free);
     m->world = world;
+    m->curve = curve;
+    if (curve == GG_CURVE_BLS12_381) {
+        m->g1a = 96;
+        m->g2a = 192;
+        m->g1j = 144;
+        m->g2j = 288;
+    }
     m->n = n;
     m->n_wires = n_wires;
-    m->dist = dist_h_ok(n, world);
+    // the four-step distributed computeH exists for BN254 fr; BLS12-381 shards
+    // compute h themselves (replicated H, sharded MSMs)
+    m->dist = curve == GG_CURVE_BN254 && dist_h_ok(n, world);
     m->dev.assign(devices, devices + world);
     m->pk.assign(world, nullptr);
     m->hs.assign(world, nullptr);
@@ -182,11 +193,11 @@ extern "C" int gg_groth16_mpk_create(int log_n, const void* omega_mont, const vo
     m->recv.assign(world, nullptr);
     m->st.assign(world, nullptr);
     m->bar.n = world;
-    memcpy(m->alpha1, alpha1, 64);
-    memcpy(m->beta1, beta1, 64);
-    memcpy(m->delta1, delta1, 64);
-    memcpy(m->beta2, beta2, 128);
-    memcpy(m->delta2, delta2, 128);
+    memcpy(m->alpha1, alpha1, m->g1a);
+    memcpy(m->beta1, beta1, m->g1a);
+    memcpy(m->delta1, delta1, m->g1a);
+    memcpy(m->beta2, beta2, m->g2a);
+    memcpy(m->delta2, delta2, m->g2a);
     // xGMI peer access between the distinct devices (copies work without it,
     // staged by the runtime)
     for (int i = 0; i < world; i++)
@@ -212,6 +223,7 @@ extern "C" int gg_groth16_mpk_create(int log_n, const void* omega_mont, const vo
     const uint8_t* B2 = (const uint8_t*)g2_B;
     const uint8_t* K = (const uint8_t*)g1_K;
     const uint8_t* Z = (const uint8_t*)g1_Z;
+    const size_t g1a = m->g1a, g2a = m->g2a;
     on_shards(m.get(), [&](int r) -> int {
         const size_t lo = n_wires * r / world, hi = n_wires * (r + 1) / world;
         size_t zl, zh;
@@ -234,7 +246,7 @@ extern "C" int gg_groth16_mpk_create(int log_n, const void* omega_mont, const vo
         if (k_wire_index) {
             for (size_t j = 0; j < nK; j++)
                 if (k_wire_index[j] >= lo && k_wire_index[j] < hi) {
-                    kp.insert(kp.end(), K + j * 64, K + (j + 1) * 64);
+                    kp.insert(kp.end(), K + j * g1a, K + (j + 1) * g1a);
                     kidx.push_back(k_wire_index[j]);
                 }
             kptr = kp.data();
@@ -244,13 +256,13 @@ extern "C" int gg_groth16_mpk_create(int log_n, const void* omega_mont, const vo
             size_t k1 = std::max(hi, nb_public) - nb_public, k0 = std::max(lo, nb_public) - nb_public;
             k1 = std::min(k1, nK);
             k0 = std::min(k0, k1);
-            kptr = K + k0 * 64;
+            kptr = K + k0 * g1a;
             kcnt = k1 - k0;
         }
-        int rc = gg_groth16_pk_create_shard(log_n, omega_mont, coset_gen_mont, A + pa[lo] * 64, pa[hi] - pa[lo],
-                                            B + pb[lo] * 64, pb[hi] - pb[lo], Z + zl * 64, zl, zh - zl, kptr, kcnt,
-                                            alpha1, beta1, delta1, B2 + pb[lo] * 128, beta2, delta2, inf_A, inf_B,
-                                            n_wires, nb_public, kix, lo, hi, &m->pk[r]);
+        int rc = gg_groth16_pk_create_shard_ex(curve, log_n, omega_mont, coset_gen_mont, A + pa[lo] * g1a,
+                                               pa[hi] - pa[lo], B + pb[lo] * g1a, pb[hi] - pb[lo], Z + zl * g1a, zl,
+                                               zh - zl, kptr, kcnt, alpha1, beta1, delta1, B2 + pb[lo] * g2a, beta2,
+                                               delta2, inf_A, inf_B, n_wires, nb_public, kix, lo, hi, &m->pk[r]);
         if (rc) return rc;
         if (hipStreamCreateWithFlags(&m->st[r], hipStreamNonBlocking) != hipSuccess) return GG_ERR_DEVICE;
         if (!m->dist) return 0;
@@ -268,6 +280,19 @@ extern "C" int gg_groth16_mpk_create(int log_n, const void* omega_mont, const vo
     GG_CAPI_END
 }
 
+extern "C" int gg_groth16_mpk_create(int log_n, const void* omega_mont, const void* coset_gen_mont,
+                                     const void* g1_A, size_t nA, const void* g1_B, size_t nB,
+                                     const void* g1_Z, size_t nZ, const void* g1_K, size_t nK,
+                                     const void* alpha1, const void* beta1, const void* delta1,
+                                     const void* g2_B, const void* beta2, const void* delta2,
+                                     const uint8_t* inf_A, const uint8_t* inf_B, size_t n_wires,
+                                     size_t nb_public, const uint32_t* k_wire_index, int world,
+                                     const int* devices, gg_groth16_mpk_t* out) {
+    return gg_groth16_mpk_create_ex(GG_CURVE_BN254, log_n, omega_mont, coset_gen_mont, g1_A, nA, g1_B, nB, g1_Z, nZ,
+                                    g1_K, nK, alpha1, beta1, delta1, g2_B, beta2, delta2, inf_A, inf_B, n_wires,
+                                    nb_public, k_wire_index, world, devices, out);
+}
+
 extern "C" int gg_groth16_mpk_release(gg_groth16_mpk_t m) {
     GG_CAPI_BEGIN
     if (m) mpk_free(m);
@@ -282,48 +307,83 @@ extern "C" int gg_groth16_mpk_info(gg_groth16_mpk_t m, int* world, int* distribu
     GG_CAPI_END
 }
 
-extern "C" int gg_groth16_mpk_prove(gg_groth16_mpk_t m, const void* wires, size_t n_wires, const void* sol_a,
-                                    const void* sol_b, const void* sol_c, size_t n_cons, const void* r_mont,
-                                    const void* s_mont, void* ar_aff, void* bs_aff, void* krs_aff) {
+extern "C" int gg_groth16_mpk_base_info(gg_groth16_mpk_t m, int shard, int which, size_t* n_points,
+                                        int* window_bits, int* n_windows) {
+    GG_CAPI_BEGIN
+    GG_CHECK(m && shard >= 0 && shard < m->world, GG_ERR_INVALID_ARG, "bad shard");
+    return gg_groth16_pk_base_info(m->pk[shard], which, n_points, window_bits, n_windows);
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_mpk_devices(gg_groth16_mpk_t m, int* devices, int cap) {
+    GG_CAPI_BEGIN
+    GG_CHECK(m && devices && cap >= m->world, GG_ERR_INVALID_ARG, "null argument or cap < world");
+    for (int r = 0; r < m->world; r++) devices[r] = m->dev[r];
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_mpk_prove_ex(gg_groth16_mpk_t m, int inputs_on_device, const void* const* wires,
+                                       size_t n_wires, const void* const* sol_a, const void* const* sol_b,
+                                       const void* const* sol_c, size_t n_cons, const void* r_mont,
+                                       const void* s_mont, void* ar_aff, void* bs_aff, void* krs_aff) {
     GG_CAPI_BEGIN
     GG_CHECK(m && wires && sol_a && sol_b && sol_c && r_mont && s_mont && ar_aff && bs_aff && krs_aff,
              GG_ERR_INVALID_ARG, "null argument");
+    for (int r = 0; r < m->world; r++)
+        GG_CHECK(wires[r] && sol_a[r] && sol_b[r] && sol_c[r], GG_ERR_INVALID_ARG, "null solution pointer");
     GG_CHECK(n_wires == m->n_wires, GG_ERR_INVALID_ARG, "wire count differs from the key's");
     GG_CHECK(n_cons <= m->n, GG_ERR_INVALID_ARG, "more constraints than the domain");
     std::lock_guard<std::mutex> lk(m->mu);
     const auto t0 = std::chrono::steady_clock::now();
     m->bar.reset();
-    std::vector<std::vector<uint8_t>> parts(m->world, std::vector<uint8_t>(576));
+    const size_t pbytes = 4 * m->g1j + m->g2j;  // a | b1 | k | z | b2 (gg_groth16_prove_partial)
+    std::vector<std::vector<uint8_t>> parts(m->world, std::vector<uint8_t>(pbytes));
     std::vector<XCtx> ctx(m->world);
     on_shards(m, [&](int r) -> int {
         ctx[r] = XCtx{m, r};
         if (m->dist)
-            return gg_groth16_prove_partial_dist(m->pk[r], m->hs[r], wires, n_wires, sol_a, sol_b, sol_c, n_cons, 0,
-                                                 mpk_exchange, &ctx[r], m->send[r], m->recv[r], parts[r].data());
-        return gg_groth16_prove_partial(m->pk[r], wires, n_wires, sol_a, sol_b, sol_c, n_cons, 0, parts[r].data(),
-                                        nullptr);
+            return gg_groth16_prove_partial_dist(m->pk[r], m->hs[r], wires[r], n_wires, sol_a[r], sol_b[r], sol_c[r],
+                                                 n_cons, inputs_on_device, mpk_exchange, &ctx[r], m->send[r],
+                                                 m->recv[r], parts[r].data());
+        return gg_groth16_prove_partial(m->pk[r], wires[r], n_wires, sol_a[r], sol_b[r], sol_c[r], n_cons,
+                                        inputs_on_device, parts[r].data(), nullptr);
     });
     const auto t1 = std::chrono::steady_clock::now();
-    // exact sum of the partials: 4 G1Jac (96 B) then one G2Jac (192 B)
+    // exact sum of the partials: 4 G1Jac then one G2Jac
+    const bool bn = m->curve == GG_CURVE_BN254;
+    auto g1add = bn ? gg_g1_jac_add : gg_bls12_381_g1_jac_add;
+    auto g2add = bn ? gg_g2_jac_add : gg_bls12_381_g2_jac_add;
     std::vector<uint8_t> sum = parts[0];
     for (int r = 1; r < m->world; r++) {
+        uint8_t tmp[288];
         for (int i = 0; i < 4; i++) {
-            uint8_t tmp[96];
-            GG_CHECK(gg_g1_jac_add(sum.data() + 96 * i, parts[r].data() + 96 * i, tmp) == GG_OK, GG_ERR_INTERNAL,
-                     "partial sum");
-            memcpy(sum.data() + 96 * i, tmp, 96);
+            uint8_t* acc = sum.data() + m->g1j * i;
+            GG_CHECK(g1add(acc, parts[r].data() + m->g1j * i, tmp) == GG_OK, GG_ERR_INTERNAL, "partial sum");
+            memcpy(acc, tmp, m->g1j);
         }
-        uint8_t tmp2[192];
-        GG_CHECK(gg_g2_jac_add(sum.data() + 384, parts[r].data() + 384, tmp2) == GG_OK, GG_ERR_INTERNAL, "partial sum");
-        memcpy(sum.data() + 384, tmp2, 192);
+        uint8_t* acc2 = sum.data() + 4 * m->g1j;
+        GG_CHECK(g2add(acc2, parts[r].data() + 4 * m->g1j, tmp) == GG_OK, GG_ERR_INTERNAL, "partial sum");
+        memcpy(acc2, tmp, m->g2j);
     }
-    const int rc = gg_groth16_finalize(m->alpha1, m->beta1, m->delta1, m->beta2, m->delta2, sum.data(), r_mont,
-                                       s_mont, ar_aff, bs_aff, krs_aff);
+    const int rc = gg_groth16_finalize_ex(m->curve, m->alpha1, m->beta1, m->delta1, m->beta2, m->delta2, sum.data(),
+                                          r_mont, s_mont, ar_aff, bs_aff, krs_aff);
     GG_CHECK(rc == GG_OK, rc, gg_last_error());
     const auto t2 = std::chrono::steady_clock::now();
     m->last_ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
     m->last_ms[1] = std::chrono::duration<double, std::milli>(t2 - t1).count();
     m->last_ms[2] = std::chrono::duration<double, std::milli>(t2 - t0).count();
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_mpk_prove(gg_groth16_mpk_t m, const void* wires, size_t n_wires, const void* sol_a,
+                                    const void* sol_b, const void* sol_c, size_t n_cons, const void* r_mont,
+                                    const void* s_mont, void* ar_aff, void* bs_aff, void* krs_aff) {
+    GG_CAPI_BEGIN
+    GG_CHECK(m, GG_ERR_INVALID_ARG, "null key");
+    // host inputs: every shard reads the same host vectors
+    const std::vector<const void*> w(m->world, wires), a(m->world, sol_a), b(m->world, sol_b), c(m->world, sol_c);
+    return gg_groth16_mpk_prove_ex(m, 0, w.data(), n_wires, a.data(), b.data(), c.data(), n_cons, r_mont, s_mont,
+                                   ar_aff, bs_aff, krs_aff);
     GG_CAPI_END
 }
 

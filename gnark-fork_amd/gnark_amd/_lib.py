@@ -105,6 +105,13 @@ def _load():
         "gg_groth16_prove_partial_dist": ([P, P, P, S, P, P, P, S, I, EXCHANGE_FN, P, P, P, P], I),
         "gg_groth16_mpk_create": ([I, P, P, P, S, P, S, P, S, P, S, P, P, P, P, P, P, P, P, S, S, P, I,
                                    ctypes.POINTER(ctypes.c_int), PP], I),
+        "gg_groth16_mpk_create_ex": ([I, I, P, P, P, S, P, S, P, S, P, S, P, P, P, P, P, P, P, P, S, S, P, I,
+                                      ctypes.POINTER(ctypes.c_int), PP], I),
+        "gg_groth16_mpk_prove_ex": ([P, I, PP, S, PP, PP, PP, S, P, P, P, P, P], I),
+        "gg_groth16_mpk_devices": ([P, ctypes.POINTER(ctypes.c_int), I], I),
+        "gg_groth16_mpk_base_info": ([P, I, I, P, P, P], I),
+        "gg_groth16_pk_create_shard_ex": ([I, I, P, P, P, S, P, S, P, S, S, P, S, P, P, P, P, P, P, P, P, S,
+                                           S, P, S, S, PP], I),
         "gg_groth16_mpk_release": ([P], I),
         "gg_groth16_mpk_info": ([P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], I),
         "gg_groth16_mpk_prove": ([P, P, S, P, P, P, S, P, P, P, P, P], I),
@@ -167,7 +174,8 @@ EXPORTED = [
     "gg_plonk_last_timings", "gg_groth16_pk_create_ex", "gg_groth16_finalize_ex",
     "gg_bls12_381_g2_jac_to_affine", "gg_bls12_381_g2_jac_add", "gg_bls12_381_g2_scalar_mul",
     "gg_groth16_mpk_create", "gg_groth16_mpk_release", "gg_groth16_mpk_info", "gg_groth16_mpk_prove",
-    "gg_groth16_mpk_last_timings", "gg_r1cs_create", "gg_r1cs_create_ex", "gg_r1cs_release", "gg_r1cs_info", "gg_r1cs_solve",
+    "gg_groth16_mpk_last_timings", "gg_groth16_mpk_create_ex", "gg_groth16_mpk_prove_ex",
+    "gg_groth16_mpk_devices", "gg_groth16_mpk_base_info", "gg_groth16_pk_create_shard_ex", "gg_r1cs_create", "gg_r1cs_create_ex", "gg_r1cs_release", "gg_r1cs_info", "gg_r1cs_solve",
     "gg_r1cs_solution_dev", "gg_scs_create", "gg_scs_release", "gg_scs_info", "gg_scs_solve",
     "gg_scs_solution_dev",
 ]

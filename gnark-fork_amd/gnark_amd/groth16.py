@@ -155,33 +155,44 @@ class ProvingKey:
 
 
 class MultiGpuProvingKey:
-    """One-process multi-GPU key (gg_groth16_mpk_create): shard r of the whole
+    """One-process multi-GPU key (gg_groth16_mpk_create_ex): shard r of the whole
     key on devices[r] (ids may repeat: several shards per GPU); proofs run one
     host thread per shard with the distributed computeH's all-to-alls done as
     peer copies inside the library -- the shape a Go caller uses, no
-    torch.distributed.  BN254, host inputs."""
+    torch.distributed.  BN254 (distributed computeH) or BLS12-381 (computeH on
+    every shard, MSMs sharded).  Host inputs, or a solution resident on every
+    device (`replicate_solution` / per-device GPU solves)."""
 
     def __init__(self, data: ProvingKeyData, devices):
-        if data.curve != "bn254":
-            raise ValueError("multi-GPU key: BN254 only")
         self.data = data
+        self.curve = data.curve
+        g1b, g2b = _SIZES[data.curve]
+        self.g1b, self.g2b = g1b, g2b
         devs = (ctypes.c_int * len(devices))(*devices)
-        omega = data.domain_generator or fr.fr_mont(fr.domain_generator(data.log_n))
-        gen = data.domain_mul_gen or fr.fr_mont(fr.FR_MULTIPLICATIVE_GEN)
+        if data.curve == "bn254":
+            cid = GG_CURVE_BN254
+            omega = data.domain_generator or fr.fr_mont(fr.domain_generator(data.log_n))
+            gen = data.domain_mul_gen or fr.fr_mont(fr.FR_MULTIPLICATIVE_GEN)
+        else:
+            cid = GG_CURVE_BLS12_381
+            omega = data.domain_generator or fr.bls_fr_mont(fr.bls_domain_generator(data.log_n))
+            gen = data.domain_mul_gen or fr.bls_fr_mont(fr.BLS_FR_MULTIPLICATIVE_GEN)
         kidx = None
         if data.k_wire_index is not None:
             kidx = np.ascontiguousarray(np.asarray(data.k_wire_index, dtype=np.uint32))
         h = ctypes.c_void_p()
-        check(lib.gg_groth16_mpk_create(
-            data.log_n, ptr(omega), ptr(gen),
-            ptr(data.g1_A), len(data.g1_A) // 64, ptr(data.g1_B), len(data.g1_B) // 64,
-            ptr(data.g1_Z), len(data.g1_Z) // 64, ptr(data.g1_K), len(data.g1_K) // 64,
+        check(lib.gg_groth16_mpk_create_ex(
+            cid, data.log_n, ptr(omega), ptr(gen),
+            ptr(data.g1_A), len(data.g1_A) // g1b, ptr(data.g1_B), len(data.g1_B) // g1b,
+            ptr(data.g1_Z), len(data.g1_Z) // g1b, ptr(data.g1_K), len(data.g1_K) // g1b,
             ptr(data.alpha1), ptr(data.beta1), ptr(data.delta1),
             ptr(data.g2_B), ptr(data.beta2), ptr(data.delta2),
             ptr(bytes(data.infinity_A)), ptr(bytes(data.infinity_B)), data.n_wires, data.nb_public,
             ptr(kidx), len(devices), devs, ctypes.byref(h)))
         self.handle = h
         self.devices = list(devices)
+        self.n_wires = data.n_wires
+        self.log_n = data.log_n
 
     def info(self):
         """(world, distributed computeH?)"""
@@ -189,18 +200,45 @@ class MultiGpuProvingKey:
         check(lib.gg_groth16_mpk_info(self.handle, ctypes.byref(w), ctypes.byref(d)))
         return w.value, bool(d.value)
 
-    def prove(self, solution: "Solution", *opts, r: bytes = None, s: bytes = None) -> "Proof":
+    def base_info(self, which: int, shard: int = 0):
+        """(resident points, window bits, windows) of MSM base `which` of a shard"""
+        n, c, w = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_int()
+        check(lib.gg_groth16_mpk_base_info(self.handle, shard, which, ctypes.byref(n), ctypes.byref(c),
+                                           ctypes.byref(w)))
+        return n.value, c.value, w.value
+
+    def shard_devices(self):
+        """device id of every shard (gg_groth16_mpk_devices)"""
+        arr = (ctypes.c_int * len(self.devices))()
+        check(lib.gg_groth16_mpk_devices(self.handle, arr, len(self.devices)))
+        return list(arr)
+
+    def prove(self, solution, *opts, r: bytes = None, s: bytes = None) -> "Proof":
+        """`solution`: a host Solution (every shard reads it), or a DeviceSolutions
+        (one resident copy per device, see replicate_solution)."""
         cfg = backend.new_prover_config(*opts)
         if not backend.accelerated(cfg):
             raise RuntimeError("accelerated prover requested without with_amd_acceleration()")
-        if solution.on_device:
-            raise ValueError("multi-GPU prove takes host inputs")
-        r = r if r is not None else _rand_fr_mont()
-        s = s if s is not None else _rand_fr_mont()
-        ar, bs, krs = bytearray(64), bytearray(128), bytearray(64)
-        check(lib.gg_groth16_mpk_prove(self.handle, ptr(solution.W), solution.n_wires, ptr(solution.A),
-                                       ptr(solution.B), ptr(solution.C), solution.n_constraints, ptr(r),
-                                       ptr(s), ptr(ar), ptr(bs), ptr(krs)))
+        rnd = _rand_fr_mont if self.curve == "bn254" else (lambda: fr.bls_fr_mont(secrets.randbelow(fr.BLS_R)))
+        r = r if r is not None else rnd()
+        s = s if s is not None else rnd()
+        world = len(self.devices)
+        if isinstance(solution, DeviceSolutions):
+            per = [solution.for_device(d) for d in self.devices]
+            on_dev = 1
+        elif solution.on_device:
+            if len(set(self.devices)) != 1:
+                raise ValueError("a device-resident Solution serves one GPU; use replicate_solution(...)")
+            per, on_dev = [solution] * world, 1
+        else:
+            per, on_dev = [solution] * world, 0
+        n_wires, n_cons = per[0].n_wires, per[0].n_constraints
+
+        def arr(field):
+            return (ctypes.c_void_p * world)(*[ptr(getattr(x, field)).value for x in per])
+        ar, bs, krs = bytearray(self.g1b), bytearray(self.g2b), bytearray(self.g1b)
+        check(lib.gg_groth16_mpk_prove_ex(self.handle, on_dev, arr("W"), n_wires, arr("A"), arr("B"), arr("C"),
+                                          n_cons, ptr(r), ptr(s), ptr(ar), ptr(bs), ptr(krs)))
         return Proof(bytes(ar), bytes(bs), bytes(krs))
 
     def last_timings(self) -> dict:
@@ -218,6 +256,30 @@ class MultiGpuProvingKey:
             self.close()
         except Exception:
             pass
+
+
+@dataclasses.dataclass
+class DeviceSolutions:
+    """One HBM-resident copy of a Solution per GPU (device id -> Solution with
+    on_device=True), for MultiGpuProvingKey.prove."""
+    by_device: dict
+
+    def for_device(self, d):
+        if d not in self.by_device:
+            raise ValueError("no resident solution on device %d" % d)
+        return self.by_device[d]
+
+
+def replicate_solution(solution: Solution, devices) -> DeviceSolutions:
+    """Upload a host Solution once to every distinct device of `devices`."""
+    from ._lib import DeviceBuffer
+    out = {}
+    for d in dict.fromkeys(devices):
+        check(lib.gg_set_device(int(d)))
+        bufs = [DeviceBuffer.from_host(bytes(getattr(solution, f))) for f in ("W", "A", "B", "C")]
+        out[d] = Solution(*bufs, solution.n_wires, solution.n_constraints, on_device=True)
+    check(lib.gg_set_device(int(devices[0])))
+    return DeviceSolutions(out)
 
 
 def _rand_fr_mont() -> bytes:

@@ -241,6 +241,17 @@ int gg_groth16_pk_create_shard(int log_n, const void *omega_mont, const void *co
                                const void *delta2, const uint8_t *inf_A, const uint8_t *inf_B,
                                size_t n_wires, size_t nb_public, const uint32_t *k_wire_index,
                                size_t wire_lo, size_t wire_hi, gg_groth16_pk_t *out);
+/* gg_groth16_pk_create_shard for a chosen curve (GG_CURVE_BN254 or
+ * GG_CURVE_BLS12_381: backend/groth16/bls12-381/prove.go:63-322, points in that
+ * curve's layout); a BLS12-381 shard computes h itself (no distributed computeH). */
+int gg_groth16_pk_create_shard_ex(int curve, int log_n, const void *omega_mont, const void *coset_gen_mont,
+                                  const void *g1_A, size_t nA, const void *g1_B, size_t nB,
+                                  const void *g1_Z, size_t z_lo, size_t nZ, const void *g1_K,
+                                  size_t nK, const void *alpha1, const void *beta1,
+                                  const void *delta1, const void *g2_B, const void *beta2,
+                                  const void *delta2, const uint8_t *inf_A, const uint8_t *inf_B,
+                                  size_t n_wires, size_t nb_public, const uint32_t *k_wire_index,
+                                  size_t wire_lo, size_t wire_hi, gg_groth16_pk_t *out);
 /* Device section of Prove on one key (shard): computeH and the five MSMs of
  * prove.go:198-301 without the combination.  Inputs as gg_groth16_prove (the
  * whole solution).  partials (host, 576 B): G1Jac sum w.A | sum w.B1 |
@@ -301,7 +312,8 @@ int gg_groth16_prove_partial_dist(gg_groth16_pk_t pk, gg_hshard_t hs, const void
  * computeH are peer copies between the shards' device buffers (xGMI DMA), done
  * inside the library -- no transport from the caller.  world a power of two
  * <= 16 with n >= world^2 distributes computeH; otherwise every shard computes
- * h itself.  devices may repeat (several shards per GPU).  BN254, host inputs.
+ * h itself.  devices may repeat (several shards per GPU).  BN254; host inputs
+ * (gg_groth16_mpk_prove_ex also takes per-device resident solutions).
  * replaces: the per-GPU setupDevicePointers + Prove of icicle.go:31-420 for a
  * node of GPUs driven from one Go process. */
 typedef struct gg_groth16_mpk *gg_groth16_mpk_t;
@@ -313,13 +325,39 @@ int gg_groth16_mpk_create(int log_n, const void *omega_mont, const void *coset_g
                           const uint8_t *inf_A, const uint8_t *inf_B, size_t n_wires,
                           size_t nb_public, const uint32_t *k_wire_index, int world,
                           const int *devices, gg_groth16_mpk_t *out);
+/* the same for a chosen curve: GG_CURVE_BN254 (= gg_groth16_mpk_create) or
+ * GG_CURVE_BLS12_381 (backend/groth16/bls12-381/prove.go:63-322; points in that
+ * curve's layout; computeH replicated on every shard, MSMs sharded) */
+int gg_groth16_mpk_create_ex(int curve, int log_n, const void *omega_mont, const void *coset_gen_mont,
+                             const void *g1_A, size_t nA, const void *g1_B, size_t nB,
+                             const void *g1_Z, size_t nZ, const void *g1_K, size_t nK,
+                             const void *alpha1, const void *beta1, const void *delta1,
+                             const void *g2_B, const void *beta2, const void *delta2,
+                             const uint8_t *inf_A, const uint8_t *inf_B, size_t n_wires,
+                             size_t nb_public, const uint32_t *k_wire_index, int world,
+                             const int *devices, gg_groth16_mpk_t *out);
 int gg_groth16_mpk_release(gg_groth16_mpk_t mpk);
+/* gg_groth16_pk_base_info of shard `shard` */
+int gg_groth16_mpk_base_info(gg_groth16_mpk_t mpk, int shard, int which, size_t *n_points,
+                             int *window_bits, int *n_windows);
+/* the device id of every shard (devices[0..world)) */
+int gg_groth16_mpk_devices(gg_groth16_mpk_t mpk, int *devices, int cap);
 /* world and whether computeH is distributed (1) or replicated per shard (0) */
 int gg_groth16_mpk_info(gg_groth16_mpk_t mpk, int *world, int *distributed_h);
 /* as gg_groth16_prove (host inputs): Ar, Bs, Krs affine */
 int gg_groth16_mpk_prove(gg_groth16_mpk_t mpk, const void *wires, size_t n_wires, const void *sol_a,
                          const void *sol_b, const void *sol_c, size_t n_cons, const void *r_mont,
                          const void *s_mont, void *ar_aff, void *bs_aff, void *krs_aff);
+/* gg_groth16_mpk_prove with the solution per shard: wires[r], sol_a[r], sol_b[r],
+ * sol_c[r] (r < world) are read by shard r -- host memory (inputs_on_device = 0;
+ * the entries may all be the same vectors), or, with inputs_on_device = 1, the
+ * WHOLE solution resident on devices[r] (e.g. solved there by gg_r1cs_solve:
+ * the 2 MB witness is the only per-proof PCIe traffic).  Shards sharing a GPU
+ * may share its copy. */
+int gg_groth16_mpk_prove_ex(gg_groth16_mpk_t mpk, int inputs_on_device, const void *const *wires,
+                            size_t n_wires, const void *const *sol_a, const void *const *sol_b,
+                            const void *const *sol_c, size_t n_cons, const void *r_mont,
+                            const void *s_mont, void *ar_aff, void *bs_aff, void *krs_aff);
 /* ms of the last gg_groth16_mpk_prove: [0] shards (device work + exchanges),
  * [1] partial sum + finalize, [2] total */
 int gg_groth16_mpk_last_timings(gg_groth16_mpk_t mpk, double *ms3);

@@ -146,8 +146,21 @@ def test_groth16_bls12_381_bit_exact(log_n):
     # the same witness solved on the GPU over BLS12-381 fr (gg_r1cs_create_ex), proved from HBM
     from gnark_amd import solver
     sys_ = solver.R1CS.from_terms(1, chains, nw, cons, curve="bls12-381")
-    pr4 = groth16.prove(pk, sys_.solve(w[1:1 + chains]), opt, r=frb(r), s=frb(s))
+    gsol = sys_.solve(w[1:1 + chains])
+    pr4 = groth16.prove(pk, gsol, opt, r=frb(r), s=frb(s))
     assert (pr4.Ar, pr4.Bs, pr4.Krs) == (pr.Ar, pr.Bs, pr.Krs)
+    # one-process multi-GPU key (gg_groth16_mpk_create_ex over BLS12-381): shards
+    # on device 0 rehearse the N-GPU layout; host, replicated and GPU-solved inputs
+    world = {6: 2, 12: 3, 16: 8}[log_n]
+    mpk = groth16.MultiGpuProvingKey(data, [0] * world)
+    assert mpk.info() == (world, False)  # BLS12-381: computeH replicated per shard
+    prm = mpk.prove(sol, opt, r=frb(r), s=frb(s))
+    assert (prm.Ar, prm.Bs, prm.Krs) == (pr.Ar, pr.Bs, pr.Krs)
+    prd = mpk.prove(groth16.replicate_solution(sol, [0] * world), opt, r=frb(r), s=frb(s))
+    assert (prd.Ar, prd.Bs, prd.Krs) == (pr.Ar, pr.Bs, pr.Krs)
+    prg = mpk.prove(sys_.solve(w[1:1 + chains]), opt, r=frb(r), s=frb(s))
+    assert (prg.Ar, prg.Bs, prg.Krs) == (pr.Ar, pr.Bs, pr.Krs)
+    mpk.close()
     sys_.close()
     bad = list(w)
     bad[-1] = (bad[-1] + 1) % R

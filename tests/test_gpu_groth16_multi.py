@@ -67,6 +67,10 @@ def test_mpk_vs_oracle(log_n, n_wires, world, kidx):
     mpk = groth16.MultiGpuProvingKey(data, [0] * world)
     pr = mpk.prove(sol, backend.with_amd_acceleration(), r=r, s=s)
     assert pr == ref
+    # the solution resident in HBM (one copy per device, gg_groth16_mpk_prove_ex)
+    prd = mpk.prove(groth16.replicate_solution(sol, mpk.devices), backend.with_amd_acceleration(), r=r, s=s)
+    assert prd == ref
+    assert mpk.shard_devices() == [0] * world
     mpk.close()
 
 

@@ -104,4 +104,37 @@ def test_groth16_mimc_bit_exact(log_n):
                         opt, r=_fr(R_), s=_fr(S_))
     assert pr3.Krs != want[2]
     pk.close()
+    if log_n == 24:  # the 8-GPU split of configs[3], rehearsed with 8 shards on this GPU
+        _mpk_check(data, sol, sol_d, want, 8, t0)
+    cr.close()
+
+
+def _mpk_check(data, sol, sol_d, want, world, t0):
+    """gg_groth16_mpk_* with `world` key shards (8 = BASELINE configs[3]'s node):
+    wire / Z shards, the four-step distributed computeH with its three
+    all-to-alls as peer copies, partials summed exactly -- same proof bytes."""
+    from gnark_amd import backend, groth16
+    opt = backend.with_amd_acceleration()
+    mpk = groth16.MultiGpuProvingKey(data, [0] * world)
+    assert mpk.info() == (world, True)
+    _log(f"{world}-shard key", t0)
+    pr = mpk.prove(sol, opt, r=_fr(R_), s=_fr(S_))
+    _log(f"{world}-shard prove (host inputs) {mpk.last_timings()['total']:.1f} ms", t0)
+    assert (pr.Ar, pr.Bs, pr.Krs) == want
+    prd = mpk.prove(sol_d, opt, r=_fr(R_), s=_fr(S_))  # resident solution, shared by the shards of GPU 0
+    _log(f"{world}-shard prove (device inputs) {mpk.last_timings()['total']:.1f} ms", t0)
+    assert (prd.Ar, prd.Bs, prd.Krs) == want
+    mpk.close()
+
+
+@pytest.mark.parametrize("log_n,world", [(16, 8), (18, 4)])
+def test_groth16_mimc_multi_gpu_shards(log_n, world):
+    """the same check at sizes the suite runs quickly"""
+    from gnark_amd import groth16, DeviceBuffer
+    t0 = time.time()
+    cr, data, wires, (A, B, C), want = _instance(log_n, t0)
+    sol = groth16.Solution(bytes(wires), bytes(A), bytes(B), bytes(C), cr.nw, cr.ncons)
+    dev = [DeviceBuffer.from_host(bytes(x)) for x in (wires, A, B, C)]
+    sol_d = groth16.Solution(*dev, cr.nw, cr.ncons, on_device=True)
+    _mpk_check(data, sol, sol_d, want, world, t0)
     cr.close()
