@@ -84,8 +84,9 @@ __global__ void __launch_bounds__(256) k_numerator_coset(NumParams P) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= P.n) return;
     const FrB res = numerator_at(P, j);
-    const uint32_t pos = __brev(P.rho * j + P.coset) >> (32 - P.log_big);
-    stf(P.cres + (P.log_big ? pos : 0), res);
+    uint32_t pos = P.log_big ? __brev(P.rho * j + P.coset) >> (32 - P.log_big) : 0u;
+    if (P.local_block) pos &= P.n - 1;
+    stf(P.cres + pos, res);
 }
 
 // n >= 256: 16 x 16 tiles.  Thread t of block m computes j = h 2^(L-4) + 16 m + l
@@ -107,7 +108,8 @@ __global__ void __launch_bounds__(256) k_numerator_coset_tiled(NumParams P, uint
     __syncthreads();
     const uint32_t r = P.log_big - log_n;
     const uint32_t l2 = t >> 4, col = t & 15;
-    const uint32_t pos = (r ? (__brev(P.coset) >> (32 - r)) << log_n : 0u) | ((__brev(l2) >> 28) << (log_n - 4)) |
+    const uint32_t pos = (r && !P.local_block ? (__brev(P.coset) >> (32 - r)) << log_n : 0u) |
+                         ((__brev(l2) >> 28) << (log_n - 4)) |
                          (log_n > 8 ? (__brev(m) >> (40 - log_n)) << 4 : 0u) | col;
     FrB o;
 #pragma unroll

@@ -65,6 +65,9 @@ struct NumParams {
     FrB ka, kb, kc;
     uint32_t n, log_big, rho, coset;
     FrB* cres;  // rho * n, bit-reversed big-domain order
+    // local_block = 1: cres is only this coset's block of n (the slots
+    // [brev(coset) n, (brev(coset) + 1) n) of the big vector), e.g. on another GPU
+    uint32_t local_block;
     // x[ID_ZS] == nullptr: ZS[j] = Z[(j + 1) % n] read from x[ID_Z] (no shifted copy)
 };
 void numerator(const NumParams& P, hipStream_t st);

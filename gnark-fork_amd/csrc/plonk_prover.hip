@@ -201,6 +201,46 @@ FrB fr_random() {
 }  // namespace
 
 // ============================================================== key
+// One-process multi-GPU (gg_plonk_pk_create_multi): device parts[p] (p >= 1) of
+// a key holds slice p of pk.Kzg.G1 / pk.KzgLagrange.G1 (every commitment is an
+// MSM split over the parts, partials summed exactly on the host) and computes
+// the numerator on the big-domain cosets i with i % owners == p (its coset
+// evaluations of the key polynomials resident there; the per-proof L, R, O, Z,
+// Qk, Pi_i arrive by peer copy, its block of cres goes back the same way).
+struct PlonkPeer {
+    int device = 0;
+    hipStream_t s[4] = {nullptr, nullptr, nullptr, nullptr};  // 0..2: MSMs (work slot), 3: cosets
+    gg_msm_base_t kzg = nullptr, kzg_lag = nullptr;
+    size_t k_lo = 0, k_hi = 0, l_lo = 0, l_hi = 0;
+    MsmWork* work[3] = {nullptr, nullptr, nullptr};
+    DevBuf scal[3];                     // scalar slice staging per work slot
+    std::vector<int> cosets;            // big-domain cosets owned here
+    std::vector<gg_domain_t> dcos;      // their small-domain coset FFTs
+    std::vector<std::vector<DevBuf>> ev;  // [key poly][owned coset]
+    DevBuf tw0, in[5 + plk::MAX_CMT];   // L R O Z (canonical bit-reversed), Qk, Pi_j
+    DevBuf cev[7 + plk::MAX_CMT];       // coset evaluation slot
+    std::vector<DevBuf> out;            // owned coset blocks of cres
+    ~PlonkPeer() {
+        int cur = 0;
+        const bool restore = hipGetDevice(&cur) == hipSuccess;
+        (void)hipSetDevice(device);
+        for (auto w : work)
+            if (w) msm_work_delete(w);
+        if (kzg) gg_msm_base_release(kzg);
+        if (kzg_lag) gg_msm_base_release(kzg_lag);
+        for (auto d : dcos) gg_domain_release(d);
+        for (auto& v : ev) v.clear();
+        for (auto& b : scal) b.release();
+        for (auto& b : in) b.release();
+        for (auto& b : cev) b.release();
+        tw0.release();
+        out.clear();
+        for (hipStream_t x : s)
+            if (x) (void)hipStreamDestroy(x);
+        if (restore) (void)hipSetDevice(cur);
+    }
+};
+
 struct gg_plonk_pk {
     int log_n = 0, log_big = 0;
     size_t n = 0, big = 0, rho = 0;
@@ -228,6 +268,9 @@ struct gg_plonk_pk {
     size_t k_lo = 0, k_hi = 0, l_lo = 0, l_hi = 0;
     gg_g1_reduce_fn reduce = nullptr;
     void* reduce_ctx = nullptr;
+    // one-process multi-GPU: this key is part 0 of 1 + peers.size() device parts
+    std::vector<std::unique_ptr<PlonkPeer>> peers;
+    int owners = 1;  // devices sharing the numerator cosets (coset i -> part i % owners)
     int n_cmt = 0;
     hipStream_t s[4] = {nullptr, nullptr, nullptr, nullptr};
     MsmWork* work[3] = {nullptr, nullptr, nullptr};
@@ -241,6 +284,7 @@ struct gg_plonk_pk {
     size_t ev_next = 0;
     std::mutex mu;
     ~gg_plonk_pk() {
+        peers.clear();
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
         for (auto w : work)
             if (w) msm_work_delete(w);
@@ -291,11 +335,33 @@ void record_wait(gg_plonk_pk* pk, hipStream_t from, hipStream_t to) {
     GG_HIP(hipEventRecord(e, from));
     GG_HIP(hipStreamWaitEvent(to, e, 0));
 }
-// this rank's partial MSM (whole MSM on one GPU); red() completes it
+// a peer part's share of an MSM: its scalar slice copied from the primary GPU
+// (xGMI peer copy), its resident base slice
+BJac peer_msm(gg_plonk_pk* pk, PlonkPeer* p, bool kzg, int wi, const FrB* scal) {
+    GG_HIP(hipSetDevice(p->device));
+    const size_t lo = kzg ? p->k_lo : p->l_lo, hi = kzg ? p->k_hi : p->l_hi;
+    BJac j = BJac::inf();
+    if (hi == lo) return j;
+    GG_HIP(hipMemcpyPeerAsync(p->scal[wi].p, p->device, scal + lo, pk->device, 32 * (hi - lo), p->s[wi]));
+    msm_device_work(kzg ? p->kzg : p->kzg_lag, p->work[wi], p->scal[wi].as<Fr>(), &j, p->s[wi]);
+    return j;
+}
+// this rank's partial MSM (the whole MSM on one GPU, or split over the key's
+// device parts and summed here); red() completes a process shard's partial
 BJac msm_jac(gg_plonk_pk* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStream_t st) {
     BJac j = BJac::inf();
-    const size_t lo = base == pk->kzg ? pk->k_lo : pk->l_lo;
+    const bool kz = base == pk->kzg;
+    const size_t lo = kz ? pk->k_lo : pk->l_lo;
+    std::vector<std::future<BJac>> fs;
+    if (!pk->peers.empty()) {
+        GG_HIP(hipStreamSynchronize(st));  // the scalars are complete before the peers copy them
+        for (auto& p : pk->peers)
+            fs.push_back(std::async(std::launch::async, [pk, pp = p.get(), kz, wi, scal] {
+                return peer_msm(pk, pp, kz, wi, scal);
+            }));
+    }
     msm_device_work(base, pk->work[wi], (const Fr*)(scal + lo), &j, st);
+    for (auto& f : fs) j = jac_add(j, f.get());
     return j;
 }
 // kzg.Commit(p, pk.Kzg) of a buffer of n + 3 scalars (zero beyond the polynomial)
@@ -333,9 +399,12 @@ static void plonk_pk_build(gg_plonk_pk* pk, int log_n, int log_big, const void* 
                            const void* coset_shift, const void* kzg_g1, size_t n_kzg,
                            const void* kzg_lagrange_g1, const void* const* trace, const void* const* qcp,
                            int n_cmt, const int64_t* perm, size_t nb_public, const uint64_t* cmt_idx,
-                           const void* vk_digests, int rank, int world, gg_g1_reduce_fn reduce, void* rctx) {
+                           const void* vk_digests, int rank, int world, gg_g1_reduce_fn reduce, void* rctx,
+                           const int* devices = nullptr, int n_devices = 1) {
     GG_CHECK(world >= 1 && rank >= 0 && rank < world && (world == 1 || reduce), GG_ERR_INVALID_ARG,
              "bad shard (rank, world) or missing reduce callback");
+    GG_CHECK(n_devices >= 1 && n_devices <= 64 && (n_devices == 1 || (devices && world == 1)), GG_ERR_INVALID_ARG,
+             "device parts: 1..64 devices, not combined with process shards");
     pk->rank = rank;
     pk->world = world;
     pk->reduce = reduce;
@@ -359,6 +428,25 @@ static void plonk_pk_build(gg_plonk_pk* pk, int log_n, int log_big, const void* 
     for (int i = 0; i < n_cmt; i++) {
         GG_CHECK(nb_public + cmt_idx[i] < n, GG_ERR_INVALID_ARG, "commitment constraint index out of range");
         pk->cmt_idx.push_back(cmt_idx[i]);
+    }
+    if (n_devices > 1) {
+        int ndev = 0;
+        GG_HIP(hipGetDeviceCount(&ndev));
+        for (int d = 0; d < n_devices; d++)
+            GG_CHECK(devices[d] >= 0 && devices[d] < ndev, GG_ERR_INVALID_ARG, "device id out of range");
+        GG_HIP(hipSetDevice(devices[0]));
+        // xGMI peer access between the distinct devices (copies work without it)
+        for (int a = 0; a < n_devices; a++)
+            for (int b = 0; b < n_devices; b++) {
+                int can = 0;
+                if (devices[a] == devices[b]) continue;
+                if (hipDeviceCanAccessPeer(&can, devices[a], devices[b]) == hipSuccess && can &&
+                    hipSetDevice(devices[a]) == hipSuccess) {
+                    const hipError_t e = hipDeviceEnablePeerAccess(devices[b], 0);
+                    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+                }
+            }
+        GG_HIP(hipSetDevice(devices[0]));
     }
     GG_HIP(hipGetDevice(&pk->device));
     memcpy(pk->omega.v, omega, 32);
@@ -389,8 +477,38 @@ static void plonk_pk_build(gg_plonk_pk* pk, int log_n, int log_big, const void* 
             lo = m * (size_t)pk->rank / (size_t)pk->world;
             hi = m * (size_t)(pk->rank + 1) / (size_t)pk->world;
         };
-        range(n + 3, pk->k_lo, pk->k_hi);
-        range(n, pk->l_lo, pk->l_hi);
+        if (n_devices > 1) {  // part 0 here, parts 1.. on the peers
+            pk->owners = std::min<int>(n_devices, (int)pk->rho);
+            for (int d = 1; d < n_devices; d++) {
+                pk->peers.emplace_back(new PlonkPeer());
+                PlonkPeer* p = pk->peers.back().get();
+                p->device = devices[d];
+                p->k_lo = (n + 3) * d / n_devices;
+                p->k_hi = (n + 3) * (d + 1) / n_devices;
+                p->l_lo = n * d / n_devices;
+                p->l_hi = n * (d + 1) / n_devices;
+                GG_HIP(hipSetDevice(p->device));
+                for (hipStream_t& x : p->s) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+                for (auto& w : p->work) w = msm_work_new();
+                for (auto& b : p->scal) b.alloc(32 * std::max<size_t>(1, std::max(p->k_hi - p->k_lo, p->l_hi - p->l_lo)));
+                int rc = gg_msm_base_create(GG_BLS12_381_G1, (const uint8_t*)kzg_g1 + 96 * p->k_lo, p->k_hi - p->k_lo,
+                                            0, nullptr, 0, &p->kzg);
+                GG_CHECK(rc == GG_OK, rc, gg_last_error());
+                rc = gg_msm_base_create(GG_BLS12_381_G1, (const uint8_t*)kzg_lagrange_g1 + 96 * p->l_lo,
+                                        p->l_hi - p->l_lo, 0, nullptr, 0, &p->kzg_lag);
+                GG_CHECK(rc == GG_OK, rc, gg_last_error());
+                for (size_t i = 0; i < pk->rho; i++)
+                    if ((int)i % pk->owners == d) p->cosets.push_back((int)i);
+            }
+            GG_HIP(hipSetDevice(pk->device));
+            pk->k_lo = 0;
+            pk->k_hi = (n + 3) / n_devices;
+            pk->l_lo = 0;
+            pk->l_hi = n / n_devices;
+        } else {
+            range(n + 3, pk->k_lo, pk->k_hi);
+            range(n, pk->l_lo, pk->l_hi);
+        }
         int rc = gg_msm_base_create(GG_BLS12_381_G1, (const uint8_t*)kzg_g1 + 96 * pk->k_lo, pk->k_hi - pk->k_lo, 0,
                                     nullptr, 0, &pk->kzg);
         GG_CHECK(rc == GG_OK, rc, gg_last_error());
@@ -461,6 +579,30 @@ static void plonk_pk_build(gg_plonk_pk* pk, int log_n, int log_big, const void* 
             coset_eval(pk, srcs[k], F(pk->ev[k][i]), (int)i, st);
         }
     }
+    // peers: their cosets' domains, key evaluations (moved off this GPU) and buffers
+    GG_HIP(hipStreamSynchronize(st));
+    for (auto& pp : pk->peers) {
+        PlonkPeer* p = pp.get();
+        if (p->cosets.empty()) continue;
+        GG_HIP(hipSetDevice(p->device));
+        p->ev.resize(srcs.size());
+        for (int c : p->cosets) p->dcos.push_back(dom(log_n, pk->omega, pk->coset_shift[c]));
+        for (size_t k = 0; k < srcs.size(); k++)
+            for (int c : p->cosets) {
+                p->ev[k].emplace_back(nb);
+                GG_HIP(hipMemcpyPeerAsync(p->ev[k].back().p, p->device, pk->ev[k][c].p, pk->device, nb, p->s[3]));
+            }
+        p->tw0.alloc(nb);
+        GG_HIP(hipMemcpyPeerAsync(p->tw0.p, p->device, pk->tw0.p, pk->device, nb, p->s[3]));
+        for (int k = 0; k < 5 + n_cmt; k++) p->in[k].alloc(nb);
+        for (int k = 0; k < 7 + n_cmt; k++)
+            if (k != 4 && k != 5) p->cev[k].alloc(nb);
+        for (size_t c = 0; c < p->cosets.size(); c++) p->out.emplace_back(nb);
+        GG_HIP(hipStreamSynchronize(p->s[3]));
+        for (size_t k = 0; k < srcs.size(); k++)
+            for (int c : p->cosets) pk->ev[k][c].release();
+    }
+    GG_HIP(hipSetDevice(pk->device));
     pk->perm.alloc(3 * n * 8);
     up(pk->perm.p, perm, 3 * n * 8, false, st);
     // per-proof buffers
@@ -607,69 +749,119 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
         for (int i = 0; i < n_cmt; i++) { g1_raw_bytes(P.bsb22[i], b); fs.bind("alpha", b, 96); }
     }
     const FrB alpha = derive(fs, "alpha", {&P.z});
-    // ---- computeNumerator (prove.go:837-1079): two cosets in flight on s[2], s[3]
+    // ---- computeNumerator (prove.go:837-1079): two cosets in flight on s[2], s[3];
+    // cosets owned by other device parts run there concurrently
     for (int k = 0; k < 4; k++) record_wait(pk, s[k == 3 ? 1 : k], s[2]), record_wait(pk, s[k == 3 ? 1 : k], s[3]);
-    {
+    // the parameters of coset i: e[] = this coset's evaluations of L R O Z (0..3),
+    // Qk (6), Pi_j (7 + j); kev(k) = the key's resident evaluation of poly k there
+    auto coset_params = [&](size_t i, FrB* const* e, auto kev, const FrB* tw0, FrB* cres, bool local) {
         const FrB cs = pk->u, css = pk->u * pk->u;
-        int lb = pk->log_big;
+        plk::NumParams NP{};
+        NP.x[plk::ID_L] = e[0];
+        NP.x[plk::ID_R] = e[1];
+        NP.x[plk::ID_O] = e[2];
+        NP.x[plk::ID_Z] = e[3];
+        NP.x[plk::ID_ZS] = nullptr;  // Z[(j + 1) % n]
+        NP.x[plk::ID_QL] = kev(gg_plonk_pk::E_QL);
+        NP.x[plk::ID_QR] = kev(gg_plonk_pk::E_QR);
+        NP.x[plk::ID_QM] = kev(gg_plonk_pk::E_QM);
+        NP.x[plk::ID_QO] = kev(gg_plonk_pk::E_QO);
+        NP.x[plk::ID_QK] = e[6];
+        NP.x[plk::ID_S1] = kev(gg_plonk_pk::E_S1);
+        NP.x[plk::ID_S2] = kev(gg_plonk_pk::E_S2);
+        NP.x[plk::ID_S3] = kev(gg_plonk_pk::E_S3);
+        NP.x[plk::ID_ID] = kev(gg_plonk_pk::E_X);  // X; beta folded into ka, kb, kc
+        NP.x[plk::ID_LONE] = kev(gg_plonk_pk::E_LONE);
+        for (int j = 0; j < n_cmt; j++) {
+            NP.x[plk::ID_QCI + 2 * j] = kev(gg_plonk_pk::E_QCP0 + j);
+            NP.x[plk::ID_QCI + 2 * j + 1] = e[7 + j];
+        }
+        NP.nx = plk::ID_QCI + 2 * n_cmt;
+        // blinding polynomials scaled for this coset: b_j s^j (s^n - 1) (prove.go:985-993)
+        const FrB sc = pk->coset_shift[i];
+        const FrB sn1 = pow_u64(sc, n) - FrB::one();
+        for (int q4 = 0; q4 < 4; q4++) {
+            FrB acc = sn1;
+            NP.bdeg[q4] = (int)bp[q4].size();
+            for (size_t j = 0; j < bp[q4].size(); j++) {
+                NP.bcoef[q4][j] = bp[q4][j] * acc;
+                acc = acc * sc;
+            }
+        }
+        NP.tw0 = tw0;
+        NP.beta = beta;
+        NP.gamma = gamma;
+        NP.alpha = alpha;
+        NP.cs = cs;
+        NP.css = css;
+        NP.ka = beta;
+        NP.kb = beta * cs;
+        NP.kc = beta * css;
+        NP.n = (uint32_t)n;
+        NP.rho = (uint32_t)pk->rho;
+        NP.coset = (uint32_t)i;
+        NP.log_big = (uint32_t)pk->log_big;
+        NP.cres = cres;
+        NP.local_block = local ? 1u : 0u;
+        return NP;
+    };
+    std::vector<std::future<void>> peer_work;
+    if (!pk->peers.empty()) {
+        for (int k = 0; k < 4; k++) GG_HIP(hipStreamSynchronize(s[k]));  // inputs complete before the copies
+        const int rb = pk->log_big - pk->log_n;
+        for (auto& pp : pk->peers) {
+            PlonkPeer* p = pp.get();
+            if (p->cosets.empty()) continue;
+            peer_work.push_back(std::async(std::launch::async, [&, p, rb] {
+                GG_HIP(hipSetDevice(p->device));
+                hipStream_t q = p->s[3];
+                const FrB* src[5 + plk::MAX_CMT] = {F(pk->cbrev[0]), F(pk->cbrev[1]), F(pk->cbrev[2]), F(pk->cbrev[3]),
+                                                    F(pk->qkc)};
+                for (int j = 0; j < n_cmt; j++) src[5 + j] = F(pk->pi_brev[j]);
+                for (int k = 0; k < 5 + n_cmt; k++)
+                    GG_HIP(hipMemcpyPeerAsync(p->in[k].p, p->device, src[k], pk->device, nb, q));
+                for (size_t c = 0; c < p->cosets.size(); c++) {
+                    const int i = p->cosets[c];
+                    auto ceval = [&](const DevBuf& from, DevBuf& to) {
+                        dcopy(to.p, from.p, nb, q);
+                        plk::ntt(p->dcos[c], to.p, 0, 1, 1, q);  // FFT DIT on the coset
+                    };
+                    for (int k = 0; k < 4; k++) ceval(p->in[k], p->cev[k]);
+                    ceval(p->in[4], p->cev[6]);
+                    for (int j = 0; j < n_cmt; j++) ceval(p->in[5 + j], p->cev[7 + j]);
+                    FrB* e[7 + plk::MAX_CMT] = {};
+                    for (int k = 0; k < 7 + n_cmt; k++) e[k] = F(p->cev[k]);
+                    plk::NumParams NP = coset_params(
+                        (size_t)i, e, [&](int k) { return (const FrB*)F(p->ev[k][c]); }, F(p->tw0), F(p->out[c]),
+                        true);
+                    plk::numerator(NP, q);
+                    const size_t blk = rb ? (size_t)(__builtin_bitreverse32((uint32_t)i) >> (32 - rb)) : 0;
+                    GG_HIP(hipMemcpyPeerAsync(F(pk->cres) + blk * n, pk->device, p->out[c].p, p->device, nb, q));
+                }
+                GG_HIP(hipStreamSynchronize(q));
+            }));
+        }
+    }
+    {
+        int slot = 0;
         for (size_t i = 0; i < pk->rho; i++) {
-            const int slot = (int)(i & 1);
+            if ((int)i % pk->owners != 0) continue;  // another device part's coset
             hipStream_t q = s[2 + slot];
             DevBuf* e = pk->cev[slot];
+            slot ^= 1;
             // per-proof polynomials on this coset: L R O Z, ZS (shift), ID = beta X, Qk, Pi_j
             // (ZS = Z shifted and beta X are formed inside the numerator kernel)
             for (int k = 0; k < 4; k++) coset_eval(pk, F(pk->cbrev[k]), F(e[k]), (int)i, q);
             coset_eval(pk, F(pk->qkc), F(e[6]), (int)i, q);
             for (int j = 0; j < n_cmt; j++) coset_eval(pk, F(pk->pi_brev[j]), F(e[7 + j]), (int)i, q);
-            plk::NumParams NP{};
-            NP.x[plk::ID_L] = F(e[0]);
-            NP.x[plk::ID_R] = F(e[1]);
-            NP.x[plk::ID_O] = F(e[2]);
-            NP.x[plk::ID_Z] = F(e[3]);
-            NP.x[plk::ID_ZS] = nullptr;  // Z[(j + 1) % n]
-            NP.x[plk::ID_QL] = F(pk->ev[gg_plonk_pk::E_QL][i]);
-            NP.x[plk::ID_QR] = F(pk->ev[gg_plonk_pk::E_QR][i]);
-            NP.x[plk::ID_QM] = F(pk->ev[gg_plonk_pk::E_QM][i]);
-            NP.x[plk::ID_QO] = F(pk->ev[gg_plonk_pk::E_QO][i]);
-            NP.x[plk::ID_QK] = F(e[6]);
-            NP.x[plk::ID_S1] = F(pk->ev[gg_plonk_pk::E_S1][i]);
-            NP.x[plk::ID_S2] = F(pk->ev[gg_plonk_pk::E_S2][i]);
-            NP.x[plk::ID_S3] = F(pk->ev[gg_plonk_pk::E_S3][i]);
-            NP.x[plk::ID_ID] = F(pk->ev[gg_plonk_pk::E_X][i]);  // X; beta folded into ka, kb, kc
-            NP.x[plk::ID_LONE] = F(pk->ev[gg_plonk_pk::E_LONE][i]);
-            for (int j = 0; j < n_cmt; j++) {
-                NP.x[plk::ID_QCI + 2 * j] = F(pk->ev[gg_plonk_pk::E_QCP0 + j][i]);
-                NP.x[plk::ID_QCI + 2 * j + 1] = F(e[7 + j]);
-            }
-            NP.nx = plk::ID_QCI + 2 * n_cmt;
-            // blinding polynomials scaled for this coset: b_j s^j (s^n - 1) (prove.go:985-993)
-            const FrB sc = pk->coset_shift[i];
-            const FrB sn1 = pow_u64(sc, n) - FrB::one();
-            for (int q4 = 0; q4 < 4; q4++) {
-                FrB acc = sn1;
-                NP.bdeg[q4] = (int)bp[q4].size();
-                for (size_t j = 0; j < bp[q4].size(); j++) {
-                    NP.bcoef[q4][j] = bp[q4][j] * acc;
-                    acc = acc * sc;
-                }
-            }
-            NP.tw0 = F(pk->tw0);
-            NP.beta = beta;
-            NP.gamma = gamma;
-            NP.alpha = alpha;
-            NP.cs = cs;
-            NP.css = css;
-            NP.ka = beta;
-            NP.kb = beta * cs;
-            NP.kc = beta * css;
-            NP.n = (uint32_t)n;
-            NP.rho = (uint32_t)pk->rho;
-            NP.coset = (uint32_t)i;
-            NP.log_big = (uint32_t)lb;
-            NP.cres = F(pk->cres);
+            FrB* ep[7 + plk::MAX_CMT] = {};
+            for (int k = 0; k < 7 + n_cmt; k++) ep[k] = F(e[k]);
+            plk::NumParams NP = coset_params(
+                i, ep, [&](int k) { return (const FrB*)F(pk->ev[k][i]); }, F(pk->tw0), F(pk->cres), false);
             plk::numerator(NP, q);
         }
     }
+    for (auto& f : peer_work) f.get();  // their blocks of cres have landed
     record_wait(pk, s[3], s[2]);
     plk::divide_by_xn_minus_one(pk->d1, n, F(pk->cres), s[2]);  // h, canonical regular
     for (int k = 0; k < 3; k++) {
@@ -846,6 +1038,34 @@ extern "C" int gg_plonk_pk_create_shard(int log_n, int log_big, const void* omeg
                    kzg_lagrange_g1, trace, qcp, n_cmt, perm, nb_public, commitment_constraint_indexes,
                    vk_digests, rank, world, reduce, reduce_ctx);
     *out = pk.release();
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_pk_create_multi(int log_n, int log_big, const void* omega_mont, const void* omega_big_mont,
+                                        const void* coset_shift_mont, const void* kzg_g1, size_t n_kzg,
+                                        const void* kzg_lagrange_g1, const void* const* trace,
+                                        const void* const* qcp, int n_cmt, const int64_t* perm, size_t nb_public,
+                                        const uint64_t* commitment_constraint_indexes, const void* vk_digests,
+                                        int n_devices, const int* devices, gg_plonk_pk_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out && devices, GG_ERR_INVALID_ARG, "null argument");
+    std::unique_ptr<gg_plonk_pk> pk(new gg_plonk_pk());
+    plonk_pk_build(pk.get(), log_n, log_big, omega_mont, omega_big_mont, coset_shift_mont, kzg_g1, n_kzg,
+                   kzg_lagrange_g1, trace, qcp, n_cmt, perm, nb_public, commitment_constraint_indexes,
+                   vk_digests, 0, 1, nullptr, nullptr, devices, n_devices);
+    *out = pk.release();
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_pk_devices(gg_plonk_pk_t pk, int* devices, int cap, int* n_devices) {
+    GG_CAPI_BEGIN
+    GG_CHECK(pk && n_devices, GG_ERR_INVALID_ARG, "null argument");
+    *n_devices = 1 + (int)pk->peers.size();
+    GG_CHECK(!devices || cap >= *n_devices, GG_ERR_INVALID_ARG, "cap < number of device parts");
+    if (devices) {
+        devices[0] = pk->device;
+        for (size_t i = 0; i < pk->peers.size(); i++) devices[1 + i] = pk->peers[i]->device;
+    }
     GG_CAPI_END
 }
 

@@ -125,12 +125,15 @@ class ProvingKey:
 
     Multi-GPU: shard=(rank, world) keeps this rank's slice of each
     KZG base; `reduce(jac144) -> jac144` (e.g. gnark_amd.dist.allgather_partial)
-    completes every partial commitment; the library calls it in one fixed order."""
+    completes every partial commitment; the library calls it in one fixed order.
+    One process, N GPUs: devices=[d0, d1, ...] splits the key over the devices
+    inside the library (gg_plonk_pk_create_multi: KZG base slices, numerator
+    cosets; ids may repeat); d0 runs the prover, device inputs live there."""
 
     def __init__(self, log_n: int, kzg_g1, kzg_lagrange_g1, ql, qr, qm, qo, qk, s1, s2, s3, perm,
                  qcp: Sequence = (), nb_public: int = 0, commitment_indexes: Sequence[int] = (),
                  basis: str = "lagrange", big_log: Optional[int] = None, shard=None, reduce=None,
-                 vk: Optional[VerifyingKey] = None):
+                 vk: Optional[VerifyingKey] = None, devices: Optional[Sequence[int]] = None):
         self.log_n = log_n
         self.n = n = 1 << log_n
         self.big_log = big_log if big_log is not None else log_n + (2 if n >= 6 else 3)
@@ -183,6 +186,9 @@ class ProvingKey:
                     return 1
             self._reduce_cb = REDUCE_FN(cb)
             check(lib.gg_plonk_pk_create_shard(*args, rank, world, self._reduce_cb, None, ctypes.byref(h)))
+        elif devices is not None and len(devices) > 1:
+            devs = (ctypes.c_int * len(devices))(*devices)
+            check(lib.gg_plonk_pk_create_multi(*args, len(devices), devs, ctypes.byref(h)))
         else:
             check(lib.gg_plonk_pk_create(*args, ctypes.byref(h)))
         self.handle = h
@@ -192,6 +198,14 @@ class ProvingKey:
         d = [bytes(out[96 * i:96 * (i + 1)]) for i in range(8 + self.n_cmt)]
         self.vk = VerifyingKey(n, self.omega, self.g, d[0:3], d[3], d[4], d[5], d[6], d[7], d[8:], nb_public,
                                list(commitment_indexes))
+
+    def devices(self) -> List[int]:
+        """the key's device parts, primary first (gg_plonk_pk_devices)"""
+        k = ctypes.c_int()
+        check(lib.gg_plonk_pk_devices(self.handle, None, 0, ctypes.byref(k)))
+        arr = (ctypes.c_int * k.value)()
+        check(lib.gg_plonk_pk_devices(self.handle, arr, k.value, ctypes.byref(k)))
+        return list(arr)
 
     def commit_lagrange(self, values) -> bytes:
         """kzg.Commit(values, pk.KzgLagrange) -- the commitment of bsb22Hint (prove.go:336)."""

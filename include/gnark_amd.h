@@ -477,6 +477,24 @@ int gg_plonk_pk_create_shard(int log_n, int log_big, const void *omega_mont, con
                              int n_cmt, const int64_t *perm, size_t nb_public,
                              const uint64_t *commitment_constraint_indexes, const void *vk_digests, int rank,
                              int world, gg_g1_reduce_fn reduce, void *reduce_ctx, gg_plonk_pk_t *out);
+/* One process, N GPUs (the Go shape of configs[4] "8xMI355X"): the
+ * key of gg_plonk_pk_create split over devices[0..n_devices) (ids may repeat:
+ * several parts on one GPU).  devices[0] runs the prover DAG; part d holds slice
+ * d of pk.Kzg.G1 and pk.KzgLagrange.G1, so every KZG commitment (prove.go:336,
+ * 494, 769, 1165-1218) is an MSM split over the parts and summed in the library;
+ * the numerator's rho cosets (prove.go:837-1079) go to parts i % min(rho, N),
+ * each with its cosets' key evaluations resident (L, R, O, Z, Qk, Pi_i by peer
+ * copy per proof, the coset block of the quotient back).  The result is the
+ * same proof as the one-GPU key; gg_plonk_prove / commit_lagrange / vk /
+ * release take this handle unchanged.  L, R, O inputs on device live on devices[0]. */
+int gg_plonk_pk_create_multi(int log_n, int log_big, const void *omega_mont, const void *omega_big_mont,
+                             const void *coset_shift_mont, const void *kzg_g1, size_t n_kzg,
+                             const void *kzg_lagrange_g1, const void *const *trace, const void *const *qcp,
+                             int n_cmt, const int64_t *perm, size_t nb_public,
+                             const uint64_t *commitment_constraint_indexes, const void *vk_digests,
+                             int n_devices, const int *devices, gg_plonk_pk_t *out);
+/* the key's device parts: *n_devices, devices[0..) (primary first; devices nullable) */
+int gg_plonk_pk_devices(gg_plonk_pk_t pk, int *devices, int cap, int *n_devices);
 /* the key's vk digests, 96-B affine each: S[0..2], Ql, Qr, Qm, Qo, Qk, Qcp[0..n_cmt) */
 int gg_plonk_pk_vk(gg_plonk_pk_t pk, void *out, size_t cap);
 /* kzg.Commit(values, pk.KzgLagrange): n Lagrange values (host or device) -> affine 96 B.

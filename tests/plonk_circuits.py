@@ -230,14 +230,15 @@ def srs(log_n, tau):
     return kzg, msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bytes(lag), n)
 
 
-def make_key(circ, tau, key_srs=None, shard=None, reduce=None):
+def make_key(circ, tau, key_srs=None, shard=None, reduce=None, devices=None):
     from gnark_amd import plonk_prover as pp, fr
     sel, qcp = circ.selectors()
     perm = circ.permutation()
     s123 = circ.s_polys(perm, fr.bls_domain_generator(circ.log_n), fr.BLS_FR_MULTIPLICATIVE_GEN)
     kzg, kzg_lag = key_srs if key_srs is not None else srs(circ.log_n, tau)
     return pp.ProvingKey(circ.log_n, kzg, kzg_lag, *sel, *s123, perm.tobytes(), qcp=qcp,
-                         nb_public=circ.nb_public, commitment_indexes=circ.cmt_idx, shard=shard, reduce=reduce)
+                         nb_public=circ.nb_public, commitment_indexes=circ.cmt_idx, shard=shard, reduce=reduce,
+                         devices=devices)
 
 
 def to_oracle(pk, proof):

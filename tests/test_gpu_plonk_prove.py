@@ -154,6 +154,36 @@ def test_plonk_prove_sharded_kzg_matches(world):
     assert bo.plonk_verify_trapdoor(pr, vk, tau, public=pub)
 
 
+@pytest.mark.parametrize("log_n,parts,n_cmt", [(6, 2, 1), (7, 3, 2), (8, 4, 0), (8, 8, 1)])
+def test_plonk_prove_multi_device_matches(log_n, parts, n_cmt):
+    """One process, `parts` device parts (gg_plonk_pk_create_multi) rehearsed on
+    this GPU: KZG-base slices per part (commitments split and summed in the
+    library), the numerator's cosets spread over min(rho, parts) parts with the
+    quotient blocks copied back -- exactly the one-GPU proof, also through
+    commit_lagrange (the BSB22 hint) and from device-resident L, R, O."""
+    from gnark_amd import DeviceBuffer, plonk_prover as pp
+    circ = Circuit(log_n, 31 + log_n, nb_public=1, n_cmt=n_cmt)
+    tau = random.Random(log_n + parts).randrange(2, R)
+    key_srs = srs(log_n, tau)
+    pk0 = make_key(circ, tau, key_srs=key_srs)
+    L, Rv, O, pub, cmts = circ.solve(pk0, 6, commit=pk0.commit_lagrange)
+    ref = pp.prove(pk0, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts)
+    pkm = make_key(circ, tau, key_srs=key_srs, devices=[0] * parts)
+    assert pkm.devices() == [0] * parts
+    assert pkm.vk == pk0.vk
+    L2, Rv2, O2, pub2, cmts2 = circ.solve(pkm, 6, commit=pkm.commit_lagrange)
+    assert (L2, Rv2, O2, pub2, cmts2) == (L, Rv, O, pub, cmts)
+    got = pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts)
+    assert got == ref
+    dev = [DeviceBuffer.from_host(x) for x in (L, Rv, O)]
+    got_d = pp.prove(pkm, *dev, rng=random.Random(17), public=pub, commitments=cmts)
+    assert got_d == ref
+    pr, vk = to_oracle(pk0, ref)
+    assert bo.plonk_verify_trapdoor(pr, vk, tau, public=pub)
+    pkm.close()
+    pk0.close()
+
+
 def test_plonk_prove_2p22_verifies():
     """BASELINE configs[4]: a satisfied 2^22 sparse-R1CS circuit (2 public inputs,
     one BSB22 commitment) proven on the GPU and verified (trapdoor KZG checks)."""
@@ -184,3 +214,13 @@ def test_plonk_prove_2p22_verifies():
     assert not bo.plonk_verify_trapdoor(bad, vk, tau, public=pub)
     log("verified")
     pk.close()
+    # BASELINE configs[4] is "8xMI355X": the same proof from a key split over 8
+    # device parts (one process; rehearsed here with every part on this GPU)
+    pk8 = make_key(circ, tau, devices=[0] * 8)
+    log("8-part key")
+    tim = {}
+    t = time.perf_counter()
+    p8 = pp.prove(pk8, L, Rv, O, rng=random.Random(4242), public=pub2, commitments=cmts, timings=tim)
+    log(f"8-part prove {1e3 * (time.perf_counter() - t):.1f} ms {tim}")
+    assert p8 == proof
+    pk8.close()

@@ -21,7 +21,7 @@ if [[ "$S" == *calib* ]]; then
 fi
 if [[ "$S" == *test* ]]; then
   step 600 pytest_$V.txt python -u -m pytest -x -v --timeout 400 --timeout-method thread -m gpu \
-    tests/test_gpu_groth16_multi.py tests/test_gpu_bls_groth16.py tests/test_gpu_groth16_size.py ${PYTEST_ARGS} || exit 2
+    tests/test_gpu_groth16_multi.py tests/test_gpu_bls_groth16.py tests/test_gpu_plonk_prove.py tests/test_gpu_groth16_size.py ${PYTEST_ARGS} || exit 2
 fi
 if [[ "$S" == *bench* ]]; then
   step 400 bench_mpk8_$V.json python -u bench.py --gpus 8 --devices 0,0,0,0,0,0,0,0 --steps 5 --warmup 1 \
