@@ -146,6 +146,7 @@ using namespace gg;
 
 struct gg_scs {
     int device = 0, curve = 0;
+    int64_t expect_inputs = -1;  // gg_scs_set_inputs: required witness length (-1 = not set)
     size_t nw = 0, ncons = 0, nb_public = 0, dom = 0, ncoef = 0;
     std::vector<uint32_t> level_off;
     DevBuf wires, qidx, flags, coef, coef_inv, level_cons, W, L, R, O, solved, fail, inputs, cnt;
@@ -297,6 +298,17 @@ extern "C" int gg_scs_info(gg_scs_t h, size_t* n_wires, size_t* n_constraints, s
     GG_CAPI_END
 }
 
+// newSolver's witness check (constraint/bls12-381/solver.go:71-76) for a
+// sparse R1CS: a solve then requires exactly nb_public + nb_secret values
+extern "C" int gg_scs_set_inputs(gg_scs_t h, size_t nb_public, size_t nb_secret) {
+    GG_CAPI_BEGIN
+    GG_CHECK(h && nb_public + nb_secret >= 1 && nb_public + nb_secret <= h->nw, GG_ERR_INVALID_ARG,
+             "null handle or input count outside [1, wires]");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->expect_inputs = (int64_t)(nb_public + nb_secret);
+    GG_CAPI_END
+}
+
 extern "C" int gg_scs_solve(gg_scs_t h, const void* witness, size_t n_witness, int witness_on_device, void* w_out,
                             void* l_out, void* r_out, void* o_out, int out_on_device, int64_t* failed) {
     GG_CAPI_BEGIN
@@ -304,6 +316,9 @@ extern "C" int gg_scs_solve(gg_scs_t h, const void* witness, size_t n_witness, i
     GG_CHECK(n_witness >= 1 && n_witness <= h->nw, GG_ERR_INVALID_ARG,
              "witness must hold at least one value (solution[0] pads L, R, O) and fit the wires");
     GG_CHECK(witness, GG_ERR_INVALID_ARG, "null witness");
+    if (h->expect_inputs >= 0 && (int64_t)n_witness != h->expect_inputs)
+        throw Error(GG_ERR_INVALID_ARG, "invalid witness size, got " + std::to_string(n_witness) + ", expected " +
+                                            std::to_string(h->expect_inputs));
     std::lock_guard<std::mutex> lk(h->mu);
     GG_HIP(hipSetDevice(h->device));
     if (failed) *failed = -1;

@@ -254,6 +254,7 @@ using namespace gg;
 
 struct gg_r1cs {
     int device = 0;
+    int64_t expect_inputs = -1;  // gg_r1cs_set_inputs: required witness length (-1 = not set)
     int curve = GG_CURVE_BN254;  // scalar field: BN254 fr or BLS12-381 fr
     size_t nw = 0, ncons = 0, nterms = 0, ncoef = 0;
     uint32_t one_idx = 0xffffffffu;
@@ -509,12 +510,26 @@ static void enqueue_levels(gg_r1cs* r) {
     else enqueue_levels_t<FrBlsCfg>(r);
 }
 
+// newSolver's witness check (constraint/bn254/solver.go:71-76): a solve then
+// requires exactly nb_public - 1 + nb_secret values (ONE_WIRE is not passed)
+extern "C" int gg_r1cs_set_inputs(gg_r1cs_t r, size_t nb_public, size_t nb_secret) {
+    GG_CAPI_BEGIN
+    GG_CHECK(r && nb_public >= 1, GG_ERR_INVALID_ARG, "null handle or nb_public < 1 (ONE_WIRE)");
+    GG_CHECK(nb_public + nb_secret <= r->nw, GG_ERR_INVALID_ARG, "more inputs than wires");
+    std::lock_guard<std::mutex> lk(r->mu);
+    r->expect_inputs = (int64_t)(nb_public - 1 + nb_secret);
+    GG_CAPI_END
+}
+
 extern "C" int gg_r1cs_solve(gg_r1cs_t r, const void* witness, size_t n_witness, int witness_on_device,
                              void* w_out, void* a_out, void* b_out, void* c_out, int out_on_device,
                              int64_t* unsatisfied) {
     GG_CAPI_BEGIN
     GG_CHECK(r, GG_ERR_INVALID_ARG, "null handle");
     GG_CHECK(n_witness + 1 <= r->nw, GG_ERR_INVALID_ARG, "witness longer than the wire vector");
+    if (r->expect_inputs >= 0 && (int64_t)n_witness != r->expect_inputs)
+        throw Error(GG_ERR_INVALID_ARG, "invalid witness size, got " + std::to_string(n_witness) + ", expected " +
+                                            std::to_string(r->expect_inputs));
     GG_CHECK(n_witness == 0 || witness, GG_ERR_INVALID_ARG, "null witness");
     std::lock_guard<std::mutex> lk(r->mu);
     GG_HIP(hipSetDevice(r->device));

@@ -138,6 +138,8 @@ def _load():
         "gg_r1cs_info": ([P, ctypes.POINTER(S), ctypes.POINTER(S), ctypes.POINTER(S)], I),
         "gg_r1cs_solve": ([P, P, S, I, P, P, P, P, I, ctypes.POINTER(ctypes.c_int64)], I),
         "gg_r1cs_solution_dev": ([P, PP, PP, PP, PP], I),
+        "gg_r1cs_set_inputs": ([P, S, S], I),
+        "gg_scs_set_inputs": ([P, S, S], I),
         "gg_scs_create": ([I, S, S, S, P, P, P, P, S, P, P, S, PP], I),
         "gg_scs_release": ([P], I),
         "gg_scs_info": ([P, ctypes.POINTER(S), ctypes.POINTER(S), ctypes.POINTER(S)], I),
@@ -180,7 +182,7 @@ EXPORTED = [
     "gg_groth16_mpk_last_timings", "gg_groth16_mpk_create_ex", "gg_groth16_mpk_prove_ex",
     "gg_groth16_mpk_devices", "gg_groth16_mpk_base_info", "gg_groth16_pk_create_shard_ex", "gg_r1cs_create", "gg_r1cs_create_ex", "gg_r1cs_release", "gg_r1cs_info", "gg_r1cs_solve",
     "gg_r1cs_solution_dev", "gg_scs_create", "gg_scs_release", "gg_scs_info", "gg_scs_solve",
-    "gg_scs_solution_dev",
+    "gg_scs_solution_dev", "gg_r1cs_set_inputs", "gg_scs_set_inputs",
 ]
 
 

@@ -87,6 +87,8 @@ class R1CS:
                                     ptr(self.term_coeff), ptr(cbytes), len(coeffs), ptr(lo), ptr(lc),
                                     len(levels), ctypes.byref(h)))
         self.handle = h
+        # newSolver's witness-size check, enforced by the library too (solver.go:71-76)
+        check(lib.gg_r1cs_set_inputs(h, nb_public, nb_secret))
 
     @classmethod
     def from_terms(cls, nb_public: int, nb_secret: int, n_wires: int, constraints, levels=None,
@@ -229,6 +231,7 @@ class SparseR1CS:
                                 ptr(self.flags), ptr(cbytes), len(coeffs), ptr(lo), ptr(lc), len(levels),
                                 ctypes.byref(h)))
         self.handle = h
+        check(lib.gg_scs_set_inputs(h, nb_public, nb_secret))
         d = ctypes.c_size_t()
         check(lib.gg_scs_info(h, None, None, ctypes.byref(d)))
         self.domain = d.value

@@ -23,14 +23,19 @@ import (
 // levels are uploaded once (gg_r1cs_create_ex, BLS12-381 fr), and a solve leaves W, A, B, C in
 // HBM for gg_groth16_prove (inputs_on_device = 1) -- only the witness crosses
 // PCIe.  Built lazily next to setupDevicePointers; nil for systems with hints
-// (hints are Go functions: those keep gnark's solver).
+// (hints are Go functions: those keep gnark's solver).  A multi-GPU key has one
+// solver per device, each leaving the whole solution on its GPU
+// (gg_groth16_mpk_prove_ex reads shard r's copy on devices[r]).
 type deviceSolver struct {
-	h       C.gg_r1cs_t
-	nbWires int
-	nbCons  int
+	h        C.gg_r1cs_t
+	nbWires  int
+	nbCons   int
+	nbInputs int // witness length: nbPublic - 1 + nbSecret (solver.go:71-76)
 }
 
-func newDeviceSolver(sys *cs.R1CS) (*deviceSolver, error) {
+// newDeviceSolvers builds the CSR form of a hint-free system once and uploads
+// it to every distinct device of devs (nil map: the system has hints).
+func newDeviceSolvers(sys *cs.R1CS, devs []int) (map[int]*deviceSolver, error) {
 	for _, inst := range sys.Instructions {
 		if _, ok := sys.Blueprints[inst.BlueprintID].(constraint.BlueprintHint); ok {
 			return nil, nil
@@ -60,19 +65,41 @@ func newDeviceSolver(sys *cs.R1CS) (*deviceSolver, error) {
 		}
 		levelOff = append(levelOff, uint32(len(levelCons)))
 	}
-	nbWires := sys.GetNbPublicVariables() + sys.GetNbSecretVariables() + sys.NbInternalVariables
+	nbPublic, nbSecret := sys.GetNbPublicVariables(), sys.GetNbSecretVariables()
+	nbWires := nbPublic + nbSecret + sys.NbInternalVariables
 	if len(wires) == 0 || len(levelCons) == 0 || len(sys.Coefficients) == 0 {
 		return nil, nil
 	}
-	var h C.gg_r1cs_t
-	if C.gg_r1cs_create_ex(C.GG_CURVE_BLS12_381, C.size_t(nbWires), C.size_t(len(rs)),
-		(*C.uint32_t)(unsafe.Pointer(&off[0])), (*C.uint32_t)(unsafe.Pointer(&wires[0])),
-		(*C.uint32_t)(unsafe.Pointer(&coeffs[0])), unsafe.Pointer(&sys.Coefficients[0]),
-		C.size_t(len(sys.Coefficients)), (*C.uint32_t)(unsafe.Pointer(&levelOff[0])),
-		(*C.uint32_t)(unsafe.Pointer(&levelCons[0])), C.size_t(len(sys.Levels)), &h) != C.GG_OK {
-		return nil, lastError()
+	out := map[int]*deviceSolver{}
+	for _, dev := range devs {
+		if _, ok := out[dev]; ok {
+			continue
+		}
+		var h C.gg_r1cs_t
+		err := onDevice(dev, func() error {
+			if C.gg_r1cs_create_ex(C.GG_CURVE_BLS12_381, C.size_t(nbWires), C.size_t(len(rs)),
+				(*C.uint32_t)(unsafe.Pointer(&off[0])), (*C.uint32_t)(unsafe.Pointer(&wires[0])),
+				(*C.uint32_t)(unsafe.Pointer(&coeffs[0])), unsafe.Pointer(&sys.Coefficients[0]),
+				C.size_t(len(sys.Coefficients)), (*C.uint32_t)(unsafe.Pointer(&levelOff[0])),
+				(*C.uint32_t)(unsafe.Pointer(&levelCons[0])), C.size_t(len(sys.Levels)), &h) != C.GG_OK {
+				return lastError()
+			}
+			// the library rejects a witness of another size too (a second line of defence)
+			if C.gg_r1cs_set_inputs(h, C.size_t(nbPublic), C.size_t(nbSecret)) != C.GG_OK {
+				C.gg_r1cs_release(h)
+				return lastError()
+			}
+			return nil
+		})
+		if err != nil {
+			for _, ds := range out {
+				ds.release()
+			}
+			return nil, err
+		}
+		out[dev] = &deviceSolver{h: h, nbWires: nbWires, nbCons: len(rs), nbInputs: nbPublic - 1 + nbSecret}
 	}
-	return &deviceSolver{h: h, nbWires: nbWires, nbCons: len(rs)}, nil
+	return out, nil
 }
 
 // solve runs the levels on the GPU and returns the device pointers of W, A, B, C
@@ -81,6 +108,9 @@ func (d *deviceSolver) solve(fullWitness witness.Witness) (w, a, b, c unsafe.Poi
 	vec, ok := fullWitness.Vector().(fr.Vector)
 	if !ok {
 		return nil, nil, nil, nil, fmt.Errorf("gnark_amd: witness is not a bls12-381 fr.Vector")
+	}
+	if len(vec) != d.nbInputs { // newSolver (solver.go:71-76)
+		return nil, nil, nil, nil, fmt.Errorf("invalid witness size, got %d, expected %d", len(vec), d.nbInputs)
 	}
 	var in unsafe.Pointer
 	if len(vec) > 0 {

@@ -13,6 +13,8 @@ import "C"
 import (
 	"fmt"
 	"math/big"
+	"runtime"
+	"sync"
 	"time"
 	"unsafe"
 
@@ -43,8 +45,23 @@ func ptrOr(b bool, p unsafe.Pointer) unsafe.Pointer {
 	return nil
 }
 
+var setupMu sync.Mutex // one key upload at a time (concurrent first Prove calls)
+
+// onDevice runs fn on an OS thread bound to GPU dev (gg_set_device binds the
+// calling thread; a goroutine must not migrate between the bind and the calls).
+func onDevice(dev int, fn func() error) error {
+	runtime.LockOSThread()
+	defer runtime.UnlockOSThread()
+	if C.gg_set_device(C.int(dev)) != C.GG_OK {
+		return lastError()
+	}
+	return fn()
+}
+
 // setupDevicePointers uploads pk once (replaces icicle.go:31-130).
 func (pk *ProvingKey) setupDevicePointers(nbPublic int, kWireIndex []uint32) error {
+	setupMu.Lock()
+	defer setupMu.Unlock()
 	if pk.deviceInfo != nil {
 		return nil
 	}
@@ -65,14 +82,15 @@ func (pk *ProvingKey) setupDevicePointers(nbPublic int, kWireIndex []uint32) err
 		}
 	}
 	p := func(s unsafe.Pointer, n int) unsafe.Pointer { return ptrOr(n > 0, s) }
-	if devs := configuredDevices(); len(devs) > 1 {
-		// one shard per GPU, driven from this process (gg_groth16_mpk_create)
+	devs := configuredDevices()
+	if len(devs) > 1 {
+		// one shard per GPU, driven from this process (gg_groth16_mpk_create_ex)
 		cdevs := make([]C.int, len(devs))
 		for i, d := range devs {
 			cdevs[i] = C.int(d)
 		}
 		var mh C.gg_groth16_mpk_t
-		rc := C.gg_groth16_mpk_create(C.int(logN),
+		rc := C.gg_groth16_mpk_create_ex(C.GG_CURVE_BN254, C.int(logN),
 			unsafe.Pointer(&pk.Domain.Generator), unsafe.Pointer(&pk.Domain.FrMultiplicativeGen),
 			p(unsafe.Pointer(unsafe.SliceData(pk.G1.A)), len(pk.G1.A)), C.size_t(len(pk.G1.A)),
 			p(unsafe.Pointer(unsafe.SliceData(pk.G1.B)), len(pk.G1.B)), C.size_t(len(pk.G1.B)),
@@ -88,40 +106,126 @@ func (pk *ProvingKey) setupDevicePointers(nbPublic int, kWireIndex []uint32) err
 		if rc != C.GG_OK {
 			return lastError()
 		}
-		pk.deviceInfo = &deviceInfo{handle: unsafe.Pointer(mh), multi: true}
+		pk.deviceInfo = &deviceInfo{handle: unsafe.Pointer(mh), multi: true, devices: devs}
 		return nil
 	}
-	var h C.gg_groth16_pk_t
-	rc := C.gg_groth16_pk_create(C.int(logN),
-		unsafe.Pointer(&pk.Domain.Generator), unsafe.Pointer(&pk.Domain.FrMultiplicativeGen),
-		p(unsafe.Pointer(unsafe.SliceData(pk.G1.A)), len(pk.G1.A)), C.size_t(len(pk.G1.A)),
-		p(unsafe.Pointer(unsafe.SliceData(pk.G1.B)), len(pk.G1.B)), C.size_t(len(pk.G1.B)),
-		p(unsafe.Pointer(unsafe.SliceData(pk.G1.Z)), len(pk.G1.Z)), C.size_t(len(pk.G1.Z)),
-		p(unsafe.Pointer(unsafe.SliceData(pk.G1.K)), len(pk.G1.K)), C.size_t(len(pk.G1.K)),
-		unsafe.Pointer(&pk.G1.Alpha), unsafe.Pointer(&pk.G1.Beta), unsafe.Pointer(&pk.G1.Delta),
-		p(unsafe.Pointer(unsafe.SliceData(pk.G2.B)), len(pk.G2.B)),
-		unsafe.Pointer(&pk.G2.Beta), unsafe.Pointer(&pk.G2.Delta),
-		(*C.uint8_t)(unsafe.Pointer(&infA[0])), (*C.uint8_t)(unsafe.Pointer(&infB[0])),
-		C.size_t(nWires), C.size_t(nbPublic),
-		(*C.uint32_t)(p(unsafe.Pointer(unsafe.SliceData(kWireIndex)), len(kWireIndex))), &h)
-	if rc != C.GG_OK {
-		return lastError()
+	dev := 0
+	if len(devs) == 1 {
+		dev = devs[0]
 	}
-	pk.deviceInfo = &deviceInfo{handle: unsafe.Pointer(h)}
+	var h C.gg_groth16_pk_t
+	err := onDevice(dev, func() error {
+		if C.gg_groth16_pk_create_ex(C.GG_CURVE_BN254, C.int(logN),
+			unsafe.Pointer(&pk.Domain.Generator), unsafe.Pointer(&pk.Domain.FrMultiplicativeGen),
+			p(unsafe.Pointer(unsafe.SliceData(pk.G1.A)), len(pk.G1.A)), C.size_t(len(pk.G1.A)),
+			p(unsafe.Pointer(unsafe.SliceData(pk.G1.B)), len(pk.G1.B)), C.size_t(len(pk.G1.B)),
+			p(unsafe.Pointer(unsafe.SliceData(pk.G1.Z)), len(pk.G1.Z)), C.size_t(len(pk.G1.Z)),
+			p(unsafe.Pointer(unsafe.SliceData(pk.G1.K)), len(pk.G1.K)), C.size_t(len(pk.G1.K)),
+			unsafe.Pointer(&pk.G1.Alpha), unsafe.Pointer(&pk.G1.Beta), unsafe.Pointer(&pk.G1.Delta),
+			p(unsafe.Pointer(unsafe.SliceData(pk.G2.B)), len(pk.G2.B)),
+			unsafe.Pointer(&pk.G2.Beta), unsafe.Pointer(&pk.G2.Delta),
+			(*C.uint8_t)(unsafe.Pointer(&infA[0])), (*C.uint8_t)(unsafe.Pointer(&infB[0])),
+			C.size_t(nWires), C.size_t(nbPublic),
+			(*C.uint32_t)(p(unsafe.Pointer(unsafe.SliceData(kWireIndex)), len(kWireIndex))), &h) != C.GG_OK {
+			return lastError()
+		}
+		return nil
+	})
+	if err != nil {
+		return err
+	}
+	pk.deviceInfo = &deviceInfo{handle: unsafe.Pointer(h), devices: []int{dev}}
 	return nil
 }
 
 // Release frees the HBM-resident key (the icicle path never frees it).
 func (pk *ProvingKey) Release() {
-	if pk.deviceInfo != nil {
-		pk.deviceInfo.solver.release()
-		if pk.deviceInfo.multi {
-			C.gg_groth16_mpk_release(C.gg_groth16_mpk_t(pk.deviceInfo.handle))
-		} else {
-			C.gg_groth16_pk_release(C.gg_groth16_pk_t(pk.deviceInfo.handle))
+	setupMu.Lock()
+	defer setupMu.Unlock()
+	if di := pk.deviceInfo; di != nil {
+		di.mu.Lock()
+		for _, ds := range di.solvers {
+			ds.release()
 		}
+		if di.multi {
+			C.gg_groth16_mpk_release(C.gg_groth16_mpk_t(di.handle))
+		} else {
+			C.gg_groth16_pk_release(C.gg_groth16_pk_t(di.handle))
+		}
+		di.mu.Unlock()
 		pk.deviceInfo = nil
 	}
+}
+
+// proveOnDeviceSolution solves a hint-free system on every GPU of the key
+// (gg_r1cs_solve, the solution stays in HBM) and proves from there: the
+// witness is the only per-proof PCIe traffic.  Holds di.mu from the solve to
+// the end of the prove (the prove reads the solvers' resident vectors).
+func (di *deviceInfo) proveOnDeviceSolution(fullWitness witness.Witness, ar *curve.G1Affine, bs *curve.G2Affine,
+	krs *curve.G1Affine) error {
+	var r, s fr.Element
+	if _, err := r.SetRandom(); err != nil {
+		return err
+	}
+	if _, err := s.SetRandom(); err != nil {
+		return err
+	}
+	di.mu.Lock()
+	defer di.mu.Unlock()
+	type sol struct{ w, a, b, c unsafe.Pointer }
+	sols := make(map[int]sol, len(di.solvers))
+	errs := make(chan error, len(di.solvers))
+	var smu sync.Mutex
+	var wg sync.WaitGroup
+	for dev, ds := range di.solvers {
+		wg.Add(1)
+		go func(dev int, ds *deviceSolver) {
+			defer wg.Done()
+			w, a, b, c, err := ds.solve(fullWitness)
+			if err != nil {
+				errs <- err
+				return
+			}
+			smu.Lock()
+			sols[dev] = sol{w, a, b, c}
+			smu.Unlock()
+		}(dev, ds)
+	}
+	wg.Wait()
+	close(errs)
+	if err := <-errs; err != nil {
+		return err
+	}
+	var ds0 *deviceSolver
+	for _, ds := range di.solvers {
+		ds0 = ds
+		break
+	}
+	if !di.multi {
+		x := sols[di.devices[0]]
+		if C.gg_groth16_prove(C.gg_groth16_pk_t(di.handle), x.w, C.size_t(ds0.nbWires), x.a, x.b, x.c,
+			C.size_t(ds0.nbCons), 1, unsafe.Pointer(&r), unsafe.Pointer(&s),
+			unsafe.Pointer(ar), unsafe.Pointer(bs), unsafe.Pointer(krs), nil) != C.GG_OK {
+			return lastError()
+		}
+		return nil
+	}
+	// per-shard device pointers (C memory: device addresses, no Go pointers)
+	world := len(di.devices)
+	ptrs := C.malloc(C.size_t(4*world) * C.size_t(unsafe.Sizeof(uintptr(0))))
+	defer C.free(ptrs)
+	ps := unsafe.Slice((*unsafe.Pointer)(ptrs), 4*world)
+	for i, dev := range di.devices {
+		x := sols[dev]
+		ps[i], ps[world+i], ps[2*world+i], ps[3*world+i] = x.w, x.a, x.b, x.c
+	}
+	if C.gg_groth16_mpk_prove_ex(C.gg_groth16_mpk_t(di.handle), 1, (*unsafe.Pointer)(&ps[0]),
+		C.size_t(ds0.nbWires), (*unsafe.Pointer)(&ps[world]), (*unsafe.Pointer)(&ps[2*world]),
+		(*unsafe.Pointer)(&ps[3*world]), C.size_t(ds0.nbCons), unsafe.Pointer(&r), unsafe.Pointer(&s),
+		unsafe.Pointer(ar), unsafe.Pointer(bs), unsafe.Pointer(krs)) != C.GG_OK {
+		return lastError()
+	}
+	return nil
 }
 
 // Prove mirrors icicle_bn254.Prove (icicle.go:133-422): identical solver,
@@ -200,35 +304,19 @@ func Prove(r1cs *cs.R1CS, pk *ProvingKey, fullWitness witness.Witness, opts ...b
 			solver.OverrideHint(r1cs.GkrInfo.ProveHintID, cs.GkrProveHint(r1cs.GkrInfo.HashName, &gkrData)))
 	}
 
-	// hint-free systems without commitments: r1cs.Solve on the GPU, the solution
-	// stays in HBM (solver_amd.go); everything else keeps gnark's solver
-	if !pk.deviceInfo.multi && len(commitmentInfo) == 0 && len(opt.SolverOpts) == 0 && !r1cs.GkrInfo.Is() {
-		if !pk.deviceInfo.solverTried {
-			pk.deviceInfo.solverTried = true
-			if pk.deviceInfo.solver, err = newDeviceSolver(r1cs); err != nil {
-				return nil, fmt.Errorf("device solver: %w", err)
-			}
+	// hint-free systems without commitments: r1cs.Solve on the GPU(s) of the
+	// key, the solution stays in HBM (solver_amd.go); everything else keeps
+	// gnark's solver
+	if len(commitmentInfo) == 0 && len(opt.SolverOpts) == 0 && !r1cs.GkrInfo.Is() {
+		di := pk.deviceInfo
+		di.solverOnce.Do(func() { di.solvers, di.solverErr = newDeviceSolvers(r1cs, di.devices) })
+		if di.solverErr != nil {
+			return nil, fmt.Errorf("device solver: %w", di.solverErr)
 		}
-		if ds := pk.deviceInfo.solver; ds != nil {
-			w, a, b, c, err := ds.solve(fullWitness)
-			if err != nil {
+		if len(di.solvers) > 0 {
+			if err := di.proveOnDeviceSolution(fullWitness, &proof.Ar, &proof.Bs, &proof.Krs); err != nil {
 				return nil, err
 			}
-			var r, s fr.Element
-			if _, err := r.SetRandom(); err != nil {
-				return nil, err
-			}
-			if _, err := s.SetRandom(); err != nil {
-				return nil, err
-			}
-			var ar, krs curve.G1Affine
-			var bs curve.G2Affine
-			if C.gg_groth16_prove(C.gg_groth16_pk_t(pk.deviceInfo.handle), w, C.size_t(ds.nbWires), a, b, c,
-				C.size_t(ds.nbCons), 1, unsafe.Pointer(&r), unsafe.Pointer(&s),
-				unsafe.Pointer(&ar), unsafe.Pointer(&bs), unsafe.Pointer(&krs), nil) != C.GG_OK {
-				return nil, lastError()
-			}
-			proof.Ar, proof.Bs, proof.Krs = ar, bs, krs
 			return proof, nil
 		}
 	}

@@ -20,37 +20,49 @@ import (
 // several devices are configured, one gg_groth16_mpk_t (a shard per GPU, the
 // distributed computeH's exchanges done inside the library).
 type deviceInfo struct {
-	handle      unsafe.Pointer
-	multi       bool
-	solver      *deviceSolver // GPU r1cs.Solve (nil: the system has hints)
-	solverTried bool
+	handle  unsafe.Pointer
+	multi   bool
+	devices []int // the key's GPUs (shard order; one entry for a single-GPU key)
+
+	// GPU r1cs.Solve, one solver per distinct device of the key (empty: the
+	// system has hints).  Built once; a GPU-solved proof holds mu from the solve
+	// to the end of the prove, because the prove reads the solvers' resident
+	// W, A, B, C, which the next solve overwrites.
+	solverOnce sync.Once
+	solverErr  error
+	solvers    map[int]*deviceSolver
+	mu         sync.Mutex
 }
 
 var (
-	devicesMu sync.Mutex
-	devices   []int
+	devicesMu  sync.Mutex
+	devices    []int
+	configured bool
 )
 
 // SetDevices selects the GPUs keys created afterwards are sharded over
-// (the SURVEY 8(b) gg_init(ngpu) shape).  nil / one id: a single GPU.  The
-// default comes from GNARK_AMD_DEVICES ("0,1,2,3,4,5,6,7").
+// (the SURVEY 8(b) gg_init(ngpu) shape).  nil / empty: the default GPU; one id:
+// that GPU.  An explicit call wins over GNARK_AMD_DEVICES ("0,1,2,3,4,5,6,7"),
+// which is read only when SetDevices was never called.
 func SetDevices(ids []int) {
 	devicesMu.Lock()
 	defer devicesMu.Unlock()
-	devices = append([]int(nil), ids...)
+	devices = append([]int{}, ids...)
+	configured = true
 }
 
 func configuredDevices() []int {
 	devicesMu.Lock()
 	defer devicesMu.Unlock()
-	if devices == nil {
+	if !configured {
 		for _, f := range strings.Split(os.Getenv("GNARK_AMD_DEVICES"), ",") {
 			if id, err := strconv.Atoi(strings.TrimSpace(f)); err == nil {
 				devices = append(devices, id)
 			}
 		}
+		configured = true
 	}
-	return devices
+	return append([]int{}, devices...)
 }
 
 // ProvingKey embeds the CPU key so WriteTo/ReadFrom/... are promoted unchanged

@@ -28,7 +28,11 @@ import (
 	"fmt"
 	"hash"
 	"math/big"
+	"os"
+	"runtime"
 	"runtime/cgo"
+	"strconv"
+	"strings"
 	"sync"
 	"unsafe"
 
@@ -51,6 +55,66 @@ func amdError() error { return fmt.Errorf("gnark_amd: %s", C.GoString(C.gg_last_
 
 // device keys, one per *ProvingKey (HBM-resident; released by ReleaseAMD)
 var amdKeys sync.Map
+
+// per-key lock of the GPU-solved path: the prove reads the solver's resident
+// L, R, O, which the next solve on the same key overwrites
+var amdLocks sync.Map // *ProvingKey -> *sync.Mutex
+
+func (pk *ProvingKey) amdLock() *sync.Mutex {
+	m, _ := amdLocks.LoadOrStore(pk, &sync.Mutex{})
+	return m.(*sync.Mutex)
+}
+
+var (
+	amdDevicesMu  sync.Mutex
+	amdDevices    []int
+	amdConfigured bool
+)
+
+// SetAMDDevices selects the GPUs PlonK keys created afterwards are split over
+// (gg_plonk_pk_create_multi: KZG base slices and numerator cosets per device,
+// all driven from this process; configs[4] "8xMI355X").  nil / empty: the
+// default GPU; one id: that GPU.  An explicit call wins over GNARK_AMD_DEVICES.
+func SetAMDDevices(ids []int) {
+	amdDevicesMu.Lock()
+	defer amdDevicesMu.Unlock()
+	amdDevices = append([]int{}, ids...)
+	amdConfigured = true
+}
+
+func amdConfiguredDevices() []int {
+	amdDevicesMu.Lock()
+	defer amdDevicesMu.Unlock()
+	if !amdConfigured {
+		for _, f := range strings.Split(os.Getenv("GNARK_AMD_DEVICES"), ",") {
+			if id, err := strconv.Atoi(strings.TrimSpace(f)); err == nil {
+				amdDevices = append(amdDevices, id)
+			}
+		}
+		amdConfigured = true
+	}
+	return append([]int{}, amdDevices...)
+}
+
+// onAMDDevice runs fn on an OS thread bound to GPU dev (gg_set_device binds the
+// calling thread; the goroutine must not migrate between the bind and the calls).
+func onAMDDevice(dev int, fn func() error) error {
+	runtime.LockOSThread()
+	defer runtime.UnlockOSThread()
+	if C.gg_set_device(C.int(dev)) != C.GG_OK {
+		return amdError()
+	}
+	return fn()
+}
+
+// amdPrimaryDevice is the GPU that runs the prover of pk's device key (and
+// holds the GPU solver's L, R, O).
+func amdPrimaryDevice() int {
+	if devs := amdConfiguredDevices(); len(devs) > 0 {
+		return devs[0]
+	}
+	return 0
+}
 
 func (pk *ProvingKey) amdKey() (C.gg_plonk_pk_t, error) {
 	if h, ok := amdKeys.Load(pk); ok {
@@ -85,15 +149,35 @@ func (pk *ProvingKey) amdKey() (C.gg_plonk_pk_t, error) {
 	defer C.free(cqcp)
 	copy(unsafe.Slice((*unsafe.Pointer)(cqcp), len(qcp)), qcp)
 	var h C.gg_plonk_pk_t
-	rc := C.gg_plonk_pk_create(C.int(logN), C.int(logBig),
-		unsafe.Pointer(&pk.Domain[0].Generator), unsafe.Pointer(&pk.Domain[1].Generator),
-		unsafe.Pointer(&pk.Domain[0].FrMultiplicativeGen),
-		unsafe.Pointer(&pk.Kzg.G1[0]), C.size_t(len(pk.Kzg.G1)), unsafe.Pointer(&pk.KzgLagrange.G1[0]),
-		(*unsafe.Pointer)(ctr), (*unsafe.Pointer)(cqcp), C.int(len(pk.trace.Qcp)),
-		(*C.int64_t)(unsafe.Pointer(&pk.trace.S[0])), C.size_t(pk.Vk.NbPublicVariables),
-		(*C.uint64_t)(unsafe.Pointer(&idx[0])), unsafe.Pointer(&vk[0]), &h)
-	if rc != C.GG_OK {
-		return nil, amdError()
+	devs := amdConfiguredDevices()
+	if len(devs) > 1 {
+		cdevs := make([]C.int, len(devs))
+		for i, d := range devs {
+			cdevs[i] = C.int(d)
+		}
+		if C.gg_plonk_pk_create_multi(C.int(logN), C.int(logBig),
+			unsafe.Pointer(&pk.Domain[0].Generator), unsafe.Pointer(&pk.Domain[1].Generator),
+			unsafe.Pointer(&pk.Domain[0].FrMultiplicativeGen),
+			unsafe.Pointer(&pk.Kzg.G1[0]), C.size_t(len(pk.Kzg.G1)), unsafe.Pointer(&pk.KzgLagrange.G1[0]),
+			(*unsafe.Pointer)(ctr), (*unsafe.Pointer)(cqcp), C.int(len(pk.trace.Qcp)),
+			(*C.int64_t)(unsafe.Pointer(&pk.trace.S[0])), C.size_t(pk.Vk.NbPublicVariables),
+			(*C.uint64_t)(unsafe.Pointer(&idx[0])), unsafe.Pointer(&vk[0]), C.int(len(devs)), &cdevs[0],
+			&h) != C.GG_OK {
+			return nil, amdError()
+		}
+	} else if err := onAMDDevice(amdPrimaryDevice(), func() error {
+		if C.gg_plonk_pk_create(C.int(logN), C.int(logBig),
+			unsafe.Pointer(&pk.Domain[0].Generator), unsafe.Pointer(&pk.Domain[1].Generator),
+			unsafe.Pointer(&pk.Domain[0].FrMultiplicativeGen),
+			unsafe.Pointer(&pk.Kzg.G1[0]), C.size_t(len(pk.Kzg.G1)), unsafe.Pointer(&pk.KzgLagrange.G1[0]),
+			(*unsafe.Pointer)(ctr), (*unsafe.Pointer)(cqcp), C.int(len(pk.trace.Qcp)),
+			(*C.int64_t)(unsafe.Pointer(&pk.trace.S[0])), C.size_t(pk.Vk.NbPublicVariables),
+			(*C.uint64_t)(unsafe.Pointer(&idx[0])), unsafe.Pointer(&vk[0]), &h) != C.GG_OK {
+			return amdError()
+		}
+		return nil
+	}); err != nil {
+		return nil, err
 	}
 	if old, loaded := amdKeys.LoadOrStore(pk, h); loaded {
 		C.gg_plonk_pk_release(h)
@@ -104,6 +188,9 @@ func (pk *ProvingKey) amdKey() (C.gg_plonk_pk_t, error) {
 
 // ReleaseAMD frees the HBM-resident copy of pk.
 func (pk *ProvingKey) ReleaseAMD() {
+	mu := pk.amdLock()
+	mu.Lock()
+	defer mu.Unlock()
 	pk.releaseSolver()
 	if h, ok := amdKeys.LoadAndDelete(pk); ok {
 		C.gg_plonk_pk_release(h.(C.gg_plonk_pk_t))
@@ -183,6 +270,11 @@ func proveAMD(spr *cs.SparseR1CS, pk *ProvingKey, fullWitness witness.Witness, o
 	if !ok {
 		return nil, witness.ErrInvalidWitness
 	}
+	// newSolver's check (constraint/bls12-381/solver.go:71-76): the public
+	// inputs below are read from w[:len(spr.Public)]
+	if exp := spr.GetNbPublicVariables() + spr.GetNbSecretVariables(); len(w) != exp {
+		return nil, fmt.Errorf("invalid witness size, got %d, expected %d", len(w), exp)
+	}
 	// hint-free systems without commitments: spr.Solve on the GPU, L, R, O stay
 	// in HBM (solver_amd.go); everything else keeps gnark's solver
 	var lro [3]unsafe.Pointer
@@ -193,6 +285,10 @@ func proveAMD(spr *cs.SparseR1CS, pk *ProvingKey, fullWitness witness.Witness, o
 			return nil, err
 		}
 		if ds != nil {
+			// held until gg_plonk_prove has read L, R, O from the solver's buffers
+			mu := pk.amdLock()
+			mu.Lock()
+			defer mu.Unlock()
 			if lro[0], lro[1], lro[2], err = ds.solve(fullWitness); err != nil {
 				return nil, err
 			}

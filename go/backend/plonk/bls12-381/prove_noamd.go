@@ -18,3 +18,6 @@ func proveAMD(spr *cs.SparseR1CS, pk *ProvingKey, fullWitness witness.Witness, o
 }
 
 func (pk *ProvingKey) ReleaseAMD() {}
+
+// SetAMDDevices is a no-op without the amd build tag.
+func SetAMDDevices(ids []int) {}

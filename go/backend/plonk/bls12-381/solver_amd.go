@@ -70,6 +70,11 @@ func newScsSolver(spr *cs.SparseR1CS) (*scsSolver, error) {
 		(*C.uint32_t)(unsafe.Pointer(&levelCons[0])), C.size_t(len(spr.Levels)), &h) != C.GG_OK {
 		return nil, amdError()
 	}
+	// the library rejects a witness of another size too (solver.go:71-76)
+	if C.gg_scs_set_inputs(h, C.size_t(spr.GetNbPublicVariables()), C.size_t(spr.GetNbSecretVariables())) != C.GG_OK {
+		C.gg_scs_release(h)
+		return nil, amdError()
+	}
 	return &scsSolver{h: h}, nil
 }
 
@@ -77,11 +82,22 @@ func (pk *ProvingKey) amdSolver(spr *cs.SparseR1CS) (*scsSolver, error) {
 	if s, ok := amdSolvers.Load(pk); ok {
 		return s.(*scsSolver), nil
 	}
-	s, err := newScsSolver(spr)
+	var s *scsSolver
+	// on the GPU that runs the prover: gg_plonk_prove reads L, R, O there
+	err := onAMDDevice(amdPrimaryDevice(), func() error {
+		var err error
+		s, err = newScsSolver(spr)
+		return err
+	})
 	if err != nil {
 		return nil, err
 	}
-	amdSolvers.Store(pk, s)
+	if old, loaded := amdSolvers.LoadOrStore(pk, s); loaded { // a concurrent first call won
+		if s != nil {
+			C.gg_scs_release(s.h)
+		}
+		return old.(*scsSolver), nil
+	}
 	return s, nil
 }
 

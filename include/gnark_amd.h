@@ -564,6 +564,10 @@ int gg_r1cs_info(gg_r1cs_t r, size_t *n_wires, size_t *n_constraints, size_t *n_
 int gg_r1cs_solve(gg_r1cs_t r, const void *witness, size_t n_witness, int witness_on_device,
                   void *w_out, void *a_out, void *b_out, void *c_out, int out_on_device,
                   int64_t *unsatisfied);
+/* newSolver's witness-size check (solver.go:71-76): afterwards gg_r1cs_solve
+ * fails with "invalid witness size, got %d, expected %d" unless
+ * n_witness == nb_public - 1 + nb_secret (r1cs.GetNbPublicVariables() counts ONE_WIRE) */
+int gg_r1cs_set_inputs(gg_r1cs_t r, size_t nb_public, size_t nb_secret);
 /* device pointers of the handle's resident W, A, B, C (valid until the next
  * solve or the release): a prove can read them without a copy */
 int gg_r1cs_solution_dev(gg_r1cs_t r, void **w, void **a, void **b, void **c);
@@ -590,6 +594,8 @@ int gg_scs_info(gg_scs_t h, size_t *n_wires, size_t *n_constraints, size_t *doma
 int gg_scs_solve(gg_scs_t h, const void *witness, size_t n_witness, int witness_on_device, void *w_out,
                  void *l_out, void *r_out, void *o_out, int out_on_device, int64_t *failed);
 int gg_scs_solution_dev(gg_scs_t h, void **w, void **l, void **r, void **o);
+/* the same check for a sparse R1CS: n_witness == nb_public + nb_secret */
+int gg_scs_set_inputs(gg_scs_t h, size_t nb_public, size_t nb_secret);
 
 /* ------------------------------------------------------------ profiling
  * Kernel-level timing with HIP events recorded on the stream each kernel is

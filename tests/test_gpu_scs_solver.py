@@ -73,6 +73,16 @@ def test_gpu_scs_solver_errors():
     assert e.value.cid == 1
     W, *_ = sys_.solve([5, 5])
     assert _vals(W.to_host(), mod) == [5, 5, 5]
+    # witness size enforced by the library (solver.go:71-76): short and long, C ABI directly
+    import ctypes
+    from gnark_amd import fr
+    from gnark_amd._lib import check, lib, ptr
+    bad = ctypes.c_int64()
+    for vals in ([5], [5, 5, 5]):
+        wb = b"".join(fr.bls_fr_mont(v) for v in vals)
+        with pytest.raises(GnarkAmdError, match="invalid witness size"):
+            check(lib.gg_scs_solve(sys_.handle, ptr(wb), len(vals), 0, None, None, None, None, 0,
+                                   ctypes.byref(bad)))
     sys_.close()
     # the new wire at xa with qL + qM xb = 0: errDivideByZero
     sys_ = solver.SparseR1CS.from_constraints(1, 1, 3, [(2, 1, 0, 0, 1, 1, 0, 0)])

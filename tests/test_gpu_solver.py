@@ -71,6 +71,17 @@ def test_gpu_solver_cubic():
     assert e.value.cid == 2
     with pytest.raises(ValueError):
         sys_.solve([35])  # invalid witness size (solver.go:72-76)
+    # the library enforces it too (a cgo caller has no Python check): a short and
+    # a long witness through the C ABI directly
+    import ctypes
+    from gnark_amd import GnarkAmdError, fr
+    from gnark_amd._lib import check, lib, ptr
+    bad = ctypes.c_int64()
+    for vals in ([35], [35, 3, 9]):
+        wb = b"".join(fr.fr_mont(v) for v in vals)
+        with pytest.raises(GnarkAmdError, match="invalid witness size"):
+            check(lib.gg_r1cs_solve(sys_.handle, ptr(wb), len(vals), 0, None, None, None, None, 0,
+                                    ctypes.byref(bad)))
     sys_.close()
 
 
