@@ -79,13 +79,7 @@ FrB fr_set_bytes(const uint8_t* b, size_t n) {
     }
     return acc;
 }
-bool fp_lex_largest(const FpBls& y) {  // y > (p - 1) / 2  <=>  y > p - y
-    const FpBls c = from_mont(y), nc = from_mont(-y);
-    for (int i = 11; i >= 0; i--)
-        if (c.v[i] != nc.v[i]) return c.v[i] > nc.v[i];
-    return false;
-}
-// G1Affine.RawBytes (uncompressed, 96 B; infinity = 0x40 | zeros)
+// G1Affine.RawBytes = Marshal (uncompressed, 96 B; infinity = 0x40 | zeros)
 void g1_raw_bytes(const BAff& p, uint8_t out[96]) {
     memset(out, 0, 96);
     if (p.is_inf()) {
@@ -94,16 +88,6 @@ void g1_raw_bytes(const BAff& p, uint8_t out[96]) {
     }
     be_bytes<12>(from_mont(p.x).v, out);
     be_bytes<12>(from_mont(p.y).v, out + 48);
-}
-// G1Affine.Marshal = Bytes (compressed, 48 B; 0x80 smallest y, 0xA0 largest, 0xC0 infinity)
-void g1_marshal(const BAff& p, uint8_t out[48]) {
-    memset(out, 0, 48);
-    if (p.is_inf()) {
-        out[0] = 0xC0;
-        return;
-    }
-    be_bytes<12>(from_mont(p.x).v, out);
-    out[0] |= fp_lex_largest(p.y) ? 0xA0 : 0x80;
 }
 
 // ------------------------------------------------------------ transcript
@@ -721,13 +705,16 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
     // canonical L, R, O (bit-reversed for the coset FFTs, regular for the openings)
     for (int k = 0; k < 3; k++) lag_to_canonical(pk, F(pk->lag[k]), F(pk->cbrev[k]), F(pk->can[k]), s[k]);
     mark();
-    // ---- gamma, beta (deriveGammaAndBeta, prove.go:454-489; bindPublicData, verify.go:296-340)
+    // ---- gamma, beta (deriveGammaAndBeta, prove.go:454-489; bindPublicData, verify.go:296-340).
+    // G1Affine.Marshal is the UNCOMPRESSED encoding (RawBytes): groth16/bls12-381/verify.go:80-82
+    // writes Marshal() into a buffer and continues at SizeOfG1AffineUncompressed, and the BN254
+    // Solidity verifier of the same transcript binds X | Y (plonk/bn254/solidity.go:407-460)
     Transcript fs({"gamma", "beta", "alpha", "zeta"}, ch);
     {
-        uint8_t b[48];
-        for (int k = 0; k < 3; k++) { g1_marshal(pk->vkS[k], b); fs.bind("gamma", b, 48); }
-        for (int k = 0; k < 5; k++) { g1_marshal(pk->vkQ[k], b); fs.bind("gamma", b, 48); }
-        for (int i = 0; i < pk->n_cmt; i++) { g1_marshal(pk->vkQcp[i], b); fs.bind("gamma", b, 48); }
+        uint8_t b[96];
+        for (int k = 0; k < 3; k++) { g1_raw_bytes(pk->vkS[k], b); fs.bind("gamma", b, 96); }
+        for (int k = 0; k < 5; k++) { g1_raw_bytes(pk->vkQ[k], b); fs.bind("gamma", b, 96); }
+        for (int i = 0; i < pk->n_cmt; i++) { g1_raw_bytes(pk->vkQcp[i], b); fs.bind("gamma", b, 96); }
         uint8_t f32[32];
         for (size_t i = 0; i < nb_pub; i++) { fr_marshal(pub[i], f32); fs.bind("gamma", f32, 32); }
     }
@@ -971,13 +958,14 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
     P.claimed[5] = s1z;
     P.claimed[6] = s2z;
     for (int j = 0; j < n_cmt; j++) P.claimed[7 + j] = qcpz[j];
-    // deriveGamma of kzg (gnark-crypto [ext]): point, digests (Marshal), claimed values, Z(w zeta)
+    // deriveGamma of kzg (gnark-crypto [ext]): point, digests (Marshal = uncompressed), claimed
+    // values, Z(w zeta) -- the order of compute_gamma_kzg, plonk/bn254/solidity.go:961-1024
     Transcript fg({"gamma"}, fh);
     {
-        uint8_t b[48];
+        uint8_t b[96];
         fr_marshal(zeta, b);
         fg.bind("gamma", b, 32);
-        for (auto& d : digests) { g1_marshal(d, b); fg.bind("gamma", b, 48); }
+        for (auto& d : digests) { g1_raw_bytes(d, b); fg.bind("gamma", b, 96); }
         for (auto& c : P.claimed) { fr_marshal(c, b); fg.bind("gamma", b, 32); }
         fr_marshal(zu, b);
         fg.bind("gamma", b, 32);

@@ -562,7 +562,8 @@ def linearized(blinded_z, s3, ql, qr, qm, qo, qk, pi2, qcp, s1, s2, alpha, l, r,
 
 # ---------------------------------------------------------------- PlonK verifier (trapdoor)
 def g1_raw_bytes(p) -> bytes:
-    """G1Affine.RawBytes (deriveRandomness, verify.go:342-360): X | Y big-endian,
+    """G1Affine.RawBytes = Marshal (deriveRandomness verify.go:342-360, bindPublicData
+    :296-340, kzg deriveGamma, the BSB22 hash prove.go:341): X | Y big-endian,
     infinity = 0x40 | zeros (gnark-crypto mUncompressedInfinity)."""
     if p is INF:
         return bytes([0x40]) + bytes(95)
@@ -573,9 +574,9 @@ g1_marshal = g1_raw_bytes  # round-1 name
 
 
 def g1_compress(p) -> bytes:
-    """G1Affine.Marshal = Bytes (bindPublicData verify.go:296-340, kzg deriveGamma):
-    X big-endian with the zcash flags 0x80 (y smallest) / 0xA0 (y largest) / 0xC0
-    (infinity); inverse of g1_decompress_zcash, which the bellman_test.go keys pin."""
+    """G1Affine.Bytes (compressed): X big-endian with the zcash flags 0x80 (y
+    smallest) / 0xA0 (y largest) / 0xC0 (infinity); inverse of g1_decompress_zcash,
+    which the bellman_test.go keys pin.  (Marshal is NOT this: it is RawBytes.)"""
     if p is INF:
         return bytes([0xC0]) + bytes(47)
     b = bytearray(p[0].to_bytes(48, "big"))
@@ -656,8 +657,10 @@ def plonk_verify_trapdoor(proof, vk, tau, public=(), challenge_hash=None, foldin
     if len(bsb) != len(qcp) or len(public) != vk.get("nb_public", 0):
         return False
     fs = Transcript("gamma", "beta", "alpha", "zeta", h=challenge_hash)
+    # G1Affine.Marshal() = the uncompressed RawBytes: groth16/bls12-381/verify.go:80-82 copies
+    # Marshal() and continues at SizeOfG1AffineUncompressed; plonk/bn254/solidity.go binds X | Y
     for p in list(vk["S"]) + [vk["Ql"], vk["Qr"], vk["Qm"], vk["Qo"], vk["Qk"]] + list(qcp):
-        fs.bind("gamma", g1_compress(p))
+        fs.bind("gamma", g1_raw_bytes(p))
     for x in public:
         fs.bind("gamma", (x % R).to_bytes(32, "big"))
     gamma = _derive(fs, "gamma", *proof["LRO"])
@@ -674,7 +677,7 @@ def plonk_verify_trapdoor(proof, vk, tau, public=(), challenge_hash=None, foldin
         li = wi * (zn - 1) % R * pow(n * (zeta - wi), -1, R) % R
         pi = (pi + li * x) % R
     for j, c in enumerate(bsb):
-        hc = hash_to_field(g1_compress(c))
+        hc = hash_to_field(g1_raw_bytes(c))
         wi = pow(w, vk["nb_public"] + vk["cmt_idx"][j], R)
         li = wi * (zn - 1) % R * pow(n * (zeta - wi), -1, R) % R
         pi = (pi + li * hc) % R
@@ -704,7 +707,7 @@ def plonk_verify_trapdoor(proof, vk, tau, public=(), challenge_hash=None, foldin
     fsg = Transcript("gamma", h=folding_hash)
     fsg.bind("gamma", (zeta % R).to_bytes(32, "big"))
     for d in digests:
-        fsg.bind("gamma", g1_compress(d))
+        fsg.bind("gamma", g1_raw_bytes(d))
     for c in cl:
         fsg.bind("gamma", (c % R).to_bytes(32, "big"))
     fsg.bind("gamma", (zu % R).to_bytes(32, "big"))

@@ -183,7 +183,8 @@ class Circuit:
                 for rr in (r, n - 1):
                     vals[32 * rr:32 * rr + 32] = m2b(hint_rng.randrange(R))
                 dig = commit(bytes(vals))
-                hv = bo.hash_to_field(bo.g1_compress(bo.g1_from_bytes(dig)))
+                # htfFunc.Write(commitment.Marshal()) (prove.go:341): the uncompressed encoding
+                hv = bo.hash_to_field(bo.g1_raw_bytes(bo.g1_from_bytes(dig)))
                 val[a[r]] = hv * MONT % R
                 cmts.append((bytes(vals), dig, hv))
                 ci += 1

@@ -133,10 +133,13 @@ def test_fold_h_is_evaluation_split():
     assert bo.evaluate(folded, zeta) == bo.evaluate(h, zeta)
 
 
-def test_g1_marshal_is_zcash_compression():
-    """G1Affine.Marshal (the encoding bindPublicData and kzg's deriveGamma hash,
-    verify.go:296-340) re-creates the reference's own compressed keys byte for
-    byte (backend/groth16/bellman_test.go:19-132), and both encodings keep the
+def test_g1_encodings():
+    """G1Affine.Bytes (compressed) re-creates the reference's own compressed keys
+    byte for byte (backend/groth16/bellman_test.go:19-132); G1Affine.Marshal, the
+    encoding bindPublicData / kzg deriveGamma / the BSB22 hash bind, is RawBytes
+    (uncompressed X | Y): groth16/bls12-381/verify.go:80-82 copies Marshal() and
+    continues at SizeOfG1AffineUncompressed, and plonk/bn254/solidity.go:407-460
+    binds X | Y words where verify.go:296-340 binds Marshal().  Both keep the
     gnark-crypto infinity flags."""
     for h in PINS["g1_compressed"]:
         raw = bytes.fromhex(h)
