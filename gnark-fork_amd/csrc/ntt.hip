@@ -665,16 +665,15 @@ size_t domain_size(gg_domain* d, int* curve) {
     if (curve) *curve = d->curve;
     return d->n;
 }
-void bls_ntt_inplace(gg_domain* d, void* data, int inverse, int dit, int coset, hipStream_t st) {
-    GG_CHECK(d->curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "needs a BLS12-381 domain");
-    ntt_apply(d->bls.get(), data, inverse, dit != 0, coset, st);
+void any_ntt_inplace(gg_domain* d, void* data, int inverse, int dit, int coset, hipStream_t st) {
+    if (d->curve == GG_CURVE_BN254) ntt_apply(d->bn.get(), data, inverse, dit != 0, coset, st);
+    else ntt_apply(d->bls.get(), data, inverse, dit != 0, coset, st);
 }
-// evaluateXnMinusOneDomainBigCoset (backend/plonk/bls12-381/prove.go:1253-1276):
+// evaluateXnMinusOneDomainBigCoset (backend/plonk/<curve>/prove.go:1253-1276):
 // res[0] = g^n, res[i] = res[i-1] * w_big^n, res[i] -= 1, then fr.BatchInvert
-void bls_xn_minus_one_inv(gg_domain* big, size_t n_small, void* out) {
-    GG_CHECK(big->curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "needs a BLS12-381 domain");
-    using F = FrBls;
-    const DomainT<FrBlsCfg>* d = big->bls.get();
+template <class C>
+static void xn_minus_one_inv_t(const DomainT<C>* d, size_t n_small, void* out) {
+    using F = Fe<C>;
     const size_t rho = d->n / n_small;
     std::vector<F> res(rho);
     res[0] = pow_u64(d->g, n_small);
@@ -686,6 +685,10 @@ void bls_xn_minus_one_inv(gg_domain* big, size_t n_small, void* out) {
         res[i] = inverse(res[i]);
     }
     memcpy(out, res.data(), rho * sizeof(F));
+}
+void xn_minus_one_inv(gg_domain* big, size_t n_small, void* out) {
+    if (big->curve == GG_CURVE_BN254) xn_minus_one_inv_t(big->bn.get(), n_small, out);
+    else xn_minus_one_inv_t(big->bls.get(), n_small, out);
 }
 }  // namespace gg
 

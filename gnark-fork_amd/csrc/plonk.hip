@@ -14,76 +14,82 @@
 #include "prof.h"
 #include <vector>
 #include <cstring>
+#include <type_traits>
 
 namespace gg {
-void bls_ntt_inplace(gg_domain* d, void* data, int inverse, int dit, int coset, hipStream_t st);
+void any_ntt_inplace(gg_domain* d, void* data, int inverse, int dit, int coset, hipStream_t st);
 size_t domain_size(gg_domain* d, int* curve);
-void bls_xn_minus_one_inv(gg_domain* big, size_t n_small, void* out);
+void xn_minus_one_inv(gg_domain* big, size_t n_small, void* out);
 }  // namespace gg
 
 namespace gg {
 namespace plk {
 
-__device__ __forceinline__ FrB ldf(const FrB* p) {
+template <class F>
+__device__ __forceinline__ F ldf(const F* p) {
     const uint4* q = reinterpret_cast<const uint4*>(p);
     uint4 a = q[0], b = q[1];
-    FrB r;
+    F r;
     r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
     r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
     return r;
 }
-__device__ __forceinline__ void stf(FrB* p, const FrB& r) {
+template <class F>
+__device__ __forceinline__ void stf(F* p, const F& r) {
     uint4* q = reinterpret_cast<uint4*>(p);
     q[0] = make_uint4(r.v[0], r.v[1], r.v[2], r.v[3]);
     q[1] = make_uint4(r.v[4], r.v[5], r.v[6], r.v[7]);
 }
 
 // sum c[k] x^k: nc - 1 products (the leading coefficient starts the chain)
-__device__ __forceinline__ FrB horner(const FrB* c, int nc, const FrB& x) {
-    if (nc <= 0) return FrB::zero();
-    FrB r = c[nc - 1];
+template <class F>
+__device__ __forceinline__ F horner_d(const F* c, int nc, const F& x) {
+    if (nc <= 0) return F::zero();
+    F r = c[nc - 1];
     for (int k = nc - 2; k >= 0; k--) r = r * x + c[k];
     return r;
 }
 
 // allConstraints at point j of the coset (prove.go:928-954)
-__device__ __forceinline__ FrB numerator_at(const NumParams& P, uint32_t j) {
-    const FrB one = FrB::one();
-    FrB L = ldf(P.x[ID_L] + j), R = ldf(P.x[ID_R] + j), O = ldf(P.x[ID_O] + j);
-    FrB Z = ldf(P.x[ID_Z] + j);
-    FrB ZS = P.x[ID_ZS] ? ldf(P.x[ID_ZS] + j) : ldf(P.x[ID_Z] + (j + 1 == P.n ? 0 : j + 1));
-    FrB S1 = ldf(P.x[ID_S1] + j) * P.beta, S2 = ldf(P.x[ID_S2] + j) * P.beta,
+template <class F>
+__device__ __forceinline__ F numerator_at(const NumParamsT<F>& P, uint32_t j) {
+    const F one = F::one();
+    F L = ldf(P.x[ID_L] + j), R = ldf(P.x[ID_R] + j), O = ldf(P.x[ID_O] + j);
+    F Z = ldf(P.x[ID_Z] + j);
+    F ZS = P.x[ID_ZS] ? ldf(P.x[ID_ZS] + j) : ldf(P.x[ID_Z] + (j + 1 == P.n ? 0 : j + 1));
+    F S1 = ldf(P.x[ID_S1] + j) * P.beta, S2 = ldf(P.x[ID_S2] + j) * P.beta,
         S3 = ldf(P.x[ID_S3] + j) * P.beta;
     // blinding: bl/br/bo/bz evaluated at twiddles0[j], bz at twiddles0[(j+1) % n] for ZS
-    const FrB t0 = ldf(P.tw0 + j), t1 = ldf(P.tw0 + (j + 1) % P.n);
-    L = L + horner(P.bcoef[0], P.bdeg[0], t0);
-    R = R + horner(P.bcoef[1], P.bdeg[1], t0);
-    O = O + horner(P.bcoef[2], P.bdeg[2], t0);
-    Z = Z + horner(P.bcoef[3], P.bdeg[3], t0);
-    ZS = ZS + horner(P.bcoef[3], P.bdeg[3], t1);
+    const F t0 = ldf(P.tw0 + j), t1 = ldf(P.tw0 + (j + 1) % P.n);
+    L = L + horner_d(P.bcoef[0], P.bdeg[0], t0);
+    R = R + horner_d(P.bcoef[1], P.bdeg[1], t0);
+    O = O + horner_d(P.bcoef[2], P.bdeg[2], t0);
+    Z = Z + horner_d(P.bcoef[3], P.bdeg[3], t0);
+    ZS = ZS + horner_d(P.bcoef[3], P.bdeg[3], t1);
     // gateConstraint
     // ql L + qm L R = L (ql + qm R): four products instead of five
-    FrB ic = L * (ldf(P.x[ID_QL] + j) + ldf(P.x[ID_QM] + j) * R) + ldf(P.x[ID_QR] + j) * R;
+    F ic = L * (ldf(P.x[ID_QL] + j) + ldf(P.x[ID_QM] + j) * R) + ldf(P.x[ID_QR] + j) * R;
     ic = ic + ldf(P.x[ID_QO] + j) * O + ldf(P.x[ID_QK] + j);
     for (int q = ID_QCI; q + 1 < P.nx; q += 2) ic = ic + ldf(P.x[q] + j) * ldf(P.x[q + 1] + j);
     // orderingConstraint
-    const FrB id = ldf(P.x[ID_ID] + j);
-    FrB a = P.gamma + L + id * P.ka, b = id * P.kb + R + P.gamma, c = id * P.kc + O + P.gamma;
-    FrB r = a * b * c * Z;
+    const F id = ldf(P.x[ID_ID] + j);
+    F a = P.gamma + L + id * P.ka, b = id * P.kb + R + P.gamma, c = id * P.kc + O + P.gamma;
+    F r = a * b * c * Z;
     a = S1 + L + P.gamma;
     b = S2 + R + P.gamma;
     c = S3 + O + P.gamma;
-    FrB l = a * b * c * ZS - r;
+    F l = a * b * c * ZS - r;
     // ratioLocalConstraint
-    FrB rl = (Z - one) * ldf(P.x[ID_LONE] + j);
+    F rl = (Z - one) * ldf(P.x[ID_LONE] + j);
     return (rl * P.alpha + l) * P.alpha + ic;
 }
 
 // small domains: one point per thread, cres[bitrev(rho*j + coset)] (prove.go:1036-1038)
-__global__ void __launch_bounds__(256) k_numerator_coset(NumParams P) {
+template <class F>
+__global__ void __launch_bounds__(256) k_numerator_coset(NumParamsT<F> P) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= P.n) return;
-    const FrB res = numerator_at(P, j);
+    const F res = numerator_at(P, j);
     uint32_t pos = P.log_big ? __brev(P.rho * j + P.coset) >> (32 - P.log_big) : 0u;
     if (P.local_block) pos &= P.n - 1;
     stf(P.cres + pos, res);
@@ -97,11 +103,12 @@ __global__ void __launch_bounds__(256) k_numerator_coset(NumParams P) {
 // so for each l the 16 values of h fill 16 consecutive slots: the results are
 // transposed through LDS and stored as 16 runs of 512 B (not 256 scattered 32-B
 // writes).
-__global__ void __launch_bounds__(256) k_numerator_coset_tiled(NumParams P, uint32_t log_n) {
+template <class F>
+__global__ void __launch_bounds__(256) k_numerator_coset_tiled(NumParamsT<F> P, uint32_t log_n) {
     __shared__ uint32_t tile[8][256 + 8];  // limb-major, padded
     const uint32_t t = threadIdx.x, h = t >> 4, l = t & 15, m = blockIdx.x;
     const uint32_t j = (h << (log_n - 4)) | (m << 4) | l;
-    const FrB res = numerator_at(P, j);
+    const F res = numerator_at(P, j);
     const uint32_t slot = l * 16 + (__brev(h) >> 28);
 #pragma unroll
     for (int k = 0; k < 8; k++) tile[k][slot + (slot >> 5)] = res.v[k];
@@ -111,16 +118,18 @@ __global__ void __launch_bounds__(256) k_numerator_coset_tiled(NumParams P, uint
     const uint32_t pos = (r && !P.local_block ? (__brev(P.coset) >> (32 - r)) << log_n : 0u) |
                          ((__brev(l2) >> 28) << (log_n - 4)) |
                          (log_n > 8 ? (__brev(m) >> (40 - log_n)) << 4 : 0u) | col;
-    FrB o;
+    F o;
 #pragma unroll
     for (int k = 0; k < 8; k++) o.v[k] = tile[k][t + (t >> 5)];
     stf(P.cres + pos, o);
 }
 
+template <class F>
 struct PeriodicTab {
-    FrB f[8];
+    F f[8];
 };
-__global__ void k_mul_periodic_bitrev(FrB* r, size_t n, int log_n, PeriodicTab t, uint32_t rho) {
+template <class F>
+__global__ void k_mul_periodic_bitrev(F* r, size_t n, int log_n, PeriodicTab<F> t, uint32_t rho) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t irev = log_n ? (__brev((uint32_t)i) >> (32 - log_n)) : 0u;
@@ -128,21 +137,22 @@ __global__ void k_mul_periodic_bitrev(FrB* r, size_t n, int log_n, PeriodicTab t
 }
 
 // Montgomery batch inversion: thread t owns elements t, t+T, ... (zeros skipped)
-__global__ void __launch_bounds__(256) k_batch_invert(FrB* a, size_t n, size_t T, FrB* prefix) {
+template <class F>
+__global__ void __launch_bounds__(256) k_batch_invert(F* a, size_t n, size_t T, F* prefix) {
     size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T || t >= n) return;
-    FrB acc = FrB::one();
+    F acc = F::one();
     for (size_t i = t; i < n; i += T) {
         stf(prefix + i, acc);
-        FrB x = ldf(a + i);
+        F x = ldf(a + i);
         if (!x.is_zero()) acc = acc * x;
     }
-    FrB inv = inverse(acc);
+    F inv = inverse(acc);
     size_t last = t + ((n - 1 - t) / T) * T;
     for (size_t i = last;; i -= T) {
-        FrB x = ldf(a + i);
+        F x = ldf(a + i);
         if (!x.is_zero()) {
-            FrB xi = inv * ldf(prefix + i);
+            F xi = inv * ldf(prefix + i);
             inv = inv * x;
             stf(a + i, xi);
         }
@@ -153,47 +163,59 @@ __global__ void __launch_bounds__(256) k_batch_invert(FrB* a, size_t n, size_t T
 size_t batch_invert_arena_bytes(size_t n) { return ((n * 32 + 255) & ~(size_t)255) + 256; }
 
 // fr.BatchInvert on device memory (zeros stay zero)
-void batch_invert(FrB* a, size_t n, hipStream_t st, Arena& ar) {
+template <class F>
+void batch_invert(F* a, size_t n, hipStream_t st, Arena& ar) {
     if (n == 0) return;
     const size_t T = std::min<size_t>(n, std::max<size_t>(16384, n / 64));
-    FrB* prefix = ar.get<FrB>(n);
-    hipLaunchKernelGGL(k_batch_invert, dim3(grid_for(T, 256)), dim3(256), 0, st, a, n, T, prefix);
+    F* prefix = ar.get<F>(n);
+    hipLaunchKernelGGL(k_batch_invert<F>, dim3(grid_for(T, 256)), dim3(256), 0, st, a, n, T, prefix);
     GG_HIP(hipGetLastError());
 }
 
-void numerator(const NumParams& P, hipStream_t st) {
+template <class F>
+void numerator(const NumParamsT<F>& P, hipStream_t st) {
     ProfScope prof("plonk_numerator", st, (double)P.n);
     uint32_t log_n = 0;
     while ((1u << log_n) < P.n) log_n++;
     if (log_n >= 8)
-        hipLaunchKernelGGL(k_numerator_coset_tiled, dim3(P.n >> 8), dim3(256), 0, st, P, log_n);
+        hipLaunchKernelGGL(k_numerator_coset_tiled<F>, dim3(P.n >> 8), dim3(256), 0, st, P, log_n);
     else
-        hipLaunchKernelGGL(k_numerator_coset, dim3(grid_for(P.n, 256)), dim3(256), 0, st, P);
+        hipLaunchKernelGGL(k_numerator_coset<F>, dim3(grid_for(P.n, 256)), dim3(256), 0, st, P);
     GG_HIP(hipGetLastError());
     prof.stop(st);
 }
 
-void divide_by_xn_minus_one(gg_domain* big, size_t n_small, FrB* data, hipStream_t st) {
+template <class F>
+void divide_by_xn_minus_one(gg_domain* big, size_t n_small, F* data, hipStream_t st) {
     int curve = -1;
     const size_t m = domain_size(big, &curve);
-    GG_CHECK(curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "needs a BLS12-381 domain");
+    GG_CHECK(curve == (std::is_same<F, FrBls>::value ? GG_CURVE_BLS12_381 : GG_CURVE_BN254), GG_ERR_INVALID_ARG,
+             "the big domain belongs to another scalar field");
     GG_CHECK(n_small >= 1 && m % n_small == 0, GG_ERR_INVALID_ARG, "big domain must be a multiple of n");
     const uint32_t rho = (uint32_t)(m / n_small);
     GG_CHECK(rho <= 8, GG_ERR_INVALID_ARG, "|big domain| / n > 8");
     // (x^n - 1)^-1 on the big coset has rho distinct values (prove.go:1253-1276)
-    PeriodicTab t{};
-    bls_xn_minus_one_inv(big, n_small, t.f);
+    PeriodicTab<F> t{};
+    xn_minus_one_inv(big, n_small, t.f);
     int lm = 0;
     while (((size_t)1 << lm) < m) lm++;
-    hipLaunchKernelGGL(k_mul_periodic_bitrev, dim3(grid_for(m, 256)), dim3(256), 0, st, data, m, lm, t, rho);
+    hipLaunchKernelGGL(k_mul_periodic_bitrev<F>, dim3(grid_for(m, 256)), dim3(256), 0, st, data, m, lm, t, rho);
     GG_HIP(hipGetLastError());
     // LagrangeCoset/BitReverse -> Canonical/Regular: FFTInverse(DIT, OnCoset)
-    bls_ntt_inplace(big, data, 1, 1, 1, st);
+    any_ntt_inplace(big, data, 1, 1, 1, st);
 }
 
 void ntt(gg_domain* d, void* data, int inverse, int dit, int coset, hipStream_t st) {
-    bls_ntt_inplace(d, data, inverse, dit, coset, st);
+    any_ntt_inplace(d, data, inverse, dit, coset, st);
 }
+
+#define GG_PLK_INST(F)                                                                                         \
+    template void batch_invert<F>(F*, size_t, hipStream_t, Arena&);                                            \
+    template void numerator<F>(const NumParamsT<F>&, hipStream_t);                                             \
+    template void divide_by_xn_minus_one<F>(gg_domain*, size_t, F*, hipStream_t);
+GG_PLK_INST(FrBls)
+GG_PLK_INST(Fr)
+#undef GG_PLK_INST
 
 }  // namespace plk
 }  // namespace gg

@@ -20,61 +20,81 @@ enum { ID_L, ID_R, ID_O, ID_Z, ID_ZS, ID_QL, ID_QR, ID_QM, ID_QO, ID_QK, ID_S1, 
        ID_LONE, ID_QCI };
 constexpr int MAX_X = ID_QCI + 2 * MAX_CMT;
 
+// Every operation is a template over the scalar field F (FrBls for
+// backend/plonk/bls12-381, Fr for backend/plonk/bn254: the same generated prover
+// over another curve); plonk_poly.hip / plonk.hip instantiate both.
+
 // ---- plonk_poly.hip
 size_t scan_arena_bytes(size_t m);
 // in place inclusive running product
-void scan_prod(FrB* x, size_t m, hipStream_t st, Arena& ar);
+template <class F>
+void scan_prod(F* x, size_t m, hipStream_t st, Arena& ar);
 size_t horner_arena_bytes(size_t n);
 // value_dev[0] = f(a) (Polynomial.Evaluate); q (nullable, n - 1 fr) = (f - f(a)) / (X - a)
-void horner(const FrB* f, size_t n, const FrB& a, FrB* q, FrB* value_dev, hipStream_t st, Arena& ar);
+template <class F>
+void horner(const F* f, size_t n, const F& a, F* q, F* value_dev, hipStream_t st, Arena& ar);
 size_t ratio_arena_bytes(size_t n);
 // iop.BuildRatioCopyConstraint into Lagrange/Regular z (prove.go:600-621)
-void ratio(const FrB* l, const FrB* r, const FrB* o, const int64_t* perm, size_t n, const FrB& beta,
-           const FrB& gamma, const FrB& omega, const FrB& u, FrB* z, hipStream_t st, Arena& ar);
+template <class F>
+void ratio(const F* l, const F* r, const F* o, const int64_t* perm, size_t n, const F& beta, const F& gamma,
+           const F& omega, const F& u, F* z, hipStream_t st, Arena& ar);
 size_t batch_invert_arena_bytes(size_t n);
-void batch_invert(FrB* a, size_t n, hipStream_t st, Arena& ar);
-void fold_h(const FrB* h, size_t n_small, const FrB& z, FrB* out, hipStream_t st);
-struct LinParams {
-    FrB* z;  // blinded Z canonical, in/out
+template <class F>
+void batch_invert(F* a, size_t n, hipStream_t st, Arena& ar);
+template <class F>
+void fold_h(const F* h, size_t n_small, const F& z, F* out, hipStream_t st);
+template <class F>
+struct LinParamsT {
+    F* z;  // blinded Z canonical, in/out
     size_t nz;
-    const FrB* s3;
+    const F* s3;
     size_t ns3;
-    const FrB *ql, *qr, *qm, *qo, *qk;
+    const F *ql, *qr, *qm, *qo, *qk;
     size_t nq;
-    const FrB* pi2[MAX_CMT];
-    FrB qcp[MAX_CMT];
+    const F* pi2[MAX_CMT];
+    F qcp[MAX_CMT];
     int ncmt;
-    FrB s1, s2, alpha, l, r, rl, o, lag;
+    F s1, s2, alpha, l, r, rl, o, lag;
 };
-void linearized(const LinParams& P, hipStream_t st);
-void bit_reverse(const FrB* in, FrB* out, size_t n, hipStream_t st);
-void axpy(FrB* y, const FrB* x, size_t n, const FrB& a, hipStream_t st);  // y += a x
-void scale(FrB* y, size_t n, const FrB& a, hipStream_t st);               // y *= a
-void shift_copy(const FrB* in, FrB* out, size_t n, hipStream_t st);        // out[i] = in[(i+1) % n]
+using LinParams = LinParamsT<FrB>;
+template <class F>
+void linearized(const LinParamsT<F>& P, hipStream_t st);
+template <class F>
+void bit_reverse(const F* in, F* out, size_t n, hipStream_t st);
+template <class F>
+void axpy(F* y, const F* x, size_t n, const F& a, hipStream_t st);  // y += a x
+template <class F>
+void scale(F* y, size_t n, const F& a, hipStream_t st);  // y *= a
+template <class F>
+void shift_copy(const F* in, F* out, size_t n, hipStream_t st);  // out[i] = in[(i+1) % n]
 
 // ---- plonk.hip
-struct NumParams {
-    const FrB* x[MAX_X];  // Lagrange-regular evaluations on this coset, length n
+template <class F>
+struct NumParamsT {
+    const F* x[MAX_X];  // Lagrange-regular evaluations on this coset, length n
     int nx;
-    FrB bcoef[4][MAX_BCOEF];  // blinding polynomials Bl, Br, Bo, Bz (coset-scaled)
-    int bdeg[4];              // number of coefficients
-    const FrB* tw0;           // s.twiddles0: omega_small^j, j < n
-    FrB beta, gamma, alpha, cs, css;
+    F bcoef[4][MAX_BCOEF];  // blinding polynomials Bl, Br, Bo, Bz (coset-scaled)
+    int bdeg[4];            // number of coefficients
+    const F* tw0;           // s.twiddles0: omega_small^j, j < n
+    F beta, gamma, alpha, cs, css;
     // orderingConstraint's identity terms: a, b, c use ka, kb, kc times x[ID_ID]
     // (x[ID_ID] = beta X with ka = 1, kb = cs, kc = cs^2; or X with ka = beta, ...)
-    FrB ka, kb, kc;
+    F ka, kb, kc;
     uint32_t n, log_big, rho, coset;
-    FrB* cres;  // rho * n, bit-reversed big-domain order
+    F* cres;  // rho * n, bit-reversed big-domain order
     // local_block = 1: cres is only this coset's block of n (the slots
     // [brev(coset) n, (brev(coset) + 1) n) of the big vector), e.g. on another GPU
     uint32_t local_block;
     // x[ID_ZS] == nullptr: ZS[j] = Z[(j + 1) % n] read from x[ID_Z] (no shifted copy)
 };
-void numerator(const NumParams& P, hipStream_t st);
-// divideByXMinusOne in place (prove.go:1223-1276), asynchronous
-void divide_by_xn_minus_one(gg_domain* big, size_t n_small, FrB* data, hipStream_t st);
+using NumParams = NumParamsT<FrB>;
+template <class F>
+void numerator(const NumParamsT<F>& P, hipStream_t st);
+// divideByXMinusOne in place (prove.go:1223-1276), asynchronous; big: a domain of F's curve
+template <class F>
+void divide_by_xn_minus_one(gg_domain* big, size_t n_small, F* data, hipStream_t st);
 
-// ---- ntt.hip
+// ---- ntt.hip (the domain's scalar field)
 void ntt(gg_domain* d, void* data, int inverse, int dit, int coset, hipStream_t st);
 
 }  // namespace plk

@@ -24,15 +24,17 @@ namespace gg {
 namespace plk {
 
 namespace {
-__device__ __forceinline__ FrB ldb(const FrB* p) {
+template <class F>
+__device__ __forceinline__ F ldb(const F* p) {
     const uint4* q = reinterpret_cast<const uint4*>(p);
     uint4 a = q[0], b = q[1];
-    FrB r;
+    F r;
     r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
     r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
     return r;
 }
-__device__ __forceinline__ void stb(FrB* p, const FrB& r) {
+template <class F>
+__device__ __forceinline__ void stb(F* p, const F& r) {
     uint4* q = reinterpret_cast<uint4*>(p);
     q[0] = make_uint4(r.v[0], r.v[1], r.v[2], r.v[3]);
     q[1] = make_uint4(r.v[4], r.v[5], r.v[6], r.v[7]);
@@ -44,32 +46,33 @@ constexpr int SCAN_BLK = 256 * SCAN_PER;       // elements per block
 enum { SCAN_PROD = 0, SCAN_AFFINE = 1 };
 
 // powers of the affine multiplier u of one scan level
+template <class F>
 struct ScanPow {
-    FrB p[SCAN_PER + 1];  // u^0 .. u^8
-    FrB step[8];          // u^(8 * 2^d): block-scan combine at offset 2^d threads
-    const FrB* lo;        // u^i, i < 64
-    const FrB* hi;        // u^(64 j), j <= 32
+    F p[SCAN_PER + 1];  // u^0 .. u^8
+    F step[8];          // u^(8 * 2^d): block-scan combine at offset 2^d threads
+    const F* lo;        // u^i, i < 64
+    const F* hi;        // u^(64 j), j <= 32
 };
 
 // In place: inclusive scan of each 2048-element block; aux[b] = block aggregate.
-template <int MODE>
-__global__ void __launch_bounds__(256) k_scan_local(FrB* x, size_t m, ScanPow P, FrB* aux) {
+template <class F, int MODE>
+__global__ void __launch_bounds__(256) k_scan_local(F* x, size_t m, ScanPow<F> P, F* aux) {
     __shared__ uint32_t sh[256 * 8];
     const size_t base = (size_t)blockIdx.x * SCAN_BLK + (size_t)threadIdx.x * SCAN_PER;
-    FrB v[SCAN_PER];
-    const FrB id = MODE == SCAN_PROD ? FrB::one() : FrB::zero();
+    F v[SCAN_PER];
+    const F id = MODE == SCAN_PROD ? F::one() : F::zero();
 #pragma unroll
     for (int k = 0; k < SCAN_PER; k++) v[k] = base + k < m ? ldb(x + base + k) : id;
 #pragma unroll
     for (int k = 1; k < SCAN_PER; k++) v[k] = MODE == SCAN_PROD ? v[k] * v[k - 1] : v[k] + P.p[1] * v[k - 1];
-    FrB agg = v[SCAN_PER - 1];
+    F agg = v[SCAN_PER - 1];
     // Hillis-Steele over the 256 thread aggregates (LDS, limb-major: no bank conflicts)
-    auto put = [&](const FrB& a) {
+    auto put = [&](const F& a) {
 #pragma unroll
         for (int l = 0; l < 8; l++) sh[l * 256 + threadIdx.x] = a.v[l];
     };
     auto get = [&](int t) {
-        FrB a;
+        F a;
 #pragma unroll
         for (int l = 0; l < 8; l++) a.v[l] = sh[l * 256 + t];
         return a;
@@ -79,7 +82,7 @@ __global__ void __launch_bounds__(256) k_scan_local(FrB* x, size_t m, ScanPow P,
 #pragma unroll 1
     for (int d = 0; d < 8; d++) {
         const int off = 1 << d;
-        FrB o = id;
+        F o = id;
         const bool has = (int)threadIdx.x >= off;
         if (has) o = get(threadIdx.x - off);
         __syncthreads();
@@ -89,7 +92,7 @@ __global__ void __launch_bounds__(256) k_scan_local(FrB* x, size_t m, ScanPow P,
     }
     // carry-in = inclusive aggregate of the previous thread
     if (threadIdx.x > 0) {
-        const FrB c = get(threadIdx.x - 1);
+        const F c = get(threadIdx.x - 1);
 #pragma unroll
         for (int k = 0; k < SCAN_PER; k++) v[k] = MODE == SCAN_PROD ? v[k] * c : v[k] + P.p[k + 1] * c;
     }
@@ -100,13 +103,13 @@ __global__ void __launch_bounds__(256) k_scan_local(FrB* x, size_t m, ScanPow P,
 }
 
 // x[e] (block b > 0) combined with the inclusive aggregate of blocks < b
-template <int MODE>
-__global__ void __launch_bounds__(256) k_scan_fix(FrB* x, size_t m, ScanPow P, const FrB* aux) {
+template <class F, int MODE>
+__global__ void __launch_bounds__(256) k_scan_fix(F* x, size_t m, ScanPow<F> P, const F* aux) {
     const size_t b = blockIdx.x + 1;
-    const FrB c = ldb(aux + b - 1);
+    const F c = ldb(aux + b - 1);
     const uint32_t o0 = threadIdx.x * SCAN_PER;
     const size_t base = b * SCAN_BLK + o0;
-    FrB f;
+    F f;
     if (MODE == SCAN_AFFINE) {
         const uint32_t e = o0 + 1;  // u^(offset + 1)
         f = ldb(P.hi + (e >> 6)) * ldb(P.lo + (e & 63)) * c;
@@ -114,7 +117,7 @@ __global__ void __launch_bounds__(256) k_scan_fix(FrB* x, size_t m, ScanPow P, c
 #pragma unroll
     for (int k = 0; k < SCAN_PER; k++) {
         if (base + k >= m) break;
-        FrB v = ldb(x + base + k);
+        F v = ldb(x + base + k);
         if (MODE == SCAN_PROD) v = v * c;
         else {
             v = v + f;
@@ -126,21 +129,23 @@ __global__ void __launch_bounds__(256) k_scan_fix(FrB* x, size_t m, ScanPow P, c
 
 // powers of u for one level (host, small) and the 97-entry u^i / u^(64 j)
 // table of the affine fix-up (device, one thread: no host buffer in flight)
-static void scan_pow_host(const FrB& u, ScanPow& P) {
-    P.p[0] = FrB::one();
+template <class F>
+static void scan_pow_host(const F& u, ScanPow<F>& P) {
+    P.p[0] = F::one();
     for (int k = 1; k <= SCAN_PER; k++) P.p[k] = P.p[k - 1] * u;
-    FrB s = P.p[SCAN_PER];
+    F s = P.p[SCAN_PER];
     for (int d = 0; d < 8; d++) {
         P.step[d] = s;
         s = s * s;
     }
 }
-__global__ void k_pow_tab(FrB u, FrB* tab) {
+template <class F>
+__global__ void k_pow_tab(F u, F* tab) {
     if (threadIdx.x || blockIdx.x) return;
-    FrB a = FrB::one();
+    F a = F::one();
     for (int i = 0; i < 64; i++) { stb(tab + i, a); a = a * u; }
-    const FrB u64 = a;
-    a = FrB::one();
+    const F u64 = a;
+    a = F::one();
     for (int j = 0; j < 33; j++) { stb(tab + 64 + j, a); a = a * u64; }
 }
 
@@ -156,76 +161,81 @@ size_t scan_arena_bytes(size_t m) {
 }
 
 // recursive in-place scan of x[0..m); u: multiplier of this level (affine)
-template <int MODE>
-static void scan_rec(FrB* x, size_t m, const FrB& u, hipStream_t st, Arena& ar) {
-    ScanPow P{};
+template <class F, int MODE>
+static void scan_rec(F* x, size_t m, const F& u, hipStream_t st, Arena& ar) {
+    ScanPow<F> P{};
     scan_pow_host(u, P);
     if (MODE == SCAN_AFFINE) {
-        FrB* tab = ar.get<FrB>(97);
-        hipLaunchKernelGGL(k_pow_tab, dim3(1), dim3(64), 0, st, u, tab);
+        F* tab = ar.get<F>(97);
+        hipLaunchKernelGGL(k_pow_tab<F>, dim3(1), dim3(64), 0, st, u, tab);
         GG_HIP(hipGetLastError());
         P.lo = tab;
         P.hi = tab + 64;
     }
     const size_t nblk = (m + SCAN_BLK - 1) / SCAN_BLK;
-    FrB* aux = nblk > 1 ? ar.get<FrB>(nblk) : nullptr;
-    hipLaunchKernelGGL(k_scan_local<MODE>, dim3((unsigned)nblk), dim3(256), 0, st, x, m, P, aux);
+    F* aux = nblk > 1 ? ar.get<F>(nblk) : nullptr;
+    hipLaunchKernelGGL((k_scan_local<F, MODE>), dim3((unsigned)nblk), dim3(256), 0, st, x, m, P, aux);
     GG_HIP(hipGetLastError());
     if (nblk <= 1) return;
     // the next level's elements each stand for SCAN_BLK of this level: u^2048
-    FrB un = u;
+    F un = u;
     for (int i = 0; i < 11; i++) un = un * un;
-    scan_rec<MODE>(aux, nblk, un, st, ar);
-    hipLaunchKernelGGL(k_scan_fix<MODE>, dim3((unsigned)(nblk - 1)), dim3(256), 0, st, x, m, P, aux);
+    scan_rec<F, MODE>(aux, nblk, un, st, ar);
+    hipLaunchKernelGGL((k_scan_fix<F, MODE>), dim3((unsigned)(nblk - 1)), dim3(256), 0, st, x, m, P, aux);
     GG_HIP(hipGetLastError());
 }
 
-void scan_prod(FrB* x, size_t m, hipStream_t st, Arena& ar) {
-    if (m) scan_rec<SCAN_PROD>(x, m, FrB::one(), st, ar);
+template <class F>
+void scan_prod(F* x, size_t m, hipStream_t st, Arena& ar) {
+    if (m) scan_rec<F, SCAN_PROD>(x, m, F::one(), st, ar);
 }
 
-__global__ void k_reverse_copy(FrB* dst, const FrB* src, size_t n) {
+template <class F>
+__global__ void k_reverse_copy(F* dst, const F* src, size_t n) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) stb(dst + i, ldb(src + n - 1 - i));
 }
 
 // q[j] = g[n-2-j] for j < n-1 where g is the reversed affine scan
-__global__ void k_quotient_out(FrB* q, const FrB* g, size_t n) {
+template <class F>
+__global__ void k_quotient_out(F* q, const F* g, size_t n) {
     size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j + 1 < n) stb(q + j, ldb(g + n - 2 - j));
 }
 
 // ---------------------------------------------------------------- ratio
+template <class F>
 struct PowSplit {  // x^e = hi[e >> S] * lo[e & (2^S - 1)]
-    const FrB *hi, *lo;
+    const F *hi, *lo;
     int S;
-    __device__ __forceinline__ FrB at(uint32_t e) const {
+    __device__ __forceinline__ F at(uint32_t e) const {
         return ldb(hi + (e >> S)) * ldb(lo + (e & ((1u << S) - 1)));
     }
 };
 
-__global__ void __launch_bounds__(256) k_ratio_numden(const FrB* L, const FrB* R, const FrB* O,
+template <class F>
+__global__ void __launch_bounds__(256) k_ratio_numden(const F* L, const F* R, const F* O,
                                                       const int64_t* perm, uint32_t n, int log_n,
-                                                      FrB beta, FrB gamma, FrB u, FrB uu, PowSplit w,
-                                                      FrB* num, FrB* den) {
+                                                      F beta, F gamma, F u, F uu, PowSplit<F> w,
+                                                      F* num, F* den) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     if (i == 0) {
-        stb(num, FrB::one());
-        stb(den, FrB::one());
+        stb(num, F::one());
+        stb(den, F::one());
     }
     if (i + 1 >= n) return;
-    const FrB* f[3] = {L, R, O};
-    const FrB wi = w.at(i);
-    FrB b = FrB::one(), d = FrB::one();
+    const F* f[3] = {L, R, O};
+    const F wi = w.at(i);
+    F b = F::one(), d = F::one();
 #pragma unroll
     for (int j = 0; j < 3; j++) {
-        const FrB fv = ldb(f[j] + i);
-        FrB id = j == 0 ? wi : (j == 1 ? wi * u : wi * uu);
+        const F fv = ldb(f[j] + i);
+        F id = j == 0 ? wi : (j == 1 ? wi * u : wi * uu);
         b = b * (fv + beta * id + gamma);
         const uint64_t s = (uint64_t)perm[(size_t)j * n + i];
         const uint32_t blk = (uint32_t)(s >> log_n), off = (uint32_t)(s & (n - 1));
-        FrB sg = w.at(off);
+        F sg = w.at(off);
         if (blk == 1) sg = sg * u;
         else if (blk == 2) sg = sg * uu;
         d = d * (fv + beta * sg + gamma);
@@ -234,29 +244,32 @@ __global__ void __launch_bounds__(256) k_ratio_numden(const FrB* L, const FrB* R
     stb(den + i + 1, d);
 }
 
-__global__ void k_mul_inplace(FrB* a, const FrB* b, size_t n) {
+template <class F>
+__global__ void k_mul_inplace(F* a, const F* b, size_t n) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) stb(a + i, ldb(a + i) * ldb(b + i));
 }
 
 // ---------------------------------------------------------------- foldH / linearized
-__global__ void k_fold_h(const FrB* h, size_t np2, FrB z, FrB* out) {
+template <class F>
+__global__ void k_fold_h(const F* h, size_t np2, F z, F* out) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= np2) return;
-    FrB t = ldb(h + 2 * np2 + i) * z + ldb(h + np2 + i);
+    F t = ldb(h + 2 * np2 + i) * z + ldb(h + np2 + i);
     stb(out + i, t * z + ldb(h + i));
 }
 
 // prove.go:1347-1386, term by term
-__global__ void __launch_bounds__(256) k_linearized(LinParams P) {
+template <class F>
+__global__ void __launch_bounds__(256) k_linearized(LinParamsT<F> P) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.nz) return;
-    const FrB zi = ldb(P.z + i);
-    FrB t = zi * P.s2;
+    const F zi = ldb(P.z + i);
+    F t = zi * P.s2;
     if (i < P.ns3) t = t + ldb(P.s3 + i) * P.s1;
     t = t * P.alpha;
     if (i < P.nq) {
-        FrB t0 = ldb(P.ql + i) * P.l + ldb(P.qm + i) * P.rl;
+        F t0 = ldb(P.ql + i) * P.l + ldb(P.qm + i) * P.rl;
         t = t + t0;
         t = t + ldb(P.qr + i) * P.r;
         t = t + (ldb(P.qo + i) * P.o + ldb(P.qk + i));
@@ -266,7 +279,8 @@ __global__ void __launch_bounds__(256) k_linearized(LinParams P) {
 }
 
 // out[bitrev(i)] = in[i] (out-of-place; fft.BitReverse / iop ToRegular)
-__global__ void k_bit_reverse(FrB* out, const FrB* in, size_t n, int log_n) {
+template <class F>
+__global__ void k_bit_reverse(F* out, const F* in, size_t n, int log_n) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t r = log_n ? (__brev((uint32_t)i) >> (32 - log_n)) : 0u;
@@ -274,34 +288,38 @@ __global__ void k_bit_reverse(FrB* out, const FrB* in, size_t n, int log_n) {
 }
 
 // y[i] += a * x[i]
-__global__ void k_axpy(FrB* y, const FrB* x, size_t n, FrB a) {
+template <class F>
+__global__ void k_axpy(F* y, const F* x, size_t n, F a) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) stb(y + i, ldb(y + i) + a * ldb(x + i));
 }
 
-__global__ void k_scale(FrB* y, size_t n, FrB a) {
+template <class F>
+__global__ void k_scale(F* y, size_t n, F a) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) stb(y + i, ldb(y + i) * a);
 }
-__global__ void k_shift_copy(const FrB* in, FrB* out, size_t n) {
+template <class F>
+__global__ void k_shift_copy(const F* in, F* out, size_t n) {
     size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) stb(out + i, ldb(in + (i + 1 == n ? 0 : i + 1)));
 }
 
 size_t horner_arena_bytes(size_t n) { return ((n * 32 + 255) & ~(size_t)255) + scan_arena_bytes(n); }
 
-void horner(const FrB* f, size_t n, const FrB& a, FrB* q, FrB* value_dev, hipStream_t st, Arena& ar) {
+template <class F>
+void horner(const F* f, size_t n, const F& a, F* q, F* value_dev, hipStream_t st, Arena& ar) {
     if (n == 0) {
         GG_HIP(hipMemsetAsync(value_dev, 0, 32, st));
         return;
     }
-    FrB* g = ar.get<FrB>(n);
-    hipLaunchKernelGGL(k_reverse_copy, dim3(grid_for(n, 256)), dim3(256), 0, st, g, f, n);
+    F* g = ar.get<F>(n);
+    hipLaunchKernelGGL(k_reverse_copy<F>, dim3(grid_for(n, 256)), dim3(256), 0, st, g, f, n);
     GG_HIP(hipGetLastError());
     // x_k = y_k + a x_(k-1) over y = reversed f: x_(n-1) = f(a), x_k = sum_(i >= n-1-k) f_i a^(i-(n-1-k))
-    scan_rec<SCAN_AFFINE>(g, n, a, st, ar);
+    scan_rec<F, SCAN_AFFINE>(g, n, a, st, ar);
     if (q && n > 1) {
-        hipLaunchKernelGGL(k_quotient_out, dim3(grid_for(n, 256)), dim3(256), 0, st, q, (const FrB*)g, n);
+        hipLaunchKernelGGL(k_quotient_out<F>, dim3(grid_for(n, 256)), dim3(256), 0, st, q, (const F*)g, n);
         GG_HIP(hipGetLastError());
     }
     GG_HIP(hipMemcpyAsync(value_dev, g + n - 1, 32, hipMemcpyDeviceToDevice, st));
@@ -310,10 +328,11 @@ void horner(const FrB* f, size_t n, const FrB& a, FrB* q, FrB* value_dev, hipStr
 // x^e tables for e < n split as hi[e >> S] * lo[e & (2^S - 1)]: thread t
 // computes lo[t] = w^t and hi[t] = w^(t 2^S) by square-and-multiply (no host
 // buffer in flight)
-__global__ void k_pow_split(FrB w, FrB step, FrB* lo, uint32_t nlo, FrB* hi, uint32_t nhi) {
+template <class F>
+__global__ void k_pow_split(F w, F step, F* lo, uint32_t nlo, F* hi, uint32_t nhi) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    auto pw = [](FrB b, uint32_t e) {
-        FrB r = FrB::one();
+    auto pw = [](F b, uint32_t e) {
+        F r = F::one();
         while (e) {
             if (e & 1) r = r * b;
             b = b * b;
@@ -337,64 +356,87 @@ size_t ratio_arena_bytes(size_t n) {
     return tabs + ((n * 32 + 255) & ~(size_t)255) + batch_invert_arena_bytes(n) + scan_arena_bytes(n) + 1024;
 }
 
-void ratio(const FrB* l, const FrB* r, const FrB* o, const int64_t* perm, size_t n, const FrB& beta,
-           const FrB& gamma, const FrB& w, const FrB& u, FrB* z, hipStream_t st, Arena& ar) {
+template <class F>
+void ratio(const F* l, const F* r, const F* o, const int64_t* perm, size_t n, const F& beta, const F& gamma,
+           const F& w, const F& u, F* z, hipStream_t st, Arena& ar) {
     const int L = log2_ceil(n);
     const int S = (L + 1) / 2;
     const uint32_t nlo = 1u << S, nhi = 1u << (L - S);
-    FrB* lo = ar.get<FrB>(nlo);
-    FrB* hi = ar.get<FrB>(nhi);
-    FrB step = w;
+    F* lo = ar.get<F>(nlo);
+    F* hi = ar.get<F>(nhi);
+    F step = w;
     for (int i = 0; i < S; i++) step = step * step;  // w^(2^S)
-    hipLaunchKernelGGL(k_pow_split, dim3(grid_for(std::max(nlo, nhi), 256)), dim3(256), 0, st, w, step, lo, nlo,
+    hipLaunchKernelGGL(k_pow_split<F>, dim3(grid_for(std::max(nlo, nhi), 256)), dim3(256), 0, st, w, step, lo, nlo,
                        hi, nhi);
     GG_HIP(hipGetLastError());
-    PowSplit ps{hi, lo, S};
-    FrB* den = ar.get<FrB>(n);
-    hipLaunchKernelGGL(k_ratio_numden, dim3(grid_for(n, 256)), dim3(256), 0, st, l, r, o, perm, (uint32_t)n, L,
+    PowSplit<F> ps{hi, lo, S};
+    F* den = ar.get<F>(n);
+    hipLaunchKernelGGL(k_ratio_numden<F>, dim3(grid_for(n, 256)), dim3(256), 0, st, l, r, o, perm, (uint32_t)n, L,
                        beta, gamma, u, u * u, ps, z, den);
     GG_HIP(hipGetLastError());
     batch_invert(den, n, st, ar);  // t = fr.BatchInvert(t)
-    hipLaunchKernelGGL(k_mul_inplace, dim3(grid_for(n, 256)), dim3(256), 0, st, z, (const FrB*)den, n);
+    hipLaunchKernelGGL(k_mul_inplace<F>, dim3(grid_for(n, 256)), dim3(256), 0, st, z, (const F*)den, n);
     GG_HIP(hipGetLastError());
     scan_prod(z, n, st, ar);  // Z[i] = Z[i-1] * num_i / den_i
 }
 
-void fold_h(const FrB* h, size_t n_small, const FrB& zz, FrB* out, hipStream_t st) {
+template <class F>
+void fold_h(const F* h, size_t n_small, const F& zz, F* out, hipStream_t st) {
     const size_t np2 = n_small + 2;
-    hipLaunchKernelGGL(k_fold_h, dim3(grid_for(np2, 256)), dim3(256), 0, st, h, np2, zz, out);
+    hipLaunchKernelGGL(k_fold_h<F>, dim3(grid_for(np2, 256)), dim3(256), 0, st, h, np2, zz, out);
     GG_HIP(hipGetLastError());
 }
 
-void linearized(const LinParams& P, hipStream_t st) {
-    hipLaunchKernelGGL(k_linearized, dim3(grid_for(P.nz, 256)), dim3(256), 0, st, P);
+template <class F>
+void linearized(const LinParamsT<F>& P, hipStream_t st) {
+    hipLaunchKernelGGL(k_linearized<F>, dim3(grid_for(P.nz, 256)), dim3(256), 0, st, P);
     GG_HIP(hipGetLastError());
 }
 
-void bit_reverse(const FrB* in, FrB* out, size_t n, hipStream_t st) {
+template <class F>
+void bit_reverse(const F* in, F* out, size_t n, hipStream_t st) {
     int L = 0;
     while (((size_t)1 << L) < n) L++;
-    hipLaunchKernelGGL(k_bit_reverse, dim3(grid_for(n, 256)), dim3(256), 0, st, out, in, n, L);
+    hipLaunchKernelGGL(k_bit_reverse<F>, dim3(grid_for(n, 256)), dim3(256), 0, st, out, in, n, L);
     GG_HIP(hipGetLastError());
 }
 
-void axpy(FrB* y, const FrB* x, size_t n, const FrB& a, hipStream_t st) {
+template <class F>
+void axpy(F* y, const F* x, size_t n, const F& a, hipStream_t st) {
     if (!n) return;
-    hipLaunchKernelGGL(k_axpy, dim3(grid_for(n, 256)), dim3(256), 0, st, y, x, n, a);
+    hipLaunchKernelGGL(k_axpy<F>, dim3(grid_for(n, 256)), dim3(256), 0, st, y, x, n, a);
     GG_HIP(hipGetLastError());
 }
 
-void scale(FrB* y, size_t n, const FrB& a, hipStream_t st) {
+template <class F>
+void scale(F* y, size_t n, const F& a, hipStream_t st) {
     if (!n) return;
-    hipLaunchKernelGGL(k_scale, dim3(grid_for(n, 256)), dim3(256), 0, st, y, n, a);
+    hipLaunchKernelGGL(k_scale<F>, dim3(grid_for(n, 256)), dim3(256), 0, st, y, n, a);
     GG_HIP(hipGetLastError());
 }
 
-void shift_copy(const FrB* in, FrB* out, size_t n, hipStream_t st) {
+template <class F>
+void shift_copy(const F* in, F* out, size_t n, hipStream_t st) {
     if (!n) return;
-    hipLaunchKernelGGL(k_shift_copy, dim3(grid_for(n, 256)), dim3(256), 0, st, in, out, n);
+    hipLaunchKernelGGL(k_shift_copy<F>, dim3(grid_for(n, 256)), dim3(256), 0, st, in, out, n);
     GG_HIP(hipGetLastError());
 }
+
+// the two scalar fields of the PlonK provers
+#define GG_PLK_INST(F)                                                                                          \
+    template void scan_prod<F>(F*, size_t, hipStream_t, Arena&);                                                \
+    template void horner<F>(const F*, size_t, const F&, F*, F*, hipStream_t, Arena&);                          \
+    template void ratio<F>(const F*, const F*, const F*, const int64_t*, size_t, const F&, const F&, const F&, \
+                           const F&, F*, hipStream_t, Arena&);                                                  \
+    template void fold_h<F>(const F*, size_t, const F&, F*, hipStream_t);                                       \
+    template void linearized<F>(const LinParamsT<F>&, hipStream_t);                                             \
+    template void bit_reverse<F>(const F*, F*, size_t, hipStream_t);                                            \
+    template void axpy<F>(F*, const F*, size_t, const F&, hipStream_t);                                         \
+    template void scale<F>(F*, size_t, const F&, hipStream_t);                                                  \
+    template void shift_copy<F>(const F*, F*, size_t, hipStream_t);
+GG_PLK_INST(FrBls)
+GG_PLK_INST(Fr)
+#undef GG_PLK_INST
 
 }  // namespace plk
 

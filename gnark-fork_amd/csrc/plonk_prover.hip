@@ -1,5 +1,7 @@
-// PlonK BLS12-381 prover behind the C ABI: the device section of gnark's
-// backend/plonk/bls12-381 Prove (prove.go:116-1079) after the solver.
+// PlonK prover behind the C ABI: the device section of gnark's
+// backend/plonk/bls12-381 and backend/plonk/bn254 Prove (prove.go:116-1079,
+// the same generated code for both curves) after the solver.  PlonkImpl<Cv> is
+// the prover over one curve; the C handle dispatches on the key's curve.
 //
 // Stages (prove.go's errgroup DAG, mapped onto 4 HIP streams and host threads):
 //   commitToLRO        3 KZG MSMs on pk.KzgLagrange at once (one MsmWork each),
@@ -18,7 +20,7 @@
 //   batchOpening       kzg.BatchOpenSinglePoint at zeta
 // Transcripts: fiat-shamir (challenge = H(name | previous | bindings)),
 // points bound with RawBytes (deriveRandomness, verify.go:342-360) or Marshal
-// (compressed: bindPublicData verify.go:296-340, kzg deriveGamma), scalars as
+// (= RawBytes too: bindPublicData verify.go:296-340, kzg deriveGamma), scalars as
 // 32-B big-endian.  The hash is the caller's (gg_hash_fn) or SHA-256.
 #include "plonk_ops.h"
 #include "curve.cuh"
@@ -33,6 +35,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <fstream>
+#include <type_traits>
 
 struct gg_msm_base;
 namespace gg {
@@ -43,9 +46,35 @@ void msm_work_delete(MsmWork* w);
 }  // namespace gg
 
 using namespace gg;
-using plk::FrB;
-using BAff = Affine<FpBls>;
-using BJac = Jac<FpBls>;
+
+// curves of the PlonK prover: backend/plonk/bls12-381 and backend/plonk/bn254
+// (the same generated prove.go over another curve)
+struct PlonkBls12381 {
+    using Fr = FrBls;
+    using Fp = FpBls;
+    static constexpr int curve = GG_CURVE_BLS12_381, group = GG_BLS12_381_G1, fp_u32 = 12;
+    static constexpr uint8_t raw_inf = 0x40;             // mUncompressedInfinity (zcash flags)
+    static constexpr uint32_t fr_top_mask = 0x7fffffffu;  // r < 2^255
+};
+struct PlonkBn254 {
+    using Fr = gg::Fr;
+    using Fp = gg::Fp;
+    static constexpr int curve = GG_CURVE_BN254, group = GG_G1, fp_u32 = 8;
+    static constexpr uint8_t raw_inf = 0x00;             // mUncompressed: infinity is all zeros
+    static constexpr uint32_t fr_top_mask = 0x3fffffffu;  // r < 2^254
+};
+
+// key polynomial ids shared by both curves
+struct PK {
+    enum { QL, QR, QM, QO, QK, S1, S2, S3, NTRACE };
+    enum { E_QL, E_QR, E_QM, E_QO, E_S1, E_S2, E_S3, E_X, E_LONE, E_QCP0 };
+};
+
+// the C handle: a PlonkImpl<Cv>::Key of its curve
+struct gg_plonk_pk {
+    int curve = GG_CURVE_BLS12_381;
+    virtual ~gg_plonk_pk() {}
+};
 
 namespace {
 
@@ -60,34 +89,6 @@ void be_bytes(const uint32_t* v, uint8_t* out) {
         out[4 * i + 2] = (uint8_t)(w >> 8);
         out[4 * i + 3] = (uint8_t)w;
     }
-}
-// fr.Element.Marshal: 32-B big-endian canonical
-void fr_marshal(const FrB& x, uint8_t out[32]) {
-    const FrB c = from_mont(x);
-    be_bytes<8>(c.v, out);
-}
-// fr.Element.SetBytes: big-endian integer mod r
-FrB fr_set_bytes(const uint8_t* b, size_t n) {
-    FrB acc = FrB::zero();
-    FrB b256 = FrB::zero();
-    b256.v[0] = 256;
-    b256 = to_mont(b256);
-    for (size_t i = 0; i < n; i++) {
-        FrB d = FrB::zero();
-        d.v[0] = b[i];
-        acc = acc * b256 + to_mont(d);
-    }
-    return acc;
-}
-// G1Affine.RawBytes = Marshal (uncompressed, 96 B; infinity = 0x40 | zeros)
-void g1_raw_bytes(const BAff& p, uint8_t out[96]) {
-    memset(out, 0, 96);
-    if (p.is_inf()) {
-        out[0] = 0x40;
-        return;
-    }
-    be_bytes<12>(from_mont(p.x).v, out);
-    be_bytes<12>(from_mont(p.y).v, out + 48);
 }
 
 // ------------------------------------------------------------ transcript
@@ -109,80 +110,9 @@ struct Hasher {
     }
 };
 
-// gnark-crypto fiat-shamir Transcript: challenge i = H(name_i | value_(i-1) | bindings_i)
-struct Transcript {
-    std::vector<std::string> names;
-    std::vector<std::vector<uint8_t>> bound, value;
-    Hasher h;
-    Transcript(std::initializer_list<const char*> ns, Hasher hh) : h(hh) {
-        for (const char* s : ns) names.emplace_back(s);
-        bound.resize(names.size());
-        value.resize(names.size());
-    }
-    size_t idx(const char* n) const {
-        for (size_t i = 0; i < names.size(); i++)
-            if (names[i] == n) return i;
-        throw Error(GG_ERR_INTERNAL, "unknown challenge");
-    }
-    void bind(const char* n, const uint8_t* b, size_t len) {
-        auto& v = bound[idx(n)];
-        v.insert(v.end(), b, b + len);
-    }
-    FrB compute(const char* n) {
-        const size_t i = idx(n);
-        std::vector<uint8_t> msg(names[i].begin(), names[i].end());
-        if (i) msg.insert(msg.end(), value[i - 1].begin(), value[i - 1].end());
-        msg.insert(msg.end(), bound[i].begin(), bound[i].end());
-        value[i] = h(msg);
-        return fr_set_bytes(value[i].data(), value[i].size());
-    }
-};
-// deriveRandomness (verify.go:342-360): RawBytes of each point, then the challenge
-FrB derive(Transcript& fs, const char* n, std::initializer_list<const BAff*> pts) {
-    uint8_t b[96];
-    for (const BAff* p : pts) {
-        g1_raw_bytes(*p, b);
-        fs.bind(n, b, 96);
-    }
-    return fs.compute(n);
-}
-
-// ------------------------------------------------------------ host G1 helpers
-BJac jmul(const BAff& p, const FrB& k) {
-    const FrB c = from_mont(k);
-    return jac_mul(BJac::from_affine(p), c.v);
-}
-BAff to_aff(const BJac& j) { return jac_to_affine(j); }
-FrB frv(uint64_t x) {
-    FrB r = FrB::zero();
-    r.v[0] = (uint32_t)x;
-    r.v[1] = (uint32_t)(x >> 32);
-    return to_mont(r);
-}
-FrB horner_host(const std::vector<FrB>& c, const FrB& x) {
-    FrB r = FrB::zero();
-    for (size_t k = c.size(); k-- > 0;) r = r * x + c[k];
-    return r;
-}
-// 255-bit random fr (rejection sampled, SetRandom of gnark-crypto)
-FrB fr_random() {
-    static std::mutex mu;
-    std::lock_guard<std::mutex> lk(mu);
-    static std::ifstream ur("/dev/urandom", std::ios::binary);
-    GG_CHECK(ur.good(), GG_ERR_INTERNAL, "no /dev/urandom");
-    const FrB p = FrB::modulus();
-    for (;;) {
-        FrB x;
-        ur.read((char*)x.v, 32);
-        x.v[7] &= 0x7fffffffu;  // r < 2^255
-        bool lt = false;
-        for (int i = 7; i >= 0; i--)
-            if (x.v[i] != p.v[i]) { lt = x.v[i] < p.v[i]; break; }
-        if (lt) return to_mont(x);
-    }
-}
 
 }  // namespace
+
 
 // ============================================================== key
 // One-process multi-GPU (gg_plonk_pk_create_multi): device parts[p] (p >= 1) of
@@ -225,7 +155,120 @@ struct PlonkPeer {
     }
 };
 
-struct gg_plonk_pk {
+// ============================================================== prover of one curve
+template <class Cv>
+struct PlonkImpl {
+    using FrB = typename Cv::Fr;
+    using BAff = Affine<typename Cv::Fp>;
+    using BJac = Jac<typename Cv::Fp>;
+    static constexpr size_t PT = sizeof(BAff);  // affine G1 bytes: 96 (BLS12-381), 64 (BN254)
+
+// fr.Element.Marshal: 32-B big-endian canonical
+static void fr_marshal(const FrB& x, uint8_t out[32]) {
+    const FrB c = from_mont(x);
+    be_bytes<8>(c.v, out);
+}
+// fr.Element.SetBytes: big-endian integer mod r
+static FrB fr_set_bytes(const uint8_t* b, size_t n) {
+    FrB acc = FrB::zero();
+    FrB b256 = FrB::zero();
+    b256.v[0] = 256;
+    b256 = to_mont(b256);
+    for (size_t i = 0; i < n; i++) {
+        FrB d = FrB::zero();
+        d.v[0] = b[i];
+        acc = acc * b256 + to_mont(d);
+    }
+    return acc;
+}
+// G1Affine.RawBytes = Marshal (uncompressed X | Y, 2 x the fp bytes; infinity:
+// BLS12-381 0x40 | zeros, BN254 all zeros -- gnark-crypto's mUncompressedInfinity)
+static void g1_raw_bytes(const BAff& p, uint8_t* out) {
+    memset(out, 0, PT);
+    if (p.is_inf()) {
+        out[0] = Cv::raw_inf;
+        return;
+    }
+    be_bytes<Cv::fp_u32>(from_mont(p.x).v, out);
+    be_bytes<Cv::fp_u32>(from_mont(p.y).v, out + PT / 2);
+}
+
+
+// gnark-crypto fiat-shamir Transcript: challenge i = H(name_i | value_(i-1) | bindings_i)
+struct Transcript {
+    std::vector<std::string> names;
+    std::vector<std::vector<uint8_t>> bound, value;
+    Hasher h;
+    Transcript(std::initializer_list<const char*> ns, Hasher hh) : h(hh) {
+        for (const char* s : ns) names.emplace_back(s);
+        bound.resize(names.size());
+        value.resize(names.size());
+    }
+    size_t idx(const char* n) const {
+        for (size_t i = 0; i < names.size(); i++)
+            if (names[i] == n) return i;
+        throw Error(GG_ERR_INTERNAL, "unknown challenge");
+    }
+    void bind(const char* n, const uint8_t* b, size_t len) {
+        auto& v = bound[idx(n)];
+        v.insert(v.end(), b, b + len);
+    }
+    FrB compute(const char* n) {
+        const size_t i = idx(n);
+        std::vector<uint8_t> msg(names[i].begin(), names[i].end());
+        if (i) msg.insert(msg.end(), value[i - 1].begin(), value[i - 1].end());
+        msg.insert(msg.end(), bound[i].begin(), bound[i].end());
+        value[i] = h(msg);
+        return fr_set_bytes(value[i].data(), value[i].size());
+    }
+};
+// deriveRandomness (verify.go:342-360): RawBytes of each point, then the challenge
+static FrB derive(Transcript& fs, const char* n, std::initializer_list<const BAff*> pts) {
+    uint8_t b[96];
+    for (const BAff* p : pts) {
+        g1_raw_bytes(*p, b);
+        fs.bind(n, b, PT);
+    }
+    return fs.compute(n);
+}
+
+// ------------------------------------------------------------ host G1 helpers
+static BJac jmul(const BAff& p, const FrB& k) {
+    const FrB c = from_mont(k);
+    return jac_mul(BJac::from_affine(p), c.v);
+}
+static BAff to_aff(const BJac& j) { return jac_to_affine(j); }
+static FrB frv(uint64_t x) {
+    FrB r = FrB::zero();
+    r.v[0] = (uint32_t)x;
+    r.v[1] = (uint32_t)(x >> 32);
+    return to_mont(r);
+}
+static FrB horner_host(const std::vector<FrB>& c, const FrB& x) {
+    FrB r = FrB::zero();
+    for (size_t k = c.size(); k-- > 0;) r = r * x + c[k];
+    return r;
+}
+// random fr (rejection sampled, SetRandom of gnark-crypto)
+static FrB fr_random() {
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lk(mu);
+    static std::ifstream ur("/dev/urandom", std::ios::binary);
+    GG_CHECK(ur.good(), GG_ERR_INTERNAL, "no /dev/urandom");
+    const FrB p = FrB::modulus();
+    for (;;) {
+        FrB x;
+        ur.read((char*)x.v, 32);
+        x.v[7] &= Cv::fr_top_mask;  // r < 2^255 (BLS12-381), < 2^254 (BN254)
+        bool lt = false;
+        for (int i = 7; i >= 0; i--)
+            if (x.v[i] != p.v[i]) { lt = x.v[i] < p.v[i]; break; }
+        if (lt) return to_mont(x);
+    }
+}
+
+struct Key : gg_plonk_pk {
+    using CvT = Cv;
     int log_n = 0, log_big = 0;
     size_t n = 0, big = 0, rho = 0;
     FrB omega, omega_big, u, n_inv;
@@ -233,11 +276,11 @@ struct gg_plonk_pk {
     std::vector<gg_domain_t> dcos;
     std::vector<FrB> coset_shift;
     // trace, canonical regular (reg) and bit-reversed (brev); Qk incomplete
-    enum { QL, QR, QM, QO, QK, S1, S2, S3, NTRACE };
+    enum { QL = PK::QL, QR, QM, QO, QK, S1, S2, S3, NTRACE };
     DevBuf reg[NTRACE], brev[NTRACE], qk_lag;
     std::vector<DevBuf> qcp_reg, qcp_brev;
     // resident coset evaluations [poly][coset]: Ql Qr Qm Qo S1 S2 S3 X LOne Qcp_i
-    enum { E_QL, E_QR, E_QM, E_QO, E_S1, E_S2, E_S3, E_X, E_LONE, E_QCP0 };
+    enum { E_QL = PK::E_QL, E_QR, E_QM, E_QO, E_S1, E_S2, E_S3, E_X, E_LONE, E_QCP0 };
     std::vector<std::vector<DevBuf>> ev;
     DevBuf perm, tw0;
     gg_msm_base_t kzg = nullptr, kzg_lag = nullptr;
@@ -267,7 +310,8 @@ struct gg_plonk_pk {
     std::vector<hipEvent_t> evs;  // cross-stream ordering events, reused by every prove
     size_t ev_next = 0;
     std::mutex mu;
-    ~gg_plonk_pk() {
+    Key() { curve = Cv::curve; }
+    ~Key() override {
         peers.clear();
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
         for (auto w : work)
@@ -282,33 +326,32 @@ struct gg_plonk_pk {
     }
 };
 
-namespace {
 
-FrB* F(const DevBuf& b) { return b.as<FrB>(); }
-void dcopy(void* dst, const void* src, size_t bytes, hipStream_t st) {
+static FrB* F(const DevBuf& b) { return b.as<FrB>(); }
+static void dcopy(void* dst, const void* src, size_t bytes, hipStream_t st) {
     if (bytes) GG_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st));
 }
-void zero(void* dst, size_t bytes, hipStream_t st) {
+static void zero(void* dst, size_t bytes, hipStream_t st) {
     if (bytes) GG_HIP(hipMemsetAsync(dst, 0, bytes, st));
 }
-void up(void* dst, const void* src, size_t bytes, bool on_dev, hipStream_t st) {
+static void up(void* dst, const void* src, size_t bytes, bool on_dev, hipStream_t st) {
     if (bytes) GG_HIP(hipMemcpyAsync(dst, src, bytes, on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
 }
 // canonical regular -> canonical bit-reversed copy
-void to_brev(gg_plonk_pk* pk, const FrB* reg, FrB* brev, hipStream_t st) { plk::bit_reverse(reg, brev, pk->n, st); }
+static void to_brev(Key* pk, const FrB* reg, FrB* brev, hipStream_t st) { plk::bit_reverse(reg, brev, pk->n, st); }
 // Lagrange regular (n) -> canonical bit-reversed (out) + canonical regular (reg)
-void lag_to_canonical(gg_plonk_pk* pk, const FrB* lag, FrB* brev, FrB* reg, hipStream_t st) {
+static void lag_to_canonical(Key* pk, const FrB* lag, FrB* brev, FrB* reg, hipStream_t st) {
     dcopy(brev, lag, pk->n * 32, st);
     plk::ntt(pk->d0, brev, 1, 0, 0, st);  // FFTInverse DIF: natural in -> bit-reversed out
     if (reg) plk::bit_reverse(brev, reg, pk->n, st);
 }
 // evaluations on coset i (natural order) of a canonical bit-reversed polynomial
-void coset_eval(gg_plonk_pk* pk, const FrB* brev, FrB* out, int i, hipStream_t st) {
+static void coset_eval(Key* pk, const FrB* brev, FrB* out, int i, hipStream_t st) {
     dcopy(out, brev, pk->n * 32, st);
     plk::ntt(pk->dcos[i], out, 0, 1, 1, st);  // FFT DIT on the coset: bit-reversed in -> natural out
 }
 // `to` waits for the work enqueued on `from` so far (events live as long as the key)
-void record_wait(gg_plonk_pk* pk, hipStream_t from, hipStream_t to) {
+static void record_wait(Key* pk, hipStream_t from, hipStream_t to) {
     if (from == to) return;
     if (pk->ev_next == pk->evs.size()) {
         hipEvent_t e;
@@ -321,7 +364,7 @@ void record_wait(gg_plonk_pk* pk, hipStream_t from, hipStream_t to) {
 }
 // a peer part's share of an MSM: its scalar slice copied from the primary GPU
 // (xGMI peer copy), its resident base slice
-BJac peer_msm(gg_plonk_pk* pk, PlonkPeer* p, bool kzg, int wi, const FrB* scal) {
+static BJac peer_msm(Key* pk, PlonkPeer* p, bool kzg, int wi, const FrB* scal) {
     GG_HIP(hipSetDevice(p->device));
     const size_t lo = kzg ? p->k_lo : p->l_lo, hi = kzg ? p->k_hi : p->l_hi;
     BJac j = BJac::inf();
@@ -332,7 +375,7 @@ BJac peer_msm(gg_plonk_pk* pk, PlonkPeer* p, bool kzg, int wi, const FrB* scal) 
 }
 // this rank's partial MSM (the whole MSM on one GPU, or split over the key's
 // device parts and summed here); red() completes a process shard's partial
-BJac msm_jac(gg_plonk_pk* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStream_t st) {
+static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStream_t st) {
     BJac j = BJac::inf();
     const bool kz = base == pk->kzg;
     const size_t lo = kz ? pk->k_lo : pk->l_lo;
@@ -349,15 +392,15 @@ BJac msm_jac(gg_plonk_pk* pk, gg_msm_base_t base, int wi, const FrB* scal, hipSt
     return j;
 }
 // kzg.Commit(p, pk.Kzg) of a buffer of n + 3 scalars (zero beyond the polynomial)
-BJac commit_kzg(gg_plonk_pk* pk, int wi, const FrB* scal, hipStream_t st) { return msm_jac(pk, pk->kzg, wi, scal, st); }
+static BJac commit_kzg(Key* pk, int wi, const FrB* scal, hipStream_t st) { return msm_jac(pk, pk->kzg, wi, scal, st); }
 // sum of the ranks' partials (called in one fixed order on every rank)
-BJac red(gg_plonk_pk* pk, BJac j) {
+static BJac red(Key* pk, BJac j) {
     if (pk->world == 1) return j;
     GG_CHECK(pk->reduce(pk->reduce_ctx, &j) == 0, GG_ERR_DEVICE, "commitment reduce callback failed");
     return j;
 }
 // commitBlindingFactor (prove.go:1159-1172): sum_j b_j (G1[n + j] - G1[j])
-BJac blind_commit(gg_plonk_pk* pk, const std::vector<FrB>& b) {
+static BJac blind_commit(Key* pk, const std::vector<FrB>& b) {
     BJac acc = BJac::inf();
     for (size_t j = 0; j < b.size(); j++) {
         acc = jac_add(acc, jmul(pk->blind_hi[j], b[j]));
@@ -365,21 +408,19 @@ BJac blind_commit(gg_plonk_pk* pk, const std::vector<FrB>& b) {
     }
     return acc;
 }
-FrB fetch(const FrB* dev, hipStream_t st) {
+static FrB fetch(const FrB* dev, hipStream_t st) {
     FrB v;
     GG_HIP(hipMemcpyAsync(v.v, dev, 32, hipMemcpyDeviceToHost, st));
     GG_HIP(hipStreamSynchronize(st));
     return v;
 }
-FrB eval_dev(gg_plonk_pk* pk, const FrB* f, size_t len, const FrB& a, FrB* q, FrB* slot, int ai, hipStream_t st) {
+static FrB eval_dev(Key* pk, const FrB* f, size_t len, const FrB& a, FrB* q, FrB* slot, int ai, hipStream_t st) {
     pk->ar[ai].reset();
     plk::horner(f, len, a, q, slot, st, pk->ar[ai]);
     return fetch(slot, st);
 }
 
-}  // namespace
-
-static void plonk_pk_build(gg_plonk_pk* pk, int log_n, int log_big, const void* omega, const void* omega_big,
+static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, const void* omega_big,
                            const void* coset_shift, const void* kzg_g1, size_t n_kzg,
                            const void* kzg_lagrange_g1, const void* const* trace, const void* const* qcp,
                            int n_cmt, const int64_t* perm, size_t nb_public, const uint64_t* cmt_idx,
@@ -440,7 +481,7 @@ static void plonk_pk_build(gg_plonk_pk* pk, int log_n, int log_big, const void* 
     GG_CHECK(pow_u64(pk->omega_big, pk->rho) == pk->omega, GG_ERR_INVALID_ARG, "omega_big^(|big|/n) != omega");
     auto dom = [&](int lg, const FrB& w, const FrB& g) {
         gg_domain_t d;
-        int rc = gg_domain_create_ex(GG_CURVE_BLS12_381, lg, w.v, g.v, &d);
+        int rc = gg_domain_create_ex(Cv::curve, lg, w.v, g.v, &d);
         GG_CHECK(rc == GG_OK, rc, gg_last_error());
         return d;
     };
@@ -475,10 +516,10 @@ static void plonk_pk_build(gg_plonk_pk* pk, int log_n, int log_big, const void* 
                 for (hipStream_t& x : p->s) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
                 for (auto& w : p->work) w = msm_work_new();
                 for (auto& b : p->scal) b.alloc(32 * std::max<size_t>(1, std::max(p->k_hi - p->k_lo, p->l_hi - p->l_lo)));
-                int rc = gg_msm_base_create(GG_BLS12_381_G1, (const uint8_t*)kzg_g1 + 96 * p->k_lo, p->k_hi - p->k_lo,
+                int rc = gg_msm_base_create(Cv::group, (const uint8_t*)kzg_g1 + PT * p->k_lo, p->k_hi - p->k_lo,
                                             0, nullptr, 0, &p->kzg);
                 GG_CHECK(rc == GG_OK, rc, gg_last_error());
-                rc = gg_msm_base_create(GG_BLS12_381_G1, (const uint8_t*)kzg_lagrange_g1 + 96 * p->l_lo,
+                rc = gg_msm_base_create(Cv::group, (const uint8_t*)kzg_lagrange_g1 + PT * p->l_lo,
                                         p->l_hi - p->l_lo, 0, nullptr, 0, &p->kzg_lag);
                 GG_CHECK(rc == GG_OK, rc, gg_last_error());
                 for (size_t i = 0; i < pk->rho; i++)
@@ -493,20 +534,20 @@ static void plonk_pk_build(gg_plonk_pk* pk, int log_n, int log_big, const void* 
             range(n + 3, pk->k_lo, pk->k_hi);
             range(n, pk->l_lo, pk->l_hi);
         }
-        int rc = gg_msm_base_create(GG_BLS12_381_G1, (const uint8_t*)kzg_g1 + 96 * pk->k_lo, pk->k_hi - pk->k_lo, 0,
+        int rc = gg_msm_base_create(Cv::group, (const uint8_t*)kzg_g1 + PT * pk->k_lo, pk->k_hi - pk->k_lo, 0,
                                     nullptr, 0, &pk->kzg);
         GG_CHECK(rc == GG_OK, rc, gg_last_error());
-        rc = gg_msm_base_create(GG_BLS12_381_G1, (const uint8_t*)kzg_lagrange_g1 + 96 * pk->l_lo,
+        rc = gg_msm_base_create(Cv::group, (const uint8_t*)kzg_lagrange_g1 + PT * pk->l_lo,
                                 pk->l_hi - pk->l_lo, 0, nullptr, 0, &pk->kzg_lag);
         GG_CHECK(rc == GG_OK, rc, gg_last_error());
         const uint8_t* g = (const uint8_t*)kzg_g1;
         for (int j = 0; j < 3; j++) {
-            memcpy(&pk->blind_lo[j], g + 96 * j, 96);
-            memcpy(&pk->blind_hi[j], g + 96 * (n + j), 96);
+            memcpy(&pk->blind_lo[j], g + PT * j, 96);
+            memcpy(&pk->blind_hi[j], g + PT * (n + j), 96);
         }
     }
     // trace polynomials
-    for (int k = 0; k < gg_plonk_pk::NTRACE; k++) {
+    for (int k = 0; k < Key::NTRACE; k++) {
         GG_CHECK(trace[k], GG_ERR_INVALID_ARG, "null trace polynomial");
         pk->reg[k].alloc(nb);
         pk->brev[k].alloc(nb);
@@ -525,7 +566,7 @@ static void plonk_pk_build(gg_plonk_pk* pk, int log_n, int log_big, const void* 
     // Qk in Lagrange regular form (completeQk: trace.Qk.Clone().ToLagrange().ToRegular())
     {
         DevBuf t(nb);
-        dcopy(t.p, pk->reg[gg_plonk_pk::QK].p, nb, st);
+        dcopy(t.p, pk->reg[Key::QK].p, nb, st);
         plk::ntt(pk->d0, t.p, 0, 0, 0, st);  // FFT DIF: natural in -> bit-reversed out
         pk->qk_lag.alloc(nb);
         plk::bit_reverse(F(t), F(pk->qk_lag), n, st);
@@ -550,10 +591,10 @@ static void plonk_pk_build(gg_plonk_pk* pk, int log_n, int log_big, const void* 
         GG_HIP(hipMemcpyAsync(lone.p, v.data(), nb, hipMemcpyHostToDevice, st));
         GG_HIP(hipStreamSynchronize(st));
     }
-    std::vector<const FrB*> srcs = {F(pk->brev[gg_plonk_pk::QL]), F(pk->brev[gg_plonk_pk::QR]),
-                                    F(pk->brev[gg_plonk_pk::QM]), F(pk->brev[gg_plonk_pk::QO]),
-                                    F(pk->brev[gg_plonk_pk::S1]), F(pk->brev[gg_plonk_pk::S2]),
-                                    F(pk->brev[gg_plonk_pk::S3]), F(xb), F(lone)};
+    std::vector<const FrB*> srcs = {F(pk->brev[Key::QL]), F(pk->brev[Key::QR]),
+                                    F(pk->brev[Key::QM]), F(pk->brev[Key::QO]),
+                                    F(pk->brev[Key::S1]), F(pk->brev[Key::S2]),
+                                    F(pk->brev[Key::S3]), F(xb), F(lone)};
     for (int i = 0; i < n_cmt; i++) srcs.push_back(F(pk->qcp_brev[i]));
     pk->ev.resize(srcs.size());
     for (size_t k = 0; k < srcs.size(); k++) {
@@ -620,23 +661,22 @@ static void plonk_pk_build(gg_plonk_pk* pk, int log_n, int log_big, const void* 
     pk->vkQcp.resize(n_cmt);
     if (vk_digests) {
         const uint8_t* d = (const uint8_t*)vk_digests;
-        for (int k = 0; k < 3; k++) memcpy(&pk->vkS[k], d + 96 * k, 96);
-        for (int k = 0; k < 5; k++) memcpy(&pk->vkQ[k], d + 96 * (3 + k), 96);
-        for (int i = 0; i < n_cmt; i++) memcpy(&pk->vkQcp[i], d + 96 * (8 + i), 96);
+        for (int k = 0; k < 3; k++) memcpy(&pk->vkS[k], d + PT * k, 96);
+        for (int k = 0; k < 5; k++) memcpy(&pk->vkQ[k], d + PT * (3 + k), 96);
+        for (int i = 0; i < n_cmt; i++) memcpy(&pk->vkQcp[i], d + PT * (8 + i), 96);
     } else {
         auto cm = [&](const DevBuf& reg) {
             zero(pk->pad.p, nb3, st);
             dcopy(pk->pad.p, reg.p, nb, st);
             return to_aff(red(pk, commit_kzg(pk, 0, F(pk->pad), st)));
         };
-        for (int k = 0; k < 3; k++) pk->vkS[k] = cm(pk->reg[gg_plonk_pk::S1 + k]);
-        for (int k = 0; k < 5; k++) pk->vkQ[k] = cm(pk->reg[gg_plonk_pk::QL + k]);
+        for (int k = 0; k < 3; k++) pk->vkS[k] = cm(pk->reg[Key::S1 + k]);
+        for (int k = 0; k < 5; k++) pk->vkQ[k] = cm(pk->reg[Key::QL + k]);
         for (int i = 0; i < n_cmt; i++) pk->vkQcp[i] = cm(pk->qcp_reg[i]);
     }
 }
 
 // ============================================================== prove
-namespace {
 
 struct PlonkProof {
     BAff lro[3], z, h[3], batched_h, zs_h;
@@ -646,12 +686,12 @@ struct PlonkProof {
 };
 
 // GG_PLONK_SERIAL=1: the concurrent MSM groups run one after another (A/B timing)
-std::launch msm_policy() {
+static std::launch msm_policy() {
     static const bool serial = getenv("GG_PLONK_SERIAL") && atoi(getenv("GG_PLONK_SERIAL"));
     return serial ? std::launch::deferred : std::launch::async;
 }
 
-void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB* pub, size_t nb_pub,
+static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* pub, size_t nb_pub,
            const void* const* cmt_values, const BAff* cmt_digests, const FrB* cmt_hashed, int n_cmt,
            const FrB* blinding, Hasher ch, Hasher fh, PlonkProof& P, double* tms) {
     const size_t n = pk->n, nb = 32 * n, nb3 = 32 * (n + 3);
@@ -712,9 +752,9 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
     Transcript fs({"gamma", "beta", "alpha", "zeta"}, ch);
     {
         uint8_t b[96];
-        for (int k = 0; k < 3; k++) { g1_raw_bytes(pk->vkS[k], b); fs.bind("gamma", b, 96); }
-        for (int k = 0; k < 5; k++) { g1_raw_bytes(pk->vkQ[k], b); fs.bind("gamma", b, 96); }
-        for (int i = 0; i < pk->n_cmt; i++) { g1_raw_bytes(pk->vkQcp[i], b); fs.bind("gamma", b, 96); }
+        for (int k = 0; k < 3; k++) { g1_raw_bytes(pk->vkS[k], b); fs.bind("gamma", b, PT); }
+        for (int k = 0; k < 5; k++) { g1_raw_bytes(pk->vkQ[k], b); fs.bind("gamma", b, PT); }
+        for (int i = 0; i < pk->n_cmt; i++) { g1_raw_bytes(pk->vkQcp[i], b); fs.bind("gamma", b, PT); }
         uint8_t f32[32];
         for (size_t i = 0; i < nb_pub; i++) { fr_marshal(pub[i], f32); fs.bind("gamma", f32, 32); }
     }
@@ -723,7 +763,7 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
     // ---- ratio Z (buildRatioCopyConstraint, prove.go:600-632) + its commitment
     for (int k = 0; k < 3; k++) record_wait(pk, s[k], s[0]);
     pk->ar[0].reset();
-    plk::ratio(F(pk->lag[0]), F(pk->lag[1]), F(pk->lag[2]), pk->perm.as<int64_t>(), n, beta, gamma, pk->omega,
+    plk::ratio(F(pk->lag[0]), F(pk->lag[1]), F(pk->lag[2]), pk->perm.template as<int64_t>(), n, beta, gamma, pk->omega,
                pk->u, F(pk->zlag), s[0], pk->ar[0]);
     record_wait(pk, s[0], s[1]);
     lag_to_canonical(pk, F(pk->zlag), F(pk->cbrev[3]), F(pk->can[3]), s[1]);  // overlaps the Z commitment
@@ -733,7 +773,7 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
     P.bsb22.assign(cmt_digests, cmt_digests + n_cmt);
     {
         uint8_t b[96];
-        for (int i = 0; i < n_cmt; i++) { g1_raw_bytes(P.bsb22[i], b); fs.bind("alpha", b, 96); }
+        for (int i = 0; i < n_cmt; i++) { g1_raw_bytes(P.bsb22[i], b); fs.bind("alpha", b, PT); }
     }
     const FrB alpha = derive(fs, "alpha", {&P.z});
     // ---- computeNumerator (prove.go:837-1079): two cosets in flight on s[2], s[3];
@@ -743,24 +783,24 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
     // Qk (6), Pi_j (7 + j); kev(k) = the key's resident evaluation of poly k there
     auto coset_params = [&](size_t i, FrB* const* e, auto kev, const FrB* tw0, FrB* cres, bool local) {
         const FrB cs = pk->u, css = pk->u * pk->u;
-        plk::NumParams NP{};
+        plk::NumParamsT<FrB> NP{};
         NP.x[plk::ID_L] = e[0];
         NP.x[plk::ID_R] = e[1];
         NP.x[plk::ID_O] = e[2];
         NP.x[plk::ID_Z] = e[3];
         NP.x[plk::ID_ZS] = nullptr;  // Z[(j + 1) % n]
-        NP.x[plk::ID_QL] = kev(gg_plonk_pk::E_QL);
-        NP.x[plk::ID_QR] = kev(gg_plonk_pk::E_QR);
-        NP.x[plk::ID_QM] = kev(gg_plonk_pk::E_QM);
-        NP.x[plk::ID_QO] = kev(gg_plonk_pk::E_QO);
+        NP.x[plk::ID_QL] = kev(Key::E_QL);
+        NP.x[plk::ID_QR] = kev(Key::E_QR);
+        NP.x[plk::ID_QM] = kev(Key::E_QM);
+        NP.x[plk::ID_QO] = kev(Key::E_QO);
         NP.x[plk::ID_QK] = e[6];
-        NP.x[plk::ID_S1] = kev(gg_plonk_pk::E_S1);
-        NP.x[plk::ID_S2] = kev(gg_plonk_pk::E_S2);
-        NP.x[plk::ID_S3] = kev(gg_plonk_pk::E_S3);
-        NP.x[plk::ID_ID] = kev(gg_plonk_pk::E_X);  // X; beta folded into ka, kb, kc
-        NP.x[plk::ID_LONE] = kev(gg_plonk_pk::E_LONE);
+        NP.x[plk::ID_S1] = kev(Key::E_S1);
+        NP.x[plk::ID_S2] = kev(Key::E_S2);
+        NP.x[plk::ID_S3] = kev(Key::E_S3);
+        NP.x[plk::ID_ID] = kev(Key::E_X);  // X; beta folded into ka, kb, kc
+        NP.x[plk::ID_LONE] = kev(Key::E_LONE);
         for (int j = 0; j < n_cmt; j++) {
-            NP.x[plk::ID_QCI + 2 * j] = kev(gg_plonk_pk::E_QCP0 + j);
+            NP.x[plk::ID_QCI + 2 * j] = kev(Key::E_QCP0 + j);
             NP.x[plk::ID_QCI + 2 * j + 1] = e[7 + j];
         }
         NP.nx = plk::ID_QCI + 2 * n_cmt;
@@ -818,7 +858,7 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
                     for (int j = 0; j < n_cmt; j++) ceval(p->in[5 + j], p->cev[7 + j]);
                     FrB* e[7 + plk::MAX_CMT] = {};
                     for (int k = 0; k < 7 + n_cmt; k++) e[k] = F(p->cev[k]);
-                    plk::NumParams NP = coset_params(
+                    plk::NumParamsT<FrB> NP = coset_params(
                         (size_t)i, e, [&](int k) { return (const FrB*)F(p->ev[k][c]); }, F(p->tw0), F(p->out[c]),
                         true);
                     plk::numerator(NP, q);
@@ -843,7 +883,7 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
             for (int j = 0; j < n_cmt; j++) coset_eval(pk, F(pk->pi_brev[j]), F(e[7 + j]), (int)i, q);
             FrB* ep[7 + plk::MAX_CMT] = {};
             for (int k = 0; k < 7 + n_cmt; k++) ep[k] = F(e[k]);
-            plk::NumParams NP = coset_params(
+            plk::NumParamsT<FrB> NP = coset_params(
                 i, ep, [&](int k) { return (const FrB*)F(pk->ev[k][i]); }, F(pk->tw0), F(pk->cres), false);
             plk::numerator(NP, q);
         }
@@ -901,8 +941,8 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
     for (int k = 0; k < 3; k++) blinded(pk->can[k], bp[k], pk->bl[k], s[1]);
     FrB lz[3];
     for (int k = 0; k < 3; k++) lz[k] = eval_dev(pk, F(pk->bl[k]), n + 2, zeta, nullptr, F(pk->vals) + 1 + k, 1, s[1]);
-    const FrB s1z = eval_dev(pk, F(pk->reg[gg_plonk_pk::S1]), n, zeta, nullptr, F(pk->vals) + 4, 1, s[1]);
-    const FrB s2z = eval_dev(pk, F(pk->reg[gg_plonk_pk::S2]), n, zeta, nullptr, F(pk->vals) + 5, 1, s[1]);
+    const FrB s1z = eval_dev(pk, F(pk->reg[Key::S1]), n, zeta, nullptr, F(pk->vals) + 4, 1, s[1]);
+    const FrB s2z = eval_dev(pk, F(pk->reg[Key::S2]), n, zeta, nullptr, F(pk->vals) + 5, 1, s[1]);
     std::vector<FrB> qcpz(n_cmt);
     for (int j = 0; j < n_cmt; j++) qcpz[j] = eval_dev(pk, F(pk->qcp_reg[j]), n, zeta, nullptr, F(pk->vals) + 6 + j, 1, s[1]);
     // ---- computeLinearizedPolynomial (prove.go:1289-1389) on s[1]
@@ -914,16 +954,16 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
         sb = -sb;
         const FrB lag = zn1 * inverse(zeta - FrB::one()) * alpha * alpha * pk->n_inv;
         dcopy(pk->lin.p, pk->bz.p, nb3, s[1]);  // bz is complete: openZ's Horner synchronised s[0]
-        plk::LinParams LP{};
+        plk::LinParamsT<FrB> LP{};
         LP.z = F(pk->lin);
         LP.nz = n + 3;
-        LP.s3 = F(pk->reg[gg_plonk_pk::S3]);
+        LP.s3 = F(pk->reg[Key::S3]);
         LP.ns3 = n;
-        LP.ql = F(pk->reg[gg_plonk_pk::QL]);
-        LP.qr = F(pk->reg[gg_plonk_pk::QR]);
-        LP.qm = F(pk->reg[gg_plonk_pk::QM]);
-        LP.qo = F(pk->reg[gg_plonk_pk::QO]);
-        LP.qk = F(pk->reg[gg_plonk_pk::QK]);
+        LP.ql = F(pk->reg[Key::QL]);
+        LP.qr = F(pk->reg[Key::QR]);
+        LP.qm = F(pk->reg[Key::QM]);
+        LP.qo = F(pk->reg[Key::QO]);
+        LP.qk = F(pk->reg[Key::QK]);
         LP.nq = n;
         LP.ncmt = n_cmt;
         for (int j = 0; j < n_cmt; j++) {
@@ -947,7 +987,7 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
     GG_HIP(hipStreamSynchronize(s[2]));  // folded H
     std::vector<std::pair<const FrB*, size_t>> polys = {
         {F(pk->fold), n + 2}, {F(pk->lin), n + 3}, {F(pk->bl[0]), n + 2}, {F(pk->bl[1]), n + 2},
-        {F(pk->bl[2]), n + 2}, {F(pk->reg[gg_plonk_pk::S1]), n}, {F(pk->reg[gg_plonk_pk::S2]), n}};
+        {F(pk->bl[2]), n + 2}, {F(pk->reg[Key::S1]), n}, {F(pk->reg[Key::S2]), n}};
     for (int j = 0; j < n_cmt; j++) polys.push_back({F(pk->qcp_reg[j]), n});
     std::vector<BAff> digests = {folded_digest, lin_digest, P.lro[0], P.lro[1], P.lro[2], pk->vkS[0], pk->vkS[1]};
     for (int j = 0; j < n_cmt; j++) digests.push_back(pk->vkQcp[j]);
@@ -965,7 +1005,7 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
         uint8_t b[96];
         fr_marshal(zeta, b);
         fg.bind("gamma", b, 32);
-        for (auto& d : digests) { g1_raw_bytes(d, b); fg.bind("gamma", b, 96); }
+        for (auto& d : digests) { g1_raw_bytes(d, b); fg.bind("gamma", b, PT); }
         for (auto& c : P.claimed) { fr_marshal(c, b); fg.bind("gamma", b, 32); }
         fr_marshal(zu, b);
         fg.bind("gamma", b, 32);
@@ -990,11 +1030,70 @@ void prove(gg_plonk_pk* pk, const void* const lro_in[3], bool on_dev, const FrB*
     for (hipStream_t q : pk->s) GG_HIP(hipStreamSynchronize(q));
 }
 
-}  // namespace
+};
 
 // ============================================================== C ABI
 // cumulative stage ends (ms) of the last gg_plonk_prove on this thread
 static thread_local double g_plonk_ms[8];
+
+namespace {
+
+template <class Cv>
+gg_plonk_pk* plonk_create(int log_n, int log_big, const void* omega, const void* omega_big, const void* coset_shift,
+                          const void* kzg_g1, size_t n_kzg, const void* kzg_lagrange_g1, const void* const* trace,
+                          const void* const* qcp, int n_cmt, const int64_t* perm, size_t nb_public,
+                          const uint64_t* cmt_idx, const void* vk_digests, int rank, int world, gg_g1_reduce_fn reduce,
+                          void* rctx, const int* devices, int n_devices) {
+    using Impl = PlonkImpl<Cv>;
+    std::unique_ptr<typename Impl::Key> pk(new typename Impl::Key());
+    Impl::plonk_pk_build(pk.get(), log_n, log_big, omega, omega_big, coset_shift, kzg_g1, n_kzg, kzg_lagrange_g1,
+                         trace, qcp, n_cmt, perm, nb_public, cmt_idx, vk_digests, rank, world, reduce, rctx, devices,
+                         n_devices);
+    return pk.release();
+}
+
+gg_plonk_pk* create_any(int curve, int log_n, int log_big, const void* omega, const void* omega_big,
+                        const void* coset_shift, const void* kzg_g1, size_t n_kzg, const void* kzg_lagrange_g1,
+                        const void* const* trace, const void* const* qcp, int n_cmt, const int64_t* perm,
+                        size_t nb_public, const uint64_t* cmt_idx, const void* vk_digests, int rank, int world,
+                        gg_g1_reduce_fn reduce, void* rctx, const int* devices, int n_devices) {
+    GG_CHECK(curve == GG_CURVE_BN254 || curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "bad curve");
+    if (curve == GG_CURVE_BN254)
+        return plonk_create<PlonkBn254>(log_n, log_big, omega, omega_big, coset_shift, kzg_g1, n_kzg,
+                                        kzg_lagrange_g1, trace, qcp, n_cmt, perm, nb_public, cmt_idx, vk_digests,
+                                        rank, world, reduce, rctx, devices, n_devices);
+    return plonk_create<PlonkBls12381>(log_n, log_big, omega, omega_big, coset_shift, kzg_g1, n_kzg,
+                                       kzg_lagrange_g1, trace, qcp, n_cmt, perm, nb_public, cmt_idx, vk_digests, rank,
+                                       world, reduce, rctx, devices, n_devices);
+}
+
+// fn(typed key) on the handle's curve
+template <class Fn>
+auto with_key(gg_plonk_pk* pk, Fn fn) {
+    if (pk->curve == GG_CURVE_BN254) return fn(static_cast<typename PlonkImpl<PlonkBn254>::Key*>(pk));
+    return fn(static_cast<typename PlonkImpl<PlonkBls12381>::Key*>(pk));
+}
+
+size_t proof_size(int curve, int n_cmt) {
+    const size_t pt = curve == GG_CURVE_BN254 ? 64 : 96;
+    return pt * (3 + 1 + 3 + (size_t)n_cmt + 1 + 1) + 32 * (7 + (size_t)n_cmt) + 32;
+}
+
+}  // namespace
+
+extern "C" int gg_plonk_pk_create_ex(int curve, int log_n, int log_big, const void* omega_mont,
+                                     const void* omega_big_mont, const void* coset_shift_mont, const void* kzg_g1,
+                                     size_t n_kzg, const void* kzg_lagrange_g1, const void* const* trace,
+                                     const void* const* qcp, int n_cmt, const int64_t* perm, size_t nb_public,
+                                     const uint64_t* commitment_constraint_indexes, const void* vk_digests,
+                                     int n_devices, const int* devices, gg_plonk_pk_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out && (n_devices <= 1 || devices), GG_ERR_INVALID_ARG, "null argument");
+    *out = create_any(curve, log_n, log_big, omega_mont, omega_big_mont, coset_shift_mont, kzg_g1, n_kzg,
+                      kzg_lagrange_g1, trace, qcp, n_cmt, perm, nb_public, commitment_constraint_indexes, vk_digests,
+                      0, 1, nullptr, nullptr, n_devices > 1 ? devices : nullptr, n_devices > 1 ? n_devices : 1);
+    GG_CAPI_END
+}
 
 extern "C" int gg_plonk_pk_create(int log_n, int log_big, const void* omega_mont, const void* omega_big_mont,
                                   const void* coset_shift_mont, const void* kzg_g1, size_t n_kzg,
@@ -1002,13 +1101,24 @@ extern "C" int gg_plonk_pk_create(int log_n, int log_big, const void* omega_mont
                                   int n_cmt, const int64_t* perm, size_t nb_public,
                                   const uint64_t* commitment_constraint_indexes, const void* vk_digests,
                                   gg_plonk_pk_t* out) {
+    return gg_plonk_pk_create_ex(GG_CURVE_BLS12_381, log_n, log_big, omega_mont, omega_big_mont, coset_shift_mont,
+                                 kzg_g1, n_kzg, kzg_lagrange_g1, trace, qcp, n_cmt, perm, nb_public,
+                                 commitment_constraint_indexes, vk_digests, 1, nullptr, out);
+}
+
+extern "C" int gg_plonk_pk_create_shard_ex(int curve, int log_n, int log_big, const void* omega_mont,
+                                           const void* omega_big_mont, const void* coset_shift_mont,
+                                           const void* kzg_g1, size_t n_kzg, const void* kzg_lagrange_g1,
+                                           const void* const* trace, const void* const* qcp, int n_cmt,
+                                           const int64_t* perm, size_t nb_public,
+                                           const uint64_t* commitment_constraint_indexes, const void* vk_digests,
+                                           int rank, int world, gg_g1_reduce_fn reduce, void* reduce_ctx,
+                                           gg_plonk_pk_t* out) {
     GG_CAPI_BEGIN
     GG_CHECK(out, GG_ERR_INVALID_ARG, "null out");
-    std::unique_ptr<gg_plonk_pk> pk(new gg_plonk_pk());
-    plonk_pk_build(pk.get(), log_n, log_big, omega_mont, omega_big_mont, coset_shift_mont, kzg_g1, n_kzg,
-                   kzg_lagrange_g1, trace, qcp, n_cmt, perm, nb_public, commitment_constraint_indexes,
-                   vk_digests, 0, 1, nullptr, nullptr);
-    *out = pk.release();
+    *out = create_any(curve, log_n, log_big, omega_mont, omega_big_mont, coset_shift_mont, kzg_g1, n_kzg,
+                      kzg_lagrange_g1, trace, qcp, n_cmt, perm, nb_public, commitment_constraint_indexes, vk_digests,
+                      rank, world, reduce, reduce_ctx, nullptr, 1);
     GG_CAPI_END
 }
 
@@ -1019,14 +1129,10 @@ extern "C" int gg_plonk_pk_create_shard(int log_n, int log_big, const void* omeg
                                         const uint64_t* commitment_constraint_indexes, const void* vk_digests,
                                         int rank, int world, gg_g1_reduce_fn reduce, void* reduce_ctx,
                                         gg_plonk_pk_t* out) {
-    GG_CAPI_BEGIN
-    GG_CHECK(out, GG_ERR_INVALID_ARG, "null out");
-    std::unique_ptr<gg_plonk_pk> pk(new gg_plonk_pk());
-    plonk_pk_build(pk.get(), log_n, log_big, omega_mont, omega_big_mont, coset_shift_mont, kzg_g1, n_kzg,
-                   kzg_lagrange_g1, trace, qcp, n_cmt, perm, nb_public, commitment_constraint_indexes,
-                   vk_digests, rank, world, reduce, reduce_ctx);
-    *out = pk.release();
-    GG_CAPI_END
+    return gg_plonk_pk_create_shard_ex(GG_CURVE_BLS12_381, log_n, log_big, omega_mont, omega_big_mont,
+                                       coset_shift_mont, kzg_g1, n_kzg, kzg_lagrange_g1, trace, qcp, n_cmt, perm,
+                                       nb_public, commitment_constraint_indexes, vk_digests, rank, world, reduce,
+                                       reduce_ctx, out);
 }
 
 extern "C" int gg_plonk_pk_create_multi(int log_n, int log_big, const void* omega_mont, const void* omega_big_mont,
@@ -1037,23 +1143,36 @@ extern "C" int gg_plonk_pk_create_multi(int log_n, int log_big, const void* omeg
                                         int n_devices, const int* devices, gg_plonk_pk_t* out) {
     GG_CAPI_BEGIN
     GG_CHECK(out && devices, GG_ERR_INVALID_ARG, "null argument");
-    std::unique_ptr<gg_plonk_pk> pk(new gg_plonk_pk());
-    plonk_pk_build(pk.get(), log_n, log_big, omega_mont, omega_big_mont, coset_shift_mont, kzg_g1, n_kzg,
-                   kzg_lagrange_g1, trace, qcp, n_cmt, perm, nb_public, commitment_constraint_indexes,
-                   vk_digests, 0, 1, nullptr, nullptr, devices, n_devices);
-    *out = pk.release();
+    *out = create_any(GG_CURVE_BLS12_381, log_n, log_big, omega_mont, omega_big_mont, coset_shift_mont, kzg_g1,
+                      n_kzg, kzg_lagrange_g1, trace, qcp, n_cmt, perm, nb_public, commitment_constraint_indexes,
+                      vk_digests, 0, 1, nullptr, nullptr, devices, n_devices);
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_pk_info(gg_plonk_pk_t pk, int* curve, int* log_n, int* n_cmt) {
+    GG_CAPI_BEGIN
+    GG_CHECK(pk, GG_ERR_INVALID_ARG, "null key");
+    with_key(pk, [&](auto* k) {
+        if (curve) *curve = k->curve;
+        if (log_n) *log_n = k->log_n;
+        if (n_cmt) *n_cmt = k->n_cmt;
+        return 0;
+    });
     GG_CAPI_END
 }
 
 extern "C" int gg_plonk_pk_devices(gg_plonk_pk_t pk, int* devices, int cap, int* n_devices) {
     GG_CAPI_BEGIN
     GG_CHECK(pk && n_devices, GG_ERR_INVALID_ARG, "null argument");
-    *n_devices = 1 + (int)pk->peers.size();
-    GG_CHECK(!devices || cap >= *n_devices, GG_ERR_INVALID_ARG, "cap < number of device parts");
-    if (devices) {
-        devices[0] = pk->device;
-        for (size_t i = 0; i < pk->peers.size(); i++) devices[1 + i] = pk->peers[i]->device;
-    }
+    with_key(pk, [&](auto* k) {
+        *n_devices = 1 + (int)k->peers.size();
+        GG_CHECK(!devices || cap >= *n_devices, GG_ERR_INVALID_ARG, "cap < number of device parts");
+        if (devices) {
+            devices[0] = k->device;
+            for (size_t i = 0; i < k->peers.size(); i++) devices[1 + i] = k->peers[i]->device;
+        }
+        return 0;
+    });
     GG_CAPI_END
 }
 
@@ -1066,28 +1185,37 @@ extern "C" int gg_plonk_pk_release(gg_plonk_pk_t pk) {
 extern "C" int gg_plonk_pk_vk(gg_plonk_pk_t pk, void* out, size_t cap) {
     GG_CAPI_BEGIN
     GG_CHECK(pk && out, GG_ERR_INVALID_ARG, "null argument");
-    GG_CHECK(cap >= 96 * (size_t)(8 + pk->n_cmt), GG_ERR_INVALID_ARG, "vk buffer too small");
-    uint8_t* o = (uint8_t*)out;
-    for (int k = 0; k < 3; k++) memcpy(o + 96 * k, &pk->vkS[k], 96);
-    for (int k = 0; k < 5; k++) memcpy(o + 96 * (3 + k), &pk->vkQ[k], 96);
-    for (int i = 0; i < pk->n_cmt; i++) memcpy(o + 96 * (8 + i), &pk->vkQcp[i], 96);
+    with_key(pk, [&](auto* k) {
+        const size_t pt = sizeof(k->vkS[0]);
+        GG_CHECK(cap >= pt * (size_t)(8 + k->n_cmt), GG_ERR_INVALID_ARG, "vk buffer too small");
+        uint8_t* o = (uint8_t*)out;
+        for (int j = 0; j < 3; j++) memcpy(o + pt * j, &k->vkS[j], pt);
+        for (int j = 0; j < 5; j++) memcpy(o + pt * (3 + j), &k->vkQ[j], pt);
+        for (int i = 0; i < k->n_cmt; i++) memcpy(o + pt * (8 + i), &k->vkQcp[i], pt);
+        return 0;
+    });
     GG_CAPI_END
 }
 
 extern "C" int gg_plonk_commit_lagrange(gg_plonk_pk_t pk, const void* values, int on_device, void* out_aff) {
     GG_CAPI_BEGIN
     GG_CHECK(pk && values && out_aff, GG_ERR_INVALID_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(pk->mu);
-    hipStream_t st = pk->s[3];
-    up(pk->pad.p, values, 32 * pk->n, on_device != 0, st);
-    BAff a = to_aff(red(pk, msm_jac(pk, pk->kzg_lag, 2, F(pk->pad), st)));
-    memcpy(out_aff, &a, 96);
+    with_key(pk, [&](auto* k) {
+        using Impl = PlonkImpl<typename std::remove_pointer<decltype(k)>::type::CvT>;
+        std::lock_guard<std::mutex> lk(k->mu);
+        GG_HIP(hipSetDevice(k->device));
+        hipStream_t st = k->s[3];
+        Impl::up(k->pad.p, values, 32 * k->n, on_device != 0, st);
+        const auto a = Impl::to_aff(Impl::red(k, Impl::msm_jac(k, k->kzg_lag, 2, Impl::F(k->pad), st)));
+        memcpy(out_aff, &a, sizeof(a));
+        return 0;
+    });
     GG_CAPI_END
 }
 
-extern "C" size_t gg_plonk_proof_size(int n_cmt) {
-    return 96 * (3 + 1 + 3 + (size_t)n_cmt + 1 + 1) + 32 * (7 + (size_t)n_cmt) + 32;
-}
+extern "C" size_t gg_plonk_proof_size(int n_cmt) { return proof_size(GG_CURVE_BLS12_381, n_cmt); }
+
+extern "C" size_t gg_plonk_proof_size_ex(int curve, int n_cmt) { return proof_size(curve, n_cmt); }
 
 extern "C" int gg_plonk_prove(gg_plonk_pk_t pk, const void* l, const void* r, const void* o, int inputs_on_device,
                               const void* public_witness, size_t nb_public, const void* const* cmt_values,
@@ -1096,43 +1224,50 @@ extern "C" int gg_plonk_prove(gg_plonk_pk_t pk, const void* l, const void* r, co
                               void* folding_ctx, void* proof_out, size_t proof_cap) {
     GG_CAPI_BEGIN
     GG_CHECK(pk && l && r && o && proof_out, GG_ERR_INVALID_ARG, "null argument");
-    GG_CHECK(nb_public == pk->nb_public, GG_ERR_INVALID_ARG, "len(public witness) != vk.NbPublicVariables");
-    GG_CHECK(nb_public == 0 || public_witness, GG_ERR_INVALID_ARG, "null public witness");
-    GG_CHECK(n_cmt == pk->n_cmt, GG_ERR_INVALID_ARG, "BSB22 commitment count differs from the key's");
-    GG_CHECK(n_cmt == 0 || (cmt_values && cmt_digests && cmt_hashed), GG_ERR_INVALID_ARG,
-             "null BSB22 commitment data");
-    GG_CHECK(proof_cap >= gg_plonk_proof_size(n_cmt), GG_ERR_INVALID_ARG, "proof buffer too small");
-    std::lock_guard<std::mutex> lk(pk->mu);
-    GG_HIP(hipSetDevice(pk->device));
-    std::vector<FrB> pub(nb_public), hashed(n_cmt), blind;
-    if (nb_public) memcpy(pub.data(), public_witness, 32 * nb_public);
-    if (n_cmt) memcpy(hashed.data(), cmt_hashed, 32 * (size_t)n_cmt);
-    std::vector<BAff> dg(n_cmt);
-    if (n_cmt) memcpy(dg.data(), cmt_digests, 96 * (size_t)n_cmt);
-    if (blinding) {
-        blind.resize(9);
-        memcpy(blind.data(), blinding, 9 * 32);
-    }
-    const void* lro[3] = {l, r, o};
-    PlonkProof P;
-    double tms[8] = {0};
-    prove(pk, lro, inputs_on_device != 0, pub.data(), nb_public, cmt_values, dg.data(), hashed.data(), n_cmt,
-          blinding ? blind.data() : nullptr, Hasher{challenge_hash, challenge_ctx},
-          Hasher{folding_hash, folding_ctx}, P, tms);
-    uint8_t* w = (uint8_t*)proof_out;
-    auto put = [&](const void* src, size_t b) {
-        memcpy(w, src, b);
-        w += b;
-    };
-    for (auto& p : P.lro) put(&p, 96);
-    put(&P.z, 96);
-    for (auto& p : P.h) put(&p, 96);
-    for (auto& p : P.bsb22) put(&p, 96);
-    put(&P.batched_h, 96);
-    for (auto& c : P.claimed) put(c.v, 32);
-    put(&P.zs_h, 96);
-    put(P.zs_value.v, 32);
-    memcpy(g_plonk_ms, tms, sizeof(tms));
+    with_key(pk, [&](auto* k) {
+        using Impl = PlonkImpl<typename std::remove_pointer<decltype(k)>::type::CvT>;
+        using FrT = typename Impl::FrB;
+        using AffT = typename Impl::BAff;
+        const size_t pt = sizeof(AffT);
+        GG_CHECK(nb_public == k->nb_public, GG_ERR_INVALID_ARG, "len(public witness) != vk.NbPublicVariables");
+        GG_CHECK(nb_public == 0 || public_witness, GG_ERR_INVALID_ARG, "null public witness");
+        GG_CHECK(n_cmt == k->n_cmt, GG_ERR_INVALID_ARG, "BSB22 commitment count differs from the key's");
+        GG_CHECK(n_cmt == 0 || (cmt_values && cmt_digests && cmt_hashed), GG_ERR_INVALID_ARG,
+                 "null BSB22 commitment data");
+        GG_CHECK(proof_cap >= proof_size(k->curve, n_cmt), GG_ERR_INVALID_ARG, "proof buffer too small");
+        std::lock_guard<std::mutex> lk(k->mu);
+        GG_HIP(hipSetDevice(k->device));
+        std::vector<FrT> pub(nb_public), hashed(n_cmt), blind;
+        if (nb_public) memcpy(pub.data(), public_witness, 32 * nb_public);
+        if (n_cmt) memcpy(hashed.data(), cmt_hashed, 32 * (size_t)n_cmt);
+        std::vector<AffT> dg(n_cmt);
+        if (n_cmt) memcpy(dg.data(), cmt_digests, pt * (size_t)n_cmt);
+        if (blinding) {
+            blind.resize(9);
+            memcpy(blind.data(), blinding, 9 * 32);
+        }
+        const void* lro[3] = {l, r, o};
+        typename Impl::PlonkProof P;
+        double tms[8] = {0};
+        Impl::prove(k, lro, inputs_on_device != 0, pub.data(), nb_public, cmt_values, dg.data(), hashed.data(), n_cmt,
+                    blinding ? blind.data() : nullptr, Hasher{challenge_hash, challenge_ctx},
+                    Hasher{folding_hash, folding_ctx}, P, tms);
+        uint8_t* w = (uint8_t*)proof_out;
+        auto put = [&](const void* src, size_t b) {
+            memcpy(w, src, b);
+            w += b;
+        };
+        for (auto& p : P.lro) put(&p, pt);
+        put(&P.z, pt);
+        for (auto& p : P.h) put(&p, pt);
+        for (auto& p : P.bsb22) put(&p, pt);
+        put(&P.batched_h, pt);
+        for (auto& c : P.claimed) put(c.v, 32);
+        put(&P.zs_h, pt);
+        put(P.zs_value.v, 32);
+        memcpy(g_plonk_ms, tms, sizeof(tms));
+        return 0;
+    });
     GG_CAPI_END
 }
 

@@ -126,6 +126,13 @@ def _load():
         "gg_plonk_pk_create_multi": ([I, I, P, P, P, P, S, P, PP, PP, I, P, S, P, P, I,
                                       ctypes.POINTER(ctypes.c_int), PP], I),
         "gg_plonk_pk_devices": ([P, ctypes.POINTER(ctypes.c_int), I, ctypes.POINTER(ctypes.c_int)], I),
+        "gg_plonk_pk_create_ex": ([I, I, I, P, P, P, P, S, P, PP, PP, I, P, S, P, P, I,
+                                   ctypes.POINTER(ctypes.c_int), PP], I),
+        "gg_plonk_pk_create_shard_ex": ([I, I, I, P, P, P, P, S, P, PP, PP, I, P, S, P, P, I, I, REDUCE_FN, P,
+                                         PP], I),
+        "gg_plonk_pk_info": ([P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                              ctypes.POINTER(ctypes.c_int)], I),
+        "gg_plonk_proof_size_ex": ([I, I], S),
         "gg_plonk_pk_release": ([P], I),
         "gg_plonk_pk_vk": ([P, P, S], I),
         "gg_plonk_commit_lagrange": ([P, P, I, P], I),
@@ -175,6 +182,7 @@ EXPORTED = [
     "gg_bls12_381_fr_axpy", "gg_bls12_381_g1_scalar_mul", "gg_fr_from_canonical_be",
     "gg_fr_to_canonical_be", "gg_groth16_last_timings_ex",
     "gg_groth16_pk_base_info", "gg_plonk_pk_create", "gg_plonk_pk_create_shard", "gg_plonk_pk_release", "gg_plonk_pk_create_multi", "gg_plonk_pk_devices",
+    "gg_plonk_pk_create_ex", "gg_plonk_pk_create_shard_ex", "gg_plonk_pk_info", "gg_plonk_proof_size_ex",
     "gg_plonk_pk_vk", "gg_plonk_commit_lagrange", "gg_plonk_proof_size", "gg_plonk_prove",
     "gg_plonk_last_timings", "gg_groth16_pk_create_ex", "gg_groth16_finalize_ex",
     "gg_bls12_381_g2_jac_to_affine", "gg_bls12_381_g2_jac_add", "gg_bls12_381_g2_scalar_mul",

@@ -30,6 +30,26 @@ from ._lib import DeviceBuffer, check, lib, ptr, GG_CURVE_BLS12_381, HASH_FN, RE
 R = fr.BLS_R
 ORDER_BLINDING = (1, 1, 1, 2)  # order_blinding_L, _R, _O, _Z (prove.go:88-93)
 
+
+class _Field:
+    """The scalar field and G1 point size of a PlonK curve (backend/plonk/bls12-381,
+    backend/plonk/bn254)."""
+
+    def __init__(self, curve):
+        from ._lib import GG_CURVE_BN254
+        self.curve = curve
+        if curve == "bn254":
+            self.cid, self.R, self.pt = GG_CURVE_BN254, fr.R, 64
+            self.mont, self.unmont = fr.fr_mont, fr.fr_unmont
+            self.gen, self.domain_generator = fr.FR_MULTIPLICATIVE_GEN, fr.domain_generator
+        elif curve == "bls12-381":
+            self.cid, self.R, self.pt = GG_CURVE_BLS12_381, fr.BLS_R, 96
+            self.mont, self.unmont = fr.bls_fr_mont, fr.bls_fr_unmont
+            self.gen, self.domain_generator = fr.BLS_FR_MULTIPLICATIVE_GEN, fr.bls_domain_generator
+        else:
+            raise ValueError("curve must be 'bls12-381' or 'bn254'")
+
+
 def fr_int(b: bytes) -> int:
     return fr.bls_fr_unmont(b)
 
@@ -77,21 +97,23 @@ class Proof:
     z_shifted_value: int
 
     @classmethod
-    def parse(cls, b: bytes, n_cmt: int) -> "Proof":
+    def parse(cls, b: bytes, n_cmt: int, curve: str = "bls12-381") -> "Proof":
         o = 0
+        F = _Field(curve)
 
         def take(k):
             nonlocal o
             o += k
             return b[o - k:o]
-        lro = [take(96) for _ in range(3)]
-        z = take(96)
-        h = [take(96) for _ in range(3)]
-        bsb = [take(96) for _ in range(n_cmt)]
-        bh = take(96)
-        cv = [fr_int(take(32)) for _ in range(7 + n_cmt)]
-        zh = take(96)
-        zv = fr_int(take(32))
+        pt = F.pt
+        lro = [take(pt) for _ in range(3)]
+        z = take(pt)
+        h = [take(pt) for _ in range(3)]
+        bsb = [take(pt) for _ in range(n_cmt)]
+        bh = take(pt)
+        cv = [F.unmont(take(32)) for _ in range(7 + n_cmt)]
+        zh = take(pt)
+        zv = F.unmont(take(32))
         return cls(lro, z, h, bsb, bh, cv, zh, zv)
 
 
@@ -133,19 +155,23 @@ class ProvingKey:
     def __init__(self, log_n: int, kzg_g1, kzg_lagrange_g1, ql, qr, qm, qo, qk, s1, s2, s3, perm,
                  qcp: Sequence = (), nb_public: int = 0, commitment_indexes: Sequence[int] = (),
                  basis: str = "lagrange", big_log: Optional[int] = None, shard=None, reduce=None,
-                 vk: Optional[VerifyingKey] = None, devices: Optional[Sequence[int]] = None):
+                 vk: Optional[VerifyingKey] = None, devices: Optional[Sequence[int]] = None,
+                 curve: str = "bls12-381"):
+        F = self.field = _Field(curve)
+        self.curve = curve
+        mont = F.mont
         self.log_n = log_n
         self.n = n = 1 << log_n
         self.big_log = big_log if big_log is not None else log_n + (2 if n >= 6 else 3)
-        self.omega = fr.bls_domain_generator(log_n)
-        self.omega_big = fr.bls_domain_generator(self.big_log)
-        self.g = fr.BLS_FR_MULTIPLICATIVE_GEN
+        self.omega = F.domain_generator(log_n)
+        self.omega_big = F.domain_generator(self.big_log)
+        self.g = F.gen
         self.n_cmt = len(qcp)
         self.nb_public = nb_public
         nb = 32 * n
         polys = [ql, qr, qm, qo, qk, s1, s2, s3] + list(qcp)
         if basis == "lagrange":
-            d0 = ntt.Domain(log_n, fr_b(self.omega), fr_b(self.g), curve=GG_CURVE_BLS12_381)
+            d0 = ntt.Domain(log_n, mont(self.omega), mont(self.g), curve=F.cid)
             canon = []
             for v in polys:
                 b = DeviceBuffer(nb)
@@ -155,6 +181,7 @@ class ProvingKey:
                     check(lib.gg_copy_to_device(ptr(b), ptr(v), nb))
                 d0.fft_inverse(b, ntt.DIF)  # Lagrange regular -> canonical bit-reversed
                 reg = DeviceBuffer(nb)
+                # a permutation of 32-B elements: the same kernel serves both scalar fields
                 check(lib.gg_bls12_381_fr_bit_reverse(ptr(b), ptr(reg), n, None))
                 canon.append(reg.to_host(nb))
             del d0
@@ -164,14 +191,14 @@ class ProvingKey:
         tr = (ctypes.c_void_p * 8)(*[ctypes.addressof(c) for c in keep[:8]])
         qa = (ctypes.c_void_p * max(1, self.n_cmt))(*[ctypes.addressof(c) for c in keep[8:]])
         idx = (ctypes.c_uint64 * max(1, self.n_cmt))(*commitment_indexes)
-        kz = _host(kzg_g1, 96 * (n + 3))
-        kl = _host(kzg_lagrange_g1, 96 * n)
+        kz = _host(kzg_g1, F.pt * (n + 3))
+        kl = _host(kzg_lagrange_g1, F.pt * n)
         pm = _host(perm, 24 * n)
         vkd = None
         if vk is not None:
             vkd = b"".join(vk.S + [vk.Ql, vk.Qr, vk.Qm, vk.Qo, vk.Qk] + list(vk.Qcp))
         h = ctypes.c_void_p()
-        args = (log_n, self.big_log, fr_b(self.omega), fr_b(self.omega_big), fr_b(self.g), kz, n + 3, kl, tr,
+        args = (F.cid, log_n, self.big_log, mont(self.omega), mont(self.omega_big), mont(self.g), kz, n + 3, kl, tr,
                 qa, self.n_cmt, pm, nb_public, idx, vkd)
         self._reduce_cb = None
         if shard is not None and shard[1] > 1:
@@ -185,17 +212,17 @@ class ProvingKey:
                 except Exception:  # pragma: no cover - surfaced as GG_ERR_DEVICE
                     return 1
             self._reduce_cb = REDUCE_FN(cb)
-            check(lib.gg_plonk_pk_create_shard(*args, rank, world, self._reduce_cb, None, ctypes.byref(h)))
-        elif devices is not None and len(devices) > 1:
-            devs = (ctypes.c_int * len(devices))(*devices)
-            check(lib.gg_plonk_pk_create_multi(*args, len(devices), devs, ctypes.byref(h)))
+            check(lib.gg_plonk_pk_create_shard_ex(*args, rank, world, self._reduce_cb, None, ctypes.byref(h)))
         else:
-            check(lib.gg_plonk_pk_create(*args, ctypes.byref(h)))
+            devs = list(devices) if devices is not None and len(devices) > 1 else []
+            check(lib.gg_plonk_pk_create_ex(*args, len(devs), (ctypes.c_int * max(1, len(devs)))(*devs),
+                                            ctypes.byref(h)))
         self.handle = h
         del keep
-        out = bytearray(96 * (8 + self.n_cmt))
+        pt = F.pt
+        out = bytearray(pt * (8 + self.n_cmt))
         check(lib.gg_plonk_pk_vk(h, ptr(out), len(out)))
-        d = [bytes(out[96 * i:96 * (i + 1)]) for i in range(8 + self.n_cmt)]
+        d = [bytes(out[pt * i:pt * (i + 1)]) for i in range(8 + self.n_cmt)]
         self.vk = VerifyingKey(n, self.omega, self.g, d[0:3], d[3], d[4], d[5], d[6], d[7], d[8:], nb_public,
                                list(commitment_indexes))
 
@@ -209,7 +236,7 @@ class ProvingKey:
 
     def commit_lagrange(self, values) -> bytes:
         """kzg.Commit(values, pk.KzgLagrange) -- the commitment of bsb22Hint (prove.go:336)."""
-        out = bytearray(96)
+        out = bytearray(self.field.pt)
         on_dev = isinstance(values, DeviceBuffer)
         check(lib.gg_plonk_commit_lagrange(self.handle, ptr(values), int(on_dev), ptr(out)))
         return bytes(out)
@@ -236,17 +263,18 @@ def prove(pk: ProvingKey, L, R_, O, rng=None, timings: Optional[dict] = None, pu
     blinding coefficients' source (random.Random for reproducible proofs, default
     secrets); challenge_hash / folding_hash: hashlib constructors (default SHA-256)."""
     assert len(public) == pk.nb_public and len(commitments) == pk.n_cmt
+    F = pk.field
     rnd = rng or secrets.SystemRandom()
-    blind = b"".join(fr_b(rnd.randrange(R)) for o in ORDER_BLINDING for _ in range(o + 1))
+    blind = b"".join(F.mont(rnd.randrange(F.R)) for o in ORDER_BLINDING for _ in range(o + 1))
     on_dev = isinstance(L, DeviceBuffer)
     nb = 32 * pk.n
     lro = [x if on_dev else _host(x, nb) for x in (L, R_, O)]
-    pub = b"".join(fr_b(v) for v in public)
+    pub = b"".join(F.mont(v % F.R) for v in public)
     cv = [ctypes.create_string_buffer(_host(c[0], nb), nb) for c in commitments]  # alive for the call
     cva = (ctypes.c_void_p * max(1, len(cv)))(*[ctypes.addressof(c) for c in cv])
     dig = b"".join(c[1] for c in commitments)
-    hashed = b"".join(fr_b(c[2]) for c in commitments)
-    size = lib.gg_plonk_proof_size(pk.n_cmt)
+    hashed = b"".join(F.mont(c[2] % F.R) for c in commitments)
+    size = lib.gg_plonk_proof_size_ex(F.cid, pk.n_cmt)
     out = bytearray(size)
     hc, hf = _hash_cb(challenge_hash), _hash_cb(folding_hash)
     check(lib.gg_plonk_prove(pk.handle, ptr(lro[0]), ptr(lro[1]), ptr(lro[2]), int(on_dev), ptr(pub) if pub else None,
@@ -262,4 +290,4 @@ def prove(pk: ProvingKey, L, R_, O, rng=None, timings: Optional[dict] = None, pu
             timings[nm] = ms[k] - prev
             prev = ms[k]
         timings["total"] = prev
-    return Proof.parse(bytes(out), pk.n_cmt)
+    return Proof.parse(bytes(out), pk.n_cmt, pk.curve)

@@ -493,6 +493,27 @@ int gg_plonk_pk_create_multi(int log_n, int log_big, const void *omega_mont, con
                              int n_cmt, const int64_t *perm, size_t nb_public,
                              const uint64_t *commitment_constraint_indexes, const void *vk_digests,
                              int n_devices, const int *devices, gg_plonk_pk_t *out);
+/* The PlonK key of either curve (backend/plonk/bls12-381 or backend/plonk/bn254:
+ * the same prove.go over BN254, whose G1 affine points are 64 B and fr the BN254
+ * scalar field); every other argument as gg_plonk_pk_create, with
+ * n_devices / devices as gg_plonk_pk_create_multi (n_devices <= 1: one GPU, the
+ * calling thread's).  The handle works with every gg_plonk_* call below; point
+ * buffers (vk, commit_lagrange, proof) then hold the curve's point size. */
+int gg_plonk_pk_create_ex(int curve, int log_n, int log_big, const void *omega_mont, const void *omega_big_mont,
+                          const void *coset_shift_mont, const void *kzg_g1, size_t n_kzg,
+                          const void *kzg_lagrange_g1, const void *const *trace, const void *const *qcp,
+                          int n_cmt, const int64_t *perm, size_t nb_public,
+                          const uint64_t *commitment_constraint_indexes, const void *vk_digests,
+                          int n_devices, const int *devices, gg_plonk_pk_t *out);
+/* gg_plonk_pk_create_shard for either curve */
+int gg_plonk_pk_create_shard_ex(int curve, int log_n, int log_big, const void *omega_mont,
+                                const void *omega_big_mont, const void *coset_shift_mont, const void *kzg_g1,
+                                size_t n_kzg, const void *kzg_lagrange_g1, const void *const *trace,
+                                const void *const *qcp, int n_cmt, const int64_t *perm, size_t nb_public,
+                                const uint64_t *commitment_constraint_indexes, const void *vk_digests, int rank,
+                                int world, gg_g1_reduce_fn reduce, void *reduce_ctx, gg_plonk_pk_t *out);
+/* the key's curve, log2 of its domain and its number of BSB22 commitments */
+int gg_plonk_pk_info(gg_plonk_pk_t pk, int *curve, int *log_n, int *n_cmt);
 /* the key's device parts: *n_devices, devices[0..) (primary first; devices nullable) */
 int gg_plonk_pk_devices(gg_plonk_pk_t pk, int *devices, int cap, int *n_devices);
 /* the key's vk digests, 96-B affine each: S[0..2], Ql, Qr, Qm, Qo, Qk, Qcp[0..n_cmt) */
@@ -500,8 +521,10 @@ int gg_plonk_pk_vk(gg_plonk_pk_t pk, void *out, size_t cap);
 /* kzg.Commit(values, pk.KzgLagrange): n Lagrange values (host or device) -> affine 96 B.
  * The BSB22 solver hint (bsb22Hint, prove.go:316-352) commits through this. */
 int gg_plonk_commit_lagrange(gg_plonk_pk_t pk, const void *values, int on_device, void *out_aff);
-/* bytes of a proof with n_cmt BSB22 commitments (layout below) */
+/* bytes of a proof with n_cmt BSB22 commitments (layout below; BLS12-381 points) */
 size_t gg_plonk_proof_size(int n_cmt);
+/* the same for a curve (BN254: 64-B points) */
+size_t gg_plonk_proof_size_ex(int curve, int n_cmt);
 /* Prove after Solve (prove.go:116-176; the errgroup DAG as HIP streams):
  *   l, r, o: solution.L, R, O (n fr Lagrange regular, host or device);
  *   public_witness[nb_public]: fullWitness[:len(spr.Public)] (host, completeQk + bindPublicData);

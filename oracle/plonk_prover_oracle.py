@@ -342,3 +342,69 @@ def _div_x_minus_a(f, fa, a, R):
     for i in range(len(f) - 2, -1, -1):
         f[i] = (f[i] + f[i + 1] * a) % R
     return f[1:]
+
+
+# ---------------------------------------------------------------- verifier
+def verify_trapdoor(key, proof, public=(), challenge_hash=None, folding_hash=None):
+    """Verify (verify.go:45-290) over the key's curve with the SRS trapdoor tau in
+    place of the two pairings; the transcript as prove() (and solidity.go) binds it."""
+    cv = key["cv"]
+    R, n, u, w, tau, vk = cv.R, key["n"], key["u"], key["omega"], key["tau"], key["vk"]
+    bsb = proof["bsb22"]
+    if len(bsb) != len(vk["Qcp"]) or len(public) != key["nb_public"]:
+        return False
+    fs = Transcript(R, ("gamma", "beta", "alpha", "zeta"), challenge_hash)
+    for p in vk["S"] + [vk["Ql"], vk["Qr"], vk["Qm"], vk["Qo"], vk["Qk"]] + vk["Qcp"]:
+        fs.bind("gamma", cv.raw(p))
+    for x in public:
+        fs.bind("gamma", (x % R).to_bytes(32, "big"))
+    for p in proof["LRO"]:
+        fs.bind("gamma", cv.raw(p))
+    gamma, beta = fs.challenge("gamma"), fs.challenge("beta")
+    for p in bsb + [proof["Z"]]:
+        fs.bind("alpha", cv.raw(p))
+    alpha = fs.challenge("alpha")
+    for p in proof["H"]:
+        fs.bind("zeta", cv.raw(p))
+    zeta = fs.challenge("zeta")
+    zn1 = (pow(zeta, n, R) - 1) % R
+    lag1 = zn1 * pow(zeta - 1, -1, R) % R * pow(n, -1, R) % R
+    # PI(zeta) with the hashed BSB22 commitments at their rows (verify.go:102-155)
+    pi = 0
+    for i, x in enumerate(public):
+        wi = pow(w, i, R)
+        pi = (pi + wi * zn1 % R * pow(n * (zeta - wi), -1, R) * x) % R
+    for j, c in enumerate(bsb):
+        wi = pow(w, key["nb_public"] + key["cmt_idx"][j], R)
+        pi = (pi + wi * zn1 % R * pow(n * (zeta - wi), -1, R) * cv.hash_to_field(cv.raw(c))) % R
+    zu, cl = proof["zu"], proof["claimed"]
+    hq, lin, l, r, o, s1, s2 = cl[:7]
+    t = (s1 * beta + l + gamma) * (s2 * beta + r + gamma) % R * (o + gamma) % R * alpha % R * zu % R
+    if hq != (lin + pi + t - lag1 * alpha % R * alpha) % R * pow(zn1, -1, R) % R:
+        return False
+    zp = pow(zeta, n + 2, R)
+    fh = cv.add(cv.add(proof["H"][0], cv.mul(proof["H"][1], zp)), cv.mul(proof["H"][2], zp * zp % R))
+    a1 = zu * beta % R * ((beta * s1 + l + gamma) % R) % R * ((beta * s2 + r + gamma) % R) % R * alpha % R
+    a2 = (beta * zeta + l + gamma) * ((beta * zeta * u + r + gamma) % R) % R * ((beta * zeta * u * u + o + gamma) % R)
+    a2 = (-a2 * alpha + lag1 * alpha % R * alpha) % R
+    ld = cv.INF
+    for p, s in zip(bsb + [vk["Ql"], vk["Qr"], vk["Qm"], vk["Qo"], vk["Qk"], vk["S"][2], proof["Z"]],
+                    cl[7:] + [l, r, l * r % R, o, 1, a1, a2]):
+        ld = cv.add(ld, cv.mul(p, s))
+    digests = [fh, ld] + proof["LRO"] + [vk["S"][0], vk["S"][1]] + vk["Qcp"]
+    fk = Transcript(R, ("gamma",), folding_hash)
+    fk.bind("gamma", zeta.to_bytes(32, "big"))
+    for d in digests:
+        fk.bind("gamma", cv.raw(d))
+    for c in cl:
+        fk.bind("gamma", (c % R).to_bytes(32, "big"))
+    fk.bind("gamma", (zu % R).to_bytes(32, "big"))
+    gk = fk.challenge("gamma")
+    fd, fy, gp = cv.INF, 0, 1
+    for d, y in zip(digests, cl):
+        fd, fy, gp = cv.add(fd, cv.mul(d, gp)), (fy + gp * y) % R, gp * gk % R
+
+    def kzg_ok(digest, h, point, value):  # [w(tau)](tau - z) == C - [y]G
+        rhs = cv.add(digest, cv.mul(cv.G1, (-value) % R))
+        return cv.mul(h, (tau - point) % R) == rhs
+    return kzg_ok(fd, proof["batched_H"], zeta, fy) and kzg_ok(proof["Z"], proof["zs_H"], zeta * w % R, zu)

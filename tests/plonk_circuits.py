@@ -15,6 +15,7 @@ import random
 import numpy as np
 
 import bls12_381_oracle as bo
+import plonk_prover_oracle as po
 
 R = bo.R
 MONT = (1 << 256) % R
@@ -25,6 +26,26 @@ NEG_ONE_M = (R - 1) * MONT % R
 K_PUB, K_ADD, K_MUL, K_CMTD, K_CMT = 0, 1, 2, 3, 4
 
 
+class Field:
+    """Scalar field (Montgomery constants) and G1 encodings of a PlonK curve."""
+
+    def __init__(self, curve="bls12-381"):
+        self.curve = curve
+        self.cv = po.curve(curve)
+        self.R = R_ = self.cv.R
+        self.MONT = (1 << 256) % R_
+        self.MINV = pow(1 << 256, -1, R_)
+        self.ONE_M, self.NEG_ONE_M = self.MONT, (R_ - 1) * self.MONT % R_
+        if curve == "bls12-381":
+            self.g1_from_bytes, self.g1_to_bytes, self.pt = bo.g1_from_bytes, bo.g1_to_bytes, 96
+        else:
+            import bn254_oracle as bn
+            self.g1_from_bytes, self.g1_to_bytes, self.pt = bn.g1_from_bytes, bn.g1_to_bytes, 64
+
+
+FIELDS = {c: Field(c) for c in ("bls12-381", "bn254")}
+
+
 def m2b(v):  # Montgomery int -> 32 B
     return v.to_bytes(32, "little")
 
@@ -33,7 +54,9 @@ class Circuit:
     """Rows of a sparse R1CS over n = 2^log_n slots (no padding rows).  a/b/c:
     variable ids of the L/R/O slots (-1 = unused), kind: row type."""
 
-    def __init__(self, log_n, seed, nb_public=0, n_cmt=0, committed_per=3):
+    def __init__(self, log_n, seed, nb_public=0, n_cmt=0, committed_per=3, curve="bls12-381"):
+        self.F = FIELDS[curve]
+        self.curve = curve
         self.log_n, self.n = log_n, 1 << log_n
         n = self.n
         self.nb_public, self.n_cmt = nb_public, n_cmt
@@ -104,7 +127,7 @@ class Circuit:
     def selectors(self):
         """ql, qr, qm, qo, qk (incomplete) and qcp_j, Lagrange regular (bytes)."""
         n, k = self.n, self.kind
-        tab = np.array([[b for b in m2b(x)] for x in (0, ONE_M, NEG_ONE_M)], np.uint8)
+        tab = np.array([[b for b in m2b(x)] for x in (0, self.F.ONE_M, self.F.NEG_ONE_M)], np.uint8)
 
         def col(idx):
             return tab[idx].tobytes()
@@ -141,6 +164,7 @@ class Circuit:
         """S1, S2, S3 in Lagrange form: ID(perm[j n + i]), ID(s) = u^(s div n) w^(s mod n)
         (getSupportPermutation, setup.go:391-407), gathered from a 3n-entry table."""
         n = self.n
+        R, MONT = self.F.R, self.F.MONT
         tab = bytearray(32 * 3 * n)
         for blk, shift in enumerate((1, u, u * u % R)):
             x = shift * MONT % R
@@ -157,6 +181,8 @@ class Circuit:
         commitment data (values, digest, hashed) of each commitment, running the
         bsb22Hint through `commit` (kzg.Commit on pk.KzgLagrange)."""
         n = self.n
+        F = self.F
+        R, MONT, MINV = F.R, F.MONT, F.MINV
         rnd = random.Random(seed)
         hint_rng = hint_rng or random.Random(seed + 1)
         val = [None] * self.nvar
@@ -184,7 +210,7 @@ class Circuit:
                     vals[32 * rr:32 * rr + 32] = m2b(hint_rng.randrange(R))
                 dig = commit(bytes(vals))
                 # htfFunc.Write(commitment.Marshal()) (prove.go:341): the uncompressed encoding
-                hv = bo.hash_to_field(bo.g1_raw_bytes(bo.g1_from_bytes(dig)))
+                hv = F.cv.hash_to_field(F.cv.raw(F.g1_from_bytes(dig)))
                 val[a[r]] = hv * MONT % R
                 cmts.append((bytes(vals), dig, hv))
                 ci += 1
@@ -199,19 +225,22 @@ class Circuit:
         return bytes(L), bytes(Rv), bytes(O), public, cmts
 
 
-def srs(log_n, tau):
+def srs(log_n, tau, curve="bls12-381"):
     """pk.Kzg.G1[:n+3] = [tau^i]G and pk.KzgLagrange.G1 = [L_i(tau)]G on the GPU
     (batch scalar multiplication); L_i(tau) = w^i (tau^n - 1) / (n (tau - w^i))
     with one batch inversion."""
-    from gnark_amd import msm, fr
+    from gnark_amd import msm
+    F = FIELDS[curve]
+    R, MONT = F.R, F.MONT
+    group = msm.BLS12_381_G1 if curve == "bls12-381" else msm.G1
     n = 1 << log_n
-    w = fr.bls_domain_generator(log_n)
-    gen = bo.g1_to_bytes(bo.G1_GEN)
+    w = F.cv.omega(n)
+    gen = F.g1_to_bytes(F.cv.G1)
     pw, x = bytearray(32 * (n + 3)), 1
     for i in range(n + 3):
         pw[32 * i:32 * i + 32] = m2b(x * MONT % R)
         x = x * tau % R
-    kzg = msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bytes(pw), n + 3)
+    kzg = msm.batch_scalar_mul(group, gen, bytes(pw), n + 3)
     wi, dens = [1] * n, [0] * n
     for i in range(n):
         if i:
@@ -228,18 +257,19 @@ def srs(log_n, tau):
         d_inv = inv * pre[i] % R
         inv = inv * dens[i] % R
         lag[32 * i:32 * i + 32] = m2b(wi[i] * d_inv % R * cst % R)
-    return kzg, msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bytes(lag), n)
+    return kzg, msm.batch_scalar_mul(group, gen, bytes(lag), n)
 
 
 def make_key(circ, tau, key_srs=None, shard=None, reduce=None, devices=None):
-    from gnark_amd import plonk_prover as pp, fr
+    from gnark_amd import plonk_prover as pp
     sel, qcp = circ.selectors()
     perm = circ.permutation()
-    s123 = circ.s_polys(perm, fr.bls_domain_generator(circ.log_n), fr.BLS_FR_MULTIPLICATIVE_GEN)
-    kzg, kzg_lag = key_srs if key_srs is not None else srs(circ.log_n, tau)
+    cv = circ.F.cv
+    s123 = circ.s_polys(perm, cv.omega(circ.n), cv.fr_gen)
+    kzg, kzg_lag = key_srs if key_srs is not None else srs(circ.log_n, tau, circ.curve)
     return pp.ProvingKey(circ.log_n, kzg, kzg_lag, *sel, *s123, perm.tobytes(), qcp=qcp,
                          nb_public=circ.nb_public, commitment_indexes=circ.cmt_idx, shard=shard, reduce=reduce,
-                         devices=devices)
+                         devices=devices, curve=circ.curve)
 
 
 def to_oracle(pk, proof):
@@ -256,6 +286,7 @@ def to_oracle(pk, proof):
 def check_gates(circ, L, Rv, O, public, cmts):
     """Every row's constraint holds (Montgomery bytes in): a sanity check of the solver."""
     n = circ.n
+    R, MINV = circ.F.R, circ.F.MINV
 
     def v(buf, i):
         return int.from_bytes(buf[32 * i:32 * i + 32], "little") * MINV % R

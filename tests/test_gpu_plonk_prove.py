@@ -2,7 +2,8 @@
 prove.go:116-1079 inside libgnark_amd.so) on synthetic sparse-R1CS circuits with
 public inputs and BSB22 commitments (tests/plonk_circuits.py), checked by the
 PlonK verifier (verify.go:45-290) restated in the oracle -- gnark's transcript
-encodings (RawBytes / compressed Marshal, pinned by the bellman_test.go keys),
+encodings (Marshal = RawBytes, uncompressed: groth16/bls12-381/verify.go:80-82,
+plonk/bn254/solidity.go:407-536),
 PI(zeta), the BSB22 terms -- with the SRS trapdoor in place of the pairing.
 Witnesses that break a gate, a copy constraint, a public input or a commitment
 must not verify.  BASELINE configs[4] size: a 2^22 circuit."""
@@ -154,6 +155,49 @@ def test_plonk_prove_sharded_kzg_matches(world):
     assert bo.plonk_verify_trapdoor(pr, vk, tau, public=pub)
 
 
+@pytest.mark.parametrize("curve,log_n,nb_public,n_cmt", [
+    ("bls12-381", 3, 0, 0), ("bls12-381", 4, 1, 0), ("bls12-381", 5, 2, 1), ("bls12-381", 6, 0, 2),
+    ("bls12-381", 7, 3, 1), ("bls12-381", 8, 2, 2),
+    ("bn254", 3, 0, 0), ("bn254", 4, 1, 0), ("bn254", 5, 2, 1), ("bn254", 6, 0, 2), ("bn254", 8, 2, 2)])
+def test_plonk_proof_bytes_match_oracle_prover(curve, log_n, nb_public, n_cmt):
+    """Byte-exact PlonK on both curves (backend/plonk/bls12-381 and
+    backend/plonk/bn254): the GPU proof equals the oracle's restatement of
+    prove.go:116-1391 (oracle/plonk_prover_oracle.py) on the same circuit, key
+    (same SRS trapdoor), witness, BSB22 hint values and blinding -- every
+    commitment, claimed value and opening, and the vk digests; the transcript
+    order and encodings are those the reference's Solidity verifier hashes
+    (plonk/bn254/solidity.go:407-536, 961-1024)."""
+    import plonk_prover_oracle as po
+    from test_oracle_plonk_prover import blinding, ints, oracle_key
+    from gnark_amd import plonk_prover as pp
+    circ = Circuit(log_n, 70 + log_n, nb_public=nb_public, n_cmt=n_cmt, curve=curve)
+    F = circ.F
+    tau = random.Random(100 + log_n).randrange(2, F.R)
+    pk = make_key(circ, tau)
+    key = oracle_key(circ, tau)
+    g = F.g1_from_bytes
+    vk = key["vk"]
+    assert [g(x) for x in pk.vk.S] == vk["S"] and [g(x) for x in pk.vk.Qcp] == vk["Qcp"]
+    assert [g(x) for x in (pk.vk.Ql, pk.vk.Qr, pk.vk.Qm, pk.vk.Qo, pk.vk.Qk)] == \
+        [vk["Ql"], vk["Qr"], vk["Qm"], vk["Qo"], vk["Qk"]]
+    L, Rv, O, pub, cmts = circ.solve(pk, 9, commit=pk.commit_lagrange)
+    for v, d, _ in cmts:  # bsb22Hint's kzg.Commit on the GPU == the oracle's
+        assert g(d) == po.commit_lagrange(key, ints(v, F))
+    got = pp.prove(pk, L, Rv, O, rng=random.Random(5), public=pub, commitments=cmts)
+    want = po.prove(key, ints(L, F), ints(Rv, F), ints(O, F), pub, [(ints(v, F), g(d), h) for v, d, h in cmts],
+                    blinding(5, F.R))
+    assert po.verify_trapdoor(key, want, pub)
+    assert [g(x) for x in got.LRO] == want["LRO"]
+    assert g(got.Z) == want["Z"]
+    assert [g(x) for x in got.H] == want["H"]
+    assert [g(x) for x in got.bsb22] == want["bsb22"]
+    assert list(got.claimed_values) == want["claimed"]
+    assert got.z_shifted_value == want["zu"]
+    assert g(got.z_shifted_H) == want["zs_H"]
+    assert g(got.batched_H) == want["batched_H"]
+    pk.close()
+
+
 @pytest.mark.parametrize("log_n,parts,n_cmt", [(6, 2, 1), (7, 3, 2), (8, 4, 0), (8, 8, 1)])
 def test_plonk_prove_multi_device_matches(log_n, parts, n_cmt):
     """One process, `parts` device parts (gg_plonk_pk_create_multi) rehearsed on
@@ -182,6 +226,34 @@ def test_plonk_prove_multi_device_matches(log_n, parts, n_cmt):
     assert bo.plonk_verify_trapdoor(pr, vk, tau, public=pub)
     pkm.close()
     pk0.close()
+
+
+@pytest.mark.parametrize("log_n,nb_public,n_cmt,parts", [(12, 2, 1, 1), (14, 1, 0, 4)])
+def test_plonk_bn254_prove_verifies(log_n, nb_public, n_cmt, parts):
+    """backend/plonk/bn254 at sizes the Python oracle verifies in seconds: the GPU
+    proof passes the verifier restatement (verify.go:45-290 over BN254), from a
+    one-GPU key and from a key split over `parts` device parts."""
+    import plonk_prover_oracle as po
+    from test_oracle_plonk_prover import oracle_key
+    from gnark_amd import plonk_prover as pp
+    circ = Circuit(log_n, 90 + log_n, nb_public=nb_public, n_cmt=n_cmt, curve="bn254")
+    F = circ.F
+    tau = random.Random(log_n).randrange(2, F.R)
+    pk = make_key(circ, tau, devices=[0] * parts if parts > 1 else None)
+    L, Rv, O, pub, cmts = circ.solve(pk, 3, commit=pk.commit_lagrange)
+    check_gates(circ, L, Rv, O, pub, cmts)
+    proof = pp.prove(pk, L, Rv, O, rng=random.Random(8), public=pub, commitments=cmts)
+    key = oracle_key(circ, tau)
+    g = F.g1_from_bytes
+    pr = {"LRO": [g(x) for x in proof.LRO], "Z": g(proof.Z), "H": [g(x) for x in proof.H],
+          "batched_H": g(proof.batched_H), "claimed": list(proof.claimed_values), "zs_H": g(proof.z_shifted_H),
+          "zu": proof.z_shifted_value, "bsb22": [g(x) for x in proof.bsb22]}
+    assert po.verify_trapdoor(key, pr, pub)
+    bad = dict(pr)
+    bad["claimed"] = list(pr["claimed"])
+    bad["claimed"][3] = (bad["claimed"][3] + 1) % F.R
+    assert not po.verify_trapdoor(key, bad, pub)
+    pk.close()
 
 
 def test_plonk_prove_2p22_verifies():
