@@ -1,7 +1,7 @@
 //go:build amd
 
-// MI355X path of plonk.Prove for BLS12-381: a file of package plonk
-// (backend/plonk/bls12-381) so it reads pk.trace / pk.Kzg / pk.KzgLagrange
+// MI355X path of plonk.Prove for BN254: a file of package plonk
+// (backend/plonk/bn254) so it reads pk.trace / pk.Kzg / pk.KzgLagrange
 // directly.  Prove (prove.go:116) dispatches here when the prover option
 // WithAMDAcceleration() / WithIcicleAcceleration() is set (INTEGRATION.md §4).
 // Hint-free systems without commitments solve on the GPU (solver_amd.go);
@@ -36,14 +36,14 @@ import (
 	"sync"
 	"unsafe"
 
-	curve "github.com/consensys/gnark-crypto/ecc/bls12-381"
-	"github.com/consensys/gnark-crypto/ecc/bls12-381/fr"
-	"github.com/consensys/gnark-crypto/ecc/bls12-381/fr/hash_to_field"
-	"github.com/consensys/gnark-crypto/ecc/bls12-381/fr/iop"
+	curve "github.com/consensys/gnark-crypto/ecc/bn254"
+	"github.com/consensys/gnark-crypto/ecc/bn254/fr"
+	"github.com/consensys/gnark-crypto/ecc/bn254/fr/hash_to_field"
+	"github.com/consensys/gnark-crypto/ecc/bn254/fr/iop"
 	"github.com/consensys/gnark/backend"
 	"github.com/consensys/gnark/backend/witness"
 	"github.com/consensys/gnark/constraint"
-	cs "github.com/consensys/gnark/constraint/bls12-381"
+	cs "github.com/consensys/gnark/constraint/bn254"
 	"github.com/consensys/gnark/constraint/solver"
 	fcs "github.com/consensys/gnark/frontend/cs"
 )
@@ -52,7 +52,7 @@ import (
 const HasAMD = true
 
 // the C ABI's id of this package's curve
-const amdCurve = C.GG_CURVE_BLS12_381
+const amdCurve = C.GG_CURVE_BN254
 
 func amdError() error { return fmt.Errorf("gnark_amd: %s", C.GoString(C.gg_last_error())) }
 
@@ -264,7 +264,7 @@ func proveAMD(spr *cs.SparseR1CS, pk *ProvingKey, fullWitness witness.Witness, o
 	if !ok {
 		return nil, witness.ErrInvalidWitness
 	}
-	// newSolver's check (constraint/bls12-381/solver.go:71-76): the public
+	// newSolver's check (constraint/bn254/solver.go:71-76): the public
 	// inputs below are read from w[:len(spr.Public)]
 	if exp := spr.GetNbPublicVariables() + spr.GetNbSecretVariables(); len(w) != exp {
 		return nil, fmt.Errorf("invalid witness size, got %d, expected %d", len(w), exp)
