@@ -19,7 +19,9 @@
 // A zero denominator is errDivideByZero.
 #include "common.h"
 #include "field.cuh"
+#include "strands.h"
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 #include <cstring>
@@ -100,6 +102,102 @@ __global__ void __launch_bounds__(256) k_scs_level(ScsDev<C> d, const uint32_t* 
     }
 }
 
+// W read around the (write-through, non-coherent) L1: a strand reads values
+// it stored earlier in the same launch
+template <class C>
+__device__ __forceinline__ Fe<C> ldfe_l2(const Fe<C>* p) {
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+    Fe<C> r;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint64_t x = __hip_atomic_load(q + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        r.v[2 * k] = (uint32_t)x;
+        r.v[2 * k + 1] = (uint32_t)(x >> 32);
+    }
+    return r;
+}
+
+// Strand schedule (strands.h): thread s walks segment s of this launch --
+// consecutive constraints of one dependency chain -- in order.  The unknown's
+// position is fixed per constraint (unk[c] = 3 c + {0, 1, 2}: xa, xb, xc;
+// ~0: none, the constraint is checked), so no solved flags are read; the
+// same formulas as k_scs_level.  The chain's last RC outputs stay in registers.
+template <class C>
+__global__ void __launch_bounds__(256) k_scs_strands(ScsDev<C> d, const uint32_t* unk, const uint32_t* order,
+                                                     const uint32_t* seg_start, uint32_t nseg, uint32_t nin) {
+    using F = Fe<C>;
+    const uint32_t sg = blockIdx.x * blockDim.x + threadIdx.x;
+    if (sg >= nseg) return;
+    constexpr int RC = 4;
+    uint32_t cw[RC];
+    F cv[RC];
+#pragma unroll
+    for (int k = 0; k < RC; k++) cw[k] = 0xffffffffu;
+    int cpos = 0;
+    auto value = [&](uint32_t w) {
+        F x;
+        int hit = -1;
+#pragma unroll
+        for (int q = 0; q < RC; q++)
+            if (cw[q] == w) hit = q;
+        if (hit >= 0) {
+#pragma unroll
+            for (int q = 0; q < RC; q++)
+                if (q == hit) x = cv[q];
+        } else {
+            x = w < nin ? ldfe(d.W + w) : ldfe_l2(d.W + w);
+        }
+        return x;
+    };
+    for (uint32_t i = seg_start[sg], e = seg_start[sg + 1]; i < e; i++) {
+        const uint32_t c = order[i], u = unk[c];
+        const int pos = u == 0xffffffffu ? 3 : (int)(u - 3 * c);
+        const uint32_t xa = d.wires[3 * c], xb = d.wires[3 * c + 1], xc = d.wires[3 * c + 2];
+        const uint32_t* q = d.qidx + 5 * c;
+        const F qL = ldfe(d.coef + q[0]), qR = ldfe(d.coef + q[1]), qM = ldfe(d.coef + q[3]),
+                qC = ldfe(d.coef + q[4]);
+        const F a = pos != 0 ? value(xa) : F::zero(), b = pos != 1 ? value(xb) : F::zero(),
+                o = pos != 2 ? value(xc) : F::zero();
+        uint32_t w = 0xffffffffu;
+        F v;
+        if (pos <= 1) {
+            const F qO = ldfe(d.coef + q[2]);
+            const F den = pos == 0 ? qM * b + qL : qM * a + qR;
+            if (den.is_zero()) {
+                atomicMin(d.fail + 2, c);
+                return;  // the solve fails: the rest of this strand is never read
+            }
+            const F num = (pos == 0 ? qR * b : qL * a) + qO * o + qC;
+            v = -(num * inverse(den));
+            w = pos == 0 ? xa : xb;
+        } else if (pos == 2) {
+            const F qOinv = ldfe(d.coef_inv + q[2]);
+            if (qOinv.is_zero()) {
+                atomicMin(d.fail + 2, c);
+                return;
+            }
+            const F t = (qM * a) * b + qL * a + qR * b + qC;
+            v = -(t * qOinv);
+            w = xc;
+        } else {
+            const F qO = ldfe(d.coef + q[2]);
+            const F t = (qM * a) * b + qL * a + qR * b + qO * o + qC;
+            if (!t.is_zero()) atomicMin(d.fail, c);
+        }
+        if (w != 0xffffffffu) {
+            stfe(d.W + w, v);
+            d.solved[w] = 1;
+#pragma unroll
+            for (int k = 0; k < RC; k++)
+                if (k == cpos) {
+                    cw[k] = w;
+                    cv[k] = v;
+                }
+            cpos = (cpos + 1) & (RC - 1);
+        }
+    }
+}
+
 template <class C>
 __global__ void k_scs_init(Fe<C>* W, uint8_t* solved, size_t nw, const Fe<C>* in, size_t n_in, uint32_t* fail) {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -149,8 +247,16 @@ struct gg_scs {
     int64_t expect_inputs = -1;  // gg_scs_set_inputs: required witness length (-1 = not set)
     size_t nw = 0, ncons = 0, nb_public = 0, dom = 0, ncoef = 0;
     std::vector<uint32_t> level_off;
+    std::vector<uint32_t> h_wires, h_level_cons;  // host copies for the strand analysis
+    std::vector<uint8_t> h_flags;
     DevBuf wires, qidx, flags, coef, coef_inv, level_cons, W, L, R, O, solved, fail, inputs, cnt;
     bool has_flags = false;
+    // strand schedule (built at the first solve, per witness length; strands.h)
+    long long strand_nin = -1;
+    bool strands = false;  // false: the level-by-level launches
+    std::vector<uint32_t> sl_seg_off;
+    DevBuf unk, order, seg_start;
+    size_t n_super = 0, n_seg = 0;
     hipStream_t st = nullptr;
     hipGraphExec_t graph = nullptr;
     std::mutex mu;
@@ -173,6 +279,17 @@ void enqueue_scs_levels(gg_scs* h) {
     ScsDev<C> d{h->wires.as<uint32_t>(), h->qidx.as<uint32_t>(), h->has_flags ? h->flags.as<uint8_t>() : nullptr,
                 h->coef.as<Fe<C>>(), h->coef_inv.as<Fe<C>>(), h->W.as<Fe<C>>(), h->solved.as<uint8_t>(),
                 h->fail.as<uint32_t>()};
+    if (h->strands) {
+        for (size_t l = 0; l < h->n_super; l++) {
+            const uint32_t a = h->sl_seg_off[l], cnt = h->sl_seg_off[l + 1] - a;
+            if (!cnt) continue;
+            hipLaunchKernelGGL(k_scs_strands<C>, dim3(grid_for(cnt, 256)), dim3(256), 0, h->st, d,
+                               h->unk.as<uint32_t>(), h->order.as<uint32_t>(), h->seg_start.as<uint32_t>() + a, cnt,
+                               (uint32_t)h->strand_nin);
+            GG_HIP(hipGetLastError());
+        }
+        return;
+    }
     const uint32_t* lc = h->level_cons.as<uint32_t>();
     for (size_t l = 0; l + 1 < h->level_off.size(); l++) {
         const uint32_t a = h->level_off[l], cnt = h->level_off[l + 1] - a;
@@ -182,11 +299,45 @@ void enqueue_scs_levels(gg_scs* h) {
     }
 }
 
+// Strand schedule for a witness of n_in values (wires 0..n_in-1 solved up
+// front, no ONE_WIRE); commitment rows solve nothing and are left out
+bool build_scs_strands(gg_scs* h, size_t n_in) {
+    StrandPlan plan;
+    const bool ok = build_strand_plan(
+        h->ncons, h->nw, (uint32_t)n_in, h->level_off, h->h_level_cons,
+        [&](uint32_t c, auto&& f) {
+            for (uint32_t k = 0; k < 3; k++) f(3 * c + k, h->h_wires[3 * c + k]);
+        },
+        [&](uint32_t c) { return h->has_flags && (h->h_flags[c] & 1u); }, plan);
+    if (!ok) return false;
+    auto up = [](DevBuf& b, const void* src, size_t bytes) {
+        b.alloc(std::max<size_t>(bytes, 16));
+        if (bytes) GG_HIP(hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+    };
+    up(h->unk, plan.unk.data(), plan.unk.size() * 4);
+    up(h->order, plan.order.data(), plan.order.size() * 4);
+    up(h->seg_start, plan.seg_start.data(), plan.seg_start.size() * 4);
+    h->sl_seg_off = std::move(plan.sl_seg_off);
+    h->n_seg = plan.seg_start.size() - 1;
+    h->n_super = h->sl_seg_off.size() - 1;
+    return true;
+}
+
 template <class C>
 void scs_solve_impl(gg_scs* h, const void* in, size_t n_in) {
     hipLaunchKernelGGL(k_scs_init<C>, dim3(grid_for(h->nw, 256)), dim3(256), 0, h->st, h->W.as<Fe<C>>(),
                        h->solved.as<uint8_t>(), h->nw, (const Fe<C>*)in, n_in, h->fail.as<uint32_t>());
     GG_HIP(hipGetLastError());
+    // schedule: strands when the levels allow it (GG_SOLVER_LEVELS=1: level launches)
+    if (h->strand_nin != (long long)n_in) {
+        const bool levels_only = getenv("GG_SOLVER_LEVELS") && atoi(getenv("GG_SOLVER_LEVELS"));
+        h->strands = !levels_only && build_scs_strands(h, n_in);
+        h->strand_nin = (long long)n_in;
+        if (h->graph) {
+            (void)hipGraphExecDestroy(h->graph);
+            h->graph = nullptr;
+        }
+    }
     if (!h->graph) {
         hipGraph_t g;
         GG_HIP(hipStreamBeginCapture(h->st, hipStreamCaptureModeThreadLocal));
@@ -257,6 +408,9 @@ extern "C" int gg_scs_create(int curve, size_t n_wires, size_t n_constraints, si
         h->dom = dom;
         h->ncoef = n_coeffs;
         h->level_off.assign(level_off, level_off + n_levels + 1);
+        h->h_wires.assign(wires, wires + 3 * n_constraints);
+        h->h_level_cons.assign(level_cons, level_cons + n_constraints);
+        if (flags) h->h_flags.assign(flags, flags + n_constraints);
         auto up = [](DevBuf& b, const void* src, size_t bytes) {
             b.alloc(std::max<size_t>(bytes, 16));
             if (bytes) GG_HIP(hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
@@ -366,5 +520,21 @@ extern "C" int gg_scs_solution_dev(gg_scs_t h, void** w, void** l, void** r, voi
     if (l) *l = h->L.p;
     if (r) *r = h->R.p;
     if (o) *o = h->O.p;
+    GG_CAPI_END
+}
+
+extern "C" int gg_scs_schedule(gg_scs_t h, int* strands, size_t* launches, size_t* segments) {
+    GG_CAPI_BEGIN
+    GG_CHECK(h, GG_ERR_INVALID_ARG, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    size_t nl = 0;
+    if (h->strands) {
+        for (size_t l = 0; l < h->n_super; l++) nl += h->sl_seg_off[l + 1] > h->sl_seg_off[l];
+    } else {
+        for (size_t l = 0; l + 1 < h->level_off.size(); l++) nl += h->level_off[l + 1] > h->level_off[l];
+    }
+    if (strands) *strands = h->strands ? 1 : 0;
+    if (launches) *launches = nl;
+    if (segments) *segments = h->strands ? h->n_seg : 0;
     GG_CAPI_END
 }

@@ -21,6 +21,7 @@
 // launches per solve otherwise).
 #include "common.h"
 #include "field.cuh"
+#include "strands.h"
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
@@ -277,89 +278,28 @@ struct gg_r1cs {
 };
 
 // Strand schedule for a witness of n_in values (wires 0..n_in are solved up
-// front).  In r1cs.Levels order: the unknown term of every constraint (the
-// single term whose wire no earlier level produced), its producer map, then
-// greedy chains -- a constraint extends the strand whose tail produced one of
-// its inputs -- and super-levels: sl(c) = max(sl(previous in its strand),
-// sl(d) + 1 for every dependency d on another strand).  One launch per
-// super-level, a thread per strand segment (the MiMC headline: 65,536 chains,
-// one launch instead of 255).  Returns false (level launches instead) when the
-// levels do not match the system; the level kernel then reports it.
+// front; strands.h): one launch per super-level, a thread per strand segment
+// (the MiMC headline: 65,536 chains, one launch instead of 255).  Returns false
+// (level launches instead) when the levels do not match the system; the level
+// kernel then reports it.
 static bool build_strands(gg_r1cs* r, size_t n_in) {
-    const uint32_t NONE = 0xffffffffu, nin = (uint32_t)n_in + 1;
-    const size_t nc = r->ncons;
-    std::vector<uint32_t> lev(nc), prod(r->nw, NONE), unk(nc, NONE);
-    for (size_t l = 0; l + 1 < r->level_off.size(); l++)
-        for (uint32_t i = r->level_off[l]; i < r->level_off[l + 1]; i++) lev[r->h_level_cons[i]] = (uint32_t)l;
-    std::vector<uint32_t> strand(nc), sl(nc), tail, deps;
-    std::vector<std::pair<uint64_t, uint32_t>> key(nc);  // ((sl, strand), position) -> order
-    for (size_t l = 0; l + 1 < r->level_off.size(); l++) {
-        for (uint32_t i = r->level_off[l]; i < r->level_off[l + 1]; i++) {
-            const uint32_t c = r->h_level_cons[i];
-            deps.clear();
-            uint32_t u = NONE;
-            for (uint32_t t = r->h_off[3 * c]; t < r->h_off[3 * c + 3]; t++) {
-                const uint32_t w = r->h_wire[t];
-                if (w < nin) continue;
-                const uint32_t p = prod[w];
-                if (p == NONE) {
-                    if (u != NONE) return false;  // two unknown terms
-                    u = t;
-                } else if (p != c) {
-                    if (lev[p] >= l) return false;  // produced in this or a later level
-                    deps.push_back(p);
-                }
-            }
-            if (u != NONE) prod[r->h_wire[u]] = c;
-            unk[c] = u;
-            uint32_t best = NONE;
-            for (uint32_t d : deps)
-                if (tail[strand[d]] == d && (best == NONE || lev[d] > lev[best])) best = d;
-            uint32_t s, level = 0;
-            if (best != NONE) {
-                s = strand[best];
-                level = sl[best];
-            } else {
-                s = (uint32_t)tail.size();
-                tail.push_back(NONE);
-            }
-            for (uint32_t d : deps)
-                if (strand[d] != s) level = std::max(level, sl[d] + 1);
-            strand[c] = s;
-            tail[s] = c;
-            sl[c] = level;
-            key[c] = {((uint64_t)level << 32) | s, (uint32_t)i};
-        }
-    }
-    std::vector<uint32_t> order(nc);
-    for (size_t c = 0; c < nc; c++) order[c] = (uint32_t)c;
-    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return key[a] < key[b]; });
-    std::vector<uint32_t> seg_start;
-    r->sl_seg_off.clear();
-    uint64_t prev = ~0ull;
-    uint32_t cur_sl = NONE;
-    for (size_t i = 0; i < nc; i++) {
-        const uint64_t k = key[order[i]].first;
-        if (k != prev) {
-            const uint32_t lvl = (uint32_t)(k >> 32);
-            while (cur_sl == NONE || cur_sl < lvl) {
-                r->sl_seg_off.push_back((uint32_t)seg_start.size());
-                cur_sl = cur_sl == NONE ? 0 : cur_sl + 1;
-            }
-            seg_start.push_back((uint32_t)i);
-            prev = k;
-        }
-    }
-    seg_start.push_back((uint32_t)nc);
-    r->sl_seg_off.push_back((uint32_t)seg_start.size() - 1);
+    StrandPlan plan;
+    const bool ok = build_strand_plan(
+        r->ncons, r->nw, (uint32_t)n_in + 1, r->level_off, r->h_level_cons,
+        [&](uint32_t c, auto&& f) {
+            for (uint32_t t = r->h_off[3 * c]; t < r->h_off[3 * c + 3]; t++) f(t, r->h_wire[t]);
+        },
+        [](uint32_t) { return false; }, plan);
+    if (!ok) return false;
     auto up = [](DevBuf& b, const void* src, size_t bytes) {
         b.alloc(std::max<size_t>(bytes, 16));
         if (bytes) GG_HIP(hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
     };
-    up(r->unk, unk.data(), nc * 4);
-    up(r->order, order.data(), nc * 4);
-    up(r->seg_start, seg_start.data(), seg_start.size() * 4);
-    r->n_seg = seg_start.size() - 1;
+    up(r->unk, plan.unk.data(), plan.unk.size() * 4);
+    up(r->order, plan.order.data(), plan.order.size() * 4);
+    up(r->seg_start, plan.seg_start.data(), plan.seg_start.size() * 4);
+    r->sl_seg_off = std::move(plan.sl_seg_off);
+    r->n_seg = plan.seg_start.size() - 1;
     r->n_super = r->sl_seg_off.size() - 1;
     return true;
 }
@@ -610,5 +550,21 @@ extern "C" int gg_r1cs_solution_dev(gg_r1cs_t r, void** w, void** a, void** b, v
     if (a) *a = r->A.p;
     if (b) *b = r->B.p;
     if (c) *c = r->C.p;
+    GG_CAPI_END
+}
+
+extern "C" int gg_r1cs_schedule(gg_r1cs_t r, int* strands, size_t* launches, size_t* segments) {
+    GG_CAPI_BEGIN
+    GG_CHECK(r, GG_ERR_INVALID_ARG, "null handle");
+    std::lock_guard<std::mutex> lk(r->mu);
+    size_t nl = 0;
+    if (r->strands) {
+        for (size_t l = 0; l < r->n_super; l++) nl += r->sl_seg_off[l + 1] > r->sl_seg_off[l];
+    } else {
+        for (size_t l = 0; l + 1 < r->level_off.size(); l++) nl += r->level_off[l + 1] > r->level_off[l];
+    }
+    if (strands) *strands = r->strands ? 1 : 0;
+    if (launches) *launches = nl;
+    if (segments) *segments = r->strands ? r->n_seg : 0;
     GG_CAPI_END
 }

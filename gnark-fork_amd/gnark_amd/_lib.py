@@ -152,6 +152,8 @@ def _load():
         "gg_scs_info": ([P, ctypes.POINTER(S), ctypes.POINTER(S), ctypes.POINTER(S)], I),
         "gg_scs_solve": ([P, P, S, I, P, P, P, P, I, ctypes.POINTER(ctypes.c_int64)], I),
         "gg_scs_solution_dev": ([P, PP, PP, PP, PP], I),
+        "gg_r1cs_schedule": ([P, ctypes.POINTER(I), ctypes.POINTER(S), ctypes.POINTER(S)], I),
+        "gg_scs_schedule": ([P, ctypes.POINTER(I), ctypes.POINTER(S), ctypes.POINTER(S)], I),
         "gg_profile_enable": ([I], I),
         "gg_profile_get": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_double)], I),
@@ -190,7 +192,7 @@ EXPORTED = [
     "gg_groth16_mpk_last_timings", "gg_groth16_mpk_create_ex", "gg_groth16_mpk_prove_ex",
     "gg_groth16_mpk_devices", "gg_groth16_mpk_base_info", "gg_groth16_pk_create_shard_ex", "gg_r1cs_create", "gg_r1cs_create_ex", "gg_r1cs_release", "gg_r1cs_info", "gg_r1cs_solve",
     "gg_r1cs_solution_dev", "gg_scs_create", "gg_scs_release", "gg_scs_info", "gg_scs_solve",
-    "gg_scs_solution_dev", "gg_r1cs_set_inputs", "gg_scs_set_inputs",
+    "gg_scs_solution_dev", "gg_r1cs_set_inputs", "gg_scs_set_inputs", "gg_r1cs_schedule", "gg_scs_schedule",
 ]
 
 

@@ -32,6 +32,12 @@ class UnsatisfiedConstraintError(RuntimeError):
         self.cid = cid
 
 
+def _schedule(fn, handle):
+    s, nl, ns = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_size_t()
+    check(fn(handle, ctypes.byref(s), ctypes.byref(nl), ctypes.byref(ns)))
+    return bool(s.value), nl.value, ns.value
+
+
 def compute_levels(nb_inputs: int, n_wires: int, term_off, term_wire) -> list:
     """r1cs.Levels from the CSR terms (blueprint_r1cs.go:61-96, core.go:405-419):
     wires < nb_inputs are inputs (not in the instruction tree)."""
@@ -115,6 +121,10 @@ class R1CS:
         a, b, c = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
         check(lib.gg_r1cs_info(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         return a.value, b.value, c.value
+
+    def schedule(self):
+        """(strands, launches, segments) of the last solve (gg_r1cs_schedule)."""
+        return _schedule(lib.gg_r1cs_schedule, self.handle)
 
     def solve(self, witness, on_device: bool = True):
         """r1cs.Solve(fullWitness): witness = public (without ONE_WIRE) then
@@ -271,6 +281,10 @@ class SparseR1CS:
             raise UnsatisfiedConstraintError(bad.value, lib.gg_last_error().decode())
         check(rc)
         return out
+
+    def schedule(self):
+        """(strands, launches, segments) of the last solve (gg_scs_schedule)."""
+        return _schedule(lib.gg_scs_schedule, self.handle)
 
     def close(self):
         if getattr(self, "handle", None):

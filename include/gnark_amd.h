@@ -594,6 +594,11 @@ int gg_r1cs_set_inputs(gg_r1cs_t r, size_t nb_public, size_t nb_secret);
 /* device pointers of the handle's resident W, A, B, C (valid until the next
  * solve or the release): a prove can read them without a copy */
 int gg_r1cs_solution_dev(gg_r1cs_t r, void **w, void **a, void **b, void **c);
+/* the schedule the last solve ran (solver.go:418-533 levels, replaced by
+ * dependency strands when the levels allow it): *strands = 1 for the strand
+ * schedule (one launch per super-level), 0 for one launch per level;
+ * *launches = kernel launches per solve, *segments = strand segments (threads) */
+int gg_r1cs_schedule(gg_r1cs_t r, int *strands, size_t *launches, size_t *segments);
 
 /* ---- sparse-R1CS (PlonK) solver: the SCS blueprints' Solve
  * (constraint/blueprint_scs.go:53-151) level by level (solver.go:418-533) and
@@ -617,6 +622,8 @@ int gg_scs_info(gg_scs_t h, size_t *n_wires, size_t *n_constraints, size_t *doma
 int gg_scs_solve(gg_scs_t h, const void *witness, size_t n_witness, int witness_on_device, void *w_out,
                  void *l_out, void *r_out, void *o_out, int out_on_device, int64_t *failed);
 int gg_scs_solution_dev(gg_scs_t h, void **w, void **l, void **r, void **o);
+/* as gg_r1cs_schedule, for the sparse-R1CS solver */
+int gg_scs_schedule(gg_scs_t h, int *strands, size_t *launches, size_t *segments);
 /* the same check for a sparse R1CS: n_witness == nb_public + nb_secret */
 int gg_scs_set_inputs(gg_scs_t h, size_t nb_public, size_t nb_secret);
 

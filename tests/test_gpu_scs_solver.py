@@ -43,10 +43,14 @@ def _vals(b, mod):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("levels_only", [False, True])
 @pytest.mark.parametrize("seed,curve,commit", [(1, "bls12-381", 0), (2, "bls12-381", 11), (3, "bn254", 0),
                                                (4, "bn254", 7)])
-def test_gpu_scs_solver_random(seed, curve, commit):
+def test_gpu_scs_solver_random(seed, curve, commit, levels_only, monkeypatch):
+    """Both schedules (strands: one launch per super-level; GG_SOLVER_LEVELS=1:
+    one launch per r1cs.Levels level) bit-exact vs the oracle."""
     from gnark_amd import solver
+    monkeypatch.setenv("GG_SOLVER_LEVELS", "1" if levels_only else "0")
     mod = BLS_R if curve == "bls12-381" else BN_R
     cons, flags, nw, wit = _circuit(seed, mod, commit_every=commit)
     lv = ss.levels_of(7, cons)
@@ -59,6 +63,9 @@ def test_gpu_scs_solver_random(seed, curve, commit):
         gW, gL, gR, gO = (x.to_host() for x in out) if on_dev else out
         assert _vals(gW, mod) == W
         assert _vals(gL, mod) == L and _vals(gR, mod) == R and _vals(gO, mod) == O
+    strands, launches, segs = sys_.schedule()
+    assert strands == (not levels_only)
+    assert launches <= len(lv) and (levels_only or segs >= 1)
     sys_.close()
 
 
@@ -95,6 +102,71 @@ def test_gpu_scs_solver_errors():
     with pytest.raises(GnarkAmdError):
         sys_.solve([5])
     sys_.close()
+
+
+def scs_mimc(nb_chains, rounds, mod):
+    """MiMC-style chains as sparse R1CS (std/hash/mimc encryptPow5 through
+    frontend/cs/scs: a = x + k_r (add gate), b = a a, c = b b, x' = c a), four
+    constraints per round, chain-major constraint ids; the witness is x0 of
+    every chain (secret).  Returns (wires, qidx, table, levels, n_wires) with
+    r1cs.Levels = the 4 rounds positions (4 * rounds levels of nb_chains)."""
+    import numpy as np
+    K, R = nb_chains, rounds
+    rng = random.Random(77)
+    ks = [rng.randrange(mod) for _ in range(R)]
+    table = [0, 1, mod - 1] + ks  # 0, 1, -1, round constants
+    c = np.arange(K * R * 4, dtype=np.int64).reshape(K, R, 4)
+    new = K + c  # the wire each constraint introduces
+    x = np.empty((K, R), dtype=np.int64)  # round input wire
+    x[:, 0] = np.arange(K)
+    x[:, 1:] = new[:, :-1, 3]
+    a, b, cc = new[..., 0], new[..., 1], new[..., 2]
+    wires = np.stack([np.stack([x, x, a], -1), np.stack([a, a, b], -1), np.stack([b, b, cc], -1),
+                      np.stack([cc, a, new[..., 3]], -1)], 2)  # K, R, 4, 3
+    q = np.zeros((K, R, 4, 5), dtype=np.int64)  # qL, qR, qO, qM, qC (table ids)
+    q[:, :, 0, 0] = 1
+    q[:, :, 0, 2] = 2
+    q[:, :, 0, 4] = 3 + np.arange(R)[None, :]
+    q[:, :, 1:, 2] = 2
+    q[:, :, 1:, 3] = 1
+    levels = [c[:, r, i].reshape(-1) for r in range(R) for i in range(4)]
+    return wires.reshape(-1), q.reshape(-1), table, levels, K + K * R * 4, ks
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("log_n", [12, 22])
+def test_gpu_scs_solver_strands_mimc(log_n, monkeypatch):
+    """configs[4]-sized sparse R1CS (2^22 constraints: 16,384 MiMC chains of 64
+    rounds, 256 levels): the strand schedule solves it in ONE launch and agrees
+    byte for byte with the 256 level launches; sampled chains match a big-int
+    restatement of the rounds."""
+    from gnark_amd import fr, solver
+    mod = BLS_R
+    K = 1 << (log_n - 8)
+    wires, qidx, table, levels, nw, ks = scs_mimc(K, 64, mod)
+    rng = random.Random(log_n)
+    wit = [rng.randrange(mod) for _ in range(K)]
+    out = {}
+    for lv_only in (True, False):
+        monkeypatch.setenv("GG_SOLVER_LEVELS", "1" if lv_only else "0")
+        sys_ = solver.SparseR1CS(0, K, nw, wires, qidx, table, levels=levels, curve="bls12-381")
+        assert sys_.domain == 1 << log_n
+        W, L, Rv, O = sys_.solve(wit, on_device=False)
+        out[lv_only] = (bytes(W), bytes(L), bytes(Rv), bytes(O))
+        strands, launches, segs = sys_.schedule()
+        assert (strands, launches) == ((False, 256) if lv_only else (True, 1))
+        if not lv_only:
+            assert segs == K
+        sys_.close()
+    assert out[True] == out[False]
+    W = out[False][0]
+    for j in rng.sample(range(K), min(K, 16)):
+        x = wit[j]
+        for r in range(64):
+            a = (x + ks[r]) % mod
+            x = pow(a, 5, mod)
+        last = K + ((j * 64 + 63) * 4 + 3)
+        assert fr.bls_fr_unmont(W[32 * last:32 * last + 32]) == x
 
 
 class _ScsCircuit:
