@@ -28,7 +28,8 @@ void compute_h_device(gg_domain* d, Fr* A, Fr* B, Fr* C, Fr* H, hipStream_t st);
 void msm_device(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st);
 size_t msm_scalars_needed(gg_msm_base* b);
 gg_msm_base* msm_base_create_internal(int group, const void* host_points, size_t n,
-                                      const uint32_t* sidx, int window_bits, bool keep_inf);
+                                      const uint32_t* sidx, int window_bits, bool keep_inf, int groups);
+int choose_groups_multi(const double* bytes, const int* W, int k, double extra);
 bool msm_same_shape(const gg_msm_base* a, const gg_msm_base* b);
 MsmSort* msm_own_sort(gg_msm_base* b);
 void msm_prepare_dev(gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
@@ -180,21 +181,36 @@ static void pk_build(gg_groth16_pk* pk, int curve, int log_n, const void* omega_
     GG_CHECK(nK == 0 || g1_K, GG_ERR_INVALID_ARG, "null g1_K");
     GG_CHECK(nZ == 0 || g1_Z, GG_ERR_INVALID_ARG, "null g1_Z");
     const size_t nw = hi - lo;
+    const int cAK = choose_c(std::max<size_t>(nw, 1), ps.g1a, tbits);
+    const int cB = choose_c(std::max<size_t>(nB, 1), 128, tbits);  // B1 shares its sort with G2
+    const int cZ = choose_c(std::max<size_t>(nZ, 1), ps.g1a, tbits);
+    // the memory knob: one precompute-group count for the whole key (bases that
+    // share a sort need equal shapes), the smallest whose tables fit HBM beside
+    // the proof's scratch (3 sorts of 16 B per entry, domain and solution vectors)
+    int groups;
+    {
+        auto W = [&](int c) { return (tbits + c - 1) / c; };
+        const double g1a = (double)ps.g1a, g2a = (double)ps.g2a;
+        const double bytes[5] = {W(cAK) * (double)nw * g1a, W(cAK) * (double)nw * g1a, W(cB) * (double)nB * g1a,
+                                 W(cB) * (double)nB * g2a, W(cZ) * (double)nZ * g1a};
+        const int ws[5] = {W(cAK), W(cAK), W(cB), W(cB), W(cZ)};
+        const double extra = 16.0 * (W(cAK) * (double)nw + W(cB) * (double)nB + W(cZ) * (double)nZ) +
+                             12.0 * 32.0 * (double)pk->n;
+        groups = choose_groups_multi(bytes, ws, 5, extra);
+    }
     // dense wire-indexed A and K (holes = infinity), one window size for both
     {
         const size_t pb = ps.g1a;
         std::vector<uint8_t> dense(nw * pb, 0);
         for (size_t j = 0; j < nA; j++) memcpy(&dense[(size_t)ia[j] * pb], (const uint8_t*)g1_A + j * pb, pb);
-        const int cAK = choose_c(std::max<size_t>(nw, 1), pb, tbits);
-        pk->A = msm_base_create_internal(g1, dense.data(), nw, nullptr, cAK, true);
+        pk->A = msm_base_create_internal(g1, dense.data(), nw, nullptr, cAK, true, groups);
         std::fill(dense.begin(), dense.end(), 0);
         for (size_t j = 0; j < nK; j++) memcpy(&dense[(size_t)ik[j] * pb], (const uint8_t*)g1_K + j * pb, pb);
-        pk->K = msm_base_create_internal(g1, dense.data(), nw, nullptr, cAK, true);
+        pk->K = msm_base_create_internal(g1, dense.data(), nw, nullptr, cAK, true, groups);
     }
-    // B1 shares its sort with the G2 base: the window that suits G2
-    pk->B = msm_base_create_internal(g1, g1_B, nB, ib.data(), choose_c(std::max<size_t>(nB, 1), 128, tbits), false);
-    pk->B2 = msm_base_create_internal(g2, g2_B, nB, ib.data(), msm_base_window(pk->B), false);
-    pk->Z = msm_base_create_internal(g1, g1_Z, nZ, nullptr, 0, false);
+    pk->B = msm_base_create_internal(g1, g1_B, nB, ib.data(), cB, false, groups);
+    pk->B2 = msm_base_create_internal(g2, g2_B, nB, ib.data(), msm_base_window(pk->B), false, groups);
+    pk->Z = msm_base_create_internal(g1, g1_Z, nZ, nullptr, cZ, false, groups);
     pk->share_AK = msm_same_shape(pk->A, pk->K);
     pk->share_B = msm_same_shape(pk->B, pk->B2);
     for (hipStream_t* x : {&pk->s0, &pk->s1, &pk->s2, &pk->s3, &pk->s4})
@@ -276,6 +292,15 @@ extern "C" int gg_groth16_pk_base_info(gg_groth16_pk_t pk, int which, size_t* n_
     GG_CHECK(pk && which >= 0 && which <= 4, GG_ERR_INVALID_ARG, "bad argument");
     gg_msm_base_t b[5] = {pk->A, pk->B, pk->K, pk->Z, pk->B2};
     return gg_msm_base_info(b[which], n_points, window_bits, n_windows);
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_pk_base_layout(gg_groth16_pk_t pk, int which, int* groups, int* stored_windows,
+                                         size_t* table_bytes) {
+    GG_CAPI_BEGIN
+    GG_CHECK(pk && which >= 0 && which <= 4, GG_ERR_INVALID_ARG, "bad argument");
+    gg_msm_base_t b[5] = {pk->A, pk->B, pk->K, pk->Z, pk->B2};
+    return gg_msm_base_layout(b[which], groups, stored_windows, table_bytes);
     GG_CAPI_END
 }
 

@@ -3,13 +3,13 @@
 
 namespace gg {
 void create_base_g1(gg_msm_base* b, const void* points, size_t n, int on_device,
-                    const uint32_t* sidx, int window_bits, bool keep_inf);
+                    const uint32_t* sidx, int window_bits, bool keep_inf, int groups);
 void create_base_g2(gg_msm_base* b, const void* points, size_t n, int on_device,
-                    const uint32_t* sidx, int window_bits, bool keep_inf);
+                    const uint32_t* sidx, int window_bits, bool keep_inf, int groups);
 void create_base_bls(gg_msm_base* b, const void* points, size_t n, int on_device,
-                     const uint32_t* sidx, int window_bits, bool keep_inf);
+                     const uint32_t* sidx, int window_bits, bool keep_inf, int groups);
 void create_base_bls2(gg_msm_base* b, const void* points, size_t n, int on_device,
-                      const uint32_t* sidx, int window_bits, bool keep_inf);
+                      const uint32_t* sidx, int window_bits, bool keep_inf, int groups);
 void msm_run_bls2(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st);
 void msm_finish_bls2(gg_msm_base* b, MsmSort* s, MsmScratch* scr, void* out_jac, hipStream_t st);
 void msm_run_g1(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st);
@@ -33,10 +33,10 @@ extern "C" int gg_msm_base_create(int group, const void* points, size_t n, int p
     GG_CHECK(n < 0x80000000ull, GG_ERR_INVALID_ARG, "n too large");
     std::unique_ptr<gg_msm_base> b(new gg_msm_base());
     b->group = group;
-    if (group == GG_G1) create_base_g1(b.get(), points, n, points_on_device, scalar_index, window_bits, false);
-    else if (group == GG_G2) create_base_g2(b.get(), points, n, points_on_device, scalar_index, window_bits, false);
-    else if (group == GG_BLS12_381_G1) create_base_bls(b.get(), points, n, points_on_device, scalar_index, window_bits, false);
-    else create_base_bls2(b.get(), points, n, points_on_device, scalar_index, window_bits, false);
+    if (group == GG_G1) create_base_g1(b.get(), points, n, points_on_device, scalar_index, window_bits, false, 0);
+    else if (group == GG_G2) create_base_g2(b.get(), points, n, points_on_device, scalar_index, window_bits, false, 0);
+    else if (group == GG_BLS12_381_G1) create_base_bls(b.get(), points, n, points_on_device, scalar_index, window_bits, false, 0);
+    else create_base_bls2(b.get(), points, n, points_on_device, scalar_index, window_bits, false, 0);
     *out = b.release();
     GG_CAPI_END
 }
@@ -44,6 +44,15 @@ extern "C" int gg_msm_base_create(int group, const void* points, size_t n, int p
 extern "C" int gg_msm_base_release(gg_msm_base_t b) {
     GG_CAPI_BEGIN
     delete b;
+    GG_CAPI_END
+}
+
+extern "C" int gg_msm_base_layout(gg_msm_base_t b, int* groups, int* stored_windows, size_t* table_bytes) {
+    GG_CAPI_BEGIN
+    GG_CHECK(b, GG_ERR_INVALID_ARG, "null base");
+    if (groups) *groups = b->G;
+    if (stored_windows) *stored_windows = b->Ws;
+    if (table_bytes) *table_bytes = b->pts.bytes;
     GG_CAPI_END
 }
 
@@ -74,17 +83,17 @@ void msm_device(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_
 }
 // ---- shared sorts (Groth16): bases of one shape reuse one MsmSort
 gg_msm_base* msm_base_create_internal(int group, const void* host_points, size_t n,
-                                      const uint32_t* sidx, int window_bits, bool keep_inf) {
+                                      const uint32_t* sidx, int window_bits, bool keep_inf, int groups) {
     std::unique_ptr<gg_msm_base> b(new gg_msm_base());
     b->group = group;
-    if (group == GG_G1) create_base_g1(b.get(), host_points, n, 0, sidx, window_bits, keep_inf);
-    else if (group == GG_G2) create_base_g2(b.get(), host_points, n, 0, sidx, window_bits, keep_inf);
-    else if (group == GG_BLS12_381_G1) create_base_bls(b.get(), host_points, n, 0, sidx, window_bits, keep_inf);
-    else create_base_bls2(b.get(), host_points, n, 0, sidx, window_bits, keep_inf);
+    if (group == GG_G1) create_base_g1(b.get(), host_points, n, 0, sidx, window_bits, keep_inf, groups);
+    else if (group == GG_G2) create_base_g2(b.get(), host_points, n, 0, sidx, window_bits, keep_inf, groups);
+    else if (group == GG_BLS12_381_G1) create_base_bls(b.get(), host_points, n, 0, sidx, window_bits, keep_inf, groups);
+    else create_base_bls2(b.get(), host_points, n, 0, sidx, window_bits, keep_inf, groups);
     return b.release();
 }
 bool msm_same_shape(const gg_msm_base* a, const gg_msm_base* b) {
-    if (a->n != b->n || a->c != b->c || a->W != b->W || a->has_sidx != b->has_sidx) return false;
+    if (a->n != b->n || a->c != b->c || a->W != b->W || a->G != b->G || a->has_sidx != b->has_sidx) return false;
     if (!a->has_sidx || a->n == 0) return true;
     std::vector<uint32_t> x(a->n), y(b->n);
     GG_HIP(hipMemcpy(x.data(), a->sidx.p, a->n * 4, hipMemcpyDeviceToHost));
@@ -95,6 +104,7 @@ MsmSort* msm_own_sort(gg_msm_base* b) { return &b->own.sort; }
 MsmWork* msm_work_new() { return new MsmWork(); }
 void msm_work_delete(MsmWork* w) { delete w; }
 int msm_base_window(const gg_msm_base* b) { return b->c; }
+int msm_base_groups(const gg_msm_base* b) { return b->G; }
 void msm_prepare_dev(gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st) {
     if (b->n) msm_prepare(b, s, scalars_dev, st);
 }

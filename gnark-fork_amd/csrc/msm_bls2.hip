@@ -5,8 +5,8 @@
 
 namespace gg {
 void create_base_bls2(gg_msm_base* b, const void* points, size_t n, int on_device,
-                      const uint32_t* sidx, int window_bits, bool keep_inf) {
-    create_base<Fp2Bls>(b, points, n, on_device, sidx, window_bits, keep_inf, 1);
+                      const uint32_t* sidx, int window_bits, bool keep_inf, int groups) {
+    create_base<Fp2Bls>(b, points, n, on_device, sidx, window_bits, keep_inf, 1, groups);
 }
 void msm_run_bls2(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
     Jac<Fp2Bls> j = xyzz_to_jac(msm_run<Fp2Bls>(b, w, scalars_dev, st));

@@ -1,5 +1,6 @@
 // Non-template MSM kernels: scalar digits, counting sort, scan, work items.
 #include "msm_impl.cuh"
+#include <atomic>
 #include <cstdlib>
 
 namespace gg {
@@ -120,7 +121,45 @@ int choose_c(size_t n, size_t point_bytes, int total_bits) {
     return best;
 }
 
+// process-wide cap on what precompute tables may take (gg_set_hbm_budget; 0 = none)
+static std::atomic<unsigned long long> g_hbm_budget{0};
+
+int choose_groups(double bytes, double extra, int W) { return choose_groups_multi(&bytes, &W, 1, extra); }
+
+int choose_groups_multi(const double* bytes, const int* W, int k, double extra) {
+    if (const char* e = getenv("GG_MSM_GROUPS")) {  // override (tests, tuning)
+        const int g = atoi(e);
+        if (g == 1 || g == 2 || g == 4 || g == 8 || g == 16) return g;
+    }
+    int wmax = 1;
+    for (int i = 0; i < k; i++) wmax = std::max(wmax, W[i]);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+        (void)hipGetLastError();
+        return 1;
+    }
+    // keep 4 GiB or 3 % of the card for the per-proof scratch of other work
+    double avail = (double)fr - std::max(4.0 * (1ull << 30), 0.03 * (double)tot);
+    const unsigned long long cap = g_hbm_budget.load();
+    if (cap) avail = std::min(avail, (double)cap);
+    int g = 1;
+    while (g < 16 && g < wmax) {
+        double need = extra;
+        for (int i = 0; i < k; i++) need += bytes[i] * (double)((W[i] + g - 1) / g) / (double)W[i];
+        if (need <= avail) break;
+        g <<= 1;
+    }
+    return g;
+}
+
 }  // namespace gg
+
+extern "C" int gg_set_hbm_budget(size_t bytes) {
+    gg::g_hbm_budget.store((unsigned long long)bytes);
+    return GG_OK;
+}
+
+extern "C" size_t gg_get_hbm_budget(void) { return (size_t)gg::g_hbm_budget.load(); }
 
 // ===================================================================== sort v2
 // Counting sort of the (window, scalar) entries by bucket without global
@@ -143,8 +182,11 @@ inline int sort_spb(int W) {
 
 // Sort order is by pi(b) = bitrev_{c-1}(b): bins take the LOW bits of the bucket
 // id, so the small ids of a narrow top window spread over all bins.
-__device__ __forceinline__ uint32_t pi_of(uint32_t b, int c) { return __brev(b) >> (33 - c); }
-__device__ __forceinline__ uint32_t bin_of(uint32_t b, int c, int h) { return pi_of(b, c) >> (c - 1 - h); }
+// With precompute groups the bucket id B = j 2^(c-1) + b carries the group in
+// its top bits (kbits = c - 1 + log2 G key bits): sort key = bucket_perm(B).
+__device__ __forceinline__ uint32_t bin_of(uint32_t B, int c, int kbits, int h) {
+    return bucket_perm(B, c) >> (kbits - h);
+}
 
 // exclusive scan of v over a 256-thread block (4 wave scans + one barrier);
 // `wsum` is 4 words of LDS.  Returns the exclusive prefix; *total = block sum.
@@ -191,9 +233,9 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t* cnt, uint32_t d, bool va
 
 template <class SC>
 __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, const uint32_t* sidx,
-                                                     size_t n, int c, int W, WinSpec ws, int spb,
-                                                     int nbins, int h, uint32_t* keys, uint32_t* hist,
-                                                     uint32_t nblocks) {
+                                                     size_t n, int c, int W, WinSpec ws, int G, int kbits,
+                                                     int spb, int nbins, int h, uint32_t* keys,
+                                                     uint32_t* hist, uint32_t nblocks) {
     extern __shared__ uint32_t hh[];
     for (int j = threadIdx.x; j < nbins; j += blockDim.x) hh[j] = 0;
     __syncthreads();
@@ -223,9 +265,10 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, cons
             if (d > (1 << (bw - 1))) { d -= (1 << bw); carry = 1; } else carry = 0;
             uint32_t key = 0xffffffffu;
             if (d) {
-                uint32_t bk = (uint32_t)((d > 0 ? d : -d) - 1);
+                // bucket |d| - 1 of group w mod G
+                const uint32_t bk = ((uint32_t)(w & (G - 1)) << (c - 1)) | (uint32_t)((d > 0 ? d : -d) - 1);
                 key = bk | (d < 0 ? 0x80000000u : 0u);
-                atomicAdd(&hh[bin_of(bk, c, h)], 1u);
+                atomicAdd(&hh[bin_of(bk, c, kbits, h)], 1u);
             }
             keys[(size_t)w * n + i] = key;
         }
@@ -237,8 +280,8 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, cons
 // Phase C, LDS-staged: the block's entries are first partitioned by bin in LDS
 // (ranks from LDS atomics, bin bases from this block's own histogram), then
 // written out as contiguous per-bin runs -> coalesced stores.
-__global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_t n, int W, int c, int spb,
-                                                     int nbins, int h, const uint32_t* hist,
+__global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_t n, int W, int c, int G,
+                                                     int kbits, int spb, int nbins, int h, const uint32_t* hist,
                                                      const uint32_t* hoff, uint32_t nblocks,
                                                      uint32_t* tmp_entry, uint32_t* tmp_key) {
     extern __shared__ uint32_t sm[];
@@ -247,7 +290,7 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_
     uint32_t* lcur = sm + nbins;      // nbins: local cursors
     uint32_t* s_entry = sm + 2 * nbins;
     uint32_t* s_key = s_entry + spb * W;
-    const int lowbits = (c - 1) - h;
+    const int lowbits = kbits - h;
     // this block's column of the histogram and of the global bin offsets, one bin
     // per thread (nbins <= 256), both loads in flight together; the local
     // exclusive scan is a wave scan + one barrier
@@ -270,24 +313,24 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_
     // the LDS atomics so the loads overlap
     for (int jb0 = 0; jb0 < tot_e; jb0 += 8 * 256) {
         uint32_t kk[8];
-        size_t ee[8];
+        uint32_t ee[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
             int j = jb0 + (int)threadIdx.x + u * 256;
             kk[u] = 0xffffffffu;
             if (j < tot_e) {
                 int w = j / ns, t = j - w * ns;
-                ee[u] = (size_t)w * n + i0 + t;
-                kk[u] = keys[ee[u]];
+                kk[u] = keys[(size_t)w * n + i0 + t];
+                ee[u] = (uint32_t)((size_t)(w / G) * n + i0 + t);  // the stored copy of window w
             }
         }
 #pragma unroll
         for (int u = 0; u < 8; u++) {
             uint32_t key = kk[u];
             if (key == 0xffffffffu) continue;
-            uint32_t pk = pi_of(key & 0x7fffffffu, c);
+            uint32_t pk = bucket_perm(key & 0x7fffffffu, c);
             uint32_t q = atomicAdd(&lcur[pk >> lowbits], 1u);
-            s_entry[q] = (uint32_t)ee[u] | (key & 0x80000000u);
+            s_entry[q] = ee[u] | (key & 0x80000000u);
             s_key[q] = pk;
         }
     }
@@ -468,11 +511,12 @@ static void sort_plan(int c, int& h, std::vector<int>& rs) {
 
 void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st) {
     const size_t n = b->n, nb = b->nb;
-    const int c = b->c, W = b->W;
+    const int c = b->c, W = b->W, G = b->G;
     const size_t total = (size_t)W * n;
+    const int kbits = (c - 1) + __builtin_ctz((unsigned)G);  // sort key bits
     int h;
     std::vector<int> rs;
-    sort_plan(c, h, rs);
+    sort_plan(kbits + 1, h, rs);
     const int nbins = 1 << h;
     const int spb = sort_spb(W);
     const uint32_t nblocks = (uint32_t)((n + spb - 1) / spb);
@@ -506,12 +550,12 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     if (b->scurve)
         hipLaunchKernelGGL(k_digits_hist<FrBlsCfg>, dim3(nblocks), dim3(256), nbins * 4, st,
                            (const FrBls*)scalars_dev, b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n,
-                           c, W, b->win, spb, nbins, h, s->keys.as<uint32_t>(), s->hist.as<uint32_t>(),
-                           nblocks);
+                           c, W, b->win, G, kbits, spb, nbins, h, s->keys.as<uint32_t>(),
+                           s->hist.as<uint32_t>(), nblocks);
     else
         hipLaunchKernelGGL(k_digits_hist<FrCfg>, dim3(nblocks), dim3(256), nbins * 4, st, scalars_dev,
-                           b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, spb, nbins,
-                           h, s->keys.as<uint32_t>(), s->hist.as<uint32_t>(), nblocks);
+                           b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, G, kbits, spb,
+                           nbins, h, s->keys.as<uint32_t>(), s->hist.as<uint32_t>(), nblocks);
     GG_HIP(hipGetLastError());
     exclusive_scan(s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nh, st, s->scan_tmp);
     // segment starts ping-pong between bin_start and seg2; the last pass writes offsets
@@ -529,11 +573,11 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     auto ent_out = [&](int j) { return ((S - 1 - j) % 2 == 0) ? &s->sorted : &s->tmp_entry; };
     auto key_out = [&](int j) { return (j % 2 == 0) ? &s->tmp_key : &s->keys; };
     hipLaunchKernelGGL(k_bin_scatter, dim3(nblocks), dim3(256), lds_c, st, s->keys.as<uint32_t>(),
-                       n, W, c, spb, nbins, h, s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nblocks,
+                       n, W, c, G, kbits, spb, nbins, h, s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nblocks,
                        ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->as<uint32_t>() : nullptr);
     GG_HIP(hipGetLastError());
     uint32_t nseg = (uint32_t)nbins;
-    int shift = (c - 1) - h;
+    int shift = kbits - h;
     for (int j = 1; j < S; j++) {
         const int r = rs[j - 1];
         const bool last = j == S - 1;

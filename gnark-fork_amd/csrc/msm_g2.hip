@@ -3,8 +3,8 @@
 
 namespace gg {
 void create_base_g2(gg_msm_base* b, const void* points, size_t n, int on_device,
-                    const uint32_t* sidx, int window_bits, bool keep_inf) {
-    create_base<Fp2>(b, points, n, on_device, sidx, window_bits, keep_inf);
+                    const uint32_t* sidx, int window_bits, bool keep_inf, int groups) {
+    create_base<Fp2>(b, points, n, on_device, sidx, window_bits, keep_inf, 0, groups);
 }
 void msm_run_g2(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
     G2Jac j = xyzz_to_jac(msm_run<Fp2>(b, w, scalars_dev, st));

@@ -61,6 +61,13 @@ __global__ void k_bucket_max(const uint32_t* offsets, size_t nb, uint32_t* maxcn
 void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, hipStream_t st,
                     std::vector<DevBuf>& tmp, int depth = 0);
 int choose_c(size_t n, size_t point_bytes, int total_bits = 255);
+// precompute groups for a table of `bytes` (all W windows stored) plus `extra`
+// bytes of other allocations: GG_MSM_GROUPS if set, else the smallest power of
+// two G <= W whose table (bytes / G, rounded up to whole copies) and extra fit
+// the free HBM less a reserve, capped by gg_set_hbm_budget
+int choose_groups(double bytes, double extra, int W);
+// the same for several tables that must share one G (bytes[i] with all W[i] windows stored)
+int choose_groups_multi(const double* bytes, const int* W, int k, double extra);
 // scalar field of a base: 0 = BN254 fr (254-bit), 1 = BLS12-381 fr (255-bit)
 inline int scalar_total_bits(int scurve) { return scurve ? 256 : 255; }
 // Window layout: W windows of bits[w] (<= c) bits at bit offset off[w], summing
@@ -88,7 +95,15 @@ struct MsmSort;
 void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
 void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
 
-constexpr uint32_t LIGHT = 16; 
+constexpr uint32_t LIGHT = 16;
+// Bucket ids: B = j 2^(c-1) + b for precompute group j (< G) and bucket b of the
+// group.  The sort orders the low c-1 bits bit-reversed (pi(b) = bitrev_{c-1}(b),
+// see sort_entries); pi is an involution, so the same map takes a sort position
+// q back to its bucket B.
+__device__ __forceinline__ uint32_t bucket_perm(uint32_t B, int c) {
+    const uint32_t m = (1u << (c - 1)) - 1;
+    return (B & ~m) | (__brev(B & m) >> (33 - c));
+}
 // which groups accumulate in a reduced-radix form, and which one
 template <class F>
 struct RadixOf {
@@ -133,7 +148,7 @@ __device__ __forceinline__ void range_store(const Xyzz<F>& acc, bool first, bool
                                             size_t t, Xyzz<F>* head, Xyzz<F>* tail, Xyzz<F>* S) {
     if (first) st(head + t, acc);
     else if (last) st(tail + t, acc);
-    else st(S + (__brev(q) >> (33 - c)), acc);
+    else st(S + bucket_perm(q, c), acc);
 }
 
 // waves per SIMD the accumulation is compiled for: 2 (<= 256 VGPRs) for the G1
@@ -399,7 +414,7 @@ __global__ void __launch_bounds__(256) k_bucket_combine(const Xyzz<F>* head, con
     if (q >= nb) return;
     const uint32_t E = offsets[nb];
     const BucketSpan s = bucket_span(offsets, (uint32_t)q, E, K);
-    Xyzz<F>* out = S + (__brev((uint32_t)q) >> (33 - c));
+    Xyzz<F>* out = S + bucket_perm((uint32_t)q, c);
     if (s.empty) {
         if (lane == 0) st(out, Xyzz<F>::inf());
         return;
@@ -587,8 +602,13 @@ struct gg_msm_base {
     size_t n = 0;  // resident points
     int c = 0, W = 0;
     gg::WinSpec win{};  // per-window bit widths / offsets
-    size_t nb = 0;
-    DevBuf pts;   // W * n affine points, window-major
+    // precompute groups (the memory knob, DESIGN.md "MSM"): only every G-th
+    // window's shift 2^off(w) P is stored (Ws = ceil(W / G) copies); window
+    // w = G w' + j reads copy w' and adds into bucket group j, whose sum is
+    // scaled by 2^(j c) at the end.  G = 1: every window stored, one group.
+    int G = 1, Ws = 0;
+    size_t nb = 0;  // buckets over all groups: G 2^(c-1)
+    DevBuf pts;   // Ws * n affine points, copy-major
     DevBuf sidx;  // n u32 or empty
     bool has_sidx = false;
     bool has_inf = false;  // wire-indexed table with infinity holes (skipped)
@@ -603,7 +623,7 @@ namespace gg {
 template <class F>
 inline void precompute(gg_msm_base* b, const Affine<F>* dev_in, hipStream_t st) {
     const size_t n = b->n;
-    b->pts.alloc((size_t)b->W * n * sizeof(Affine<F>));
+    b->pts.alloc((size_t)b->Ws * n * sizeof(Affine<F>));
     Affine<F>* out = b->pts.as<Affine<F>>();
     DevBuf cur(n * sizeof(Xyzz<F>));
     // ~64 elements per thread amortise one Fermat inversion, >= 16K threads
@@ -612,9 +632,11 @@ inline void precompute(gg_msm_base* b, const Affine<F>* dev_in, hipStream_t st) 
     hipLaunchKernelGGL(k_pre_init<F>, dim3(grid_for(n, 256)), dim3(256), 0, st, dev_in, n, out,
                        cur.as<Xyzz<F>>());
     GG_HIP(hipGetLastError());
-    for (int w = 1; w < b->W; w++) {
+    for (int w = 1; w < b->Ws; w++) {
+        // copy w holds 2^off(G w) P: G windows of (uniform, when G > 1) width c on
+        const int dbl = b->G == 1 ? (int)b->win.bits[w - 1] : b->G * b->c;
         hipLaunchKernelGGL(k_pre_dbl<F>, dim3(grid_for(n, 256)), dim3(256), 0, st,
-                           cur.as<Xyzz<F>>(), n, (int)b->win.bits[w - 1]);
+                           cur.as<Xyzz<F>>(), n, dbl);
         GG_HIP(hipGetLastError());
         hipLaunchKernelGGL(k_pre_normalize<F>, dim3(grid_for(T, 256)), dim3(256), 0, st,
                            (const Xyzz<F>*)cur.p, n, T, prefix.as<F>(), out + (size_t)w * n);
@@ -625,7 +647,7 @@ inline void precompute(gg_msm_base* b, const Affine<F>* dev_in, hipStream_t st) 
         // domain (field29.cuh): x R' mod p, same layout
         using C = typename RadixOf<F>::C;
         using E = Fe<typename C::Std>;
-        const size_t total = (size_t)b->W * n * 2 * (sizeof(F) / sizeof(E));
+        const size_t total = (size_t)b->Ws * n * 2 * (sizeof(F) / sizeof(E));
         hipLaunchKernelGGL(k_to_radix<C>, dim3(grid_for(total, 256)), dim3(256), 0, st, (E*)out, total);
         GG_HIP(hipGetLastError());
     }
@@ -639,8 +661,7 @@ inline void precompute(gg_msm_base* b, const Affine<F>* dev_in, hipStream_t st) 
 // tree sums that run wide on the GPU.  Pieces of <= 16 elements finish on the
 // host, combined by Horner over their 2^mlog factors.
 template <class F>
-inline Xyzz<F> bucket_reduce_2d(gg_msm_base* b, const Xyzz<F>* S, MsmScratch* scr, hipStream_t st) {
-    const size_t nb = b->nb;
+inline Xyzz<F> bucket_reduce_2d(size_t nb, const Xyzz<F>* S, MsmScratch* scr, hipStream_t st) {
     const size_t XB = sizeof(Xyzz<F>);
     const size_t arena_elems = 3 * nb + 1024;
     scr->arena.reserve(arena_elems * XB);
@@ -851,7 +872,13 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
     ps_acc2.stop(st);
     // ---- bucket reduction: sum_b (b+1) S_b
     ProfScope ps_red("msm_reduce", st, (double)nb);
-    Xyzz<F> res = bucket_reduce_2d<F>(b, (const Xyzz<F>*)S, scr, st);
+    // one weighted sum per precompute group, then sum_j 2^(j c) R_j by Horner
+    const size_t nbg = nb / (size_t)b->G;
+    Xyzz<F> res = Xyzz<F>::inf();
+    for (int j = b->G - 1; j >= 0; j--) {
+        for (int k = 0; k < b->c && !res.is_inf() && j < b->G - 1; k++) res = xyzz_dbl(res);
+        res = xyzz_add(res, bucket_reduce_2d<F>(nbg, (const Xyzz<F>*)S + (size_t)j * nbg, scr, st));
+    }
     ps_red.stop(st);
     return res;
 }
@@ -881,16 +908,31 @@ __global__ void k_base_compact(const Affine<F>* pts, size_t n, const uint32_t* k
     idx[pos[i]] = (uint32_t)i;
 }
 
+// groups: precompute groups G (power of two), 0 = choose from free HBM
+// (choose_groups: the smallest G whose table fits)
 template <class F>
-inline void window_layout(gg_msm_base* b, int window_bits, int total) {
+inline void window_layout(gg_msm_base* b, int window_bits, int total, int groups) {
     const size_t pb = sizeof(Affine<F>);
     b->c = window_bits ? window_bits : choose_c(std::max<size_t>(b->n, 1), pb, total);
     GG_CHECK(b->c >= 2 && b->c <= 24, GG_ERR_INVALID_ARG, "window_bits out of range [2, 24]");
     b->W = (total + b->c - 1) / b->c;
     b->c = (total + b->W - 1) / b->W;  // widest balanced window for this W
     GG_CHECK(b->W <= 64, GG_ERR_INVALID_ARG, "too many windows");
-    b->win = make_windows(b->c, b->W, total);
-    b->nb = (size_t)1 << (b->c - 1);
+    if (groups == 0) groups = choose_groups((double)b->W * (double)b->n * (double)pb, 0.0, b->W);
+    GG_CHECK(groups >= 1 && groups <= 16 && (groups & (groups - 1)) == 0, GG_ERR_INVALID_ARG,
+             "precompute groups must be 1, 2, 4, 8 or 16");
+    b->G = std::min(groups, 1 << (31 - __builtin_clz((unsigned)b->W)));  // at most W groups
+    b->Ws = (b->W + b->G - 1) / b->G;
+    if (b->G == 1) {
+        b->win = make_windows(b->c, b->W, total);
+    } else {  // uniform widths: window G w' + j sits j c bits above copy w'
+        for (int w = 0; w < b->W; w++) {
+            b->win.bits[w] = (uint8_t)b->c;
+            b->win.off[w] = (uint8_t)(w * b->c);
+        }
+    }
+    b->nb = (size_t)b->G << (b->c - 1);
+    GG_CHECK(b->nb < ((size_t)1 << 30), GG_ERR_UNSUPPORTED, "too many buckets");
     GG_CHECK((double)b->W * (double)b->n < 2147483648.0, GG_ERR_UNSUPPORTED,
              "too many points x windows for 31-bit entry ids");
 }
@@ -899,7 +941,7 @@ inline void window_layout(gg_msm_base* b, int window_bits, int total) {
 // flag / scan / scatter on the device, no round trip through host memory
 template <class F>
 inline void create_base_dev(gg_msm_base* b, const Affine<F>* pts, size_t n, int window_bits, bool keep_inf,
-                            int total) {
+                            int total, int groups) {
     hipStream_t st = hipStreamPerThread;
     DevBuf keep(std::max<size_t>(n, 1) * 4), pos(std::max<size_t>(n, 1) * 4), flag(16);
     GG_HIP(hipMemsetAsync(flag.p, 0, 4, st));
@@ -918,7 +960,7 @@ inline void create_base_dev(gg_msm_base* b, const Affine<F>* pts, size_t n, int 
     b->has_inf = keep_inf && any_inf;
     const bool dropped = kept < n;
     b->has_sidx = dropped;
-    window_layout<F>(b, window_bits, total);
+    window_layout<F>(b, window_bits, total, groups);
     if (!kept) {
         b->max_sidx = 0;
         if (dropped) b->sidx.alloc(4);
@@ -939,12 +981,12 @@ inline void create_base_dev(gg_msm_base* b, const Affine<F>* pts, size_t n, int 
 template <class F>
 inline void create_base(gg_msm_base* b, const void* points, size_t n, int on_device,
                         const uint32_t* sidx, int window_bits, bool keep_inf = false,
-                        int scurve = 0) {
+                        int scurve = 0, int groups = 0) {
     b->scurve = scurve;
     const int total = scalar_total_bits(scurve);
     const size_t pb = sizeof(Affine<F>);
     if (on_device && !sidx && n) {
-        create_base_dev<F>(b, (const Affine<F>*)points, n, window_bits, keep_inf, total);
+        create_base_dev<F>(b, (const Affine<F>*)points, n, window_bits, keep_inf, total, groups);
         return;
     }
     std::vector<uint8_t> host;
@@ -977,7 +1019,7 @@ inline void create_base(gg_msm_base* b, const void* points, size_t n, int on_dev
     b->has_sidx = dropped || sidx != nullptr;
     b->max_sidx = 0;
     for (uint32_t v : idx) b->max_sidx = std::max(b->max_sidx, v);
-    window_layout<F>(b, window_bits, total);
+    window_layout<F>(b, window_bits, total, groups);
     if (b->has_sidx) {
         b->sidx.alloc(std::max<size_t>(b->n, 1) * 4);
         if (b->n) GG_HIP(hipMemcpy(b->sidx.p, idx.data(), b->n * 4, hipMemcpyHostToDevice));

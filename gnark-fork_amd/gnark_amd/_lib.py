@@ -67,6 +67,10 @@ def _load():
         "gg_msm_base_create": ([I, P, S, I, P, I, PP], I),
         "gg_msm_base_release": ([P], I),
         "gg_msm_base_info": ([P, ctypes.POINTER(S), ctypes.POINTER(I), ctypes.POINTER(I)], I),
+        "gg_msm_base_layout": ([P, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(S)], I),
+        "gg_groth16_pk_base_layout": ([P, I, ctypes.POINTER(I), ctypes.POINTER(I), ctypes.POINTER(S)], I),
+        "gg_set_hbm_budget": ([S], I),
+        "gg_get_hbm_budget": ([], S),
         "gg_msm": ([P, P, S, I, P, P], I),
         "gg_g1_jac_to_affine": ([P, P], I),
         "gg_g2_jac_to_affine": ([P, P], I),
@@ -171,7 +175,8 @@ EXPORTED = [
     "gg_copy_to_device", "gg_copy_to_host", "gg_synchronize", "gg_domain_create",
     "gg_domain_create_ex", "gg_bls12_381_g1_jac_to_affine", "gg_bls12_381_g1_jac_add",
     "gg_domain_release", "gg_domain_log_n", "gg_ntt", "gg_groth16_compute_h",
-    "gg_msm_base_create", "gg_msm_base_release", "gg_msm_base_info", "gg_msm",
+    "gg_msm_base_create", "gg_msm_base_release", "gg_msm_base_info", "gg_msm", "gg_msm_base_layout",
+    "gg_groth16_pk_base_layout", "gg_set_hbm_budget", "gg_get_hbm_budget",
     "gg_g1_jac_to_affine", "gg_g2_jac_to_affine", "gg_g1_jac_add", "gg_g2_jac_add",
     "gg_g1_scalar_mul", "gg_g2_scalar_mul", "gg_groth16_pk_create", "gg_groth16_pk_release",
     "gg_groth16_prove", "gg_groth16_last_timings", "gg_batch_scalar_mul", "gg_profile_enable",

@@ -139,6 +139,11 @@ class ProvingKey:
                                           ctypes.byref(w)))
         return n.value, c.value, w.value
 
+    def base_layout(self, which: int):
+        """(groups, stored_windows, table_bytes) of base `which` (0 A, 1 B, 2 K, 3 Z, 4 G2.B)."""
+        from .msm import _layout
+        return _layout(lib.gg_groth16_pk_base_layout, self.handle, which)
+
     def close(self):
         for k in getattr(self, "commitment_keys", ()):
             k.close()

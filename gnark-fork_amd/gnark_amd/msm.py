@@ -40,6 +40,10 @@ class MsmBase:
         check(lib.gg_msm_base_info(self.handle, ctypes.byref(n), ctypes.byref(c), ctypes.byref(w)))
         return n.value, c.value, w.value
 
+    def layout(self):
+        """(groups, stored_windows, table_bytes) of the precomputed table."""
+        return _layout(lib.gg_msm_base_layout, self.handle)
+
     def msm_jac(self, scalars, n_scalars: int, on_device=False, stream=None) -> bytes:
         out = bytearray(_JAC[self.group])
         check(lib.gg_msm(self.handle, ptr(scalars), n_scalars, int(on_device), ptr(out), ptr(stream)))
@@ -93,3 +97,20 @@ def batch_scalar_mul(group: int, base_aff: bytes, scalars, n: int, scalars_on_de
     check(lib.gg_batch_scalar_mul(group, ptr(base_aff), ptr(scalars), n, int(scalars_on_device),
                                   ptr(res), 0))
     return bytes(res)
+
+
+def _layout(fn, *args):
+    g, w, b = ctypes.c_int(), ctypes.c_int(), ctypes.c_size_t()
+    check(fn(*args, ctypes.byref(g), ctypes.byref(w), ctypes.byref(b)))
+    return g.value, w.value, b.value
+
+
+def set_hbm_budget(nbytes: int) -> None:
+    """Cap (bytes per device) on what new precomputed tables may take; 0 = the
+    free HBM less a reserve.  Keys built afterwards pick their precompute groups
+    (gg_msm_base_layout) to fit it."""
+    check(lib.gg_set_hbm_budget(int(nbytes)))
+
+
+def get_hbm_budget() -> int:
+    return int(lib.gg_get_hbm_budget())

@@ -142,6 +142,16 @@ int gg_msm_base_create(int group, const void *points, size_t n, int points_on_de
 int gg_msm_base_release(gg_msm_base_t b);
 /* number of resident (non-infinity) points, and window size actually used */
 int gg_msm_base_info(gg_msm_base_t b, size_t *n_points, int *window_bits, int *n_windows);
+/* memory layout of the precomputed table: every `groups`-th window shift is
+ * stored (stored_windows copies of the points, table_bytes of HBM); groups > 1
+ * trades HBM for more buckets.  Chosen at creation from the free HBM (and the
+ * gg_set_hbm_budget cap; GG_MSM_GROUPS=1|2|4|8|16 forces it) */
+int gg_msm_base_layout(gg_msm_base_t b, int *groups, int *stored_windows, size_t *table_bytes);
+/* process-wide cap (bytes, per device) on what new precomputed tables may
+ * take beside the scratch their proofs need; 0 = the free HBM less a reserve
+ * (gnark sizes nothing like this: its keys live in host memory, setup.go:111) */
+int gg_set_hbm_budget(size_t bytes);
+size_t gg_get_hbm_budget(void);
 
 /* out = sum_i scalars[idx(i)] * P_i as a Jacobian point (gnark G1Jac/G2Jac
  * layout, Montgomery).  Replaces MsmOnDevice / MsmG2OnDevice
@@ -211,6 +221,9 @@ int gg_groth16_pk_release(gg_groth16_pk_t pk);
  * 4 = G2.B): as gg_msm_base_info */
 int gg_groth16_pk_base_info(gg_groth16_pk_t pk, int which, size_t *n_points, int *window_bits,
                             int *n_windows);
+/* as gg_msm_base_layout for base `which` of the key (one groups value per key) */
+int gg_groth16_pk_base_layout(gg_groth16_pk_t pk, int which, int *groups, int *stored_windows,
+                              size_t *table_bytes);
 
 /* Groth16 Prove after Solve (prove.go:127-320; icicle.go:198-420):
  *   wires[n_wires] = solution.W; sol_a/b/c[n_cons] = solution.A/B/C
