@@ -542,8 +542,8 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
         GG_CHECK(rc == GG_OK, rc, gg_last_error());
         const uint8_t* g = (const uint8_t*)kzg_g1;
         for (int j = 0; j < 3; j++) {
-            memcpy(&pk->blind_lo[j], g + PT * j, 96);
-            memcpy(&pk->blind_hi[j], g + PT * (n + j), 96);
+            memcpy(&pk->blind_lo[j], g + PT * j, PT);
+            memcpy(&pk->blind_hi[j], g + PT * (n + j), PT);
         }
     }
     // trace polynomials
@@ -661,9 +661,9 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
     pk->vkQcp.resize(n_cmt);
     if (vk_digests) {
         const uint8_t* d = (const uint8_t*)vk_digests;
-        for (int k = 0; k < 3; k++) memcpy(&pk->vkS[k], d + PT * k, 96);
-        for (int k = 0; k < 5; k++) memcpy(&pk->vkQ[k], d + PT * (3 + k), 96);
-        for (int i = 0; i < n_cmt; i++) memcpy(&pk->vkQcp[i], d + PT * (8 + i), 96);
+        for (int k = 0; k < 3; k++) memcpy(&pk->vkS[k], d + PT * k, PT);
+        for (int k = 0; k < 5; k++) memcpy(&pk->vkQ[k], d + PT * (3 + k), PT);
+        for (int i = 0; i < n_cmt; i++) memcpy(&pk->vkQcp[i], d + PT * (8 + i), PT);
     } else {
         auto cm = [&](const DevBuf& reg) {
             zero(pk->pad.p, nb3, st);

@@ -51,6 +51,16 @@ def test_ntt_roundtrip_2p24():
     assert buf.to_host() == v
 
 
+@pytest.mark.parametrize("inv,dif,cos", [(0, 1, 0), (0, 0, 1), (1, 1, 1)])
+def test_ntt_2p24_vs_oracle(inv, dif, cos):
+    """BASELINE configs[2] at its size: 2^24 transforms compared element for
+    element with the C oracle (the computeH forms: DIF iFFT, coset DIT FFT,
+    coset DIF iFFT)."""
+    log_n = 24
+    v = random_fr_mont(1 << log_n, 24 + 2 * inv + dif).tobytes()
+    assert gpu_fft(v, log_n, inv, dif, cos) == coracle.ntt(v, log_n, inv, dif, cos)
+
+
 def test_ntt_2p22_vs_oracle_single_variant():
     log_n = 22
     v = random_fr_mont(1 << log_n, 8).tobytes()
