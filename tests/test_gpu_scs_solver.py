@@ -178,8 +178,9 @@ class _ScsCircuit:
 
     def __init__(self, cons, nb_public, n_wires):
         import numpy as np
-        from plonk_circuits import Circuit
+        from plonk_circuits import Circuit, FIELDS
         self._C = Circuit
+        self.F, self.curve = FIELDS["bls12-381"], "bls12-381"
         n = 1
         while n < len(cons) + nb_public:
             n <<= 1
@@ -192,7 +193,8 @@ class _ScsCircuit:
             self.a[nb_public + j], self.b[nb_public + j], self.c[nb_public + j] = k[0], k[1], k[2]
 
     def selectors(self):
-        from plonk_circuits import m2b, MONT, NEG_ONE_M
+        from plonk_circuits import m2b
+        MONT, NEG_ONE_M = self.F.MONT, self.F.NEG_ONE_M
         cols = [bytearray(32 * self.n) for _ in range(5)]  # ql, qr, qm, qo, qk
         for i in range(self.nb_public):
             cols[0][32 * i:32 * i + 32] = m2b(NEG_ONE_M)
