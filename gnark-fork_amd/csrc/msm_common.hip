@@ -283,7 +283,7 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, cons
 __global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_t n, int W, int c, int G,
                                                      int kbits, int spb, int nbins, int h, const uint32_t* hist,
                                                      const uint32_t* hoff, uint32_t nblocks,
-                                                     uint32_t* tmp_entry, uint32_t* tmp_key) {
+                                                     uint32_t* tmp_entry, void* tmp_key, int key16) {
     extern __shared__ uint32_t sm[];
     const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
     uint32_t* lbase = sm;             // nbins: local exclusive offsets
@@ -343,7 +343,10 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_
         const uint32_t pk = s_key[q];
         const uint32_t pos = lbase[pk >> lowbits] + q;
         tmp_entry[pos] = s_entry[q];
-        if (tmp_key) tmp_key[pos] = pk;
+        if (tmp_key) {
+            if (key16) static_cast<uint16_t*>(tmp_key)[pos] = (uint16_t)pk;  // the low kbits - h <= 16 bits
+            else static_cast<uint32_t*>(tmp_key)[pos] = pk;
+        }
     }
 }
 
@@ -402,7 +405,11 @@ __global__ void k_seg_chunk_desc(const uint32_t* seg_start, const uint32_t* chun
 
 // counters laid out [segment][digit][chunk-in-segment]: one global exclusive
 // scan then yields absolute output positions.
-__global__ void __launch_bounds__(256) k_seg_hist(const uint32_t* keys, const uint4* desc, int shift,
+// KT: the key word of the segmented passes -- u16 once the bins hold the high
+// bits and <= 16 remain (the usual case: c - 1 = 21 bucket bits, 8 of them bins),
+// halving the key traffic of every later pass
+template <class KT>
+__global__ void __launch_bounds__(256) k_seg_hist(const KT* keys, const uint4* desc, int shift,
                                                   int rbits, uint32_t* ch) {
     __shared__ uint32_t hist[256];
     const uint32_t g = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -418,10 +425,11 @@ __global__ void __launch_bounds__(256) k_seg_hist(const uint32_t* keys, const ui
     if (threadIdx.x < R) ch[(size_t)g0 * R + (size_t)threadIdx.x * nch + k] = hist[threadIdx.x];
 }
 
-__global__ void __launch_bounds__(256) k_seg_scatter(const uint32_t* ent_in, const uint32_t* key_in,
+template <class KT>
+__global__ void __launch_bounds__(256) k_seg_scatter(const uint32_t* ent_in, const KT* key_in,
                                                      const uint4* desc, int shift, int rbits,
                                                      const uint32_t* chpos, uint32_t* ent_out,
-                                                     uint32_t* key_out) {
+                                                     KT* key_out) {
     __shared__ uint32_t cnt[256], base[256], part[256];
     extern __shared__ uint32_t stage[];  // SEG_CH entries, SEG_CH digits (u8) [, SEG_CH keys]
     const uint32_t g = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -476,7 +484,7 @@ __global__ void __launch_bounds__(256) k_seg_scatter(const uint32_t* ent_in, con
         const uint32_t dl = s_dig[q];
         uint32_t pos = cnt[dl] + (q - base[dl]);
         ent_out[pos] = stage[q];
-        if (key_out) key_out[pos] = kk;
+        if (key_out) key_out[pos] = (KT)kk;
     }
 }
 
@@ -572,9 +580,10 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     const int S = 1 + (int)rs.size();
     auto ent_out = [&](int j) { return ((S - 1 - j) % 2 == 0) ? &s->sorted : &s->tmp_entry; };
     auto key_out = [&](int j) { return (j % 2 == 0) ? &s->tmp_key : &s->keys; };
+    const bool key16 = kbits - h <= 16;
     hipLaunchKernelGGL(k_bin_scatter, dim3(nblocks), dim3(256), lds_c, st, s->keys.as<uint32_t>(),
                        n, W, c, G, kbits, spb, nbins, h, s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nblocks,
-                       ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->as<uint32_t>() : nullptr);
+                       ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->p : nullptr, (int)key16);
     GG_HIP(hipGetLastError());
     uint32_t nseg = (uint32_t)nbins;
     int shift = kbits - h;
@@ -597,17 +606,29 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
                            s->chunk_start.as<uint32_t>(), nseg, (uint32_t)max_chunks,
                            s->chunk_desc.as<uint4>());
         GG_HIP(hipGetLastError());
-        const uint32_t* kin = key_out(j - 1)->as<uint32_t>();
-        hipLaunchKernelGGL(k_seg_hist, dim3((unsigned)max_chunks), dim3(256), 0, st, kin,
-                           s->chunk_desc.as<uint4>(), shift, r, s->chunk_hist.as<uint32_t>());
+        const void* kin = key_out(j - 1)->p;
+        if (key16)
+            hipLaunchKernelGGL(k_seg_hist<uint16_t>, dim3((unsigned)max_chunks), dim3(256), 0, st,
+                               (const uint16_t*)kin, s->chunk_desc.as<uint4>(), shift, r,
+                               s->chunk_hist.as<uint32_t>());
+        else
+            hipLaunchKernelGGL(k_seg_hist<uint32_t>, dim3((unsigned)max_chunks), dim3(256), 0, st,
+                               (const uint32_t*)kin, s->chunk_desc.as<uint4>(), shift, r,
+                               s->chunk_hist.as<uint32_t>());
         GG_HIP(hipGetLastError());
         exclusive_scan(s->chunk_hist.as<uint32_t>(), s->chunk_pos.as<uint32_t>(), max_chunks * R, st,
                        s->scan_tmp);
         const size_t lds_s = (size_t)SEG_CH * (last ? 5 : 9);
-        hipLaunchKernelGGL(k_seg_scatter, dim3((unsigned)max_chunks), dim3(256), lds_s, st,
-                           ent_out(j - 1)->as<uint32_t>(), kin, s->chunk_desc.as<uint4>(), shift, r,
-                           s->chunk_pos.as<uint32_t>(), ent_out(j)->as<uint32_t>(),
-                           last ? nullptr : key_out(j)->as<uint32_t>());
+        if (key16)
+            hipLaunchKernelGGL(k_seg_scatter<uint16_t>, dim3((unsigned)max_chunks), dim3(256), lds_s, st,
+                               ent_out(j - 1)->as<uint32_t>(), (const uint16_t*)kin, s->chunk_desc.as<uint4>(),
+                               shift, r, s->chunk_pos.as<uint32_t>(), ent_out(j)->as<uint32_t>(),
+                               last ? nullptr : key_out(j)->as<uint16_t>());
+        else
+            hipLaunchKernelGGL(k_seg_scatter<uint32_t>, dim3((unsigned)max_chunks), dim3(256), lds_s, st,
+                               ent_out(j - 1)->as<uint32_t>(), (const uint32_t*)kin, s->chunk_desc.as<uint4>(),
+                               shift, r, s->chunk_pos.as<uint32_t>(), ent_out(j)->as<uint32_t>(),
+                               last ? nullptr : key_out(j)->as<uint32_t>());
         GG_HIP(hipGetLastError());
         uint32_t* next = last ? s->offsets.as<uint32_t>() : segb[j & 1]->as<uint32_t>();
         hipLaunchKernelGGL(k_seg_next, dim3(grid_for((size_t)nseg * R, 256)), dim3(256), 0, st, segp,
