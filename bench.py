@@ -684,9 +684,12 @@ def accum_roofline(k, pt_bytes, kernel, workload, desc, windows):
 
 
 def _profile_order(path):
-    """(round, version) of a profiles/rNN_vMM_* file, so r02_v13 sorts after r02_v9."""
-    m = re.match(r"r(\d+)_v(\d+)_", os.path.basename(path))
-    return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
+    """(round, version) of a profiles/rNN_vMM_* or rNN_<letter>_* file (a round's
+    GPU sessions a, b, ...), so r02_v13 sorts after r02_v9 and r03_e after r03_a."""
+    m = re.match(r"r(\d+)_(?:v(\d+)|([a-z]))_", os.path.basename(path))
+    if not m:
+        return (0, 0)
+    return (int(m.group(1)), int(m.group(2)) if m.group(2) else 1000 + ord(m.group(3)))
 
 
 def fetch_calibration():

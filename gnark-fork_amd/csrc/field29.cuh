@@ -58,6 +58,9 @@ struct Fp29Cfg {
     // 2^256 mod p as a 29-bit-limb integer: mul(x * 2^261, C_OUT) = x * 2^256
     static constexpr uint32_t C_OUT[9] = {0x058f0d9du, 0x1aea1c6eu, 0x11c2cf74u, 0x11d651ebu, 0x1462c0a7u,
                                           0x11b7bc3cu, 0x1cbd99bau, 0x183340fbu, 0x000e0a77u};
+    // 2^266 mod p as limbs: mul(x * 2^256 (unpacked), C_LOAD) = x * 2^261 (from_std)
+    static constexpr uint32_t C_LOAD[9] = {0x13349ca1u, 0x1a5d84a8u, 0x0a3e5cacu, 0x100249e0u, 0x12b951e8u,
+                                           0x0e92d304u, 0x14cb95b3u, 0x041b9d3du, 0x00058003u};
     // 2^261 mod p in the gnark 32-bit layout: mont256(x * 2^256, C_IN) = x * 2^261
     static constexpr uint32_t C_IN[8] = {0x157ccc21u, 0x4e8384ebu, 0x0ce148c3u, 0xfb90a602u,
                                          0x819caa36u, 0x5301fa84u, 0x563d4475u, 0x0dc83629u};
@@ -96,6 +99,9 @@ struct FpBls28Cfg {
     static constexpr uint32_t C_OUT[14] = {0x0002fffdu, 0x00900000u, 0x0c000276u, 0x0000bc40u, 0x08baebf4u,
                                            0x05753c75u, 0x055f4898u, 0x07052574u, 0x07ce5853u, 0x056ec6d7u,
                                            0x071a97a2u, 0x0e4935c0u, 0x0ec3fa80u, 0x00015f65u};
+    static constexpr uint32_t C_LOAD[14] = {0x080e6299u, 0x03500034u, 0x0eb12856u, 0x0deb2699u, 0x0c988670u,
+                                            0x04ef6697u, 0x070983e8u, 0x0a4e6fe9u, 0x03e8a053u, 0x0ecf271eu,
+                                            0x0c20d323u, 0x06eb6385u, 0x047f1286u, 0x000156dau};  // 2^400 mod p
     static constexpr uint32_t C_IN[12] = {0x0347fcb8u, 0x19d80000u, 0x6d2002b1u, 0x12e00cdeu, 0xa2090c72u, 0x37669f83u,
                                           0xda0f73e0u, 0x09b09b42u, 0x8f1297bbu, 0xa7c515d9u, 0xfcfa012cu, 0x0577a659u};
     static constexpr uint32_t KP[8][14] = {
@@ -609,6 +615,54 @@ __device__ __forceinline__ void xyzz29_madd(Xyzz29& p, const Fp29& x, const Fp29
 template <class C>
 __device__ __forceinline__ Xyzz<Fe<typename C::Std>> to_std(const XyzzL<C>& p) {
     return Xyzz<Fe<typename C::Std>>{to_std(p.x), to_std(p.y), to_std(p.zz), to_std(p.zzz)};
+}
+
+// gnark form (x R mod p, canonical) -> x R' mod p (< 1.01 p, normalised): one
+// product by C_LOAD = R'^2 / R mod p.  Zero stays exactly zero (infinity's ZZ).
+template <class C>
+__device__ __forceinline__ Fl<C> from_std(const Fe<typename C::Std>& v) {
+    return mul(unpack_l<C>(v), fl_const<C>(C::C_LOAD));
+}
+template <class C>
+__device__ __forceinline__ XyzzL<C> from_std(const Xyzz<Fe<typename C::Std>>& p) {
+    return XyzzL<C>{from_std<C>(p.x), from_std<C>(p.y), from_std<C>(p.zz), from_std<C>(p.zzz)};
+}
+
+// dbl-2008-s-1 (a = 0) of an XYZZ point, coordinates < 7 p normalised in and
+// out (bounds for BN254's M = 169.28 p; BLS12-381's M = 2520 p only helps)
+template <class C>
+__device__ __noinline__ XyzzL<C> xyzzl_dbl(const XyzzL<C>& p) {  // rare (P = Q): kept out of line
+    const Fl<C> U = add(p.y, p.y);                     // < 14p
+    const Fl<C> V = sqr(U);                            // < 196/169.28 p + p < 2.16p
+    const Fl<C> W = mul(U, V);                         // < 1.18p
+    const Fl<C> S = mul(p.x, V);                       // < 1.09p
+    const Fl<C> xx = sqr(p.x);                         // < 1.29p
+    const Fl<C> M = add(xx, add(xx, xx));              // < 3.87p
+    const Fl<C> X3 = sub<4>(sqr(M), add(S, S));        // sqr < 1.09p, 2S < 2.18p: < 5.09p
+    const Fl<C> D = sub<7>(S, X3);                     // < 8.09p
+    const Fl<C> Y3 = sub<3>(mul(M, D), mul(W, p.y));   // M D < 1.19p, W y < 1.05p: < 4.19p
+    return XyzzL<C>{X3, Y3, mul(V, p.zz), mul(W, p.zzz)};
+}
+
+// p + q, add-2008-s (XYZZ); coordinates < 7 p normalised in, out X3 < 6.11p,
+// Y3 < 1.25p, ZZ3, ZZZ3 < 1.01p.  Used where bucket sums meet (level 2 and the
+// weighted bucket reduction), not in the mixed-add hot loop.
+template <class C>
+__device__ __forceinline__ XyzzL<C> xyzzl_add(const XyzzL<C>& p, const XyzzL<C>& q) {
+    if (is_inf_l(q)) return p;
+    if (is_inf_l(p)) return q;
+    const Fl<C> U1 = mul(p.x, q.zz), U2 = mul(q.x, p.zz);      // < 49/169.28 p + p < 1.29p
+    const Fl<C> S1 = mul(p.y, q.zzz), S2 = mul(q.y, p.zzz);    // < 1.29p
+    const Fl<C> P = sub<3>(U2, U1), R = sub<3>(S2, S1);        // < 4.29p
+    if (is_zero_mod(P, 5)) return is_zero_mod(R, 5) ? xyzzl_dbl(p) : inf_l<C>();
+    const Fl<C> PP = sqr(P);                                   // < 18.4/169.28 p + p < 1.11p
+    const Fl<C> PPP = mul(P, PP);                              // < 1.03p
+    const Fl<C> Q = mul(U1, PP);                               // < 1.01p
+    const Fl<C> X3 = sub<5>(sqr(R), add(PPP, add(Q, Q)));      // PPP + 2Q < 3.05p: < 6.11p
+    // Y3 = R (Q - X3) - S1 PPP as R (Q + 8p - X3) + S1 (3p - PPP), one reduction
+    // (the operands' column bound as in xyzzl_madd: R < 4.29p < 9.09p, S1 < 7p)
+    const Fl<C> Y3 = mul2(R, sub_nn<8>(Q, X3), S1, sub_nn<3>(Fl<C>{}, PPP));  // < 1.25p
+    return XyzzL<C>{X3, Y3, mul(mul(p.zz, q.zz), PP), mul(mul(p.zzz, q.zzz), PPP)};
 }
 
 // ---------------------------------------------------------------------------

@@ -92,11 +92,6 @@ struct gg_groth16_pk {
     bool share_AK = false, share_B = false;
     DevBuf wires, sa, sb, sc;
     hipStream_t s0 = nullptr, s1 = nullptr, s2 = nullptr, s3 = nullptr, s4 = nullptr;
-    // sort streams restricted to a CU subset (GG_SORT_CUS > 0): the HBM-bound
-    // sorts then run beside the VALU-bound NTTs / accumulations instead of
-    // taking every CU in turn; ev[k] hands the inputs over from the task stream
-    hipStream_t ss[3] = {nullptr, nullptr, nullptr};
-    hipEvent_t sev[3] = {nullptr, nullptr, nullptr};
     std::unique_ptr<Stager> stager;  // host inputs -> HBM (created on first host-input prove)
     int device = 0;
     std::mutex mu;
@@ -108,10 +103,8 @@ struct gg_groth16_pk {
         if (Z) gg_msm_base_release(Z);
         if (B2) gg_msm_base_release(B2);
         if (dom) gg_domain_release(dom);
-        for (hipStream_t x : {s0, s1, s2, s3, s4, ss[0], ss[1], ss[2]})
+        for (hipStream_t x : {s0, s1, s2, s3, s4})
             if (x) (void)hipStreamDestroy(x);
-        for (hipEvent_t e : sev)
-            if (e) (void)hipEventDestroy(e);
     }
 };
 
@@ -375,40 +368,6 @@ struct Joiner {
     }
 };
 
-// CUs the sort streams may use (GG_SORT_CUS; 0 = all, the default)
-static int sort_cus() {
-    static const int v = [] {
-        const char* e = getenv("GG_SORT_CUS");
-        return e ? std::max(0, atoi(e)) : 0;
-    }();
-    return v;
-}
-// the key's masked sort streams: `cus` CUs spread evenly over the device's CUs
-static void ensure_sort_streams(gg_groth16_pk* pk, int cus) {
-    if (pk->ss[0]) return;
-    int total = 0;
-    GG_HIP(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, pk->device));
-    cus = std::min(cus, total);
-    std::vector<uint32_t> mask((total + 31) / 32, 0u);
-    for (int k = 0; k < cus; k++) {
-        const int cu = (int)((long long)k * total / cus);
-        mask[cu / 32] |= 1u << (cu % 32);
-    }
-    for (int k = 0; k < 3; k++) {
-        GG_HIP(hipExtStreamCreateWithCUMask(&pk->ss[k], (uint32_t)mask.size(), mask.data()));
-        GG_HIP(hipEventCreateWithFlags(&pk->sev[k], hipEventDisableTiming));
-    }
-}
-// the stream a sort of task stream `task` runs on (k: 0 A/K, 1 B, 2 Z), after
-// the work already enqueued on `task`
-static hipStream_t sort_stream(gg_groth16_pk* pk, int k, hipStream_t task) {
-    if (!sort_cus()) return task;
-    ensure_sort_streams(pk, sort_cus());
-    GG_HIP(hipEventRecord(pk->sev[k], task));
-    GG_HIP(hipStreamWaitEvent(pk->ss[k], pk->sev[k], 0));
-    return pk->ss[k];
-}
-
 // Uploads the solution and runs computeH + the five MSMs of `pk` (a shard, or
 // the whole key).  Host inputs go through the key's pinned stager: the wires
 // first (the MSM sorts start as soon as they land), then A, B, C from the H
@@ -527,11 +486,7 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
         double b = now_ms();
         t_h = b - a;
         if (h_dev_out) GG_HIP(hipMemcpyAsync(h_dev_out, A, nbytes, hipMemcpyDeviceToDevice, pk->s1));
-        if (n > 1) {
-            MsmSort* sZ = msm_own_sort(pk->Z);
-            msm_prepare_dev(pk->Z, sZ, A + pk->z_lo, sort_stream(pk, 2, pk->s1));
-            msm_finish_dev(pk->Z, sZ, out.z, pk->s1);
-        }
+        if (n > 1) msm_device(pk->Z, A + pk->z_lo, out.z, pk->s1);
         t_z = now_ms() - b;
     }));
     // wire sorts, enqueued from this thread before any finisher waits on their
@@ -542,8 +497,8 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
         sB = msm_own_sort(pk->B);
         sK = pk->share_AK ? sAK : msm_own_sort(pk->K);
         sB2 = pk->share_B ? sB : msm_own_sort(pk->B2);
-        msm_prepare_dev(pk->A, sAK, wdev, sort_stream(pk, 0, pk->s2));
-        msm_prepare_dev(pk->B, sB, wdev, sort_stream(pk, 1, pk->s3));
+        msm_prepare_dev(pk->A, sAK, wdev, pk->s2);
+        msm_prepare_dev(pk->B, sB, wdev, pk->s3);
         if (!pk->share_AK) msm_prepare_dev(pk->K, sK, wdev, pk->s4);
         if (!pk->share_B) msm_prepare_dev(pk->B2, sB2, wdev, pk->s0);
     })();

@@ -428,6 +428,96 @@ __global__ void __launch_bounds__(256) k_bucket_combine(const Xyzz<F>* head, con
     if (lane == 0) st(out, acc);
 }
 
+// Level 2 and the weighted bucket sum in one pass, for the groups that
+// accumulate in a reduced-radix form (BN254 / BLS12-381 G1): thread t of
+// precompute group j walks the natural buckets [s L, (s+1) L) (s = t mod T) from
+// the top, forms each bucket's sum from its range partials as k_bucket_combine
+// does (a direct bucket from S, else the first range's head or tail plus the
+// later heads -- after k_range_tree for heavy buckets), and keeps the running
+// sum R and the sum of running sums A = sum_i (i + 1) S_{sL+i}, all in radix
+// form (one lane per segment: every lane busy, no quads).  Writes
+// D_s = A_s - L R_s and R_s in gnark's form; the group's weighted sum is then
+// sum_s D_s + L sum_s (s + 1) R_s (msm_finish).
+template <class F>
+__global__ void __launch_bounds__(256, 2) k_bucket_segsum(const Xyzz<F>* head, const Xyzz<F>* tail,
+                                                          const Xyzz<F>* S, const uint32_t* offsets,
+                                                          uint32_t nb_total, int c, uint32_t K, uint32_t nbg,
+                                                          int logL, uint32_t T, uint32_t G, Xyzz<F>* Dout,
+                                                          Xyzz<F>* Rout) {
+    using C = typename RadixOf<F>::C;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= G * T) return;
+    const uint32_t j = t / T, sg = t - j * T;
+    const uint32_t E = offsets[nb_total];
+    // One addition per step, chosen per lane by a small state machine, so the
+    // kernel holds ONE inlined xyzzl_add (the code of several would overflow
+    // the instruction cache) and lanes in different phases still add together:
+    //   NEXT: start bucket i (its first partial), HEAD: sb += head[r],
+    //   RUN: R += sb, ACC: A += R, DBL: X = 2X (L R), FIN: D = A - L R
+    enum { NEXT, HEAD, RUN, ACC, DBL, FIN, DONE };
+    XyzzL<C> R = inf_l<C>(), A = inf_l<C>(), sb = inf_l<C>();
+    int i = (1 << logL) - 1, ph = NEXT, k = 0;
+    uint32_t r = 0, rend = 0;
+    while (ph != DONE) {
+        if (ph == NEXT) {
+            if (i < 0) {
+                ph = is_inf_l(R) ? FIN : DBL;
+                sb = R;  // X = R, doubled logL times, then negated
+                continue;
+            }
+            const uint32_t B = j * nbg + ((uint32_t)sg << logL) + (uint32_t)i;
+            const BucketSpan sp = bucket_span(offsets, bucket_perm(B, c), E, K);
+            if (sp.empty) {
+                ph = ACC;
+            } else {
+                sb = from_std<C>(ld(sp.direct ? S + B : (sp.first ? head : tail) + sp.t0));
+                r = sp.t0 + 1;
+                rend = sp.direct ? sp.t0 : (sp.t1 - sp.t0 > LIGHT ? sp.t0 + 1 : sp.t1);  // heavy: tree result
+                ph = r <= rend ? HEAD : RUN;
+            }
+            continue;
+        }
+        XyzzL<C> x, y;
+        if (ph == HEAD) {
+            x = sb;
+            y = from_std<C>(ld(head + r));
+        } else if (ph == RUN) {
+            x = R;
+            y = sb;
+        } else if (ph == ACC) {
+            x = A;
+            y = R;
+        } else if (ph == DBL) {
+            x = sb;
+            y = sb;
+        } else {  // FIN: A + (-(L R)), y < 7p
+            x = A;
+            y = sb;
+            if (!is_inf_l(y)) y.y = sub<8>(Fl<C>{}, y.y);
+        }
+        const XyzzL<C> z = xyzzl_add(x, y);
+        if (ph == HEAD) {
+            sb = z;
+            if (++r > rend) ph = RUN;
+        } else if (ph == RUN) {
+            R = z;
+            ph = ACC;
+        } else if (ph == ACC) {
+            A = z;
+            i--;
+            ph = NEXT;
+        } else if (ph == DBL) {
+            sb = z;
+            if (++k == logL) ph = FIN;
+        } else {
+            A = z;
+            ph = DONE;
+        }
+    }
+    st(Dout + t, to_std(A));
+    st(Rout + t, to_std(R));
+}
+
 // copy a list of small device arrays into one contiguous staging buffer
 template <class F>
 struct GatherList {
@@ -587,7 +677,7 @@ struct MsmSort {
 // Accumulation / reduction scratch of one MSM in flight: range partials
 // (head, tail), range -> bucket map, dense bucket sums S, reduction arena.
 struct MsmScratch {
-    DevBuf head, tail, tbucket, S, arena, scal;
+    DevBuf head, tail, tbucket, S, arena, scal, seg;
 };
 // Everything one MSM needs besides the (read-only) base: several MSMs over one
 // base run concurrently on different streams with one MsmWork each.
@@ -800,6 +890,42 @@ inline Xyzz<F> bucket_reduce_2d(size_t nb, const Xyzz<F>* S, MsmScratch* scr, hi
     return acc;
 }
 
+// sum of n (a power of two) points by block-wide tree sums (k_reduce_block),
+// 256 -> 1 per round, the last <= 256 on the host
+template <class F>
+inline Xyzz<F> tree_sum(const Xyzz<F>* X, size_t n, MsmScratch* scr, hipStream_t st) {
+    scr->arena.reserve((n / 256 + 2) * 2 * sizeof(Xyzz<F>));
+    Xyzz<F>* buf[2] = {scr->arena.as<Xyzz<F>>(), scr->arena.as<Xyzz<F>>() + n / 256 + 1};
+    const Xyzz<F>* in = X;
+    int k = 0;
+    while (n > 256) {
+        RedJobs<F> J;
+        J.n = 1;
+        const uint32_t bc = (uint32_t)(n / 256);
+        J.j[0] = RedJob<F>{in, buf[k], 256u, bc, 1u, 256u, 256u, bc};
+        hipLaunchKernelGGL(k_reduce_block<F>, dim3(bc), dim3(256), 0, st, J);
+        GG_HIP(hipGetLastError());
+        in = buf[k];
+        k ^= 1;
+        n = bc;
+    }
+    std::vector<Xyzz<F>> h(n);
+    GG_HIP(hipMemcpyAsync(h.data(), in, n * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st));
+    GG_HIP(hipStreamSynchronize(st));
+    Xyzz<F> acc = Xyzz<F>::inf();
+    for (const auto& x : h) acc = xyzz_add(acc, x);
+    return acc;
+}
+
+// level 2 + bucket reduction through k_bucket_segsum (reduced-radix G1 groups);
+// GG_MSM_SEGSUM=0 keeps k_bucket_combine + bucket_reduce_2d
+template <class F>
+constexpr bool kSegsumGroup = RadixOf<F>::on && (std::is_same<F, Fp>::value || std::is_same<F, FpBls>::value);
+inline bool segsum_enabled() {
+    static const bool on = !(getenv("GG_MSM_SEGSUM") && atoi(getenv("GG_MSM_SEGSUM")) == 0);
+    return on;
+}
+
 // Entries per accumulation range (one thread each).  Every range costs the same,
 // so the grid runs in whole "rounds" of the chip's concurrent threads C (occupancy
 // of k_accum_range<F> x CUs x 256): R = entries / (C K_pref) rounds, rounded, and
@@ -866,6 +992,33 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
         GG_HIP(hipGetLastError());
         stride *= fan;
     }
+    const size_t nbg = nb / (size_t)b->G;
+    if constexpr (kSegsumGroup<F>) {
+        if (segsum_enabled()) {
+            // level 2 and the weighted sums in one radix-form pass (k_bucket_segsum)
+            const int logL = std::min(4, 31 - __builtin_clz((unsigned)nbg));
+            const uint32_t L = 1u << logL, Tg = (uint32_t)(nbg >> logL), G = (uint32_t)b->G;
+            scr->seg.reserve(2 * (size_t)G * Tg * sizeof(Xyzz<F>));
+            Xyzz<F>* D = scr->seg.as<Xyzz<F>>();
+            Xyzz<F>* Rs = D + (size_t)G * Tg;
+            hipLaunchKernelGGL(k_bucket_segsum<F>, dim3(grid_for((size_t)G * Tg, 256)), dim3(256), 0, st,
+                               (const Xyzz<F>*)head, (const Xyzz<F>*)scr->tail.p, (const Xyzz<F>*)S, offs,
+                               (uint32_t)nb, b->c, K, (uint32_t)nbg, logL, Tg, G, D, Rs);
+            GG_HIP(hipGetLastError());
+            ps_acc2.stop(st);
+            ProfScope ps_red("msm_reduce", st, (double)nb);
+            // per group: sum_s D_s + L sum_s (s + 1) R_s, then sum_j 2^(j c) of them
+            Xyzz<F> res = Xyzz<F>::inf();
+            for (int jg = b->G - 1; jg >= 0; jg--) {
+                for (int k = 0; k < b->c && !res.is_inf() && jg < b->G - 1; k++) res = xyzz_dbl(res);
+                Xyzz<F> w = bucket_reduce_2d<F>(Tg, (const Xyzz<F>*)Rs + (size_t)jg * Tg, scr, st);
+                for (uint32_t k = 1; k < L && !w.is_inf(); k <<= 1) w = xyzz_dbl(w);
+                res = xyzz_add(res, xyzz_add(w, tree_sum<F>(D + (size_t)jg * Tg, Tg, scr, st)));
+            }
+            ps_red.stop(st);
+            return res;
+        }
+    }
     hipLaunchKernelGGL(k_bucket_combine<F>, dim3(grid_for(4 * nb, 256)), dim3(256), 0, st, (const Xyzz<F>*)head,
                        (const Xyzz<F>*)scr->tail.p, offs, (uint32_t)nb, b->c, K, S);
     GG_HIP(hipGetLastError());
@@ -873,7 +1026,6 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
     // ---- bucket reduction: sum_b (b+1) S_b
     ProfScope ps_red("msm_reduce", st, (double)nb);
     // one weighted sum per precompute group, then sum_j 2^(j c) R_j by Horner
-    const size_t nbg = nb / (size_t)b->G;
     Xyzz<F> res = Xyzz<F>::inf();
     for (int j = b->G - 1; j >= 0; j--) {
         for (int k = 0; k < b->c && !res.is_inf() && j < b->G - 1; k++) res = xyzz_dbl(res);
