@@ -631,7 +631,7 @@ __device__ __forceinline__ XyzzL<C> from_std(const Xyzz<Fe<typename C::Std>>& p)
 // dbl-2008-s-1 (a = 0) of an XYZZ point, coordinates < 7 p normalised in and
 // out (bounds for BN254's M = 169.28 p; BLS12-381's M = 2520 p only helps)
 template <class C>
-__device__ __noinline__ XyzzL<C> xyzzl_dbl(const XyzzL<C>& p) {  // rare (P = Q): kept out of line
+__device__ __forceinline__ XyzzL<C> xyzzl_dbl(const XyzzL<C>& p) {
     const Fl<C> U = add(p.y, p.y);                     // < 14p
     const Fl<C> V = sqr(U);                            // < 196/169.28 p + p < 2.16p
     const Fl<C> W = mul(U, V);                         // < 1.18p

@@ -428,90 +428,77 @@ __global__ void __launch_bounds__(256) k_bucket_combine(const Xyzz<F>* head, con
     if (lane == 0) st(out, acc);
 }
 
-// Level 2 and the weighted bucket sum in one pass, for the groups that
-// accumulate in a reduced-radix form (BN254 / BLS12-381 G1): thread t of
-// precompute group j walks the natural buckets [s L, (s+1) L) (s = t mod T) from
-// the top, forms each bucket's sum from its range partials as k_bucket_combine
-// does (a direct bucket from S, else the first range's head or tail plus the
-// later heads -- after k_range_tree for heavy buckets), and keeps the running
-// sum R and the sum of running sums A = sum_i (i + 1) S_{sL+i}, all in radix
-// form (one lane per segment: every lane busy, no quads).  Writes
-// D_s = A_s - L R_s and R_s in gnark's form; the group's weighted sum is then
-// sum_s D_s + L sum_s (s + 1) R_s (msm_finish).
+// Level 2 and the weighted bucket sums in the reduced-radix form, for the
+// groups that accumulate in it (BN254 / BLS12-381 G1): one lane per bucket or
+// per segment (every lane busy) instead of quad-cooperative adds.
+// k_bucket_sum_r: lane B (natural bucket id, all groups) forms the bucket's sum
+// from its range partials as k_bucket_combine does (a direct bucket from S,
+// else the first range's head or tail plus the later heads -- after
+// k_range_tree for heavy buckets) and stores it in radix form, laid out
+// [i][t] for bucket B = t L + i so that k_bucket_runsum's loads coalesce.
 template <class F>
-__global__ void __launch_bounds__(256, 2) k_bucket_segsum(const Xyzz<F>* head, const Xyzz<F>* tail,
-                                                          const Xyzz<F>* S, const uint32_t* offsets,
-                                                          uint32_t nb_total, int c, uint32_t K, uint32_t nbg,
-                                                          int logL, uint32_t T, uint32_t G, Xyzz<F>* Dout,
-                                                          Xyzz<F>* Rout) {
+__global__ void __launch_bounds__(256) k_bucket_sum_r(const Xyzz<F>* head, const Xyzz<F>* tail, const Xyzz<F>* S,
+                                                       const uint32_t* offsets, uint32_t nb_total, int c, uint32_t K,
+                                                       int logL, XyzzL<typename RadixOf<F>::C>* Sr) {
+    using C = typename RadixOf<F>::C;
+    const uint32_t B = blockIdx.x * blockDim.x + threadIdx.x;
+    if (B >= nb_total) return;
+    const uint32_t nseg = nb_total >> logL;
+    const BucketSpan sp = bucket_span(offsets, bucket_perm(B, c), offsets[nb_total], K);
+    XyzzL<C> acc = inf_l<C>();
+    if (!sp.empty) {
+        acc = from_std<C>(ld(sp.direct ? S + B : (sp.first ? head : tail) + sp.t0));
+        const uint32_t rend = sp.direct ? sp.t0 : (sp.t1 - sp.t0 > LIGHT ? sp.t0 + 1 : sp.t1);  // heavy: tree result
+        for (uint32_t r = sp.t0 + 1; r <= rend; r++) acc = xyzzl_add(acc, from_std<C>(ld(head + r)));
+    }
+    st(Sr + (size_t)(B & ((1u << logL) - 1)) * nseg + (B >> logL), acc);
+}
+
+// k_bucket_runsum: lane t walks the L buckets of segment t (group j = t / T)
+// from the top, R = running sum, A = sum of the running sums =
+// sum_i (i + 1) S_{tL+i}; then D_t = A - L R.  Writes D_t and R_t in gnark's
+// form: the group's weighted sum is sum_t D_t + L sum_t (t + 1) R_t.  Every lane
+// runs the same step sequence through ONE inlined add (the code of several
+// would overflow the instruction cache): R += S_i, A += R (L times), X = 2X
+// (log L times, X = R), A += -X.
+template <class F>
+__global__ void __launch_bounds__(256) k_bucket_runsum(const XyzzL<typename RadixOf<F>::C>* Sr, uint32_t nseg, int logL,
+                                                        Xyzz<F>* Dout, Xyzz<F>* Rout) {
     using C = typename RadixOf<F>::C;
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= G * T) return;
-    const uint32_t j = t / T, sg = t - j * T;
-    const uint32_t E = offsets[nb_total];
-    // One addition per step, chosen per lane by a small state machine, so the
-    // kernel holds ONE inlined xyzzl_add (the code of several would overflow
-    // the instruction cache) and lanes in different phases still add together:
-    //   NEXT: start bucket i (its first partial), HEAD: sb += head[r],
-    //   RUN: R += sb, ACC: A += R, DBL: X = 2X (L R), FIN: D = A - L R
-    enum { NEXT, HEAD, RUN, ACC, DBL, FIN, DONE };
-    XyzzL<C> R = inf_l<C>(), A = inf_l<C>(), sb = inf_l<C>();
-    int i = (1 << logL) - 1, ph = NEXT, k = 0;
-    uint32_t r = 0, rend = 0;
-    while (ph != DONE) {
-        if (ph == NEXT) {
-            if (i < 0) {
-                ph = is_inf_l(R) ? FIN : DBL;
-                sb = R;  // X = R, doubled logL times, then negated
-                continue;
-            }
-            const uint32_t B = j * nbg + ((uint32_t)sg << logL) + (uint32_t)i;
-            const BucketSpan sp = bucket_span(offsets, bucket_perm(B, c), E, K);
-            if (sp.empty) {
-                ph = ACC;
-            } else {
-                sb = from_std<C>(ld(sp.direct ? S + B : (sp.first ? head : tail) + sp.t0));
-                r = sp.t0 + 1;
-                rend = sp.direct ? sp.t0 : (sp.t1 - sp.t0 > LIGHT ? sp.t0 + 1 : sp.t1);  // heavy: tree result
-                ph = r <= rend ? HEAD : RUN;
-            }
-            continue;
-        }
+    if (t >= nseg) return;
+    const int L = 1 << logL, steps = 2 * L + logL + 1;
+    XyzzL<C> R = inf_l<C>(), A = inf_l<C>(), X, cur = ld(Sr + (size_t)(L - 1) * nseg + t), nxt = cur;
+    for (int st = 0; st < steps; st++) {
         XyzzL<C> x, y;
-        if (ph == HEAD) {
-            x = sb;
-            y = from_std<C>(ld(head + r));
-        } else if (ph == RUN) {
-            x = R;
-            y = sb;
-        } else if (ph == ACC) {
+        if (st < 2 * L) {
+            const int i = L - 1 - (st >> 1);
+            if (st & 1) {
+                x = A;
+                y = R;
+            } else {
+                cur = nxt;
+                if (i > 0) nxt = ld(Sr + (size_t)(i - 1) * nseg + t);  // in flight during the two adds
+                x = R;
+                y = cur;
+            }
+        } else if (st < 2 * L + logL) {
+            if (st == 2 * L) X = R;
+            x = X;
+            y = X;
+        } else {
             x = A;
-            y = R;
-        } else if (ph == DBL) {
-            x = sb;
-            y = sb;
-        } else {  // FIN: A + (-(L R)), y < 7p
-            x = A;
-            y = sb;
-            if (!is_inf_l(y)) y.y = sub<8>(Fl<C>{}, y.y);
+            y = X;
+            if (!is_inf_l(y)) y.y = sub<8>(Fl<C>{}, y.y);  // -X (y < 7p)
         }
         const XyzzL<C> z = xyzzl_add(x, y);
-        if (ph == HEAD) {
-            sb = z;
-            if (++r > rend) ph = RUN;
-        } else if (ph == RUN) {
-            R = z;
-            ph = ACC;
-        } else if (ph == ACC) {
-            A = z;
-            i--;
-            ph = NEXT;
-        } else if (ph == DBL) {
-            sb = z;
-            if (++k == logL) ph = FIN;
+        if (st < 2 * L) {
+            if (st & 1) A = z;
+            else R = z;
+        } else if (st < 2 * L + logL) {
+            X = z;
         } else {
             A = z;
-            ph = DONE;
         }
     }
     st(Dout + t, to_std(A));
@@ -917,7 +904,7 @@ inline Xyzz<F> tree_sum(const Xyzz<F>* X, size_t n, MsmScratch* scr, hipStream_t
     return acc;
 }
 
-// level 2 + bucket reduction through k_bucket_segsum (reduced-radix G1 groups);
+// level 2 + bucket reduction through k_bucket_sum_r / k_bucket_runsum (reduced-radix G1 groups);
 // GG_MSM_SEGSUM=0 keeps k_bucket_combine + bucket_reduce_2d
 template <class F>
 constexpr bool kSegsumGroup = RadixOf<F>::on && (std::is_same<F, Fp>::value || std::is_same<F, FpBls>::value);
@@ -995,15 +982,19 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
     const size_t nbg = nb / (size_t)b->G;
     if constexpr (kSegsumGroup<F>) {
         if (segsum_enabled()) {
-            // level 2 and the weighted sums in one radix-form pass (k_bucket_segsum)
+            // level 2 and the weighted sums in radix form, a lane per bucket / segment
+            using C = typename RadixOf<F>::C;
             const int logL = std::min(4, 31 - __builtin_clz((unsigned)nbg));
             const uint32_t L = 1u << logL, Tg = (uint32_t)(nbg >> logL), G = (uint32_t)b->G;
-            scr->seg.reserve(2 * (size_t)G * Tg * sizeof(Xyzz<F>));
+            scr->seg.reserve(2 * (size_t)G * Tg * sizeof(Xyzz<F>) + nb * sizeof(XyzzL<C>));
             Xyzz<F>* D = scr->seg.as<Xyzz<F>>();
             Xyzz<F>* Rs = D + (size_t)G * Tg;
-            hipLaunchKernelGGL(k_bucket_segsum<F>, dim3(grid_for((size_t)G * Tg, 256)), dim3(256), 0, st,
-                               (const Xyzz<F>*)head, (const Xyzz<F>*)scr->tail.p, (const Xyzz<F>*)S, offs,
-                               (uint32_t)nb, b->c, K, (uint32_t)nbg, logL, Tg, G, D, Rs);
+            XyzzL<C>* Sr = reinterpret_cast<XyzzL<C>*>(Rs + (size_t)G * Tg);
+            hipLaunchKernelGGL(k_bucket_sum_r<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, (const Xyzz<F>*)head,
+                               (const Xyzz<F>*)scr->tail.p, (const Xyzz<F>*)S, offs, (uint32_t)nb, b->c, K, logL, Sr);
+            GG_HIP(hipGetLastError());
+            hipLaunchKernelGGL(k_bucket_runsum<F>, dim3(grid_for((size_t)G * Tg, 256)), dim3(256), 0, st,
+                               (const XyzzL<C>*)Sr, (uint32_t)(G * Tg), logL, D, Rs);
             GG_HIP(hipGetLastError());
             ps_acc2.stop(st);
             ProfScope ps_red("msm_reduce", st, (double)nb);

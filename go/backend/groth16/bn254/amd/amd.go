@@ -138,6 +138,17 @@ func (pk *ProvingKey) setupDevicePointers(nbPublic int, kWireIndex []uint32) err
 	return nil
 }
 
+// SetHBMBudget caps (bytes per device, 0 = the free HBM less a reserve) what
+// the precomputed tables of keys created afterwards may take: a key that would
+// not fit stores every G-th window shift instead (gg_set_hbm_budget,
+// DESIGN.md §3), e.g. a 2^25-domain key, or a Groth16 and a PlonK key on one GPU.
+func SetHBMBudget(bytes uint64) error {
+	if C.gg_set_hbm_budget(C.size_t(bytes)) != C.GG_OK {
+		return lastError()
+	}
+	return nil
+}
+
 // Release frees the HBM-resident key (the icicle path never frees it).
 func (pk *ProvingKey) Release() {
 	setupMu.Lock()
