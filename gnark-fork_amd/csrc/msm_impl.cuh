@@ -909,8 +909,8 @@ inline Xyzz<F> tree_sum(const Xyzz<F>* X, size_t n, MsmScratch* scr, hipStream_t
 template <class F>
 constexpr bool kSegsumGroup = RadixOf<F>::on && (std::is_same<F, Fp>::value || std::is_same<F, FpBls>::value);
 inline bool segsum_enabled() {
-    static const bool on = !(getenv("GG_MSM_SEGSUM") && atoi(getenv("GG_MSM_SEGSUM")) == 0);
-    return on;
+    const char* e = getenv("GG_MSM_SEGSUM");  // per MSM: tests switch it
+    return !(e && atoi(e) == 0);
 }
 
 // Entries per accumulation range (one thread each).  Every range costs the same,
@@ -980,11 +980,14 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
         stride *= fan;
     }
     const size_t nbg = nb / (size_t)b->G;
+    // segments of L = 2^logL buckets, >= 2^17 of them per group (a lane each:
+    // fewer leave the chip idle while each lane walks its chain); below 2^18
+    // buckets per group the quad path is faster (MI355X: 2^20 MSM, c = 17)
+    const int logL = std::min(4, 31 - __builtin_clz((unsigned)std::max<size_t>(nbg, 1)) - 17);
     if constexpr (kSegsumGroup<F>) {
-        if (segsum_enabled()) {
+        if (segsum_enabled() && logL >= 1) {
             // level 2 and the weighted sums in radix form, a lane per bucket / segment
             using C = typename RadixOf<F>::C;
-            const int logL = std::min(4, 31 - __builtin_clz((unsigned)nbg));
             const uint32_t L = 1u << logL, Tg = (uint32_t)(nbg >> logL), G = (uint32_t)b->G;
             scr->seg.reserve(2 * (size_t)G * Tg * sizeof(Xyzz<F>) + nb * sizeof(XyzzL<C>));
             Xyzz<F>* D = scr->seg.as<Xyzz<F>>();

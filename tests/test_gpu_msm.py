@@ -102,6 +102,25 @@ def test_msm_skewed_scalars(n, frac_one):
     assert base.msm(sc, n) == coracle.msm_g1(pts.tobytes(), sc.tobytes(), n)
 
 
+@pytest.mark.parametrize("seg", ["1", "0"])
+@pytest.mark.parametrize("n,c,dist", [(1 << 18, 20, "skew"), (1 << 18, 22, "witness"), (1 << 17, 19, "uniform")])
+def test_msm_radix_bucket_reduction(n, c, dist, seg, monkeypatch):
+    """Windows with >= 2^18 buckets take the radix-form level 2 + weighted sum
+    (k_bucket_sum_r / k_bucket_runsum, the 2^24 proof's path); GG_MSM_SEGSUM=0
+    the quad path: both bit-exact vs the C oracle, including heavy buckets
+    (half of all scalars on one value: k_range_tree first) and empty ones."""
+    from gnark_amd import msm
+    monkeypatch.setenv("GG_MSM_SEGSUM", seg)
+    pts = random_g1_points(n, 80 + c)
+    sc = random_fr_mont(n, 81 + c, "uniform" if dist == "skew" else dist)
+    if dist == "skew":
+        sc[: n // 2] = sc[0]
+    base = msm.MsmBase(msm.G1, pts, n, window_bits=c)
+    assert base.info()[1] == c
+    assert base.msm(sc, n) == coracle.msm_g1(pts.tobytes(), sc.tobytes(), n)
+    base.close()
+
+
 def test_msm_scalar_index_map():
     from gnark_amd import msm
     n, nw = 3000, 5000
