@@ -143,9 +143,31 @@ __global__ void __launch_bounds__(256) k_to_radix(Fe<typename C::Std>* v, size_t
 // a segment that starts and ends inside the range is a whole bucket, written
 // straight to S[brev(q)] (natural bucket order, see sort_entries).
 // tbucket[t] = bucket (sort order) of the range's first entry.
+// Partials are stored in the accumulator's own form (radix limbs for the
+// groups that accumulate in one): a flush is then a few stores instead of a
+// conversion (4 or 8 products), which matters because a wave executes the
+// flush whenever ANY of its lanes crosses a bucket boundary -- about every
+// other step at 2^24.  The consumers convert once, a lane per partial.
 template <class F>
-__device__ __forceinline__ void range_store(const Xyzz<F>& acc, bool first, bool last, uint32_t q, int c,
-                                            size_t t, Xyzz<F>* head, Xyzz<F>* tail, Xyzz<F>* S) {
+struct PartialOf {
+    using T = Xyzz<F>;
+};
+template <>
+struct PartialOf<Fp> {
+    using T = XyzzL<Fp29Cfg>;
+};
+template <>
+struct PartialOf<FpBls> {
+    using T = XyzzL<FpBls28Cfg>;
+};
+template <>
+struct PartialOf<Fp2> {
+    using T = Xyzz2_29;
+};
+
+template <class P>
+__device__ __forceinline__ void range_store(const P& acc, bool first, bool last, uint32_t q, int c, size_t t,
+                                            P* head, P* tail, P* S) {
     if (first) st(head + t, acc);
     else if (last) st(tail + t, acc);
     else st(S + bucket_perm(q, c), acc);
@@ -168,8 +190,9 @@ constexpr int kAccumWaves = (GG_G2_WAVES1 && std::is_same<F, Fp2>::value) || std
 template <class F>
 __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affine<F>* pts, const uint32_t* sorted,
                                                      const uint32_t* offsets, uint32_t nb, int c,
-                                                     uint32_t K, int skip_inf, Xyzz<F>* head,
-                                                     Xyzz<F>* tail, Xyzz<F>* S, uint32_t* tbucket) {
+                                                     uint32_t K, int skip_inf, typename PartialOf<F>::T* head,
+                                                     typename PartialOf<F>::T* tail, typename PartialOf<F>::T* S,
+                                                     uint32_t* tbucket) {
     const uint32_t E = offsets[nb];
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t e0w = (uint64_t)t * K;
@@ -190,7 +213,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
     uint32_t seg0 = e0;
     if constexpr (std::is_same<F, Fp>::value || std::is_same<F, FpBls>::value) {
         // G1: reduced-radix accumulator (field29.cuh; BN254 9 x 29, BLS12-381
-        // 14 x 28 bits); the base holds x R' mod p, partials leave in gnark's form
+        // 14 x 28 bits); the base holds x R' mod p, partials leave in radix form
         using C = typename RadixOf<F>::C;
         XyzzL<C> acc = inf_l<C>();
         uint32_t v = sorted[e0], vn = (e0 + 1 < e1) ? sorted[e0 + 1] : 0u;
@@ -204,7 +227,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                 if (e + 2 < e1) vn = sorted[e + 2];
             }
             if (e == bnd) {
-                range_store(to_std(acc), seg0 == e0, false, q, c, t, head, tail, S);
+                range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
                 acc = inf_l<C>();
                 seg0 = e;
                 do { q++; bnd = offsets[q + 1]; } while (bnd == e);
@@ -215,7 +238,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
             if (cv >> 31) y = sub_nn<2>(Fl<C>{}, y);  // 2p - y, limbs < 2^(B+1) (xyzzl_madd takes it)
             xyzzl_madd(acc, x, y);
         }
-        range_store(to_std(acc), seg0 == e0, true, q, c, t, head, tail, S);
+        range_store(acc, seg0 == e0, true, q, c, t, head, tail, S);
         return;
     }
     if constexpr (std::is_same<F, Fp2>::value) {
@@ -223,7 +246,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
         Xyzz2_29 acc = inf2_29();
         for (uint32_t e = e0; e < e1; e++) {
             if (e == bnd) {
-                range_store(to_std(acc), seg0 == e0, false, q, c, t, head, tail, S);
+                range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
                 acc = inf2_29();
                 seg0 = e;
                 do { q++; bnd = offsets[q + 1]; } while (bnd == e);
@@ -236,49 +259,51 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
             if (v >> 31) y = Fp2_29{sub<2>(Fp29{}, y.c0), sub<2>(Fp29{}, y.c1)};  // 2p - y
             xyzz2_29_madd(acc, x, y);
         }
-        range_store(to_std(acc), seg0 == e0, true, q, c, t, head, tail, S);
+        range_store(acc, seg0 == e0, true, q, c, t, head, tail, S);
         return;
     }
-    Xyzz<F> acc = Xyzz<F>::inf();
-    if constexpr (sizeof(F) <= 32) {
-        // G1: software pipeline, the next point is in flight while this one is added
-        uint32_t v = sorted[e0], vn = (e0 + 1 < e1) ? sorted[e0 + 1] : 0u;
-        Affine<F> p = ld(pts + (v & 0x7fffffffu));
-        for (uint32_t e = e0; e < e1; e++) {
-            Affine<F> qp = p;
-            const uint32_t cv = v;
-            if (e + 1 < e1) {
-                p = ld(pts + (vn & 0x7fffffffu));
-                v = vn;
-                if (e + 2 < e1) vn = sorted[e + 2];
-            }
-            if (e == bnd) {  // bucket boundary: flush [seg0, e) of bucket q
-                range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
-                acc = Xyzz<F>::inf();
-                seg0 = e;
-                do { q++; bnd = offsets[q + 1]; } while (bnd == e);
-            }
-            if (skip_inf && qp.is_inf()) continue;  // hole of a wire-indexed table
-            if (cv >> 31) qp.y = -qp.y;
-            xyzz_madd_inplace(acc, qp);
-        }
-    } else {
-        // G2: no room for a second point in registers
-        for (uint32_t e = e0; e < e1; e++) {
-            if (e == bnd) {
-                range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
-                acc = Xyzz<F>::inf();
-                seg0 = e;
-                do { q++; bnd = offsets[q + 1]; } while (bnd == e);
-            }
-            const uint32_t v = sorted[e];
+    if constexpr (std::is_same<typename PartialOf<F>::T, Xyzz<F>>::value) {  // gnark's form (BLS12-381 G2)
+        Xyzz<F> acc = Xyzz<F>::inf();
+        if constexpr (sizeof(F) <= 32) {
+            // G1: software pipeline, the next point is in flight while this one is added
+            uint32_t v = sorted[e0], vn = (e0 + 1 < e1) ? sorted[e0 + 1] : 0u;
             Affine<F> p = ld(pts + (v & 0x7fffffffu));
-            if (skip_inf && p.is_inf()) continue;
-            if (v >> 31) p.y = -p.y;
-            xyzz_madd_inplace(acc, p);
+            for (uint32_t e = e0; e < e1; e++) {
+                Affine<F> qp = p;
+                const uint32_t cv = v;
+                if (e + 1 < e1) {
+                    p = ld(pts + (vn & 0x7fffffffu));
+                    v = vn;
+                    if (e + 2 < e1) vn = sorted[e + 2];
+                }
+                if (e == bnd) {  // bucket boundary: flush [seg0, e) of bucket q
+                    range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
+                    acc = Xyzz<F>::inf();
+                    seg0 = e;
+                    do { q++; bnd = offsets[q + 1]; } while (bnd == e);
+                }
+                if (skip_inf && qp.is_inf()) continue;  // hole of a wire-indexed table
+                if (cv >> 31) qp.y = -qp.y;
+                xyzz_madd_inplace(acc, qp);
+            }
+        } else {
+            // G2: no room for a second point in registers
+            for (uint32_t e = e0; e < e1; e++) {
+                if (e == bnd) {
+                    range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
+                    acc = Xyzz<F>::inf();
+                    seg0 = e;
+                    do { q++; bnd = offsets[q + 1]; } while (bnd == e);
+                }
+                const uint32_t v = sorted[e];
+                Affine<F> p = ld(pts + (v & 0x7fffffffu));
+                if (skip_inf && p.is_inf()) continue;
+                if (v >> 31) p.y = -p.y;
+                xyzz_madd_inplace(acc, p);
+            }
         }
+        range_store(acc, seg0 == e0, true, q, c, t, head, tail, S);
     }
-    range_store(acc, seg0 == e0, true, q, c, t, head, tail, S);
 }
 
 // ---- quad-cooperative XYZZ add (latency-bound tree levels) -----------------
@@ -428,6 +453,33 @@ __global__ void __launch_bounds__(256) k_bucket_combine(const Xyzz<F>* head, con
     if (lane == 0) st(out, acc);
 }
 
+// k_range_tree over radix-form partials, a lane per slot (xyzzl_add)
+template <class F>
+__global__ void __launch_bounds__(256) k_range_tree_r(XyzzL<typename RadixOf<F>::C>* head, const uint32_t* tbucket,
+                                                      const uint32_t* offsets, uint32_t nb, uint32_t K,
+                                                      uint32_t stride, uint32_t fan) {
+    using C = typename RadixOf<F>::C;
+    const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t E = offsets[nb];
+    if ((uint64_t)p * K >= E) return;
+    const BucketSpan s = bucket_span(offsets, tbucket[p], E, K);
+    const uint32_t m = s.t1 - s.t0;
+    if (m <= LIGHT || p <= s.t0) return;
+    const uint32_t j = (uint32_t)p - (s.t0 + 1);
+    if (j % (fan * stride) || j + stride >= m) return;
+    XyzzL<C> acc = ld(head + p);
+    for (uint32_t k = 1; k < fan && j + k * stride < m; k++) acc = xyzzl_add(acc, ld(head + p + k * stride));
+    st(head + p, acc);
+}
+
+// partials in the accumulator's form -> gnark's (for the quad-cooperative path)
+template <class F>
+__global__ void __launch_bounds__(256) k_partials_to_std(const typename PartialOf<F>::T* in, size_t n,
+                                                         Xyzz<F>* out) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) st(out + i, to_std(ld(in + i)));
+}
+
 // Level 2 and the weighted bucket sums in the reduced-radix form, for the
 // groups that accumulate in it (BN254 / BLS12-381 G1): one lane per bucket or
 // per segment (every lane busy) instead of quad-cooperative adds.
@@ -437,9 +489,11 @@ __global__ void __launch_bounds__(256) k_bucket_combine(const Xyzz<F>* head, con
 // k_range_tree for heavy buckets) and stores it in radix form, laid out
 // [i][t] for bucket B = t L + i so that k_bucket_runsum's loads coalesce.
 template <class F>
-__global__ void __launch_bounds__(256) k_bucket_sum_r(const Xyzz<F>* head, const Xyzz<F>* tail, const Xyzz<F>* S,
-                                                       const uint32_t* offsets, uint32_t nb_total, int c, uint32_t K,
-                                                       int logL, XyzzL<typename RadixOf<F>::C>* Sr) {
+__global__ void __launch_bounds__(256) k_bucket_sum_r(const XyzzL<typename RadixOf<F>::C>* head,
+                                                       const XyzzL<typename RadixOf<F>::C>* tail,
+                                                       const XyzzL<typename RadixOf<F>::C>* S, const uint32_t* offsets,
+                                                       uint32_t nb_total, int c, uint32_t K, int logL,
+                                                       XyzzL<typename RadixOf<F>::C>* Sr) {
     using C = typename RadixOf<F>::C;
     const uint32_t B = blockIdx.x * blockDim.x + threadIdx.x;
     if (B >= nb_total) return;
@@ -447,9 +501,9 @@ __global__ void __launch_bounds__(256) k_bucket_sum_r(const Xyzz<F>* head, const
     const BucketSpan sp = bucket_span(offsets, bucket_perm(B, c), offsets[nb_total], K);
     XyzzL<C> acc = inf_l<C>();
     if (!sp.empty) {
-        acc = from_std<C>(ld(sp.direct ? S + B : (sp.first ? head : tail) + sp.t0));
+        acc = ld(sp.direct ? S + B : (sp.first ? head : tail) + sp.t0);
         const uint32_t rend = sp.direct ? sp.t0 : (sp.t1 - sp.t0 > LIGHT ? sp.t0 + 1 : sp.t1);  // heavy: tree result
-        for (uint32_t r = sp.t0 + 1; r <= rend; r++) acc = xyzzl_add(acc, from_std<C>(ld(head + r)));
+        for (uint32_t r = sp.t0 + 1; r <= rend; r++) acc = xyzzl_add(acc, ld(head + r));
     }
     st(Sr + (size_t)(B & ((1u << logL) - 1)) * nseg + (B >> logL), acc);
 }
@@ -665,6 +719,7 @@ struct MsmSort {
 // (head, tail), range -> bucket map, dense bucket sums S, reduction arena.
 struct MsmScratch {
     DevBuf head, tail, tbucket, S, arena, scal, seg;
+    DevBuf headP, tailP, SP;  // partials in the accumulator's form (radix groups)
 };
 // Everything one MSM needs besides the (read-only) base: several MSMs over one
 // base run concurrently on different streams with one MsmWork each.
@@ -949,19 +1004,30 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
     const uint32_t* offs = s->offsets.as<uint32_t>();
     const uint32_t K = range_length<F>((size_t)b->W * n);
     const size_t T = ((size_t)b->W * n + K - 1) / K;  // ranges (upper bound: digit-0 entries are not sorted)
+    using PT = typename PartialOf<F>::T;
+    constexpr bool kRadixP = !std::is_same<PT, Xyzz<F>>::value;  // partials in the accumulator's form
     scr->head.reserve((T + 1) * sizeof(Xyzz<F>));
     scr->tail.reserve((T + 1) * sizeof(Xyzz<F>));
     scr->tbucket.reserve((T + 1) * 4);
     scr->S.reserve(nb * sizeof(Xyzz<F>));
     Xyzz<F>* head = scr->head.as<Xyzz<F>>();
     Xyzz<F>* S = scr->S.as<Xyzz<F>>();
+    PT *hP = (PT*)head, *tP = scr->tail.as<PT>(), *SP = (PT*)S;
+    if constexpr (kRadixP) {
+        scr->headP.reserve((T + 1) * sizeof(PT));
+        scr->tailP.reserve((T + 1) * sizeof(PT));
+        scr->SP.reserve(nb * sizeof(PT));
+        hP = scr->headP.as<PT>();
+        tP = scr->tailP.as<PT>();
+        SP = scr->SP.as<PT>();
+    }
     {
         // per-group names: the Groth16 prove runs G1 and G2 accumulations at once
         const char* acc_name = sizeof(F) == sizeof(Fp) ? "msm_accum" : (sizeof(F) == sizeof(Fp2) ? "msm_accum_g2" : "msm_accum_bls");
         ProfScope ps_acc(acc_name, st, (double)n);
         hipLaunchKernelGGL(k_accum_range<F>, dim3(grid_for(T, 256)), dim3(256), 0, st, (const Affine<F>*)b->pts.p,
-                           s->sorted.as<uint32_t>(), offs, (uint32_t)nb, b->c, K, (int)b->has_inf, head,
-                           scr->tail.as<Xyzz<F>>(), S, scr->tbucket.as<uint32_t>());
+                           s->sorted.as<uint32_t>(), offs, (uint32_t)nb, b->c, K, (int)b->has_inf, hP, tP, SP,
+                           scr->tbucket.as<uint32_t>());
         GG_HIP(hipGetLastError());
         ps_acc.stop(st);
     }
@@ -972,13 +1038,6 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
     // ---- level 2: heavy buckets' ranges by a segmented tree (skew-robust,
     // log_fan(ranges) launches), then every bucket's partials into S
     ProfScope ps_acc2("msm_accum2", st, (double)n);
-    for (uint32_t stride = 1; max_ranges > LIGHT && stride < max_ranges;) {
-        const uint32_t fan = (stride == 1) ? 4u : 2u;
-        hipLaunchKernelGGL(k_range_tree<F>, dim3(grid_for(4 * T, 256)), dim3(256), 0, st, head,
-                           (const uint32_t*)scr->tbucket.p, offs, (uint32_t)nb, K, stride, fan);
-        GG_HIP(hipGetLastError());
-        stride *= fan;
-    }
     const size_t nbg = nb / (size_t)b->G;
     // segments of L = 2^logL buckets, >= 2^17 of them per group (a lane each:
     // fewer leave the chip idle while each lane walks its chain); below 2^18
@@ -988,13 +1047,20 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
         if (segsum_enabled() && logL >= 1) {
             // level 2 and the weighted sums in radix form, a lane per bucket / segment
             using C = typename RadixOf<F>::C;
+            for (uint32_t stride = 1; max_ranges > LIGHT && stride < max_ranges;) {
+                const uint32_t fan = (stride == 1) ? 4u : 2u;
+                hipLaunchKernelGGL(k_range_tree_r<F>, dim3(grid_for(T, 256)), dim3(256), 0, st, hP,
+                                   (const uint32_t*)scr->tbucket.p, offs, (uint32_t)nb, K, stride, fan);
+                GG_HIP(hipGetLastError());
+                stride *= fan;
+            }
             const uint32_t L = 1u << logL, Tg = (uint32_t)(nbg >> logL), G = (uint32_t)b->G;
             scr->seg.reserve(2 * (size_t)G * Tg * sizeof(Xyzz<F>) + nb * sizeof(XyzzL<C>));
             Xyzz<F>* D = scr->seg.as<Xyzz<F>>();
             Xyzz<F>* Rs = D + (size_t)G * Tg;
             XyzzL<C>* Sr = reinterpret_cast<XyzzL<C>*>(Rs + (size_t)G * Tg);
-            hipLaunchKernelGGL(k_bucket_sum_r<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, (const Xyzz<F>*)head,
-                               (const Xyzz<F>*)scr->tail.p, (const Xyzz<F>*)S, offs, (uint32_t)nb, b->c, K, logL, Sr);
+            hipLaunchKernelGGL(k_bucket_sum_r<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, (const XyzzL<C>*)hP,
+                               (const XyzzL<C>*)tP, (const XyzzL<C>*)SP, offs, (uint32_t)nb, b->c, K, logL, Sr);
             GG_HIP(hipGetLastError());
             hipLaunchKernelGGL(k_bucket_runsum<F>, dim3(grid_for((size_t)G * Tg, 256)), dim3(256), 0, st,
                                (const XyzzL<C>*)Sr, (uint32_t)(G * Tg), logL, D, Rs);
@@ -1012,6 +1078,21 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
             ps_red.stop(st);
             return res;
         }
+    }
+    if constexpr (kRadixP) {  // the quad path works on gnark's form
+        hipLaunchKernelGGL(k_partials_to_std<F>, dim3(grid_for(T + 1, 256)), dim3(256), 0, st, (const PT*)hP, T + 1,
+                           head);
+        hipLaunchKernelGGL(k_partials_to_std<F>, dim3(grid_for(T + 1, 256)), dim3(256), 0, st, (const PT*)tP, T + 1,
+                           scr->tail.as<Xyzz<F>>());
+        hipLaunchKernelGGL(k_partials_to_std<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, (const PT*)SP, nb, S);
+        GG_HIP(hipGetLastError());
+    }
+    for (uint32_t stride = 1; max_ranges > LIGHT && stride < max_ranges;) {
+        const uint32_t fan = (stride == 1) ? 4u : 2u;
+        hipLaunchKernelGGL(k_range_tree<F>, dim3(grid_for(4 * T, 256)), dim3(256), 0, st, head,
+                           (const uint32_t*)scr->tbucket.p, offs, (uint32_t)nb, K, stride, fan);
+        GG_HIP(hipGetLastError());
+        stride *= fan;
     }
     hipLaunchKernelGGL(k_bucket_combine<F>, dim3(grid_for(4 * nb, 256)), dim3(256), 0, st, (const Xyzz<F>*)head,
                        (const Xyzz<F>*)scr->tail.p, offs, (uint32_t)nb, b->c, K, S);
