@@ -209,7 +209,9 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
     }
     uint32_t q = lo;
     tbucket[t] = q;
-    uint32_t bnd = offsets[q + 1];
+    // the next boundary is loaded one flush ahead: a flush (taken by the whole
+    // wave when any lane crosses a boundary) then never waits on a load
+    uint32_t bnd = offsets[q + 1], bnd2 = offsets[min(q + 2, nb)];
     uint32_t seg0 = e0;
     if constexpr (std::is_same<F, Fp>::value || std::is_same<F, FpBls>::value) {
         // G1: reduced-radix accumulator (field29.cuh; BN254 9 x 29, BLS12-381
@@ -230,7 +232,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                 range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
                 acc = inf_l<C>();
                 seg0 = e;
-                do { q++; bnd = offsets[q + 1]; } while (bnd == e);
+                do { q++; bnd = bnd2; bnd2 = offsets[min(q + 2, nb)]; } while (bnd == e);
             }
             if (skip_inf && qp.is_inf()) continue;
             const Fl<C> x = unpack_l<C>(qp.x);
@@ -249,7 +251,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                 range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
                 acc = inf2_29();
                 seg0 = e;
-                do { q++; bnd = offsets[q + 1]; } while (bnd == e);
+                do { q++; bnd = bnd2; bnd2 = offsets[min(q + 2, nb)]; } while (bnd == e);
             }
             const uint32_t v = sorted[e];
             const Affine<F> pt = ld(pts + (v & 0x7fffffffu));
@@ -280,7 +282,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                     range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
                     acc = Xyzz<F>::inf();
                     seg0 = e;
-                    do { q++; bnd = offsets[q + 1]; } while (bnd == e);
+                    do { q++; bnd = bnd2; bnd2 = offsets[min(q + 2, nb)]; } while (bnd == e);
                 }
                 if (skip_inf && qp.is_inf()) continue;  // hole of a wire-indexed table
                 if (cv >> 31) qp.y = -qp.y;
@@ -293,7 +295,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                     range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
                     acc = Xyzz<F>::inf();
                     seg0 = e;
-                    do { q++; bnd = offsets[q + 1]; } while (bnd == e);
+                    do { q++; bnd = bnd2; bnd2 = offsets[min(q + 2, nb)]; } while (bnd == e);
                 }
                 const uint32_t v = sorted[e];
                 Affine<F> p = ld(pts + (v & 0x7fffffffu));
