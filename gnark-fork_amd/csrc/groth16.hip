@@ -1,7 +1,7 @@
 // Groth16 BN254 prover on one MI355X: the device section of gnark's
 // icicle_bn254.Prove (icicle.go:133-422) / groth16_bn254.Prove (prove.go:127-320).
 //
-//   stream 1: computeH (7 fused NTTs) -> Z-MSM over h
+//   stream 1: computeH (6 fused NTTs) -> Z-MSM over h
 //   streams 2, 3, 4, 0: A-MSM, B1-MSM, K-MSM, G2-MSM, concurrently (wire
 //                       scalars gathered through per-base index maps)
 //   host pool: r*delta, s*delta, kr*delta, s*delta2 while the GPU works;

@@ -36,7 +36,8 @@ enum ScaleKind {
     SK_NINV = 4,        // 1/n
     SK_H_FWD = 5,       // g^bitrev(i) / n          (computeH: iFFT -> coset FFT)
     SK_H_INV = 6,       // den * g^-bitrev(i) / n   (computeH: final coset iFFT)
-    SK_COUNT = 7
+    SK_DEN_N = 7,       // den / n                  (computeH: iFFT of C)
+    SK_COUNT = 8
 };
 
 template <class F>
@@ -62,6 +63,8 @@ struct PassParams {
     int has_post;
     ScaleSpec<F> post;
     int epi_mul_sub;  // out = ea*eb - x
+    int epi_mul;      // out = ea*x
+    int epi_sub;      // out = x - ea
     const F* ea;
     const F* eb;
     int canon_out;    // last pass of the transform: write canonical values (lazy fields)
@@ -253,6 +256,8 @@ __device__ __forceinline__ void ntt_round(const PassParams<F>& P, uint32_t* lds,
                 if (NttLazy<F>::on && P.canon_out && !P.has_post) y = canon(y);
                 if (P.has_post) y = apply_scale(P.post, g[m], P.log_n, y);
                 if (P.epi_mul_sub) y = load_fr(P.ea + g[m]) * load_fr(P.eb + g[m]) - y;
+                if (P.epi_mul) y = load_fr(P.ea + g[m]) * y;
+                if (P.epi_sub) y = y - load_fr(P.ea + g[m]);
                 store_fr(P.out + g[m], y);
             }
         } else {
@@ -291,6 +296,8 @@ __global__ void __launch_bounds__(kNttThreads<MAXNB>, kNttWaves<MAXNB>) k_ntt_pa
             if (P.has_pre) x = apply_scale(P.pre, g, P.log_n, x);
             if (P.has_post) x = apply_scale(P.post, g, P.log_n, x);
             if (P.epi_mul_sub) x = load_fr(P.ea + g) * load_fr(P.eb + g) - x;
+            if (P.epi_mul) x = load_fr(P.ea + g) * x;
+            if (P.epi_sub) x = x - load_fr(P.ea + g);
             store_fr(P.out + g, x);
         }
         return;
@@ -429,9 +436,12 @@ static int ntt_radix() {
 
 static hipStream_t pick_stream(void* s) { return s ? (hipStream_t)s : hipStreamPerThread; }
 
+// epilogue of the last pass: EPI_MUL_SUB out = ea*eb - x, EPI_MUL out = ea*x,
+// EPI_SUB out = x - ea (none when ea is null)
+enum { EPI_MUL_SUB = 0, EPI_MUL = 1, EPI_SUB = 2 };
 template <class C>
 void run_transform(DomainT<C>* d, const Fe<C>* in, Fe<C>* out, bool dit, bool inverse_tw, int pre_kind,
-                   int post_kind, const Fe<C>* ea, const Fe<C>* eb, hipStream_t st) {
+                   int post_kind, const Fe<C>* ea, const Fe<C>* eb, hipStream_t st, int epi = EPI_MUL_SUB) {
     using F = Fe<C>;
     const int L = d->log_n;
     auto passes = plan_passes(L, dit);
@@ -450,7 +460,13 @@ void run_transform(DomainT<C>* d, const Fe<C>* in, Fe<C>* out, bool dit, bool in
         if (pi == 0 && pre_kind >= 0) { P.has_pre = 1; P.pre = d->spec[pre_kind]; }
         bool last = (pi + 1 == passes.size());
         if (last && post_kind >= 0) { P.has_post = 1; P.post = d->spec[post_kind]; }
-        if (last && ea) { P.epi_mul_sub = 1; P.ea = ea; P.eb = eb; }
+        if (last && ea) {
+            P.epi_mul_sub = epi == EPI_MUL_SUB;
+            P.epi_mul = epi == EPI_MUL;
+            P.epi_sub = epi == EPI_SUB;
+            P.ea = ea;
+            P.eb = eb;
+        }
         P.canon_out = last ? 1 : 0;
         int T = 1 << (ps.k + ps.tl);
         unsigned tiles = (unsigned)(d->n / (size_t)T);
@@ -519,6 +535,7 @@ static DomainT<C>* domain_build(int log_n, const void* omega_mont, const void* c
         {F::one(), d->n_inv, 0},
         {d->g, d->n_inv, 1},
         {d->g_inv, d->den * d->n_inv, 1},
+        {F::one(), d->den * d->n_inv, 0},
     };
     for (int kd = 0; kd < SK_COUNT; kd++) {
         build_pow_tables(L, S, defs[kd].x, defs[kd].c, hi, lo);
@@ -611,20 +628,26 @@ extern "C" int gg_ntt(gg_domain_t d, void* data_dev, int inverse, int decimation
 namespace gg {
 // computeH (prove.go:353-396) on device buffers A (becomes h), B, C, each 2^L fr
 // (already padded), for the domain's scalar field
+// Six transforms instead of prove.go's seven: the coset iFFT is linear and
+// undoes the coset FFT, so coset_iFFT((a b - c) den) = coset_iFFT(a b) den -
+// c_coeffs den, where c_coeffs = iFFT(c) -- c's coset FFT is never needed.  The
+// field arithmetic is exact, so h is the reference's, bit for bit (h for any
+// a, b, c, satisfied or not: only linearity is used).
 template <class C>
 static void compute_h_t(DomainT<C>* d, Fe<C>* A, Fe<C>* B, Fe<C>* Cv, Fe<C>* H, hipStream_t st) {
     const Fe<C>* nul = nullptr;
-    // a, b: iFFT(DIF) with g^br(i)/n folded in, then DIT FFT -> coset evaluations
+    // a, b: iFFT(DIF) with g^br(i)/n folded in, then DIT FFT -> coset evaluations;
+    // the last pass of b's emits a*b in place
     run_transform(d, A, A, false, true, -1, SK_H_FWD, nul, nul, st);
     run_transform(d, A, A, true, false, -1, -1, nul, nul, st);
     run_transform(d, B, B, false, true, -1, SK_H_FWD, nul, nul, st);
-    run_transform(d, B, B, true, false, -1, -1, nul, nul, st);
-    run_transform(d, Cv, Cv, false, true, -1, SK_H_FWD, nul, nul, st);
-    // last pass of c's coset FFT emits a*b - c in place (PolyOps fused)
-    run_transform(d, Cv, Cv, true, false, -1, -1, (const Fe<C>*)A, (const Fe<C>*)B, st);
-    // coset iFFT (DIF) with den * g^-br(i) / n folded in -> h bit-reversed.
-    // H may alias A, B or C.
-    run_transform(d, Cv, H, false, true, -1, SK_H_INV, nul, nul, st);
+    run_transform(d, B, B, true, false, -1, -1, (const Fe<C>*)A, nul, st, EPI_MUL);
+    // c: plain iFFT (DIF, natural -> bit-reversed coefficients) with den / n
+    run_transform(d, Cv, Cv, false, true, -1, SK_DEN_N, nul, nul, st);
+    // coset iFFT (DIF) of a*b with den * g^-br(i) / n folded in, minus den c:
+    // h bit-reversed.  H may alias A or B (C is read by the last pass).
+    GG_CHECK(H != Cv, GG_ERR_INTERNAL, "computeH: h must not alias c");
+    run_transform(d, B, H, false, true, -1, SK_H_INV, (const Fe<C>*)Cv, nul, st, EPI_SUB);
 }
 // any curve's domain (BN254 or BLS12-381 Groth16); fr buffers as opaque 32-B elements
 void compute_h_device(gg_domain* dom, Fr* A, Fr* B, Fr* C, Fr* H, hipStream_t st) {
