@@ -777,4 +777,60 @@ __device__ __forceinline__ Xyzz<Fp2> to_std(const Xyzz2_29& p) {
     return Xyzz<Fp2>{to_std2(p.x), to_std2(p.y), to_std2(p.zz), to_std2(p.zzz)};
 }
 
+// Where bucket sums meet (level 2 and the weighted bucket reduction of the G2
+// groups): dbl-2008-s-1 and add-2008-s over Fp2, coordinates < 2p per
+// component and normalised in and out (the accumulator's partials satisfy it:
+// X < 2p, Y < 1.3p, ZZ, ZZZ < 1.5p; M = 169.28 p).
+__device__ __forceinline__ Xyzz2_29 xyzz2_29_dbl(const Xyzz2_29& p) {
+    const Fp2_29 U{add(p.y.c0, p.y.c0), add(p.y.c1, p.y.c1)};  // < 4p
+    const Fp2_29 V = sqr_fp2<5>(U);                          // (8p 9p / M + p, 4p 8p / M + p) < (1.43p, 1.19p)
+    const Fp2_29 W = mul_fp2<3>(U, V);                       // (4p 1.43p + 4p 3p) / M + p < 1.11p
+    const Fp2_29 S = mul_fp2<3>(p.x, V);                     // < 1.06p
+    const Fp2_29 xx = sqr_fp2<3>(p.x);                       // (4p 5p, 2p 4p) / M + p < 1.12p
+    const Fp2_29 M{add(xx.c0, add(xx.c0, xx.c0)), add(xx.c1, add(xx.c1, xx.c1))};  // < 3.36p
+    const Fp2_29 MM = sqr_fp2<5>(M);                         // (6.72p 8.36p / M + p) < 1.34p
+    const Fp2_29 X3{reduce_small(sub<4>(MM.c0, add(S.c0, S.c0))), reduce_small(sub<4>(MM.c1, add(S.c1, S.c1)))};
+    const Fp2_29 D{sub<3>(S.c0, X3.c0), sub<3>(S.c1, X3.c1)};  // < 4.06p
+    // Y3 = M D - W Y (components as in xyzz2_29_dbl_affine; Y < 2p):
+    // < (3.36 4.06 + 3.36 6 + 2 3 + 2 1.11) p^2 / M + p < 1.25p; 36 products
+    // of normalised limbs per column + the reduction < 2^63.3
+    const Fp29 nD1 = sub<6>(Fp29{}, D.c1), nW0 = sub<3>(Fp29{}, W.c0), nW1 = sub<3>(Fp29{}, W.c1);
+    const Fp2_29 Y3{mul4(M.c0, D.c0, M.c1, nD1, p.y.c0, nW0, p.y.c1, W.c1),
+                    mul4(M.c0, D.c1, M.c1, D.c0, p.y.c0, nW1, p.y.c1, nW0)};
+    return Xyzz2_29{X3, Y3, mul_fp2<3>(V, p.zz), mul_fp2<3>(W, p.zzz)};  // < 1.05p
+}
+
+// p + q (add-2008-s): out X3 < 2p, Y3 < 1.28p, ZZ3, ZZZ3 < 1.06p
+__device__ __forceinline__ Xyzz2_29 xyzz2_29_add(const Xyzz2_29& p, const Xyzz2_29& q) {
+    if (is_inf2_29(q)) return p;
+    if (is_inf2_29(p)) return q;
+    const Fp2_29 U1 = mul_fp2<3>(p.x, q.zz), U2 = mul_fp2<3>(q.x, p.zz);     // (2p 2p + 2p 3p) / M + p < 1.06p
+    const Fp2_29 S1 = mul_fp2<3>(p.y, q.zzz), S2 = mul_fp2<3>(q.y, p.zzz);  // < 1.06p
+    const Fp2_29 P{sub<3>(U2.c0, U1.c0), sub<3>(U2.c1, U1.c1)};             // < 4.06p
+    const Fp2_29 R{sub<3>(S2.c0, S1.c0), sub<3>(S2.c1, S1.c1)};             // < 4.06p
+    if (is_zero_mod(P.c0, 5) && is_zero_mod(P.c1, 5))
+        return (is_zero_mod(R.c0, 5) && is_zero_mod(R.c1, 5)) ? xyzz2_29_dbl(p) : inf2_29();
+    const Fp2_29 PP = sqr_fp2<6>(P);            // (1.48p, 1.19p)
+    const Fp2_29 PPP = mul_fp2<3>(P, PP);       // < 1.11p
+    const Fp2_29 Q = mul_fp2<3>(U1, PP);        // < 1.04p
+    const Fp2_29 RR = sqr_fp2<6>(R);            // (1.48p, 1.19p)
+    const Fp2_29 X3{reduce_small(subw5(RR.c0, add_nn(PPP.c0, add_nn(Q.c0, Q.c0)))),
+                    reduce_small(subw5(RR.c1, add_nn(PPP.c1, add_nn(Q.c1, Q.c1))))};  // PPP + 2Q < 3.2p
+    // Y3 = R (Q - X3) - S1 PPP as in xyzz2_29_madd (S1 in Y's place):
+    // < (4.06 4.03 + 4.06 6 + 1.06 3 + 1.06 1.11) p^2 / M + p < 1.28p
+    const Fp2_29 U{sub<3>(Q.c0, X3.c0), sub<3>(Q.c1, X3.c1)};  // < 4.04p
+    const Fp29 nU1 = sub<6>(Fp29{}, U.c1), nP0 = sub<3>(Fp29{}, PPP.c0), nP1 = sub<3>(Fp29{}, PPP.c1);
+    const Fp2_29 Y3{mul4(R.c0, U.c0, R.c1, nU1, S1.c0, nP0, S1.c1, PPP.c1),
+                    mul4(R.c0, U.c1, R.c1, U.c0, S1.c0, nP1, S1.c1, nP0)};
+    return Xyzz2_29{X3, Y3, mul_fp2<3>(mul_fp2<3>(p.zz, q.zz), PP), mul_fp2<3>(mul_fp2<3>(p.zzz, q.zzz), PPP)};
+}
+
+// -p: Y -> 3p - Y reduced below 2p (Y < 2p)
+__device__ __forceinline__ Xyzz2_29 xyzz2_29_neg(const Xyzz2_29& p) {
+    if (is_inf2_29(p)) return p;
+    Xyzz2_29 r = p;
+    r.y = Fp2_29{reduce_small(sub<3>(Fp29{}, p.y.c0)), reduce_small(sub<3>(Fp29{}, p.y.c1))};
+    return r;
+}
+
 }  // namespace gg

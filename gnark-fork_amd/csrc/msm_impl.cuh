@@ -165,6 +165,28 @@ struct PartialOf<Fp2> {
     using T = Xyzz2_29;
 };
 
+// the group law on the partial form, for the lane-per-bucket level 2 and
+// weighted sums (k_range_tree_r, k_bucket_sum_r, k_bucket_runsum)
+template <class F>
+struct PartialOps {  // G1 groups: XyzzL, coordinates < 7p
+    using T = typename PartialOf<F>::T;
+    using C = typename RadixOf<F>::C;
+    static __device__ __forceinline__ T inf() { return inf_l<C>(); }
+    static __device__ __forceinline__ T add(const T& p, const T& q) { return xyzzl_add(p, q); }
+    static __device__ __forceinline__ T neg(const T& p) {
+        T r = p;
+        if (!is_inf_l(r)) r.y = sub<8>(Fl<C>{}, r.y);  // y < 7p
+        return r;
+    }
+};
+template <>
+struct PartialOps<Fp2> {  // BN254 G2: Xyzz2_29, coordinates < 2p
+    using T = Xyzz2_29;
+    static __device__ __forceinline__ T inf() { return inf2_29(); }
+    static __device__ __forceinline__ T add(const T& p, const T& q) { return xyzz2_29_add(p, q); }
+    static __device__ __forceinline__ T neg(const T& p) { return xyzz2_29_neg(p); }
+};
+
 template <class P>
 __device__ __forceinline__ void range_store(const P& acc, bool first, bool last, uint32_t q, int c, size_t t,
                                             P* head, P* tail, P* S) {
@@ -457,10 +479,10 @@ __global__ void __launch_bounds__(256) k_bucket_combine(const Xyzz<F>* head, con
 
 // k_range_tree over radix-form partials, a lane per slot (xyzzl_add)
 template <class F>
-__global__ void __launch_bounds__(256) k_range_tree_r(XyzzL<typename RadixOf<F>::C>* head, const uint32_t* tbucket,
+__global__ void __launch_bounds__(256) k_range_tree_r(typename PartialOf<F>::T* head, const uint32_t* tbucket,
                                                       const uint32_t* offsets, uint32_t nb, uint32_t K,
                                                       uint32_t stride, uint32_t fan) {
-    using C = typename RadixOf<F>::C;
+    using O = PartialOps<F>;
     const size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t E = offsets[nb];
     if ((uint64_t)p * K >= E) return;
@@ -469,8 +491,8 @@ __global__ void __launch_bounds__(256) k_range_tree_r(XyzzL<typename RadixOf<F>:
     if (m <= LIGHT || p <= s.t0) return;
     const uint32_t j = (uint32_t)p - (s.t0 + 1);
     if (j % (fan * stride) || j + stride >= m) return;
-    XyzzL<C> acc = ld(head + p);
-    for (uint32_t k = 1; k < fan && j + k * stride < m; k++) acc = xyzzl_add(acc, ld(head + p + k * stride));
+    typename O::T acc = ld(head + p);
+    for (uint32_t k = 1; k < fan && j + k * stride < m; k++) acc = O::add(acc, ld(head + p + k * stride));
     st(head + p, acc);
 }
 
@@ -491,21 +513,21 @@ __global__ void __launch_bounds__(256) k_partials_to_std(const typename PartialO
 // k_range_tree for heavy buckets) and stores it in radix form, laid out
 // [i][t] for bucket B = t L + i so that k_bucket_runsum's loads coalesce.
 template <class F>
-__global__ void __launch_bounds__(256) k_bucket_sum_r(const XyzzL<typename RadixOf<F>::C>* head,
-                                                       const XyzzL<typename RadixOf<F>::C>* tail,
-                                                       const XyzzL<typename RadixOf<F>::C>* S, const uint32_t* offsets,
+__global__ void __launch_bounds__(256) k_bucket_sum_r(const typename PartialOf<F>::T* head,
+                                                       const typename PartialOf<F>::T* tail,
+                                                       const typename PartialOf<F>::T* S, const uint32_t* offsets,
                                                        uint32_t nb_total, int c, uint32_t K, int logL,
-                                                       XyzzL<typename RadixOf<F>::C>* Sr) {
-    using C = typename RadixOf<F>::C;
+                                                       typename PartialOf<F>::T* Sr) {
+    using O = PartialOps<F>;
     const uint32_t B = blockIdx.x * blockDim.x + threadIdx.x;
     if (B >= nb_total) return;
     const uint32_t nseg = nb_total >> logL;
     const BucketSpan sp = bucket_span(offsets, bucket_perm(B, c), offsets[nb_total], K);
-    XyzzL<C> acc = inf_l<C>();
+    typename O::T acc = O::inf();
     if (!sp.empty) {
         acc = ld(sp.direct ? S + B : (sp.first ? head : tail) + sp.t0);
         const uint32_t rend = sp.direct ? sp.t0 : (sp.t1 - sp.t0 > LIGHT ? sp.t0 + 1 : sp.t1);  // heavy: tree result
-        for (uint32_t r = sp.t0 + 1; r <= rend; r++) acc = xyzzl_add(acc, ld(head + r));
+        for (uint32_t r = sp.t0 + 1; r <= rend; r++) acc = O::add(acc, ld(head + r));
     }
     st(Sr + (size_t)(B & ((1u << logL) - 1)) * nseg + (B >> logL), acc);
 }
@@ -515,50 +537,55 @@ __global__ void __launch_bounds__(256) k_bucket_sum_r(const XyzzL<typename Radix
 // sum_i (i + 1) S_{tL+i}; then D_t = A - L R.  Writes D_t and R_t in gnark's
 // form: the group's weighted sum is sum_t D_t + L sum_t (t + 1) R_t.  Every lane
 // runs the same step sequence through ONE inlined add (the code of several
-// would overflow the instruction cache): R += S_i, A += R (L times), X = 2X
-// (log L times, X = R), A += -X.
+// would overflow the instruction cache): R += S_i, A += R (L times), R = 2R
+// (log L times, after R is written out), A += -R.
 template <class F>
-__global__ void __launch_bounds__(256) k_bucket_runsum(const XyzzL<typename RadixOf<F>::C>* Sr, uint32_t nseg, int logL,
+__global__ void __launch_bounds__(256) k_bucket_runsum(const typename PartialOf<F>::T* Sr, uint32_t nseg, int logL,
                                                         Xyzz<F>* Dout, Xyzz<F>* Rout) {
-    using C = typename RadixOf<F>::C;
+    using O = PartialOps<F>;
+    using T = typename O::T;
+    // the next bucket's load in flight during the two adds -- not for the Fp2
+    // points (288 B each), whose live set would spill
+    constexpr bool kPf = !std::is_same<F, Fp2>::value;
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nseg) return;
     const int L = 1 << logL, steps = 2 * L + logL + 1;
-    XyzzL<C> R = inf_l<C>(), A = inf_l<C>(), X, cur = ld(Sr + (size_t)(L - 1) * nseg + t), nxt = cur;
-    for (int st = 0; st < steps; st++) {
-        XyzzL<C> x, y;
-        if (st < 2 * L) {
-            const int i = L - 1 - (st >> 1);
-            if (st & 1) {
+    T R = O::inf(), A = O::inf(), cur, nxt;
+    if constexpr (kPf) nxt = ld(Sr + (size_t)(L - 1) * nseg + t);
+    for (int k = 0; k < steps; k++) {
+        T x, y;
+        if (k < 2 * L) {
+            const int i = L - 1 - (k >> 1);
+            if (k & 1) {
                 x = A;
                 y = R;
             } else {
-                cur = nxt;
-                if (i > 0) nxt = ld(Sr + (size_t)(i - 1) * nseg + t);  // in flight during the two adds
+                if constexpr (kPf) {
+                    cur = nxt;
+                    if (i > 0) nxt = ld(Sr + (size_t)(i - 1) * nseg + t);
+                } else {
+                    cur = ld(Sr + (size_t)i * nseg + t);
+                }
                 x = R;
                 y = cur;
             }
-        } else if (st < 2 * L + logL) {
-            if (st == 2 * L) X = R;
-            x = X;
-            y = X;
         } else {
-            x = A;
-            y = X;
-            if (!is_inf_l(y)) y.y = sub<8>(Fl<C>{}, y.y);  // -X (y < 7p)
+            // R is final: written out, then doubled in place (X = L R)
+            if (k == 2 * L) st(Rout + t, to_std(R));
+            x = k < 2 * L + logL ? R : A;
+            y = k < 2 * L + logL ? R : O::neg(R);
         }
-        const XyzzL<C> z = xyzzl_add(x, y);
-        if (st < 2 * L) {
-            if (st & 1) A = z;
+        const T z = O::add(x, y);
+        if (k < 2 * L) {
+            if (k & 1) A = z;
             else R = z;
-        } else if (st < 2 * L + logL) {
-            X = z;
+        } else if (k < 2 * L + logL) {
+            R = z;
         } else {
             A = z;
         }
     }
     st(Dout + t, to_std(A));
-    st(Rout + t, to_std(R));
 }
 
 // copy a list of small device arrays into one contiguous staging buffer
@@ -964,7 +991,8 @@ inline Xyzz<F> tree_sum(const Xyzz<F>* X, size_t n, MsmScratch* scr, hipStream_t
 // level 2 + bucket reduction through k_bucket_sum_r / k_bucket_runsum (reduced-radix G1 groups);
 // GG_MSM_SEGSUM=0 keeps k_bucket_combine + bucket_reduce_2d
 template <class F>
-constexpr bool kSegsumGroup = RadixOf<F>::on && (std::is_same<F, Fp>::value || std::is_same<F, FpBls>::value);
+constexpr bool kSegsumGroup = RadixOf<F>::on && (std::is_same<F, Fp>::value || std::is_same<F, FpBls>::value ||
+                                                   std::is_same<F, Fp2>::value);
 inline bool segsum_enabled() {
     const char* e = getenv("GG_MSM_SEGSUM");  // per MSM: tests switch it
     return !(e && atoi(e) == 0);
@@ -1048,7 +1076,6 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
     if constexpr (kSegsumGroup<F>) {
         if (segsum_enabled() && logL >= 1) {
             // level 2 and the weighted sums in radix form, a lane per bucket / segment
-            using C = typename RadixOf<F>::C;
             for (uint32_t stride = 1; max_ranges > LIGHT && stride < max_ranges;) {
                 const uint32_t fan = (stride == 1) ? 4u : 2u;
                 hipLaunchKernelGGL(k_range_tree_r<F>, dim3(grid_for(T, 256)), dim3(256), 0, st, hP,
@@ -1057,15 +1084,15 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
                 stride *= fan;
             }
             const uint32_t L = 1u << logL, Tg = (uint32_t)(nbg >> logL), G = (uint32_t)b->G;
-            scr->seg.reserve(2 * (size_t)G * Tg * sizeof(Xyzz<F>) + nb * sizeof(XyzzL<C>));
+            scr->seg.reserve(2 * (size_t)G * Tg * sizeof(Xyzz<F>) + nb * sizeof(PT));
             Xyzz<F>* D = scr->seg.as<Xyzz<F>>();
             Xyzz<F>* Rs = D + (size_t)G * Tg;
-            XyzzL<C>* Sr = reinterpret_cast<XyzzL<C>*>(Rs + (size_t)G * Tg);
-            hipLaunchKernelGGL(k_bucket_sum_r<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, (const XyzzL<C>*)hP,
-                               (const XyzzL<C>*)tP, (const XyzzL<C>*)SP, offs, (uint32_t)nb, b->c, K, logL, Sr);
+            PT* Sr = reinterpret_cast<PT*>(Rs + (size_t)G * Tg);
+            hipLaunchKernelGGL(k_bucket_sum_r<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, (const PT*)hP,
+                               (const PT*)tP, (const PT*)SP, offs, (uint32_t)nb, b->c, K, logL, Sr);
             GG_HIP(hipGetLastError());
             hipLaunchKernelGGL(k_bucket_runsum<F>, dim3(grid_for((size_t)G * Tg, 256)), dim3(256), 0, st,
-                               (const XyzzL<C>*)Sr, (uint32_t)(G * Tg), logL, D, Rs);
+                               (const PT*)Sr, (uint32_t)(G * Tg), logL, D, Rs);
             GG_HIP(hipGetLastError());
             ps_acc2.stop(st);
             ProfScope ps_red("msm_reduce", st, (double)nb);

@@ -182,6 +182,26 @@ def test_msm_g2_window20(n, dist):
     assert base.msm(ss, n) == _g2_trapdoor(ks, ss)
 
 
+@pytest.mark.parametrize("seg", ["1", "0"])
+@pytest.mark.parametrize("n,c,dist", [(1 << 16, 20, "skew"), (1 << 17, 22, "witness"), (1 << 16, 19, "uniform")])
+def test_msm_g2_radix_bucket_reduction(n, c, dist, seg, monkeypatch):
+    """G2 windows with >= 2^18 buckets take the radix-form Fp2 level 2 and
+    weighted sums (k_bucket_sum_r / k_bucket_runsum over Xyzz2_29, segments of
+    L = 2 / 16 / 2 buckets here); GG_MSM_SEGSUM=0 the quad path.  Trapdoor-
+    checked, with heavy buckets ('skew': k_range_tree_r first) and empty ones."""
+    from gnark_amd import msm
+    monkeypatch.setenv("GG_MSM_SEGSUM", seg)
+    ks = random_fr_mont(n, 710 + c)
+    pts = coracle.g2_batch_mul(o.g2_to_bytes(o.G2_GEN), ks.tobytes(), n)
+    ss = random_fr_mont(n, 810 + c, "uniform" if dist == "skew" else dist)
+    if dist == "skew":
+        ss[: n // 2] = ss[0]
+    base = msm.MsmBase(msm.G2, bytes(pts), n, window_bits=c)
+    assert base.info()[1] == c
+    assert base.msm(ss, n) == _g2_trapdoor(ks, ss)
+    base.close()
+
+
 def test_msm_g2_window20_2p20():
     """2^20 G2 points at c = 20, trapdoor-checked."""
     from gnark_amd import msm
