@@ -701,6 +701,39 @@ extern "C" int gg_groth16_finalize_ex(int curve, const void* alpha1, const void*
     GG_CAPI_END
 }
 
+struct gg_g16_fixed {
+    int curve = GG_CURVE_BN254;
+    std::future<G16Fixed<CurveBn254>> bn;
+    std::future<G16Fixed<CurveBls12381>> bls;
+};
+
+extern "C" int gg_groth16_finalize_begin(int curve, const void* delta1, const void* delta2, const void* r_mont,
+                                         const void* s_mont, gg_g16_fixed_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(delta1 && delta2 && r_mont && s_mont && out, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(curve == GG_CURVE_BN254 || curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "bad curve");
+    std::unique_ptr<gg_g16_fixed> h(new gg_g16_fixed());
+    h->curve = curve;
+    if (curve == GG_CURVE_BN254) h->bn = fixed_terms_async<CurveBn254>(delta1, delta2, r_mont, s_mont);
+    else h->bls = fixed_terms_async<CurveBls12381>(delta1, delta2, r_mont, s_mont);
+    *out = h.release();
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_finalize_end(gg_g16_fixed_t h, const void* alpha1, const void* beta1, const void* beta2,
+                                       const void* partials, void* ar_aff, void* bs_aff, void* krs_aff) {
+    GG_CAPI_BEGIN
+    GG_CHECK(h, GG_ERR_INVALID_ARG, "null handle");
+    std::unique_ptr<gg_g16_fixed> own(h);  // released on every path (the futures join their threads)
+    if (!partials) return GG_OK;
+    GG_CHECK(alpha1 && beta1 && beta2 && ar_aff && bs_aff && krs_aff, GG_ERR_INVALID_ARG, "null argument");
+    G16Partials p;
+    partials_get(h->curve, partials, p);
+    if (h->curve == GG_CURVE_BN254) g16_combine<CurveBn254>(p, h->bn.get(), alpha1, beta1, beta2, ar_aff, bs_aff, krs_aff);
+    else g16_combine<CurveBls12381>(p, h->bls.get(), alpha1, beta1, beta2, ar_aff, bs_aff, krs_aff);
+    GG_CAPI_END
+}
+
 extern "C" int gg_groth16_finalize(const void* alpha1, const void* beta1, const void* delta1,
                                    const void* beta2, const void* delta2, const void* partials,
                                    const void* r_mont, const void* s_mont, void* ar_aff,

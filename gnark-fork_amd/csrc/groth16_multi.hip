@@ -335,6 +335,17 @@ extern "C" int gg_groth16_mpk_prove_ex(gg_groth16_mpk_t m, int inputs_on_device,
     GG_CHECK(n_cons <= m->n, GG_ERR_INVALID_ARG, "more constraints than the domain");
     std::lock_guard<std::mutex> lk(m->mu);
     const auto t0 = std::chrono::steady_clock::now();
+    // the fixed-point terms (r.delta, s.delta, kr.delta, s.delta2) on host
+    // threads while the shards prove
+    gg_g16_fixed_t fx = nullptr;
+    {
+        const int rc = gg_groth16_finalize_begin(m->curve, m->delta1, m->delta2, r_mont, s_mont, &fx);
+        GG_CHECK(rc == GG_OK, rc, gg_last_error());
+    }
+    struct FxGuard {
+        gg_g16_fixed_t& h;
+        ~FxGuard() { if (h) gg_groth16_finalize_end(h, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr); }
+    } fx_guard{fx};
     m->bar.reset();
     const size_t pbytes = 4 * m->g1j + m->g2j;  // a | b1 | k | z | b2 (gg_groth16_prove_partial)
     std::vector<std::vector<uint8_t>> parts(m->world, std::vector<uint8_t>(pbytes));
@@ -365,8 +376,9 @@ extern "C" int gg_groth16_mpk_prove_ex(gg_groth16_mpk_t m, int inputs_on_device,
         GG_CHECK(g2add(acc2, parts[r].data() + 4 * m->g1j, tmp) == GG_OK, GG_ERR_INTERNAL, "partial sum");
         memcpy(acc2, tmp, m->g2j);
     }
-    const int rc = gg_groth16_finalize_ex(m->curve, m->alpha1, m->beta1, m->delta1, m->beta2, m->delta2, sum.data(),
-                                          r_mont, s_mont, ar_aff, bs_aff, krs_aff);
+    gg_g16_fixed_t h = fx;
+    fx = nullptr;  // end releases it
+    const int rc = gg_groth16_finalize_end(h, m->alpha1, m->beta1, m->beta2, sum.data(), ar_aff, bs_aff, krs_aff);
     GG_CHECK(rc == GG_OK, rc, gg_last_error());
     const auto t2 = std::chrono::steady_clock::now();
     m->last_ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();

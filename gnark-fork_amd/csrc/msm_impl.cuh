@@ -589,10 +589,11 @@ __global__ void __launch_bounds__(256) k_bucket_runsum(const typename PartialOf<
 }
 
 // copy a list of small device arrays into one contiguous staging buffer
+constexpr int MAX_GATHER = 192;
 template <class F>
 struct GatherList {
-    const Xyzz<F>* src[64];
-    uint32_t off[65];
+    const Xyzz<F>* src[MAX_GATHER];
+    uint32_t off[MAX_GATHER + 1];
     int n;
 };
 template <class F>
@@ -815,16 +816,35 @@ inline void precompute(gg_msm_base* b, const Affine<F>* dev_in, hipStream_t st) 
     GG_HIP(hipStreamSynchronize(st));
 }
 
-// Weighted bucket sum sum_{b<nb} (b+1) S_b with log-depth, wide tree sums
-// (DESIGN.md "MSM / bucket reduction"): a weighted sum WS(X, off) =
-// sum_j (j + off) X_j over n = 2^k elements is split as j = q*M + r into
-// M * WS(H, 0) + WS(G, off) with row sums H_q and column sums G_r -- both plain
-// tree sums that run wide on the GPU.  Pieces of <= 16 elements finish on the
-// host, combined by Horner over their 2^mlog factors.
+// One term of a batched reduction: 2^mlog * sum_j (j + off) X_j over n = 2^k
+// elements (weighted), or 2^mlog * sum_j X_j (plain).
 template <class F>
-inline Xyzz<F> bucket_reduce_2d(size_t nb, const Xyzz<F>* S, MsmScratch* scr, hipStream_t st) {
+struct RedItem {
+    const Xyzz<F>* X;
+    uint32_t n, off;
+    int mlog;
+    bool plain;
+};
+
+// Sum of reduction terms with log-depth, wide tree sums (DESIGN.md "MSM /
+// bucket reduction"): a weighted sum WS(X, off) = sum_j (j + off) X_j over
+// n = 2^k elements is split as j = q*M + r into M * WS(H, 0) + WS(G, off) with
+// row sums H_q and column sums G_r; a plain sum keeps its row sums.  Every
+// round's jobs of every term go into the same launches (one add's latency per
+// round for all of them), pieces of <= HOST_N elements finish on the host after
+// ONE read-back, combined by Horner over their 2^mlog factors.
+template <class F>
+inline Xyzz<F> reduce_terms(std::vector<RedItem<F>> items, MsmScratch* scr, hipStream_t st) {
+    static const bool split = getenv("GG_RED_SPLIT") && atoi(getenv("GG_RED_SPLIT"));  // A/B: a read-back per term
+    if (split && items.size() > 1) {
+        Xyzz<F> acc = Xyzz<F>::inf();
+        for (const auto& it : items) acc = xyzz_add(acc, reduce_terms<F>({it}, scr, st));
+        return acc;
+    }
     const size_t XB = sizeof(Xyzz<F>);
-    const size_t arena_elems = 3 * nb + 1024;
+    size_t total = 0;
+    for (const auto& it : items) total += it.n;
+    const size_t arena_elems = 3 * total + 1024 * (items.size() + 1);
     scr->arena.reserve(arena_elems * XB);
     Xyzz<F>* arena = scr->arena.as<Xyzz<F>>();
     size_t used = 0;
@@ -834,9 +854,8 @@ inline Xyzz<F> bucket_reduce_2d(size_t nb, const Xyzz<F>* S, MsmScratch* scr, hi
         used += cnt;
         return p;
     };
-    struct Item { const Xyzz<F>* X; uint32_t n, off; int mlog; };
+    using Item = RedItem<F>;
     struct Job { const Xyzz<F>* in; uint32_t A, Bc, sa, sb; Item dest; };
-    std::vector<Item> items{{S, (uint32_t)nb, 1u, 0}};
     std::vector<Item> host_items;
     uint32_t HOST_N = 8;  // weighted sums of <= HOST_N elements finish on the host (MI355X sweep: 8)
     if (const char* e = getenv("GG_RED_HOST_N")) HOST_N = (uint32_t)std::max(2, atoi(e));  // tuning
@@ -847,8 +866,12 @@ inline Xyzz<F> bucket_reduce_2d(size_t nb, const Xyzz<F>* S, MsmScratch* scr, hi
             int lg = 31 - __builtin_clz(it.n);
             int mlg = lg / 2;
             uint32_t M = 1u << mlg, rows = it.n >> mlg;
-            jobs.push_back({it.X, M, rows, 1u, M, Item{nullptr, rows, 0u, it.mlog + mlg}});
-            jobs.push_back({it.X, rows, M, M, 1u, Item{nullptr, M, it.off, it.mlog}});
+            if (it.plain) {  // row sums only
+                jobs.push_back({it.X, M, rows, 1u, M, Item{nullptr, rows, 0u, it.mlog, true}});
+                continue;
+            }
+            jobs.push_back({it.X, M, rows, 1u, M, Item{nullptr, rows, 0u, it.mlog + mlg, false}});
+            jobs.push_back({it.X, rows, M, M, 1u, Item{nullptr, M, it.off, it.mlog, false}});
         }
         // one launch per round: every output of every job is a block-wide sum
         static const bool block_mode = !(getenv("GG_RED_BLOCK") && atoi(getenv("GG_RED_BLOCK")) == 0);
@@ -916,8 +939,8 @@ inline Xyzz<F> bucket_reduce_2d(size_t nb, const Xyzz<F>* S, MsmScratch* scr, hi
         for (auto& j : jobs) { Item it = j.dest; it.X = j.in; next.push_back(it); }
         items.swap(next);
     }
-    // host: tiny weighted sums + Horner over the 2^mlog factors
-    GG_CHECK(host_items.size() <= 64, GG_ERR_INTERNAL, "too many host reduction items");
+    // host: tiny weighted / plain sums + Horner over the 2^mlog factors
+    GG_CHECK(host_items.size() <= (size_t)MAX_GATHER, GG_ERR_INTERNAL, "too many host reduction items");
     GatherList<F> GL;
     GL.n = (int)host_items.size();
     GL.off[0] = 0;
@@ -940,6 +963,11 @@ inline Xyzz<F> bucket_reduce_2d(size_t nb, const Xyzz<F>* S, MsmScratch* scr, hi
     for (size_t k = 0; k < host_items.size(); k++) {
         const auto& X = hx[k];
         Xyzz<F> run = Xyzz<F>::inf(), acc = Xyzz<F>::inf();
+        if (host_items[k].plain) {
+            for (const auto& x : X) acc = xyzz_add(acc, x);
+            vals.push_back({host_items[k].mlog, acc});
+            continue;
+        }
         for (size_t j = X.size(); j-- > 1;) {
             run = xyzz_add(run, X[j]);
             acc = xyzz_add(acc, run);
@@ -958,33 +986,6 @@ inline Xyzz<F> bucket_reduce_2d(size_t nb, const Xyzz<F>* S, MsmScratch* scr, hi
         acc = xyzz_add(acc, v.second);
     }
     for (; cur > 0; cur--) acc = acc.is_inf() ? acc : xyzz_dbl(acc);
-    return acc;
-}
-
-// sum of n (a power of two) points by block-wide tree sums (k_reduce_block),
-// 256 -> 1 per round, the last <= 256 on the host
-template <class F>
-inline Xyzz<F> tree_sum(const Xyzz<F>* X, size_t n, MsmScratch* scr, hipStream_t st) {
-    scr->arena.reserve((n / 256 + 2) * 2 * sizeof(Xyzz<F>));
-    Xyzz<F>* buf[2] = {scr->arena.as<Xyzz<F>>(), scr->arena.as<Xyzz<F>>() + n / 256 + 1};
-    const Xyzz<F>* in = X;
-    int k = 0;
-    while (n > 256) {
-        RedJobs<F> J;
-        J.n = 1;
-        const uint32_t bc = (uint32_t)(n / 256);
-        J.j[0] = RedJob<F>{in, buf[k], 256u, bc, 1u, 256u, 256u, bc};
-        hipLaunchKernelGGL(k_reduce_block<F>, dim3(bc), dim3(256), 0, st, J);
-        GG_HIP(hipGetLastError());
-        in = buf[k];
-        k ^= 1;
-        n = bc;
-    }
-    std::vector<Xyzz<F>> h(n);
-    GG_HIP(hipMemcpyAsync(h.data(), in, n * sizeof(Xyzz<F>), hipMemcpyDeviceToHost, st));
-    GG_HIP(hipStreamSynchronize(st));
-    Xyzz<F> acc = Xyzz<F>::inf();
-    for (const auto& x : h) acc = xyzz_add(acc, x);
     return acc;
 }
 
@@ -1083,7 +1084,7 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
                 GG_HIP(hipGetLastError());
                 stride *= fan;
             }
-            const uint32_t L = 1u << logL, Tg = (uint32_t)(nbg >> logL), G = (uint32_t)b->G;
+            const uint32_t Tg = (uint32_t)(nbg >> logL), G = (uint32_t)b->G;
             scr->seg.reserve(2 * (size_t)G * Tg * sizeof(Xyzz<F>) + nb * sizeof(PT));
             Xyzz<F>* D = scr->seg.as<Xyzz<F>>();
             Xyzz<F>* Rs = D + (size_t)G * Tg;
@@ -1096,14 +1097,14 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
             GG_HIP(hipGetLastError());
             ps_acc2.stop(st);
             ProfScope ps_red("msm_reduce", st, (double)nb);
-            // per group: sum_s D_s + L sum_s (s + 1) R_s, then sum_j 2^(j c) of them
-            Xyzz<F> res = Xyzz<F>::inf();
-            for (int jg = b->G - 1; jg >= 0; jg--) {
-                for (int k = 0; k < b->c && !res.is_inf() && jg < b->G - 1; k++) res = xyzz_dbl(res);
-                Xyzz<F> w = bucket_reduce_2d<F>(Tg, (const Xyzz<F>*)Rs + (size_t)jg * Tg, scr, st);
-                for (uint32_t k = 1; k < L && !w.is_inf(); k <<= 1) w = xyzz_dbl(w);
-                res = xyzz_add(res, xyzz_add(w, tree_sum<F>(D + (size_t)jg * Tg, Tg, scr, st)));
+            // sum_j 2^(j c) (sum_s D_s + L sum_s (s + 1) R_s) over the groups j:
+            // every group's two lists reduced in the same launches, one read-back
+            std::vector<RedItem<F>> terms;
+            for (int jg = 0; jg < b->G; jg++) {
+                terms.push_back({(const Xyzz<F>*)Rs + (size_t)jg * Tg, Tg, 1u, jg * b->c + logL, false});
+                terms.push_back({(const Xyzz<F>*)D + (size_t)jg * Tg, Tg, 0u, jg * b->c, true});
             }
+            Xyzz<F> res = reduce_terms<F>(std::move(terms), scr, st);
             ps_red.stop(st);
             return res;
         }
@@ -1129,12 +1130,10 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
     ps_acc2.stop(st);
     // ---- bucket reduction: sum_b (b+1) S_b
     ProfScope ps_red("msm_reduce", st, (double)nb);
-    // one weighted sum per precompute group, then sum_j 2^(j c) R_j by Horner
-    Xyzz<F> res = Xyzz<F>::inf();
-    for (int j = b->G - 1; j >= 0; j--) {
-        for (int k = 0; k < b->c && !res.is_inf() && j < b->G - 1; k++) res = xyzz_dbl(res);
-        res = xyzz_add(res, bucket_reduce_2d<F>(nbg, (const Xyzz<F>*)S + (size_t)j * nbg, scr, st));
-    }
+    // one weighted sum per precompute group, sum_j 2^(j c) R_j, in one batched reduction
+    std::vector<RedItem<F>> terms;
+    for (int j = 0; j < b->G; j++) terms.push_back({(const Xyzz<F>*)S + (size_t)j * nbg, (uint32_t)nbg, 1u, j * b->c, false});
+    Xyzz<F> res = reduce_terms<F>(std::move(terms), scr, st);
     ps_red.stop(st);
     return res;
 }

@@ -85,6 +85,8 @@ def _load():
         "gg_groth16_pk_release": ([P], I),
         "gg_groth16_pk_create_ex": ([I, I, P, P, P, S, P, S, P, S, P, S, P, P, P, P, P, P, P, P, S, S, P, PP], I),
         "gg_groth16_finalize_ex": ([I, P, P, P, P, P, P, P, P, P, P, P], I),
+        "gg_groth16_finalize_begin": ([I, P, P, P, P, PP], I),
+        "gg_groth16_finalize_end": ([P, P, P, P, P, P, P, P], I),
         "gg_bls12_381_g2_jac_to_affine": ([P, P], I),
         "gg_bls12_381_g2_jac_add": ([P, P, P], I),
         "gg_bls12_381_g2_scalar_mul": ([P, P, P], I),
@@ -192,6 +194,7 @@ EXPORTED = [
     "gg_plonk_pk_create_ex", "gg_plonk_pk_create_shard_ex", "gg_plonk_pk_info", "gg_plonk_proof_size_ex",
     "gg_plonk_pk_vk", "gg_plonk_commit_lagrange", "gg_plonk_proof_size", "gg_plonk_prove",
     "gg_plonk_last_timings", "gg_groth16_pk_create_ex", "gg_groth16_finalize_ex",
+    "gg_groth16_finalize_begin", "gg_groth16_finalize_end",
     "gg_bls12_381_g2_jac_to_affine", "gg_bls12_381_g2_jac_add", "gg_bls12_381_g2_scalar_mul",
     "gg_groth16_mpk_create", "gg_groth16_mpk_release", "gg_groth16_mpk_info", "gg_groth16_mpk_prove",
     "gg_groth16_mpk_last_timings", "gg_groth16_mpk_create_ex", "gg_groth16_mpk_prove_ex",

@@ -450,6 +450,39 @@ def add_partials(parts: Sequence[bytes]) -> bytes:
     return bytes(acc)
 
 
+class FixedTerms:
+    """gg_groth16_finalize_begin / _end: the fixed-point terms of prove.go:177-192
+    (r.delta, s.delta, kr.delta, s.delta2) computed on host threads while the
+    sharded prove runs; finish() combines them with the summed partials."""
+
+    def __init__(self, data: ProvingKeyData, r: bytes, s: bytes):
+        cid = GG_CURVE_BN254 if data.curve == "bn254" else GG_CURVE_BLS12_381
+        h = ctypes.c_void_p()
+        check(lib.gg_groth16_finalize_begin(cid, ptr(data.delta1), ptr(data.delta2), ptr(r), ptr(s),
+                                            ctypes.byref(h)))
+        self.data, self.handle = data, h
+
+    def finish(self, partials: bytes) -> Proof:
+        g1b, g2b = _SIZES[self.data.curve]
+        ar, bs, krs = bytearray(g1b), bytearray(g2b), bytearray(g1b)
+        h, self.handle = self.handle, None
+        d = self.data
+        check(lib.gg_groth16_finalize_end(h, ptr(d.alpha1), ptr(d.beta1), ptr(d.beta2), ptr(partials),
+                                          ptr(ar), ptr(bs), ptr(krs)))
+        return Proof(bytes(ar), bytes(bs), bytes(krs))
+
+    def close(self):
+        if self.handle:
+            h, self.handle = self.handle, None
+            lib.gg_groth16_finalize_end(h, None, None, None, None, None, None, None)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def finalize(data: ProvingKeyData, partials: bytes, r: bytes, s: bytes) -> Proof:
     """Combination of prove.go:177-299 on the summed partials (host, gg_groth16_finalize_ex)."""
     g1b, g2b = _SIZES[data.curve]
@@ -479,21 +512,36 @@ def prove_distributed(pk: ProvingKeyShard, solution: Solution, *opts, r: bytes =
             tdist.broadcast(rs, 0)
         rsb = bytes(rs.cpu().numpy())
         r, s = rsb[:32], rsb[32:]
-    return gather_and_finalize(pk.data, prove_partial(pk, solution), r, s, device)
+    fixed = FixedTerms(pk.data, r, s)  # host threads, overlapped with the GPU work
+    try:
+        part = prove_partial(pk, solution)
+    except BaseException:
+        fixed.close()
+        raise
+    return gather_and_finalize(pk.data, part, r, s, device, fixed=fixed)
 
 
-def gather_and_finalize(data: ProvingKeyData, part: bytes, r: bytes, s: bytes, device=None) -> Proof:
-    """All-gather every rank's 576-B partials, add them exactly, combine (all ranks)."""
+def gather_and_finalize(data: ProvingKeyData, part: bytes, r: bytes, s: bytes, device=None,
+                        fixed: "FixedTerms" = None) -> Proof:
+    """All-gather every rank's 576-B partials, add them exactly, combine (all ranks).
+    fixed: the fixed-point terms already started (FixedTerms) for this r, s."""
     import torch
     import torch.distributed as tdist
     world = tdist.get_world_size() if tdist.is_initialized() else 1
-    if world > 1:
-        t = torch.frombuffer(bytearray(part), dtype=torch.uint8)
-        if device is not None:
-            t = t.to(device)
-        bufs = [torch.empty_like(t) for _ in range(world)]
-        tdist.all_gather(bufs, t)
-        part = add_partials([bytes(b.cpu().numpy()) for b in bufs])
+    try:
+        if world > 1:
+            t = torch.frombuffer(bytearray(part), dtype=torch.uint8)
+            if device is not None:
+                t = t.to(device)
+            bufs = [torch.empty_like(t) for _ in range(world)]
+            tdist.all_gather(bufs, t)
+            part = add_partials([bytes(b.cpu().numpy()) for b in bufs])
+    except BaseException:
+        if fixed is not None:
+            fixed.close()
+        raise
+    if fixed is not None:
+        return fixed.finish(part)
     return finalize(data, part, r, s)
 
 
@@ -595,5 +643,10 @@ def prove_distributed_h(pk: ProvingKeyShard, hs: HShard, xchg: TorchExchange, so
     cfg = backend.new_prover_config(*opts)
     if not backend.accelerated(cfg):
         raise RuntimeError("accelerated prover requested without with_amd_acceleration()")
-    part = prove_partial_dist(pk, hs, solution, xchg, xchg.send.data_ptr(), xchg.recv.data_ptr())
-    return gather_and_finalize(pk.data, part, r, s, device)
+    fixed = FixedTerms(pk.data, r, s)  # host threads, overlapped with the GPU work
+    try:
+        part = prove_partial_dist(pk, hs, solution, xchg, xchg.send.data_ptr(), xchg.recv.data_ptr())
+    except BaseException:
+        fixed.close()
+        raise
+    return gather_and_finalize(pk.data, part, r, s, device, fixed=fixed)

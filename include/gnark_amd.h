@@ -287,6 +287,19 @@ int gg_groth16_finalize_ex(int curve, const void *alpha1, const void *beta1, con
                            const void *beta2, const void *delta2, const void *partials,
                            const void *r_mont, const void *s_mont, void *ar_aff, void *bs_aff,
                            void *krs_aff);
+/* gg_groth16_finalize in two halves, so the fixed-point terms of
+ * prove.go:177-192, 293-296 (r.delta, s.delta, kr.delta, s.delta2: host scalar
+ * multiplications independent of the MSMs) run on host threads while a
+ * sharded prove's GPU work and partial exchange are in flight.  begin starts
+ * them; end waits for them, combines them with the summed partials
+ * (prove.go:206-299) and releases the handle.  end with partials == NULL only
+ * releases it (a prove that failed). */
+typedef struct gg_g16_fixed *gg_g16_fixed_t;
+int gg_groth16_finalize_begin(int curve, const void *delta1, const void *delta2, const void *r_mont,
+                              const void *s_mont, gg_g16_fixed_t *out);
+int gg_groth16_finalize_end(gg_g16_fixed_t h, const void *alpha1, const void *beta1,
+                            const void *beta2, const void *partials, void *ar_aff, void *bs_aff,
+                            void *krs_aff);
 
 /* ---- distributed computeH ("four-step multi-GPU NTT").
  * n = 2^log_n = m * world (world a power of two <= 16, n >= world^2).  Rank r
