@@ -41,6 +41,10 @@ MIMC_ROUNDS = 85      # 3 constraints per round; 2^(log_n-8) chains -> 255 * 2^(
 ROOFLINE_PROVES = 3   # serial proves timed kernel by kernel for the roofline
 
 
+SPLIT_DESC = {"stripes": "bucket stripes of the whole A/B/K/G2 tables held on every GPU",
+              "wires": "wire slices of the A/B/K/G2 tables", None: ""}
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -286,15 +290,18 @@ def main():
                                   else "resident in HBM when the timed region starts"),
                    "log_n": args.log_n, "n_constraints": ncons, "n_wires": g.shape["nw"],
                    "inputs": "host" if args.host_inputs else "device",
-                   "parallelism": ("key shard x%d (wires + Z positions), distributed computeH "
+                   "parallelism": ("key shard x%d (%s + Z positions), distributed computeH "
                                    "(3 RCCL all-to-alls), RCCL all-gather of 576-B partials; one process per "
-                                   "GPU (torch.distributed.run)" % world) if mode == "torch" else
-                                  ("key shard x%d on devices %s (wires + Z positions), distributed computeH "
-                                   "(3 all-to-alls as in-library xGMI peer copies), partials summed in the "
-                                   "library; ONE process (gg_groth16_mpk_*, the Go shape)"
-                                   % (n_shards, devices)) if mode == "mpk" else
+                                   "GPU (torch.distributed.run)" % (world, SPLIT_DESC[g.split])) if mode == "torch"
+                                  else ("key shard x%d on devices %s (%s + Z positions), distributed computeH "
+                                        "(3 all-to-alls as in-library xGMI peer copies), partials summed in the "
+                                        "library; ONE process (gg_groth16_mpk_*, the Go shape)"
+                                        % (n_shards, devices, SPLIT_DESC[g.split])) if mode == "mpk" else
                                   "one GPU, 5 concurrent HIP streams",
-                   "launcher": mode, "shards": n_shards},
+                   "split": g.split,
+                   "launcher": mode, "shards": n_shards,
+                   # GG_MPK_SOLO=r: timing rehearsal of ONE shard's work (no peers, invalid proof)
+                   "solo_shard": int(os.environ["GG_MPK_SOLO"]) if os.environ.get("GG_MPK_SOLO") else None},
         "prove_ms": ms_per_step, "stage_ms": stage, "proof_identical_on_all_ranks": same,
         "other_inputs": other,
         "product_paths": {
@@ -409,6 +416,7 @@ class Groth16Bench:
         from gnark_amd import backend, groth16, msm, DeviceBuffer
         self.log_n, self.rank, self.world, self.dist, self.xdev = log_n, rank, world, dist, xdev
         self.devices = devices  # one process, N GPUs (gg_groth16_mpk_*)
+        self.split = None  # N > 1: "stripes" (bucket stripes) or "wires" (wire slices)
         self.shape = sh = mimc_shape(log_n)
         n, nw, nbp = 1 << log_n, sh["nw"], sh["nb_public"]
         infA, infB = sh["infA"], sh["infB"]
@@ -431,9 +439,26 @@ class Groth16Bench:
             if devices:
                 self.pk = groth16.MultiGpuProvingKey(self.data, devices)
                 self.nB2 = self.pk.base_info(groth16.BASE_B2)[0]
+                self.split = self.pk.split()
             else:
                 self.pk = groth16.ProvingKey(self.data)
                 self.nB2 = nB
+        elif world & (world - 1) == 0 and os.environ.get("GG_MPK_SPLIT", "stripes") != "wires":
+            # bucket stripes: every rank holds the whole A, B, K, G2 tables (the
+            # same points on every rank: fixed seeds) and its Z slice; its A, B1,
+            # K, G2 MSMs take the buckets b = rank mod world
+            _, _, zl, zh = groth16.shard_ranges(nw, n, rank, world)
+            nA, nB = int((infA == 0).sum()), int((infB == 0).sum())
+            self.data = groth16.ProvingKeyData(
+                log_n=log_n, g1_A=g1pts(nA, 101), g1_B=g1pts(nB, 102), g1_Z=b"",
+                g1_K=g1pts(nw - nbp, 104), g2_B=g2pts(nB, 108), **common)
+            self.pk = groth16.ProvingKeyStripe(self.data, rank, world, g1_Z=g1pts(zh - zl, sd + 3), z_lo=zl)
+            self.nB2 = nB
+            self.split = "stripes"
+            assert groth16.dist_h_supported(n, world)
+            self.hs = groth16.HShard(log_n, rank, world)
+            self.xchg = groth16.TorchExchange(self.hs.exchange_bytes,
+                                              torch.device("cuda", torch.cuda.current_device()))
         else:
             lo, hi, zl, zh = groth16.shard_ranges(nw, n, rank, world)
             nA = int((infA[lo:hi] == 0).sum())
@@ -446,6 +471,7 @@ class Groth16Bench:
                                                g2_B=b"", **common)
             self.pk = groth16.ProvingKeyShard(self.data, rank, world, shard=shard)
             self.nB2 = nB
+            self.split = "wires"
             del shard
             assert groth16.dist_h_supported(n, world)
             self.hs = groth16.HShard(log_n, rank, world)

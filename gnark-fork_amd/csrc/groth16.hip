@@ -24,6 +24,8 @@ struct gg_msm_base;
 
 namespace gg {
 struct MsmSort;
+struct MsmScratch;
+struct MsmWork;
 void compute_h_device(gg_domain* d, Fr* A, Fr* B, Fr* C, Fr* H, hipStream_t st);
 void msm_device(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st);
 size_t msm_scalars_needed(gg_msm_base* b);
@@ -32,8 +34,13 @@ gg_msm_base* msm_base_create_internal(int group, const void* host_points, size_t
 int choose_groups_multi(const double* bytes, const int* W, int k, double extra);
 bool msm_same_shape(const gg_msm_base* a, const gg_msm_base* b);
 MsmSort* msm_own_sort(gg_msm_base* b);
-void msm_prepare_dev(gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
-void msm_finish_dev(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st);
+void msm_prepare_dev(gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st, int slog = 0,
+                     uint32_t sres = 0);
+void msm_finish_dev(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st, MsmScratch* scr = nullptr);
+MsmWork* msm_work_new();
+void msm_work_delete(MsmWork* w);
+MsmSort* msm_work_sort(MsmWork* w);
+MsmScratch* msm_work_scratch(MsmWork* w);
 int msm_base_window(const gg_msm_base* b);
 int choose_c(size_t n, size_t point_bytes, int total_bits);
 void hshard_run(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len, bool compact, Fr* send,
@@ -75,12 +82,53 @@ static PointSizes point_sizes(int curve) {
     return {96, 192, 144, 288};
 }
 
+// The wire-indexed tables of a key (or of a wire shard): A and K (infinity
+// holes kept, one sort of the wires), B and G2 B (B-filtered, one sort).  A
+// bucket-stripe multi-GPU key keeps ONE whole copy per device, shared by the
+// stripe shards placed there.
+struct WireBases {
+    gg_msm_base_t A = nullptr, B = nullptr, K = nullptr, B2 = nullptr;
+    bool share_AK = false, share_B = false;
+    int groups = 1;
+    WireBases() = default;
+    WireBases(const WireBases&) = delete;
+    WireBases& operator=(const WireBases&) = delete;
+    ~WireBases() {
+        for (gg_msm_base_t b : {A, B, K, B2})
+            if (b) gg_msm_base_release(b);
+    }
+};
+
+// MSM sort + scratch of one prove over shared tables (a stripe shard's own)
+struct WorkSet {
+    MsmWork *A = nullptr, *B = nullptr, *K = nullptr, *B2 = nullptr;
+    WorkSet() {
+        A = msm_work_new();
+        B = msm_work_new();
+        K = msm_work_new();
+        B2 = msm_work_new();
+    }
+    WorkSet(const WorkSet&) = delete;
+    WorkSet& operator=(const WorkSet&) = delete;
+    ~WorkSet() {
+        for (MsmWork* w : {A, B, K, B2})
+            if (w) msm_work_delete(w);
+    }
+};
+
 struct gg_groth16_pk {
     int curve = GG_CURVE_BN254;
     int log_n = 0;
     size_t n = 0;
     gg_domain_t dom = nullptr;
+    // A, B, K, B2 alias wb's tables (shared between the stripe shards of one device)
+    std::shared_ptr<WireBases> wb;
     gg_msm_base_t A = nullptr, B = nullptr, K = nullptr, Z = nullptr, B2 = nullptr;
+    // bucket stripe of a multi-GPU key: the A, B1, K and G2 MSMs of this shard
+    // take the buckets b = spart mod 2^slog of the whole tables (slog = 0: all)
+    int slog = 0;
+    uint32_t spart = 0;
+    std::unique_ptr<WorkSet> work;  // stripe shards: their own sorts / scratch over the shared tables
     // pk.G1.{Alpha, Beta, Delta}, pk.G2.{Beta, Delta} in the curve's affine layout
     uint8_t alpha[96], beta[96], delta[96], beta2[192], delta2[192];
     size_t n_wires = 0, nb_public = 0;
@@ -97,11 +145,9 @@ struct gg_groth16_pk {
     std::mutex mu;
     ~gg_groth16_pk() {
         stager.reset();
-        if (A) gg_msm_base_release(A);
-        if (B) gg_msm_base_release(B);
-        if (K) gg_msm_base_release(K);
+        work.reset();
+        wb.reset();
         if (Z) gg_msm_base_release(Z);
-        if (B2) gg_msm_base_release(B2);
         if (dom) gg_domain_release(dom);
         for (hipStream_t x : {s0, s1, s2, s3, s4})
             if (x) (void)hipStreamDestroy(x);
@@ -117,49 +163,26 @@ static void ck(int rc) {
     if (rc != GG_OK) throw Error(rc, gg_last_error());
 }
 
-// Builds the resident key of one shard: wires [wire_lo, wire_hi) of the A, B, K
-// and G2 tables and domain positions [z_lo, z_lo + nZ) of Z.  The full key is
-// the single shard (0, n_wires, 0, n - 1).  Point arrays are the shard's
-// slices, in pk order (setup.go:259-275): g1_A = the non-infinity A points of
-// the shard's wires, likewise g1_B / g2_B; g1_K = the K points whose wires lie
-// in the shard (k_wire_index gives their absolute wire ids; NULL = the default
-// nb_public + j numbering of the full key).
-static void pk_build(gg_groth16_pk* pk, int curve, int log_n, const void* omega_mont, const void* coset_gen_mont,
-                     const void* g1_A, size_t nA, const void* g1_B, size_t nB, const void* g1_Z,
-                     size_t z_lo, size_t nZ, const void* g1_K, size_t nK, const void* alpha1,
-                     const void* beta1, const void* delta1, const void* g2_B, const void* beta2,
-                     const void* delta2, const uint8_t* inf_A, const uint8_t* inf_B, size_t n_wires,
-                     size_t nb_public, const uint32_t* k_wire_index, size_t lo, size_t hi) {
-    GG_CHECK(omega_mont && coset_gen_mont && alpha1 && beta1 && delta1 && beta2 && delta2,
-             GG_ERR_INVALID_ARG, "null argument");
+// The A, K, B and G2 B tables of wires [lo, hi) (pk order, setup.go:259-275):
+// g1_A = the non-infinity A points of those wires, likewise g1_B / g2_B; g1_K =
+// the K points whose wires lie in the range (k_wire_index gives their absolute
+// wire ids; NULL = the default nb_public + j numbering of the full key).  One
+// precompute-group count for every table (bases that share a sort need equal
+// shapes), the smallest whose tables fit HBM beside the proof's scratch and
+// the nZ Z points that will sit beside them.
+static std::shared_ptr<WireBases> wire_bases_build(int curve, int log_n, const void* g1_A, size_t nA,
+                                                   const void* g1_B, size_t nB, const void* g1_K, size_t nK,
+                                                   const void* g2_B, const uint8_t* inf_A, const uint8_t* inf_B,
+                                                   size_t n_wires, size_t nb_public, const uint32_t* k_wire_index,
+                                                   size_t lo, size_t hi, size_t nZ) {
     GG_CHECK(inf_A && inf_B, GG_ERR_INVALID_ARG, "null infinity masks");
     GG_CHECK(nb_public <= n_wires, GG_ERR_INVALID_ARG, "nb_public > n_wires");
-    GG_CHECK(log_n >= 0 && log_n <= 28, GG_ERR_INVALID_ARG, "log_n out of range");
     GG_CHECK(lo <= hi && hi <= n_wires, GG_ERR_INVALID_ARG, "bad wire shard range");
     GG_CHECK(curve == GG_CURVE_BN254 || curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "bad curve");
     const PointSizes ps = point_sizes(curve);
     const int g1 = curve == GG_CURVE_BN254 ? GG_G1 : GG_BLS12_381_G1;
     const int g2 = curve == GG_CURVE_BN254 ? GG_G2 : GG_BLS12_381_G2;
     const int tbits = curve == GG_CURVE_BN254 ? 255 : 256;
-    pk->curve = curve;
-    pk->log_n = log_n;
-    pk->n = (size_t)1 << log_n;
-    pk->n_wires = n_wires;
-    pk->nb_public = nb_public;
-    pk->wire_lo = lo;
-    pk->wire_hi = hi;
-    pk->z_lo = z_lo;
-    pk->nZ = nZ;
-    const size_t nz_full = pk->n > 1 ? pk->n - 1 : 0;
-    GG_CHECK(z_lo + nZ <= nz_full, GG_ERR_INVALID_ARG,
-             "Z shard beyond domain cardinality - 1 (setup.go:266)");
-    GG_HIP(hipGetDevice(&pk->device));
-    memcpy(pk->alpha, alpha1, ps.g1a);
-    memcpy(pk->beta, beta1, ps.g1a);
-    memcpy(pk->delta, delta1, ps.g1a);
-    memcpy(pk->beta2, beta2, ps.g2a);
-    memcpy(pk->delta2, delta2, ps.g2a);
-    ck(gg_domain_create_ex(curve, log_n, omega_mont, coset_gen_mont, &pk->dom));
     // wire index maps (prove.go:151-175: drop wires whose A/B point is infinity),
     // relative to the shard's first wire
     std::vector<uint32_t> ia, ib, ik;
@@ -179,15 +202,11 @@ static void pk_build(gg_groth16_pk* pk, int curve, int log_n, const void* omega_
     GG_CHECK(nA == 0 || g1_A, GG_ERR_INVALID_ARG, "null g1_A");
     GG_CHECK(nB == 0 || (g1_B && g2_B), GG_ERR_INVALID_ARG, "null g1_B / g2_B");
     GG_CHECK(nK == 0 || g1_K, GG_ERR_INVALID_ARG, "null g1_K");
-    GG_CHECK(nZ == 0 || g1_Z, GG_ERR_INVALID_ARG, "null g1_Z");
     const size_t nw = hi - lo;
     const int cAK = choose_c(std::max<size_t>(nw, 1), ps.g1a, tbits);
     const int cB = choose_c(std::max<size_t>(nB, 1), 128, tbits);  // B1 shares its sort with G2
     const int cZ = choose_c(std::max<size_t>(nZ, 1), ps.g1a, tbits);
-    // the memory knob: one precompute-group count for the whole key (bases that
-    // share a sort need equal shapes), the smallest whose tables fit HBM beside
-    // the proof's scratch (3 sorts of 16 B per entry, domain and solution vectors)
-    int groups;
+    auto wb = std::make_shared<WireBases>();
     {
         auto W = [&](int c) { return (tbits + c - 1) / c; };
         const double g1a = (double)ps.g1a, g2a = (double)ps.g2a;
@@ -195,27 +214,128 @@ static void pk_build(gg_groth16_pk* pk, int curve, int log_n, const void* omega_
                                  W(cB) * (double)nB * g2a, W(cZ) * (double)nZ * g1a};
         const int ws[5] = {W(cAK), W(cAK), W(cB), W(cB), W(cZ)};
         const double extra = 16.0 * (W(cAK) * (double)nw + W(cB) * (double)nB + W(cZ) * (double)nZ) +
-                             12.0 * 32.0 * (double)pk->n;
-        groups = choose_groups_multi(bytes, ws, 5, extra);
+                             12.0 * 32.0 * (double)((size_t)1 << log_n);
+        wb->groups = choose_groups_multi(bytes, ws, 5, extra);
     }
     // dense wire-indexed A and K (holes = infinity), one window size for both
     {
         const size_t pb = ps.g1a;
         std::vector<uint8_t> dense(nw * pb, 0);
         for (size_t j = 0; j < nA; j++) memcpy(&dense[(size_t)ia[j] * pb], (const uint8_t*)g1_A + j * pb, pb);
-        pk->A = msm_base_create_internal(g1, dense.data(), nw, nullptr, cAK, true, groups);
+        wb->A = msm_base_create_internal(g1, dense.data(), nw, nullptr, cAK, true, wb->groups);
         std::fill(dense.begin(), dense.end(), 0);
         for (size_t j = 0; j < nK; j++) memcpy(&dense[(size_t)ik[j] * pb], (const uint8_t*)g1_K + j * pb, pb);
-        pk->K = msm_base_create_internal(g1, dense.data(), nw, nullptr, cAK, true, groups);
+        wb->K = msm_base_create_internal(g1, dense.data(), nw, nullptr, cAK, true, wb->groups);
     }
-    pk->B = msm_base_create_internal(g1, g1_B, nB, ib.data(), cB, false, groups);
-    pk->B2 = msm_base_create_internal(g2, g2_B, nB, ib.data(), msm_base_window(pk->B), false, groups);
-    pk->Z = msm_base_create_internal(g1, g1_Z, nZ, nullptr, cZ, false, groups);
-    pk->share_AK = msm_same_shape(pk->A, pk->K);
-    pk->share_B = msm_same_shape(pk->B, pk->B2);
+    wb->B = msm_base_create_internal(g1, g1_B, nB, ib.data(), cB, false, wb->groups);
+    wb->B2 = msm_base_create_internal(g2, g2_B, nB, ib.data(), msm_base_window(wb->B), false, wb->groups);
+    wb->share_AK = msm_same_shape(wb->A, wb->K);
+    wb->share_B = msm_same_shape(wb->B, wb->B2);
+    return wb;
+}
+
+// The rest of a resident key (shard) around its wire tables: domain, Z
+// positions [z_lo, z_lo + nZ), the fixed points, streams.  slog > 0: a bucket
+// stripe shard over whole (shared) wire tables.
+static void pk_finish(gg_groth16_pk* pk, std::shared_ptr<WireBases> wb, int curve, int log_n,
+                      const void* omega_mont, const void* coset_gen_mont, const void* g1_Z, size_t z_lo, size_t nZ,
+                      const void* alpha1, const void* beta1, const void* delta1, const void* beta2,
+                      const void* delta2, size_t n_wires, size_t nb_public, size_t lo, size_t hi, int slog,
+                      uint32_t spart) {
+    GG_CHECK(omega_mont && coset_gen_mont && alpha1 && beta1 && delta1 && beta2 && delta2,
+             GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(log_n >= 0 && log_n <= 28, GG_ERR_INVALID_ARG, "log_n out of range");
+    const PointSizes ps = point_sizes(curve);
+    const int g1 = curve == GG_CURVE_BN254 ? GG_G1 : GG_BLS12_381_G1;
+    const int tbits = curve == GG_CURVE_BN254 ? 255 : 256;
+    pk->curve = curve;
+    pk->log_n = log_n;
+    pk->n = (size_t)1 << log_n;
+    pk->n_wires = n_wires;
+    pk->nb_public = nb_public;
+    pk->wire_lo = lo;
+    pk->wire_hi = hi;
+    pk->z_lo = z_lo;
+    pk->nZ = nZ;
+    const size_t nz_full = pk->n > 1 ? pk->n - 1 : 0;
+    GG_CHECK(z_lo + nZ <= nz_full, GG_ERR_INVALID_ARG,
+             "Z shard beyond domain cardinality - 1 (setup.go:266)");
+    GG_CHECK(nZ == 0 || g1_Z, GG_ERR_INVALID_ARG, "null g1_Z");
+    GG_HIP(hipGetDevice(&pk->device));
+    memcpy(pk->alpha, alpha1, ps.g1a);
+    memcpy(pk->beta, beta1, ps.g1a);
+    memcpy(pk->delta, delta1, ps.g1a);
+    memcpy(pk->beta2, beta2, ps.g2a);
+    memcpy(pk->delta2, delta2, ps.g2a);
+    ck(gg_domain_create_ex(curve, log_n, omega_mont, coset_gen_mont, &pk->dom));
+    pk->wb = std::move(wb);
+    pk->A = pk->wb->A;
+    pk->B = pk->wb->B;
+    pk->K = pk->wb->K;
+    pk->B2 = pk->wb->B2;
+    pk->share_AK = pk->wb->share_AK;
+    pk->share_B = pk->wb->share_B;
+    if (slog) {
+        int cmin = 64;
+        for (gg_msm_base_t b : {pk->A, pk->B})
+            if (msm_scalars_needed(b)) cmin = std::min(cmin, msm_base_window(b));
+        GG_CHECK(slog <= cmin - 2, GG_ERR_INVALID_ARG, "bucket stripe too fine for the tables' windows");
+        GG_CHECK(spart < (1u << slog), GG_ERR_INVALID_ARG, "stripe part out of range");
+        pk->slog = slog;
+        pk->spart = spart;
+        pk->work.reset(new WorkSet());
+    }
+    const int cZ = choose_c(std::max<size_t>(nZ, 1), ps.g1a, tbits);
+    pk->Z = msm_base_create_internal(g1, g1_Z, nZ, nullptr, cZ, false, pk->wb->groups);
     for (hipStream_t* x : {&pk->s0, &pk->s1, &pk->s2, &pk->s3, &pk->s4})
         GG_HIP(hipStreamCreateWithFlags(x, hipStreamNonBlocking));
 }
+
+// Builds the resident key of one shard: wires [wire_lo, wire_hi) of the A, B, K
+// and G2 tables and domain positions [z_lo, z_lo + nZ) of Z.  The full key is
+// the single shard (0, n_wires, 0, n - 1).
+static void pk_build(gg_groth16_pk* pk, int curve, int log_n, const void* omega_mont, const void* coset_gen_mont,
+                     const void* g1_A, size_t nA, const void* g1_B, size_t nB, const void* g1_Z,
+                     size_t z_lo, size_t nZ, const void* g1_K, size_t nK, const void* alpha1,
+                     const void* beta1, const void* delta1, const void* g2_B, const void* beta2,
+                     const void* delta2, const uint8_t* inf_A, const uint8_t* inf_B, size_t n_wires,
+                     size_t nb_public, const uint32_t* k_wire_index, size_t lo, size_t hi) {
+    GG_CHECK(log_n >= 0 && log_n <= 28, GG_ERR_INVALID_ARG, "log_n out of range");
+    auto wb = wire_bases_build(curve, log_n, g1_A, nA, g1_B, nB, g1_K, nK, g2_B, inf_A, inf_B, n_wires, nb_public,
+                               k_wire_index, lo, hi, nZ);
+    pk_finish(pk, std::move(wb), curve, log_n, omega_mont, coset_gen_mont, g1_Z, z_lo, nZ, alpha1, beta1, delta1,
+              beta2, delta2, n_wires, nb_public, lo, hi, 0, 0);
+}
+
+namespace gg {
+// for the one-process multi-GPU key (groth16_multi.hip): whole wire tables
+// once per device, stripe shards over them
+std::shared_ptr<WireBases> g16_wire_bases(int curve, int log_n, const void* g1_A, size_t nA, const void* g1_B,
+                                          size_t nB, const void* g1_K, size_t nK, const void* g2_B,
+                                          const uint8_t* inf_A, const uint8_t* inf_B, size_t n_wires,
+                                          size_t nb_public, const uint32_t* k_wire_index, size_t nZ) {
+    return wire_bases_build(curve, log_n, g1_A, nA, g1_B, nB, g1_K, nK, g2_B, inf_A, inf_B, n_wires, nb_public,
+                            k_wire_index, 0, n_wires, nZ);
+}
+gg_groth16_pk* g16_stripe_shard(std::shared_ptr<WireBases> wb, int curve, int log_n, const void* omega_mont,
+                                const void* coset_gen_mont, const void* g1_Z, size_t z_lo, size_t nZ,
+                                const void* alpha1, const void* beta1, const void* delta1, const void* beta2,
+                                const void* delta2, size_t n_wires, size_t nb_public, int slog, uint32_t spart) {
+    std::unique_ptr<gg_groth16_pk> pk(new gg_groth16_pk());
+    pk_finish(pk.get(), std::move(wb), curve, log_n, omega_mont, coset_gen_mont, g1_Z, z_lo, nZ, alpha1, beta1,
+              delta1, beta2, delta2, n_wires, nb_public, 0, n_wires, slog, spart);
+    return pk.release();
+}
+// the smallest window of a key's wire tables (a stripe needs log2(world) <= it - 2)
+int g16_wire_window(int curve, size_t n_wires, size_t nB) {
+    const PointSizes ps = point_sizes(curve);
+    const int tbits = curve == GG_CURVE_BN254 ? 255 : 256;
+    int c = 64;
+    if (n_wires) c = std::min(c, choose_c(n_wires, ps.g1a, tbits));
+    if (nB) c = std::min(c, choose_c(nB, 128, tbits));
+    return c;
+}
+}  // namespace gg
 
 extern "C" int gg_groth16_pk_create_ex(int curve, int log_n, const void* omega_mont, const void* coset_gen_mont,
                                        const void* g1_A, size_t nA, const void* g1_B, size_t nB,
@@ -284,6 +404,36 @@ extern "C" int gg_groth16_pk_create_shard(int log_n, const void* omega_mont, con
     return gg_groth16_pk_create_shard_ex(GG_CURVE_BN254, log_n, omega_mont, coset_gen_mont, g1_A, nA, g1_B, nB,
                                          g1_Z, z_lo, nZ, g1_K, nK, alpha1, beta1, delta1, g2_B, beta2, delta2,
                                          inf_A, inf_B, n_wires, nb_public, k_wire_index, wire_lo, wire_hi, out);
+}
+
+extern "C" int gg_groth16_pk_create_stripe_ex(int curve, int log_n, const void* omega_mont,
+                                              const void* coset_gen_mont, const void* g1_A, size_t nA,
+                                              const void* g1_B, size_t nB, const void* g1_Z, size_t z_lo,
+                                              size_t nZ, const void* g1_K, size_t nK, const void* alpha1,
+                                              const void* beta1, const void* delta1, const void* g2_B,
+                                              const void* beta2, const void* delta2, const uint8_t* inf_A,
+                                              const uint8_t* inf_B, size_t n_wires, size_t nb_public,
+                                              const uint32_t* k_wire_index, int stripe_log, int stripe_part,
+                                              gg_groth16_pk_t* out) {
+    GG_CAPI_BEGIN
+    GG_CHECK(out, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(stripe_log >= 0 && stripe_log <= 8 && stripe_part >= 0 && stripe_part < (1 << stripe_log),
+             GG_ERR_INVALID_ARG, "stripe_log in [0, 8], stripe_part < 2^stripe_log");
+    GG_CHECK(log_n >= 0 && log_n <= 28, GG_ERR_INVALID_ARG, "log_n out of range");
+    if (!k_wire_index) GG_CHECK(nb_public + nK <= n_wires, GG_ERR_INVALID_ARG, "len(pk.G1.K) too large");
+    auto wb = wire_bases_build(curve, log_n, g1_A, nA, g1_B, nB, g1_K, nK, g2_B, inf_A, inf_B, n_wires, nb_public,
+                               k_wire_index, 0, n_wires, nZ);
+    *out = g16_stripe_shard(std::move(wb), curve, log_n, omega_mont, coset_gen_mont, g1_Z, z_lo, nZ, alpha1, beta1,
+                            delta1, beta2, delta2, n_wires, nb_public, stripe_log, (uint32_t)stripe_part);
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_pk_stripe(gg_groth16_pk_t pk, int* stripe_log, int* stripe_part) {
+    GG_CAPI_BEGIN
+    GG_CHECK(pk, GG_ERR_INVALID_ARG, "null key");
+    if (stripe_log) *stripe_log = pk->slog;
+    if (stripe_part) *stripe_part = (int)pk->spart;
+    GG_CAPI_END
 }
 
 extern "C" int gg_groth16_pk_base_info(gg_groth16_pk_t pk, int which, size_t* n_points, int* window_bits,
@@ -491,24 +641,34 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
     }));
     // wire sorts, enqueued from this thread before any finisher waits on their
     // events: A's (shared with K) on s2, B1's (shared with G2) on s3
+    // (a stripe shard sorts its bucket stripe into its own work set: the tables
+    // are shared with the other shards on this device)
     MsmSort *sAK = nullptr, *sB = nullptr, *sK = nullptr, *sB2 = nullptr;
+    MsmScratch *xA = nullptr, *xB = nullptr, *xK = nullptr, *xB2 = nullptr;
+    WorkSet* ws = pk->work.get();
     guarded([&] {
-        sAK = msm_own_sort(pk->A);
-        sB = msm_own_sort(pk->B);
-        sK = pk->share_AK ? sAK : msm_own_sort(pk->K);
-        sB2 = pk->share_B ? sB : msm_own_sort(pk->B2);
-        msm_prepare_dev(pk->A, sAK, wdev, pk->s2);
-        msm_prepare_dev(pk->B, sB, wdev, pk->s3);
-        if (!pk->share_AK) msm_prepare_dev(pk->K, sK, wdev, pk->s4);
-        if (!pk->share_B) msm_prepare_dev(pk->B2, sB2, wdev, pk->s0);
+        sAK = ws ? msm_work_sort(ws->A) : msm_own_sort(pk->A);
+        sB = ws ? msm_work_sort(ws->B) : msm_own_sort(pk->B);
+        sK = pk->share_AK ? sAK : (ws ? msm_work_sort(ws->K) : msm_own_sort(pk->K));
+        sB2 = pk->share_B ? sB : (ws ? msm_work_sort(ws->B2) : msm_own_sort(pk->B2));
+        if (ws) {
+            xA = msm_work_scratch(ws->A);
+            xB = msm_work_scratch(ws->B);
+            xK = msm_work_scratch(ws->K);
+            xB2 = msm_work_scratch(ws->B2);
+        }
+        msm_prepare_dev(pk->A, sAK, wdev, pk->s2, pk->slog, pk->spart);
+        msm_prepare_dev(pk->B, sB, wdev, pk->s3, pk->slog, pk->spart);
+        if (!pk->share_AK) msm_prepare_dev(pk->K, sK, wdev, pk->s4, pk->slog, pk->spart);
+        if (!pk->share_B) msm_prepare_dev(pk->B2, sB2, wdev, pk->s0, pk->slog, pk->spart);
     })();
     double t2 = now_ms(), te = t2;
     if (wcode == GG_OK) {  // the sorts are enqueued: run the finishers
-        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->A, sAK, out.a, pk->s2); t_a = now_ms() - a; }));
-        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->B, sB, out.b1, pk->s3); t_b = now_ms() - a; }));
-        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->K, sK, out.k, pk->s4); t_k = now_ms() - a; }));
+        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->A, sAK, out.a, pk->s2, xA); t_a = now_ms() - a; }));
+        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->B, sB, out.b1, pk->s3, xB); t_b = now_ms() - a; }));
+        spawn(guarded([&] { double a = now_ms(); msm_finish_dev(pk->K, sK, out.k, pk->s4, xK); t_k = now_ms() - a; }));
         t2 = now_ms();
-        guarded([&] { msm_finish_dev(pk->B2, sB2, out.b2, pk->s0); })();
+        guarded([&] { msm_finish_dev(pk->B2, sB2, out.b2, pk->s0, xB2); })();
         te = now_ms();
     }
     for (auto& w : workers) w.join();
@@ -619,7 +779,7 @@ extern "C" int gg_groth16_prove(gg_groth16_pk_t pk, const void* wires, size_t n_
     GG_CAPI_BEGIN
     check_prove_args(pk, wires, n_wires, sol_a, sol_b, sol_c, n_cons);
     GG_CHECK(r_mont && s_mont && ar_aff && bs_aff && krs_aff, GG_ERR_INVALID_ARG, "null argument");
-    GG_CHECK(pk->wire_lo == 0 && pk->wire_hi == pk->n_wires && pk->z_lo == 0 &&
+    GG_CHECK(pk->wire_lo == 0 && pk->wire_hi == pk->n_wires && pk->z_lo == 0 && pk->slog == 0 &&
                  pk->nZ == (pk->n > 1 ? pk->n - 1 : 0),
              GG_ERR_INVALID_ARG, "gg_groth16_prove needs the whole key; a shard proves with "
                                  "gg_groth16_prove_partial + gg_groth16_finalize");

@@ -20,9 +20,24 @@
 #include <memory>
 #include <cstring>
 #include <mutex>
+#include <algorithm>
 #include <string>
 #include <thread>
 #include <vector>
+
+struct gg_groth16_pk;
+struct WireBases;
+namespace gg {
+std::shared_ptr<WireBases> g16_wire_bases(int curve, int log_n, const void* g1_A, size_t nA, const void* g1_B,
+                                          size_t nB, const void* g1_K, size_t nK, const void* g2_B,
+                                          const uint8_t* inf_A, const uint8_t* inf_B, size_t n_wires,
+                                          size_t nb_public, const uint32_t* k_wire_index, size_t nZ);
+gg_groth16_pk* g16_stripe_shard(std::shared_ptr<WireBases> wb, int curve, int log_n, const void* omega_mont,
+                                const void* coset_gen_mont, const void* g1_Z, size_t z_lo, size_t nZ,
+                                const void* alpha1, const void* beta1, const void* delta1, const void* beta2,
+                                const void* delta2, size_t n_wires, size_t nb_public, int slog, uint32_t spart);
+int g16_wire_window(int curve, size_t n_wires, size_t nB);
+}  // namespace gg
 
 namespace {
 
@@ -66,6 +81,15 @@ bool dist_h_ok(size_t n, int world) {
 
 struct gg_groth16_mpk {
     int world = 0, curve = GG_CURVE_BN254;
+    // how the A, B1, K and G2 MSMs are split: bucket stripes (every device holds
+    // the whole wire tables, shard r takes the buckets b = r mod world) or wire
+    // slices (shard r holds wires [r W / world, (r + 1) W / world))
+    bool stripes = false;
+    // GG_MPK_SOLO=r (timing rehearsal only): a prove runs shard r ALONE -- its
+    // exchanges skip the peers, the other shards do nothing -- so one GPU
+    // times the work one GPU of an N-GPU node does (less the xGMI transfers);
+    // the proof it returns is not valid
+    int solo = -1;
     size_t n = 0, n_wires = 0;
     size_t g1a = 64, g2a = 128, g1j = 96, g2j = 192;  // the curve's point sizes
     bool dist = false;
@@ -74,6 +98,7 @@ struct gg_groth16_mpk {
     std::vector<gg_hshard_t> hs;
     std::vector<void*> send, recv;
     std::vector<hipStream_t> st;
+    std::vector<std::vector<hipStream_t>> xst;  // per shard: one copy stream per destination
     uint8_t alpha1[96], beta1[96], delta1[96], beta2[192], delta2[192];
     Barrier bar;
     std::mutex mu;  // one proof at a time per key
@@ -90,7 +115,10 @@ struct XCtx {
 // gg_exchange_fn of shard `rank`: chunk k of its send buffer -> chunk rank of
 // shard k's recv buffer.  First barrier: every shard's send is written and its
 // recv no longer read (the caller synchronised its stream); second: every push
-// into this shard's recv has landed.
+// into this shard's recv has landed.  The world pushes go out on one stream
+// each, so the copies to the N-1 peers run at once over their own xGMI links
+// (on one stream they would take the links one after another: at 2^24 over 8
+// GPUs, 392 MB per shard per proof).
 int mpk_exchange(void* ctx, const void* send_dev, void* recv_dev, size_t bytes) {
     XCtx* x = (XCtx*)ctx;
     gg_groth16_mpk* m = x->m;
@@ -98,16 +126,27 @@ int mpk_exchange(void* ctx, const void* send_dev, void* recv_dev, size_t bytes) 
     (void)recv_dev;
     if (!m->bar.wait()) return GG_ERR_INTERNAL;
     bool ok = hipSetDevice(m->dev[r]) == hipSuccess;
-    for (int k = 0; ok && k < m->world; k++)
+    for (int j = 0; ok && j < m->world; j++) {
+        const int k = (r + j) % m->world;  // staggered: shard r starts with its own chunk, then r+1, ...
+        if (m->solo >= 0 && k != r) continue;  // timing rehearsal: no peers
         ok = hipMemcpyPeerAsync((char*)m->recv[k] + (size_t)r * bytes, m->dev[k],
-                                (const char*)send_dev + (size_t)k * bytes, m->dev[r], bytes, m->st[r]) == hipSuccess;
-    ok = ok && hipStreamSynchronize(m->st[r]) == hipSuccess;
+                                (const char*)send_dev + (size_t)k * bytes, m->dev[r], bytes,
+                                m->xst[r][j]) == hipSuccess;
+    }
+    for (int j = 0; ok && j < m->world; j++) ok = hipStreamSynchronize(m->xst[r][j]) == hipSuccess;
     if (!ok) {
         (void)hipGetLastError();
         m->bar.abort();
         return GG_ERR_DEVICE;
     }
     return m->bar.wait() ? 0 : GG_ERR_INTERNAL;
+}
+
+// identity partials (Jacobian infinity: x = y = 1, z = 0 in Montgomery form --
+// gg_g1_jac_add treats z = 0 as the identity whatever x, y hold)
+void G16PartialsInf(int curve, uint8_t* p, size_t g1j, size_t g2j) {
+    (void)curve;
+    memset(p, 0, 4 * g1j + g2j);
 }
 
 void mpk_free(gg_groth16_mpk* m) {
@@ -118,6 +157,9 @@ void mpk_free(gg_groth16_mpk* m) {
         if (r < (int)m->send.size() && m->send[r]) (void)hipFree(m->send[r]);
         if (r < (int)m->recv.size() && m->recv[r]) (void)hipFree(m->recv[r]);
         if (r < (int)m->st.size() && m->st[r]) (void)hipStreamDestroy(m->st[r]);
+        if (r < (int)m->xst.size())
+            for (hipStream_t s : m->xst[r])
+                if (s) (void)hipStreamDestroy(s);
     }
     delete m;
 }
@@ -192,6 +234,7 @@ extern "C" int gg_groth16_mpk_create_ex(int curve, int log_n, const void* omega_
     m->send.assign(world, nullptr);
     m->recv.assign(world, nullptr);
     m->st.assign(world, nullptr);
+    m->xst.assign(world, {});
     m->bar.n = world;
     memcpy(m->alpha1, alpha1, m->g1a);
     memcpy(m->beta1, beta1, m->g1a);
@@ -224,9 +267,8 @@ extern "C" int gg_groth16_mpk_create_ex(int curve, int log_n, const void* omega_
     const uint8_t* K = (const uint8_t*)g1_K;
     const uint8_t* Z = (const uint8_t*)g1_Z;
     const size_t g1a = m->g1a, g2a = m->g2a;
-    on_shards(m.get(), [&](int r) -> int {
-        const size_t lo = n_wires * r / world, hi = n_wires * (r + 1) / world;
-        size_t zl, zh;
+    // Z positions of shard r: the slice the distributed computeH leaves on rank r
+    auto zrange = [&](int r, size_t& zl, size_t& zh) {
         if (m->dist) {
             const size_t mm = n / world;
             zl = std::min(r * mm, n - 1);
@@ -237,6 +279,85 @@ extern "C" int gg_groth16_mpk_create_ex(int curve, int log_n, const void* omega_
         }
         zl = std::min(zl, nZ);
         zh = std::min(zh, nZ);
+    };
+    // bucket stripes (default for a power-of-two world whose windows allow it;
+    // GG_MPK_SPLIT=wires keeps the wire slices): the whole wire tables once per
+    // device, each shard's A, B1, K, G2 MSMs over its 2^-log2(world) of the buckets
+    int slog = 0;
+    while ((1 << slog) < world) slog++;
+    {
+        const char* e = getenv("GG_MPK_SPLIT");
+        const bool want = !(e && strcmp(e, "wires") == 0);
+        m->stripes = want && world > 1 && (1 << slog) == world &&
+                     slog <= gg::g16_wire_window(curve, n_wires, nB) - 2;
+    }
+    if (m->stripes) {
+        std::vector<int> uniq;
+        for (int d : m->dev)
+            if (std::find(uniq.begin(), uniq.end(), d) == uniq.end()) uniq.push_back(d);
+        std::vector<std::shared_ptr<WireBases>> wbs(uniq.size());
+        std::vector<std::thread> th;
+        std::mutex emu;
+        std::string err;
+        int code = GG_OK;
+        for (size_t u = 0; u < uniq.size(); u++)
+            th.emplace_back([&, u] {
+                int rc = gg_set_device(uniq[u]);
+                try {
+                    if (rc) throw gg::Error(rc, gg_last_error());
+                    size_t zdev = 0;  // Z points of the shards placed on this device
+                    for (int r = 0; r < world; r++)
+                        if (m->dev[r] == uniq[u]) {
+                            size_t zl, zh;
+                            zrange(r, zl, zh);
+                            zdev += zh - zl;
+                        }
+                    wbs[u] = gg::g16_wire_bases(curve, log_n, g1_A, nA, g1_B, nB, g1_K, nK, g2_B, inf_A, inf_B,
+                                                n_wires, nb_public, k_wire_index, zdev);
+                } catch (const gg::Error& ex) {
+                    std::lock_guard<std::mutex> g(emu);
+                    if (code == GG_OK) { code = ex.code; err = ex.what(); }
+                } catch (const std::exception& ex) {
+                    std::lock_guard<std::mutex> g(emu);
+                    if (code == GG_OK) { code = GG_ERR_INTERNAL; err = ex.what(); }
+                }
+            });
+        for (auto& t : th) t.join();
+        if (code != GG_OK) throw gg::Error(code, "wire tables (device): " + err);
+        on_shards(m.get(), [&](int r) -> int {
+            size_t zl, zh;
+            zrange(r, zl, zh);
+            const size_t u = std::find(uniq.begin(), uniq.end(), m->dev[r]) - uniq.begin();
+            try {
+                m->pk[r] = gg::g16_stripe_shard(wbs[u], curve, log_n, omega_mont, coset_gen_mont, Z + zl * g1a, zl,
+                                                zh - zl, alpha1, beta1, delta1, beta2, delta2, n_wires, nb_public,
+                                                slog, (uint32_t)r);
+            } catch (const gg::Error& ex) {
+                gg::set_last_error(ex.what());
+                return ex.code;
+            }
+            if (hipStreamCreateWithFlags(&m->st[r], hipStreamNonBlocking) != hipSuccess) return GG_ERR_DEVICE;
+            if (!m->dist) return 0;
+            m->xst[r].assign(world, nullptr);
+            for (auto& x : m->xst[r])
+                if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return GG_ERR_DEVICE;
+            int rc = gg_hshard_create(log_n, omega_mont, coset_gen_mont, r, world, &m->hs[r]);
+            if (rc) return rc;
+            size_t mm = 0, xb = 0;
+            rc = gg_hshard_info(m->hs[r], &mm, &xb);
+            if (rc) return rc;
+            if (hipMalloc(&m->send[r], std::max<size_t>(xb, 256)) != hipSuccess ||
+                hipMalloc(&m->recv[r], std::max<size_t>(xb, 256)) != hipSuccess)
+                return GG_ERR_OOM;
+            return 0;
+        });
+        *out = m.release();
+        return GG_OK;
+    }
+    on_shards(m.get(), [&](int r) -> int {
+        const size_t lo = n_wires * r / world, hi = n_wires * (r + 1) / world;
+        size_t zl, zh;
+        zrange(r, zl, zh);
         // K points of this shard's wires, with absolute wire ids
         std::vector<uint8_t> kp;
         std::vector<uint32_t> kidx;
@@ -266,6 +387,9 @@ extern "C" int gg_groth16_mpk_create_ex(int curve, int log_n, const void* omega_
         if (rc) return rc;
         if (hipStreamCreateWithFlags(&m->st[r], hipStreamNonBlocking) != hipSuccess) return GG_ERR_DEVICE;
         if (!m->dist) return 0;
+        m->xst[r].assign(world, nullptr);
+        for (auto& s : m->xst[r])
+            if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GG_ERR_DEVICE;
         rc = gg_hshard_create(log_n, omega_mont, coset_gen_mont, r, world, &m->hs[r]);
         if (rc) return rc;
         size_t mm = 0, xb = 0;
@@ -304,6 +428,13 @@ extern "C" int gg_groth16_mpk_info(gg_groth16_mpk_t m, int* world, int* distribu
     GG_CHECK(m, GG_ERR_INVALID_ARG, "null key");
     if (world) *world = m->world;
     if (distributed_h) *distributed_h = m->dist ? 1 : 0;
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_mpk_split(gg_groth16_mpk_t m, int* bucket_stripes) {
+    GG_CAPI_BEGIN
+    GG_CHECK(m && bucket_stripes, GG_ERR_INVALID_ARG, "null argument");
+    *bucket_stripes = m->stripes ? 1 : 0;
     GG_CAPI_END
 }
 
@@ -346,12 +477,19 @@ extern "C" int gg_groth16_mpk_prove_ex(gg_groth16_mpk_t m, int inputs_on_device,
         gg_g16_fixed_t& h;
         ~FxGuard() { if (h) gg_groth16_finalize_end(h, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr); }
     } fx_guard{fx};
+    m->solo = -1;
+    if (const char* e = getenv("GG_MPK_SOLO")) m->solo = std::max(-1, std::min(atoi(e), m->world - 1));
+    m->bar.n = m->solo >= 0 ? 1 : m->world;
     m->bar.reset();
     const size_t pbytes = 4 * m->g1j + m->g2j;  // a | b1 | k | z | b2 (gg_groth16_prove_partial)
     std::vector<std::vector<uint8_t>> parts(m->world, std::vector<uint8_t>(pbytes));
     std::vector<XCtx> ctx(m->world);
     on_shards(m, [&](int r) -> int {
         ctx[r] = XCtx{m, r};
+        if (m->solo >= 0 && r != m->solo) {  // timing rehearsal: identity partials
+            G16PartialsInf(m->curve, parts[r].data(), m->g1j, m->g2j);
+            return 0;
+        }
         if (m->dist)
             return gg_groth16_prove_partial_dist(m->pk[r], m->hs[r], wires[r], n_wires, sol_a[r], sol_b[r], sol_c[r],
                                                  n_cons, inputs_on_device, mpk_exchange, &ctx[r], m->send[r],

@@ -105,15 +105,19 @@ MsmWork* msm_work_new() { return new MsmWork(); }
 void msm_work_delete(MsmWork* w) { delete w; }
 int msm_base_window(const gg_msm_base* b) { return b->c; }
 int msm_base_groups(const gg_msm_base* b) { return b->G; }
-void msm_prepare_dev(gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st) {
-    if (b->n) msm_prepare(b, s, scalars_dev, st);
+void msm_prepare_dev(gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st, int slog, uint32_t sres) {
+    if (b->n) msm_prepare(b, s, scalars_dev, st, slog, sres);
 }
-void msm_finish_dev(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st) {
-    if (b->group == GG_G1) msm_finish_g1(b, s, &b->own.scr, out_jac, st);
-    else if (b->group == GG_G2) msm_finish_g2(b, s, &b->own.scr, out_jac, st);
-    else if (b->group == GG_BLS12_381_G1) msm_finish_bls(b, s, &b->own.scr, out_jac, st);
-    else msm_finish_bls2(b, s, &b->own.scr, out_jac, st);
+// scr: the MSM's scratch (nullptr = the base's own)
+void msm_finish_dev(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st, MsmScratch* scr) {
+    if (!scr) scr = &b->own.scr;
+    if (b->group == GG_G1) msm_finish_g1(b, s, scr, out_jac, st);
+    else if (b->group == GG_G2) msm_finish_g2(b, s, scr, out_jac, st);
+    else if (b->group == GG_BLS12_381_G1) msm_finish_bls(b, s, scr, out_jac, st);
+    else msm_finish_bls2(b, s, scr, out_jac, st);
 }
+MsmSort* msm_work_sort(MsmWork* w) { return &w->sort; }
+MsmScratch* msm_work_scratch(MsmWork* w) { return &w->scr; }
 size_t msm_scalars_needed(gg_msm_base* b) {
     return b->has_sidx ? (b->n ? (size_t)b->max_sidx + 1 : 0) : b->n;
 }
@@ -136,5 +140,32 @@ extern "C" int gg_msm(gg_msm_base_t b, const void* scalars, size_t n_scalars, in
         sdev = b->own.scr.scal.as<Fr>();
     }
     msm_device_locked(b, sdev, out_jac, st);
+    GG_CAPI_END
+}
+
+extern "C" int gg_msm_stripe(gg_msm_base_t b, const void* scalars, size_t n_scalars, int scalars_on_device,
+                             int stripe_log, int stripe_part, void* out_jac, void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(b && out_jac, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(stripe_log >= 0 && stripe_log <= b->c - 2 && stripe_part >= 0 && stripe_part < (1 << stripe_log),
+             GG_ERR_INVALID_ARG, "bucket stripe out of range (stripe_log <= window_bits - 2, part < 2^stripe_log)");
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : hipStreamPerThread;
+    size_t need = msm_scalars_needed(b);
+    GG_CHECK(n_scalars >= need, GG_ERR_INVALID_ARG,
+             "scalar vector shorter than the points/index map require");
+    GG_CHECK(need == 0 || scalars, GG_ERR_INVALID_ARG, "null scalars");
+    std::lock_guard<std::mutex> lk(b->mu);
+    const Fr* sdev = (const Fr*)scalars;
+    if (!scalars_on_device && need) {
+        b->own.scr.scal.reserve(need * 32);
+        GG_HIP(hipMemcpyAsync(b->own.scr.scal.p, scalars, need * 32, hipMemcpyHostToDevice, st));
+        sdev = b->own.scr.scal.as<Fr>();
+    }
+    if (b->n == 0) {  // the identity, in the group's Jacobian layout
+        msm_device_work(b, &b->own, sdev, out_jac, st);
+        return GG_OK;
+    }
+    msm_prepare_dev(b, &b->own.sort, sdev, st, stripe_log, (uint32_t)stripe_part);
+    msm_finish_dev(b, &b->own.sort, out_jac, st, nullptr);
     GG_CAPI_END
 }

@@ -235,8 +235,9 @@ template <class SC>
 __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, const uint32_t* sidx,
                                                      size_t n, int c, int W, WinSpec ws, int G, int kbits,
                                                      int spb, int nbins, int h, uint32_t* keys,
-                                                     uint32_t* hist, uint32_t nblocks) {
+                                                     uint32_t* hist, uint32_t nblocks, int slog, uint32_t sres) {
     extern __shared__ uint32_t hh[];
+    const uint32_t smask = (1u << slog) - 1u;
     for (int j = threadIdx.x; j < nbins; j += blockDim.x) hh[j] = 0;
     __syncthreads();
     // spb <= 512: at most two scalars per thread, both loaded before any digit work
@@ -264,9 +265,11 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, cons
             int d = (int)extract_bits(k, ws.off[w], bw) + carry;
             if (d > (1 << (bw - 1))) { d -= (1 << bw); carry = 1; } else carry = 0;
             uint32_t key = 0xffffffffu;
-            if (d) {
-                // bucket |d| - 1 of group w mod G
-                const uint32_t bk = ((uint32_t)(w & (G - 1)) << (c - 1)) | (uint32_t)((d > 0 ? d : -d) - 1);
+            const uint32_t bb = (uint32_t)((d > 0 ? d : -d) - 1);  // bucket |d| - 1 of group w mod G
+            if (d && (bb & smask) == sres) {
+                // bucket stripe (slog > 0): only buckets bb = 2^slog j + sres, renumbered j;
+                // c is then the stripe's c - slog
+                const uint32_t bk = ((uint32_t)(w & (G - 1)) << (c - 1)) | (bb >> slog);
                 key = bk | (d < 0 ? 0x80000000u : 0u);
                 atomicAdd(&hh[bin_of(bk, c, kbits, h)], 1u);
             }
@@ -518,8 +521,10 @@ static void sort_plan(int c, int& h, std::vector<int>& rs) {
 }
 
 void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st) {
-    const size_t n = b->n, nb = b->nb;
-    const int c = b->c, W = b->W, G = b->G;
+    // a bucket stripe sorts a 2^-slog share of the buckets, renumbered densely:
+    // the bucket ids (and every sort key) are those of a c - slog window
+    const size_t n = b->n, nb = b->nb >> s->slog;
+    const int c = b->c - s->slog, W = b->W, G = b->G;
     const size_t total = (size_t)W * n;
     const int kbits = (c - 1) + __builtin_ctz((unsigned)G);  // sort key bits
     int h;
@@ -559,11 +564,11 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
         hipLaunchKernelGGL(k_digits_hist<FrBlsCfg>, dim3(nblocks), dim3(256), nbins * 4, st,
                            (const FrBls*)scalars_dev, b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n,
                            c, W, b->win, G, kbits, spb, nbins, h, s->keys.as<uint32_t>(),
-                           s->hist.as<uint32_t>(), nblocks);
+                           s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
     else
         hipLaunchKernelGGL(k_digits_hist<FrCfg>, dim3(nblocks), dim3(256), nbins * 4, st, scalars_dev,
                            b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, G, kbits, spb,
-                           nbins, h, s->keys.as<uint32_t>(), s->hist.as<uint32_t>(), nblocks);
+                           nbins, h, s->keys.as<uint32_t>(), s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
     GG_HIP(hipGetLastError());
     exclusive_scan(s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nh, st, s->scan_tmp);
     // segment starts ping-pong between bin_start and seg2; the last pass writes offsets
@@ -640,8 +645,13 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
 
 // Sort of one scalar vector over b's shape into s; records s->ready_ev (sort
 // done) and s->pin_ev (the fullest bucket's entry count on the host).
-void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st) {
-    const size_t n = b->n, nb = b->nb;
+void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st, int slog,
+                 uint32_t sres) {
+    GG_CHECK(slog >= 0 && slog <= b->c - 2 && sres < (1u << slog), GG_ERR_INVALID_ARG,
+             "bucket stripe out of range (stripe_log <= window_bits - 2, part < 2^stripe_log)");
+    s->slog = slog;
+    s->sres = sres;
+    const size_t n = b->n, nb = b->nb >> slog;
     s->ensure_events();
     s->counts.reserve(nb * 4);
     s->offsets.reserve((nb + 1) * 4);
@@ -656,6 +666,7 @@ void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStr
                        s->maxcnt.as<uint32_t>());
     GG_HIP(hipGetLastError());
     GG_HIP(hipMemcpyAsync(s->pin, s->maxcnt.p, 4, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipMemcpyAsync(s->pin + 1, s->offsets.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
     GG_HIP(hipEventRecord(s->pin_ev, st));
     GG_HIP(hipEventRecord(s->ready_ev, st));
 }

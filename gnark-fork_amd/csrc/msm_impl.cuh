@@ -93,7 +93,10 @@ inline WinSpec make_windows(int c, int W, int total) {
 }
 struct MsmSort;
 void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
-void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
+// slog > 0: the sort keeps the bucket stripe sres of 2^slog (buckets b with
+// b mod 2^slog = sres, see MsmSort)
+void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st, int slog = 0,
+                 uint32_t sres = 0);
 
 constexpr uint32_t LIGHT = 16;
 // Bucket ids: B = j 2^(c-1) + b for precompute group j (< G) and bucket b of the
@@ -728,7 +731,15 @@ struct MsmSort {
     DevBuf keys, tmp_entry, tmp_key, hist, hoff, bin_start, seg2, chunk_start, chunk_hist, chunk_pos,
         chunk_desc;
     std::vector<DevBuf> scan_tmp;
-    uint32_t* pin = nullptr;          // pinned read-back: [0] = entries of the fullest bucket
+    // Bucket stripe (multi-GPU split of one MSM by buckets): with
+    // slog > 0 only the buckets b = 2^slog j + sres of every group are sorted,
+    // renumbered j -- a c - slog bucket space -- and msm_finish returns
+    // sum_b (b + 1) S_b over the stripe, so the 2^slog stripes' results add up
+    // to the whole MSM.  Every stripe reads all scalars, but sorts, accumulates
+    // and reduces only its 2^-slog share of the entries and buckets.
+    int slog = 0;
+    uint32_t sres = 0;
+    uint32_t* pin = nullptr;          // pinned read-back: [0] = entries of the fullest bucket, [1] = entries
     hipEvent_t pin_ev = nullptr;      // after the read-back copy
     hipEvent_t ready_ev = nullptr;    // after the sort
     void ensure_events() {
@@ -824,6 +835,7 @@ struct RedItem {
     uint32_t n, off;
     int mlog;
     bool plain;
+    int mult = 1;  // small signed factor of the whole term (bucket stripes), applied on the host
 };
 
 // Sum of reduction terms with log-depth, wide tree sums (DESIGN.md "MSM /
@@ -867,11 +879,11 @@ inline Xyzz<F> reduce_terms(std::vector<RedItem<F>> items, MsmScratch* scr, hipS
             int mlg = lg / 2;
             uint32_t M = 1u << mlg, rows = it.n >> mlg;
             if (it.plain) {  // row sums only
-                jobs.push_back({it.X, M, rows, 1u, M, Item{nullptr, rows, 0u, it.mlog, true}});
+                jobs.push_back({it.X, M, rows, 1u, M, Item{nullptr, rows, 0u, it.mlog, true, it.mult}});
                 continue;
             }
-            jobs.push_back({it.X, M, rows, 1u, M, Item{nullptr, rows, 0u, it.mlog + mlg, false}});
-            jobs.push_back({it.X, rows, M, M, 1u, Item{nullptr, M, it.off, it.mlog, false}});
+            jobs.push_back({it.X, M, rows, 1u, M, Item{nullptr, rows, 0u, it.mlog + mlg, false, it.mult}});
+            jobs.push_back({it.X, rows, M, M, 1u, Item{nullptr, M, it.off, it.mlog, false, it.mult}});
         }
         // one launch per round: every output of every job is a block-wide sum
         static const bool block_mode = !(getenv("GG_RED_BLOCK") && atoi(getenv("GG_RED_BLOCK")) == 0);
@@ -960,12 +972,23 @@ inline Xyzz<F> reduce_terms(std::vector<RedItem<F>> items, MsmScratch* scr, hipS
     for (size_t k = 0; k < host_items.size(); k++)
         hx[k].assign(flat.begin() + GL.off[k], flat.begin() + GL.off[k + 1]);
     std::vector<std::pair<int, Xyzz<F>>> vals;
+    auto scaled = [](const Xyzz<F>& v, int m) {  // m v by double-and-add (|m| small)
+        if (m == 1 || v.is_inf()) return v;
+        const uint32_t u = (uint32_t)(m < 0 ? -m : m);
+        Xyzz<F> r = Xyzz<F>::inf();
+        for (int bit = 31; bit >= 0; bit--) {
+            if (!r.is_inf()) r = xyzz_dbl(r);
+            if ((u >> bit) & 1u) r = xyzz_add(r, v);
+        }
+        if (m < 0 && !r.is_inf()) r.y = -r.y;
+        return r;
+    };
     for (size_t k = 0; k < host_items.size(); k++) {
         const auto& X = hx[k];
         Xyzz<F> run = Xyzz<F>::inf(), acc = Xyzz<F>::inf();
         if (host_items[k].plain) {
             for (const auto& x : X) acc = xyzz_add(acc, x);
-            vals.push_back({host_items[k].mlog, acc});
+            vals.push_back({host_items[k].mlog, scaled(acc, host_items[k].mult)});
             continue;
         }
         for (size_t j = X.size(); j-- > 1;) {
@@ -976,7 +999,7 @@ inline Xyzz<F> reduce_terms(std::vector<RedItem<F>> items, MsmScratch* scr, hipS
             run = xyzz_add(run, X[0]);  // run = sum of all
             for (uint32_t o = 0; o < host_items[k].off; o++) acc = xyzz_add(acc, run);
         }
-        vals.push_back({host_items[k].mlog, acc});
+        vals.push_back({host_items[k].mlog, scaled(acc, host_items[k].mult)});
     }
     std::sort(vals.begin(), vals.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
     Xyzz<F> acc = Xyzz<F>::inf();
@@ -1029,12 +1052,23 @@ inline uint32_t range_length(size_t E) {
 // s->ready_ev.
 template <class F>
 inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream_t st) {
-    const size_t n = b->n, nb = b->nb;
+    // a bucket stripe (s->slog > 0) works in its c - slog bucket space: nb and ce
+    // below; the group scales 2^(j c) keep the base's c
+    const int slog = s->slog;
+    const size_t n = b->n, nb = b->nb >> slog;
+    const int ce = b->c - slog;
     if (n == 0) return Xyzz<F>::inf();
     GG_HIP(hipStreamWaitEvent(st, s->ready_ev, 0));
     const uint32_t* offs = s->offsets.as<uint32_t>();
-    const uint32_t K = range_length<F>((size_t)b->W * n);
-    const size_t T = ((size_t)b->W * n + K - 1) / K;  // ranges (upper bound: digit-0 entries are not sorted)
+    size_t E = (size_t)b->W * n;  // entries (upper bound: digit-0 entries are not sorted)
+    if (slog) {
+        // a stripe holds ~2^-slog of the entries: wait for the sort's count so
+        // the ranges fill the chip for the entries there are
+        GG_HIP(hipEventSynchronize(s->pin_ev));
+        E = std::max<size_t>(s->pin[1], 1);
+    }
+    const uint32_t K = range_length<F>(E);
+    const size_t T = (E + K - 1) / K;  // ranges
     using PT = typename PartialOf<F>::T;
     constexpr bool kRadixP = !std::is_same<PT, Xyzz<F>>::value;  // partials in the accumulator's form
     scr->head.reserve((T + 1) * sizeof(Xyzz<F>));
@@ -1057,7 +1091,7 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
         const char* acc_name = sizeof(F) == sizeof(Fp) ? "msm_accum" : (sizeof(F) == sizeof(Fp2) ? "msm_accum_g2" : "msm_accum_bls");
         ProfScope ps_acc(acc_name, st, (double)n);
         hipLaunchKernelGGL(k_accum_range<F>, dim3(grid_for(T, 256)), dim3(256), 0, st, (const Affine<F>*)b->pts.p,
-                           s->sorted.as<uint32_t>(), offs, (uint32_t)nb, b->c, K, (int)b->has_inf, hP, tP, SP,
+                           s->sorted.as<uint32_t>(), offs, (uint32_t)nb, ce, K, (int)b->has_inf, hP, tP, SP,
                            scr->tbucket.as<uint32_t>());
         GG_HIP(hipGetLastError());
         ps_acc.stop(st);
@@ -1090,7 +1124,7 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
             Xyzz<F>* Rs = D + (size_t)G * Tg;
             PT* Sr = reinterpret_cast<PT*>(Rs + (size_t)G * Tg);
             hipLaunchKernelGGL(k_bucket_sum_r<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, (const PT*)hP,
-                               (const PT*)tP, (const PT*)SP, offs, (uint32_t)nb, b->c, K, logL, Sr);
+                               (const PT*)tP, (const PT*)SP, offs, (uint32_t)nb, ce, K, logL, Sr);
             GG_HIP(hipGetLastError());
             hipLaunchKernelGGL(k_bucket_runsum<F>, dim3(grid_for((size_t)G * Tg, 256)), dim3(256), 0, st,
                                (const PT*)Sr, (uint32_t)(G * Tg), logL, D, Rs);
@@ -1099,10 +1133,15 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
             ProfScope ps_red("msm_reduce", st, (double)nb);
             // sum_j 2^(j c) (sum_s D_s + L sum_s (s + 1) R_s) over the groups j:
             // every group's two lists reduced in the same launches, one read-back
+            // A stripe's buckets are b = 2^slog j + sres (j its dense id), so
+            // sum_b (b + 1) S_b = 2^slog sum_j (j + 1) T_j - (2^slog - 1 - sres) sum_j T_j,
+            // and sum_j T_j = sum_s R_s.
+            const int sneg = slog ? -(int)((1u << slog) - 1u - s->sres) : 0;
             std::vector<RedItem<F>> terms;
             for (int jg = 0; jg < b->G; jg++) {
-                terms.push_back({(const Xyzz<F>*)Rs + (size_t)jg * Tg, Tg, 1u, jg * b->c + logL, false});
-                terms.push_back({(const Xyzz<F>*)D + (size_t)jg * Tg, Tg, 0u, jg * b->c, true});
+                terms.push_back({(const Xyzz<F>*)Rs + (size_t)jg * Tg, Tg, 1u, jg * b->c + logL + slog, false});
+                terms.push_back({(const Xyzz<F>*)D + (size_t)jg * Tg, Tg, 0u, jg * b->c + slog, true});
+                if (sneg) terms.push_back({(const Xyzz<F>*)Rs + (size_t)jg * Tg, Tg, 0u, jg * b->c, true, sneg});
             }
             Xyzz<F> res = reduce_terms<F>(std::move(terms), scr, st);
             ps_red.stop(st);
@@ -1125,14 +1164,19 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
         stride *= fan;
     }
     hipLaunchKernelGGL(k_bucket_combine<F>, dim3(grid_for(4 * nb, 256)), dim3(256), 0, st, (const Xyzz<F>*)head,
-                       (const Xyzz<F>*)scr->tail.p, offs, (uint32_t)nb, b->c, K, S);
+                       (const Xyzz<F>*)scr->tail.p, offs, (uint32_t)nb, ce, K, S);
     GG_HIP(hipGetLastError());
     ps_acc2.stop(st);
     // ---- bucket reduction: sum_b (b+1) S_b
     ProfScope ps_red("msm_reduce", st, (double)nb);
     // one weighted sum per precompute group, sum_j 2^(j c) R_j, in one batched reduction
+    const int sneg = slog ? -(int)((1u << slog) - 1u - s->sres) : 0;  // bucket stripe, as above
     std::vector<RedItem<F>> terms;
-    for (int j = 0; j < b->G; j++) terms.push_back({(const Xyzz<F>*)S + (size_t)j * nbg, (uint32_t)nbg, 1u, j * b->c, false});
+    for (int j = 0; j < b->G; j++) {
+        const Xyzz<F>* Sj = (const Xyzz<F>*)S + (size_t)j * nbg;
+        terms.push_back({Sj, (uint32_t)nbg, 1u, j * b->c + slog, false});
+        if (sneg) terms.push_back({Sj, (uint32_t)nbg, 0u, j * b->c, true, sneg});
+    }
     Xyzz<F> res = reduce_terms<F>(std::move(terms), scr, st);
     ps_red.stop(st);
     return res;

@@ -72,6 +72,11 @@ def _load():
         "gg_set_hbm_budget": ([S], I),
         "gg_get_hbm_budget": ([], S),
         "gg_msm": ([P, P, S, I, P, P], I),
+        "gg_msm_stripe": ([P, P, S, I, I, I, P, P], I),
+        "gg_groth16_pk_create_stripe_ex": ([I, I, P, P, P, S, P, S, P, S, S, P, S, P, P, P, P, P, P, P, P, S,
+                                            S, P, I, I, PP], I),
+        "gg_groth16_pk_stripe": ([P, ctypes.POINTER(I), ctypes.POINTER(I)], I),
+        "gg_groth16_mpk_split": ([P, ctypes.POINTER(I)], I),
         "gg_g1_jac_to_affine": ([P, P], I),
         "gg_g2_jac_to_affine": ([P, P], I),
         "gg_g1_jac_add": ([P, P, P], I),
@@ -201,6 +206,7 @@ EXPORTED = [
     "gg_groth16_mpk_devices", "gg_groth16_mpk_base_info", "gg_groth16_pk_create_shard_ex", "gg_r1cs_create", "gg_r1cs_create_ex", "gg_r1cs_release", "gg_r1cs_info", "gg_r1cs_solve",
     "gg_r1cs_solution_dev", "gg_scs_create", "gg_scs_release", "gg_scs_info", "gg_scs_solve",
     "gg_scs_solution_dev", "gg_r1cs_set_inputs", "gg_scs_set_inputs", "gg_r1cs_schedule", "gg_scs_schedule",
+    "gg_msm_stripe", "gg_groth16_pk_create_stripe_ex", "gg_groth16_pk_stripe", "gg_groth16_mpk_split",
 ]
 
 

@@ -205,6 +205,12 @@ class MultiGpuProvingKey:
         check(lib.gg_groth16_mpk_info(self.handle, ctypes.byref(w), ctypes.byref(d)))
         return w.value, bool(d.value)
 
+    def split(self) -> str:
+        """'stripes' (bucket stripes over whole per-device wire tables) or 'wires'."""
+        v = ctypes.c_int()
+        check(lib.gg_groth16_mpk_split(self.handle, ctypes.byref(v)))
+        return "stripes" if v.value else "wires"
+
     def base_info(self, which: int, shard: int = 0):
         """(resident points, window bits, windows) of MSM base `which` of a shard"""
         n, c, w = ctypes.c_size_t(), ctypes.c_int(), ctypes.c_int()
@@ -423,6 +429,51 @@ class ProvingKeyShard:
         self.handle = h
         self.n_wires = data.n_wires
         self.log_n = data.log_n
+
+    base_info = ProvingKey.base_info
+    close = ProvingKey.close
+    __del__ = ProvingKey.__del__
+
+
+class ProvingKeyStripe:
+    """Bucket-stripe shard `rank` of `world` (a power of two) of a proving key
+    (gg_groth16_pk_create_stripe_ex): the WHOLE A, B, K and G2 B tables, whose
+    A, B1, K and G2 MSMs this shard computes over the buckets b = rank mod world,
+    and the Z slice of shard_ranges (the h block the distributed computeH leaves
+    on this rank).  Proves with prove_partial / prove_distributed_h like a
+    ProvingKeyShard; the partials of all ranks add up to the proof's.
+    g1_Z / z_lo: this rank's Z slice when `data` does not hold the whole Z."""
+
+    def __init__(self, data: ProvingKeyData, rank: int = 0, world: int = 1, g1_Z: bytes = None,
+                 z_lo: int = None):
+        assert world >= 1 and world & (world - 1) == 0, "world must be a power of two"
+        n = 1 << data.log_n
+        _, _, zl, zh = shard_ranges(data.n_wires, n, rank, world)
+        if g1_Z is None:
+            g1_Z, z_lo = data.g1_Z[64 * zl:64 * zh], zl
+        assert z_lo == zl and len(g1_Z) == 64 * (zh - zl), "Z slice differs from shard_ranges"
+        self.data, self.rank, self.world = data, rank, world
+        omega = data.domain_generator or fr.fr_mont(fr.domain_generator(data.log_n))
+        gen = data.domain_mul_gen or fr.fr_mont(fr.FR_MULTIPLICATIVE_GEN)
+        kidx = None if data.k_wire_index is None else np.ascontiguousarray(data.k_wire_index, dtype=np.uint32)
+        h = ctypes.c_void_p()
+        check(lib.gg_groth16_pk_create_stripe_ex(
+            GG_CURVE_BN254, data.log_n, ptr(omega), ptr(gen),
+            ptr(data.g1_A), len(data.g1_A) // 64, ptr(data.g1_B), len(data.g1_B) // 64,
+            ptr(g1_Z), z_lo, len(g1_Z) // 64, ptr(data.g1_K), len(data.g1_K) // 64,
+            ptr(data.alpha1), ptr(data.beta1), ptr(data.delta1),
+            ptr(data.g2_B), ptr(data.beta2), ptr(data.delta2),
+            ptr(bytes(data.infinity_A)), ptr(bytes(data.infinity_B)), data.n_wires,
+            data.nb_public, ptr(kidx), world.bit_length() - 1, rank, ctypes.byref(h)))
+        self.handle = h
+        self.n_wires = data.n_wires
+        self.log_n = data.log_n
+
+    def stripe(self):
+        """(stripe_log, stripe_part) of the key."""
+        a, b = ctypes.c_int(), ctypes.c_int()
+        check(lib.gg_groth16_pk_stripe(self.handle, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     base_info = ProvingKey.base_info
     close = ProvingKey.close

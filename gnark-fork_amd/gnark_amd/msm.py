@@ -49,6 +49,15 @@ class MsmBase:
         check(lib.gg_msm(self.handle, ptr(scalars), n_scalars, int(on_device), ptr(out), ptr(stream)))
         return bytes(out)
 
+    def msm_stripe_jac(self, scalars, n_scalars: int, stripe_log: int, part: int, on_device=False,
+                       stream=None) -> bytes:
+        """Bucket stripe `part` of 2^stripe_log of the MSM (gg_msm_stripe): the
+        stripes' Jacobian results add up to msm_jac's."""
+        out = bytearray(_JAC[self.group])
+        check(lib.gg_msm_stripe(self.handle, ptr(scalars), n_scalars, int(on_device), stripe_log, part,
+                                ptr(out), ptr(stream)))
+        return bytes(out)
+
     def msm(self, scalars, n_scalars: int, on_device=False, stream=None) -> bytes:
         """Affine result (Montgomery, gnark layout; infinity = zeros)."""
         return jac_to_affine(self.group, self.msm_jac(scalars, n_scalars, on_device, stream))

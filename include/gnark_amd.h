@@ -161,6 +161,17 @@ size_t gg_get_hbm_budget(void);
  * hip_stream may be NULL. */
 int gg_msm(gg_msm_base_t b, const void *scalars, size_t n_scalars, int scalars_on_device,
            void *out_jac, void *hip_stream);
+/* One bucket stripe of gg_msm: with N = 2^stripe_log, the part of the MSM whose
+ * signed-digit buckets b (|digit| - 1, every window) satisfy b mod N ==
+ * stripe_part, i.e. sum over those buckets of (b + 1) S_b.  The N stripes'
+ * results add up to gg_msm's.  This is how one MSM splits over N GPUs that each
+ * hold the whole base (MI355X: 288 GB of HBM per GPU): every GPU reads all
+ * scalars but sorts, accumulates and reduces only 1/N of the entries and
+ * buckets -- unlike a split by points, whose every part pays the whole bucket
+ * reduction.  Replaces the point-sharded MultiExp of a multi-GPU prover
+ * (prove.go:201-290 on one node's GPUs).  stripe_log <= window_bits - 2. */
+int gg_msm_stripe(gg_msm_base_t b, const void *scalars, size_t n_scalars, int scalars_on_device,
+                  int stripe_log, int stripe_part, void *out_jac, void *hip_stream);
 
 /* host-side point helpers (epilogue of prove.go:206-299) */
 int gg_g1_jac_to_affine(const void *jac, void *aff);
@@ -265,6 +276,24 @@ int gg_groth16_pk_create_shard_ex(int curve, int log_n, const void *omega_mont, 
                                   const void *delta2, const uint8_t *inf_A, const uint8_t *inf_B,
                                   size_t n_wires, size_t nb_public, const uint32_t *k_wire_index,
                                   size_t wire_lo, size_t wire_hi, gg_groth16_pk_t *out);
+/* Bucket-stripe shard of a multi-GPU key: the WHOLE A, B, K and
+ * G2 B tables (arguments as gg_groth16_pk_create_ex) and Z positions
+ * [z_lo, z_lo + nZ); its A, B1, K and G2 MSMs take the bucket stripe
+ * stripe_part of 2^stripe_log (gg_msm_stripe).  Shard r of N = 2^stripe_log
+ * takes stripe r and the Z slice the distributed computeH leaves on rank r;
+ * gg_groth16_prove_partial(_dist) over the whole solution, partials added as
+ * for wire shards.  The per-GPU MSM work is 1/N of the whole key's with no
+ * per-shard bucket reduction of the full bucket space. */
+int gg_groth16_pk_create_stripe_ex(int curve, int log_n, const void *omega_mont, const void *coset_gen_mont,
+                                   const void *g1_A, size_t nA, const void *g1_B, size_t nB,
+                                   const void *g1_Z, size_t z_lo, size_t nZ, const void *g1_K,
+                                   size_t nK, const void *alpha1, const void *beta1,
+                                   const void *delta1, const void *g2_B, const void *beta2,
+                                   const void *delta2, const uint8_t *inf_A, const uint8_t *inf_B,
+                                   size_t n_wires, size_t nb_public, const uint32_t *k_wire_index,
+                                   int stripe_log, int stripe_part, gg_groth16_pk_t *out);
+/* stripe of a key: 0 / 0 for a whole key or a wire shard */
+int gg_groth16_pk_stripe(gg_groth16_pk_t pk, int *stripe_log, int *stripe_part);
 /* Device section of Prove on one key (shard): computeH and the five MSMs of
  * prove.go:198-301 without the combination.  Inputs as gg_groth16_prove (the
  * whole solution).  partials (host, 576 B): G1Jac sum w.A | sum w.B1 |
@@ -370,6 +399,10 @@ int gg_groth16_mpk_base_info(gg_groth16_mpk_t mpk, int shard, int which, size_t 
 int gg_groth16_mpk_devices(gg_groth16_mpk_t mpk, int *devices, int cap);
 /* world and whether computeH is distributed (1) or replicated per shard (0) */
 int gg_groth16_mpk_info(gg_groth16_mpk_t mpk, int *world, int *distributed_h);
+/* 1: the shards split the A, B1, K, G2 MSMs by bucket stripes (each device
+ * holds the whole wire tables; the default for a power-of-two world,
+ * GG_MPK_SPLIT=wires selects wire slices); 0: by wire slices */
+int gg_groth16_mpk_split(gg_groth16_mpk_t mpk, int *bucket_stripes);
 /* as gg_groth16_prove (host inputs): Ar, Bs, Krs affine */
 int gg_groth16_mpk_prove(gg_groth16_mpk_t mpk, const void *wires, size_t n_wires, const void *sol_a,
                          const void *sol_b, const void *sol_c, size_t n_cons, const void *r_mont,

@@ -102,10 +102,14 @@ class LocalExchange:
         return fn
 
 
-def _prove_threads(data, sol, world):
+def _prove_threads(data, sol, world, stripes=False):
     from gnark_amd import groth16
     log_n = data.log_n
-    shards = [groth16.ProvingKeyShard(data, r, world) for r in range(world)]
+    if stripes:  # bucket stripes: the whole wire tables per rank, stripe r of the buckets
+        shards = [groth16.ProvingKeyStripe(data, r, world) for r in range(world)]
+        assert [sh.stripe() for sh in shards] == [(world.bit_length() - 1, r) for r in range(world)]
+    else:
+        shards = [groth16.ProvingKeyShard(data, r, world) for r in range(world)]
     hs = [groth16.HShard(log_n, r, world) for r in range(world)]
     ex = LocalExchange(world, hs[0].exchange_bytes)
     parts, errs = [None] * world, []
@@ -139,8 +143,10 @@ def test_prove_dist_h_golden(idx, world):
     assert (pr.Ar.hex(), pr.Bs.hex(), pr.Krs.hex()) == (g["Ar"], g["Bs"], g["Krs"])
 
 
-@pytest.mark.parametrize("log_n,n_wires,world,on_device", [(12, 3000, 4, False), (15, 30000, 8, True)])
-def test_prove_dist_h_vs_oracle(log_n, n_wires, world, on_device):
+@pytest.mark.parametrize("stripes", [False, True])
+@pytest.mark.parametrize("log_n,n_wires,world,on_device", [(12, 3000, 4, False), (15, 30000, 8, True),
+                                                           (13, 6000, 2, True)])
+def test_prove_dist_h_vs_oracle(log_n, n_wires, world, on_device, stripes):
     from gnark_amd import groth16, DeviceBuffer
     from test_gpu_groth16 import synthetic_case
     d, wires, sa, sb, sc, ncons, r, s = synthetic_case(log_n, n_wires, 3, 10 + log_n, k_inf_every=5)
@@ -155,5 +161,5 @@ def test_prove_dist_h_vs_oracle(log_n, n_wires, world, on_device):
                                ncons, on_device=True)
     else:
         sol = groth16.Solution(wires, sa, sb, sc, n_wires, ncons)
-    pr = groth16.finalize(data, _prove_threads(data, sol, world), r, s)
+    pr = groth16.finalize(data, _prove_threads(data, sol, world, stripes), r, s)
     assert (pr.Ar, pr.Bs, pr.Krs) == exp[:3]

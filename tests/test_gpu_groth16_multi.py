@@ -40,10 +40,15 @@ def test_mpk_golden(idx, world):
     mpk.close()
 
 
+@pytest.mark.parametrize("split", ["stripes", "wires"])
 @pytest.mark.parametrize("log_n,n_wires,world,kidx", [(12, 3000, 4, False), (13, 7000, 8, True),
                                                       (12, 2500, 3, False), (14, 16000, 16, False)])
-def test_mpk_vs_oracle(log_n, n_wires, world, kidx):
+def test_mpk_vs_oracle(log_n, n_wires, world, kidx, split, monkeypatch):
+    """split: bucket stripes (the default for a power-of-two world: whole wire
+    tables per device, shard r takes the buckets b = r mod world) or wire slices
+    (GG_MPK_SPLIT=wires); a world of 3 always slices wires."""
     from gnark_amd import backend, groth16
+    monkeypatch.setenv("GG_MPK_SPLIT", split)
     from test_gpu_groth16 import synthetic_case
     d, wires, sa, sb, sc, ncons, r, s = synthetic_case(log_n, n_wires, 3, 40 + log_n + world, k_inf_every=5)
     if kidx:
@@ -65,6 +70,7 @@ def test_mpk_vs_oracle(log_n, n_wires, world, kidx):
             ncons, r, s)
         assert (ref.Ar, ref.Bs, ref.Krs) == exp[:3]
     mpk = groth16.MultiGpuProvingKey(data, [0] * world)
+    assert mpk.split() == (split if world & (world - 1) == 0 else "wires")
     pr = mpk.prove(sol, backend.with_amd_acceleration(), r=r, s=s)
     assert pr == ref
     # the solution resident in HBM (one copy per device, gg_groth16_mpk_prove_ex)

@@ -109,14 +109,24 @@ def test_groth16_mimc_bit_exact(log_n):
     cr.close()
 
 
-def _mpk_check(data, sol, sol_d, want, world, t0):
+def _mpk_check(data, sol, sol_d, want, world, t0, split="stripes"):
     """gg_groth16_mpk_* with `world` key shards (8 = BASELINE configs[3]'s node):
-    wire / Z shards, the four-step distributed computeH with its three
-    all-to-alls as peer copies, partials summed exactly -- same proof bytes."""
+    bucket stripes over whole per-device wire tables (or wire slices) and Z
+    slices, the four-step distributed computeH with its three all-to-alls as
+    peer copies, partials summed exactly -- same proof bytes."""
+    import os
     from gnark_amd import backend, groth16
     opt = backend.with_amd_acceleration()
-    mpk = groth16.MultiGpuProvingKey(data, [0] * world)
-    assert mpk.info() == (world, True)
+    old = os.environ.get("GG_MPK_SPLIT")
+    os.environ["GG_MPK_SPLIT"] = split
+    try:
+        mpk = groth16.MultiGpuProvingKey(data, [0] * world)
+    finally:
+        if old is None:
+            del os.environ["GG_MPK_SPLIT"]
+        else:
+            os.environ["GG_MPK_SPLIT"] = old
+    assert mpk.info() == (world, True) and mpk.split() == split
     _log(f"{world}-shard key", t0)
     pr = mpk.prove(sol, opt, r=_fr(R_), s=_fr(S_))
     _log(f"{world}-shard prove (host inputs) {mpk.last_timings()['total']:.1f} ms", t0)
@@ -127,8 +137,9 @@ def _mpk_check(data, sol, sol_d, want, world, t0):
     mpk.close()
 
 
+@pytest.mark.parametrize("split", ["stripes", "wires"])
 @pytest.mark.parametrize("log_n,world", [(16, 8), (18, 4)])
-def test_groth16_mimc_multi_gpu_shards(log_n, world):
+def test_groth16_mimc_multi_gpu_shards(log_n, world, split):
     """the same check at sizes the suite runs quickly"""
     from gnark_amd import groth16, DeviceBuffer
     t0 = time.time()
@@ -136,5 +147,5 @@ def test_groth16_mimc_multi_gpu_shards(log_n, world):
     sol = groth16.Solution(bytes(wires), bytes(A), bytes(B), bytes(C), cr.nw, cr.ncons)
     dev = [DeviceBuffer.from_host(bytes(x)) for x in (wires, A, B, C)]
     sol_d = groth16.Solution(*dev, cr.nw, cr.ncons, on_device=True)
-    _mpk_check(data, sol, sol_d, want, world, t0)
+    _mpk_check(data, sol, sol_d, want, world, t0, split)
     cr.close()
