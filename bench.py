@@ -443,7 +443,7 @@ class Groth16Bench:
             else:
                 self.pk = groth16.ProvingKey(self.data)
                 self.nB2 = nB
-        elif world & (world - 1) == 0 and os.environ.get("GG_MPK_SPLIT", "stripes") != "wires":
+        elif world & (world - 1) == 0 and os.environ.get("GG_MPK_SPLIT", "wires") == "stripes":
             # bucket stripes: every rank holds the whole A, B, K, G2 tables (the
             # same points on every rank: fixed seeds) and its Z slice; its A, B1,
             # K, G2 MSMs take the buckets b = rank mod world

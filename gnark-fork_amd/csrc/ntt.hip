@@ -738,6 +738,7 @@ struct gg_hshard {
     DevBuf w_hi, w_lo, wi_hi, wi_lo, g_hi, g_lo, gi_hi, gi_lo;  // split power tables over [0, n)
     int S = 0;
     Fr wN[16], wNi[16];
+    Fr gm[16], gmi[16];  // g^(m i), g^(-m i): the coset factors of the size-N steps
     DevBuf y, full;  // 3 x m local vectors; staging of host inputs
     DevBuf hblk;     // m elements: h_bitrev[rank m, (rank+1) m)
     hipStream_t st = nullptr;
@@ -756,10 +757,43 @@ struct PowTab {
     }
 };
 
+// the size-N steps' constants: powers of the primitive N-th root and its
+// inverse, and the per-output scale cs[i] (folding 1/N and g^(+-m i))
 template <int N>
 struct SmallRoots {
-    Fr fwd[N], inv[N];
+    Fr fwd[N], inv[N], cs[N];
 };
+
+// X[j] = sum_k x[k] r^(j k) in place, r[i] = r^i: radix-2 DIT in registers
+// (N/2 log N butterflies, the r^0 ones without a product -- 5 products for
+// N = 8 where the direct sum takes 49)
+template <int N>
+__device__ __forceinline__ void dft_small(Fr (&x)[N], const Fr (&r)[N]) {
+    constexpr int LG = N <= 1 ? 0 : (N == 2 ? 1 : (N == 4 ? 2 : (N == 8 ? 3 : 4)));
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        int j = 0;
+#pragma unroll
+        for (int b = 0; b < LG; b++) j |= ((i >> b) & 1) << (LG - 1 - b);
+        if (i < j) {
+            Fr t = x[i];
+            x[i] = x[j];
+            x[j] = t;
+        }
+    }
+#pragma unroll
+    for (int len = 2; len <= N; len <<= 1)
+#pragma unroll
+        for (int i = 0; i < N; i += len)
+#pragma unroll
+            for (int j = 0; j < len / 2; j++) {
+                const Fr u = x[i + j];
+                Fr v = x[i + j + len / 2];
+                if (j) v = v * r[(N / len) * j];
+                x[i + j] = u + v;
+                x[i + j + len / 2] = u - v;
+            }
+}
 
 // y[j] = x[rank + N j] (zero past len)
 __global__ void k_gather_cyclic(Fr* y, const Fr* x, size_t len, size_t m, int rank, int N) {
@@ -793,23 +827,23 @@ __global__ void __launch_bounds__(256) k_cross_fwd(Fr* send, const Fr* recv, siz
     const int poly = (int)(t / chunk);
     const size_t q = t - (size_t)poly * chunk;
     const uint32_t c1 = brev_bits((uint32_t)(rank * chunk + q), M);
-    Fr in[N], co[N];
+    (void)invN;
+    (void)m;
+    // co[c2] = iDFT_N(in)[c2] / N * g^(c1 + m c2) = g^c1 * (iDFT_N(in)[c2] * cs[c2]);
+    // out[k2] = DFT_N(co)[k2] * w^(c1 k2) = g^c1 w^(c1 k2) * DFT_N(iDFT_N(in) * cs)[k2]
+    Fr x[N];
 #pragma unroll
-    for (int k = 0; k < N; k++) in[k] = load_fr(recv + ((size_t)k * npoly + poly) * chunk + q);
+    for (int k = 0; k < N; k++) x[k] = load_fr(recv + ((size_t)k * npoly + poly) * chunk + q);
+    dft_small<N>(x, R.inv);
 #pragma unroll
-    for (int c2 = 0; c2 < N; c2++) {
-        Fr acc = in[0];
-#pragma unroll
-        for (int k = 1; k < N; k++) acc = acc + in[k] * R.inv[(k * c2) % N];
-        co[c2] = acc * invN * gpow.at(c1 + (uint32_t)(m * c2));
-    }
+    for (int c2 = 0; c2 < N; c2++) x[c2] = x[c2] * R.cs[c2];
+    dft_small<N>(x, R.fwd);
+    const Fr wc = wpow.at(c1);
+    Fr f = gpow.at(c1);
 #pragma unroll
     for (int k2 = 0; k2 < N; k2++) {
-        Fr acc = co[0];
-#pragma unroll
-        for (int c2 = 1; c2 < N; c2++) acc = acc + co[c2] * R.fwd[(c2 * k2) % N];
-        if (k2) acc = acc * wpow.at(c1 * (uint32_t)k2);
-        store_fr(send + ((size_t)k2 * npoly + poly) * chunk + q, acc);
+        if (k2) f = f * wc;
+        store_fr(send + ((size_t)k2 * npoly + poly) * chunk + q, x[k2] * f);
     }
 }
 
@@ -829,17 +863,17 @@ __global__ void __launch_bounds__(256) k_cross_inv_out(Fr* h, const Fr* recv, si
     size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= chunk) return;
     const uint32_t c1 = brev_bits((uint32_t)(rank * chunk + q), M);
-    Fr in[N];
+    (void)scale;
+    (void)m;
+    // iDFT_N(in)[c2] * scale * g^-(c1 + m c2) = g^-c1 * (iDFT_N(in)[c2] * cs[c2])
+    Fr x[N];
 #pragma unroll
-    for (int k = 0; k < N; k++) in[k] = load_fr(recv + (size_t)k * chunk + q);
+    for (int k = 0; k < N; k++) x[k] = load_fr(recv + (size_t)k * chunk + q);
+    dft_small<N>(x, R.inv);
+    const Fr gi = gipow.at(c1);
 #pragma unroll
-    for (int c2 = 0; c2 < N; c2++) {
-        Fr acc = in[0];
-#pragma unroll
-        for (int k = 1; k < N; k++) acc = acc + in[k] * R.inv[(k * c2) % N];
-        acc = acc * scale * gipow.at(c1 + (uint32_t)(m * c2));
-        store_fr(h + (size_t)N * q + brev_bits((uint32_t)c2, logN), acc);
-    }
+    for (int c2 = 0; c2 < N; c2++)
+        store_fr(h + (size_t)N * q + brev_bits((uint32_t)c2, logN), x[c2] * R.cs[c2] * gi);
 }
 
 static void pow_tab_upload(int L, int S, const Fr& x, DevBuf& hi, DevBuf& lo) {
@@ -852,7 +886,11 @@ static void pow_tab_upload(int L, int S, const Fr& x, DevBuf& hi, DevBuf& lo) {
 template <int N>
 static void launch_cross_fwd(gg_hshard* hs, Fr* send, const Fr* recv, int npoly, hipStream_t st) {
     SmallRoots<N> R;
-    for (int i = 0; i < N; i++) { R.fwd[i] = hs->wN[i]; R.inv[i] = hs->wNi[i]; }
+    for (int i = 0; i < N; i++) {
+        R.fwd[i] = hs->wN[i];
+        R.inv[i] = hs->wNi[i];
+        R.cs[i] = hs->invN * hs->gm[i];
+    }
     PowTab gp{hs->g_hi.as<Fr>(), hs->g_lo.as<Fr>(), hs->S};
     PowTab wp{hs->w_hi.as<Fr>(), hs->w_lo.as<Fr>(), hs->S};
     hipLaunchKernelGGL(k_cross_fwd<N>, dim3(grid_for(hs->chunk * npoly, 256)), dim3(256), 0, st, send,
@@ -863,7 +901,11 @@ static void launch_cross_fwd(gg_hshard* hs, Fr* send, const Fr* recv, int npoly,
 template <int N>
 static void launch_cross_inv(gg_hshard* hs, Fr* h, const Fr* recv, hipStream_t st) {
     SmallRoots<N> R;
-    for (int i = 0; i < N; i++) { R.fwd[i] = hs->wN[i]; R.inv[i] = hs->wNi[i]; }
+    for (int i = 0; i < N; i++) {
+        R.fwd[i] = hs->wN[i];
+        R.inv[i] = hs->wNi[i];
+        R.cs[i] = hs->invN_den * hs->gmi[i];
+    }
     PowTab gi{hs->gi_hi.as<Fr>(), hs->gi_lo.as<Fr>(), hs->S};
     hipLaunchKernelGGL(k_cross_inv_out<N>, dim3(grid_for(hs->chunk, 256)), dim3(256), 0, st, h, recv,
                        hs->chunk, hs->M, hs->log_w, (uint32_t)hs->rank, hs->m, hs->invN_den, R, gi);
@@ -990,6 +1032,16 @@ gg_hshard* hshard_create(int log_n, const void* omega_mont, const void* coset_ge
     Fr gn = pow_u64(g, hs->n) - Fr::one();
     GG_CHECK(!gn.is_zero(), GG_ERR_INVALID_ARG, "g^n == 1: coset generator in the domain");
     hs->invN_den = hs->invN * inverse(gn);
+    {
+        const Fr gmr = pow_u64(g, hs->m), gmr_i = inverse(gmr);
+        Fr x = Fr::one(), y = Fr::one();
+        for (int i = 0; i < 16; i++) {
+            hs->gm[i] = x;
+            hs->gmi[i] = y;
+            x = x * gmr;
+            y = y * gmr_i;
+        }
+    }
     hs->S = (log_n + 1) / 2;
     pow_tab_upload(log_n, hs->S, w, hs->w_hi, hs->w_lo);
     pow_tab_upload(log_n, hs->S, inverse(w), hs->wi_hi, hs->wi_lo);

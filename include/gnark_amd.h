@@ -400,8 +400,8 @@ int gg_groth16_mpk_devices(gg_groth16_mpk_t mpk, int *devices, int cap);
 /* world and whether computeH is distributed (1) or replicated per shard (0) */
 int gg_groth16_mpk_info(gg_groth16_mpk_t mpk, int *world, int *distributed_h);
 /* 1: the shards split the A, B1, K, G2 MSMs by bucket stripes (each device
- * holds the whole wire tables; the default for a power-of-two world,
- * GG_MPK_SPLIT=wires selects wire slices); 0: by wire slices */
+ * holds the whole wire tables; GG_MPK_SPLIT=stripes at creation, power-of-two
+ * worlds); 0: by wire slices (the default, measured faster per GPU) */
 int gg_groth16_mpk_split(gg_groth16_mpk_t mpk, int *bucket_stripes);
 /* as gg_groth16_prove (host inputs): Ar, Bs, Krs affine */
 int gg_groth16_mpk_prove(gg_groth16_mpk_t mpk, const void *wires, size_t n_wires, const void *sol_a,

@@ -44,9 +44,9 @@ def test_mpk_golden(idx, world):
 @pytest.mark.parametrize("log_n,n_wires,world,kidx", [(12, 3000, 4, False), (13, 7000, 8, True),
                                                       (12, 2500, 3, False), (14, 16000, 16, False)])
 def test_mpk_vs_oracle(log_n, n_wires, world, kidx, split, monkeypatch):
-    """split: bucket stripes (the default for a power-of-two world: whole wire
-    tables per device, shard r takes the buckets b = r mod world) or wire slices
-    (GG_MPK_SPLIT=wires); a world of 3 always slices wires."""
+    """split: wire slices (the default) or bucket stripes (GG_MPK_SPLIT=stripes,
+    power-of-two worlds: whole wire tables per device, shard r takes the
+    buckets b = r mod world); a world of 3 always slices wires."""
     from gnark_amd import backend, groth16
     monkeypatch.setenv("GG_MPK_SPLIT", split)
     from test_gpu_groth16 import synthetic_case
