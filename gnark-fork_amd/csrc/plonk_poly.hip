@@ -139,14 +139,34 @@ static void scan_pow_host(const F& u, ScanPow<F>& P) {
         s = s * s;
     }
 }
+// thread i < 64 writes u^i, thread 64 + j (j <= 32) writes u^(64 j), each by
+// square-and-multiply (<= 12 dependent products instead of a 97-long chain on
+// one lane: this table heads every affine scan level)
+template <class F>
+__device__ __forceinline__ F pow_small(F base, uint32_t e) {
+    F r = F::one();
+    bool any = false;
+    for (int b = 5; b >= 0; b--) {
+        if (any) r = r * r;
+        if ((e >> b) & 1u) {
+            r = any ? r * base : base;
+            any = true;
+        }
+    }
+    return r;
+}
 template <class F>
 __global__ void k_pow_tab(F u, F* tab) {
-    if (threadIdx.x || blockIdx.x) return;
-    F a = F::one();
-    for (int i = 0; i < 64; i++) { stb(tab + i, a); a = a * u; }
-    const F u64 = a;
-    a = F::one();
-    for (int j = 0; j < 33; j++) { stb(tab + 64 + j, a); a = a * u64; }
+    const uint32_t t = threadIdx.x;
+    if (blockIdx.x || t >= 97) return;
+    if (t < 64) {
+        stb(tab + t, pow_small(u, t));
+        return;
+    }
+    F u64 = u;
+#pragma unroll
+    for (int k = 0; k < 6; k++) u64 = u64 * u64;
+    stb(tab + t, pow_small(u64, t - 64));  // j = t - 64 <= 32
 }
 
 size_t scan_arena_bytes(size_t m) {
@@ -167,7 +187,7 @@ static void scan_rec(F* x, size_t m, const F& u, hipStream_t st, Arena& ar) {
     scan_pow_host(u, P);
     if (MODE == SCAN_AFFINE) {
         F* tab = ar.get<F>(97);
-        hipLaunchKernelGGL(k_pow_tab<F>, dim3(1), dim3(64), 0, st, u, tab);
+        hipLaunchKernelGGL(k_pow_tab<F>, dim3(1), dim3(128), 0, st, u, tab);
         GG_HIP(hipGetLastError());
         P.lo = tab;
         P.hi = tab + 64;

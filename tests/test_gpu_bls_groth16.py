@@ -161,6 +161,17 @@ def test_groth16_bls12_381_bit_exact(log_n):
     prg = mpk.prove(sys_.solve(w[1:1 + chains]), opt, r=frb(r), s=frb(s))
     assert (prg.Ar, prg.Bs, prg.Krs) == (pr.Ar, pr.Bs, pr.Krs)
     mpk.close()
+    if world & (world - 1) == 0:  # bucket stripes over BLS12-381 G1 / G2 tables
+        import os
+        os.environ["GG_MPK_SPLIT"] = "stripes"
+        try:
+            mps = groth16.MultiGpuProvingKey(data, [0] * world)
+        finally:
+            del os.environ["GG_MPK_SPLIT"]
+        assert mps.split() == "stripes"
+        prs = mps.prove(sol, opt, r=frb(r), s=frb(s))
+        assert (prs.Ar, prs.Bs, prs.Krs) == (pr.Ar, pr.Bs, pr.Krs)
+        mps.close()
     sys_.close()
     bad = list(w)
     bad[-1] = (bad[-1] + 1) % R
