@@ -113,6 +113,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--solver", type=int, default=1,
                     help="time the GPU R1CS solver on the headline circuit and witness -> proof (1/0)")
+    ap.add_argument("--projection", default="2,4,8",
+                    help="N = 1 only: time ONE shard of the N-way split of the headline prove run alone "
+                         "on this GPU (GG_MPK_SOLO), for each N listed -- the per-GPU work of an N-GPU node "
+                         "less the xGMI transfers ('' = skip)")
     ap.add_argument("--no-variants", action="store_true",
                     help="skip the serial / device-input prove variants (profiling runs)")
     ap.add_argument("--extras-timeout", type=float, default=420.0,
@@ -352,6 +356,15 @@ def main():
         except Exception as e:  # report, never hide
             out["solver"] = {"error": repr(e)}
     g.close()
+    # ---- per-GPU work of the N-GPU split (N = 1 only): one shard of an N-way
+    # key (wire slices, distributed computeH) proved ALONE on this GPU
+    stage_now["now"] = "projection"
+    if mode == "single" and args.projection:
+        try:
+            out["split_projection"] = split_projection(g, [int(x) for x in args.projection.split(",") if x],
+                                                       ms_per_step)
+        except Exception as e:  # report, never hide
+            out["split_projection"] = {"error": repr(e)}
     del g
 
     # ---- standalone 2^20 G1 MSM (BASELINE configs[1]); weak scaling at N > 1
@@ -547,6 +560,42 @@ class Groth16Bench:
         self.pk.close()
         if self.world > 1:
             self.hs.close()
+
+
+def split_projection(g, worlds, one_gpu_ms, steps=5):
+    """Per-GPU prove time of the headline split over N GPUs, measured on this one
+    GPU: an N-shard one-process key (gg_groth16_mpk_*, wire slices, the
+    distributed computeH) whose shard 0 proves alone (GG_MPK_SOLO=0: its
+    exchanges skip the peers; the proof it returns is not valid).  What it
+    leaves out is the xGMI traffic of the three all-to-alls (3 x 3 n/N^2 x 32 B
+    to each peer, pushed to the N - 1 peers at once)."""
+    from gnark_amd import backend, groth16
+    res = {"note": "one shard of the N-way split of this prove run alone on this GPU (GG_MPK_SOLO=0, "
+                   "solution resident): the work one GPU of an N-GPU node does, without the xGMI transfers "
+                   "of the distributed computeH; speedup = one-GPU ms / this", "one_gpu_ms": one_gpu_ms}
+    sol = groth16.Solution(*g.host, g.shape["nw"], g.shape["ncons"])
+    opt = backend.with_amd_acceleration()
+    os.environ["GG_MPK_SOLO"] = "0"
+    try:
+        for n in worlds:
+            t0 = time.time()
+            mpk = groth16.MultiGpuProvingKey(g.data, [0] * n)
+            sd = groth16.replicate_solution(sol, [0] * n)
+            setup = time.time() - t0
+            mpk.prove(sd, opt, r=g.r, s=g.s)
+            ts = []
+            for _ in range(steps):
+                a = time.perf_counter()
+                mpk.prove(sd, opt, r=g.r, s=g.s)
+                ts.append(1e3 * (time.perf_counter() - a))
+            med = sorted(ts)[len(ts) // 2]
+            res[str(n)] = {"shard_ms_median": med, "shard_ms": [round(x, 2) for x in ts],
+                           "speedup": one_gpu_ms / med, "split": mpk.split(), "key_setup_s": round(setup, 1)}
+            del sd
+            mpk.close()
+    finally:
+        del os.environ["GG_MPK_SOLO"]
+    return res
 
 
 def mimc_chain_system(nb_chains, rounds, nb_public_inputs):

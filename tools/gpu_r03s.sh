@@ -21,6 +21,6 @@ fi
 if [[ "$S" == *bench* ]]; then step 600 bench_$V.json python3 -u bench.py || exit 2; fi
 if [[ "$S" == *prof* ]]; then
   step 600 prof_$V.txt rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$V -o run -- \
-    python3 -u bench.py --steps 5 --warmup 1 --no-variants --msm-log-n 0 --ntt-log-n 0 --plonk-log-n 0 --no-cpu-baseline --solver 0 || exit 2
+    python3 -u bench.py --steps 5 --warmup 1 --no-variants --msm-log-n 0 --ntt-log-n 0 --plonk-log-n 0 --no-cpu-baseline --solver 0 --projection '' || exit 2
 fi
 echo done >> gpurun_out/progress_$V.txt
