@@ -398,7 +398,9 @@ def main():
     if args.plonk_log_n:
         try:
             pr = plonk_prove_bench(args.plonk_log_n, rank=rank, world=world, dist=dist, xdev=xdev,
-                                   barrier=barrier)
+                                   barrier=barrier,
+                                   projection=[int(x) for x in args.projection.split(",") if x]
+                                   if mode == "single" else ())
         except Exception as e:  # report, never hide
             pr = {"error": repr(e)}
         if rank == 0:
@@ -1019,7 +1021,7 @@ def plonk_bench(log_n, reps=5):
 
 
 def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, xdev=None,
-                      barrier=None):
+                      barrier=None, projection=()):
     """BLS12-381 PlonK prove (gg_plonk_prove: prove.go:116-1079 inside the library,
     errgroup DAG on HIP streams) at n = 2^log_n with a synthetic key (random SRS
     points, selectors and copy permutation) and a random witness, inputs resident
@@ -1078,6 +1080,36 @@ def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, 
         tims.append(tim)
     tim = tims[ts.index(min(ts))]
     extra = {"stage_ms_all": tims} if per_rep else {}
+    # configs[4] is 8 x MI355X: the primary part of an N-part one-process key
+    # (KZG base slices, numerator cosets over min(N, 4) parts) proved with its
+    # peers idle (GG_PLONK_SOLO) -- the critical GPU's work on an N-GPU node
+    if projection and world == 1:
+        del pk
+        proj = {"note": "primary part of an N-part key (gg_plonk_pk_create_multi) proved with the peer parts "
+                        "idle (GG_PLONK_SOLO=1): the work of the GPU that runs every step outside the MSM "
+                        "slices and the other parts' cosets, without the xGMI copies; speedup = one-GPU ms / this"}
+        kzg = DeviceBuffer(96 * (n + 3))
+        msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bls_dev(n + 3, 61), n + 3, scalars_on_device=True, out=kzg)
+        lag = DeviceBuffer(96 * n)
+        msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bls_dev(n, 62), n, scalars_on_device=True, out=lag)
+        sel = [bls_dev(n, 70 + i) for i in range(8)]
+        os.environ["GG_PLONK_SOLO"] = "1"
+        try:
+            for nd in projection:
+                pkm = pp.ProvingKey(log_n, kzg, lag, *sel, perm, devices=[0] * nd)
+                pp.prove(pkm, L, R_, O, rng=rng())
+                tp = []
+                for _ in range(max(reps, 3)):
+                    t = time.perf_counter()
+                    pp.prove(pkm, L, R_, O, rng=rng())
+                    tp.append(1e3 * (time.perf_counter() - t))
+                med = sorted(tp)[len(tp) // 2]
+                proj[str(nd)] = {"primary_part_ms_median": med, "ms": [round(x, 2) for x in tp],
+                                 "speedup": min(ts) / med}
+                pkm.close()
+        finally:
+            del os.environ["GG_PLONK_SOLO"]
+        extra["split_projection"] = proj
     return {"log_n": log_n, "n_gpus": world, "prove_ms": min(ts), "prove_ms_all": ts, "stage_ms": tim,
             **extra, "kzg_bases": "1/%d slice per GPU, partial commitments all-gathered" % world,
             "key_setup_s": t_setup, "msms_per_proof": 10,

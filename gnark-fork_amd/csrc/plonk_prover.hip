@@ -373,6 +373,14 @@ static BJac peer_msm(Key* pk, PlonkPeer* p, bool kzg, int wi, const FrB* scal) {
     msm_device_work(kzg ? p->kzg : p->kzg_lag, p->work[wi], p->scal[wi].as<Fr>(), &j, p->s[wi]);
     return j;
 }
+// GG_PLONK_SOLO=1 (timing rehearsal only): a multi-part key's peer parts do
+// nothing -- no MSM slices, no cosets -- so one GPU times the work of the
+// primary part of an N-GPU node (every step outside the MSM slices and the
+// peers' cosets runs there); the proof is not valid
+static bool plonk_solo() {
+    const char* e = getenv("GG_PLONK_SOLO");
+    return e && atoi(e) != 0;
+}
 // this rank's partial MSM (the whole MSM on one GPU, or split over the key's
 // device parts and summed here); red() completes a process shard's partial
 static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStream_t st) {
@@ -380,7 +388,7 @@ static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStr
     const bool kz = base == pk->kzg;
     const size_t lo = kz ? pk->k_lo : pk->l_lo;
     std::vector<std::future<BJac>> fs;
-    if (!pk->peers.empty()) {
+    if (!pk->peers.empty() && !plonk_solo()) {
         GG_HIP(hipStreamSynchronize(st));  // the scalars are complete before the peers copy them
         for (auto& p : pk->peers)
             fs.push_back(std::async(std::launch::async, [pk, pp = p.get(), kz, wi, scal] {
@@ -833,7 +841,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         return NP;
     };
     std::vector<std::future<void>> peer_work;
-    if (!pk->peers.empty()) {
+    if (!pk->peers.empty() && !plonk_solo()) {
         for (int k = 0; k < 4; k++) GG_HIP(hipStreamSynchronize(s[k]));  // inputs complete before the copies
         const int rb = pk->log_big - pk->log_n;
         for (auto& pp : pk->peers) {
