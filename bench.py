@@ -1098,14 +1098,15 @@ def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, 
             for nd in projection:
                 pkm = pp.ProvingKey(log_n, kzg, lag, *sel, perm, devices=[0] * nd)
                 pp.prove(pkm, L, R_, O, rng=rng())
-                tp = []
+                tp, stg = [], {}
                 for _ in range(max(reps, 3)):
                     t = time.perf_counter()
-                    pp.prove(pkm, L, R_, O, rng=rng())
+                    stg = {}
+                    pp.prove(pkm, L, R_, O, timings=stg, rng=rng())
                     tp.append(1e3 * (time.perf_counter() - t))
                 med = sorted(tp)[len(tp) // 2]
                 proj[str(nd)] = {"primary_part_ms_median": med, "ms": [round(x, 2) for x in tp],
-                                 "speedup": min(ts) / med}
+                                 "speedup": min(ts) / med, "stage_ms": stg}
                 pkm.close()
         finally:
             del os.environ["GG_PLONK_SOLO"]

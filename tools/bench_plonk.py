@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """PlonK BLS12-381 prove timing (gnark_amd.plonk_prover) with per-stage times.
-usage: bench_plonk.py log_n [reps]"""
+usage: bench_plonk.py log_n [reps] [projection, e.g. 8 or 2,4,8]"""
 import json
 import os
 import sys
@@ -14,7 +14,8 @@ import bench  # noqa: E402
 def main():
     L = int(sys.argv[1]) if len(sys.argv) > 1 else 22
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-    r = bench.plonk_prove_bench(L, reps=reps, per_rep=True)
+    proj = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else ()
+    r = bench.plonk_prove_bench(L, reps=reps, per_rep=True, projection=proj)
     print(json.dumps(r), flush=True)
 
 
