@@ -1107,7 +1107,17 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
     // segments of L = 2^logL buckets, >= 2^17 of them per group (a lane each:
     // fewer leave the chip idle while each lane walks its chain); below 2^18
     // buckets per group the quad path is faster (MI355X: 2^20 MSM, c = 17)
-    const int logL = std::min(4, 31 - __builtin_clz((unsigned)std::max<size_t>(nbg, 1)) - 17);
+    // groups of 2^17 buckets take the segment path too, with L = 2 (the B1 / G2
+    // MSMs of a 2^21-wire key shard; the 8-way 2^24 shard alone, alternating
+    // A/B: 18.62 / 18.26 vs 19.11 / 18.04 ms, profiles/r03_af_*; 2^16 .. 2^18:
+    // 18.20 / 18.08 vs 18.57 / 18.63, r03_ae_*); the 2^20 MSM's 2^16 buckets
+    // stay on the quad path.  GG_MSM_SEGSUM_MINLOG=k moves the threshold
+    static const int seg_minlog = [] {
+        const char* e = getenv("GG_MSM_SEGSUM_MINLOG");
+        return e ? std::max(8, std::min(18, atoi(e))) : 17;
+    }();
+    const int lgb = 31 - __builtin_clz((unsigned)std::max<size_t>(nbg, 1));
+    const int logL = lgb >= 18 ? std::min(4, lgb - 17) : (lgb >= seg_minlog ? 1 : 0);
     if constexpr (kSegsumGroup<F>) {
         if (segsum_enabled() && logL >= 1) {
             // level 2 and the weighted sums in radix form, a lane per bucket / segment
