@@ -40,6 +40,10 @@ void msm_finish_dev(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st, M
 MsmWork* msm_work_new();
 void msm_work_delete(MsmWork* w);
 MsmSort* msm_work_sort(MsmWork* w);
+void msm_prepare_derived_dev(gg_msm_base* a, MsmSort* sa, gg_msm_base* b, MsmSort* sb, const uint32_t* bmap,
+                             hipStream_t st);
+bool msm_derivable(const gg_msm_base* a, const gg_msm_base* b);
+void msm_build_bmap(const gg_msm_base* a, const gg_msm_base* b, DevBuf& bmap);
 MsmScratch* msm_work_scratch(MsmWork* w);
 int msm_base_window(const gg_msm_base* b);
 int choose_c(size_t n, size_t point_bytes, int total_bits);
@@ -89,6 +93,10 @@ static PointSizes point_sizes(int curve) {
 struct WireBases {
     gg_msm_base_t A = nullptr, B = nullptr, K = nullptr, B2 = nullptr;
     bool share_AK = false, share_B = false;
+    // B1 / G2 on A's window: their sorted entries filtered from the A / K sort
+    // (msm_prepare_derived) instead of a sort of their own; bmap: wire -> B point
+    bool derive_B = false;
+    DevBuf bmap;
     int groups = 1;
     WireBases() = default;
     WireBases(const WireBases&) = delete;
@@ -204,7 +212,14 @@ static std::shared_ptr<WireBases> wire_bases_build(int curve, int log_n, const v
     GG_CHECK(nK == 0 || g1_K, GG_ERR_INVALID_ARG, "null g1_K");
     const size_t nw = hi - lo;
     const int cAK = choose_c(std::max<size_t>(nw, 1), ps.g1a, tbits);
-    const int cB = choose_c(std::max<size_t>(nB, 1), 128, tbits);  // B1 shares its sort with G2
+    int cB = choose_c(std::max<size_t>(nB, 1), 128, tbits);  // B1 shares its sort with G2
+    // B1 / G2 take A's window when it is at most two bits wider than their own:
+    // their entries then come out of the A / K sort by a filter (one sort fewer
+    // per proof; at 2^24 the window 22 B1 / G2 MSMs cost what window 20 did,
+    // profiles/r03_ah_*).  Opt-in until measured: GG_G16_B_DERIVE=1
+    const bool try_derive = getenv("GG_G16_B_DERIVE") && atoi(getenv("GG_G16_B_DERIVE")) != 0;
+    if (try_derive && cAK >= cB && cAK - cB <= 2 && nB) cB = cAK;
+    if (const char* e = getenv("GG_G16_B_WINDOW")) cB = std::max(4, std::min(24, atoi(e)));  // A/B
     const int cZ = choose_c(std::max<size_t>(nZ, 1), ps.g1a, tbits);
     auto wb = std::make_shared<WireBases>();
     {
@@ -231,6 +246,10 @@ static std::shared_ptr<WireBases> wire_bases_build(int curve, int log_n, const v
     wb->B2 = msm_base_create_internal(g2, g2_B, nB, ib.data(), msm_base_window(wb->B), false, wb->groups);
     wb->share_AK = msm_same_shape(wb->A, wb->K);
     wb->share_B = msm_same_shape(wb->B, wb->B2);
+    if (try_derive && wb->share_B && msm_derivable(wb->A, wb->B)) {
+        msm_build_bmap(wb->A, wb->B, wb->bmap);
+        wb->derive_B = true;
+    }
     return wb;
 }
 
@@ -658,7 +677,10 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
             xB2 = msm_work_scratch(ws->B2);
         }
         msm_prepare_dev(pk->A, sAK, wdev, pk->s2, pk->slog, pk->spart);
-        msm_prepare_dev(pk->B, sB, wdev, pk->s3, pk->slog, pk->spart);
+        if (pk->wb->derive_B)  // B1 / G2's entries filtered out of the A / K sort
+            msm_prepare_derived_dev(pk->A, sAK, pk->B, sB, pk->wb->bmap.as<uint32_t>(), pk->s3);
+        else
+            msm_prepare_dev(pk->B, sB, wdev, pk->s3, pk->slog, pk->spart);
         if (!pk->share_AK) msm_prepare_dev(pk->K, sK, wdev, pk->s4, pk->slog, pk->spart);
         if (!pk->share_B) msm_prepare_dev(pk->B2, sB2, wdev, pk->s0, pk->slog, pk->spart);
     })();

@@ -116,6 +116,31 @@ void msm_finish_dev(gg_msm_base* b, MsmSort* s, void* out_jac, hipStream_t st, M
     else if (b->group == GG_BLS12_381_G1) msm_finish_bls(b, s, scr, out_jac, st);
     else msm_finish_bls2(b, s, scr, out_jac, st);
 }
+void msm_prepare_derived_dev(gg_msm_base* a, MsmSort* sa, gg_msm_base* b, MsmSort* sb, const uint32_t* bmap,
+                             hipStream_t st) {
+    if (b->n) msm_prepare_derived(a, sa, b, sb, bmap, st);
+}
+// bmap[i] = j where b's point j takes a's scalar i (b's index map), else ~0
+__global__ void k_bmap_scatter(const uint32_t* sidx, size_t nb_pts, uint32_t na, uint32_t* bmap) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < nb_pts && sidx[j] < na) bmap[sidx[j]] = (uint32_t)j;
+}
+void msm_build_bmap(const gg_msm_base* a, const gg_msm_base* b, DevBuf& bmap) {
+    bmap.alloc(std::max<size_t>(a->n, 1) * 4);
+    GG_HIP(hipMemset(bmap.p, 0xff, std::max<size_t>(a->n, 1) * 4));
+    if (b->n) {
+        hipLaunchKernelGGL(k_bmap_scatter, dim3(grid_for(b->n, 256)), dim3(256), 0, hipStreamPerThread,
+                           b->sidx.as<uint32_t>(), b->n, (uint32_t)a->n, bmap.as<uint32_t>());
+        GG_HIP(hipGetLastError());
+    }
+    GG_HIP(hipStreamSynchronize(hipStreamPerThread));
+}
+bool msm_derivable(const gg_msm_base* a, const gg_msm_base* b) {
+    if (a->c != b->c || a->W != b->W || a->G != b->G || a->has_sidx || !b->has_sidx) return false;
+    for (int w = 0; w < a->W; w++)
+        if (a->win.bits[w] != b->win.bits[w] || a->win.off[w] != b->win.off[w]) return false;
+    return (double)a->W * (double)a->n < 4294967295.0;
+}
 MsmSort* msm_work_sort(MsmWork* w) { return &w->sort; }
 MsmScratch* msm_work_scratch(MsmWork* w) { return &w->scr; }
 size_t msm_scalars_needed(gg_msm_base* b) {

@@ -643,6 +643,79 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     }
 }
 
+// ---- a sort derived from another base's (Groth16: B1 / G2 from the A / K sort).
+// Base a indexes the scalars directly (entry = w' n_a + i, i = the scalar's
+// index), base b through its map (entry = w' n_b + j, scalar sidx_b[j]), with
+// the same window layout.  bmap[i] = j for the scalars b uses, else ~0.  The
+// entries of a's sorted list whose scalar b uses, renumbered and kept in order,
+// are b's sorted list: same digits, same buckets.  A stable filter (flags,
+// exclusive scan, scatter) instead of a second sort; b's bucket offsets are the
+// kept counts before a's.
+__global__ void k_derive_flags(const uint32_t* sorted, const uint32_t* offsets, uint32_t nb, size_t cap, uint32_t n,
+                               const uint32_t* bmap, uint32_t* flags) {
+    const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= cap) return;
+    uint32_t f = 0;
+    if (e < offsets[nb]) f = bmap[(sorted[e] & 0x7fffffffu) % n] != 0xffffffffu;
+    flags[e] = f;
+}
+__global__ void k_derive_scatter(const uint32_t* sorted, const uint32_t* offsets, uint32_t nb, uint32_t n, uint32_t nb_pts,
+                                 const uint32_t* bmap, const uint32_t* pos, uint32_t* out) {
+    const size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= offsets[nb]) return;
+    const uint32_t v = sorted[e], idx = v & 0x7fffffffu;
+    const uint32_t j = bmap[idx % n];
+    if (j == 0xffffffffu) return;
+    out[pos[e]] = ((idx / n) * nb_pts + j) | (v & 0x80000000u);
+}
+__global__ void k_derive_offsets(const uint32_t* offa, const uint32_t* pos, uint32_t nb, uint32_t* offb) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q <= nb) offb[q] = pos[offa[q]];
+}
+
+void msm_prepare_derived(const gg_msm_base* a, const MsmSort* sa, const gg_msm_base* b, MsmSort* sb,
+                         const uint32_t* bmap, hipStream_t st) {
+    GG_CHECK(a->c == b->c && a->W == b->W && a->G == b->G && !a->has_sidx, GG_ERR_INTERNAL,
+             "derived sort: the bases' window layouts differ");
+    const size_t cap = (size_t)a->W * a->n, nb = a->nb >> sa->slog;
+    sb->slog = sa->slog;
+    sb->sres = sa->sres;
+    sb->ensure_events();
+    sb->keys.reserve(std::max<size_t>(cap, 1) * 4);           // flags
+    sb->tmp_entry.reserve((std::max<size_t>(cap, 1) + 1) * 4);  // kept positions (+ the total)
+    sb->sorted.reserve(std::max<size_t>((size_t)b->W * b->n, 1) * 4);
+    sb->offsets.reserve((nb + 1) * 4);
+    sb->maxcnt.reserve(4);
+    GG_HIP(hipStreamWaitEvent(st, sa->ready_ev, 0));
+    {
+        ProfScope ps_sort("msm_sort", st, (double)b->n);
+        uint32_t* flags = sb->keys.as<uint32_t>();
+        uint32_t* pos = sb->tmp_entry.as<uint32_t>();
+        const uint32_t* offa = sa->offsets.as<uint32_t>();
+        hipLaunchKernelGGL(k_derive_flags, dim3(grid_for(cap, 256)), dim3(256), 0, st, sa->sorted.as<uint32_t>(),
+                           offa, (uint32_t)nb, cap, (uint32_t)a->n, bmap, flags);
+        GG_HIP(hipGetLastError());
+        exclusive_scan(flags, pos, cap, st, sb->scan_tmp);
+        hipLaunchKernelGGL(k_set_total, dim3(1), dim3(1), 0, st, pos, flags, cap);
+        GG_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_derive_scatter, dim3(grid_for(cap, 256)), dim3(256), 0, st, sa->sorted.as<uint32_t>(),
+                           offa, (uint32_t)nb, (uint32_t)a->n, (uint32_t)b->n, bmap, pos, sb->sorted.as<uint32_t>());
+        GG_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_derive_offsets, dim3(grid_for(nb + 1, 256)), dim3(256), 0, st, offa, pos, (uint32_t)nb,
+                           sb->offsets.as<uint32_t>());
+        GG_HIP(hipGetLastError());
+        ps_sort.stop(st);
+    }
+    GG_HIP(hipMemsetAsync(sb->maxcnt.p, 0, 4, st));
+    hipLaunchKernelGGL(k_bucket_max, dim3(grid_for(nb, 256)), dim3(256), 0, st, sb->offsets.as<uint32_t>(), nb,
+                       sb->maxcnt.as<uint32_t>());
+    GG_HIP(hipGetLastError());
+    GG_HIP(hipMemcpyAsync(sb->pin, sb->maxcnt.p, 4, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipMemcpyAsync(sb->pin + 1, sb->offsets.as<uint32_t>() + nb, 4, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipEventRecord(sb->pin_ev, st));
+    GG_HIP(hipEventRecord(sb->ready_ev, st));
+}
+
 // Sort of one scalar vector over b's shape into s; records s->ready_ev (sort
 // done) and s->pin_ev (the fullest bucket's entry count on the host).
 void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st, int slog,

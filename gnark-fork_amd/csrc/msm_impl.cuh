@@ -97,6 +97,10 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
 // b mod 2^slog = sres, see MsmSort)
 void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st, int slog = 0,
                  uint32_t sres = 0);
+// b's sort from a's (same window layout, a indexes its scalars directly, bmap:
+// a's scalar index -> b's point or ~0); waits for sa->ready_ev on st
+void msm_prepare_derived(const gg_msm_base* a, const MsmSort* sa, const gg_msm_base* b, MsmSort* sb,
+                         const uint32_t* bmap, hipStream_t st);
 
 constexpr uint32_t LIGHT = 16;
 // Bucket ids: B = j 2^(c-1) + b for precompute group j (< G) and bucket b of the
