@@ -483,6 +483,12 @@ extern "C" int gg_groth16_mpk_prove_ex(gg_groth16_mpk_t m, int inputs_on_device,
     } fx_guard{fx};
     m->solo = -1;
     if (const char* e = getenv("GG_MPK_SOLO")) m->solo = std::max(-1, std::min(atoi(e), m->world - 1));
+    if (m->solo >= 0) {
+        static std::once_flag warned;
+        std::call_once(warned, [] {
+            fprintf(stderr, "gnark_amd: GG_MPK_SOLO is set -- timing rehearsal, multi-GPU proofs are NOT valid\n");
+        });
+    }
     m->bar.n = m->solo >= 0 ? 1 : m->world;
     m->bar.reset();
     const size_t pbytes = 4 * m->g1j + m->g2j;  // a | b1 | k | z | b2 (gg_groth16_prove_partial)

@@ -379,7 +379,14 @@ static BJac peer_msm(Key* pk, PlonkPeer* p, bool kzg, int wi, const FrB* scal) {
 // peers' cosets runs there); the proof is not valid
 static bool plonk_solo() {
     const char* e = getenv("GG_PLONK_SOLO");
-    return e && atoi(e) != 0;
+    const bool on = e && atoi(e) != 0;
+    if (on) {
+        static std::once_flag warned;
+        std::call_once(warned, [] {
+            fprintf(stderr, "gnark_amd: GG_PLONK_SOLO is set -- timing rehearsal, multi-GPU proofs are NOT valid\n");
+        });
+    }
+    return on;
 }
 // this rank's partial MSM (the whole MSM on one GPU, or split over the key's
 // device parts and summed here); red() completes a process shard's partial
