@@ -96,3 +96,23 @@ def test_mpk_errors():
     pr = mpk.prove(sol, backend.with_amd_acceleration(), r=b(g["r"]), s=b(g["s"]))
     assert pr.Ar.hex() == g["Ar"]
     mpk.close()
+
+
+def test_mpk_solo_timing_mode(monkeypatch):
+    """GG_MPK_SOLO=r (bench.py's split_projection): shard r proves alone -- it
+    runs with the exchanges skipping the peers, its proof is not the real one,
+    and the next proof on the same key without it is bit-exact again."""
+    from gnark_amd import backend, groth16
+    from test_gpu_groth16 import synthetic_case
+    d, wires, sa, sb, sc, ncons, r, s = synthetic_case(12, 3000, 3, 77, k_inf_every=5)
+    data = groth16.ProvingKeyData(**d)
+    sol = groth16.Solution(wires, sa, sb, sc, 3000, ncons)
+    mpk = groth16.MultiGpuProvingKey(data, [0] * 4)
+    opt = backend.with_amd_acceleration()
+    ref = mpk.prove(sol, opt, r=r, s=s)
+    monkeypatch.setenv("GG_MPK_SOLO", "1")
+    solo = mpk.prove(sol, opt, r=r, s=s)
+    assert solo != ref
+    monkeypatch.delenv("GG_MPK_SOLO")
+    assert mpk.prove(sol, opt, r=r, s=s) == ref
+    mpk.close()

@@ -296,3 +296,23 @@ def test_plonk_prove_2p22_verifies():
     log(f"8-part prove {1e3 * (time.perf_counter() - t):.1f} ms {tim}")
     assert p8 == proof
     pk8.close()
+
+
+def test_plonk_solo_timing_mode(monkeypatch):
+    """GG_PLONK_SOLO=1 (bench.py's split_projection): the primary part of a
+    multi-part key proves with its peers idle -- it runs, its proof is not the
+    real one (the peers' MSM slices and cosets are missing), and unsetting it
+    gives the real proof again on the same key."""
+    from gnark_amd import plonk_prover as pp
+    log_n, parts = 7, 4
+    circ = Circuit(log_n, 45, nb_public=1, n_cmt=0)
+    tau = random.Random(99).randrange(2, R)
+    pkm = make_key(circ, tau, devices=[0] * parts)
+    L, Rv, O, pub, cmts = circ.solve(pkm, 6, commit=pkm.commit_lagrange)
+    ref = pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts)
+    monkeypatch.setenv("GG_PLONK_SOLO", "1")
+    solo = pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts)
+    assert solo != ref
+    monkeypatch.delenv("GG_PLONK_SOLO")
+    assert pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts) == ref
+    pkm.close()
