@@ -741,6 +741,7 @@ struct gg_hshard {
     Fr gm[16], gmi[16];  // g^(m i), g^(-m i): the coset factors of the size-N steps
     DevBuf y, full;  // 3 x m local vectors; staging of host inputs
     DevBuf hblk;     // m elements: h_bitrev[rank m, (rank+1) m)
+    DevBuf ccoef;    // m elements: den * c's coefficients of this rank's (q, c2), [c2 chunk + q]
     hipStream_t st = nullptr;
     std::mutex mu;
     ~gg_hshard() {
@@ -818,10 +819,14 @@ __global__ void k_twist_scatter(Fr* send, const Fr* y, size_t m, size_t chunk, i
 
 // phase 2: finish the inverse transform (size-N iDFT, 1/N), scale by g^c, start
 // the forward coset transform (size-N DFT, twist w^(c1 k')) -- per (poly, q)
+// poly 2 (c) stops after the inverse half: by linearity h = den coset_iFFT(a b)
+// - den c_coef, so c needs no coset evaluation -- its coefficients times den
+// go to ccoef for phase 4 (its send slot stays unused)
 template <int N>
 __global__ void __launch_bounds__(256) k_cross_fwd(Fr* send, const Fr* recv, size_t chunk, int npoly,
                                                    int M, uint32_t rank, size_t m, Fr invN,
-                                                   SmallRoots<N> R, PowTab gpow, PowTab wpow) {
+                                                   SmallRoots<N> R, PowTab gpow, PowTab wpow, Fr* ccoef,
+                                                   Fr cden) {
     size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= chunk * npoly) return;
     const int poly = (int)(t / chunk);
@@ -835,6 +840,11 @@ __global__ void __launch_bounds__(256) k_cross_fwd(Fr* send, const Fr* recv, siz
 #pragma unroll
     for (int k = 0; k < N; k++) x[k] = load_fr(recv + ((size_t)k * npoly + poly) * chunk + q);
     dft_small<N>(x, R.inv);
+    if (poly == 2) {
+#pragma unroll
+        for (int c2 = 0; c2 < N; c2++) store_fr(ccoef + (size_t)c2 * chunk + q, x[c2] * cden);
+        return;
+    }
 #pragma unroll
     for (int c2 = 0; c2 < N; c2++) x[c2] = x[c2] * R.cs[c2];
     dft_small<N>(x, R.fwd);
@@ -859,7 +869,7 @@ __global__ void k_unpack(Fr* y, const Fr* recv, size_t m, size_t chunk, int npol
 template <int N>
 __global__ void __launch_bounds__(256) k_cross_inv_out(Fr* h, const Fr* recv, size_t chunk, int M,
                                                        int logN, uint32_t rank, size_t m, Fr scale,
-                                                       SmallRoots<N> R, PowTab gipow) {
+                                                       SmallRoots<N> R, PowTab gipow, const Fr* ccoef) {
     size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= chunk) return;
     const uint32_t c1 = brev_bits((uint32_t)(rank * chunk + q), M);
@@ -873,7 +883,8 @@ __global__ void __launch_bounds__(256) k_cross_inv_out(Fr* h, const Fr* recv, si
     const Fr gi = gipow.at(c1);
 #pragma unroll
     for (int c2 = 0; c2 < N; c2++)
-        store_fr(h + (size_t)N * q + brev_bits((uint32_t)c2, logN), x[c2] * R.cs[c2] * gi);
+        store_fr(h + (size_t)N * q + brev_bits((uint32_t)c2, logN),
+                 x[c2] * R.cs[c2] * gi - load_fr(ccoef + (size_t)c2 * chunk + q));
 }
 
 static void pow_tab_upload(int L, int S, const Fr& x, DevBuf& hi, DevBuf& lo) {
@@ -894,7 +905,8 @@ static void launch_cross_fwd(gg_hshard* hs, Fr* send, const Fr* recv, int npoly,
     PowTab gp{hs->g_hi.as<Fr>(), hs->g_lo.as<Fr>(), hs->S};
     PowTab wp{hs->w_hi.as<Fr>(), hs->w_lo.as<Fr>(), hs->S};
     hipLaunchKernelGGL(k_cross_fwd<N>, dim3(grid_for(hs->chunk * npoly, 256)), dim3(256), 0, st, send,
-                       recv, hs->chunk, npoly, hs->M, (uint32_t)hs->rank, hs->m, hs->invN, R, gp, wp);
+                       recv, hs->chunk, npoly, hs->M, (uint32_t)hs->rank, hs->m, hs->invN, R, gp, wp,
+                       hs->ccoef.as<Fr>(), hs->invN_den);
     GG_HIP(hipGetLastError());
 }
 
@@ -908,7 +920,8 @@ static void launch_cross_inv(gg_hshard* hs, Fr* h, const Fr* recv, hipStream_t s
     }
     PowTab gi{hs->gi_hi.as<Fr>(), hs->gi_lo.as<Fr>(), hs->S};
     hipLaunchKernelGGL(k_cross_inv_out<N>, dim3(grid_for(hs->chunk, 256)), dim3(256), 0, st, h, recv,
-                       hs->chunk, hs->M, hs->log_w, (uint32_t)hs->rank, hs->m, hs->invN_den, R, gi);
+                       hs->chunk, hs->M, hs->log_w, (uint32_t)hs->rank, hs->m, hs->invN_den, R, gi,
+                       (const Fr*)hs->ccoef.as<Fr>());
     GG_HIP(hipGetLastError());
 }
 
@@ -950,20 +963,19 @@ void hshard_phase3(gg_hshard* hs, const Fr* recv, Fr* send, hipStream_t st) {
     const size_t m = hs->m;
     Fr* y = hs->y.as<Fr>();
     const Fr* nul = nullptr;
-    for (int p = 0; p < 3; p++) {
+    for (int p = 0; p < 2; p++) {  // a, b (c's slot carries nothing: phase 2 kept its coefficients)
         hipLaunchKernelGGL(k_unpack, dim3(grid_for(m, 256)), dim3(256), 0, st, y + (size_t)p * m, recv, m,
                            hs->chunk, 3, p);
         GG_HIP(hipGetLastError());
     }
     // coset evaluations on this rank's points g w^(rank + N j) (DIT: bit-reversed -> natural);
-    // the last pass of c's transform emits a*b - c (PolyOps)
+    // the last pass of b's transform emits a*b
     run_transform(hs->loc.get(), y, y, true, false, -1, -1, nul, nul, st);
-    run_transform(hs->loc.get(), y + m, y + m, true, false, -1, -1, nul, nul, st);
-    run_transform(hs->loc.get(), y + 2 * m, y + 2 * m, true, false, -1, -1, y, y + m, st);
-    // inverse of the quotient evaluations: iDFT_m, then twist w^(-rank c1)
-    run_transform(hs->loc.get(), y + 2 * m, y + 2 * m, false, true, -1, SK_NINV, nul, nul, st);
+    run_transform(hs->loc.get(), y + m, y + m, true, false, -1, -1, y, nul, st, EPI_MUL);
+    // inverse of the product's evaluations: iDFT_m, then twist w^(-rank c1)
+    run_transform(hs->loc.get(), y + m, y + m, false, true, -1, SK_NINV, nul, nul, st);
     PowTab twi{hs->wi_hi.as<Fr>(), hs->wi_lo.as<Fr>(), hs->S};
-    hipLaunchKernelGGL(k_twist_scatter, dim3(grid_for(m, 256)), dim3(256), 0, st, send, y + 2 * m, m,
+    hipLaunchKernelGGL(k_twist_scatter, dim3(grid_for(m, 256)), dim3(256), 0, st, send, y + m, m,
                        hs->chunk, hs->M, 1, 0, (uint32_t)hs->rank, twi);
     GG_HIP(hipGetLastError());
 }
@@ -1049,6 +1061,7 @@ gg_hshard* hshard_create(int log_n, const void* omega_mont, const void* coset_ge
     pow_tab_upload(log_n, hs->S, inverse(g), hs->gi_hi, hs->gi_lo);
     hs->y.alloc(3 * hs->m * 32);
     hs->hblk.alloc(hs->m * 32);
+    hs->ccoef.alloc(hs->m * 32);
     GG_HIP(hipStreamCreateWithFlags(&hs->st, hipStreamNonBlocking));
     return hs.release();
 }
