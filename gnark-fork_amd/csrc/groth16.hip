@@ -51,6 +51,7 @@ void hshard_run(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len
                 Fr* recv, gg_exchange_fn xchg, void* ctx, hipStream_t st);
 size_t hshard_m(const gg_hshard* hs, int* rank, int* world, int* log_n);
 Fr* hshard_h(gg_hshard* hs);
+int hshard_curve(const gg_hshard* hs);
 }  // namespace gg
 
 // distributed computeH of a shard (gg_groth16_prove_partial_dist)
@@ -844,7 +845,7 @@ extern "C" int gg_groth16_prove_partial_dist(gg_groth16_pk_t pk, gg_hshard_t hs,
     GG_CAPI_BEGIN
     check_prove_args(pk, wires, n_wires, sol_a, sol_b, sol_c, n_cons);
     GG_CHECK(hs && xchg && send_dev && recv_dev && partials, GG_ERR_INVALID_ARG, "null argument");
-    GG_CHECK(pk->curve == GG_CURVE_BN254, GG_ERR_UNSUPPORTED, "distributed computeH: BN254 only");
+    GG_CHECK(hshard_curve(hs) == pk->curve, GG_ERR_INVALID_ARG, "hshard and key are over different curves");
     int rank = 0, world = 1, log_n = 0;
     size_t m = hshard_m(hs, &rank, &world, &log_n);
     GG_CHECK(log_n == pk->log_n, GG_ERR_INVALID_ARG, "hshard and key have different domains");

@@ -85,10 +85,10 @@ struct gg_groth16_mpk {
     // the whole wire tables, shard r takes the buckets b = r mod world) or wire
     // slices (shard r holds wires [r W / world, (r + 1) W / world))
     bool stripes = false;
-    // GG_MPK_SOLO=r (timing rehearsal only): a prove runs shard r ALONE -- its
-    // exchanges skip the peers, the other shards do nothing -- so one GPU
-    // times the work one GPU of an N-GPU node does (less the xGMI transfers);
-    // the proof it returns is not valid
+    // gg_groth16_mpk_set_rehearsal(m, r) (timing rehearsal only): a prove runs
+    // shard r ALONE -- its exchanges skip the peers, the other shards do
+    // nothing -- so one GPU times the work one GPU of an N-GPU node does (less
+    // the xGMI transfers); such a prove returns GG_REHEARSAL, never GG_OK
     int solo = -1;
     size_t n = 0, n_wires = 0;
     size_t g1a = 64, g2a = 128, g1j = 96, g2j = 192;  // the curve's point sizes
@@ -103,6 +103,14 @@ struct gg_groth16_mpk {
     Barrier bar;
     std::mutex mu;  // one proof at a time per key
     double last_ms[4] = {0, 0, 0, 0};
+    // per shard, last proof: where its time went (gg_groth16_mpk_shard_timings)
+    struct ShardTimes {
+        double prove_ms = 0;
+        int nx = 0;
+        double wait_in[GG_MPK_MAX_EXCHANGES] = {}, copy[GG_MPK_MAX_EXCHANGES] = {},
+               wait_out[GG_MPK_MAX_EXCHANGES] = {}, mbytes[GG_MPK_MAX_EXCHANGES] = {};
+    };
+    std::vector<ShardTimes> times;
 };
 
 namespace {
@@ -119,19 +127,28 @@ struct XCtx {
 // each, so the copies to the N-1 peers run at once over their own xGMI links
 // (on one stream they would take the links one after another: at 2^24 over 8
 // GPUs, 392 MB per shard per proof).
+// Per exchange the shard records: the wait at the first barrier (peers still
+// computing: load imbalance), the push time (its N-1 copies issued until all
+// have landed: xGMI), and the wait at the second barrier (peers' pushes into
+// it still in flight).
 int mpk_exchange(void* ctx, const void* send_dev, void* recv_dev, size_t bytes) {
     XCtx* x = (XCtx*)ctx;
     gg_groth16_mpk* m = x->m;
     const int r = x->rank;
     (void)recv_dev;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     if (!m->bar.wait()) return GG_ERR_INTERNAL;
+    const auto t1 = clk::now();
     bool ok = hipSetDevice(m->dev[r]) == hipSuccess;
+    size_t pushed = 0;
     for (int j = 0; ok && j < m->world; j++) {
         const int k = (r + j) % m->world;  // staggered: shard r starts with its own chunk, then r+1, ...
         if (m->solo >= 0 && k != r) continue;  // timing rehearsal: no peers
         ok = hipMemcpyPeerAsync((char*)m->recv[k] + (size_t)r * bytes, m->dev[k],
                                 (const char*)send_dev + (size_t)k * bytes, m->dev[r], bytes,
                                 m->xst[r][j]) == hipSuccess;
+        if (k != r) pushed += bytes;
     }
     for (int j = 0; ok && j < m->world; j++) ok = hipStreamSynchronize(m->xst[r][j]) == hipSuccess;
     if (!ok) {
@@ -139,7 +156,19 @@ int mpk_exchange(void* ctx, const void* send_dev, void* recv_dev, size_t bytes) 
         m->bar.abort();
         return GG_ERR_DEVICE;
     }
-    return m->bar.wait() ? 0 : GG_ERR_INTERNAL;
+    const auto t2 = clk::now();
+    const bool ok2 = m->bar.wait();
+    const auto t3 = clk::now();
+    auto& T = m->times[r];
+    if (T.nx < GG_MPK_MAX_EXCHANGES) {
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        T.wait_in[T.nx] = ms(t0, t1);
+        T.copy[T.nx] = ms(t1, t2);
+        T.wait_out[T.nx] = ms(t2, t3);
+        T.mbytes[T.nx] = pushed / 1e6;
+    }
+    T.nx++;
+    return ok2 ? 0 : GG_ERR_INTERNAL;
 }
 
 // identity partials (Jacobian infinity: x = y = 1, z = 0 in Montgomery form --
@@ -225,9 +254,9 @@ extern "C" int gg_groth16_mpk_create_ex(int curve, int log_n, const void* omega_
     }
     m->n = n;
     m->n_wires = n_wires;
-    // the four-step distributed computeH exists for BN254 fr; BLS12-381 shards
-    // compute h themselves (replicated H, sharded MSMs)
-    m->dist = curve == GG_CURVE_BN254 && dist_h_ok(n, world);
+    // the four-step distributed computeH (either curve's fr); a world it does
+    // not support (not a power of two, n < world^2) replicates H on every shard
+    m->dist = dist_h_ok(n, world);
     m->dev.assign(devices, devices + world);
     m->pk.assign(world, nullptr);
     m->hs.assign(world, nullptr);
@@ -345,7 +374,7 @@ extern "C" int gg_groth16_mpk_create_ex(int curve, int log_n, const void* omega_
             m->xst[r].assign(world, nullptr);
             for (auto& x : m->xst[r])
                 if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return GG_ERR_DEVICE;
-            int rc = gg_hshard_create(log_n, omega_mont, coset_gen_mont, r, world, &m->hs[r]);
+            int rc = gg_hshard_create_ex(curve, log_n, omega_mont, coset_gen_mont, r, world, &m->hs[r]);
             if (rc) return rc;
             size_t mm = 0, xb = 0;
             rc = gg_hshard_info(m->hs[r], &mm, &xb);
@@ -394,7 +423,7 @@ extern "C" int gg_groth16_mpk_create_ex(int curve, int log_n, const void* omega_
         m->xst[r].assign(world, nullptr);
         for (auto& s : m->xst[r])
             if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GG_ERR_DEVICE;
-        rc = gg_hshard_create(log_n, omega_mont, coset_gen_mont, r, world, &m->hs[r]);
+        rc = gg_hshard_create_ex(curve, log_n, omega_mont, coset_gen_mont, r, world, &m->hs[r]);
         if (rc) return rc;
         size_t mm = 0, xb = 0;
         rc = gg_hshard_info(m->hs[r], &mm, &xb);
@@ -481,31 +510,30 @@ extern "C" int gg_groth16_mpk_prove_ex(gg_groth16_mpk_t m, int inputs_on_device,
         gg_g16_fixed_t& h;
         ~FxGuard() { if (h) gg_groth16_finalize_end(h, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr); }
     } fx_guard{fx};
-    m->solo = -1;
-    if (const char* e = getenv("GG_MPK_SOLO")) m->solo = std::max(-1, std::min(atoi(e), m->world - 1));
-    if (m->solo >= 0) {
-        static std::once_flag warned;
-        std::call_once(warned, [] {
-            fprintf(stderr, "gnark_amd: GG_MPK_SOLO is set -- timing rehearsal, multi-GPU proofs are NOT valid\n");
-        });
-    }
     m->bar.n = m->solo >= 0 ? 1 : m->world;
     m->bar.reset();
     const size_t pbytes = 4 * m->g1j + m->g2j;  // a | b1 | k | z | b2 (gg_groth16_prove_partial)
     std::vector<std::vector<uint8_t>> parts(m->world, std::vector<uint8_t>(pbytes));
     std::vector<XCtx> ctx(m->world);
+    m->times.assign(m->world, gg_groth16_mpk::ShardTimes());
     on_shards(m, [&](int r) -> int {
         ctx[r] = XCtx{m, r};
         if (m->solo >= 0 && r != m->solo) {  // timing rehearsal: identity partials
             G16PartialsInf(m->curve, parts[r].data(), m->g1j, m->g2j);
             return 0;
         }
+        const auto a = std::chrono::steady_clock::now();
+        int rc;
         if (m->dist)
-            return gg_groth16_prove_partial_dist(m->pk[r], m->hs[r], wires[r], n_wires, sol_a[r], sol_b[r], sol_c[r],
-                                                 n_cons, inputs_on_device, mpk_exchange, &ctx[r], m->send[r],
-                                                 m->recv[r], parts[r].data());
-        return gg_groth16_prove_partial(m->pk[r], wires[r], n_wires, sol_a[r], sol_b[r], sol_c[r], n_cons,
-                                        inputs_on_device, parts[r].data(), nullptr);
+            rc = gg_groth16_prove_partial_dist(m->pk[r], m->hs[r], wires[r], n_wires, sol_a[r], sol_b[r], sol_c[r],
+                                               n_cons, inputs_on_device, mpk_exchange, &ctx[r], m->send[r],
+                                               m->recv[r], parts[r].data());
+        else
+            rc = gg_groth16_prove_partial(m->pk[r], wires[r], n_wires, sol_a[r], sol_b[r], sol_c[r], n_cons,
+                                          inputs_on_device, parts[r].data(), nullptr);
+        m->times[r].prove_ms =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+        return rc;
     });
     const auto t1 = std::chrono::steady_clock::now();
     // exact sum of the partials: 4 G1Jac then one G2Jac
@@ -532,6 +560,11 @@ extern "C" int gg_groth16_mpk_prove_ex(gg_groth16_mpk_t m, int inputs_on_device,
     m->last_ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
     m->last_ms[1] = std::chrono::duration<double, std::milli>(t2 - t1).count();
     m->last_ms[2] = std::chrono::duration<double, std::milli>(t2 - t0).count();
+    if (m->solo >= 0) {
+        gg::set_last_error("timing rehearsal (gg_groth16_mpk_set_rehearsal): shard " + std::to_string(m->solo) +
+                           " proved alone, the proof is NOT valid");
+        return GG_REHEARSAL;
+    }
     GG_CAPI_END
 }
 
@@ -551,5 +584,35 @@ extern "C" int gg_groth16_mpk_last_timings(gg_groth16_mpk_t m, double* ms3) {
     GG_CAPI_BEGIN
     GG_CHECK(m && ms3, GG_ERR_INVALID_ARG, "null argument");
     for (int i = 0; i < 3; i++) ms3[i] = m->last_ms[i];
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_mpk_set_rehearsal(gg_groth16_mpk_t m, int solo_shard) {
+    GG_CAPI_BEGIN
+    GG_CHECK(m, GG_ERR_INVALID_ARG, "null key");
+    GG_CHECK(solo_shard >= -1 && solo_shard < m->world, GG_ERR_INVALID_ARG, "solo shard out of range");
+    std::lock_guard<std::mutex> lk(m->mu);
+    m->solo = solo_shard;
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_mpk_shard_timings(gg_groth16_mpk_t m, int shard, double* out, int cap) {
+    GG_CAPI_BEGIN
+    GG_CHECK(m && out, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(shard >= 0 && shard < m->world, GG_ERR_INVALID_ARG, "shard out of range");
+    GG_CHECK(cap >= GG_MPK_TIMING_SLOTS, GG_ERR_INVALID_ARG, "cap < GG_MPK_TIMING_SLOTS");
+    std::lock_guard<std::mutex> lk(m->mu);
+    for (int i = 0; i < GG_MPK_TIMING_SLOTS; i++) out[i] = 0;
+    if (shard >= (int)m->times.size()) return GG_OK;  // no proof yet
+    const auto& T = m->times[shard];
+    out[0] = T.prove_ms;
+    const int nx = std::min(T.nx, GG_MPK_MAX_EXCHANGES);
+    out[1] = nx;
+    for (int e = 0; e < nx; e++) {
+        out[2 + 4 * e] = T.wait_in[e];
+        out[3 + 4 * e] = T.copy[e];
+        out[4 + 4 * e] = T.wait_out[e];
+        out[5 + 4 * e] = T.mbytes[e];
+    }
     GG_CAPI_END
 }

@@ -25,6 +25,7 @@
 #include <memory>
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 
 namespace gg {
 
@@ -716,8 +717,12 @@ void xn_minus_one_inv(gg_domain* big, size_t n_small, void* out) {
 }  // namespace gg
 
 
+
+
 // ===========================================================================
-// Distributed computeH over N GPUs (DESIGN.md "Multi-GPU").
+// Distributed computeH over N GPUs (DESIGN.md "Multi-GPU"), for the
+// scalar field of either Groth16 curve (backend/groth16/bn254/prove.go:353-396
+// and backend/groth16/bls12-381/prove.go:353-396, the same generated code).
 // n = m * N.  Rank k holds the cyclic slice y_k[j] = x[k + N j] of every input
 // vector.  A transform of size n is a local size-m transform (root w^N),
 // a twist by w^(+-k c1), one all-to-all, and m/N size-N transforms per rank:
@@ -728,20 +733,35 @@ void xn_minus_one_inv(gg_domain* big, size_t n_small, void* out) {
 // bit-reversed order: coefficient c1 + m c2 lands at r m + N q + bitrev_N(c2),
 // i.e. rank r holds h_bitrev[r m, (r+1) m) -- the Z slice [r m, (r+1) m) of
 // pk.G1.Z (setup.go:265) -- so the Z-MSM needs no further exchange.
-// Three all-to-alls per proof (a, b, c bundled; then a, b, c again; then h).
+// Three all-to-alls per proof: a, b, c (3 chunks per rank pair); a, b on the
+// coset (2 chunks: c stops at its coefficients, h = den coset_iFFT(a b) - den c
+// by linearity); then a b (1 chunk).
 // ===========================================================================
-struct gg_hshard {
-    int log_n = 0, rank = 0, world = 1, log_w = 0, M = 0;
-    size_t n = 0, m = 0, chunk = 0;  // chunk = m / N elements per (rank, poly)
-    std::unique_ptr<DomainT<FrCfg>> loc;  // size-m domain, root w^N
-    Fr invN, invN_den;
+namespace gg {
+template <class C>
+struct HShardT {
+    using F = Fe<C>;
+    std::unique_ptr<DomainT<C>> loc;  // size-m domain, root w^N
+    F invN, invN_den;
     DevBuf w_hi, w_lo, wi_hi, wi_lo, g_hi, g_lo, gi_hi, gi_lo;  // split power tables over [0, n)
     int S = 0;
-    Fr wN[16], wNi[16];
-    Fr gm[16], gmi[16];  // g^(m i), g^(-m i): the coset factors of the size-N steps
-    DevBuf y, full;  // 3 x m local vectors; staging of host inputs
-    DevBuf hblk;     // m elements: h_bitrev[rank m, (rank+1) m)
-    DevBuf ccoef;    // m elements: den * c's coefficients of this rank's (q, c2), [c2 chunk + q]
+    F wN[16], wNi[16];
+    F gm[16], gmi[16];  // g^(m i), g^(-m i): the coset factors of the size-N steps
+    DevBuf y, full;     // 3 x m local vectors; staging of host inputs
+    DevBuf hblk;        // m elements: h_bitrev[rank m, (rank+1) m)
+    DevBuf ccoef;       // m elements: den * c's coefficients of this rank's (q, c2), [c2 chunk + q]
+};
+}  // namespace gg
+
+struct gg_hshard {
+    int curve = GG_CURVE_BN254;
+    int log_n = 0, rank = 0, world = 1, log_w = 0, M = 0;
+    size_t n = 0, m = 0, chunk = 0;  // chunk = m / N elements per (rank, poly)
+    std::unique_ptr<gg::HShardT<gg::FrCfg>> bn;
+    std::unique_ptr<gg::HShardT<gg::FrBlsCfg>> bls;
+    // phase 4 subtracts the c coefficients phase 2 left in ccoef: set by phase 2,
+    // consumed by phase 4 (a phase 4 without its phase 2 is refused)
+    bool ccoef_ready = false;
     hipStream_t st = nullptr;
     std::mutex mu;
     ~gg_hshard() {
@@ -750,26 +770,27 @@ struct gg_hshard {
 };
 
 namespace gg {
+template <class F>
 struct PowTab {
-    const Fr *hi, *lo;
+    const F *hi, *lo;
     int S;
-    __device__ __forceinline__ Fr at(uint32_t e) const {
+    __device__ __forceinline__ F at(uint32_t e) const {
         return load_fr(hi + (e >> S)) * load_fr(lo + (e & ((1u << S) - 1)));
     }
 };
 
 // the size-N steps' constants: powers of the primitive N-th root and its
 // inverse, and the per-output scale cs[i] (folding 1/N and g^(+-m i))
-template <int N>
+template <class F, int N>
 struct SmallRoots {
-    Fr fwd[N], inv[N], cs[N];
+    F fwd[N], inv[N], cs[N];
 };
 
 // X[j] = sum_k x[k] r^(j k) in place, r[i] = r^i: radix-2 DIT in registers
 // (N/2 log N butterflies, the r^0 ones without a product -- 5 products for
 // N = 8 where the direct sum takes 49)
-template <int N>
-__device__ __forceinline__ void dft_small(Fr (&x)[N], const Fr (&r)[N]) {
+template <class F, int N>
+__device__ __forceinline__ void dft_small(F (&x)[N], const F (&r)[N]) {
     constexpr int LG = N <= 1 ? 0 : (N == 2 ? 1 : (N == 4 ? 2 : (N == 8 ? 3 : 4)));
 #pragma unroll
     for (int i = 0; i < N; i++) {
@@ -777,7 +798,7 @@ __device__ __forceinline__ void dft_small(Fr (&x)[N], const Fr (&r)[N]) {
 #pragma unroll
         for (int b = 0; b < LG; b++) j |= ((i >> b) & 1) << (LG - 1 - b);
         if (i < j) {
-            Fr t = x[i];
+            F t = x[i];
             x[i] = x[j];
             x[j] = t;
         }
@@ -788,8 +809,8 @@ __device__ __forceinline__ void dft_small(Fr (&x)[N], const Fr (&r)[N]) {
         for (int i = 0; i < N; i += len)
 #pragma unroll
             for (int j = 0; j < len / 2; j++) {
-                const Fr u = x[i + j];
-                Fr v = x[i + j + len / 2];
+                const F u = x[i + j];
+                F v = x[i + j + len / 2];
                 if (j) v = v * r[(N / len) * j];
                 x[i + j] = u + v;
                 x[i + j + len / 2] = u - v;
@@ -797,49 +818,49 @@ __device__ __forceinline__ void dft_small(Fr (&x)[N], const Fr (&r)[N]) {
 }
 
 // y[j] = x[rank + N j] (zero past len)
-__global__ void k_gather_cyclic(Fr* y, const Fr* x, size_t len, size_t m, int rank, int N) {
+template <class F>
+__global__ void k_gather_cyclic(F* y, const F* x, size_t len, size_t m, int rank, int N) {
     size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= m) return;
     size_t i = (size_t)rank + (size_t)N * j;
-    Fr v = i < len ? load_fr(x + i) : Fr::zero();
+    F v = i < len ? load_fr(x + i) : F::zero();
     store_fr(y + j, v);
 }
 
 // send[(r * npoly + poly) * chunk + q] = y[p] * w^(sign * rank * bitrev_M(p)), p = r chunk + q
-__global__ void k_twist_scatter(Fr* send, const Fr* y, size_t m, size_t chunk, int M, int npoly,
-                                int poly, uint32_t rank, PowTab tw) {
+template <class F>
+__global__ void k_twist_scatter(F* send, const F* y, size_t m, size_t chunk, int M, int npoly, int poly,
+                                uint32_t rank, PowTab<F> tw) {
     size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= m) return;
     uint32_t c1 = brev_bits((uint32_t)p, M);
-    Fr v = load_fr(y + p);
+    F v = load_fr(y + p);
     if (rank) v = v * tw.at(rank * c1);
     size_t r = p / chunk, q = p - r * chunk;
     store_fr(send + (r * npoly + poly) * chunk + q, v);
 }
 
 // phase 2: finish the inverse transform (size-N iDFT, 1/N), scale by g^c, start
-// the forward coset transform (size-N DFT, twist w^(c1 k')) -- per (poly, q)
-// poly 2 (c) stops after the inverse half: by linearity h = den coset_iFFT(a b)
-// - den c_coef, so c needs no coset evaluation -- its coefficients times den
-// go to ccoef for phase 4 (its send slot stays unused)
-template <int N>
-__global__ void __launch_bounds__(256) k_cross_fwd(Fr* send, const Fr* recv, size_t chunk, int npoly,
-                                                   int M, uint32_t rank, size_t m, Fr invN,
-                                                   SmallRoots<N> R, PowTab gpow, PowTab wpow, Fr* ccoef,
-                                                   Fr cden) {
+// the forward coset transform (size-N DFT, twist w^(c1 k')) -- per (poly, q).
+// recv holds a, b, c (3 chunks per source rank); send gets a, b (2 chunks per
+// destination).  c (poly 2) stops after the inverse half: by linearity
+// h = den coset_iFFT(a b) - den c_coef, so c needs no coset evaluation -- its
+// coefficients times den go to ccoef for phase 4.
+template <class F, int N>
+__global__ void __launch_bounds__(256) k_cross_fwd(F* send, const F* recv, size_t chunk, int M, uint32_t rank,
+                                                   SmallRoots<F, N> R, PowTab<F> gpow, PowTab<F> wpow, F* ccoef,
+                                                   F cden) {
     size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= chunk * npoly) return;
+    if (t >= chunk * 3) return;
     const int poly = (int)(t / chunk);
     const size_t q = t - (size_t)poly * chunk;
     const uint32_t c1 = brev_bits((uint32_t)(rank * chunk + q), M);
-    (void)invN;
-    (void)m;
     // co[c2] = iDFT_N(in)[c2] / N * g^(c1 + m c2) = g^c1 * (iDFT_N(in)[c2] * cs[c2]);
     // out[k2] = DFT_N(co)[k2] * w^(c1 k2) = g^c1 w^(c1 k2) * DFT_N(iDFT_N(in) * cs)[k2]
-    Fr x[N];
+    F x[N];
 #pragma unroll
-    for (int k = 0; k < N; k++) x[k] = load_fr(recv + ((size_t)k * npoly + poly) * chunk + q);
-    dft_small<N>(x, R.inv);
+    for (int k = 0; k < N; k++) x[k] = load_fr(recv + ((size_t)k * 3 + poly) * chunk + q);
+    dft_small<F, N>(x, R.inv);
     if (poly == 2) {
 #pragma unroll
         for (int c2 = 0; c2 < N; c2++) store_fr(ccoef + (size_t)c2 * chunk + q, x[c2] * cden);
@@ -847,18 +868,19 @@ __global__ void __launch_bounds__(256) k_cross_fwd(Fr* send, const Fr* recv, siz
     }
 #pragma unroll
     for (int c2 = 0; c2 < N; c2++) x[c2] = x[c2] * R.cs[c2];
-    dft_small<N>(x, R.fwd);
-    const Fr wc = wpow.at(c1);
-    Fr f = gpow.at(c1);
+    dft_small<F, N>(x, R.fwd);
+    const F wc = wpow.at(c1);
+    F f = gpow.at(c1);
 #pragma unroll
     for (int k2 = 0; k2 < N; k2++) {
         if (k2) f = f * wc;
-        store_fr(send + ((size_t)k2 * npoly + poly) * chunk + q, x[k2] * f);
+        store_fr(send + ((size_t)k2 * 2 + poly) * chunk + q, x[k2] * f);
     }
 }
 
 // y[p] = recv[(r * npoly + poly) * chunk + q], p = r chunk + q
-__global__ void k_unpack(Fr* y, const Fr* recv, size_t m, size_t chunk, int npoly, int poly) {
+template <class F>
+__global__ void k_unpack(F* y, const F* recv, size_t m, size_t chunk, int npoly, int poly) {
     size_t p = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= m) return;
     size_t r = p / chunk, q = p - r * chunk;
@@ -866,129 +888,169 @@ __global__ void k_unpack(Fr* y, const Fr* recv, size_t m, size_t chunk, int npol
 }
 
 // phase 4: size-N iDFT * den / N * g^-c, written at N q + bitrev_N(c2)
-template <int N>
-__global__ void __launch_bounds__(256) k_cross_inv_out(Fr* h, const Fr* recv, size_t chunk, int M,
-                                                       int logN, uint32_t rank, size_t m, Fr scale,
-                                                       SmallRoots<N> R, PowTab gipow, const Fr* ccoef) {
+template <class F, int N>
+__global__ void __launch_bounds__(256) k_cross_inv_out(F* h, const F* recv, size_t chunk, int M, int logN,
+                                                       uint32_t rank, SmallRoots<F, N> R, PowTab<F> gipow,
+                                                       const F* ccoef) {
     size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= chunk) return;
     const uint32_t c1 = brev_bits((uint32_t)(rank * chunk + q), M);
-    (void)scale;
-    (void)m;
     // iDFT_N(in)[c2] * scale * g^-(c1 + m c2) = g^-c1 * (iDFT_N(in)[c2] * cs[c2])
-    Fr x[N];
+    F x[N];
 #pragma unroll
     for (int k = 0; k < N; k++) x[k] = load_fr(recv + (size_t)k * chunk + q);
-    dft_small<N>(x, R.inv);
-    const Fr gi = gipow.at(c1);
+    dft_small<F, N>(x, R.inv);
+    const F gi = gipow.at(c1);
 #pragma unroll
     for (int c2 = 0; c2 < N; c2++)
         store_fr(h + (size_t)N * q + brev_bits((uint32_t)c2, logN),
                  x[c2] * R.cs[c2] * gi - load_fr(ccoef + (size_t)c2 * chunk + q));
 }
 
-static void pow_tab_upload(int L, int S, const Fr& x, DevBuf& hi, DevBuf& lo) {
-    std::vector<Fr> h, l;
-    build_pow_tables(L, S, x, Fr::one(), h, l);
+template <class F>
+static void pow_tab_upload(int L, int S, const F& x, DevBuf& hi, DevBuf& lo) {
+    std::vector<F> h, l;
+    build_pow_tables(L, S, x, F::one(), h, l);
     upload(hi, h);
     upload(lo, l);
 }
 
-template <int N>
-static void launch_cross_fwd(gg_hshard* hs, Fr* send, const Fr* recv, int npoly, hipStream_t st) {
-    SmallRoots<N> R;
+template <class C>
+static HShardT<C>* hs_impl(gg_hshard* hs) {
+    if constexpr (std::is_same<C, FrCfg>::value) return hs->bn.get();
+    else return hs->bls.get();
+}
+
+template <class C, int N>
+static void launch_cross_fwd(gg_hshard* hs, Fe<C>* send, const Fe<C>* recv, hipStream_t st) {
+    using F = Fe<C>;
+    HShardT<C>* t = hs_impl<C>(hs);
+    SmallRoots<F, N> R;
     for (int i = 0; i < N; i++) {
-        R.fwd[i] = hs->wN[i];
-        R.inv[i] = hs->wNi[i];
-        R.cs[i] = hs->invN * hs->gm[i];
+        R.fwd[i] = t->wN[i];
+        R.inv[i] = t->wNi[i];
+        R.cs[i] = t->invN * t->gm[i];
     }
-    PowTab gp{hs->g_hi.as<Fr>(), hs->g_lo.as<Fr>(), hs->S};
-    PowTab wp{hs->w_hi.as<Fr>(), hs->w_lo.as<Fr>(), hs->S};
-    hipLaunchKernelGGL(k_cross_fwd<N>, dim3(grid_for(hs->chunk * npoly, 256)), dim3(256), 0, st, send,
-                       recv, hs->chunk, npoly, hs->M, (uint32_t)hs->rank, hs->m, hs->invN, R, gp, wp,
-                       hs->ccoef.as<Fr>(), hs->invN_den);
+    PowTab<F> gp{t->g_hi.template as<F>(), t->g_lo.template as<F>(), t->S};
+    PowTab<F> wp{t->w_hi.template as<F>(), t->w_lo.template as<F>(), t->S};
+    hipLaunchKernelGGL((k_cross_fwd<F, N>), dim3(grid_for(hs->chunk * 3, 256)), dim3(256), 0, st, send, recv,
+                       hs->chunk, hs->M, (uint32_t)hs->rank, R, gp, wp, t->ccoef.template as<F>(), t->invN_den);
     GG_HIP(hipGetLastError());
 }
 
-template <int N>
-static void launch_cross_inv(gg_hshard* hs, Fr* h, const Fr* recv, hipStream_t st) {
-    SmallRoots<N> R;
+template <class C, int N>
+static void launch_cross_inv(gg_hshard* hs, Fe<C>* h, const Fe<C>* recv, hipStream_t st) {
+    using F = Fe<C>;
+    HShardT<C>* t = hs_impl<C>(hs);
+    SmallRoots<F, N> R;
     for (int i = 0; i < N; i++) {
-        R.fwd[i] = hs->wN[i];
-        R.inv[i] = hs->wNi[i];
-        R.cs[i] = hs->invN_den * hs->gmi[i];
+        R.fwd[i] = t->wN[i];
+        R.inv[i] = t->wNi[i];
+        R.cs[i] = t->invN_den * t->gmi[i];
     }
-    PowTab gi{hs->gi_hi.as<Fr>(), hs->gi_lo.as<Fr>(), hs->S};
-    hipLaunchKernelGGL(k_cross_inv_out<N>, dim3(grid_for(hs->chunk, 256)), dim3(256), 0, st, h, recv,
-                       hs->chunk, hs->M, hs->log_w, (uint32_t)hs->rank, hs->m, hs->invN_den, R, gi,
-                       (const Fr*)hs->ccoef.as<Fr>());
+    PowTab<F> gi{t->gi_hi.template as<F>(), t->gi_lo.template as<F>(), t->S};
+    hipLaunchKernelGGL((k_cross_inv_out<F, N>), dim3(grid_for(hs->chunk, 256)), dim3(256), 0, st, h, recv,
+                       hs->chunk, hs->M, hs->log_w, (uint32_t)hs->rank, R, gi,
+                       (const F*)t->ccoef.template as<F>());
     GG_HIP(hipGetLastError());
 }
 
 // ---- the four local phases (exchanges between them are the caller's) ----
 // compact: a, b, c already hold this rank's cyclic slices x[rank + N j] (len of
 // them), e.g. gathered on the host by the stager, instead of full vectors
-void hshard_phase1(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len, Fr* send,
-                   hipStream_t st, bool compact = false) {
+template <class C>
+static void phase1_t(gg_hshard* hs, const Fe<C>* a, const Fe<C>* b, const Fe<C>* c, size_t len, Fe<C>* send,
+                     hipStream_t st, bool compact) {
+    using F = Fe<C>;
+    HShardT<C>* t = hs_impl<C>(hs);
     const size_t m = hs->m;
-    Fr* y = hs->y.as<Fr>();
-    PowTab twi{hs->wi_hi.as<Fr>(), hs->wi_lo.as<Fr>(), hs->S};
-    const Fr* src[3] = {a, b, c};
+    F* y = t->y.template as<F>();
+    PowTab<F> twi{t->wi_hi.template as<F>(), t->wi_lo.template as<F>(), t->S};
+    const F* src[3] = {a, b, c};
     for (int p = 0; p < 3; p++) {
-        Fr* yp = y + (size_t)p * m;
-        hipLaunchKernelGGL(k_gather_cyclic, dim3(grid_for(m, 256)), dim3(256), 0, st, yp, src[p], len,
-                           m, compact ? 0 : hs->rank, compact ? 1 : hs->world);
+        F* yp = y + (size_t)p * m;
+        hipLaunchKernelGGL(k_gather_cyclic<F>, dim3(grid_for(m, 256)), dim3(256), 0, st, yp, src[p], len, m,
+                           compact ? 0 : hs->rank, compact ? 1 : hs->world);
         GG_HIP(hipGetLastError());
         // iDFT_m (DIF: natural -> bit-reversed), 1/m folded in
-        run_transform(hs->loc.get(), yp, yp, false, true, -1, SK_NINV, (const Fr*)nullptr,
-                      (const Fr*)nullptr, st);
-        hipLaunchKernelGGL(k_twist_scatter, dim3(grid_for(m, 256)), dim3(256), 0, st, send, yp, m,
-                           hs->chunk, hs->M, 3, p, (uint32_t)hs->rank, twi);
+        run_transform(t->loc.get(), yp, yp, false, true, -1, SK_NINV, (const F*)nullptr, (const F*)nullptr, st);
+        hipLaunchKernelGGL(k_twist_scatter<F>, dim3(grid_for(m, 256)), dim3(256), 0, st, send, yp, m, hs->chunk,
+                           hs->M, 3, p, (uint32_t)hs->rank, twi);
         GG_HIP(hipGetLastError());
     }
 }
 
-void hshard_phase2(gg_hshard* hs, const Fr* recv, Fr* send, hipStream_t st) {
+template <class C>
+static void phase2_t(gg_hshard* hs, const Fe<C>* recv, Fe<C>* send, hipStream_t st) {
     switch (hs->world) {
-        case 1: launch_cross_fwd<1>(hs, send, recv, 3, st); break;
-        case 2: launch_cross_fwd<2>(hs, send, recv, 3, st); break;
-        case 4: launch_cross_fwd<4>(hs, send, recv, 3, st); break;
-        case 8: launch_cross_fwd<8>(hs, send, recv, 3, st); break;
-        case 16: launch_cross_fwd<16>(hs, send, recv, 3, st); break;
+        case 1: launch_cross_fwd<C, 1>(hs, send, recv, st); break;
+        case 2: launch_cross_fwd<C, 2>(hs, send, recv, st); break;
+        case 4: launch_cross_fwd<C, 4>(hs, send, recv, st); break;
+        case 8: launch_cross_fwd<C, 8>(hs, send, recv, st); break;
+        case 16: launch_cross_fwd<C, 16>(hs, send, recv, st); break;
         default: throw Error(GG_ERR_UNSUPPORTED, "distributed computeH: world must be 1, 2, 4, 8 or 16");
     }
 }
 
-void hshard_phase3(gg_hshard* hs, const Fr* recv, Fr* send, hipStream_t st) {
+template <class C>
+static void phase3_t(gg_hshard* hs, const Fe<C>* recv, Fe<C>* send, hipStream_t st) {
+    using F = Fe<C>;
+    HShardT<C>* t = hs_impl<C>(hs);
     const size_t m = hs->m;
-    Fr* y = hs->y.as<Fr>();
-    const Fr* nul = nullptr;
-    for (int p = 0; p < 2; p++) {  // a, b (c's slot carries nothing: phase 2 kept its coefficients)
-        hipLaunchKernelGGL(k_unpack, dim3(grid_for(m, 256)), dim3(256), 0, st, y + (size_t)p * m, recv, m,
-                           hs->chunk, 3, p);
+    F* y = t->y.template as<F>();
+    const F* nul = nullptr;
+    for (int p = 0; p < 2; p++) {  // a, b: phase 2 sent 2 polys per rank pair
+        hipLaunchKernelGGL(k_unpack<F>, dim3(grid_for(m, 256)), dim3(256), 0, st, y + (size_t)p * m, recv, m,
+                           hs->chunk, 2, p);
         GG_HIP(hipGetLastError());
     }
     // coset evaluations on this rank's points g w^(rank + N j) (DIT: bit-reversed -> natural);
     // the last pass of b's transform emits a*b
-    run_transform(hs->loc.get(), y, y, true, false, -1, -1, nul, nul, st);
-    run_transform(hs->loc.get(), y + m, y + m, true, false, -1, -1, y, nul, st, EPI_MUL);
+    run_transform(t->loc.get(), y, y, true, false, -1, -1, nul, nul, st);
+    run_transform(t->loc.get(), y + m, y + m, true, false, -1, -1, y, nul, st, EPI_MUL);
     // inverse of the product's evaluations: iDFT_m, then twist w^(-rank c1)
-    run_transform(hs->loc.get(), y + m, y + m, false, true, -1, SK_NINV, nul, nul, st);
-    PowTab twi{hs->wi_hi.as<Fr>(), hs->wi_lo.as<Fr>(), hs->S};
-    hipLaunchKernelGGL(k_twist_scatter, dim3(grid_for(m, 256)), dim3(256), 0, st, send, y + m, m,
-                       hs->chunk, hs->M, 1, 0, (uint32_t)hs->rank, twi);
+    run_transform(t->loc.get(), y + m, y + m, false, true, -1, SK_NINV, nul, nul, st);
+    PowTab<F> twi{t->wi_hi.template as<F>(), t->wi_lo.template as<F>(), t->S};
+    hipLaunchKernelGGL(k_twist_scatter<F>, dim3(grid_for(m, 256)), dim3(256), 0, st, send, y + m, m, hs->chunk,
+                       hs->M, 1, 0, (uint32_t)hs->rank, twi);
     GG_HIP(hipGetLastError());
 }
 
-void hshard_phase4(gg_hshard* hs, const Fr* recv, Fr* h, hipStream_t st) {
+template <class C>
+static void phase4_t(gg_hshard* hs, const Fe<C>* recv, Fe<C>* h, hipStream_t st) {
     switch (hs->world) {
-        case 1: launch_cross_inv<1>(hs, h, recv, st); break;
-        case 2: launch_cross_inv<2>(hs, h, recv, st); break;
-        case 4: launch_cross_inv<4>(hs, h, recv, st); break;
-        case 8: launch_cross_inv<8>(hs, h, recv, st); break;
-        case 16: launch_cross_inv<16>(hs, h, recv, st); break;
+        case 1: launch_cross_inv<C, 1>(hs, h, recv, st); break;
+        case 2: launch_cross_inv<C, 2>(hs, h, recv, st); break;
+        case 4: launch_cross_inv<C, 4>(hs, h, recv, st); break;
+        case 8: launch_cross_inv<C, 8>(hs, h, recv, st); break;
+        case 16: launch_cross_inv<C, 16>(hs, h, recv, st); break;
         default: throw Error(GG_ERR_UNSUPPORTED, "distributed computeH: world must be 1, 2, 4, 8 or 16");
     }
+}
+
+// curve dispatch over opaque 32-B elements (Fr* for both fields)
+void hshard_phase1(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len, Fr* send, hipStream_t st,
+                   bool compact = false) {
+    hs->ccoef_ready = false;
+    if (hs->curve == GG_CURVE_BN254) phase1_t<FrCfg>(hs, a, b, c, len, send, st, compact);
+    else phase1_t<FrBlsCfg>(hs, (const FrBls*)a, (const FrBls*)b, (const FrBls*)c, len, (FrBls*)send, st, compact);
+}
+void hshard_phase2(gg_hshard* hs, const Fr* recv, Fr* send, hipStream_t st) {
+    if (hs->curve == GG_CURVE_BN254) phase2_t<FrCfg>(hs, recv, send, st);
+    else phase2_t<FrBlsCfg>(hs, (const FrBls*)recv, (FrBls*)send, st);
+    hs->ccoef_ready = true;
+}
+void hshard_phase3(gg_hshard* hs, const Fr* recv, Fr* send, hipStream_t st) {
+    if (hs->curve == GG_CURVE_BN254) phase3_t<FrCfg>(hs, recv, send, st);
+    else phase3_t<FrBlsCfg>(hs, (const FrBls*)recv, (FrBls*)send, st);
+}
+void hshard_phase4(gg_hshard* hs, const Fr* recv, Fr* h, hipStream_t st) {
+    GG_CHECK(hs->ccoef_ready, GG_ERR_INVALID_ARG,
+             "distributed computeH: phase 4 needs the c coefficients of a phase 2 on this handle "
+             "(phases 2 -> 4 in order, one proof at a time per handle)");
+    if (hs->curve == GG_CURVE_BN254) phase4_t<FrCfg>(hs, recv, h, st);
+    else phase4_t<FrBlsCfg>(hs, (const FrBls*)recv, (FrBls*)h, st);
+    hs->ccoef_ready = false;
 }
 
 size_t hshard_m(const gg_hshard* hs, int* rank, int* world, int* log_n) {
@@ -997,14 +1059,67 @@ size_t hshard_m(const gg_hshard* hs, int* rank, int* world, int* log_n) {
     *log_n = hs->log_n;
     return hs->m;
 }
-Fr* hshard_h(gg_hshard* hs) { return hs->hblk.as<Fr>(); }
-
-size_t hshard_exchange_bytes(const gg_hshard* hs, int phase) {
-    return hs->chunk * 32 * (phase == 3 ? 1 : 3);
+int hshard_curve(const gg_hshard* hs) { return hs->curve; }
+Fr* hshard_h(gg_hshard* hs) {
+    return hs->curve == GG_CURVE_BN254 ? hs->bn->hblk.as<Fr>() : hs->bls->hblk.as<Fr>();
 }
 
-gg_hshard* hshard_create(int log_n, const void* omega_mont, const void* coset_gen_mont, int rank, int world) {
+// bytes per rank pair of the all-to-all that follows phase `phase` (1..3):
+// 3 polys after phase 1, 2 after phase 2, 1 after phase 3
+size_t hshard_exchange_bytes(const gg_hshard* hs, int phase) {
+    return hs->chunk * 32 * (size_t)(phase == 1 ? 3 : phase == 2 ? 2 : 1);
+}
+
+template <class C>
+static void hshard_build(gg_hshard* hs, HShardT<C>* t, const void* omega_mont, const void* coset_gen_mont) {
+    using F = Fe<C>;
+    F w, g;
+    memcpy(w.v, omega_mont, 32);
+    memcpy(g.v, coset_gen_mont, 32);
+    F wm = pow_u64(w, (uint64_t)hs->world);
+    t->loc.reset(domain_build<C>(hs->M, wm.v, g.v));  // checks the order of w^N = m
+    // w must have order exactly n: w^(n/2) != 1 (w^N already has order m)
+    GG_CHECK(!(pow_u64(w, hs->n / 2) == F::one()), GG_ERR_INVALID_ARG, "omega order < n");
+    GG_CHECK(pow_u64(w, hs->n) == F::one(), GG_ERR_INVALID_ARG, "omega^n != 1");
+    F wNroot = pow_u64(w, hs->m);  // primitive N-th root
+    F wNinv = inverse(wNroot);
+    F a = F::one(), b = F::one();
+    for (int i = 0; i < 16; i++) {
+        t->wN[i] = a;
+        t->wNi[i] = b;
+        a = a * wNroot;
+        b = b * wNinv;
+    }
+    F nn = F::zero();
+    nn.v[0] = (uint32_t)hs->world;
+    t->invN = inverse(to_mont(nn));
+    F gn = pow_u64(g, hs->n) - F::one();
+    GG_CHECK(!gn.is_zero(), GG_ERR_INVALID_ARG, "g^n == 1: coset generator in the domain");
+    t->invN_den = t->invN * inverse(gn);
+    {
+        const F gmr = pow_u64(g, hs->m), gmr_i = inverse(gmr);
+        F x = F::one(), y = F::one();
+        for (int i = 0; i < 16; i++) {
+            t->gm[i] = x;
+            t->gmi[i] = y;
+            x = x * gmr;
+            y = y * gmr_i;
+        }
+    }
+    t->S = (hs->log_n + 1) / 2;
+    pow_tab_upload(hs->log_n, t->S, w, t->w_hi, t->w_lo);
+    pow_tab_upload(hs->log_n, t->S, inverse(w), t->wi_hi, t->wi_lo);
+    pow_tab_upload(hs->log_n, t->S, g, t->g_hi, t->g_lo);
+    pow_tab_upload(hs->log_n, t->S, inverse(g), t->gi_hi, t->gi_lo);
+    t->y.alloc(3 * hs->m * 32);
+    t->hblk.alloc(hs->m * 32);
+    t->ccoef.alloc(hs->m * 32);
+}
+
+gg_hshard* hshard_create(int curve, int log_n, const void* omega_mont, const void* coset_gen_mont, int rank,
+                         int world) {
     GG_CHECK(omega_mont && coset_gen_mont, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(curve == GG_CURVE_BN254 || curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "bad curve");
     GG_CHECK(world >= 1 && world <= 16 && (world & (world - 1)) == 0, GG_ERR_UNSUPPORTED,
              "distributed computeH: world must be a power of two <= 16");
     GG_CHECK(rank >= 0 && rank < world, GG_ERR_INVALID_ARG, "rank out of range");
@@ -1013,6 +1128,7 @@ gg_hshard* hshard_create(int log_n, const void* omega_mont, const void* coset_ge
     GG_CHECK(log_n >= 1 && log_n <= 28 && log_n >= 2 * lw, GG_ERR_INVALID_ARG,
              "distributed computeH needs 2^log_n >= world^2");
     std::unique_ptr<gg_hshard> hs(new gg_hshard());
+    hs->curve = curve;
     hs->log_n = log_n;
     hs->rank = rank;
     hs->world = world;
@@ -1021,47 +1137,13 @@ gg_hshard* hshard_create(int log_n, const void* omega_mont, const void* coset_ge
     hs->M = log_n - lw;
     hs->m = hs->n >> lw;
     hs->chunk = hs->m >> lw;
-    Fr w, g;
-    memcpy(w.v, omega_mont, 32);
-    memcpy(g.v, coset_gen_mont, 32);
-    Fr wm = pow_u64(w, (uint64_t)world);
-    hs->loc.reset(domain_build<FrCfg>(hs->M, wm.v, g.v));  // checks the order of w^N = m
-    // w must have order exactly n: w^(n/2) != 1 (w^N already has order m)
-    GG_CHECK(!(pow_u64(w, hs->n / 2) == Fr::one()), GG_ERR_INVALID_ARG, "omega order < n");
-    GG_CHECK(pow_u64(w, hs->n) == Fr::one(), GG_ERR_INVALID_ARG, "omega^n != 1");
-    Fr wNroot = pow_u64(w, hs->m);  // primitive N-th root
-    Fr wNinv = inverse(wNroot);
-    Fr a = Fr::one(), b = Fr::one();
-    for (int i = 0; i < 16; i++) {
-        hs->wN[i] = a;
-        hs->wNi[i] = b;
-        a = a * wNroot;
-        b = b * wNinv;
+    if (curve == GG_CURVE_BN254) {
+        hs->bn.reset(new HShardT<FrCfg>());
+        hshard_build(hs.get(), hs->bn.get(), omega_mont, coset_gen_mont);
+    } else {
+        hs->bls.reset(new HShardT<FrBlsCfg>());
+        hshard_build(hs.get(), hs->bls.get(), omega_mont, coset_gen_mont);
     }
-    Fr nn = Fr::zero();
-    nn.v[0] = (uint32_t)world;
-    hs->invN = inverse(to_mont(nn));
-    Fr gn = pow_u64(g, hs->n) - Fr::one();
-    GG_CHECK(!gn.is_zero(), GG_ERR_INVALID_ARG, "g^n == 1: coset generator in the domain");
-    hs->invN_den = hs->invN * inverse(gn);
-    {
-        const Fr gmr = pow_u64(g, hs->m), gmr_i = inverse(gmr);
-        Fr x = Fr::one(), y = Fr::one();
-        for (int i = 0; i < 16; i++) {
-            hs->gm[i] = x;
-            hs->gmi[i] = y;
-            x = x * gmr;
-            y = y * gmr_i;
-        }
-    }
-    hs->S = (log_n + 1) / 2;
-    pow_tab_upload(log_n, hs->S, w, hs->w_hi, hs->w_lo);
-    pow_tab_upload(log_n, hs->S, inverse(w), hs->wi_hi, hs->wi_lo);
-    pow_tab_upload(log_n, hs->S, g, hs->g_hi, hs->g_lo);
-    pow_tab_upload(log_n, hs->S, inverse(g), hs->gi_hi, hs->gi_lo);
-    hs->y.alloc(3 * hs->m * 32);
-    hs->hblk.alloc(hs->m * 32);
-    hs->ccoef.alloc(hs->m * 32);
     GG_HIP(hipStreamCreateWithFlags(&hs->st, hipStreamNonBlocking));
     return hs.release();
 }
@@ -1070,7 +1152,7 @@ gg_hshard* hshard_create(int log_n, const void* omega_mont, const void* coset_ge
 // performs the all-to-all (blocking).  a/b/c: full vectors on the device.
 void hshard_run(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len, bool compact, Fr* send,
                 Fr* recv, gg_exchange_fn xchg, void* ctx, hipStream_t st) {
-    std::lock_guard<std::mutex> lk(hs->mu);  // hs->y / hblk are per-handle scratch
+    std::lock_guard<std::mutex> lk(hs->mu);  // y / hblk / ccoef are per-handle scratch
     auto exchange = [&](int phase) {
         GG_HIP(hipStreamSynchronize(st));
         int rc = xchg(ctx, send, recv, hshard_exchange_bytes(hs, phase));
@@ -1082,16 +1164,21 @@ void hshard_run(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len
     exchange(2);
     hshard_phase3(hs, recv, send, st);
     exchange(3);
-    hshard_phase4(hs, recv, hs->hblk.as<Fr>(), st);
+    hshard_phase4(hs, recv, hshard_h(hs), st);
 }
 }  // namespace gg
 
-extern "C" int gg_hshard_create(int log_n, const void* omega_mont, const void* coset_gen_mont, int rank,
-                                int world, gg_hshard_t* out) {
+extern "C" int gg_hshard_create_ex(int curve, int log_n, const void* omega_mont, const void* coset_gen_mont,
+                                   int rank, int world, gg_hshard_t* out) {
     GG_CAPI_BEGIN
     GG_CHECK(out, GG_ERR_INVALID_ARG, "null argument");
-    *out = hshard_create(log_n, omega_mont, coset_gen_mont, rank, world);
+    *out = hshard_create(curve, log_n, omega_mont, coset_gen_mont, rank, world);
     GG_CAPI_END
+}
+
+extern "C" int gg_hshard_create(int log_n, const void* omega_mont, const void* coset_gen_mont, int rank,
+                                int world, gg_hshard_t* out) {
+    return gg_hshard_create_ex(GG_CURVE_BN254, log_n, omega_mont, coset_gen_mont, rank, world, out);
 }
 
 extern "C" int gg_hshard_release(gg_hshard_t hs) {
@@ -1108,6 +1195,14 @@ extern "C" int gg_hshard_info(gg_hshard_t hs, size_t* m, size_t* exchange_bytes)
     GG_CAPI_END
 }
 
+extern "C" int gg_hshard_exchange_bytes(gg_hshard_t hs, int phase, size_t* bytes_per_rank) {
+    GG_CAPI_BEGIN
+    GG_CHECK(hs && bytes_per_rank, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(phase >= 1 && phase <= 3, GG_ERR_INVALID_ARG, "phase must be 1..3");
+    *bytes_per_rank = hshard_exchange_bytes(hs, phase);
+    GG_CAPI_END
+}
+
 extern "C" int gg_hshard_phase(gg_hshard_t hs, int phase, const void* a, const void* b, const void* c,
                                size_t len, int inputs_on_device, const void* recv, void* send_or_h,
                                void* hip_stream) {
@@ -1120,9 +1215,10 @@ extern "C" int gg_hshard_phase(gg_hshard_t hs, int phase, const void* a, const v
         GG_CHECK(len <= hs->n, GG_ERR_INVALID_ARG, "len > domain cardinality");
         const Fr* src[3] = {(const Fr*)a, (const Fr*)b, (const Fr*)c};
         if (!inputs_on_device) {
-            hs->full.reserve(3 * std::max<size_t>(len, 1) * 32);
+            DevBuf& full = hs->curve == GG_CURVE_BN254 ? hs->bn->full : hs->bls->full;
+            full.reserve(3 * std::max<size_t>(len, 1) * 32);
             for (int i = 0; i < 3; i++) {
-                Fr* d = hs->full.as<Fr>() + i * len;
+                Fr* d = full.as<Fr>() + i * len;
                 if (len) GG_HIP(hipMemcpyAsync(d, src[i], len * 32, hipMemcpyHostToDevice, st));
                 src[i] = d;
             }

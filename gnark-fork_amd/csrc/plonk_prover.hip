@@ -134,6 +134,7 @@ struct PlonkPeer {
     DevBuf tw0, in[5 + plk::MAX_CMT];   // L R O Z (canonical bit-reversed), Qk, Pi_j
     DevBuf cev[7 + plk::MAX_CMT];       // coset evaluation slot
     std::vector<DevBuf> out;            // owned coset blocks of cres
+    hipEvent_t ea[4] = {}, eb[4] = {};  // per stream: around the last peer copy (timing)
     ~PlonkPeer() {
         int cur = 0;
         const bool restore = hipGetDevice(&cur) == hipSuccess;
@@ -151,8 +152,19 @@ struct PlonkPeer {
         out.clear();
         for (hipStream_t x : s)
             if (x) (void)hipStreamDestroy(x);
+        for (int i = 0; i < 4; i++) {
+            if (ea[i]) (void)hipEventDestroy(ea[i]);
+            if (eb[i]) (void)hipEventDestroy(eb[i]);
+        }
         if (restore) (void)hipSetDevice(cur);
     }
+};
+
+// where a device part's time went in the last proof (gg_plonk_pk_part_timings)
+struct PlonkPartTimes {
+    double msm_count = 0, msm_ms = 0, scalar_copy_ms = 0, scalar_mb = 0;
+    double coset_count = 0, coset_ms = 0, coset_in_copy_ms = 0, coset_out_copy_ms = 0, coset_mb = 0;
+    double wait_ms = 0;  // part 0: time spent waiting for the peers' MSM slices and cosets
 };
 
 // ============================================================== prover of one curve
@@ -298,6 +310,11 @@ struct Key : gg_plonk_pk {
     // one-process multi-GPU: this key is part 0 of 1 + peers.size() device parts
     std::vector<std::unique_ptr<PlonkPeer>> peers;
     int owners = 1;  // devices sharing the numerator cosets (coset i -> part i % owners)
+    // gg_plonk_pk_set_rehearsal (timing only): the peer parts do nothing, the
+    // proof is not valid and gg_plonk_prove returns GG_REHEARSAL
+    bool solo = false;
+    std::mutex tmu;
+    std::vector<PlonkPartTimes> ptimes;  // [part], last proof
     int n_cmt = 0;
     hipStream_t s[4] = {nullptr, nullptr, nullptr, nullptr};
     MsmWork* work[3] = {nullptr, nullptr, nullptr};
@@ -364,30 +381,31 @@ static void record_wait(Key* pk, hipStream_t from, hipStream_t to) {
 }
 // a peer part's share of an MSM: its scalar slice copied from the primary GPU
 // (xGMI peer copy), its resident base slice
-static BJac peer_msm(Key* pk, PlonkPeer* p, bool kzg, int wi, const FrB* scal) {
+static double ms_since(std::chrono::steady_clock::time_point a) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+}
+static BJac peer_msm(Key* pk, int part, PlonkPeer* p, bool kzg, int wi, const FrB* scal) {
     GG_HIP(hipSetDevice(p->device));
     const size_t lo = kzg ? p->k_lo : p->l_lo, hi = kzg ? p->k_hi : p->l_hi;
     BJac j = BJac::inf();
     if (hi == lo) return j;
+    const auto a = std::chrono::steady_clock::now();
+    GG_HIP(hipEventRecord(p->ea[wi], p->s[wi]));
     GG_HIP(hipMemcpyPeerAsync(p->scal[wi].p, p->device, scal + lo, pk->device, 32 * (hi - lo), p->s[wi]));
+    GG_HIP(hipEventRecord(p->eb[wi], p->s[wi]));
     msm_device_work(kzg ? p->kzg : p->kzg_lag, p->work[wi], p->scal[wi].as<Fr>(), &j, p->s[wi]);
+    float cp = 0;
+    GG_HIP(hipEventElapsedTime(&cp, p->ea[wi], p->eb[wi]));  // the MSM synchronised the stream
+    std::lock_guard<std::mutex> lk(pk->tmu);
+    if ((size_t)part >= pk->ptimes.size()) return j;  // outside a proof (key setup)
+    PlonkPartTimes& T = pk->ptimes[part];
+    T.msm_count += 1;
+    T.msm_ms += ms_since(a);
+    T.scalar_copy_ms += cp;
+    T.scalar_mb += 32.0 * (hi - lo) / 1e6;
     return j;
 }
-// GG_PLONK_SOLO=1 (timing rehearsal only): a multi-part key's peer parts do
-// nothing -- no MSM slices, no cosets -- so one GPU times the work of the
-// primary part of an N-GPU node (every step outside the MSM slices and the
-// peers' cosets runs there); the proof is not valid
-static bool plonk_solo() {
-    const char* e = getenv("GG_PLONK_SOLO");
-    const bool on = e && atoi(e) != 0;
-    if (on) {
-        static std::once_flag warned;
-        std::call_once(warned, [] {
-            fprintf(stderr, "gnark_amd: GG_PLONK_SOLO is set -- timing rehearsal, multi-GPU proofs are NOT valid\n");
-        });
-    }
-    return on;
-}
+static bool plonk_solo(Key* pk) { return pk->solo; }
 // this rank's partial MSM (the whole MSM on one GPU, or split over the key's
 // device parts and summed here); red() completes a process shard's partial
 static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStream_t st) {
@@ -395,15 +413,26 @@ static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStr
     const bool kz = base == pk->kzg;
     const size_t lo = kz ? pk->k_lo : pk->l_lo;
     std::vector<std::future<BJac>> fs;
-    if (!pk->peers.empty() && !plonk_solo()) {
+    if (!pk->peers.empty() && !plonk_solo(pk)) {
         GG_HIP(hipStreamSynchronize(st));  // the scalars are complete before the peers copy them
-        for (auto& p : pk->peers)
-            fs.push_back(std::async(std::launch::async, [pk, pp = p.get(), kz, wi, scal] {
-                return peer_msm(pk, pp, kz, wi, scal);
+        for (size_t q = 0; q < pk->peers.size(); q++)
+            fs.push_back(std::async(std::launch::async, [pk, q, pp = pk->peers[q].get(), kz, wi, scal] {
+                return peer_msm(pk, (int)q + 1, pp, kz, wi, scal);
             }));
     }
+    const auto a = std::chrono::steady_clock::now();
     msm_device_work(base, pk->work[wi], (const Fr*)(scal + lo), &j, st);
+    const double own = ms_since(a);
+    const auto w = std::chrono::steady_clock::now();
     for (auto& f : fs) j = jac_add(j, f.get());
+    const double waited = ms_since(w);
+    if (!pk->ptimes.empty()) {
+        std::lock_guard<std::mutex> lk(pk->tmu);
+        PlonkPartTimes& T = pk->ptimes[0];
+        T.msm_count += 1;
+        T.msm_ms += own;
+        T.wait_ms += waited;
+    }
     return j;
 }
 // kzg.Commit(p, pk.Kzg) of a buffer of n + 3 scalars (zero beyond the polynomial)
@@ -529,6 +558,10 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
                 p->l_hi = n * (d + 1) / n_devices;
                 GG_HIP(hipSetDevice(p->device));
                 for (hipStream_t& x : p->s) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+                for (int e = 0; e < 4; e++) {
+                    GG_HIP(hipEventCreate(&p->ea[e]));
+                    GG_HIP(hipEventCreate(&p->eb[e]));
+                }
                 for (auto& w : p->work) w = msm_work_new();
                 for (auto& b : p->scal) b.alloc(32 * std::max<size_t>(1, std::max(p->k_hi - p->k_lo, p->l_hi - p->l_lo)));
                 int rc = gg_msm_base_create(Cv::group, (const uint8_t*)kzg_g1 + PT * p->k_lo, p->k_hi - p->k_lo,
@@ -712,6 +745,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     const size_t n = pk->n, nb = 32 * n, nb3 = 32 * (n + 3);
     hipStream_t* s = pk->s;
     pk->ev_next = 0;
+    pk->ptimes.assign(1 + pk->peers.size(), PlonkPartTimes());
     auto t0 = std::chrono::steady_clock::now();
     int tk = 0;
     auto mark = [&]() {
@@ -848,20 +882,23 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         return NP;
     };
     std::vector<std::future<void>> peer_work;
-    if (!pk->peers.empty() && !plonk_solo()) {
+    if (!pk->peers.empty() && !plonk_solo(pk)) {
         for (int k = 0; k < 4; k++) GG_HIP(hipStreamSynchronize(s[k]));  // inputs complete before the copies
         const int rb = pk->log_big - pk->log_n;
-        for (auto& pp : pk->peers) {
-            PlonkPeer* p = pp.get();
+        for (size_t pi = 0; pi < pk->peers.size(); pi++) {
+            PlonkPeer* p = pk->peers[pi].get();
             if (p->cosets.empty()) continue;
-            peer_work.push_back(std::async(std::launch::async, [&, p, rb] {
+            peer_work.push_back(std::async(std::launch::async, [&, p, pi, rb] {
                 GG_HIP(hipSetDevice(p->device));
+                const auto ta = std::chrono::steady_clock::now();
                 hipStream_t q = p->s[3];
                 const FrB* src[5 + plk::MAX_CMT] = {F(pk->cbrev[0]), F(pk->cbrev[1]), F(pk->cbrev[2]), F(pk->cbrev[3]),
                                                     F(pk->qkc)};
                 for (int j = 0; j < n_cmt; j++) src[5 + j] = F(pk->pi_brev[j]);
+                GG_HIP(hipEventRecord(p->ea[3], q));
                 for (int k = 0; k < 5 + n_cmt; k++)
                     GG_HIP(hipMemcpyPeerAsync(p->in[k].p, p->device, src[k], pk->device, nb, q));
+                GG_HIP(hipEventRecord(p->eb[3], q));
                 for (size_t c = 0; c < p->cosets.size(); c++) {
                     const int i = p->cosets[c];
                     auto ceval = [&](const DevBuf& from, DevBuf& to) {
@@ -877,10 +914,28 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                         (size_t)i, e, [&](int k) { return (const FrB*)F(p->ev[k][c]); }, F(p->tw0), F(p->out[c]),
                         true);
                     plk::numerator(NP, q);
+                }
+                // the owned blocks back to the primary's cres (timed separately)
+                GG_HIP(hipEventSynchronize(p->eb[3]));
+                float cin = 0;
+                GG_HIP(hipEventElapsedTime(&cin, p->ea[3], p->eb[3]));
+                GG_HIP(hipEventRecord(p->ea[3], q));
+                for (size_t c = 0; c < p->cosets.size(); c++) {
+                    const int i = p->cosets[c];
                     const size_t blk = rb ? (size_t)(__builtin_bitreverse32((uint32_t)i) >> (32 - rb)) : 0;
                     GG_HIP(hipMemcpyPeerAsync(F(pk->cres) + blk * n, pk->device, p->out[c].p, p->device, nb, q));
                 }
+                GG_HIP(hipEventRecord(p->eb[3], q));
                 GG_HIP(hipStreamSynchronize(q));
+                float cout = 0;
+                GG_HIP(hipEventElapsedTime(&cout, p->ea[3], p->eb[3]));
+                std::lock_guard<std::mutex> lk(pk->tmu);
+                PlonkPartTimes& T = pk->ptimes[pi + 1];
+                T.coset_count += (double)p->cosets.size();
+                T.coset_ms += ms_since(ta);
+                T.coset_in_copy_ms += cin;
+                T.coset_out_copy_ms += cout;
+                T.coset_mb += (double)nb * (5 + n_cmt + p->cosets.size()) / 1e6;
             }));
         }
     }
@@ -903,7 +958,12 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
             plk::numerator(NP, q);
         }
     }
-    for (auto& f : peer_work) f.get();  // their blocks of cres have landed
+    {
+        const auto w = std::chrono::steady_clock::now();
+        for (auto& f : peer_work) f.get();  // their blocks of cres have landed
+        std::lock_guard<std::mutex> lk(pk->tmu);
+        pk->ptimes[0].wait_ms += ms_since(w);
+    }
     record_wait(pk, s[3], s[2]);
     plk::divide_by_xn_minus_one(pk->d1, n, F(pk->cres), s[2]);  // h, canonical regular
     for (int k = 0; k < 3; k++) {
@@ -1281,6 +1341,42 @@ extern "C" int gg_plonk_prove(gg_plonk_pk_t pk, const void* l, const void* r, co
         put(&P.zs_h, pt);
         put(P.zs_value.v, 32);
         memcpy(g_plonk_ms, tms, sizeof(tms));
+        return 0;
+    });
+    const bool rehearsal = with_key(pk, [](auto* k) { return k->solo && !k->peers.empty(); });
+    if (rehearsal) {
+        gg::set_last_error("timing rehearsal (gg_plonk_pk_set_rehearsal): the peer parts did nothing, the proof "
+                           "is NOT valid");
+        return GG_REHEARSAL;
+    }
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_pk_set_rehearsal(gg_plonk_pk_t pk, int on) {
+    GG_CAPI_BEGIN
+    GG_CHECK(pk, GG_ERR_INVALID_ARG, "null key");
+    with_key(pk, [&](auto* k) {
+        std::lock_guard<std::mutex> lk(k->mu);
+        k->solo = on != 0;
+        return 0;
+    });
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_pk_part_timings(gg_plonk_pk_t pk, int part, double* out, int cap) {
+    GG_CAPI_BEGIN
+    GG_CHECK(pk && out, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(cap >= GG_PLONK_PART_SLOTS, GG_ERR_INVALID_ARG, "cap < GG_PLONK_PART_SLOTS");
+    with_key(pk, [&](auto* k) {
+        std::lock_guard<std::mutex> lk(k->mu);
+        GG_CHECK(part >= 0 && part <= (int)k->peers.size(), GG_ERR_INVALID_ARG, "part out of range");
+        for (int i = 0; i < GG_PLONK_PART_SLOTS; i++) out[i] = 0;
+        if (part >= (int)k->ptimes.size()) return 0;  // no proof yet
+        std::lock_guard<std::mutex> lt(k->tmu);
+        const PlonkPartTimes& T = k->ptimes[part];
+        const double v[10] = {T.msm_count, T.msm_ms,   T.scalar_copy_ms,    T.scalar_mb,         T.coset_count,
+                              T.coset_ms,  T.coset_in_copy_ms, T.coset_out_copy_ms, T.coset_mb, T.wait_ms};
+        for (int i = 0; i < 10; i++) out[i] = v[i];
         return 0;
     });
     GG_CAPI_END

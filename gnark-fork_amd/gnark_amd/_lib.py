@@ -12,6 +12,9 @@ _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GNARK_AMD_LIB", os.path.join(_PKG_DIR, "lib", "libgnark_amd.so"))
 
 GG_OK = 0
+GG_REHEARSAL = 7  # a multi-GPU timing rehearsal: the proof written is not valid
+GG_MPK_TIMING_SLOTS = 18
+GG_PLONK_PART_SLOTS = 10
 GG_G1, GG_G2, GG_BLS12_381_G1, GG_BLS12_381_G2 = 1, 2, 3, 4
 GG_CURVE_BN254, GG_CURVE_BLS12_381 = 0, 1
 GG_DIF, GG_DIT = 0, 1
@@ -110,6 +113,8 @@ def _load():
         "gg_plonk_linearized": ([P, S, P, S, ctypes.POINTER(ctypes.c_void_p), S,
                                  ctypes.POINTER(ctypes.c_void_p), P, I, P, P], I),
         "gg_hshard_create": ([I, P, P, I, I, PP], I),
+        "gg_hshard_create_ex": ([I, I, P, P, I, I, PP], I),
+        "gg_hshard_exchange_bytes": ([P, I, ctypes.POINTER(S)], I),
         "gg_hshard_release": ([P], I),
         "gg_hshard_info": ([P, ctypes.POINTER(S), ctypes.POINTER(S)], I),
         "gg_hshard_phase": ([P, I, P, P, P, S, I, P, P, P], I),
@@ -127,6 +132,8 @@ def _load():
         "gg_groth16_mpk_info": ([P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)], I),
         "gg_groth16_mpk_prove": ([P, P, S, P, P, P, S, P, P, P, P, P], I),
         "gg_groth16_mpk_last_timings": ([P, ctypes.POINTER(ctypes.c_double)], I),
+        "gg_groth16_mpk_shard_timings": ([P, I, ctypes.POINTER(ctypes.c_double), I], I),
+        "gg_groth16_mpk_set_rehearsal": ([P, I], I),
         "gg_batch_scalar_mul": ([I, P, P, S, I, P, I], I),
         "gg_plonk_numerator_coset": ([ctypes.POINTER(ctypes.c_void_p), I, P, ctypes.POINTER(I), P,
                                       P, P, P, P, S, I, I, P, P], I),
@@ -137,6 +144,8 @@ def _load():
         "gg_plonk_pk_create_multi": ([I, I, P, P, P, P, S, P, PP, PP, I, P, S, P, P, I,
                                       ctypes.POINTER(ctypes.c_int), PP], I),
         "gg_plonk_pk_devices": ([P, ctypes.POINTER(ctypes.c_int), I, ctypes.POINTER(ctypes.c_int)], I),
+        "gg_plonk_pk_set_rehearsal": ([P, I], I),
+        "gg_plonk_pk_part_timings": ([P, I, ctypes.POINTER(ctypes.c_double), I], I),
         "gg_plonk_pk_create_ex": ([I, I, I, P, P, P, P, S, P, PP, PP, I, P, S, P, P, I,
                                    ctypes.POINTER(ctypes.c_int), PP], I),
         "gg_plonk_pk_create_shard_ex": ([I, I, I, P, P, P, P, S, P, PP, PP, I, P, S, P, P, I, I, REDUCE_FN, P,
@@ -207,6 +216,8 @@ EXPORTED = [
     "gg_r1cs_solution_dev", "gg_scs_create", "gg_scs_release", "gg_scs_info", "gg_scs_solve",
     "gg_scs_solution_dev", "gg_r1cs_set_inputs", "gg_scs_set_inputs", "gg_r1cs_schedule", "gg_scs_schedule",
     "gg_msm_stripe", "gg_groth16_pk_create_stripe_ex", "gg_groth16_pk_stripe", "gg_groth16_mpk_split",
+    "gg_hshard_create_ex", "gg_hshard_exchange_bytes", "gg_groth16_mpk_shard_timings",
+    "gg_groth16_mpk_set_rehearsal", "gg_plonk_pk_set_rehearsal", "gg_plonk_pk_part_timings",
 ]
 
 

@@ -22,7 +22,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import backend, fr
-from ._lib import check, lib, ptr, GG_CURVE_BN254, GG_CURVE_BLS12_381
+from ._lib import check, lib, ptr, GG_CURVE_BN254, GG_CURVE_BLS12_381, GG_MPK_TIMING_SLOTS, GG_REHEARSAL
 
 # (G1 affine, G2 affine) bytes per curve
 _SIZES = {"bn254": (64, 128), "bls12-381": (96, 192)}
@@ -224,7 +224,29 @@ class MultiGpuProvingKey:
         check(lib.gg_groth16_mpk_devices(self.handle, arr, len(self.devices)))
         return list(arr)
 
-    def prove(self, solution, *opts, r: bytes = None, s: bytes = None) -> "Proof":
+    def set_rehearsal(self, solo_shard: int = -1):
+        """Timing rehearsal (gg_groth16_mpk_set_rehearsal): solo_shard >= 0 makes
+        later proves run that shard ALONE (the per-GPU work of an N-GPU node on
+        one GPU); those proofs are NOT valid and prove() refuses them unless
+        called with rehearsal_ok=True.  -1 restores real proofs."""
+        check(lib.gg_groth16_mpk_set_rehearsal(self.handle, int(solo_shard)))
+        self._solo = int(solo_shard)
+
+    def shard_timings(self) -> list:
+        """Per shard, the last proof: prove ms and, per exchange of the distributed
+        computeH, the wait at the first barrier, the peer-copy push time, the wait
+        at the second barrier and the MB pushed (gg_groth16_mpk_shard_timings)."""
+        out = []
+        for r in range(len(self.devices)):
+            v = (ctypes.c_double * GG_MPK_TIMING_SLOTS)()
+            check(lib.gg_groth16_mpk_shard_timings(self.handle, r, v, GG_MPK_TIMING_SLOTS))
+            nx = int(v[1])
+            ex = [{"wait_before_ms": v[2 + 4 * e], "push_ms": v[3 + 4 * e], "wait_after_ms": v[4 + 4 * e],
+                   "pushed_MB": v[5 + 4 * e]} for e in range(nx)]
+            out.append({"shard": r, "device": self.devices[r], "prove_ms": v[0], "exchanges": ex})
+        return out
+
+    def prove(self, solution, *opts, r: bytes = None, s: bytes = None, rehearsal_ok: bool = False) -> "Proof":
         """`solution`: a host Solution (every shard reads it), or a DeviceSolutions
         (one resident copy per device, see replicate_solution)."""
         cfg = backend.new_prover_config(*opts)
@@ -248,8 +270,10 @@ class MultiGpuProvingKey:
         def arr(field):
             return (ctypes.c_void_p * world)(*[ptr(getattr(x, field)).value for x in per])
         ar, bs, krs = bytearray(self.g1b), bytearray(self.g2b), bytearray(self.g1b)
-        check(lib.gg_groth16_mpk_prove_ex(self.handle, on_dev, arr("W"), n_wires, arr("A"), arr("B"), arr("C"),
-                                          n_cons, ptr(r), ptr(s), ptr(ar), ptr(bs), ptr(krs)))
+        rc = lib.gg_groth16_mpk_prove_ex(self.handle, on_dev, arr("W"), n_wires, arr("A"), arr("B"), arr("C"),
+                                         n_cons, ptr(r), ptr(s), ptr(ar), ptr(bs), ptr(krs))
+        if not (rc == GG_REHEARSAL and rehearsal_ok):
+            check(rc)
         return Proof(bytes(ar), bytes(bs), bytes(krs))
 
     def last_timings(self) -> dict:
@@ -601,15 +625,28 @@ class HShard:
     """This rank's part of the distributed computeH (gg_hshard_*): three
     all-to-alls per proof instead of h computed on every GPU."""
 
-    def __init__(self, log_n: int, rank: int, world: int, omega: bytes = None, gen: bytes = None):
-        omega = omega or fr.fr_mont(fr.domain_generator(log_n))
-        gen = gen or fr.fr_mont(fr.FR_MULTIPLICATIVE_GEN)
+    def __init__(self, log_n: int, rank: int, world: int, omega: bytes = None, gen: bytes = None,
+                 curve: str = "bn254"):
+        if curve == "bn254":
+            omega = omega or fr.fr_mont(fr.domain_generator(log_n))
+            gen = gen or fr.fr_mont(fr.FR_MULTIPLICATIVE_GEN)
+            cid = GG_CURVE_BN254
+        else:
+            omega = omega or fr.bls_fr_mont(fr.bls_domain_generator(log_n))
+            gen = gen or fr.bls_fr_mont(fr.BLS_FR_MULTIPLICATIVE_GEN)
+            cid = GG_CURVE_BLS12_381
         h = ctypes.c_void_p()
-        check(lib.gg_hshard_create(log_n, ptr(omega), ptr(gen), rank, world, ctypes.byref(h)))
+        check(lib.gg_hshard_create_ex(cid, log_n, ptr(omega), ptr(gen), rank, world, ctypes.byref(h)))
         self.handle, self.log_n, self.rank, self.world = h, log_n, rank, world
         m, xb = ctypes.c_size_t(), ctypes.c_size_t()
         check(lib.gg_hshard_info(h, ctypes.byref(m), ctypes.byref(xb)))
         self.m, self.exchange_bytes = m.value, xb.value
+
+    def exchange_bytes_after(self, phase: int) -> int:
+        """bytes per rank pair of the all-to-all after phase 1, 2 or 3"""
+        v = ctypes.c_size_t()
+        check(lib.gg_hshard_exchange_bytes(self.handle, phase, ctypes.byref(v)))
+        return v.value
 
     def phase(self, k: int, a=None, b=None, c=None, length: int = 0, on_device: bool = False,
               recv=None, out=None):

@@ -25,7 +25,7 @@ import secrets
 from typing import Callable, List, Optional, Sequence, Tuple
 
 from . import fr, ntt
-from ._lib import DeviceBuffer, check, lib, ptr, GG_CURVE_BLS12_381, HASH_FN, REDUCE_FN
+from ._lib import DeviceBuffer, check, lib, ptr, GG_CURVE_BLS12_381, GG_PLONK_PART_SLOTS, GG_REHEARSAL, HASH_FN, REDUCE_FN
 
 R = fr.BLS_R
 ORDER_BLINDING = (1, 1, 1, 2)  # order_blinding_L, _R, _O, _Z (prove.go:88-93)
@@ -234,6 +234,26 @@ class ProvingKey:
         check(lib.gg_plonk_pk_devices(self.handle, arr, k.value, ctypes.byref(k)))
         return list(arr)
 
+    def set_rehearsal(self, on: bool = True):
+        """Timing rehearsal (gg_plonk_pk_set_rehearsal): the peer parts of a
+        multi-part key do nothing in later proves (the primary part's work on
+        one GPU); those proofs are NOT valid and prove() refuses them unless
+        called with rehearsal_ok=True."""
+        check(lib.gg_plonk_pk_set_rehearsal(self.handle, int(bool(on))))
+
+    def part_timings(self) -> list:
+        """Per device part (0 = primary), the last proof: MSM slices and their ms,
+        scalar-slice copies (ms, MB), numerator cosets (ms, copies in / out, MB),
+        and part 0's wait for its peers (gg_plonk_pk_part_timings)."""
+        names = ["msm_slices", "msm_ms", "scalar_copy_ms", "scalar_MB", "cosets", "coset_ms",
+                 "coset_in_copy_ms", "coset_out_copy_ms", "coset_MB", "wait_for_peers_ms"]
+        out = []
+        for p in range(len(self.devices())):
+            v = (ctypes.c_double * GG_PLONK_PART_SLOTS)()
+            check(lib.gg_plonk_pk_part_timings(self.handle, p, v, GG_PLONK_PART_SLOTS))
+            out.append(dict(zip(names, list(v))))
+        return out
+
     def commit_lagrange(self, values) -> bytes:
         """kzg.Commit(values, pk.KzgLagrange) -- the commitment of bsb22Hint (prove.go:336)."""
         out = bytearray(self.field.pt)
@@ -255,7 +275,7 @@ class ProvingKey:
 
 def prove(pk: ProvingKey, L, R_, O, rng=None, timings: Optional[dict] = None, public: Sequence[int] = (),
           commitments: Sequence[Tuple[bytes, bytes, int]] = (), challenge_hash: Optional[Callable] = None,
-          folding_hash: Optional[Callable] = None) -> Proof:
+          folding_hash: Optional[Callable] = None, rehearsal_ok: bool = False) -> Proof:
     """Prove after Solve (prove.go:116-176).  L, R_, O: the solver's Lagrange-regular
     vectors (bytes or DeviceBuffers of n fr); public: fullWitness[:nb_public] (ints);
     commitments: per BSB22 commitment (committed values, Lagrange, n fr bytes;
@@ -277,9 +297,11 @@ def prove(pk: ProvingKey, L, R_, O, rng=None, timings: Optional[dict] = None, pu
     size = lib.gg_plonk_proof_size_ex(F.cid, pk.n_cmt)
     out = bytearray(size)
     hc, hf = _hash_cb(challenge_hash), _hash_cb(folding_hash)
-    check(lib.gg_plonk_prove(pk.handle, ptr(lro[0]), ptr(lro[1]), ptr(lro[2]), int(on_dev), ptr(pub) if pub else None,
-                             len(public), cva, ptr(dig) if dig else None, ptr(hashed) if hashed else None,
-                             pk.n_cmt, ptr(blind), hc, None, hf, None, ptr(out), size))
+    rc = lib.gg_plonk_prove(pk.handle, ptr(lro[0]), ptr(lro[1]), ptr(lro[2]), int(on_dev), ptr(pub) if pub else None,
+                            len(public), cva, ptr(dig) if dig else None, ptr(hashed) if hashed else None,
+                            pk.n_cmt, ptr(blind), hc, None, hf, None, ptr(out), size)
+    if not (rc == GG_REHEARSAL and rehearsal_ok):
+        check(rc)
     if timings is not None:
         ms = (ctypes.c_double * 8)()
         check(lib.gg_plonk_last_timings(ms, 8))

@@ -36,6 +36,10 @@ extern "C" {
 #define GG_ERR_UNSUPPORTED 4
 #define GG_ERR_INTERNAL 5
 #define GG_ERR_UNSATISFIED 6 /* R1CS solver: a constraint is not satisfied */
+/* a multi-GPU prove ran as a timing rehearsal (gg_groth16_mpk_set_rehearsal,
+ * gg_plonk_pk_set_rehearsal): the proof written is NOT valid.  Never GG_OK, so
+ * a caller checking for success cannot pass such a proof on. */
+#define GG_REHEARSAL 7
 
 #define GG_G1 1
 #define GG_G2 2
@@ -330,21 +334,34 @@ int gg_groth16_finalize_end(gg_g16_fixed_t h, const void *alpha1, const void *be
                             const void *beta2, const void *partials, void *ar_aff, void *bs_aff,
                             void *krs_aff);
 
-/* ---- distributed computeH ("four-step multi-GPU NTT").
+/* ---- distributed computeH ("four-step multi-GPU NTT";
+ * computeH of groth16/bn254/prove.go:353-396 and groth16/bls12-381/prove.go:353-396).
  * n = 2^log_n = m * world (world a power of two <= 16, n >= world^2).  Rank r
  * computes the local transforms of the cyclic slices x[r + world*j] and, after
  * three all-to-alls, holds h_bitrev[r*m, (r+1)*m): exactly the Z positions of
  * its key shard (gg_groth16_pk_create_shard with z_lo = r*m).
+ * gg_hshard_create = gg_hshard_create_ex(GG_CURVE_BN254, ...); _ex takes the
+ * curve whose fr the vectors hold (BN254 or BLS12-381).
  * gg_hshard_info: m and the size of the send / recv device buffers the caller
- * provides (bytes, all ranks' chunks).
+ * provides (bytes, all ranks' chunks: the largest exchange).
+ * gg_hshard_exchange_bytes: bytes per rank pair of the all-to-all that follows
+ * phase `phase` (1: a, b, c = 3 m/world^2 fr; 2: a, b = 2; 3: the product = 1).
  * gg_hshard_phase (the building blocks, synchronous on hip_stream):
  *   1: a, b, c (len <= n, full vectors, host or device per inputs_on_device)
  *      -> send;   2: recv -> send;   3: recv -> send;   4: recv -> h (m fr)
- * with an all-to-all send -> recv between consecutive phases. */
+ * with an all-to-all send -> recv between consecutive phases.  State carried
+ * between calls: phase 2 leaves den * c's coefficients in the handle and
+ * phase 4 subtracts them (h = den coset_iFFT(a b) - den c, by linearity), so
+ * the phases of one proof run in order on one handle, one proof at a time;
+ * a phase 4 with no phase 2 since the last phase 1 / phase 4 fails
+ * (GG_ERR_INVALID_ARG) instead of returning a wrong h. */
 int gg_hshard_create(int log_n, const void *omega_mont, const void *coset_gen_mont, int rank,
                      int world, gg_hshard_t *out);
+int gg_hshard_create_ex(int curve, int log_n, const void *omega_mont, const void *coset_gen_mont,
+                        int rank, int world, gg_hshard_t *out);
 int gg_hshard_release(gg_hshard_t hs);
 int gg_hshard_info(gg_hshard_t hs, size_t *m, size_t *exchange_bytes);
+int gg_hshard_exchange_bytes(gg_hshard_t hs, int phase, size_t *bytes_per_rank);
 int gg_hshard_phase(gg_hshard_t hs, int phase, const void *a, const void *b, const void *c,
                     size_t len, int inputs_on_device, const void *recv, void *send_or_h,
                     void *hip_stream);
@@ -367,8 +384,9 @@ int gg_groth16_prove_partial_dist(gg_groth16_pk_t pk, gg_hshard_t hs, const void
  * computeH are peer copies between the shards' device buffers (xGMI DMA), done
  * inside the library -- no transport from the caller.  world a power of two
  * <= 16 with n >= world^2 distributes computeH; otherwise every shard computes
- * h itself.  devices may repeat (several shards per GPU).  BN254; host inputs
- * (gg_groth16_mpk_prove_ex also takes per-device resident solutions).
+ * h itself.  devices may repeat (several shards per GPU).  BN254 (or either
+ * curve through _ex); host inputs (gg_groth16_mpk_prove_ex also takes
+ * per-device resident solutions).
  * replaces: the per-GPU setupDevicePointers + Prove of icicle.go:31-420 for a
  * node of GPUs driven from one Go process. */
 typedef struct gg_groth16_mpk *gg_groth16_mpk_t;
@@ -382,7 +400,7 @@ int gg_groth16_mpk_create(int log_n, const void *omega_mont, const void *coset_g
                           const int *devices, gg_groth16_mpk_t *out);
 /* the same for a chosen curve: GG_CURVE_BN254 (= gg_groth16_mpk_create) or
  * GG_CURVE_BLS12_381 (backend/groth16/bls12-381/prove.go:63-322; points in that
- * curve's layout; computeH replicated on every shard, MSMs sharded) */
+ * curve's layout; computeH distributed over the shards as for BN254) */
 int gg_groth16_mpk_create_ex(int curve, int log_n, const void *omega_mont, const void *coset_gen_mont,
                              const void *g1_A, size_t nA, const void *g1_B, size_t nB,
                              const void *g1_Z, size_t nZ, const void *g1_K, size_t nK,
@@ -420,6 +438,22 @@ int gg_groth16_mpk_prove_ex(gg_groth16_mpk_t mpk, int inputs_on_device, const vo
 /* ms of the last gg_groth16_mpk_prove: [0] shards (device work + exchanges),
  * [1] partial sum + finalize, [2] total */
 int gg_groth16_mpk_last_timings(gg_groth16_mpk_t mpk, double *ms3);
+/* where shard `shard`'s time went in the last proof (cap >= GG_MPK_TIMING_SLOTS):
+ * [0] the shard's prove ms (its thread: GPU work + exchanges), [1] exchanges
+ * recorded (3 with the distributed computeH), then per exchange e
+ * [2+4e] ms waiting at the first barrier (peers still computing),
+ * [3+4e] ms pushing its chunks to the peers (hipMemcpyPeerAsync over xGMI,
+ *        issue to completion), [4+4e] ms waiting at the second barrier (peers'
+ *        pushes into this shard still in flight), [5+4e] MB pushed to peers. */
+#define GG_MPK_MAX_EXCHANGES 4
+#define GG_MPK_TIMING_SLOTS (2 + 4 * GG_MPK_MAX_EXCHANGES)
+int gg_groth16_mpk_shard_timings(gg_groth16_mpk_t mpk, int shard, double *out, int cap);
+/* Timing rehearsal (bench / tests only): solo_shard >= 0 makes every later
+ * prove run shard solo_shard ALONE (its exchanges skip the peers, the other
+ * shards contribute identity partials), so one GPU times the work one GPU of
+ * an N-GPU node does; such proves write an INVALID proof and return
+ * GG_REHEARSAL.  -1 (the default) restores real proofs. */
+int gg_groth16_mpk_set_rehearsal(gg_groth16_mpk_t mpk, int solo_shard);
 
 /* per-stage timings (ms) of the last gg_groth16_prove on this thread:
  * [0]=upload [1]=computeH [2]=msm_A [3]=msm_B1 [4]=msm_K [5]=msm_Z [6]=msm_G2
@@ -575,6 +609,20 @@ int gg_plonk_pk_create_shard_ex(int curve, int log_n, int log_big, const void *o
 int gg_plonk_pk_info(gg_plonk_pk_t pk, int *curve, int *log_n, int *n_cmt);
 /* the key's device parts: *n_devices, devices[0..) (primary first; devices nullable) */
 int gg_plonk_pk_devices(gg_plonk_pk_t pk, int *devices, int cap, int *n_devices);
+/* Timing rehearsal (bench / tests only): on != 0 makes the peer parts of a
+ * multi-part key do nothing in later proves (no MSM slices, no cosets), so one
+ * GPU times the primary part's work; such proves write an INVALID proof and
+ * return GG_REHEARSAL.  0 (the default) restores real proofs. */
+int gg_plonk_pk_set_rehearsal(gg_plonk_pk_t pk, int on);
+/* where device part `part` (0 = primary) spent the last proof (cap >=
+ * GG_PLONK_PART_SLOTS): [0] MSM slices, [1] their ms (incl. the scalar copy),
+ * [2] ms copying scalar slices from the primary (xGMI), [3] MB copied, [4]
+ * numerator cosets, [5] their ms (copies + FFTs + numerator), [6] ms copying
+ * the per-proof polynomials in, [7] ms copying the coset blocks back, [8] MB
+ * moved for the cosets, [9] part 0 only: ms waiting for the peers' MSM slices
+ * and cosets after finishing its own work. */
+#define GG_PLONK_PART_SLOTS 10
+int gg_plonk_pk_part_timings(gg_plonk_pk_t pk, int part, double *out, int cap);
 /* the key's vk digests, 96-B affine each: S[0..2], Ql, Qr, Qm, Qo, Qk, Qcp[0..n_cmt) */
 int gg_plonk_pk_vk(gg_plonk_pk_t pk, void *out, size_t cap);
 /* kzg.Commit(values, pk.KzgLagrange): n Lagrange values (host or device) -> affine 96 B.

@@ -153,7 +153,7 @@ def test_groth16_bls12_381_bit_exact(log_n):
     # on device 0 rehearse the N-GPU layout; host, replicated and GPU-solved inputs
     world = {6: 2, 12: 3, 16: 8}[log_n]
     mpk = groth16.MultiGpuProvingKey(data, [0] * world)
-    assert mpk.info() == (world, False)  # BLS12-381: computeH replicated per shard
+    assert mpk.info() == (world, world & (world - 1) == 0)  # distributed computeH (power-of-two worlds)
     prm = mpk.prove(sol, opt, r=frb(r), s=frb(s))
     assert (prm.Ar, prm.Bs, prm.Krs) == (pr.Ar, pr.Bs, pr.Krs)
     prd = mpk.prove(groth16.replicate_solution(sol, [0] * world), opt, r=frb(r), s=frb(s))

@@ -20,9 +20,9 @@ def _exchange_host(sends, world, B):
     return [b"".join(sends[k][r * B:(r + 1) * B] for k in range(world)) for r in range(world)]
 
 
-def dist_h_blocks(a, bb, c, fill, log_n, world, on_device=False):
+def dist_h_blocks(a, bb, c, fill, log_n, world, on_device=False, curve="bn254"):
     from gnark_amd import groth16, DeviceBuffer
-    hs = [groth16.HShard(log_n, r, world) for r in range(world)]
+    hs = [groth16.HShard(log_n, r, world, curve=curve) for r in range(world)]
     xb = hs[0].exchange_bytes
     inputs = (a, bb, c)
     if on_device:
@@ -32,14 +32,17 @@ def dist_h_blocks(a, bb, c, fill, log_n, world, on_device=False):
         s = DeviceBuffer(xb)
         hs[r].phase(1, *inputs, length=fill, on_device=on_device, out=s)
         sends.append(s.to_host())
+    # per rank pair: 3 chunks (a, b, c) after phase 1, 2 (a, b) after phase 2
+    assert hs[0].exchange_bytes_after(1) == xb // world
     for ph in (2, 3):
-        recvs = _exchange_host(sends, world, xb // world)
+        recvs = _exchange_host(sends, world, hs[0].exchange_bytes_after(ph - 1))
         sends = []
         for r in range(world):
             rb, s = DeviceBuffer.from_host(recvs[r]), DeviceBuffer(xb)
             hs[r].phase(ph, recv=rb, out=s)
             sends.append(s.to_host())
-    recvs = _exchange_host(sends, world, hs[0].m // world * 32)  # h: one polynomial
+    assert hs[0].exchange_bytes_after(3) == hs[0].m // world * 32  # h: one polynomial
+    recvs = _exchange_host(sends, world, hs[0].exchange_bytes_after(3))
     blocks = []
     for r in range(world):
         h = DeviceBuffer(hs[r].m * 32)
@@ -65,6 +68,77 @@ def test_dist_h_golden():
         fill = len(b(g["solA"])) // 32
         blocks = dist_h_blocks(b(g["solA"]), b(g["solB"]), b(g["solC"]), fill, g["log_n"], 2)
         assert b"".join(blocks).hex() == g["h"]
+
+
+BLS_R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+def _bls_vec(k, seed):
+    from gnark_amd import fr
+    rng = np.random.default_rng(seed)
+    v = [int.from_bytes(rng.bytes(32), "little") % BLS_R for _ in range(k)]
+    return v, b"".join(fr.bls_fr_mont(x) for x in v)
+
+
+@pytest.mark.parametrize("log_n,world,fill", [(4, 2, 13), (6, 8, 61), (10, 4, 1000), (16, 8, 65000),
+                                              (18, 2, 262000)])
+def test_dist_h_bls12_381(log_n, world, fill):
+    """The four-step computeH over BLS12-381 fr (groth16/bls12-381/prove.go:353-396):
+    the blocks equal the one-GPU computeH of the same domain (whose proofs are
+    bit-exact vs the oracle, test_gpu_bls_groth16.py); at small sizes h also
+    satisfies h(z) (z^n - 1) = A(z) B(z) - C(z) at a random z (pure Python)."""
+    from gnark_amd import fr, ntt, DeviceBuffer
+    n = 1 << log_n
+    vs = [_bls_vec(fill, 900 + log_n + i) for i in range(3)]
+    blocks = dist_h_blocks(*(x[1] for x in vs), fill, log_n, world, on_device=(world == 8), curve="bls12-381")
+    assert all(len(x) == n // world * 32 for x in blocks)
+    dom = ntt.Domain(log_n, fr.bls_fr_mont(fr.bls_domain_generator(log_n)),
+                     fr.bls_fr_mont(fr.BLS_FR_MULTIPLICATIVE_GEN), curve=ntt.GG_CURVE_BLS12_381)
+    h = DeviceBuffer(32 * n)
+    dom.compute_h(*(x[1] for x in vs), fill, h)
+    assert b"".join(blocks) == h.to_host()
+    dom.close()
+    if log_n <= 10:
+        hb = b"".join(blocks)
+        brev = [int(format(i, f"0{log_n}b")[::-1], 2) for i in range(n)]
+        coef = [fr.bls_fr_unmont(hb[32 * brev[i]:32 * brev[i] + 32]) for i in range(n)]
+        z = 0x5EED1234 + log_n
+        w = fr.bls_domain_generator(log_n)
+        zn1 = (pow(z, n, BLS_R) - 1) % BLS_R
+        ninv = pow(n, BLS_R - 2, BLS_R)
+
+        def lag(vals):  # sum_j v_j L_j(z), L_j(z) = w^j (z^n - 1) / (n (z - w^j))
+            acc, wj = 0, 1
+            for v in vals:
+                acc += v * wj * pow(z - wj, BLS_R - 2, BLS_R)
+                wj = wj * w % BLS_R
+            return acc * zn1 * ninv % BLS_R
+        hz = 0
+        for cf in reversed(coef):
+            hz = (hz * z + cf) % BLS_R
+        ea, eb, ec = (lag(x[0]) for x in vs)
+        assert hz * zn1 % BLS_R == (ea * eb - ec) % BLS_R
+
+
+def test_dist_h_phase_order():
+    """Phase 4 subtracts the c coefficients phase 2 leaves in the handle: a
+    phase 4 with no phase 2 before it is refused, not answered with a wrong h."""
+    from gnark_amd import groth16, DeviceBuffer, GnarkAmdError
+    hs = groth16.HShard(8, 0, 2)
+    xb = hs.exchange_bytes
+    recv, h = DeviceBuffer.from_host(bytes(xb)), DeviceBuffer(hs.m * 32)
+    with pytest.raises(GnarkAmdError):
+        hs.phase(4, recv=recv, out=h)
+    a = random_fr_mont(200, 5).tobytes()
+    s = DeviceBuffer(xb)
+    hs.phase(1, a, a, a, length=200, out=s)
+    with pytest.raises(GnarkAmdError):  # phase 1 then 4: c's coefficients were never formed
+        hs.phase(4, recv=recv, out=h)
+    hs.phase(2, recv=recv, out=s)
+    hs.phase(4, recv=recv, out=h)  # in order: accepted
+    with pytest.raises(GnarkAmdError):  # consumed
+        hs.phase(4, recv=recv, out=h)
+    hs.close()
 
 
 def test_dist_h_rejects_bad_world():

@@ -98,11 +98,15 @@ def test_mpk_errors():
     mpk.close()
 
 
-def test_mpk_solo_timing_mode(monkeypatch):
-    """GG_MPK_SOLO=r (bench.py's split_projection): shard r proves alone -- it
-    runs with the exchanges skipping the peers, its proof is not the real one,
-    and the next proof on the same key without it is bit-exact again."""
-    from gnark_amd import backend, groth16
+def test_mpk_rehearsal_mode():
+    """gg_groth16_mpk_set_rehearsal(r) (bench.py's split_projection): shard r
+    proves alone -- the library returns GG_REHEARSAL (never GG_OK), prove()
+    refuses that proof unless asked for a rehearsal, the proof is not the real
+    one, and after set_rehearsal(-1) the same key is bit-exact again.  The
+    per-shard timings report one prove time per shard and the three exchanges
+    of the distributed computeH."""
+    from gnark_amd import backend, groth16, GnarkAmdError
+    from gnark_amd._lib import GG_REHEARSAL
     from test_gpu_groth16 import synthetic_case
     d, wires, sa, sb, sc, ncons, r, s = synthetic_case(12, 3000, 3, 77, k_inf_every=5)
     data = groth16.ProvingKeyData(**d)
@@ -110,9 +114,24 @@ def test_mpk_solo_timing_mode(monkeypatch):
     mpk = groth16.MultiGpuProvingKey(data, [0] * 4)
     opt = backend.with_amd_acceleration()
     ref = mpk.prove(sol, opt, r=r, s=s)
-    monkeypatch.setenv("GG_MPK_SOLO", "1")
-    solo = mpk.prove(sol, opt, r=r, s=s)
+    st = mpk.shard_timings()
+    assert len(st) == 4
+    for t in st:
+        assert t["prove_ms"] > 0 and len(t["exchanges"]) == 3
+        # pushes to the 3 peers: phase 1 sends 3 chunks, phase 2 two, phase 3 one
+        mb = [e["pushed_MB"] for e in t["exchanges"]]
+        assert mb[0] > mb[1] > mb[2] > 0 and abs(mb[0] - 3 * mb[2]) < 1e-9
+    mpk.set_rehearsal(1)
+    with pytest.raises(GnarkAmdError) as ei:
+        mpk.prove(sol, opt, r=r, s=s)
+    assert ei.value.code == GG_REHEARSAL
+    solo = mpk.prove(sol, opt, r=r, s=s, rehearsal_ok=True)
     assert solo != ref
-    monkeypatch.delenv("GG_MPK_SOLO")
+    st = mpk.shard_timings()
+    assert st[1]["prove_ms"] > 0 and st[0]["prove_ms"] == 0
+    assert all(e["pushed_MB"] == 0 for e in st[1]["exchanges"])
+    mpk.set_rehearsal(-1)
     assert mpk.prove(sol, opt, r=r, s=s) == ref
+    with pytest.raises(GnarkAmdError):
+        mpk.set_rehearsal(4)  # out of range
     mpk.close()

@@ -104,16 +104,20 @@ def test_groth16_mimc_bit_exact(log_n):
                         opt, r=_fr(R_), s=_fr(S_))
     assert pr3.Krs != want[2]
     pk.close()
-    if log_n == 24:  # the 8-GPU split of configs[3], rehearsed with 8 shards on this GPU
-        _mpk_check(data, sol, sol_d, want, 8, t0)
+    if log_n == 24:  # the 8-GPU split of configs[3], rehearsed with 8 shards on this GPU:
+        # wire slices (the product default: gg_groth16_mpk_create_ex, the Go shims'
+        # SetDevices, bench's split_projection), then the opt-in bucket stripes
+        _mpk_check(data, sol, sol_d, want, 8, t0, split="wires")
+        _mpk_check(data, sol, sol_d, want, 8, t0, split="stripes")
     cr.close()
 
 
-def _mpk_check(data, sol, sol_d, want, world, t0, split="stripes"):
+def _mpk_check(data, sol, sol_d, want, world, t0, split="wires"):
     """gg_groth16_mpk_* with `world` key shards (8 = BASELINE configs[3]'s node):
-    bucket stripes over whole per-device wire tables (or wire slices) and Z
-    slices, the four-step distributed computeH with its three all-to-alls as
-    peer copies, partials summed exactly -- same proof bytes."""
+    wire slices (the default) or bucket stripes over whole per-device wire
+    tables, and Z slices, the four-step distributed computeH with its three
+    all-to-alls as peer copies, partials summed exactly -- same proof bytes,
+    from host and from device-resident solutions."""
     import os
     from gnark_amd import backend, groth16
     opt = backend.with_amd_acceleration()
@@ -127,7 +131,11 @@ def _mpk_check(data, sol, sol_d, want, world, t0, split="stripes"):
         else:
             os.environ["GG_MPK_SPLIT"] = old
     assert mpk.info() == (world, True) and mpk.split() == split
-    _log(f"{world}-shard key", t0)
+    if split == "wires":  # a 2^21-wire slice of the 2^24 key picks its own (smaller) window
+        _log(f"{world}-shard key (shard 0 A: c={mpk.base_info(groth16.BASE_A)[1]}, "
+             f"W={mpk.base_info(groth16.BASE_A)[2]})", t0)
+    else:
+        _log(f"{world}-shard key", t0)
     pr = mpk.prove(sol, opt, r=_fr(R_), s=_fr(S_))
     _log(f"{world}-shard prove (host inputs) {mpk.last_timings()['total']:.1f} ms", t0)
     assert (pr.Ar, pr.Bs, pr.Krs) == want

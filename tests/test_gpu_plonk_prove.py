@@ -298,21 +298,33 @@ def test_plonk_prove_2p22_verifies():
     pk8.close()
 
 
-def test_plonk_solo_timing_mode(monkeypatch):
-    """GG_PLONK_SOLO=1 (bench.py's split_projection): the primary part of a
-    multi-part key proves with its peers idle -- it runs, its proof is not the
-    real one (the peers' MSM slices and cosets are missing), and unsetting it
-    gives the real proof again on the same key."""
-    from gnark_amd import plonk_prover as pp
+def test_plonk_rehearsal_mode():
+    """gg_plonk_pk_set_rehearsal (bench.py's split_projection): the primary part
+    of a multi-part key proves with its peers idle -- the library returns
+    GG_REHEARSAL, prove() refuses the proof unless asked for a rehearsal, the
+    proof is not the real one (the peers' MSM slices and cosets are missing),
+    and switching it off gives the real proof again on the same key.  Part
+    timings: every part ran MSM slices, the coset owners their cosets."""
+    from gnark_amd import plonk_prover as pp, GnarkAmdError
+    from gnark_amd._lib import GG_REHEARSAL
     log_n, parts = 7, 4
     circ = Circuit(log_n, 45, nb_public=1, n_cmt=0)
     tau = random.Random(99).randrange(2, R)
     pkm = make_key(circ, tau, devices=[0] * parts)
     L, Rv, O, pub, cmts = circ.solve(pkm, 6, commit=pkm.commit_lagrange)
     ref = pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts)
-    monkeypatch.setenv("GG_PLONK_SOLO", "1")
-    solo = pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts)
+    pt = pkm.part_timings()
+    assert len(pt) == parts
+    assert all(p["msm_slices"] == 10 and p["msm_ms"] > 0 for p in pt)  # the ten KZG commitments
+    assert all(p["scalar_MB"] > 0 for p in pt[1:])
+    assert sum(p["cosets"] for p in pt[1:]) == 3  # rho = 4: one coset on each peer (part 0 keeps one)
+    pkm.set_rehearsal(True)
+    with pytest.raises(GnarkAmdError) as ei:
+        pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts)
+    assert ei.value.code == GG_REHEARSAL
+    solo = pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts, rehearsal_ok=True)
     assert solo != ref
-    monkeypatch.delenv("GG_PLONK_SOLO")
+    assert all(p["msm_slices"] == 0 and p["cosets"] == 0 for p in pkm.part_timings()[1:])
+    pkm.set_rehearsal(False)
     assert pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts) == ref
     pkm.close()

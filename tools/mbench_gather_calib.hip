@@ -2,8 +2,10 @@
 // (MI355X_MICROARCH.md "HBM": "Other access widths are uncalibrated: calibrate
 // on a known byte count in your own access pattern").
 //
-// One dispatch per pattern, each over a 4 GB table (>> the 256 MiB Infinity
-// Cache), every byte read exactly once:
+// One dispatch per pattern, each over a table of argv[1] GiB (default 4; >> the
+// 256 MiB Infinity Cache; 16 covers the 12.9-GB G1 tables of the 2^24 key, where
+// address translation of random gathers costs extra fetches), every byte read
+// exactly once:
 //   k_stream16   : 16 B per lane, coalesced (the guide's calibrated case: raw = 1/2)
 //   k_gather<64> : 64-B points gathered through a shuffled permutation (G1 BN254)
 //   k_gather<128>: 128-B points, same (G2 BN254 / the G2 accumulation)
@@ -15,6 +17,7 @@
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <numeric>
 #include <random>
 #include <vector>
@@ -64,8 +67,10 @@ static void gather(const void* tab, size_t table, uint32_t* idx, uint32_t* out, 
            n * BYTES + n * 4, ms);
 }
 
-int main() {
-    const size_t table = (size_t)4 << 30;
+int main(int argc, char** argv) {
+    const size_t gib = argc > 1 ? (size_t)atoi(argv[1]) : 4;
+    const size_t table = gib << 30;
+    printf("{\"table_bytes\": %zu}\n", table);
     void* tab;
     uint32_t *idx, *out;
     const int grid = 256 * 8 * 4;

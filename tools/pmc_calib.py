@@ -9,11 +9,14 @@ import sys
 
 
 def main(db, log, out):
-    known = {}
+    known, table = {}, None
     for line in open(log):
         line = line.strip()
         if line.startswith("{"):
             d = json.loads(line)
+            if "table_bytes" in d:
+                table = d["table_bytes"]
+                continue
             known[d["kernel"]] = d["known_bytes"]
     con = sqlite3.connect(db)
     rows = con.execute("select kernel_name, dispatch_id, sum(value) from counters_collection "
@@ -24,7 +27,7 @@ def main(db, log, out):
             if name.startswith(k.replace("k_gather<", "void k_gather<")) or name.split("(")[0].endswith(k):
                 fetch[k] = v * 1024.0
     widths = {"k_stream16": 16, "k_gather<64>": 64, "k_gather<96>": 96, "k_gather<128>": 128}
-    res = {"source": [db, log], "known_bytes": known, "fetch_bytes_raw": fetch,
+    res = {"source": [db, log], "table_bytes": table, "known_bytes": known, "fetch_bytes_raw": fetch,
            "factor": {str(widths[k]): known[k] / fetch[k] for k in known if k in fetch and fetch[k] > 0},
            "note": "factor = known bytes read once (table >> the 256 MiB Infinity Cache) / FETCH_SIZE bytes; "
                    "gathers include the coalesced 4-B permutation reads"}

@@ -7,9 +7,13 @@ usage: pmc_traffic.py fetch.db write.db out.json [workload-json]
 (workload-json: e.g. '{"workload": "groth16", "log_n": 24, "n_gpus": 1}', the key
 bench.py matches a profile on)"""
 import json
+import os
 import sqlite3
 import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import csrc_digest  # noqa: E402  (the kernel tree this profile measured)
 
 
 def per_kernel(db, counter):
@@ -35,7 +39,7 @@ def main(fdb, wdb, out, workload=None):
                   "fetch_bytes_raw": fetch_b, "fetch_bytes_x2": 2.0 * fetch_b,
                   "write_bytes": write_b, "traffic_bytes": 2.0 * fetch_b + write_b,
                   "traffic_bytes_raw": fetch_b + write_b}
-    json.dump({"source": [fdb, wdb], "unit": "bytes per dispatch",
+    json.dump({"source": [fdb, wdb], "unit": "bytes per dispatch", "csrc_sha16": csrc_digest(),
                "workload": json.loads(workload) if workload else {},
                "correction": "FETCH_SIZE KiB x 1024 x 2 (gfx950 wide-read undercount, measured for 16-B/lane "
                              "coalesced streams), WRITE_SIZE KiB x 1024; traffic_bytes_raw: no x2 (the "
