@@ -440,12 +440,15 @@ static hipStream_t pick_stream(void* s) { return s ? (hipStream_t)s : hipStreamP
 // epilogue of the last pass: EPI_MUL_SUB out = ea*eb - x, EPI_MUL out = ea*x,
 // EPI_SUB out = x - ea (none when ea is null)
 enum { EPI_MUL_SUB = 0, EPI_MUL = 1, EPI_SUB = 2 };
+// passes: nullptr = the whole transform (plan_passes); else only these (e.g. the
+// last stages of a DIT whose first stages ran elsewhere, ntt_tail_inverse_coset)
 template <class C>
 void run_transform(DomainT<C>* d, const Fe<C>* in, Fe<C>* out, bool dit, bool inverse_tw, int pre_kind,
-                   int post_kind, const Fe<C>* ea, const Fe<C>* eb, hipStream_t st, int epi = EPI_MUL_SUB) {
+                   int post_kind, const Fe<C>* ea, const Fe<C>* eb, hipStream_t st, int epi = EPI_MUL_SUB,
+                   const std::vector<Pass>* only = nullptr) {
     using F = Fe<C>;
     const int L = d->log_n;
-    auto passes = plan_passes(L, dit);
+    auto passes = only ? *only : plan_passes(L, dit);
     const F* src = in;
     for (size_t pi = 0; pi < passes.size(); pi++) {
         const Pass& ps = passes[pi];
@@ -692,6 +695,32 @@ size_t domain_size(gg_domain* d, int* curve) {
 void any_ntt_inplace(gg_domain* d, void* data, int inverse, int dit, int coset, hipStream_t st) {
     if (d->curve == GG_CURVE_BN254) ntt_apply(d->bn.get(), data, inverse, dit != 0, coset, st);
     else ntt_apply(d->bls.get(), data, inverse, dit != 0, coset, st);
+}
+// The distributed big-domain inverse of the PlonK quotient (plonk_prover.hip):
+// a DIT with bit-reversed input runs its first L - u stages inside contiguous
+// blocks of 2^(L - u) elements -- each block's size-2^(L - u) inverse DFT (root
+// w^(2^u), the same stage twiddles), computed by the block's owner without any
+// scaling (ntt_inverse_dit_noscale) -- and its last u stages across the blocks,
+// with the coset inverse's g^-i / n on the natural-order output
+// (ntt_tail_inverse_coset).  Together: FFTInverse(DIT, OnCoset).
+void ntt_inverse_dit_noscale(gg_domain* d, void* data, hipStream_t st) {
+    if (d->curve == GG_CURVE_BN254)
+        run_transform(d->bn.get(), (const Fr*)data, (Fr*)data, true, true, -1, -1, (const Fr*)nullptr,
+                      (const Fr*)nullptr, st);
+    else
+        run_transform(d->bls.get(), (const FrBls*)data, (FrBls*)data, true, true, -1, -1, (const FrBls*)nullptr,
+                      (const FrBls*)nullptr, st);
+}
+void ntt_tail_inverse_coset(gg_domain* d, void* data, int u, hipStream_t st) {
+    const int L = d->log_n;
+    GG_CHECK(u >= 1 && u <= 4 && L >= 12, GG_ERR_INTERNAL, "tail transform: 1..4 stages of a >= 2^12 domain");
+    const std::vector<Pass> tail = {{L - u, u, 11 - u}};
+    if (d->curve == GG_CURVE_BN254)
+        run_transform(d->bn.get(), (const Fr*)data, (Fr*)data, true, true, -1, SK_GINV_NAT_N, (const Fr*)nullptr,
+                      (const Fr*)nullptr, st, EPI_MUL_SUB, &tail);
+    else
+        run_transform(d->bls.get(), (const FrBls*)data, (FrBls*)data, true, true, -1, SK_GINV_NAT_N,
+                      (const FrBls*)nullptr, (const FrBls*)nullptr, st, EPI_MUL_SUB, &tail);
 }
 // evaluateXnMinusOneDomainBigCoset (backend/plonk/<curve>/prove.go:1253-1276):
 // res[0] = g^n, res[i] = res[i-1] * w_big^n, res[i] -= 1, then fr.BatchInvert

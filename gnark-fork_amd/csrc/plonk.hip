@@ -56,11 +56,12 @@ __device__ __forceinline__ F numerator_at(const NumParamsT<F>& P, uint32_t j) {
     const F one = F::one();
     F L = ldf(P.x[ID_L] + j), R = ldf(P.x[ID_R] + j), O = ldf(P.x[ID_O] + j);
     F Z = ldf(P.x[ID_Z] + j);
-    F ZS = P.x[ID_ZS] ? ldf(P.x[ID_ZS] + j) : ldf(P.x[ID_Z] + (j + 1 == P.n ? 0 : j + 1));
+    const uint32_t j1 = j + 1 == P.n ? 0 : j + 1;
+    F ZS = P.x[ID_ZS] ? ldf(P.x[ID_ZS] + (P.zs_shift ? j1 : j)) : ldf(P.x[ID_Z] + j1);
     F S1 = ldf(P.x[ID_S1] + j) * P.beta, S2 = ldf(P.x[ID_S2] + j) * P.beta,
         S3 = ldf(P.x[ID_S3] + j) * P.beta;
     // blinding: bl/br/bo/bz evaluated at twiddles0[j], bz at twiddles0[(j+1) % n] for ZS
-    const F t0 = ldf(P.tw0 + j), t1 = ldf(P.tw0 + (j + 1) % P.n);
+    const F t0 = ldf(P.tw0 + j), t1 = P.tw1 ? ldf(P.tw1 + j) : ldf(P.tw0 + j1);
     L = L + horner_d(P.bcoef[0], P.bdeg[0], t0);
     R = R + horner_d(P.bcoef[1], P.bdeg[1], t0);
     O = O + horner_d(P.bcoef[2], P.bdeg[2], t0);
@@ -81,7 +82,8 @@ __device__ __forceinline__ F numerator_at(const NumParamsT<F>& P, uint32_t j) {
     F l = a * b * c * ZS - r;
     // ratioLocalConstraint
     F rl = (Z - one) * ldf(P.x[ID_LONE] + j);
-    return (rl * P.alpha + l) * P.alpha + ic;
+    const F res = (rl * P.alpha + l) * P.alpha + ic;
+    return P.has_out_scale ? res * P.out_scale : res;
 }
 
 // small domains: one point per thread, cres[bitrev(rho*j + coset)] (prove.go:1036-1038)
@@ -173,6 +175,42 @@ void batch_invert(F* a, size_t n, hipStream_t st, Arena& ar) {
 }
 
 template <class F>
+__global__ void __launch_bounds__(256) k_fold_brev(const F* in, size_t m, int S, int logS, F kappa, F* out) {
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= m) return;
+    // coefficient m' + t m (m' = bitrev_m(k)) sits at S k + bitrev_S(t) of the bit-reversed input
+    F acc = F::zero();
+    for (int t = S - 1; t >= 0; t--) {
+        const uint32_t bt = logS ? (__brev((uint32_t)t) >> (32 - logS)) : 0u;
+        acc = acc * kappa + ldf(in + (size_t)S * k + bt);
+    }
+    stf(out + k, acc);
+}
+
+template <class F>
+void fold_brev(const F* in, size_t n, int S, const F& kappa, F* out, hipStream_t st) {
+    int logS = 0;
+    while ((1 << logS) < S) logS++;
+    GG_CHECK((1 << logS) == S && n % S == 0, GG_ERR_INTERNAL, "fold: S must be a power of two dividing n");
+    const size_t m = n / S;
+    hipLaunchKernelGGL(k_fold_brev<F>, dim3(grid_for(m, 256)), dim3(256), 0, st, in, m, S, logS, kappa, out);
+    GG_HIP(hipGetLastError());
+}
+
+template <class F>
+__global__ void k_gather_strided(const F* in, size_t n, int S, int s, F* out) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n / S) return;
+    stf(out + j, ldf(in + ((size_t)s + (size_t)S * j) % n));
+}
+
+template <class F>
+void gather_strided(const F* in, size_t n, int S, int s, F* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_gather_strided<F>, dim3(grid_for(n / S, 256)), dim3(256), 0, st, in, n, S, s, out);
+    GG_HIP(hipGetLastError());
+}
+
+template <class F>
 void numerator(const NumParamsT<F>& P, hipStream_t st) {
     ProfScope prof("plonk_numerator", st, (double)P.n);
     uint32_t log_n = 0;
@@ -212,7 +250,9 @@ void ntt(gg_domain* d, void* data, int inverse, int dit, int coset, hipStream_t 
 #define GG_PLK_INST(F)                                                                                         \
     template void batch_invert<F>(F*, size_t, hipStream_t, Arena&);                                            \
     template void numerator<F>(const NumParamsT<F>&, hipStream_t);                                             \
-    template void divide_by_xn_minus_one<F>(gg_domain*, size_t, F*, hipStream_t);
+    template void divide_by_xn_minus_one<F>(gg_domain*, size_t, F*, hipStream_t);                             \
+    template void fold_brev<F>(const F*, size_t, int, const F&, F*, hipStream_t);                              \
+    template void gather_strided<F>(const F*, size_t, int, int, F*, hipStream_t);
 GG_PLK_INST(FrBls)
 GG_PLK_INST(Fr)
 #undef GG_PLK_INST

@@ -41,6 +41,21 @@ void ratio(const F* l, const F* r, const F* o, const int64_t* perm, size_t n, co
 size_t batch_invert_arena_bytes(size_t n);
 template <class F>
 void batch_invert(F* a, size_t n, hipStream_t st, Arena& ar);
+// Batched Polynomial.Evaluate at one point (prove.go:640-660, 763-775, 800-810:
+// every evaluation of a proof at zeta without a quotient): out_dev[k] =
+// sum_i f_k[i] a^i for k < count (<= EVAL_MAX).  One pass over the
+// polynomials (coalesced, one product per coefficient: Horner over a
+// grid-strided slice with multiplier a^G, scaled by a^g), block sums, then one
+// small kernel for the totals -- no scan, no host round trip per polynomial.
+constexpr int EVAL_MAX = 16;
+size_t eval_many_arena_bytes(size_t max_len, int count);
+template <class F>
+void eval_many(const F* const* f, const size_t* len, int count, const F& a, F* out_dev, hipStream_t st,
+               Arena& ar);
+// out[j] = sum_k c_k f_k[j] for j < n_out (f_k zero past lens[k]), count <= EVAL_MAX:
+// kzg.BatchOpenSinglePoint's folded polynomial (prove.go:823-830) in one pass
+template <class F>
+void lincomb(F* out, size_t n_out, const F* const* f, const size_t* len, const F* c, int count, hipStream_t st);
 template <class F>
 void fold_h(const F* h, size_t n_small, const F& z, F* out, hipStream_t st);
 template <class F>
@@ -85,7 +100,14 @@ struct NumParamsT {
     // local_block = 1: cres is only this coset's block of n (the slots
     // [brev(coset) n, (brev(coset) + 1) n) of the big vector), e.g. on another GPU
     uint32_t local_block;
-    // x[ID_ZS] == nullptr: ZS[j] = Z[(j + 1) % n] read from x[ID_Z] (no shifted copy)
+    // x[ID_ZS] == nullptr: ZS[j] = Z[(j + 1) % n] read from x[ID_Z] (no shifted copy);
+    // else ZS[j] = x[ID_ZS][(j + zs_shift) % n]
+    uint32_t zs_shift;
+    // blinding of ZS at tw1[j] (nullptr: tw0[(j + 1) % n])
+    const F* tw1;
+    // has_out_scale: every result times out_scale (the quotient unit's 1 / (x^n - 1))
+    uint32_t has_out_scale;
+    F out_scale;
 };
 using NumParams = NumParamsT<FrB>;
 template <class F>
@@ -93,9 +115,24 @@ void numerator(const NumParamsT<F>& P, hipStream_t st);
 // divideByXMinusOne in place (prove.go:1223-1276), asynchronous; big: a domain of F's curve
 template <class F>
 void divide_by_xn_minus_one(gg_domain* big, size_t n_small, F* data, hipStream_t st);
+// out (bit-reversed, m = n / S) = the fold sum_t kappa^t f[m' + t m] of a
+// bit-reversed polynomial of n coefficients: the coefficients whose size-m
+// coset FFT with shift s (kappa = s^m) gives f on s <w^S> (a quotient unit's
+// class of the big domain, prove.go:995-1017 split over the GPUs)
+template <class F>
+void fold_brev(const F* in, size_t n, int S, const F& kappa, F* out, hipStream_t st);
+// out[j] = in[(s + S j) % n] for j < n / S (the unit's points' twiddles0)
+template <class F>
+void gather_strided(const F* in, size_t n, int S, int s, F* out, hipStream_t st);
 
 // ---- ntt.hip (the domain's scalar field)
 void ntt(gg_domain* d, void* data, int inverse, int dit, int coset, hipStream_t st);
+
+}  // namespace plk
+// the distributed coset iFFT of the quotient (ntt.hip): per block, and the tail
+void ntt_inverse_dit_noscale(gg_domain* d, void* data, hipStream_t st);
+void ntt_tail_inverse_coset(gg_domain* d, void* data, int u, hipStream_t st);
+namespace plk {
 
 }  // namespace plk
 }  // namespace gg

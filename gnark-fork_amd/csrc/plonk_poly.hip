@@ -18,6 +18,7 @@
 #include "plonk_ops.h"
 #include "prof.h"
 #include <vector>
+#include <algorithm>
 #include <cstring>
 
 namespace gg {
@@ -400,6 +401,149 @@ void ratio(const F* l, const F* r, const F* o, const int64_t* perm, size_t n, co
     scan_prod(z, n, st, ar);  // Z[i] = Z[i-1] * num_i / den_i
 }
 
+// ---------------------------------------------------------------- batched evaluation
+template <class F>
+struct EvalJob {
+    const F* f[EVAL_MAX];
+    uint32_t len[EVAL_MAX];
+    int count;
+};
+constexpr int EVAL_BLOCKS = 1024;  // x 256 threads: G = 2^18 lanes, 16 coefficients each at 2^22
+
+// thread g of G: acc_k = sum_j f_k[g + j G] (a^G)^j by Horner over j, times
+// a^g; block sums per polynomial into part[k * gridDim.x + block]
+template <class F>
+__global__ void __launch_bounds__(256) k_eval_many(EvalJob<F> J, PowSplit<F> ap, F aG, F* part) {
+    __shared__ uint32_t sh[256 * 8];
+    const uint32_t G = gridDim.x * blockDim.x;
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const F ag = ap.at(g);
+    for (int k = 0; k < J.count; k++) {
+        const uint32_t len = J.len[k];
+        F acc = F::zero();
+        if (g < len) {
+            const uint32_t jn = (len - 1 - g) / G;  // last j with g + j G < len
+            const F* f = J.f[k];
+            acc = ldb(f + g + (size_t)jn * G);
+            for (uint32_t j = jn; j-- > 0;) acc = acc * aG + ldb(f + g + (size_t)j * G);
+            acc = acc * ag;
+        }
+        // block sum (LDS, limb-major)
+#pragma unroll
+        for (int l = 0; l < 8; l++) sh[l * 256 + threadIdx.x] = acc.v[l];
+        __syncthreads();
+        for (int s = 128; s > 0; s >>= 1) {
+            if ((int)threadIdx.x < s) {
+                F o;
+#pragma unroll
+                for (int l = 0; l < 8; l++) o.v[l] = sh[l * 256 + threadIdx.x + s];
+                acc = acc + o;
+#pragma unroll
+                for (int l = 0; l < 8; l++) sh[l * 256 + threadIdx.x] = acc.v[l];
+            }
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) stb(part + (size_t)k * gridDim.x + blockIdx.x, acc);
+        __syncthreads();
+    }
+}
+
+// out[k] = sum_b part[k * nb + b]: one block per polynomial
+template <class F>
+__global__ void __launch_bounds__(256) k_eval_sum(const F* part, uint32_t nb, F* out) {
+    __shared__ uint32_t sh[256 * 8];
+    const int k = blockIdx.x;
+    F acc = F::zero();
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) acc = acc + ldb(part + (size_t)k * nb + b);
+#pragma unroll
+    for (int l = 0; l < 8; l++) sh[l * 256 + threadIdx.x] = acc.v[l];
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) {
+            F o;
+#pragma unroll
+            for (int l = 0; l < 8; l++) o.v[l] = sh[l * 256 + threadIdx.x + s];
+            acc = acc + o;
+#pragma unroll
+            for (int l = 0; l < 8; l++) sh[l * 256 + threadIdx.x] = acc.v[l];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) stb(out + k, acc);
+}
+
+size_t eval_many_arena_bytes(size_t max_len, int count) {
+    (void)max_len;
+    const uint32_t G = EVAL_BLOCKS * 256;
+    int L = 0;
+    while ((1u << L) < G) L++;
+    const int S = (L + 1) / 2;
+    return (((size_t)1 << S) + ((size_t)1 << (L - S))) * 32 + 512 + (size_t)count * EVAL_BLOCKS * 32 + 512;
+}
+
+template <class F>
+void eval_many(const F* const* f, const size_t* len, int count, const F& a, F* out_dev, hipStream_t st,
+               Arena& ar) {
+    GG_CHECK(count >= 1 && count <= EVAL_MAX, GG_ERR_INVALID_ARG, "eval_many: 1..16 polynomials");
+    EvalJob<F> J{};
+    J.count = count;
+    for (int k = 0; k < count; k++) {
+        GG_CHECK(len[k] < ((size_t)1 << 31), GG_ERR_INVALID_ARG, "eval_many: polynomial too long");
+        J.f[k] = f[k];
+        J.len[k] = (uint32_t)len[k];
+    }
+    const uint32_t G = EVAL_BLOCKS * 256;
+    int L = 0;
+    while ((1u << L) < G) L++;
+    const int S = (L + 1) / 2;
+    const uint32_t nlo = 1u << S, nhi = 1u << (L - S);
+    F* lo = ar.get<F>(nlo);
+    F* hi = ar.get<F>(nhi);
+    F step = a;
+    for (int i = 0; i < S; i++) step = step * step;  // a^(2^S)
+    hipLaunchKernelGGL(k_pow_split<F>, dim3(grid_for(std::max(nlo, nhi), 256)), dim3(256), 0, st, a, step, lo, nlo,
+                       hi, nhi);
+    GG_HIP(hipGetLastError());
+    F aG = a;
+    for (int i = 0; i < L; i++) aG = aG * aG;  // a^G, G = 2^L
+    F* part = ar.get<F>((size_t)count * EVAL_BLOCKS);
+    hipLaunchKernelGGL(k_eval_many<F>, dim3(EVAL_BLOCKS), dim3(256), 0, st, J, PowSplit<F>{hi, lo, S}, aG, part);
+    GG_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_eval_sum<F>, dim3(count), dim3(256), 0, st, (const F*)part, (uint32_t)EVAL_BLOCKS, out_dev);
+    GG_HIP(hipGetLastError());
+}
+
+template <class F>
+struct LinComb {
+    const F* f[EVAL_MAX];
+    uint32_t len[EVAL_MAX];
+    F c[EVAL_MAX];
+    int count;
+};
+template <class F>
+__global__ void __launch_bounds__(256) k_lincomb(F* out, size_t n_out, LinComb<F> L) {
+    const size_t j = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_out) return;
+    F acc = F::zero();
+    for (int k = 0; k < L.count; k++)
+        if (j < L.len[k]) acc = acc + L.c[k] * ldb(L.f[k] + j);
+    stb(out + j, acc);
+}
+
+template <class F>
+void lincomb(F* out, size_t n_out, const F* const* f, const size_t* len, const F* c, int count, hipStream_t st) {
+    GG_CHECK(count >= 1 && count <= EVAL_MAX, GG_ERR_INVALID_ARG, "lincomb: 1..16 polynomials");
+    LinComb<F> L{};
+    L.count = count;
+    for (int k = 0; k < count; k++) {
+        L.f[k] = f[k];
+        L.len[k] = (uint32_t)std::min(len[k], n_out);
+        L.c[k] = c[k];
+    }
+    hipLaunchKernelGGL(k_lincomb<F>, dim3(grid_for(n_out, 256)), dim3(256), 0, st, out, n_out, L);
+    GG_HIP(hipGetLastError());
+}
+
 template <class F>
 void fold_h(const F* h, size_t n_small, const F& zz, F* out, hipStream_t st) {
     const size_t np2 = n_small + 2;
@@ -446,6 +590,8 @@ void shift_copy(const F* in, F* out, size_t n, hipStream_t st) {
 #define GG_PLK_INST(F)                                                                                          \
     template void scan_prod<F>(F*, size_t, hipStream_t, Arena&);                                                \
     template void horner<F>(const F*, size_t, const F&, F*, F*, hipStream_t, Arena&);                          \
+    template void eval_many<F>(const F* const*, const size_t*, int, const F&, F*, hipStream_t, Arena&);          \
+    template void lincomb<F>(F*, size_t, const F* const*, const size_t*, const F*, int, hipStream_t);           \
     template void ratio<F>(const F*, const F*, const F*, const int64_t*, size_t, const F&, const F&, const F&, \
                            const F&, F*, hipStream_t, Arena&);                                                  \
     template void fold_h<F>(const F*, size_t, const F&, F*, hipStream_t);                                       \
@@ -498,6 +644,34 @@ extern "C" int gg_bls12_381_fr_horner(const void* f_dev, size_t n, const void* a
     FrB* v = ar.get<FrB>(1);
     plk::horner((const FrB*)f_dev, n, frb(a_mont), (FrB*)q_dev, v, st, ar);
     GG_HIP(hipMemcpyAsync(value_out, v, 32, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipStreamSynchronize(st));
+    GG_CAPI_END
+}
+
+extern "C" int gg_fr_evaluate_many(int curve, const void* const* polys_dev, const size_t* lens, int count,
+                                   const void* point_mont, void* values_out, void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(polys_dev && lens && point_mont && values_out, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(curve == GG_CURVE_BN254 || curve == GG_CURVE_BLS12_381, GG_ERR_INVALID_ARG, "bad curve");
+    GG_CHECK(count >= 1 && count <= plk::EVAL_MAX, GG_ERR_INVALID_ARG, "1..16 polynomials");
+    size_t mx = 0;
+    for (int k = 0; k < count; k++) {
+        GG_CHECK(polys_dev[k] || lens[k] == 0, GG_ERR_INVALID_ARG, "null polynomial");
+        mx = std::max(mx, lens[k]);
+    }
+    hipStream_t st = pick(hip_stream);
+    Arena ar;
+    ar.reserve(plk::eval_many_arena_bytes(mx, count) + 256 + 32 * (size_t)count);
+    auto run = [&](auto tag) {
+        using F = decltype(tag);
+        F a;
+        memcpy(a.v, point_mont, 32);
+        F* out = ar.get<F>(count);
+        plk::eval_many((const F* const*)polys_dev, lens, count, a, out, st, ar);
+        GG_HIP(hipMemcpyAsync(values_out, out, 32 * (size_t)count, hipMemcpyDeviceToHost, st));
+    };
+    if (curve == GG_CURVE_BN254) run(Fr{});
+    else run(FrB{});
     GG_HIP(hipStreamSynchronize(st));
     GG_CAPI_END
 }

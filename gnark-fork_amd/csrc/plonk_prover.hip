@@ -115,12 +115,52 @@ struct Hasher {
 
 
 // ============================================================== key
+// Quotient units (computeNumerator + divideByXMinusOne, prove.go:837-1079,
+// 1223-1276, split over device parts).  The big domain u<w_big> (4n points,
+// rho = |big| / n cosets) is cut into U = rho S classes K = p (mod U), S >= 1 a
+// power of two (S = 1: the cosets; S = 2 on 8 GPUs: half cosets).  Unit p owns
+// the m = n / S points u w_big^p <w^S>:
+//   * each per-proof polynomial (canonical, bit-reversed) is folded to m
+//     coefficients (fold_brev, kappa = s_p^m) and coset-FFTed there (size m,
+//     shift s_p = u w_big^p); ZS's points are class p + rho (mod U): for S > 1
+//     Z is evaluated there too;
+//   * the numerator (allConstraints) is taken on the m points and scaled by
+//     1 / (x^n - 1) (constant on a coset);
+//   * the values sit in cres at bitrev(U j + p): one contiguous block of m
+//     (block bitrev_u(p), u = log2 U), whose first L - u stages of the big
+//     coset iFFT (DIT) stay inside the block -- the unit runs them as a size-m
+//     inverse DFT; the owner of cres (part 0) runs the last u stages over all
+//     blocks (ntt_tail_inverse_coset).
+// Unit p runs on part p mod N; on one GPU (N = 1) the four coset units and the
+// tail are exactly FFTInverse(DIT, OnCoset) of the whole vector.
+struct QUnit {
+    int p = 0, device = 0;
+    gg_domain_t dom = nullptr;   // size m, root w^S, coset generator s_p
+    gg_domain_t zdom = nullptr;  // S > 1: the class (p + rho) mod U (ZS)
+    uint32_t kappa[8] = {}, zkappa[8] = {}, inv_den[8] = {};  // s_p^m, s_p'^m, 1 / (s_c^n - 1)
+    std::vector<DevBuf> ev;      // the key polynomials on the class (Ql Qr Qm Qo S1 S2 S3 X LOne Qcp_i)
+    DevBuf tw0, tw1;             // S > 1: twiddles0 at the class's points and at the next ones
+    DevBuf out;                  // on a peer: the class's block of the quotient
+    ~QUnit() {
+        int cur = 0;
+        const bool restore = hipGetDevice(&cur) == hipSuccess;
+        (void)hipSetDevice(device);
+        if (dom) gg_domain_release(dom);
+        if (zdom) gg_domain_release(zdom);
+        ev.clear();
+        tw0.release();
+        tw1.release();
+        out.release();
+        if (restore) (void)hipSetDevice(cur);
+    }
+};
+
 // One-process multi-GPU (gg_plonk_pk_create_multi): device parts[p] (p >= 1) of
 // a key holds slice p of pk.Kzg.G1 / pk.KzgLagrange.G1 (every commitment is an
-// MSM split over the parts, partials summed exactly on the host) and computes
-// the numerator on the big-domain cosets i with i % owners == p (its coset
-// evaluations of the key polynomials resident there; the per-proof L, R, O, Z,
-// Qk, Pi_i arrive by peer copy, its block of cres goes back the same way).
+// MSM split over the parts, partials summed exactly on the host) and runs its
+// quotient units (the key polynomials' evaluations on their classes resident
+// there; the per-proof L, R, O, Z, Qk, Pi_i arrive by peer copy, each unit's
+// block of the quotient goes back the same way).
 struct PlonkPeer {
     int device = 0;
     hipStream_t s[4] = {nullptr, nullptr, nullptr, nullptr};  // 0..2: MSMs (work slot), 3: cosets
@@ -128,12 +168,9 @@ struct PlonkPeer {
     size_t k_lo = 0, k_hi = 0, l_lo = 0, l_hi = 0;
     MsmWork* work[3] = {nullptr, nullptr, nullptr};
     DevBuf scal[3];                     // scalar slice staging per work slot
-    std::vector<int> cosets;            // big-domain cosets owned here
-    std::vector<gg_domain_t> dcos;      // their small-domain coset FFTs
-    std::vector<std::vector<DevBuf>> ev;  // [key poly][owned coset]
-    DevBuf tw0, in[5 + plk::MAX_CMT];   // L R O Z (canonical bit-reversed), Qk, Pi_j
-    DevBuf cev[7 + plk::MAX_CMT];       // coset evaluation slot
-    std::vector<DevBuf> out;            // owned coset blocks of cres
+    std::vector<std::unique_ptr<QUnit>> units;  // quotient units placed here
+    DevBuf tw0, in[5 + plk::MAX_CMT];   // twiddles0 (S = 1); L R O Z (canonical bit-reversed), Qk, Pi_j
+    DevBuf cev[7 + plk::MAX_CMT], zc;   // a unit's evaluation slot; ZS (S > 1)
     hipEvent_t ea[4] = {}, eb[4] = {};  // per stream: around the last peer copy (timing)
     ~PlonkPeer() {
         int cur = 0;
@@ -143,13 +180,12 @@ struct PlonkPeer {
             if (w) msm_work_delete(w);
         if (kzg) gg_msm_base_release(kzg);
         if (kzg_lag) gg_msm_base_release(kzg_lag);
-        for (auto d : dcos) gg_domain_release(d);
-        for (auto& v : ev) v.clear();
+        units.clear();
         for (auto& b : scal) b.release();
         for (auto& b : in) b.release();
         for (auto& b : cev) b.release();
+        zc.release();
         tw0.release();
-        out.clear();
         for (hipStream_t x : s)
             if (x) (void)hipStreamDestroy(x);
         for (int i = 0; i < 4; i++) {
@@ -285,15 +321,16 @@ struct Key : gg_plonk_pk {
     size_t n = 0, big = 0, rho = 0;
     FrB omega, omega_big, u, n_inv;
     gg_domain_t d0 = nullptr, d1 = nullptr;
-    std::vector<gg_domain_t> dcos;
-    std::vector<FrB> coset_shift;
+    std::vector<FrB> coset_shift;  // u w_big^i, i < rho
     // trace, canonical regular (reg) and bit-reversed (brev); Qk incomplete
     enum { QL = PK::QL, QR, QM, QO, QK, S1, S2, S3, NTRACE };
     DevBuf reg[NTRACE], brev[NTRACE], qk_lag;
     std::vector<DevBuf> qcp_reg, qcp_brev;
-    // resident coset evaluations [poly][coset]: Ql Qr Qm Qo S1 S2 S3 X LOne Qcp_i
+    // resident evaluations of Ql Qr Qm Qo S1 S2 S3 X LOne Qcp_i on every quotient unit's class
     enum { E_QL = PK::E_QL, E_QR, E_QM, E_QO, E_S1, E_S2, E_S3, E_X, E_LONE, E_QCP0 };
-    std::vector<std::vector<DevBuf>> ev;
+    int U = 1, S = 1, log_u = 0;  // quotient units: U = rho S classes of the big domain
+    bool split_idft = false;      // units run the first L - log_u stages of the big coset iFFT
+    std::vector<std::unique_ptr<QUnit>> units;  // units of part 0
     DevBuf perm, tw0;
     gg_msm_base_t kzg = nullptr, kzg_lag = nullptr;
     BAff blind_lo[3], blind_hi[3];  // G1[0..3), G1[n..n+3)
@@ -309,7 +346,7 @@ struct Key : gg_plonk_pk {
     void* reduce_ctx = nullptr;
     // one-process multi-GPU: this key is part 0 of 1 + peers.size() device parts
     std::vector<std::unique_ptr<PlonkPeer>> peers;
-    int owners = 1;  // devices sharing the numerator cosets (coset i -> part i % owners)
+    int n_parts = 1;  // device parts (unit p -> part p mod n_parts)
     // gg_plonk_pk_set_rehearsal (timing only): the peer parts do nothing, the
     // proof is not valid and gg_plonk_prove returns GG_REHEARSAL
     bool solo = false;
@@ -321,7 +358,7 @@ struct Key : gg_plonk_pk {
     Arena ar[4];
     // per-proof buffers
     DevBuf lag[3], can[4], cbrev[4], zlag, qkc, pi_reg[plk::MAX_CMT], pi_brev[plk::MAX_CMT];
-    DevBuf cev[2][7 + plk::MAX_CMT];  // coset evaluation slots (two cosets in flight)
+    DevBuf cev[2][7 + plk::MAX_CMT], zc[2];  // unit evaluation slots (two units in flight), ZS (S > 1)
     DevBuf cres, hpad[3], bz, bl[3], fold, lin, q1, q2, vals, pad;
     int device = 0;
     std::vector<hipEvent_t> evs;  // cross-stream ordering events, reused by every prove
@@ -337,7 +374,7 @@ struct Key : gg_plonk_pk {
         if (kzg_lag) gg_msm_base_release(kzg_lag);
         if (d0) gg_domain_release(d0);
         if (d1) gg_domain_release(d1);
-        for (auto d : dcos) gg_domain_release(d);
+        units.clear();
         for (hipStream_t x : s)
             if (x) (void)hipStreamDestroy(x);
     }
@@ -362,14 +399,19 @@ static void lag_to_canonical(Key* pk, const FrB* lag, FrB* brev, FrB* reg, hipSt
     plk::ntt(pk->d0, brev, 1, 0, 0, st);  // FFTInverse DIF: natural in -> bit-reversed out
     if (reg) plk::bit_reverse(brev, reg, pk->n, st);
 }
-// evaluations on coset i (natural order) of a canonical bit-reversed polynomial
-static void coset_eval(Key* pk, const FrB* brev, FrB* out, int i, hipStream_t st) {
-    dcopy(out, brev, pk->n * 32, st);
-    plk::ntt(pk->dcos[i], out, 0, 1, 1, st);  // FFT DIT on the coset: bit-reversed in -> natural out
+// evaluations (natural order, m = n / S) of a canonical bit-reversed polynomial on
+// a quotient unit's class: fold to m coefficients, then the coset FFT there
+static void unit_eval(Key* pk, gg_domain_t dom, const uint32_t* kappa, const FrB* brev, FrB* out, hipStream_t st) {
+    if (pk->S == 1) dcopy(out, brev, pk->n * 32, st);
+    else {
+        FrB k;
+        memcpy(k.v, kappa, 32);
+        plk::fold_brev(brev, pk->n, pk->S, k, out, st);
+    }
+    plk::ntt(dom, out, 0, 1, 1, st);  // FFT DIT on the coset: bit-reversed in -> natural out
 }
-// `to` waits for the work enqueued on `from` so far (events live as long as the key)
-static void record_wait(Key* pk, hipStream_t from, hipStream_t to) {
-    if (from == to) return;
+// an event marking the work enqueued on `from` so far (events live as long as the key)
+static hipEvent_t record(Key* pk, hipStream_t from) {
     if (pk->ev_next == pk->evs.size()) {
         hipEvent_t e;
         GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -377,7 +419,12 @@ static void record_wait(Key* pk, hipStream_t from, hipStream_t to) {
     }
     hipEvent_t e = pk->evs[pk->ev_next++];
     GG_HIP(hipEventRecord(e, from));
-    GG_HIP(hipStreamWaitEvent(to, e, 0));
+    return e;
+}
+// `to` waits for the work enqueued on `from` so far
+static void record_wait(Key* pk, hipStream_t from, hipStream_t to) {
+    if (from == to) return;
+    GG_HIP(hipStreamWaitEvent(to, record(pk, from), 0));
 }
 // a peer part's share of an MSM: its scalar slice copied from the primary GPU
 // (xGMI peer copy), its resident base slice
@@ -464,6 +511,17 @@ static FrB eval_dev(Key* pk, const FrB* f, size_t len, const FrB& a, FrB* q, FrB
     return fetch(slot, st);
 }
 
+// evaluations of `count` polynomials at a (plk::eval_many) read back at once
+static std::vector<FrB> eval_batch(Key* pk, const FrB* const* f, const size_t* len, int count, const FrB& a,
+                                   FrB* slot, int ai, hipStream_t st) {
+    pk->ar[ai].reset();
+    plk::eval_many(f, len, count, a, slot, st, pk->ar[ai]);
+    std::vector<FrB> v(count);
+    GG_HIP(hipMemcpyAsync(v.data(), slot, 32 * (size_t)count, hipMemcpyDeviceToHost, st));
+    GG_HIP(hipStreamSynchronize(st));
+    return v;
+}
+
 static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, const void* omega_big,
                            const void* coset_shift, const void* kzg_g1, size_t n_kzg,
                            const void* kzg_lagrange_g1, const void* const* trace, const void* const* qcp,
@@ -534,9 +592,18 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
     FrB sh = pk->u;
     for (size_t i = 0; i < pk->rho; i++) {  // coset i of the big domain: shift u w_big^i
         pk->coset_shift.push_back(sh);
-        pk->dcos.push_back(dom(log_n, pk->omega, sh));
         sh = sh * pk->omega_big;
     }
+    // quotient units: U = rho S classes, S the largest power of two with U <= the
+    // device parts (and <= 16, m = n / S >= 16); unit p runs on part p mod N
+    pk->n_parts = n_devices > 1 ? n_devices : 1;
+    pk->S = 1;
+    while ((size_t)pk->rho * pk->S * 2 <= (size_t)pk->n_parts && pk->rho * pk->S * 2 <= 16 && n / (pk->S * 2) >= 16)
+        pk->S *= 2;
+    pk->U = (int)pk->rho * pk->S;
+    pk->log_u = 0;
+    while ((1 << pk->log_u) < pk->U) pk->log_u++;
+    pk->split_idft = log_big >= 12;
     for (hipStream_t& x : pk->s) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
     for (auto& w : pk->work) w = msm_work_new();
     hipStream_t st = pk->s[0];
@@ -547,7 +614,6 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
             hi = m * (size_t)(pk->rank + 1) / (size_t)pk->world;
         };
         if (n_devices > 1) {  // part 0 here, parts 1.. on the peers
-            pk->owners = std::min<int>(n_devices, (int)pk->rho);
             for (int d = 1; d < n_devices; d++) {
                 pk->peers.emplace_back(new PlonkPeer());
                 PlonkPeer* p = pk->peers.back().get();
@@ -570,8 +636,6 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
                 rc = gg_msm_base_create(Cv::group, (const uint8_t*)kzg_lagrange_g1 + PT * p->l_lo,
                                         p->l_hi - p->l_lo, 0, nullptr, 0, &p->kzg_lag);
                 GG_CHECK(rc == GG_OK, rc, gg_last_error());
-                for (size_t i = 0; i < pk->rho; i++)
-                    if ((int)i % pk->owners == d) p->cosets.push_back((int)i);
             }
             GG_HIP(hipSetDevice(pk->device));
             pk->k_lo = 0;
@@ -644,36 +708,57 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
                                     F(pk->brev[Key::S1]), F(pk->brev[Key::S2]),
                                     F(pk->brev[Key::S3]), F(xb), F(lone)};
     for (int i = 0; i < n_cmt; i++) srcs.push_back(F(pk->qcp_brev[i]));
-    pk->ev.resize(srcs.size());
-    for (size_t k = 0; k < srcs.size(); k++) {
-        pk->ev[k].resize(pk->rho);
-        for (size_t i = 0; i < pk->rho; i++) {
-            pk->ev[k][i].alloc(nb);
-            coset_eval(pk, srcs[k], F(pk->ev[k][i]), (int)i, st);
-        }
-    }
-    // peers: their cosets' domains, key evaluations (moved off this GPU) and buffers
     GG_HIP(hipStreamSynchronize(st));
-    for (auto& pp : pk->peers) {
-        PlonkPeer* p = pp.get();
-        if (p->cosets.empty()) continue;
-        GG_HIP(hipSetDevice(p->device));
-        p->ev.resize(srcs.size());
-        for (int c : p->cosets) p->dcos.push_back(dom(log_n, pk->omega, pk->coset_shift[c]));
-        for (size_t k = 0; k < srcs.size(); k++)
-            for (int c : p->cosets) {
-                p->ev[k].emplace_back(nb);
-                GG_HIP(hipMemcpyPeerAsync(p->ev[k].back().p, p->device, pk->ev[k][c].p, pk->device, nb, p->s[3]));
+    // quotient units: domains, resident key evaluations on the class, twiddles0 there
+    const size_t m = n / pk->S, mb = 32 * m;
+    const FrB wS = pow_u64(pk->omega, (uint64_t)pk->S);
+    for (int p = 0; p < pk->U; p++) {
+        const int part = p % pk->n_parts;
+        PlonkPeer* peer = part ? pk->peers[part - 1].get() : nullptr;
+        std::unique_ptr<QUnit> up_(new QUnit());
+        QUnit* q = up_.get();
+        q->p = p;
+        q->device = peer ? peer->device : pk->device;
+        GG_HIP(hipSetDevice(q->device));
+        hipStream_t qs = peer ? peer->s[3] : st;
+        const FrB sp = pk->u * pow_u64(pk->omega_big, (uint64_t)p);
+        const FrB spz = pk->u * pow_u64(pk->omega_big, (uint64_t)((p + (int)pk->rho) % pk->U));
+        const FrB kap = pow_u64(sp, m), zkap = pow_u64(spz, m);
+        const FrB den = inverse(pow_u64(pk->coset_shift[p % pk->rho], n) - FrB::one());
+        GG_CHECK(!(pow_u64(pk->coset_shift[p % pk->rho], n) == FrB::one()), GG_ERR_INVALID_ARG,
+                 "x^n - 1 vanishes on the big coset");
+        memcpy(q->kappa, kap.v, 32);
+        memcpy(q->zkappa, zkap.v, 32);
+        memcpy(q->inv_den, den.v, 32);
+        q->dom = dom(log_n - (pk->log_u - (int)(pk->log_big - pk->log_n)), wS, sp);
+        if (pk->S > 1) q->zdom = dom(log_n - (pk->log_u - (int)(pk->log_big - pk->log_n)), wS, spz);
+        if (peer && !peer->tw0.p) {  // the peer's per-proof buffers, once
+            peer->tw0.alloc(nb);
+            GG_HIP(hipMemcpyPeerAsync(peer->tw0.p, peer->device, pk->tw0.p, pk->device, nb, qs));
+            for (int k = 0; k < 5 + n_cmt; k++) peer->in[k].alloc(nb);
+            for (int k = 0; k < 7 + n_cmt; k++)
+                if (k != 4 && k != 5) peer->cev[k].alloc(mb);
+            if (pk->S > 1) peer->zc.alloc(mb);
+        }
+        for (size_t k = 0; k < srcs.size(); k++) {
+            q->ev.emplace_back(mb);
+            const FrB* src = srcs[k];
+            if (peer) {  // the key polynomial to the peer (staged in its input buffer), evaluated there
+                GG_HIP(hipMemcpyPeerAsync(peer->in[0].p, peer->device, src, pk->device, nb, qs));
+                src = F(peer->in[0]);
             }
-        p->tw0.alloc(nb);
-        GG_HIP(hipMemcpyPeerAsync(p->tw0.p, p->device, pk->tw0.p, pk->device, nb, p->s[3]));
-        for (int k = 0; k < 5 + n_cmt; k++) p->in[k].alloc(nb);
-        for (int k = 0; k < 7 + n_cmt; k++)
-            if (k != 4 && k != 5) p->cev[k].alloc(nb);
-        for (size_t c = 0; c < p->cosets.size(); c++) p->out.emplace_back(nb);
-        GG_HIP(hipStreamSynchronize(p->s[3]));
-        for (size_t k = 0; k < srcs.size(); k++)
-            for (int c : p->cosets) pk->ev[k][c].release();
+            unit_eval(pk, q->dom, q->kappa, src, F(q->ev.back()), qs);
+        }
+        if (pk->S > 1) {  // twiddles0 at the class's points w^(s + S j) and the next ones (ZS)
+            const FrB* t0 = peer ? F(peer->tw0) : F(pk->tw0);
+            q->tw0.alloc(mb);
+            q->tw1.alloc(mb);
+            plk::gather_strided(t0, n, pk->S, p / (int)pk->rho, F(q->tw0), qs);
+            plk::gather_strided(t0, n, pk->S, p / (int)pk->rho + 1, F(q->tw1), qs);
+        }
+        if (peer) q->out.alloc(mb);
+        GG_HIP(hipStreamSynchronize(qs));
+        (peer ? peer->units : pk->units).push_back(std::move(up_));
     }
     GG_HIP(hipSetDevice(pk->device));
     pk->perm.alloc(3 * n * 8);
@@ -690,7 +775,9 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
     }
     for (auto& slot : pk->cev)
         for (int k = 0; k < 7 + n_cmt; k++)
-            if (k != 4 && k != 5) slot[k].alloc(nb);  // 4 (ZS), 5 (beta X): formed in the numerator kernel
+            if (k != 4 && k != 5) slot[k].alloc(mb);  // 4 (ZS), 5 (beta X): formed in the numerator kernel
+    if (pk->S > 1)
+        for (auto& z : pk->zc) z.alloc(mb);
     pk->cres.alloc(32 * pk->big);
     const size_t nb3 = 32 * (n + 3);
     for (auto& b : pk->hpad) b.alloc(nb3);
@@ -702,7 +789,8 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
     pk->q2.alloc(nb3);
     pk->pad.alloc(nb3);
     pk->vals.alloc(32 * 64);
-    const size_t ab = std::max(plk::ratio_arena_bytes(n), plk::horner_arena_bytes(n + 3)) + 65536;
+    const size_t ab = std::max(std::max(plk::ratio_arena_bytes(n), plk::horner_arena_bytes(n + 3)),
+                               plk::eval_many_arena_bytes(n + 3, plk::EVAL_MAX)) + 65536;
     for (auto& a : pk->ar) a.reserve(ab);
     GG_HIP(hipStreamSynchronize(st));
     // vk digests (commitTrace, setup.go:229-272) unless the caller has them
@@ -759,7 +847,11 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     for (int q = 0, k = 0; q < 4; q++)
         for (int j = 0; j <= ord[q]; j++) bp[q].push_back(blinding ? blinding[k++] : fr_random());
     // ---- inputs: L, R, O (Lagrange regular) on streams 0..2
-    for (int k = 0; k < 3; k++) up(pk->lag[k].p, lro_in[k], nb, on_dev, s[k]);
+    hipEvent_t uploaded[3];
+    for (int k = 0; k < 3; k++) {
+        up(pk->lag[k].p, lro_in[k], nb, on_dev, s[k]);
+        uploaded[k] = record(pk, s[k]);
+    }
     // blinding commitments of L, R, O, Z on host threads while the GPU works
     std::future<BJac> fblind[4];
     for (int q = 0; q < 4; q++) fblind[q] = std::async(std::launch::async, [pk, &bp, q] { return blind_commit(pk, bp[q]); });
@@ -786,13 +878,17 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                 lag_to_canonical(pk, F(pk->pi_reg[i]), F(pk->pi_brev[i]), nullptr, q);
                 plk::bit_reverse(F(pk->pi_brev[i]), F(pk->pi_reg[i]), n, q);
             }
+            // canonical L, R, O (bit-reversed for the coset FFTs, regular for the
+            // openings) while the commitments run: they only read lag[k]
+            for (int k = 0; k < 3; k++) {
+                GG_HIP(hipStreamWaitEvent(q, uploaded[k], 0));
+                lag_to_canonical(pk, F(pk->lag[k]), F(pk->cbrev[k]), F(pk->can[k]), q);
+            }
             GG_HIP(hipStreamSynchronize(q));
         }
         for (auto& f : fs) f.get();
     }
     for (int k = 0; k < 3; k++) P.lro[k] = to_aff(jac_add(red(pk, lroj[k]), fblind[k].get()));
-    // canonical L, R, O (bit-reversed for the coset FFTs, regular for the openings)
-    for (int k = 0; k < 3; k++) lag_to_canonical(pk, F(pk->lag[k]), F(pk->cbrev[k]), F(pk->can[k]), s[k]);
     mark();
     // ---- gamma, beta (deriveGammaAndBeta, prove.go:454-489; bindPublicData, verify.go:296-340).
     // G1Affine.Marshal is the UNCOMPRESSED encoding (RawBytes): groth16/bls12-381/verify.go:80-82
@@ -825,19 +921,24 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         for (int i = 0; i < n_cmt; i++) { g1_raw_bytes(P.bsb22[i], b); fs.bind("alpha", b, PT); }
     }
     const FrB alpha = derive(fs, "alpha", {&P.z});
-    // ---- computeNumerator (prove.go:837-1079): two cosets in flight on s[2], s[3];
-    // cosets owned by other device parts run there concurrently
+    // ---- computeNumerator + divideByXMinusOne (prove.go:837-1079, 1223-1276) as
+    // quotient units (QUnit): this part's units two in flight on s[2], s[3], the
+    // other parts' units on their devices concurrently; then the tail stages of
+    // the big coset iFFT here
     for (int k = 0; k < 4; k++) record_wait(pk, s[k == 3 ? 1 : k], s[2]), record_wait(pk, s[k == 3 ? 1 : k], s[3]);
-    // the parameters of coset i: e[] = this coset's evaluations of L R O Z (0..3),
-    // Qk (6), Pi_j (7 + j); kev(k) = the key's resident evaluation of poly k there
-    auto coset_params = [&](size_t i, FrB* const* e, auto kev, const FrB* tw0, FrB* cres, bool local) {
+    const size_t m = n / pk->S, mb = 32 * m;
+    // the parameters of unit q: e[] = its evaluations of L R O Z (0..3), Qk (6),
+    // Pi_j (7 + j); zc = Z on class p + rho (S > 1); the key's evaluations in q->ev
+    auto unit_params = [&](const QUnit* q, FrB* const* e, const FrB* zc, FrB* cres, bool local) {
         const FrB cs = pk->u, css = pk->u * pk->u;
         plk::NumParamsT<FrB> NP{};
+        auto kev = [&](int k) { return (const FrB*)F(q->ev[k]); };
         NP.x[plk::ID_L] = e[0];
         NP.x[plk::ID_R] = e[1];
         NP.x[plk::ID_O] = e[2];
         NP.x[plk::ID_Z] = e[3];
-        NP.x[plk::ID_ZS] = nullptr;  // Z[(j + 1) % n]
+        NP.x[plk::ID_ZS] = zc;  // nullptr (S = 1): Z[(j + 1) % m]
+        NP.zs_shift = (zc && q->p + (int)pk->rho >= pk->U) ? 1u : 0u;
         NP.x[plk::ID_QL] = kev(Key::E_QL);
         NP.x[plk::ID_QR] = kev(Key::E_QR);
         NP.x[plk::ID_QM] = kev(Key::E_QM);
@@ -853,8 +954,8 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
             NP.x[plk::ID_QCI + 2 * j + 1] = e[7 + j];
         }
         NP.nx = plk::ID_QCI + 2 * n_cmt;
-        // blinding polynomials scaled for this coset: b_j s^j (s^n - 1) (prove.go:985-993)
-        const FrB sc = pk->coset_shift[i];
+        // blinding polynomials scaled for the unit's coset c: b_j s^j (s^n - 1) (prove.go:985-993)
+        const FrB sc = pk->coset_shift[q->p % pk->rho];
         const FrB sn1 = pow_u64(sc, n) - FrB::one();
         for (int q4 = 0; q4 < 4; q4++) {
             FrB acc = sn1;
@@ -864,7 +965,9 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                 acc = acc * sc;
             }
         }
-        NP.tw0 = tw0;
+        // twiddles0 at the class's points (S = 1: the small domain itself)
+        NP.tw0 = pk->S > 1 ? (const FrB*)F(q->tw0) : nullptr;
+        NP.tw1 = pk->S > 1 ? (const FrB*)F(q->tw1) : nullptr;
         NP.beta = beta;
         NP.gamma = gamma;
         NP.alpha = alpha;
@@ -873,22 +976,39 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         NP.ka = beta;
         NP.kb = beta * cs;
         NP.kc = beta * css;
-        NP.n = (uint32_t)n;
-        NP.rho = (uint32_t)pk->rho;
-        NP.coset = (uint32_t)i;
+        NP.n = (uint32_t)m;
+        NP.rho = (uint32_t)pk->U;
+        NP.coset = (uint32_t)q->p;
         NP.log_big = (uint32_t)pk->log_big;
         NP.cres = cres;
         NP.local_block = local ? 1u : 0u;
+        NP.has_out_scale = 1;  // divideByXMinusOne: 1 / (x^n - 1), constant on the coset
+        memcpy(NP.out_scale.v, q->inv_den, 32);
         return NP;
+    };
+    // one unit: its polynomials' evaluations, the numerator (scaled), and the
+    // first L - u stages of the big coset iFFT on its block
+    auto run_unit = [&](const QUnit* q, const FrB* const* src, FrB* const* e, FrB* zc, const FrB* tw0, FrB* cres,
+                        bool local, hipStream_t st) {
+        for (int k = 0; k < 4; k++) unit_eval(pk, q->dom, q->kappa, src[k], e[k], st);
+        unit_eval(pk, q->dom, q->kappa, src[4], e[6], st);
+        for (int j = 0; j < n_cmt; j++) unit_eval(pk, q->dom, q->kappa, src[5 + j], e[7 + j], st);
+        if (pk->S > 1) unit_eval(pk, q->zdom, q->zkappa, src[3], zc, st);
+        plk::NumParamsT<FrB> NP = unit_params(q, e, pk->S > 1 ? zc : nullptr, cres, local);
+        if (pk->S == 1) NP.tw0 = tw0;
+        plk::numerator(NP, st);
+        if (pk->split_idft) {
+            const size_t blk = (size_t)(__builtin_bitreverse32((uint32_t)q->p) >> (32 - pk->log_u));
+            ntt_inverse_dit_noscale(q->dom, local ? (void*)cres : (void*)(cres + blk * m), st);
+        }
     };
     std::vector<std::future<void>> peer_work;
     if (!pk->peers.empty() && !plonk_solo(pk)) {
         for (int k = 0; k < 4; k++) GG_HIP(hipStreamSynchronize(s[k]));  // inputs complete before the copies
-        const int rb = pk->log_big - pk->log_n;
         for (size_t pi = 0; pi < pk->peers.size(); pi++) {
             PlonkPeer* p = pk->peers[pi].get();
-            if (p->cosets.empty()) continue;
-            peer_work.push_back(std::async(std::launch::async, [&, p, pi, rb] {
+            if (p->units.empty()) continue;
+            peer_work.push_back(std::async(std::launch::async, [&, p, pi] {
                 GG_HIP(hipSetDevice(p->device));
                 const auto ta = std::chrono::steady_clock::now();
                 hipStream_t q = p->s[3];
@@ -899,31 +1019,19 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                 for (int k = 0; k < 5 + n_cmt; k++)
                     GG_HIP(hipMemcpyPeerAsync(p->in[k].p, p->device, src[k], pk->device, nb, q));
                 GG_HIP(hipEventRecord(p->eb[3], q));
-                for (size_t c = 0; c < p->cosets.size(); c++) {
-                    const int i = p->cosets[c];
-                    auto ceval = [&](const DevBuf& from, DevBuf& to) {
-                        dcopy(to.p, from.p, nb, q);
-                        plk::ntt(p->dcos[c], to.p, 0, 1, 1, q);  // FFT DIT on the coset
-                    };
-                    for (int k = 0; k < 4; k++) ceval(p->in[k], p->cev[k]);
-                    ceval(p->in[4], p->cev[6]);
-                    for (int j = 0; j < n_cmt; j++) ceval(p->in[5 + j], p->cev[7 + j]);
-                    FrB* e[7 + plk::MAX_CMT] = {};
-                    for (int k = 0; k < 7 + n_cmt; k++) e[k] = F(p->cev[k]);
-                    plk::NumParamsT<FrB> NP = coset_params(
-                        (size_t)i, e, [&](int k) { return (const FrB*)F(p->ev[k][c]); }, F(p->tw0), F(p->out[c]),
-                        true);
-                    plk::numerator(NP, q);
-                }
-                // the owned blocks back to the primary's cres (timed separately)
+                const FrB* ins[5 + plk::MAX_CMT] = {};
+                for (int k = 0; k < 5 + n_cmt; k++) ins[k] = F(p->in[k]);
+                FrB* e[7 + plk::MAX_CMT] = {};
+                for (int k = 0; k < 7 + n_cmt; k++) e[k] = F(p->cev[k]);
+                for (auto& qu : p->units) run_unit(qu.get(), ins, e, F(p->zc), F(p->tw0), F(qu->out), true, q);
+                // the units' blocks back to the primary's cres (timed separately)
                 GG_HIP(hipEventSynchronize(p->eb[3]));
                 float cin = 0;
                 GG_HIP(hipEventElapsedTime(&cin, p->ea[3], p->eb[3]));
                 GG_HIP(hipEventRecord(p->ea[3], q));
-                for (size_t c = 0; c < p->cosets.size(); c++) {
-                    const int i = p->cosets[c];
-                    const size_t blk = rb ? (size_t)(__builtin_bitreverse32((uint32_t)i) >> (32 - rb)) : 0;
-                    GG_HIP(hipMemcpyPeerAsync(F(pk->cres) + blk * n, pk->device, p->out[c].p, p->device, nb, q));
+                for (auto& qu : p->units) {
+                    const size_t blk = (size_t)(__builtin_bitreverse32((uint32_t)qu->p) >> (32 - pk->log_u));
+                    GG_HIP(hipMemcpyPeerAsync(F(pk->cres) + blk * m, pk->device, qu->out.p, p->device, mb, q));
                 }
                 GG_HIP(hipEventRecord(p->eb[3], q));
                 GG_HIP(hipStreamSynchronize(q));
@@ -931,32 +1039,28 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                 GG_HIP(hipEventElapsedTime(&cout, p->ea[3], p->eb[3]));
                 std::lock_guard<std::mutex> lk(pk->tmu);
                 PlonkPartTimes& T = pk->ptimes[pi + 1];
-                T.coset_count += (double)p->cosets.size();
+                T.coset_count += (double)p->units.size();
                 T.coset_ms += ms_since(ta);
                 T.coset_in_copy_ms += cin;
                 T.coset_out_copy_ms += cout;
-                T.coset_mb += (double)nb * (5 + n_cmt + p->cosets.size()) / 1e6;
+                T.coset_mb += ((double)nb * (5 + n_cmt) + (double)mb * p->units.size()) / 1e6;
             }));
         }
     }
     {
         int slot = 0;
-        for (size_t i = 0; i < pk->rho; i++) {
-            if ((int)i % pk->owners != 0) continue;  // another device part's coset
+        const FrB* src[5 + plk::MAX_CMT] = {F(pk->cbrev[0]), F(pk->cbrev[1]), F(pk->cbrev[2]), F(pk->cbrev[3]),
+                                            F(pk->qkc)};
+        for (int j = 0; j < n_cmt; j++) src[5 + j] = F(pk->pi_brev[j]);
+        for (auto& qu : pk->units) {
             hipStream_t q = s[2 + slot];
-            DevBuf* e = pk->cev[slot];
+            FrB* e[7 + plk::MAX_CMT] = {};
+            for (int k = 0; k < 7 + n_cmt; k++) e[k] = F(pk->cev[slot][k]);
+            run_unit(qu.get(), src, e, F(pk->zc[slot]), F(pk->tw0), F(pk->cres), false, q);
             slot ^= 1;
-            // per-proof polynomials on this coset: L R O Z, ZS (shift), ID = beta X, Qk, Pi_j
-            // (ZS = Z shifted and beta X are formed inside the numerator kernel)
-            for (int k = 0; k < 4; k++) coset_eval(pk, F(pk->cbrev[k]), F(e[k]), (int)i, q);
-            coset_eval(pk, F(pk->qkc), F(e[6]), (int)i, q);
-            for (int j = 0; j < n_cmt; j++) coset_eval(pk, F(pk->pi_brev[j]), F(e[7 + j]), (int)i, q);
-            FrB* ep[7 + plk::MAX_CMT] = {};
-            for (int k = 0; k < 7 + n_cmt; k++) ep[k] = F(e[k]);
-            plk::NumParamsT<FrB> NP = coset_params(
-                i, ep, [&](int k) { return (const FrB*)F(pk->ev[k][i]); }, F(pk->tw0), F(pk->cres), false);
-            plk::numerator(NP, q);
         }
+        std::lock_guard<std::mutex> lk(pk->tmu);
+        pk->ptimes[0].coset_count += (double)pk->units.size();
     }
     {
         const auto w = std::chrono::steady_clock::now();
@@ -965,7 +1069,10 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         pk->ptimes[0].wait_ms += ms_since(w);
     }
     record_wait(pk, s[3], s[2]);
-    plk::divide_by_xn_minus_one(pk->d1, n, F(pk->cres), s[2]);  // h, canonical regular
+    // h, canonical regular: the last log2(U) stages of FFTInverse(DIT, OnCoset) over
+    // the units' blocks (or, for domains below 2^12, the whole inverse here)
+    if (pk->split_idft) ntt_tail_inverse_coset(pk->d1, F(pk->cres), pk->log_u, s[2]);
+    else plk::ntt(pk->d1, F(pk->cres), 1, 1, 1, s[2]);
     for (int k = 0; k < 3; k++) {
         zero(pk->hpad[k].p, nb3, s[2]);
         dcopy(pk->hpad[k].p, F(pk->cres) + (n + 2) * k, 32 * (n + 2), s[2]);
@@ -1012,14 +1119,25 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     plk::fold_h(F(pk->cres), n, zp, F(pk->fold), s[2]);
     BJac fhd = jac_add(jac_add(BJac::from_affine(P.h[0]), jmul(P.h[1], zp)), jmul(P.h[2], zp * zp));
     const BAff folded_digest = to_aff(fhd);
-    // ---- evaluations at zeta (blinded L, R, O; S1, S2; Qcp_i) on s[1]
+    // ---- evaluations at zeta (blinded L, R, O; S1, S2; Qcp_i) on s[1]: one
+    // batched pass over the 5 + n_cmt polynomials, one read-back
     for (int k = 0; k < 3; k++) blinded(pk->can[k], bp[k], pk->bl[k], s[1]);
-    FrB lz[3];
-    for (int k = 0; k < 3; k++) lz[k] = eval_dev(pk, F(pk->bl[k]), n + 2, zeta, nullptr, F(pk->vals) + 1 + k, 1, s[1]);
-    const FrB s1z = eval_dev(pk, F(pk->reg[Key::S1]), n, zeta, nullptr, F(pk->vals) + 4, 1, s[1]);
-    const FrB s2z = eval_dev(pk, F(pk->reg[Key::S2]), n, zeta, nullptr, F(pk->vals) + 5, 1, s[1]);
+    FrB lz[3], s1z, s2z;
     std::vector<FrB> qcpz(n_cmt);
-    for (int j = 0; j < n_cmt; j++) qcpz[j] = eval_dev(pk, F(pk->qcp_reg[j]), n, zeta, nullptr, F(pk->vals) + 6 + j, 1, s[1]);
+    {
+        const FrB* fz[plk::EVAL_MAX] = {F(pk->bl[0]), F(pk->bl[1]), F(pk->bl[2]), F(pk->reg[Key::S1]),
+                                        F(pk->reg[Key::S2])};
+        size_t lz_len[plk::EVAL_MAX] = {n + 2, n + 2, n + 2, n, n};
+        for (int j = 0; j < n_cmt; j++) {
+            fz[5 + j] = F(pk->qcp_reg[j]);
+            lz_len[5 + j] = n;
+        }
+        std::vector<FrB> v = eval_batch(pk, fz, lz_len, 5 + n_cmt, zeta, F(pk->vals) + 1, 1, s[1]);
+        for (int k = 0; k < 3; k++) lz[k] = v[k];
+        s1z = v[3];
+        s2z = v[4];
+        for (int j = 0; j < n_cmt; j++) qcpz[j] = v[5 + j];
+    }
     // ---- computeLinearizedPolynomial (prove.go:1289-1389) on s[1]
     {
         const FrB l = lz[0], r = lz[1], o = lz[2];
@@ -1067,8 +1185,13 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     std::vector<BAff> digests = {folded_digest, lin_digest, P.lro[0], P.lro[1], P.lro[2], pk->vkS[0], pk->vkS[1]};
     for (int j = 0; j < n_cmt; j++) digests.push_back(pk->vkQcp[j]);
     P.claimed.resize(polys.size());
-    P.claimed[0] = eval_dev(pk, polys[0].first, polys[0].second, zeta, nullptr, F(pk->vals) + 16, 2, s[2]);
-    P.claimed[1] = eval_dev(pk, polys[1].first, polys[1].second, zeta, nullptr, F(pk->vals) + 17, 2, s[2]);
+    {
+        const FrB* fz[plk::EVAL_MAX] = {polys[0].first, polys[1].first};
+        const size_t fl[plk::EVAL_MAX] = {polys[0].second, polys[1].second};
+        std::vector<FrB> v = eval_batch(pk, fz, fl, 2, zeta, F(pk->vals) + 16, 2, s[2]);
+        P.claimed[0] = v[0];
+        P.claimed[1] = v[1];
+    }
     for (int k = 0; k < 3; k++) P.claimed[2 + k] = lz[k];
     P.claimed[5] = s1z;
     P.claimed[6] = s2z;
@@ -1088,13 +1211,19 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     const FrB gf = fg.compute("gamma");
     FrB fe = P.claimed.back();
     for (size_t i = P.claimed.size() - 1; i-- > 0;) fe = fe * gf + P.claimed[i];
-    // folded polynomial sum_i gamma^i p_i, then the quotient (f - f(zeta)) / (X - zeta)
-    zero(pk->q2.p, nb3, s[2]);
-    dcopy(pk->q2.p, polys[0].first, 32 * polys[0].second, s[2]);
-    FrB gp = gf;
-    for (size_t i = 1; i < polys.size(); i++) {
-        plk::axpy(F(pk->q2), polys[i].first, polys[i].second, gp, s[2]);
-        gp = gp * gf;
+    // folded polynomial sum_i gamma^i p_i (one pass), then the quotient (f - f(zeta)) / (X - zeta)
+    {
+        const FrB* fp[plk::EVAL_MAX];
+        size_t fl[plk::EVAL_MAX];
+        FrB cf[plk::EVAL_MAX];
+        FrB gp = FrB::one();
+        for (size_t i = 0; i < polys.size(); i++) {
+            fp[i] = polys[i].first;
+            fl[i] = polys[i].second;
+            cf[i] = gp;
+            gp = gp * gf;
+        }
+        plk::lincomb(F(pk->q2), n + 3, fp, fl, cf, (int)polys.size(), s[2]);
     }
     zero(pk->fold.p, nb3, s[2]);  // reuse as the batch quotient (n + 2 of n + 3)
     const FrB fv = eval_dev(pk, F(pk->q2), n + 3, zeta, F(pk->fold), F(pk->vals) + 18, 2, s[2]);

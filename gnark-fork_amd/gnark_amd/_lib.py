@@ -109,6 +109,7 @@ def _load():
         "gg_plonk_ratio_copy_constraint": ([P, P, P, P, S, P, P, P, P, P, P], I),
         "gg_bls12_381_fr_prefix_product": ([P, S, P], I),
         "gg_bls12_381_fr_horner": ([P, S, P, P, P, P], I),
+        "gg_fr_evaluate_many": ([I, PP, ctypes.POINTER(S), I, P, P, P], I),
         "gg_plonk_fold_h": ([P, S, P, P, P], I),
         "gg_plonk_linearized": ([P, S, P, S, ctypes.POINTER(ctypes.c_void_p), S,
                                  ctypes.POINTER(ctypes.c_void_p), P, I, P, P], I),
@@ -218,6 +219,7 @@ EXPORTED = [
     "gg_msm_stripe", "gg_groth16_pk_create_stripe_ex", "gg_groth16_pk_stripe", "gg_groth16_mpk_split",
     "gg_hshard_create_ex", "gg_hshard_exchange_bytes", "gg_groth16_mpk_shard_timings",
     "gg_groth16_mpk_set_rehearsal", "gg_plonk_pk_set_rehearsal", "gg_plonk_pk_part_timings",
+    "gg_fr_evaluate_many",
 ]
 
 

@@ -78,6 +78,22 @@ def evaluate(f, n: int, a: bytes, q_out=None, stream=None) -> bytes:
     return bytes(out)
 
 
+def evaluate_many(polys, lens, a: bytes, curve: int = None, stream=None):
+    """[f_k(a)] for up to 16 canonical regular device polynomials (one batched
+    pass, gg_fr_evaluate_many); curve: GG_CURVE_BLS12_381 (default) or GG_CURVE_BN254."""
+    import ctypes as _c
+    from ._lib import GG_CURVE_BLS12_381
+    k = len(polys)
+    for f, n in zip(polys, lens):
+        _need(f, 32 * n, "f")
+    arr = (_c.c_void_p * k)(*[ptr(f).value for f in polys])
+    ln = (_c.c_size_t * k)(*lens)
+    out = bytearray(32 * k)
+    check(lib.gg_fr_evaluate_many(GG_CURVE_BLS12_381 if curve is None else curve, arr, ln, k, ptr(a), ptr(out),
+                                  ptr(stream)))
+    return [bytes(out[32 * i:32 * i + 32]) for i in range(k)]
+
+
 def fold_h(h, n_small: int, zeta_pow_np2: bytes, out, stream=None):
     _need(h, 3 * 32 * (n_small + 2), "h")
     _need(out, 32 * (n_small + 2), "folded h")

@@ -110,13 +110,28 @@ func onAMDDevice(dev int, fn func() error) error {
 	return fn()
 }
 
-// amdPrimaryDevice is the GPU that runs the prover of pk's device key (and
-// holds the GPU solver's L, R, O).
+// amdPrimaryDevice is the GPU a device key created now would run its prover
+// on (the first configured device).  An existing key's GPU is keyPrimaryDevice.
 func amdPrimaryDevice() int {
 	if devs := amdConfiguredDevices(); len(devs) > 0 {
 		return devs[0]
 	}
 	return 0
+}
+
+// keyPrimaryDevice is the GPU that runs h's prover -- where gg_plonk_prove
+// reads device-resident L, R, O -- as recorded when h was created (a later
+// SetAMDDevices does not move it).
+func keyPrimaryDevice(h C.gg_plonk_pk_t) (int, error) {
+	var nd C.int
+	if C.gg_plonk_pk_devices(h, nil, 0, &nd) != C.GG_OK || nd < 1 {
+		return 0, amdError()
+	}
+	devs := make([]C.int, int(nd))
+	if C.gg_plonk_pk_devices(h, &devs[0], nd, &nd) != C.GG_OK {
+		return 0, amdError()
+	}
+	return int(devs[0]), nil
 }
 
 func (pk *ProvingKey) amdKey() (C.gg_plonk_pk_t, error) {
@@ -131,14 +146,24 @@ func (pk *ProvingKey) amdKey() (C.gg_plonk_pk_t, error) {
 	for (uint64(1) << logBig) < pk.Domain[1].Cardinality {
 		logBig++
 	}
+	// The arrays of polynomial pointers live in C memory (ctr, cqcp below), and
+	// cgo forbids storing Go pointers there unless the objects are pinned: pin
+	// every coefficient slice for the duration of gg_plonk_pk_create_ex (the
+	// library copies the polynomials to HBM before it returns).
+	var pin runtime.Pinner
+	defer pin.Unpin()
 	tr := [8]unsafe.Pointer{}
 	for i, p := range []*iop.Polynomial{pk.trace.Ql, pk.trace.Qr, pk.trace.Qm, pk.trace.Qo, pk.trace.Qk,
 		pk.trace.S1, pk.trace.S2, pk.trace.S3} {
-		tr[i] = unsafe.Pointer(&p.Coefficients()[0]) // canonical regular after Setup (setup.go:229-240)
+		c := &p.Coefficients()[0] // canonical regular after Setup (setup.go:229-240)
+		pin.Pin(c)
+		tr[i] = unsafe.Pointer(c)
 	}
 	qcp := make([]unsafe.Pointer, len(pk.trace.Qcp)+1)
 	for i, p := range pk.trace.Qcp {
-		qcp[i] = unsafe.Pointer(&p.Coefficients()[0])
+		c := &p.Coefficients()[0]
+		pin.Pin(c)
+		qcp[i] = unsafe.Pointer(c)
 	}
 	idx := append(pk.Vk.CommitmentConstraintIndexes, 0)
 	vk := make([]curve.G1Affine, 0, 8+len(pk.Vk.Qcp))
@@ -274,7 +299,7 @@ func proveAMD(spr *cs.SparseR1CS, pk *ProvingKey, fullWitness witness.Witness, o
 	var lro [3]unsafe.Pointer
 	onDevice := 0
 	if nCmt == 0 && !userHints && !spr.GkrInfo.Is() {
-		ds, err := pk.amdSolver(spr)
+		ds, err := pk.amdSolver(spr, h)
 		if err != nil {
 			return nil, err
 		}

@@ -78,13 +78,19 @@ func newScsSolver(spr *cs.SparseR1CS) (*scsSolver, error) {
 	return &scsSolver{h: h}, nil
 }
 
-func (pk *ProvingKey) amdSolver(spr *cs.SparseR1CS) (*scsSolver, error) {
+func (pk *ProvingKey) amdSolver(spr *cs.SparseR1CS, h C.gg_plonk_pk_t) (*scsSolver, error) {
 	if s, ok := amdSolvers.Load(pk); ok {
 		return s.(*scsSolver), nil
 	}
 	var s *scsSolver
-	// on the GPU that runs the prover: gg_plonk_prove reads L, R, O there
-	err := onAMDDevice(amdPrimaryDevice(), func() error {
+	// on the GPU that runs the key's prover (gg_plonk_prove reads L, R, O
+	// there): the device the key was created on, not the current
+	// SetAMDDevices / GNARK_AMD_DEVICES choice, which may have changed since
+	dev, err := keyPrimaryDevice(h)
+	if err != nil {
+		return nil, err
+	}
+	err = onAMDDevice(dev, func() error {
 		var err error
 		s, err = newScsSolver(spr)
 		return err

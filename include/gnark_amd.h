@@ -518,6 +518,13 @@ int gg_bls12_381_fr_prefix_product(void *data_dev, size_t n, void *hip_stream);
  * KZG opening quotient (f - f(a)) / (X - a) of kzg.Open (prove.go:646, 823-830). */
 int gg_bls12_381_fr_horner(const void *f_dev, size_t n, const void *a_mont, void *q_dev,
                            void *value_out, void *hip_stream);
+/* values_out[k] (host, count fr) = f_k(a) for count <= 16 device polynomials
+ * (canonical regular, lens[k] coefficients, any lengths) at one point: the
+ * evaluations of a PlonK proof at zeta that need no quotient (prove.go:640-660
+ * the blinded L, R, O and S1, S2, Qcp_i; kzg.BatchOpenSinglePoint's claimed
+ * values), batched into one pass; curve: GG_CURVE_BN254 or GG_CURVE_BLS12_381 fr. */
+int gg_fr_evaluate_many(int curve, const void *const *polys_dev, const size_t *lens, int count,
+                        const void *point_mont, void *values_out, void *hip_stream);
 /* foldH (prove.go:670-705): out[i] = (h3[i]*z + h2[i])*z + h1[i], i < n_small + 2,
  * h_dev = h1 | h2 | h3 (3 (n_small + 2) fr), z = zeta^(n_small + 2) (host). */
 int gg_plonk_fold_h(const void *h_dev, size_t n_small, const void *zeta_pow_np2, void *out_dev,

@@ -130,6 +130,42 @@ def test_horner_and_kzg_quotient_vs_oracle(n):
         assert host(q, n - 1) == bo.divide_by_x_minus_a(f, fa, a)
 
 
+@pytest.mark.parametrize("lens", [[1], [3, 1, 2], [100, 0, 2049], [300000, 262144, 262145, 7, 262143]])
+def test_evaluate_many_vs_oracle(lens):
+    """gg_fr_evaluate_many (the batched evaluations at zeta of prove.go:640-660 and
+    the batch opening's claimed values): every f_k(a) equals Horner's (oracle),
+    lengths around the 2^18-lane grid edge, an empty polynomial gives 0."""
+    from gnark_amd import plonk, DeviceBuffer
+    fs = [rand_vec(n, 500 + i + n) for i, n in enumerate(lens)]
+    a = rand_vec(1, sum(lens))[0]
+    bufs = [dev(f) if f else DeviceBuffer(32) for f in fs]
+    got = plonk.evaluate_many(bufs, lens, bo.fr_to_bytes(a))
+    assert [bo.fr_from_bytes(g) for g in got] == [bo.evaluate(f, a) if f else 0 for f in fs]
+
+
+def test_evaluate_many_bn254_and_2p22():
+    """BN254 fr (backend/plonk/bn254) against a Python Horner, and at 2^22 + 3
+    the batched value equals the scan-based evaluation (gg_bls12_381_fr_horner)."""
+    from gnark_amd import plonk, DeviceBuffer
+    from gnark_amd._lib import GG_CURVE_BN254
+    import bn254_oracle as o
+    rnd = random.Random(12)
+    f = [rnd.randrange(o.R) for _ in range(5000)]
+    a = rnd.randrange(o.R)
+    d = DeviceBuffer.from_host(b"".join(o.fr_to_bytes(x) for x in f))
+    got = plonk.evaluate_many([d], [5000], o.fr_to_bytes(a), curve=GG_CURVE_BN254)[0]
+    acc = 0
+    for c in reversed(f):
+        acc = (acc * a + c) % o.R
+    assert o.fr_from_bytes(got) == acc
+    n = (1 << 22) + 3
+    big = DeviceBuffer.from_host(rand_mont_bytes(n, 8))
+    x = rand_vec(1, 10)[0]
+    v = plonk.evaluate_many([big, big], [n, n - 3], bo.fr_to_bytes(x))
+    assert v[0] == plonk.evaluate(big, n, bo.fr_to_bytes(x))
+    assert v[1] == plonk.evaluate(big, n - 3, bo.fr_to_bytes(x))
+
+
 def test_horner_quotient_property_2p22():
     """At 2^22 + 3 (three scan levels): q(x)(x - a) + f(a) = f(x) at a random x."""
     from gnark_amd import plonk, DeviceBuffer

@@ -24,7 +24,7 @@ fi
 if [[ "$S" == *test* ]]; then
   step 900 pytest_$V.txt python3 -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu \
     tests/test_gpu_dist_h.py tests/test_gpu_groth16_multi.py tests/test_gpu_bls_groth16.py \
-    tests/test_gpu_plonk_prove.py tests/test_gpu_groth16_size.py ${PYTEST_ARGS} || exit 2
+    tests/test_gpu_plonk_poly.py tests/test_gpu_plonk_prove.py tests/test_gpu_groth16_size.py ${PYTEST_ARGS} || exit 2
 fi
 if [[ "$S" == *probe* ]]; then
   step 300 probe_$V.txt python3 -u tools/plonk_part_probe.py 22 8 3 || exit 2
