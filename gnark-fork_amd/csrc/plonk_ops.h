@@ -38,6 +38,19 @@ size_t ratio_arena_bytes(size_t n);
 template <class F>
 void ratio(const F* l, const F* r, const F* o, const int64_t* perm, size_t n, const F& beta, const F& gamma,
            const F& omega, const F& u, F* z, hipStream_t st, Arena& ar);
+// BuildRatioCopyConstraint over the slice [lo, lo + cnt) of the factors
+// f_i = prod_j (f_j[i] + b ID(j n + i) + g) / (f_j[i] + b ID(S[j n + i]) + g):
+// P = their running product inside the slice (P[cnt - 1] = the slice's product).
+// l, r, o, perm0..2 point at the slice's entries.  A device part's share of the
+// ratio; ratio_fixup then writes its slice of Z: z[0] = prefix, z[t + 1] =
+// prefix P[t] (prefix = the product of the factors before lo).
+size_t ratio_range_arena_bytes(size_t n, size_t cnt);
+template <class F>
+void ratio_range(const F* l, const F* r, const F* o, const int64_t* perm0, const int64_t* perm1,
+                 const int64_t* perm2, size_t lo, size_t cnt, size_t n, const F& beta, const F& gamma,
+                 const F& omega, const F& u, F* P, hipStream_t st, Arena& ar);
+template <class F>
+void ratio_fixup(const F* P, size_t cnt, const F& prefix, F* z, hipStream_t st);
 size_t batch_invert_arena_bytes(size_t n);
 template <class F>
 void batch_invert(F* a, size_t n, hipStream_t st, Arena& ar);

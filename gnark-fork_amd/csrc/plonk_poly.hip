@@ -544,6 +544,80 @@ void lincomb(F* out, size_t n_out, const F* const* f, const size_t* len, const F
     GG_HIP(hipGetLastError());
 }
 
+// ---------------------------------------------------------------- ratio over a slice
+template <class F>
+__global__ void __launch_bounds__(256) k_ratio_factors(const F* L, const F* R, const F* O, const int64_t* p0,
+                                                       const int64_t* p1, const int64_t* p2, uint32_t lo, uint32_t cnt,
+                                                       int log_n, F beta, F gamma, F u, F uu, PowSplit<F> w, F* num,
+                                                       F* den) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const uint32_t i = lo + t, nmask = (1u << log_n) - 1;
+    const F* f[3] = {L, R, O};
+    const int64_t* pm[3] = {p0, p1, p2};
+    const F wi = w.at(i);
+    F b = F::one(), d = F::one();
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const F fv = ldb(f[j] + t);
+        F id = j == 0 ? wi : (j == 1 ? wi * u : wi * uu);
+        b = b * (fv + beta * id + gamma);
+        const uint64_t s = (uint64_t)pm[j][t];
+        const uint32_t blk = (uint32_t)(s >> log_n), off = (uint32_t)(s & nmask);
+        F sg = w.at(off);
+        if (blk == 1) sg = sg * u;
+        else if (blk == 2) sg = sg * uu;
+        d = d * (fv + beta * sg + gamma);
+    }
+    stb(num + t, b);
+    stb(den + t, d);
+}
+
+template <class F>
+__global__ void k_ratio_fixup(const F* P, size_t cnt, F prefix, F* z) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    stb(z + t, t ? prefix * ldb(P + t - 1) : prefix);
+}
+
+size_t ratio_range_arena_bytes(size_t n, size_t cnt) {
+    const int L = log2_ceil(n), S = (L + 1) / 2;
+    const size_t tabs = (((size_t)1 << S) + ((size_t)1 << (L - S))) * 32 + 512;
+    return tabs + ((cnt * 32 + 255) & ~(size_t)255) + batch_invert_arena_bytes(cnt) + scan_arena_bytes(cnt) + 1024;
+}
+
+template <class F>
+void ratio_range(const F* l, const F* r, const F* o, const int64_t* perm0, const int64_t* perm1,
+                 const int64_t* perm2, size_t lo, size_t cnt, size_t n, const F& beta, const F& gamma,
+                 const F& w, const F& u, F* P, hipStream_t st, Arena& ar) {
+    if (!cnt) return;
+    const int L = log2_ceil(n);
+    const int S = (L + 1) / 2;
+    const uint32_t nlo = 1u << S, nhi = 1u << (L - S);
+    F* tlo = ar.get<F>(nlo);
+    F* thi = ar.get<F>(nhi);
+    F step = w;
+    for (int i = 0; i < S; i++) step = step * step;  // w^(2^S)
+    hipLaunchKernelGGL(k_pow_split<F>, dim3(grid_for(std::max(nlo, nhi), 256)), dim3(256), 0, st, w, step, tlo, nlo,
+                       thi, nhi);
+    GG_HIP(hipGetLastError());
+    F* den = ar.get<F>(cnt);
+    hipLaunchKernelGGL(k_ratio_factors<F>, dim3(grid_for(cnt, 256)), dim3(256), 0, st, l, r, o, perm0, perm1, perm2,
+                       (uint32_t)lo, (uint32_t)cnt, L, beta, gamma, u, u * u, PowSplit<F>{thi, tlo, S}, P, den);
+    GG_HIP(hipGetLastError());
+    batch_invert(den, cnt, st, ar);
+    hipLaunchKernelGGL(k_mul_inplace<F>, dim3(grid_for(cnt, 256)), dim3(256), 0, st, P, (const F*)den, cnt);
+    GG_HIP(hipGetLastError());
+    scan_prod(P, cnt, st, ar);
+}
+
+template <class F>
+void ratio_fixup(const F* P, size_t cnt, const F& prefix, F* z, hipStream_t st) {
+    if (!cnt) return;
+    hipLaunchKernelGGL(k_ratio_fixup<F>, dim3(grid_for(cnt, 256)), dim3(256), 0, st, P, cnt, prefix, z);
+    GG_HIP(hipGetLastError());
+}
+
 template <class F>
 void fold_h(const F* h, size_t n_small, const F& zz, F* out, hipStream_t st) {
     const size_t np2 = n_small + 2;
@@ -592,6 +666,10 @@ void shift_copy(const F* in, F* out, size_t n, hipStream_t st) {
     template void horner<F>(const F*, size_t, const F&, F*, F*, hipStream_t, Arena&);                          \
     template void eval_many<F>(const F* const*, const size_t*, int, const F&, F*, hipStream_t, Arena&);          \
     template void lincomb<F>(F*, size_t, const F* const*, const size_t*, const F*, int, hipStream_t);           \
+    template void ratio_range<F>(const F*, const F*, const F*, const int64_t*, const int64_t*, const int64_t*,    \
+                                 size_t, size_t, size_t, const F&, const F&, const F&, const F&, F*, hipStream_t,  \
+                                 Arena&);                                                                          \
+    template void ratio_fixup<F>(const F*, size_t, const F&, F*, hipStream_t);                                  \
     template void ratio<F>(const F*, const F*, const F*, const int64_t*, size_t, const F&, const F&, const F&, \
                            const F&, F*, hipStream_t, Arena&);                                                  \
     template void fold_h<F>(const F*, size_t, const F&, F*, hipStream_t);                                       \

@@ -169,6 +169,8 @@ struct PlonkPeer {
     MsmWork* work[3] = {nullptr, nullptr, nullptr};
     DevBuf scal[3];                     // scalar slice staging per work slot
     std::vector<std::unique_ptr<QUnit>> units;  // quotient units placed here
+    DevBuf perm_slice, pz;              // S of its KzgLagrange slice (3 columns), its ratio scan
+    Arena ar;                           // ratio scratch
     DevBuf tw0, in[5 + plk::MAX_CMT];   // twiddles0 (S = 1); L R O Z (canonical bit-reversed), Qk, Pi_j
     DevBuf cev[7 + plk::MAX_CMT], zc;   // a unit's evaluation slot; ZS (S > 1)
     hipEvent_t ea[4] = {}, eb[4] = {};  // per stream: around the last peer copy (timing)
@@ -186,6 +188,9 @@ struct PlonkPeer {
         for (auto& b : cev) b.release();
         zc.release();
         tw0.release();
+        perm_slice.release();
+        pz.release();
+        ar.buf.release();
         for (hipStream_t x : s)
             if (x) (void)hipStreamDestroy(x);
         for (int i = 0; i < 4; i++) {
@@ -201,6 +206,7 @@ struct PlonkPartTimes {
     double msm_count = 0, msm_ms = 0, scalar_copy_ms = 0, scalar_mb = 0;
     double coset_count = 0, coset_ms = 0, coset_in_copy_ms = 0, coset_out_copy_ms = 0, coset_mb = 0;
     double wait_ms = 0;  // part 0: time spent waiting for the peers' MSM slices and cosets
+    double ratio_ms = 0;  // its slice of the copy-constraint ratio (factors, scan, fix-up)
 };
 
 // ============================================================== prover of one curve
@@ -357,7 +363,7 @@ struct Key : gg_plonk_pk {
     MsmWork* work[3] = {nullptr, nullptr, nullptr};
     Arena ar[4];
     // per-proof buffers
-    DevBuf lag[3], can[4], cbrev[4], zlag, qkc, pi_reg[plk::MAX_CMT], pi_brev[plk::MAX_CMT];
+    DevBuf lag[3], can[4], cbrev[4], zlag, pz, qkc, pi_reg[plk::MAX_CMT], pi_brev[plk::MAX_CMT];
     DevBuf cev[2][7 + plk::MAX_CMT], zc[2];  // unit evaluation slots (two units in flight), ZS (S > 1)
     DevBuf cres, hpad[3], bz, bl[3], fold, lin, q1, q2, vals, pad;
     int device = 0;
@@ -431,14 +437,16 @@ static void record_wait(Key* pk, hipStream_t from, hipStream_t to) {
 static double ms_since(std::chrono::steady_clock::time_point a) {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
 }
-static BJac peer_msm(Key* pk, int part, PlonkPeer* p, bool kzg, int wi, const FrB* scal) {
+// (resident: the slice is already in the peer's slot, e.g. its slice of Z)
+static BJac peer_msm(Key* pk, int part, PlonkPeer* p, bool kzg, int wi, const FrB* scal, bool resident = false) {
     GG_HIP(hipSetDevice(p->device));
     const size_t lo = kzg ? p->k_lo : p->l_lo, hi = kzg ? p->k_hi : p->l_hi;
     BJac j = BJac::inf();
     if (hi == lo) return j;
     const auto a = std::chrono::steady_clock::now();
     GG_HIP(hipEventRecord(p->ea[wi], p->s[wi]));
-    GG_HIP(hipMemcpyPeerAsync(p->scal[wi].p, p->device, scal + lo, pk->device, 32 * (hi - lo), p->s[wi]));
+    if (!resident)
+        GG_HIP(hipMemcpyPeerAsync(p->scal[wi].p, p->device, scal + lo, pk->device, 32 * (hi - lo), p->s[wi]));
     GG_HIP(hipEventRecord(p->eb[wi], p->s[wi]));
     msm_device_work(kzg ? p->kzg : p->kzg_lag, p->work[wi], p->scal[wi].as<Fr>(), &j, p->s[wi]);
     float cp = 0;
@@ -449,13 +457,14 @@ static BJac peer_msm(Key* pk, int part, PlonkPeer* p, bool kzg, int wi, const Fr
     T.msm_count += 1;
     T.msm_ms += ms_since(a);
     T.scalar_copy_ms += cp;
-    T.scalar_mb += 32.0 * (hi - lo) / 1e6;
+    if (!resident) T.scalar_mb += 32.0 * (hi - lo) / 1e6;
     return j;
 }
 static bool plonk_solo(Key* pk) { return pk->solo; }
 // this rank's partial MSM (the whole MSM on one GPU, or split over the key's
 // device parts and summed here); red() completes a process shard's partial
-static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStream_t st) {
+static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStream_t st,
+                    bool peer_resident = false) {
     BJac j = BJac::inf();
     const bool kz = base == pk->kzg;
     const size_t lo = kz ? pk->k_lo : pk->l_lo;
@@ -463,8 +472,8 @@ static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStr
     if (!pk->peers.empty() && !plonk_solo(pk)) {
         GG_HIP(hipStreamSynchronize(st));  // the scalars are complete before the peers copy them
         for (size_t q = 0; q < pk->peers.size(); q++)
-            fs.push_back(std::async(std::launch::async, [pk, q, pp = pk->peers[q].get(), kz, wi, scal] {
-                return peer_msm(pk, (int)q + 1, pp, kz, wi, scal);
+            fs.push_back(std::async(std::launch::async, [pk, q, pp = pk->peers[q].get(), kz, wi, scal, peer_resident] {
+                return peer_msm(pk, (int)q + 1, pp, kz, wi, scal, peer_resident);
             }));
     }
     const auto a = std::chrono::steady_clock::now();
@@ -760,6 +769,19 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
         GG_HIP(hipStreamSynchronize(qs));
         (peer ? peer->units : pk->units).push_back(std::move(up_));
     }
+    // peers: the permutation's columns over their KzgLagrange slice, for their share of the ratio
+    for (auto& pp : pk->peers) {
+        PlonkPeer* p = pp.get();
+        const size_t cnt = p->l_hi - p->l_lo;
+        if (!cnt) continue;
+        GG_HIP(hipSetDevice(p->device));
+        p->perm_slice.alloc(3 * cnt * 8);
+        for (int j = 0; j < 3; j++)
+            up(p->perm_slice.as<int64_t>() + j * cnt, perm + (size_t)j * n + p->l_lo, cnt * 8, false, p->s[0]);
+        p->pz.alloc(32 * cnt);
+        p->ar.reserve(plk::ratio_range_arena_bytes(n, cnt) + 65536);
+        GG_HIP(hipStreamSynchronize(p->s[0]));
+    }
     GG_HIP(hipSetDevice(pk->device));
     pk->perm.alloc(3 * n * 8);
     up(pk->perm.p, perm, 3 * n * 8, false, st);
@@ -768,6 +790,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
     for (auto& b : pk->can) b.alloc(nb);
     for (auto& b : pk->cbrev) b.alloc(nb);
     pk->zlag.alloc(nb);
+    pk->pz.alloc(nb);
     pk->qkc.alloc(nb);
     for (int i = 0; i < n_cmt; i++) {
         pk->pi_reg[i].alloc(nb);
@@ -905,14 +928,69 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     }
     const FrB gamma = derive(fs, "gamma", {&P.lro[0], &P.lro[1], &P.lro[2]});
     const FrB beta = fs.compute("beta");
-    // ---- ratio Z (buildRatioCopyConstraint, prove.go:600-632) + its commitment
+    // ---- ratio Z (buildRatioCopyConstraint, prove.go:600-632) + its commitment.
+    // With device parts every part takes the factors of its KzgLagrange slice
+    // [l_lo, l_hi) (its L, R, O slices are still in its scalar slots from
+    // commitToLRO) and scans them; the slice products are chained here and each
+    // part writes its slice of Z where its share of the Z commitment reads it
+    // (and into the primary's Z for the rest of the proof).
     for (int k = 0; k < 3; k++) record_wait(pk, s[k], s[0]);
-    pk->ar[0].reset();
-    plk::ratio(F(pk->lag[0]), F(pk->lag[1]), F(pk->lag[2]), pk->perm.template as<int64_t>(), n, beta, gamma, pk->omega,
-               pk->u, F(pk->zlag), s[0], pk->ar[0]);
+    const bool dz = !pk->peers.empty();
+    const bool peers_on = dz && !plonk_solo(pk);
+    {
+        const size_t zlo = dz ? pk->l_lo : 0, zcnt = dz ? pk->l_hi - pk->l_lo : n;
+        const auto ta = std::chrono::steady_clock::now();
+        const int64_t* pm = pk->perm.template as<int64_t>();
+        pk->ar[0].reset();
+        plk::ratio_range(F(pk->lag[0]) + zlo, F(pk->lag[1]) + zlo, F(pk->lag[2]) + zlo, pm + zlo, pm + n + zlo,
+                         pm + 2 * n + zlo, zlo, zcnt, n, beta, gamma, pk->omega, pk->u, F(pk->pz), s[0], pk->ar[0]);
+        std::vector<FrB> agg(1 + pk->peers.size(), FrB::one());
+        std::vector<std::future<void>> pf;
+        if (peers_on)
+            for (size_t q = 0; q < pk->peers.size(); q++)
+                pf.push_back(std::async(std::launch::async, [&, q] {
+                    PlonkPeer* p = pk->peers[q].get();
+                    const size_t cnt = p->l_hi - p->l_lo;
+                    if (!cnt) return;
+                    GG_HIP(hipSetDevice(p->device));
+                    const auto a = std::chrono::steady_clock::now();
+                    p->ar.reset();
+                    const int64_t* ps = p->perm_slice.as<int64_t>();
+                    plk::ratio_range(F(p->scal[0]), F(p->scal[1]), F(p->scal[2]), ps, ps + cnt, ps + 2 * cnt, p->l_lo,
+                                     cnt, n, beta, gamma, pk->omega, pk->u, F(p->pz), p->s[0], p->ar);
+                    agg[q + 1] = fetch(F(p->pz) + cnt - 1, p->s[0]);
+                    std::lock_guard<std::mutex> lk(pk->tmu);
+                    pk->ptimes[q + 1].ratio_ms += ms_since(a);
+                }));
+        agg[0] = zcnt ? fetch(F(pk->pz) + zcnt - 1, s[0]) : FrB::one();
+        for (auto& f : pf) f.get();
+        // prefix of part r = the product of the factors of the slices before it
+        std::vector<FrB> pre(agg.size(), FrB::one());
+        for (size_t r = 1; r < agg.size(); r++) pre[r] = pre[r - 1] * agg[r - 1];
+        plk::ratio_fixup(F(pk->pz), zcnt, pre[0], F(pk->zlag) + zlo, s[0]);
+        pf.clear();
+        if (peers_on)
+            for (size_t q = 0; q < pk->peers.size(); q++)
+                pf.push_back(std::async(std::launch::async, [&, q] {
+                    PlonkPeer* p = pk->peers[q].get();
+                    const size_t cnt = p->l_hi - p->l_lo;
+                    if (!cnt) return;
+                    GG_HIP(hipSetDevice(p->device));
+                    const auto a = std::chrono::steady_clock::now();
+                    plk::ratio_fixup(F(p->pz), cnt, pre[q + 1], F(p->scal[0]), p->s[0]);  // the Z slot of its MSM
+                    GG_HIP(hipMemcpyPeerAsync(F(pk->zlag) + p->l_lo, pk->device, p->scal[0].p, p->device, 32 * cnt,
+                                              p->s[0]));
+                    GG_HIP(hipStreamSynchronize(p->s[0]));
+                    std::lock_guard<std::mutex> lk(pk->tmu);
+                    pk->ptimes[q + 1].ratio_ms += ms_since(a);
+                }));
+        for (auto& f : pf) f.get();
+        std::lock_guard<std::mutex> lk(pk->tmu);
+        pk->ptimes[0].ratio_ms += ms_since(ta);
+    }
     record_wait(pk, s[0], s[1]);
     lag_to_canonical(pk, F(pk->zlag), F(pk->cbrev[3]), F(pk->can[3]), s[1]);  // overlaps the Z commitment
-    P.z = to_aff(jac_add(red(pk, msm_jac(pk, pk->kzg_lag, 0, F(pk->zlag), s[0])), fblind[3].get()));
+    P.z = to_aff(jac_add(red(pk, msm_jac(pk, pk->kzg_lag, 0, F(pk->zlag), s[0], peers_on)), fblind[3].get()));
     mark();
     // ---- alpha (deriveAlpha, prove.go:504-512)
     P.bsb22.assign(cmt_digests, cmt_digests + n_cmt);
@@ -1503,9 +1581,10 @@ extern "C" int gg_plonk_pk_part_timings(gg_plonk_pk_t pk, int part, double* out,
         if (part >= (int)k->ptimes.size()) return 0;  // no proof yet
         std::lock_guard<std::mutex> lt(k->tmu);
         const PlonkPartTimes& T = k->ptimes[part];
-        const double v[10] = {T.msm_count, T.msm_ms,   T.scalar_copy_ms,    T.scalar_mb,         T.coset_count,
-                              T.coset_ms,  T.coset_in_copy_ms, T.coset_out_copy_ms, T.coset_mb, T.wait_ms};
-        for (int i = 0; i < 10; i++) out[i] = v[i];
+        const double v[11] = {T.msm_count, T.msm_ms,   T.scalar_copy_ms,    T.scalar_mb,         T.coset_count,
+                              T.coset_ms,  T.coset_in_copy_ms, T.coset_out_copy_ms, T.coset_mb, T.wait_ms,
+                              T.ratio_ms};
+        for (int i = 0; i < 11; i++) out[i] = v[i];
         return 0;
     });
     GG_CAPI_END
