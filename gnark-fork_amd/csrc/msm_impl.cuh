@@ -221,7 +221,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                                                      const uint32_t* offsets, uint32_t nb, int c,
                                                      uint32_t K, int skip_inf, typename PartialOf<F>::T* head,
                                                      typename PartialOf<F>::T* tail, typename PartialOf<F>::T* S,
-                                                     uint32_t* tbucket) {
+                                                     uint32_t* tbucket, uint32_t pmask) {
     const uint32_t E = offsets[nb];
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t e0w = (uint64_t)t * K;
@@ -248,12 +248,12 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
         using C = typename RadixOf<F>::C;
         XyzzL<C> acc = inf_l<C>();
         uint32_t v = sorted[e0], vn = (e0 + 1 < e1) ? sorted[e0 + 1] : 0u;
-        Affine<F> p = ld(pts + (v & 0x7fffffffu));
+        Affine<F> p = ld(pts + (v & pmask));
         for (uint32_t e = e0; e < e1; e++) {
             Affine<F> qp = p;
             const uint32_t cv = v;
             if (e + 1 < e1) {
-                p = ld(pts + (vn & 0x7fffffffu));
+                p = ld(pts + (vn & pmask));
                 v = vn;
                 if (e + 2 < e1) vn = sorted[e + 2];
             }
@@ -283,7 +283,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                 do { q++; bnd = bnd2; bnd2 = offsets[min(q + 2, nb)]; } while (bnd == e);
             }
             const uint32_t v = sorted[e];
-            const Affine<F> pt = ld(pts + (v & 0x7fffffffu));
+            const Affine<F> pt = ld(pts + (v & pmask));
             if (skip_inf && pt.is_inf()) continue;
             const Fp2_29 x{unpack29(pt.x.a0), unpack29(pt.x.a1)};
             Fp2_29 y{unpack29(pt.y.a0), unpack29(pt.y.a1)};
@@ -298,12 +298,12 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
         if constexpr (sizeof(F) <= 32) {
             // G1: software pipeline, the next point is in flight while this one is added
             uint32_t v = sorted[e0], vn = (e0 + 1 < e1) ? sorted[e0 + 1] : 0u;
-            Affine<F> p = ld(pts + (v & 0x7fffffffu));
+            Affine<F> p = ld(pts + (v & pmask));
             for (uint32_t e = e0; e < e1; e++) {
                 Affine<F> qp = p;
                 const uint32_t cv = v;
                 if (e + 1 < e1) {
-                    p = ld(pts + (vn & 0x7fffffffu));
+                    p = ld(pts + (vn & pmask));
                     v = vn;
                     if (e + 2 < e1) vn = sorted[e + 2];
                 }
@@ -327,7 +327,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                     do { q++; bnd = bnd2; bnd2 = offsets[min(q + 2, nb)]; } while (bnd == e);
                 }
                 const uint32_t v = sorted[e];
-                Affine<F> p = ld(pts + (v & 0x7fffffffu));
+                Affine<F> p = ld(pts + (v & pmask));
                 if (skip_inf && p.is_inf()) continue;
                 if (v >> 31) p.y = -p.y;
                 xyzz_madd_inplace(acc, p);
@@ -1094,9 +1094,13 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
         // per-group names: the Groth16 prove runs G1 and G2 accumulations at once
         const char* acc_name = sizeof(F) == sizeof(Fp) ? "msm_accum" : (sizeof(F) == sizeof(Fp2) ? "msm_accum_g2" : "msm_accum_bls");
         ProfScope ps_acc(acc_name, st, (double)n);
+        // GG_ACCUM_PROBE=1 (traffic attribution only, wrong sums): every entry reads
+        // one of the first 1024 points, so HBM sees everything but the point gathers
+        const char* probe = getenv("GG_ACCUM_PROBE");
+        const uint32_t pmask = probe && atoi(probe) ? 1023u : 0x7fffffffu;
         hipLaunchKernelGGL(k_accum_range<F>, dim3(grid_for(T, 256)), dim3(256), 0, st, (const Affine<F>*)b->pts.p,
                            s->sorted.as<uint32_t>(), offs, (uint32_t)nb, ce, K, (int)b->has_inf, hP, tP, SP,
-                           scr->tbucket.as<uint32_t>());
+                           scr->tbucket.as<uint32_t>(), pmask);
         GG_HIP(hipGetLastError());
         ps_acc.stop(st);
     }

@@ -79,3 +79,26 @@ def test_proof_raw_encoding_matches_oracle():
     g = golden()["groth16"][0]
     pr = groth16.Proof(b(g["Ar"]), b(g["Bs"]), b(g["Krs"]))
     assert pr.write_raw()[:256].hex() == g["raw_prefix"]
+
+
+def test_multi_gpu_timing_and_rehearsal_abi():
+    """The N-GPU instrumentation and rehearsal entry points (no GPU needed: the
+    argument checks run first): slot counts agree between header and binding,
+    null handles / short buffers / bad shards are GG_ERR_INVALID_ARG, and
+    GG_REHEARSAL is distinct from every error code."""
+    from gnark_amd import _lib
+    src = open(os.path.join(ROOT, "include", "gnark_amd.h")).read()
+    consts = dict(re.findall(r"#define (GG_[A-Z0-9_]+) ([0-9]+)\b", src))
+    assert int(consts["GG_REHEARSAL"]) == _lib.GG_REHEARSAL == 7
+    assert int(consts["GG_PLONK_PART_SLOTS"]) == _lib.GG_PLONK_PART_SLOTS
+    assert 2 + 4 * int(consts["GG_MPK_MAX_EXCHANGES"]) == _lib.GG_MPK_TIMING_SLOTS
+    errs = {int(v) for k, v in consts.items() if k.startswith("GG_ERR_")}
+    assert _lib.GG_REHEARSAL not in errs and _lib.GG_REHEARSAL != _lib.GG_OK
+    buf = (ctypes.c_double * 32)()
+    L = _lib.lib
+    assert L.gg_groth16_mpk_shard_timings(None, 0, buf, 32) == 1
+    assert L.gg_groth16_mpk_set_rehearsal(None, 0) == 1
+    assert L.gg_plonk_pk_part_timings(None, 0, buf, 32) == 1
+    assert L.gg_plonk_pk_set_rehearsal(None, 1) == 1
+    assert L.gg_hshard_exchange_bytes(None, 1, ctypes.byref(ctypes.c_size_t())) == 1
+    assert b"null" in L.gg_last_error()

@@ -16,10 +16,16 @@ step() {  # step <secs> <log> cmd...
   echo "=== rc=$rc $(date +%T)" >> gpurun_out/progress_$V.txt
   return $rc
 }
-S="${STEPS:-calib,test,probe}"
+S="${STEPS:-calib,r29,test,probe}"
 if [[ "$S" == *calib* ]]; then
   step 120 calib_stdout_$V.txt tools/mbench_gather_calib 16 || exit 2
   step 120 calib_pmc_$V.txt timeout -s KILL 110 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/calib_$V -o run -- tools/mbench_gather_calib 16 || exit 2
+fi
+if [[ "$S" == *r29* ]]; then  # the radix-2^29 BN254 fr passes (opt-in until measured)
+  step 300 pytest_r29_$V.txt env GG_NTT_R29=1 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu \
+    tests/test_gpu_ntt.py tests/test_gpu_dist_h.py -k "not bls" || exit 2
+  step 200 ntt_r29_$V.txt env GG_NTT_R29=1 python3 -u tools/bench_ntt.py || exit 2
+  step 200 ntt_r32_$V.txt python3 -u tools/bench_ntt.py || exit 2
 fi
 if [[ "$S" == *test* ]]; then
   step 900 pytest_$V.txt python3 -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu \
