@@ -547,7 +547,7 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     s->keys.reserve(total * 4);
     s->tmp_entry.reserve(total * 4);
     s->tmp_key.reserve(total * 4);
-    s->sorted.reserve(total * 4);
+    s->sorted.reserve(total * 4 + 64);  // + 64: the accumulation reads 16-B chunks past its last entry
     s->hist.reserve(nh * 4);
     s->hoff.reserve((nh + 1) * 4);
     s->bin_start.reserve(((size_t)nb + 1) * 4);
@@ -683,7 +683,7 @@ void msm_prepare_derived(const gg_msm_base* a, const MsmSort* sa, const gg_msm_b
     sb->ensure_events();
     sb->keys.reserve(std::max<size_t>(cap, 1) * 4);           // flags
     sb->tmp_entry.reserve((std::max<size_t>(cap, 1) + 1) * 4);  // kept positions (+ the total)
-    sb->sorted.reserve(std::max<size_t>((size_t)b->W * b->n, 1) * 4);
+    sb->sorted.reserve(std::max<size_t>((size_t)b->W * b->n, 1) * 4 + 64);  // 16-B chunk reads
     sb->offsets.reserve((nb + 1) * 4);
     sb->maxcnt.reserve(4);
     GG_HIP(hipStreamWaitEvent(st, sa->ready_ev, 0));

@@ -216,6 +216,14 @@ constexpr int kAccumWaves = (GG_G2_WAVES1 && std::is_same<F, Fp2>::value) || std
                                 ? 1
                                 : (std::is_same<F, Fp>::value ? GG_G1_WAVES : 2);
 
+// entry k (0..3) of a 16-B chunk of sorted entries held in registers
+__device__ __forceinline__ uint32_t chunk_at(const uint4& c, uint32_t k) {
+    return k == 0 ? c.x : (k == 1 ? c.y : (k == 2 ? c.z : c.w));
+}
+__device__ __forceinline__ uint4 chunk_ld(const uint32_t* sorted, uint32_t base4) {
+    return *reinterpret_cast<const uint4*>(sorted + base4);
+}
+
 template <class F>
 __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affine<F>* pts, const uint32_t* sorted,
                                                      const uint32_t* offsets, uint32_t nb, int c,
@@ -247,7 +255,12 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
         // 14 x 28 bits); the base holds x R' mod p, partials leave in radix form
         using C = typename RadixOf<F>::C;
         XyzzL<C> acc = inf_l<C>();
-        uint32_t v = sorted[e0], vn = (e0 + 1 < e1) ? sorted[e0 + 1] : 0u;
+        // The sorted entries come in 16-B chunks (four per load, the chunk of
+        // entry j loaded when j reaches it): each lane walks its own range, so
+        // one 4-B load per entry re-fetched a whole line whenever the point
+        // gathers had evicted it in between (traffic)
+        uint4 ch = chunk_ld(sorted, (e0 + 1) & ~3u);
+        uint32_t v = sorted[e0], vn = (e0 + 1 < e1) ? chunk_at(ch, (e0 + 1) & 3u) : 0u;
         Affine<F> p = ld(pts + (v & pmask));
         for (uint32_t e = e0; e < e1; e++) {
             Affine<F> qp = p;
@@ -255,7 +268,11 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
             if (e + 1 < e1) {
                 p = ld(pts + (vn & pmask));
                 v = vn;
-                if (e + 2 < e1) vn = sorted[e + 2];
+                if (e + 2 < e1) {
+                    const uint32_t j = e + 2;
+                    if ((j & 3u) == 0) ch = chunk_ld(sorted, j);
+                    vn = chunk_at(ch, j & 3u);
+                }
             }
             if (e == bnd) {
                 range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
@@ -275,6 +292,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
     if constexpr (std::is_same<F, Fp2>::value) {
         // BN254 G2: radix-2^29 Fp2 accumulator (field29.cuh), base in x * 2^261 form
         Xyzz2_29 acc = inf2_29();
+        // (one 4-B entry load per point here: a 16-B chunk in registers spills at 2 waves)
         for (uint32_t e = e0; e < e1; e++) {
             if (e == bnd) {
                 range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);

@@ -19,7 +19,6 @@
 //     den = 1/(g^n - 1) into the final inverse-transform scaling.
 #include "common.h"
 #include "field.cuh"
-#include "field29.cuh"
 #include "prof.h"
 #include <vector>
 #include <mutex>
@@ -334,171 +333,6 @@ __global__ void __launch_bounds__(kNttThreads<MAXNB>, kNttWaves<MAXNB>) k_ntt_pa
     }
 }
 
-// ---- BN254 fr passes in 9 x 29-bit limbs (field29.cuh), GG_NTT_R29 ---------
-// The 32-bit-limb butterfly spends a v_addc per v_mad_u64_u32 (the column
-// carry) plus compare/select chains keeping values below 2r: ~400 VALU
-// instructions per butterfly, issue-bound.  Here a value is gnark's x 2^256
-// (Montgomery, R = 2^256) unpacked into 9 limbs of 29 bits; the stage twiddles
-// are stored as w 2^261 (tw29), so the radix-2^29 Montgomery product
-// (x 2^256)(w 2^261) / 2^261 = x w 2^256 keeps the representation: 162
-// v_mad_u64_u32 and no carry chain (M = 2^261 = 169.28 r).  Bounds:
-//   DIT  t = y w < y / 169 + r;  x + t, x + 3r - t: the magnitude grows by < 3r
-//        per stage, the limbs by < 2^30 (renormalised at every LDS write), and
-//        the pass end reduces (< 2r, reduce_small) before packing;
-//   DIF  x + y doubles per stage: the sum is renormalised and reduced below 2r
-//        at every stage, so x + 3r - y always has a normalised y < 2r.
-// Results are the same field elements as the 32-bit path (exact arithmetic).
-struct Fr29Cfg {
-    using Std = FrCfg;
-    static constexpr int N = 9;
-    static constexpr int B = 29;
-    static constexpr uint32_t MASK = (1u << B) - 1;
-    static constexpr uint32_t P[9] = {0x10000001u, 0x1f0fac9fu, 0x0e5c2450u, 0x07d090f3u, 0x1585d283u,
-                                      0x02db40c0u, 0x00a6e141u, 0x0e5c2634u, 0x0030644eu};
-    static constexpr uint32_t INV = 0x0fffffffu;   // -r^-1 mod 2^29
-    static constexpr uint32_t PINV = 0x10000001u;  // r^-1 mod 2^29
-    // 2^261 mod r in the gnark 32-bit layout: mont256(x 2^256, C_IN) = x 2^261
-    static constexpr uint32_t C_IN[8] = {0x8fffff57u, 0x2fd4e156u, 0xa494b01au, 0x75bba827u,
-                                         0x819caa80u, 0x5301fa84u, 0x563d4475u, 0x0dc83629u};
-    // k r (k = 1..8) with limbs 0..7 borrowed into [2^29, 2^30) (tools/gen_field29.py)
-    static constexpr uint32_t KP[8][9] = {
-        {0x30000001u, 0x3f0fac9eu, 0x2e5c244fu, 0x27d090f2u, 0x3585d282u, 0x22db40bfu, 0x20a6e140u, 0x2e5c2633u, 0x0030644du},
-        {0x20000002u, 0x3e1f593eu, 0x3cb848a0u, 0x2fa121e5u, 0x2b0ba505u, 0x25b68180u, 0x214dc281u, 0x3cb84c67u, 0x0060c89bu},
-        {0x30000003u, 0x3d2f05ddu, 0x2b146cf1u, 0x3771b2d9u, 0x20917788u, 0x2891c241u, 0x21f4a3c2u, 0x2b14729bu, 0x00912ceau},
-        {0x20000004u, 0x3c3eb27du, 0x39709142u, 0x3f4243ccu, 0x36174a0bu, 0x2b6d0301u, 0x229b8503u, 0x397098cfu, 0x00c19138u},
-        {0x30000005u, 0x3b4e5f1cu, 0x27ccb593u, 0x2712d4c0u, 0x2b9d1c8fu, 0x2e4843c2u, 0x23426644u, 0x27ccbf03u, 0x00f1f587u},
-        {0x20000006u, 0x3a5e0bbcu, 0x3628d9e4u, 0x2ee365b3u, 0x2122ef12u, 0x31238483u, 0x23e94785u, 0x3628e537u, 0x012259d5u},
-        {0x30000007u, 0x396db85bu, 0x2484fe35u, 0x36b3f6a7u, 0x36a8c195u, 0x33fec543u, 0x249028c6u, 0x24850b6bu, 0x0152be24u},
-        {0x20000008u, 0x387d64fbu, 0x32e12286u, 0x3e84879au, 0x2c2e9418u, 0x36da0604u, 0x25370a07u, 0x32e1319fu, 0x01832272u}};
-};
-using Fr29 = Fl<Fr29Cfg>;
-
-template <int NB, bool DIT>
-__device__ __forceinline__ void ntt_round29(const PassParams<Fr>& P, uint32_t* lds, int TP, int T, int qlo,
-                                            bool first, bool last, uint32_t base_hi, uint32_t lo0) {
-    constexpr int R = 1 << NB;
-    const int tl = P.tl;
-    const uint32_t tl_mask = (1u << tl) - 1;
-    const int pos = qlo + tl;
-    const uint32_t lowmask = (1u << pos) - 1;
-    const int groups = T >> NB;
-    for (int gi = threadIdx.x; gi < groups; gi += blockDim.x) {
-        uint32_t e[R], g[R];
-        Fr29 x[R];
-        const uint32_t low = (uint32_t)gi & lowmask, high = ((uint32_t)gi >> pos) << (pos + NB);
-#pragma unroll
-        for (int m = 0; m < R; m++) {
-            e[m] = high | ((uint32_t)m << pos) | low;
-            g[m] = base_hi | ((e[m] >> tl) << P.b_lo) | (lo0 + (e[m] & tl_mask));
-        }
-        if (first) {
-#pragma unroll
-            for (int m = 0; m < R; m++) {
-                Fr v = load_fr(P.in + g[m]);  // < 2r (lazy) or canonical
-                if (P.has_pre) v = apply_scale(P.pre, g[m], P.log_n, v);
-                x[m] = unpack_l<Fr29Cfg>(v);
-            }
-        } else {
-#pragma unroll
-            for (int m = 0; m < R; m++) {
-#pragma unroll
-                for (int l = 0; l < 9; l++) x[m].l[l] = lds[l * TP + lidx((int)e[m])];
-            }
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < NB; s2++) {
-            const int r = DIT ? s2 : (NB - 1 - s2);
-            const int b = P.b_lo + qlo + r;
-            const uint32_t bmask = (1u << b) - 1;
-            const Fr* twb = P.tw + bmask;  // stage-b table (w 2^261 form) starts at 2^b - 1
-#pragma unroll
-            for (int m = 0; m < R; m++) {
-                if (m & (1 << r)) continue;
-                const int m2 = m | (1 << r);
-                const Fr29 w = unpack_l<Fr29Cfg>(load_fr(twb + (g[m] & bmask)));
-                if (DIT) {
-                    const Fr29 tt = mul(x[m2], w);  // < y / 169 + r, normalised
-                    x[m2] = sub_nn<3>(x[m], tt);    // x + 3r - t
-                    x[m] = add_nn(x[m], tt);
-                } else {
-                    // x, y normalised < 2r: (x + y) reduced below 2r, (x + 3r - y) w
-                    const Fr29 d = sub_nn<3>(x[m], x[m2]);
-                    x[m] = reduce_small(norm(add_nn(x[m], x[m2])));
-                    x[m2] = mul(d, w);
-                }
-            }
-        }
-        if (last) {
-#pragma unroll
-            for (int m = 0; m < R; m++) {
-                // < 2r, packed (2r < 2^255); the lazy invariant between passes
-                Fr y = pack_l(reduce_small(norm(x[m])));
-                if (P.canon_out && !P.has_post) y = canon(y);
-                if (P.has_post) y = apply_scale(P.post, g[m], P.log_n, y);
-                if (P.epi_mul_sub) y = load_fr(P.ea + g[m]) * load_fr(P.eb + g[m]) - y;
-                if (P.epi_mul) y = load_fr(P.ea + g[m]) * y;
-                if (P.epi_sub) y = y - load_fr(P.ea + g[m]);
-                store_fr(P.out + g[m], y);
-            }
-        } else {
-#pragma unroll
-            for (int m = 0; m < R; m++) {
-                const Fr29 y = norm(x[m]);  // limbs < 2^29 again; magnitude kept (DIT) / < 2r (DIF)
-#pragma unroll
-                for (int l = 0; l < 9; l++) lds[l * TP + lidx((int)e[m])] = y.l[l];
-            }
-        }
-    }
-}
-
-template <bool DIT, int MAXNB>
-__global__ void __launch_bounds__(kNttThreads<MAXNB>, kNttWaves<MAXNB>) k_ntt_pass29(PassParams<Fr> P) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const int k = P.k, tl = P.tl;
-    const int T = 1 << (k + tl);
-    const int TP = T + (T >> 5);
-    const int nlo_log = P.b_lo - tl;
-    const uint32_t tile = blockIdx.x;
-    const uint32_t lob = tile & ((1u << nlo_log) - 1);
-    const uint32_t hi = tile >> nlo_log;
-    const uint32_t base_hi = hi << (P.b_lo + k);
-    const uint32_t lo0 = lob << tl;
-    int done = 0;
-    bool first = true;
-    while (done < k) {
-        const int nb = min(MAXNB, k - done);
-        const int qlo = DIT ? done : (k - done - nb);
-        const bool last = (done + nb == k);
-        if (!first) __syncthreads();
-        if constexpr (MAXNB >= 2) {
-            if (nb == 2) {
-                ntt_round29<2, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
-                first = false;
-                done += nb;
-                continue;
-            }
-        }
-        ntt_round29<1, DIT>(P, lds, TP, T, qlo, first, last, base_hi, lo0);
-        first = false;
-        done += nb;
-    }
-}
-
-template <class C>
-__global__ void k_table_times(Fe<C>* out, const Fe<C>* in, size_t count, Fe<C> c) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < count) store_fr(out + i, load_fr(in + i) * c);
-}
-
-// GG_NTT_R29=1: BN254 fr on the radix-2^29 passes (read once per process)
-static bool ntt_r29() {
-    static const bool on = [] {
-        const char* e = getenv("GG_NTT_R29");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
-
 // per-stage twiddle table: tw[(2^b - 1) + i] = w^(i << (L-1-b)), i < 2^b
 template <class F>
 __global__ void k_stage_twiddles(F* out, size_t count, int L, const F* hi, const F* lo, int S) {
@@ -553,7 +387,6 @@ struct DomainT {
     size_t n = 1;
     F omega, omega_inv, g, g_inv, n_inv, den;
     DevBuf tw, twinv;
-    DevBuf tw29, twinv29;  // BN254 fr with GG_NTT_R29: the stage tables times 2^261 (w 2^261 form)
     int S = 0;
     DevBuf scale_hi[SK_COUNT], scale_lo[SK_COUNT];
     ScaleSpec<F> spec[SK_COUNT];
@@ -644,21 +477,6 @@ void run_transform(DomainT<C>* d, const Fe<C>* in, Fe<C>* out, bool dit, bool in
         size_t lds = (ps.k > 3) ? (size_t)(T + (T >> 5)) * 32 : 0;  // single-round passes skip LDS
         ProfScope prof("ntt_pass", st, (double)d->n);
         static const int radix = ntt_radix();
-        if constexpr (std::is_same<C, FrCfg>::value) {
-            if (radix == 4 && d->tw29.p) {  // 9 x 29-bit limbs (the k = 0 scaling-only pass stays below)
-                if (ps.k > 0) {
-                    PassParams<F> Q = P;
-                    Q.tw = (const F*)(inverse_tw ? d->twinv29.p : d->tw29.p);
-                    const size_t lds29 = (ps.k > 2) ? (size_t)(T + (T >> 5)) * 36 : 0;
-                    if (dit) hipLaunchKernelGGL((k_ntt_pass29<true, 2>), dim3(tiles), dim3(512), lds29, st, Q);
-                    else hipLaunchKernelGGL((k_ntt_pass29<false, 2>), dim3(tiles), dim3(512), lds29, st, Q);
-                    GG_HIP(hipGetLastError());
-                    prof.stop(st);
-                    src = out;
-                    continue;
-                }
-            }
-        }
         if (radix == 4) {
             lds = (ps.k > 2) ? (size_t)(T + (T >> 5)) * 32 : 0;
             if (dit) hipLaunchKernelGGL((k_ntt_pass<F, true, 2>), dim3(tiles), dim3(512), lds, st, P);
@@ -744,20 +562,6 @@ static DomainT<C>* domain_build(int log_n, const void* omega_mont, const void* c
                                (inv ? d->twinv : d->tw).template as<F>(), cnt, L, h1.as<F>(), l1.as<F>(), S);
             GG_HIP(hipGetLastError());
             GG_HIP(hipDeviceSynchronize());
-        }
-        if constexpr (std::is_same<C, FrCfg>::value) {
-            if (ntt_r29()) {  // the same tables in w 2^261 form for the radix-2^29 passes
-                F cin;
-                memcpy(cin.v, Fr29Cfg::C_IN, 32);
-                for (int inv = 0; inv < 2; inv++) {
-                    DevBuf& o = inv ? d->twinv29 : d->tw29;
-                    o.alloc((cnt + 1) * 32);
-                    hipLaunchKernelGGL(k_table_times<C>, dim3(grid_for(cnt, 256)), dim3(256), 0, 0, o.template as<F>(),
-                                       (inv ? d->twinv : d->tw).template as<F>(), cnt, cin);
-                    GG_HIP(hipGetLastError());
-                }
-                GG_HIP(hipDeviceSynchronize());
-            }
         }
     }
     return d.release();
@@ -984,9 +788,11 @@ struct gg_hshard {
     size_t n = 0, m = 0, chunk = 0;  // chunk = m / N elements per (rank, poly)
     std::unique_ptr<gg::HShardT<gg::FrCfg>> bn;
     std::unique_ptr<gg::HShardT<gg::FrBlsCfg>> bls;
-    // phase 4 subtracts the c coefficients phase 2 left in ccoef: set by phase 2,
-    // consumed by phase 4 (a phase 4 without its phase 2 is refused)
-    bool ccoef_ready = false;
+    // the phases of one proof run in order 1, 2, 3, 4 on a handle (phase 4
+    // subtracts the c coefficients phase 2 left in ccoef): the last phase run,
+    // 0 = none / completed.  Phase 1 may start over at any point (a proof
+    // abandoned after a failed exchange); any other phase out of order is refused.
+    int last_phase = 0;
     hipStream_t st = nullptr;
     std::mutex mu;
     ~gg_hshard() {
@@ -1254,28 +1060,33 @@ static void phase4_t(gg_hshard* hs, const Fe<C>* recv, Fe<C>* h, hipStream_t st)
 }
 
 // curve dispatch over opaque 32-B elements (Fr* for both fields)
+static void phase_order(gg_hshard* hs, int phase) {
+    GG_CHECK(phase == 1 || hs->last_phase == phase - 1, GG_ERR_INVALID_ARG,
+             "distributed computeH: phase " + std::to_string(phase) + " after phase " +
+                 std::to_string(hs->last_phase) +
+                 " on this handle (phases run 1, 2, 3, 4 in order, one proof at a time per handle)");
+    hs->last_phase = phase == 4 ? 0 : phase;
+}
 void hshard_phase1(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len, Fr* send, hipStream_t st,
                    bool compact = false) {
-    hs->ccoef_ready = false;
+    phase_order(hs, 1);
     if (hs->curve == GG_CURVE_BN254) phase1_t<FrCfg>(hs, a, b, c, len, send, st, compact);
     else phase1_t<FrBlsCfg>(hs, (const FrBls*)a, (const FrBls*)b, (const FrBls*)c, len, (FrBls*)send, st, compact);
 }
 void hshard_phase2(gg_hshard* hs, const Fr* recv, Fr* send, hipStream_t st) {
+    phase_order(hs, 2);
     if (hs->curve == GG_CURVE_BN254) phase2_t<FrCfg>(hs, recv, send, st);
     else phase2_t<FrBlsCfg>(hs, (const FrBls*)recv, (FrBls*)send, st);
-    hs->ccoef_ready = true;
 }
 void hshard_phase3(gg_hshard* hs, const Fr* recv, Fr* send, hipStream_t st) {
+    phase_order(hs, 3);
     if (hs->curve == GG_CURVE_BN254) phase3_t<FrCfg>(hs, recv, send, st);
     else phase3_t<FrBlsCfg>(hs, (const FrBls*)recv, (FrBls*)send, st);
 }
 void hshard_phase4(gg_hshard* hs, const Fr* recv, Fr* h, hipStream_t st) {
-    GG_CHECK(hs->ccoef_ready, GG_ERR_INVALID_ARG,
-             "distributed computeH: phase 4 needs the c coefficients of a phase 2 on this handle "
-             "(phases 2 -> 4 in order, one proof at a time per handle)");
+    phase_order(hs, 4);
     if (hs->curve == GG_CURVE_BN254) phase4_t<FrCfg>(hs, recv, h, st);
     else phase4_t<FrBlsCfg>(hs, (const FrBls*)recv, (FrBls*)h, st);
-    hs->ccoef_ready = false;
 }
 
 size_t hshard_m(const gg_hshard* hs, int* rank, int* world, int* log_n) {

@@ -352,9 +352,9 @@ int gg_groth16_finalize_end(gg_g16_fixed_t h, const void *alpha1, const void *be
  * with an all-to-all send -> recv between consecutive phases.  State carried
  * between calls: phase 2 leaves den * c's coefficients in the handle and
  * phase 4 subtracts them (h = den coset_iFFT(a b) - den c, by linearity), so
- * the phases of one proof run in order on one handle, one proof at a time;
- * a phase 4 with no phase 2 since the last phase 1 / phase 4 fails
- * (GG_ERR_INVALID_ARG) instead of returning a wrong h. */
+ * the phases of one proof run in order 1, 2, 3, 4 on one handle, one proof at
+ * a time; a phase out of that order fails (GG_ERR_INVALID_ARG) instead of
+ * returning a wrong h (phase 1 may always start a new proof). */
 int gg_hshard_create(int log_n, const void *omega_mont, const void *coset_gen_mont, int rank,
                      int world, gg_hshard_t *out);
 int gg_hshard_create_ex(int curve, int log_n, const void *omega_mont, const void *coset_gen_mont,

@@ -89,7 +89,11 @@ def test_dist_h_bls12_381(log_n, world, fill):
     satisfies h(z) (z^n - 1) = A(z) B(z) - C(z) at a random z (pure Python)."""
     from gnark_amd import fr, ntt, DeviceBuffer
     n = 1 << log_n
-    vs = [_bls_vec(fill, 900 + log_n + i) for i in range(3)]
+    # a satisfied "R1CS": c = a b on the domain, so A B - C vanishes there and
+    # h (X^n - 1) = A B - C holds as polynomials (checked below at small sizes)
+    vs = [_bls_vec(fill, 900 + log_n + i) for i in range(2)]
+    cv = [x * y % BLS_R for x, y in zip(vs[0][0], vs[1][0])]
+    vs.append((cv, b"".join(fr.bls_fr_mont(x) for x in cv)))
     blocks = dist_h_blocks(*(x[1] for x in vs), fill, log_n, world, on_device=(world == 8), curve="bls12-381")
     assert all(len(x) == n // world * 32 for x in blocks)
     dom = ntt.Domain(log_n, fr.bls_fr_mont(fr.bls_domain_generator(log_n)),
@@ -121,8 +125,10 @@ def test_dist_h_bls12_381(log_n, world, fill):
 
 
 def test_dist_h_phase_order():
-    """Phase 4 subtracts the c coefficients phase 2 leaves in the handle: a
-    phase 4 with no phase 2 before it is refused, not answered with a wrong h."""
+    """Phase 4 subtracts the c coefficients phase 2 leaves in the handle: the
+    phases of a proof must run 1, 2, 3, 4 on a handle -- a phase out of order
+    (a phase 4 with no phase 2, a second proof's phase 2 interleaved) is
+    refused, not answered with a wrong h; phase 1 may start over."""
     from gnark_amd import groth16, DeviceBuffer, GnarkAmdError
     hs = groth16.HShard(8, 0, 2)
     xb = hs.exchange_bytes
@@ -134,7 +140,11 @@ def test_dist_h_phase_order():
     hs.phase(1, a, a, a, length=200, out=s)
     with pytest.raises(GnarkAmdError):  # phase 1 then 4: c's coefficients were never formed
         hs.phase(4, recv=recv, out=h)
+    hs.phase(1, a, a, a, length=200, out=s)  # starting over is allowed
     hs.phase(2, recv=recv, out=s)
+    with pytest.raises(GnarkAmdError):  # another proof's phase 2 interleaved
+        hs.phase(2, recv=recv, out=s)
+    hs.phase(3, recv=recv, out=s)
     hs.phase(4, recv=recv, out=h)  # in order: accepted
     with pytest.raises(GnarkAmdError):  # consumed
         hs.phase(4, recv=recv, out=h)

@@ -198,13 +198,17 @@ def test_plonk_proof_bytes_match_oracle_prover(curve, log_n, nb_public, n_cmt):
     pk.close()
 
 
-@pytest.mark.parametrize("log_n,parts,n_cmt", [(6, 2, 1), (7, 3, 2), (8, 4, 0), (8, 8, 1)])
+@pytest.mark.parametrize("log_n,parts,n_cmt", [(6, 2, 1), (7, 3, 2), (8, 4, 0), (8, 8, 1), (10, 2, 0),
+                                               (11, 8, 1), (11, 16, 0), (12, 3, 1)])
 def test_plonk_prove_multi_device_matches(log_n, parts, n_cmt):
     """One process, `parts` device parts (gg_plonk_pk_create_multi) rehearsed on
     this GPU: KZG-base slices per part (commitments split and summed in the
-    library), the numerator's cosets spread over min(rho, parts) parts with the
-    quotient blocks copied back -- exactly the one-GPU proof, also through
-    commit_lagrange (the BSB22 hint) and from device-resident L, R, O."""
+    library), the copy-constraint ratio scanned per KzgLagrange slice and
+    chained, the quotient units (U = rho S classes of the big domain: cosets,
+    half cosets at 8 parts, quarter cosets at 16; per-unit inverse DFT blocks
+    and the tail stages from 2^12 big domains) with the blocks copied back --
+    exactly the one-GPU proof, also through commit_lagrange (the BSB22 hint)
+    and from device-resident L, R, O."""
     from gnark_amd import DeviceBuffer, plonk_prover as pp
     circ = Circuit(log_n, 31 + log_n, nb_public=1, n_cmt=n_cmt)
     tau = random.Random(log_n + parts).randrange(2, R)

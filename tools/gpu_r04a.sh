@@ -16,7 +16,7 @@ step() {  # step <secs> <log> cmd...
   echo "=== rc=$rc $(date +%T)" >> gpurun_out/progress_$V.txt
   return $rc
 }
-S="${STEPS:-calib,r29,test,probe}"
+S="${STEPS:-test,probe}"
 if [[ "$S" == *calib* ]]; then
   step 120 calib_stdout_$V.txt tools/mbench_gather_calib 16 || exit 2
   step 120 calib_pmc_$V.txt timeout -s KILL 110 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/calib_$V -o run -- tools/mbench_gather_calib 16 || exit 2
@@ -29,7 +29,7 @@ if [[ "$S" == *r29* ]]; then  # the radix-2^29 BN254 fr passes (opt-in until mea
 fi
 if [[ "$S" == *test* ]]; then
   step 900 pytest_$V.txt python3 -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu \
-    tests/test_gpu_dist_h.py tests/test_gpu_groth16_multi.py tests/test_gpu_bls_groth16.py \
+    tests/test_gpu_ntt.py tests/test_gpu_msm.py tests/test_gpu_dist_h.py tests/test_gpu_groth16_multi.py tests/test_gpu_bls_groth16.py \
     tests/test_gpu_plonk_poly.py tests/test_gpu_plonk_prove.py tests/test_gpu_groth16_size.py ${PYTEST_ARGS} || exit 2
 fi
 if [[ "$S" == *probe* ]]; then
