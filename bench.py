@@ -9,7 +9,7 @@ region starts (the bench contract); the same prove with the solution in HOST
 memory, as gnark's Prove hands it over (prove.go:127-320; icicle.go:231-278,
 478-480 copy it to the GPU per proof), is timed beside it in "other_inputs"
 (PCIe-inclusive: pinned, chunked upload overlapped with the MSMs;
---host-inputs swaps the two).  A "step" is one proof: computeH (7 fused NTTs),
+--host-inputs swaps the two).  A "step" is one proof: computeH (6 fused NTTs),
 the A/B1/K/Z G1 MSMs and the B G2 MSM, and the host combination.  The key is
 resident in HBM (uploaded once, as setupDevicePointers does).
 value = constraints / s.  For N > 1 one proof is spread over the N GPUs (strong

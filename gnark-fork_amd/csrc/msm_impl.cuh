@@ -292,7 +292,8 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
     if constexpr (std::is_same<F, Fp2>::value) {
         // BN254 G2: radix-2^29 Fp2 accumulator (field29.cuh), base in x * 2^261 form
         Xyzz2_29 acc = inf2_29();
-        // (one 4-B entry load per point here: a 16-B chunk in registers spills at 2 waves)
+        // 8-B chunks of entries (a 16-B chunk in registers spills at 2 waves)
+        uint2 ch = *reinterpret_cast<const uint2*>(sorted + (e0 & ~1u));
         for (uint32_t e = e0; e < e1; e++) {
             if (e == bnd) {
                 range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
@@ -300,7 +301,8 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                 seg0 = e;
                 do { q++; bnd = bnd2; bnd2 = offsets[min(q + 2, nb)]; } while (bnd == e);
             }
-            const uint32_t v = sorted[e];
+            if ((e & 1u) == 0 && e != e0) ch = *reinterpret_cast<const uint2*>(sorted + e);
+            const uint32_t v = (e & 1u) ? ch.y : ch.x;
             const Affine<F> pt = ld(pts + (v & pmask));
             if (skip_inf && pt.is_inf()) continue;
             const Fp2_29 x{unpack29(pt.x.a0), unpack29(pt.x.a1)};
