@@ -146,8 +146,8 @@ def main():
         mode, world, devices = "torch", env_world, None
     elif args.gpus > 1 or args.devices:
         devices = [int(x) for x in args.devices.split(",")] if args.devices else list(range(args.gpus))
-        if len(devices) != args.gpus:
-            raise SystemExit(f"bench: --gpus {args.gpus} but {len(devices)} devices listed")
+        if len(set(devices)) != args.gpus:  # --gpus counts distinct GPUs; shards may share one
+            raise SystemExit(f"bench: --gpus {args.gpus} but {len(set(devices))} distinct devices listed")
         mode, world = "mpk", 1
     else:
         mode, world, devices = "single", 1, None

@@ -17,7 +17,7 @@ step() {  # step <secs> <log> cmd...
   echo "=== rc=$rc $(date +%T)" >> gpurun_out/progress_$V.txt
   return $rc
 }
-S="${STEPS:-pmc,probe,prof,bench}"
+S="${STEPS:-pmc,probe,prof,reh,bench}"
 if [[ "$S" == *pmc* ]]; then
   step 300 pmc_f_$V.txt timeout -s KILL 280 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_f_$V -o run -- python3 bench.py $HEAD || exit 2
   step 300 pmc_w_$V.txt timeout -s KILL 280 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_w_$V -o run -- python3 bench.py $HEAD || exit 2
@@ -32,6 +32,9 @@ fi
 if [[ "$S" == *prof* ]]; then
   step 400 prof_$V.txt rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$V -o run -- \
     python3 -u bench.py --steps 5 --warmup 1 --no-variants --msm-log-n 0 --ntt-log-n 0 --plonk-log-n 0 --no-cpu-baseline --solver 0 --projection '' || exit 2
+fi
+if [[ "$S" == *reh* ]]; then
+  step 400 reh8_$V.json python3 -u bench.py --gpus 1 --devices 0,0,0,0,0,0,0,0 --steps 3 --warmup 1 --no-variants --msm-log-n 0 --ntt-log-n 0 --no-cpu-baseline --solver 0 --projection '' || exit 2
 fi
 if [[ "$S" == *bench* ]]; then step 600 bench_$V.json python3 -u bench.py || exit 2; fi
 echo done >> gpurun_out/progress_$V.txt
