@@ -1151,9 +1151,9 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     // the units' blocks (or, for domains below 2^12, the whole inverse here)
     if (pk->split_idft) ntt_tail_inverse_coset(pk->d1, F(pk->cres), pk->log_u, s[2]);
     else plk::ntt(pk->d1, F(pk->cres), 1, 1, 1, s[2]);
-    for (int k = 0; k < 3; k++) {
-        zero(pk->hpad[k].p, nb3, s[2]);
+    for (int k = 0; k < 3; k++) {  // n + 2 coefficients, the (n + 3)-th MSM scalar zero
         dcopy(pk->hpad[k].p, F(pk->cres) + (n + 2) * k, 32 * (n + 2), s[2]);
+        zero(F(pk->hpad[k]) + n + 2, 32, s[2]);
     }
     for (int k = 0; k < 3; k++) record_wait(pk, s[2], s[k]);
     mark();
@@ -1174,8 +1174,8 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     const FrB zn = pow_u64(zeta, n), zn1 = zn - FrB::one();
     // ---- openZ (prove.go:635-652): blinded Z = Z - bz + bz X^n, opened at zeta * omega
     auto blinded = [&](const DevBuf& canon, const std::vector<FrB>& b, DevBuf& out, hipStream_t q) {
-        zero(out.p, nb3, q);
         dcopy(out.p, canon.p, nb, q);
+        zero(F(out) + n, nb3 - nb, q);
         std::vector<FrB> head(b.size()), tail(b);
         for (size_t j = 0; j < b.size(); j++) head[j] = -b[j];
         GG_HIP(hipMemcpyAsync(F(pk->pad), head.data(), 32 * b.size(), hipMemcpyHostToDevice, q));
@@ -1184,7 +1184,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         GG_HIP(hipStreamSynchronize(q));  // host vectors
     };
     blinded(pk->can[3], bp[3], pk->bz, s[0]);
-    zero(pk->q1.p, nb3, s[0]);
+    zero(F(pk->q1) + n + 2, 32, s[0]);  // Horner writes the n + 2 quotient coefficients
     const FrB zu = eval_dev(pk, F(pk->bz), n + 3, zeta * pk->omega, F(pk->q1), F(pk->vals), 0, s[0]);
     P.zs_value = zu;
     std::future<BJac> fzs = std::async(msm_policy(), [&] {
@@ -1193,7 +1193,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     });
     // ---- foldH (prove.go:670-705) on s[2]
     const FrB zp = pow_u64(zeta, n + 2);
-    zero(pk->fold.p, nb3, s[2]);
+    zero(F(pk->fold) + n + 2, 32, s[2]);  // fold_h writes n + 2 coefficients
     plk::fold_h(F(pk->cres), n, zp, F(pk->fold), s[2]);
     BJac fhd = jac_add(jac_add(BJac::from_affine(P.h[0]), jmul(P.h[1], zp)), jmul(P.h[2], zp * zp));
     const BAff folded_digest = to_aff(fhd);
@@ -1303,7 +1303,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         }
         plk::lincomb(F(pk->q2), n + 3, fp, fl, cf, (int)polys.size(), s[2]);
     }
-    zero(pk->fold.p, nb3, s[2]);  // reuse as the batch quotient (n + 2 of n + 3)
+    zero(F(pk->fold) + n + 2, 32, s[2]);  // reuse as the batch quotient (n + 2 of n + 3)
     const FrB fv = eval_dev(pk, F(pk->q2), n + 3, zeta, F(pk->fold), F(pk->vals) + 18, 2, s[2]);
     GG_CHECK(fv == fe, GG_ERR_INTERNAL, "batch opening: folded evaluation mismatch");
     P.batched_h = to_aff(red(pk, commit_kzg(pk, 2, F(pk->fold), s[2])));
