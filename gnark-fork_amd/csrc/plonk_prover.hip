@@ -25,6 +25,7 @@
 #include "plonk_ops.h"
 #include "curve.cuh"
 #include "sha256.h"
+#include <functional>
 #include <future>
 #include <memory>
 #include <mutex>
@@ -174,6 +175,12 @@ struct PlonkPeer {
     DevBuf tw0, in[5 + plk::MAX_CMT];   // twiddles0 (S = 1); L R O Z (canonical bit-reversed), Qk, Pi_j
     DevBuf cev[7 + plk::MAX_CMT], zc;   // a unit's evaluation slot; ZS (S > 1)
     hipEvent_t ea[4] = {}, eb[4] = {};  // per stream: around the last peer copy (timing)
+    // canonical-form tasks placed here (Key::canon_owner): the size-n domain, the
+    // regular form of a task's polynomial, pk's Qk in Lagrange form (Qk's owner),
+    // one push stream per destination part
+    gg_domain_t d0 = nullptr;
+    DevBuf creg, qk_lag;
+    std::vector<hipStream_t> xs;
     ~PlonkPeer() {
         int cur = 0;
         const bool restore = hipGetDevice(&cur) == hipSuccess;
@@ -188,6 +195,10 @@ struct PlonkPeer {
         for (auto& b : cev) b.release();
         zc.release();
         tw0.release();
+        if (d0) gg_domain_release(d0);
+        creg.release();
+        qk_lag.release();
+        for (hipStream_t x : xs) (void)hipStreamDestroy(x);
         perm_slice.release();
         pz.release();
         ar.buf.release();
@@ -207,6 +218,7 @@ struct PlonkPartTimes {
     double coset_count = 0, coset_ms = 0, coset_in_copy_ms = 0, coset_out_copy_ms = 0, coset_mb = 0;
     double wait_ms = 0;  // part 0: time spent waiting for the peers' MSM slices and cosets
     double ratio_ms = 0;  // its slice of the copy-constraint ratio (factors, scan, fix-up)
+    double canon_count = 0, canon_ms = 0, canon_mb = 0;  // canonical-form tasks: count, ms, MB pushed
 };
 
 // ============================================================== prover of one curve
@@ -531,6 +543,53 @@ static std::vector<FrB> eval_batch(Key* pk, const FrB* const* f, const size_t* l
     return v;
 }
 
+// The canonical forms of a multi-part key's per-proof polynomials are taken on
+// the peers: task i (PlonkPeer::in index: 0..2 L R O, 4 Qk, 5 + j Pi_j, then 3 Z,
+// which is complete only after the ratio) runs on peer i mod (N - 1); its owner
+// pushes the bit-reversed form to every peer with quotient units and both forms
+// to part 0, so part 0 runs no size-n transform of its own and no polynomial
+// leaves it whole.
+static std::vector<int> canon_tasks(const Key* pk) {
+    std::vector<int> t = {0, 1, 2, 4};
+    for (int j = 0; j < pk->n_cmt; j++) t.push_back(5 + j);
+    t.push_back(3);
+    return t;
+}
+static PlonkPeer* canon_owner(const Key* pk, size_t i) { return pk->peers[i % pk->peers.size()].get(); }
+
+// one canonical-form task on peer pi: `fill` leaves the polynomial's Lagrange
+// form in p->in[b] (ordered on p->s[3]); the size-n inverse DIF there (canonical
+// bit-reversed, in place), the regular form in creg when part 0 needs it, then the
+// pushes, each on its own stream (one xGMI link each): bit-reversed to every other
+// peer with quotient units and to brev0 on part 0, regular to reg0
+static void canon_run(Key* pk, size_t pi, int b, FrB* brev0, FrB* reg0, const std::function<void(hipStream_t)>& fill) {
+    PlonkPeer* p = pk->peers[pi].get();
+    const size_t n = pk->n, nb = 32 * n;
+    GG_HIP(hipSetDevice(p->device));
+    const auto a = std::chrono::steady_clock::now();
+    hipStream_t q = p->s[3];
+    fill(q);
+    plk::ntt(p->d0, p->in[b].p, 1, 0, 0, q);  // FFTInverse DIF: natural in -> bit-reversed out
+    if (reg0) plk::bit_reverse(F(p->in[b]), F(p->creg), n, q);
+    GG_HIP(hipStreamSynchronize(q));
+    size_t x = 0;
+    double mb = 0;
+    for (auto& o : pk->peers)
+        if (o.get() != p && !o->units.empty()) {
+            GG_HIP(hipMemcpyPeerAsync(o->in[b].p, o->device, p->in[b].p, p->device, nb, p->xs[x++]));
+            mb += nb / 1e6;
+        }
+    GG_HIP(hipMemcpyPeerAsync(brev0, pk->device, p->in[b].p, p->device, nb, p->xs[x++]));
+    if (reg0) GG_HIP(hipMemcpyPeerAsync(reg0, pk->device, p->creg.p, p->device, nb, p->xs[x++]));
+    mb += (reg0 ? 2.0 : 1.0) * nb / 1e6;
+    for (size_t i = 0; i < x; i++) GG_HIP(hipStreamSynchronize(p->xs[i]));
+    std::lock_guard<std::mutex> lk(pk->tmu);
+    PlonkPartTimes& T = pk->ptimes[pi + 1];
+    T.canon_count += 1;
+    T.canon_ms += ms_since(a);
+    T.canon_mb += mb;
+}
+
 static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, const void* omega_big,
                            const void* coset_shift, const void* kzg_g1, size_t n_kzg,
                            const void* kzg_lagrange_g1, const void* const* trace, const void* const* qcp,
@@ -782,6 +841,28 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
         p->ar.reserve(plk::ratio_range_arena_bytes(n, cnt) + 65536);
         GG_HIP(hipStreamSynchronize(p->s[0]));
     }
+    // peers: the canonical-form tasks (canon_tasks) -- a size-n domain, the regular
+    // form's buffer and push streams on each owner, Qk in Lagrange form on Qk's
+    if (!pk->peers.empty()) {
+        const std::vector<int> tasks = canon_tasks(pk);
+        for (size_t i = 0; i < tasks.size(); i++) {
+            PlonkPeer* p = canon_owner(pk, i);
+            GG_HIP(hipSetDevice(p->device));
+            if (!p->in[0].p)
+                for (int k = 0; k < 5 + n_cmt; k++) p->in[k].alloc(nb);
+            if (!p->d0) {
+                p->d0 = dom(log_n, pk->omega, pk->u);
+                p->creg.alloc(nb);
+                p->xs.resize(pk->peers.size() + 2);
+                for (hipStream_t& x : p->xs) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+            }
+            if (tasks[i] == 4) {
+                p->qk_lag.alloc(nb);
+                GG_HIP(hipMemcpyPeerAsync(p->qk_lag.p, p->device, pk->qk_lag.p, pk->device, nb, p->s[3]));
+                GG_HIP(hipStreamSynchronize(p->s[3]));
+            }
+        }
+    }
     GG_HIP(hipSetDevice(pk->device));
     pk->perm.alloc(3 * n * 8);
     up(pk->perm.p, perm, 3 * n * 8, false, st);
@@ -875,6 +956,41 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         up(pk->lag[k].p, lro_in[k], nb, on_dev, s[k]);
         uploaded[k] = record(pk, s[k]);
     }
+    const bool dz = !pk->peers.empty();
+    const bool peers_on = dz && !plonk_solo(pk);
+    // multi-part keys: the canonical forms on the peers (canon_tasks), L R O as
+    // soon as uploaded, Qk and Pi_j at once; Z after the ratio
+    const std::vector<int> ctasks = dz ? canon_tasks(pk) : std::vector<int>();
+    std::vector<std::shared_future<void>> cfut(pk->peers.size());  // per owner: its tasks before Z, in order
+    if (peers_on) {
+        for (size_t pi = 0; pi < pk->peers.size(); pi++) {
+            std::vector<int> mine;
+            for (size_t i = 0; i + 1 < ctasks.size(); i++)
+                if (i % pk->peers.size() == pi) mine.push_back(ctasks[i]);
+            if (mine.empty()) continue;
+            cfut[pi] = std::async(std::launch::async, [&, pi, mine] {
+                PlonkPeer* p = pk->peers[pi].get();
+                for (int b : mine) {
+                    if (b < 3)
+                        canon_run(pk, pi, b, F(pk->cbrev[b]), F(pk->can[b]), [&](hipStream_t q) {
+                            GG_HIP(hipEventSynchronize(uploaded[b]));
+                            GG_HIP(hipMemcpyPeerAsync(p->in[b].p, p->device, pk->lag[b].p, pk->device, nb, q));
+                        });
+                    else if (b == 4)  // completeQk (prove.go:397-423) on its owner
+                        canon_run(pk, pi, 4, F(pk->qkc), nullptr, [&](hipStream_t q) {
+                            dcopy(p->in[4].p, p->qk_lag.p, nb, q);
+                            if (nb_pub) GG_HIP(hipMemcpyAsync(p->in[4].p, pub, 32 * nb_pub, hipMemcpyHostToDevice, q));
+                            for (int i = 0; i < n_cmt; i++)
+                                GG_HIP(hipMemcpyAsync(F(p->in[4]) + pk->nb_public + pk->cmt_idx[i], cmt_hashed[i].v, 32,
+                                                      hipMemcpyHostToDevice, q));
+                        });
+                    else
+                        canon_run(pk, pi, b, F(pk->pi_brev[b - 5]), F(pk->pi_reg[b - 5]),
+                                  [&](hipStream_t q) { up(p->in[b].p, cmt_values[b - 5], nb, false, q); });
+                }
+            }).share();
+        }
+    }
     // blinding commitments of L, R, O, Z on host threads while the GPU works
     std::future<BJac> fblind[4];
     for (int q = 0; q < 4; q++) fblind[q] = std::async(std::launch::async, [pk, &bp, q] { return blind_commit(pk, bp[q]); });
@@ -887,8 +1003,9 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                 GG_HIP(hipSetDevice(pk->device));
                 lroj[k] = msm_jac(pk, pk->kzg_lag, k, F(pk->lag[k]), s[k]);
             }));
-        // meanwhile on stream 3: completeQk (prove.go:397-423) and the BSB22 Pi_i
-        {
+        // meanwhile on stream 3 (one part; with peers: canon_tasks): completeQk
+        // (prove.go:397-423) and the BSB22 Pi_i
+        if (!dz) {
             hipStream_t q = s[3];
             dcopy(pk->qkc.p, pk->qk_lag.p, nb, q);
             if (nb_pub) GG_HIP(hipMemcpyAsync(pk->qkc.p, pub, 32 * nb_pub, hipMemcpyHostToDevice, q));
@@ -935,8 +1052,8 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     // part writes its slice of Z where its share of the Z commitment reads it
     // (and into the primary's Z for the rest of the proof).
     for (int k = 0; k < 3; k++) record_wait(pk, s[k], s[0]);
-    const bool dz = !pk->peers.empty();
-    const bool peers_on = dz && !plonk_solo(pk);
+    // the owner of Z's canonical form: every part pushes its slice of Z there
+    PlonkPeer* zown = peers_on ? canon_owner(pk, ctasks.size() - 1) : nullptr;
     {
         const size_t zlo = dz ? pk->l_lo : 0, zcnt = dz ? pk->l_hi - pk->l_lo : n;
         const auto ta = std::chrono::steady_clock::now();
@@ -968,6 +1085,8 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         std::vector<FrB> pre(agg.size(), FrB::one());
         for (size_t r = 1; r < agg.size(); r++) pre[r] = pre[r - 1] * agg[r - 1];
         plk::ratio_fixup(F(pk->pz), zcnt, pre[0], F(pk->zlag) + zlo, s[0]);
+        if (zown && zcnt)
+            GG_HIP(hipMemcpyPeerAsync(F(zown->in[3]) + zlo, zown->device, F(pk->zlag) + zlo, pk->device, 32 * zcnt, s[0]));
         pf.clear();
         if (peers_on)
             for (size_t q = 0; q < pk->peers.size(); q++)
@@ -978,7 +1097,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                     GG_HIP(hipSetDevice(p->device));
                     const auto a = std::chrono::steady_clock::now();
                     plk::ratio_fixup(F(p->pz), cnt, pre[q + 1], F(p->scal[0]), p->s[0]);  // the Z slot of its MSM
-                    GG_HIP(hipMemcpyPeerAsync(F(pk->zlag) + p->l_lo, pk->device, p->scal[0].p, p->device, 32 * cnt,
+                    GG_HIP(hipMemcpyPeerAsync(F(zown->in[3]) + p->l_lo, zown->device, p->scal[0].p, p->device, 32 * cnt,
                                               p->s[0]));
                     GG_HIP(hipStreamSynchronize(p->s[0]));
                     std::lock_guard<std::mutex> lk(pk->tmu);
@@ -989,7 +1108,17 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         pk->ptimes[0].ratio_ms += ms_since(ta);
     }
     record_wait(pk, s[0], s[1]);
-    lag_to_canonical(pk, F(pk->zlag), F(pk->cbrev[3]), F(pk->can[3]), s[1]);  // overlaps the Z commitment
+    std::shared_future<void> zfut;
+    if (peers_on) {  // Z's canonical forms on its owner, once every slice has landed there
+        GG_HIP(hipStreamSynchronize(s[0]));
+        const size_t zi = (ctasks.size() - 1) % pk->peers.size();
+        zfut = std::async(std::launch::async, [&, zi] {
+            if (cfut[zi].valid()) cfut[zi].wait();  // its earlier tasks (creg, stream 3) first
+            canon_run(pk, zi, 3, F(pk->cbrev[3]), F(pk->can[3]), [](hipStream_t) {});
+        }).share();
+    } else if (!dz) {
+        lag_to_canonical(pk, F(pk->zlag), F(pk->cbrev[3]), F(pk->can[3]), s[1]);  // overlaps the Z commitment
+    }
     P.z = to_aff(jac_add(red(pk, msm_jac(pk, pk->kzg_lag, 0, F(pk->zlag), s[0], peers_on)), fblind[3].get()));
     mark();
     // ---- alpha (deriveAlpha, prove.go:504-512)
@@ -1081,8 +1210,15 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         }
     };
     std::vector<std::future<void>> peer_work;
-    if (!pk->peers.empty() && !plonk_solo(pk)) {
-        for (int k = 0; k < 4; k++) GG_HIP(hipStreamSynchronize(s[k]));  // inputs complete before the copies
+    if (peers_on) {  // every part's inputs: the canonical forms pushed by their owners
+        const auto w = std::chrono::steady_clock::now();
+        for (auto& f : cfut)
+            if (f.valid()) f.get();
+        zfut.get();
+        std::lock_guard<std::mutex> lk(pk->tmu);
+        pk->ptimes[0].wait_ms += ms_since(w);
+    }
+    if (peers_on) {
         for (size_t pi = 0; pi < pk->peers.size(); pi++) {
             PlonkPeer* p = pk->peers[pi].get();
             if (p->units.empty()) continue;
@@ -1090,22 +1226,12 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                 GG_HIP(hipSetDevice(p->device));
                 const auto ta = std::chrono::steady_clock::now();
                 hipStream_t q = p->s[3];
-                const FrB* src[5 + plk::MAX_CMT] = {F(pk->cbrev[0]), F(pk->cbrev[1]), F(pk->cbrev[2]), F(pk->cbrev[3]),
-                                                    F(pk->qkc)};
-                for (int j = 0; j < n_cmt; j++) src[5 + j] = F(pk->pi_brev[j]);
-                GG_HIP(hipEventRecord(p->ea[3], q));
-                for (int k = 0; k < 5 + n_cmt; k++)
-                    GG_HIP(hipMemcpyPeerAsync(p->in[k].p, p->device, src[k], pk->device, nb, q));
-                GG_HIP(hipEventRecord(p->eb[3], q));
                 const FrB* ins[5 + plk::MAX_CMT] = {};
                 for (int k = 0; k < 5 + n_cmt; k++) ins[k] = F(p->in[k]);
                 FrB* e[7 + plk::MAX_CMT] = {};
                 for (int k = 0; k < 7 + n_cmt; k++) e[k] = F(p->cev[k]);
                 for (auto& qu : p->units) run_unit(qu.get(), ins, e, F(p->zc), F(p->tw0), F(qu->out), true, q);
                 // the units' blocks back to the primary's cres (timed separately)
-                GG_HIP(hipEventSynchronize(p->eb[3]));
-                float cin = 0;
-                GG_HIP(hipEventElapsedTime(&cin, p->ea[3], p->eb[3]));
                 GG_HIP(hipEventRecord(p->ea[3], q));
                 for (auto& qu : p->units) {
                     const size_t blk = (size_t)(__builtin_bitreverse32((uint32_t)qu->p) >> (32 - pk->log_u));
@@ -1119,9 +1245,8 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                 PlonkPartTimes& T = pk->ptimes[pi + 1];
                 T.coset_count += (double)p->units.size();
                 T.coset_ms += ms_since(ta);
-                T.coset_in_copy_ms += cin;
                 T.coset_out_copy_ms += cout;
-                T.coset_mb += ((double)nb * (5 + n_cmt) + (double)mb * p->units.size()) / 1e6;
+                T.coset_mb += (double)mb * p->units.size() / 1e6;
             }));
         }
     }
@@ -1581,10 +1706,11 @@ extern "C" int gg_plonk_pk_part_timings(gg_plonk_pk_t pk, int part, double* out,
         if (part >= (int)k->ptimes.size()) return 0;  // no proof yet
         std::lock_guard<std::mutex> lt(k->tmu);
         const PlonkPartTimes& T = k->ptimes[part];
-        const double v[11] = {T.msm_count, T.msm_ms,   T.scalar_copy_ms,    T.scalar_mb,         T.coset_count,
-                              T.coset_ms,  T.coset_in_copy_ms, T.coset_out_copy_ms, T.coset_mb, T.wait_ms,
-                              T.ratio_ms};
-        for (int i = 0; i < 11; i++) out[i] = v[i];
+        const double v[GG_PLONK_PART_SLOTS] = {T.msm_count,   T.msm_ms,    T.scalar_copy_ms,    T.scalar_mb,
+                                               T.coset_count, T.coset_ms,  T.coset_in_copy_ms, T.coset_out_copy_ms,
+                                               T.coset_mb,    T.wait_ms,   T.ratio_ms,        T.canon_count,
+                                               T.canon_ms,    T.canon_mb};
+        for (int i = 0; i < GG_PLONK_PART_SLOTS; i++) out[i] = v[i];
         return 0;
     });
     GG_CAPI_END

@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("GNARK_AMD_LIB", os.path.join(_PKG_DIR, "lib", "libgna
 GG_OK = 0
 GG_REHEARSAL = 7  # a multi-GPU timing rehearsal: the proof written is not valid
 GG_MPK_TIMING_SLOTS = 18
-GG_PLONK_PART_SLOTS = 11
+GG_PLONK_PART_SLOTS = 14
 GG_G1, GG_G2, GG_BLS12_381_G1, GG_BLS12_381_G2 = 1, 2, 3, 4
 GG_CURVE_BN254, GG_CURVE_BLS12_381 = 0, 1
 GG_DIF, GG_DIT = 0, 1

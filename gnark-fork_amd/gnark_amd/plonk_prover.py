@@ -244,10 +244,11 @@ class ProvingKey:
     def part_timings(self) -> list:
         """Per device part (0 = primary), the last proof: MSM slices and their ms,
         scalar-slice copies (ms, MB), quotient units (ms, copies in / out, MB),
-        part 0's wait for its peers, and the part's slice of the ratio
-        (gg_plonk_pk_part_timings)."""
+        part 0's wait for its peers, the part's slice of the ratio, and its
+        canonical-form tasks (count, ms, MB pushed) (gg_plonk_pk_part_timings)."""
         names = ["msm_slices", "msm_ms", "scalar_copy_ms", "scalar_MB", "quotient_units", "unit_ms",
-                 "unit_in_copy_ms", "unit_out_copy_ms", "unit_MB", "wait_for_peers_ms", "ratio_ms"]
+                 "unit_in_copy_ms", "unit_out_copy_ms", "unit_MB", "wait_for_peers_ms", "ratio_ms",
+                 "canon_tasks", "canon_ms", "canon_MB"]
         out = []
         for p in range(len(self.devices())):
             v = (ctypes.c_double * GG_PLONK_PART_SLOTS)()

@@ -624,13 +624,16 @@ int gg_plonk_pk_set_rehearsal(gg_plonk_pk_t pk, int on);
 /* where device part `part` (0 = primary) spent the last proof (cap >=
  * GG_PLONK_PART_SLOTS): [0] MSM slices, [1] their ms (incl. the scalar copy),
  * [2] ms copying scalar slices from the primary (xGMI), [3] MB copied, [4]
- * quotient units (classes of the big domain), [5] their ms (copies, FFTs,
- * numerator, block inverse DFT), [6] ms copying the per-proof polynomials in,
- * [7] ms copying the units' blocks back, [8] MB
- * moved for the quotient units, [9] part 0 only: ms waiting for the peers'
- * MSM slices and quotient units after finishing its own work, [10] ms of its
- * slice of the copy-constraint ratio (factors, scan, fix-up). */
-#define GG_PLONK_PART_SLOTS 11
+ * quotient units (classes of the big domain), [5] their ms (FFTs, numerator,
+ * block inverse DFT, blocks back), [6] 0 (kept for layout: the per-proof
+ * polynomials now arrive by the canonical-form pushes of [11..13]), [7] ms
+ * copying the units' blocks back, [8] MB moved for the quotient units, [9]
+ * part 0 only: ms waiting for the peers' canonical forms, MSM slices and
+ * quotient units after finishing its own work, [10] ms of its slice of the
+ * copy-constraint ratio (factors, scan, fix-up), [11] canonical-form tasks run
+ * (a size-n inverse DFT of L, R, O, Z, Qk or Pi_j: peers only), [12] their ms
+ * (input, transform, pushes), [13] MB they pushed over xGMI. */
+#define GG_PLONK_PART_SLOTS 14
 int gg_plonk_pk_part_timings(gg_plonk_pk_t pk, int part, double *out, int cap);
 /* the key's vk digests, 96-B affine each: S[0..2], Ql, Qr, Qm, Qo, Qk, Qcp[0..n_cmt) */
 int gg_plonk_pk_vk(gg_plonk_pk_t pk, void *out, size_t cap);

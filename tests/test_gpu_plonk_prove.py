@@ -323,13 +323,17 @@ def test_plonk_rehearsal_mode():
     assert all(p["scalar_MB"] > 0 for p in pt[1:])
     assert all(p["ratio_ms"] > 0 for p in pt)  # every part scans its slice of the ratio
     assert [p["quotient_units"] for p in pt] == [1, 1, 1, 1]  # rho = 4 classes: one per part
+    # canonical forms (L R O Qk, then Z) on the 3 peers, none on part 0
+    assert [p["canon_tasks"] for p in pt] == [0, 2, 2, 1]
+    assert all(p["canon_MB"] > 0 for p in pt[1:])
     pkm.set_rehearsal(True)
     with pytest.raises(GnarkAmdError) as ei:
         pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts)
     assert ei.value.code == GG_REHEARSAL
     solo = pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts, rehearsal_ok=True)
     assert solo != ref
-    assert all(p["msm_slices"] == 0 and p["quotient_units"] == 0 for p in pkm.part_timings()[1:])
+    assert all(p["msm_slices"] == 0 and p["quotient_units"] == 0 and p["canon_tasks"] == 0
+               for p in pkm.part_timings()[1:])
     pkm.set_rehearsal(False)
     assert pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts) == ref
     pkm.close()
