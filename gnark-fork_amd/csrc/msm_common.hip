@@ -231,13 +231,40 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t* cnt, uint32_t d, bool va
     return b + rank;
 }
 
+// The sort key of every window of one scalar, in window order (the signed digits
+// carry upward): fn(w, key), key = bucket | sign bit, or 0xffffffff for a zero
+// digit or (bucket stripes, slog > 0) a bucket outside stripe sres.  Phases A and
+// C both derive their keys here, so their counts agree by construction.
+template <class SC, class Fn>
+__device__ __forceinline__ void scalar_keys(const Fe<SC>& scl, int c, int W, const WinSpec& ws, int G, int slog,
+                                            uint32_t sres, Fn&& fn) {
+    const uint32_t smask = (1u << slog) - 1u;
+    const Fe<SC> k = from_mont(scl);
+    int carry = 0;
+    for (int w = 0; w < W; w++) {
+        const int bw = ws.bits[w];
+        int d = (int)extract_bits(k, ws.off[w], bw) + carry;
+        if (d > (1 << (bw - 1))) { d -= (1 << bw); carry = 1; } else carry = 0;
+        uint32_t key = 0xffffffffu;
+        const uint32_t bb = (uint32_t)((d > 0 ? d : -d) - 1);  // bucket |d| - 1 of group w mod G
+        if (d && (bb & smask) == sres) {
+            // bucket stripe (slog > 0): only buckets bb = 2^slog j + sres, renumbered j;
+            // c is then the stripe's c - slog
+            const uint32_t bk = ((uint32_t)(w & (G - 1)) << (c - 1)) | (bb >> slog);
+            key = bk | (d < 0 ? 0x80000000u : 0u);
+        }
+        fn(w, key);
+    }
+}
+
+// Phase A: the block's bin histogram; keys (nullable) keeps every key for a
+// phase C that reads them (GG_SORT_KEYS=1) instead of deriving them again
 template <class SC>
 __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, const uint32_t* sidx,
                                                      size_t n, int c, int W, WinSpec ws, int G, int kbits,
                                                      int spb, int nbins, int h, uint32_t* keys,
                                                      uint32_t* hist, uint32_t nblocks, int slog, uint32_t sres) {
     extern __shared__ uint32_t hh[];
-    const uint32_t smask = (1u << slog) - 1u;
     for (int j = threadIdx.x; j < nbins; j += blockDim.x) hh[j] = 0;
     __syncthreads();
     // spb <= 512: at most two scalars per thread, both loaded before any digit work
@@ -258,23 +285,10 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, cons
     for (int s = 0; s < 2; s++) {
         if (idx[s] == ~(size_t)0) continue;
         const size_t i = idx[s];
-        Fe<SC> k = from_mont(scl[s]);
-        int carry = 0;
-        for (int w = 0; w < W; w++) {
-            const int bw = ws.bits[w];
-            int d = (int)extract_bits(k, ws.off[w], bw) + carry;
-            if (d > (1 << (bw - 1))) { d -= (1 << bw); carry = 1; } else carry = 0;
-            uint32_t key = 0xffffffffu;
-            const uint32_t bb = (uint32_t)((d > 0 ? d : -d) - 1);  // bucket |d| - 1 of group w mod G
-            if (d && (bb & smask) == sres) {
-                // bucket stripe (slog > 0): only buckets bb = 2^slog j + sres, renumbered j;
-                // c is then the stripe's c - slog
-                const uint32_t bk = ((uint32_t)(w & (G - 1)) << (c - 1)) | (bb >> slog);
-                key = bk | (d < 0 ? 0x80000000u : 0u);
-                atomicAdd(&hh[bin_of(bk, c, kbits, h)], 1u);
-            }
-            keys[(size_t)w * n + i] = key;
-        }
+        scalar_keys<SC>(scl[s], c, W, ws, G, slog, sres, [&](int w, uint32_t key) {
+            if (key != 0xffffffffu) atomicAdd(&hh[bin_of(key & 0x7fffffffu, c, kbits, h)], 1u);
+            if (keys) keys[(size_t)w * n + i] = key;
+        });
     }
     __syncthreads();
     for (int j = threadIdx.x; j < nbins; j += blockDim.x) hist[(size_t)j * nblocks + blockIdx.x] = hh[j];
@@ -348,6 +362,69 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_
         tmp_entry[pos] = s_entry[q];
         if (tmp_key) {
             if (key16) static_cast<uint16_t*>(tmp_key)[pos] = (uint16_t)pk;  // the low kbits - h <= 16 bits
+            else static_cast<uint32_t*>(tmp_key)[pos] = pk;
+        }
+    }
+}
+
+// Phase C from the scalars: the block's keys derived again (scalar_keys) rather
+// than read back -- phase A then writes no key array (W n 4 B each way, ~1 GB per
+// 2^24 sort); otherwise k_bin_scatter's LDS-staged partition and coalesced runs
+template <class SC>
+__global__ void __launch_bounds__(256) k_bin_scatter_s(const Fe<SC>* scalars, const uint32_t* sidx, size_t n, int W,
+                                                       int c, WinSpec ws, int G, int kbits, int spb, int nbins, int h,
+                                                       const uint32_t* hist, const uint32_t* hoff, uint32_t nblocks,
+                                                       uint32_t* tmp_entry, void* tmp_key, int key16, int slog,
+                                                       uint32_t sres) {
+    extern __shared__ uint32_t sm[];
+    const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
+    uint32_t* lbase = sm;         // nbins: local exclusive offsets
+    uint32_t* lcur = sm + nbins;  // nbins: local cursors
+    uint32_t* s_entry = sm + 2 * nbins;
+    uint32_t* s_key = s_entry + spb * W;
+    const int lowbits = kbits - h;
+    const uint32_t jb = threadIdx.x;
+    const bool has = (int)jb < nbins;
+    const uint32_t cnt = has ? hist[(size_t)jb * nblocks + tile] : 0u;
+    const uint32_t gof = has ? hoff[(size_t)jb * nblocks + tile] : 0u;
+    __shared__ uint32_t wsum[4];
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan256(cnt, wsum, &tot);
+    if (has) {
+        lbase[jb] = ex;
+        lcur[jb] = ex;
+    }
+    __syncthreads();
+    const size_t i0 = (size_t)tile * spb;
+    const int ns = (int)min((size_t)spb, n - i0);
+    // spb <= 512: at most two scalars per thread, both loaded before any digit work
+    Fe<SC> scl[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; s2++) {
+        const int t = (int)threadIdx.x + 256 * s2;
+        if (t < ns) scl[s2] = ld(scalars + (sidx ? sidx[i0 + t] : i0 + t));
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; s2++) {
+        const int t = (int)threadIdx.x + 256 * s2;
+        if (t >= ns) continue;
+        scalar_keys<SC>(scl[s2], c, W, ws, G, slog, sres, [&](int w, uint32_t key) {
+            if (key == 0xffffffffu) return;
+            const uint32_t pk = bucket_perm(key & 0x7fffffffu, c);
+            const uint32_t q = atomicAdd(&lcur[pk >> lowbits], 1u);
+            s_entry[q] = (uint32_t)((size_t)(w / G) * n + i0 + t) | (key & 0x80000000u);  // the stored copy of window w
+            s_key[q] = pk;
+        });
+    }
+    __syncthreads();
+    if (has) lbase[jb] = gof - ex;
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < tot; q += blockDim.x) {
+        const uint32_t pk = s_key[q];
+        const uint32_t pos = lbase[pk >> lowbits] + q;
+        tmp_entry[pos] = s_entry[q];
+        if (tmp_key) {
+            if (key16) static_cast<uint16_t*>(tmp_key)[pos] = (uint16_t)pk;
             else static_cast<uint32_t*>(tmp_key)[pos] = pk;
         }
     }
@@ -544,6 +621,8 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
             ns <<= r;
         }
     }
+    // GG_SORT_KEYS=1 (A/B): phase A stores every key and phase C reads them back
+    static const bool keys_path = getenv("GG_SORT_KEYS") && atoi(getenv("GG_SORT_KEYS"));
     s->keys.reserve(total * 4);
     s->tmp_entry.reserve(total * 4);
     s->tmp_key.reserve(total * 4);
@@ -563,12 +642,13 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     if (b->scurve)
         hipLaunchKernelGGL(k_digits_hist<FrBlsCfg>, dim3(nblocks), dim3(256), nbins * 4, st,
                            (const FrBls*)scalars_dev, b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n,
-                           c, W, b->win, G, kbits, spb, nbins, h, s->keys.as<uint32_t>(),
+                           c, W, b->win, G, kbits, spb, nbins, h, keys_path ? s->keys.as<uint32_t>() : nullptr,
                            s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
     else
         hipLaunchKernelGGL(k_digits_hist<FrCfg>, dim3(nblocks), dim3(256), nbins * 4, st, scalars_dev,
                            b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, G, kbits, spb,
-                           nbins, h, s->keys.as<uint32_t>(), s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
+                           nbins, h, keys_path ? s->keys.as<uint32_t>() : nullptr, s->hist.as<uint32_t>(), nblocks,
+                           s->slog, s->sres);
     GG_HIP(hipGetLastError());
     exclusive_scan(s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nh, st, s->scan_tmp);
     // segment starts ping-pong between bin_start and seg2; the last pass writes offsets
@@ -586,9 +666,21 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     auto ent_out = [&](int j) { return ((S - 1 - j) % 2 == 0) ? &s->sorted : &s->tmp_entry; };
     auto key_out = [&](int j) { return (j % 2 == 0) ? &s->tmp_key : &s->keys; };
     const bool key16 = kbits - h <= 16;
-    hipLaunchKernelGGL(k_bin_scatter, dim3(nblocks), dim3(256), lds_c, st, s->keys.as<uint32_t>(),
-                       n, W, c, G, kbits, spb, nbins, h, s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nblocks,
-                       ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->p : nullptr, (int)key16);
+    const uint32_t* sidx = b->has_sidx ? b->sidx.as<uint32_t>() : nullptr;
+    if (keys_path)
+        hipLaunchKernelGGL(k_bin_scatter, dim3(nblocks), dim3(256), lds_c, st, s->keys.as<uint32_t>(),
+                           n, W, c, G, kbits, spb, nbins, h, s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nblocks,
+                           ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->p : nullptr, (int)key16);
+    else if (b->scurve)
+        hipLaunchKernelGGL(k_bin_scatter_s<FrBlsCfg>, dim3(nblocks), dim3(256), lds_c, st,
+                           (const FrBls*)scalars_dev, sidx, n, W, c, b->win, G, kbits, spb, nbins, h,
+                           s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nblocks, ent_out(0)->as<uint32_t>(),
+                           S > 1 ? key_out(0)->p : nullptr, (int)key16, s->slog, s->sres);
+    else
+        hipLaunchKernelGGL(k_bin_scatter_s<FrCfg>, dim3(nblocks), dim3(256), lds_c, st, scalars_dev, sidx, n, W,
+                           c, b->win, G, kbits, spb, nbins, h, s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(),
+                           nblocks, ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->p : nullptr, (int)key16,
+                           s->slog, s->sres);
     GG_HIP(hipGetLastError());
     uint32_t nseg = (uint32_t)nbins;
     int shift = kbits - h;
