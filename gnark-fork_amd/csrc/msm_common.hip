@@ -233,8 +233,7 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t* cnt, uint32_t d, bool va
 
 // The sort key of every window of one scalar, in window order (the signed digits
 // carry upward): fn(w, key), key = bucket | sign bit, or 0xffffffff for a zero
-// digit or (bucket stripes, slog > 0) a bucket outside stripe sres.  Phases A and
-// C both derive their keys here, so their counts agree by construction.
+// digit or (bucket stripes, slog > 0) a bucket outside stripe sres.
 template <class SC, class Fn>
 __device__ __forceinline__ void scalar_keys(const Fe<SC>& scl, int c, int W, const WinSpec& ws, int G, int slog,
                                             uint32_t sres, Fn&& fn) {
@@ -257,8 +256,9 @@ __device__ __forceinline__ void scalar_keys(const Fe<SC>& scl, int c, int W, con
     }
 }
 
-// Phase A: the block's bin histogram; keys (nullable) keeps every key for a
-// phase C that reads them (GG_SORT_KEYS=1) instead of deriving them again
+// Phase A: the block's bin histogram and every entry's key for phase C.  (Round
+// 4 measured phase C deriving the keys again from the scalars instead: 3.37 vs
+// 3.14 ms per 2^24 sort, profiles/r04_c_sort_ab.txt -- the key array stays.)
 template <class SC>
 __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, const uint32_t* sidx,
                                                      size_t n, int c, int W, WinSpec ws, int G, int kbits,
@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, cons
         const size_t i = idx[s];
         scalar_keys<SC>(scl[s], c, W, ws, G, slog, sres, [&](int w, uint32_t key) {
             if (key != 0xffffffffu) atomicAdd(&hh[bin_of(key & 0x7fffffffu, c, kbits, h)], 1u);
-            if (keys) keys[(size_t)w * n + i] = key;
+            keys[(size_t)w * n + i] = key;
         });
     }
     __syncthreads();
@@ -362,69 +362,6 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_
         tmp_entry[pos] = s_entry[q];
         if (tmp_key) {
             if (key16) static_cast<uint16_t*>(tmp_key)[pos] = (uint16_t)pk;  // the low kbits - h <= 16 bits
-            else static_cast<uint32_t*>(tmp_key)[pos] = pk;
-        }
-    }
-}
-
-// Phase C from the scalars: the block's keys derived again (scalar_keys) rather
-// than read back -- phase A then writes no key array (W n 4 B each way, ~1 GB per
-// 2^24 sort); otherwise k_bin_scatter's LDS-staged partition and coalesced runs
-template <class SC>
-__global__ void __launch_bounds__(256) k_bin_scatter_s(const Fe<SC>* scalars, const uint32_t* sidx, size_t n, int W,
-                                                       int c, WinSpec ws, int G, int kbits, int spb, int nbins, int h,
-                                                       const uint32_t* hist, const uint32_t* hoff, uint32_t nblocks,
-                                                       uint32_t* tmp_entry, void* tmp_key, int key16, int slog,
-                                                       uint32_t sres) {
-    extern __shared__ uint32_t sm[];
-    const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
-    uint32_t* lbase = sm;         // nbins: local exclusive offsets
-    uint32_t* lcur = sm + nbins;  // nbins: local cursors
-    uint32_t* s_entry = sm + 2 * nbins;
-    uint32_t* s_key = s_entry + spb * W;
-    const int lowbits = kbits - h;
-    const uint32_t jb = threadIdx.x;
-    const bool has = (int)jb < nbins;
-    const uint32_t cnt = has ? hist[(size_t)jb * nblocks + tile] : 0u;
-    const uint32_t gof = has ? hoff[(size_t)jb * nblocks + tile] : 0u;
-    __shared__ uint32_t wsum[4];
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan256(cnt, wsum, &tot);
-    if (has) {
-        lbase[jb] = ex;
-        lcur[jb] = ex;
-    }
-    __syncthreads();
-    const size_t i0 = (size_t)tile * spb;
-    const int ns = (int)min((size_t)spb, n - i0);
-    // spb <= 512: at most two scalars per thread, both loaded before any digit work
-    Fe<SC> scl[2];
-#pragma unroll
-    for (int s2 = 0; s2 < 2; s2++) {
-        const int t = (int)threadIdx.x + 256 * s2;
-        if (t < ns) scl[s2] = ld(scalars + (sidx ? sidx[i0 + t] : i0 + t));
-    }
-#pragma unroll
-    for (int s2 = 0; s2 < 2; s2++) {
-        const int t = (int)threadIdx.x + 256 * s2;
-        if (t >= ns) continue;
-        scalar_keys<SC>(scl[s2], c, W, ws, G, slog, sres, [&](int w, uint32_t key) {
-            if (key == 0xffffffffu) return;
-            const uint32_t pk = bucket_perm(key & 0x7fffffffu, c);
-            const uint32_t q = atomicAdd(&lcur[pk >> lowbits], 1u);
-            s_entry[q] = (uint32_t)((size_t)(w / G) * n + i0 + t) | (key & 0x80000000u);  // the stored copy of window w
-            s_key[q] = pk;
-        });
-    }
-    __syncthreads();
-    if (has) lbase[jb] = gof - ex;
-    __syncthreads();
-    for (uint32_t q = threadIdx.x; q < tot; q += blockDim.x) {
-        const uint32_t pk = s_key[q];
-        const uint32_t pos = lbase[pk >> lowbits] + q;
-        tmp_entry[pos] = s_entry[q];
-        if (tmp_key) {
-            if (key16) static_cast<uint16_t*>(tmp_key)[pos] = (uint16_t)pk;
             else static_cast<uint32_t*>(tmp_key)[pos] = pk;
         }
     }
@@ -621,8 +558,6 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
             ns <<= r;
         }
     }
-    // GG_SORT_KEYS=1 (A/B): phase A stores every key and phase C reads them back
-    static const bool keys_path = getenv("GG_SORT_KEYS") && atoi(getenv("GG_SORT_KEYS"));
     s->keys.reserve(total * 4);
     s->tmp_entry.reserve(total * 4);
     s->tmp_key.reserve(total * 4);
@@ -642,13 +577,12 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     if (b->scurve)
         hipLaunchKernelGGL(k_digits_hist<FrBlsCfg>, dim3(nblocks), dim3(256), nbins * 4, st,
                            (const FrBls*)scalars_dev, b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n,
-                           c, W, b->win, G, kbits, spb, nbins, h, keys_path ? s->keys.as<uint32_t>() : nullptr,
+                           c, W, b->win, G, kbits, spb, nbins, h, s->keys.as<uint32_t>(),
                            s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
     else
         hipLaunchKernelGGL(k_digits_hist<FrCfg>, dim3(nblocks), dim3(256), nbins * 4, st, scalars_dev,
                            b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, G, kbits, spb,
-                           nbins, h, keys_path ? s->keys.as<uint32_t>() : nullptr, s->hist.as<uint32_t>(), nblocks,
-                           s->slog, s->sres);
+                           nbins, h, s->keys.as<uint32_t>(), s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
     GG_HIP(hipGetLastError());
     exclusive_scan(s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nh, st, s->scan_tmp);
     // segment starts ping-pong between bin_start and seg2; the last pass writes offsets
@@ -666,21 +600,9 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     auto ent_out = [&](int j) { return ((S - 1 - j) % 2 == 0) ? &s->sorted : &s->tmp_entry; };
     auto key_out = [&](int j) { return (j % 2 == 0) ? &s->tmp_key : &s->keys; };
     const bool key16 = kbits - h <= 16;
-    const uint32_t* sidx = b->has_sidx ? b->sidx.as<uint32_t>() : nullptr;
-    if (keys_path)
-        hipLaunchKernelGGL(k_bin_scatter, dim3(nblocks), dim3(256), lds_c, st, s->keys.as<uint32_t>(),
-                           n, W, c, G, kbits, spb, nbins, h, s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nblocks,
-                           ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->p : nullptr, (int)key16);
-    else if (b->scurve)
-        hipLaunchKernelGGL(k_bin_scatter_s<FrBlsCfg>, dim3(nblocks), dim3(256), lds_c, st,
-                           (const FrBls*)scalars_dev, sidx, n, W, c, b->win, G, kbits, spb, nbins, h,
-                           s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nblocks, ent_out(0)->as<uint32_t>(),
-                           S > 1 ? key_out(0)->p : nullptr, (int)key16, s->slog, s->sres);
-    else
-        hipLaunchKernelGGL(k_bin_scatter_s<FrCfg>, dim3(nblocks), dim3(256), lds_c, st, scalars_dev, sidx, n, W,
-                           c, b->win, G, kbits, spb, nbins, h, s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(),
-                           nblocks, ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->p : nullptr, (int)key16,
-                           s->slog, s->sres);
+    hipLaunchKernelGGL(k_bin_scatter, dim3(nblocks), dim3(256), lds_c, st, s->keys.as<uint32_t>(),
+                       n, W, c, G, kbits, spb, nbins, h, s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nblocks,
+                       ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->p : nullptr, (int)key16);
     GG_HIP(hipGetLastError());
     uint32_t nseg = (uint32_t)nbins;
     int shift = kbits - h;
