@@ -181,6 +181,8 @@ struct PlonkPeer {
     gg_domain_t d0 = nullptr;
     DevBuf creg, qk_lag;
     std::vector<hipStream_t> xs;
+    hipEvent_t reg_ev = nullptr;  // the last regular-form push to part 0 (creg free again)
+    bool reg_pending = false;
     ~PlonkPeer() {
         int cur = 0;
         const bool restore = hipGetDevice(&cur) == hipSuccess;
@@ -199,6 +201,7 @@ struct PlonkPeer {
         creg.release();
         qk_lag.release();
         for (hipStream_t x : xs) (void)hipStreamDestroy(x);
+        if (reg_ev) (void)hipEventDestroy(reg_ev);
         perm_slice.release();
         pz.release();
         ar.buf.release();
@@ -561,13 +564,20 @@ static PlonkPeer* canon_owner(const Key* pk, size_t i) { return pk->peers[i % pk
 // form in p->in[b] (ordered on p->s[3]); the size-n inverse DIF there (canonical
 // bit-reversed, in place), the regular form in creg when part 0 needs it, then the
 // pushes, each on its own stream (one xGMI link each): bit-reversed to every other
-// peer with quotient units and to brev0 on part 0, regular to reg0
+// peer with quotient units and to brev0 on part 0, regular to reg0.  Returns once
+// the bit-reversed form is everywhere (the quotient units need it next); the
+// regular push (the openings need it, much later) stays in flight behind
+// p->reg_ev, which canon_wait_regular and the owner's next task wait for.
 static void canon_run(Key* pk, size_t pi, int b, FrB* brev0, FrB* reg0, const std::function<void(hipStream_t)>& fill) {
     PlonkPeer* p = pk->peers[pi].get();
     const size_t n = pk->n, nb = 32 * n;
     GG_HIP(hipSetDevice(p->device));
     const auto a = std::chrono::steady_clock::now();
     hipStream_t q = p->s[3];
+    if (p->reg_pending) {  // creg is read by the previous task's regular push
+        GG_HIP(hipEventSynchronize(p->reg_ev));
+        p->reg_pending = false;
+    }
     fill(q);
     plk::ntt(p->d0, p->in[b].p, 1, 0, 0, q);  // FFTInverse DIF: natural in -> bit-reversed out
     if (reg0) plk::bit_reverse(F(p->in[b]), F(p->creg), n, q);
@@ -580,7 +590,12 @@ static void canon_run(Key* pk, size_t pi, int b, FrB* brev0, FrB* reg0, const st
             mb += nb / 1e6;
         }
     GG_HIP(hipMemcpyPeerAsync(brev0, pk->device, p->in[b].p, p->device, nb, p->xs[x++]));
-    if (reg0) GG_HIP(hipMemcpyPeerAsync(reg0, pk->device, p->creg.p, p->device, nb, p->xs[x++]));
+    if (reg0) {
+        hipStream_t r = p->xs[x];
+        GG_HIP(hipMemcpyPeerAsync(reg0, pk->device, p->creg.p, p->device, nb, r));
+        GG_HIP(hipEventRecord(p->reg_ev, r));
+        p->reg_pending = true;
+    }
     mb += (reg0 ? 2.0 : 1.0) * nb / 1e6;
     for (size_t i = 0; i < x; i++) GG_HIP(hipStreamSynchronize(p->xs[i]));
     std::lock_guard<std::mutex> lk(pk->tmu);
@@ -588,6 +603,16 @@ static void canon_run(Key* pk, size_t pi, int b, FrB* brev0, FrB* reg0, const st
     T.canon_count += 1;
     T.canon_ms += ms_since(a);
     T.canon_mb += mb;
+}
+
+// every owner's last regular-form push to part 0 has landed (before the openings)
+static void canon_wait_regular(Key* pk) {
+    for (auto& pp : pk->peers) {
+        PlonkPeer* p = pp.get();
+        if (!p->reg_pending) continue;
+        GG_HIP(hipEventSynchronize(p->reg_ev));
+        p->reg_pending = false;
+    }
 }
 
 static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, const void* omega_big,
@@ -855,6 +880,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
                 p->creg.alloc(nb);
                 p->xs.resize(pk->peers.size() + 2);
                 for (hipStream_t& x : p->xs) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+                GG_HIP(hipEventCreateWithFlags(&p->reg_ev, hipEventDisableTiming));
             }
             if (tasks[i] == 4) {
                 p->qk_lag.alloc(nb);
@@ -1297,6 +1323,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     mark();
     const FrB zeta = derive(fs, "zeta", {&P.h[0], &P.h[1], &P.h[2]});
     const FrB zn = pow_u64(zeta, n), zn1 = zn - FrB::one();
+    if (peers_on) canon_wait_regular(pk);  // the regular L, R, O, Z, Pi_j for the openings
     // ---- openZ (prove.go:635-652): blinded Z = Z - bz + bz X^n, opened at zeta * omega
     auto blinded = [&](const DevBuf& canon, const std::vector<FrB>& b, DevBuf& out, hipStream_t q) {
         dcopy(out.p, canon.p, nb, q);
