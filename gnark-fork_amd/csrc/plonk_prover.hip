@@ -183,6 +183,7 @@ struct PlonkPeer {
     std::vector<hipStream_t> xs;
     hipEvent_t reg_ev = nullptr;  // the last regular-form push to part 0 (creg free again)
     bool reg_pending = false;
+    hipStream_t cs = nullptr;     // the tasks' transforms (stream 3 belongs to the quotient units)
     ~PlonkPeer() {
         int cur = 0;
         const bool restore = hipGetDevice(&cur) == hipSuccess;
@@ -202,6 +203,7 @@ struct PlonkPeer {
         qk_lag.release();
         for (hipStream_t x : xs) (void)hipStreamDestroy(x);
         if (reg_ev) (void)hipEventDestroy(reg_ev);
+        if (cs) (void)hipStreamDestroy(cs);
         perm_slice.release();
         pz.release();
         ar.buf.release();
@@ -561,7 +563,7 @@ static std::vector<int> canon_tasks(const Key* pk) {
 static PlonkPeer* canon_owner(const Key* pk, size_t i) { return pk->peers[i % pk->peers.size()].get(); }
 
 // one canonical-form task on peer pi: `fill` leaves the polynomial's Lagrange
-// form in p->in[b] (ordered on p->s[3]); the size-n inverse DIF there (canonical
+// form in p->in[b] (ordered on p->cs); the size-n inverse DIF there (canonical
 // bit-reversed, in place), the regular form in creg when part 0 needs it, then the
 // pushes, each on its own stream (one xGMI link each): bit-reversed to every other
 // peer with quotient units and to brev0 on part 0, regular to reg0.  Returns once
@@ -573,7 +575,7 @@ static void canon_run(Key* pk, size_t pi, int b, FrB* brev0, FrB* reg0, const st
     const size_t n = pk->n, nb = 32 * n;
     GG_HIP(hipSetDevice(p->device));
     const auto a = std::chrono::steady_clock::now();
-    hipStream_t q = p->s[3];
+    hipStream_t q = p->cs;
     if (p->reg_pending) {  // creg is read by the previous task's regular push
         GG_HIP(hipEventSynchronize(p->reg_ev));
         p->reg_pending = false;
@@ -881,6 +883,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
                 p->xs.resize(pk->peers.size() + 2);
                 for (hipStream_t& x : p->xs) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
                 GG_HIP(hipEventCreateWithFlags(&p->reg_ev, hipEventDisableTiming));
+                GG_HIP(hipStreamCreateWithFlags(&p->cs, hipStreamNonBlocking));
             }
             if (tasks[i] == 4) {
                 p->qk_lag.alloc(nb);
@@ -1139,13 +1142,52 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         GG_HIP(hipStreamSynchronize(s[0]));
         const size_t zi = (ctasks.size() - 1) % pk->peers.size();
         zfut = std::async(std::launch::async, [&, zi] {
-            if (cfut[zi].valid()) cfut[zi].wait();  // its earlier tasks (creg, stream 3) first
+            if (cfut[zi].valid()) cfut[zi].wait();  // its earlier tasks (creg, stream cs) first
             canon_run(pk, zi, 3, F(pk->cbrev[3]), F(pk->can[3]), [](hipStream_t) {});
         }).share();
     } else if (!dz) {
         lag_to_canonical(pk, F(pk->zlag), F(pk->cbrev[3]), F(pk->can[3]), s[1]);  // overlaps the Z commitment
     }
-    P.z = to_aff(jac_add(red(pk, msm_jac(pk, pk->kzg_lag, 0, F(pk->zlag), s[0], peers_on)), fblind[3].get()));
+    // the Z commitment in flight; meanwhile each part's first quotient unit takes
+    // its evaluations of L, R, O, Qk, Pi_j (only Z's wait for Z)
+    std::future<BJac> fzc = std::async(msm_policy(), [&] {
+        GG_HIP(hipSetDevice(pk->device));
+        return msm_jac(pk, pk->kzg_lag, 0, F(pk->zlag), s[0], peers_on);
+    });
+    auto unit_pre = [&](const QUnit* q, const FrB* const* src, FrB* const* e, hipStream_t st) {
+        for (int k = 0; k < 3; k++) unit_eval(pk, q->dom, q->kappa, src[k], e[k], st);
+        unit_eval(pk, q->dom, q->kappa, src[4], e[6], st);
+        for (int j = 0; j < n_cmt; j++) unit_eval(pk, q->dom, q->kappa, src[5 + j], e[7 + j], st);
+    };
+    if (peers_on) {  // L R O Qk Pi_j have reached every part
+        const auto w = std::chrono::steady_clock::now();
+        for (auto& f : cfut)
+            if (f.valid()) f.get();
+        {
+            std::lock_guard<std::mutex> lk(pk->tmu);
+            pk->ptimes[0].wait_ms += ms_since(w);
+        }
+        for (auto& pp : pk->peers) {
+            PlonkPeer* p = pp.get();
+            if (p->units.empty()) continue;
+            GG_HIP(hipSetDevice(p->device));
+            const FrB* ins[5 + plk::MAX_CMT] = {};
+            for (int k = 0; k < 5 + n_cmt; k++) ins[k] = F(p->in[k]);
+            FrB* e[7 + plk::MAX_CMT] = {};
+            for (int k = 0; k < 7 + n_cmt; k++) e[k] = F(p->cev[k]);
+            unit_pre(p->units[0].get(), ins, e, p->s[3]);
+        }
+        GG_HIP(hipSetDevice(pk->device));
+    }
+    if (!pk->units.empty()) {  // part 0's first unit: slot 0, stream 2
+        const FrB* src[5 + plk::MAX_CMT] = {F(pk->cbrev[0]), F(pk->cbrev[1]), F(pk->cbrev[2]), F(pk->cbrev[3]),
+                                            F(pk->qkc)};
+        for (int j = 0; j < n_cmt; j++) src[5 + j] = F(pk->pi_brev[j]);
+        FrB* e[7 + plk::MAX_CMT] = {};
+        for (int k = 0; k < 7 + n_cmt; k++) e[k] = F(pk->cev[0][k]);
+        unit_pre(pk->units[0].get(), src, e, s[2]);
+    }
+    P.z = to_aff(jac_add(red(pk, fzc.get()), fblind[3].get()));
     mark();
     // ---- alpha (deriveAlpha, prove.go:504-512)
     P.bsb22.assign(cmt_digests, cmt_digests + n_cmt);
@@ -1219,13 +1261,13 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         memcpy(NP.out_scale.v, q->inv_den, 32);
         return NP;
     };
-    // one unit: its polynomials' evaluations, the numerator (scaled), and the
-    // first L - u stages of the big coset iFFT on its block
+    // one unit: its polynomials' evaluations (L R O Qk Pi_j already taken for a
+    // part's first unit: pre), the numerator (scaled), and the first L - u stages
+    // of the big coset iFFT on its block
     auto run_unit = [&](const QUnit* q, const FrB* const* src, FrB* const* e, FrB* zc, const FrB* tw0, FrB* cres,
-                        bool local, hipStream_t st) {
-        for (int k = 0; k < 4; k++) unit_eval(pk, q->dom, q->kappa, src[k], e[k], st);
-        unit_eval(pk, q->dom, q->kappa, src[4], e[6], st);
-        for (int j = 0; j < n_cmt; j++) unit_eval(pk, q->dom, q->kappa, src[5 + j], e[7 + j], st);
+                        bool local, bool pre, hipStream_t st) {
+        if (!pre) unit_pre(q, src, e, st);
+        unit_eval(pk, q->dom, q->kappa, src[3], e[3], st);
         if (pk->S > 1) unit_eval(pk, q->zdom, q->zkappa, src[3], zc, st);
         plk::NumParamsT<FrB> NP = unit_params(q, e, pk->S > 1 ? zc : nullptr, cres, local);
         if (pk->S == 1) NP.tw0 = tw0;
@@ -1236,10 +1278,8 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         }
     };
     std::vector<std::future<void>> peer_work;
-    if (peers_on) {  // every part's inputs: the canonical forms pushed by their owners
+    if (peers_on) {  // Z's canonical form pushed by its owner
         const auto w = std::chrono::steady_clock::now();
-        for (auto& f : cfut)
-            if (f.valid()) f.get();
         zfut.get();
         std::lock_guard<std::mutex> lk(pk->tmu);
         pk->ptimes[0].wait_ms += ms_since(w);
@@ -1256,7 +1296,8 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                 for (int k = 0; k < 5 + n_cmt; k++) ins[k] = F(p->in[k]);
                 FrB* e[7 + plk::MAX_CMT] = {};
                 for (int k = 0; k < 7 + n_cmt; k++) e[k] = F(p->cev[k]);
-                for (auto& qu : p->units) run_unit(qu.get(), ins, e, F(p->zc), F(p->tw0), F(qu->out), true, q);
+                for (size_t u = 0; u < p->units.size(); u++)
+                    run_unit(p->units[u].get(), ins, e, F(p->zc), F(p->tw0), F(p->units[u]->out), true, u == 0, q);
                 // the units' blocks back to the primary's cres (timed separately)
                 GG_HIP(hipEventRecord(p->ea[3], q));
                 for (auto& qu : p->units) {
@@ -1281,11 +1322,11 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         const FrB* src[5 + plk::MAX_CMT] = {F(pk->cbrev[0]), F(pk->cbrev[1]), F(pk->cbrev[2]), F(pk->cbrev[3]),
                                             F(pk->qkc)};
         for (int j = 0; j < n_cmt; j++) src[5 + j] = F(pk->pi_brev[j]);
-        for (auto& qu : pk->units) {
+        for (size_t u = 0; u < pk->units.size(); u++) {
             hipStream_t q = s[2 + slot];
             FrB* e[7 + plk::MAX_CMT] = {};
             for (int k = 0; k < 7 + n_cmt; k++) e[k] = F(pk->cev[slot][k]);
-            run_unit(qu.get(), src, e, F(pk->zc[slot]), F(pk->tw0), F(pk->cres), false, q);
+            run_unit(pk->units[u].get(), src, e, F(pk->zc[slot]), F(pk->tw0), F(pk->cres), false, u == 0, q);
             slot ^= 1;
         }
         std::lock_guard<std::mutex> lk(pk->tmu);
