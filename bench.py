@@ -546,7 +546,10 @@ class Groth16Bench:
                                                  for s in st) for e in range(len(st[0]["exchanges"]))],
                 "note": "last timed proof; per exchange of the distributed computeH: wait_before = peers still "
                         "computing (imbalance), push = this shard's N-1 hipMemcpyPeerAsync (xGMI), wait_after = "
-                        "peers' pushes into it in flight"}
+                        "peers' pushes into it in flight" + (
+                            "; REHEARSAL: shards share GPU(s) %s, so every shard's compute and copies contend for "
+                            "the same device(s) -- the times are not those of an N-GPU node" % sorted(set(self.devices))
+                            if len(set(self.devices)) < len(self.devices) else "")}
 
     def rank_timings(self, dist, xdev):
         """N > 1, one process per GPU: every rank's in-library stage times of the
