@@ -1164,15 +1164,15 @@ def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, 
     if devices and len(devices) > 1:  # one process, N device parts: where each part's time went
         extra["part_timings"] = [{k: round(v, 3) for k, v in p.items()} for p in pk.part_timings()]
         extra["devices"] = list(devices)
-    # configs[4] is 8 x MI355X: the primary part of an N-part one-process key
-    # (KZG base slices, numerator cosets over min(N, 4) parts) proved with its
-    # peers idle (rehearsal mode) -- the critical GPU's work on an N-GPU node
+    # configs[4] is 8 x MI355X: each device part of an N-part one-process key
+    # proved alone (rehearsal: the other parts skip their work) -- every GPU's
+    # share of an N-GPU proof timed on one GPU; the slowest part bounds the proof
     if projection and world == 1:
         del pk
-        proj = {"note": "primary part of an N-part key (gg_plonk_pk_create_multi) proved with the peer parts "
-                        "idle (gg_plonk_pk_set_rehearsal): the work of the GPU that runs every step outside the "
-                        "MSM slices and the other parts' cosets, without the xGMI copies; speedup = one-GPU ms / "
-                        "this"}
+        proj = {"note": "each device part of an N-part key (gg_plonk_pk_create_ex with devices) proved with only "
+                        "that part working (gg_plonk_pk_set_rehearsal_part): its MSM slices, ratio slice, quotient "
+                        "units, canonical-form tasks (peers) or tail stages and openings (part 0), without the xGMI "
+                        "copies; speedup = one-GPU ms / the slowest part"}
         kzg = DeviceBuffer(96 * (n + 3))
         msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bls_dev(n + 3, 61), n + 3, scalars_on_device=True, out=kzg)
         lag = DeviceBuffer(96 * n)
@@ -1183,17 +1183,24 @@ def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, 
             # one real N-part proof first: every part's MSM slices / cosets and copies
             pp.prove(pkm, L, R_, O, rng=rng())
             parts = pkm.part_timings()
-            pkm.set_rehearsal(True)
-            pp.prove(pkm, L, R_, O, rng=rng(), rehearsal_ok=True)
-            tp, stg = [], {}
-            for _ in range(max(reps, 3)):
-                t = time.perf_counter()
-                stg = {}
-                pp.prove(pkm, L, R_, O, timings=stg, rng=rng(), rehearsal_ok=True)
-                tp.append(1e3 * (time.perf_counter() - t))
-            med = sorted(tp)[len(tp) // 2]
-            proj[str(nd)] = {"primary_part_ms_median": med, "ms": [round(x, 2) for x in tp],
-                             "speedup": min(ts) / med, "stage_ms": stg,
+            per_part, stg0 = [], {}
+            for part in range(nd):
+                pkm.set_rehearsal(True, part=part)
+                pp.prove(pkm, L, R_, O, rng=rng(), rehearsal_ok=True)
+                tp = []
+                for _ in range(max(reps, 3)):
+                    t = time.perf_counter()
+                    stg = {}
+                    pp.prove(pkm, L, R_, O, timings=stg, rng=rng(), rehearsal_ok=True)
+                    tp.append(1e3 * (time.perf_counter() - t))
+                    if part == 0:
+                        stg0 = stg
+                per_part.append(sorted(tp)[len(tp) // 2])
+            pkm.set_rehearsal(False)
+            worst = max(per_part)
+            proj[str(nd)] = {"part_ms_median": [round(x, 2) for x in per_part], "slowest_part": per_part.index(worst),
+                             "slowest_part_ms": worst, "primary_part_ms_median": per_part[0],
+                             "speedup": min(ts) / worst, "primary_stage_ms": stg0,
                              "parts_of_a_real_proof_on_one_gpu": [{k: round(v, 3) for k, v in p.items()}
                                                                   for p in parts]}
             pkm.close()

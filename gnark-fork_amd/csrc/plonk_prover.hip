@@ -370,9 +370,10 @@ struct Key : gg_plonk_pk {
     // one-process multi-GPU: this key is part 0 of 1 + peers.size() device parts
     std::vector<std::unique_ptr<PlonkPeer>> peers;
     int n_parts = 1;  // device parts (unit p -> part p mod n_parts)
-    // gg_plonk_pk_set_rehearsal (timing only): the peer parts do nothing, the
-    // proof is not valid and gg_plonk_prove returns GG_REHEARSAL
+    // gg_plonk_pk_set_rehearsal / _part (timing only): only part solo_part does
+    // its work, the proof is not valid and gg_plonk_prove returns GG_REHEARSAL
     bool solo = false;
+    int solo_part = 0;
     std::mutex tmu;
     std::vector<PlonkPartTimes> ptimes;  // [part], last proof
     int n_cmt = 0;
@@ -478,6 +479,11 @@ static BJac peer_msm(Key* pk, int part, PlonkPeer* p, bool kzg, int wi, const Fr
     return j;
 }
 static bool plonk_solo(Key* pk) { return pk->solo; }
+// does device part `part` (0 = primary) do its work in this proof (a rehearsal
+// keeps only one part busy)
+static bool part_runs(const Key* pk, int part) { return !pk->solo || pk->solo_part == part; }
+// the multi-part protocol: peers exist and at least one of them works
+static bool peers_active(const Key* pk) { return !pk->peers.empty() && (!pk->solo || pk->solo_part > 0); }
 // this rank's partial MSM (the whole MSM on one GPU, or split over the key's
 // device parts and summed here); red() completes a process shard's partial
 static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStream_t st,
@@ -486,15 +492,16 @@ static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStr
     const bool kz = base == pk->kzg;
     const size_t lo = kz ? pk->k_lo : pk->l_lo;
     std::vector<std::future<BJac>> fs;
-    if (!pk->peers.empty() && !plonk_solo(pk)) {
+    if (peers_active(pk)) {
         GG_HIP(hipStreamSynchronize(st));  // the scalars are complete before the peers copy them
         for (size_t q = 0; q < pk->peers.size(); q++)
-            fs.push_back(std::async(std::launch::async, [pk, q, pp = pk->peers[q].get(), kz, wi, scal, peer_resident] {
+            if (part_runs(pk, (int)q + 1))
+                fs.push_back(std::async(std::launch::async, [pk, q, pp = pk->peers[q].get(), kz, wi, scal, peer_resident] {
                 return peer_msm(pk, (int)q + 1, pp, kz, wi, scal, peer_resident);
             }));
     }
     const auto a = std::chrono::steady_clock::now();
-    msm_device_work(base, pk->work[wi], (const Fr*)(scal + lo), &j, st);
+    if (part_runs(pk, 0)) msm_device_work(base, pk->work[wi], (const Fr*)(scal + lo), &j, st);
     const double own = ms_since(a);
     const auto w = std::chrono::steady_clock::now();
     for (auto& f : fs) j = jac_add(j, f.get());
@@ -986,7 +993,8 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         uploaded[k] = record(pk, s[k]);
     }
     const bool dz = !pk->peers.empty();
-    const bool peers_on = dz && !plonk_solo(pk);
+    const bool peers_on = peers_active(pk);
+    const bool run0 = part_runs(pk, 0);  // part 0's own kernels (a peer's rehearsal skips them)
     // multi-part keys: the canonical forms on the peers (canon_tasks), L R O as
     // soon as uploaded, Qk and Pi_j at once; Z after the ratio
     const std::vector<int> ctasks = dz ? canon_tasks(pk) : std::vector<int>();
@@ -996,7 +1004,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
             std::vector<int> mine;
             for (size_t i = 0; i + 1 < ctasks.size(); i++)
                 if (i % pk->peers.size() == pi) mine.push_back(ctasks[i]);
-            if (mine.empty()) continue;
+            if (mine.empty() || !part_runs(pk, (int)pi + 1)) continue;
             cfut[pi] = std::async(std::launch::async, [&, pi, mine] {
                 PlonkPeer* p = pk->peers[pi].get();
                 for (int b : mine) {
@@ -1088,8 +1096,9 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         const auto ta = std::chrono::steady_clock::now();
         const int64_t* pm = pk->perm.template as<int64_t>();
         pk->ar[0].reset();
-        plk::ratio_range(F(pk->lag[0]) + zlo, F(pk->lag[1]) + zlo, F(pk->lag[2]) + zlo, pm + zlo, pm + n + zlo,
-                         pm + 2 * n + zlo, zlo, zcnt, n, beta, gamma, pk->omega, pk->u, F(pk->pz), s[0], pk->ar[0]);
+        if (run0)
+            plk::ratio_range(F(pk->lag[0]) + zlo, F(pk->lag[1]) + zlo, F(pk->lag[2]) + zlo, pm + zlo, pm + n + zlo,
+                             pm + 2 * n + zlo, zlo, zcnt, n, beta, gamma, pk->omega, pk->u, F(pk->pz), s[0], pk->ar[0]);
         std::vector<FrB> agg(1 + pk->peers.size(), FrB::one());
         std::vector<std::future<void>> pf;
         if (peers_on)
@@ -1097,7 +1106,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                 pf.push_back(std::async(std::launch::async, [&, q] {
                     PlonkPeer* p = pk->peers[q].get();
                     const size_t cnt = p->l_hi - p->l_lo;
-                    if (!cnt) return;
+                    if (!cnt || !part_runs(pk, (int)q + 1)) return;
                     GG_HIP(hipSetDevice(p->device));
                     const auto a = std::chrono::steady_clock::now();
                     p->ar.reset();
@@ -1108,13 +1117,13 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                     std::lock_guard<std::mutex> lk(pk->tmu);
                     pk->ptimes[q + 1].ratio_ms += ms_since(a);
                 }));
-        agg[0] = zcnt ? fetch(F(pk->pz) + zcnt - 1, s[0]) : FrB::one();
+        agg[0] = zcnt && run0 ? fetch(F(pk->pz) + zcnt - 1, s[0]) : FrB::one();
         for (auto& f : pf) f.get();
         // prefix of part r = the product of the factors of the slices before it
         std::vector<FrB> pre(agg.size(), FrB::one());
         for (size_t r = 1; r < agg.size(); r++) pre[r] = pre[r - 1] * agg[r - 1];
-        plk::ratio_fixup(F(pk->pz), zcnt, pre[0], F(pk->zlag) + zlo, s[0]);
-        if (zown && zcnt)
+        if (run0) plk::ratio_fixup(F(pk->pz), zcnt, pre[0], F(pk->zlag) + zlo, s[0]);
+        if (zown && zcnt && run0)
             GG_HIP(hipMemcpyPeerAsync(F(zown->in[3]) + zlo, zown->device, F(pk->zlag) + zlo, pk->device, 32 * zcnt, s[0]));
         pf.clear();
         if (peers_on)
@@ -1122,7 +1131,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                 pf.push_back(std::async(std::launch::async, [&, q] {
                     PlonkPeer* p = pk->peers[q].get();
                     const size_t cnt = p->l_hi - p->l_lo;
-                    if (!cnt) return;
+                    if (!cnt || !part_runs(pk, (int)q + 1)) return;
                     GG_HIP(hipSetDevice(p->device));
                     const auto a = std::chrono::steady_clock::now();
                     plk::ratio_fixup(F(p->pz), cnt, pre[q + 1], F(p->scal[0]), p->s[0]);  // the Z slot of its MSM
@@ -1141,7 +1150,8 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     if (peers_on) {  // Z's canonical forms on its owner, once every slice has landed there
         GG_HIP(hipStreamSynchronize(s[0]));
         const size_t zi = (ctasks.size() - 1) % pk->peers.size();
-        zfut = std::async(std::launch::async, [&, zi] {
+        if (part_runs(pk, (int)zi + 1))
+            zfut = std::async(std::launch::async, [&, zi] {
             if (cfut[zi].valid()) cfut[zi].wait();  // its earlier tasks (creg, stream cs) first
             canon_run(pk, zi, 3, F(pk->cbrev[3]), F(pk->can[3]), [](hipStream_t) {});
         }).share();
@@ -1167,9 +1177,9 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
             std::lock_guard<std::mutex> lk(pk->tmu);
             pk->ptimes[0].wait_ms += ms_since(w);
         }
-        for (auto& pp : pk->peers) {
-            PlonkPeer* p = pp.get();
-            if (p->units.empty()) continue;
+        for (size_t pi = 0; pi < pk->peers.size(); pi++) {
+            PlonkPeer* p = pk->peers[pi].get();
+            if (p->units.empty() || !part_runs(pk, (int)pi + 1)) continue;
             GG_HIP(hipSetDevice(p->device));
             const FrB* ins[5 + plk::MAX_CMT] = {};
             for (int k = 0; k < 5 + n_cmt; k++) ins[k] = F(p->in[k]);
@@ -1179,7 +1189,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         }
         GG_HIP(hipSetDevice(pk->device));
     }
-    if (!pk->units.empty()) {  // part 0's first unit: slot 0, stream 2
+    if (run0 && !pk->units.empty()) {  // part 0's first unit: slot 0, stream 2
         const FrB* src[5 + plk::MAX_CMT] = {F(pk->cbrev[0]), F(pk->cbrev[1]), F(pk->cbrev[2]), F(pk->cbrev[3]),
                                             F(pk->qkc)};
         for (int j = 0; j < n_cmt; j++) src[5 + j] = F(pk->pi_brev[j]);
@@ -1280,14 +1290,14 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     std::vector<std::future<void>> peer_work;
     if (peers_on) {  // Z's canonical form pushed by its owner
         const auto w = std::chrono::steady_clock::now();
-        zfut.get();
+        if (zfut.valid()) zfut.get();
         std::lock_guard<std::mutex> lk(pk->tmu);
         pk->ptimes[0].wait_ms += ms_since(w);
     }
     if (peers_on) {
         for (size_t pi = 0; pi < pk->peers.size(); pi++) {
             PlonkPeer* p = pk->peers[pi].get();
-            if (p->units.empty()) continue;
+            if (p->units.empty() || !part_runs(pk, (int)pi + 1)) continue;
             peer_work.push_back(std::async(std::launch::async, [&, p, pi] {
                 GG_HIP(hipSetDevice(p->device));
                 const auto ta = std::chrono::steady_clock::now();
@@ -1322,7 +1332,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         const FrB* src[5 + plk::MAX_CMT] = {F(pk->cbrev[0]), F(pk->cbrev[1]), F(pk->cbrev[2]), F(pk->cbrev[3]),
                                             F(pk->qkc)};
         for (int j = 0; j < n_cmt; j++) src[5 + j] = F(pk->pi_brev[j]);
-        for (size_t u = 0; u < pk->units.size(); u++) {
+        for (size_t u = 0; run0 && u < pk->units.size(); u++) {
             hipStream_t q = s[2 + slot];
             FrB* e[7 + plk::MAX_CMT] = {};
             for (int k = 0; k < 7 + n_cmt; k++) e[k] = F(pk->cev[slot][k]);
@@ -1330,7 +1340,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
             slot ^= 1;
         }
         std::lock_guard<std::mutex> lk(pk->tmu);
-        pk->ptimes[0].coset_count += (double)pk->units.size();
+        if (run0) pk->ptimes[0].coset_count += (double)pk->units.size();
     }
     {
         const auto w = std::chrono::steady_clock::now();
@@ -1341,11 +1351,13 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     record_wait(pk, s[3], s[2]);
     // h, canonical regular: the last log2(U) stages of FFTInverse(DIT, OnCoset) over
     // the units' blocks (or, for domains below 2^12, the whole inverse here)
-    if (pk->split_idft) ntt_tail_inverse_coset(pk->d1, F(pk->cres), pk->log_u, s[2]);
-    else plk::ntt(pk->d1, F(pk->cres), 1, 1, 1, s[2]);
-    for (int k = 0; k < 3; k++) {  // n + 2 coefficients, the (n + 3)-th MSM scalar zero
-        dcopy(pk->hpad[k].p, F(pk->cres) + (n + 2) * k, 32 * (n + 2), s[2]);
-        zero(F(pk->hpad[k]) + n + 2, 32, s[2]);
+    if (run0) {
+        if (pk->split_idft) ntt_tail_inverse_coset(pk->d1, F(pk->cres), pk->log_u, s[2]);
+        else plk::ntt(pk->d1, F(pk->cres), 1, 1, 1, s[2]);
+        for (int k = 0; k < 3; k++) {  // n + 2 coefficients, the (n + 3)-th MSM scalar zero
+            dcopy(pk->hpad[k].p, F(pk->cres) + (n + 2) * k, 32 * (n + 2), s[2]);
+            zero(F(pk->hpad[k]) + n + 2, 32, s[2]);
+        }
     }
     for (int k = 0; k < 3; k++) record_wait(pk, s[2], s[k]);
     mark();
@@ -1367,6 +1379,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     if (peers_on) canon_wait_regular(pk);  // the regular L, R, O, Z, Pi_j for the openings
     // ---- openZ (prove.go:635-652): blinded Z = Z - bz + bz X^n, opened at zeta * omega
     auto blinded = [&](const DevBuf& canon, const std::vector<FrB>& b, DevBuf& out, hipStream_t q) {
+        if (!run0) return;
         dcopy(out.p, canon.p, nb, q);
         zero(F(out) + n, nb3 - nb, q);
         std::vector<FrB> head(b.size()), tail(b);
@@ -1377,8 +1390,8 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         GG_HIP(hipStreamSynchronize(q));  // host vectors
     };
     blinded(pk->can[3], bp[3], pk->bz, s[0]);
-    zero(F(pk->q1) + n + 2, 32, s[0]);  // Horner writes the n + 2 quotient coefficients
-    const FrB zu = eval_dev(pk, F(pk->bz), n + 3, zeta * pk->omega, F(pk->q1), F(pk->vals), 0, s[0]);
+    if (run0) zero(F(pk->q1) + n + 2, 32, s[0]);  // Horner writes the n + 2 quotient coefficients
+    const FrB zu = run0 ? eval_dev(pk, F(pk->bz), n + 3, zeta * pk->omega, F(pk->q1), F(pk->vals), 0, s[0]) : FrB::zero();
     P.zs_value = zu;
     std::future<BJac> fzs = std::async(msm_policy(), [&] {
         GG_HIP(hipSetDevice(pk->device));
@@ -1386,8 +1399,10 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     });
     // ---- foldH (prove.go:670-705) on s[2]
     const FrB zp = pow_u64(zeta, n + 2);
-    zero(F(pk->fold) + n + 2, 32, s[2]);  // fold_h writes n + 2 coefficients
-    plk::fold_h(F(pk->cres), n, zp, F(pk->fold), s[2]);
+    if (run0) {
+        zero(F(pk->fold) + n + 2, 32, s[2]);  // fold_h writes n + 2 coefficients
+        plk::fold_h(F(pk->cres), n, zp, F(pk->fold), s[2]);
+    }
     BJac fhd = jac_add(jac_add(BJac::from_affine(P.h[0]), jmul(P.h[1], zp)), jmul(P.h[2], zp * zp));
     const BAff folded_digest = to_aff(fhd);
     // ---- evaluations at zeta (blinded L, R, O; S1, S2; Qcp_i) on s[1]: one
@@ -1403,7 +1418,8 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
             fz[5 + j] = F(pk->qcp_reg[j]);
             lz_len[5 + j] = n;
         }
-        std::vector<FrB> v = eval_batch(pk, fz, lz_len, 5 + n_cmt, zeta, F(pk->vals) + 1, 1, s[1]);
+        std::vector<FrB> v = run0 ? eval_batch(pk, fz, lz_len, 5 + n_cmt, zeta, F(pk->vals) + 1, 1, s[1])
+                                  : std::vector<FrB>(5 + n_cmt, FrB::zero());
         for (int k = 0; k < 3; k++) lz[k] = v[k];
         s1z = v[3];
         s2z = v[4];
@@ -1417,7 +1433,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         FrB sb = (beta * zeta + l + gamma) * (beta * uz + r + gamma) * (beta * uuz + o + gamma);
         sb = -sb;
         const FrB lag = zn1 * inverse(zeta - FrB::one()) * alpha * alpha * pk->n_inv;
-        dcopy(pk->lin.p, pk->bz.p, nb3, s[1]);  // bz is complete: openZ's Horner synchronised s[0]
+        if (run0) dcopy(pk->lin.p, pk->bz.p, nb3, s[1]);  // bz is complete: openZ's Horner synchronised s[0]
         plk::LinParamsT<FrB> LP{};
         LP.z = F(pk->lin);
         LP.nz = n + 3;
@@ -1442,7 +1458,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         LP.rl = l * r;
         LP.o = o;
         LP.lag = lag;
-        plk::linearized(LP, s[1]);
+        if (run0) plk::linearized(LP, s[1]);
     }
     mark();
     const BAff lin_digest = to_aff(red(pk, commit_kzg(pk, 1, F(pk->lin), s[1])));
@@ -1459,7 +1475,8 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     {
         const FrB* fz[plk::EVAL_MAX] = {polys[0].first, polys[1].first};
         const size_t fl[plk::EVAL_MAX] = {polys[0].second, polys[1].second};
-        std::vector<FrB> v = eval_batch(pk, fz, fl, 2, zeta, F(pk->vals) + 16, 2, s[2]);
+        std::vector<FrB> v = run0 ? eval_batch(pk, fz, fl, 2, zeta, F(pk->vals) + 16, 2, s[2])
+                                  : std::vector<FrB>(2, FrB::zero());
         P.claimed[0] = v[0];
         P.claimed[1] = v[1];
     }
@@ -1494,11 +1511,13 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
             cf[i] = gp;
             gp = gp * gf;
         }
-        plk::lincomb(F(pk->q2), n + 3, fp, fl, cf, (int)polys.size(), s[2]);
+        if (run0) plk::lincomb(F(pk->q2), n + 3, fp, fl, cf, (int)polys.size(), s[2]);
     }
-    zero(F(pk->fold) + n + 2, 32, s[2]);  // reuse as the batch quotient (n + 2 of n + 3)
-    const FrB fv = eval_dev(pk, F(pk->q2), n + 3, zeta, F(pk->fold), F(pk->vals) + 18, 2, s[2]);
-    GG_CHECK(fv == fe, GG_ERR_INTERNAL, "batch opening: folded evaluation mismatch");
+    if (run0) {
+        zero(F(pk->fold) + n + 2, 32, s[2]);  // reuse as the batch quotient (n + 2 of n + 3)
+        const FrB fv = eval_dev(pk, F(pk->q2), n + 3, zeta, F(pk->fold), F(pk->vals) + 18, 2, s[2]);
+        GG_CHECK(fv == fe, GG_ERR_INTERNAL, "batch opening: folded evaluation mismatch");
+    }
     P.batched_h = to_aff(red(pk, commit_kzg(pk, 2, F(pk->fold), s[2])));
     P.zs_h = to_aff(red(pk, fzs.get()));
     mark();
@@ -1745,23 +1764,27 @@ extern "C" int gg_plonk_prove(gg_plonk_pk_t pk, const void* l, const void* r, co
     });
     const bool rehearsal = with_key(pk, [](auto* k) { return k->solo && !k->peers.empty(); });
     if (rehearsal) {
-        gg::set_last_error("timing rehearsal (gg_plonk_pk_set_rehearsal): the peer parts did nothing, the proof "
+        gg::set_last_error("timing rehearsal (gg_plonk_pk_set_rehearsal): only one device part worked, the proof "
                            "is NOT valid");
         return GG_REHEARSAL;
     }
     GG_CAPI_END
 }
 
-extern "C" int gg_plonk_pk_set_rehearsal(gg_plonk_pk_t pk, int on) {
+extern "C" int gg_plonk_pk_set_rehearsal_part(gg_plonk_pk_t pk, int part) {
     GG_CAPI_BEGIN
     GG_CHECK(pk, GG_ERR_INVALID_ARG, "null key");
     with_key(pk, [&](auto* k) {
         std::lock_guard<std::mutex> lk(k->mu);
-        k->solo = on != 0;
+        GG_CHECK(part >= -1 && part <= (int)k->peers.size(), GG_ERR_INVALID_ARG, "rehearsal part out of range");
+        k->solo = part >= 0;
+        k->solo_part = part >= 0 ? part : 0;
         return 0;
     });
     GG_CAPI_END
 }
+
+extern "C" int gg_plonk_pk_set_rehearsal(gg_plonk_pk_t pk, int on) { return gg_plonk_pk_set_rehearsal_part(pk, on ? 0 : -1); }
 
 extern "C" int gg_plonk_pk_part_timings(gg_plonk_pk_t pk, int part, double* out, int cap) {
     GG_CAPI_BEGIN

@@ -146,6 +146,7 @@ def _load():
                                       ctypes.POINTER(ctypes.c_int), PP], I),
         "gg_plonk_pk_devices": ([P, ctypes.POINTER(ctypes.c_int), I, ctypes.POINTER(ctypes.c_int)], I),
         "gg_plonk_pk_set_rehearsal": ([P, I], I),
+        "gg_plonk_pk_set_rehearsal_part": ([P, I], I),
         "gg_plonk_pk_part_timings": ([P, I, ctypes.POINTER(ctypes.c_double), I], I),
         "gg_plonk_pk_create_ex": ([I, I, I, P, P, P, P, S, P, PP, PP, I, P, S, P, P, I,
                                    ctypes.POINTER(ctypes.c_int), PP], I),
@@ -218,7 +219,8 @@ EXPORTED = [
     "gg_scs_solution_dev", "gg_r1cs_set_inputs", "gg_scs_set_inputs", "gg_r1cs_schedule", "gg_scs_schedule",
     "gg_msm_stripe", "gg_groth16_pk_create_stripe_ex", "gg_groth16_pk_stripe", "gg_groth16_mpk_split",
     "gg_hshard_create_ex", "gg_hshard_exchange_bytes", "gg_groth16_mpk_shard_timings",
-    "gg_groth16_mpk_set_rehearsal", "gg_plonk_pk_set_rehearsal", "gg_plonk_pk_part_timings",
+    "gg_groth16_mpk_set_rehearsal", "gg_plonk_pk_set_rehearsal", "gg_plonk_pk_set_rehearsal_part",
+    "gg_plonk_pk_part_timings",
     "gg_fr_evaluate_many",
 ]
 

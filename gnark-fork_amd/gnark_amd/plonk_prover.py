@@ -234,12 +234,12 @@ class ProvingKey:
         check(lib.gg_plonk_pk_devices(self.handle, arr, k.value, ctypes.byref(k)))
         return list(arr)
 
-    def set_rehearsal(self, on: bool = True):
-        """Timing rehearsal (gg_plonk_pk_set_rehearsal): the peer parts of a
-        multi-part key do nothing in later proves (the primary part's work on
-        one GPU); those proofs are NOT valid and prove() refuses them unless
-        called with rehearsal_ok=True."""
-        check(lib.gg_plonk_pk_set_rehearsal(self.handle, int(bool(on))))
+    def set_rehearsal(self, on: bool = True, part: int = 0):
+        """Timing rehearsal (gg_plonk_pk_set_rehearsal_part): only device part
+        `part` (0 = primary) of a multi-part key does its work in later proves
+        (one part's work timed on one GPU); those proofs are NOT valid and
+        prove() refuses them unless called with rehearsal_ok=True."""
+        check(lib.gg_plonk_pk_set_rehearsal_part(self.handle, int(part) if on else -1))
 
     def part_timings(self) -> list:
         """Per device part (0 = primary), the last proof: MSM slices and their ms,

@@ -621,6 +621,11 @@ int gg_plonk_pk_devices(gg_plonk_pk_t pk, int *devices, int cap, int *n_devices)
  * GPU times the primary part's work; such proves write an INVALID proof and
  * return GG_REHEARSAL.  0 (the default) restores real proofs. */
 int gg_plonk_pk_set_rehearsal(gg_plonk_pk_t pk, int on);
+/* The same for any one device part: part p >= 0 alone does its work (its MSM
+ * slices, ratio slice, quotient units, canonical-form tasks; part 0 also the
+ * tail stages and the openings), the others skip theirs; -1 ends rehearsals.
+ * gg_plonk_pk_set_rehearsal(pk, on) = part 0 / -1. */
+int gg_plonk_pk_set_rehearsal_part(gg_plonk_pk_t pk, int part);
 /* where device part `part` (0 = primary) spent the last proof (cap >=
  * GG_PLONK_PART_SLOTS): [0] MSM slices, [1] their ms (incl. the scalar copy),
  * [2] ms copying scalar slices from the primary (xGMI), [3] MB copied, [4]

@@ -334,6 +334,15 @@ def test_plonk_rehearsal_mode():
     assert solo != ref
     assert all(p["msm_slices"] == 0 and p["quotient_units"] == 0 and p["canon_tasks"] == 0
                for p in pkm.part_timings()[1:])
+    # a peer alone: its MSM slices, unit and canonical-form tasks (R, then Z), nothing of the others
+    pkm.set_rehearsal(True, part=2)
+    assert pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts, rehearsal_ok=True) != ref
+    pt = pkm.part_timings()
+    assert [p["msm_slices"] for p in pt] == [0, 0, 10, 0]
+    assert [p["quotient_units"] for p in pt] == [0, 0, 1, 0]
+    assert [p["canon_tasks"] for p in pt] == [0, 0, 2, 0]
+    with pytest.raises(GnarkAmdError):
+        pkm.set_rehearsal(True, part=parts)
     pkm.set_rehearsal(False)
     assert pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts) == ref
     pkm.close()

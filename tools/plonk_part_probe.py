@@ -1,7 +1,7 @@
 """Where the primary part of an N-part PlonK key spends a proof (configs[4]:
 BLS12-381, 2^22, 8 x MI355X), on one GPU: the key is split over N device parts
-that all live on device 0; the proof runs in rehearsal mode (peers idle) so a
-kernel trace (rocprofv3 --kernel-trace) shows only the primary part's work.
+that all live on device 0; each part is then rehearsed alone (the others skip
+their work), so a kernel trace (rocprofv3 --kernel-trace) shows one part's work.
 usage: plonk_part_probe.py [log_n] [parts] [reps]"""
 import os
 import sys
@@ -40,12 +40,18 @@ def main():
     if parts > 1:
         pp.prove(pk, L, R_, O, rng=random.Random(1))
         print(json.dumps({"parts_real_proof": pk.part_timings()}), flush=True)
-        pk.set_rehearsal(True)
-    for _ in range(reps):
-        tim = {}
-        t = time.perf_counter()
-        pp.prove(pk, L, R_, O, rng=random.Random(1), timings=tim, rehearsal_ok=True)
-        print(json.dumps({"ms": 1e3 * (time.perf_counter() - t), "stage_ms": tim}), flush=True)
+    # rehearse part 0 and the peers listed in PROBE_PARTS (default: every part)
+    which = [int(x) for x in os.environ.get("PROBE_PARTS", ",".join(map(str, range(parts)))).split(",") if x]
+    for part in which:
+        if parts > 1:
+            pk.set_rehearsal(True, part=part)
+        for _ in range(reps):
+            tim = {}
+            t = time.perf_counter()
+            pp.prove(pk, L, R_, O, rng=random.Random(1), timings=tim, rehearsal_ok=True)
+            print(json.dumps({"part": part, "ms": 1e3 * (time.perf_counter() - t), "stage_ms": tim}), flush=True)
+        if parts == 1:
+            break
     pk.close()
 
 
