@@ -509,8 +509,10 @@ static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStr
     if (!pk->ptimes.empty()) {
         std::lock_guard<std::mutex> lk(pk->tmu);
         PlonkPartTimes& T = pk->ptimes[0];
-        T.msm_count += 1;
-        T.msm_ms += own;
+        if (part_runs(pk, 0)) {
+            T.msm_count += 1;
+            T.msm_ms += own;
+        }
         T.wait_ms += waited;
     }
     return j;
