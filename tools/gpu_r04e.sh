@@ -17,10 +17,11 @@ step() {  # step <secs> <log> cmd...
 S="${STEPS:-test,probe,plonk1}"
 if [[ "$S" == *test* ]]; then
   step 600 pytest_$V.txt python3 -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
-    tests/test_gpu_plonk_prove.py || exit 2
+    tests/test_gpu_plonk_prove.py tests/test_gpu_scs_solver.py tests/test_gpu_solver.py || exit 2
 fi
 if [[ "$S" == *probe* ]]; then
   step 300 probe_$V.txt python3 -u tools/plonk_part_probe.py 22 8 3 || exit 2
+  step 300 smoke_$V.txt python3 -u -c "import __graft_entry__ as g; g.smoke()" || exit 2
 fi
 if [[ "$S" == *plonk1* ]]; then
   step 300 plonk1_prof_$V.txt rocprofv3 --kernel-trace --stats -d gpurun_out/plonk1_prof_$V -o run -- \
