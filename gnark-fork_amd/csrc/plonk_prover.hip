@@ -626,6 +626,16 @@ static void canon_wait_regular(Key* pk) {
     }
 }
 
+// part 0's share of the KZG slices relative to a peer's (1): part 0 also runs
+// the quotient's tail stages and the openings, so it takes fewer points
+static double plonk_part0_weight(int n_devices) {
+    if (const char* e = getenv("GG_PLONK_PART0_WEIGHT")) {  // tuning / A/B
+        const double w = atof(e);
+        if (w > 0.05 && w <= 4.0) return w;
+    }
+    return n_devices > 1 ? 1.0 : 1.0;
+}
+
 static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, const void* omega_big,
                            const void* coset_shift, const void* kzg_g1, size_t n_kzg,
                            const void* kzg_lagrange_g1, const void* const* trace, const void* const* qcp,
@@ -717,15 +727,24 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
             lo = m * (size_t)pk->rank / (size_t)pk->world;
             hi = m * (size_t)(pk->rank + 1) / (size_t)pk->world;
         };
+        // device parts: slice boundaries by weight, part 0 w0 (it also runs the
+        // tail stages and the openings), each peer 1 (GG_PLONK_PART0_WEIGHT overrides)
+        double w0 = plonk_part0_weight(n_devices);
+        auto bound = [&](size_t m, int d) -> size_t {
+            if (d <= 0) return 0;
+            if (d >= n_devices) return m;
+            const long double cum = (long double)w0 + (d - 1), tot = (long double)w0 + (n_devices - 1);
+            return (size_t)((long double)m * cum / tot);
+        };
         if (n_devices > 1) {  // part 0 here, parts 1.. on the peers
             for (int d = 1; d < n_devices; d++) {
                 pk->peers.emplace_back(new PlonkPeer());
                 PlonkPeer* p = pk->peers.back().get();
                 p->device = devices[d];
-                p->k_lo = (n + 3) * d / n_devices;
-                p->k_hi = (n + 3) * (d + 1) / n_devices;
-                p->l_lo = n * d / n_devices;
-                p->l_hi = n * (d + 1) / n_devices;
+                p->k_lo = bound(n + 3, d);
+                p->k_hi = bound(n + 3, d + 1);
+                p->l_lo = bound(n, d);
+                p->l_hi = bound(n, d + 1);
                 GG_HIP(hipSetDevice(p->device));
                 for (hipStream_t& x : p->s) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
                 for (int e = 0; e < 4; e++) {
@@ -743,9 +762,9 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
             }
             GG_HIP(hipSetDevice(pk->device));
             pk->k_lo = 0;
-            pk->k_hi = (n + 3) / n_devices;
+            pk->k_hi = bound(n + 3, 1);
             pk->l_lo = 0;
-            pk->l_hi = n / n_devices;
+            pk->l_hi = bound(n, 1);
         } else {
             range(n + 3, pk->k_lo, pk->k_hi);
             range(n, pk->l_lo, pk->l_hi);
