@@ -627,13 +627,19 @@ static void canon_wait_regular(Key* pk) {
 }
 
 // part 0's share of the KZG slices relative to a peer's (1): part 0 also runs
-// the quotient's tail stages and the openings, so it takes fewer points
+// the quotient's tail stages and the openings.  Measured with equal slices
+// (2^22, 8 parts, each part rehearsed alone, profiles/r04_e_plonk_part_probe.txt):
+// part 0 23.8 ms, peers 21.6-22.7 ms, i.e. part 0 carries ~1.4 % of the
+// one-GPU MSM work extra; its share of the points is cut by that much
+// (N = 8: weight 0.87, N = 2: 0.94).
 static double plonk_part0_weight(int n_devices) {
     if (const char* e = getenv("GG_PLONK_PART0_WEIGHT")) {  // tuning / A/B
         const double w = atof(e);
         if (w > 0.05 && w <= 4.0) return w;
     }
-    return n_devices > 1 ? 1.0 : 1.0;
+    if (n_devices <= 1) return 1.0;
+    const double f = 1.0 / n_devices - 0.014;  // part 0's share of the points
+    return std::max(0.5, std::min(1.0, (n_devices - 1) * f / (1.0 - f)));
 }
 
 static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, const void* omega_big,
