@@ -302,6 +302,27 @@ def test_plonk_prove_2p22_verifies():
     pk8.close()
 
 
+@pytest.mark.parametrize("weight", ["0.5", "1.7"])
+def test_plonk_multi_device_part0_weight(weight, monkeypatch):
+    """Part 0's share of the KZG slices is a weight (plonk_part0_weight;
+    GG_PLONK_PART0_WEIGHT): uneven slice boundaries on both bases, the ratio
+    slices and Z's slices follow them -- the proof is still the one-GPU one."""
+    from gnark_amd import plonk_prover as pp
+    log_n, parts = 9, 5
+    circ = Circuit(log_n, 40, nb_public=1, n_cmt=1)
+    tau = random.Random(5).randrange(2, R)
+    key_srs = srs(log_n, tau)
+    pk0 = make_key(circ, tau, key_srs=key_srs)
+    L, Rv, O, pub, cmts = circ.solve(pk0, 6, commit=pk0.commit_lagrange)
+    ref = pp.prove(pk0, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts)
+    monkeypatch.setenv("GG_PLONK_PART0_WEIGHT", weight)
+    pkm = make_key(circ, tau, key_srs=key_srs, devices=[0] * parts)
+    monkeypatch.delenv("GG_PLONK_PART0_WEIGHT")
+    assert pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts) == ref
+    pkm.close()
+    pk0.close()
+
+
 def test_plonk_rehearsal_mode():
     """gg_plonk_pk_set_rehearsal (bench.py's split_projection): the primary part
     of a multi-part key proves with its peers idle -- the library returns
