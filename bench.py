@@ -874,8 +874,8 @@ def pmc_traffic(kernel, workload, gather_bytes=None, table_bytes=0):
         except (OSError, ValueError):
             continue
         wl = d.get("workload", {})
-        if any(wl.get(k) != v for k, v in workload.items()):
-            continue
+        if d.get("probe") or any(wl.get(k) != v for k, v in workload.items()):
+            continue  # probe builds (GG_ACCUM_PROBE) measure what is NOT point bytes, never the kernel
         if not _same_tree(d):
             stale = stale or os.path.basename(f)
             continue
