@@ -626,20 +626,24 @@ static void canon_wait_regular(Key* pk) {
     }
 }
 
-// part 0's share of the KZG slices relative to a peer's (1): part 0 also runs
-// the quotient's tail stages and the openings.  Measured with equal slices
-// (2^22, 8 parts, each part rehearsed alone, profiles/r04_e_plonk_part_probe.txt):
-// part 0 23.8 ms, peers 21.6-22.7 ms, i.e. part 0 carries ~1.4 % of the
-// one-GPU MSM work extra; its share of the points is cut by that much
-// (N = 8: weight 0.87, N = 2: 0.94).
-static double plonk_part0_weight(int n_devices) {
+// part 0's share of the KZG slices relative to a peer's (1).  Beside its MSM
+// slices part 0 runs the quotient's tail stages and the openings (e0 ~ 2 % of
+// the one-GPU MSM work at 2^22), a peer its canonical-form tasks (~0.75 % each,
+// ceil(T / (N - 1)) of the T = 5 + n_cmt tasks on the busiest peer).  Part 0's
+// share f0 balances f0 + e0 = (1 - f0) / (N - 1) + ep, i.e.
+// f0 = (1 + (N - 1)(ep - e0)) / N, as a weight (N - 1) f0 / (1 - f0).
+// Measured with equal slices (2^22, each part rehearsed alone,
+// profiles/r04_e_plonk_part_probe.txt): N = 8 part 0 23.8 ms, peers 21.6-22.7.
+static double plonk_part0_weight(int n_devices, int n_cmt) {
     if (const char* e = getenv("GG_PLONK_PART0_WEIGHT")) {  // tuning / A/B
         const double w = atof(e);
         if (w > 0.05 && w <= 4.0) return w;
     }
     if (n_devices <= 1) return 1.0;
-    const double f = 1.0 / n_devices - 0.014;  // part 0's share of the points
-    return std::max(0.5, std::min(1.0, (n_devices - 1) * f / (1.0 - f)));
+    const int T = 5 + n_cmt, busiest = (T + n_devices - 2) / (n_devices - 1);
+    const double e0 = 0.020, ep = 0.0075 * busiest;
+    const double f0 = (1.0 + (n_devices - 1) * (ep - e0)) / n_devices;
+    return std::max(0.5, std::min(2.0, (n_devices - 1) * f0 / (1.0 - f0)));
 }
 
 static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, const void* omega_big,
@@ -735,7 +739,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
         };
         // device parts: slice boundaries by weight, part 0 w0 (it also runs the
         // tail stages and the openings), each peer 1 (GG_PLONK_PART0_WEIGHT overrides)
-        double w0 = plonk_part0_weight(n_devices);
+        const double w0 = plonk_part0_weight(n_devices, n_cmt);
         auto bound = [&](size_t m, int d) -> size_t {
             if (d <= 0) return 0;
             if (d >= n_devices) return m;
