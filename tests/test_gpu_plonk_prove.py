@@ -232,7 +232,7 @@ def test_plonk_prove_multi_device_matches(log_n, parts, n_cmt):
     pk0.close()
 
 
-@pytest.mark.parametrize("log_n,nb_public,n_cmt,parts", [(12, 2, 1, 1), (14, 1, 0, 4)])
+@pytest.mark.parametrize("log_n,nb_public,n_cmt,parts", [(12, 2, 1, 1), (14, 1, 0, 4), (12, 1, 1, 8)])
 def test_plonk_bn254_prove_verifies(log_n, nb_public, n_cmt, parts):
     """backend/plonk/bn254 at sizes the Python oracle verifies in seconds: the GPU
     proof passes the verifier restatement (verify.go:45-290 over BN254), from a
