@@ -1183,19 +1183,20 @@ def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, 
             # one real N-part proof first: every part's MSM slices / cosets and copies
             pp.prove(pkm, L, R_, O, rng=rng())
             parts = pkm.part_timings()
-            per_part, stg0 = [], {}
-            for part in range(nd):
-                pkm.set_rehearsal(True, part=part)
-                pp.prove(pkm, L, R_, O, rng=rng(), rehearsal_ok=True)
-                tp = []
-                for _ in range(max(reps, 3)):
+            # rounds over the parts (part 0, 1, ..., N-1, then again) so a drift of
+            # the box's clocks during the sweep lands on every part alike
+            tps, stg0 = [[] for _ in range(nd)], {}
+            for rnd in range(1 + max(reps, 5)):
+                for part in range(nd):
+                    pkm.set_rehearsal(True, part=part)
                     t = time.perf_counter()
                     stg = {}
                     pp.prove(pkm, L, R_, O, timings=stg, rng=rng(), rehearsal_ok=True)
-                    tp.append(1e3 * (time.perf_counter() - t))
-                    if part == 0:
-                        stg0 = stg
-                per_part.append(sorted(tp)[len(tp) // 2])
+                    if rnd:  # round 0 warms every part's path
+                        tps[part].append(1e3 * (time.perf_counter() - t))
+                        if part == 0:
+                            stg0 = stg
+            per_part = [sorted(tp)[len(tp) // 2] for tp in tps]
             pkm.set_rehearsal(False)
             worst = max(per_part)
             proj[str(nd)] = {"part_ms_median": [round(x, 2) for x in per_part], "slowest_part": per_part.index(worst),
