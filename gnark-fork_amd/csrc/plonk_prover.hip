@@ -626,24 +626,36 @@ static void canon_wait_regular(Key* pk) {
     }
 }
 
-// part 0's share of the KZG slices relative to a peer's (1).  Beside its MSM
-// slices part 0 runs the quotient's tail stages and the openings (e0 ~ 2 % of
-// the one-GPU MSM work at 2^22), a peer its canonical-form tasks (~0.75 % each,
-// ceil(T / (N - 1)) of the T = 5 + n_cmt tasks on the busiest peer).  Part 0's
-// share f0 balances f0 + e0 = (1 - f0) / (N - 1) + ep, i.e.
-// f0 = (1 + (N - 1)(ep - e0)) / N, as a weight (N - 1) f0 / (1 - f0).
-// Measured with equal slices (2^22, each part rehearsed alone,
-// profiles/r04_e_plonk_part_probe.txt): N = 8 part 0 23.8 ms, peers 21.6-22.7.
-static double plonk_part0_weight(int n_devices, int n_cmt) {
-    if (const char* e = getenv("GG_PLONK_PART0_WEIGHT")) {  // tuning / A/B
-        const double w = atof(e);
-        if (w > 0.05 && w <= 4.0) return w;
+// Each device part's share of the KZG slices (both bases, the ratio, Z's
+// slices).  Beside its MSM slices part 0 runs the quotient's tail stages and
+// the openings, a peer its canonical-form tasks (canon_tasks; Z's transform and
+// pushes sit between the ratio and the quotient units).  With E_p that extra
+// work as a fraction of the one-GPU MSM work, the shares f_p = (1 + sum E) / N
+// - E_p equalise f_p + E_p.  E from the parts rehearsed alone at 2^22 x 8
+// (profiles/r04_l_bench_driver_command.json: parts without tasks 23.1 ms, with
+// L / R / O / Qk +0.0-0.7, Z's owner +0.9, part 0 +2.3 at equal-MSM terms;
+// MSM work ~120 ms): part 0 0.019, a task 0.0033, Z's 0.0075.
+// GG_PLONK_PART0_WEIGHT=w instead: part 0 weight w, every peer 1.
+static std::vector<double> plonk_part_shares(int n_devices, int n_cmt) {
+    std::vector<double> f(std::max(1, n_devices), 1.0);
+    if (n_devices > 1) {
+        if (const char* e = getenv("GG_PLONK_PART0_WEIGHT")) {  // tuning / A/B
+            const double w = atof(e);
+            if (w > 0.05 && w <= 4.0) f[0] = w;
+        } else {
+            std::vector<double> E(n_devices, 0.0);
+            E[0] = 0.019;
+            const int T = 5 + n_cmt;  // canon_tasks order: L R O Qk Pi_j..., Z last
+            for (int i = 0; i < T; i++) E[1 + i % (n_devices - 1)] += (i == T - 1) ? 0.0075 : 0.0033;
+            double sum = 0;
+            for (double x : E) sum += x;
+            for (int p = 0; p < n_devices; p++) f[p] = std::max(0.3 / n_devices, (1.0 + sum) / n_devices - E[p]);
+        }
     }
-    if (n_devices <= 1) return 1.0;
-    const int T = 5 + n_cmt, busiest = (T + n_devices - 2) / (n_devices - 1);
-    const double e0 = 0.020, ep = 0.0075 * busiest;
-    const double f0 = (1.0 + (n_devices - 1) * (ep - e0)) / n_devices;
-    return std::max(0.5, std::min(2.0, (n_devices - 1) * f0 / (1.0 - f0)));
+    double tot = 0;
+    for (double x : f) tot += x;
+    for (double& x : f) x /= tot;
+    return f;
 }
 
 static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, const void* omega_big,
@@ -737,14 +749,14 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
             lo = m * (size_t)pk->rank / (size_t)pk->world;
             hi = m * (size_t)(pk->rank + 1) / (size_t)pk->world;
         };
-        // device parts: slice boundaries by weight, part 0 w0 (it also runs the
-        // tail stages and the openings), each peer 1 (GG_PLONK_PART0_WEIGHT overrides)
-        const double w0 = plonk_part0_weight(n_devices, n_cmt);
+        // device parts: slice boundaries by share (plonk_part_shares)
+        const std::vector<double> share = plonk_part_shares(n_devices, n_cmt);
         auto bound = [&](size_t m, int d) -> size_t {
             if (d <= 0) return 0;
             if (d >= n_devices) return m;
-            const long double cum = (long double)w0 + (d - 1), tot = (long double)w0 + (n_devices - 1);
-            return (size_t)((long double)m * cum / tot);
+            long double cum = 0;
+            for (int q = 0; q < d; q++) cum += share[q];
+            return std::min(m, (size_t)((long double)m * cum));
         };
         if (n_devices > 1) {  // part 0 here, parts 1.. on the peers
             for (int d = 1; d < n_devices; d++) {
