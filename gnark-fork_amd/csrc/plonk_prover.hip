@@ -379,6 +379,7 @@ struct Key : gg_plonk_pk {
     int n_cmt = 0;
     hipStream_t s[4] = {nullptr, nullptr, nullptr, nullptr};
     MsmWork* work[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t msm_ready[3] = {nullptr, nullptr, nullptr};  // per work slot: its scalars are complete
     Arena ar[4];
     // per-proof buffers
     DevBuf lag[3], can[4], cbrev[4], zlag, pz, qkc, pi_reg[plk::MAX_CMT], pi_brev[plk::MAX_CMT];
@@ -392,6 +393,8 @@ struct Key : gg_plonk_pk {
     ~Key() override {
         peers.clear();
         for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+        for (hipEvent_t e : msm_ready)
+            if (e) (void)hipEventDestroy(e);
         for (auto w : work)
             if (w) msm_work_delete(w);
         if (kzg) gg_msm_base_release(kzg);
@@ -493,12 +496,17 @@ static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStr
     const size_t lo = kz ? pk->k_lo : pk->l_lo;
     std::vector<std::future<BJac>> fs;
     if (peers_active(pk)) {
-        GG_HIP(hipStreamSynchronize(st));  // the scalars are complete before the peers copy them
+        // the peers' threads start at once; each waits for the scalars (complete
+        // at this point of st) before its copy -- not for a resident slice
+        hipEvent_t ready = pk->msm_ready[wi];
+        GG_HIP(hipEventRecord(ready, st));
         for (size_t q = 0; q < pk->peers.size(); q++)
             if (part_runs(pk, (int)q + 1))
-                fs.push_back(std::async(std::launch::async, [pk, q, pp = pk->peers[q].get(), kz, wi, scal, peer_resident] {
-                return peer_msm(pk, (int)q + 1, pp, kz, wi, scal, peer_resident);
-            }));
+                fs.push_back(std::async(std::launch::async, [pk, q, pp = pk->peers[q].get(), kz, wi, scal, peer_resident,
+                                                             ready] {
+                    if (!peer_resident) GG_HIP(hipEventSynchronize(ready));
+                    return peer_msm(pk, (int)q + 1, pp, kz, wi, scal, peer_resident);
+                }));
     }
     const auto a = std::chrono::steady_clock::now();
     if (part_runs(pk, 0)) msm_device_work(base, pk->work[wi], (const Fr*)(scal + lo), &j, st);
@@ -742,6 +750,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
     pk->split_idft = log_big >= 12;
     for (hipStream_t& x : pk->s) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
     for (auto& w : pk->work) w = msm_work_new();
+    for (hipEvent_t& e : pk->msm_ready) GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     hipStream_t st = pk->s[0];
     // KZG bases (resident, fixed-base precomputation): pk.Kzg.G1[:n+3], pk.KzgLagrange.G1
     {
