@@ -25,6 +25,7 @@
 #include "plonk_ops.h"
 #include "curve.cuh"
 #include "sha256.h"
+#include <atomic>
 #include <functional>
 #include <future>
 #include <memory>
@@ -1152,47 +1153,63 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
             plk::ratio_range(F(pk->lag[0]) + zlo, F(pk->lag[1]) + zlo, F(pk->lag[2]) + zlo, pm + zlo, pm + n + zlo,
                              pm + 2 * n + zlo, zlo, zcnt, n, beta, gamma, pk->omega, pk->u, F(pk->pz), s[0], pk->ar[0]);
         std::vector<FrB> agg(1 + pk->peers.size(), FrB::one());
+        std::vector<FrB> pre(agg.size(), FrB::one());
+        // one thread per peer: factors + scan of its slice, hand its slice product
+        // over, wait for the chained prefixes, fix its slice of Z up and push it
+        // to Z's owner (a failing peer releases the others through `stop`)
+        std::vector<std::promise<void>> agg_done(pk->peers.size());
+        std::promise<void> pre_ready;
+        std::shared_future<void> pre_f = pre_ready.get_future().share();
+        std::atomic<bool> stop{false};
         std::vector<std::future<void>> pf;
         if (peers_on)
             for (size_t q = 0; q < pk->peers.size(); q++)
                 pf.push_back(std::async(std::launch::async, [&, q] {
                     PlonkPeer* p = pk->peers[q].get();
                     const size_t cnt = p->l_hi - p->l_lo;
-                    if (!cnt || !part_runs(pk, (int)q + 1)) return;
-                    GG_HIP(hipSetDevice(p->device));
-                    const auto a = std::chrono::steady_clock::now();
-                    p->ar.reset();
-                    const int64_t* ps = p->perm_slice.as<int64_t>();
-                    plk::ratio_range(F(p->scal[0]), F(p->scal[1]), F(p->scal[2]), ps, ps + cnt, ps + 2 * cnt, p->l_lo,
-                                     cnt, n, beta, gamma, pk->omega, pk->u, F(p->pz), p->s[0], p->ar);
-                    agg[q + 1] = fetch(F(p->pz) + cnt - 1, p->s[0]);
-                    std::lock_guard<std::mutex> lk(pk->tmu);
-                    pk->ptimes[q + 1].ratio_ms += ms_since(a);
-                }));
-        agg[0] = zcnt && run0 ? fetch(F(pk->pz) + zcnt - 1, s[0]) : FrB::one();
-        for (auto& f : pf) f.get();
-        // prefix of part r = the product of the factors of the slices before it
-        std::vector<FrB> pre(agg.size(), FrB::one());
-        for (size_t r = 1; r < agg.size(); r++) pre[r] = pre[r - 1] * agg[r - 1];
-        if (run0) plk::ratio_fixup(F(pk->pz), zcnt, pre[0], F(pk->zlag) + zlo, s[0]);
-        if (zown && zcnt && run0)
-            GG_HIP(hipMemcpyPeerAsync(F(zown->in[3]) + zlo, zown->device, F(pk->zlag) + zlo, pk->device, 32 * zcnt, s[0]));
-        pf.clear();
-        if (peers_on)
-            for (size_t q = 0; q < pk->peers.size(); q++)
-                pf.push_back(std::async(std::launch::async, [&, q] {
-                    PlonkPeer* p = pk->peers[q].get();
-                    const size_t cnt = p->l_hi - p->l_lo;
-                    if (!cnt || !part_runs(pk, (int)q + 1)) return;
-                    GG_HIP(hipSetDevice(p->device));
-                    const auto a = std::chrono::steady_clock::now();
+                    const bool mine = cnt && part_runs(pk, (int)q + 1);
+                    double ms = 0;
+                    try {
+                        if (mine) {
+                            GG_HIP(hipSetDevice(p->device));
+                            const auto a = std::chrono::steady_clock::now();
+                            p->ar.reset();
+                            const int64_t* ps = p->perm_slice.as<int64_t>();
+                            plk::ratio_range(F(p->scal[0]), F(p->scal[1]), F(p->scal[2]), ps, ps + cnt, ps + 2 * cnt,
+                                             p->l_lo, cnt, n, beta, gamma, pk->omega, pk->u, F(p->pz), p->s[0], p->ar);
+                            agg[q + 1] = fetch(F(p->pz) + cnt - 1, p->s[0]);
+                            ms += ms_since(a);
+                        }
+                        agg_done[q].set_value();
+                    } catch (...) {
+                        agg_done[q].set_exception(std::current_exception());
+                        return;
+                    }
+                    pre_f.wait();
+                    if (!mine || stop) return;
+                    const auto b = std::chrono::steady_clock::now();
                     plk::ratio_fixup(F(p->pz), cnt, pre[q + 1], F(p->scal[0]), p->s[0]);  // the Z slot of its MSM
                     GG_HIP(hipMemcpyPeerAsync(F(zown->in[3]) + p->l_lo, zown->device, p->scal[0].p, p->device, 32 * cnt,
                                               p->s[0]));
                     GG_HIP(hipStreamSynchronize(p->s[0]));
                     std::lock_guard<std::mutex> lk(pk->tmu);
-                    pk->ptimes[q + 1].ratio_ms += ms_since(a);
+                    pk->ptimes[q + 1].ratio_ms += ms + ms_since(b);
                 }));
+        try {
+            agg[0] = zcnt && run0 ? fetch(F(pk->pz) + zcnt - 1, s[0]) : FrB::one();
+            for (size_t q = 0; q < pf.size(); q++) agg_done[q].get_future().get();
+        } catch (...) {
+            stop = true;
+            pre_ready.set_value();
+            for (auto& f : pf) f.wait();
+            throw;
+        }
+        // prefix of part r = the product of the factors of the slices before it
+        for (size_t r = 1; r < agg.size(); r++) pre[r] = pre[r - 1] * agg[r - 1];
+        pre_ready.set_value();
+        if (run0) plk::ratio_fixup(F(pk->pz), zcnt, pre[0], F(pk->zlag) + zlo, s[0]);
+        if (zown && zcnt && run0)
+            GG_HIP(hipMemcpyPeerAsync(F(zown->in[3]) + zlo, zown->device, F(pk->zlag) + zlo, pk->device, 32 * zcnt, s[0]));
         for (auto& f : pf) f.get();
         std::lock_guard<std::mutex> lk(pk->tmu);
         pk->ptimes[0].ratio_ms += ms_since(ta);
