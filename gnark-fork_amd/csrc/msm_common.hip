@@ -436,8 +436,25 @@ __global__ void __launch_bounds__(256) k_seg_hist(const KT* keys, const uint4* d
     const uint32_t R = 1u << rbits;
     if (threadIdx.x < R) hist[threadIdx.x] = 0;
     __syncthreads();
+#ifdef GG_SEG_HIST_V
+    // the chunk's aligned middle in 4-key vectors, the unaligned ends one key a lane
+    const uint32_t a0 = min(hi, (lo + 3u) & ~3u), a1 = max(a0, hi & ~3u);
+    for (uint32_t e = lo + threadIdx.x; e < a0; e += blockDim.x)
+        atomicAdd(&hist[(keys[e] >> shift) & (R - 1)], 1u);
+    for (uint32_t e = a1 + threadIdx.x; e < hi; e += blockDim.x)
+        atomicAdd(&hist[(keys[e] >> shift) & (R - 1)], 1u);
+    struct alignas(4 * sizeof(KT)) K4 { KT k[4]; };
+    const K4* kv = reinterpret_cast<const K4*>(keys + a0);
+    const uint32_t nv = (a1 - a0) >> 2;
+    for (uint32_t q = threadIdx.x; q < nv; q += blockDim.x) {
+        const K4 x = kv[q];
+#pragma unroll
+        for (int u = 0; u < 4; u++) atomicAdd(&hist[(x.k[u] >> shift) & (R - 1)], 1u);
+    }
+#else
     for (uint32_t e = lo + threadIdx.x; e < hi; e += blockDim.x)
         atomicAdd(&hist[(keys[e] >> shift) & (R - 1)], 1u);
+#endif
     __syncthreads();
     if (threadIdx.x < R) ch[(size_t)g0 * R + (size_t)threadIdx.x * nch + k] = hist[threadIdx.x];
 }
