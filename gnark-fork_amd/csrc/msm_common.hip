@@ -262,7 +262,7 @@ __device__ __forceinline__ void scalar_keys(const Fe<SC>& scl, int c, int W, con
 template <class SC>
 __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, const uint32_t* sidx,
                                                      size_t n, int c, int W, WinSpec ws, int G, int kbits,
-                                                     int spb, int nbins, int h, uint32_t* keys,
+                                                     int spb, int nbins, int h, uint32_t* keys, size_t kst,
                                                      uint32_t* hist, uint32_t nblocks, int slog, uint32_t sres) {
     extern __shared__ uint32_t hh[];
     for (int j = threadIdx.x; j < nbins; j += blockDim.x) hh[j] = 0;
@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, cons
         const size_t i = idx[s];
         scalar_keys<SC>(scl[s], c, W, ws, G, slog, sres, [&](int w, uint32_t key) {
             if (key != 0xffffffffu) atomicAdd(&hh[bin_of(key & 0x7fffffffu, c, kbits, h)], 1u);
-            keys[(size_t)w * n + i] = key;
+            keys[(size_t)w * kst + i] = key;
         });
     }
     __syncthreads();
@@ -297,7 +297,7 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, cons
 // Phase C, LDS-staged: the block's entries are first partitioned by bin in LDS
 // (ranks from LDS atomics, bin bases from this block's own histogram), then
 // written out as contiguous per-bin runs -> coalesced stores.
-__global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_t n, int W, int c, int G,
+__global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_t kst, size_t n, int W, int c, int G,
                                                      int kbits, int spb, int nbins, int h, const uint32_t* hist,
                                                      const uint32_t* hoff, uint32_t nblocks,
                                                      uint32_t* tmp_entry, void* tmp_key, int key16) {
@@ -337,7 +337,7 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_
             kk[u] = 0xffffffffu;
             if (j < tot_e) {
                 int w = j / ns, t = j - w * ns;
-                kk[u] = keys[(size_t)w * n + i0 + t];
+                kk[u] = keys[(size_t)w * kst + i0 + t];
                 ee[u] = (uint32_t)((size_t)(w / G) * n + i0 + t);  // the stored copy of window w
             }
         }
@@ -575,7 +575,11 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
             ns <<= r;
         }
     }
-    s->keys.reserve(total * 4);
+    // key rows of phase A: stride n, or (GG_SORT_KEYPAD=1) n rounded up to 64 keys so
+    // every row starts on a 256-B boundary
+    static const bool keypad = [] { const char* e = getenv("GG_SORT_KEYPAD"); return e && atoi(e) == 1; }();
+    const size_t kst = keypad ? (n + 63) & ~(size_t)63 : n;
+    s->keys.reserve(std::max(total, (size_t)W * kst) * 4);
     s->tmp_entry.reserve(total * 4);
     s->tmp_key.reserve(total * 4);
     s->sorted.reserve(total * 4 + 64);  // + 64: the accumulation reads 16-B chunks past its last entry
@@ -594,12 +598,12 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     if (b->scurve)
         hipLaunchKernelGGL(k_digits_hist<FrBlsCfg>, dim3(nblocks), dim3(256), nbins * 4, st,
                            (const FrBls*)scalars_dev, b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n,
-                           c, W, b->win, G, kbits, spb, nbins, h, s->keys.as<uint32_t>(),
+                           c, W, b->win, G, kbits, spb, nbins, h, s->keys.as<uint32_t>(), kst,
                            s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
     else
         hipLaunchKernelGGL(k_digits_hist<FrCfg>, dim3(nblocks), dim3(256), nbins * 4, st, scalars_dev,
                            b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, G, kbits, spb,
-                           nbins, h, s->keys.as<uint32_t>(), s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
+                           nbins, h, s->keys.as<uint32_t>(), kst, s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
     GG_HIP(hipGetLastError());
     exclusive_scan(s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nh, st, s->scan_tmp);
     // segment starts ping-pong between bin_start and seg2; the last pass writes offsets
@@ -617,7 +621,7 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     auto ent_out = [&](int j) { return ((S - 1 - j) % 2 == 0) ? &s->sorted : &s->tmp_entry; };
     auto key_out = [&](int j) { return (j % 2 == 0) ? &s->tmp_key : &s->keys; };
     const bool key16 = kbits - h <= 16;
-    hipLaunchKernelGGL(k_bin_scatter, dim3(nblocks), dim3(256), lds_c, st, s->keys.as<uint32_t>(),
+    hipLaunchKernelGGL(k_bin_scatter, dim3(nblocks), dim3(256), lds_c, st, s->keys.as<uint32_t>(), kst,
                        n, W, c, G, kbits, spb, nbins, h, s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nblocks,
                        ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->p : nullptr, (int)key16);
     GG_HIP(hipGetLastError());

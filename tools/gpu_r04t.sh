@@ -2,7 +2,8 @@
 # Round 4 t: sort-pass A/B through GNARK_AMD_LIB variants built from the same
 # tree (build_var/): segmented-pass chunk size GG_SEG_CH 2048 / 8192 against the
 # default 4096, and the 4-key-vector chunk histogram (GG_SEG_HIST_V).  Each
-# variant: the MSM parity tests, then a kernel trace of the 2^24 prove.
+# variant (kp: the default library with GG_SORT_KEYPAD=1, key rows on 256-B
+# boundaries): the MSM parity tests, then a kernel trace of the 2^24 prove.
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -16,8 +17,9 @@ step() {  # step <secs> <log> cmd...
   echo "=== rc=$rc $(date +%T)" >> gpurun_out/progress_$V.txt
   return $rc
 }
-for var in base ch2048 ch8192 hv hv8192 base2; do
-  case $var in base|base2) lib=gnark-fork_amd/lib/libgnark_amd.so ;; *) lib=build_var/libgnark_amd_$var.so ;; esac
+for var in base ch2048 ch8192 hv hv8192 kp base2; do
+  unset GG_SORT_KEYPAD; [ $var = kp ] && export GG_SORT_KEYPAD=1
+  case $var in base|base2|kp) lib=gnark-fork_amd/lib/libgnark_amd.so ;; *) lib=build_var/libgnark_amd_$var.so ;; esac
   export GNARK_AMD_LIB=$PWD/$lib
   if [ "$var" != base2 ]; then
     step 400 pytest_${var}_$V.txt python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_msm.py tests/test_gpu_msm_stripe.py || exit 2
