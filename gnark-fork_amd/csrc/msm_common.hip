@@ -263,8 +263,12 @@ template <class SC>
 __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, const uint32_t* sidx,
                                                      size_t n, int c, int W, WinSpec ws, int G, int kbits,
                                                      int spb, int nbins, int h, uint32_t* keys, size_t kst,
-                                                     uint32_t* hist, uint32_t nblocks, int slog, uint32_t sres) {
+                                                     uint32_t* hist, uint32_t nblocks, int slog, uint32_t sres,
+                                                     int swz) {
     extern __shared__ uint32_t hh[];
+    // tile (scalar range and histogram column); swz: XCD-aware, so the blocks
+    // writing neighbouring words of a histogram row share one L2
+    const uint32_t tile = swz ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
     for (int j = threadIdx.x; j < nbins; j += blockDim.x) hh[j] = 0;
     __syncthreads();
     // spb <= 512: at most two scalars per thread, both loaded before any digit work
@@ -274,7 +278,7 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, cons
     for (int s = 0; s < 2; s++) {
         idx[s] = ~(size_t)0;
         if (s * 256 + (int)threadIdx.x < spb) {
-            size_t i = (size_t)blockIdx.x * spb + s * 256 + threadIdx.x;
+            size_t i = (size_t)tile * spb + s * 256 + threadIdx.x;
             if (i < n) {
                 idx[s] = i;
                 scl[s] = ld(scalars + (sidx ? sidx[i] : i));
@@ -291,7 +295,7 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, cons
         });
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < nbins; j += blockDim.x) hist[(size_t)j * nblocks + blockIdx.x] = hh[j];
+    for (int j = threadIdx.x; j < nbins; j += blockDim.x) hist[(size_t)j * nblocks + tile] = hh[j];
 }
 
 // Phase C, LDS-staged: the block's entries are first partitioned by bin in LDS
@@ -579,6 +583,7 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     // every row starts on a 256-B boundary
     static const bool keypad = [] { const char* e = getenv("GG_SORT_KEYPAD"); return e && atoi(e) == 1; }();
     const size_t kst = keypad ? (n + 63) & ~(size_t)63 : n;
+    static const int swz = [] { const char* e = getenv("GG_SORT_SWZ"); return e && atoi(e) == 1 ? 1 : 0; }();
     s->keys.reserve(std::max(total, (size_t)W * kst) * 4);
     s->tmp_entry.reserve(total * 4);
     s->tmp_key.reserve(total * 4);
@@ -599,11 +604,11 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
         hipLaunchKernelGGL(k_digits_hist<FrBlsCfg>, dim3(nblocks), dim3(256), nbins * 4, st,
                            (const FrBls*)scalars_dev, b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n,
                            c, W, b->win, G, kbits, spb, nbins, h, s->keys.as<uint32_t>(), kst,
-                           s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
+                           s->hist.as<uint32_t>(), nblocks, s->slog, s->sres, swz);
     else
         hipLaunchKernelGGL(k_digits_hist<FrCfg>, dim3(nblocks), dim3(256), nbins * 4, st, scalars_dev,
                            b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, G, kbits, spb,
-                           nbins, h, s->keys.as<uint32_t>(), kst, s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
+                           nbins, h, s->keys.as<uint32_t>(), kst, s->hist.as<uint32_t>(), nblocks, s->slog, s->sres, swz);
     GG_HIP(hipGetLastError());
     exclusive_scan(s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nh, st, s->scan_tmp);
     // segment starts ping-pong between bin_start and seg2; the last pass writes offsets
