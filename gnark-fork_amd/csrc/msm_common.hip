@@ -263,12 +263,9 @@ template <class SC>
 __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, const uint32_t* sidx,
                                                      size_t n, int c, int W, WinSpec ws, int G, int kbits,
                                                      int spb, int nbins, int h, uint32_t* keys, size_t kst,
-                                                     uint32_t* hist, uint32_t nblocks, int slog, uint32_t sres,
-                                                     int swz) {
+                                                     uint32_t* hist, uint32_t nblocks, int slog, uint32_t sres) {
     extern __shared__ uint32_t hh[];
-    // tile (scalar range and histogram column); swz: XCD-aware, so the blocks
-    // writing neighbouring words of a histogram row share one L2
-    const uint32_t tile = swz ? xcd_swizzle(blockIdx.x, gridDim.x) : blockIdx.x;
+    const uint32_t tile = blockIdx.x;  // scalar range and histogram column
     for (int j = threadIdx.x; j < nbins; j += blockDim.x) hh[j] = 0;
     __syncthreads();
     // spb <= 512: at most two scalars per thread, both loaded before any digit work
@@ -579,12 +576,10 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
             ns <<= r;
         }
     }
-    // key rows of phase A: stride n, or (GG_SORT_KEYPAD=1) n rounded up to 64 keys so
-    // every row starts on a 256-B boundary
-    static const bool keypad = [] { const char* e = getenv("GG_SORT_KEYPAD"); return e && atoi(e) == 1; }();
-    const size_t kst = keypad ? (n + 63) & ~(size_t)63 : n;
-    static const int swz = [] { const char* e = getenv("GG_SORT_SWZ"); return e && atoi(e) == 1 ? 1 : 0; }();
-    s->keys.reserve(std::max(total, (size_t)W * kst) * 4);
+    // key rows of phase A, stride kst = n (round 4: rows padded to 256-B
+    // boundaries and XCD-aware histogram tiles measured no change, r04_u)
+    const size_t kst = n;
+    s->keys.reserve(total * 4);
     s->tmp_entry.reserve(total * 4);
     s->tmp_key.reserve(total * 4);
     s->sorted.reserve(total * 4 + 64);  // + 64: the accumulation reads 16-B chunks past its last entry
@@ -604,11 +599,11 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
         hipLaunchKernelGGL(k_digits_hist<FrBlsCfg>, dim3(nblocks), dim3(256), nbins * 4, st,
                            (const FrBls*)scalars_dev, b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n,
                            c, W, b->win, G, kbits, spb, nbins, h, s->keys.as<uint32_t>(), kst,
-                           s->hist.as<uint32_t>(), nblocks, s->slog, s->sres, swz);
+                           s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
     else
         hipLaunchKernelGGL(k_digits_hist<FrCfg>, dim3(nblocks), dim3(256), nbins * 4, st, scalars_dev,
                            b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, G, kbits, spb,
-                           nbins, h, s->keys.as<uint32_t>(), kst, s->hist.as<uint32_t>(), nblocks, s->slog, s->sres, swz);
+                           nbins, h, s->keys.as<uint32_t>(), kst, s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
     GG_HIP(hipGetLastError());
     exclusive_scan(s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nh, st, s->scan_tmp);
     // segment starts ping-pong between bin_start and seg2; the last pass writes offsets
