@@ -385,8 +385,10 @@ __global__ void k_bin_starts(const uint32_t* hoff, const uint32_t* hist, uint32_
 // half of all entries, as 0/1-heavy witnesses produce) spreads over many
 // workgroups.  The scatter is LDS-staged: a chunk is first ordered by digit in
 // LDS, then written as per-digit runs of ~SEG_CH / 2^r entries (coalesced).
+// 2048 (round 4, r04_v): 2^24 G1 sort 3.29 -> 3.12 ms against 4096 (half the
+// registers and LDS per workgroup: twice the resident scatter waves); 1024 slower
 #ifndef GG_SEG_CH
-#define GG_SEG_CH 4096
+#define GG_SEG_CH 2048
 #endif
 constexpr uint32_t SEG_CH = GG_SEG_CH;
 constexpr int SEG_PER = SEG_CH / 256;  // entries per thread
