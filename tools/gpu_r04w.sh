@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4 s: the sort changes (4-key-vector chunk histogram, 2048-entry chunks) -- PlonK parity, every
+# Round 4 w: the sort changes (4-key-vector chunk histogram, 2048-entry chunks) -- PlonK parity, every
 # part rehearsed alone, the roofline record's PMC passes of this tree, the
 # driver's bench command, then the full -m gpu suite and smoke.
 cd "${GRAFT_REPO_ROOT:-.}"
