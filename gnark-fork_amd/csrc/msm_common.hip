@@ -188,9 +188,8 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t B, int c, int kbits, int h) 
     return bucket_perm(B, c) >> (kbits - h);
 }
 
-// exclusive scan of v over a block of NW waves (NW wave scans + one barrier);
-// `wsum` is NW words of LDS.  Returns the exclusive prefix; *total = block sum.
-template <int NW = 4>
+// exclusive scan of v over a 256-thread block (4 wave scans + one barrier);
+// `wsum` is 4 words of LDS.  Returns the exclusive prefix; *total = block sum.
 __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* wsum, uint32_t* total) {
     const int lane = __lane_id(), wv = threadIdx.x >> 6;
     uint32_t x = v;
@@ -203,7 +202,7 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* wsu
     __syncthreads();
     uint32_t pre = 0, tot = 0;
 #pragma unroll
-    for (int i = 0; i < NW; i++) {
+    for (int i = 0; i < 4; i++) {
         uint32_t w = wsum[i];
         if (i < wv) pre += w;
         tot += w;
@@ -298,11 +297,8 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, cons
 
 // Phase C, LDS-staged: the block's entries are first partitioned by bin in LDS
 // (ranks from LDS atomics, bin bases from this block's own histogram), then
-// written out as contiguous per-bin runs -> coalesced stores.  BS threads per
-// tile: the LDS tile (~50 KiB) allows 3 tiles per CU, so wider tiles keep more
-// waves in flight.
-template <int BS>
-__global__ void __launch_bounds__(BS) k_bin_scatter(const uint32_t* keys, size_t kst, size_t n, int W, int c, int G,
+// written out as contiguous per-bin runs -> coalesced stores.
+__global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_t kst, size_t n, int W, int c, int G,
                                                      int kbits, int spb, int nbins, int h, const uint32_t* hist,
                                                      const uint32_t* hoff, uint32_t nblocks,
                                                      uint32_t* tmp_entry, void* tmp_key, int key16) {
@@ -320,9 +316,9 @@ __global__ void __launch_bounds__(BS) k_bin_scatter(const uint32_t* keys, size_t
     const bool has = (int)jb < nbins;
     const uint32_t cnt = has ? hist[(size_t)jb * nblocks + tile] : 0u;
     const uint32_t gof = has ? hoff[(size_t)jb * nblocks + tile] : 0u;
-    __shared__ uint32_t wsum[BS / 64];
+    __shared__ uint32_t wsum[4];
     uint32_t tot;
-    const uint32_t ex = block_excl_scan256<BS / 64>(cnt, wsum, &tot);
+    const uint32_t ex = block_excl_scan256(cnt, wsum, &tot);
     if (has) {
         lbase[jb] = ex;
         lcur[jb] = ex;
@@ -333,12 +329,12 @@ __global__ void __launch_bounds__(BS) k_bin_scatter(const uint32_t* keys, size_t
     const int tot_e = ns * W;
     // flat (window, scalar) index j = w * ns + t; keys loaded 8 per batch before
     // the LDS atomics so the loads overlap
-    for (int jb0 = 0; jb0 < tot_e; jb0 += 8 * BS) {
+    for (int jb0 = 0; jb0 < tot_e; jb0 += 8 * 256) {
         uint32_t kk[8];
         uint32_t ee[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-            int j = jb0 + (int)threadIdx.x + u * BS;
+            int j = jb0 + (int)threadIdx.x + u * 256;
             kk[u] = 0xffffffffu;
             if (j < tot_e) {
                 int w = j / ns, t = j - w * ns;
@@ -627,13 +623,7 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     auto ent_out = [&](int j) { return ((S - 1 - j) % 2 == 0) ? &s->sorted : &s->tmp_entry; };
     auto key_out = [&](int j) { return (j % 2 == 0) ? &s->tmp_key : &s->keys; };
     const bool key16 = kbits - h <= 16;
-    static const int bin_bs = [] {
-        const char* e = getenv("GG_BIN_BS");  // tuning override: 256 / 512 / 1024 threads per tile
-        const int v = e ? atoi(e) : 256;
-        return v == 512 || v == 1024 ? v : 256;
-    }();
-    auto bin_scatter = bin_bs == 1024 ? k_bin_scatter<1024> : bin_bs == 512 ? k_bin_scatter<512> : k_bin_scatter<256>;
-    hipLaunchKernelGGL(bin_scatter, dim3(nblocks), dim3(bin_bs), lds_c, st, s->keys.as<uint32_t>(), kst,
+    hipLaunchKernelGGL(k_bin_scatter, dim3(nblocks), dim3(256), lds_c, st, s->keys.as<uint32_t>(), kst,
                        n, W, c, G, kbits, spb, nbins, h, s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nblocks,
                        ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->p : nullptr, (int)key16);
     GG_HIP(hipGetLastError());
