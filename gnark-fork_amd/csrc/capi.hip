@@ -11,9 +11,42 @@ void set_last_error(const std::string& m) { g_last_error = m; }
 
 using namespace gg;
 
+std::vector<int> gg::enable_peer_access(const std::vector<int>& devs) {
+    const int k = (int)devs.size();
+    std::vector<int> code((size_t)k * k, GG_PEER_SAME_DEVICE);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (int i = 0; i < k; i++)
+        for (int j = 0; j < k; j++) {
+            if (devs[i] == devs[j]) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, devs[i], devs[j]) != hipSuccess || !can) {
+                (void)hipGetLastError();
+                code[(size_t)i * k + j] = GG_PEER_UNAVAILABLE;
+                continue;
+            }
+            if (hipSetDevice(devs[i]) != hipSuccess) {
+                (void)hipGetLastError();
+                code[(size_t)i * k + j] = GG_PEER_FAILED;
+                continue;
+            }
+            const hipError_t e = hipDeviceEnablePeerAccess(devs[j], 0);
+            if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) {
+                code[(size_t)i * k + j] = GG_PEER_ENABLED;
+            } else {
+                code[(size_t)i * k + j] = GG_PEER_FAILED;
+            }
+            (void)hipGetLastError();
+        }
+    (void)hipSetDevice(cur);
+    return code;
+}
+
 extern "C" const char* gg_last_error(void) { return g_last_error.c_str(); }
 
 extern "C" int gg_version(void) { return 100; }  // 0.1.0
+
+extern "C" int gg_build_flags(void) { return kAccumProbe ? GG_BUILD_ACCUM_PROBE : 0; }
 
 extern "C" int gg_device_count(int* count) {
     GG_CAPI_BEGIN

@@ -5,9 +5,20 @@
 #include <stdexcept>
 #include <string>
 #include <cstdio>
+#include <vector>
 #include "../../include/gnark_amd.h"
 
+// -DGG_ACCUM_PROBE=1 builds a traffic-attribution variant (build_var/, never
+// the product library): the MSM accumulation reads its points from <= 1024
+// cached entries, so its sums are wrong.  gg_build_flags() reports it and the
+// provers of such a build return GG_REHEARSAL, never GG_OK.
+#ifndef GG_ACCUM_PROBE
+#define GG_ACCUM_PROBE 0
+#endif
+
 namespace gg {
+
+constexpr bool kAccumProbe = GG_ACCUM_PROBE != 0;
 
 struct Error : std::runtime_error {
     int code;
@@ -117,6 +128,12 @@ __device__ __forceinline__ uint32_t xcd_swizzle(uint32_t bid, uint32_t nwg) {
     const uint32_t q = nwg >> 3, r = nwg & 7, x = bid & 7;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
 }
+
+// Enables xGMI peer access from every listed device to every other one and
+// returns the outcome per ordered pair (i, j) as GG_PEER_* codes (row-major,
+// devs.size()^2): a pair whose access failed still copies, staged through host
+// memory by the runtime, so callers report it (capi.hip).
+std::vector<int> enable_peer_access(const std::vector<int>& devs);
 
 inline unsigned grid_for(size_t n, unsigned block) {
     size_t g = (n + block - 1) / block;

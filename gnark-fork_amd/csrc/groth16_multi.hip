@@ -111,6 +111,9 @@ struct gg_groth16_mpk {
                wait_out[GG_MPK_MAX_EXCHANGES] = {}, mbytes[GG_MPK_MAX_EXCHANGES] = {};
     };
     std::vector<ShardTimes> times;
+    // peer access of shard i's device to shard j's (gg_groth16_mpk_peer_access):
+    // GG_PEER_* codes, world x world
+    std::vector<int> peer;
 };
 
 namespace {
@@ -271,17 +274,9 @@ extern "C" int gg_groth16_mpk_create_ex(int curve, int log_n, const void* omega_
     memcpy(m->beta2, beta2, m->g2a);
     memcpy(m->delta2, delta2, m->g2a);
     // xGMI peer access between the distinct devices (copies work without it,
-    // staged by the runtime)
-    for (int i = 0; i < world; i++)
-        for (int j = 0; j < world; j++) {
-            if (m->dev[i] == m->dev[j]) continue;
-            int can = 0;
-            if (hipDeviceCanAccessPeer(&can, m->dev[i], m->dev[j]) == hipSuccess && can &&
-                hipSetDevice(m->dev[i]) == hipSuccess) {
-                const hipError_t e = hipDeviceEnablePeerAccess(m->dev[j], 0);
-                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
-            }
-        }
+    // staged through host memory by the runtime -- which would look like slow
+    // xGMI, so the outcome is kept per pair: gg_groth16_mpk_peer_access)
+    m->peer = gg::enable_peer_access(m->dev);
     // prefix counts of the non-infinity A / B points (key order = wire order)
     std::vector<size_t> pa(n_wires + 1, 0), pb(n_wires + 1, 0);
     for (size_t w = 0; w < n_wires; w++) {
@@ -560,7 +555,11 @@ extern "C" int gg_groth16_mpk_prove_ex(gg_groth16_mpk_t m, int inputs_on_device,
     m->last_ms[0] = std::chrono::duration<double, std::milli>(t1 - t0).count();
     m->last_ms[1] = std::chrono::duration<double, std::milli>(t2 - t1).count();
     m->last_ms[2] = std::chrono::duration<double, std::milli>(t2 - t0).count();
-    if (m->solo >= 0) {
+    if (gg::kAccumProbe || m->solo >= 0) {
+        if (gg::kAccumProbe) {
+            gg::set_last_error("traffic-probe build (GG_ACCUM_PROBE): the MSM sums are wrong, the proof is NOT valid");
+            return GG_REHEARSAL;
+        }
         gg::set_last_error("timing rehearsal (gg_groth16_mpk_set_rehearsal): shard " + std::to_string(m->solo) +
                            " proved alone, the proof is NOT valid");
         return GG_REHEARSAL;
@@ -593,6 +592,14 @@ extern "C" int gg_groth16_mpk_set_rehearsal(gg_groth16_mpk_t m, int solo_shard) 
     GG_CHECK(solo_shard >= -1 && solo_shard < m->world, GG_ERR_INVALID_ARG, "solo shard out of range");
     std::lock_guard<std::mutex> lk(m->mu);
     m->solo = solo_shard;
+    GG_CAPI_END
+}
+
+extern "C" int gg_groth16_mpk_peer_access(gg_groth16_mpk_t m, int* codes, int cap) {
+    GG_CAPI_BEGIN
+    GG_CHECK(m && codes, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(cap >= m->world * m->world, GG_ERR_INVALID_ARG, "cap < world * world");
+    for (int i = 0; i < m->world * m->world; i++) codes[i] = m->peer[i];
     GG_CAPI_END
 }
 

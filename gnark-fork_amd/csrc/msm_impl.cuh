@@ -1114,10 +1114,15 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
         // per-group names: the Groth16 prove runs G1 and G2 accumulations at once
         const char* acc_name = sizeof(F) == sizeof(Fp) ? "msm_accum" : (sizeof(F) == sizeof(Fp2) ? "msm_accum_g2" : "msm_accum_bls");
         ProfScope ps_acc(acc_name, st, (double)n);
-        // GG_ACCUM_PROBE=1 (traffic attribution only, wrong sums): every entry reads
-        // one of the first 1024 points, so HBM sees everything but the point gathers
-        const char* probe = getenv("GG_ACCUM_PROBE");
-        const uint32_t pmask = probe && atoi(probe) ? 1023u : 0x7fffffffu;
+        // A probe BUILD (-DGG_ACCUM_PROBE=1, traffic attribution only, wrong sums;
+        // never an environment switch of the product library): every entry reads
+        // one of the first <= 1024 points, so HBM sees everything but the point
+        // gathers.  Such a library refuses proofs (gg_build_flags, capi.hip).
+        uint32_t pmask = 0x7fffffffu;
+        if (kAccumProbe) {
+            pmask = 1023u;
+            while (pmask && pmask >= n) pmask >>= 1;  // stay inside the base
+        }
         hipLaunchKernelGGL(k_accum_range<F>, dim3(grid_for(T, 256)), dim3(256), 0, st, (const Affine<F>*)b->pts.p,
                            s->sorted.as<uint32_t>(), offs, (uint32_t)nb, ce, K, (int)b->has_inf, hP, tP, SP,
                            scr->tbucket.as<uint32_t>(), pmask);

@@ -1065,28 +1065,40 @@ static void phase_order(gg_hshard* hs, int phase) {
              "distributed computeH: phase " + std::to_string(phase) + " after phase " +
                  std::to_string(hs->last_phase) +
                  " on this handle (phases run 1, 2, 3, 4 in order, one proof at a time per handle)");
-    hs->last_phase = phase == 4 ? 0 : phase;
 }
+// records a phase as done only once its body has been enqueued; a phase that
+// throws leaves the handle expecting phase 1 again (its y / ccoef state is stale)
+struct PhaseStep {
+    gg_hshard* hs;
+    int phase;
+    bool ok = false;
+    PhaseStep(gg_hshard* h, int p) : hs(h), phase(p) { phase_order(h, p); }
+    ~PhaseStep() { hs->last_phase = ok && phase != 4 ? phase : 0; }
+};
 void hshard_phase1(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len, Fr* send, hipStream_t st,
                    bool compact = false) {
-    phase_order(hs, 1);
+    PhaseStep step(hs, 1);
     if (hs->curve == GG_CURVE_BN254) phase1_t<FrCfg>(hs, a, b, c, len, send, st, compact);
     else phase1_t<FrBlsCfg>(hs, (const FrBls*)a, (const FrBls*)b, (const FrBls*)c, len, (FrBls*)send, st, compact);
+    step.ok = true;
 }
 void hshard_phase2(gg_hshard* hs, const Fr* recv, Fr* send, hipStream_t st) {
-    phase_order(hs, 2);
+    PhaseStep step(hs, 2);
     if (hs->curve == GG_CURVE_BN254) phase2_t<FrCfg>(hs, recv, send, st);
     else phase2_t<FrBlsCfg>(hs, (const FrBls*)recv, (FrBls*)send, st);
+    step.ok = true;
 }
 void hshard_phase3(gg_hshard* hs, const Fr* recv, Fr* send, hipStream_t st) {
-    phase_order(hs, 3);
+    PhaseStep step(hs, 3);
     if (hs->curve == GG_CURVE_BN254) phase3_t<FrCfg>(hs, recv, send, st);
     else phase3_t<FrBlsCfg>(hs, (const FrBls*)recv, (FrBls*)send, st);
+    step.ok = true;
 }
 void hshard_phase4(gg_hshard* hs, const Fr* recv, Fr* h, hipStream_t st) {
-    phase_order(hs, 4);
+    PhaseStep step(hs, 4);
     if (hs->curve == GG_CURVE_BN254) phase4_t<FrCfg>(hs, recv, h, st);
     else phase4_t<FrBlsCfg>(hs, (const FrBls*)recv, (FrBls*)h, st);
+    step.ok = true;
 }
 
 size_t hshard_m(const gg_hshard* hs, int* rank, int* world, int* log_n) {

@@ -377,6 +377,7 @@ struct Key : gg_plonk_pk {
     int solo_part = 0;
     std::mutex tmu;
     std::vector<PlonkPartTimes> ptimes;  // [part], last proof
+    std::vector<int> peer_codes;         // GG_PEER_* per ordered part pair (one-process parts)
     int n_cmt = 0;
     hipStream_t s[4] = {nullptr, nullptr, nullptr, nullptr};
     MsmWork* work[3] = {nullptr, nullptr, nullptr};
@@ -707,17 +708,9 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
         for (int d = 0; d < n_devices; d++)
             GG_CHECK(devices[d] >= 0 && devices[d] < ndev, GG_ERR_INVALID_ARG, "device id out of range");
         GG_HIP(hipSetDevice(devices[0]));
-        // xGMI peer access between the distinct devices (copies work without it)
-        for (int a = 0; a < n_devices; a++)
-            for (int b = 0; b < n_devices; b++) {
-                int can = 0;
-                if (devices[a] == devices[b]) continue;
-                if (hipDeviceCanAccessPeer(&can, devices[a], devices[b]) == hipSuccess && can &&
-                    hipSetDevice(devices[a]) == hipSuccess) {
-                    const hipError_t e = hipDeviceEnablePeerAccess(devices[b], 0);
-                    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
-                }
-            }
+        // xGMI peer access between the distinct devices (copies work without it,
+        // staged through host memory: kept per pair, gg_plonk_pk_peer_access)
+        pk->peer_codes = gg::enable_peer_access(std::vector<int>(devices, devices + n_devices));
         GG_HIP(hipSetDevice(devices[0]));
     }
     GG_HIP(hipGetDevice(&pk->device));
@@ -1769,7 +1762,16 @@ extern "C" int gg_plonk_commit_lagrange(gg_plonk_pk_t pk, const void* values, in
         GG_HIP(hipSetDevice(k->device));
         hipStream_t st = k->s[3];
         Impl::up(k->pad.p, values, 32 * k->n, on_device != 0, st);
+        // a hint commitment is a value the circuit consumes: every part works on
+        // it even while the key rehearses one part (gg_plonk_pk_set_rehearsal_part)
+        struct SoloGuard {
+            bool& f;
+            bool saved;
+            ~SoloGuard() { f = saved; }
+        } solo_guard{k->solo, k->solo};
+        k->solo = false;
         const auto a = Impl::to_aff(Impl::red(k, Impl::msm_jac(k, k->kzg_lag, 2, Impl::F(k->pad), st)));
+        if (gg::kAccumProbe) throw gg::Error(GG_REHEARSAL, "traffic-probe build (GG_ACCUM_PROBE): wrong MSM sums");
         memcpy(out_aff, &a, sizeof(a));
         return 0;
     });
@@ -1832,6 +1834,10 @@ extern "C" int gg_plonk_prove(gg_plonk_pk_t pk, const void* l, const void* r, co
         return 0;
     });
     const bool rehearsal = with_key(pk, [](auto* k) { return k->solo && !k->peers.empty(); });
+    if (gg::kAccumProbe) {
+        gg::set_last_error("traffic-probe build (GG_ACCUM_PROBE): the MSM sums are wrong, the proof is NOT valid");
+        return GG_REHEARSAL;
+    }
     if (rehearsal) {
         gg::set_last_error("timing rehearsal (gg_plonk_pk_set_rehearsal): only one device part worked, the proof "
                            "is NOT valid");
@@ -1871,6 +1877,21 @@ extern "C" int gg_plonk_pk_part_timings(gg_plonk_pk_t pk, int part, double* out,
                                                T.coset_mb,    T.wait_ms,   T.ratio_ms,        T.canon_count,
                                                T.canon_ms,    T.canon_mb};
         for (int i = 0; i < GG_PLONK_PART_SLOTS; i++) out[i] = v[i];
+        return 0;
+    });
+    GG_CAPI_END
+}
+
+extern "C" int gg_plonk_pk_peer_access(gg_plonk_pk_t pk, int* codes, int cap, int* n_parts) {
+    GG_CAPI_BEGIN
+    GG_CHECK(pk && n_parts, GG_ERR_INVALID_ARG, "null argument");
+    with_key(pk, [&](auto* k) {
+        const int np = 1 + (int)k->peers.size();
+        *n_parts = np;
+        if (!codes) return 0;  // size query
+        GG_CHECK(cap >= np * np, GG_ERR_INVALID_ARG, "cap < parts * parts");
+        for (int i = 0; i < np * np; i++)
+            codes[i] = i < (int)k->peer_codes.size() ? k->peer_codes[i] : GG_PEER_SAME_DEVICE;
         return 0;
     });
     GG_CAPI_END

@@ -12,11 +12,13 @@ _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("GNARK_AMD_LIB", os.path.join(_PKG_DIR, "lib", "libgnark_amd.so"))
 
 GG_OK = 0
+GG_BUILD_ACCUM_PROBE = 1  # gg_build_flags(): a traffic-attribution build, MSM sums wrong by design
 GG_REHEARSAL = 7  # a multi-GPU timing rehearsal: the proof written is not valid
 GG_MPK_TIMING_SLOTS = 18
 GG_PLONK_PART_SLOTS = 14
 GG_G1, GG_G2, GG_BLS12_381_G1, GG_BLS12_381_G2 = 1, 2, 3, 4
 GG_CURVE_BN254, GG_CURVE_BLS12_381 = 0, 1
+PEER_ACCESS = {0: "same_device", 1: "enabled", 2: "unavailable", 3: "enable_failed"}  # GG_PEER_*
 GG_DIF, GG_DIT = 0, 1
 
 
@@ -48,6 +50,7 @@ def _load():
     sig = {
         "gg_last_error": ([], ctypes.c_char_p),
         "gg_version": ([], I),
+        "gg_build_flags": ([], I),
         "gg_device_count": ([ctypes.POINTER(I)], I),
         "gg_set_device": ([I], I),
         "gg_malloc": ([PP, S], I),
@@ -135,6 +138,8 @@ def _load():
         "gg_groth16_mpk_last_timings": ([P, ctypes.POINTER(ctypes.c_double)], I),
         "gg_groth16_mpk_shard_timings": ([P, I, ctypes.POINTER(ctypes.c_double), I], I),
         "gg_groth16_mpk_set_rehearsal": ([P, I], I),
+        "gg_groth16_mpk_peer_access": ([P, ctypes.POINTER(I), I], I),
+        "gg_plonk_pk_peer_access": ([P, ctypes.POINTER(I), I, ctypes.POINTER(I)], I),
         "gg_batch_scalar_mul": ([I, P, P, S, I, P, I], I),
         "gg_plonk_numerator_coset": ([ctypes.POINTER(ctypes.c_void_p), I, P, ctypes.POINTER(I), P,
                                       P, P, P, P, S, I, I, P, P], I),
@@ -188,8 +193,14 @@ def _load():
 
 
 lib = _load()
+# a diagnostic build (GG_BUILD_ACCUM_PROBE: wrong MSM sums) is loaded only when
+# asked for by name; its provers return GG_REHEARSAL
+BUILD_FLAGS = lib.gg_build_flags()
+if BUILD_FLAGS and os.environ.get("GNARK_AMD_ALLOW_PROBE") != "1":
+    raise ImportError(f"{LIB_PATH} is a diagnostic build (flags {BUILD_FLAGS}): its MSM sums are wrong; "
+                      "set GNARK_AMD_ALLOW_PROBE=1 to load it for traffic attribution")
 EXPORTED = [
-    "gg_last_error", "gg_version", "gg_device_count", "gg_set_device", "gg_malloc", "gg_free",
+    "gg_last_error", "gg_version", "gg_build_flags", "gg_device_count", "gg_set_device", "gg_malloc", "gg_free",
     "gg_copy_to_device", "gg_copy_to_host", "gg_synchronize", "gg_domain_create",
     "gg_domain_create_ex", "gg_bls12_381_g1_jac_to_affine", "gg_bls12_381_g1_jac_add",
     "gg_domain_release", "gg_domain_log_n", "gg_ntt", "gg_groth16_compute_h",
@@ -220,7 +231,7 @@ EXPORTED = [
     "gg_msm_stripe", "gg_groth16_pk_create_stripe_ex", "gg_groth16_pk_stripe", "gg_groth16_mpk_split",
     "gg_hshard_create_ex", "gg_hshard_exchange_bytes", "gg_groth16_mpk_shard_timings",
     "gg_groth16_mpk_set_rehearsal", "gg_plonk_pk_set_rehearsal", "gg_plonk_pk_set_rehearsal_part",
-    "gg_plonk_pk_part_timings",
+    "gg_plonk_pk_part_timings", "gg_groth16_mpk_peer_access", "gg_plonk_pk_peer_access",
     "gg_fr_evaluate_many",
 ]
 

@@ -241,6 +241,17 @@ class ProvingKey:
         prove() refuses them unless called with rehearsal_ok=True."""
         check(lib.gg_plonk_pk_set_rehearsal_part(self.handle, int(part) if on else -1))
 
+    def peer_access(self) -> list:
+        """[i][j]: how device part i reaches part j ('same_device', 'enabled',
+        'unavailable', 'enable_failed'; gg_plonk_pk_peer_access)"""
+        from ._lib import PEER_ACCESS
+        k = ctypes.c_int()
+        check(lib.gg_plonk_pk_peer_access(self.handle, None, 0, ctypes.byref(k)))
+        w = k.value
+        arr = (ctypes.c_int * (w * w))()
+        check(lib.gg_plonk_pk_peer_access(self.handle, arr, w * w, ctypes.byref(k)))
+        return [[PEER_ACCESS.get(arr[i * w + j], str(arr[i * w + j])) for j in range(w)] for i in range(w)]
+
     def part_timings(self) -> list:
         """Per device part (0 = primary), the last proof: MSM slices and their ms,
         scalar-slice copies (ms, MB), quotient units (ms, copies in / out, MB),

@@ -40,6 +40,9 @@ extern "C" {
  * gg_plonk_pk_set_rehearsal): the proof written is NOT valid.  Never GG_OK, so
  * a caller checking for success cannot pass such a proof on. */
 #define GG_REHEARSAL 7
+/* gg_build_flags() bits: a diagnostic build whose MSM sums are wrong by design
+ * (traffic attribution, never shipped); its provers return GG_REHEARSAL */
+#define GG_BUILD_ACCUM_PROBE 1
 
 #define GG_G1 1
 #define GG_G2 2
@@ -78,6 +81,8 @@ typedef int (*gg_exchange_fn)(void *ctx, const void *send_dev, void *recv_dev,
 /* ---------------------------------------------------------------- runtime */
 const char *gg_last_error(void);
 int gg_version(void);
+/* GG_BUILD_* bits of this library build (0 for the product library) */
+int gg_build_flags(void);
 int gg_device_count(int *count);
 /* binds the calling host thread to a GPU (one process per GPU is the norm) */
 int gg_set_device(int device);
@@ -448,6 +453,16 @@ int gg_groth16_mpk_last_timings(gg_groth16_mpk_t mpk, double *ms3);
 #define GG_MPK_MAX_EXCHANGES 4
 #define GG_MPK_TIMING_SLOTS (2 + 4 * GG_MPK_MAX_EXCHANGES)
 int gg_groth16_mpk_shard_timings(gg_groth16_mpk_t mpk, int shard, double *out, int cap);
+/* xGMI peer access between the parts of a one-process multi-GPU key, as the
+ * key's creation left it (hipDeviceEnablePeerAccess, icicle has no such step):
+ * codes[i * world + j] for shard i's device reaching shard j's.  A failed pair
+ * still copies, staged through host memory by the runtime -- slow, so a first
+ * N-GPU run reports it instead of swallowing it. */
+#define GG_PEER_SAME_DEVICE 0 /* both parts on one GPU (a rehearsal) */
+#define GG_PEER_ENABLED 1     /* peer access on (enabled now or already) */
+#define GG_PEER_UNAVAILABLE 2 /* hipDeviceCanAccessPeer says no */
+#define GG_PEER_FAILED 3      /* hipDeviceEnablePeerAccess failed */
+int gg_groth16_mpk_peer_access(gg_groth16_mpk_t mpk, int *codes, int cap);
 /* Timing rehearsal (bench / tests only): solo_shard >= 0 makes every later
  * prove run shard solo_shard ALONE (its exchanges skip the peers, the other
  * shards contribute identity partials), so one GPU times the work one GPU of
@@ -640,6 +655,9 @@ int gg_plonk_pk_set_rehearsal_part(gg_plonk_pk_t pk, int part);
  * (input, transform, pushes), [13] MB they pushed over xGMI. */
 #define GG_PLONK_PART_SLOTS 14
 int gg_plonk_pk_part_timings(gg_plonk_pk_t pk, int part, double *out, int cap);
+/* GG_PEER_* codes per ordered pair of device parts (codes[i * parts + j]);
+ * codes = NULL only stores the part count in *n_parts */
+int gg_plonk_pk_peer_access(gg_plonk_pk_t pk, int *codes, int cap, int *n_parts);
 /* the key's vk digests, 96-B affine each: S[0..2], Ql, Qr, Qm, Qo, Qk, Qcp[0..n_cmt) */
 int gg_plonk_pk_vk(gg_plonk_pk_t pk, void *out, size_t cap);
 /* kzg.Commit(values, pk.KzgLagrange): n Lagrange values (host or device) -> affine 96 B.
