@@ -174,6 +174,18 @@ def main():
         else:
             dist.init_process_group(backend, timeout=datetime.timedelta(minutes=10))
 
+    # GPUs actually used: the distinct devices of the ranks (gloo rehearsals may
+    # put every rank on one GPU; under RCCL each rank needs a GPU of its own)
+    rank_devices = [dev]
+    if world > 1:
+        t = torch.tensor([dev], dtype=torch.int64, device=xdev)
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        rank_devices = [int(x.item()) for x in allt]
+        if backend == "nccl" and len(set(rank_devices)) < world:
+            raise SystemExit(f"bench: --gpus {args.gpus} under RCCL but the ranks see only "
+                             f"{len(set(rank_devices))} distinct GPU(s) {rank_devices}")
+
     def barrier():
         if dist is not None:
             dist.barrier()
@@ -194,7 +206,7 @@ def main():
     g = Groth16Bench(args.log_n, rank, world, dist, xdev, host_inputs=args.host_inputs, devices=devices)
     log(f"[rank {rank}] key ready: 2^{args.log_n}, {g.shape['ncons']} constraints, "
         f"{g.shape['nw']} wires ({time.time() - t0:.1f}s)")
-    n_gpus = len(set(devices)) if mode == "mpk" else world
+    n_gpus = len(set(devices)) if mode == "mpk" else len(set(rank_devices))
     n_shards = len(devices) if mode == "mpk" else world
     import gc
 
@@ -296,8 +308,13 @@ def main():
                    "log_n": args.log_n, "n_constraints": ncons, "n_wires": g.shape["nw"],
                    "inputs": "host" if args.host_inputs else "device",
                    "parallelism": ("key shard x%d (%s + Z positions), distributed computeH "
-                                   "(3 RCCL all-to-alls), RCCL all-gather of 576-B partials; one process per "
-                                   "GPU (torch.distributed.run)" % (world, SPLIT_DESC[g.split])) if mode == "torch"
+                                   "(3 %s all-to-alls), %s all-gather of 576-B partials; one process per "
+                                   "rank (torch.distributed.run) on GPU(s) %s%s"
+                                   % (world, SPLIT_DESC[g.split], "RCCL" if backend == "nccl" else backend,
+                                      "RCCL" if backend == "nccl" else backend, sorted(set(rank_devices)),
+                                      "" if len(set(rank_devices)) == world else
+                                      " -- REHEARSAL: ranks share GPUs, not an N-GPU measurement"))
+                                  if mode == "torch"
                                   else ("key shard x%d on devices %s (%s + Z positions), distributed computeH "
                                         "(3 all-to-alls as in-library xGMI peer copies), partials summed in the "
                                         "library; ONE process (gg_groth16_mpk_*, the Go shape)"
@@ -319,6 +336,7 @@ def main():
     }
     if mode == "mpk":  # where each shard's time went (last timed proof): compute vs barrier waits vs xGMI
         out["shard_timings"] = g.shard_timings
+        out["peer_access"] = g.pk.peer_access()
     elif mode == "torch":
         out["shard_timings"] = g.rank_timings(dist, xdev)
 
@@ -630,12 +648,18 @@ def split_projection(g, worlds, one_gpu_ms, steps=5):
             mpk.prove(sd, opt, r=g.r, s=g.s, rehearsal_ok=True)
             ts.append(1e3 * (time.perf_counter() - a))
         med = sorted(ts)[len(ts) // 2]
-        s0 = mpk.shard_timings()[0]
+        # the exchanges a real N-GPU proof makes (the rehearsal skips the peers):
+        # bytes per rank pair of the three all-to-alls (gg_hshard_exchange_bytes)
+        hs = groth16.HShard(g.log_n, 0, n)
+        planned = [hs.exchange_bytes_after(p) for p in (1, 2, 3)]
+        hs.close()
         res[str(n)] = {"shard_ms_median": med, "shard_ms": [round(x, 2) for x in ts],
                        "speedup": one_gpu_ms / med, "split": mpk.split(), "key_setup_s": round(setup, 1),
-                       "exchange_MB_per_peer": [round(e["pushed_MB"], 3) for e in s0["exchanges"]],
-                       "xgmi_bytes_not_timed": "per exchange the shard pushes (N-1) x these MB; at ~50 GB/s "
-                                               "per xGMI link that is the transfer time one real N-GPU proof adds"}
+                       "exchange_MB_per_peer": [round(x / 1e6, 3) for x in planned],
+                       "exchange_MB_per_shard": [round((n - 1) * x / 1e6, 3) for x in planned],
+                       "xgmi_bytes_not_timed": "planned bytes of the three all-to-alls (gg_hshard_exchange_bytes): "
+                                               "per exchange a shard pushes exchange_MB_per_peer to each of its "
+                                               "N-1 peers at once, one link each; the rehearsal skips them"}
         del sd
         mpk.close()
     return res
@@ -1119,36 +1143,57 @@ def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, 
 
     t0 = time.time()
     gen = fr.bls_fp_mont(BLS_G1_GEN[0]) + fr.bls_fp_mont(BLS_G1_GEN[1])
-    kzg = DeviceBuffer(96 * (n + 3))
-    msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bls_dev(n + 3, 61), n + 3, scalars_on_device=True, out=kzg)
-    lag = DeviceBuffer(96 * n)
-    msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bls_dev(n, 62), n, scalars_on_device=True, out=lag)
-    sel = [bls_dev(n, 70 + i) for i in range(8)]
+    # process-per-GPU launch: "leader" (default) = rank 0 drives a one-process
+    # multi-part key over every rank's GPU (plonk_prover.GroupProvingKey, the
+    # whole part split); GG_PLONK_TORCH=shard = every rank keeps its KZG base
+    # slice and replicates the non-MSM work (the round-3 design)
+    group = world > 1 and os.environ.get("GG_PLONK_TORCH", "leader") != "shard"
+    builds = not group or rank == 0
     perm = np.random.default_rng(71).permutation(3 * n).astype(np.int64).tobytes()
+    kzg = lag = None
+    sel = [None] * 8
+    if builds:
+        kzg = DeviceBuffer(96 * (n + 3))
+        msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bls_dev(n + 3, 61), n + 3, scalars_on_device=True, out=kzg)
+        lag = DeviceBuffer(96 * n)
+        msm.batch_scalar_mul(msm.BLS12_381_G1, gen, bls_dev(n, 62), n, scalars_on_device=True, out=lag)
+        sel = [bls_dev(n, 70 + i) for i in range(8)]
     shard, reduce = None, None
-    if world > 1:
-        from gnark_amd import dist as gdist
-        shard = (rank, world)
+    if group:
+        import torch
+        gpk = pp.GroupProvingKey(log_n, kzg, lag, *sel, perm, local_device=torch.cuda.current_device(),
+                                 comm_device=xdev)
+        pk = gpk.pk
+        devices = gpk.devices
+    else:
+        if world > 1:
+            from gnark_amd import dist as gdist
+            shard = (rank, world)
 
-        def reduce(jac):
-            return gdist.allgather_partial(msm.BLS12_381_G1, jac, device=xdev)
-    pk = pp.ProvingKey(log_n, kzg, lag, *sel, perm, shard=shard, reduce=reduce, devices=devices)
+            def reduce(jac):
+                return gdist.allgather_partial(msm.BLS12_381_G1, jac, device=xdev)
+        pk = pp.ProvingKey(log_n, kzg, lag, *sel, perm, shard=shard, reduce=reduce, devices=devices)
     del kzg, lag, sel
-    L, R_, O = (bls_dev(n, 80 + i) for i in range(3))
+    L, R_, O = (bls_dev(n, 80 + i) for i in range(3)) if builds else (None, None, None)
     t_setup = time.time() - t0
 
     def rng():  # the blinding randomness must be identical on every rank
         import random
         return random.Random(1234)
 
-    pp.prove(pk, L, R_, O, rng=rng())
+    def prove_once(**kw):
+        if group:
+            return pp.prove_group(gpk, L, R_, O, **kw)
+        return pp.prove(pk, L, R_, O, **kw)
+
+    prove_once(rng=rng())
     ts, tim, tims = [], {}, []
     for _ in range(reps):
         if barrier is not None and world > 1:
             barrier()
         t = time.perf_counter()
         tim = {}
-        pp.prove(pk, L, R_, O, timings=tim, rng=rng())
+        prove_once(timings=tim, rng=rng())
         if barrier is not None and world > 1:
             barrier()
         el = 1e3 * (time.perf_counter() - t)
@@ -1161,9 +1206,21 @@ def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, 
         tims.append(tim)
     tim = tims[ts.index(min(ts))]
     extra = {"stage_ms_all": tims} if per_rep else {}
-    if devices and len(devices) > 1:  # one process, N device parts: where each part's time went
+    if devices and len(devices) > 1:
+        kzg_desc = ("%s, %d device parts on GPU(s) %s: KZG base slices cut by per-part shares, partial "
+                    "commitments summed in the library"
+                    % ("process-per-GPU launch, rank 0 drives every rank's GPU (GroupProvingKey)" if group
+                       else "one process", len(devices), sorted(set(devices))))
+        if pk is not None:
+            extra["peer_access"] = pk.peer_access()
+    elif world > 1:
+        kzg_desc = "1/%d slice per rank, partial commitments all-gathered" % world
+    else:
+        kzg_desc = "whole KZG bases on one GPU"
+    if devices and len(devices) > 1 and pk is not None:  # N device parts: where each part's time went
         extra["part_timings"] = [{k: round(v, 3) for k, v in p.items()} for p in pk.part_timings()]
         extra["devices"] = list(devices)
+        extra["launch"] = "leader (rank 0 of %d processes)" % world if group else "one process"
     # configs[4] is 8 x MI355X: each device part of an N-part one-process key
     # proved alone (rehearsal: the other parts skip their work) -- every GPU's
     # share of an N-GPU proof timed on one GPU; the slowest part bounds the proof
@@ -1207,7 +1264,7 @@ def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, 
             pkm.close()
         extra["split_projection"] = proj
     return {"log_n": log_n, "n_gpus": len(set(devices)) if devices else world, "prove_ms": min(ts), "prove_ms_all": ts, "stage_ms": tim,
-            **extra, "kzg_bases": "1/%d slice per GPU, partial commitments all-gathered" % world,
+            **extra, "kzg_bases": kzg_desc,
             "key_setup_s": t_setup, "msms_per_proof": 10,
             "ntts_per_proof": "20 coset FFTs (L,R,O,Z,Qk x 4 cosets; key polynomials resident) + 5 iFFTs of n + 1 coset iFFT of 4n",
             "orchestration": "C++ (gg_plonk_prove): 3 concurrent KZG MSMs for LRO and for H, openZ || linearized, two cosets in flight",

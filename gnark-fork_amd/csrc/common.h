@@ -135,6 +135,19 @@ __device__ __forceinline__ uint32_t xcd_swizzle(uint32_t bid, uint32_t nwg) {
 // memory by the runtime, so callers report it (capi.hip).
 std::vector<int> enable_peer_access(const std::vector<int>& devs);
 
+// A stream for copies that must not wait behind kernels of other streams: HIP
+// maps the streams of a device round-robin onto GPU_MAX_HW_QUEUES (4) hardware
+// queues per priority, and a queue runs its packets in order -- with 8 streams
+// the 5th shares the 1st's queue and a copy on it waits for the 1st's MSM
+// kernel (tools/mbench_xqueue, profiles/r05_a_xqueue.txt: 6.3 ms instead of
+// 0.1 ms behind a 6-ms kernel).  Streams of the greatest priority live in their
+// own queues, so copies on them start at once whatever the compute streams run.
+inline void create_copy_stream(hipStream_t* s) {
+    int lo = 0, hi = 0;
+    GG_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    GG_HIP(hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi));
+}
+
 inline unsigned grid_for(size_t n, unsigned block) {
     size_t g = (n + block - 1) / block;
     return (unsigned)(g ? g : 1);

@@ -97,8 +97,9 @@ struct gg_groth16_mpk {
     std::vector<gg_groth16_pk_t> pk;
     std::vector<gg_hshard_t> hs;
     std::vector<void*> send, recv;
-    std::vector<hipStream_t> st;
-    std::vector<std::vector<hipStream_t>> xst;  // per shard: one copy stream per destination
+    // per shard: one copy stream per destination, of the greatest priority
+    // (common.h create_copy_stream: their own hardware queues)
+    std::vector<std::vector<hipStream_t>> xst;
     uint8_t alpha1[96], beta1[96], delta1[96], beta2[192], delta2[192];
     Barrier bar;
     std::mutex mu;  // one proof at a time per key
@@ -188,7 +189,6 @@ void mpk_free(gg_groth16_mpk* m) {
         if (r < (int)m->hs.size() && m->hs[r]) gg_hshard_release(m->hs[r]);
         if (r < (int)m->send.size() && m->send[r]) (void)hipFree(m->send[r]);
         if (r < (int)m->recv.size() && m->recv[r]) (void)hipFree(m->recv[r]);
-        if (r < (int)m->st.size() && m->st[r]) (void)hipStreamDestroy(m->st[r]);
         if (r < (int)m->xst.size())
             for (hipStream_t s : m->xst[r])
                 if (s) (void)hipStreamDestroy(s);
@@ -265,7 +265,6 @@ extern "C" int gg_groth16_mpk_create_ex(int curve, int log_n, const void* omega_
     m->hs.assign(world, nullptr);
     m->send.assign(world, nullptr);
     m->recv.assign(world, nullptr);
-    m->st.assign(world, nullptr);
     m->xst.assign(world, {});
     m->bar.n = world;
     memcpy(m->alpha1, alpha1, m->g1a);
@@ -364,11 +363,9 @@ extern "C" int gg_groth16_mpk_create_ex(int curve, int log_n, const void* omega_
                 gg::set_last_error(ex.what());
                 return ex.code;
             }
-            if (hipStreamCreateWithFlags(&m->st[r], hipStreamNonBlocking) != hipSuccess) return GG_ERR_DEVICE;
             if (!m->dist) return 0;
             m->xst[r].assign(world, nullptr);
-            for (auto& x : m->xst[r])
-                if (hipStreamCreateWithFlags(&x, hipStreamNonBlocking) != hipSuccess) return GG_ERR_DEVICE;
+            for (auto& x : m->xst[r]) gg::create_copy_stream(&x);  // own queues: pushes never wait behind MSMs
             int rc = gg_hshard_create_ex(curve, log_n, omega_mont, coset_gen_mont, r, world, &m->hs[r]);
             if (rc) return rc;
             size_t mm = 0, xb = 0;
@@ -413,11 +410,9 @@ extern "C" int gg_groth16_mpk_create_ex(int curve, int log_n, const void* omega_
                                                zh - zl, kptr, kcnt, alpha1, beta1, delta1, B2 + pb[lo] * g2a, beta2,
                                                delta2, inf_A, inf_B, n_wires, nb_public, kix, lo, hi, &m->pk[r]);
         if (rc) return rc;
-        if (hipStreamCreateWithFlags(&m->st[r], hipStreamNonBlocking) != hipSuccess) return GG_ERR_DEVICE;
         if (!m->dist) return 0;
         m->xst[r].assign(world, nullptr);
-        for (auto& s : m->xst[r])
-            if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GG_ERR_DEVICE;
+        for (auto& x : m->xst[r]) gg::create_copy_stream(&x);  // own queues: pushes never wait behind MSMs
         rc = gg_hshard_create_ex(curve, log_n, omega_mont, coset_gen_mont, r, world, &m->hs[r]);
         if (rc) return rc;
         size_t mm = 0, xb = 0;

@@ -224,6 +224,14 @@ __device__ __forceinline__ uint4 chunk_ld(const uint32_t* sorted, uint32_t base4
     return *reinterpret_cast<const uint4*>(sorted + base4);
 }
 
+// dynamic LDS of k_accum_range<F>: the BN254 G2 gather slots (two 8-KB slots
+// per wave, four waves per block)
+#ifndef GG_ACCUM_R4LOOP
+#define GG_ACCUM_R4LOOP 0
+#endif
+template <class F>
+constexpr size_t kAccumLds = std::is_same<F, Fp2>::value && !GG_ACCUM_R4LOOP ? 4 * 2 * 8 * 64 * sizeof(uint4) : 0;
+
 template <class F>
 __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affine<F>* pts, const uint32_t* sorted,
                                                      const uint32_t* offsets, uint32_t nb, int c,
@@ -255,10 +263,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
         // 14 x 28 bits); the base holds x R' mod p, partials leave in radix form
         using C = typename RadixOf<F>::C;
         XyzzL<C> acc = inf_l<C>();
-        // The sorted entries come in 16-B chunks (four per load, the chunk of
-        // entry j loaded when j reaches it): each lane walks its own range, so
-        // one 4-B load per entry re-fetched a whole line whenever the point
-        // gathers had evicted it in between (traffic)
+#if GG_ACCUM_R4LOOP  // A/B build only: round 4's loop (entry chunks, conditional loads)
         uint4 ch = chunk_ld(sorted, (e0 + 1) & ~3u);
         uint32_t v = sorted[e0], vn = (e0 + 1 < e1) ? chunk_at(ch, (e0 + 1) & 3u) : 0u;
         Affine<F> p = ld(pts + (v & pmask));
@@ -280,6 +285,45 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                 seg0 = e;
                 do { q++; bnd = bnd2; bnd2 = offsets[min(q + 2, nb)]; } while (bnd == e);
             }
+#else
+        // Software pipeline, distance one: the gather of point e + 1 is issued
+        // before the add of point e and only waited for at the next step.  The
+        // VM counter is in order, so nothing the step needs may come from a
+        // load issued after that gather, and every load of the step is
+        // unconditional (a load under a branch left its value in a register
+        // the loop then copies -- a wait at the copy).  Round 4's version
+        // (16-B entry chunks loaded every fourth step, the boundary loaded
+        // inside the flush) waited for the fresh gather in every step: the
+        // gathers did not overlap the adds (traffic probe: 14.3 -> 11.6 ms per
+        // 2^24 launch with the points in L2).
+        const uint32_t elast = e1 - 1;
+        uint32_t v = sorted[e0], vn = sorted[min(e0 + 1, elast)];
+        Affine<F> p = ld(pts + (v & pmask));
+        for (uint32_t e = e0; e < e1; e++) {
+            Affine<F> qp = p;
+            const uint32_t cv = v;
+            // the last step re-gathers its own point (a valid index, unused)
+            const uint32_t nidx = (e + 1 < e1) ? vn : v;
+            p = ld(pts + (nidx & pmask));
+            v = nidx;
+            vn = sorted[min(e + 2, elast)];
+            if (e == bnd) {
+                range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
+                acc = inf_l<C>();
+                seg0 = e;
+                q++;
+                bnd = bnd2;  // offsets[q + 1], loaded in an earlier step
+                if (bnd == e) {  // a run of empty buckets: walk to the next boundary (rare)
+                    uint32_t b2;
+                    do {
+                        q++;
+                        b2 = offsets[min(q + 1, nb)];
+                    } while (b2 == e);
+                    bnd = b2;
+                }
+            }
+            bnd2 = offsets[min(q + 2, nb)];
+#endif
             if (skip_inf && qp.is_inf()) continue;
             const Fl<C> x = unpack_l<C>(qp.x);
             Fl<C> y = unpack_l<C>(qp.y);
@@ -290,9 +334,16 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
         return;
     }
     if constexpr (std::is_same<F, Fp2>::value) {
-        // BN254 G2: radix-2^29 Fp2 accumulator (field29.cuh), base in x * 2^261 form
+        // BN254 G2: radix-2^29 Fp2 accumulator (field29.cuh), base in x * 2^261 form.
+        // The 128-B points do not fit a register prefetch at two waves per SIMD
+        // (the adds use all 256 VGPRs), so the next point is gathered straight
+        // into LDS (global_load_lds_dwordx4, no VGPRs): two 8-KB slots per wave,
+        // [slot][16-B chunk][lane], the gather of point e + 1 issued after point
+        // e has been read out of its slot.  The flush (which reads a boundary
+        // loaded in an earlier step) comes before that gather: a use of an
+        // ordinary load's value while an LDS DMA is in flight waits for the DMA.
+#if GG_ACCUM_R4LOOP  // A/B build only: round 4's loop (no prefetch)
         Xyzz2_29 acc = inf2_29();
-        // 8-B chunks of entries (a 16-B chunk in registers spills at 2 waves)
         uint2 ch = *reinterpret_cast<const uint2*>(sorted + (e0 & ~1u));
         for (uint32_t e = e0; e < e1; e++) {
             if (e == bnd) {
@@ -302,12 +353,58 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                 do { q++; bnd = bnd2; bnd2 = offsets[min(q + 2, nb)]; } while (bnd == e);
             }
             if ((e & 1u) == 0 && e != e0) ch = *reinterpret_cast<const uint2*>(sorted + e);
-            const uint32_t v = (e & 1u) ? ch.y : ch.x;
-            const Affine<F> pt = ld(pts + (v & pmask));
+            const uint32_t cv = (e & 1u) ? ch.y : ch.x;
+            const Affine<F> pt = ld(pts + (cv & pmask));
+#else
+        extern __shared__ uint4 g2_lds[];
+        const uint32_t lane = threadIdx.x & 63u;
+        uint4* wb = g2_lds + (threadIdx.x >> 6) * (2u * 8u * 64u);
+        auto gather = [&](uint32_t idx, uint32_t slot) {
+            const char* src = reinterpret_cast<const char*>(pts + (idx & pmask));
+#pragma unroll
+            for (int k = 0; k < 8; k++)
+                __builtin_amdgcn_global_load_lds((const void*)(src + 16 * k),
+                                                 (__attribute__((address_space(3))) void*)(wb + (slot * 8u + k) * 64u),
+                                                 16, 0, 0);
+        };
+        Xyzz2_29 acc = inf2_29();
+        const uint32_t elast = e1 - 1;
+        uint32_t v = sorted[e0], vn = sorted[min(e0 + 1, elast)];
+        gather(v, 0);
+        for (uint32_t e = e0; e < e1; e++) {
+            const uint32_t s = (e - e0) & 1u;
+            Affine<F> pt;
+            {
+                uint4* d = reinterpret_cast<uint4*>(&pt);
+#pragma unroll
+                for (int k = 0; k < 8; k++) d[k] = wb[(s * 8u + k) * 64u + lane];
+            }
+            const uint32_t cv = v;
+            if (e == bnd) {
+                range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
+                acc = inf2_29();
+                seg0 = e;
+                q++;
+                bnd = bnd2;  // offsets[q + 1], loaded in an earlier step
+                if (bnd == e) {  // a run of empty buckets (rare)
+                    uint32_t b2;
+                    do {
+                        q++;
+                        b2 = offsets[min(q + 1, nb)];
+                    } while (b2 == e);
+                    bnd = b2;
+                }
+            }
+            const uint32_t nidx = (e + 1 < e1) ? vn : v;  // the last step re-gathers its own point
+            gather(nidx, s ^ 1u);
+            v = nidx;
+            vn = sorted[min(e + 2, elast)];
+            bnd2 = offsets[min(q + 2, nb)];
+#endif
             if (skip_inf && pt.is_inf()) continue;
             const Fp2_29 x{unpack29(pt.x.a0), unpack29(pt.x.a1)};
             Fp2_29 y{unpack29(pt.y.a0), unpack29(pt.y.a1)};
-            if (v >> 31) y = Fp2_29{sub<2>(Fp29{}, y.c0), sub<2>(Fp29{}, y.c1)};  // 2p - y
+            if (cv >> 31) y = Fp2_29{sub<2>(Fp29{}, y.c0), sub<2>(Fp29{}, y.c1)};  // 2p - y
             xyzz2_29_madd(acc, x, y);
         }
         range_store(acc, seg0 == e0, true, q, c, t, head, tail, S);
@@ -1059,7 +1156,7 @@ inline uint32_t range_length(size_t E) {
         int blocks = 0, cus = 0, dev = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_accum_range<F>, 256, 0) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_accum_range<F>, 256, kAccumLds<F>) != hipSuccess ||
             blocks < 1 || cus < 1) {
             (void)hipGetLastError();
             return 256.0 * 256 * 2;
@@ -1123,7 +1220,8 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
             pmask = 1023u;
             while (pmask && pmask >= n) pmask >>= 1;  // stay inside the base
         }
-        hipLaunchKernelGGL(k_accum_range<F>, dim3(grid_for(T, 256)), dim3(256), 0, st, (const Affine<F>*)b->pts.p,
+        hipLaunchKernelGGL(k_accum_range<F>, dim3(grid_for(T, 256)), dim3(256), kAccumLds<F>, st,
+                           (const Affine<F>*)b->pts.p,
                            s->sorted.as<uint32_t>(), offs, (uint32_t)nb, ce, K, (int)b->has_inf, hP, tP, SP,
                            scr->tbucket.as<uint32_t>(), pmask);
         GG_HIP(hipGetLastError());

@@ -1192,7 +1192,6 @@ gg_hshard* hshard_create(int curve, int log_n, const void* omega_mont, const voi
         hs->bls.reset(new HShardT<FrBlsCfg>());
         hshard_build(hs.get(), hs->bls.get(), omega_mont, coset_gen_mont);
     }
-    GG_HIP(hipStreamCreateWithFlags(&hs->st, hipStreamNonBlocking));
     return hs.release();
 }
 

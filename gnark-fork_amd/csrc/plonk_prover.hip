@@ -934,7 +934,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
                 p->d0 = dom(log_n, pk->omega, pk->u);
                 p->creg.alloc(nb);
                 p->xs.resize(pk->peers.size() + 2);
-                for (hipStream_t& x : p->xs) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+                for (hipStream_t& x : p->xs) gg::create_copy_stream(&x);  // pushes: own hardware queues
                 GG_HIP(hipEventCreateWithFlags(&p->reg_ev, hipEventDisableTiming));
                 GG_HIP(hipStreamCreateWithFlags(&p->cs, hipStreamNonBlocking));
             }

@@ -16,10 +16,10 @@ Stager::Stager(int device) : device_(device) {
             GG_HIP(hipEventCreateWithFlags(&ev_[t][b], hipEventDisableTiming));
         }
         GG_HIP(hipEventCreateWithFlags(&end_[t], hipEventDisableTiming));
-        // one DMA stream shared by the copy threads (GG_STAGE_STREAMS=1, default):
-        // every extra stream takes a HIP hardware queue (GPU_MAX_HW_QUEUES, 4 by
-        // default), and a copy queued behind a long MSM kernel waits for it
-        if (t < nst_) GG_HIP(hipStreamCreateWithFlags(&st_[t], hipStreamNonBlocking));
+        // one DMA stream shared by the copy threads (GG_STAGE_STREAMS=1, default),
+        // of the greatest priority: its own hardware queue, so the H2D copies
+        // never queue behind an MSM kernel of the prove's streams (common.h)
+        if (t < nst_) create_copy_stream(&st_[t]);
         else st_[t] = st_[t % nst_];
     }
 }

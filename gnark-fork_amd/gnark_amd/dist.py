@@ -42,3 +42,33 @@ def allgather_partial(group: int, jac: bytes, device=None) -> bytes:
     parts = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(parts, t)
     return combine_partials(group, [bytes(p.cpu().numpy()) for p in parts])
+
+
+def group_devices(local_device: int, device=None) -> list:
+    """The GPU id of every rank of the process group, in rank order (all-gather)."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return [int(local_device)]
+    t = torch.tensor([int(local_device)], dtype=torch.int64)
+    if device is not None:
+        t = t.to(device)
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    return [int(p.item()) for p in parts]
+
+
+def broadcast_bytes(data, nbytes: int, src: int = 0, device=None) -> bytes:
+    """`data` (nbytes, significant on rank `src`) on every rank."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return bytes(data)
+    if dist.get_rank() == src:
+        t = torch.frombuffer(bytearray(data), dtype=torch.uint8)
+    else:
+        t = torch.zeros(nbytes, dtype=torch.uint8)
+    if device is not None:
+        t = t.to(device)
+    dist.broadcast(t, src)
+    return bytes(t.cpu().numpy())

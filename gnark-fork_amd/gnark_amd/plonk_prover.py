@@ -326,3 +326,62 @@ def prove(pk: ProvingKey, L, R_, O, rng=None, timings: Optional[dict] = None, pu
             prev = ms[k]
         timings["total"] = prev
     return Proof.parse(bytes(out), pk.n_cmt, pk.curve)
+
+
+class GroupProvingKey:
+    """PlonK under a process-per-GPU launch (torch.distributed.run, one rank per
+    GPU; SURVEY 8(e), BASELINE configs[4] "8 x MI355X").
+
+    Rank 0 ("leader") holds a one-process multi-part key whose device parts are
+    the GPUs of all ranks, in rank order (gg_plonk_pk_create_ex with devices =
+    every rank's device): its proof runs the whole device-part split -- KZG
+    shares, quotient units, ratio slices, canonical forms -- with
+    the cross-part hand-offs as in-library peer copies over xGMI, exactly as a
+    one-process (Go) caller's key does.  The other ranks hold no PlonK state;
+    they take part in the process group's collectives (the device all-gather
+    here, the proof broadcast in prove_group).  Why not a callback per hand-off
+    (as gg_hshard does for Groth16's three all-to-alls): a PlonK proof has ~20
+    dependent cross-part hand-offs (Z slices to the Z owner, canonical forms to
+    every unit, unit blocks back, scalar slices ahead of each MSM stage), each a
+    device-to-device copy ordered by HIP events; a host round trip through a
+    collective per hand-off would serialise what the event graph overlaps.
+
+    `key_args` / `key_kw`: the ProvingKey arguments (significant on rank 0 only;
+    other ranks may pass None for the buffers).  local_device: this rank's GPU."""
+
+    def __init__(self, *key_args, local_device: int = 0, comm_device=None, **key_kw):
+        import torch.distributed as dist
+        from . import dist as gdist
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.devices = gdist.group_devices(local_device, comm_device)
+        self.comm_device = comm_device
+        self.pk = ProvingKey(*key_args, devices=self.devices, **key_kw) if self.rank == 0 else None
+        curve = key_kw.get("curve", "bls12-381")
+        self.curve = curve
+        self.n_cmt = len(key_kw.get("qcp", ()))
+
+    def close(self):
+        if self.pk is not None:
+            self.pk.close()
+            self.pk = None
+
+
+def prove_group(gpk: GroupProvingKey, L, R_, O, **kw) -> Proof:
+    """prove() on the leader's multi-part key; every rank returns the proof
+    (broadcast from rank 0).  Inputs and options are significant on rank 0."""
+    from . import dist as gdist
+    size = lib.gg_plonk_proof_size_ex(_Field(gpk.curve).cid, gpk.n_cmt)
+    raw = None
+    if gpk.rank == 0:
+        pr = prove(gpk.pk, L, R_, O, **kw)
+        raw = proof_bytes(pr, gpk.curve)
+    raw = gdist.broadcast_bytes(raw if raw is not None else bytes(size), size, 0, gpk.comm_device)
+    return Proof.parse(raw, gpk.n_cmt, gpk.curve)
+
+
+def proof_bytes(pr: Proof, curve: str = "bls12-381") -> bytes:
+    """the library's proof layout (Proof.parse's inverse)"""
+    F = _Field(curve)
+    return b"".join(pr.LRO + [pr.Z] + pr.H + pr.bsb22 + [pr.batched_H] +
+                    [F.mont(v) for v in pr.claimed_values] + [pr.z_shifted_H, F.mont(pr.z_shifted_value)])
+
