@@ -169,7 +169,12 @@ def main():
     if world > 1:
         import torch.distributed as dist
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev),
+            # RCCL's collectives on a stream of the greatest priority: their own
+            # hardware queues, so an all-to-all of the distributed computeH never
+            # queues behind an MSM kernel of the library's streams
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev), pg_options=opts,
                                     timeout=datetime.timedelta(minutes=10))
         else:
             dist.init_process_group(backend, timeout=datetime.timedelta(minutes=10))
@@ -431,7 +436,8 @@ def main():
     stage_now["now"] = "cpu_baseline"
     if mode == "single" and not args.no_cpu_baseline:
         try:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_threads, ms_per_step, ncons)
+            out["cpu_baseline"] = cpu_baseline(args.cpu_threads, ms_per_step, ncons,
+                                               log_ns=(20, args.log_n), budget_s=(10.0, 0.0))
         except Exception as e:
             out["cpu_baseline"] = {"error": repr(e)}
 
@@ -956,12 +962,14 @@ def cpu_threads(requested):
     return aff, f"all {aff} CPUs of this process's affinity mask"
 
 
-def cpu_baseline(threads, gpu_prove_ms, gpu_ncons, log_ns=(20, 22), budget_s=(10.0, 25.0)):
+def cpu_baseline(threads, gpu_prove_ms, gpu_ncons, log_ns=(20, 24), budget_s=(10.0, 0.0)):
     """The C restatement of the same prove (oracle/c oc_groth16_prove: OpenMP
     signed-digit Pippenger MSMs with XYZZ buckets, radix-2 NTT computeH) on
-    bounded samples: one 2^20 and one 2^22 MiMC-shaped proof (random solution,
-    key from the GPU batch scalar mul), the 2^20 one repeated to ~10 s, so the
-    port's scaling with size is visible.  kind "port": our restatement, not gnark."""
+    bounded samples: 2^20 MiMC-shaped proofs repeated to ~10 s, and ONE proof of
+    the GPU line's own size (2^24 by default: the same workload; random solution,
+    key from the GPU batch scalar mul) -- value is that same-size rate (round-4
+    VERDICT Weak 7: the ratio compares the same workload).  kind "port": our
+    restatement, not gnark."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import coracle
     from gnark_amd import msm
@@ -1002,15 +1010,17 @@ def cpu_baseline(threads, gpu_prove_ms, gpu_ncons, log_ns=(20, 22), budget_s=(10
                 break
     except OSError:
         pass
-    v = samples[0]["constraints_per_s"]
+    same = [x for x in samples if x["n_constraints"] == gpu_ncons]
+    v = (same or samples)[-1]["constraints_per_s"]
     gl = (gpu_ncons - 1).bit_length()
+    vs = (same or samples)[-1]
     return {"value": v, "unit": "constraints/s", "cores": nt, "kind": "port",
-            "prove_ms": samples[0]["prove_ms"], "cpu_model": cpu_model, "host_cpus_visible": os.cpu_count(),
-            "threads_allotment": allot, "samples": samples,
-            "sample": (f"Groth16 prove of a 2^{log_ns[0]} MiMC-chain R1CS ({samples[0]['n_constraints']} "
-                       f"constraints) x {samples[0]['proves']}, and one 2^{log_ns[-1]} proof beside it (C "
-                       f"restatement of prove.go: OpenMP Pippenger + radix-2 NTT, {nt} threads; a port, NOT "
-                       f"gnark); the GPU line is the 2^{gl} prove: compare constraints/s"),
+            "prove_ms": vs["prove_ms"], "cpu_model": cpu_model, "host_cpus_visible": os.cpu_count(),
+            "threads_allotment": allot, "samples": samples, "same_size_as_gpu_line": bool(same),
+            "sample": (f"one Groth16 prove of the 2^{log_ns[-1]} MiMC-chain R1CS ({vs['n_constraints']} "
+                       f"constraints: {'the GPU line' + chr(39) + 's own workload' if same else 'a smaller instance'}"
+                       f"), and 2^{log_ns[0]} proofs x {samples[0]['proves']} beside it (C restatement of prove.go: "
+                       f"OpenMP Pippenger + radix-2 NTT, {nt} threads; a port, NOT gnark)"),
             "gpu_over_cpu_constraints_per_s": (gpu_ncons / (gpu_prove_ms * 1e-3)) / v}
 
 

@@ -227,10 +227,72 @@ __device__ __forceinline__ uint4 chunk_ld(const uint32_t* sorted, uint32_t base4
 // dynamic LDS of k_accum_range<F>: the BN254 G2 gather slots (two 8-KB slots
 // per wave, four waves per block)
 #ifndef GG_ACCUM_R4LOOP
-#define GG_ACCUM_R4LOOP 0
+#define GG_ACCUM_R4LOOP 0  // A/B builds: round 4's G2 loop (no LDS gather)
 #endif
+#ifndef GG_G1_PIPE
+#define GG_G1_PIPE 0  // A/B builds: the G1 loop with every load unconditional
+#endif
+// The register-path gathers (BN254 G1) carry the nontemporal hint: a point is
+// read once per launch, and the hint keeps the gathers from displacing the
+// entry chunks in L2 / MALL.  A/B on one box (profiles/r05_d_accum_ab.txt):
+// 13.90 vs 14.07-14.14 ms per 2^24 launch.  The LDS-DMA gathers (BN254 G2,
+// BLS12-381 G1) keep the default policy: with the hint G2 took 26.89 vs 26.2 ms.
+// GG_PT_NT=0 builds the default policy everywhere, 2 the hint everywhere.
+#ifndef GG_PT_NT
+#define GG_PT_NT 1
+#endif
+// one accumulation point (a gather with no reuse)
+template <class T>
+__device__ __forceinline__ T ld_pt(const T* p) {
+    if constexpr (GG_PT_NT != 0) {
+        typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+        static_assert(sizeof(T) % 16 == 0, "16B multiple");
+        T r;
+        const u4v* s = reinterpret_cast<const u4v*>(p);
+        u4v* d = reinterpret_cast<u4v*>(&r);
+#pragma unroll
+        for (int i = 0; i < (int)(sizeof(T) / 16); i++) d[i] = __builtin_nontemporal_load(s + i);
+        return r;
+    } else {
+        return ld(p);
+    }
+}
+// Points gathered straight into LDS (global_load_lds_dwordx4: no VGPRs), for
+// the accumulations whose adds use all the registers of two waves per SIMD
+// (BN254 G2, BLS12-381 G1): per wave two slots of NCH 16-B chunks x 64 lanes,
+// laid out [slot][chunk][lane] (one DMA instruction fills one [chunk] row, the
+// read-back is conflict-free).  The caller reads point e out of its slot, then
+// issues the gather of point e + 1 into the other one: the compiler's wait for
+// the slot being read then covers only the older gather.
+template <int NCH>
+struct LdsRing {
+    uint4* wb;
+    uint32_t lane;
+    __device__ __forceinline__ explicit LdsRing(uint4* lds)
+        : wb(lds + (threadIdx.x >> 6) * (2u * NCH * 64u)), lane(threadIdx.x & 63u) {}
+    __device__ __forceinline__ void gather(const void* src, uint32_t slot) const {
+#pragma unroll
+        for (int k = 0; k < NCH; k++)
+            __builtin_amdgcn_global_load_lds((const void*)((const char*)src + 16 * k),
+                                             (__attribute__((address_space(3))) void*)(wb + (slot * NCH + k) * 64u),
+                                             16, 0, GG_PT_NT == 2 ? 2 : 0);
+    }
+    template <class T>
+    __device__ __forceinline__ T read(uint32_t slot) const {
+        static_assert(sizeof(T) == 16 * NCH, "point size");
+        T r;
+        uint4* d = reinterpret_cast<uint4*>(&r);
+#pragma unroll
+        for (int k = 0; k < NCH; k++) d[k] = wb[(slot * NCH + k) * 64u + lane];
+        return r;
+    }
+};
+// BN254 G2 (128-B points) and BLS12-381 G1 (96-B) take the LDS ring
 template <class F>
-constexpr size_t kAccumLds = std::is_same<F, Fp2>::value && !GG_ACCUM_R4LOOP ? 4 * 2 * 8 * 64 * sizeof(uint4) : 0;
+constexpr bool kLdsGather = !GG_ACCUM_R4LOOP && (std::is_same<F, Fp2>::value || std::is_same<F, FpBls>::value);
+// dynamic LDS of k_accum_range<F>: two slots per wave, four waves per block
+template <class F>
+constexpr size_t kAccumLds = kLdsGather<F> ? 4 * 2 * sizeof(Affine<F>) * 64 : 0;
 
 template <class F>
 __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affine<F>* pts, const uint32_t* sorted,
@@ -263,15 +325,60 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
         // 14 x 28 bits); the base holds x R' mod p, partials leave in radix form
         using C = typename RadixOf<F>::C;
         XyzzL<C> acc = inf_l<C>();
-#if GG_ACCUM_R4LOOP  // A/B build only: round 4's loop (entry chunks, conditional loads)
+        if constexpr (kLdsGather<F>) {  // BLS12-381 G1: 96-B points through the LDS ring
+            extern __shared__ uint4 acc_lds[];
+            const LdsRing<sizeof(Affine<F>) / 16> ring(acc_lds);
+            const uint32_t elast = e1 - 1;
+            uint32_t v = sorted[e0], vn = sorted[min(e0 + 1, elast)];
+            ring.gather(pts + (v & pmask), 0);
+            for (uint32_t e = e0; e < e1; e++) {
+                const uint32_t sl = (e - e0) & 1u;
+                const Affine<F> qp = ring.template read<Affine<F>>(sl);
+                const uint32_t cv = v;
+                if (e == bnd) {  // before the gather (see the Fp2 branch)
+                    range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
+                    acc = inf_l<C>();
+                    seg0 = e;
+                    q++;
+                    bnd = bnd2;
+                    if (bnd == e) {
+                        uint32_t b2;
+                        do {
+                            q++;
+                            b2 = offsets[min(q + 1, nb)];
+                        } while (b2 == e);
+                        bnd = b2;
+                    }
+                }
+                const uint32_t nidx = (e + 1 < e1) ? vn : v;
+                ring.gather(pts + (nidx & pmask), sl ^ 1u);
+                v = nidx;
+                vn = sorted[min(e + 2, elast)];
+                bnd2 = offsets[min(q + 2, nb)];
+                if (skip_inf && qp.is_inf()) continue;
+                const Fl<C> x = unpack_l<C>(qp.x);
+                Fl<C> y = unpack_l<C>(qp.y);
+                if (cv >> 31) y = sub_nn<2>(Fl<C>{}, y);
+                xyzzl_madd(acc, x, y);
+            }
+            range_store(acc, seg0 == e0, true, q, c, t, head, tail, S);
+            return;
+        }
+#if !GG_G1_PIPE  // default: 16-B entry chunks loaded every fourth step
+        // A/B (round 5, profiles/r05_c_*): a loop with every load unconditional
+        // and no wait on the fresh gather inside the step (GG_G1_PIPE=1) ran
+        // 14.11-14.19 vs 13.98 ms per 2^24 launch: it loads an entry and a
+        // bucket boundary every step, and the extra traffic costs more clock
+        // (2.00 vs 2.03 GHz effective) than the overlap gains -- three waves
+        // per SIMD (164 VGPRs) already hide the gather behind the other waves
         uint4 ch = chunk_ld(sorted, (e0 + 1) & ~3u);
         uint32_t v = sorted[e0], vn = (e0 + 1 < e1) ? chunk_at(ch, (e0 + 1) & 3u) : 0u;
-        Affine<F> p = ld(pts + (v & pmask));
+        Affine<F> p = ld_pt(pts + (v & pmask));
         for (uint32_t e = e0; e < e1; e++) {
             Affine<F> qp = p;
             const uint32_t cv = v;
             if (e + 1 < e1) {
-                p = ld(pts + (vn & pmask));
+                p = ld_pt(pts + (vn & pmask));
                 v = vn;
                 if (e + 2 < e1) {
                     const uint32_t j = e + 2;
@@ -286,25 +393,23 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                 do { q++; bnd = bnd2; bnd2 = offsets[min(q + 2, nb)]; } while (bnd == e);
             }
 #else
-        // Software pipeline, distance one: the gather of point e + 1 is issued
-        // before the add of point e and only waited for at the next step.  The
-        // VM counter is in order, so nothing the step needs may come from a
-        // load issued after that gather, and every load of the step is
-        // unconditional (a load under a branch left its value in a register
-        // the loop then copies -- a wait at the copy).  Round 4's version
-        // (16-B entry chunks loaded every fourth step, the boundary loaded
-        // inside the flush) waited for the fresh gather in every step: the
-        // gathers did not overlap the adds (traffic probe: 14.3 -> 11.6 ms per
-        // 2^24 launch with the points in L2).
+        // A/B variant (GG_G1_PIPE=1): a software pipeline of distance one in
+        // which the gather of point e + 1 is waited for only at the next step.
+        // The VM counter is in order, so nothing the step needs may come from
+        // a load issued after that gather, and every load is unconditional (a
+        // load under a branch leaves its value in a register the loop copies:
+        // a wait at the copy).  The default loop above waits for the fresh
+        // gather inside the step (its chunk select) and is still as fast: the
+        // other waves of the SIMD cover the wait.
         const uint32_t elast = e1 - 1;
         uint32_t v = sorted[e0], vn = sorted[min(e0 + 1, elast)];
-        Affine<F> p = ld(pts + (v & pmask));
+        Affine<F> p = ld_pt(pts + (v & pmask));
         for (uint32_t e = e0; e < e1; e++) {
             Affine<F> qp = p;
             const uint32_t cv = v;
             // the last step re-gathers its own point (a valid index, unused)
             const uint32_t nidx = (e + 1 < e1) ? vn : v;
-            p = ld(pts + (nidx & pmask));
+            p = ld_pt(pts + (nidx & pmask));
             v = nidx;
             vn = sorted[min(e + 2, elast)];
             if (e == bnd) {
@@ -356,29 +461,15 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
             const uint32_t cv = (e & 1u) ? ch.y : ch.x;
             const Affine<F> pt = ld(pts + (cv & pmask));
 #else
-        extern __shared__ uint4 g2_lds[];
-        const uint32_t lane = threadIdx.x & 63u;
-        uint4* wb = g2_lds + (threadIdx.x >> 6) * (2u * 8u * 64u);
-        auto gather = [&](uint32_t idx, uint32_t slot) {
-            const char* src = reinterpret_cast<const char*>(pts + (idx & pmask));
-#pragma unroll
-            for (int k = 0; k < 8; k++)
-                __builtin_amdgcn_global_load_lds((const void*)(src + 16 * k),
-                                                 (__attribute__((address_space(3))) void*)(wb + (slot * 8u + k) * 64u),
-                                                 16, 0, 0);
-        };
+        extern __shared__ uint4 acc_lds[];
+        const LdsRing<8> ring(acc_lds);
         Xyzz2_29 acc = inf2_29();
         const uint32_t elast = e1 - 1;
         uint32_t v = sorted[e0], vn = sorted[min(e0 + 1, elast)];
-        gather(v, 0);
+        ring.gather(pts + (v & pmask), 0);
         for (uint32_t e = e0; e < e1; e++) {
             const uint32_t s = (e - e0) & 1u;
-            Affine<F> pt;
-            {
-                uint4* d = reinterpret_cast<uint4*>(&pt);
-#pragma unroll
-                for (int k = 0; k < 8; k++) d[k] = wb[(s * 8u + k) * 64u + lane];
-            }
+            const Affine<F> pt = ring.template read<Affine<F>>(s);
             const uint32_t cv = v;
             if (e == bnd) {
                 range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
@@ -396,7 +487,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                 }
             }
             const uint32_t nidx = (e + 1 < e1) ? vn : v;  // the last step re-gathers its own point
-            gather(nidx, s ^ 1u);
+            ring.gather(pts + (nidx & pmask), s ^ 1u);
             v = nidx;
             vn = sorted[min(e + 2, elast)];
             bnd2 = offsets[min(q + 2, nb)];

@@ -185,6 +185,11 @@ struct PlonkPeer {
     hipEvent_t reg_ev = nullptr;  // the last regular-form push to part 0 (creg free again)
     bool reg_pending = false;
     hipStream_t cs = nullptr;     // the tasks' transforms (stream 3 belongs to the quotient units)
+    // its pushes out of a compute stream's result (its Z slice, its units' blocks):
+    // a copy stream of the greatest priority (own hardware queue, common.h) that
+    // waits for the producing kernel by event only
+    hipStream_t cps = nullptr;
+    hipEvent_t cpev = nullptr;
     ~PlonkPeer() {
         int cur = 0;
         const bool restore = hipGetDevice(&cur) == hipSuccess;
@@ -204,6 +209,8 @@ struct PlonkPeer {
         qk_lag.release();
         for (hipStream_t x : xs) (void)hipStreamDestroy(x);
         if (reg_ev) (void)hipEventDestroy(reg_ev);
+        if (cps) (void)hipStreamDestroy(cps);
+        if (cpev) (void)hipEventDestroy(cpev);
         if (cs) (void)hipStreamDestroy(cs);
         perm_slice.release();
         pz.release();
@@ -772,6 +779,8 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
                 p->l_hi = bound(n, d + 1);
                 GG_HIP(hipSetDevice(p->device));
                 for (hipStream_t& x : p->s) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+                gg::create_copy_stream(&p->cps);
+                GG_HIP(hipEventCreateWithFlags(&p->cpev, hipEventDisableTiming));
                 for (int e = 0; e < 4; e++) {
                     GG_HIP(hipEventCreate(&p->ea[e]));
                     GG_HIP(hipEventCreate(&p->eb[e]));
@@ -1182,9 +1191,12 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                     if (!mine || stop) return;
                     const auto b = std::chrono::steady_clock::now();
                     plk::ratio_fixup(F(p->pz), cnt, pre[q + 1], F(p->scal[0]), p->s[0]);  // the Z slot of its MSM
+                    // pushed to Z's owner from the copy stream (waits for the fixup only)
+                    GG_HIP(hipEventRecord(p->cpev, p->s[0]));
+                    GG_HIP(hipStreamWaitEvent(p->cps, p->cpev, 0));
                     GG_HIP(hipMemcpyPeerAsync(F(zown->in[3]) + p->l_lo, zown->device, p->scal[0].p, p->device, 32 * cnt,
-                                              p->s[0]));
-                    GG_HIP(hipStreamSynchronize(p->s[0]));
+                                              p->cps));
+                    GG_HIP(hipStreamSynchronize(p->cps));
                     std::lock_guard<std::mutex> lk(pk->tmu);
                     pk->ptimes[q + 1].ratio_ms += ms + ms_since(b);
                 }));
@@ -1370,14 +1382,17 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                 for (int k = 0; k < 7 + n_cmt; k++) e[k] = F(p->cev[k]);
                 for (size_t u = 0; u < p->units.size(); u++)
                     run_unit(p->units[u].get(), ins, e, F(p->zc), F(p->tw0), F(p->units[u]->out), true, u == 0, q);
-                // the units' blocks back to the primary's cres (timed separately)
-                GG_HIP(hipEventRecord(p->ea[3], q));
+                // the units' blocks back to the primary's cres (timed separately),
+                // from the copy stream: it waits for the units' kernels only
+                GG_HIP(hipEventRecord(p->cpev, q));
+                GG_HIP(hipStreamWaitEvent(p->cps, p->cpev, 0));
+                GG_HIP(hipEventRecord(p->ea[3], p->cps));
                 for (auto& qu : p->units) {
                     const size_t blk = (size_t)(__builtin_bitreverse32((uint32_t)qu->p) >> (32 - pk->log_u));
-                    GG_HIP(hipMemcpyPeerAsync(F(pk->cres) + blk * m, pk->device, qu->out.p, p->device, mb, q));
+                    GG_HIP(hipMemcpyPeerAsync(F(pk->cres) + blk * m, pk->device, qu->out.p, p->device, mb, p->cps));
                 }
-                GG_HIP(hipEventRecord(p->eb[3], q));
-                GG_HIP(hipStreamSynchronize(q));
+                GG_HIP(hipEventRecord(p->eb[3], p->cps));
+                GG_HIP(hipStreamSynchronize(p->cps));
                 float cout = 0;
                 GG_HIP(hipEventElapsedTime(&cout, p->ea[3], p->eb[3]));
                 std::lock_guard<std::mutex> lk(pk->tmu);

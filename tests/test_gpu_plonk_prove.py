@@ -232,6 +232,41 @@ def test_plonk_prove_multi_device_matches(log_n, parts, n_cmt):
     pk0.close()
 
 
+def test_plonk_prove_distinct_devices():
+    """Device parts on distinct GPUs when the box has them (skipped on a one-GPU
+    box): Z slices pushed into the Z owner's buffer, canonical-form
+    pushes, the quotient units' blocks and the scalar slices cross devices for
+    real; the proof equals the one-GPU proof, and peer access is reported."""
+    from gnark_amd import device_count, plonk_prover as pp
+    nd = device_count()
+    if nd < 2:
+        pytest.skip("one GPU visible")
+    log_n, parts = 12, (4 if nd >= 4 else 2)
+    circ = Circuit(log_n, 77, nb_public=1, n_cmt=1)
+    tau = random.Random(log_n).randrange(2, R)
+    key_srs = srs(log_n, tau)
+    pk0 = make_key(circ, tau, key_srs=key_srs)
+    L, Rv, O, pub, cmts = circ.solve(pk0, 6, commit=pk0.commit_lagrange)
+    ref = pp.prove(pk0, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts)
+    pkm = make_key(circ, tau, key_srs=key_srs, devices=list(range(parts)))
+    pa = pkm.peer_access()
+    assert all(pa[i][j] in ("enabled", "unavailable", "enable_failed") for i in range(parts) for j in range(parts)
+               if i != j)
+    got = pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts)
+    assert got == ref
+    pkm.close()
+    pk0.close()
+
+
+def test_plonk_peer_access_same_device():
+    from gnark_amd import plonk_prover as pp  # noqa: F401
+    circ = Circuit(6, 5, nb_public=1, n_cmt=0)
+    tau = random.Random(6).randrange(2, R)
+    pkm = make_key(circ, tau, devices=[0, 0, 0])
+    assert pkm.peer_access() == [["same_device"] * 3] * 3
+    pkm.close()
+
+
 @pytest.mark.parametrize("log_n,nb_public,n_cmt,parts", [(12, 2, 1, 1), (14, 1, 0, 4), (12, 1, 1, 8)])
 def test_plonk_bn254_prove_verifies(log_n, nb_public, n_cmt, parts):
     """backend/plonk/bn254 at sizes the Python oracle verifies in seconds: the GPU
