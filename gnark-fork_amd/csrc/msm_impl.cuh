@@ -211,10 +211,14 @@ __device__ __forceinline__ void range_store(const P& acc, bool first, bool last,
 #ifndef GG_G1_WAVES
 #define GG_G1_WAVES 2
 #endif
+#ifndef GG_BLS_WAVES
+#define GG_BLS_WAVES 2
+#endif
 template <class F>
 constexpr int kAccumWaves = (GG_G2_WAVES1 && std::is_same<F, Fp2>::value) || std::is_same<F, Fp2Bls>::value
                                 ? 1
-                                : (std::is_same<F, Fp>::value ? GG_G1_WAVES : 2);
+                                : (std::is_same<F, Fp>::value ? GG_G1_WAVES
+                                                              : (std::is_same<F, FpBls>::value ? GG_BLS_WAVES : 2));
 
 // entry k (0..3) of a 16-B chunk of sorted entries held in registers
 __device__ __forceinline__ uint32_t chunk_at(const uint4& c, uint32_t k) {

@@ -719,20 +719,24 @@ class TorchExchange:
         self.recv = torch.empty(nbytes, dtype=torch.uint8, device=self.dev)
         self.gloo = tdist.get_backend() != "nccl"
         self.world = tdist.get_world_size()
+        # the collective is joined on a stream of the greatest priority: its
+        # own hardware queue, so the host's wait for it never sits behind an MSM
+        # kernel of the library's streams on a shared queue
+        self.stream = torch.cuda.Stream(device=self.dev, priority=-1)
 
     def __call__(self, s_ptr, r_ptr, nbytes):
         import torch
         import torch.distributed as tdist
         total = nbytes * self.world
         s, r = self.send[:total], self.recv[:total]
-        with torch.cuda.device(self.dev):
+        with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
             if self.gloo:
                 rc = torch.empty(total, dtype=torch.uint8)
                 tdist.all_to_all_single(rc, s.cpu())
                 r.copy_(rc)
             else:
                 tdist.all_to_all_single(r, s)
-            torch.cuda.current_stream(self.dev).synchronize()
+            self.stream.synchronize()
 
 
 def prove_distributed_h(pk: ProvingKeyShard, hs: HShard, xchg: TorchExchange, solution: Solution,

@@ -157,8 +157,10 @@ def test_plonk_prove_sharded_kzg_matches(world):
 
 @pytest.mark.parametrize("curve,log_n,nb_public,n_cmt", [
     ("bls12-381", 3, 0, 0), ("bls12-381", 4, 1, 0), ("bls12-381", 5, 2, 1), ("bls12-381", 6, 0, 2),
-    ("bls12-381", 7, 3, 1), ("bls12-381", 8, 2, 2),
-    ("bn254", 3, 0, 0), ("bn254", 4, 1, 0), ("bn254", 5, 2, 1), ("bn254", 6, 0, 2), ("bn254", 8, 2, 2)])
+    ("bls12-381", 7, 3, 1), ("bls12-381", 8, 2, 2), ("bls12-381", 10, 2, 1), ("bls12-381", 12, 1, 2),
+    ("bls12-381", 14, 1, 1),
+    ("bn254", 3, 0, 0), ("bn254", 4, 1, 0), ("bn254", 5, 2, 1), ("bn254", 6, 0, 2), ("bn254", 8, 2, 2),
+    ("bn254", 10, 1, 1), ("bn254", 12, 2, 1)])
 def test_plonk_proof_bytes_match_oracle_prover(curve, log_n, nb_public, n_cmt):
     """Byte-exact PlonK on both curves (backend/plonk/bls12-381 and
     backend/plonk/bn254): the GPU proof equals the oracle's restatement of
@@ -184,6 +186,10 @@ def test_plonk_proof_bytes_match_oracle_prover(curve, log_n, nb_public, n_cmt):
     for v, d, _ in cmts:  # bsb22Hint's kzg.Commit on the GPU == the oracle's
         assert g(d) == po.commit_lagrange(key, ints(v, F))
     got = pp.prove(pk, L, Rv, O, rng=random.Random(5), public=pub, commitments=cmts)
+    if log_n >= 12:  # the split-iDFT quotient path (2^14+ big domains) through 4 device parts, same bytes
+        pkm = make_key(circ, tau, devices=[0] * 4)
+        assert pp.prove(pkm, L, Rv, O, rng=random.Random(5), public=pub, commitments=cmts) == got
+        pkm.close()
     want = po.prove(key, ints(L, F), ints(Rv, F), ints(O, F), pub, [(ints(v, F), g(d), h) for v, d, h in cmts],
                     blinding(5, F.R))
     assert po.verify_trapdoor(key, want, pub)
