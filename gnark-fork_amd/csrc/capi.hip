@@ -2,6 +2,8 @@
 #include "common.h"
 #include "curve.cuh"
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 
 namespace gg {
@@ -40,6 +42,44 @@ std::vector<int> gg::enable_peer_access(const std::vector<int>& devs) {
         }
     (void)hipSetDevice(cur);
     return code;
+}
+
+namespace {
+std::mutex g_tq_mu;
+std::map<int, int> g_tq_used;                // device -> dedicated task queues in use
+std::map<hipStream_t, int> g_tq_streams;     // dedicated stream -> its device
+}  // namespace
+
+void gg::create_task_stream(hipStream_t* s, int device) {
+    int cap = 8;
+    if (const char* e = getenv("GG_TASK_QUEUES")) cap = std::max(0, atoi(e));
+    std::lock_guard<std::mutex> g(g_tq_mu);
+    if (g_tq_used[device] < cap) {
+        int cus = 0;
+        GG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+        for (int c = 0; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
+        if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
+            g_tq_used[device]++;
+            g_tq_streams[*s] = device;
+            return;
+        }
+        (void)hipGetLastError();
+    }
+    GG_HIP(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+}
+
+void gg::destroy_task_stream(hipStream_t s) {
+    if (!s) return;
+    {
+        std::lock_guard<std::mutex> g(g_tq_mu);
+        auto it = g_tq_streams.find(s);
+        if (it != g_tq_streams.end()) {
+            g_tq_used[it->second]--;
+            g_tq_streams.erase(it);
+        }
+    }
+    (void)hipStreamDestroy(s);
 }
 
 extern "C" const char* gg_last_error(void) { return g_last_error.c_str(); }

@@ -148,6 +148,17 @@ inline void create_copy_stream(hipStream_t* s) {
     GG_HIP(hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi));
 }
 
+// A compute stream for one of a prove's concurrent tasks, on a hardware queue of
+// its own when the device still has one to give: with 5 tasks on 4 queues two
+// tasks share a queue and the second one's kernels wait for the first one's
+// whole chain (the 8-shard Groth16 trace, profiles/r05_g_groth16_shard0.md: the
+// G2 accumulation started 7 ms late behind the A-MSM's reduction).  A stream
+// with a CU mask (all CUs here) gets a queue of its own (r05_b_xqueue2); at most
+// GG_TASK_QUEUES (default 8) such streams live per device and process, later
+// ones come from the shared pool.  destroy_task_stream returns the slot.
+void create_task_stream(hipStream_t* s, int device);
+void destroy_task_stream(hipStream_t s);
+
 inline unsigned grid_for(size_t n, unsigned block) {
     size_t g = (n + block - 1) / block;
     return (unsigned)(g ? g : 1);

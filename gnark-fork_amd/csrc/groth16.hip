@@ -158,8 +158,7 @@ struct gg_groth16_pk {
         wb.reset();
         if (Z) gg_msm_base_release(Z);
         if (dom) gg_domain_release(dom);
-        for (hipStream_t x : {s0, s1, s2, s3, s4})
-            if (x) (void)hipStreamDestroy(x);
+        for (hipStream_t x : {s0, s1, s2, s3, s4}) destroy_task_stream(x);
     }
 };
 
@@ -307,8 +306,10 @@ static void pk_finish(gg_groth16_pk* pk, std::shared_ptr<WireBases> wb, int curv
     }
     const int cZ = choose_c(std::max<size_t>(nZ, 1), ps.g1a, tbits);
     pk->Z = msm_base_create_internal(g1, g1_Z, nZ, nullptr, cZ, false, pk->wb->groups);
-    for (hipStream_t* x : {&pk->s0, &pk->s1, &pk->s2, &pk->s3, &pk->s4})
-        GG_HIP(hipStreamCreateWithFlags(x, hipStreamNonBlocking));
+    // the longest task (G2) and the computeH chain first to a queue of their own
+    int cur = 0;
+    GG_HIP(hipGetDevice(&cur));
+    for (hipStream_t* x : {&pk->s0, &pk->s1, &pk->s2, &pk->s3, &pk->s4}) create_task_stream(x, cur);
 }
 
 // Builds the resident key of one shard: wires [wire_lo, wire_hi) of the A, B, K
@@ -354,6 +355,24 @@ int g16_wire_window(int curve, size_t n_wires, size_t nB) {
     if (n_wires) c = std::min(c, choose_c(n_wires, ps.g1a, tbits));
     if (nB) c = std::min(c, choose_c(nB, 128, tbits));
     return c;
+}
+// new task streams for a key between proofs: `dedicated` false = HIP's shared
+// pool (returns the key's dedicated queues to the device), true = queues of
+// their own while the device has them (the timing rehearsal gives its solo
+// shard what one GPU of a node gives its only shard)
+void g16_restream(gg_groth16_pk* pk, bool dedicated) {
+    std::lock_guard<std::mutex> lk(pk->mu);
+    int cur = 0;
+    GG_HIP(hipGetDevice(&cur));
+    GG_HIP(hipSetDevice(pk->device));
+    for (hipStream_t* x : {&pk->s0, &pk->s1, &pk->s2, &pk->s3, &pk->s4}) {
+        GG_HIP(hipStreamSynchronize(*x));
+        destroy_task_stream(*x);
+        *x = nullptr;
+        if (dedicated) create_task_stream(x, pk->device);
+        else GG_HIP(hipStreamCreateWithFlags(x, hipStreamNonBlocking));
+    }
+    GG_HIP(hipSetDevice(cur));
 }
 }  // namespace gg
 

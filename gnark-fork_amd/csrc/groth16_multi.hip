@@ -37,6 +37,7 @@ gg_groth16_pk* g16_stripe_shard(std::shared_ptr<WireBases> wb, int curve, int lo
                                 const void* alpha1, const void* beta1, const void* delta1, const void* beta2,
                                 const void* delta2, size_t n_wires, size_t nb_public, int slog, uint32_t spart);
 int g16_wire_window(int curve, size_t n_wires, size_t nB);
+void g16_restream(gg_groth16_pk* pk, bool dedicated);
 }  // namespace gg
 
 namespace {
@@ -586,6 +587,13 @@ extern "C" int gg_groth16_mpk_set_rehearsal(gg_groth16_mpk_t m, int solo_shard) 
     GG_CHECK(m, GG_ERR_INVALID_ARG, "null key");
     GG_CHECK(solo_shard >= -1 && solo_shard < m->world, GG_ERR_INVALID_ARG, "solo shard out of range");
     std::lock_guard<std::mutex> lk(m->mu);
+    // shards sharing a device share its dedicated hardware queues (common.h
+    // create_task_stream): the solo shard gets them, as on a node
+    if (solo_shard >= 0 && solo_shard != m->solo) {
+        for (int r = 0; r < m->world; r++)
+            if (r != solo_shard && m->dev[r] == m->dev[solo_shard]) gg::g16_restream(m->pk[r], false);
+        gg::g16_restream(m->pk[solo_shard], true);
+    }
     m->solo = solo_shard;
     GG_CAPI_END
 }

@@ -132,3 +132,18 @@ def test_bench_reports_planned_exchange_and_devices():
     assert "len(set(rank_devices))" in src and "distinct GPU(s)" in src
     assert '"RCCL" if backend == "nccl" else backend' in src
     assert "1/%d slice per GPU" not in src
+
+
+def test_every_environment_knob_is_documented():
+    """Every GG_* variable the library reads is in INTEGRATION.md's tables."""
+    csrc = os.path.join(ROOT, "gnark-fork_amd", "csrc")
+    knobs = set()
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".cuh", ".h")):
+            with open(os.path.join(csrc, f)) as fh:
+                knobs.update(re.findall(r'getenv\("(GG_[A-Z0-9_]+)"\)', fh.read()))
+    assert "GG_TASK_QUEUES" in knobs
+    with open(os.path.join(ROOT, "INTEGRATION.md")) as fh:
+        doc = fh.read()
+    missing = sorted(k for k in knobs if f"`{k}`" not in doc)
+    assert not missing, missing
