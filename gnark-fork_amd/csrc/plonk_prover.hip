@@ -215,8 +215,7 @@ struct PlonkPeer {
         perm_slice.release();
         pz.release();
         ar.buf.release();
-        for (hipStream_t x : s)
-            if (x) (void)hipStreamDestroy(x);
+        for (hipStream_t x : s) destroy_task_stream(x);
         for (int i = 0; i < 4; i++) {
             if (ea[i]) (void)hipEventDestroy(ea[i]);
             if (eb[i]) (void)hipEventDestroy(eb[i]);
@@ -411,8 +410,7 @@ struct Key : gg_plonk_pk {
         if (d0) gg_domain_release(d0);
         if (d1) gg_domain_release(d1);
         units.clear();
-        for (hipStream_t x : s)
-            if (x) (void)hipStreamDestroy(x);
+        for (hipStream_t x : s) destroy_task_stream(x);
     }
 };
 
@@ -749,7 +747,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
     pk->log_u = 0;
     while ((1 << pk->log_u) < pk->U) pk->log_u++;
     pk->split_idft = log_big >= 12;
-    for (hipStream_t& x : pk->s) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    for (hipStream_t& x : pk->s) create_task_stream(&x, pk->device);  // own hardware queues (common.h)
     for (auto& w : pk->work) w = msm_work_new();
     for (hipEvent_t& e : pk->msm_ready) GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     hipStream_t st = pk->s[0];
@@ -778,7 +776,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
                 p->l_lo = bound(n, d);
                 p->l_hi = bound(n, d + 1);
                 GG_HIP(hipSetDevice(p->device));
-                for (hipStream_t& x : p->s) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+                for (hipStream_t& x : p->s) create_task_stream(&x, p->device);
                 gg::create_copy_stream(&p->cps);
                 GG_HIP(hipEventCreateWithFlags(&p->cpev, hipEventDisableTiming));
                 for (int e = 0; e < 4; e++) {
@@ -1867,6 +1865,32 @@ extern "C" int gg_plonk_pk_set_rehearsal_part(gg_plonk_pk_t pk, int part) {
     with_key(pk, [&](auto* k) {
         std::lock_guard<std::mutex> lk(k->mu);
         GG_CHECK(part >= -1 && part <= (int)k->peers.size(), GG_ERR_INVALID_ARG, "rehearsal part out of range");
+        // parts sharing a device share its dedicated hardware queues (common.h
+        // create_task_stream): the rehearsed part gets them, as on a node
+        if (part >= 0 && !(k->solo && k->solo_part == part)) {
+            auto streams = [&](int q) -> std::pair<hipStream_t*, int> {
+                return q == 0 ? std::make_pair(k->s, k->device)
+                              : std::make_pair(k->peers[q - 1]->s, k->peers[q - 1]->device);
+            };
+            auto restream = [&](int q, bool dedicated) {
+                auto [ss, dev] = streams(q);
+                GG_HIP(hipSetDevice(dev));
+                for (int i = 0; i < 4; i++) {
+                    GG_HIP(hipStreamSynchronize(ss[i]));
+                    destroy_task_stream(ss[i]);
+                    ss[i] = nullptr;
+                    if (dedicated) create_task_stream(&ss[i], dev);
+                    else GG_HIP(hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking));
+                }
+            };
+            int cur = 0;
+            GG_HIP(hipGetDevice(&cur));
+            const int dev = streams(part).second;
+            for (int q = 0; q <= (int)k->peers.size(); q++)
+                if (q != part && streams(q).second == dev) restream(q, false);
+            restream(part, true);
+            GG_HIP(hipSetDevice(cur));
+        }
         k->solo = part >= 0;
         k->solo_part = part >= 0 ? part : 0;
         return 0;
