@@ -747,7 +747,14 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
     pk->log_u = 0;
     while ((1 << pk->log_u) < pk->U) pk->log_u++;
     pk->split_idft = log_big >= 12;
-    for (hipStream_t& x : pk->s) create_task_stream(&x, pk->device);  // own hardware queues (common.h)
+    // a one-device key's four streams on hardware queues of their own (common.h
+    // create_task_stream: 125.9 vs 127.5-128.1 ms at 2^22, profiles/r05_l_*); a
+    // key with device parts keeps HIP's shared pool -- its 8-part rehearsal on
+    // one GPU stalled on dedicated queues (r05k)
+    for (hipStream_t& x : pk->s) {
+        if (n_devices <= 1) create_task_stream(&x, pk->device);
+        else GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+    }
     for (auto& w : pk->work) w = msm_work_new();
     for (hipEvent_t& e : pk->msm_ready) GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     hipStream_t st = pk->s[0];
@@ -776,7 +783,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
                 p->l_lo = bound(n, d);
                 p->l_hi = bound(n, d + 1);
                 GG_HIP(hipSetDevice(p->device));
-                for (hipStream_t& x : p->s) create_task_stream(&x, p->device);
+                for (hipStream_t& x : p->s) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
                 gg::create_copy_stream(&p->cps);
                 GG_HIP(hipEventCreateWithFlags(&p->cpev, hipEventDisableTiming));
                 for (int e = 0; e < 4; e++) {
@@ -1865,32 +1872,6 @@ extern "C" int gg_plonk_pk_set_rehearsal_part(gg_plonk_pk_t pk, int part) {
     with_key(pk, [&](auto* k) {
         std::lock_guard<std::mutex> lk(k->mu);
         GG_CHECK(part >= -1 && part <= (int)k->peers.size(), GG_ERR_INVALID_ARG, "rehearsal part out of range");
-        // parts sharing a device share its dedicated hardware queues (common.h
-        // create_task_stream): the rehearsed part gets them, as on a node
-        if (part >= 0 && !(k->solo && k->solo_part == part)) {
-            auto streams = [&](int q) -> std::pair<hipStream_t*, int> {
-                return q == 0 ? std::make_pair(k->s, k->device)
-                              : std::make_pair(k->peers[q - 1]->s, k->peers[q - 1]->device);
-            };
-            auto restream = [&](int q, bool dedicated) {
-                auto [ss, dev] = streams(q);
-                GG_HIP(hipSetDevice(dev));
-                for (int i = 0; i < 4; i++) {
-                    GG_HIP(hipStreamSynchronize(ss[i]));
-                    destroy_task_stream(ss[i]);
-                    ss[i] = nullptr;
-                    if (dedicated) create_task_stream(&ss[i], dev);
-                    else GG_HIP(hipStreamCreateWithFlags(&ss[i], hipStreamNonBlocking));
-                }
-            };
-            int cur = 0;
-            GG_HIP(hipGetDevice(&cur));
-            const int dev = streams(part).second;
-            for (int q = 0; q <= (int)k->peers.size(); q++)
-                if (q != part && streams(q).second == dev) restream(q, false);
-            restream(part, true);
-            GG_HIP(hipSetDevice(cur));
-        }
         k->solo = part >= 0;
         k->solo_part = part >= 0 ? part : 0;
         return 0;
