@@ -216,14 +216,16 @@ def main():
     import gc
 
     def timed_proves(steps, warmup):
+        # Collect cyclic garbage first (the setup's holds GB-sized buffers whose
+        # release took ~0.5 s when a collection ran inside a timed step) and move
+        # the survivors out of the collector's generations -- before the warm-up,
+        # so the GPU does not idle (and clock down) between the warm-up and the
+        # first timed step (r05j: 119.8 ms first step, 106.6-107.6 after).
+        gc.collect()
+        gc.freeze()
         for _ in range(warmup):
             g.prove()
         barrier()
-        # Collect cyclic garbage now (the setup's holds GB-sized buffers whose
-        # release took ~0.5 s when a collection ran inside a timed step) and move
-        # the survivors out of the collector's generations.
-        gc.collect()
-        gc.freeze()
         t0 = time.perf_counter()
         ends, stages = [], []
         for _ in range(steps):
