@@ -241,14 +241,17 @@ __device__ __forceinline__ uint4 chunk_ld(const uint32_t* sorted, uint32_t base4
 // entry chunks in L2 / MALL.  A/B on one box (profiles/r05_d_accum_ab.txt):
 // 13.90 vs 14.07-14.14 ms per 2^24 launch.  The LDS-DMA gathers (BN254 G2,
 // BLS12-381 G1) keep the default policy: with the hint G2 took 26.89 vs 26.2 ms.
+// The hint pays on big tables only: the 8-way shard's 1.7-GB tables (2^21 wires)
+// proved in 17.33 / 17.65 vs 17.71-18.13 ms without it (r05_m, r05_n), so a
+// launch takes it from a table of GG_ACCUM_NT_GB (default 4) GB up.
 // GG_PT_NT=0 builds the default policy everywhere, 2 the hint everywhere.
 #ifndef GG_PT_NT
 #define GG_PT_NT 1
 #endif
-// one accumulation point (a gather with no reuse)
-template <class T>
+// one accumulation point (a gather with no reuse), NT: with the nontemporal hint
+template <bool NT, class T>
 __device__ __forceinline__ T ld_pt(const T* p) {
-    if constexpr (GG_PT_NT != 0) {
+    if constexpr (NT) {
         typedef unsigned int u4v __attribute__((ext_vector_type(4)));
         static_assert(sizeof(T) % 16 == 0, "16B multiple");
         T r;
@@ -298,7 +301,7 @@ constexpr bool kLdsGather = !GG_ACCUM_R4LOOP && (std::is_same<F, Fp2>::value || 
 template <class F>
 constexpr size_t kAccumLds = kLdsGather<F> ? 4 * 2 * sizeof(Affine<F>) * 64 : 0;
 
-template <class F>
+template <class F, bool NT>
 __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affine<F>* pts, const uint32_t* sorted,
                                                      const uint32_t* offsets, uint32_t nb, int c,
                                                      uint32_t K, int skip_inf, typename PartialOf<F>::T* head,
@@ -377,12 +380,12 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
         // per SIMD (164 VGPRs) already hide the gather behind the other waves
         uint4 ch = chunk_ld(sorted, (e0 + 1) & ~3u);
         uint32_t v = sorted[e0], vn = (e0 + 1 < e1) ? chunk_at(ch, (e0 + 1) & 3u) : 0u;
-        Affine<F> p = ld_pt(pts + (v & pmask));
+        Affine<F> p = ld_pt<NT>(pts + (v & pmask));
         for (uint32_t e = e0; e < e1; e++) {
             Affine<F> qp = p;
             const uint32_t cv = v;
             if (e + 1 < e1) {
-                p = ld_pt(pts + (vn & pmask));
+                p = ld_pt<NT>(pts + (vn & pmask));
                 v = vn;
                 if (e + 2 < e1) {
                     const uint32_t j = e + 2;
@@ -407,13 +410,13 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
         // other waves of the SIMD cover the wait.
         const uint32_t elast = e1 - 1;
         uint32_t v = sorted[e0], vn = sorted[min(e0 + 1, elast)];
-        Affine<F> p = ld_pt(pts + (v & pmask));
+        Affine<F> p = ld_pt<NT>(pts + (v & pmask));
         for (uint32_t e = e0; e < e1; e++) {
             Affine<F> qp = p;
             const uint32_t cv = v;
             // the last step re-gathers its own point (a valid index, unused)
             const uint32_t nidx = (e + 1 < e1) ? vn : v;
-            p = ld_pt(pts + (nidx & pmask));
+            p = ld_pt<NT>(pts + (nidx & pmask));
             v = nidx;
             vn = sorted[min(e + 2, elast)];
             if (e == bnd) {
@@ -1251,7 +1254,7 @@ inline uint32_t range_length(size_t E) {
         int blocks = 0, cus = 0, dev = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_accum_range<F>, 256, kAccumLds<F>) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_accum_range<F, false>, 256, kAccumLds<F>) != hipSuccess ||
             blocks < 1 || cus < 1) {
             (void)hipGetLastError();
             return 256.0 * 256 * 2;
@@ -1315,7 +1318,15 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
             pmask = 1023u;
             while (pmask && pmask >= n) pmask >>= 1;  // stay inside the base
         }
-        hipLaunchKernelGGL(k_accum_range<F>, dim3(grid_for(T, 256)), dim3(256), kAccumLds<F>, st,
+        // the nontemporal hint on the BN254 G1 register path, for big tables (above)
+        static const double nt_min = [] {
+            const char* e = getenv("GG_ACCUM_NT_GB");
+            return 1e9 * (e ? atof(e) : 4.0);
+        }();
+        const bool nt = GG_PT_NT == 2 ||
+                        (GG_PT_NT == 1 && std::is_same<F, Fp>::value && (double)b->pts.bytes >= nt_min);
+        auto* const accum = nt ? &k_accum_range<F, true> : &k_accum_range<F, false>;
+        hipLaunchKernelGGL(accum, dim3(grid_for(T, 256)), dim3(256), kAccumLds<F>, st,
                            (const Affine<F>*)b->pts.p,
                            s->sorted.as<uint32_t>(), offs, (uint32_t)nb, ce, K, (int)b->has_inf, hP, tP, SP,
                            scr->tbucket.as<uint32_t>(), pmask);
