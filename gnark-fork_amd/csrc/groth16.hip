@@ -256,6 +256,14 @@ static std::shared_ptr<WireBases> wire_bases_build(int curve, int log_n, const v
 // The rest of a resident key (shard) around its wire tables: domain, Z
 // positions [z_lo, z_lo + nZ), the fixed points, streams.  slog > 0: a bucket
 // stripe shard over whole (shared) wire tables.
+// A/B (GG_G16_H_PRIORITY=1): the computeH -> Z-MSM task on a stream of the
+// greatest priority, its kernels dispatched ahead of the other tasks'
+static void h_priority_ab(gg_groth16_pk* pk) {
+    if (!(getenv("GG_G16_H_PRIORITY") && atoi(getenv("GG_G16_H_PRIORITY")))) return;
+    destroy_task_stream(pk->s1);
+    create_copy_stream(&pk->s1);
+}
+
 static void pk_finish(gg_groth16_pk* pk, std::shared_ptr<WireBases> wb, int curve, int log_n,
                       const void* omega_mont, const void* coset_gen_mont, const void* g1_Z, size_t z_lo, size_t nZ,
                       const void* alpha1, const void* beta1, const void* delta1, const void* beta2,
@@ -310,6 +318,7 @@ static void pk_finish(gg_groth16_pk* pk, std::shared_ptr<WireBases> wb, int curv
     int cur = 0;
     GG_HIP(hipGetDevice(&cur));
     for (hipStream_t* x : {&pk->s0, &pk->s1, &pk->s2, &pk->s3, &pk->s4}) create_task_stream(x, cur);
+    h_priority_ab(pk);
 }
 
 // Builds the resident key of one shard: wires [wire_lo, wire_hi) of the A, B, K
@@ -372,6 +381,7 @@ void g16_restream(gg_groth16_pk* pk, bool dedicated) {
         if (dedicated) create_task_stream(x, pk->device);
         else GG_HIP(hipStreamCreateWithFlags(x, hipStreamNonBlocking));
     }
+    if (dedicated) h_priority_ab(pk);
     GG_HIP(hipSetDevice(cur));
 }
 }  // namespace gg
