@@ -289,10 +289,10 @@ def main():
     wl = {"workload": "groth16", "log_n": args.log_n, "n_gpus": n_shards}
     # dominant kernel per proof: the G1 bucket accumulation (4 launches: A, B1, K, Z);
     # the G2 accumulation (the longest single launch) is the second entry
-    r_g1 = accum_roofline(kernels["msm_accum"], 64, "k_accum_range<gg::Fe<gg::FpCfg> >", wl,
+    r_g1 = accum_roofline(kernels["msm_accum"], 64, "k_accum_range<gg::Fe<gg::FpCfg>, ", wl,
                           "k_accum_range<Fe<FpCfg>> (BN254 G1 bucket accumulation, radix-2^29 XYZZ mixed adds: "
                           "the A, B1, K and Z MSMs -- the largest share of each proof)", g.g1_windows)
-    r_g2 = accum_roofline(kernels["msm_accum_g2"], 128, "k_accum_range<gg::Fp2>", wl,
+    r_g2 = accum_roofline(kernels["msm_accum_g2"], 128, "k_accum_range<gg::Fp2, ", wl,
                           "k_accum_range<Fp2> (BN254 G2 bucket accumulation of the B MSM: the longest single "
                           "launch of the prove)", g.g2_windows)
     roofline = dict(r_g1)
@@ -780,7 +780,7 @@ def msm_bench(log_n, rank, world, dist, xdev, barrier, max_over_ranks, steps=20,
            "window_bits": c, "windows": W, "kernel_avg_ms": kern}
     if acc:
         alg = n * 96
-        traffic, note = pmc_traffic("k_accum_range<gg::Fe<gg::FpCfg> >",
+        traffic, note = pmc_traffic("k_accum_range<gg::Fe<gg::FpCfg>, ",
                                     {"log_n": log_n, "window_bits": c, "windows": W}, 64)
         res["accum_roofline"] = {"achieved_GBps": alg / (acc * 1e-3) / 1e9,
                                  "frac_hbm": alg / (acc * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -816,7 +816,7 @@ def accum_roofline(k, pt_bytes, kernel, workload, desc, windows):
          "kernel": desc, "algorithmic_bytes_per_launch": alg, "units_per_launch": units, "windows": windows,
          "kernel_avg_ms": ms,
          "timing": "HIP events on the kernel's launch stream over %d proves run task by task (rocprof summary of "
-                   "the same workload: profiles/r03_*groth16_2p24_kernel_stats.md)" % ROOFLINE_PROVES,
+                   "the same workload: profiles/r05_z_groth16_2p24_kernel_stats.md)" % ROOFLINE_PROVES,
          "note": "EC MSM is VALU-integer bound (SURVEY 8d); the HBM fraction is reported as required, the "
                  "issue-rate fraction below is the kernel's real ceiling"}
     sq = pmc_sq(kernel, workload)
