@@ -18,6 +18,11 @@ void msm_run_bls(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_ja
 void msm_finish_g1(gg_msm_base* b, MsmSort* s, MsmScratch* scr, void* out_jac, hipStream_t st);
 void msm_finish_g2(gg_msm_base* b, MsmSort* s, MsmScratch* scr, void* out_jac, hipStream_t st);
 void msm_finish_bls(gg_msm_base* b, MsmSort* s, MsmScratch* scr, void* out_jac, hipStream_t st);
+void msm_run_batch_g1(gg_msm_base* b, MsmWork* w, const VecPtrs& vp, int nvec, void* const* out_jac, hipStream_t st);
+void msm_run_batch_g2(gg_msm_base* b, MsmWork* w, const VecPtrs& vp, int nvec, void* const* out_jac, hipStream_t st);
+void msm_run_batch_bls(gg_msm_base* b, MsmWork* w, const VecPtrs& vp, int nvec, void* const* out_jac, hipStream_t st);
+void msm_run_batch_bls2(gg_msm_base* b, MsmWork* w, const VecPtrs& vp, int nvec, void* const* out_jac,
+                        hipStream_t st);
 }  // namespace gg
 
 using namespace gg;
@@ -72,6 +77,18 @@ void msm_device_work(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* ou
     else if (b->group == GG_G2) msm_run_g2(b, w, scalars_dev, out_jac, st);
     else if (b->group == GG_BLS12_381_G1) msm_run_bls(b, w, scalars_dev, out_jac, st);
     else msm_run_bls2(b, w, scalars_dev, out_jac, st);
+}
+// nvec (<= kMaxBatch) MSMs over b as one (same-base commitments); out_jac[v]
+// receives the v-th
+void msm_device_work_batch(gg_msm_base* b, MsmWork* w, const Fr* const* scalars_dev, int nvec, void* const* out_jac,
+                           hipStream_t st) {
+    GG_CHECK(nvec >= 1 && nvec <= kMaxBatch, GG_ERR_INVALID_ARG, "batch of 1..4 scalar vectors");
+    VecPtrs vp{};
+    for (int v = 0; v < nvec; v++) vp.p[v] = scalars_dev[v];
+    if (b->group == GG_G1) msm_run_batch_g1(b, w, vp, nvec, out_jac, st);
+    else if (b->group == GG_G2) msm_run_batch_g2(b, w, vp, nvec, out_jac, st);
+    else if (b->group == GG_BLS12_381_G1) msm_run_batch_bls(b, w, vp, nvec, out_jac, st);
+    else msm_run_batch_bls2(b, w, vp, nvec, out_jac, st);
 }
 static void msm_device_locked(gg_msm_base* b, const Fr* scalars_dev, void* out_jac, hipStream_t st) {
     msm_device_work(b, &b->own, scalars_dev, out_jac, st);
@@ -165,6 +182,33 @@ extern "C" int gg_msm(gg_msm_base_t b, const void* scalars, size_t n_scalars, in
         sdev = b->own.scr.scal.as<Fr>();
     }
     msm_device_locked(b, sdev, out_jac, st);
+    GG_CAPI_END
+}
+
+extern "C" int gg_msm_batch(gg_msm_base_t b, const void* const* scalars, int n_vectors, size_t n_scalars,
+                            int scalars_on_device, void* const* out_jac, void* hip_stream) {
+    GG_CAPI_BEGIN
+    GG_CHECK(b && scalars && out_jac, GG_ERR_INVALID_ARG, "null argument");
+    GG_CHECK(n_vectors >= 1 && n_vectors <= kMaxBatch, GG_ERR_INVALID_ARG, "n_vectors must be 1..4");
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : hipStreamPerThread;
+    const size_t need = msm_scalars_needed(b);
+    GG_CHECK(n_scalars >= need, GG_ERR_INVALID_ARG, "scalar vector shorter than the points/index map require");
+    for (int v = 0; v < n_vectors; v++) {
+        GG_CHECK(need == 0 || scalars[v], GG_ERR_INVALID_ARG, "null scalars");
+        GG_CHECK(out_jac[v], GG_ERR_INVALID_ARG, "null out_jac");
+    }
+    std::lock_guard<std::mutex> lk(b->mu);
+    const Fr* sdev[kMaxBatch] = {};
+    if (!scalars_on_device && need) {
+        b->own.scr.scal.reserve((size_t)n_vectors * need * 32);
+        for (int v = 0; v < n_vectors; v++) {
+            sdev[v] = b->own.scr.scal.as<Fr>() + (size_t)v * need;
+            GG_HIP(hipMemcpyAsync((void*)sdev[v], scalars[v], need * 32, hipMemcpyHostToDevice, st));
+        }
+    } else {
+        for (int v = 0; v < n_vectors; v++) sdev[v] = (const Fr*)scalars[v];
+    }
+    msm_device_work_batch(b, &b->own, sdev, n_vectors, out_jac, st);
     GG_CAPI_END
 }
 

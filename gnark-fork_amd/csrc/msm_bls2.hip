@@ -16,4 +16,14 @@ void msm_finish_bls2(gg_msm_base* b, MsmSort* s, MsmScratch* scr, void* out_jac,
     Jac<Fp2Bls> j = xyzz_to_jac(msm_finish<Fp2Bls>(b, s, scr, st));
     memcpy(out_jac, &j, sizeof(j));
 }
+// a batch of nvec MSMs over b (msm_run_batch): out_jac[v] = the v-th result
+void msm_run_batch_bls2(gg_msm_base* b, MsmWork* w, const VecPtrs& vp, int nvec, void* const* out_jac,
+                        hipStream_t st) {
+    Xyzz<Fp2Bls> r[kMaxBatch];
+    msm_run_batch<Fp2Bls>(b, w, vp, nvec, st, r);
+    for (int v = 0; v < nvec; v++) {
+        Jac<Fp2Bls> j = xyzz_to_jac(r[v]);
+        memcpy(out_jac[v], &j, sizeof(j));
+    }
+}
 }  // namespace gg

@@ -236,7 +236,7 @@ __device__ __forceinline__ uint32_t wave_rank(uint32_t* cnt, uint32_t d, bool va
 // digit or (bucket stripes, slog > 0) a bucket outside stripe sres.
 template <class SC, class Fn>
 __device__ __forceinline__ void scalar_keys(const Fe<SC>& scl, int c, int W, const WinSpec& ws, int G, int slog,
-                                            uint32_t sres, Fn&& fn) {
+                                            uint32_t sres, uint32_t gofs, Fn&& fn) {
     const uint32_t smask = (1u << slog) - 1u;
     const Fe<SC> k = from_mont(scl);
     int carry = 0;
@@ -249,7 +249,7 @@ __device__ __forceinline__ void scalar_keys(const Fe<SC>& scl, int c, int W, con
         if (d && (bb & smask) == sres) {
             // bucket stripe (slog > 0): only buckets bb = 2^slog j + sres, renumbered j;
             // c is then the stripe's c - slog
-            const uint32_t bk = ((uint32_t)(w & (G - 1)) << (c - 1)) | (bb >> slog);
+            const uint32_t bk = ((gofs + (uint32_t)(w & (G - 1))) << (c - 1)) | (bb >> slog);
             key = bk | (d < 0 ? 0x80000000u : 0u);
         }
         fn(w, key);
@@ -259,13 +259,21 @@ __device__ __forceinline__ void scalar_keys(const Fe<SC>& scl, int c, int W, con
 // Phase A: the block's bin histogram and every entry's key for phase C.  (Round
 // 4 measured phase C deriving the keys again from the scalars instead: 3.37 vs
 // 3.14 ms per 2^24 sort, profiles/r04_c_sort_ab.txt -- the key array stays.)
+// A batch of nvec scalar vectors over one base (same-base commitments): block
+// column = v vblocks + tile, vector v's keys in rows v W + w, its buckets in
+// groups v G .. v G + G - 1 (sort_entries).
 template <class SC>
-__global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, const uint32_t* sidx,
+__global__ void __launch_bounds__(256) k_digits_hist(VecPtrs vp, const uint32_t* sidx,
                                                      size_t n, int c, int W, WinSpec ws, int G, int kbits,
                                                      int spb, int nbins, int h, uint32_t* keys, size_t kst,
-                                                     uint32_t* hist, uint32_t nblocks, int slog, uint32_t sres) {
+                                                     uint32_t* hist, uint32_t nblocks, uint32_t vblocks, int slog,
+                                                     uint32_t sres) {
     extern __shared__ uint32_t hh[];
-    const uint32_t tile = blockIdx.x;  // scalar range and histogram column
+    const uint32_t col = blockIdx.x;        // histogram column
+    const uint32_t v = col / vblocks;       // scalar vector of the batch
+    const uint32_t tile = col - v * vblocks;  // its scalar range
+    const Fe<SC>* scalars = static_cast<const Fe<SC>*>(vp.p[v]);
+    uint32_t* vkeys = keys + (size_t)v * W * kst;
     for (int j = threadIdx.x; j < nbins; j += blockDim.x) hh[j] = 0;
     __syncthreads();
     // spb <= 512: at most two scalars per thread, both loaded before any digit work
@@ -286,13 +294,13 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, cons
     for (int s = 0; s < 2; s++) {
         if (idx[s] == ~(size_t)0) continue;
         const size_t i = idx[s];
-        scalar_keys<SC>(scl[s], c, W, ws, G, slog, sres, [&](int w, uint32_t key) {
+        scalar_keys<SC>(scl[s], c, W, ws, G, slog, sres, v * (uint32_t)G, [&](int w, uint32_t key) {
             if (key != 0xffffffffu) atomicAdd(&hh[bin_of(key & 0x7fffffffu, c, kbits, h)], 1u);
-            keys[(size_t)w * kst + i] = key;
+            vkeys[(size_t)w * kst + i] = key;
         });
     }
     __syncthreads();
-    for (int j = threadIdx.x; j < nbins; j += blockDim.x) hist[(size_t)j * nblocks + tile] = hh[j];
+    for (int j = threadIdx.x; j < nbins; j += blockDim.x) hist[(size_t)j * nblocks + col] = hh[j];
 }
 
 // Phase C, LDS-staged: the block's entries are first partitioned by bin in LDS
@@ -300,10 +308,13 @@ __global__ void __launch_bounds__(256) k_digits_hist(const Fe<SC>* scalars, cons
 // written out as contiguous per-bin runs -> coalesced stores.
 __global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_t kst, size_t n, int W, int c, int G,
                                                      int kbits, int spb, int nbins, int h, const uint32_t* hist,
-                                                     const uint32_t* hoff, uint32_t nblocks,
+                                                     const uint32_t* hoff, uint32_t nblocks, uint32_t vblocks,
                                                      uint32_t* tmp_entry, void* tmp_key, int key16) {
     extern __shared__ uint32_t sm[];
-    const uint32_t tile = xcd_swizzle(blockIdx.x, gridDim.x);
+    const uint32_t col = xcd_swizzle(blockIdx.x, gridDim.x);  // histogram column (k_digits_hist)
+    const uint32_t v = col / vblocks;
+    const uint32_t tile = col - v * vblocks;
+    keys += (size_t)v * W * kst;
     uint32_t* lbase = sm;             // nbins: local exclusive offsets
     uint32_t* lcur = sm + nbins;      // nbins: local cursors
     uint32_t* s_entry = sm + 2 * nbins;
@@ -314,8 +325,8 @@ __global__ void __launch_bounds__(256) k_bin_scatter(const uint32_t* keys, size_
     // exclusive scan is a wave scan + one barrier
     const uint32_t jb = threadIdx.x;
     const bool has = (int)jb < nbins;
-    const uint32_t cnt = has ? hist[(size_t)jb * nblocks + tile] : 0u;
-    const uint32_t gof = has ? hoff[(size_t)jb * nblocks + tile] : 0u;
+    const uint32_t cnt = has ? hist[(size_t)jb * nblocks + col] : 0u;
+    const uint32_t gof = has ? hoff[(size_t)jb * nblocks + col] : 0u;
     __shared__ uint32_t wsum[4];
     uint32_t tot;
     const uint32_t ex = block_excl_scan256(cnt, wsum, &tot);
@@ -550,13 +561,15 @@ static void sort_plan(int c, int& h, std::vector<int>& rs) {
     }
 }
 
-void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st) {
+void sort_entries(const gg_msm_base* b, MsmSort* s, const VecPtrs& vp, hipStream_t st) {
     // a bucket stripe sorts a 2^-slog share of the buckets, renumbered densely:
-    // the bucket ids (and every sort key) are those of a c - slog window
-    const size_t n = b->n, nb = b->nb >> s->slog;
+    // the bucket ids (and every sort key) are those of a c - slog window.  A
+    // batch of s->nvec vectors sorts into s->kp (power of two >= nvec) copies of
+    // the bucket space, vector v in groups v G .. v G + G - 1.
+    const size_t n = b->n, nb = (b->nb >> s->slog) * (size_t)s->kp;
     const int c = b->c - s->slog, W = b->W, G = b->G;
-    const size_t total = (size_t)W * n;
-    const int kbits = (c - 1) + __builtin_ctz((unsigned)G);  // sort key bits
+    const size_t total = (size_t)W * n * (size_t)s->nvec;
+    const int kbits = (c - 1) + __builtin_ctz((unsigned)(G * s->kp));  // sort key bits
     int h;
     std::vector<int> rs;
     sort_plan(kbits + 1, h, rs);
@@ -566,7 +579,8 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
         const int v = atoi(e);
         if (v >= 32 && v <= spb && (v & (v - 1)) == 0) spb = v;
     }
-    const uint32_t nblocks = (uint32_t)((n + spb - 1) / spb);
+    const uint32_t vblocks = (uint32_t)((n + spb - 1) / spb);  // per vector
+    const uint32_t nblocks = vblocks * (uint32_t)s->nvec;
     const size_t nh = (size_t)nbins * nblocks;
     // all scratch reserved up front (no reallocation between launches)
     size_t ch_max = 0, chunks_max = 0;
@@ -598,14 +612,15 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
         s->chunk_desc.reserve(chunks_max * 16);
     }
     if (b->scurve)
-        hipLaunchKernelGGL(k_digits_hist<FrBlsCfg>, dim3(nblocks), dim3(256), nbins * 4, st,
-                           (const FrBls*)scalars_dev, b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n,
-                           c, W, b->win, G, kbits, spb, nbins, h, s->keys.as<uint32_t>(), kst,
-                           s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
+        hipLaunchKernelGGL(k_digits_hist<FrBlsCfg>, dim3(nblocks), dim3(256), nbins * 4, st, vp,
+                           b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, G, kbits, spb, nbins,
+                           h, s->keys.as<uint32_t>(), kst, s->hist.as<uint32_t>(), nblocks, vblocks, s->slog,
+                           s->sres);
     else
-        hipLaunchKernelGGL(k_digits_hist<FrCfg>, dim3(nblocks), dim3(256), nbins * 4, st, scalars_dev,
-                           b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, G, kbits, spb,
-                           nbins, h, s->keys.as<uint32_t>(), kst, s->hist.as<uint32_t>(), nblocks, s->slog, s->sres);
+        hipLaunchKernelGGL(k_digits_hist<FrCfg>, dim3(nblocks), dim3(256), nbins * 4, st, vp,
+                           b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, G, kbits, spb, nbins,
+                           h, s->keys.as<uint32_t>(), kst, s->hist.as<uint32_t>(), nblocks, vblocks, s->slog,
+                           s->sres);
     GG_HIP(hipGetLastError());
     exclusive_scan(s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nh, st, s->scan_tmp);
     // segment starts ping-pong between bin_start and seg2; the last pass writes offsets
@@ -625,7 +640,7 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipSt
     const bool key16 = kbits - h <= 16;
     hipLaunchKernelGGL(k_bin_scatter, dim3(nblocks), dim3(256), lds_c, st, s->keys.as<uint32_t>(), kst,
                        n, W, c, G, kbits, spb, nbins, h, s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nblocks,
-                       ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->p : nullptr, (int)key16);
+                       vblocks, ent_out(0)->as<uint32_t>(), S > 1 ? key_out(0)->p : nullptr, (int)key16);
     GG_HIP(hipGetLastError());
     uint32_t nseg = (uint32_t)nbins;
     int shift = kbits - h;
@@ -712,8 +727,10 @@ __global__ void k_derive_offsets(const uint32_t* offa, const uint32_t* pos, uint
 
 void msm_prepare_derived(const gg_msm_base* a, const MsmSort* sa, const gg_msm_base* b, MsmSort* sb,
                          const uint32_t* bmap, hipStream_t st) {
-    GG_CHECK(a->c == b->c && a->W == b->W && a->G == b->G && !a->has_sidx, GG_ERR_INTERNAL,
-             "derived sort: the bases' window layouts differ");
+    GG_CHECK(a->c == b->c && a->W == b->W && a->G == b->G && !a->has_sidx && sa->nvec == 1, GG_ERR_INTERNAL,
+             "derived sort: the bases' window layouts differ (or a batch sort)");
+    sb->nvec = 1;
+    sb->kp = 1;
     const size_t cap = (size_t)a->W * a->n, nb = a->nb >> sa->slog;
     sb->slog = sa->slog;
     sb->sres = sa->sres;
@@ -757,18 +774,32 @@ void msm_prepare_derived(const gg_msm_base* a, const MsmSort* sa, const gg_msm_b
 // done) and s->pin_ev (the fullest bucket's entry count on the host).
 void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st, int slog,
                  uint32_t sres) {
+    VecPtrs vp{};
+    vp.p[0] = scalars_dev;
+    msm_prepare_batch(b, s, vp, 1, st, slog, sres);
+}
+
+// the sort of nvec scalar vectors over b's points in one pass (same-base
+// commitments: PlonK's L, R, O and H1, H2, H3, prove.go:425-502, 1199-1218)
+void msm_prepare_batch(const gg_msm_base* b, MsmSort* s, const VecPtrs& vp, int nvec, hipStream_t st, int slog,
+                       uint32_t sres) {
     GG_CHECK(slog >= 0 && slog <= b->c - 2 && sres < (1u << slog), GG_ERR_INVALID_ARG,
              "bucket stripe out of range (stripe_log <= window_bits - 2, part < 2^stripe_log)");
+    GG_CHECK(nvec >= 1 && nvec <= kMaxBatch && (nvec == 1 || slog == 0), GG_ERR_INVALID_ARG,
+             "batch of 1..4 scalar vectors (no bucket stripes)");
     s->slog = slog;
     s->sres = sres;
-    const size_t n = b->n, nb = b->nb >> slog;
+    s->nvec = nvec;
+    s->kp = 1;
+    while (s->kp < nvec) s->kp <<= 1;
+    const size_t n = b->n, nb = (b->nb >> slog) * (size_t)s->kp;
     s->ensure_events();
     s->counts.reserve(nb * 4);
     s->offsets.reserve((nb + 1) * 4);
     s->maxcnt.reserve(4);
     {
         ProfScope ps_sort("msm_sort", st, (double)n);
-        sort_entries(b, s, scalars_dev, st);
+        sort_entries(b, s, vp, st);
         ps_sort.stop(st);
     }
     GG_HIP(hipMemsetAsync(s->maxcnt.p, 0, 4, st));

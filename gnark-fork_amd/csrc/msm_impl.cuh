@@ -92,11 +92,18 @@ inline WinSpec make_windows(int c, int W, int total) {
     return ws;
 }
 struct MsmSort;
-void sort_entries(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st);
+// up to kMaxBatch scalar vectors sorted together over one base (msm_prepare_batch)
+constexpr int kMaxBatch = 4;
+struct VecPtrs {
+    const void* p[kMaxBatch];
+};
+void sort_entries(const gg_msm_base* b, MsmSort* s, const VecPtrs& vp, hipStream_t st);
 // slog > 0: the sort keeps the bucket stripe sres of 2^slog (buckets b with
 // b mod 2^slog = sres, see MsmSort)
 void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st, int slog = 0,
                  uint32_t sres = 0);
+void msm_prepare_batch(const gg_msm_base* b, MsmSort* s, const VecPtrs& vp, int nvec, hipStream_t st, int slog = 0,
+                       uint32_t sres = 0);
 // b's sort from a's (same window layout, a indexes its scalars directly, bmap:
 // a's scalar index -> b's point or ~0); waits for sa->ready_ev on st
 void msm_prepare_derived(const gg_msm_base* a, const MsmSort* sa, const gg_msm_base* b, MsmSort* sb,
@@ -958,6 +965,9 @@ struct MsmSort {
     // and reduces only its 2^-slog share of the entries and buckets.
     int slog = 0;
     uint32_t sres = 0;
+    // a batch of nvec scalar vectors (msm_prepare_batch): kp = the power of two
+    // >= nvec copies of the bucket space, vector v in groups v G .. v G + G - 1
+    int nvec = 1, kp = 1;
     uint32_t* pin = nullptr;          // pinned read-back: [0] = entries of the fullest bucket, [1] = entries
     hipEvent_t pin_ev = nullptr;      // after the read-back copy
     hipEvent_t ready_ev = nullptr;    // after the sort
@@ -1055,6 +1065,7 @@ struct RedItem {
     int mlog;
     bool plain;
     int mult = 1;  // small signed factor of the whole term (bucket stripes), applied on the host
+    int res = 0;   // which result the term adds to (a batch of MSMs: one per scalar vector)
 };
 
 // Sum of reduction terms with log-depth, wide tree sums (DESIGN.md "MSM /
@@ -1064,12 +1075,16 @@ struct RedItem {
 // round's jobs of every term go into the same launches (one add's latency per
 // round for all of them), pieces of <= HOST_N elements finish on the host after
 // ONE read-back, combined by Horner over their 2^mlog factors.
+// Terms carry a result index (RedItem::res < nres): a batch's results come out of
+// the same launches and the same read-back.
 template <class F>
-inline Xyzz<F> reduce_terms(std::vector<RedItem<F>> items, MsmScratch* scr, hipStream_t st) {
+inline std::vector<Xyzz<F>> reduce_terms_multi(std::vector<RedItem<F>> items, int nres, MsmScratch* scr,
+                                               hipStream_t st) {
     static const bool split = getenv("GG_RED_SPLIT") && atoi(getenv("GG_RED_SPLIT"));  // A/B: a read-back per term
     if (split && items.size() > 1) {
-        Xyzz<F> acc = Xyzz<F>::inf();
-        for (const auto& it : items) acc = xyzz_add(acc, reduce_terms<F>({it}, scr, st));
+        std::vector<Xyzz<F>> acc(nres, Xyzz<F>::inf());
+        for (const auto& it : items)
+            acc[it.res] = xyzz_add(acc[it.res], reduce_terms_multi<F>({it}, nres, scr, st)[it.res]);
         return acc;
     }
     const size_t XB = sizeof(Xyzz<F>);
@@ -1098,11 +1113,11 @@ inline Xyzz<F> reduce_terms(std::vector<RedItem<F>> items, MsmScratch* scr, hipS
             int mlg = lg / 2;
             uint32_t M = 1u << mlg, rows = it.n >> mlg;
             if (it.plain) {  // row sums only
-                jobs.push_back({it.X, M, rows, 1u, M, Item{nullptr, rows, 0u, it.mlog, true, it.mult}});
+                jobs.push_back({it.X, M, rows, 1u, M, Item{nullptr, rows, 0u, it.mlog, true, it.mult, it.res}});
                 continue;
             }
-            jobs.push_back({it.X, M, rows, 1u, M, Item{nullptr, rows, 0u, it.mlog + mlg, false, it.mult}});
-            jobs.push_back({it.X, rows, M, M, 1u, Item{nullptr, M, it.off, it.mlog, false, it.mult}});
+            jobs.push_back({it.X, M, rows, 1u, M, Item{nullptr, rows, 0u, it.mlog + mlg, false, it.mult, it.res}});
+            jobs.push_back({it.X, rows, M, M, 1u, Item{nullptr, M, it.off, it.mlog, false, it.mult, it.res}});
         }
         // one launch per round: every output of every job is a block-wide sum
         static const bool block_mode = !(getenv("GG_RED_BLOCK") && atoi(getenv("GG_RED_BLOCK")) == 0);
@@ -1190,7 +1205,7 @@ inline Xyzz<F> reduce_terms(std::vector<RedItem<F>> items, MsmScratch* scr, hipS
     std::vector<std::vector<Xyzz<F>>> hx(host_items.size());
     for (size_t k = 0; k < host_items.size(); k++)
         hx[k].assign(flat.begin() + GL.off[k], flat.begin() + GL.off[k + 1]);
-    std::vector<std::pair<int, Xyzz<F>>> vals;
+    std::vector<std::vector<std::pair<int, Xyzz<F>>>> vals(nres);
     auto scaled = [](const Xyzz<F>& v, int m) {  // m v by double-and-add (|m| small)
         if (m == 1 || v.is_inf()) return v;
         const uint32_t u = (uint32_t)(m < 0 ? -m : m);
@@ -1205,9 +1220,10 @@ inline Xyzz<F> reduce_terms(std::vector<RedItem<F>> items, MsmScratch* scr, hipS
     for (size_t k = 0; k < host_items.size(); k++) {
         const auto& X = hx[k];
         Xyzz<F> run = Xyzz<F>::inf(), acc = Xyzz<F>::inf();
+        auto& vr = vals[host_items[k].res];
         if (host_items[k].plain) {
             for (const auto& x : X) acc = xyzz_add(acc, x);
-            vals.push_back({host_items[k].mlog, scaled(acc, host_items[k].mult)});
+            vr.push_back({host_items[k].mlog, scaled(acc, host_items[k].mult)});
             continue;
         }
         for (size_t j = X.size(); j-- > 1;) {
@@ -1218,17 +1234,26 @@ inline Xyzz<F> reduce_terms(std::vector<RedItem<F>> items, MsmScratch* scr, hipS
             run = xyzz_add(run, X[0]);  // run = sum of all
             for (uint32_t o = 0; o < host_items[k].off; o++) acc = xyzz_add(acc, run);
         }
-        vals.push_back({host_items[k].mlog, scaled(acc, host_items[k].mult)});
+        vr.push_back({host_items[k].mlog, scaled(acc, host_items[k].mult)});
     }
-    std::sort(vals.begin(), vals.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
-    Xyzz<F> acc = Xyzz<F>::inf();
-    int cur = vals.empty() ? 0 : vals[0].first;
-    for (auto& v : vals) {
-        for (; cur > v.first; cur--) acc = acc.is_inf() ? acc : xyzz_dbl(acc);
-        acc = xyzz_add(acc, v.second);
+    std::vector<Xyzz<F>> out(nres, Xyzz<F>::inf());
+    for (int r = 0; r < nres; r++) {
+        auto& vr = vals[r];
+        std::sort(vr.begin(), vr.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
+        Xyzz<F> acc = Xyzz<F>::inf();
+        int cur = vr.empty() ? 0 : vr[0].first;
+        for (auto& v : vr) {
+            for (; cur > v.first; cur--) acc = acc.is_inf() ? acc : xyzz_dbl(acc);
+            acc = xyzz_add(acc, v.second);
+        }
+        for (; cur > 0; cur--) acc = acc.is_inf() ? acc : xyzz_dbl(acc);
+        out[r] = acc;
     }
-    for (; cur > 0; cur--) acc = acc.is_inf() ? acc : xyzz_dbl(acc);
-    return acc;
+    return out;
+}
+template <class F>
+inline Xyzz<F> reduce_terms(std::vector<RedItem<F>> items, MsmScratch* scr, hipStream_t st) {
+    return reduce_terms_multi<F>(std::move(items), 1, scr, st)[0];
 }
 
 // level 2 + bucket reduction through k_bucket_sum_r / k_bucket_runsum (reduced-radix G1 groups);
@@ -1268,18 +1293,22 @@ inline uint32_t range_length(size_t E) {
 
 // Accumulation + reduction of base b over a prepared sort s (its own or one
 // shared with a base of identical shape), scratch scr.  Waits (device side) for
-// s->ready_ev.
+// s->ready_ev.  A batch sort (s->nvec vectors) gives one result per vector in
+// out[0 .. nvec): one accumulation launch, one level 2, one reduction -- the
+// vectors' buckets are groups v G .. v G + G - 1 of a kp times larger space.
 template <class F>
-inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream_t st) {
+inline void msm_finish_multi(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream_t st, Xyzz<F>* out) {
     // a bucket stripe (s->slog > 0) works in its c - slog bucket space: nb and ce
     // below; the group scales 2^(j c) keep the base's c
-    const int slog = s->slog;
-    const size_t n = b->n, nb = b->nb >> slog;
+    const int slog = s->slog, nvec = s->nvec, kp = s->kp;
+    const size_t n = b->n, nb = (b->nb >> slog) * (size_t)kp;
     const int ce = b->c - slog;
-    if (n == 0) return Xyzz<F>::inf();
+    const int Gb = b->G, Ge = b->G * kp;  // the base's groups, the batch's
+    for (int v = 0; v < nvec; v++) out[v] = Xyzz<F>::inf();
+    if (n == 0) return;
     GG_HIP(hipStreamWaitEvent(st, s->ready_ev, 0));
     const uint32_t* offs = s->offsets.as<uint32_t>();
-    size_t E = (size_t)b->W * n;  // entries (upper bound: digit-0 entries are not sorted)
+    size_t E = (size_t)b->W * n * (size_t)nvec;  // entries (upper bound: digit-0 entries are not sorted)
     if (slog) {
         // a stripe holds ~2^-slog of the entries: wait for the sort's count so
         // the ranges fill the chip for the entries there are
@@ -1340,7 +1369,7 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
     // ---- level 2: heavy buckets' ranges by a segmented tree (skew-robust,
     // log_fan(ranges) launches), then every bucket's partials into S
     ProfScope ps_acc2("msm_accum2", st, (double)n);
-    const size_t nbg = nb / (size_t)b->G;
+    const size_t nbg = nb / (size_t)Ge;
     // segments of L = 2^logL buckets, >= 2^17 of them per group (a lane each:
     // fewer leave the chip idle while each lane walks its chain); below 2^18
     // buckets per group the quad path is faster (MI355X: 2^20 MSM, c = 17)
@@ -1365,7 +1394,7 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
                 GG_HIP(hipGetLastError());
                 stride *= fan;
             }
-            const uint32_t Tg = (uint32_t)(nbg >> logL), G = (uint32_t)b->G;
+            const uint32_t Tg = (uint32_t)(nbg >> logL), G = (uint32_t)Ge;
             scr->seg.reserve(2 * (size_t)G * Tg * sizeof(Xyzz<F>) + nb * sizeof(PT));
             Xyzz<F>* D = scr->seg.as<Xyzz<F>>();
             Xyzz<F>* Rs = D + (size_t)G * Tg;
@@ -1385,14 +1414,16 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
             // and sum_j T_j = sum_s R_s.
             const int sneg = slog ? -(int)((1u << slog) - 1u - s->sres) : 0;
             std::vector<RedItem<F>> terms;
-            for (int jg = 0; jg < b->G; jg++) {
-                terms.push_back({(const Xyzz<F>*)Rs + (size_t)jg * Tg, Tg, 1u, jg * b->c + logL + slog, false});
-                terms.push_back({(const Xyzz<F>*)D + (size_t)jg * Tg, Tg, 0u, jg * b->c + slog, true});
-                if (sneg) terms.push_back({(const Xyzz<F>*)Rs + (size_t)jg * Tg, Tg, 0u, jg * b->c, true, sneg});
+            for (int jg = 0; jg < nvec * Gb; jg++) {
+                const int j = jg % Gb, v = jg / Gb;  // group j of vector v
+                terms.push_back({(const Xyzz<F>*)Rs + (size_t)jg * Tg, Tg, 1u, j * b->c + logL + slog, false, 1, v});
+                terms.push_back({(const Xyzz<F>*)D + (size_t)jg * Tg, Tg, 0u, j * b->c + slog, true, 1, v});
+                if (sneg) terms.push_back({(const Xyzz<F>*)Rs + (size_t)jg * Tg, Tg, 0u, j * b->c, true, sneg, v});
             }
-            Xyzz<F> res = reduce_terms<F>(std::move(terms), scr, st);
+            const std::vector<Xyzz<F>> res = reduce_terms_multi<F>(std::move(terms), nvec, scr, st);
+            for (int v = 0; v < nvec; v++) out[v] = res[v];
             ps_red.stop(st);
-            return res;
+            return;
         }
     }
     if constexpr (kRadixP) {  // the quad path works on gnark's form
@@ -1419,14 +1450,23 @@ inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream
     // one weighted sum per precompute group, sum_j 2^(j c) R_j, in one batched reduction
     const int sneg = slog ? -(int)((1u << slog) - 1u - s->sres) : 0;  // bucket stripe, as above
     std::vector<RedItem<F>> terms;
-    for (int j = 0; j < b->G; j++) {
-        const Xyzz<F>* Sj = (const Xyzz<F>*)S + (size_t)j * nbg;
-        terms.push_back({Sj, (uint32_t)nbg, 1u, j * b->c + slog, false});
-        if (sneg) terms.push_back({Sj, (uint32_t)nbg, 0u, j * b->c, true, sneg});
+    for (int jg = 0; jg < nvec * Gb; jg++) {
+        const int j = jg % Gb, v = jg / Gb;
+        const Xyzz<F>* Sj = (const Xyzz<F>*)S + (size_t)jg * nbg;
+        terms.push_back({Sj, (uint32_t)nbg, 1u, j * b->c + slog, false, 1, v});
+        if (sneg) terms.push_back({Sj, (uint32_t)nbg, 0u, j * b->c, true, sneg, v});
     }
-    Xyzz<F> res = reduce_terms<F>(std::move(terms), scr, st);
+    const std::vector<Xyzz<F>> res = reduce_terms_multi<F>(std::move(terms), nvec, scr, st);
+    for (int v = 0; v < nvec; v++) out[v] = res[v];
     ps_red.stop(st);
-    return res;
+}
+
+template <class F>
+inline Xyzz<F> msm_finish(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStream_t st) {
+    GG_CHECK(s->nvec == 1, GG_ERR_INTERNAL, "msm_finish of a batch sort");
+    Xyzz<F> r;
+    msm_finish_multi<F>(b, s, scr, st, &r);
+    return r;
 }
 
 template <class F>
@@ -1434,6 +1474,18 @@ inline Xyzz<F> msm_run(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, hipStr
     if (b->n == 0) return Xyzz<F>::inf();
     msm_prepare(b, &w->sort, scalars_dev, st);
     return msm_finish<F>(b, &w->sort, &w->scr, st);
+}
+
+// nvec MSMs over one base (same points, different scalars) as one: one sort, one
+// accumulation launch, one level 2 and one bucket reduction (msm_prepare_batch)
+template <class F>
+inline void msm_run_batch(gg_msm_base* b, MsmWork* w, const VecPtrs& vp, int nvec, hipStream_t st, Xyzz<F>* out) {
+    if (b->n == 0) {
+        for (int v = 0; v < nvec; v++) out[v] = Xyzz<F>::inf();
+        return;
+    }
+    msm_prepare_batch(b, &w->sort, vp, nvec, st);
+    msm_finish_multi<F>(b, &w->sort, &w->scr, st, out);
 }
 
 // device-resident points: keep[i] = point i is not infinity (or keep_inf)

@@ -43,6 +43,8 @@ struct gg_msm_base;
 namespace gg {
 struct MsmWork;
 void msm_device_work(gg_msm_base* b, MsmWork* w, const Fr* scalars_dev, void* out_jac, hipStream_t st);
+void msm_device_work_batch(gg_msm_base* b, MsmWork* w, const Fr* const* scalars_dev, int nvec, void* const* out_jac,
+                           hipStream_t st);
 MsmWork* msm_work_new();
 void msm_work_delete(MsmWork* w);
 }  // namespace gg
@@ -534,6 +536,88 @@ static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStr
 }
 // kzg.Commit(p, pk.Kzg) of a buffer of n + 3 scalars (zero beyond the polynomial)
 static BJac commit_kzg(Key* pk, int wi, const FrB* scal, hipStream_t st) { return msm_jac(pk, pk->kzg, wi, scal, st); }
+
+// Same-base commitments batched (commitToLRO on pk.KzgLagrange, prove.go:425-502;
+// commitToQuotient on pk.Kzg, :1199-1218): every part runs ONE MSM over its
+// base slice for all nv scalar vectors (gg_msm_batch: one sort, accumulation,
+// level 2 and reduction) in work slot 0; the scalars are complete on st.
+// GG_PLONK_BATCH=0 keeps three MSMs on three streams.
+static bool plonk_batch() {
+    static const bool on = !(getenv("GG_PLONK_BATCH") && atoi(getenv("GG_PLONK_BATCH")) == 0);
+    return on;
+}
+static void peer_msm_batch(Key* pk, int part, PlonkPeer* p, bool kzg, const FrB* const* scal, int nv, BJac* out) {
+    GG_HIP(hipSetDevice(p->device));
+    const size_t lo = kzg ? p->k_lo : p->l_lo, hi = kzg ? p->k_hi : p->l_hi;
+    for (int v = 0; v < nv; v++) out[v] = BJac::inf();
+    if (hi == lo) return;
+    const auto a = std::chrono::steady_clock::now();
+    hipStream_t q = p->s[0];
+    GG_HIP(hipEventRecord(p->ea[0], q));
+    const Fr* sv[4];
+    void* ov[4];
+    for (int v = 0; v < nv; v++) {
+        GG_HIP(hipMemcpyPeerAsync(p->scal[v].p, p->device, scal[v] + lo, pk->device, 32 * (hi - lo), q));
+        sv[v] = p->scal[v].as<Fr>();
+        ov[v] = &out[v];
+    }
+    GG_HIP(hipEventRecord(p->eb[0], q));
+    msm_device_work_batch(kzg ? p->kzg : p->kzg_lag, p->work[0], sv, nv, ov, q);
+    float cp = 0;
+    GG_HIP(hipEventElapsedTime(&cp, p->ea[0], p->eb[0]));  // the MSM synchronised the stream
+    std::lock_guard<std::mutex> lk(pk->tmu);
+    if ((size_t)part >= pk->ptimes.size()) return;
+    PlonkPartTimes& T = pk->ptimes[part];
+    T.msm_count += nv;
+    T.msm_ms += ms_since(a);
+    T.scalar_copy_ms += cp;
+    T.scalar_mb += 32.0 * (hi - lo) * nv / 1e6;
+}
+static void msm_jac_batch(Key* pk, gg_msm_base_t base, const FrB* const* scal, int nv, hipStream_t st, BJac* out) {
+    const bool kz = base == pk->kzg;
+    const size_t lo = kz ? pk->k_lo : pk->l_lo;
+    for (int v = 0; v < nv; v++) out[v] = BJac::inf();
+    std::vector<std::future<std::vector<BJac>>> fs;
+    if (peers_active(pk)) {
+        hipEvent_t ready = pk->msm_ready[0];
+        GG_HIP(hipEventRecord(ready, st));
+        std::vector<const FrB*> sc(scal, scal + nv);
+        for (size_t q = 0; q < pk->peers.size(); q++)
+            if (part_runs(pk, (int)q + 1))
+                fs.push_back(std::async(std::launch::async, [pk, q, pp = pk->peers[q].get(), kz, sc, nv, ready] {
+                    GG_HIP(hipEventSynchronize(ready));
+                    std::vector<BJac> r(nv);
+                    peer_msm_batch(pk, (int)q + 1, pp, kz, sc.data(), nv, r.data());
+                    return r;
+                }));
+    }
+    const auto a = std::chrono::steady_clock::now();
+    if (part_runs(pk, 0)) {
+        const Fr* sv[4];
+        void* ov[4];
+        for (int v = 0; v < nv; v++) {
+            sv[v] = (const Fr*)(scal[v] + lo);
+            ov[v] = &out[v];
+        }
+        msm_device_work_batch(base, pk->work[0], sv, nv, ov, st);
+    }
+    const double own = ms_since(a);
+    const auto w = std::chrono::steady_clock::now();
+    for (auto& f : fs) {
+        const std::vector<BJac> r = f.get();
+        for (int v = 0; v < nv; v++) out[v] = jac_add(out[v], r[v]);
+    }
+    const double waited = ms_since(w);
+    if (!pk->ptimes.empty()) {
+        std::lock_guard<std::mutex> lk(pk->tmu);
+        PlonkPartTimes& T = pk->ptimes[0];
+        if (part_runs(pk, 0)) {
+            T.msm_count += nv;
+            T.msm_ms += own;
+        }
+        T.wait_ms += waited;
+    }
+}
 // sum of the ranks' partials (called in one fixed order on every rank)
 static BJac red(Key* pk, BJac j) {
     if (pk->world == 1) return j;
@@ -1095,11 +1179,21 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     BJac lroj[3];
     {
         std::vector<std::future<void>> fs;
-        for (int k = 0; k < 3; k++)
-            fs.push_back(std::async(msm_policy(), [&, k] {
+        if (plonk_batch()) {
+            // one batched MSM on s[0] once L, R, O are uploaded
+            for (int k = 1; k < 3; k++) GG_HIP(hipStreamWaitEvent(s[0], uploaded[k], 0));
+            fs.push_back(std::async(msm_policy(), [&] {
                 GG_HIP(hipSetDevice(pk->device));
-                lroj[k] = msm_jac(pk, pk->kzg_lag, k, F(pk->lag[k]), s[k]);
+                const FrB* sc[3] = {F(pk->lag[0]), F(pk->lag[1]), F(pk->lag[2])};
+                msm_jac_batch(pk, pk->kzg_lag, sc, 3, s[0], lroj);
             }));
+        } else {
+            for (int k = 0; k < 3; k++)
+                fs.push_back(std::async(msm_policy(), [&, k] {
+                    GG_HIP(hipSetDevice(pk->device));
+                    lroj[k] = msm_jac(pk, pk->kzg_lag, k, F(pk->lag[k]), s[k]);
+                }));
+        }
         // meanwhile on stream 3 (one part; with peers: canon_tasks): completeQk
         // (prove.go:397-423) and the BSB22 Pi_i
         if (!dz) {
@@ -1446,13 +1540,19 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     // ---- commitToQuotient: H1, H2, H3 at once (prove.go:1199-1218)
     {
         BJac hj[3];
-        std::vector<std::future<void>> fs3;
-        for (int k = 0; k < 3; k++)
-            fs3.push_back(std::async(msm_policy(), [&, k] {
-                GG_HIP(hipSetDevice(pk->device));
-                hj[k] = commit_kzg(pk, k, F(pk->hpad[k]), s[k]);
-            }));
-        for (auto& f : fs3) f.get();
+        if (plonk_batch()) {
+            // hpad[k] are complete on s[2] (recorded just above into s[0..2])
+            const FrB* sc[3] = {F(pk->hpad[0]), F(pk->hpad[1]), F(pk->hpad[2])};
+            msm_jac_batch(pk, pk->kzg, sc, 3, s[0], hj);
+        } else {
+            std::vector<std::future<void>> fs3;
+            for (int k = 0; k < 3; k++)
+                fs3.push_back(std::async(msm_policy(), [&, k] {
+                    GG_HIP(hipSetDevice(pk->device));
+                    hj[k] = commit_kzg(pk, k, F(pk->hpad[k]), s[k]);
+                }));
+            for (auto& f : fs3) f.get();
+        }
         for (int k = 0; k < 3; k++) P.h[k] = to_aff(red(pk, hj[k]));
     }
     mark();

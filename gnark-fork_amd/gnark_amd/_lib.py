@@ -79,6 +79,7 @@ def _load():
         "gg_get_hbm_budget": ([], S),
         "gg_msm": ([P, P, S, I, P, P], I),
         "gg_msm_stripe": ([P, P, S, I, I, I, P, P], I),
+        "gg_msm_batch": ([P, P, I, S, I, P, P], I),
         "gg_groth16_pk_create_stripe_ex": ([I, I, P, P, P, S, P, S, P, S, S, P, S, P, P, P, P, P, P, P, P, S,
                                             S, P, I, I, PP], I),
         "gg_groth16_pk_stripe": ([P, ctypes.POINTER(I), ctypes.POINTER(I)], I),
@@ -228,7 +229,7 @@ EXPORTED = [
     "gg_groth16_mpk_devices", "gg_groth16_mpk_base_info", "gg_groth16_pk_create_shard_ex", "gg_r1cs_create", "gg_r1cs_create_ex", "gg_r1cs_release", "gg_r1cs_info", "gg_r1cs_solve",
     "gg_r1cs_solution_dev", "gg_scs_create", "gg_scs_release", "gg_scs_info", "gg_scs_solve",
     "gg_scs_solution_dev", "gg_r1cs_set_inputs", "gg_scs_set_inputs", "gg_r1cs_schedule", "gg_scs_schedule",
-    "gg_msm_stripe", "gg_groth16_pk_create_stripe_ex", "gg_groth16_pk_stripe", "gg_groth16_mpk_split",
+    "gg_msm_stripe", "gg_msm_batch", "gg_groth16_pk_create_stripe_ex", "gg_groth16_pk_stripe", "gg_groth16_mpk_split",
     "gg_hshard_create_ex", "gg_hshard_exchange_bytes", "gg_groth16_mpk_shard_timings",
     "gg_groth16_mpk_set_rehearsal", "gg_plonk_pk_set_rehearsal", "gg_plonk_pk_set_rehearsal_part",
     "gg_plonk_pk_part_timings", "gg_groth16_mpk_peer_access", "gg_plonk_pk_peer_access",

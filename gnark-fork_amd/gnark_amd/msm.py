@@ -58,6 +58,18 @@ class MsmBase:
                                 ptr(out), ptr(stream)))
         return bytes(out)
 
+    def msm_batch_jac(self, scalar_vectors, n_scalars: int, on_device=False, stream=None) -> list:
+        """1..4 MSMs over this base as one (gg_msm_batch: one sort, accumulation
+        and reduction; PlonK's same-base commitments): one Jacobian result per
+        scalar vector, equal to msm_jac of each."""
+        k = len(scalar_vectors)
+        outs = [bytearray(_JAC[self.group]) for _ in range(k)]
+        keep = [ptr(v) for v in scalar_vectors] + [ptr(o) for o in outs]  # alive across the call
+        sv = (ctypes.c_void_p * k)(*[p.value if p is not None else None for p in keep[:k]])
+        ov = (ctypes.c_void_p * k)(*[p.value for p in keep[k:]])
+        check(lib.gg_msm_batch(self.handle, sv, k, n_scalars, int(on_device), ov, ptr(stream)))
+        return [bytes(o) for o in outs]
+
     def msm(self, scalars, n_scalars: int, on_device=False, stream=None) -> bytes:
         """Affine result (Montgomery, gnark layout; infinity = zeros)."""
         return jac_to_affine(self.group, self.msm_jac(scalars, n_scalars, on_device, stream))

@@ -170,6 +170,15 @@ size_t gg_get_hbm_budget(void);
  * hip_stream may be NULL. */
 int gg_msm(gg_msm_base_t b, const void *scalars, size_t n_scalars, int scalars_on_device,
            void *out_jac, void *hip_stream);
+/* n_vectors (1..4) MSMs over the same base as one: out_jac[v] = sum_i
+ * scalars[v][idx(i)] * P_i, with one sort, one accumulation launch, one level 2
+ * and one bucket reduction for all of them (the vectors' buckets are disjoint
+ * groups of one bucket space).  Replaces the same-base kzg.Commit calls of
+ * commitToLRO (backend/plonk/bls12-381/prove.go:425-502: L, R, O on
+ * pk.KzgLagrange) and commitToQuotient (:1199-1218: h1, h2, h3 on pk.Kzg).
+ * Arguments as gg_msm's, one scalar vector and one output per v. */
+int gg_msm_batch(gg_msm_base_t b, const void *const *scalars, int n_vectors, size_t n_scalars,
+                 int scalars_on_device, void *const *out_jac, void *hip_stream);
 /* One bucket stripe of gg_msm: with N = 2^stripe_log, the part of the MSM whose
  * signed-digit buckets b (|digit| - 1, every window) satisfy b mod N ==
  * stripe_part, i.e. sum over those buckets of (b + 1) S_b.  The N stripes'
