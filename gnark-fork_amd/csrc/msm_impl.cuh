@@ -243,7 +243,7 @@ __device__ __forceinline__ uint4 chunk_ld(const uint32_t* sorted, uint32_t base4
 #ifndef GG_G1_PIPE
 #define GG_G1_PIPE 0  // A/B builds: the G1 loop with every load unconditional
 #endif
-// The register-path gathers (BN254 G1) carry the nontemporal hint: a point is
+// The register-path gathers (BN254 G1 in GG_G1_LDS=0 builds) carry the nontemporal hint: a point is
 // read once per launch, and the hint keeps the gathers from displacing the
 // entry chunks in L2 / MALL.  A/B on one box (profiles/r05_d_accum_ab.txt):
 // 13.90 vs 14.07-14.14 ms per 2^24 launch.  The LDS-DMA gathers (BN254 G2,
@@ -301,9 +301,17 @@ struct LdsRing {
         return r;
     }
 };
-// BN254 G2 (128-B points) and BLS12-381 G1 (96-B) take the LDS ring
+// BN254 G2 (128-B points), BLS12-381 G1 (96-B) and BN254 G1 (64-B) take the LDS
+// ring.  BN254 G1 too since r05w: 149 instead of 164 VGPRs, three waves per
+// SIMD either way, the one-GPU 2^24 prove 106.8 / 106.8 vs 108.8 / 108.7 ms,
+// the 8-way shard 17.48 vs 17.66 ms (profiles/r05_w_g1_lds_ab.md); GG_G1_LDS=0
+// builds the register loop (with the nontemporal policy below) for A/B.
+#ifndef GG_G1_LDS
+#define GG_G1_LDS 1
+#endif
 template <class F>
-constexpr bool kLdsGather = !GG_ACCUM_R4LOOP && (std::is_same<F, Fp2>::value || std::is_same<F, FpBls>::value);
+constexpr bool kLdsGather = !GG_ACCUM_R4LOOP && (std::is_same<F, Fp2>::value || std::is_same<F, FpBls>::value ||
+                                                 (GG_G1_LDS && std::is_same<F, Fp>::value));
 // dynamic LDS of k_accum_range<F>: two slots per wave, four waves per block
 template <class F>
 constexpr size_t kAccumLds = kLdsGather<F> ? 4 * 2 * sizeof(Affine<F>) * 64 : 0;
@@ -1352,8 +1360,8 @@ inline void msm_finish_multi(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStr
             const char* e = getenv("GG_ACCUM_NT_GB");
             return 1e9 * (e ? atof(e) : 4.0);
         }();
-        const bool nt = GG_PT_NT == 2 ||
-                        (GG_PT_NT == 1 && std::is_same<F, Fp>::value && (double)b->pts.bytes >= nt_min);
+        const bool nt = !kLdsGather<F> && (GG_PT_NT == 2 || (GG_PT_NT == 1 && std::is_same<F, Fp>::value &&
+                                                              (double)b->pts.bytes >= nt_min));
         auto* const accum = nt ? &k_accum_range<F, true> : &k_accum_range<F, false>;
         hipLaunchKernelGGL(accum, dim3(grid_for(T, 256)), dim3(256), kAccumLds<F>, st,
                            (const Affine<F>*)b->pts.p,
