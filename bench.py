@@ -36,6 +36,9 @@ sys.path.insert(0, os.path.join(ROOT, "gnark-fork_amd"))
 METRIC = ("Groth16 prove time + MSM G1 throughput (Mscalar-mul/s) BN254 2^24 R1CS, 1/2/4/8 GPU")
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FPMUL_PEAK_G = 135.7  # measured BN254 Fp Montgomery multiplies/s (G), profiles/r01_v2_mbench_field.txt
+# v_mad_u64_u32 share of the G1 / G2 accumulation loops' VALU stream (ISA of the
+# loop block: 1,361 of 2,375 instructions)
+ACCUM_MAD_FRACTION = 0.57
 VALU_ISSUE_CAP = 0.22  # wave-instructions / SIMD-cycle of the ~60 %-mad mix (profiles/r02_mbench_field29_v2.txt)
 MIMC_ROUNDS = 85      # 3 constraints per round; 2^(log_n-8) chains -> 255 * 2^(log_n-8) constraints
 ROOFLINE_PROVES = 3   # serial proves timed kernel by kernel for the roofline
@@ -821,16 +824,27 @@ def accum_roofline(k, pt_bytes, kernel, workload, desc, windows):
                  "issue-rate fraction below is the kernel's real ceiling"}
     sq = pmc_sq(kernel, workload)
     if sq:
-        # VALU issue rate: wave instructions per SIMD cycle (1024 SIMDs at 2.4 GHz);
-        # ~60 % of the mix is v_mad_u64_u32 (~5.5 cycles/wave), the rest ~3.1, which
-        # caps the mix at ~0.22 (profiles/r02_mbench_field29_v2.txt)
-        ipc = sq["valu_insts"] / (ms * 1e-3 * 2.4e9 * 1024)
+        # VALU issue rate in wave-instructions per SIMD-cycle (1024 SIMDs) at the
+        # kernel's REAL clock: the cycles are GRBM_GUI_ACTIVE / 8 XCDs of the same
+        # counter pass (the 2.4-GHz nominal clock overstated the cycles);
+        # the ceiling of the mix (~57 % v_mad_u64_u32 in the loop's ISA) from the
+        # microbenchmark counted the same way (issue_cap)
+        cap, cap_src = issue_cap(ACCUM_MAD_FRACTION)
+        grbm = sq.get("grbm_gui_active")
+        if grbm:
+            cycles = grbm / 8.0
+            clock = cycles / (ms * 1e-3) / 1e9
+            basis = ("SQ_INSTS_VALU / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs), both per dispatch of the committed "
+                     "SQ-counter profile; clock = those cycles / this run's launch ms")
+        else:
+            cycles, clock = ms * 1e-3 * 2.4e9, None
+            basis = "SQ_INSTS_VALU / (launch ms x 2.4 GHz x 1024 SIMDs): no GRBM_GUI_ACTIVE in the profile"
+        ipc = sq["valu_insts"] / (cycles * 1024)
         r["valu"] = {"insts_per_launch": sq["valu_insts"],
                      "insts_per_madd_per_lane": sq["valu_insts"] * 64 / (units * windows),
-                     "insts_per_simd_cycle": ipc, "issue_cap_for_mix": VALU_ISSUE_CAP,
-                     "frac": ipc / VALU_ISSUE_CAP, "source": sq["source"],
-                     "basis": "SQ_INSTS_VALU of the committed SQ-counter profile / (launch ms x 2.4 GHz x 1024 "
-                              "SIMDs) against the measured issue ceiling of this instruction mix"}
+                     "clock_GHz": clock, "insts_per_simd_cycle": ipc, "issue_cap_for_mix": cap,
+                     "issue_cap_source": cap_src, "mad_fraction": ACCUM_MAD_FRACTION,
+                     "frac": ipc / cap, "source": sq["source"], "basis": basis}
     return r
 
 
@@ -945,8 +959,29 @@ def pmc_sq(kernel, workload):
         for k, v in d.get("kernels", {}).items():
             if kernel in k and "SQ_INSTS_VALU" in v:
                 return {"valu_insts": v["SQ_INSTS_VALU"], "waves": v.get("SQ_WAVES"),
-                        "source": os.path.basename(f)}
+                        "grbm_gui_active": v.get("GRBM_GUI_ACTIVE"), "source": os.path.basename(f)}
     return None
+
+
+def issue_cap(mad_fraction):
+    """The VALU issue ceiling (wave-instructions per SIMD-cycle, 1024 SIMDs) of an
+    instruction mix with `mad_fraction` v_mad_u64_u32, from the committed
+    microbenchmark profile (tools/issue_cap.py: k_mad_tp with and without
+    interleaved simple ops under rocprofv3 --pmc SQ_INSTS_VALU GRBM_GUI_ACTIVE, so
+    the cycles are the chip's real ones, not wall time x a nominal clock).
+    (cap, source) or (VALU_ISSUE_CAP, note) if no such profile exists."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*issue_cap*.json")), key=_profile_order, reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        cm, cs = d.get("cycles_per_mad"), d.get("cycles_per_simple")
+        if cm and cs:
+            return 1.0 / (mad_fraction * cm + (1.0 - mad_fraction) * cs), (
+                "%s: %.2f cycles per v_mad_u64_u32, %.2f per simple VALU op per wave (GRBM_GUI_ACTIVE cycles)"
+                % (os.path.basename(f), cm, cs))
+    return VALU_ISSUE_CAP, "r02 microbenchmark at a nominal 2.4 GHz (no GRBM-clocked issue-cap profile)"
 
 
 def cpu_threads(requested):
@@ -1229,6 +1264,11 @@ def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, 
         kzg_desc = "1/%d slice per rank, partial commitments all-gathered" % world
     else:
         kzg_desc = "whole KZG bases on one GPU"
+    # the orchestration that ran: batched same-base commitments unless GG_PLONK_BATCH=0
+    # (the library also falls back per vector when a batch is too large)
+    batched = os.environ.get("GG_PLONK_BATCH", "1") != "0"
+    if group:  # the leader key's shape
+        extra["leader"] = {"mode": gpk.mode, "devices": list(gpk.devices), "identities": gpk.identities}
     if devices and len(devices) > 1 and pk is not None:  # N device parts: where each part's time went
         extra["part_timings"] = [{k: round(v, 3) for k, v in p.items()} for p in pk.part_timings()]
         extra["devices"] = list(devices)
@@ -1277,9 +1317,13 @@ def plonk_prove_bench(log_n, reps=2, per_rep=False, rank=0, world=1, dist=None, 
         extra["split_projection"] = proj
     return {"log_n": log_n, "n_gpus": len(set(devices)) if devices else world, "prove_ms": min(ts), "prove_ms_all": ts, "stage_ms": tim,
             **extra, "kzg_bases": kzg_desc,
-            "key_setup_s": t_setup, "msms_per_proof": 10,
+            "key_setup_s": t_setup, "msms_per_proof": 6 if batched else 10,
             "ntts_per_proof": "20 coset FFTs (L,R,O,Z,Qk x 4 cosets; key polynomials resident) + 5 iFFTs of n + 1 coset iFFT of 4n",
-            "orchestration": "C++ (gg_plonk_prove): 3 concurrent KZG MSMs for LRO and for H, openZ || linearized, two cosets in flight",
+            "orchestration": "C++ (gg_plonk_prove): %s, openZ || linearized, two cosets in flight" % (
+                "one batched MSM (gg_msm_batch: one sort / accumulation / reduction) for L, R, O and one for H1, "
+                "H2, H3 -- 10 commitments in 6 MSMs" if batched else
+                "3 concurrent KZG MSMs for LRO and for H (GG_PLONK_BATCH=0) -- 10 MSMs"),
+            "plonk_batch": batched,
             "note": "synthetic key + random witness (timing only; proofs of valid witnesses verify in "
                     "tests/test_gpu_plonk_prove.py)"}
 

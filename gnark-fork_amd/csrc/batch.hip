@@ -116,7 +116,7 @@ static void batch_mul(const void* base_aff, const void* scalars, size_t n, int s
     GG_HIP(hipGetLastError());
     if (!out_on_device)
         GG_HIP(hipMemcpyAsync(out, o, n * sizeof(Affine<F>), hipMemcpyDeviceToHost, st));
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
 }
 
 }  // namespace gg

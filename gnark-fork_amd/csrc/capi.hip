@@ -2,7 +2,10 @@
 #include "common.h"
 #include "curve.cuh"
 #include <cstring>
+#include <atomic>
+#include <chrono>
 #include <map>
+#include <thread>
 #include <mutex>
 #include <string>
 
@@ -46,40 +49,246 @@ std::vector<int> gg::enable_peer_access(const std::vector<int>& devs) {
 
 namespace {
 std::mutex g_tq_mu;
-std::map<int, int> g_tq_used;                // device -> dedicated task queues in use
-std::map<hipStream_t, int> g_tq_streams;     // dedicated stream -> its device
+struct DedQueue {
+    hipStream_t s;
+    bool used;
+};
+std::map<int, std::vector<DedQueue>> g_tq;  // device -> its dedicated task queues (CU-masked streams)
+int task_queue_cap() {
+    const char* e = getenv("GG_TASK_QUEUES");  // read per borrow: tests switch budgets between keys
+    return e ? std::max(0, atoi(e)) : 8;
+}
+// a dedicated queue of `device` (the set grows up to the budget), or null
+hipStream_t borrow_task_queue(int device) {
+    std::lock_guard<std::mutex> g(g_tq_mu);
+    auto& v = g_tq[device];
+    int used = 0;
+    for (auto& d : v) used += d.used;
+    if (used >= task_queue_cap()) return nullptr;
+    for (auto& d : v)
+        if (!d.used) {
+            d.used = true;
+            if (gg::trace_streams()) fprintf(stderr, "[gg] borrow dedicated queue %p (device %d)\n", (void*)d.s, device);
+            return d.s;
+        }
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
+    for (int c = 0; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    hipStream_t s = nullptr;
+    const bool ok = hipSetDevice(device) == hipSuccess &&
+                    hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) == hipSuccess;
+    (void)hipSetDevice(cur);
+    if (!ok) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    v.push_back({s, true});
+    if (gg::trace_streams()) fprintf(stderr, "[gg] new dedicated queue %p (device %d, %zu)\n", (void*)s, device, v.size());
+    return s;
+}
+void return_task_queue(hipStream_t s) {
+    std::lock_guard<std::mutex> g(g_tq_mu);
+    for (auto& kv : g_tq)
+        for (auto& d : kv.second)
+            if (d.s == s) {
+                d.used = false;
+                if (gg::trace_streams()) fprintf(stderr, "[gg] return dedicated queue %p\n", (void*)s);
+                return;
+            }
+}
+void wait_idle(hipStream_t s) {
+    GG_WAIT_STREAM(s);                    // bounded
+    GG_HIP(hipStreamSynchronize(s));      // returns at once; settles the runtime's view of the stream
+}
 }  // namespace
 
-void gg::create_task_stream(hipStream_t* s, int device) {
-    int cap = 8;
-    if (const char* e = getenv("GG_TASK_QUEUES")) cap = std::max(0, atoi(e));
-    std::lock_guard<std::mutex> g(g_tq_mu);
-    if (g_tq_used[device] < cap) {
-        int cus = 0;
-        GG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-        std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
-        for (int c = 0; c < cus; c++) mask[(size_t)c / 32] |= 1u << (c % 32);
-        if (hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
-            g_tq_used[device]++;
-            g_tq_streams[*s] = device;
-            return;
-        }
-        (void)hipGetLastError();
-    }
-    GG_HIP(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+// GG_TRACE_STREAMS=1: a stderr line per borrowed / returned dedicated queue
+bool gg::trace_streams() {
+    static const bool on = getenv("GG_TRACE_STREAMS") && atoi(getenv("GG_TRACE_STREAMS")) == 1;
+    return on;
 }
 
-void gg::destroy_task_stream(hipStream_t s) {
-    if (!s) return;
-    {
-        std::lock_guard<std::mutex> g(g_tq_mu);
-        auto it = g_tq_streams.find(s);
-        if (it != g_tq_streams.end()) {
-            g_tq_used[it->second]--;
-            g_tq_streams.erase(it);
+void gg::task_streams_init(hipStream_t* const* active, TaskQueue* q, int n, int device, bool dedicated) {
+    int cur = 0;
+    GG_HIP(hipGetDevice(&cur));
+    GG_HIP(hipSetDevice(device));
+    for (int i = 0; i < n; i++) {
+        if (!q[i].own) GG_HIP(hipStreamCreateWithFlags(&q[i].own, hipStreamNonBlocking));
+        q[i].ded = dedicated ? borrow_task_queue(device) : nullptr;
+        *active[i] = q[i].ded ? q[i].ded : q[i].own;
+    }
+    GG_HIP(hipSetDevice(cur));
+}
+
+void gg::task_streams_switch(hipStream_t* const* active, TaskQueue* q, int n, int device, bool dedicated) {
+    int cur = 0;
+    GG_HIP(hipGetDevice(&cur));
+    GG_HIP(hipSetDevice(device));
+    for (int i = 0; i < n; i++) {
+        wait_idle(q[i].own);
+        if (q[i].ded) wait_idle(q[i].ded);
+    }
+    for (int i = 0; i < n; i++)
+        if (q[i].ded && !dedicated) {
+            return_task_queue(q[i].ded);
+            q[i].ded = nullptr;
+        }
+    for (int i = 0; i < n; i++) {
+        if (dedicated && !q[i].ded) q[i].ded = borrow_task_queue(device);
+        *active[i] = q[i].ded ? q[i].ded : q[i].own;
+    }
+    GG_HIP(hipSetDevice(cur));
+}
+
+void gg::task_streams_release(TaskQueue* q, int n) {
+    for (int i = 0; i < n; i++) {
+        if (q[i].ded) {
+            (void)hipStreamSynchronize(q[i].ded);
+            return_task_queue(q[i].ded);
+            q[i].ded = nullptr;
+        }
+        if (q[i].own) (void)hipStreamDestroy(q[i].own);
+        q[i].own = nullptr;
+    }
+}
+
+// ---- bounded waits (common.h)
+namespace {
+std::atomic<double> g_wait_timeout{-1.0};  // < 0: GG_WAIT_TIMEOUT_S or the default
+thread_local std::string g_wait_label;
+}  // namespace
+
+double gg::wait_timeout_s() {
+    const double t = g_wait_timeout.load();
+    if (t > 0) return t;
+    static const double env = [] {
+        const char* e = getenv("GG_WAIT_TIMEOUT_S");
+        const double v = e ? atof(e) : 0.0;
+        return v > 0 ? v : 300.0;
+    }();
+    return env;
+}
+
+gg::WaitScope::WaitScope(const std::string& label) : prev(g_wait_label) { g_wait_label = label; }
+gg::WaitScope::~WaitScope() { g_wait_label = prev; }
+
+namespace {
+std::string wait_where(const char* what, const char* fn, int line) {
+    std::string w = g_wait_label.empty() ? std::string() : g_wait_label + ": ";
+    return w + fn + ":" + std::to_string(line) + " waiting for " + what;
+}
+// poll q() (hipEventQuery / hipStreamQuery) until it is no longer NotReady: a
+// yield loop for the first 2 ms (the latency of hipEventSynchronize's spin), then
+// 20-us sleeps, up to the deadline
+template <class Q>
+void poll_ready(Q q, const char* what, const char* fn, int line) {
+    hipError_t e = q();
+    if (e == hipErrorNotReady) {
+        using clk = std::chrono::steady_clock;
+        const auto t0 = clk::now();
+        const double lim = gg::wait_timeout_s();
+        while (e == hipErrorNotReady) {
+            const double el = std::chrono::duration<double>(clk::now() - t0).count();
+            if (el > lim) {
+                char b[64];
+                snprintf(b, sizeof b, "timed out after %.0f s: ", el);
+                throw gg::Error(GG_ERR_TIMEOUT, b + wait_where(what, fn, line) +
+                                                    " (GG_WAIT_TIMEOUT_S / gg_set_wait_timeout)");
+            }
+            if (el < 0.002) std::this_thread::yield();
+            else std::this_thread::sleep_for(std::chrono::microseconds(20));
+            e = q();
         }
     }
-    (void)hipStreamDestroy(s);
+    if (e != hipSuccess) {
+        const int code = e == hipErrorOutOfMemory ? GG_ERR_OOM : GG_ERR_DEVICE;
+        throw gg::Error(code, std::string(hipGetErrorString(e)) + " at " + wait_where(what, fn, line));
+    }
+}
+}  // namespace
+
+void gg::wait_event_(hipEvent_t e, const char* what, const char* fn, int line) {
+    poll_ready([e] { return hipEventQuery(e); }, what, fn, line);
+}
+void gg::wait_stream_(hipStream_t s, const char* what, const char* fn, int line) {
+    poll_ready([s] { return hipStreamQuery(s); }, what, fn, line);
+}
+
+int gg::PartBarrier::wait(const char* what) {
+    std::unique_lock<std::mutex> l(mu);
+    if (broken) return why.empty() ? GG_ERR_INTERNAL : GG_ERR_TIMEOUT;
+    const uint64_t g = gen;
+    if (++count == n) {
+        count = 0;
+        gen++;
+        cv.notify_all();
+        return GG_OK;
+    }
+    const auto lim = std::chrono::duration<double>(wait_timeout_s());
+    if (!cv.wait_for(l, lim, [&] { return gen != g || broken; })) {
+        broken = true;
+        char b[96];
+        snprintf(b, sizeof b, "timed out after %.0f s at a barrier of %d (%d arrived): ", lim.count(), n, count);
+        why = b + wait_where(what, "barrier", 0);
+        cv.notify_all();
+        set_last_error(why);
+        return GG_ERR_TIMEOUT;
+    }
+    if (broken && !why.empty()) set_last_error(why);
+    return broken ? (why.empty() ? GG_ERR_INTERNAL : GG_ERR_TIMEOUT) : GG_OK;
+}
+void gg::PartBarrier::abort() {
+    std::lock_guard<std::mutex> l(mu);
+    broken = true;
+    cv.notify_all();
+}
+void gg::PartBarrier::reset() {
+    std::lock_guard<std::mutex> l(mu);
+    broken = false;
+    count = 0;
+    why.clear();
+}
+
+extern "C" int gg_set_wait_timeout(double seconds) {
+    GG_CAPI_BEGIN
+    GG_CHECK(seconds >= 0, GG_ERR_INVALID_ARG, "timeout must be >= 0 (0: GG_WAIT_TIMEOUT_S or 300 s)");
+    g_wait_timeout.store(seconds > 0 ? seconds : -1.0);
+    GG_CAPI_END
+}
+extern "C" double gg_get_wait_timeout(void) { return gg::wait_timeout_s(); }
+
+// host-only self-test of the bounded barrier (no GPU): `parties` threads are
+// expected, `arriving` of them come; with arriving < parties every waiter must
+// return GG_ERR_TIMEOUT after timeout_s instead of blocking
+extern "C" int gg_wait_selftest(int parties, int arriving, double timeout_s) {
+    GG_CAPI_BEGIN
+    GG_CHECK(parties >= 1 && parties <= 64 && arriving >= 1 && arriving <= parties && timeout_s > 0,
+             GG_ERR_INVALID_ARG, "1 <= arriving <= parties <= 64, timeout_s > 0");
+    const double saved = g_wait_timeout.load();
+    g_wait_timeout.store(timeout_s);
+    gg::PartBarrier bar;
+    bar.n = parties;
+    std::vector<int> rc(arriving, GG_OK);
+    std::vector<std::string> msg(arriving);
+    {
+        std::vector<std::thread> th;
+        for (int i = 0; i < arriving; i++)
+            th.emplace_back([&, i] {
+                gg::WaitScope ws("selftest part " + std::to_string(i));
+                rc[i] = bar.wait("the other parts");
+                if (rc[i]) msg[i] = gg_last_error();
+            });
+        for (auto& t : th) t.join();
+    }
+    g_wait_timeout.store(saved);
+    for (int i = 0; i < arriving; i++) GG_CHECK(rc[i] == GG_OK, rc[i], msg[i]);
+    GG_CAPI_END
 }
 
 extern "C" const char* gg_last_error(void) { return g_last_error.c_str(); }

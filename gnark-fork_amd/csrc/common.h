@@ -6,6 +6,8 @@
 #include <string>
 #include <cstdio>
 #include <vector>
+#include <condition_variable>
+#include <mutex>
 #include "../../include/gnark_amd.h"
 
 // -DGG_ACCUM_PROBE=1 builds a traffic-attribution variant (build_var/, never
@@ -40,6 +42,16 @@ void set_last_error(const std::string& m);
 #define GG_CHECK(cond, code, msg)                       \
     do {                                                \
         if (!(cond)) throw ::gg::Error((code), (msg));  \
+    } while (0)
+
+// a probe build's results are wrong by design: every entry point that returns
+// MSM sums or proof parts ends with this instead of GG_OK
+#define GG_PROBE_GUARD()                                                                         \
+    do {                                                                                         \
+        if (::gg::kAccumProbe) {                                                                 \
+            ::gg::set_last_error("traffic-probe build (GG_ACCUM_PROBE): the MSM sums are wrong"); \
+            return GG_REHEARSAL;                                                                 \
+        }                                                                                        \
     } while (0)
 
 #define GG_CAPI_BEGIN try {
@@ -148,16 +160,64 @@ inline void create_copy_stream(hipStream_t* s) {
     GG_HIP(hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi));
 }
 
-// A compute stream for one of a prove's concurrent tasks, on a hardware queue of
-// its own when the device still has one to give: with 5 tasks on 4 queues two
+// The compute streams of a prove's concurrent tasks.  HIP maps a device's
+// streams onto 4 hardware queues per priority, so with 5 tasks on 4 queues two
 // tasks share a queue and the second one's kernels wait for the first one's
 // whole chain (the 8-shard Groth16 trace, profiles/r05_g_groth16_shard0.md: the
 // G2 accumulation started 7 ms late behind the A-MSM's reduction).  A stream
-// with a CU mask (all CUs here) gets a queue of its own (r05_b_xqueue2); at most
-// GG_TASK_QUEUES (default 8) such streams live per device and process, later
-// ones come from the shared pool.  destroy_task_stream returns the slot.
-void create_task_stream(hipStream_t* s, int device);
-void destroy_task_stream(hipStream_t s);
+// with a CU mask (all CUs here) gets a hardware queue of its own (r05_b_xqueue2).
+// Each task slot (TaskQueue) has a plain stream of its own, created once with
+// its key, and while the device has one to give a DEDICATED queue borrowed from
+// the process's per-device set: at most GG_TASK_QUEUES (default 8) CU-masked
+// streams per device and process, created on first use and never destroyed.
+// Handing the dedicated queues from one key (shard, part) to another -- the
+// timing rehearsals -- is a pointer swap between idle streams: no stream is
+// created or destroyed then.  (Round 6: re-creating streams in the rehearsal
+// stalled inside hipStreamDestroy of a pool stream after CU-masked streams had
+// been destroyed, profiles/r06_d_restream_stall.md, the r05k stall's pattern.)
+struct TaskQueue {
+    hipStream_t own = nullptr;  // plain non-blocking stream of the slot (the key's)
+    hipStream_t ded = nullptr;  // borrowed dedicated queue, or null
+};
+// active[i] <- slot i's stream: dedicated if `dedicated` and the budget allows
+void task_streams_init(hipStream_t* const* active, TaskQueue* q, int n, int device, bool dedicated);
+// between proofs: wait until the slots' streams are idle, return / borrow the
+// dedicated queues, repoint active[] (never creates or destroys a stream)
+void task_streams_switch(hipStream_t* const* active, TaskQueue* q, int n, int device, bool dedicated);
+// the key goes away: dedicated queues back to the set, own streams destroyed
+void task_streams_release(TaskQueue* q, int n);
+bool trace_streams();
+
+// ---- bounded host waits (round 6, VERDICT r5: a stall must end in an error,
+// not a hang).  Every wait of the library's host threads for GPU work or for
+// another part / shard of a proof has a deadline: gg_set_wait_timeout or
+// GG_WAIT_TIMEOUT_S (seconds, default 300).  Past it the wait throws GG_ERR_TIMEOUT
+// naming what it waited for and the thread's WaitScope (part, stage).
+double wait_timeout_s();
+void wait_event_(hipEvent_t e, const char* what, const char* fn, int line);
+void wait_stream_(hipStream_t s, const char* what, const char* fn, int line);
+#define GG_WAIT_EVENT(e) ::gg::wait_event_((e), #e, __func__, __LINE__)
+#define GG_WAIT_STREAM(s) ::gg::wait_stream_((s), #s, __func__, __LINE__)
+// the calling thread's part of a proof, for timeout messages ("part 3: ratio")
+struct WaitScope {
+    std::string prev;
+    explicit WaitScope(const std::string& label);
+    ~WaitScope();
+};
+// A reusable barrier of n host threads that a failing thread breaks (abort) and
+// whose wait gives up at the wait deadline (the Groth16 one-process exchanges).
+struct PartBarrier {
+    std::mutex mu;
+    std::condition_variable cv;
+    int n = 1, count = 0;
+    uint64_t gen = 0;
+    bool broken = false;
+    std::string why;  // set when broken by a timeout
+    // GG_OK, GG_ERR_INTERNAL (broken by a peer) or GG_ERR_TIMEOUT (this wait or a peer's timed out)
+    int wait(const char* what);
+    void abort();
+    void reset();
+};
 
 inline unsigned grid_for(size_t n, unsigned block) {
     size_t g = (n + block - 1) / block;

@@ -149,6 +149,13 @@ struct gg_groth16_pk {
     bool share_AK = false, share_B = false;
     DevBuf wires, sa, sb, sc;
     hipStream_t s0 = nullptr, s1 = nullptr, s2 = nullptr, s3 = nullptr, s4 = nullptr;
+    TaskQueue tq[5];  // the task slots behind s0..s4 (common.h: own stream + borrowed dedicated queue)
+    hipStream_t* const* active() {
+        act[0] = &s0, act[1] = &s1, act[2] = &s2, act[3] = &s3, act[4] = &s4;
+        return act;
+    }
+    hipStream_t* act[5] = {};
+    hipStream_t hprio = nullptr;  // GG_G16_H_PRIORITY=1: s1 on a stream of the greatest priority
     std::unique_ptr<Stager> stager;  // host inputs -> HBM (created on first host-input prove)
     int device = 0;
     std::mutex mu;
@@ -158,7 +165,8 @@ struct gg_groth16_pk {
         wb.reset();
         if (Z) gg_msm_base_release(Z);
         if (dom) gg_domain_release(dom);
-        for (hipStream_t x : {s0, s1, s2, s3, s4}) destroy_task_stream(x);
+        task_streams_release(tq, 5);
+        if (hprio) (void)hipStreamDestroy(hprio);
     }
 };
 
@@ -260,8 +268,8 @@ static std::shared_ptr<WireBases> wire_bases_build(int curve, int log_n, const v
 // greatest priority, its kernels dispatched ahead of the other tasks'
 static void h_priority_ab(gg_groth16_pk* pk) {
     if (!(getenv("GG_G16_H_PRIORITY") && atoi(getenv("GG_G16_H_PRIORITY")))) return;
-    destroy_task_stream(pk->s1);
-    create_copy_stream(&pk->s1);
+    if (!pk->hprio) create_copy_stream(&pk->hprio);
+    pk->s1 = pk->hprio;
 }
 
 static void pk_finish(gg_groth16_pk* pk, std::shared_ptr<WireBases> wb, int curve, int log_n,
@@ -317,7 +325,7 @@ static void pk_finish(gg_groth16_pk* pk, std::shared_ptr<WireBases> wb, int curv
     // the longest task (G2) and the computeH chain first to a queue of their own
     int cur = 0;
     GG_HIP(hipGetDevice(&cur));
-    for (hipStream_t* x : {&pk->s0, &pk->s1, &pk->s2, &pk->s3, &pk->s4}) create_task_stream(x, cur);
+    task_streams_init(pk->active(), pk->tq, 5, cur, true);
     h_priority_ab(pk);
 }
 
@@ -365,24 +373,15 @@ int g16_wire_window(int curve, size_t n_wires, size_t nB) {
     if (nB) c = std::min(c, choose_c(nB, 128, tbits));
     return c;
 }
-// new task streams for a key between proofs: `dedicated` false = HIP's shared
-// pool (returns the key's dedicated queues to the device), true = queues of
-// their own while the device has them (the timing rehearsal gives its solo
-// shard what one GPU of a node gives its only shard)
+// a key's task slots between proofs: `dedicated` false = the slots' own plain
+// streams (the key's dedicated queues go back to the device's set), true =
+// dedicated queues while the device has them (the timing rehearsal gives its
+// solo shard what one GPU of a node gives its only shard).  No stream is
+// created or destroyed (common.h TaskQueue).
 void g16_restream(gg_groth16_pk* pk, bool dedicated) {
     std::lock_guard<std::mutex> lk(pk->mu);
-    int cur = 0;
-    GG_HIP(hipGetDevice(&cur));
-    GG_HIP(hipSetDevice(pk->device));
-    for (hipStream_t* x : {&pk->s0, &pk->s1, &pk->s2, &pk->s3, &pk->s4}) {
-        GG_HIP(hipStreamSynchronize(*x));
-        destroy_task_stream(*x);
-        *x = nullptr;
-        if (dedicated) create_task_stream(x, pk->device);
-        else GG_HIP(hipStreamCreateWithFlags(x, hipStreamNonBlocking));
-    }
-    if (dedicated) h_priority_ab(pk);
-    GG_HIP(hipSetDevice(cur));
+    task_streams_switch(pk->active(), pk->tq, 5, pk->device, dedicated);
+    h_priority_ab(pk);
 }
 }  // namespace gg
 
@@ -669,7 +668,7 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
         inputs_abc(A, B, C, len);
         const bool compact = !inputs_on_device;
         hshard_run(dh->hs, A, B, C, len, compact, dh->send, dh->recv, dh->xchg, dh->ctx, pk->s1);
-        GG_HIP(hipStreamSynchronize(pk->s1));
+        GG_WAIT_STREAM(pk->s1);
         double b = now_ms();
         t_h = b - a;
         msm_device(pk->Z, hshard_h(dh->hs), out.z, pk->s1);
@@ -681,7 +680,7 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
         double a = now_ms();
         inputs_abc(A, B, C, len);
         compute_h_device(pk->dom, A, B, C, A, pk->s1);
-        GG_HIP(hipStreamSynchronize(pk->s1));
+        GG_WAIT_STREAM(pk->s1);
         double b = now_ms();
         t_h = b - a;
         if (h_dev_out) GG_HIP(hipMemcpyAsync(h_dev_out, A, nbytes, hipMemcpyDeviceToDevice, pk->s1));
@@ -867,6 +866,7 @@ extern "C" int gg_groth16_prove_partial(gg_groth16_pk_t pk, const void* wires, s
     partials_put(pk->curve, p, partials);
     g_timings[7] = 0;
     g_timings[8] = now_ms() - t0;
+    GG_PROBE_GUARD();
     GG_CAPI_END
 }
 
@@ -893,6 +893,7 @@ extern "C" int gg_groth16_prove_partial_dist(gg_groth16_pk_t pk, gg_hshard_t hs,
     partials_put(pk->curve, p, partials);
     g_timings[7] = 0;
     g_timings[8] = now_ms() - t0;
+    GG_PROBE_GUARD();
     GG_CAPI_END
 }
 

@@ -42,38 +42,6 @@ void g16_restream(gg_groth16_pk* pk, bool dedicated);
 
 namespace {
 
-// reusable barrier that can be broken (a failing shard releases the others)
-struct Barrier {
-    std::mutex mu;
-    std::condition_variable cv;
-    int n = 1, count = 0;
-    uint64_t gen = 0;
-    bool broken = false;
-    bool wait() {
-        std::unique_lock<std::mutex> l(mu);
-        if (broken) return false;
-        const uint64_t g = gen;
-        if (++count == n) {
-            count = 0;
-            gen++;
-            cv.notify_all();
-            return true;
-        }
-        cv.wait(l, [&] { return gen != g || broken; });
-        return !broken;
-    }
-    void abort() {
-        std::lock_guard<std::mutex> l(mu);
-        broken = true;
-        cv.notify_all();
-    }
-    void reset() {
-        std::lock_guard<std::mutex> l(mu);
-        broken = false;
-        count = 0;
-    }
-};
-
 bool dist_h_ok(size_t n, int world) {
     return world >= 1 && world <= 16 && (world & (world - 1)) == 0 && n >= 2 && n >= (size_t)world * world;
 }
@@ -102,7 +70,7 @@ struct gg_groth16_mpk {
     // (common.h create_copy_stream: their own hardware queues)
     std::vector<std::vector<hipStream_t>> xst;
     uint8_t alpha1[96], beta1[96], delta1[96], beta2[192], delta2[192];
-    Barrier bar;
+    gg::PartBarrier bar;  // the exchanges' meeting point (bounded: gg_set_wait_timeout)
     std::mutex mu;  // one proof at a time per key
     double last_ms[4] = {0, 0, 0, 0};
     // per shard, last proof: where its time went (gg_groth16_mpk_shard_timings)
@@ -143,7 +111,9 @@ int mpk_exchange(void* ctx, const void* send_dev, void* recv_dev, size_t bytes) 
     (void)recv_dev;
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
-    if (!m->bar.wait()) return GG_ERR_INTERNAL;
+    int rc = m->bar.wait("the shards' sends written (exchange, first barrier)");
+    if (rc == GG_ERR_INTERNAL) gg::set_last_error("exchange aborted: another shard failed");
+    if (rc) return rc;
     const auto t1 = clk::now();
     bool ok = hipSetDevice(m->dev[r]) == hipSuccess;
     size_t pushed = 0;
@@ -155,14 +125,22 @@ int mpk_exchange(void* ctx, const void* send_dev, void* recv_dev, size_t bytes) 
                                 m->xst[r][j]) == hipSuccess;
         if (k != r) pushed += bytes;
     }
-    for (int j = 0; ok && j < m->world; j++) ok = hipStreamSynchronize(m->xst[r][j]) == hipSuccess;
     if (!ok) {
         (void)hipGetLastError();
         m->bar.abort();
         return GG_ERR_DEVICE;
     }
+    try {
+        gg::WaitScope ws("shard " + std::to_string(r) + " exchange " + std::to_string(m->times[r].nx + 1));
+        for (int j = 0; j < m->world; j++) GG_WAIT_STREAM(m->xst[r][j]);  // its pushes have landed
+    } catch (const gg::Error& e) {
+        gg::set_last_error(e.what());
+        m->bar.abort();
+        return e.code;
+    }
     const auto t2 = clk::now();
-    const bool ok2 = m->bar.wait();
+    const int rc2 = m->bar.wait("the peers' pushes into this shard (exchange, second barrier)");
+    if (rc2 == GG_ERR_INTERNAL) gg::set_last_error("exchange aborted: another shard failed");
     const auto t3 = clk::now();
     auto& T = m->times[r];
     if (T.nx < GG_MPK_MAX_EXCHANGES) {
@@ -173,7 +151,7 @@ int mpk_exchange(void* ctx, const void* send_dev, void* recv_dev, size_t bytes) 
         T.mbytes[T.nx] = pushed / 1e6;
     }
     T.nx++;
-    return ok2 ? 0 : GG_ERR_INTERNAL;
+    return rc2;
 }
 
 // identity partials (Jacobian infinity: x = y = 1, z = 0 in Montgomery form --
@@ -203,6 +181,7 @@ void on_shards(gg_groth16_mpk* m, Fn fn) {
     std::mutex emu;
     std::string err;
     int code = GG_OK;
+    bool echo_only = false;
     std::vector<std::thread> th;
     for (int r = 0; r < m->world; r++)
         th.emplace_back([&, r] {
@@ -215,8 +194,11 @@ void on_shards(gg_groth16_mpk* m, Fn fn) {
             if (rc) {
                 m->bar.abort();
                 std::lock_guard<std::mutex> g(emu);
-                if (code == GG_OK) {
+                // the failing shard's own error wins over its peers' "another shard failed"
+                const bool echo = msg.find("another shard failed") != std::string::npos;
+                if (code == GG_OK || (echo_only && !echo)) {
                     code = rc;
+                    echo_only = echo;
                     err = "shard " + std::to_string(r) + " (device " + std::to_string(m->dev[r]) + "): " + msg;
                 }
             }
@@ -588,11 +570,16 @@ extern "C" int gg_groth16_mpk_set_rehearsal(gg_groth16_mpk_t m, int solo_shard) 
     GG_CHECK(solo_shard >= -1 && solo_shard < m->world, GG_ERR_INVALID_ARG, "solo shard out of range");
     std::lock_guard<std::mutex> lk(m->mu);
     // shards sharing a device share its dedicated hardware queues (common.h
-    // create_task_stream): the solo shard gets them, as on a node
+    // task_streams_switch): the solo shard gets them, as on a node
     if (solo_shard >= 0 && solo_shard != m->solo) {
         for (int r = 0; r < m->world; r++)
             if (r != solo_shard && m->dev[r] == m->dev[solo_shard]) gg::g16_restream(m->pk[r], false);
         gg::g16_restream(m->pk[solo_shard], true);
+    } else if (solo_shard < 0 && m->solo >= 0) {
+        // back to the creation layout: every shard released, then
+        // re-created in shard order, as gg_groth16_mpk_create placed them
+        for (int r = 0; r < m->world; r++) gg::g16_restream(m->pk[r], false);
+        for (int r = 0; r < m->world; r++) gg::g16_restream(m->pk[r], true);
     }
     m->solo = solo_shard;
     GG_CAPI_END

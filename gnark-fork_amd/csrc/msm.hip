@@ -1,5 +1,6 @@
 // C ABI of the MSM engine (see msm_impl.cuh for the algorithm).
 #include "msm_impl.cuh"
+#include <cmath>
 
 namespace gg {
 void create_base_g1(gg_msm_base* b, const void* points, size_t n, int on_device,
@@ -150,7 +151,7 @@ void msm_build_bmap(const gg_msm_base* a, const gg_msm_base* b, DevBuf& bmap) {
                            b->sidx.as<uint32_t>(), b->n, (uint32_t)a->n, bmap.as<uint32_t>());
         GG_HIP(hipGetLastError());
     }
-    GG_HIP(hipStreamSynchronize(hipStreamPerThread));
+    GG_WAIT_STREAM(hipStreamPerThread);
 }
 bool msm_derivable(const gg_msm_base* a, const gg_msm_base* b) {
     if (a->c != b->c || a->W != b->W || a->G != b->G || a->has_sidx || !b->has_sidx) return false;
@@ -160,6 +161,18 @@ bool msm_derivable(const gg_msm_base* a, const gg_msm_base* b) {
 }
 MsmSort* msm_work_sort(MsmWork* w) { return &w->sort; }
 MsmScratch* msm_work_scratch(MsmWork* w) { return &w->scr; }
+// A batch's sort counts and positions nvec W n entries and numbers kp G 2^(c-1)
+// buckets (kp = the power of two >= nvec) in 32-bit words whose bit 31 is a
+// digit's sign and whose all-ones value means "no key" (W n alone is
+// checked at base creation; a batch multiplies both).
+bool msm_batch_fits(size_t n, int W, int c, int G, int nvec) {
+    int kp = 1;
+    while (kp < nvec) kp <<= 1;
+    const double entries = (double)W * (double)n * (double)nvec;
+    const double buckets = (double)G * std::ldexp(1.0, c - 1) * (double)kp;
+    return entries + 64.0 < 4294967296.0 && buckets < 2147483648.0;
+}
+bool msm_base_batch_fits(const gg_msm_base* b, int nvec) { return msm_batch_fits(b->n, b->W, b->c, b->G, nvec); }
 size_t msm_scalars_needed(gg_msm_base* b) {
     return b->has_sidx ? (b->n ? (size_t)b->max_sidx + 1 : 0) : b->n;
 }
@@ -182,6 +195,7 @@ extern "C" int gg_msm(gg_msm_base_t b, const void* scalars, size_t n_scalars, in
         sdev = b->own.scr.scal.as<Fr>();
     }
     msm_device_locked(b, sdev, out_jac, st);
+    GG_PROBE_GUARD();
     GG_CAPI_END
 }
 
@@ -197,6 +211,8 @@ extern "C" int gg_msm_batch(gg_msm_base_t b, const void* const* scalars, int n_v
         GG_CHECK(need == 0 || scalars[v], GG_ERR_INVALID_ARG, "null scalars");
         GG_CHECK(out_jac[v], GG_ERR_INVALID_ARG, "null out_jac");
     }
+    GG_CHECK(msm_base_batch_fits(b, n_vectors), GG_ERR_UNSUPPORTED,
+             "MSM batch too large for 32-bit sort indices (gg_msm_batch_shape); use one MSM per vector");
     std::lock_guard<std::mutex> lk(b->mu);
     const Fr* sdev[kMaxBatch] = {};
     if (!scalars_on_device && need) {
@@ -209,6 +225,7 @@ extern "C" int gg_msm_batch(gg_msm_base_t b, const void* const* scalars, int n_v
         for (int v = 0; v < n_vectors; v++) sdev[v] = (const Fr*)scalars[v];
     }
     msm_device_work_batch(b, &b->own, sdev, n_vectors, out_jac, st);
+    GG_PROBE_GUARD();
     GG_CAPI_END
 }
 
@@ -236,5 +253,17 @@ extern "C" int gg_msm_stripe(gg_msm_base_t b, const void* scalars, size_t n_scal
     }
     msm_prepare_dev(b, &b->own.sort, sdev, st, stripe_log, (uint32_t)stripe_part);
     msm_finish_dev(b, &b->own.sort, out_jac, st, nullptr);
+    GG_PROBE_GUARD();
+    GG_CAPI_END
+}
+
+extern "C" int gg_msm_batch_shape(size_t n_points, int window_bits, int n_windows, int groups, int n_vectors) {
+    GG_CAPI_BEGIN
+    GG_CHECK(window_bits >= 2 && window_bits <= 30 && n_windows >= 1 && groups >= 1 && (groups & (groups - 1)) == 0,
+             GG_ERR_INVALID_ARG, "window_bits 2..30, n_windows >= 1, groups a power of two");
+    GG_CHECK(n_vectors >= 1 && n_vectors <= kMaxBatch, GG_ERR_INVALID_ARG, "n_vectors must be 1..4");
+    GG_CHECK(msm_batch_fits(n_points, n_windows, window_bits, groups, n_vectors), GG_ERR_UNSUPPORTED,
+             "MSM batch too large for 32-bit sort indices: n_vectors * n_windows * n_points entries must stay "
+             "below 2^32 and n_vectors' bucket spaces below 2^31 buckets; use one MSM per vector");
     GG_CAPI_END
 }

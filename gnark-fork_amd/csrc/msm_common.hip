@@ -787,6 +787,8 @@ void msm_prepare_batch(const gg_msm_base* b, MsmSort* s, const VecPtrs& vp, int 
              "bucket stripe out of range (stripe_log <= window_bits - 2, part < 2^stripe_log)");
     GG_CHECK(nvec >= 1 && nvec <= kMaxBatch && (nvec == 1 || slog == 0), GG_ERR_INVALID_ARG,
              "batch of 1..4 scalar vectors (no bucket stripes)");
+    GG_CHECK(nvec == 1 || msm_batch_fits(b->n, b->W, b->c, b->G, nvec), GG_ERR_UNSUPPORTED,
+             "MSM batch too large for 32-bit sort indices (gg_msm_batch_shape)");
     s->slog = slog;
     s->sres = sres;
     s->nvec = nvec;

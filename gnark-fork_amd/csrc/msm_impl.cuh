@@ -102,6 +102,8 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const VecPtrs& vp, hipStream
 // b mod 2^slog = sres, see MsmSort)
 void msm_prepare(const gg_msm_base* b, MsmSort* s, const Fr* scalars_dev, hipStream_t st, int slog = 0,
                  uint32_t sres = 0);
+// does a batch of nvec vectors over a base of this shape fit the sort's 32-bit words (msm.hip)
+bool msm_batch_fits(size_t n, int W, int c, int G, int nvec);
 void msm_prepare_batch(const gg_msm_base* b, MsmSort* s, const VecPtrs& vp, int nvec, hipStream_t st, int slog = 0,
                        uint32_t sres = 0);
 // b's sort from a's (same window layout, a indexes its scalars directly, bmap:
@@ -301,6 +303,42 @@ struct LdsRing {
         return r;
     }
 };
+// The sorted entries of an LDS-ring accumulation, read in 16-B chunks (round 6).
+// The ring loops of round 5 loaded one 4-B entry and one bucket boundary per
+// step: each lane's next entry sits K entries away from its neighbour's, so every
+// such load touches a line of its own, and the point gathers streaming through
+// L2 evict it between a lane's steps -- 2.3 GB of re-fetches per 2^24 G1 launch
+// above the register loop's (r05_z2 vs r05_z3 PMC: 14.89 -> 17.23 GB FETCH).
+// Here a lane holds two chunks: c0 with the entry the next gather needs, c1 the
+// four after it, loaded four steps before use.  Step i is the same on every lane
+// of a wave (all start at their e0 together), so the reload is a uniform branch;
+// K is a multiple of 4 (msm_finish_multi), so e0 and every chunk are 16-B aligned.
+// GG_RING_CHUNKS=0 builds round 5's per-step loads (A/B).
+// BN254 G2 (256 VGPRs at two waves per SIMD) keeps its per-step entry loads:
+// the chunks' 8 VGPRs spill 196 instead of 16 B there (GG_RING_CHUNKS_G2=1).
+#ifndef GG_RING_CHUNKS
+#define GG_RING_CHUNKS 1
+#endif
+#ifndef GG_RING_CHUNKS_G2
+#define GG_RING_CHUNKS_G2 0
+#endif
+struct EntryChunks {
+    uint4 c0, c1;
+    // entries e0 .. e0 + 7 (the sorted list has 64 B of slack past its end)
+    __device__ __forceinline__ EntryChunks(const uint32_t* sorted, uint32_t e0)
+        : c0(chunk_ld(sorted, e0)), c1(chunk_ld(sorted, e0 + 4)) {}
+    // step i (uniform): the chunk holding entry e0 + i + 2 moves into c0 when that
+    // entry starts a chunk, and the chunk after it is requested; issue this before
+    // the step's gather, so the wait for that gather covers the load
+    __device__ __forceinline__ void advance(const uint32_t* sorted, uint32_t e0, uint32_t i) {
+        if (((i + 2) & 3u) == 0) {
+            c0 = c1;
+            c1 = chunk_ld(sorted, e0 + i + 6);
+        }
+    }
+    // entry e0 + i + 2 (after advance(i))
+    __device__ __forceinline__ uint32_t next2(uint32_t i) const { return chunk_at(c0, (i + 2) & 3u); }
+};
 // BN254 G2 (128-B points), BLS12-381 G1 (96-B) and BN254 G1 (64-B) take the LDS
 // ring.  BN254 G1 too since r05w: 149 instead of 164 VGPRs, three waves per
 // SIMD either way, the one-GPU 2^24 prove 106.8 / 106.8 vs 108.8 / 108.7 ms,
@@ -347,9 +385,44 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
         // 14 x 28 bits); the base holds x R' mod p, partials leave in radix form
         using C = typename RadixOf<F>::C;
         XyzzL<C> acc = inf_l<C>();
-        if constexpr (kLdsGather<F>) {  // BLS12-381 G1: 96-B points through the LDS ring
+        if constexpr (kLdsGather<F>) {  // 64-B (BN254) / 96-B (BLS12-381) points through the LDS ring
             extern __shared__ uint4 acc_lds[];
             const LdsRing<sizeof(Affine<F>) / 16> ring(acc_lds);
+#if GG_RING_CHUNKS
+            EntryChunks ec(sorted, e0);
+            uint32_t v = ec.c0.x, vn = ec.c0.y;
+            ring.gather(pts + (v & pmask), 0);
+            for (uint32_t i = 0;; i++) {
+                const uint32_t e = e0 + i;
+                if (e >= e1) break;
+                const uint32_t sl = i & 1u;
+                const Affine<F> qp = ring.template read<Affine<F>>(sl);
+                const uint32_t cv = v;
+                if (e == bnd) {  // before the gather (see the Fp2 branch)
+                    range_store(acc, seg0 == e0, false, q, c, t, head, tail, S);
+                    acc = inf_l<C>();
+                    seg0 = e;
+                    q++;
+                    bnd = bnd2;
+                    if (bnd == e) {
+                        uint32_t b2;
+                        do {
+                            q++;
+                            b2 = offsets[min(q + 1, nb)];
+                        } while (b2 == e);
+                        bnd = b2;
+                    }
+                }
+                ec.advance(sorted, e0, i);
+                const uint32_t nidx = (e + 1 < e1) ? vn : v;
+                ring.gather(pts + (nidx & pmask), sl ^ 1u);
+                v = nidx;
+                vn = ec.next2(i);
+                // every step, after the gather: loaded at the flush instead, its
+                // value is copied into the loop-carried register at once, which
+                // waits for it (ISA); a wave's lanes share 2-3 lines of offsets
+                bnd2 = offsets[min(q + 2, nb)];
+#else
             const uint32_t elast = e1 - 1;
             uint32_t v = sorted[e0], vn = sorted[min(e0 + 1, elast)];
             ring.gather(pts + (v & pmask), 0);
@@ -377,6 +450,7 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                 v = nidx;
                 vn = sorted[min(e + 2, elast)];
                 bnd2 = offsets[min(q + 2, nb)];
+#endif
                 if (skip_inf && qp.is_inf()) continue;
                 const Fl<C> x = unpack_l<C>(qp.x);
                 Fl<C> y = unpack_l<C>(qp.y);
@@ -486,11 +560,21 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
         extern __shared__ uint4 acc_lds[];
         const LdsRing<8> ring(acc_lds);
         Xyzz2_29 acc = inf2_29();
+#if GG_RING_CHUNKS_G2
+        EntryChunks ec(sorted, e0);
+        uint32_t v = ec.c0.x, vn = ec.c0.y;
+        ring.gather(pts + (v & pmask), 0);
+        for (uint32_t i = 0;; i++) {
+            const uint32_t e = e0 + i;
+            if (e >= e1) break;
+            const uint32_t s = i & 1u;
+#else
         const uint32_t elast = e1 - 1;
         uint32_t v = sorted[e0], vn = sorted[min(e0 + 1, elast)];
         ring.gather(pts + (v & pmask), 0);
         for (uint32_t e = e0; e < e1; e++) {
             const uint32_t s = (e - e0) & 1u;
+#endif
             const Affine<F> pt = ring.template read<Affine<F>>(s);
             const uint32_t cv = v;
             if (e == bnd) {
@@ -508,10 +592,18 @@ __global__ void __launch_bounds__(256, kAccumWaves<F>) k_accum_range(const Affin
                     bnd = b2;
                 }
             }
+#if GG_RING_CHUNKS_G2
+            ec.advance(sorted, e0, i);
+            const uint32_t nidx = (e + 1 < e1) ? vn : v;  // the last step re-gathers its own point
+            ring.gather(pts + (nidx & pmask), s ^ 1u);
+            v = nidx;
+            vn = ec.next2(i);
+#else
             const uint32_t nidx = (e + 1 < e1) ? vn : v;  // the last step re-gathers its own point
             ring.gather(pts + (nidx & pmask), s ^ 1u);
             v = nidx;
             vn = sorted[min(e + 2, elast)];
+#endif
             bnd2 = offsets[min(q + 2, nb)];
 #endif
             if (skip_inf && pt.is_inf()) continue;
@@ -1061,7 +1153,7 @@ inline void precompute(gg_msm_base* b, const Affine<F>* dev_in, hipStream_t st) 
         hipLaunchKernelGGL(k_to_radix<C>, dim3(grid_for(total, 256)), dim3(256), 0, st, (E*)out, total);
         GG_HIP(hipGetLastError());
     }
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
 }
 
 // One term of a batched reduction: 2^mlog * sum_j (j + off) X_j over n = 2^k
@@ -1209,7 +1301,7 @@ inline std::vector<Xyzz<F>> reduce_terms_multi(std::vector<RedItem<F>> items, in
         GG_HIP(hipGetLastError());
         GG_HIP(hipMemcpyAsync(flat.data(), stage, flat.size() * XB, hipMemcpyDeviceToHost, st));
     }
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     std::vector<std::vector<Xyzz<F>>> hx(host_items.size());
     for (size_t k = 0; k < host_items.size(); k++)
         hx[k].assign(flat.begin() + GL.off[k], flat.begin() + GL.off[k + 1]);
@@ -1320,10 +1412,13 @@ inline void msm_finish_multi(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStr
     if (slog) {
         // a stripe holds ~2^-slog of the entries: wait for the sort's count so
         // the ranges fill the chip for the entries there are
-        GG_HIP(hipEventSynchronize(s->pin_ev));
+        GG_WAIT_EVENT(s->pin_ev);
         E = std::max<size_t>(s->pin[1], 1);
     }
-    const uint32_t K = range_length<F>(E);
+    uint32_t K = range_length<F>(E);
+    // the LDS-ring loops read their entries in aligned 16-B chunks (EntryChunks)
+    if constexpr (kLdsGather<F>)
+        if ((std::is_same<F, Fp2>::value ? GG_RING_CHUNKS_G2 : GG_RING_CHUNKS) != 0) K = (K + 3u) & ~3u;
     const size_t T = (E + K - 1) / K;  // ranges
     using PT = typename PartialOf<F>::T;
     constexpr bool kRadixP = !std::is_same<PT, Xyzz<F>>::value;  // partials in the accumulator's form
@@ -1370,7 +1465,7 @@ inline void msm_finish_multi(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStr
         GG_HIP(hipGetLastError());
         ps_acc.stop(st);
     }
-    GG_HIP(hipEventSynchronize(s->pin_ev));
+    GG_WAIT_EVENT(s->pin_ev);
     const uint32_t maxcnt = s->pin[0];
     // ranges after the first one of the fullest bucket (upper bound)
     const uint32_t max_ranges = maxcnt / K + 1;
@@ -1560,7 +1655,7 @@ inline void create_base_dev(gg_msm_base* b, const Affine<F>* pts, size_t n, int 
     GG_HIP(hipMemcpyAsync(&last_pos, pos.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, st));
     GG_HIP(hipMemcpyAsync(&last_keep, keep.as<uint32_t>() + (n - 1), 4, hipMemcpyDeviceToHost, st));
     GG_HIP(hipMemcpyAsync(&any_inf, flag.p, 4, hipMemcpyDeviceToHost, st));
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     const size_t kept = (size_t)last_pos + last_keep;
     b->n = kept;
     b->has_inf = keep_inf && any_inf;
@@ -1578,7 +1673,7 @@ inline void create_base_dev(gg_msm_base* b, const Affine<F>* pts, size_t n, int 
     GG_HIP(hipGetLastError());
     uint32_t max_idx = 0;  // indices increase: the last kept one is the largest
     GG_HIP(hipMemcpyAsync(&max_idx, idx.as<uint32_t>() + (kept - 1), 4, hipMemcpyDeviceToHost, st));
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     b->max_sidx = max_idx;
     if (dropped) b->sidx = std::move(idx);
     precompute<F>(b, cmp.as<Affine<F>>(), st);

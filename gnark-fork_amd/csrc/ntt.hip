@@ -682,7 +682,7 @@ extern "C" int gg_groth16_compute_h(gg_domain_t d, const void* a, const void* b,
         if (len < d->n) GG_HIP(hipMemsetAsync((char*)dst[i] + len * 32, 0, nb - len * 32, st));
     }
     compute_h_device(d, A, B, C, (Fr*)h_dev, st);
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     GG_CAPI_END
 }
 
@@ -1201,9 +1201,13 @@ void hshard_run(gg_hshard* hs, const Fr* a, const Fr* b, const Fr* c, size_t len
                 Fr* recv, gg_exchange_fn xchg, void* ctx, hipStream_t st) {
     std::lock_guard<std::mutex> lk(hs->mu);  // y / hblk / ccoef are per-handle scratch
     auto exchange = [&](int phase) {
-        GG_HIP(hipStreamSynchronize(st));
+        GG_WAIT_STREAM(st);
+        set_last_error("");
         int rc = xchg(ctx, send, recv, hshard_exchange_bytes(hs, phase));
-        GG_CHECK(rc == 0, GG_ERR_INTERNAL, "exchange callback failed");
+        if (rc == GG_ERR_TIMEOUT) throw Error(rc, gg_last_error());  // the one-process barrier's deadline
+        const std::string why = gg_last_error();
+        GG_CHECK(rc == 0, GG_ERR_INTERNAL,
+                 "exchange callback failed after phase " + std::to_string(phase) + (why.empty() ? "" : ": " + why));
     };
     hshard_phase1(hs, a, b, c, len, send, st, compact);
     exchange(1);
@@ -1278,6 +1282,6 @@ extern "C" int gg_hshard_phase(gg_hshard_t hs, int phase, const void* a, const v
         else if (phase == 4) hshard_phase4(hs, (const Fr*)recv, (Fr*)send_or_h, st);
         else throw Error(GG_ERR_INVALID_ARG, "phase must be 1..4");
     }
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     GG_CAPI_END
 }

@@ -316,7 +316,7 @@ extern "C" int gg_plonk_divide_by_xn_minus_one(gg_domain_t big, size_t n_small, 
     GG_CHECK(big && data_dev, GG_ERR_INVALID_ARG, "null argument");
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : hipStreamPerThread;
     plk::divide_by_xn_minus_one(big, n_small, (FrB*)data_dev, st);
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     GG_CAPI_END
 }
 
@@ -328,6 +328,6 @@ extern "C" int gg_bls12_381_fr_batch_invert(void* data_dev, size_t n, void* hip_
     Arena ar;
     ar.reserve(plk::batch_invert_arena_bytes(n));
     plk::batch_invert((FrB*)data_dev, n, st, ar);
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     GG_CAPI_END
 }

@@ -704,7 +704,7 @@ extern "C" int gg_bls12_381_fr_prefix_product(void* data_dev, size_t n, void* hi
     Arena ar;
     ar.reserve(plk::scan_arena_bytes(n));
     plk::scan_prod((FrB*)data_dev, n, st, ar);
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     GG_CAPI_END
 }
 
@@ -722,7 +722,7 @@ extern "C" int gg_bls12_381_fr_horner(const void* f_dev, size_t n, const void* a
     FrB* v = ar.get<FrB>(1);
     plk::horner((const FrB*)f_dev, n, frb(a_mont), (FrB*)q_dev, v, st, ar);
     GG_HIP(hipMemcpyAsync(value_out, v, 32, hipMemcpyDeviceToHost, st));
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     GG_CAPI_END
 }
 
@@ -750,7 +750,7 @@ extern "C" int gg_fr_evaluate_many(int curve, const void* const* polys_dev, cons
     };
     if (curve == GG_CURVE_BN254) run(Fr{});
     else run(FrB{});
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     GG_CAPI_END
 }
 
@@ -771,7 +771,7 @@ extern "C" int gg_plonk_ratio_copy_constraint(const void* l_dev, const void* r_d
     ar.reserve(plk::ratio_arena_bytes(n));
     plk::ratio((const FrB*)l_dev, (const FrB*)r_dev, (const FrB*)o_dev, perm_dev, n, frb(beta), frb(gamma), w,
                frb(coset_shift_mont), (FrB*)z_dev, st, ar);
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     GG_CAPI_END
 }
 
@@ -781,7 +781,7 @@ extern "C" int gg_plonk_fold_h(const void* h_dev, size_t n_small, const void* ze
     GG_CHECK(h_dev && zeta_pow_np2 && out_dev, GG_ERR_INVALID_ARG, "null argument");
     hipStream_t st = pick(hip_stream);
     plk::fold_h((const FrB*)h_dev, n_small, frb(zeta_pow_np2), (FrB*)out_dev, st);
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     GG_CAPI_END
 }
 
@@ -816,7 +816,7 @@ extern "C" int gg_plonk_linearized(void* blinded_z_dev, size_t nz, const void* s
     for (int k = 0; k < 8; k++) *dst[k] = frb(s + 32 * k);
     hipStream_t st = pick(hip_stream);
     plk::linearized(P, st);
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     GG_CAPI_END
 }
 
@@ -826,7 +826,7 @@ extern "C" int gg_bls12_381_fr_bit_reverse(const void* in_dev, void* out_dev, si
     GG_CHECK(n >= 1 && (n & (n - 1)) == 0 && n <= ((size_t)1 << 31), GG_ERR_INVALID_ARG, "n must be a power of 2");
     hipStream_t st = pick(hip_stream);
     plk::bit_reverse((const FrB*)in_dev, (FrB*)out_dev, n, st);
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     GG_CAPI_END
 }
 
@@ -837,6 +837,6 @@ extern "C" int gg_bls12_381_fr_axpy(void* y_dev, const void* x_dev, size_t n, co
     if (n == 0) return GG_OK;
     hipStream_t st = pick(hip_stream);
     plk::axpy((FrB*)y_dev, (const FrB*)x_dev, n, frb(a_mont), st);
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     GG_CAPI_END
 }

@@ -47,6 +47,7 @@ void msm_device_work_batch(gg_msm_base* b, MsmWork* w, const Fr* const* scalars_
                            hipStream_t st);
 MsmWork* msm_work_new();
 void msm_work_delete(MsmWork* w);
+bool msm_base_batch_fits(const gg_msm_base* b, int nvec);
 }  // namespace gg
 
 using namespace gg;
@@ -168,6 +169,8 @@ struct QUnit {
 struct PlonkPeer {
     int device = 0;
     hipStream_t s[4] = {nullptr, nullptr, nullptr, nullptr};  // 0..2: MSMs (work slot), 3: cosets
+    TaskQueue tq[4];                                          // the slots behind s (common.h)
+    hipStream_t* act[4] = {&s[0], &s[1], &s[2], &s[3]};
     gg_msm_base_t kzg = nullptr, kzg_lag = nullptr;
     size_t k_lo = 0, k_hi = 0, l_lo = 0, l_hi = 0;
     MsmWork* work[3] = {nullptr, nullptr, nullptr};
@@ -217,7 +220,7 @@ struct PlonkPeer {
         perm_slice.release();
         pz.release();
         ar.buf.release();
-        for (hipStream_t x : s) destroy_task_stream(x);
+        task_streams_release(tq, 4);
         for (int i = 0; i < 4; i++) {
             if (ea[i]) (void)hipEventDestroy(ea[i]);
             if (eb[i]) (void)hipEventDestroy(eb[i]);
@@ -383,11 +386,19 @@ struct Key : gg_plonk_pk {
     // its work, the proof is not valid and gg_plonk_prove returns GG_REHEARSAL
     bool solo = false;
     int solo_part = 0;
+    // device parts' task streams on hardware queues of their own (task_streams_init):
+    // creation layout = part order while the device's GG_TASK_QUEUES last; a
+    // rehearsal of part p gives p's device's queues to p (restream), -1 restores
+    // the creation layout (GG_PLONK_PART_QUEUES=1)
+    bool part_queues = false;
+    int queue_owner = -1;  // part holding its device's dedicated queues (-1: creation layout)
     std::mutex tmu;
     std::vector<PlonkPartTimes> ptimes;  // [part], last proof
     std::vector<int> peer_codes;         // GG_PEER_* per ordered part pair (one-process parts)
     int n_cmt = 0;
     hipStream_t s[4] = {nullptr, nullptr, nullptr, nullptr};
+    TaskQueue tq[4];  // the slots behind s (common.h: own stream + borrowed dedicated queue)
+    hipStream_t* act[4] = {&s[0], &s[1], &s[2], &s[3]};
     MsmWork* work[3] = {nullptr, nullptr, nullptr};
     hipEvent_t msm_ready[3] = {nullptr, nullptr, nullptr};  // per work slot: its scalars are complete
     Arena ar[4];
@@ -412,7 +423,7 @@ struct Key : gg_plonk_pk {
         if (d0) gg_domain_release(d0);
         if (d1) gg_domain_release(d1);
         units.clear();
-        for (hipStream_t x : s) destroy_task_stream(x);
+        task_streams_release(tq, 4);
     }
 };
 
@@ -513,7 +524,7 @@ static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStr
             if (part_runs(pk, (int)q + 1))
                 fs.push_back(std::async(std::launch::async, [pk, q, pp = pk->peers[q].get(), kz, wi, scal, peer_resident,
                                                              ready] {
-                    if (!peer_resident) GG_HIP(hipEventSynchronize(ready));
+                    if (!peer_resident) GG_WAIT_EVENT(ready);
                     return peer_msm(pk, (int)q + 1, pp, kz, wi, scal, peer_resident);
                 }));
     }
@@ -545,6 +556,15 @@ static BJac commit_kzg(Key* pk, int wi, const FrB* scal, hipStream_t st) { retur
 static bool plonk_batch() {
     static const bool on = !(getenv("GG_PLONK_BATCH") && atoi(getenv("GG_PLONK_BATCH")) == 0);
     return on;
+}
+// the batch on every part's slice of the base fits the sort's 32-bit words
+// (gg_msm_batch_shape); else the three MSMs run one per stream
+static bool batch_ok(Key* pk, bool kzg, int nv) {
+    if (!plonk_batch()) return false;
+    if (!msm_base_batch_fits(kzg ? pk->kzg : pk->kzg_lag, nv)) return false;
+    for (auto& p : pk->peers)
+        if (!msm_base_batch_fits(kzg ? p->kzg : p->kzg_lag, nv)) return false;
+    return true;
 }
 static void peer_msm_batch(Key* pk, int part, PlonkPeer* p, bool kzg, const FrB* const* scal, int nv, BJac* out) {
     GG_HIP(hipSetDevice(p->device));
@@ -585,7 +605,7 @@ static void msm_jac_batch(Key* pk, gg_msm_base_t base, const FrB* const* scal, i
         for (size_t q = 0; q < pk->peers.size(); q++)
             if (part_runs(pk, (int)q + 1))
                 fs.push_back(std::async(std::launch::async, [pk, q, pp = pk->peers[q].get(), kz, sc, nv, ready] {
-                    GG_HIP(hipEventSynchronize(ready));
+                    GG_WAIT_EVENT(ready);
                     std::vector<BJac> r(nv);
                     peer_msm_batch(pk, (int)q + 1, pp, kz, sc.data(), nv, r.data());
                     return r;
@@ -636,7 +656,7 @@ static BJac blind_commit(Key* pk, const std::vector<FrB>& b) {
 static FrB fetch(const FrB* dev, hipStream_t st) {
     FrB v;
     GG_HIP(hipMemcpyAsync(v.v, dev, 32, hipMemcpyDeviceToHost, st));
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     return v;
 }
 static FrB eval_dev(Key* pk, const FrB* f, size_t len, const FrB& a, FrB* q, FrB* slot, int ai, hipStream_t st) {
@@ -652,7 +672,7 @@ static std::vector<FrB> eval_batch(Key* pk, const FrB* const* f, const size_t* l
     plk::eval_many(f, len, count, a, slot, st, pk->ar[ai]);
     std::vector<FrB> v(count);
     GG_HIP(hipMemcpyAsync(v.data(), slot, 32 * (size_t)count, hipMemcpyDeviceToHost, st));
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     return v;
 }
 
@@ -685,13 +705,13 @@ static void canon_run(Key* pk, size_t pi, int b, FrB* brev0, FrB* reg0, const st
     const auto a = std::chrono::steady_clock::now();
     hipStream_t q = p->cs;
     if (p->reg_pending) {  // creg is read by the previous task's regular push
-        GG_HIP(hipEventSynchronize(p->reg_ev));
+        GG_WAIT_EVENT(p->reg_ev);
         p->reg_pending = false;
     }
     fill(q);
     plk::ntt(p->d0, p->in[b].p, 1, 0, 0, q);  // FFTInverse DIF: natural in -> bit-reversed out
     if (reg0) plk::bit_reverse(F(p->in[b]), F(p->creg), n, q);
-    GG_HIP(hipStreamSynchronize(q));
+    GG_WAIT_STREAM(q);
     size_t x = 0;
     double mb = 0;
     for (auto& o : pk->peers)
@@ -707,7 +727,7 @@ static void canon_run(Key* pk, size_t pi, int b, FrB* brev0, FrB* reg0, const st
         p->reg_pending = true;
     }
     mb += (reg0 ? 2.0 : 1.0) * nb / 1e6;
-    for (size_t i = 0; i < x; i++) GG_HIP(hipStreamSynchronize(p->xs[i]));
+    for (size_t i = 0; i < x; i++) GG_WAIT_STREAM(p->xs[i]);
     std::lock_guard<std::mutex> lk(pk->tmu);
     PlonkPartTimes& T = pk->ptimes[pi + 1];
     T.canon_count += 1;
@@ -720,7 +740,7 @@ static void canon_wait_regular(Key* pk) {
     for (auto& pp : pk->peers) {
         PlonkPeer* p = pp.get();
         if (!p->reg_pending) continue;
-        GG_HIP(hipEventSynchronize(p->reg_ev));
+        GG_WAIT_EVENT(p->reg_ev);
         p->reg_pending = false;
     }
 }
@@ -755,6 +775,38 @@ static std::vector<double> plonk_part_shares(int n_devices, int n_cmt) {
     for (double x : f) tot += x;
     for (double& x : f) x /= tot;
     return f;
+}
+
+// GG_PLONK_PART_QUEUES=1: device parts' task streams on dedicated hardware queues
+static bool part_queues_enabled() {
+    const char* e = getenv("GG_PLONK_PART_QUEUES");
+    return e && atoi(e) == 1;
+}
+// part q's four task slots on dedicated queues or their own streams (between
+// proofs; no stream is created or destroyed: common.h TaskQueue)
+static void restream_part(Key* pk, int q, bool dedicated) {
+    if (q == 0) task_streams_switch(pk->act, pk->tq, 4, pk->device, dedicated);
+    else task_streams_switch(pk->peers[q - 1]->act, pk->peers[q - 1]->tq, 4, pk->peers[q - 1]->device, dedicated);
+}
+// the queue layout for a rehearsal of `part` (-1: none): its device's dedicated
+// queues go to it, as on a node where it is alone on its GPU; -1 restores the
+// creation layout (every part released first, then re-created in part order)
+static void queue_layout(Key* pk, int part) {
+    if (!pk->part_queues || part == pk->queue_owner) return;
+    int cur = 0;
+    GG_HIP(hipGetDevice(&cur));
+    const int np = 1 + (int)pk->peers.size();
+    auto dev_of = [&](int q) { return q == 0 ? pk->device : pk->peers[q - 1]->device; };
+    if (part >= 0) {
+        for (int q = 0; q < np; q++)
+            if (q != part && dev_of(q) == dev_of(part)) restream_part(pk, q, false);
+        restream_part(pk, part, true);
+    } else {  // the creation layout: dedicated queues in part order while they last
+        for (int q = 0; q < np; q++) restream_part(pk, q, false);
+        for (int q = 0; q < np; q++) restream_part(pk, q, true);
+    }
+    pk->queue_owner = part;
+    GG_HIP(hipSetDevice(cur));
 }
 
 static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, const void* omega_big,
@@ -832,13 +884,11 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
     while ((1 << pk->log_u) < pk->U) pk->log_u++;
     pk->split_idft = log_big >= 12;
     // a one-device key's four streams on hardware queues of their own (common.h
-    // create_task_stream: 125.9 vs 127.5-128.1 ms at 2^22, profiles/r05_l_*); a
-    // key with device parts keeps HIP's shared pool -- its 8-part rehearsal on
-    // one GPU stalled on dedicated queues (r05k)
-    for (hipStream_t& x : pk->s) {
-        if (n_devices <= 1) create_task_stream(&x, pk->device);
-        else GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
-    }
+    // TaskQueue: 125.9 vs 127.5-128.1 ms at 2^22, profiles/r05_l_*); a key with
+    // device parts on them only with GG_PLONK_PART_QUEUES=1 (r05k's stall, in the
+    // stream re-creation its rehearsal did then: DESIGN.md §5)
+    pk->part_queues = n_devices > 1 && part_queues_enabled();
+    task_streams_init(pk->act, pk->tq, 4, pk->device, n_devices <= 1 || pk->part_queues);
     for (auto& w : pk->work) w = msm_work_new();
     for (hipEvent_t& e : pk->msm_ready) GG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     hipStream_t st = pk->s[0];
@@ -867,7 +917,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
                 p->l_lo = bound(n, d);
                 p->l_hi = bound(n, d + 1);
                 GG_HIP(hipSetDevice(p->device));
-                for (hipStream_t& x : p->s) GG_HIP(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+                task_streams_init(p->act, p->tq, 4, p->device, pk->part_queues);
                 gg::create_copy_stream(&p->cps);
                 GG_HIP(hipEventCreateWithFlags(&p->cpev, hipEventDisableTiming));
                 for (int e = 0; e < 4; e++) {
@@ -928,7 +978,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
         plk::ntt(pk->d0, t.p, 0, 0, 0, st);  // FFT DIF: natural in -> bit-reversed out
         pk->qk_lag.alloc(nb);
         plk::bit_reverse(F(t), F(pk->qk_lag), n, st);
-        GG_HIP(hipStreamSynchronize(st));
+        GG_WAIT_STREAM(st);
     }
     // s.twiddles0 = w^j: DIT FFT of the coefficients of X (bit-reversed layout)
     // (every upload below is ordered on st and waited for: a plain hipMemcpy runs
@@ -937,7 +987,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
     zero(pk->tw0.p, nb, st);
     const FrB one = FrB::one();
     GG_HIP(hipMemcpyAsync(F(pk->tw0) + n / 2, one.v, 32, hipMemcpyHostToDevice, st));
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     plk::ntt(pk->d0, pk->tw0.p, 0, 1, 0, st);
     // resident coset evaluations of the key's polynomials (the reference redoes
     // these 2 rho FFTs per polynomial per proof, prove.go:995-1017)
@@ -947,14 +997,14 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
     {
         std::vector<FrB> v(n, pk->n_inv);  // LOne canonical: 1/n everywhere
         GG_HIP(hipMemcpyAsync(lone.p, v.data(), nb, hipMemcpyHostToDevice, st));
-        GG_HIP(hipStreamSynchronize(st));
+        GG_WAIT_STREAM(st);
     }
     std::vector<const FrB*> srcs = {F(pk->brev[Key::QL]), F(pk->brev[Key::QR]),
                                     F(pk->brev[Key::QM]), F(pk->brev[Key::QO]),
                                     F(pk->brev[Key::S1]), F(pk->brev[Key::S2]),
                                     F(pk->brev[Key::S3]), F(xb), F(lone)};
     for (int i = 0; i < n_cmt; i++) srcs.push_back(F(pk->qcp_brev[i]));
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     // quotient units: domains, resident key evaluations on the class, twiddles0 there
     const size_t m = n / pk->S, mb = 32 * m;
     const FrB wS = pow_u64(pk->omega, (uint64_t)pk->S);
@@ -1003,7 +1053,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
             plk::gather_strided(t0, n, pk->S, p / (int)pk->rho + 1, F(q->tw1), qs);
         }
         if (peer) q->out.alloc(mb);
-        GG_HIP(hipStreamSynchronize(qs));
+        GG_WAIT_STREAM(qs);
         (peer ? peer->units : pk->units).push_back(std::move(up_));
     }
     // peers: the permutation's columns over their KzgLagrange slice, for their share of the ratio
@@ -1017,7 +1067,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
             up(p->perm_slice.as<int64_t>() + j * cnt, perm + (size_t)j * n + p->l_lo, cnt * 8, false, p->s[0]);
         p->pz.alloc(32 * cnt);
         p->ar.reserve(plk::ratio_range_arena_bytes(n, cnt) + 65536);
-        GG_HIP(hipStreamSynchronize(p->s[0]));
+        GG_WAIT_STREAM(p->s[0]);
     }
     // peers: the canonical-form tasks (canon_tasks) -- a size-n domain, the regular
     // form's buffer and push streams on each owner, Qk in Lagrange form on Qk's
@@ -1039,7 +1089,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
             if (tasks[i] == 4) {
                 p->qk_lag.alloc(nb);
                 GG_HIP(hipMemcpyPeerAsync(p->qk_lag.p, p->device, pk->qk_lag.p, pk->device, nb, p->s[3]));
-                GG_HIP(hipStreamSynchronize(p->s[3]));
+                GG_WAIT_STREAM(p->s[3]);
             }
         }
     }
@@ -1076,7 +1126,7 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
     const size_t ab = std::max(std::max(plk::ratio_arena_bytes(n), plk::horner_arena_bytes(n + 3)),
                                plk::eval_many_arena_bytes(n + 3, plk::EVAL_MAX)) + 65536;
     for (auto& a : pk->ar) a.reserve(ab);
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     // vk digests (commitTrace, setup.go:229-272) unless the caller has them
     pk->vkQcp.resize(n_cmt);
     if (vk_digests) {
@@ -1154,7 +1204,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                 for (int b : mine) {
                     if (b < 3)
                         canon_run(pk, pi, b, F(pk->cbrev[b]), F(pk->can[b]), [&](hipStream_t q) {
-                            GG_HIP(hipEventSynchronize(uploaded[b]));
+                            GG_WAIT_EVENT(uploaded[b]);
                             GG_HIP(hipMemcpyPeerAsync(p->in[b].p, p->device, pk->lag[b].p, pk->device, nb, q));
                         });
                     else if (b == 4)  // completeQk (prove.go:397-423) on its owner
@@ -1179,7 +1229,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     BJac lroj[3];
     {
         std::vector<std::future<void>> fs;
-        if (plonk_batch()) {
+        if (batch_ok(pk, false, 3)) {
             // one batched MSM on s[0] once L, R, O are uploaded
             for (int k = 1; k < 3; k++) GG_HIP(hipStreamWaitEvent(s[0], uploaded[k], 0));
             fs.push_back(std::async(msm_policy(), [&] {
@@ -1215,7 +1265,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                 GG_HIP(hipStreamWaitEvent(q, uploaded[k], 0));
                 lag_to_canonical(pk, F(pk->lag[k]), F(pk->cbrev[k]), F(pk->can[k]), q);
             }
-            GG_HIP(hipStreamSynchronize(q));
+            GG_WAIT_STREAM(q);
         }
         for (auto& f : fs) f.get();
     }
@@ -1295,7 +1345,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                     GG_HIP(hipStreamWaitEvent(p->cps, p->cpev, 0));
                     GG_HIP(hipMemcpyPeerAsync(F(zown->in[3]) + p->l_lo, zown->device, p->scal[0].p, p->device, 32 * cnt,
                                               p->cps));
-                    GG_HIP(hipStreamSynchronize(p->cps));
+                    GG_WAIT_STREAM(p->cps);
                     std::lock_guard<std::mutex> lk(pk->tmu);
                     pk->ptimes[q + 1].ratio_ms += ms + ms_since(b);
                 }));
@@ -1321,7 +1371,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     record_wait(pk, s[0], s[1]);
     std::shared_future<void> zfut;
     if (peers_on) {  // Z's canonical forms on its owner, once every slice has landed there
-        GG_HIP(hipStreamSynchronize(s[0]));
+        GG_WAIT_STREAM(s[0]);
         const size_t zi = (ctasks.size() - 1) % pk->peers.size();
         if (part_runs(pk, (int)zi + 1))
             zfut = std::async(std::launch::async, [&, zi] {
@@ -1491,7 +1541,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                     GG_HIP(hipMemcpyPeerAsync(F(pk->cres) + blk * m, pk->device, qu->out.p, p->device, mb, p->cps));
                 }
                 GG_HIP(hipEventRecord(p->eb[3], p->cps));
-                GG_HIP(hipStreamSynchronize(p->cps));
+                GG_WAIT_STREAM(p->cps);
                 float cout = 0;
                 GG_HIP(hipEventElapsedTime(&cout, p->ea[3], p->eb[3]));
                 std::lock_guard<std::mutex> lk(pk->tmu);
@@ -1540,7 +1590,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     // ---- commitToQuotient: H1, H2, H3 at once (prove.go:1199-1218)
     {
         BJac hj[3];
-        if (plonk_batch()) {
+        if (batch_ok(pk, true, 3)) {
             // hpad[k] are complete on s[2] (recorded just above into s[0..2])
             const FrB* sc[3] = {F(pk->hpad[0]), F(pk->hpad[1]), F(pk->hpad[2])};
             msm_jac_batch(pk, pk->kzg, sc, 3, s[0], hj);
@@ -1569,7 +1619,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         GG_HIP(hipMemcpyAsync(F(pk->pad), head.data(), 32 * b.size(), hipMemcpyHostToDevice, q));
         plk::axpy(F(out), F(pk->pad), b.size(), FrB::one(), q);
         GG_HIP(hipMemcpyAsync(F(out) + n, tail.data(), 32 * b.size(), hipMemcpyHostToDevice, q));
-        GG_HIP(hipStreamSynchronize(q));  // host vectors
+        GG_WAIT_STREAM(q);  // host vectors
     };
     blinded(pk->can[3], bp[3], pk->bz, s[0]);
     if (run0) zero(F(pk->q1) + n + 2, 32, s[0]);  // Horner writes the n + 2 quotient coefficients
@@ -1646,7 +1696,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     const BAff lin_digest = to_aff(red(pk, commit_kzg(pk, 1, F(pk->lin), s[1])));
     mark();
     // ---- batchOpening: kzg.BatchOpenSinglePoint at zeta (prove.go:777-835)
-    GG_HIP(hipStreamSynchronize(s[2]));  // folded H
+    GG_WAIT_STREAM(s[2]);  // folded H
     std::vector<std::pair<const FrB*, size_t>> polys = {
         {F(pk->fold), n + 2}, {F(pk->lin), n + 3}, {F(pk->bl[0]), n + 2}, {F(pk->bl[1]), n + 2},
         {F(pk->bl[2]), n + 2}, {F(pk->reg[Key::S1]), n}, {F(pk->reg[Key::S2]), n}};
@@ -1703,7 +1753,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     P.batched_h = to_aff(red(pk, commit_kzg(pk, 2, F(pk->fold), s[2])));
     P.zs_h = to_aff(red(pk, fzs.get()));
     mark();
-    for (hipStream_t q : pk->s) GG_HIP(hipStreamSynchronize(q));
+    for (hipStream_t q : pk->s) GG_WAIT_STREAM(q);
 }
 
 };
@@ -1972,6 +2022,8 @@ extern "C" int gg_plonk_pk_set_rehearsal_part(gg_plonk_pk_t pk, int part) {
     with_key(pk, [&](auto* k) {
         std::lock_guard<std::mutex> lk(k->mu);
         GG_CHECK(part >= -1 && part <= (int)k->peers.size(), GG_ERR_INVALID_ARG, "rehearsal part out of range");
+        using Impl = PlonkImpl<typename std::remove_pointer<decltype(k)>::type::CvT>;
+        Impl::queue_layout(k, part);
         k->solo = part >= 0;
         k->solo_part = part >= 0 ? part : 0;
         return 0;

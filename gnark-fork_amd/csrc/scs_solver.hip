@@ -492,7 +492,7 @@ extern "C" int gg_scs_solve(gg_scs_t h, const void* witness, size_t n_witness, i
     unsigned long long unsolved = 0;
     GG_HIP(hipMemcpyAsync(fail, h->fail.p, 12, hipMemcpyDeviceToHost, h->st));
     GG_HIP(hipMemcpyAsync(&unsolved, h->cnt.p, 8, hipMemcpyDeviceToHost, h->st));
-    GG_HIP(hipStreamSynchronize(h->st));
+    GG_WAIT_STREAM(h->st);
     GG_CHECK(fail[1] == 0xffffffffu, GG_ERR_INVALID_ARG,
              "constraint #" + std::to_string(fail[1]) +
                  ": more than one unsolved wire at its level (the levels do not match the system)");
@@ -509,7 +509,7 @@ extern "C" int gg_scs_solve(gg_scs_t h, const void* witness, size_t n_witness, i
     if (l_out) GG_HIP(hipMemcpyAsync(l_out, h->L.p, h->dom * 32, k, h->st));
     if (r_out) GG_HIP(hipMemcpyAsync(r_out, h->R.p, h->dom * 32, k, h->st));
     if (o_out) GG_HIP(hipMemcpyAsync(o_out, h->O.p, h->dom * 32, k, h->st));
-    GG_HIP(hipStreamSynchronize(h->st));
+    GG_WAIT_STREAM(h->st);
     GG_CAPI_END
 }
 

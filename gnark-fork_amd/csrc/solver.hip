@@ -522,7 +522,7 @@ extern "C" int gg_r1cs_solve(gg_r1cs_t r, const void* witness, size_t n_witness,
     unsigned long long unsolved = 0;
     GG_HIP(hipMemcpyAsync(fail, r->fail.p, 8, hipMemcpyDeviceToHost, r->st));
     GG_HIP(hipMemcpyAsync(&unsolved, r->cnt.p, 8, hipMemcpyDeviceToHost, r->st));
-    GG_HIP(hipStreamSynchronize(r->st));
+    GG_WAIT_STREAM(r->st);
     GG_CHECK(fail[1] == 0xffffffffu, GG_ERR_INVALID_ARG,
              "constraint #" + std::to_string(fail[1]) +
                  ": more than one unsolved wire at its level, or a zero coefficient on the unknown "
@@ -538,7 +538,7 @@ extern "C" int gg_r1cs_solve(gg_r1cs_t r, const void* witness, size_t n_witness,
     if (a_out && r->ncons) GG_HIP(hipMemcpyAsync(a_out, r->A.p, r->ncons * 32, k, r->st));
     if (b_out && r->ncons) GG_HIP(hipMemcpyAsync(b_out, r->B.p, r->ncons * 32, k, r->st));
     if (c_out && r->ncons) GG_HIP(hipMemcpyAsync(c_out, r->C.p, r->ncons * 32, k, r->st));
-    GG_HIP(hipStreamSynchronize(r->st));
+    GG_WAIT_STREAM(r->st);
     GG_CAPI_END
 }
 

@@ -51,7 +51,7 @@ void Stager::run(void* dst, const void* src, size_t elem, size_t first, size_t s
                 const size_t j0 = k * per, cnt = std::min(per, count - j0);
                 const int b = next_[t];
                 next_[t] ^= 1;
-                GG_HIP(hipEventSynchronize(ev_[t][b]));  // previous DMA out of this buffer
+                GG_WAIT_EVENT(ev_[t][b]);  // previous DMA out of this buffer
                 uint8_t* pin = (uint8_t*)pin_[t][b];
                 const uint8_t* s = (const uint8_t*)src;
                 if (stride == 1) {
@@ -96,7 +96,7 @@ void Stager::ready(const hipStream_t* consumers, int k) {
 
 void Stager::sync() {
     std::lock_guard<std::mutex> lk(mu_);
-    for (int t = 0; t < nst_; t++) GG_HIP(hipStreamSynchronize(st_[t]));
+    for (int t = 0; t < nst_; t++) GG_WAIT_STREAM(st_[t]);
 }
 
 }  // namespace gg

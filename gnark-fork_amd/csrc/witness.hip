@@ -79,7 +79,7 @@ extern "C" int gg_fr_from_canonical_be(int curve, const void* in_dev, void* out_
     GG_HIP(hipGetLastError());
     uint64_t nb = 0;
     GG_HIP(hipMemcpyAsync(&nb, bad.p, 8, hipMemcpyDeviceToHost, st));
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     if (n_invalid) *n_invalid = nb;
     GG_CHECK(nb == 0, GG_ERR_INVALID_ARG, "non-canonical field element (>= modulus) in the vector");
     GG_CAPI_END
@@ -101,6 +101,6 @@ extern "C" int gg_fr_to_canonical_be(int curve, const void* in_dev, void* out_de
         hipLaunchKernelGGL(k_fr_to_be<FrBlsCfg>, dim3(grid_for(n, 256)), dim3(256), 0, st,
                            (const FrBls*)in_dev, (uint8_t*)out_dev, n);
     GG_HIP(hipGetLastError());
-    GG_HIP(hipStreamSynchronize(st));
+    GG_WAIT_STREAM(st);
     GG_CAPI_END
 }

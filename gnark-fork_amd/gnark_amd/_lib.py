@@ -14,6 +14,8 @@ LIB_PATH = os.environ.get("GNARK_AMD_LIB", os.path.join(_PKG_DIR, "lib", "libgna
 GG_OK = 0
 GG_BUILD_ACCUM_PROBE = 1  # gg_build_flags(): a traffic-attribution build, MSM sums wrong by design
 GG_REHEARSAL = 7  # a multi-GPU timing rehearsal: the proof written is not valid
+GG_ERR_UNSUPPORTED = 4
+GG_ERR_TIMEOUT = 8  # a host wait of the library passed its deadline (gg_set_wait_timeout)
 GG_MPK_TIMING_SLOTS = 18
 GG_PLONK_PART_SLOTS = 14
 GG_G1, GG_G2, GG_BLS12_381_G1, GG_BLS12_381_G2 = 1, 2, 3, 4
@@ -80,6 +82,10 @@ def _load():
         "gg_msm": ([P, P, S, I, P, P], I),
         "gg_msm_stripe": ([P, P, S, I, I, I, P, P], I),
         "gg_msm_batch": ([P, P, I, S, I, P, P], I),
+        "gg_msm_batch_shape": ([S, I, I, I, I], I),
+        "gg_set_wait_timeout": ([ctypes.c_double], I),
+        "gg_get_wait_timeout": ([], ctypes.c_double),
+        "gg_wait_selftest": ([I, I, ctypes.c_double], I),
         "gg_groth16_pk_create_stripe_ex": ([I, I, P, P, P, S, P, S, P, S, S, P, S, P, P, P, P, P, P, P, P, S,
                                             S, P, I, I, PP], I),
         "gg_groth16_pk_stripe": ([P, ctypes.POINTER(I), ctypes.POINTER(I)], I),
@@ -233,7 +239,8 @@ EXPORTED = [
     "gg_hshard_create_ex", "gg_hshard_exchange_bytes", "gg_groth16_mpk_shard_timings",
     "gg_groth16_mpk_set_rehearsal", "gg_plonk_pk_set_rehearsal", "gg_plonk_pk_set_rehearsal_part",
     "gg_plonk_pk_part_timings", "gg_groth16_mpk_peer_access", "gg_plonk_pk_peer_access",
-    "gg_fr_evaluate_many",
+    "gg_fr_evaluate_many", "gg_msm_batch_shape", "gg_set_wait_timeout", "gg_get_wait_timeout",
+    "gg_wait_selftest",
 ]
 
 

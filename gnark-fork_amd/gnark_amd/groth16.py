@@ -22,6 +22,7 @@ from typing import Optional, Sequence
 import numpy as np
 
 from . import backend, fr
+from . import dist as gdist
 from ._lib import BUILD_FLAGS, check, lib, ptr, GG_CURVE_BN254, GG_CURVE_BLS12_381, GG_MPK_TIMING_SLOTS, GG_REHEARSAL
 
 # (G1 affine, G2 affine) bytes per curve
@@ -598,23 +599,30 @@ def prove_distributed(pk: ProvingKeyShard, solution: Solution, *opts, r: bytes =
             tdist.broadcast(rs, 0)
         rsb = bytes(rs.cpu().numpy())
         r, s = rsb[:32], rsb[32:]
-    fixed = FixedTerms(pk.data, r, s)  # host threads, overlapped with the GPU work
+    # errgroup across ranks (prove.go:198-209): a rank whose partial fails makes
+    # every rank raise at the status step before the gather (dist.RankGuard)
+    guard = gdist.RankGuard(device, "Groth16 prove (shard partials)")
+    fixed = guard.run(FixedTerms, pk.data, r, s)  # host threads, overlapped with the GPU work
     try:
-        part = prove_partial(pk, solution)
+        part = guard.run(prove_partial, pk, solution)
     except BaseException:
         fixed.close()
         raise
-    return gather_and_finalize(pk.data, part, r, s, device, fixed=fixed)
+    return gather_and_finalize(pk.data, part, r, s, device, fixed=fixed, guard=guard)
 
 
 def gather_and_finalize(data: ProvingKeyData, part: bytes, r: bytes, s: bytes, device=None,
-                        fixed: "FixedTerms" = None) -> Proof:
+                        fixed: "FixedTerms" = None, guard=None) -> Proof:
     """All-gather every rank's 576-B partials, add them exactly, combine (all ranks).
-    fixed: the fixed-point terms already started (FixedTerms) for this r, s."""
+    fixed: the fixed-point terms already started (FixedTerms) for this r, s.
+    guard: the proof's dist.RankGuard (its status step comes first: a failed
+    rank makes every rank raise instead of waiting in the gather)."""
     import torch
     import torch.distributed as tdist
     world = tdist.get_world_size() if tdist.is_initialized() else 1
     try:
+        if guard is not None:
+            guard.check("partial all-gather")
         if world > 1:
             t = torch.frombuffer(bytearray(part), dtype=torch.uint8)
             if device is not None:
@@ -703,13 +711,12 @@ class TorchExchange:
     """All-to-all over torch.distributed for the distributed computeH: RCCL
     (backend "nccl") on device buffers, or gloo through host staging.
 
-    Failure semantics: a rank whose prove fails before or inside an exchange
-    leaves its peers blocked in all_to_all_single until the process group's
-    timeout (torch.distributed's, 10 minutes by default) -- the collective
-    cannot be cancelled from one side.  Jobs that must fail fast should create
-    the group with a short `timeout=`; the one-process multi-GPU prover
-    (MultiGpuProvingKey) has no such wait: its in-library barrier is broken by
-    the failing shard and every shard returns the error."""
+    Failure semantics: while prove_distributed_h runs, `guard` is its
+    dist.RankGuard and every all-to-all is preceded by a status step: a rank
+    whose prove fails before an exchange joins that step with its error
+    (RankGuard.fail), so its peers raise RankFailure there instead of waiting in
+    all_to_all_single until the group's timeout.  (A collective that fails
+    half-way, e.g. a dead peer, still ends by the transport's own timeout.)"""
 
     def __init__(self, nbytes: int, device):
         import torch
@@ -723,10 +730,13 @@ class TorchExchange:
         # own hardware queue, so the host's wait for it never sits behind an MSM
         # kernel of the library's streams on a shared queue
         self.stream = torch.cuda.Stream(device=self.dev, priority=-1)
+        self.guard = None
 
     def __call__(self, s_ptr, r_ptr, nbytes):
         import torch
         import torch.distributed as tdist
+        if self.guard is not None:
+            self.guard.check("computeH all-to-all")
         total = nbytes * self.world
         s, r = self.send[:total], self.recv[:total]
         with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
@@ -746,10 +756,14 @@ def prove_distributed_h(pk: ProvingKeyShard, hs: HShard, xchg: TorchExchange, so
     cfg = backend.new_prover_config(*opts)
     if not backend.accelerated(cfg):
         raise RuntimeError("accelerated prover requested without with_amd_acceleration()")
-    fixed = FixedTerms(pk.data, r, s)  # host threads, overlapped with the GPU work
+    guard = gdist.RankGuard(device, "Groth16 prove (distributed computeH)")
+    fixed = guard.run(FixedTerms, pk.data, r, s)  # host threads, overlapped with the GPU work
+    xchg.guard = guard  # a status step before each of the three all-to-alls
     try:
-        part = prove_partial_dist(pk, hs, solution, xchg, xchg.send.data_ptr(), xchg.recv.data_ptr())
+        part = guard.run(prove_partial_dist, pk, hs, solution, xchg, xchg.send.data_ptr(), xchg.recv.data_ptr())
     except BaseException:
         fixed.close()
         raise
-    return gather_and_finalize(pk.data, part, r, s, device, fixed=fixed)
+    finally:
+        xchg.guard = None
+    return gather_and_finalize(pk.data, part, r, s, device, fixed=fixed, guard=guard)

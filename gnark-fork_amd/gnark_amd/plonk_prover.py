@@ -347,15 +347,42 @@ class GroupProvingKey:
     collective per hand-off would serialise what the event graph overlaps.
 
     `key_args` / `key_kw`: the ProvingKey arguments (significant on rank 0 only;
-    other ranks may pass None for the buffers).  local_device: this rank's GPU."""
+    other ranks may pass None for the buffers).  local_device: this rank's GPU.
 
-    def __init__(self, *key_args, local_device: int = 0, comm_device=None, **key_kw):
+    Preconditions, checked at creation (dist.check_leader_devices): every rank's
+    GPU id must name the same GPU on rank 0 (a launcher that isolates
+    HIP_VISIBLE_DEVICES per rank breaks the leader design) and, under RCCL, no two
+    ranks may share a GPU.  A violation -- or any failure of rank 0's key
+    creation -- raises on every rank (RankFailure on the others), never a hang.
+    `identity` / `view`: test hooks for the device identities (default
+    dist.device_identity)."""
+
+    mode = "leader"  # rank 0 runs the whole device-part split; the others receive the proof
+
+    def __init__(self, *key_args, local_device: int = 0, comm_device=None, identity=None, view=None, **key_kw):
         import torch.distributed as dist
         from . import dist as gdist
         self.rank = dist.get_rank() if dist.is_initialized() else 0
+        backend = dist.get_backend() if dist.is_initialized() else None
         self.devices = gdist.group_devices(local_device, comm_device)
+        ident = identity(local_device) if identity else gdist.device_identity(local_device)
+        self.identities = gdist.group_identities(ident, comm_device)
         self.comm_device = comm_device
-        self.pk = ProvingKey(*key_args, devices=self.devices, **key_kw) if self.rank == 0 else None
+        self.pk = None
+        err = None
+        if self.rank == 0:
+            try:
+                probs = gdist.check_leader_devices(self.devices, self.identities, view or gdist.device_identity,
+                                                   backend)
+                if probs:
+                    raise ValueError("PlonK leader key refused: " + "; ".join(probs))
+                self.pk = ProvingKey(*key_args, devices=self.devices, **key_kw)
+            except BaseException as e:
+                err = e
+        gdist.broadcast_status(err is None, f"{type(err).__name__}: {err}" if err else "", b"", 0, 0, comm_device,
+                               "PlonK leader key creation")
+        if err is not None:
+            raise err
         curve = key_kw.get("curve", "bls12-381")
         self.curve = curve
         self.n_cmt = len(key_kw.get("qcp", ()))
@@ -371,11 +398,18 @@ def prove_group(gpk: GroupProvingKey, L, R_, O, **kw) -> Proof:
     (broadcast from rank 0).  Inputs and options are significant on rank 0."""
     from . import dist as gdist
     size = lib.gg_plonk_proof_size_ex(_Field(gpk.curve).cid, gpk.n_cmt)
-    raw = None
+    raw, err = b"", None
     if gpk.rank == 0:
-        pr = prove(gpk.pk, L, R_, O, **kw)
-        raw = proof_bytes(pr, gpk.curve)
-    raw = gdist.broadcast_bytes(raw if raw is not None else bytes(size), size, 0, gpk.comm_device)
+        try:
+            pr = prove(gpk.pk, L, R_, O, **kw)
+            raw = proof_bytes(pr, gpk.curve)
+        except BaseException as e:  # errgroup (prove.go:132-173): the proof ends on every rank
+            err = e
+    # the leader's status with the proof: a failed prove raises on every rank
+    raw = gdist.broadcast_status(err is None, f"{type(err).__name__}: {err}" if err else "", raw, size, 0,
+                                 gpk.comm_device, "PlonK prove (leader)")
+    if err is not None:
+        raise err
     return Proof.parse(raw, gpk.n_cmt, gpk.curve)
 
 

