@@ -102,6 +102,24 @@ void return_task_queue(hipStream_t s) {
                 return;
             }
 }
+// destroy every dedicated queue of `device` that no task slot holds (all of
+// them idle: a returned queue was waited for)
+void drop_idle_task_queues(int device) {
+    std::lock_guard<std::mutex> g(g_tq_mu);
+    auto it = g_tq.find(device);
+    if (it == g_tq.end()) return;
+    auto& v = it->second;
+    for (auto& d : v) if (d.used) return;  // a key still runs on this device's set
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
+    for (auto& d : v) {
+        if (gg::trace_streams()) fprintf(stderr, "[gg] destroy dedicated queue %p (device %d)\n", (void*)d.s, device);
+        (void)hipStreamDestroy(d.s);
+    }
+    v.clear();
+    (void)hipSetDevice(cur);
+}
 void wait_idle(hipStream_t s) {
     GG_WAIT_STREAM(s);                    // bounded
     GG_HIP(hipStreamSynchronize(s));      // returns at once; settles the runtime's view of the stream
@@ -146,7 +164,7 @@ void gg::task_streams_switch(hipStream_t* const* active, TaskQueue* q, int n, in
     GG_HIP(hipSetDevice(cur));
 }
 
-void gg::task_streams_release(TaskQueue* q, int n) {
+void gg::task_streams_release(TaskQueue* q, int n, int device) {
     for (int i = 0; i < n; i++) {
         if (q[i].ded) {
             (void)hipStreamSynchronize(q[i].ded);
@@ -156,6 +174,22 @@ void gg::task_streams_release(TaskQueue* q, int n) {
         if (q[i].own) (void)hipStreamDestroy(q[i].own);
         q[i].own = nullptr;
     }
+    // the last key on the device gone: its dedicated queues too (as round 5
+    // destroyed them with their keys -- none outlives the process's keys, so
+    // none is left for the runtime's teardown at exit, which crashed under
+    // rocprofv3 --pmc, r06e)
+    drop_idle_task_queues(device);
+}
+
+extern "C" int gg_release_task_queues(void) {
+    GG_CAPI_BEGIN
+    std::vector<int> devs;
+    {
+        std::lock_guard<std::mutex> g(g_tq_mu);
+        for (auto& kv : g_tq) devs.push_back(kv.first);
+    }
+    for (int d : devs) drop_idle_task_queues(d);
+    GG_CAPI_END
 }
 
 // ---- bounded waits (common.h)

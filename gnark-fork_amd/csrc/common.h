@@ -184,8 +184,9 @@ void task_streams_init(hipStream_t* const* active, TaskQueue* q, int n, int devi
 // between proofs: wait until the slots' streams are idle, return / borrow the
 // dedicated queues, repoint active[] (never creates or destroys a stream)
 void task_streams_switch(hipStream_t* const* active, TaskQueue* q, int n, int device, bool dedicated);
-// the key goes away: dedicated queues back to the set, own streams destroyed
-void task_streams_release(TaskQueue* q, int n);
+// the key goes away: dedicated queues back to the set, own streams destroyed;
+// a device's set is destroyed once no key holds any of it
+void task_streams_release(TaskQueue* q, int n, int device);
 bool trace_streams();
 
 // ---- bounded host waits (round 6, VERDICT r5: a stall must end in an error,

@@ -165,7 +165,7 @@ struct gg_groth16_pk {
         wb.reset();
         if (Z) gg_msm_base_release(Z);
         if (dom) gg_domain_release(dom);
-        task_streams_release(tq, 5);
+        task_streams_release(tq, 5, device);
         if (hprio) (void)hipStreamDestroy(hprio);
     }
 };

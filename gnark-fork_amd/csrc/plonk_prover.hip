@@ -220,7 +220,7 @@ struct PlonkPeer {
         perm_slice.release();
         pz.release();
         ar.buf.release();
-        task_streams_release(tq, 4);
+        task_streams_release(tq, 4, device);
         for (int i = 0; i < 4; i++) {
             if (ea[i]) (void)hipEventDestroy(ea[i]);
             if (eb[i]) (void)hipEventDestroy(eb[i]);
@@ -423,7 +423,7 @@ struct Key : gg_plonk_pk {
         if (d0) gg_domain_release(d0);
         if (d1) gg_domain_release(d1);
         units.clear();
-        task_streams_release(tq, 4);
+        task_streams_release(tq, 4, device);
     }
 };
 

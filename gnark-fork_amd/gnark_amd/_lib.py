@@ -86,6 +86,7 @@ def _load():
         "gg_set_wait_timeout": ([ctypes.c_double], I),
         "gg_get_wait_timeout": ([], ctypes.c_double),
         "gg_wait_selftest": ([I, I, ctypes.c_double], I),
+        "gg_release_task_queues": ([], I),
         "gg_groth16_pk_create_stripe_ex": ([I, I, P, P, P, S, P, S, P, S, S, P, S, P, P, P, P, P, P, P, P, S,
                                             S, P, I, I, PP], I),
         "gg_groth16_pk_stripe": ([P, ctypes.POINTER(I), ctypes.POINTER(I)], I),
@@ -200,6 +201,19 @@ def _load():
 
 
 lib = _load()
+
+
+def _release_queues_at_exit():
+    # the dedicated queues no key holds any more, while the runtime (and a
+    # profiler's hooks) are still up (gg_release_task_queues)
+    try:
+        lib.gg_release_task_queues()
+    except Exception:  # pragma: no cover - exiting anyway
+        pass
+
+
+import atexit  # noqa: E402
+atexit.register(_release_queues_at_exit)
 # a diagnostic build (GG_BUILD_ACCUM_PROBE: wrong MSM sums) is loaded only when
 # asked for by name; its provers return GG_REHEARSAL
 BUILD_FLAGS = lib.gg_build_flags()
@@ -240,7 +254,7 @@ EXPORTED = [
     "gg_groth16_mpk_set_rehearsal", "gg_plonk_pk_set_rehearsal", "gg_plonk_pk_set_rehearsal_part",
     "gg_plonk_pk_part_timings", "gg_groth16_mpk_peer_access", "gg_plonk_pk_peer_access",
     "gg_fr_evaluate_many", "gg_msm_batch_shape", "gg_set_wait_timeout", "gg_get_wait_timeout",
-    "gg_wait_selftest",
+    "gg_wait_selftest", "gg_release_task_queues",
 ]
 
 

@@ -173,6 +173,12 @@ int gg_set_hbm_budget(size_t bytes);
  * the first failing task: prove.go:198-209 channels, plonk prove.go:132-173
  * errgroup; a hang ends nothing). */
 int gg_set_wait_timeout(double seconds);
+/* Destroys the dedicated hardware queues (CU-masked streams: at most
+ * GG_TASK_QUEUES per device, lent to the keys' prove tasks) that no live key
+ * holds.  The library does this itself when a device's last key is released;
+ * call it before process exit if keys may still be alive then (the Python
+ * mirror does, atexit), so no stream is left for the runtime's own teardown. */
+int gg_release_task_queues(void);
 double gg_get_wait_timeout(void);
 /* Host-only self-test of the bounded wait (no GPU needed): `parties` threads
  * meet at a barrier, `arriving` of them come; GG_OK if all arrive, else every

@@ -63,6 +63,14 @@ def main(db, gap_ms=10.0, title="PlonK part"):
     print("|---|---|---|---|")
     for f, iv in sorted(fam.items(), key=lambda kv: -union_len(kv[1])):
         print(f"| {f} | {len(iv)} | {union_len(iv) / 1e6:.2f} | {sum(e - s for s, e in iv) / 1e6:.2f} |")
+    # per kernel (template arguments dropped), the largest first
+    per = defaultdict(list)
+    for n, s, e in last:
+        per[re.sub(r"\(.*", "", n)].append(e - s)
+    print("\n| kernel | dispatches | sum ms | avg us |")
+    print("|---|---|---|---|")
+    for k, ds in sorted(per.items(), key=lambda kv: -sum(kv[1]))[:40]:
+        print(f"| `{k[:90]}` | {len(ds)} | {sum(ds) / 1e6:.3f} | {sum(ds) / len(ds) / 1e3:.1f} |")
 
 
 if __name__ == "__main__":
