@@ -41,6 +41,25 @@ __global__ void k_scan_add(uint32_t* out, const uint32_t* sums, size_t n) {
         if (base + i < n) out[base + i] += a;
 }
 
+// k_scan_add with each block's prefix summed from the block sums directly (no
+// scan of the sums: one launch fewer; for up to kScanPrefixMax blocks, <= 16
+// loads a thread)
+constexpr size_t kScanPrefixMax = 4096;
+__global__ void __launch_bounds__(256) k_scan_add_prefix(uint32_t* out, const uint32_t* sums, size_t n) {
+    __shared__ uint32_t wsum[4];
+    uint32_t acc = 0;
+    for (uint32_t i = threadIdx.x; i < blockIdx.x; i += 256) acc += sums[i];
+    for (int off = 32; off > 0; off >>= 1) acc += (uint32_t)__shfl_xor((int)acc, off);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    const uint32_t a = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (!a) return;
+    const size_t base = ((size_t)blockIdx.x * 256 + threadIdx.x) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+        if (base + i < n) out[base + i] += a;
+}
+
 // exclusive scan of n >= 1 u32: out[0..n) (out[n] is set by k_set_total)
 void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, hipStream_t st,
                     std::vector<DevBuf>& tmp, int depth) {
@@ -48,6 +67,16 @@ void exclusive_scan(const uint32_t* in, uint32_t* out, size_t n, hipStream_t st,
     size_t blocks = (n + per_block - 1) / per_block;
     if (blocks <= 1) {
         hipLaunchKernelGGL(k_scan_block, dim3(1), dim3(256), 0, st, in, out, nullptr, n);
+        GG_HIP(hipGetLastError());
+        return;
+    }
+    if (blocks <= kScanPrefixMax) {  // two launches (round 6: the sort's launch count)
+        if (tmp.size() < (size_t)(depth + 1) * 2) tmp.resize((size_t)(depth + 1) * 2);
+        tmp[2 * depth].reserve(blocks * 4);
+        uint32_t* sums = tmp[2 * depth].as<uint32_t>();
+        hipLaunchKernelGGL(k_scan_block, dim3((unsigned)blocks), dim3(256), 0, st, in, out, sums, n);
+        GG_HIP(hipGetLastError());
+        hipLaunchKernelGGL(k_scan_add_prefix, dim3((unsigned)blocks), dim3(256), 0, st, out, sums, n);
         GG_HIP(hipGetLastError());
         return;
     }
@@ -404,35 +433,59 @@ __global__ void k_bin_starts(const uint32_t* hoff, const uint32_t* hist, uint32_
 constexpr uint32_t SEG_CH = GG_SEG_CH;
 constexpr int SEG_PER = SEG_CH / 256;  // entries per thread
 
+// chunk_start[0..nseg] (exclusive scan of the segments' chunk counts, total at
+// [nseg]) in one block, for nseg <= 2048: the first segmented pass's 256 bins
+__global__ void __launch_bounds__(256) k_seg_plan_small(const uint32_t* seg_start, uint32_t nseg,
+                                                        uint32_t* chunk_start) {
+    __shared__ uint32_t wsum[4];
+    uint32_t c[8], t = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint32_t sg = threadIdx.x * 8 + i;
+        c[i] = sg < nseg ? (seg_start[sg + 1] - seg_start[sg] + SEG_CH - 1) / SEG_CH : 0u;
+        t += c[i];
+    }
+    uint32_t tot;
+    uint32_t run = block_excl_scan256(t, wsum, &tot);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint32_t sg = threadIdx.x * 8 + i;
+        if (sg < nseg) chunk_start[sg] = run;
+        run += c[i];
+    }
+    if (threadIdx.x == 0) chunk_start[nseg] = tot;
+}
+
+// a chunk's descriptor {lo, hi, g0, nch} -- its entry range, the first chunk of
+// its segment, the segment's chunks; nch = 0 marks a grid slot past the last
+// chunk -- computed by one thread of the block that works on the chunk
+__device__ __forceinline__ uint4 chunk_desc_block(const uint32_t* seg_start, const uint32_t* chunk_start,
+                                                  uint32_t nseg, uint32_t g) {
+    __shared__ uint4 d;
+    if (threadIdx.x == 0) {
+        uint4 r = make_uint4(0, 0, 0, 0);
+        if (g < chunk_start[nseg]) {
+            uint32_t lo = 0, hi = nseg;  // largest s with chunk_start[s] <= g
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (chunk_start[mid] <= g) lo = mid;
+                else hi = mid;
+            }
+            const uint32_t g0 = chunk_start[lo], nch = chunk_start[lo + 1] - g0, k = g - g0;
+            const uint32_t a = seg_start[lo] + k * SEG_CH, b = min(seg_start[lo + 1], a + SEG_CH);
+            r = make_uint4(a, b, g0, nch);
+        }
+        d = r;
+    }
+    __syncthreads();
+    return d;
+}
+
 __global__ void k_seg_chunk_counts(const uint32_t* seg_start, uint32_t nseg, uint32_t* cnt) {
     uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s < nseg) cnt[s] = (seg_start[s + 1] - seg_start[s] + SEG_CH - 1) / SEG_CH;
 }
 
-__device__ __forceinline__ uint32_t find_seg(const uint32_t* chunk_start, uint32_t nseg, uint32_t g) {
-    uint32_t lo = 0, hi = nseg;  // largest s with chunk_start[s] <= g
-    while (hi - lo > 1) {
-        uint32_t mid = (lo + hi) >> 1;
-        if (chunk_start[mid] <= g) lo = mid; else hi = mid;
-    }
-    return lo;
-}
-
-// chunk descriptor {lo, hi, g0, nch}: entry range, first chunk of its segment,
-// chunks in the segment; nch = 0 marks a grid slot past the last chunk
-__global__ void k_seg_chunk_desc(const uint32_t* seg_start, const uint32_t* chunk_start, uint32_t nseg,
-                                 uint32_t max_chunks, uint4* desc) {
-    uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= max_chunks) return;
-    uint4 d = make_uint4(0, 0, 0, 0);
-    if (g < chunk_start[nseg]) {
-        uint32_t sg = find_seg(chunk_start, nseg, g);
-        uint32_t g0 = chunk_start[sg], nch = chunk_start[sg + 1] - g0, k = g - g0;
-        uint32_t lo = seg_start[sg] + k * SEG_CH, hi = min(seg_start[sg + 1], lo + SEG_CH);
-        d = make_uint4(lo, hi, g0, nch);
-    }
-    desc[g] = d;
-}
 
 // counters laid out [segment][digit][chunk-in-segment]: one global exclusive
 // scan then yields absolute output positions.
@@ -440,11 +493,12 @@ __global__ void k_seg_chunk_desc(const uint32_t* seg_start, const uint32_t* chun
 // bits and <= 16 remain (the usual case: c - 1 = 21 bucket bits, 8 of them bins),
 // halving the key traffic of every later pass
 template <class KT>
-__global__ void __launch_bounds__(256) k_seg_hist(const KT* keys, const uint4* desc, int shift,
+__global__ void __launch_bounds__(256) k_seg_hist(const KT* keys, const uint32_t* seg_start,
+                                                  const uint32_t* chunk_start, uint32_t nseg, int shift,
                                                   int rbits, uint32_t* ch) {
     __shared__ uint32_t hist[256];
     const uint32_t g = xcd_swizzle(blockIdx.x, gridDim.x);
-    const uint4 dsc = desc[g];
+    const uint4 dsc = chunk_desc_block(seg_start, chunk_start, nseg, g);
     const uint32_t lo = dsc.x, hi = dsc.y, g0 = dsc.z, nch = dsc.w, k = g - g0;
     if (nch == 0) return;
     const uint32_t R = 1u << rbits;
@@ -471,13 +525,14 @@ __global__ void __launch_bounds__(256) k_seg_hist(const KT* keys, const uint4* d
 
 template <class KT>
 __global__ void __launch_bounds__(256) k_seg_scatter(const uint32_t* ent_in, const KT* key_in,
-                                                     const uint4* desc, int shift, int rbits,
+                                                     const uint32_t* seg_start, const uint32_t* chunk_start,
+                                                     uint32_t nseg, int shift, int rbits,
                                                      const uint32_t* chpos, uint32_t* ent_out,
                                                      KT* key_out) {
     __shared__ uint32_t cnt[256], base[256], part[256];
     extern __shared__ uint32_t stage[];  // SEG_CH entries, SEG_CH digits (u8) [, SEG_CH keys]
     const uint32_t g = xcd_swizzle(blockIdx.x, gridDim.x);
-    const uint4 dsc = desc[g];
+    const uint4 dsc = chunk_desc_block(seg_start, chunk_start, nseg, g);
     const uint32_t lo = dsc.x, hi = dsc.y, g0 = dsc.z, nch = dsc.w, k = g - g0;
     if (nch == 0) return;
     const uint32_t R = 1u << rbits;
@@ -583,11 +638,10 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const VecPtrs& vp, hipStream
     const uint32_t nblocks = vblocks * (uint32_t)s->nvec;
     const size_t nh = (size_t)nbins * nblocks;
     // all scratch reserved up front (no reallocation between launches)
-    size_t ch_max = 0, chunks_max = 0;
+    size_t ch_max = 0;
     {
         size_t ns = (size_t)nbins;
         for (int r : rs) {
-            chunks_max = std::max(chunks_max, (total + SEG_CH - 1) / SEG_CH + ns);
             ch_max = std::max(ch_max, ((total + SEG_CH - 1) / SEG_CH + ns) << r);
             ns <<= r;
         }
@@ -609,7 +663,6 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const VecPtrs& vp, hipStream
     if (ch_max) {
         s->chunk_hist.reserve(ch_max * 4);
         s->chunk_pos.reserve((ch_max + 1) * 4);
-        s->chunk_desc.reserve(chunks_max * 16);
     }
     if (b->scurve)
         hipLaunchKernelGGL(k_digits_hist<FrBlsCfg>, dim3(nblocks), dim3(256), nbins * 4, st, vp,
@@ -651,39 +704,43 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const VecPtrs& vp, hipStream
         const uint32_t R = 1u << r;
         const size_t max_chunks = (total + SEG_CH - 1) / SEG_CH + nseg;
         const uint32_t* segp = segb[(j - 1) & 1]->as<uint32_t>();
-        hipLaunchKernelGGL(k_seg_chunk_counts, dim3(grid_for(nseg, 256)), dim3(256), 0, st, segp, nseg,
-                           s->counts.as<uint32_t>());
-        GG_HIP(hipGetLastError());
-        exclusive_scan(s->counts.as<uint32_t>(), s->chunk_start.as<uint32_t>(), nseg, st, s->scan_tmp);
-        hipLaunchKernelGGL(k_set_total, dim3(1), dim3(1), 0, st, s->chunk_start.as<uint32_t>(),
-                           s->counts.as<uint32_t>(), (size_t)nseg);
-        GG_HIP(hipGetLastError());
-        GG_HIP(hipMemsetAsync(s->chunk_hist.p, 0, max_chunks * R * 4, st));
-        hipLaunchKernelGGL(k_seg_chunk_desc, dim3(grid_for(max_chunks, 256)), dim3(256), 0, st, segp,
-                           s->chunk_start.as<uint32_t>(), nseg, (uint32_t)max_chunks,
-                           s->chunk_desc.as<uint4>());
-        GG_HIP(hipGetLastError());
+        const uint32_t* cst = s->chunk_start.as<uint32_t>();
+        // round 6: fewer launches per pass (each costs ~5 us of dependent-launch
+        // gap on the sort's stream, 24 per sort before): the chunk plan in one
+        // block when it fits, the descriptors inside the hist / scatter blocks,
+        // no zeroing of the chunk histogram (every real chunk's counters are
+        // written and the scan's stale tail lies past them)
+        if (nseg <= 2048) {
+            hipLaunchKernelGGL(k_seg_plan_small, dim3(1), dim3(256), 0, st, segp, nseg, s->chunk_start.as<uint32_t>());
+            GG_HIP(hipGetLastError());
+        } else {
+            hipLaunchKernelGGL(k_seg_chunk_counts, dim3(grid_for(nseg, 256)), dim3(256), 0, st, segp, nseg,
+                               s->counts.as<uint32_t>());
+            GG_HIP(hipGetLastError());
+            exclusive_scan(s->counts.as<uint32_t>(), s->chunk_start.as<uint32_t>(), nseg, st, s->scan_tmp);
+            hipLaunchKernelGGL(k_set_total, dim3(1), dim3(1), 0, st, s->chunk_start.as<uint32_t>(),
+                               s->counts.as<uint32_t>(), (size_t)nseg);
+            GG_HIP(hipGetLastError());
+        }
         const void* kin = key_out(j - 1)->p;
         if (key16)
             hipLaunchKernelGGL(k_seg_hist<uint16_t>, dim3((unsigned)max_chunks), dim3(256), 0, st,
-                               (const uint16_t*)kin, s->chunk_desc.as<uint4>(), shift, r,
-                               s->chunk_hist.as<uint32_t>());
+                               (const uint16_t*)kin, segp, cst, nseg, shift, r, s->chunk_hist.as<uint32_t>());
         else
             hipLaunchKernelGGL(k_seg_hist<uint32_t>, dim3((unsigned)max_chunks), dim3(256), 0, st,
-                               (const uint32_t*)kin, s->chunk_desc.as<uint4>(), shift, r,
-                               s->chunk_hist.as<uint32_t>());
+                               (const uint32_t*)kin, segp, cst, nseg, shift, r, s->chunk_hist.as<uint32_t>());
         GG_HIP(hipGetLastError());
         exclusive_scan(s->chunk_hist.as<uint32_t>(), s->chunk_pos.as<uint32_t>(), max_chunks * R, st,
                        s->scan_tmp);
         const size_t lds_s = (size_t)SEG_CH * (last ? 5 : 9);
         if (key16)
             hipLaunchKernelGGL(k_seg_scatter<uint16_t>, dim3((unsigned)max_chunks), dim3(256), lds_s, st,
-                               ent_out(j - 1)->as<uint32_t>(), (const uint16_t*)kin, s->chunk_desc.as<uint4>(),
+                               ent_out(j - 1)->as<uint32_t>(), (const uint16_t*)kin, segp, cst, nseg,
                                shift, r, s->chunk_pos.as<uint32_t>(), ent_out(j)->as<uint32_t>(),
                                last ? nullptr : key_out(j)->as<uint16_t>());
         else
             hipLaunchKernelGGL(k_seg_scatter<uint32_t>, dim3((unsigned)max_chunks), dim3(256), lds_s, st,
-                               ent_out(j - 1)->as<uint32_t>(), (const uint32_t*)kin, s->chunk_desc.as<uint4>(),
+                               ent_out(j - 1)->as<uint32_t>(), (const uint32_t*)kin, segp, cst, nseg,
                                shift, r, s->chunk_pos.as<uint32_t>(), ent_out(j)->as<uint32_t>(),
                                last ? nullptr : key_out(j)->as<uint32_t>());
         GG_HIP(hipGetLastError());

@@ -841,8 +841,13 @@ __global__ void __launch_bounds__(256) k_partials_to_std(const typename PartialO
 // else the first range's head or tail plus the later heads -- after
 // k_range_tree for heavy buckets) and stores it in radix form, laid out
 // [i][t] for bucket B = t L + i so that k_bucket_runsum's loads coalesce.
+#ifndef GG_G2_SUM_WAVES
+#define GG_G2_SUM_WAVES 1  // A/B builds: waves per SIMD of the BN254 G2 level 2 (2 spills)
+#endif
 template <class F>
-__global__ void __launch_bounds__(256) k_bucket_sum_r(const typename PartialOf<F>::T* head,
+constexpr int kSumWaves = std::is_same<F, Fp2>::value ? GG_G2_SUM_WAVES : 1;
+template <class F>
+__global__ void __launch_bounds__(256, kSumWaves<F>) k_bucket_sum_r(const typename PartialOf<F>::T* head,
                                                        const typename PartialOf<F>::T* tail,
                                                        const typename PartialOf<F>::T* S, const uint32_t* offsets,
                                                        uint32_t nb_total, int c, uint32_t K, int logL,

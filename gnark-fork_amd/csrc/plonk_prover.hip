@@ -900,6 +900,12 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
         };
         // device parts: slice boundaries by share (plonk_part_shares)
         const std::vector<double> share = plonk_part_shares(n_devices, n_cmt);
+        // the window of the parts' KZG slices (0 = the cost model's choose_c);
+        // GG_PLONK_PART_WINDOW forces one (A/B of the per-part bucket reductions)
+        const int part_c = [&] {
+            const char* e = getenv("GG_PLONK_PART_WINDOW");
+            return n_devices > 1 && e ? std::max(0, std::min(atoi(e), 23)) : 0;
+        }();
         auto bound = [&](size_t m, int d) -> size_t {
             if (d <= 0) return 0;
             if (d >= n_devices) return m;
@@ -927,10 +933,10 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
                 for (auto& w : p->work) w = msm_work_new();
                 for (auto& b : p->scal) b.alloc(32 * std::max<size_t>(1, std::max(p->k_hi - p->k_lo, p->l_hi - p->l_lo)));
                 int rc = gg_msm_base_create(Cv::group, (const uint8_t*)kzg_g1 + PT * p->k_lo, p->k_hi - p->k_lo,
-                                            0, nullptr, 0, &p->kzg);
+                                            0, nullptr, part_c, &p->kzg);
                 GG_CHECK(rc == GG_OK, rc, gg_last_error());
                 rc = gg_msm_base_create(Cv::group, (const uint8_t*)kzg_lagrange_g1 + PT * p->l_lo,
-                                        p->l_hi - p->l_lo, 0, nullptr, 0, &p->kzg_lag);
+                                        p->l_hi - p->l_lo, 0, nullptr, part_c, &p->kzg_lag);
                 GG_CHECK(rc == GG_OK, rc, gg_last_error());
             }
             GG_HIP(hipSetDevice(pk->device));
@@ -943,10 +949,10 @@ static void plonk_pk_build(Key* pk, int log_n, int log_big, const void* omega, c
             range(n, pk->l_lo, pk->l_hi);
         }
         int rc = gg_msm_base_create(Cv::group, (const uint8_t*)kzg_g1 + PT * pk->k_lo, pk->k_hi - pk->k_lo, 0,
-                                    nullptr, 0, &pk->kzg);
+                                    nullptr, part_c, &pk->kzg);
         GG_CHECK(rc == GG_OK, rc, gg_last_error());
         rc = gg_msm_base_create(Cv::group, (const uint8_t*)kzg_lagrange_g1 + PT * pk->l_lo,
-                                pk->l_hi - pk->l_lo, 0, nullptr, 0, &pk->kzg_lag);
+                                pk->l_hi - pk->l_lo, 0, nullptr, part_c, &pk->kzg_lag);
         GG_CHECK(rc == GG_OK, rc, gg_last_error());
         const uint8_t* g = (const uint8_t*)kzg_g1;
         for (int j = 0; j < 3; j++) {

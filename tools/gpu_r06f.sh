@@ -29,4 +29,12 @@ step 150 msm_w_$V.txt timeout -s KILL 140 rocprofv3 --pmc WRITE_SIZE -d gpurun_o
 step 150 msm_sq_$V.txt timeout -s KILL 140 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/msm_sq_$V -o run -- python3 tools/bench_msm.py G1 20 5 || exit 2
 step 100 msm_t_$V.txt python3 tools/bench_msm.py G1 20 20 || exit 2
 step 200 shard_ser_$V.txt env GG_G16_SERIAL=1 PROBE_SLEEP=0.05 rocprofv3 --kernel-trace --stats -d gpurun_out/shard_ser_$V -o run -- python3 -u tools/g16_shard_probe.py 24 8 0 3 || exit 2
+VG=gnark-fork_amd/lib/var/libgnark_amd_g2s2.so
+step 150 g_new_$V.txt python3 -u tools/g16_time.py 24 20 3 || exit 2
+step 150 g_g2s2_$V.txt env GNARK_AMD_LIB=$VG python3 -u tools/g16_time.py 24 20 3 || exit 2
+step 150 g_new2_$V.txt python3 -u tools/g16_time.py 24 20 3 || exit 2
+step 150 g_g2s22_$V.txt env GNARK_AMD_LIB=$VG python3 -u tools/g16_time.py 24 20 3 || exit 2
+step 200 plonk_def_$V.json python3 -u tools/bench_plonk.py 22 3 8 || exit 2
+step 200 plonk_w16_$V.json env GG_MSM_WINDOW=16 python3 -u tools/bench_plonk.py 22 3 8 || exit 2
+step 200 plonk_w15_$V.json env GG_MSM_WINDOW=15 python3 -u tools/bench_plonk.py 22 3 8 || exit 2
 echo done >> gpurun_out/progress_$V.txt
