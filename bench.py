@@ -783,12 +783,18 @@ def msm_bench(log_n, rank, world, dist, xdev, barrier, max_over_ranks, steps=20,
            "window_bits": c, "windows": W, "kernel_avg_ms": kern}
     if acc:
         alg = n * 96
-        traffic, note = pmc_traffic("k_accum_range<gg::Fe<gg::FpCfg>, ",
-                                    {"log_n": log_n, "window_bits": c, "windows": W}, 64)
+        wl = {"log_n": log_n, "window_bits": c, "windows": W}
+        traffic, note = pmc_traffic("k_accum_range<gg::Fe<gg::FpCfg>, ", wl, 64,
+                                    table_bytes=int(n * W * 64))
         res["accum_roofline"] = {"achieved_GBps": alg / (acc * 1e-3) / 1e9,
                                  "frac_hbm": alg / (acc * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                  "traffic_bytes": traffic, "traffic_note": note,
                                  "fpmul_equiv_G_per_s": n * W * 10 / (acc * 1e-3) / 1e9}
+        # the same VALU accounting as the headline's roofline (GRBM-counted cycles)
+        r = accum_roofline({"avg_ms": acc, "units_per_launch": n}, 64, "k_accum_range<gg::Fe<gg::FpCfg>, ", wl,
+                           "k_accum_range<Fe<FpCfg>> of the 2^%d G1 MSM" % log_n, W)
+        if "valu" in r:
+            res["accum_roofline"]["valu"] = r["valu"]
     return res
 
 
@@ -819,7 +825,7 @@ def accum_roofline(k, pt_bytes, kernel, workload, desc, windows):
          "kernel": desc, "algorithmic_bytes_per_launch": alg, "units_per_launch": units, "windows": windows,
          "kernel_avg_ms": ms,
          "timing": "HIP events on the kernel's launch stream over %d proves run task by task (rocprof summary of "
-                   "the same workload: profiles/r05_z3_groth16_2p24_kernel_stats.md)" % ROOFLINE_PROVES,
+                   "the same workload: profiles/r06_h_groth16_2p24_kernel_stats.md)" % ROOFLINE_PROVES,
          "note": "EC MSM is VALU-integer bound (SURVEY 8d); the HBM fraction is reported as required, the "
                  "issue-rate fraction below is the kernel's real ceiling"}
     sq = pmc_sq(kernel, workload)
