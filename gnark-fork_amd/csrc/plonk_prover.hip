@@ -1631,10 +1631,20 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     if (run0) zero(F(pk->q1) + n + 2, 32, s[0]);  // Horner writes the n + 2 quotient coefficients
     const FrB zu = run0 ? eval_dev(pk, F(pk->bz), n + 3, zeta * pk->omega, F(pk->q1), F(pk->vals), 0, s[0]) : FrB::zero();
     P.zs_value = zu;
-    std::future<BJac> fzs = std::async(msm_policy(), [&] {
-        GG_HIP(hipSetDevice(pk->device));
-        return commit_kzg(pk, 0, F(pk->q1), s[0]);
-    });
+    // openZ's quotient and the linearized polynomial are both committed on
+    // pk.Kzg.  GG_PLONK_BATCH_OPEN=1: one batched MSM once the linearized
+    // polynomial is formed (one sort and one bucket reduction fewer per part) --
+    // measured slower (r06i: one GPU 126.8 vs 125.5 ms, slowest of 8 parts 25.0
+    // vs 24.1 ms): openZ's MSM no longer overlaps the linearized polynomial's
+    // evaluations and kernel.  Default: openZ's MSM at once on s[0]
+    static const bool open_batch_env = getenv("GG_PLONK_BATCH_OPEN") && atoi(getenv("GG_PLONK_BATCH_OPEN")) == 1;
+    const bool open_batch = open_batch_env && batch_ok(pk, true, 2);
+    std::future<BJac> fzs;
+    if (!open_batch)
+        fzs = std::async(msm_policy(), [&] {
+            GG_HIP(hipSetDevice(pk->device));
+            return commit_kzg(pk, 0, F(pk->q1), s[0]);
+        });
     // ---- foldH (prove.go:670-705) on s[2]
     const FrB zp = pow_u64(zeta, n + 2);
     if (run0) {
@@ -1699,7 +1709,18 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         if (run0) plk::linearized(LP, s[1]);
     }
     mark();
-    const BAff lin_digest = to_aff(red(pk, commit_kzg(pk, 1, F(pk->lin), s[1])));
+    BAff lin_digest;
+    BJac zs_jac = BJac::inf();
+    if (open_batch) {
+        record_wait(pk, s[0], s[1]);  // q1 (openZ's Horner on s[0]) and lin (s[1]) complete on s[1]
+        const FrB* sc[2] = {F(pk->q1), F(pk->lin)};
+        BJac oj[2];
+        msm_jac_batch(pk, pk->kzg, sc, 2, s[1], oj);
+        zs_jac = oj[0];
+        lin_digest = to_aff(red(pk, oj[1]));
+    } else {
+        lin_digest = to_aff(red(pk, commit_kzg(pk, 1, F(pk->lin), s[1])));
+    }
     mark();
     // ---- batchOpening: kzg.BatchOpenSinglePoint at zeta (prove.go:777-835)
     GG_WAIT_STREAM(s[2]);  // folded H
@@ -1757,7 +1778,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         GG_CHECK(fv == fe, GG_ERR_INTERNAL, "batch opening: folded evaluation mismatch");
     }
     P.batched_h = to_aff(red(pk, commit_kzg(pk, 2, F(pk->fold), s[2])));
-    P.zs_h = to_aff(red(pk, fzs.get()));
+    P.zs_h = to_aff(red(pk, open_batch ? zs_jac : fzs.get()));
     mark();
     for (hipStream_t q : pk->s) GG_WAIT_STREAM(q);
 }
