@@ -325,6 +325,47 @@ extern "C" int gg_wait_selftest(int parties, int arriving, double timeout_s) {
     GG_CAPI_END
 }
 
+namespace {
+// one wave that sleeps `sleeps` times (s_sleep 127: ~8k cycles each) and
+// writes a flag; every wave reaches the end on its own
+__global__ void k_sleep_wave(uint32_t sleeps, uint32_t* done) {
+    for (uint32_t i = 0; i < sleeps; i++) __builtin_amdgcn_s_sleep(127);
+    if (threadIdx.x == 0) done[0] = sleeps;
+}
+}  // namespace
+
+// the same deadline on a real stream wait: a one-wave kernel that sleeps
+// `sleeps` x ~3.4 us on the calling thread's stream, waited for with the
+// library's bounded stream wait (GG_WAIT_STREAM) under timeout_s.  The kernel
+// always drains before the call returns (it ends on its own), so a timeout here
+// leaves nothing in flight
+extern "C" int gg_wait_selftest_device(uint32_t sleeps, double timeout_s) {
+    GG_CAPI_BEGIN
+    GG_CHECK(timeout_s > 0 && sleeps <= (1u << 20), GG_ERR_INVALID_ARG, "timeout_s > 0, sleeps <= 2^20");
+    hipStream_t st = hipStreamPerThread;
+    DevBuf done(4);
+    hipLaunchKernelGGL(k_sleep_wave, dim3(1), dim3(64), 0, st, sleeps, done.as<uint32_t>());
+    GG_HIP(hipGetLastError());
+    const double saved = g_wait_timeout.load();
+    g_wait_timeout.store(timeout_s);
+    int rc = GG_OK;
+    std::string msg;
+    try {
+        gg::WaitScope ws("device selftest");
+        GG_WAIT_STREAM(st);
+    } catch (const gg::Error& e) {
+        rc = e.code;
+        msg = e.what();
+    }
+    g_wait_timeout.store(saved);
+    GG_HIP(hipStreamSynchronize(st));  // the wave ends by itself: drain before `done` goes
+    uint32_t got = 0;
+    GG_HIP(hipMemcpy(&got, done.p, 4, hipMemcpyDeviceToHost));
+    GG_CHECK(got == sleeps, GG_ERR_INTERNAL, "selftest wave did not finish");
+    GG_CHECK(rc == GG_OK, rc, msg);
+    GG_CAPI_END
+}
+
 extern "C" const char* gg_last_error(void) { return g_last_error.c_str(); }
 
 extern "C" int gg_version(void) { return 100; }  // 0.1.0

@@ -184,6 +184,11 @@ double gg_get_wait_timeout(void);
  * meet at a barrier, `arriving` of them come; GG_OK if all arrive, else every
  * waiter returns GG_ERR_TIMEOUT after timeout_s (the message names the wait). */
 int gg_wait_selftest(int parties, int arriving, double timeout_s);
+/* The same deadline on a real stream: one wave sleeps `sleeps` x ~3.4 us on the
+ * calling thread's stream and the library's bounded stream wait waits for it
+ * under timeout_s: GG_ERR_TIMEOUT (message names the wait) if it was still
+ * running, else GG_OK.  The wave always drains before the call returns. */
+int gg_wait_selftest_device(uint32_t sleeps, double timeout_s);
 size_t gg_get_hbm_budget(void);
 
 /* out = sum_i scalars[idx(i)] * P_i as a Jacobian point (gnark G1Jac/G2Jac
