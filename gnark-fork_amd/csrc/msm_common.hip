@@ -291,7 +291,8 @@ __device__ __forceinline__ void scalar_keys(const Fe<SC>& scl, int c, int W, con
 // A batch of nvec scalar vectors over one base (same-base commitments): block
 // column = v vblocks + tile, vector v's keys in rows v W + w, its buckets in
 // groups v G .. v G + G - 1 (sort_entries).
-template <class SC>
+// SPT = scalars per thread (spb <= 256 SPT), all loaded before any digit work
+template <class SC, int SPT>
 __global__ void __launch_bounds__(256) k_digits_hist(VecPtrs vp, const uint32_t* sidx,
                                                      size_t n, int c, int W, WinSpec ws, int G, int kbits,
                                                      int spb, int nbins, int h, uint32_t* keys, size_t kst,
@@ -305,11 +306,10 @@ __global__ void __launch_bounds__(256) k_digits_hist(VecPtrs vp, const uint32_t*
     uint32_t* vkeys = keys + (size_t)v * W * kst;
     for (int j = threadIdx.x; j < nbins; j += blockDim.x) hh[j] = 0;
     __syncthreads();
-    // spb <= 512: at most two scalars per thread, both loaded before any digit work
-    Fe<SC> scl[2];
-    size_t idx[2];
+    Fe<SC> scl[SPT];
+    size_t idx[SPT];
 #pragma unroll
-    for (int s = 0; s < 2; s++) {
+    for (int s = 0; s < SPT; s++) {
         idx[s] = ~(size_t)0;
         if (s * 256 + (int)threadIdx.x < spb) {
             size_t i = (size_t)tile * spb + s * 256 + threadIdx.x;
@@ -320,7 +320,7 @@ __global__ void __launch_bounds__(256) k_digits_hist(VecPtrs vp, const uint32_t*
         }
     }
 #pragma unroll
-    for (int s = 0; s < 2; s++) {
+    for (int s = 0; s < SPT; s++) {
         if (idx[s] == ~(size_t)0) continue;
         const size_t i = idx[s];
         scalar_keys<SC>(scl[s], c, W, ws, G, slog, sres, v * (uint32_t)G, [&](int w, uint32_t key) {
@@ -630,9 +630,9 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const VecPtrs& vp, hipStream
     sort_plan(kbits + 1, h, rs);
     const int nbins = 1 << h;
     int spb = sort_spb(W);
-    if (const char* e = getenv("GG_SORT_SPB")) {  // tuning override: a smaller power of two
-        const int v = atoi(e);
-        if (v >= 32 && v <= spb && (v & (v - 1)) == 0) spb = v;
+    if (const char* e = getenv("GG_SORT_SPB")) {  // tuning override: a power of two, 32..1024,
+        const int v = atoi(e);                     // the bin-scatter tile spb W <= 16384 entries
+        if (v >= 32 && v <= 1024 && (v & (v - 1)) == 0 && v * W <= 16384) spb = v;
     }
     const uint32_t vblocks = (uint32_t)((n + spb - 1) / spb);  // per vector
     const uint32_t nblocks = vblocks * (uint32_t)s->nvec;
@@ -664,17 +664,15 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const VecPtrs& vp, hipStream
         s->chunk_hist.reserve(ch_max * 4);
         s->chunk_pos.reserve((ch_max + 1) * 4);
     }
-    if (b->scurve)
-        hipLaunchKernelGGL(k_digits_hist<FrBlsCfg>, dim3(nblocks), dim3(256), nbins * 4, st, vp,
+    {
+        auto* const hk = b->scurve ? (spb > 512 ? &k_digits_hist<FrBlsCfg, 4> : &k_digits_hist<FrBlsCfg, 2>)
+                                   : (spb > 512 ? &k_digits_hist<FrCfg, 4> : &k_digits_hist<FrCfg, 2>);
+        hipLaunchKernelGGL(hk, dim3(nblocks), dim3(256), nbins * 4, st, vp,
                            b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, G, kbits, spb, nbins,
                            h, s->keys.as<uint32_t>(), kst, s->hist.as<uint32_t>(), nblocks, vblocks, s->slog,
                            s->sres);
-    else
-        hipLaunchKernelGGL(k_digits_hist<FrCfg>, dim3(nblocks), dim3(256), nbins * 4, st, vp,
-                           b->has_sidx ? b->sidx.as<uint32_t>() : nullptr, n, c, W, b->win, G, kbits, spb, nbins,
-                           h, s->keys.as<uint32_t>(), kst, s->hist.as<uint32_t>(), nblocks, vblocks, s->slog,
-                           s->sres);
-    GG_HIP(hipGetLastError());
+        GG_HIP(hipGetLastError());
+    }
     exclusive_scan(s->hist.as<uint32_t>(), s->hoff.as<uint32_t>(), nh, st, s->scan_tmp);
     // segment starts ping-pong between bin_start and seg2; the last pass writes offsets
     DevBuf* segb[2] = {&s->bin_start, &s->seg2};
@@ -684,6 +682,8 @@ void sort_entries(const gg_msm_base* b, MsmSort* s, const VecPtrs& vp, hipStream
     GG_HIP(hipGetLastError());
     const size_t lds_c = (2 * (size_t)nbins + 2 * (size_t)spb * W) * 4;
     GG_CHECK(lds_c <= 160 * 1024, GG_ERR_INTERNAL, "bin scatter LDS tile too large");
+    if (lds_c > 64 * 1024)  // GG_SORT_SPB tiles past 64 KiB: opt in to the CU's 160 KiB
+        GG_HIP(hipFuncSetAttribute((const void*)k_bin_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_c));
     GG_CHECK(nbins <= 256, GG_ERR_INTERNAL, "bin scatter: one bin per thread");
     // scatter stage j (0 = bin scatter) writes entries to `sorted` when the number
     // of stages after it is even, else tmp_entry; keys to tmp_key (j even) / keys (j odd)
