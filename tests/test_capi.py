@@ -168,6 +168,10 @@ def test_bounded_wait_times_out_instead_of_blocking():
     assert _lib.lib.gg_set_wait_timeout(12.5) == 0 and _lib.lib.gg_get_wait_timeout() == 12.5
     assert _lib.lib.gg_set_wait_timeout(0) == 0 and _lib.lib.gg_get_wait_timeout() > 0
     assert _lib.lib.gg_set_wait_timeout(-1) == 1
+    # the real-stream variant (tests/test_gpu_wait_timeout.py) checks its
+    # arguments before touching the device
+    assert _lib.lib.gg_wait_selftest_device(10, 0.0) == 1
+    assert _lib.lib.gg_wait_selftest_device((1 << 20) + 1, 1.0) == 1
 
 
 def test_msm_batch_shape_refuses_32bit_overflow():
