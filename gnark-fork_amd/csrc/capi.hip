@@ -4,6 +4,7 @@
 #include <cstring>
 #include <atomic>
 #include <chrono>
+#include <deque>
 #include <map>
 #include <thread>
 #include <mutex>
@@ -190,6 +191,52 @@ extern "C" int gg_release_task_queues(void) {
     }
     for (int d : devs) drop_idle_task_queues(d);
     GG_CAPI_END
+}
+
+// ---- kept worker threads (common.h run_task)
+namespace {
+struct WorkerPool {
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> q;
+    int idle = 0;
+};
+WorkerPool& worker_pool() {
+    static WorkerPool* p = new WorkerPool();  // never destroyed: its workers outlive static teardown
+    return *p;
+}
+void pool_worker() {
+    WorkerPool& P = worker_pool();
+    std::unique_lock<std::mutex> l(P.m);
+    for (;;) {
+        P.idle++;
+        P.cv.wait(l, [&] { return !P.q.empty(); });
+        P.idle--;
+        std::function<void()> fn = std::move(P.q.front());
+        P.q.pop_front();
+        l.unlock();
+        fn();  // TaskState::run catches everything
+        l.lock();
+    }
+}
+}  // namespace
+
+bool gg::pool_enabled() {
+    static const bool on = !(getenv("GG_TASK_POOL") && atoi(getenv("GG_TASK_POOL")) == 0);
+    return on;
+}
+
+void gg::pool_post(std::function<void()> fn) {
+    if (!pool_enabled()) {  // A/B: a fresh thread per task, as std::async
+        std::thread(std::move(fn)).detach();
+        return;
+    }
+    WorkerPool& P = worker_pool();
+    std::lock_guard<std::mutex> l(P.m);
+    P.q.push_back(std::move(fn));
+    // every queued task has a worker to take it: an idle one, else a new one
+    if (P.idle >= (int)P.q.size()) P.cv.notify_one();
+    else std::thread(pool_worker).detach();
 }
 
 // ---- bounded waits (common.h)

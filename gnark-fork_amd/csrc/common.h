@@ -7,7 +7,11 @@
 #include <cstdio>
 #include <vector>
 #include <condition_variable>
+#include <exception>
+#include <functional>
+#include <memory>
 #include <mutex>
+#include <type_traits>
 #include "../../include/gnark_amd.h"
 
 // -DGG_ACCUM_PROBE=1 builds a traffic-attribution variant (build_var/, never
@@ -219,6 +223,106 @@ struct PartBarrier {
     void abort();
     void reset();
 };
+
+// ---- host tasks on kept worker threads (round 6).  The provers start a host
+// thread per concurrent task (a Groth16 MSM, a PlonK part's slice MSM, the ratio
+// slice of a part, ...): std::async made a fresh thread each time, which pays the
+// thread's creation and the HIP runtime's per-thread set-up before its first
+// launch -- on the critical path of every stage hand-over.  run_task posts the
+// task to a process-wide set of workers instead, which grows whenever no worker
+// is idle (a task that waits for another task never starves) and keeps its
+// threads.  The task runs on the submitting thread's current device.  Task<R>
+// keeps std::async's contract: get() rethrows the task's exception, and the
+// last copy of a Task waits for the task when it goes away, so a task may refer
+// to its caller's locals.  GG_TASK_POOL=0: a fresh thread per task (A/B).
+bool pool_enabled();
+void pool_post(std::function<void()> fn);
+template <class R>
+struct TaskState {
+    std::mutex m;
+    std::condition_variable cv;
+    bool done = false;
+    std::exception_ptr ex;
+    std::function<void()> deferred;  // run by the first waiter (deferred tasks)
+    typename std::conditional<std::is_void<R>::value, char, R>::type val{};
+    void wait() {
+        std::function<void()> d;
+        {
+            std::unique_lock<std::mutex> l(m);
+            if (!deferred) {
+                cv.wait(l, [&] { return done; });
+                return;
+            }
+            d.swap(deferred);
+        }
+        d();
+    }
+    // the last handle goes: wait for a started task, drop a deferred one (as a
+    // std::async future does)
+    void release() {
+        std::unique_lock<std::mutex> l(m);
+        if (deferred) {
+            deferred = nullptr;
+            return;
+        }
+        cv.wait(l, [&] { return done; });
+    }
+    template <class Fn>
+    void run(Fn& fn) {
+        try {
+            if constexpr (std::is_void<R>::value) fn();
+            else val = fn();
+        } catch (...) {
+            ex = std::current_exception();
+        }
+        {
+            std::lock_guard<std::mutex> l(m);
+            done = true;
+        }
+        cv.notify_all();
+    }
+};
+template <class R>
+class Task {
+    struct Guard {
+        std::shared_ptr<TaskState<R>> st;
+        ~Guard() {
+            if (st) st->release();
+        }
+    };
+    std::shared_ptr<Guard> g_;
+
+   public:
+    Task() = default;
+    explicit Task(std::shared_ptr<TaskState<R>> st) : g_(new Guard{std::move(st)}) {}
+    bool valid() const { return (bool)g_; }
+    void wait() const { g_->st->wait(); }
+    R get() const {
+        wait();
+        if (g_->st->ex) std::rethrow_exception(g_->st->ex);
+        if constexpr (!std::is_void<R>::value) return g_->st->val;
+    }
+    Task share() const { return *this; }
+};
+// fn on a kept worker (deferred: on the first get() / wait(), the serial modes)
+template <class Fn>
+auto run_task(Fn fn, bool deferred = false) -> Task<decltype(fn())> {
+    using R = decltype(fn());
+    auto st = std::make_shared<TaskState<R>>();
+    if (deferred) {
+        TaskState<R>* raw = st.get();  // the state outlives its waiters' calls
+        st->deferred = [raw, fn]() mutable { raw->run(fn); };
+    } else {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        auto job = [st, fn, dev]() mutable {
+            (void)hipSetDevice(dev);
+            st->run(fn);
+        };
+        pool_post(std::function<void()>(std::move(job)));
+    }
+    return Task<R>(st);
+}
 
 inline unsigned grid_for(size_t n, unsigned block) {
     size_t g = (n + block - 1) / block;

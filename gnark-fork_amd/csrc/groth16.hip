@@ -559,10 +559,10 @@ static void partials_get(int curve, const void* in, G16Partials& p) {
 // Joins every worker on scope exit, also while an exception unwinds (the
 // workers reference locals of prove_device, declared before the joiner).
 struct Joiner {
-    std::vector<std::thread>& v;
+    std::vector<gg::Task<void>>& v;
     ~Joiner() {
         for (auto& t : v)
-            if (t.joinable()) t.join();
+            if (t.valid()) t.wait();
     }
 };
 
@@ -619,11 +619,11 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
     };
     // GG_G16_SERIAL=1 runs the tasks one after another (per-stage isolated timings)
     const bool serial = getenv("GG_G16_SERIAL") && atoi(getenv("GG_G16_SERIAL"));
-    std::vector<std::thread> workers;
+    std::vector<gg::Task<void>> workers;  // on kept worker threads (common.h run_task)
     Joiner joiner{workers};
     auto spawn = [&](auto fn) {
         if (serial) fn();
-        else workers.emplace_back(fn);
+        else workers.push_back(gg::run_task(fn));
     };
     // A, B, C -> device (or the distributed H's cyclic slices), on the H task
     auto inputs_abc = [&](Fr*& A, Fr*& B, Fr*& C, size_t& len) {
@@ -722,7 +722,7 @@ static void prove_device(gg_groth16_pk* pk, const void* wires, const void* sol_a
         guarded([&] { msm_finish_dev(pk->B2, sB2, out.b2, pk->s0, xB2); })();
         te = now_ms();
     }
-    for (auto& w : workers) w.join();
+    for (auto& w : workers) w.wait();
     if (wcode != GG_OK) throw Error(wcode, werr);
     g_timings[0] = t_up - t0;
     g_timings[1] = t_h;
@@ -744,7 +744,7 @@ struct G16Fixed {
 };
 
 template <class Cv>
-static std::future<G16Fixed<Cv>> fixed_terms_async(const void* delta_aff, const void* delta2_aff, const void* r_mont,
+static gg::Task<G16Fixed<Cv>> fixed_terms_async(const void* delta_aff, const void* delta2_aff, const void* r_mont,
                                                    const void* s_mont) {
     using G1 = typename Cv::G1F;
     using G2 = typename Cv::G2F;
@@ -752,16 +752,16 @@ static std::future<G16Fixed<Cv>> fixed_terms_async(const void* delta_aff, const 
     const Affine<G1> delta = from_bytes<Affine<G1>>(delta_aff);
     const Affine<G2> delta2 = from_bytes<Affine<G2>>(delta2_aff);
     const FrT r = from_bytes<FrT>(r_mont), s = from_bytes<FrT>(s_mont);
-    return std::async(std::launch::async, [delta, delta2, r, s] {
+    return gg::run_task([delta, delta2, r, s] {
         G16Fixed<Cv> f;
         FrT kr = -(r * s);
         f.rc = from_mont(r);
         f.sc = from_mont(s);
         FrT krc = from_mont(kr);
         Jac<G1> dl = Jac<G1>::from_affine(delta);
-        auto f_rd = std::async(std::launch::async, [&] { return jac_mul(dl, f.rc.v); });
-        auto f_sd = std::async(std::launch::async, [&] { return jac_mul(dl, f.sc.v); });
-        auto f_sd2 = std::async(std::launch::async, [&] { return jac_mul(Jac<G2>::from_affine(delta2), f.sc.v); });
+        auto f_rd = gg::run_task([&] { return jac_mul(dl, f.rc.v); });
+        auto f_sd = gg::run_task([&] { return jac_mul(dl, f.sc.v); });
+        auto f_sd2 = gg::run_task([&] { return jac_mul(Jac<G2>::from_affine(delta2), f.sc.v); });
         f.krd = jac_mul(dl, krc.v);
         f.rd = f_rd.get();
         f.sd = f_sd.get();
@@ -786,7 +786,7 @@ static void g16_combine(const G16Partials& p, const G16Fixed<Cv>& f, const void*
     const Jac<G2> pb2 = from_bytes<Jac<G2>>(p.b2);
     Jac<G1> ar = jac_add(jac_add_affine(pa, alpha), f.rd);
     Jac<G1> bs1 = jac_add(jac_add_affine(pb1, beta), f.sd);
-    auto f_sar = std::async(std::launch::async, [&] { return jac_mul(ar, f.sc.v); });
+    auto f_sar = gg::run_task([&] { return jac_mul(ar, f.sc.v); });
     Jac<G1> rbs = jac_mul(bs1, f.rc.v);
     Jac<G1> krs = jac_add(jac_add(pk, f.krd), pz);
     krs = jac_add(krs, f_sar.get());
@@ -920,8 +920,8 @@ extern "C" int gg_groth16_finalize_ex(int curve, const void* alpha1, const void*
 
 struct gg_g16_fixed {
     int curve = GG_CURVE_BN254;
-    std::future<G16Fixed<CurveBn254>> bn;
-    std::future<G16Fixed<CurveBls12381>> bls;
+    gg::Task<G16Fixed<CurveBn254>> bn;
+    gg::Task<G16Fixed<CurveBls12381>> bls;
 };
 
 extern "C" int gg_groth16_finalize_begin(int curve, const void* delta1, const void* delta2, const void* r_mont,

@@ -514,7 +514,7 @@ static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStr
     BJac j = BJac::inf();
     const bool kz = base == pk->kzg;
     const size_t lo = kz ? pk->k_lo : pk->l_lo;
-    std::vector<std::future<BJac>> fs;
+    std::vector<gg::Task<BJac>> fs;
     if (peers_active(pk)) {
         // the peers' threads start at once; each waits for the scalars (complete
         // at this point of st) before its copy -- not for a resident slice
@@ -522,7 +522,7 @@ static BJac msm_jac(Key* pk, gg_msm_base_t base, int wi, const FrB* scal, hipStr
         GG_HIP(hipEventRecord(ready, st));
         for (size_t q = 0; q < pk->peers.size(); q++)
             if (part_runs(pk, (int)q + 1))
-                fs.push_back(std::async(std::launch::async, [pk, q, pp = pk->peers[q].get(), kz, wi, scal, peer_resident,
+                fs.push_back(gg::run_task([pk, q, pp = pk->peers[q].get(), kz, wi, scal, peer_resident,
                                                              ready] {
                     if (!peer_resident) GG_WAIT_EVENT(ready);
                     return peer_msm(pk, (int)q + 1, pp, kz, wi, scal, peer_resident);
@@ -597,14 +597,14 @@ static void msm_jac_batch(Key* pk, gg_msm_base_t base, const FrB* const* scal, i
     const bool kz = base == pk->kzg;
     const size_t lo = kz ? pk->k_lo : pk->l_lo;
     for (int v = 0; v < nv; v++) out[v] = BJac::inf();
-    std::vector<std::future<std::vector<BJac>>> fs;
+    std::vector<gg::Task<std::vector<BJac>>> fs;
     if (peers_active(pk)) {
         hipEvent_t ready = pk->msm_ready[0];
         GG_HIP(hipEventRecord(ready, st));
         std::vector<const FrB*> sc(scal, scal + nv);
         for (size_t q = 0; q < pk->peers.size(); q++)
             if (part_runs(pk, (int)q + 1))
-                fs.push_back(std::async(std::launch::async, [pk, q, pp = pk->peers[q].get(), kz, sc, nv, ready] {
+                fs.push_back(gg::run_task([pk, q, pp = pk->peers[q].get(), kz, sc, nv, ready] {
                     GG_WAIT_EVENT(ready);
                     std::vector<BJac> r(nv);
                     peer_msm_batch(pk, (int)q + 1, pp, kz, sc.data(), nv, r.data());
@@ -1166,6 +1166,11 @@ static std::launch msm_policy() {
     static const bool serial = getenv("GG_PLONK_SERIAL") && atoi(getenv("GG_PLONK_SERIAL"));
     return serial ? std::launch::deferred : std::launch::async;
 }
+// a commitment's MSM task: on a kept worker, or deferred to its get() (GG_PLONK_SERIAL)
+template <class Fn>
+static auto msm_task(Fn fn) {
+    return gg::run_task(std::move(fn), msm_policy() == std::launch::deferred);
+}
 
 static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* pub, size_t nb_pub,
            const void* const* cmt_values, const BAff* cmt_digests, const FrB* cmt_hashed, int n_cmt,
@@ -1198,14 +1203,14 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     // multi-part keys: the canonical forms on the peers (canon_tasks), L R O as
     // soon as uploaded, Qk and Pi_j at once; Z after the ratio
     const std::vector<int> ctasks = dz ? canon_tasks(pk) : std::vector<int>();
-    std::vector<std::shared_future<void>> cfut(pk->peers.size());  // per owner: its tasks before Z, in order
+    std::vector<gg::Task<void>> cfut(pk->peers.size());  // per owner: its tasks before Z, in order
     if (peers_on) {
         for (size_t pi = 0; pi < pk->peers.size(); pi++) {
             std::vector<int> mine;
             for (size_t i = 0; i + 1 < ctasks.size(); i++)
                 if (i % pk->peers.size() == pi) mine.push_back(ctasks[i]);
             if (mine.empty() || !part_runs(pk, (int)pi + 1)) continue;
-            cfut[pi] = std::async(std::launch::async, [&, pi, mine] {
+            cfut[pi] = gg::run_task([&, pi, mine] {
                 PlonkPeer* p = pk->peers[pi].get();
                 for (int b : mine) {
                     if (b < 3)
@@ -1229,23 +1234,23 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         }
     }
     // blinding commitments of L, R, O, Z on host threads while the GPU works
-    std::future<BJac> fblind[4];
-    for (int q = 0; q < 4; q++) fblind[q] = std::async(std::launch::async, [pk, &bp, q] { return blind_commit(pk, bp[q]); });
+    gg::Task<BJac> fblind[4];
+    for (int q = 0; q < 4; q++) fblind[q] = gg::run_task([pk, &bp, q] { return blind_commit(pk, bp[q]); });
     // ---- commitToLRO: three KZG MSMs on pk.KzgLagrange at once
     BJac lroj[3];
     {
-        std::vector<std::future<void>> fs;
+        std::vector<gg::Task<void>> fs;
         if (batch_ok(pk, false, 3)) {
             // one batched MSM on s[0] once L, R, O are uploaded
             for (int k = 1; k < 3; k++) GG_HIP(hipStreamWaitEvent(s[0], uploaded[k], 0));
-            fs.push_back(std::async(msm_policy(), [&] {
+            fs.push_back(msm_task([&] {
                 GG_HIP(hipSetDevice(pk->device));
                 const FrB* sc[3] = {F(pk->lag[0]), F(pk->lag[1]), F(pk->lag[2])};
                 msm_jac_batch(pk, pk->kzg_lag, sc, 3, s[0], lroj);
             }));
         } else {
             for (int k = 0; k < 3; k++)
-                fs.push_back(std::async(msm_policy(), [&, k] {
+                fs.push_back(msm_task([&, k] {
                     GG_HIP(hipSetDevice(pk->device));
                     lroj[k] = msm_jac(pk, pk->kzg_lag, k, F(pk->lag[k]), s[k]);
                 }));
@@ -1318,10 +1323,10 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         std::promise<void> pre_ready;
         std::shared_future<void> pre_f = pre_ready.get_future().share();
         std::atomic<bool> stop{false};
-        std::vector<std::future<void>> pf;
+        std::vector<gg::Task<void>> pf;
         if (peers_on)
             for (size_t q = 0; q < pk->peers.size(); q++)
-                pf.push_back(std::async(std::launch::async, [&, q] {
+                pf.push_back(gg::run_task([&, q] {
                     PlonkPeer* p = pk->peers[q].get();
                     const size_t cnt = p->l_hi - p->l_lo;
                     const bool mine = cnt && part_runs(pk, (int)q + 1);
@@ -1375,12 +1380,12 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         pk->ptimes[0].ratio_ms += ms_since(ta);
     }
     record_wait(pk, s[0], s[1]);
-    std::shared_future<void> zfut;
+    gg::Task<void> zfut;
     if (peers_on) {  // Z's canonical forms on its owner, once every slice has landed there
         GG_WAIT_STREAM(s[0]);
         const size_t zi = (ctasks.size() - 1) % pk->peers.size();
         if (part_runs(pk, (int)zi + 1))
-            zfut = std::async(std::launch::async, [&, zi] {
+            zfut = gg::run_task([&, zi] {
             if (cfut[zi].valid()) cfut[zi].wait();  // its earlier tasks (creg, stream cs) first
             canon_run(pk, zi, 3, F(pk->cbrev[3]), F(pk->can[3]), [](hipStream_t) {});
         }).share();
@@ -1389,7 +1394,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     }
     // the Z commitment in flight; meanwhile each part's first quotient unit takes
     // its evaluations of L, R, O, Qk, Pi_j (only Z's wait for Z)
-    std::future<BJac> fzc = std::async(msm_policy(), [&] {
+    gg::Task<BJac> fzc = msm_task([&] {
         GG_HIP(hipSetDevice(pk->device));
         return msm_jac(pk, pk->kzg_lag, 0, F(pk->zlag), s[0], peers_on);
     });
@@ -1516,7 +1521,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
             ntt_inverse_dit_noscale(q->dom, local ? (void*)cres : (void*)(cres + blk * m), st);
         }
     };
-    std::vector<std::future<void>> peer_work;
+    std::vector<gg::Task<void>> peer_work;
     if (peers_on) {  // Z's canonical form pushed by its owner
         const auto w = std::chrono::steady_clock::now();
         if (zfut.valid()) zfut.get();
@@ -1527,7 +1532,7 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         for (size_t pi = 0; pi < pk->peers.size(); pi++) {
             PlonkPeer* p = pk->peers[pi].get();
             if (p->units.empty() || !part_runs(pk, (int)pi + 1)) continue;
-            peer_work.push_back(std::async(std::launch::async, [&, p, pi] {
+            peer_work.push_back(gg::run_task([&, p, pi] {
                 GG_HIP(hipSetDevice(p->device));
                 const auto ta = std::chrono::steady_clock::now();
                 hipStream_t q = p->s[3];
@@ -1601,9 +1606,9 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
             const FrB* sc[3] = {F(pk->hpad[0]), F(pk->hpad[1]), F(pk->hpad[2])};
             msm_jac_batch(pk, pk->kzg, sc, 3, s[0], hj);
         } else {
-            std::vector<std::future<void>> fs3;
+            std::vector<gg::Task<void>> fs3;
             for (int k = 0; k < 3; k++)
-                fs3.push_back(std::async(msm_policy(), [&, k] {
+                fs3.push_back(msm_task([&, k] {
                     GG_HIP(hipSetDevice(pk->device));
                     hj[k] = commit_kzg(pk, k, F(pk->hpad[k]), s[k]);
                 }));
@@ -1639,9 +1644,9 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
     // evaluations and kernel.  Default: openZ's MSM at once on s[0]
     static const bool open_batch_env = getenv("GG_PLONK_BATCH_OPEN") && atoi(getenv("GG_PLONK_BATCH_OPEN")) == 1;
     const bool open_batch = open_batch_env && batch_ok(pk, true, 2);
-    std::future<BJac> fzs;
+    gg::Task<BJac> fzs;
     if (!open_batch)
-        fzs = std::async(msm_policy(), [&] {
+        fzs = msm_task([&] {
             GG_HIP(hipSetDevice(pk->device));
             return commit_kzg(pk, 0, F(pk->q1), s[0]);
         });
