@@ -182,9 +182,9 @@ void on_shards(gg_groth16_mpk* m, Fn fn) {
     std::string err;
     int code = GG_OK;
     bool echo_only = false;
-    std::vector<std::thread> th;
+    std::vector<gg::Task<void>> th;  // kept worker threads (common.h run_task); all shards run at once
     for (int r = 0; r < m->world; r++)
-        th.emplace_back([&, r] {
+        th.push_back(gg::run_task([&, r] {
             int rc = gg_set_device(m->dev[r]);
             std::string msg = rc ? gg_last_error() : "";
             if (!rc) {
@@ -202,8 +202,8 @@ void on_shards(gg_groth16_mpk* m, Fn fn) {
                     err = "shard " + std::to_string(r) + " (device " + std::to_string(m->dev[r]) + "): " + msg;
                 }
             }
-        });
-    for (auto& t : th) t.join();
+        }));
+    for (auto& t : th) t.wait();
     if (code != GG_OK) throw gg::Error(code, err);
 }
 
