@@ -1322,28 +1322,29 @@ inline std::vector<Xyzz<F>> reduce_terms_multi(std::vector<RedItem<F>> items, in
         if (m < 0 && !r.is_inf()) r.y = -r.y;
         return r;
     };
-    for (size_t k = 0; k < host_items.size(); k++) {
-        const auto& X = hx[k];
-        Xyzz<F> run = Xyzz<F>::inf(), acc = Xyzz<F>::inf();
-        auto& vr = vals[host_items[k].res];
-        if (host_items[k].plain) {
-            for (const auto& x : X) acc = xyzz_add(acc, x);
-            vr.push_back({host_items[k].mlog, scaled(acc, host_items[k].mult)});
-            continue;
-        }
-        for (size_t j = X.size(); j-- > 1;) {
-            run = xyzz_add(run, X[j]);
-            acc = xyzz_add(acc, run);
-        }
-        if (host_items[k].off) {
-            run = xyzz_add(run, X[0]);  // run = sum of all
-            for (uint32_t o = 0; o < host_items[k].off; o++) acc = xyzz_add(acc, run);
-        }
-        vr.push_back({host_items[k].mlog, scaled(acc, host_items[k].mult)});
-    }
-    std::vector<Xyzz<F>> out(nres, Xyzz<F>::inf());
-    for (int r = 0; r < nres; r++) {
+    // result r: its items' sums, then Horner over their 2^mlog factors (r06q: the
+    // results of a batch finished side by side on kept workers measured neutral)
+    auto finish = [&](int r) {
         auto& vr = vals[r];
+        for (size_t k = 0; k < host_items.size(); k++) {
+            if (host_items[k].res != r) continue;
+            const auto& X = hx[k];
+            Xyzz<F> run = Xyzz<F>::inf(), acc = Xyzz<F>::inf();
+            if (host_items[k].plain) {
+                for (const auto& x : X) acc = xyzz_add(acc, x);
+                vr.push_back({host_items[k].mlog, scaled(acc, host_items[k].mult)});
+                continue;
+            }
+            for (size_t j = X.size(); j-- > 1;) {
+                run = xyzz_add(run, X[j]);
+                acc = xyzz_add(acc, run);
+            }
+            if (host_items[k].off) {
+                run = xyzz_add(run, X[0]);  // run = sum of all
+                for (uint32_t o = 0; o < host_items[k].off; o++) acc = xyzz_add(acc, run);
+            }
+            vr.push_back({host_items[k].mlog, scaled(acc, host_items[k].mult)});
+        }
         std::sort(vr.begin(), vr.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
         Xyzz<F> acc = Xyzz<F>::inf();
         int cur = vr.empty() ? 0 : vr[0].first;
@@ -1352,8 +1353,10 @@ inline std::vector<Xyzz<F>> reduce_terms_multi(std::vector<RedItem<F>> items, in
             acc = xyzz_add(acc, v.second);
         }
         for (; cur > 0; cur--) acc = acc.is_inf() ? acc : xyzz_dbl(acc);
-        out[r] = acc;
-    }
+        return acc;
+    };
+    std::vector<Xyzz<F>> out(nres, Xyzz<F>::inf());
+    for (int r = 0; r < nres; r++) out[r] = finish(r);
     return out;
 }
 template <class F>

@@ -321,6 +321,29 @@ static BJac jmul(const BAff& p, const FrB& k) {
     return jac_mul(BJac::from_affine(p), c.v);
 }
 static BAff to_aff(const BJac& j) { return jac_to_affine(j); }
+// k <= 4 points with one field inversion (Montgomery's trick): the commitments
+// of a stage come out together, and each host inversion is ~25 us on the
+// critical path of the stage's hand-over (r06p HIP trace)
+static void to_aff_batch(const BJac* j, int k, BAff* out) {
+    using Fq = decltype(j[0].z);
+    Fq pre[4];
+    Fq acc = Fq::one();
+    for (int i = 0; i < k; i++) {
+        pre[i] = acc;
+        if (!j[i].is_inf()) acc = acc * j[i].z;
+    }
+    Fq inv = inverse(acc);
+    for (int i = k - 1; i >= 0; i--) {
+        if (j[i].is_inf()) {
+            out[i] = BAff::inf();
+            continue;
+        }
+        const Fq zi = inv * pre[i];
+        inv = inv * j[i].z;
+        const Fq zi2 = sqr(zi);
+        out[i] = BAff{j[i].x * zi2, j[i].y * zi2 * zi};
+    }
+}
 static FrB frv(uint64_t x) {
     FrB r = FrB::zero();
     r.v[0] = (uint32_t)x;
@@ -1280,7 +1303,11 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
         }
         for (auto& f : fs) f.get();
     }
-    for (int k = 0; k < 3; k++) P.lro[k] = to_aff(jac_add(red(pk, lroj[k]), fblind[k].get()));
+    {
+        BJac t[3];
+        for (int k = 0; k < 3; k++) t[k] = jac_add(red(pk, lroj[k]), fblind[k].get());
+        to_aff_batch(t, 3, P.lro);
+    }
     mark();
     // ---- gamma, beta (deriveGammaAndBeta, prove.go:454-489; bindPublicData, verify.go:296-340).
     // G1Affine.Marshal is the UNCOMPRESSED encoding (RawBytes): groth16/bls12-381/verify.go:80-82
@@ -1614,7 +1641,9 @@ static void prove(Key* pk, const void* const lro_in[3], bool on_dev, const FrB* 
                 }));
             for (auto& f : fs3) f.get();
         }
-        for (int k = 0; k < 3; k++) P.h[k] = to_aff(red(pk, hj[k]));
+        BJac t[3];
+        for (int k = 0; k < 3; k++) t[k] = red(pk, hj[k]);
+        to_aff_batch(t, 3, P.h);
     }
     mark();
     const FrB zeta = derive(fs, "zeta", {&P.h[0], &P.h[1], &P.h[2]});
