@@ -866,65 +866,6 @@ __global__ void __launch_bounds__(256, kSumWaves<F>) k_bucket_sum_r(const typena
     st(Sr + (size_t)(B & ((1u << logL) - 1)) * nseg + (B >> logL), acc);
 }
 
-// The same level 2 in two launches (round 6, GG_MSM_SUM_SPLIT, default on).
-// In k_bucket_sum_r nearly every wave holds a bucket that straddles a range
-// boundary (about one bucket per range does), so every wave ran the group add
-// -- for BN254 G2 a 14-product Fp2 add at one wave per SIMD, for 1 bucket in ~6.
-// k_bucket_pass_r copies the buckets that need no add (inside one range, or
-// empty) at full occupancy and lists the others; k_bucket_add_r adds those,
-// one listed bucket per lane.  The same loads and adds in the same order per
-// bucket: bit-identical partials.
-template <class F>
-__global__ void __launch_bounds__(256) k_bucket_pass_r(const typename PartialOf<F>::T* head,
-                                                       const typename PartialOf<F>::T* tail,
-                                                       const typename PartialOf<F>::T* S, const uint32_t* offsets,
-                                                       uint32_t nb_total, int c, uint32_t K, int logL,
-                                                       typename PartialOf<F>::T* Sr, uint32_t* list,
-                                                       uint32_t* count) {
-    using O = PartialOps<F>;
-    const uint32_t B = blockIdx.x * blockDim.x + threadIdx.x;
-    bool need = false;
-    if (B < nb_total) {  // no early return: the whole wave takes part in the append
-        const uint32_t nseg = nb_total >> logL;
-        const BucketSpan sp = bucket_span(offsets, bucket_perm(B, c), offsets[nb_total], K);
-        need = !sp.empty && sp.t1 > sp.t0;
-        if (!need) {
-            const typename O::T acc =
-                sp.empty ? O::inf() : ld(sp.direct ? S + B : (sp.first ? head : tail) + sp.t0);
-            st(Sr + (size_t)(B & ((1u << logL) - 1)) * nseg + (B >> logL), acc);
-        }
-    }
-    // one vector atomic per wave appends its straddling buckets
-    const uint64_t m = __ballot(need);
-    if (m) {
-        const int lane = __lane_id();
-        const int leader = __ffsll((unsigned long long)m) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
-        base = __shfl(base, leader);
-        if (need) list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = B;
-    }
-}
-// lane i: listed bucket list[i] (i < *count <= the number of ranges: a straddling
-// bucket holds the start of its second range, and no two share one)
-template <class F>
-__global__ void __launch_bounds__(256, kSumWaves<F>) k_bucket_add_r(const typename PartialOf<F>::T* head,
-                                                       const typename PartialOf<F>::T* tail, const uint32_t* offsets,
-                                                       uint32_t nb_total, int c, uint32_t K, int logL,
-                                                       typename PartialOf<F>::T* Sr, const uint32_t* list,
-                                                       const uint32_t* count) {
-    using O = PartialOps<F>;
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *count) return;
-    const uint32_t B = list[i];
-    const uint32_t nseg = nb_total >> logL;
-    const BucketSpan sp = bucket_span(offsets, bucket_perm(B, c), offsets[nb_total], K);
-    typename O::T acc = ld((sp.first ? head : tail) + sp.t0);
-    const uint32_t rend = sp.t1 - sp.t0 > LIGHT ? sp.t0 + 1 : sp.t1;  // heavy: tree result
-    for (uint32_t r = sp.t0 + 1; r <= rend; r++) acc = O::add(acc, ld(head + r));
-    st(Sr + (size_t)(B & ((1u << logL) - 1)) * nseg + (B >> logL), acc);
-}
-
 // k_bucket_runsum: lane t walks the L buckets of segment t (group j = t / T)
 // from the top, R = running sum, A = sum of the running sums =
 // sum_i (i + 1) S_{tL+i}; then D_t = A - L R.  Writes D_t and R_t in gnark's
@@ -1432,12 +1373,7 @@ inline bool segsum_enabled() {
     const char* e = getenv("GG_MSM_SEGSUM");  // per MSM: tests switch it
     return !(e && atoi(e) == 0);
 }
-// GG_MSM_SUM_SPLIT=0: the one-launch level 2 (k_bucket_sum_r) instead of
-// k_bucket_pass_r + k_bucket_add_r (per MSM: tests switch it)
-inline bool sum_split_enabled() {
-    const char* e = getenv("GG_MSM_SUM_SPLIT");
-    return !(e && atoi(e) == 0);
-}
+
 
 // Entries per accumulation range (one thread each).  Every range costs the same,
 // so the grid runs in whole "rounds" of the chip's concurrent threads C (occupancy
@@ -1558,8 +1494,13 @@ inline void msm_finish_multi(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStr
         const char* e = getenv("GG_MSM_SEGSUM_MINLOG");
         return e ? std::max(8, std::min(18, atoi(e))) : 17;
     }();
+    // GG_MSM_SEGS_LOG=s: segments per group >= 2^s (default 17) where L > 2
+    static const int segs_log = [] {
+        const char* e = getenv("GG_MSM_SEGS_LOG");
+        return e ? std::max(12, std::min(20, atoi(e))) : 17;
+    }();
     const int lgb = 31 - __builtin_clz((unsigned)std::max<size_t>(nbg, 1));
-    const int logL = lgb >= 18 ? std::min(4, lgb - 17) : (lgb >= seg_minlog ? 1 : 0);
+    const int logL = lgb >= segs_log + 1 ? std::min(4, lgb - segs_log) : (lgb >= seg_minlog ? 1 : 0);
     if constexpr (kSegsumGroup<F>) {
         if (segsum_enabled() && logL >= 1) {
             // level 2 and the weighted sums in radix form, a lane per bucket / segment
@@ -1571,27 +1512,16 @@ inline void msm_finish_multi(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStr
                 stride *= fan;
             }
             const uint32_t Tg = (uint32_t)(nbg >> logL), G = (uint32_t)Ge;
-            // + the split level 2's list of straddling buckets (<= T) and its count
-            scr->seg.reserve(2 * (size_t)G * Tg * sizeof(Xyzz<F>) + nb * sizeof(PT) + ((size_t)T + 64) * 4);
+            scr->seg.reserve(2 * (size_t)G * Tg * sizeof(Xyzz<F>) + nb * sizeof(PT));
             Xyzz<F>* D = scr->seg.as<Xyzz<F>>();
             Xyzz<F>* Rs = D + (size_t)G * Tg;
             PT* Sr = reinterpret_cast<PT*>(Rs + (size_t)G * Tg);
-            if (sum_split_enabled()) {
-                uint32_t* lst = reinterpret_cast<uint32_t*>(Sr + nb);
-                uint32_t* cnt = lst + T + 32;
-                GG_HIP(hipMemsetAsync(cnt, 0, 4, st));
-                hipLaunchKernelGGL(k_bucket_pass_r<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, (const PT*)hP,
-                                   (const PT*)tP, (const PT*)SP, offs, (uint32_t)nb, ce, K, logL, Sr, lst, cnt);
-                GG_HIP(hipGetLastError());
-                hipLaunchKernelGGL(k_bucket_add_r<F>, dim3(grid_for(T, 256)), dim3(256), 0, st, (const PT*)hP,
-                                   (const PT*)tP, offs, (uint32_t)nb, ce, K, logL, Sr, (const uint32_t*)lst,
-                                   (const uint32_t*)cnt);
-                GG_HIP(hipGetLastError());
-            } else {
-                hipLaunchKernelGGL(k_bucket_sum_r<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, (const PT*)hP,
-                                   (const PT*)tP, (const PT*)SP, offs, (uint32_t)nb, ce, K, logL, Sr);
-                GG_HIP(hipGetLastError());
-            }
+            // (r06r: this level 2 split into a copy pass that lists the buckets
+            // straddling a range boundary and an add pass over the list measured
+            // slower -- the adds of those buckets are the kernel's time either way)
+            hipLaunchKernelGGL(k_bucket_sum_r<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, (const PT*)hP,
+                               (const PT*)tP, (const PT*)SP, offs, (uint32_t)nb, ce, K, logL, Sr);
+            GG_HIP(hipGetLastError());
             hipLaunchKernelGGL(k_bucket_runsum<F>, dim3(grid_for((size_t)G * Tg, 256)), dim3(256), 0, st,
                                (const PT*)Sr, (uint32_t)(G * Tg), logL, D, Rs);
             GG_HIP(hipGetLastError());
