@@ -372,6 +372,53 @@ extern "C" int gg_wait_selftest(int parties, int arriving, double timeout_s) {
     GG_CAPI_END
 }
 
+// host-only self-test of the kept worker threads (common.h run_task): n tasks
+// that all wait at one barrier (they need n workers at once: the set grows),
+// the last of them failing after it; its error comes back through get().  A
+// dropped deferred task never runs, a waited one runs once.
+extern "C" int gg_task_selftest(int n) {
+    GG_CAPI_BEGIN
+    GG_CHECK(n >= 1 && n <= 256, GG_ERR_INVALID_ARG, "1 <= n <= 256");
+    const double saved = g_wait_timeout.load();
+    g_wait_timeout.store(20.0);
+    gg::PartBarrier bar;
+    bar.n = n;
+    std::atomic<int> ran{0};
+    std::vector<gg::Task<int>> t;
+    for (int i = 0; i < n; i++)
+        t.push_back(gg::run_task([i, n, &bar, &ran]() -> int {
+            gg::WaitScope ws("selftest task " + std::to_string(i));
+            const int rc = bar.wait("the other tasks");
+            if (rc) throw gg::Error(rc, gg_last_error());
+            ran++;
+            if (i == n - 1) throw gg::Error(GG_ERR_INTERNAL, "selftest: the last task fails");
+            return i;
+        }));
+    int code = GG_OK;
+    std::string msg;
+    for (int i = 0; i < n; i++) {
+        try {
+            GG_CHECK(t[i].get() == i, GG_ERR_INTERNAL, "selftest: a task returned the wrong value");
+        } catch (const gg::Error& e) {
+            if (code == GG_OK) {
+                code = e.code;
+                msg = e.what();
+            }
+        }
+    }
+    g_wait_timeout.store(saved);
+    GG_CHECK(ran.load() == n, code ? code : GG_ERR_INTERNAL, "selftest: not every task passed the barrier: " + msg);
+    GG_CHECK(code == GG_ERR_INTERNAL && msg.find("the last task fails") != std::string::npos, GG_ERR_INTERNAL,
+             "selftest: the failing task's error did not come back: " + msg);
+    bool dropped_ran = false;
+    { auto d = gg::run_task([&dropped_ran] { dropped_ran = true; return 0; }, true); }
+    GG_CHECK(!dropped_ran, GG_ERR_INTERNAL, "selftest: a dropped deferred task ran");
+    int calls = 0;
+    auto w = gg::run_task([&calls] { return ++calls; }, true);
+    GG_CHECK(w.get() == 1 && w.get() == 1 && calls == 1, GG_ERR_INTERNAL, "selftest: a deferred task did not run once");
+    GG_CAPI_END
+}
+
 namespace {
 // one wave that sleeps `sleeps` times (s_sleep 127: ~8k cycles each) and
 // writes a flag; every wave reaches the end on its own

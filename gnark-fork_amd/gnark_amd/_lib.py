@@ -87,6 +87,7 @@ def _load():
         "gg_get_wait_timeout": ([], ctypes.c_double),
         "gg_wait_selftest": ([I, I, ctypes.c_double], I),
         "gg_wait_selftest_device": ([ctypes.c_uint32, ctypes.c_double], I),
+        "gg_task_selftest": ([I], I),
         "gg_release_task_queues": ([], I),
         "gg_groth16_pk_create_stripe_ex": ([I, I, P, P, P, S, P, S, P, S, S, P, S, P, P, P, P, P, P, P, P, S,
                                             S, P, I, I, PP], I),
@@ -255,7 +256,7 @@ EXPORTED = [
     "gg_groth16_mpk_set_rehearsal", "gg_plonk_pk_set_rehearsal", "gg_plonk_pk_set_rehearsal_part",
     "gg_plonk_pk_part_timings", "gg_groth16_mpk_peer_access", "gg_plonk_pk_peer_access",
     "gg_fr_evaluate_many", "gg_msm_batch_shape", "gg_set_wait_timeout", "gg_get_wait_timeout",
-    "gg_wait_selftest", "gg_wait_selftest_device", "gg_release_task_queues",
+    "gg_wait_selftest", "gg_wait_selftest_device", "gg_task_selftest", "gg_release_task_queues",
 ]
 
 

@@ -189,6 +189,11 @@ int gg_wait_selftest(int parties, int arriving, double timeout_s);
  * under timeout_s: GG_ERR_TIMEOUT (message names the wait) if it was still
  * running, else GG_OK.  The wave always drains before the call returns. */
 int gg_wait_selftest_device(uint32_t sleeps, double timeout_s);
+/* Host-only self-test of the library's kept worker threads (no GPU needed): n
+ * tasks that all meet at one barrier (so the worker set must grow to n), the
+ * last failing after it; GG_OK if all ran and the failure came back to the
+ * waiter, a dropped deferred task never ran and a waited one ran once. */
+int gg_task_selftest(int n);
 size_t gg_get_hbm_budget(void);
 
 /* out = sum_i scalars[idx(i)] * P_i as a Jacobian point (gnark G1Jac/G2Jac

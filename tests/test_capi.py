@@ -174,6 +174,17 @@ def test_bounded_wait_times_out_instead_of_blocking():
     assert _lib.lib.gg_wait_selftest_device((1 << 20) + 1, 1.0) == 1
 
 
+def test_kept_worker_threads_run_blocked_tasks_and_return_errors():
+    """The provers' host tasks run on kept worker threads (common.h run_task,
+    round 6): 64 tasks that all wait at one barrier need 64 workers at once --
+    the set grows instead of deadlocking -- and the failing task's error comes
+    back to the waiter, as with std::async (host only, no GPU)."""
+    from gnark_amd import _lib
+    for n in (1, 8, 64):
+        assert _lib.lib.gg_task_selftest(n) == 0, _lib.lib.gg_last_error()
+    assert _lib.lib.gg_task_selftest(0) == 1
+
+
 def test_msm_batch_shape_refuses_32bit_overflow():
     """a batch multiplies the sort's entries by n_vectors and its
     bucket space by the next power of two; past 32-bit words it is refused
