@@ -806,6 +806,41 @@ __global__ void __launch_bounds__(256) k_bucket_combine(const Xyzz<F>* head, con
     if (lane == 0) st(out, acc);
 }
 
+// k_bucket_combine over radix-form partials (round 6): each partial converted
+// to gnark's form as it is loaded -- a direct bucket from SP, a straddling one
+// from its ranges' heads / tail -- instead of three conversion launches over
+// every head, tail and S slot before the combine (the small MSMs of the quad
+// path: a PlonK part's slices, configs[1]'s 2^20 MSM).  The heavy buckets' tree
+// runs before it on the radix heads (k_range_tree_r).
+template <class F>
+__global__ void __launch_bounds__(256) k_bucket_combine_r(const typename PartialOf<F>::T* headP,
+                                                          const typename PartialOf<F>::T* tailP,
+                                                          const typename PartialOf<F>::T* SP, const uint32_t* offsets,
+                                                          uint32_t nb, int c, uint32_t K, Xyzz<F>* S) {
+    const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = (uint32_t)g & 3;
+    const size_t q = g >> 2;
+    if (q >= nb) return;
+    const uint32_t E = offsets[nb];
+    const BucketSpan s = bucket_span(offsets, (uint32_t)q, E, K);
+    const uint32_t pq = bucket_perm((uint32_t)q, c);
+    Xyzz<F>* out = S + pq;
+    if (s.empty) {
+        if (lane == 0) st(out, Xyzz<F>::inf());
+        return;
+    }
+    if (s.direct) {
+        if (lane == 0) st(out, to_std(ld(SP + pq)));
+        return;
+    }
+    Xyzz<F> acc = to_std(ld((s.first ? headP : tailP) + s.t0));
+    const uint32_t m = s.t1 - s.t0;
+    if (m > LIGHT) xyzz_add_quad(acc, to_std(ld(headP + s.t0 + 1)), lane);  // tree result
+    else
+        for (uint32_t t = s.t0 + 1; t <= s.t1; t++) xyzz_add_quad(acc, to_std(ld(headP + t)), lane);
+    if (lane == 0) st(out, acc);
+}
+
 // k_range_tree over radix-form partials, a lane per slot (xyzzl_add)
 template <class F>
 __global__ void __launch_bounds__(256) k_range_tree_r(typename PartialOf<F>::T* head, const uint32_t* tbucket,
@@ -1373,6 +1408,12 @@ inline bool segsum_enabled() {
     const char* e = getenv("GG_MSM_SEGSUM");  // per MSM: tests switch it
     return !(e && atoi(e) == 0);
 }
+// GG_MSM_COMBINE_FUSED=0: the quad path converts every partial in three launches
+// before k_bucket_combine (A/B; per MSM: tests switch it)
+inline bool combine_fused() {
+    const char* e = getenv("GG_MSM_COMBINE_FUSED");
+    return !(e && atoi(e) == 0);
+}
 
 
 // Entries per accumulation range (one thread each).  Every range costs the same,
@@ -1546,24 +1587,41 @@ inline void msm_finish_multi(gg_msm_base* b, MsmSort* s, MsmScratch* scr, hipStr
             return;
         }
     }
-    if constexpr (kRadixP) {  // the quad path works on gnark's form
-        hipLaunchKernelGGL(k_partials_to_std<F>, dim3(grid_for(T + 1, 256)), dim3(256), 0, st, (const PT*)hP, T + 1,
-                           head);
-        hipLaunchKernelGGL(k_partials_to_std<F>, dim3(grid_for(T + 1, 256)), dim3(256), 0, st, (const PT*)tP, T + 1,
-                           scr->tail.as<Xyzz<F>>());
-        hipLaunchKernelGGL(k_partials_to_std<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, (const PT*)SP, nb, S);
+    bool combined = false;
+    if constexpr (kRadixP) {
+        if (combine_fused()) {  // the quad path's conversions inside the combine (k_bucket_combine_r)
+            for (uint32_t stride = 1; max_ranges > LIGHT && stride < max_ranges;) {
+                const uint32_t fan = (stride == 1) ? 4u : 2u;
+                hipLaunchKernelGGL(k_range_tree_r<F>, dim3(grid_for(T, 256)), dim3(256), 0, st, hP,
+                                   (const uint32_t*)scr->tbucket.p, offs, (uint32_t)nb, K, stride, fan);
+                GG_HIP(hipGetLastError());
+                stride *= fan;
+            }
+            hipLaunchKernelGGL(k_bucket_combine_r<F>, dim3(grid_for(4 * nb, 256)), dim3(256), 0, st, (const PT*)hP,
+                               (const PT*)tP, (const PT*)SP, offs, (uint32_t)nb, ce, K, S);
+            GG_HIP(hipGetLastError());
+            combined = true;
+        } else {  // the quad path works on gnark's form
+            hipLaunchKernelGGL(k_partials_to_std<F>, dim3(grid_for(T + 1, 256)), dim3(256), 0, st, (const PT*)hP,
+                               T + 1, head);
+            hipLaunchKernelGGL(k_partials_to_std<F>, dim3(grid_for(T + 1, 256)), dim3(256), 0, st, (const PT*)tP,
+                               T + 1, scr->tail.as<Xyzz<F>>());
+            hipLaunchKernelGGL(k_partials_to_std<F>, dim3(grid_for(nb, 256)), dim3(256), 0, st, (const PT*)SP, nb, S);
+            GG_HIP(hipGetLastError());
+        }
+    }
+    if (!combined) {
+        for (uint32_t stride = 1; max_ranges > LIGHT && stride < max_ranges;) {
+            const uint32_t fan = (stride == 1) ? 4u : 2u;
+            hipLaunchKernelGGL(k_range_tree<F>, dim3(grid_for(4 * T, 256)), dim3(256), 0, st, head,
+                               (const uint32_t*)scr->tbucket.p, offs, (uint32_t)nb, K, stride, fan);
+            GG_HIP(hipGetLastError());
+            stride *= fan;
+        }
+        hipLaunchKernelGGL(k_bucket_combine<F>, dim3(grid_for(4 * nb, 256)), dim3(256), 0, st, (const Xyzz<F>*)head,
+                           (const Xyzz<F>*)scr->tail.p, offs, (uint32_t)nb, ce, K, S);
         GG_HIP(hipGetLastError());
     }
-    for (uint32_t stride = 1; max_ranges > LIGHT && stride < max_ranges;) {
-        const uint32_t fan = (stride == 1) ? 4u : 2u;
-        hipLaunchKernelGGL(k_range_tree<F>, dim3(grid_for(4 * T, 256)), dim3(256), 0, st, head,
-                           (const uint32_t*)scr->tbucket.p, offs, (uint32_t)nb, K, stride, fan);
-        GG_HIP(hipGetLastError());
-        stride *= fan;
-    }
-    hipLaunchKernelGGL(k_bucket_combine<F>, dim3(grid_for(4 * nb, 256)), dim3(256), 0, st, (const Xyzz<F>*)head,
-                       (const Xyzz<F>*)scr->tail.p, offs, (uint32_t)nb, ce, K, S);
-    GG_HIP(hipGetLastError());
     ps_acc2.stop(st);
     // ---- bucket reduction: sum_b (b+1) S_b
     ProfScope ps_red("msm_reduce", st, (double)nb);
