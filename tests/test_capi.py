@@ -183,6 +183,16 @@ def test_kept_worker_threads_run_blocked_tasks_and_return_errors():
     for n in (1, 8, 64):
         assert _lib.lib.gg_task_selftest(n) == 0, _lib.lib.gg_last_error()
     assert _lib.lib.gg_task_selftest(0) == 1
+    # the A/B switch (a fresh thread per task) keeps the same contract; the
+    # variable is read once per process, hence a child process
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); from gnark_amd import _lib; "
+            "rc = _lib.lib.gg_task_selftest(16); print(rc, _lib.lib.gg_last_error().decode()); "
+            "sys.exit(rc)" % os.path.join(ROOT, "gnark-fork_amd"))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, GG_TASK_POOL="0"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
 
 
 def test_msm_batch_shape_refuses_32bit_overflow():
