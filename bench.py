@@ -825,7 +825,7 @@ def accum_roofline(k, pt_bytes, kernel, workload, desc, windows):
          "kernel": desc, "algorithmic_bytes_per_launch": alg, "units_per_launch": units, "windows": windows,
          "kernel_avg_ms": ms,
          "timing": "HIP events on the kernel's launch stream over %d proves run task by task (rocprof summary of "
-                   "the same workload: profiles/r06_h_groth16_2p24_kernel_stats.md)" % ROOFLINE_PROVES,
+                   "the same workload: profiles/r06_v_groth16_2p24_kernel_stats.md)" % ROOFLINE_PROVES,
          "note": "EC MSM is VALU-integer bound (SURVEY 8d); the HBM fraction is reported as required, the "
                  "issue-rate fraction below is the kernel's real ceiling"}
     sq = pmc_sq(kernel, workload)
